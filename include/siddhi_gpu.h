@@ -1,0 +1,130 @@
+/*
+ * siddhi_gpu.h — C-ABI of the MI355X pattern/sequence engine.
+ *
+ * This is the drop-in seam that replaces the reference's per-key NFA advance:
+ *
+ *   ingest seam   StreamJunction.Receiver.receive(...)
+ *                 /root/reference/modules/siddhi-core/src/main/java/io/siddhi/core/stream/StreamJunction.java:469-482
+ *                 implemented today by PartitionStreamReceiver (partition/PartitionStreamReceiver.java:81-283)
+ *                 and the Pattern/Sequence*ProcessStreamReceiver family
+ *                 (query/input/MultiProcessStreamReceiver.java:93-241, SingleProcessStreamReceiver.java:55-78)
+ *                 -> sg_push_batch()
+ *   output seam   QuerySelector.process(ComplexEventChunk<StateEvent>)
+ *                 (query/selector/QuerySelector.java:77-100), fed one StateEvent per match
+ *                 by StateMultiProcessStreamReceiver.processAndClear (StateMultiProcessStreamReceiver.java:47-68)
+ *                 -> sg_poll_matches(): one record per emitted StateEvent, slots given as event seqs
+ *   compile seam  StateInputStreamParser.parseInputStream (util/parser/StateInputStreamParser.java:76-146)
+ *                 -> sg_engine_create() with the IR of siddhi_gpu_ir.h
+ *   playback clock  Scheduler/TimestampGenerator (util/Scheduler.java:65-105) -> sg_advance_time()
+ *   persistence   StreamPreStateProcessor.StreamPreState.snapshot/restore (StreamPreStateProcessor.java:450-469)
+ *                 -> sg_snapshot()/sg_restore()
+ *
+ * Threading mirrors the reference's single writer per query (QueryParser.java:169-213 lock,
+ * MultiProcessStreamReceiver.java:97 synchronized): one host thread per engine; calls are not re-entrant.
+ * Errors: every call returns SG_OK (0) or a negative SG_ERR_*; sg_last_error() gives the message of the
+ * calling thread's last failure.  The Java shim maps them to SiddhiAppRuntimeException and routes them
+ * through StreamJunction.handleError (StreamJunction.java:372-464).
+ */
+#ifndef SIDDHI_GPU_H
+#define SIDDHI_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SG_ABI_VERSION 1
+
+#define SG_OK 0
+#define SG_ERR_INVALID (-1)     /* bad argument / malformed IR */
+#define SG_ERR_UNSUPPORTED (-2) /* query shape not supported by this engine */
+#define SG_ERR_DEVICE (-3)      /* HIP runtime failure */
+#define SG_ERR_CAPACITY (-4)    /* per-key partial or match buffer capacity exceeded */
+#define SG_ERR_STATE (-5)       /* call out of order (e.g. push while matches are held) */
+
+#define SG_MEM_HOST 0u   /* pointers are host memory */
+#define SG_MEM_DEVICE 1u /* pointers are device (HBM) memory of the engine's device */
+
+#define SG_NULL_SEQ UINT64_MAX
+
+/* engine configuration flags */
+#define SG_CFG_NO_ORDER 1u /* deliver matches per-key ordered only (skip the global trigger-seq order) */
+
+typedef struct sg_engine sg_engine;
+
+typedef struct sg_config {
+    uint32_t struct_size;      /* sizeof(sg_config) */
+    int32_t device;            /* HIP device ordinal */
+    uint32_t n_keys;           /* partition key ids are dense in [0, n_keys); 1 when unpartitioned */
+    uint32_t max_batch;        /* max events in one sg_push_batch */
+    uint32_t partial_capacity; /* max live partial matches per key */
+    uint32_t flags;            /* SG_CFG_* */
+    uint64_t match_capacity;   /* max matches held between two polls */
+} sg_config;
+
+/* One micro-batch of events of ONE input stream, in arrival order (columnar / SoA). */
+typedef struct sg_batch {
+    uint32_t struct_size;       /* sizeof(sg_batch) */
+    uint32_t stream;            /* stream index in the IR stream table */
+    uint64_t n;                 /* number of events */
+    uint64_t seq_base;          /* arrival sequence number of event 0 (event i has seq_base + i) */
+    const uint32_t* key;        /* [n] partition key ids; NULL when the query is not partitioned */
+    const int64_t* ts;          /* [n] event timestamps in ms */
+    const void* const* cols;    /* [n_cols] attribute columns, typed per the IR stream table */
+    const uint8_t* const* nulls;/* [n_cols] per-event null flags (1 = null) or NULL entries */
+    uint32_t n_cols;
+    uint32_t mem;               /* SG_MEM_HOST or SG_MEM_DEVICE for all pointers above */
+} sg_batch;
+
+/* Matches emitted since the previous poll.  Library-owned until sg_release_matches().
+ * Order: ascending trigger_seq, then emission order (the reference's callback order for
+ * per-event sends, MultiProcessStreamReceiver.java:119-121); per key the order is always the
+ * reference's per-partition order. */
+typedef struct sg_match_batch {
+    uint64_t n;
+    uint32_t n_slots;              /* state stream events per match (IR slot count) */
+    uint32_t max_chain;            /* max events per slot (count states chain several) */
+    const uint64_t* trigger_seq;   /* [n] seq of the event whose processing emitted the match */
+    const uint32_t* key;           /* [n] partition key id */
+    const int64_t* ts;             /* [n] StateEvent timestamp at emission */
+    const uint64_t* slot_seq;      /* [n][n_slots][max_chain] event seqs, SG_NULL_SEQ = none */
+    const uint32_t* chain_len;     /* [n][n_slots] events in each slot */
+    uint32_t mem;                  /* where the arrays live */
+    uint32_t reserved;
+} sg_match_batch;
+
+/* Exact work counters (the algorithmic-byte model of DESIGN.md is computed from these). */
+typedef struct sg_stats {
+    uint64_t events;            /* events pushed */
+    uint64_t batches;
+    uint64_t partials_scanned;  /* partial matches visited by an event */
+    uint64_t partials_created;  /* partial matches created */
+    uint64_t partials_live;     /* partial matches alive after the last batch */
+    uint64_t matches;           /* matches emitted */
+    uint64_t keys_touched;      /* sum over batches of keys with >= 1 event */
+    uint64_t live_at_batch_start; /* sum over batches of the live partials of the touched keys */
+} sg_stats;
+
+/* ir/ir_len: an IR blob (siddhi_gpu_ir.h) of one query */
+int sg_engine_create(const void* ir, size_t ir_len, const sg_config* cfg, sg_engine** out);
+int sg_push_batch(sg_engine* e, const sg_batch* b);
+int sg_advance_time(sg_engine* e, int64_t now_ms);
+/* mem = SG_MEM_HOST copies matches to host memory; SG_MEM_DEVICE returns device pointers */
+int sg_poll_matches(sg_engine* e, uint32_t mem, sg_match_batch* out);
+int sg_release_matches(sg_engine* e, sg_match_batch* m);
+int sg_get_stats(sg_engine* e, sg_stats* out);
+int sg_synchronize(sg_engine* e);
+int sg_snapshot(sg_engine* e, void** buf, size_t* len);
+int sg_restore(sg_engine* e, const void* buf, size_t len);
+int sg_free_buffer(void* buf);
+void sg_engine_destroy(sg_engine* e);
+const char* sg_last_error(void);
+int sg_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SIDDHI_GPU_H */

@@ -1,0 +1,214 @@
+"""ctypes binding of the engine C-ABI (include/siddhi_gpu.h).
+
+`NativeEngine` drives any library that exports the `sg_*` entry points under a given symbol
+prefix.  The product loads the HIP engine `libsiddhi_gpu.so` built next to this file
+(`load_hip_library`); there is no fallback: if the library is missing the call raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+SG_OK = 0
+SG_MEM_HOST = 0
+SG_MEM_DEVICE = 1
+SG_NULL_SEQ = np.uint64(0xFFFFFFFFFFFFFFFF)
+SG_CFG_NO_ORDER = 1
+
+ERRORS = {-1: "SG_ERR_INVALID", -2: "SG_ERR_UNSUPPORTED", -3: "SG_ERR_DEVICE",
+          -4: "SG_ERR_CAPACITY", -5: "SG_ERR_STATE"}
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+HIP_LIBRARY = os.path.join(HERE, "lib", "libsiddhi_gpu.so")
+
+
+class EngineError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"{ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+class sg_config(C.Structure):
+    _fields_ = [("struct_size", C.c_uint32), ("device", C.c_int32), ("n_keys", C.c_uint32),
+                ("max_batch", C.c_uint32), ("partial_capacity", C.c_uint32), ("flags", C.c_uint32),
+                ("match_capacity", C.c_uint64)]
+
+
+class sg_batch(C.Structure):
+    _fields_ = [("struct_size", C.c_uint32), ("stream", C.c_uint32), ("n", C.c_uint64),
+                ("seq_base", C.c_uint64), ("key", C.c_void_p), ("ts", C.c_void_p),
+                ("cols", C.POINTER(C.c_void_p)), ("nulls", C.POINTER(C.c_void_p)),
+                ("n_cols", C.c_uint32), ("mem", C.c_uint32)]
+
+
+class sg_match_batch(C.Structure):
+    _fields_ = [("n", C.c_uint64), ("n_slots", C.c_uint32), ("max_chain", C.c_uint32),
+                ("trigger_seq", C.c_void_p), ("key", C.c_void_p), ("ts", C.c_void_p),
+                ("slot_seq", C.c_void_p), ("chain_len", C.c_void_p), ("mem", C.c_uint32),
+                ("reserved", C.c_uint32)]
+
+
+class sg_stats(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in ("events", "batches", "partials_scanned", "partials_created",
+                                          "partials_live", "matches", "keys_touched",
+                                          "live_at_batch_start")]
+
+
+@dataclass
+class Matches:
+    """Host copy of one sg_match_batch."""
+    trigger_seq: np.ndarray   # [n] uint64
+    key: np.ndarray           # [n] uint32
+    ts: np.ndarray            # [n] int64
+    slot_seq: np.ndarray      # [n, n_slots, max_chain] uint64
+    chain_len: np.ndarray     # [n, n_slots] uint32
+
+    def __len__(self):
+        return int(self.trigger_seq.shape[0])
+
+
+_LIBS = {}
+
+
+def load_library(path):
+    path = os.path.abspath(path)
+    if path not in _LIBS:
+        if not os.path.exists(path):
+            raise FileNotFoundError(f"engine library {path} is missing: build it with "
+                                    f"`python __graft_entry__.py build` (no CPU fallback exists)")
+        _LIBS[path] = C.CDLL(path)
+    return _LIBS[path]
+
+
+def load_hip_library():
+    return load_library(HIP_LIBRARY)
+
+
+def _np_ptr(a):
+    return C.c_void_p(a.ctypes.data) if a is not None else None
+
+
+class NativeEngine:
+    """One sg_engine (one compiled query on one device)."""
+
+    def __init__(self, lib, prefix, ir: bytes, n_keys=1, max_batch=1 << 16, partial_capacity=64,
+                 match_capacity=1 << 20, device=0, flags=0):
+        self.lib = lib
+        self.p = prefix
+        f = lambda n: getattr(lib, prefix + n)
+        self._create = f("engine_create")
+        self._create.argtypes = [C.c_void_p, C.c_size_t, C.POINTER(sg_config), C.POINTER(C.c_void_p)]
+        self._push = f("push_batch")
+        self._push.argtypes = [C.c_void_p, C.POINTER(sg_batch)]
+        self._poll = f("poll_matches")
+        self._poll.argtypes = [C.c_void_p, C.c_uint32, C.POINTER(sg_match_batch)]
+        self._release = f("release_matches")
+        self._release.argtypes = [C.c_void_p, C.POINTER(sg_match_batch)]
+        self._stats = f("get_stats")
+        self._stats.argtypes = [C.c_void_p, C.POINTER(sg_stats)]
+        self._destroy = f("engine_destroy")
+        self._destroy.argtypes = [C.c_void_p]
+        self._destroy.restype = None
+        self._err = f("last_error")
+        self._err.restype = C.c_char_p
+        self._advance = f("advance_time")
+        self._advance.argtypes = [C.c_void_p, C.c_int64]
+        self._sync = getattr(lib, prefix + "synchronize", None)
+        if self._sync is not None:
+            self._sync.argtypes = [C.c_void_p]
+        cfg = sg_config(C.sizeof(sg_config), device, n_keys, max_batch, partial_capacity, flags,
+                        match_capacity)
+        self._ir = C.create_string_buffer(ir, len(ir))
+        h = C.c_void_p()
+        self._check(self._create(self._ir, len(ir), C.byref(cfg), C.byref(h)))
+        self.h = h
+        self.n_keys = n_keys
+
+    def _check(self, rc):
+        if rc != SG_OK:
+            raise EngineError(rc, self._err().decode(errors="replace"))
+
+    def push(self, stream, seq_base, ts, cols, nulls=None, key=None, mem=SG_MEM_HOST):
+        """Push one batch.  cols/nulls/key/ts: numpy arrays (host) or raw pointers (device)."""
+        n_cols = len(cols)
+        if mem == SG_MEM_HOST:
+            ts = np.ascontiguousarray(ts, dtype=np.int64)
+            n = ts.shape[0]
+            keep = [ts]
+            colp = (C.c_void_p * max(1, n_cols))(*[c.ctypes.data for c in cols])
+            keep += list(cols)
+            nullp = None
+            if nulls is not None and any(x is not None for x in nulls):
+                nullp = (C.c_void_p * max(1, n_cols))(*[(x.ctypes.data if x is not None else None)
+                                                        for x in nulls])
+                keep += [x for x in nulls if x is not None]
+            kp = None
+            if key is not None:
+                key = np.ascontiguousarray(key, dtype=np.uint32)
+                keep.append(key)
+                kp = key.ctypes.data
+            b = sg_batch(C.sizeof(sg_batch), stream, n, seq_base, kp, ts.ctypes.data,
+                         C.cast(colp, C.POINTER(C.c_void_p)),
+                         C.cast(nullp, C.POINTER(C.c_void_p)) if nullp is not None else None,
+                         n_cols, SG_MEM_HOST)
+            self._check(self._push(self.h, C.byref(b)))
+            del keep
+        else:
+            n, ts_ptr, col_ptrs, key_ptr = ts
+            colp = (C.c_void_p * max(1, n_cols))(*col_ptrs)
+            b = sg_batch(C.sizeof(sg_batch), stream, n, seq_base, key_ptr, ts_ptr,
+                         C.cast(colp, C.POINTER(C.c_void_p)), None, n_cols, SG_MEM_DEVICE)
+            self._check(self._push(self.h, C.byref(b)))
+
+    def poll(self) -> Matches:
+        m = sg_match_batch()
+        self._check(self._poll(self.h, SG_MEM_HOST, C.byref(m)))
+        n, ns, mc = int(m.n), int(m.n_slots), int(m.max_chain)
+
+        def arr(ptr, dtype, shape):
+            cnt = int(np.prod(shape))
+            if cnt == 0 or not ptr:
+                return np.zeros(shape, dtype=dtype)
+            buf = (C.c_char * (cnt * np.dtype(dtype).itemsize)).from_address(ptr)
+            return np.frombuffer(buf, dtype=dtype).reshape(shape).copy()
+
+        out = Matches(arr(m.trigger_seq, np.uint64, (n,)), arr(m.key, np.uint32, (n,)),
+                      arr(m.ts, np.int64, (n,)), arr(m.slot_seq, np.uint64, (n, ns, mc)),
+                      arr(m.chain_len, np.uint32, (n, ns)))
+        self._check(self._release(self.h, C.byref(m)))
+        return out
+
+    def poll_device(self):
+        """Matches stay in HBM; returns the raw sg_match_batch (caller must release())."""
+        m = sg_match_batch()
+        self._check(self._poll(self.h, SG_MEM_DEVICE, C.byref(m)))
+        return m
+
+    def release(self, m):
+        self._check(self._release(self.h, C.byref(m)))
+
+    def advance_time(self, now):
+        self._check(self._advance(self.h, int(now)))
+
+    def synchronize(self):
+        if self._sync is not None:
+            self._check(self._sync(self.h))
+
+    def stats(self):
+        s = sg_stats()
+        self._check(self._stats(self.h, C.byref(s)))
+        return {n: int(getattr(s, n)) for n, _ in sg_stats._fields_}
+
+    def close(self):
+        if getattr(self, "h", None):
+            self._destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

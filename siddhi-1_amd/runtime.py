@@ -1,0 +1,485 @@
+"""Host-side mirror of the reference's public API for the pattern path.
+
+    SiddhiManager().createSiddhiAppRuntime(app)          C/SiddhiManager.java:95-98
+    runtime.addCallback("query1", QueryCallback)          C/SiddhiAppRuntimeImpl.java:266,277
+    runtime.getInputHandler("Stream1").send(...)          C/stream/input/InputHandler.java:51-97
+    StreamCallback.receive(Event[]) / QueryCallback.receive(ts, in, remove)
+                                                          C/stream/output/StreamCallback.java:94-130,
+                                                          C/query/output/callback/QueryCallback.java:62-107
+
+(`C/` = /root/reference/modules/siddhi-core/src/main/java/io/siddhi/core/.)
+
+Below the API, every pattern/sequence query is compiled to the engine IR and run by an engine
+behind the C-ABI (include/siddhi_gpu.h): the HIP engine by default.  Events are packed into columnar
+batches (one per `send` call and input stream), partition keys are mapped to dense ids by a host
+dictionary (keys are compared only by String.equals in ValuePartitionExecutor.java:34-41, so any
+injective map preserves semantics), and emitted matches are projected through the select list on the
+host (QuerySelector.processNoGroupBy, C/query/selector/QuerySelector.java:162-206).
+"""
+from __future__ import annotations
+
+import struct
+import time
+from typing import Callable, Dict, List, Optional
+
+import numpy as np
+
+from . import compiler as cp
+from . import siddhiql as q
+from .native import NativeEngine, load_hip_library
+
+
+# ------------------------------------------------------------------------------------------------
+# public value types
+# ------------------------------------------------------------------------------------------------
+class Event:
+    """io.siddhi.core.event.Event"""
+
+    def __init__(self, timestamp=-1, data=None, is_expired=False):
+        self.timestamp = timestamp
+        self.data = list(data) if data is not None else []
+        self.is_expired = is_expired
+
+    def getData(self, i=None):
+        return self.data if i is None else self.data[i]
+
+    def getTimestamp(self):
+        return self.timestamp
+
+    def isExpired(self):
+        return self.is_expired
+
+    def __repr__(self):
+        return f"Event{{timestamp={self.timestamp}, data={self.data}, isExpired={self.is_expired}}}"
+
+
+class StreamCallback:
+    def receive(self, events: List[Event]):
+        raise NotImplementedError
+
+
+class QueryCallback:
+    def receive(self, timestamp, in_events, remove_events):
+        raise NotImplementedError
+
+
+class _FnStreamCallback(StreamCallback):
+    def __init__(self, fn):
+        self.fn = fn
+
+    def receive(self, events):
+        self.fn(events)
+
+
+class _FnQueryCallback(QueryCallback):
+    def __init__(self, fn):
+        self.fn = fn
+
+    def receive(self, timestamp, in_events, remove_events):
+        self.fn(timestamp, in_events, remove_events)
+
+
+class SiddhiAppCreationException(cp.SiddhiAppCreationException):
+    pass
+
+
+# ------------------------------------------------------------------------------------------------
+# Java value helpers (output attributes keep Java types: float -> np.float32)
+# ------------------------------------------------------------------------------------------------
+def _wrap32(x):
+    x &= 0xFFFFFFFF
+    return x - (1 << 32) if x >= (1 << 31) else x
+
+
+def _wrap64(x):
+    x &= 0xFFFFFFFFFFFFFFFF
+    return x - (1 << 64) if x >= (1 << 63) else x
+
+
+def _to_type(v, t):
+    if v is None:
+        return None
+    if t == "INT":
+        return int(v)
+    if t == "LONG":
+        return int(v)
+    if t == "FLOAT":
+        return np.float32(v)
+    if t == "DOUBLE":
+        return float(v)
+    return v
+
+
+def _java_div(a, b):
+    qv = abs(a) // abs(b)
+    return qv if (a >= 0) == (b >= 0) else -qv
+
+
+def _java_mod(a, b):
+    return a - b * _java_div(a, b)
+
+
+def _arith(op, t, a, b):
+    """executor/math/*/*ExpressionExecutor{Int,Long,Float,Double}.java"""
+    if a is None or b is None:
+        return None
+    a = _to_type(a, t)
+    b = _to_type(b, t)
+    if t in ("INT", "LONG"):
+        w = _wrap32 if t == "INT" else _wrap64
+        if op == "+":
+            return w(a + b)
+        if op == "-":
+            return w(a - b)
+        if op == "*":
+            return w(a * b)
+        if b == 0:
+            return None
+        if op == "/":
+            return w(_java_div(a, b))
+        return w(_java_mod(a, b))
+    with np.errstate(all="ignore"):
+        if op == "+":
+            r = a + b
+        elif op == "-":
+            r = a - b
+        elif op == "*":
+            r = a * b
+        elif op == "/":
+            if b == 0:
+                return None
+            r = a / b
+        else:
+            if b == 0:
+                return None
+            r = np.fmod(a, b)
+    return np.float32(r) if t == "FLOAT" else float(r)
+
+
+def _compare(op, dom, a, b):
+    if a is None or b is None:
+        return op == "!="
+    if dom in ("INT", "LONG", "FLOAT", "DOUBLE"):
+        a = _to_type(a, dom)
+        b = _to_type(b, dom)
+    if op == "==":
+        return bool(a == b)
+    if op == "!=":
+        return bool(a != b)
+    if op == ">":
+        return bool(a > b)
+    if op == ">=":
+        return bool(a >= b)
+    if op == "<":
+        return bool(a < b)
+    return bool(a <= b)
+
+
+# ------------------------------------------------------------------------------------------------
+# host event store: payloads by arrival seq (strings never go to the device)
+# ------------------------------------------------------------------------------------------------
+class _EventStore:
+    def __init__(self):
+        self.rows = []          # seq -> (stream name, ts, data tuple)
+
+    def add(self, stream, ts, data):
+        self.rows.append((stream, ts, data))
+        return len(self.rows) - 1
+
+    def get(self, seq):
+        return self.rows[int(seq)]
+
+
+class StringDictionary:
+    """Host dictionary: STRING attribute values -> dense uint32 ids (equality preserved)."""
+
+    def __init__(self):
+        self.ids: Dict[str, int] = {}
+        self.strs: List[str] = []
+
+    def id_of(self, s):
+        i = self.ids.get(s)
+        if i is None:
+            i = len(self.strs)
+            self.ids[s] = i
+            self.strs.append(s)
+        return i
+
+
+def java_string(v):
+    """String.valueOf / toString for partition keys (ValuePartitionExecutor.java:34-41)."""
+    if v is None:
+        return None
+    if isinstance(v, bool):
+        return "true" if v else "false"
+    if isinstance(v, (np.floating, float)):
+        f = float(v)
+        if f == int(f) and abs(f) < 1e7:
+            return f"{int(f)}.0"
+        return repr(np.float32(v)) if isinstance(v, np.float32) else repr(f)
+    return str(v)
+
+
+# ------------------------------------------------------------------------------------------------
+# query runtime
+# ------------------------------------------------------------------------------------------------
+class _QueryRuntime:
+    def __init__(self, app_rt, cq: cp.CompiledQuery, engine_factory, key_dict):
+        self.app_rt = app_rt
+        self.cq = cq
+        self.key_dict = key_dict
+        self.n_keys = app_rt.n_keys if cq.partitioned else 1
+        self.engine = engine_factory(cq.ir, self.n_keys)
+        self.query_callbacks: List[QueryCallback] = []
+
+    # -- projection (QuerySelector) --------------------------------------------------------------
+    def _eval(self, t, chains, store):
+        k = t.kind
+        if k == "const":
+            return t.value if t.type != "FLOAT" else np.float32(t.value)
+        if k == "var":
+            v = t.var
+            chain = chains[v.slot]
+            if v.multi_value:
+                out = []
+                for s in chain:
+                    out.append(_to_type(store.get(s)[2][v.attr_idx], v.type))
+                return out
+            n = len(chain)
+            i = v.chain_index
+            if i >= 0:
+                if i >= n:
+                    return None
+                s = chain[i]
+            else:
+                j = n + i
+                if j < 0 or n == 0:
+                    return None
+                s = chain[j]
+            return _to_type(store.get(s)[2][v.attr_idx], v.type)
+        if k == "arith":
+            return _arith(t.op, t.type, self._eval(t.left, chains, store), self._eval(t.right, chains, store))
+        if k == "cmp":
+            return _compare(t.op, t.dom, self._eval(t.left, chains, store), self._eval(t.right, chains, store))
+        if k == "and":
+            return bool(self._eval(t.left, chains, store)) and bool(self._eval(t.right, chains, store))
+        if k == "or":
+            return bool(self._eval(t.left, chains, store)) or bool(self._eval(t.right, chains, store))
+        if k == "not":
+            return not (self._eval(t.arg, chains, store) is True)
+        if k == "isnull":
+            return self._eval(t.arg, chains, store) is None
+        if k == "isnull_ev":
+            chain = chains[t.slot]
+            n = len(chain)
+            i = t.chain
+            return not ((0 <= i < n) or (i < 0 and n + i >= 0 and n > 0))
+        raise RuntimeError(k)
+
+    def project(self, m, store):
+        out = []
+        strings = self.app_rt.strings
+        n = len(m)
+        for i in range(n):
+            chains = []
+            for s in range(m.slot_seq.shape[1]):
+                ln = int(m.chain_len[i, s])
+                chains.append([int(x) for x in m.slot_seq[i, s, :ln]])
+            data = []
+            for name, typ, t in self.cq.select:
+                v = self._eval(t, chains, store)
+                data.append(v)
+            out.append((int(m.trigger_seq[i]), int(m.ts[i]), data))
+        return out
+
+    def dispatch(self, projected):
+        """Deliver in trigger order; one callback call per trigger event (ReturnEventHolder)."""
+        if not projected:
+            return
+        groups = []
+        cur = None
+        for trig, ts, data in projected:
+            if cur is None or cur[0] != trig:
+                cur = (trig, [])
+                groups.append(cur)
+            cur[1].append(Event(ts, data))
+        for _, evs in groups:
+            if self.cq.output_stream is not None:
+                self.app_rt._emit_stream(self.cq.output_stream, evs)
+            for cb in self.query_callbacks:
+                cb.receive(evs[-1].timestamp, evs, None)
+
+
+class InputHandler:
+    """io.siddhi.core.stream.input.InputHandler"""
+
+    def __init__(self, app_rt, stream):
+        self.app_rt = app_rt
+        self.stream = stream
+
+    def send(self, *args):
+        # send(Object[]) | send(long, Object[]) | send(Event) | send(Event[])
+        if len(args) == 2:
+            self.app_rt._send(self.stream, [(int(args[0]), list(args[1]))])
+            return
+        a = args[0]
+        if isinstance(a, Event):
+            self.app_rt._send(self.stream, [(a.timestamp, a.data)])
+        elif isinstance(a, (list, tuple)) and a and isinstance(a[0], Event):
+            self.app_rt._send(self.stream, [(e.timestamp, e.data) for e in a])
+        else:
+            self.app_rt._send(self.stream, [(self.app_rt.current_time(), list(a))])
+
+
+class SiddhiAppRuntime:
+    def __init__(self, text, engine_factory, n_keys=1 << 16):
+        self.app = q.parse_app(text)
+        self.n_keys = n_keys
+        self.strings = StringDictionary()
+        self.store = _EventStore()
+        self.stream_callbacks: Dict[str, List[StreamCallback]] = {}
+        self.queries: List[_QueryRuntime] = []
+        self.by_name: Dict[str, _QueryRuntime] = {}
+        self.playback = any(a.name.lower() == "app:playback" for a in self.app.annotations)
+        self._last_ts = None
+        self.key_dicts = {}
+        for i, qq in enumerate(self.app.queries):
+            cq = cp.compile_query(self.app, qq, self.strings)
+            kd = None
+            if qq.partition is not None:
+                kd = self.key_dicts.setdefault(id(qq.partition), {})
+            qr = _QueryRuntime(self, cq, engine_factory, kd)
+            self.queries.append(qr)
+            self.by_name[qq.name or f"query{i + 1}"] = qr
+        self.started = False
+
+    # public API (camelCase as in the reference) -------------------------------------------------
+    def getInputHandler(self, stream):
+        if stream not in self.app.streams:
+            raise KeyError(f"stream {stream} is not defined")
+        return InputHandler(self, stream)
+
+    def addCallback(self, name, cb):
+        if callable(cb) and not isinstance(cb, (StreamCallback, QueryCallback)):
+            cb = _FnStreamCallback(cb) if name not in self.by_name else _FnQueryCallback(cb)
+        if isinstance(cb, QueryCallback):
+            if name not in self.by_name:
+                raise KeyError(f"query {name} does not exist")
+            self.by_name[name].query_callbacks.append(cb)
+        else:
+            self.stream_callbacks.setdefault(name, []).append(cb)
+
+    def start(self):
+        self.started = True
+
+    def shutdown(self):
+        for qr in self.queries:
+            qr.engine.close()
+
+    get_input_handler = getInputHandler
+    add_callback = addCallback
+
+    def current_time(self):
+        if self.playback and self._last_ts is not None:
+            return self._last_ts
+        return int(time.time() * 1000)
+
+    # internals ----------------------------------------------------------------------------------
+    def _emit_stream(self, name, events):
+        for cb in self.stream_callbacks.get(name, []):
+            cb.receive(events)
+
+    def _columns(self, sd: q.StreamDef, rows):
+        cols, nulls = [], []
+        for ai, (an, at) in enumerate(sd.attrs):
+            vals = [r[ai] for r in rows]
+            isnull = np.array([v is None for v in vals], dtype=np.uint8)
+            if at == "STRING":
+                arr = np.array([self.strings.id_of(v) if v is not None else 0 for v in vals], dtype=np.uint32)
+            elif at == "INT":
+                arr = np.array([int(v) if v is not None else 0 for v in vals], dtype=np.int32)
+            elif at == "LONG":
+                arr = np.array([int(v) if v is not None else 0 for v in vals], dtype=np.int64)
+            elif at == "FLOAT":
+                arr = np.array([v if v is not None else 0 for v in vals], dtype=np.float32)
+            elif at == "DOUBLE":
+                arr = np.array([v if v is not None else 0 for v in vals], dtype=np.float64)
+            elif at == "BOOL":
+                arr = np.array([1 if v else 0 for v in vals], dtype=np.uint8)
+            else:
+                raise SiddhiAppCreationException(f"attribute type {at} is not supported")
+            cols.append(arr)
+            nulls.append(isnull if isnull.any() else None)
+        return cols, nulls
+
+    def _send(self, stream, events):
+        if stream not in self.app.streams:
+            raise KeyError(stream)
+        sd = self.app.streams[stream]
+        seqs = []
+        for ts, data in events:
+            if len(data) != len(sd.attrs):
+                raise ValueError(f"event for {stream} has {len(data)} attributes, expected {len(sd.attrs)}")
+            seqs.append(self.store.add(stream, ts, tuple(data)))
+            self._last_ts = ts
+        for qr in self.queries:
+            si = qr.cq.stream_index(stream)
+            if si < 0:
+                continue
+            ts_all = np.array([e[0] for e in events], dtype=np.int64)
+            rows = [e[1] for e in events]
+            keys = None
+            keep = list(range(len(events)))
+            if qr.cq.partitioned:
+                attr = qr.cq.partition_keys[stream]
+                ai = sd.attr_index(attr)
+                keys = []
+                keep = []
+                for i, r in enumerate(rows):
+                    ks = java_string(r[ai])
+                    if ks is None:
+                        continue          # PartitionStreamReceiver drops events whose key is null
+                    kid = qr.key_dict.get(ks)
+                    if kid is None:
+                        kid = len(qr.key_dict)
+                        if kid >= qr.n_keys:
+                            raise RuntimeError(f"more than {qr.n_keys} partition keys")
+                        qr.key_dict[ks] = kid
+                    keys.append(kid)
+                    keep.append(i)
+            # contiguous seq runs (events dropped for a null key split the batch)
+            start = 0
+            while start < len(keep):
+                end = start + 1
+                while end < len(keep) and keep[end] == keep[end - 1] + 1:
+                    end += 1
+                idx = keep[start:end]
+                cols, nulls = self._columns(sd, [rows[i] for i in idx])
+                kk = np.array(keys[start:end], dtype=np.uint32) if keys is not None else None
+                qr.engine.push(si, seqs[idx[0]], ts_all[idx], cols, nulls, kk)
+                start = end
+            m = qr.engine.poll()
+            qr.dispatch(qr.project(m, self.store))
+
+
+class SiddhiManager:
+    """io.siddhi.core.SiddhiManager (pattern path only)."""
+
+    def __init__(self, engine_factory: Optional[Callable] = None, n_keys=1 << 16, device=0,
+                 partial_capacity=64, max_batch=1 << 16):
+        if engine_factory is None:
+            lib = load_hip_library()          # raises if the HIP engine is not built
+
+            def engine_factory(ir, nk):
+                return NativeEngine(lib, "sg_", ir, n_keys=nk, max_batch=max_batch,
+                                    partial_capacity=partial_capacity, device=device)
+        self.engine_factory = engine_factory
+        self.n_keys = n_keys
+
+    def createSiddhiAppRuntime(self, text) -> SiddhiAppRuntime:
+        return SiddhiAppRuntime(text, self.engine_factory, self.n_keys)
+
+    create_siddhi_app_runtime = createSiddhiAppRuntime
+
+    def shutdown(self):
+        pass
