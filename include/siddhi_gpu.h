@@ -51,6 +51,7 @@ extern "C" {
 
 /* engine configuration flags */
 #define SG_CFG_NO_ORDER 1u /* deliver matches per-key ordered only (skip the global trigger-seq order) */
+#define SG_CFG_TIMING 2u   /* record HIP events around every kernel stage (sg_stats *_ns fields) */
 
 typedef struct sg_engine sg_engine;
 
@@ -105,6 +106,10 @@ typedef struct sg_stats {
     uint64_t matches;           /* matches emitted */
     uint64_t keys_touched;      /* sum over batches of keys with >= 1 event */
     uint64_t live_at_batch_start; /* sum over batches of the live partials of the touched keys */
+    uint64_t group_ns;          /* SG_CFG_TIMING: device time of key grouping (sort + bounds) */
+    uint64_t advance_ns;        /* SG_CFG_TIMING: device time of the NFA advance kernel */
+    uint64_t order_ns;          /* SG_CFG_TIMING: device time of match ordering in polls */
+    uint64_t advance_launches;  /* NFA advance kernel launches */
 } sg_stats;
 
 /* ir/ir_len: an IR blob (siddhi_gpu_ir.h) of one query */

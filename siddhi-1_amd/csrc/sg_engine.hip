@@ -1,0 +1,736 @@
+// sg_engine.hip — host side of the C-ABI (include/siddhi_gpu.h) for the MI355X engine.
+//
+// Per engine (= one compiled query on one HIP device) it keeps the partial-match state of every
+// partition key resident in HBM (SoA slabs sized n_keys x partial_capacity), and per pushed
+// micro-batch runs:
+//   1. (host batches only) H2D copy of the SoA columns the filters read
+//   2. key grouping: stable LSD radix sort of (key id -> batch position) on ceil(log2 n_keys) bits
+//      (rocPRIM onesweep), then per-key segment bounds            — replaces the key-run grouping
+//      of PartitionStreamReceiver.receive(Event[]) (partition/PartitionStreamReceiver.java:175-260)
+//      and the per-key state lookup (util/snapshot/state/PartitionStateHolder.java:43-80)
+//   3. k_p2_advance: one lane per key advances that key's NFA over its events in arrival order
+//      (query/input/stream/state/StreamPreStateProcessor.java:308-403 and friends)
+// and on poll orders the accumulated matches by trigger seq (stable: per-key emission order kept).
+#include <hip/hip_runtime.h>
+
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/siddhi_gpu.h"
+#include "../../include/siddhi_gpu_ir.h"
+#include "sg_engine.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+struct HipError : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+
+#define HIP_OK(x)                                                                                       \
+    do {                                                                                                \
+        hipError_t e_ = (x);                                                                            \
+        if (e_ != hipSuccess)                                                                           \
+            throw HipError(std::string(#x) + ": " + hipGetErrorString(e_));                             \
+    } while (0)
+
+struct IRStream {
+    std::vector<uint32_t> types;
+};
+
+// P2 plan: the lowered two-state query
+struct Plan {
+    int mode = 0;
+    int s0 = -1, s1 = -1;     // stream of state 0 / 1
+    uint32_t slot0 = 0, slot1 = 1;
+    int64_t within = -1;
+    bool partitioned = false;
+    // per stream: event columns the kernel loads (attr indices)
+    std::vector<std::vector<uint32_t>> evcols;
+    std::vector<uint32_t> caps;          // slot-0 attrs captured into partials
+    std::vector<uint8_t> cap_col;        // index of each capture in evcols[s0]
+    DProg f0{}, f1{};
+};
+
+uint32_t bits_for(uint64_t n) {
+    uint32_t b = 1;
+    while (b < 64 && (1ull << b) < n) b++;
+    return b;
+}
+
+template <class T> T* dalloc(size_t n, std::vector<void*>& owned) {
+    void* p = nullptr;
+    if (n == 0) n = 1;
+    HIP_OK(hipMalloc(&p, n * sizeof(T)));
+    owned.push_back(p);
+    return (T*)p;
+}
+
+size_t type_size(uint32_t t) {
+    switch (t) {
+    case SG_T_LONG: case SG_T_DOUBLE: return 8;
+    case SG_T_BOOL: return 1;
+    default: return 4;
+    }
+}
+
+}  // namespace
+
+struct sg_engine {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    sg_config cfg{};
+    std::vector<uint32_t> ir;
+    std::vector<IRStream> streams;
+    Plan plan;
+    uint32_t K = 1, cap = 64, maxb = 0;
+    uint64_t mcap = 0;
+    std::vector<void*> owned;
+
+    // state
+    uint32_t* hdr = nullptr;
+    int64_t* p_ts = nullptr;
+    uint64_t* p_seq = nullptr;
+    uint64_t* p_cap = nullptr;
+    uint32_t* p_capnull = nullptr;
+    bool nullable = false;
+    // batch staging
+    int64_t* b_ts = nullptr;
+    uint32_t* b_key = nullptr;
+    std::vector<void*> b_cols;      // per attr slot (max attrs over streams)
+    std::vector<uint8_t*> b_nulls;
+    uint32_t* skeys = nullptr;
+    uint32_t* sidx = nullptr;
+    uint32_t* seg_begin = nullptr;
+    uint32_t* seg_end = nullptr;
+    uint32_t* iota = nullptr;
+    void* sort_tmp = nullptr;
+    size_t sort_tmp_bytes = 0;
+    // matches
+    uint64_t* m_trig = nullptr;
+    uint64_t* m_e1 = nullptr;
+    uint32_t* m_key = nullptr;
+    int64_t* m_ts = nullptr;
+    unsigned long long* m_count = nullptr;
+    unsigned long long* stats = nullptr;
+    uint32_t* err = nullptr;
+    // ordered output
+    uint32_t* o_rel = nullptr;
+    uint32_t* o_rel2 = nullptr;
+    uint32_t* o_perm = nullptr;
+    uint64_t* o_trig = nullptr;
+    uint64_t* o_slot = nullptr;
+    uint32_t* o_key = nullptr;
+    int64_t* o_ts = nullptr;
+    uint32_t* o_len = nullptr;
+    void* order_tmp = nullptr;
+    size_t order_tmp_bytes = 0;
+    // host copies
+    std::vector<uint64_t> h_trig, h_slot;
+    std::vector<uint32_t> h_key, h_len;
+    std::vector<int64_t> h_ts;
+    uint64_t poll_base = 0;
+    bool have_base = false;
+    uint64_t next_seq = 0;
+    bool held = false;
+    sg_stats st{};
+    // SG_CFG_TIMING: event pairs per stage, resolved at the next synchronisation point
+    struct Span { hipEvent_t a, b; int stage; };
+    std::vector<Span> spans;
+    std::vector<hipEvent_t> free_events;
+    bool timing = false;
+
+    hipEvent_t ev() {
+        hipEvent_t x;
+        if (!free_events.empty()) { x = free_events.back(); free_events.pop_back(); return x; }
+        if (hipEventCreate(&x) != hipSuccess) throw std::runtime_error("hipEventCreate failed");
+        return x;
+    }
+    void mark(hipEvent_t x) {
+        if (hipEventRecord(x, stream) != hipSuccess) throw std::runtime_error("hipEventRecord failed");
+    }
+    void resolve_spans() {  // call after the stream is synchronised
+        for (auto& s : spans) {
+            float ms = 0.f;
+            if (hipEventElapsedTime(&ms, s.a, s.b) == hipSuccess) {
+                uint64_t ns = (uint64_t)((double)ms * 1e6);
+                if (s.stage == 0) st.group_ns += ns;
+                else if (s.stage == 1) st.advance_ns += ns;
+                else st.order_ns += ns;
+            }
+            free_events.push_back(s.a);
+            free_events.push_back(s.b);
+        }
+        spans.clear();
+    }
+
+    ~sg_engine() {
+        if (device >= 0) (void)hipSetDevice(device);
+        if (stream) (void)hipStreamSynchronize(stream);
+        for (auto& sp : spans) { (void)hipEventDestroy(sp.a); (void)hipEventDestroy(sp.b); }
+        for (auto x : free_events) (void)hipEventDestroy(x);
+        for (void* p : owned) (void)hipFree(p);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
+namespace {
+
+// ------------------------------------------------------------------------------------------------
+// IR -> Plan (two-state pattern shapes)
+// ------------------------------------------------------------------------------------------------
+struct Node {
+    uint32_t tag = 0;
+    uint32_t slot = 0, stream = 0, fpc = 0, flen = 0, absent = 0;
+    uint32_t a = 0, b = 0;  // logical type / count min,max
+    std::vector<Node> kids;
+};
+
+Node read_node(const uint32_t* w, size_t n, size_t& pos) {
+    if (pos >= n) throw std::runtime_error("truncated IR node tree");
+    Node x;
+    x.tag = w[pos++];
+    switch (x.tag) {
+    case SG_N_STREAM:
+        if (pos + 7 > n) throw std::runtime_error("truncated IR node");
+        x.slot = w[pos]; x.stream = w[pos + 1]; x.fpc = w[pos + 2]; x.flen = w[pos + 3]; x.absent = w[pos + 4];
+        pos += 7;
+        break;
+    case SG_N_NEXT: x.kids.push_back(read_node(w, n, pos)); x.kids.push_back(read_node(w, n, pos)); break;
+    case SG_N_EVERY: x.kids.push_back(read_node(w, n, pos)); break;
+    case SG_N_LOGICAL: x.a = w[pos++]; x.kids.push_back(read_node(w, n, pos)); x.kids.push_back(read_node(w, n, pos)); break;
+    case SG_N_COUNT: x.a = w[pos++]; x.b = w[pos++]; x.kids.push_back(read_node(w, n, pos)); break;
+    default: throw std::runtime_error("bad IR node tag");
+    }
+    return x;
+}
+
+uint32_t col_index(std::vector<uint32_t>& cols, uint32_t attr) {
+    for (size_t i = 0; i < cols.size(); i++)
+        if (cols[i] == attr) return (uint32_t)i;
+    if (cols.size() >= SGD_MAX_EVCOLS) throw std::runtime_error("filters read too many attributes");
+    cols.push_back(attr);
+    return (uint32_t)cols.size() - 1;
+}
+
+// lower one filter's bytecode: `own` = slot of the state the filter belongs to
+void lower_filter(const uint32_t* code, uint32_t pc, uint32_t len, uint32_t own, Plan& pl,
+                  std::vector<uint32_t>& evcols, DProg& out, bool is_state1) {
+    out = DProg{};
+    uint32_t end = pc + len;
+    int sp = 0, maxsp = 0;
+    while (pc < end) {
+        uint32_t w = code[pc];
+        uint32_t op = w & 0xff, a = (w >> 8) & 0xff, b = (w >> 16) & 0xff;
+        if (out.len >= SGD_MAX_PROG) throw std::runtime_error("filter program too long for the device");
+        DInst I{};
+        I.op = (uint8_t)op;
+        switch (op) {
+        case SG_OP_VAR: {
+            uint32_t attr = code[pc + 1];
+            int32_t chain = (int32_t)code[pc + 2];
+            bool single = (chain == 0 || chain == -1);  // a stream slot holds exactly one event
+            I.t = (uint8_t)a;
+            if (!single) {
+                I.src = SGD_SRC_NULL;
+            } else if (b == own) {
+                I.src = SGD_SRC_EV;
+                I.arg = (int32_t)col_index(evcols, attr);
+            } else if (is_state1 && b == pl.slot0) {
+                I.src = SGD_SRC_CAP;
+                uint32_t ci = 0;
+                for (; ci < pl.caps.size(); ci++)
+                    if (pl.caps[ci] == attr) break;
+                if (ci == pl.caps.size()) {
+                    if (pl.caps.size() >= SGD_MAX_CAPS) throw std::runtime_error("too many captured attributes");
+                    pl.caps.push_back(attr);
+                }
+                I.arg = (int32_t)ci;
+            } else {
+                throw std::runtime_error("filter refers to a state that is not visible");
+            }
+            sp++;
+            break;
+        }
+        case SG_OP_CONST:
+            I.t = (uint8_t)a;
+            I.t2 = (uint8_t)(b != 0);
+            I.imm = (uint64_t)code[pc + 1] | ((uint64_t)code[pc + 2] << 32);
+            sp++;
+            break;
+        case SG_OP_ISNULL_EV: {
+            int32_t chain = (int32_t)code[pc + 1];
+            bool exists = (chain == 0 || chain == -1) && (b == own || (is_state1 && b == pl.slot0));
+            I.op = SG_OP_CONST;
+            I.t = SG_T_BOOL;
+            I.imm = exists ? 0 : 1;
+            sp++;
+            break;
+        }
+        case SG_OP_CVT: I.t = (uint8_t)a; I.t2 = (uint8_t)b; break;
+        case SG_OP_ADD: case SG_OP_SUB: case SG_OP_MUL: case SG_OP_DIV: case SG_OP_MOD:
+        case SG_OP_EQ: case SG_OP_NE: case SG_OP_GT: case SG_OP_GE: case SG_OP_LT: case SG_OP_LE:
+        case SG_OP_AND: case SG_OP_OR:
+            I.t = (uint8_t)a;
+            sp--;
+            break;
+        case SG_OP_NOT: case SG_OP_ISNULL: break;
+        default: throw std::runtime_error("unknown bytecode op");
+        }
+        maxsp = std::max(maxsp, sp);
+        out.ins[out.len++] = I;
+        pc += sg_op_len(op);
+    }
+    if (maxsp > SGD_MAX_STACK) throw std::runtime_error("filter expression too deep for the device");
+}
+
+void build_plan(sg_engine* e, const void* ir, size_t len) {
+    if (len < SG_IR_HDR_WORDS * 4 || len % 4) throw std::runtime_error("IR too short");
+    e->ir.assign((const uint32_t*)ir, (const uint32_t*)ir + len / 4);
+    const uint32_t* w = e->ir.data();
+    size_t nw = e->ir.size();
+    if (w[0] != SG_IR_MAGIC || w[1] != SG_IR_VERSION) throw std::runtime_error("bad IR magic/version");
+    uint32_t qtype = w[2], nstreams = w[3], nslots = w[4];
+    int64_t within = (int64_t)((uint64_t)w[5] | ((uint64_t)w[6] << 32));
+    uint32_t offS = w[7], offN = w[8], nN = w[9], offC = w[10], nC = w[11];
+    if (offN + nN > nw || offC + nC > nw || offS > nw) throw std::runtime_error("IR offsets out of range");
+    Plan& pl = e->plan;
+    pl.partitioned = (w[12] & SG_IR_F_PARTITIONED) != 0;
+    pl.within = within;
+    size_t p = offS;
+    e->streams.resize(nstreams);
+    for (uint32_t s = 0; s < nstreams; s++) {
+        if (p >= nw) throw std::runtime_error("IR stream table truncated");
+        uint32_t na = w[p++];
+        if (p + na > nw) throw std::runtime_error("IR stream table truncated");
+        e->streams[s].types.assign(w + p, w + p + na);
+        p += na;
+    }
+    size_t pos = 0;
+    Node root = read_node(w + offN, nN, pos);
+    if (qtype != SG_Q_PATTERN)
+        throw std::runtime_error("HIP engine: SEQUENCE queries are not on the device yet (oracle only)");
+    if (nslots != 2) throw std::runtime_error("HIP engine: only two-state patterns run on the device so far");
+    const Node *a = nullptr, *b = nullptr;
+    if (root.tag == SG_N_NEXT) {
+        const Node& x = root.kids[0];
+        if (x.tag == SG_N_EVERY && x.kids[0].tag == SG_N_STREAM) {
+            a = &x.kids[0];
+            pl.mode = SGD_P2_EVERY_FIRST;
+        } else if (x.tag == SG_N_STREAM) {
+            a = &x;
+            pl.mode = 0;
+        }
+        if (root.kids[1].tag == SG_N_STREAM) b = &root.kids[1];
+    } else if (root.tag == SG_N_EVERY && root.kids[0].tag == SG_N_NEXT &&
+               root.kids[0].kids[0].tag == SG_N_STREAM && root.kids[0].kids[1].tag == SG_N_STREAM) {
+        a = &root.kids[0].kids[0];
+        b = &root.kids[0].kids[1];
+        pl.mode = SGD_P2_EVERY_BOTH;
+    }
+    if (!a || !b) throw std::runtime_error("HIP engine: pattern shape not supported on the device yet");
+    if (a->absent || b->absent) throw std::runtime_error("HIP engine: absent states are not on the device yet");
+    pl.s0 = (int)a->stream;
+    pl.s1 = (int)b->stream;
+    pl.slot0 = a->slot;
+    pl.slot1 = b->slot;
+    if ((int)nstreams <= std::max(pl.s0, pl.s1)) throw std::runtime_error("IR stream index out of range");
+    pl.evcols.assign(nstreams, {});
+    const uint32_t* code = w + offC;
+    if (a->fpc + a->flen > nC || b->fpc + b->flen > nC) throw std::runtime_error("IR filter out of range");
+    lower_filter(code, b->fpc, b->flen, b->slot, pl, pl.evcols[pl.s1], pl.f1, true);
+    lower_filter(code, a->fpc, a->flen, a->slot, pl, pl.evcols[pl.s0], pl.f0, false);
+    for (uint32_t attr : pl.caps) pl.cap_col.push_back((uint8_t)col_index(pl.evcols[pl.s0], attr));
+    for (size_t s = 0; s < nstreams; s++)
+        for (uint32_t attr : pl.evcols[s])
+            if (attr >= e->streams[s].types.size()) throw std::runtime_error("attribute index out of range");
+}
+
+void allocate(sg_engine* e) {
+    const size_t K = e->K, C = e->cap, B = e->maxb, M = e->mcap;
+    auto& o = e->owned;
+    e->hdr = dalloc<uint32_t>(K, o);
+    HIP_OK(hipMemset(e->hdr, 0, K * 4));
+    e->p_ts = dalloc<int64_t>(C * K, o);
+    e->p_seq = dalloc<uint64_t>(C * K, o);
+    e->p_cap = dalloc<uint64_t>(std::max<size_t>(1, e->plan.caps.size()) * C * K, o);
+    e->p_capnull = dalloc<uint32_t>(C * K, o);
+    HIP_OK(hipMemset(e->p_capnull, 0, C * K * 4));
+    e->b_ts = dalloc<int64_t>(B, o);
+    e->b_key = dalloc<uint32_t>(B, o);
+    size_t maxattr = 0;
+    for (auto& s : e->streams) maxattr = std::max(maxattr, s.types.size());
+    for (size_t a = 0; a < maxattr; a++) {
+        e->b_cols.push_back(dalloc<uint64_t>(B, o));
+        e->b_nulls.push_back(dalloc<uint8_t>(B, o));
+    }
+    e->skeys = dalloc<uint32_t>(B, o);
+    e->sidx = dalloc<uint32_t>(B, o);
+    e->iota = dalloc<uint32_t>(B, o);
+    {
+        std::vector<uint32_t> h(B);
+        for (size_t i = 0; i < B; i++) h[i] = (uint32_t)i;
+        HIP_OK(hipMemcpy(e->iota, h.data(), B * 4, hipMemcpyHostToDevice));
+    }
+    e->seg_begin = dalloc<uint32_t>(K, o);
+    e->seg_end = dalloc<uint32_t>(K, o);
+    HIP_OK(rocprim::radix_sort_pairs(nullptr, e->sort_tmp_bytes, e->b_key, e->skeys, e->iota, e->sidx,
+                                     (uint32_t)B, 0, 32, e->stream));
+    e->sort_tmp = dalloc<uint8_t>(e->sort_tmp_bytes, o);
+    e->m_trig = dalloc<uint64_t>(M, o);
+    e->m_e1 = dalloc<uint64_t>(M, o);
+    e->m_key = dalloc<uint32_t>(M, o);
+    e->m_ts = dalloc<int64_t>(M, o);
+    e->m_count = dalloc<unsigned long long>(1, o);
+    e->stats = dalloc<unsigned long long>(SGD_ST_N, o);
+    e->err = dalloc<uint32_t>(1, o);
+    HIP_OK(hipMemset(e->m_count, 0, 8));
+    HIP_OK(hipMemset(e->stats, 0, SGD_ST_N * 8));
+    HIP_OK(hipMemset(e->err, 0, 4));
+    e->o_rel = dalloc<uint32_t>(M, o);
+    e->o_rel2 = dalloc<uint32_t>(M, o);
+    e->o_perm = dalloc<uint32_t>(M, o);
+    e->o_trig = dalloc<uint64_t>(M, o);
+    e->o_slot = dalloc<uint64_t>(2 * M, o);
+    e->o_key = dalloc<uint32_t>(M, o);
+    e->o_ts = dalloc<int64_t>(M, o);
+    e->o_len = dalloc<uint32_t>(2 * M, o);
+    HIP_OK(rocprim::radix_sort_pairs(nullptr, e->order_tmp_bytes, e->o_rel, e->o_rel2,
+                                     rocprim::counting_iterator<uint32_t>(0), e->o_perm, (uint32_t)M, 0, 32,
+                                     e->stream));
+    e->order_tmp = dalloc<uint8_t>(e->order_tmp_bytes, o);
+    HIP_OK(hipDeviceSynchronize());
+}
+
+int push(sg_engine* e, const sg_batch* b) {
+    const Plan& pl = e->plan;
+    if (b->stream >= e->streams.size()) return fail(SG_ERR_INVALID, "stream index out of range");
+    const auto& types = e->streams[b->stream].types;
+    if (b->n_cols != types.size()) return fail(SG_ERR_INVALID, "column count does not match the stream");
+    if (b->n == 0) return SG_OK;
+    if (b->n > e->maxb) return fail(SG_ERR_INVALID, "batch larger than max_batch");
+    if (pl.partitioned && !b->key) return fail(SG_ERR_INVALID, "partitioned query needs key ids");
+    if (!b->ts) return fail(SG_ERR_INVALID, "timestamps missing");
+    if (e->have_base && b->seq_base < e->next_seq) return fail(SG_ERR_INVALID, "sequence numbers must increase");
+    if (e->held) return fail(SG_ERR_STATE, "release the polled matches before pushing");
+    const bool is0 = (int)b->stream == pl.s0, is1 = (int)b->stream == pl.s1;
+    if (!is0 && !is1) return SG_OK;  // stream not read by this query
+    const uint32_t n = (uint32_t)b->n;
+    if (!e->have_base) {
+        e->poll_base = b->seq_base;
+        e->have_base = true;
+    }
+    e->next_seq = b->seq_base + b->n;
+    e->st.events += b->n;
+    e->st.batches++;
+
+    const auto& cols = pl.evcols[b->stream];
+    const bool dev = b->mem == SG_MEM_DEVICE;
+    const hipMemcpyKind kind = dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    P2Params p{};
+    p.n_keys = e->K;
+    p.cap = e->cap;
+    p.mode = (uint32_t)pl.mode;
+    p.multi = pl.s0 == pl.s1;
+    p.is_s0 = is0;
+    p.is_s1 = is1;
+    p.within = pl.within;
+    p.n = n;
+    p.seq_base = b->seq_base;
+    // timestamps / key ids / the columns the filters read
+    if (dev) {
+        p.ts = b->ts;
+    } else {
+        HIP_OK(hipMemcpyAsync(e->b_ts, b->ts, (size_t)n * 8, kind, e->stream));
+        p.ts = e->b_ts;
+    }
+    bool any_null = false;
+    p.n_evcols = (uint32_t)cols.size();
+    for (size_t c = 0; c < cols.size(); c++) {
+        uint32_t attr = cols[c];
+        p.evtype[c] = (uint8_t)types[attr];
+        if (dev) {
+            p.evcol[c] = b->cols[attr];
+            p.evnull[c] = b->nulls ? b->nulls[attr] : nullptr;
+        } else {
+            HIP_OK(hipMemcpyAsync(e->b_cols[c], b->cols[attr], (size_t)n * type_size(types[attr]), kind, e->stream));
+            p.evcol[c] = e->b_cols[c];
+            p.evnull[c] = nullptr;
+            if (b->nulls && b->nulls[attr]) {
+                HIP_OK(hipMemcpyAsync(e->b_nulls[c], b->nulls[attr], n, kind, e->stream));
+                p.evnull[c] = e->b_nulls[c];
+            }
+        }
+        if (p.evnull[c]) any_null = true;
+    }
+    if (any_null) e->nullable = true;
+    // grouping by key
+    hipEvent_t g0 = nullptr, g1 = nullptr;
+    if (e->timing) { g0 = e->ev(); e->mark(g0); }
+    if (pl.partitioned) {
+        const uint32_t* keys = b->key;
+        if (!dev) {
+            for (uint32_t i = 0; i < n; i++)
+                if (b->key[i] >= e->K) return fail(SG_ERR_INVALID, "key id outside [0, n_keys)");
+            HIP_OK(hipMemcpyAsync(e->b_key, b->key, (size_t)n * 4, kind, e->stream));
+            keys = e->b_key;
+        }
+        size_t tmp = e->sort_tmp_bytes;
+        HIP_OK(rocprim::radix_sort_pairs(e->sort_tmp, tmp, keys, e->skeys, e->iota, e->sidx, n, 0,
+                                         bits_for(e->K), e->stream));
+        HIP_OK(hipMemsetAsync(e->seg_begin, 0, (size_t)e->K * 4, e->stream));
+        HIP_OK(hipMemsetAsync(e->seg_end, 0, (size_t)e->K * 4, e->stream));
+        if (sgd_launch_bounds(e->skeys, n, e->K, e->seg_begin, e->seg_end, e->err, e->stream) != 0)
+            throw HipError("k_seg_bounds launch failed");
+        p.sorted_idx = e->sidx;
+    } else {
+        const uint32_t z = 0;
+        HIP_OK(hipMemcpyAsync(e->seg_begin, &z, 4, hipMemcpyHostToDevice, e->stream));
+        HIP_OK(hipMemcpyAsync(e->seg_end, &n, 4, hipMemcpyHostToDevice, e->stream));
+        HIP_OK(hipStreamSynchronize(e->stream));  // &n / &z are stack values
+        p.sorted_idx = e->iota;
+    }
+    if (e->timing) { g1 = e->ev(); e->mark(g1); e->spans.push_back({g0, g1, 0}); }
+    p.seg_begin = e->seg_begin;
+    p.seg_end = e->seg_end;
+    p.hdr = e->hdr;
+    p.p_ts = e->p_ts;
+    p.p_seq = e->p_seq;
+    p.p_cap = e->p_cap;
+    p.p_capnull = e->p_capnull;
+    p.n_caps = (uint32_t)pl.caps.size();
+    p.nullable = e->nullable;
+    for (size_t c = 0; c < pl.cap_col.size(); c++) p.cap_col[c] = pl.cap_col[c];
+    p.m_trig = e->m_trig;
+    p.m_e1 = e->m_e1;
+    p.m_key = e->m_key;
+    p.m_ts = e->m_ts;
+    p.m_count = e->m_count;
+    p.m_capacity = e->mcap;
+    p.stats = e->stats;
+    p.err = e->err;
+    p.f0 = pl.f0;
+    p.f1 = pl.f1;
+    hipEvent_t a0 = nullptr, a1 = nullptr;
+    if (e->timing) { a0 = e->ev(); e->mark(a0); }
+    if (sgd_launch_p2(p, e->stream) != 0) throw HipError("k_p2_advance launch failed");
+    if (e->timing) { a1 = e->ev(); e->mark(a1); e->spans.push_back({a0, a1, 1}); }
+    e->st.advance_launches++;
+    if (!dev) HIP_OK(hipStreamSynchronize(e->stream));  // host buffers may be reused by the caller
+    return SG_OK;
+}
+
+int poll(sg_engine* e, uint32_t mem, sg_match_batch* out) {
+    if (e->held) return fail(SG_ERR_STATE, "previous matches not released");
+    unsigned long long n = 0;
+    uint32_t err = 0;
+    HIP_OK(hipMemcpyAsync(&n, e->m_count, 8, hipMemcpyDeviceToHost, e->stream));
+    HIP_OK(hipMemcpyAsync(&err, e->err, 4, hipMemcpyDeviceToHost, e->stream));
+    HIP_OK(hipStreamSynchronize(e->stream));
+    if (err & SGD_ERR_KEY_RANGE) return fail(SG_ERR_INVALID, "a batch carried key ids outside [0, n_keys)");
+    if (err & SGD_ERR_PARTIAL_CAP)
+        return fail(SG_ERR_CAPACITY, "a partition key exceeded partial_capacity live partial matches");
+    if ((err & SGD_ERR_MATCH_CAP) || n > e->mcap)
+        return fail(SG_ERR_CAPACITY, "more matches than match_capacity between two polls");
+    e->resolve_spans();
+    const uint32_t* perm = nullptr;
+    hipEvent_t o0 = nullptr, o1 = nullptr;
+    if (e->timing) { o0 = e->ev(); e->mark(o0); }
+    if (n > 1 && !(e->cfg.flags & SG_CFG_NO_ORDER)) {
+        uint64_t span = e->next_seq - e->poll_base;
+        if (span >= (1ull << 32)) return fail(SG_ERR_CAPACITY, "poll window spans more than 2^32 events");
+        if (sgd_launch_rel_keys(e->m_trig, e->poll_base, n, e->o_rel, e->stream) != 0)
+            throw HipError("k_rel_keys launch failed");
+        size_t tmp = e->order_tmp_bytes;
+        HIP_OK(rocprim::radix_sort_pairs(e->order_tmp, tmp, e->o_rel, e->o_rel2,
+                                         rocprim::counting_iterator<uint32_t>(0), e->o_perm, (uint32_t)n, 0,
+                                         bits_for(span + 1), e->stream));
+        perm = e->o_perm;
+    }
+    if (sgd_launch_order(e->m_trig, e->m_e1, e->m_key, e->m_ts, perm, n, e->o_trig, e->o_slot, e->o_key, e->o_ts,
+                         e->o_len, e->stream) != 0)
+        throw HipError("k_order launch failed");
+    if (e->timing) { o1 = e->ev(); e->mark(o1); e->spans.push_back({o0, o1, 2}); }
+    out->n = n;
+    out->n_slots = 2;
+    out->max_chain = 1;
+    out->reserved = 0;
+    if (mem == SG_MEM_DEVICE) {
+        out->trigger_seq = e->o_trig;
+        out->slot_seq = e->o_slot;
+        out->key = e->o_key;
+        out->ts = e->o_ts;
+        out->chain_len = e->o_len;
+        out->mem = SG_MEM_DEVICE;
+    } else {
+        e->h_trig.resize(n);
+        e->h_slot.resize(2 * n);
+        e->h_key.resize(n);
+        e->h_ts.resize(n);
+        e->h_len.resize(2 * n);
+        if (n) {
+            HIP_OK(hipMemcpyAsync(e->h_trig.data(), e->o_trig, n * 8, hipMemcpyDeviceToHost, e->stream));
+            HIP_OK(hipMemcpyAsync(e->h_slot.data(), e->o_slot, 2 * n * 8, hipMemcpyDeviceToHost, e->stream));
+            HIP_OK(hipMemcpyAsync(e->h_key.data(), e->o_key, n * 4, hipMemcpyDeviceToHost, e->stream));
+            HIP_OK(hipMemcpyAsync(e->h_ts.data(), e->o_ts, n * 8, hipMemcpyDeviceToHost, e->stream));
+            HIP_OK(hipMemcpyAsync(e->h_len.data(), e->o_len, 2 * n * 4, hipMemcpyDeviceToHost, e->stream));
+            HIP_OK(hipStreamSynchronize(e->stream));
+        }
+        out->trigger_seq = e->h_trig.data();
+        out->slot_seq = e->h_slot.data();
+        out->key = e->h_key.data();
+        out->ts = e->h_ts.data();
+        out->chain_len = e->h_len.data();
+        out->mem = SG_MEM_HOST;
+    }
+    // the window restarts after this poll
+    HIP_OK(hipMemsetAsync(e->m_count, 0, 8, e->stream));
+    e->poll_base = e->next_seq;
+    e->held = true;
+    return SG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* sg_last_error(void) { return g_err.c_str(); }
+int sg_abi_version(void) { return SG_ABI_VERSION; }
+
+int sg_engine_create(const void* ir, size_t ir_len, const sg_config* cfg, sg_engine** out) {
+    if (!ir || !out || !cfg) return fail(SG_ERR_INVALID, "null argument");
+    if (cfg->struct_size < sizeof(sg_config)) return fail(SG_ERR_INVALID, "sg_config too small");
+    sg_engine* e = nullptr;
+    try {
+        e = new sg_engine();
+        e->cfg = *cfg;
+        e->device = cfg->device;
+        e->timing = (cfg->flags & SG_CFG_TIMING) != 0;
+        e->K = cfg->n_keys ? cfg->n_keys : 1;
+        e->cap = cfg->partial_capacity ? cfg->partial_capacity : 64;
+        e->maxb = cfg->max_batch ? cfg->max_batch : (1u << 20);
+        e->mcap = cfg->match_capacity ? cfg->match_capacity : (uint64_t)e->maxb * 4;
+        if (e->cap > SGD_MAX_CAP) throw std::invalid_argument("partial_capacity above 4095");
+        if (e->mcap >= (1ull << 32)) throw std::invalid_argument("match_capacity must be < 2^32");
+        build_plan(e, ir, ir_len);
+        if (!e->plan.partitioned && e->K != 1) e->K = 1;
+        int ndev = 0;
+        HIP_OK(hipGetDeviceCount(&ndev));
+        if (cfg->device < 0 || cfg->device >= ndev) throw HipError("no such HIP device");
+        HIP_OK(hipSetDevice(cfg->device));
+        HIP_OK(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+        allocate(e);
+        *out = e;
+        return SG_OK;
+    } catch (const HipError& ex) {
+        delete e;
+        return fail(SG_ERR_DEVICE, ex.what());
+    } catch (const std::invalid_argument& ex) {
+        delete e;
+        return fail(SG_ERR_INVALID, ex.what());
+    } catch (const std::exception& ex) {
+        delete e;
+        return fail(SG_ERR_UNSUPPORTED, ex.what());
+    }
+}
+
+void sg_engine_destroy(sg_engine* e) { delete e; }
+
+int sg_push_batch(sg_engine* e, const sg_batch* b) {
+    if (!e || !b) return fail(SG_ERR_INVALID, "null argument");
+    try {
+        HIP_OK(hipSetDevice(e->device));
+        return push(e, b);
+    } catch (const std::exception& ex) {
+        return fail(SG_ERR_DEVICE, ex.what());
+    }
+}
+
+int sg_advance_time(sg_engine* e, int64_t now_ms) {
+    (void)now_ms;
+    if (!e) return fail(SG_ERR_INVALID, "null argument");
+    return SG_OK;  // no absent (timer) states on the device yet; nothing is time driven
+}
+
+int sg_poll_matches(sg_engine* e, uint32_t mem, sg_match_batch* out) {
+    if (!e || !out) return fail(SG_ERR_INVALID, "null argument");
+    try {
+        HIP_OK(hipSetDevice(e->device));
+        return poll(e, mem, out);
+    } catch (const std::exception& ex) {
+        return fail(SG_ERR_DEVICE, ex.what());
+    }
+}
+
+int sg_release_matches(sg_engine* e, sg_match_batch* m) {
+    if (!e) return fail(SG_ERR_INVALID, "null argument");
+    e->held = false;
+    if (m) memset(m, 0, sizeof(*m));
+    return SG_OK;
+}
+
+int sg_synchronize(sg_engine* e) {
+    if (!e) return fail(SG_ERR_INVALID, "null argument");
+    try {
+        HIP_OK(hipSetDevice(e->device));
+        HIP_OK(hipStreamSynchronize(e->stream));
+        e->resolve_spans();
+        return SG_OK;
+    } catch (const std::exception& ex) {
+        return fail(SG_ERR_DEVICE, ex.what());
+    }
+}
+
+int sg_get_stats(sg_engine* e, sg_stats* out) {
+    if (!e || !out) return fail(SG_ERR_INVALID, "null argument");
+    try {
+        HIP_OK(hipSetDevice(e->device));
+        unsigned long long s[SGD_ST_N];
+        HIP_OK(hipMemcpyAsync(s, e->stats, sizeof(s), hipMemcpyDeviceToHost, e->stream));
+        HIP_OK(hipStreamSynchronize(e->stream));
+        e->resolve_spans();
+        *out = e->st;
+        out->partials_scanned = s[SGD_ST_SCANNED];
+        out->partials_created = s[SGD_ST_CREATED];
+        out->matches = s[SGD_ST_MATCHES];
+        out->keys_touched = s[SGD_ST_KEYS];
+        out->live_at_batch_start = s[SGD_ST_LIVE0];
+        // live partials now: sum of the headers' counts (host reduction; diagnostics only)
+        std::vector<uint32_t> h(e->K);
+        HIP_OK(hipMemcpy(h.data(), e->hdr, (size_t)e->K * 4, hipMemcpyDeviceToHost));
+        uint64_t live = 0;
+        for (uint32_t x : h) live += SGD_H_NPEND(x) + SGD_H_NSTG(x);
+        out->partials_live = live;
+        return SG_OK;
+    } catch (const std::exception& ex) {
+        return fail(SG_ERR_DEVICE, ex.what());
+    }
+}
+
+int sg_snapshot(sg_engine* e, void** buf, size_t* len) {
+    (void)e; (void)buf; (void)len;
+    return fail(SG_ERR_UNSUPPORTED, "snapshot of device NFA state is SURVEY §8f row f3 (not built yet)");
+}
+int sg_restore(sg_engine* e, const void* buf, size_t len) {
+    (void)e; (void)buf; (void)len;
+    return fail(SG_ERR_UNSUPPORTED, "restore of device NFA state is SURVEY §8f row f3 (not built yet)");
+}
+int sg_free_buffer(void* buf) {
+    free(buf);
+    return SG_OK;
+}
+
+}  // extern "C"

@@ -17,6 +17,7 @@ SG_MEM_HOST = 0
 SG_MEM_DEVICE = 1
 SG_NULL_SEQ = np.uint64(0xFFFFFFFFFFFFFFFF)
 SG_CFG_NO_ORDER = 1
+SG_CFG_TIMING = 2
 
 ERRORS = {-1: "SG_ERR_INVALID", -2: "SG_ERR_UNSUPPORTED", -3: "SG_ERR_DEVICE",
           -4: "SG_ERR_CAPACITY", -5: "SG_ERR_STATE"}
@@ -54,7 +55,8 @@ class sg_match_batch(C.Structure):
 class sg_stats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in ("events", "batches", "partials_scanned", "partials_created",
                                           "partials_live", "matches", "keys_touched",
-                                          "live_at_batch_start")]
+                                          "live_at_batch_start", "group_ns", "advance_ns", "order_ns",
+                                          "advance_launches")]
 
 
 @dataclass

@@ -1,0 +1,70 @@
+"""Synthetic stock-tick streams, stateless per event so any slice can be regenerated.
+
+Schema `StockStream (symbol string, price float, volume int)` (siddhi-samples PartitionSample.java:41)
+plus the event timestamp.  Every field of event i is a function of (seed, i) through splitmix64:
+
+    key    = h0 % n_keys                      (uniform; symbol id == key id)
+    price  = float32(10 + 30 * u),  u = (h1 >> 40) / 2^24      (price > 20 for ~2/3 of events)
+    volume = 1 + h2 % 2000
+    ts     = t0 + i // rate_per_ms            (global, non-decreasing)
+
+(The survey's per-key random walk is replaced by i.i.d. prices so that generation is stateless and
+identical for the host baseline and the device run; documented in DESIGN.md.)
+"""
+from __future__ import annotations
+
+import numpy as np
+
+C2_QUERY = """
+define stream StockStream (symbol string, price float, volume int);
+partition with (symbol of StockStream)
+begin
+  @info(name = 'query1')
+  from every e1=StockStream[price > 20] -> e2=StockStream[price > e1.price]
+       within 10 sec
+  select e1.symbol as symbol, e1.price as price1, e2.price as price2, e2.price - e1.price as d
+  insert into OutputStream;
+end;
+"""
+
+C1_QUERY = """
+define stream StockStream (symbol string, price float, volume int);
+@info(name = 'query1')
+from every e1=StockStream[price > 20] -> e2=StockStream[price > e1.price]
+     within 10 sec
+select e1.symbol as symbol, e1.price as price1, e2.price as price2, e2.price - e1.price as d
+insert into OutputStream;
+"""
+
+T0 = 1_700_000_000_000
+SEED = 0x5EED5EED
+
+_M1 = np.uint64(0xBF58476D1CE4E5B9)
+_M2 = np.uint64(0x94D049BB133111EB)
+_G = np.uint64(0x9E3779B97F4A7C15)
+
+
+def splitmix64(x: np.ndarray) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        z = x + _G
+        z = (z ^ (z >> np.uint64(30))) * _M1
+        z = (z ^ (z >> np.uint64(27))) * _M2
+        return z ^ (z >> np.uint64(31))
+
+
+def stock_ticks(start: int, n: int, n_keys: int, seed: int = SEED, rate_per_ms: int = 2000, t0: int = T0):
+    """Events [start, start + n) of the stream: dict of numpy arrays (key, ts, symbol, price, volume)."""
+    i = np.arange(start, start + n, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        base = np.uint64(seed) * np.uint64(0x100000001B3) if seed else np.uint64(0)
+    with np.errstate(over="ignore"):
+        s = (i * np.uint64(3) + base)
+        h0 = splitmix64(s)
+        h1 = splitmix64(s + np.uint64(1))
+        h2 = splitmix64(s + np.uint64(2))
+    key = (h0 % np.uint64(n_keys)).astype(np.uint32)
+    u = (h1 >> np.uint64(40)).astype(np.float64) / float(1 << 24)
+    price = (10.0 + 30.0 * u).astype(np.float32)
+    volume = (np.uint64(1) + h2 % np.uint64(2000)).astype(np.int32)
+    ts = (np.int64(t0) + (i // np.uint64(rate_per_ms)).astype(np.int64)).astype(np.int64)
+    return {"key": key, "ts": ts, "symbol": key.copy(), "price": price, "volume": volume}
