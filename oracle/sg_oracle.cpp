@@ -1257,9 +1257,16 @@ int sgo_release_matches(sgo_engine* h, sg_match_batch* m) {
 int sgo_get_stats(sgo_engine* h, sg_stats* out) {
     if (!h || !out) return fail(SG_ERR_INVALID, "null argument");
     Engine& e = h->e;
+    // live partial matches: StateEvents holding at least one event (start-state seeds excluded)
     uint64_t live = 0;
+    auto count = [&](const SEList& l) {
+        for (auto& se : l) {
+            for (auto& sl : se->slots)
+                if (sl) { live++; break; }
+        }
+    };
     for (auto& ks : e.keyStates)
-        for (auto& s : ks) live += s.pending.size() + s.newAndEvery.size();
+        for (auto& s : ks) { count(s.pending); count(s.newAndEvery); }
     e.stats.partials_live = live;
     *out = e.stats;
     return SG_OK;
