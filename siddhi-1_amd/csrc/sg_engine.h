@@ -8,12 +8,20 @@
 #define SGD_MAX_STACK 8    // filter evaluation stack depth
 #define SGD_MAX_EVCOLS 8   // event columns a query's filters read
 #define SGD_MAX_CAPS 8     // slot-0 attributes captured into a partial match
+#define SGD_MAX_ATOMS 4    // comparisons in a conjunctive predicate
 #define SGD_WAVE 64
+#define SGD_BLOCK 256      // lanes (= keys) per workgroup of the advance kernel
+#define SGD_RAW_CHUNK 2048 // raw match slots a wave reserves at a time
+#define SGD_STAGE_UNROLL 8 // 8-byte loads in flight per lane while staging a chunk
 
-// device filter program: the IR bytecode (siddhi_gpu_ir.h) with every variable resolved to where the
-// kernel finds it — a column of the current event, a captured attribute of the partial's slot-0 event,
-// or null (chain index outside a single-event slot)
-enum { SGD_SRC_EV = 0, SGD_SRC_CAP = 1, SGD_SRC_NULL = 2 };
+// ---- filters ------------------------------------------------------------------------------------
+// Every filter is lowered twice from the IR bytecode (siddhi_gpu_ir.h):
+//  * DPred: a conjunction of <= 4 typed comparisons whose operands are an event column, a captured
+//    slot-0 attribute or a constant already converted to the comparison domain.  Nearly every
+//    pattern filter has this form (`price > 20`, `price > e1.price and symbol == e1.symbol`); it is
+//    evaluated with wave-uniform scalar branches only.
+//  * DProg: the full stack program (every other filter), evaluated by a device interpreter.
+enum { SGD_SRC_EV = 0, SGD_SRC_CAP = 1, SGD_SRC_CONST = 2, SGD_SRC_NULL = 3 };
 
 struct DInst {
     uint8_t op;   // SG_OP_*
@@ -28,6 +36,37 @@ struct DProg {
     uint32_t len;
     uint32_t pad;
     DInst ins[SGD_MAX_PROG];
+};
+
+struct DOperand {
+    uint8_t kind;   // SGD_SRC_*
+    uint8_t from;   // type of the value before conversion to the domain
+    uint8_t idx;    // event column / capture index
+    uint8_t pad;
+    uint32_t pad2;
+    uint64_t bits;  // constant (already in the domain)
+};
+
+struct DAtom {
+    uint8_t op;     // SG_OP_EQ .. SG_OP_LE
+    uint8_t dom;    // comparison domain (sg_type)
+    uint8_t pad[6];
+    DOperand l, r;
+};
+
+// DAtom packed into one word: op-EQ | dom<<4 | lkind<<8 | lfrom<<12 | lidx<<16 | rkind<<20 | rfrom<<24 |
+// ridx<<28, plus the bits of the (at most one) constant operand
+struct DPredPacked {
+    uint32_t n;
+    uint32_t prog;      // 1: not conjunctive, evaluate the stack program
+    uint32_t code[SGD_MAX_ATOMS];
+    uint64_t cbits[SGD_MAX_ATOMS];
+};
+
+struct DPred {
+    uint32_t use_prog;  // 1: not conjunctive, evaluate the DProg
+    uint32_t n_atoms;   // 0 = no filter (always true)
+    DAtom atoms[SGD_MAX_ATOMS];
 };
 
 // two-state pattern shapes handled by the P2 kernel family
@@ -67,29 +106,44 @@ struct P2Params {
     const void* evcol[SGD_MAX_EVCOLS];
     const uint8_t* evnull[SGD_MAX_EVCOLS];
     uint8_t evtype[SGD_MAX_EVCOLS];
-    const uint32_t* sorted_idx;   // batch positions grouped by key, arrival order inside a key
-    const uint32_t* seg_begin;    // [n_keys]
-    const uint32_t* seg_end;      // [n_keys]
+    uint8_t ev_word[SGD_MAX_EVCOLS];   // first LDS word of column c
+    uint32_t n_evwords;                // 32-bit LDS words per staged event (64-bit columns take two)
+    uint32_t chunk;                    // events staged in LDS per pass
+    uint32_t any_null;                 // the batch carries null flags
+    uint32_t lds_slots;                // partial-match window per lane in LDS
+    uint32_t dbg;                      // profiling ablation switches (SGD_DBG), 0 in production
+    unsigned long long* dbg_out;       // per-wave section stamps (dbg & 64)
+    const uint32_t* sorted_idx;        // batch positions grouped by key, arrival order inside a key
+    const uint32_t* payload;           // or: key-sorted events with payload [idx][cols..][ts] (NULL: gather)
+    uint32_t pay_stride;               // words per payload element ([idx][cols..][ts]; even)
+    uint32_t lds_stride;               // words per staged event in LDS (pay_stride (+2 with null bits))
+    const uint32_t* seg_begin;         // [n_keys]
+    const uint32_t* seg_end;           // [n_keys]
     // per-key state (SoA, partial j of key k at j * n_keys + k)
     uint32_t* hdr;
     int64_t* p_ts;
     uint64_t* p_seq;
-    uint64_t* p_cap;              // [n_caps][cap][n_keys]
-    uint32_t* p_capnull;          // [cap][n_keys] null bits of the captures
+    uint32_t* p_capw;                  // [n_capw][cap][n_keys] captured attribute words
+    uint32_t* p_capnull;               // [cap][n_keys] null bits of the captures
     uint32_t n_caps;
-    uint32_t nullable;            // capture null bits are live
-    uint8_t cap_col[SGD_MAX_CAPS];// event column captured into capture c
-    // matches (appended)
-    uint64_t* m_trig;
-    uint64_t* m_e1;
-    uint32_t* m_key;
-    int64_t* m_ts;
-    unsigned long long* m_count;
-    uint64_t m_capacity;
-    unsigned long long* stats;    // [SGD_ST_N]
+    uint32_t n_capw;
+    uint32_t nullable;                 // capture null bits are live
+    uint8_t cap_col[SGD_MAX_CAPS];     // event column captured into capture c
+    uint8_t cap_word[SGD_MAX_CAPS];    // first word of capture c
+    uint8_t cap_type[SGD_MAX_CAPS];
+    // matches: slot-0 event seq of every emitted match, appended in wave-reserved chunks; per batch
+    // event t the number of matches it triggered and the position of the first (a trigger's matches
+    // are contiguous, in emission order)
+    uint64_t* raw_e1;
+    unsigned long long* raw_count;
+    uint64_t raw_capacity;
+    uint32_t* t_cnt;                   // [max_batch], zero outside the advance -> scatter window
+    uint32_t* t_first;                 // [max_batch]
+    unsigned long long* stats;         // [SGD_ST_N]
     uint32_t* err;
-    DProg f0;
-    DProg f1;
+    DPredPacked q0, q1;
+    const DProg* f0g;                  // general filter programs (device memory)
+    const DProg* f1g;
 };
 
 // launch wrappers (p2_kernels.hip)
@@ -97,7 +151,25 @@ struct ihipStream_t;
 int sgd_launch_bounds(const uint32_t* sorted_keys, uint32_t n, uint32_t n_keys, uint32_t* seg_begin,
                       uint32_t* seg_end, uint32_t* err, ihipStream_t* stream);
 int sgd_launch_p2(const P2Params& p, ihipStream_t* stream);
-int sgd_launch_order(const uint64_t* trig, const uint64_t* e1, const uint32_t* key, const int64_t* ts,
-                     const uint32_t* perm, uint64_t n, uint64_t* o_trig, uint64_t* o_slot, uint32_t* o_key,
-                     int64_t* o_ts, uint32_t* o_len, ihipStream_t* stream);
-int sgd_launch_rel_keys(const uint64_t* trig, uint64_t base, uint64_t n, uint32_t* out, ihipStream_t* stream);
+size_t sgd_p2_lds_bytes(const P2Params& p);
+// ordered output of one batch: o_*[out_count + t_off[t] + r] for the r-th match of batch event t
+struct ScatterParams {
+    uint32_t n;
+    uint64_t seq_base;
+    const uint32_t* key;       // batch key ids (NULL: unpartitioned -> key 0)
+    const int64_t* ts;
+    uint32_t* t_cnt;
+    const uint32_t* t_first;
+    const uint32_t* t_off;     // exclusive scan of t_cnt
+    const uint64_t* raw_e1;
+    unsigned long long* out_count;
+    unsigned long long* batch_total;
+    uint64_t capacity;
+    uint64_t* o_trig;
+    uint64_t* o_slot;          // [n][2]
+    uint32_t* o_key;
+    int64_t* o_ts;
+    uint32_t* o_len;           // [n][2]
+    uint32_t* err;
+};
+int sgd_launch_scatter(const ScatterParams& s, ihipStream_t* stream);

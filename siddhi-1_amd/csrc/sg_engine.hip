@@ -14,7 +14,9 @@
 #include <hip/hip_runtime.h>
 
 #include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
 #include <rocprim/iterator/counting_iterator.hpp>
+#include <rocprim/iterator/transform_iterator.hpp>
 
 #include <algorithm>
 #include <cstdio>
@@ -62,7 +64,9 @@ struct Plan {
     std::vector<std::vector<uint32_t>> evcols;
     std::vector<uint32_t> caps;          // slot-0 attrs captured into partials
     std::vector<uint8_t> cap_col;        // index of each capture in evcols[s0]
+    std::vector<uint8_t> cap_type;
     DProg f0{}, f1{};
+    DPred p0{}, p1{};
 };
 
 uint32_t bits_for(uint64_t n) {
@@ -87,6 +91,56 @@ size_t type_size(uint32_t t) {
     }
 }
 
+// key-sorted event payload: batch position, the filter columns (32-bit words), timestamp
+template <int W> struct alignas(8) Pay {
+    uint32_t idx;
+    uint32_t w[W];
+    int64_t ts;
+};
+static_assert(sizeof(Pay<1>) == 16 && sizeof(Pay<2>) == 24 && sizeof(Pay<3>) == 24 && sizeof(Pay<4>) == 32,
+              "payload layout: ts in the last 8 bytes");
+
+struct PackSrc {
+    const void* p[4];
+    uint8_t kind[4];  // 0: 32-bit column, 1: low / 2: high word of a 64-bit column, 3: bool byte
+    const int64_t* ts;
+};
+
+template <int W> struct PackFn {
+    PackSrc s;
+    __host__ __device__ Pay<W> operator()(uint32_t i) const {
+        Pay<W> o;
+        o.idx = i;
+        o.ts = s.ts[i];
+        for (int w = 0; w < W; ++w) {
+            switch (s.kind[w]) {
+            case 0: o.w[w] = ((const uint32_t*)s.p[w])[i]; break;
+            case 1: o.w[w] = (uint32_t)((const uint64_t*)s.p[w])[i]; break;
+            case 2: o.w[w] = (uint32_t)(((const uint64_t*)s.p[w])[i] >> 32); break;
+            default: o.w[w] = ((const uint8_t*)s.p[w])[i] ? 1u : 0u;
+            }
+        }
+        return o;
+    }
+};
+
+template <int W>
+hipError_t sort_payload(void* tmp, size_t& tmp_bytes, const uint32_t* keys, uint32_t* skeys, const PackSrc& src,
+                        void* out, uint32_t n, uint32_t bits, hipStream_t stream) {
+    auto it = rocprim::make_transform_iterator(rocprim::counting_iterator<uint32_t>(0), PackFn<W>{src});
+    return rocprim::radix_sort_pairs(tmp, tmp_bytes, keys, skeys, it, (Pay<W>*)out, n, 0u, bits, stream);
+}
+
+hipError_t sort_payload_w(int W, void* tmp, size_t& tmp_bytes, const uint32_t* keys, uint32_t* skeys,
+                          const PackSrc& src, void* out, uint32_t n, uint32_t bits, hipStream_t stream) {
+    switch (W) {
+    case 1: return sort_payload<1>(tmp, tmp_bytes, keys, skeys, src, out, n, bits, stream);
+    case 2: return sort_payload<2>(tmp, tmp_bytes, keys, skeys, src, out, n, bits, stream);
+    case 3: return sort_payload<3>(tmp, tmp_bytes, keys, skeys, src, out, n, bits, stream);
+    default: return sort_payload<4>(tmp, tmp_bytes, keys, skeys, src, out, n, bits, stream);
+    }
+}
+
 }  // namespace
 
 struct sg_engine {
@@ -104,9 +158,11 @@ struct sg_engine {
     uint32_t* hdr = nullptr;
     int64_t* p_ts = nullptr;
     uint64_t* p_seq = nullptr;
-    uint64_t* p_cap = nullptr;
+    uint32_t* p_capw = nullptr;
+    uint32_t n_capw = 0;
     uint32_t* p_capnull = nullptr;
     bool nullable = false;
+    DProg* d_prog = nullptr;  // [f0, f1]
     // batch staging
     int64_t* b_ts = nullptr;
     uint32_t* b_key = nullptr;
@@ -119,25 +175,25 @@ struct sg_engine {
     uint32_t* iota = nullptr;
     void* sort_tmp = nullptr;
     size_t sort_tmp_bytes = 0;
+    void* pay = nullptr;           // key-sorted payload [max_batch] x 32 B
     // matches
-    uint64_t* m_trig = nullptr;
-    uint64_t* m_e1 = nullptr;
-    uint32_t* m_key = nullptr;
-    int64_t* m_ts = nullptr;
-    unsigned long long* m_count = nullptr;
+    uint64_t* raw_e1 = nullptr;
+    unsigned long long* raw_count = nullptr;
+    uint32_t* t_cnt = nullptr;
+    uint32_t* t_first = nullptr;
+    uint32_t* t_off = nullptr;
+    unsigned long long* out_count = nullptr;
+    unsigned long long* batch_total = nullptr;
+    void* scan_tmp = nullptr;
+    size_t scan_tmp_bytes = 0;
     unsigned long long* stats = nullptr;
     uint32_t* err = nullptr;
     // ordered output
-    uint32_t* o_rel = nullptr;
-    uint32_t* o_rel2 = nullptr;
-    uint32_t* o_perm = nullptr;
     uint64_t* o_trig = nullptr;
     uint64_t* o_slot = nullptr;
     uint32_t* o_key = nullptr;
     int64_t* o_ts = nullptr;
     uint32_t* o_len = nullptr;
-    void* order_tmp = nullptr;
-    size_t order_tmp_bytes = 0;
     // host copies
     std::vector<uint64_t> h_trig, h_slot;
     std::vector<uint32_t> h_key, h_len;
@@ -152,6 +208,9 @@ struct sg_engine {
     std::vector<Span> spans;
     std::vector<hipEvent_t> free_events;
     bool timing = false;
+    uint32_t dbg = 0;        // SGD_DBG: kernel ablation switches for profiling only
+    unsigned long long* dbg_out = nullptr;
+    uint32_t lds_slots = 8;  // SGD_LDS_SLOTS
 
     hipEvent_t ev() {
         hipEvent_t x;
@@ -297,6 +356,90 @@ void lower_filter(const uint32_t* code, uint32_t pc, uint32_t len, uint32_t own,
     if (maxsp > SGD_MAX_STACK) throw std::runtime_error("filter expression too deep for the device");
 }
 
+// Java widening conversion of a constant (JLS 5.1.2), used to fold CONST+CVT at lowering time
+uint64_t fold_cvt(uint64_t b, uint32_t from, uint32_t to) {
+    if (from == to) return b;
+    if (from == SG_T_INT) {
+        int32_t x = (int32_t)(uint32_t)b;
+        if (to == SG_T_LONG) return (uint64_t)(int64_t)x;
+        if (to == SG_T_FLOAT) { float f = (float)x; uint32_t u; memcpy(&u, &f, 4); return u; }
+        double d = (double)x; uint64_t u; memcpy(&u, &d, 8); return u;
+    }
+    if (from == SG_T_LONG) {
+        int64_t x = (int64_t)b;
+        if (to == SG_T_FLOAT) { float f = (float)x; uint32_t u; memcpy(&u, &f, 4); return u; }
+        double d = (double)x; uint64_t u; memcpy(&u, &d, 8); return u;
+    }
+    if (from == SG_T_FLOAT && to == SG_T_DOUBLE) {
+        uint32_t u = (uint32_t)b; float f; memcpy(&f, &u, 4); double d = (double)f; uint64_t o; memcpy(&o, &d, 8);
+        return o;
+    }
+    throw std::runtime_error("bad constant conversion");
+}
+
+// recognise `cmp (and cmp)*` over simple operands in a lowered program
+DPred to_pred(const DProg& f) {
+    DPred P{};
+    if (f.len == 0) return P;
+    uint32_t i = 0;
+    auto operand = [&](DOperand& o, uint32_t& type) -> bool {
+        if (i >= f.len) return false;
+        const DInst& I = f.ins[i];
+        if (I.op == SG_OP_VAR) {
+            o.kind = I.src == SGD_SRC_EV ? SGD_SRC_EV : I.src == SGD_SRC_CAP ? SGD_SRC_CAP : SGD_SRC_NULL;
+            o.idx = (uint8_t)I.arg;
+            o.from = I.t;
+            type = I.t;
+        } else if (I.op == SG_OP_CONST) {
+            o.kind = I.t2 ? SGD_SRC_NULL : SGD_SRC_CONST;
+            o.bits = I.imm;
+            o.from = I.t;
+            type = I.t;
+        } else {
+            return false;
+        }
+        i++;
+        if (i < f.len && f.ins[i].op == SG_OP_CVT) {
+            type = f.ins[i].t2;
+            i++;
+        }
+        return true;
+    };
+    while (i < f.len) {
+        if (P.n_atoms >= SGD_MAX_ATOMS) { P.use_prog = 1; return P; }
+        DAtom A{};
+        uint32_t lt = 0, rt = 0;
+        if (!operand(A.l, lt) || !operand(A.r, rt) || i >= f.len) { P.use_prog = 1; return P; }
+        const DInst& C = f.ins[i++];
+        if (C.op < SG_OP_EQ || C.op > SG_OP_LE || lt != rt || lt != C.t) { P.use_prog = 1; return P; }
+        A.op = C.op;
+        A.dom = C.t;
+        for (DOperand* o : {&A.l, &A.r})
+            if (o->kind == SGD_SRC_CONST) { o->bits = fold_cvt(o->bits, o->from, A.dom); o->from = A.dom; }
+        P.atoms[P.n_atoms++] = A;
+        if (P.n_atoms > 1) {
+            if (i >= f.len || f.ins[i].op != SG_OP_AND) { P.use_prog = 1; return P; }
+            i++;
+        }
+    }
+    return P;
+}
+
+DPredPacked pack_pred(const DPred& P) {
+    DPredPacked q{};
+    q.n = P.n_atoms;
+    q.prog = P.use_prog;
+    for (uint32_t a = 0; a < P.n_atoms && !P.use_prog; a++) {
+        const DAtom& A = P.atoms[a];
+        if (A.l.kind == SGD_SRC_CONST && A.r.kind == SGD_SRC_CONST) { q.prog = 1; break; }
+        q.code[a] = (uint32_t)(A.op - SG_OP_EQ) | ((uint32_t)A.dom << 4) | ((uint32_t)A.l.kind << 8) |
+                    ((uint32_t)A.l.from << 12) | ((uint32_t)A.l.idx << 16) | ((uint32_t)A.r.kind << 20) |
+                    ((uint32_t)A.r.from << 24) | ((uint32_t)A.r.idx << 28);
+        q.cbits[a] = A.l.kind == SGD_SRC_CONST ? A.l.bits : A.r.bits;
+    }
+    return q;
+}
+
 void build_plan(sg_engine* e, const void* ir, size_t len) {
     if (len < SG_IR_HDR_WORDS * 4 || len % 4) throw std::runtime_error("IR too short");
     e->ir.assign((const uint32_t*)ir, (const uint32_t*)ir + len / 4);
@@ -353,7 +496,12 @@ void build_plan(sg_engine* e, const void* ir, size_t len) {
     if (a->fpc + a->flen > nC || b->fpc + b->flen > nC) throw std::runtime_error("IR filter out of range");
     lower_filter(code, b->fpc, b->flen, b->slot, pl, pl.evcols[pl.s1], pl.f1, true);
     lower_filter(code, a->fpc, a->flen, a->slot, pl, pl.evcols[pl.s0], pl.f0, false);
-    for (uint32_t attr : pl.caps) pl.cap_col.push_back((uint8_t)col_index(pl.evcols[pl.s0], attr));
+    for (uint32_t attr : pl.caps) {
+        pl.cap_col.push_back((uint8_t)col_index(pl.evcols[pl.s0], attr));
+        pl.cap_type.push_back((uint8_t)e->streams[pl.s0].types.at(attr));
+    }
+    pl.p0 = to_pred(pl.f0);
+    pl.p1 = to_pred(pl.f1);
     for (size_t s = 0; s < nstreams; s++)
         for (uint32_t attr : pl.evcols[s])
             if (attr >= e->streams[s].types.size()) throw std::runtime_error("attribute index out of range");
@@ -366,9 +514,19 @@ void allocate(sg_engine* e) {
     HIP_OK(hipMemset(e->hdr, 0, K * 4));
     e->p_ts = dalloc<int64_t>(C * K, o);
     e->p_seq = dalloc<uint64_t>(C * K, o);
-    e->p_cap = dalloc<uint64_t>(std::max<size_t>(1, e->plan.caps.size()) * C * K, o);
+    e->n_capw = 0;
+    for (uint8_t t : e->plan.cap_type) e->n_capw += (t == SG_T_LONG || t == SG_T_DOUBLE) ? 2 : 1;
+    e->p_capw = dalloc<uint32_t>(std::max<size_t>(1, e->n_capw) * C * K, o);
     e->p_capnull = dalloc<uint32_t>(C * K, o);
     HIP_OK(hipMemset(e->p_capnull, 0, C * K * 4));
+    if (e->dbg & 64) {
+        const size_t nw = ((size_t)K + SGD_BLOCK - 1) / SGD_BLOCK * (SGD_BLOCK / SGD_WAVE);
+        e->dbg_out = dalloc<unsigned long long>(nw * 8, o);
+        HIP_OK(hipMemset(e->dbg_out, 0, nw * 8 * 8));
+    }
+    e->d_prog = dalloc<DProg>(2, o);
+    HIP_OK(hipMemcpy(e->d_prog, &e->plan.f0, sizeof(DProg), hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(e->d_prog + 1, &e->plan.f1, sizeof(DProg), hipMemcpyHostToDevice));
     e->b_ts = dalloc<int64_t>(B, o);
     e->b_key = dalloc<uint32_t>(B, o);
     size_t maxattr = 0;
@@ -389,29 +547,35 @@ void allocate(sg_engine* e) {
     e->seg_end = dalloc<uint32_t>(K, o);
     HIP_OK(rocprim::radix_sort_pairs(nullptr, e->sort_tmp_bytes, e->b_key, e->skeys, e->iota, e->sidx,
                                      (uint32_t)B, 0, 32, e->stream));
+    for (int W = 1; W <= 4; ++W) {
+        size_t tb = 0;
+        PackSrc ps{};
+        HIP_OK(sort_payload_w(W, nullptr, tb, e->b_key, e->skeys, ps, nullptr, (uint32_t)B, 32, e->stream));
+        e->sort_tmp_bytes = std::max(e->sort_tmp_bytes, tb);
+    }
     e->sort_tmp = dalloc<uint8_t>(e->sort_tmp_bytes, o);
-    e->m_trig = dalloc<uint64_t>(M, o);
-    e->m_e1 = dalloc<uint64_t>(M, o);
-    e->m_key = dalloc<uint32_t>(M, o);
-    e->m_ts = dalloc<int64_t>(M, o);
-    e->m_count = dalloc<unsigned long long>(1, o);
+    e->pay = dalloc<uint64_t>(4 * B, o);
+    e->raw_e1 = dalloc<uint64_t>(M, o);
+    e->raw_count = dalloc<unsigned long long>(1, o);
+    e->t_cnt = dalloc<uint32_t>(B, o);
+    e->t_first = dalloc<uint32_t>(B, o);
+    e->t_off = dalloc<uint32_t>(B, o);
+    e->out_count = dalloc<unsigned long long>(1, o);
+    e->batch_total = dalloc<unsigned long long>(1, o);
     e->stats = dalloc<unsigned long long>(SGD_ST_N, o);
     e->err = dalloc<uint32_t>(1, o);
-    HIP_OK(hipMemset(e->m_count, 0, 8));
+    HIP_OK(hipMemset(e->t_cnt, 0, B * 4));
+    HIP_OK(hipMemset(e->out_count, 0, 8));
     HIP_OK(hipMemset(e->stats, 0, SGD_ST_N * 8));
     HIP_OK(hipMemset(e->err, 0, 4));
-    e->o_rel = dalloc<uint32_t>(M, o);
-    e->o_rel2 = dalloc<uint32_t>(M, o);
-    e->o_perm = dalloc<uint32_t>(M, o);
+    HIP_OK(rocprim::exclusive_scan(nullptr, e->scan_tmp_bytes, e->t_cnt, e->t_off, 0u, (uint32_t)B,
+                                   rocprim::plus<uint32_t>(), e->stream));
+    e->scan_tmp = dalloc<uint8_t>(e->scan_tmp_bytes, o);
     e->o_trig = dalloc<uint64_t>(M, o);
     e->o_slot = dalloc<uint64_t>(2 * M, o);
     e->o_key = dalloc<uint32_t>(M, o);
     e->o_ts = dalloc<int64_t>(M, o);
     e->o_len = dalloc<uint32_t>(2 * M, o);
-    HIP_OK(rocprim::radix_sort_pairs(nullptr, e->order_tmp_bytes, e->o_rel, e->o_rel2,
-                                     rocprim::counting_iterator<uint32_t>(0), e->o_perm, (uint32_t)M, 0, 32,
-                                     e->stream));
-    e->order_tmp = dalloc<uint8_t>(e->order_tmp_bytes, o);
     HIP_OK(hipDeviceSynchronize());
 }
 
@@ -459,9 +623,12 @@ int push(sg_engine* e, const sg_batch* b) {
     }
     bool any_null = false;
     p.n_evcols = (uint32_t)cols.size();
+    uint32_t words = 0;
     for (size_t c = 0; c < cols.size(); c++) {
         uint32_t attr = cols[c];
         p.evtype[c] = (uint8_t)types[attr];
+        p.ev_word[c] = (uint8_t)words;
+        words += type_size(types[attr]) == 8 ? 2 : 1;
         if (dev) {
             p.evcol[c] = b->cols[attr];
             p.evnull[c] = b->nulls ? b->nulls[attr] : nullptr;
@@ -477,6 +644,16 @@ int push(sg_engine* e, const sg_batch* b) {
         if (p.evnull[c]) any_null = true;
     }
     if (any_null) e->nullable = true;
+    p.n_evwords = words;
+    p.any_null = any_null;
+    // events staged per LDS pass: keep the workgroup's staging area near 40 KB
+    // staged event layout (payload order [idx][cols..][ts]); gather mode appends the null bits
+    p.pay_stride = (1 + words + 2 + 1) & ~1u;
+    p.lds_stride = p.pay_stride + (any_null ? 2 : 0);
+    p.chunk = std::max<uint32_t>(256, std::min<uint32_t>(4096, (20u * 1024u) / (4u * p.lds_stride)) & ~255u);
+    p.lds_slots = std::min<uint32_t>(e->cap, e->lds_slots);
+    p.dbg = e->dbg;
+    p.dbg_out = e->dbg_out;
     // grouping by key
     hipEvent_t g0 = nullptr, g1 = nullptr;
     if (e->timing) { g0 = e->ev(); e->mark(g0); }
@@ -489,8 +666,28 @@ int push(sg_engine* e, const sg_batch* b) {
             keys = e->b_key;
         }
         size_t tmp = e->sort_tmp_bytes;
-        HIP_OK(rocprim::radix_sort_pairs(e->sort_tmp, tmp, keys, e->skeys, e->iota, e->sidx, n, 0,
-                                         bits_for(e->K), e->stream));
+        if (!any_null && words >= 1 && words <= 4) {
+            // sort the events WITH their payload: the advance kernel then stages a contiguous,
+            // coalesced range per workgroup instead of gathering every event by index
+            PackSrc ps{};
+            ps.ts = p.ts;
+            uint32_t wi = 0;
+            for (size_t c = 0; c < cols.size(); c++) {
+                const uint32_t ty = types[cols[c]];
+                if (ty == SG_T_LONG || ty == SG_T_DOUBLE) {
+                    ps.p[wi] = p.evcol[c]; ps.kind[wi++] = 1;
+                    ps.p[wi] = p.evcol[c]; ps.kind[wi++] = 2;
+                } else {
+                    ps.p[wi] = p.evcol[c]; ps.kind[wi++] = ty == SG_T_BOOL ? 3 : 0;
+                }
+            }
+            HIP_OK(sort_payload_w((int)words, e->sort_tmp, tmp, keys, e->skeys, ps, e->pay, n, bits_for(e->K),
+                                  e->stream));
+            p.payload = (const uint32_t*)e->pay;
+        } else {
+            HIP_OK(rocprim::radix_sort_pairs(e->sort_tmp, tmp, keys, e->skeys, e->iota, e->sidx, n, 0,
+                                             bits_for(e->K), e->stream));
+        }
         HIP_OK(hipMemsetAsync(e->seg_begin, 0, (size_t)e->K * 4, e->stream));
         HIP_OK(hipMemsetAsync(e->seg_end, 0, (size_t)e->K * 4, e->stream));
         if (sgd_launch_bounds(e->skeys, n, e->K, e->seg_begin, e->seg_end, e->err, e->stream) != 0)
@@ -509,26 +706,65 @@ int push(sg_engine* e, const sg_batch* b) {
     p.hdr = e->hdr;
     p.p_ts = e->p_ts;
     p.p_seq = e->p_seq;
-    p.p_cap = e->p_cap;
+    p.p_capw = e->p_capw;
     p.p_capnull = e->p_capnull;
     p.n_caps = (uint32_t)pl.caps.size();
+    p.n_capw = e->n_capw;
     p.nullable = e->nullable;
-    for (size_t c = 0; c < pl.cap_col.size(); c++) p.cap_col[c] = pl.cap_col[c];
-    p.m_trig = e->m_trig;
-    p.m_e1 = e->m_e1;
-    p.m_key = e->m_key;
-    p.m_ts = e->m_ts;
-    p.m_count = e->m_count;
-    p.m_capacity = e->mcap;
+    {
+        uint32_t w = 0;
+        for (size_t c = 0; c < pl.cap_col.size(); c++) {
+            p.cap_col[c] = pl.cap_col[c];
+            p.cap_type[c] = pl.cap_type[c];
+            p.cap_word[c] = (uint8_t)w;
+            w += (pl.cap_type[c] == SG_T_LONG || pl.cap_type[c] == SG_T_DOUBLE) ? 2 : 1;
+        }
+    }
+    p.q0 = pack_pred(pl.p0);
+    p.q1 = pack_pred(pl.p1);
+    p.raw_e1 = e->raw_e1;
+    p.raw_count = e->raw_count;
+    p.raw_capacity = e->mcap;
+    p.t_cnt = e->t_cnt;
+    p.t_first = e->t_first;
+    HIP_OK(hipMemsetAsync(e->raw_count, 0, 8, e->stream));
     p.stats = e->stats;
     p.err = e->err;
-    p.f0 = pl.f0;
-    p.f1 = pl.f1;
+    p.f0g = e->d_prog;
+    p.f1g = e->d_prog + 1;
     hipEvent_t a0 = nullptr, a1 = nullptr;
     if (e->timing) { a0 = e->ev(); e->mark(a0); }
     if (sgd_launch_p2(p, e->stream) != 0) throw HipError("k_p2_advance launch failed");
     if (e->timing) { a1 = e->ev(); e->mark(a1); e->spans.push_back({a0, a1, 1}); }
     e->st.advance_launches++;
+    // order this batch's matches by trigger (exclusive scan of per-event counts + scatter)
+    hipEvent_t o0 = nullptr, o1 = nullptr;
+    if (e->timing) { o0 = e->ev(); e->mark(o0); }
+    {
+        size_t tmp = e->scan_tmp_bytes;
+        HIP_OK(rocprim::exclusive_scan(e->scan_tmp, tmp, e->t_cnt, e->t_off, 0u, n, rocprim::plus<uint32_t>(),
+                                       e->stream));
+        ScatterParams sp{};
+        sp.n = n;
+        sp.seq_base = b->seq_base;
+        sp.key = pl.partitioned ? (dev ? b->key : e->b_key) : nullptr;
+        sp.ts = p.ts;
+        sp.t_cnt = e->t_cnt;
+        sp.t_first = e->t_first;
+        sp.t_off = e->t_off;
+        sp.raw_e1 = e->raw_e1;
+        sp.out_count = e->out_count;
+        sp.batch_total = e->batch_total;
+        sp.capacity = e->mcap;
+        sp.o_trig = e->o_trig;
+        sp.o_slot = e->o_slot;
+        sp.o_key = e->o_key;
+        sp.o_ts = e->o_ts;
+        sp.o_len = e->o_len;
+        sp.err = e->err;
+        if (sgd_launch_scatter(sp, e->stream) != 0) throw HipError("k_scatter launch failed");
+    }
+    if (e->timing) { o1 = e->ev(); e->mark(o1); e->spans.push_back({o0, o1, 2}); }
     if (!dev) HIP_OK(hipStreamSynchronize(e->stream));  // host buffers may be reused by the caller
     return SG_OK;
 }
@@ -537,33 +773,15 @@ int poll(sg_engine* e, uint32_t mem, sg_match_batch* out) {
     if (e->held) return fail(SG_ERR_STATE, "previous matches not released");
     unsigned long long n = 0;
     uint32_t err = 0;
-    HIP_OK(hipMemcpyAsync(&n, e->m_count, 8, hipMemcpyDeviceToHost, e->stream));
+    HIP_OK(hipMemcpyAsync(&n, e->out_count, 8, hipMemcpyDeviceToHost, e->stream));
     HIP_OK(hipMemcpyAsync(&err, e->err, 4, hipMemcpyDeviceToHost, e->stream));
     HIP_OK(hipStreamSynchronize(e->stream));
+    e->resolve_spans();
     if (err & SGD_ERR_KEY_RANGE) return fail(SG_ERR_INVALID, "a batch carried key ids outside [0, n_keys)");
     if (err & SGD_ERR_PARTIAL_CAP)
         return fail(SG_ERR_CAPACITY, "a partition key exceeded partial_capacity live partial matches");
     if ((err & SGD_ERR_MATCH_CAP) || n > e->mcap)
         return fail(SG_ERR_CAPACITY, "more matches than match_capacity between two polls");
-    e->resolve_spans();
-    const uint32_t* perm = nullptr;
-    hipEvent_t o0 = nullptr, o1 = nullptr;
-    if (e->timing) { o0 = e->ev(); e->mark(o0); }
-    if (n > 1 && !(e->cfg.flags & SG_CFG_NO_ORDER)) {
-        uint64_t span = e->next_seq - e->poll_base;
-        if (span >= (1ull << 32)) return fail(SG_ERR_CAPACITY, "poll window spans more than 2^32 events");
-        if (sgd_launch_rel_keys(e->m_trig, e->poll_base, n, e->o_rel, e->stream) != 0)
-            throw HipError("k_rel_keys launch failed");
-        size_t tmp = e->order_tmp_bytes;
-        HIP_OK(rocprim::radix_sort_pairs(e->order_tmp, tmp, e->o_rel, e->o_rel2,
-                                         rocprim::counting_iterator<uint32_t>(0), e->o_perm, (uint32_t)n, 0,
-                                         bits_for(span + 1), e->stream));
-        perm = e->o_perm;
-    }
-    if (sgd_launch_order(e->m_trig, e->m_e1, e->m_key, e->m_ts, perm, n, e->o_trig, e->o_slot, e->o_key, e->o_ts,
-                         e->o_len, e->stream) != 0)
-        throw HipError("k_order launch failed");
-    if (e->timing) { o1 = e->ev(); e->mark(o1); e->spans.push_back({o0, o1, 2}); }
     out->n = n;
     out->n_slots = 2;
     out->max_chain = 1;
@@ -596,8 +814,8 @@ int poll(sg_engine* e, uint32_t mem, sg_match_batch* out) {
         out->chain_len = e->h_len.data();
         out->mem = SG_MEM_HOST;
     }
-    // the window restarts after this poll
-    HIP_OK(hipMemsetAsync(e->m_count, 0, 8, e->stream));
+    // the window restarts after this poll (device pointers stay valid until the next push)
+    HIP_OK(hipMemsetAsync(e->out_count, 0, 8, e->stream));
     e->poll_base = e->next_seq;
     e->held = true;
     return SG_OK;
@@ -619,6 +837,8 @@ int sg_engine_create(const void* ir, size_t ir_len, const sg_config* cfg, sg_eng
         e->cfg = *cfg;
         e->device = cfg->device;
         e->timing = (cfg->flags & SG_CFG_TIMING) != 0;
+        if (const char* d = getenv("SGD_DBG")) e->dbg = (uint32_t)strtoul(d, nullptr, 0);
+        if (const char* d = getenv("SGD_LDS_SLOTS")) e->lds_slots = (uint32_t)strtoul(d, nullptr, 0);
         e->K = cfg->n_keys ? cfg->n_keys : 1;
         e->cap = cfg->partial_capacity ? cfg->partial_capacity : 64;
         e->maxb = cfg->max_batch ? cfg->max_batch : (1u << 20);
@@ -647,7 +867,21 @@ int sg_engine_create(const void* ir, size_t ir_len, const sg_config* cfg, sg_eng
     }
 }
 
-void sg_engine_destroy(sg_engine* e) { delete e; }
+void sg_engine_destroy(sg_engine* e) {
+    if (e && e->dbg_out) {  // profiling builds: per-section wave time of the last advance launch
+        const size_t nw = ((size_t)e->K + SGD_BLOCK - 1) / SGD_BLOCK * (SGD_BLOCK / SGD_WAVE);
+        std::vector<unsigned long long> h(nw * 8);
+        if (hipMemcpy(h.data(), e->dbg_out, h.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
+            double sum[8] = {0};
+            for (size_t w = 0; w < nw; w++)
+                for (int i = 0; i < 8; i++) sum[i] += (double)h[w * 8 + i];
+            fprintf(stderr, "[sgd stamps] mean cycles per wave:");
+            for (int i = 0; i < 8; i++) fprintf(stderr, " s%d=%.0f", i, sum[i] / nw);
+            fprintf(stderr, "\n");
+        }
+    }
+    delete e;
+}
 
 int sg_push_batch(sg_engine* e, const sg_batch* b) {
     if (!e || !b) return fail(SG_ERR_INVALID, "null argument");
