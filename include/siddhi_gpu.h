@@ -110,6 +110,7 @@ typedef struct sg_stats {
     uint64_t advance_ns;        /* SG_CFG_TIMING: device time of the NFA advance kernel */
     uint64_t order_ns;          /* SG_CFG_TIMING: device time of match ordering in polls */
     uint64_t advance_launches;  /* NFA advance kernel launches */
+    uint64_t window_spills;     /* keys whose live partials outgrew the register window (moved to HBM) */
 } sg_stats;
 
 /* ir/ir_len: an IR blob (siddhi_gpu_ir.h) of one query */
@@ -127,6 +128,11 @@ int sg_free_buffer(void* buf);
 void sg_engine_destroy(sg_engine* e);
 const char* sg_last_error(void);
 int sg_abi_version(void);
+
+/* Diagnostics (no device needed): generate and compile the query-specialised advance kernel of an IR
+ * blob for gfx950.  variant_flags: bit 0 = batches carry null flags, bit 1 = captures carry null bits.
+ * out (optional) receives the generated query header, or the compiler log on failure. */
+int sg_jit_check(const void* ir, size_t ir_len, uint32_t variant_flags, char* out, size_t out_len);
 
 #ifdef __cplusplus
 }

@@ -49,9 +49,9 @@
  *                                            -1 last, -2 second to last, ...)  (StateEvent.java:138-182)
  *     SG_OP_CONST  a=type  b=is_null       w1=lo  w2=hi   (int/bool/string id in lo; long/double bits)
  *     SG_OP_CVT    a=from  b=to                           (Java widening primitive conversion)
- *     SG_OP_ADD..SG_OP_MOD  a=result type                 (executor/math/*: null in -> null,
+ *     SG_OP_ADD..SG_OP_MOD  a=result type                 (executor/math: null in -> null,
  *                                                          / and % by zero -> null)
- *     SG_OP_EQ..SG_OP_LE    a=compare domain type         (executor/condition/compare/*: null -> false,
+ *     SG_OP_EQ..SG_OP_LE    a=compare domain type         (executor/condition/compare: null -> false,
  *                                                          except NE: null -> true)
  *     SG_OP_AND, SG_OP_OR, SG_OP_NOT                      (never null; not(null) = true)
  *     SG_OP_ISNULL                                        (value is null)

@@ -1,0 +1,648 @@
+// p2_jit.hip — the NFA advance kernel for two-state partitioned patterns
+//   every? e1=S0[f0] -> e2=S1[f1(e1,e2)] (within T)   and   every (e1=S0[f0] -> e2=S1[f1])
+//
+// This file is compiled by hipRTC when an engine is created (sg_jit.cpp), together with a generated
+// header "sgq_query.h" that turns the query into code: the event layout of each stream, the filters
+// f0 / f1 as typed straight-line HIP (Java value semantics below), the capture layout of a partial
+// match and the register-window size SGQ_R.  Nothing in the hot loop interprets anything.
+//
+// Execution model: one lane owns one partition key (adjacent lanes = adjacent keys, so the SoA slabs
+// "partial j of key k at j*K + k" are read and written coalesced).  The key-sorted micro-batch is a
+// contiguous run of payload elements per key; a lane walks its own run in arrival order, the next
+// element always in flight (software-pipelined loads), with the key's live partial matches held in
+// registers: SGQ_R slots + a live mask + a staged mask (slot order = list order).  A key that
+// outgrows the window spills to its HBM slab and continues there (exact, slower).
+//
+// Semantics restated from (paths under
+// /root/reference/modules/siddhi-core/src/main/java/io/siddhi/core/query/input/):
+//   stabilize: expire all states, then promote staged partials
+//       stream/state/receiver/PatternMultiProcessStreamReceiver.java:42-51 (Single: :34-41)
+//   expiry: StreamPreStateProcessor.java:118-129 (isExpired), :325-361 (prefix of pending, all of
+//       staged, re-arm of the withinEvery start state)
+//   promotion: StreamPreStateProcessor.java:308-323 (stable sort by ts, -1 last, :66-80)
+//   state order per event: later state first (PatternMultiProcessStreamReceiver.java:31-40)
+//   advance: StreamPreStateProcessor.java:364-403 + StreamPostStateProcessor.java:64-83
+//   filters: FilterProcessor.java:48-60 and the typed executors under core/executor/
+#include "siddhi_gpu_ir.h"
+#include "sg_engine.h"
+
+// ---- Java value semantics (executor/condition/compare/*, executor/math/*) -------------------------
+template <class T> struct JV {
+    T v;
+    bool n;  // null
+};
+__device__ __forceinline__ bool jtrue(const JV<bool>& x) { return !x.n && x.v; }
+
+// JLS 5.1.2 widening (int/long -> float/double round to nearest)
+template <class TO, class FROM> __device__ __forceinline__ JV<TO> jcvt(const JV<FROM>& x) {
+    return JV<TO>{(TO)x.v, x.n};
+}
+
+// CompareConditionExpressionExecutor.java:38-42: a null operand -> false; NotEqual: null -> true
+template <int OP, class T> __device__ __forceinline__ JV<bool> jcmp(const JV<T>& a, const JV<T>& b) {
+    bool r;
+    if (OP == SG_OP_EQ) r = a.v == b.v;
+    else if (OP == SG_OP_NE) r = a.v != b.v;
+    else if (OP == SG_OP_GT) r = a.v > b.v;
+    else if (OP == SG_OP_GE) r = a.v >= b.v;
+    else if (OP == SG_OP_LT) r = a.v < b.v;
+    else r = a.v <= b.v;
+    return JV<bool>{(a.n || b.n) ? (OP == SG_OP_NE) : r, false};
+}
+
+// arithmetic: null in -> null; x/0, x%0 -> null; int/long wrap; MIN/-1 = MIN; MIN%-1 = 0
+__device__ __forceinline__ JV<int32_t> jarith(int op, const JV<int32_t>& a, const JV<int32_t>& b) {
+    const uint32_t x = (uint32_t)a.v, y = (uint32_t)b.v;
+    const int32_t d = (b.v == 0 || b.v == -1) ? 1 : b.v;  // no undefined division on any lane
+    JV<int32_t> o{0, a.n || b.n};
+    switch (op) {
+    case SG_OP_ADD: o.v = (int32_t)(x + y); break;
+    case SG_OP_SUB: o.v = (int32_t)(x - y); break;
+    case SG_OP_MUL: o.v = (int32_t)(x * y); break;
+    case SG_OP_DIV: o.v = (b.v == -1) ? (int32_t)(0u - x) : a.v / d; o.n |= b.v == 0; break;
+    default: o.v = (b.v == -1) ? 0 : a.v % d; o.n |= b.v == 0;
+    }
+    return o;
+}
+__device__ __forceinline__ JV<int64_t> jarith(int op, const JV<int64_t>& a, const JV<int64_t>& b) {
+    const uint64_t x = (uint64_t)a.v, y = (uint64_t)b.v;
+    const int64_t d = (b.v == 0 || b.v == -1) ? 1 : b.v;
+    JV<int64_t> o{0, a.n || b.n};
+    switch (op) {
+    case SG_OP_ADD: o.v = (int64_t)(x + y); break;
+    case SG_OP_SUB: o.v = (int64_t)(x - y); break;
+    case SG_OP_MUL: o.v = (int64_t)(x * y); break;
+    case SG_OP_DIV: o.v = (b.v == -1) ? (int64_t)(0ull - x) : a.v / d; o.n |= b.v == 0; break;
+    default: o.v = (b.v == -1) ? 0 : a.v % d; o.n |= b.v == 0;
+    }
+    return o;
+}
+__device__ __forceinline__ JV<float> jarith(int op, const JV<float>& a, const JV<float>& b) {
+    JV<float> o{0.f, a.n || b.n};
+    switch (op) {
+    case SG_OP_ADD: o.v = __fadd_rn(a.v, b.v); break;
+    case SG_OP_SUB: o.v = __fsub_rn(a.v, b.v); break;
+    case SG_OP_MUL: o.v = __fmul_rn(a.v, b.v); break;
+    case SG_OP_DIV: o.v = __fdiv_rn(a.v, b.v); o.n |= b.v == 0.0f; break;
+    default: o.v = fmodf(a.v, b.v); o.n |= b.v == 0.0f;
+    }
+    return o;
+}
+__device__ __forceinline__ JV<double> jarith(int op, const JV<double>& a, const JV<double>& b) {
+    JV<double> o{0.0, a.n || b.n};
+    switch (op) {
+    case SG_OP_ADD: o.v = __dadd_rn(a.v, b.v); break;
+    case SG_OP_SUB: o.v = __dsub_rn(a.v, b.v); break;
+    case SG_OP_MUL: o.v = __dmul_rn(a.v, b.v); break;
+    case SG_OP_DIV: o.v = __ddiv_rn(a.v, b.v); o.n |= b.v == 0.0; break;
+    default: o.v = fmod(a.v, b.v); o.n |= b.v == 0.0;
+    }
+    return o;
+}
+
+__device__ __forceinline__ float sg_f32(uint32_t w) { return __uint_as_float(w); }
+__device__ __forceinline__ double sg_f64(uint32_t lo, uint32_t hi) {
+    return __longlong_as_double((long long)((uint64_t)lo | ((uint64_t)hi << 32)));
+}
+__device__ __forceinline__ int64_t sg_i64(uint32_t lo, uint32_t hi) {
+    return (int64_t)((uint64_t)lo | ((uint64_t)hi << 32));
+}
+
+template <bool C, class A, class B> struct SgSel { typedef A type; };
+template <class A, class B> struct SgSel<false, A, B> { typedef B type; };
+
+// the query: SGQ_* constants, SgEv0/SgEv1 + sgq_ev0/1 (payload decode), sgq_f0, sgq_f1,
+// sgq_capture, sgq_pack0/1
+#include "sgq_query.h"
+
+#define R SGQ_R
+
+namespace {
+
+__device__ __forceinline__ int wave_max(int x) {
+    for (int off = 32; off > 0; off >>= 1) x = max(x, __shfl_xor(x, off, SGD_WAVE));
+    return x;
+}
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long x) {
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, SGD_WAVE);
+    return x;
+}
+// inclusive prefix sum over the wave (all 64 lanes must be active)
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, int lane) {
+    for (int off = 1; off < SGD_WAVE; off <<= 1) {
+        const uint32_t y = __shfl_up(x, off, SGD_WAVE);
+        if (lane >= off) x += y;
+    }
+    return x;
+}
+
+template <int S> struct PayEl { uint32_t w[S]; };
+typedef uint32_t sg_u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t sg_u32x2 __attribute__((ext_vector_type(2)));
+
+template <int S> __device__ __forceinline__ PayEl<S> load_pay(const uint32_t* __restrict__ base, uint32_t i) {
+    PayEl<S> x;
+    if constexpr (S % 4 == 0) {
+        const sg_u32x4* s = (const sg_u32x4*)(base + (size_t)i * S);
+#pragma unroll
+        for (int q = 0; q < S / 4; ++q) {
+            const sg_u32x4 v = __builtin_nontemporal_load(s + q);
+            x.w[4 * q] = v.x; x.w[4 * q + 1] = v.y; x.w[4 * q + 2] = v.z; x.w[4 * q + 3] = v.w;
+        }
+    } else {
+        const sg_u32x2* s = (const sg_u32x2*)(base + (size_t)i * S);
+#pragma unroll
+        for (int q = 0; q < S / 2; ++q) {
+            const sg_u32x2 v = __builtin_nontemporal_load(s + q);
+            x.w[2 * q] = v.x; x.w[2 * q + 1] = v.y;
+        }
+    }
+    return x;
+}
+
+__device__ __forceinline__ bool expired(int64_t pts, int64_t now, int64_t within) {
+    const int64_t d = pts - now;  // StreamPreStateProcessor.isExpired: |slot0.ts - now| > within
+    return (d < 0 ? -d : d) > within;
+}
+// eventTimeComparator (StreamPreStateProcessor.java:66-80): a sorts strictly before b; -1 sorts last
+__device__ __forceinline__ bool ts_before(int64_t a, int64_t b) { return (a != -1) && (b == -1 || a < b); }
+
+// one key's HBM slab (partial j at j * K)
+struct Slab {
+    int64_t* ts;
+    uint64_t* seq;
+    uint32_t* cap;
+    uint32_t* nul;
+    uint32_t K;
+    size_t plane;  // cap * K
+    __device__ __forceinline__ int64_t& TS(uint32_t j) const { return ts[(size_t)j * K]; }
+    __device__ __forceinline__ uint64_t& SEQ(uint32_t j) const { return seq[(size_t)j * K]; }
+    __device__ __forceinline__ uint32_t& CAP(uint32_t w, uint32_t j) const { return cap[w * plane + (size_t)j * K]; }
+    __device__ __forceinline__ uint32_t& NUL(uint32_t j) const { return nul[(size_t)j * K]; }
+    __device__ __forceinline__ void move(uint32_t dst, uint32_t src) const {
+        TS(dst) = TS(src);
+        SEQ(dst) = SEQ(src);
+#pragma unroll
+        for (int w = 0; w < SGQ_NCAPW; ++w) CAP(w, dst) = CAP(w, src);
+        if (SGQ_CAPNULL) NUL(dst) = NUL(src);
+    }
+};
+
+// the register window of one key: slot order = list order (pending slots before staged slots)
+struct Win {
+    int64_t ts[R];
+    uint64_t seq[R];
+    uint32_t cw[R][SGQ_NCAPW > 0 ? SGQ_NCAPW : 1];
+    uint32_t cn[R];
+    uint32_t live;  // slot holds a partial
+    uint32_t stg;   // subset of live: staged (pre1's newAndEvery list), all above the pending slots
+    uint32_t tail;  // appends go here (one past the highest live slot)
+
+    __device__ __forceinline__ void copy_slot(int d, int s) {
+        ts[d] = ts[s];
+        seq[d] = seq[s];
+#pragma unroll
+        for (int w = 0; w < SGQ_NCAPW; ++w) cw[d][w] = cw[s][w];
+        if (SGQ_CAPNULL) cn[d] = cn[s];
+    }
+    __device__ __forceinline__ void fix_tail() { tail = live ? 32u - __clz(live) : 0u; }
+
+    // close the holes, keeping slot order: every live slot moves down by the number of free
+    // slots below it, in log2(R) collision-free steps of 1, 2, 4, ... (static register indices)
+    __device__ __forceinline__ void compact() {
+        if ((live & (live + 1u)) == 0u) { tail = __popc(live); return; }  // already a prefix
+        uint32_t d[R];
+#pragma unroll
+        for (int j = 0; j < R; ++j) d[j] = __popc(~live & ((1u << j) - 1u));
+        uint32_t cur = live;
+#pragma unroll
+        for (int s = 0; (1 << s) < R; ++s) {
+            const int sh = 1 << s;
+#pragma unroll
+            for (int j = sh; j < R; ++j) {
+                const bool mv = ((cur >> j) & 1u) && ((d[j] >> s) & 1u);
+                if (mv) {
+                    copy_slot(j - sh, j);
+                    d[j - sh] = d[j];
+                    cur = (cur & ~(1u << j)) | (1u << (j - sh));
+                }
+            }
+        }
+        const uint32_t n = __popc(live), ns = __popc(stg);
+        live = (n >= 32u) ? 0xffffffffu : ((1u << n) - 1u);
+        stg = live & ~((1u << (n - ns)) - 1u);
+        tail = n;
+    }
+
+    // stable sort of the staged slots by ts (eventTimeComparator); the window is compacted
+    __device__ __forceinline__ void sort_staged() {
+        compact();
+        const uint32_t n = tail, lo = n - __popc(stg);
+#pragma unroll
+        for (int pass = 0; pass < R - 1; ++pass) {
+#pragma unroll
+            for (int j = 0; j + 1 < R; ++j) {
+                if ((uint32_t)j >= lo && (uint32_t)(j + 1) < n && ts_before(ts[j + 1], ts[j])) {
+                    int64_t t = ts[j]; ts[j] = ts[j + 1]; ts[j + 1] = t;
+                    uint64_t q = seq[j]; seq[j] = seq[j + 1]; seq[j + 1] = q;
+#pragma unroll
+                    for (int w = 0; w < SGQ_NCAPW; ++w) { uint32_t c = cw[j][w]; cw[j][w] = cw[j + 1][w]; cw[j + 1][w] = c; }
+                    if (SGQ_CAPNULL) { uint32_t c = cn[j]; cn[j] = cn[j + 1]; cn[j + 1] = c; }
+                }
+            }
+        }
+    }
+};
+
+// per-lane NFA counters of one key during a batch
+struct KeySt {
+    uint32_t spend, sstg;              // start-state seeds: pending, staged
+    uint32_t gnp, gns;                 // HBM mode: pending, staged list lengths
+    unsigned long long scanned, created, matches;
+};
+
+// ---- HBM-mode list operations (a key with more than SGQ_R live partials) ------------------------
+template <bool UPD0, bool UPD1>
+__device__ __forceinline__ void glb_stabilize(const Slab& g, KeySt& s, int64_t ts, int64_t within) {
+    if (SGQ_WITHIN && (s.gnp + s.gns) > 0) {
+        uint32_t pre = 0;
+        while (pre < s.gnp && expired(g.TS(pre), ts, within)) pre++;
+        bool stg_exp = false;
+        for (uint32_t r = s.gnp; r < s.gnp + s.gns; ++r) stg_exp |= expired(g.TS(r), ts, within);
+        if (pre > 0 || stg_exp) {
+            uint32_t w = 0, stg_drop = 0;
+            const uint32_t end = s.gnp + s.gns;
+            for (uint32_t r = pre; r < end; ++r) {
+                if (r >= s.gnp && expired(g.TS(r), ts, within)) { stg_drop++; continue; }
+                if (w != r) g.move(w, r);
+                w++;
+            }
+            s.gnp -= pre;
+            s.gns -= stg_drop;
+            if (SGQ_MODE & SGD_P2_EVERY_BOTH) {  // withinEveryPreStateProcessor.addEveryState + updateState
+                s.spend += s.sstg + 1;
+                s.sstg = 0;
+                s.created++;
+            }
+        }
+    }
+    if (UPD0) { s.spend += s.sstg; s.sstg = 0; }
+    if (UPD1 && s.gns > 0) {
+        // stable insertion sort of the staged region by ts
+        for (uint32_t r = s.gnp + 1; r < s.gnp + s.gns; ++r) {
+            const int64_t kt = g.TS(r);
+            if (!ts_before(kt, g.TS(r - 1))) continue;
+            const uint64_t ks = g.SEQ(r);
+            const uint32_t kn = SGQ_CAPNULL ? g.NUL(r) : 0u;
+            uint32_t kw[SGQ_NCAPW > 0 ? SGQ_NCAPW : 1];
+#pragma unroll
+            for (int w = 0; w < SGQ_NCAPW; ++w) kw[w] = g.CAP(w, r);
+            uint32_t q = r;
+            while (q > s.gnp && ts_before(kt, g.TS(q - 1))) { g.move(q, q - 1); q--; }
+            g.TS(q) = kt;
+            g.SEQ(q) = ks;
+#pragma unroll
+            for (int w = 0; w < SGQ_NCAPW; ++w) g.CAP(w, q) = kw[w];
+            if (SGQ_CAPNULL) g.NUL(q) = kn;
+        }
+        s.gnp += s.gns;
+        s.gns = 0;
+    }
+}
+
+template <class Ev>
+__device__ __forceinline__ bool glb_hit(const Slab& g, uint32_t j, const Ev& ev, const P2Params& p) {
+    uint32_t cw[SGQ_NCAPW > 0 ? SGQ_NCAPW : 1];
+#pragma unroll
+    for (int w = 0; w < SGQ_NCAPW; ++w) cw[w] = g.CAP(w, j);
+    return sgq_f1(ev, cw, SGQ_CAPNULL ? g.NUL(j) : 0u, p);
+}
+
+// e2's filter over the pending partials: count and the hit bits of the first 64
+template <class Ev>
+__device__ __forceinline__ uint32_t glb_scan(const Slab& g, const KeySt& s, const Ev& ev, const P2Params& p,
+                                          uint64_t& mask) {
+    uint32_t c = 0;
+    mask = 0;
+    for (uint32_t j = 0; j < s.gnp; ++j) {
+        if (glb_hit(g, j, ev, p)) {
+            if (j < 64) mask |= 1ull << j;
+            c++;
+        }
+    }
+    return c;
+}
+
+// emit the matches of one event (raw[pos ..]) and compact the survivors, pending-list order
+template <class Ev>
+__device__ __forceinline__ void glb_emit(const Slab& g, KeySt& s, const Ev& ev, const P2Params& p, uint64_t mask,
+                                      unsigned long long pos) {
+    uint32_t w1 = 0;
+    for (uint32_t j = 0; j < s.gnp; ++j) {
+        const bool hit = (j < 64) ? ((mask >> j) & 1ull) != 0 : glb_hit(g, j, ev, p);
+        if (hit) {
+            if (pos < p.raw_capacity) p.raw_e1[pos] = g.SEQ(j);
+            pos++;
+        } else {
+            if (w1 != j) g.move(w1, j);
+            w1++;
+        }
+    }
+    s.gnp = w1;
+}
+
+// ---- the kernel ---------------------------------------------------------------------------------
+template <bool S0, bool S1>
+__device__ __forceinline__ void advance(const P2Params& p) {
+    typedef typename SgSel<S0, SgEv0, SgEv1>::type Ev;
+    constexpr int STRIDE = S0 ? SGQ_STRIDE0 : SGQ_STRIDE1;
+    const int lane = threadIdx.x & (SGD_WAVE - 1);
+    const uint32_t k = blockIdx.x * SGD_BLOCK + threadIdx.x;
+    const uint32_t K = p.n_keys;
+    uint32_t b = 0, e = 0, h = 0;
+    if (k < K) {
+        b = p.seg_begin[k];
+        e = p.seg_end[k];
+    }
+    const int nev = (int)(e - b);
+    const int iters = wave_max(nev);
+    if (iters == 0) return;  // no key of this wave has an event in the batch (wave-uniform)
+    if (nev > 0) h = p.hdr[k];
+
+    KeySt s{SGD_H_SPEND(h), SGD_H_SSTG(h), SGD_H_NPEND(h), SGD_H_NSTG(h), 0, 0, 0};
+    if (nev > 0 && !SGD_H_INIT(h)) s.sstg = 1;  // PartitionRuntimeImpl.initPartition -> init(): one seed
+    const uint32_t n0 = s.gnp + s.gns;
+    const unsigned long long st_live0 = (nev > 0) ? (unsigned long long)n0 : 0ull;
+    const Slab G{p.p_ts + k, p.p_seq + k, p.p_capw + k, p.p_capnull + k, K, (size_t)p.cap * K};
+    bool hbm = n0 > (uint32_t)R;
+    bool overflow = false;
+    unsigned long long spills = 0;
+    const int64_t within = p.within;
+
+    Win W;
+    W.live = 0; W.stg = 0; W.tail = 0;
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+        const bool ld = nev > 0 && !hbm && (uint32_t)j < n0;
+        W.ts[j] = ld ? G.TS(j) : 0;
+        W.seq[j] = ld ? G.SEQ(j) : 0;
+#pragma unroll
+        for (int w = 0; w < SGQ_NCAPW; ++w) W.cw[j][w] = ld ? G.CAP(w, j) : 0u;
+        W.cn[j] = (SGQ_CAPNULL && ld) ? G.NUL(j) : 0u;
+    }
+    if (nev > 0 && !hbm) {
+        W.live = (1u << n0) - 1u;
+        W.stg = W.live & ~((1u << s.gnp) - 1u);
+        W.tail = n0;
+    }
+
+    unsigned long long chunk_base = 0;  // this wave's reserved slots of the raw match buffer
+    uint32_t chunk_left = 0;
+    PayEl<STRIDE> cur, nxt;
+    if (nev > 0) cur = load_pay<STRIDE>(p.payload, b);
+
+    for (int it = 0; it < iters; ++it) {
+        const bool act = it < nev;
+        if (it + 1 < nev) nxt = load_pay<STRIDE>(p.payload, b + (uint32_t)it + 1);  // next event in flight
+        Ev ev;
+        int64_t ts = 0;
+        uint32_t bi = 0;
+        if (act) {
+            bi = cur.w[0];
+            ts = sg_i64(cur.w[STRIDE - 2], cur.w[STRIDE - 1]);
+            if constexpr (S0) ev = sgq_ev0(cur.w); else ev = sgq_ev1(cur.w);
+            // ---- stabilize (receiver.stabilizeStates) ----
+            if (!hbm) {
+                if (SGQ_WITHIN && W.live) {
+                    uint32_t X = 0;
+#pragma unroll
+                    for (int j = 0; j < R; ++j) X |= (expired(W.ts[j], ts, within) ? 1u : 0u) << j;
+                    X &= W.live;
+                    if (X) {
+                        const uint32_t P = W.live & ~W.stg;
+                        const uint32_t f = P & ~X;  // first live pending partial that survives
+                        const uint32_t pre = f ? (P & X & ((f & (0u - f)) - 1u)) : (P & X);
+                        const uint32_t sx = W.stg & X;
+                        if (pre | sx) {
+                            W.live &= ~(pre | sx);
+                            W.stg &= ~sx;
+                            W.fix_tail();
+                            if (SGQ_MODE & SGD_P2_EVERY_BOTH) {
+                                s.spend += s.sstg + 1;
+                                s.sstg = 0;
+                                s.created++;
+                            }
+                        }
+                    }
+                }
+                if (S0) { s.spend += s.sstg; s.sstg = 0; }
+                if (S1 && W.stg) {
+                    // promotion: staged partials join the pending list sorted by ts (stable)
+                    bool bad = false, have = false;
+                    int64_t prev = 0;
+#pragma unroll
+                    for (int j = 0; j < R; ++j) {
+                        if ((W.stg >> j) & 1u) {
+                            bad |= have && ts_before(W.ts[j], prev);
+                            prev = W.ts[j];
+                            have = true;
+                        }
+                    }
+                    if (bad) W.sort_staged();
+                    W.stg = 0;
+                }
+            } else {
+                glb_stabilize<S0, S1>(G, s, ts, within);
+            }
+        }
+        // ---- state 1 first (reverse state order, PatternMultiProcessStreamReceiver.java:31-40) ----
+        uint32_t c1 = 0, H = 0;
+        uint64_t gmask = 0;
+        if constexpr (S1) {
+            if (act) {
+                if (!hbm) {
+                    const uint32_t P = W.live & ~W.stg;
+#pragma unroll
+                    for (int j = 0; j < R; ++j)
+                        if (((P >> j) & 1u) && sgq_f1(ev, W.cw[j], W.cn[j], p)) H |= 1u << j;
+                    c1 = __popc(H);
+                    s.scanned += __popc(P);
+                } else {
+                    c1 = glb_scan(G, s, ev, p, gmask);
+                    s.scanned += s.gnp;
+                }
+            }
+        }
+        // wave-wide reservation of the emitted matches (one atomic per wave chunk of slots)
+        if constexpr (S1) {
+        const uint32_t incl = wave_incl_scan(c1, lane);
+        const uint32_t total = __shfl(incl, SGD_WAVE - 1, SGD_WAVE);
+        if (total) {
+            if (total > chunk_left) {
+                const uint32_t want = max(total, (uint32_t)SGD_RAW_CHUNK);
+                unsigned long long nb = 0;
+                if (lane == 0) nb = atomicAdd(p.raw_count, (unsigned long long)want);
+                chunk_base = __shfl(nb, 0, SGD_WAVE);
+                chunk_left = want;
+            }
+            if (c1) {
+                unsigned long long pos = chunk_base + incl - c1;
+                if (pos + c1 <= p.raw_capacity) {
+                    p.t_cnt[bi] = c1;
+                    p.t_first[bi] = (uint32_t)pos;
+                } else {
+                    atomicOr(p.err, (uint32_t)SGD_ERR_MATCH_CAP);
+                }
+                if (!hbm) {
+#pragma unroll
+                    for (int j = 0; j < R; ++j) {
+                        if ((H >> j) & 1u) {
+                            if (pos < p.raw_capacity) p.raw_e1[pos] = W.seq[j];
+                            pos++;
+                        }
+                    }
+                    W.live &= ~H;
+                    W.fix_tail();
+                } else {
+                    glb_emit(G, s, ev, p, gmask, pos);
+                }
+                if (SGQ_MODE & SGD_P2_EVERY_BOTH) s.sstg += c1;  // post1 -> pre0.addEveryState
+                s.matches += c1;
+            }
+            chunk_base += total;
+            chunk_left -= total;
+        }
+        }
+        // ---- state 0: the start-state seeds ----
+        if constexpr (S0) {
+            if (act && s.spend > 0) {
+                s.scanned += s.spend;
+                if (sgq_f0(ev, p)) {
+                    // post0: partial (slot0 = this event, ts = its ts) -> pre1.addState (staged);
+                    // every e1: pre0.addEveryState (a new seed, staged)
+                    uint32_t cw[SGQ_NCAPW > 0 ? SGQ_NCAPW : 1];
+                    uint32_t cn = 0;
+                    sgq_capture(ev, cw, cn);
+                    const uint64_t seq = p.seq_base + bi;
+                    for (uint32_t q = 0; q < s.spend; ++q) {
+                        if (!hbm && W.tail >= (uint32_t)R) W.compact();
+                        if (!hbm && W.tail >= (uint32_t)R) {
+                            // the window is full of live partials: move the list to the HBM slab
+#pragma unroll
+                            for (int j = 0; j < R; ++j) {
+                                G.TS(j) = W.ts[j];
+                                G.SEQ(j) = W.seq[j];
+#pragma unroll
+                                for (int w = 0; w < SGQ_NCAPW; ++w) G.CAP(w, j) = W.cw[j][w];
+                                if (SGQ_CAPNULL) G.NUL(j) = W.cn[j];
+                            }
+                            s.gns = __popc(W.stg);
+                            s.gnp = R - s.gns;
+                            hbm = true;
+                            spills++;
+                        }
+                        if (!hbm) {
+                            const uint32_t t = W.tail;
+#pragma unroll
+                            for (int j = 0; j < R; ++j) {
+                                if ((uint32_t)j == t) {
+                                    W.ts[j] = ts;
+                                    W.seq[j] = seq;
+#pragma unroll
+                                    for (int w = 0; w < SGQ_NCAPW; ++w) W.cw[j][w] = cw[w];
+                                    if (SGQ_CAPNULL) W.cn[j] = cn;
+                                }
+                            }
+                            W.live |= 1u << t;
+                            W.stg |= 1u << t;
+                            W.tail = t + 1;
+                        } else {
+                            const uint32_t j = s.gnp + s.gns;
+                            if (j >= p.cap) { overflow = true; break; }
+                            G.TS(j) = ts;
+                            G.SEQ(j) = seq;
+#pragma unroll
+                            for (int w = 0; w < SGQ_NCAPW; ++w) G.CAP(w, j) = cw[w];
+                            if (SGQ_CAPNULL) G.NUL(j) = cn;
+                            s.gns++;
+                        }
+                        s.created++;
+                    }
+                    if (SGQ_MODE & SGD_P2_EVERY_FIRST) s.sstg += s.spend;
+                    s.spend = 0;
+                }
+            }
+        }
+        cur = nxt;
+    }
+    if (nev > 0) {
+        uint32_t np, ns;
+        if (!hbm) {
+            W.compact();
+            const uint32_t n = W.tail;
+#pragma unroll
+            for (int j = 0; j < R; ++j) {
+                if ((uint32_t)j < n) {
+                    G.TS(j) = W.ts[j];
+                    G.SEQ(j) = W.seq[j];
+#pragma unroll
+                    for (int w = 0; w < SGQ_NCAPW; ++w) G.CAP(w, j) = W.cw[j][w];
+                    if (SGQ_CAPNULL) G.NUL(j) = W.cn[j];
+                }
+            }
+            ns = __popc(W.stg);
+            np = n - ns;
+        } else {
+            np = s.gnp;
+            ns = s.gns;
+        }
+        if (s.sstg > 3 || s.spend > 3) overflow = true;
+        p.hdr[k] = SGD_H_MAKE(np, ns, min(s.spend, 3u), min(s.sstg, 3u), 1);
+    }
+    if (overflow) atomicOr(p.err, (uint32_t)SGD_ERR_PARTIAL_CAP);
+    // exact work counters (wave-reduced, one atomic per wave and counter)
+    const unsigned long long v0 = wave_sum(s.scanned), v1 = wave_sum(s.created), v2 = wave_sum(s.matches);
+    const unsigned long long v3 = wave_sum(nev > 0 ? 1ull : 0ull), v4 = wave_sum(st_live0), v5 = wave_sum(spills);
+    if (lane == 0) {
+        if (v0) atomicAdd(&p.stats[SGD_ST_SCANNED], v0);
+        if (v1) atomicAdd(&p.stats[SGD_ST_CREATED], v1);
+        if (v2) atomicAdd(&p.stats[SGD_ST_MATCHES], v2);
+        if (v3) atomicAdd(&p.stats[SGD_ST_KEYS], v3);
+        if (v4) atomicAdd(&p.stats[SGD_ST_LIVE0], v4);
+        if (v5) atomicAdd(&p.stats[SGD_ST_SPILLS], v5);
+    }
+}
+
+template <int STRIDE, int WHICH>
+__device__ __forceinline__ void pack(const PackParams& q) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= q.n) return;
+    const uint32_t j = q.sidx ? q.sidx[i] : i;
+    PayEl<STRIDE> x;
+#pragma unroll
+    for (int w = 0; w < STRIDE; ++w) x.w[w] = 0;
+    x.w[0] = j;
+    if constexpr (WHICH == 0) sgq_pack0(q, j, x.w); else sgq_pack1(q, j, x.w);
+    const uint64_t t = (uint64_t)q.ts[j];
+    x.w[STRIDE - 2] = (uint32_t)t;
+    x.w[STRIDE - 1] = (uint32_t)(t >> 32);
+    uint2* d = (uint2*)(q.payload + (size_t)i * STRIDE);
+#pragma unroll
+    for (int w = 0; w < STRIDE / 2; ++w) d[w] = make_uint2(x.w[2 * w], x.w[2 * w + 1]);
+}
+
+}  // namespace
+
+// occupancy target of the advance kernel (waves per SIMD); the register allocator keeps within it
+#ifndef SGQ_WAVES
+#define SGQ_WAVES 2
+#endif
+#define SGQ_OCC __attribute__((amdgpu_waves_per_eu(SGQ_WAVES, 8)))
+#if SGQ_MULTI
+extern "C" __global__ void __launch_bounds__(SGD_BLOCK) SGQ_OCC k_adv_m(const P2Params p) { advance<true, true>(p); }
+#else
+extern "C" __global__ void __launch_bounds__(SGD_BLOCK) SGQ_OCC k_adv_s0(const P2Params p) { advance<true, false>(p); }
+extern "C" __global__ void __launch_bounds__(SGD_BLOCK) SGQ_OCC k_adv_s1(const P2Params p) { advance<false, true>(p); }
+#endif
+extern "C" __global__ void __launch_bounds__(256) k_pack0(const PackParams q) { pack<SGQ_STRIDE0, 0>(q); }
+extern "C" __global__ void __launch_bounds__(256) k_pack1(const PackParams q) { pack<SGQ_STRIDE1, 1>(q); }

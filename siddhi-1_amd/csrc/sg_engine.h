@@ -1,26 +1,24 @@
-// sg_engine.h — internal definitions shared by the host side of the C-ABI (sg_engine.hip) and the
-// gfx950 kernels (p2_kernels.hip).  Not part of the public ABI (that is include/siddhi_gpu.h).
+// sg_engine.h — internal definitions shared by the host side of the C-ABI (sg_engine.hip, sg_jit.cpp),
+// the ahead-of-time kernels (p2_kernels.hip) and the query-specialised advance kernel (p2_jit.hip,
+// compiled at engine creation by hipRTC).  Not part of the public ABI (that is include/siddhi_gpu.h).
+// Keep this header free of host-only includes: hipRTC compiles it as part of the JIT source.
 #pragma once
 
 #include <stdint.h>
 
-#define SGD_MAX_PROG 48    // device filter program length (instructions)
-#define SGD_MAX_STACK 8    // filter evaluation stack depth
-#define SGD_MAX_EVCOLS 8   // event columns a query's filters read
+#define SGD_MAX_PROG 64    // filter program length (instructions)
+#define SGD_MAX_STACK 16   // filter evaluation stack depth
+#define SGD_MAX_EVCOLS 8   // event columns a query's filters read (per stream)
 #define SGD_MAX_CAPS 8     // slot-0 attributes captured into a partial match
-#define SGD_MAX_ATOMS 4    // comparisons in a conjunctive predicate
+#define SGD_MAX_CONST 32   // filter constants (kernel arguments, so equal-shaped queries share code)
+#define SGD_MAX_REG 16     // register window (partials per lane) upper bound
 #define SGD_WAVE 64
 #define SGD_BLOCK 256      // lanes (= keys) per workgroup of the advance kernel
 #define SGD_RAW_CHUNK 2048 // raw match slots a wave reserves at a time
-#define SGD_STAGE_UNROLL 8 // 8-byte loads in flight per lane while staging a chunk
 
 // ---- filters ------------------------------------------------------------------------------------
-// Every filter is lowered twice from the IR bytecode (siddhi_gpu_ir.h):
-//  * DPred: a conjunction of <= 4 typed comparisons whose operands are an event column, a captured
-//    slot-0 attribute or a constant already converted to the comparison domain.  Nearly every
-//    pattern filter has this form (`price > 20`, `price > e1.price and symbol == e1.symbol`); it is
-//    evaluated with wave-uniform scalar branches only.
-//  * DProg: the full stack program (every other filter), evaluated by a device interpreter.
+// A filter's IR bytecode (siddhi_gpu_ir.h) is lowered to DProg (variables resolved to event
+// columns / captured slot-0 attributes), from which sg_jit.cpp generates typed HIP code.
 enum { SGD_SRC_EV = 0, SGD_SRC_CAP = 1, SGD_SRC_CONST = 2, SGD_SRC_NULL = 3 };
 
 struct DInst {
@@ -36,37 +34,6 @@ struct DProg {
     uint32_t len;
     uint32_t pad;
     DInst ins[SGD_MAX_PROG];
-};
-
-struct DOperand {
-    uint8_t kind;   // SGD_SRC_*
-    uint8_t from;   // type of the value before conversion to the domain
-    uint8_t idx;    // event column / capture index
-    uint8_t pad;
-    uint32_t pad2;
-    uint64_t bits;  // constant (already in the domain)
-};
-
-struct DAtom {
-    uint8_t op;     // SG_OP_EQ .. SG_OP_LE
-    uint8_t dom;    // comparison domain (sg_type)
-    uint8_t pad[6];
-    DOperand l, r;
-};
-
-// DAtom packed into one word: op-EQ | dom<<4 | lkind<<8 | lfrom<<12 | lidx<<16 | rkind<<20 | rfrom<<24 |
-// ridx<<28, plus the bits of the (at most one) constant operand
-struct DPredPacked {
-    uint32_t n;
-    uint32_t prog;      // 1: not conjunctive, evaluate the stack program
-    uint32_t code[SGD_MAX_ATOMS];
-    uint64_t cbits[SGD_MAX_ATOMS];
-};
-
-struct DPred {
-    uint32_t use_prog;  // 1: not conjunctive, evaluate the DProg
-    uint32_t n_atoms;   // 0 = no filter (always true)
-    DAtom atoms[SGD_MAX_ATOMS];
 };
 
 // two-state pattern shapes handled by the P2 kernel family
@@ -85,38 +52,20 @@ enum {
     ((uint32_t)(np) | ((uint32_t)(ns) << 12) | ((uint32_t)(sp) << 24) | ((uint32_t)(ss) << 26) | ((uint32_t)(in) << 28))
 #define SGD_MAX_CAP 4095u
 
-enum { SGD_ST_SCANNED = 0, SGD_ST_CREATED, SGD_ST_MATCHES, SGD_ST_KEYS, SGD_ST_LIVE0, SGD_ST_N };
+enum { SGD_ST_SCANNED = 0, SGD_ST_CREATED, SGD_ST_MATCHES, SGD_ST_KEYS, SGD_ST_LIVE0, SGD_ST_SPILLS, SGD_ST_N };
 
 enum { SGD_ERR_PARTIAL_CAP = 1, SGD_ERR_MATCH_CAP = 2, SGD_ERR_KEY_RANGE = 4 };
 
+// Advance-kernel arguments.  Everything that shapes the code (pattern mode, stream roles, column
+// types, filter expressions, capture layout, register window) is compiled into the kernel; this
+// struct carries only pointers, sizes and the filter constants.
 struct P2Params {
-    // query shape
     uint32_t n_keys;
-    uint32_t cap;          // partial capacity per key
-    uint32_t mode;         // SGD_P2_*
-    uint32_t multi;        // both states read the same stream (PatternMultiProcessStreamReceiver)
-    uint32_t is_s0;        // this batch's stream feeds state 0
-    uint32_t is_s1;        // ... state 1
-    int64_t within;        // -1 = none
-    // batch (device pointers)
-    uint32_t n;
-    uint32_t n_evcols;
+    uint32_t cap;                      // partial capacity per key (HBM slab depth)
     uint64_t seq_base;
-    const int64_t* ts;
-    const void* evcol[SGD_MAX_EVCOLS];
-    const uint8_t* evnull[SGD_MAX_EVCOLS];
-    uint8_t evtype[SGD_MAX_EVCOLS];
-    uint8_t ev_word[SGD_MAX_EVCOLS];   // first LDS word of column c
-    uint32_t n_evwords;                // 32-bit LDS words per staged event (64-bit columns take two)
-    uint32_t chunk;                    // events staged in LDS per pass
-    uint32_t any_null;                 // the batch carries null flags
-    uint32_t lds_slots;                // partial-match window per lane in LDS
-    uint32_t dbg;                      // profiling ablation switches (SGD_DBG), 0 in production
-    unsigned long long* dbg_out;       // per-wave section stamps (dbg & 64)
-    const uint32_t* sorted_idx;        // batch positions grouped by key, arrival order inside a key
-    const uint32_t* payload;           // or: key-sorted events with payload [idx][cols..][ts] (NULL: gather)
-    uint32_t pay_stride;               // words per payload element ([idx][cols..][ts]; even)
-    uint32_t lds_stride;               // words per staged event in LDS (pay_stride (+2 with null bits))
+    int64_t within;                    // -1 = none
+    // key-sorted batch: element i = [batch position][filter column words..][null bits?][ts lo, hi]
+    const uint32_t* payload;
     const uint32_t* seg_begin;         // [n_keys]
     const uint32_t* seg_end;           // [n_keys]
     // per-key state (SoA, partial j of key k at j * n_keys + k)
@@ -125,12 +74,6 @@ struct P2Params {
     uint64_t* p_seq;
     uint32_t* p_capw;                  // [n_capw][cap][n_keys] captured attribute words
     uint32_t* p_capnull;               // [cap][n_keys] null bits of the captures
-    uint32_t n_caps;
-    uint32_t n_capw;
-    uint32_t nullable;                 // capture null bits are live
-    uint8_t cap_col[SGD_MAX_CAPS];     // event column captured into capture c
-    uint8_t cap_word[SGD_MAX_CAPS];    // first word of capture c
-    uint8_t cap_type[SGD_MAX_CAPS];
     // matches: slot-0 event seq of every emitted match, appended in wave-reserved chunks; per batch
     // event t the number of matches it triggered and the position of the first (a trigger's matches
     // are contiguous, in emission order)
@@ -141,17 +84,24 @@ struct P2Params {
     uint32_t* t_first;                 // [max_batch]
     unsigned long long* stats;         // [SGD_ST_N]
     uint32_t* err;
-    DPredPacked q0, q1;
-    const DProg* f0g;                  // general filter programs (device memory)
-    const DProg* f1g;
+    uint64_t cst[SGD_MAX_CONST];       // filter constants, already in their comparison domain
 };
 
-// launch wrappers (p2_kernels.hip)
+// payload packing (JIT kernel k_pack): batch arrival order or key-sorted order via sidx
+struct PackParams {
+    uint32_t n;
+    uint32_t pad;
+    const uint32_t* sidx;              // NULL: identity
+    const int64_t* ts;
+    const void* col[SGD_MAX_EVCOLS];   // the stream's filter columns (device)
+    const uint8_t* nul[SGD_MAX_EVCOLS];
+    uint32_t* payload;
+};
+
+// ahead-of-time launch wrappers (p2_kernels.hip)
 struct ihipStream_t;
 int sgd_launch_bounds(const uint32_t* sorted_keys, uint32_t n, uint32_t n_keys, uint32_t* seg_begin,
                       uint32_t* seg_end, uint32_t* err, ihipStream_t* stream);
-int sgd_launch_p2(const P2Params& p, ihipStream_t* stream);
-size_t sgd_p2_lds_bytes(const P2Params& p);
 // ordered output of one batch: o_*[out_count + t_off[t] + r] for the r-th match of batch event t
 struct ScatterParams {
     uint32_t n;

@@ -20,6 +20,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <map>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -28,6 +29,7 @@
 #include "../../include/siddhi_gpu.h"
 #include "../../include/siddhi_gpu_ir.h"
 #include "sg_engine.h"
+#include "sg_jit.h"
 
 namespace {
 
@@ -66,7 +68,6 @@ struct Plan {
     std::vector<uint8_t> cap_col;        // index of each capture in evcols[s0]
     std::vector<uint8_t> cap_type;
     DProg f0{}, f1{};
-    DPred p0{}, p1{};
 };
 
 uint32_t bits_for(uint64_t n) {
@@ -102,7 +103,9 @@ static_assert(sizeof(Pay<1>) == 16 && sizeof(Pay<2>) == 24 && sizeof(Pay<3>) == 
 
 struct PackSrc {
     const void* p[4];
-    uint8_t kind[4];  // 0: 32-bit column, 1: low / 2: high word of a 64-bit column, 3: bool byte
+    uint8_t kind[4];  // 0: 32-bit column, 1: low / 2: high word of a 64-bit column, 3: bool byte,
+                      // 4: null bits of the columns, 5: zero
+    const uint8_t* nul[SGD_MAX_EVCOLS];
     const int64_t* ts;
 };
 
@@ -117,7 +120,15 @@ template <int W> struct PackFn {
             case 0: o.w[w] = ((const uint32_t*)s.p[w])[i]; break;
             case 1: o.w[w] = (uint32_t)((const uint64_t*)s.p[w])[i]; break;
             case 2: o.w[w] = (uint32_t)(((const uint64_t*)s.p[w])[i] >> 32); break;
-            default: o.w[w] = ((const uint8_t*)s.p[w])[i] ? 1u : 0u;
+            case 3: o.w[w] = ((const uint8_t*)s.p[w])[i] ? 1u : 0u; break;
+            case 4: {
+                uint32_t nb = 0;
+                for (int c = 0; c < SGD_MAX_EVCOLS; ++c)
+                    if (s.nul[c]) nb |= (s.nul[c][i] != 0 ? 1u : 0u) << c;
+                o.w[w] = nb;
+                break;
+            }
+            default: o.w[w] = 0u;
             }
         }
         return o;
@@ -162,7 +173,15 @@ struct sg_engine {
     uint32_t n_capw = 0;
     uint32_t* p_capnull = nullptr;
     bool nullable = false;
-    DProg* d_prog = nullptr;  // [f0, f1]
+    // query-specialised kernels (sg_jit.cpp), one code object per null variant
+    struct Variant {
+        hipModule_t mod = nullptr;
+        hipFunction_t adv[2] = {nullptr, nullptr};   // [0]: multi / state-0 stream, [1]: state-1 stream
+        hipFunction_t pack[2] = {nullptr, nullptr};
+    };
+    JitQuery jq;
+    std::vector<uint64_t> consts;
+    std::map<int, Variant> variants;  // key: evnull | capnull << 1
     // batch staging
     int64_t* b_ts = nullptr;
     uint32_t* b_key = nullptr;
@@ -175,7 +194,8 @@ struct sg_engine {
     uint32_t* iota = nullptr;
     void* sort_tmp = nullptr;
     size_t sort_tmp_bytes = 0;
-    void* pay = nullptr;           // key-sorted payload [max_batch] x 32 B
+    void* pay = nullptr;           // key-sorted payload [max_batch] x pay_words
+    uint32_t pay_words = 0;
     // matches
     uint64_t* raw_e1 = nullptr;
     unsigned long long* raw_count = nullptr;
@@ -208,9 +228,8 @@ struct sg_engine {
     std::vector<Span> spans;
     std::vector<hipEvent_t> free_events;
     bool timing = false;
-    uint32_t dbg = 0;        // SGD_DBG: kernel ablation switches for profiling only
-    unsigned long long* dbg_out = nullptr;
-    uint32_t lds_slots = 8;  // SGD_LDS_SLOTS
+    uint32_t reg_slots = 8;  // SGD_REG_SLOTS: partials per key held in registers by the advance kernel
+    uint64_t spills = 0;
 
     hipEvent_t ev() {
         hipEvent_t x;
@@ -242,6 +261,8 @@ struct sg_engine {
         for (auto& sp : spans) { (void)hipEventDestroy(sp.a); (void)hipEventDestroy(sp.b); }
         for (auto x : free_events) (void)hipEventDestroy(x);
         for (void* p : owned) (void)hipFree(p);
+        for (auto& kv : variants)
+            if (kv.second.mod) (void)hipModuleUnload(kv.second.mod);
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
@@ -356,90 +377,6 @@ void lower_filter(const uint32_t* code, uint32_t pc, uint32_t len, uint32_t own,
     if (maxsp > SGD_MAX_STACK) throw std::runtime_error("filter expression too deep for the device");
 }
 
-// Java widening conversion of a constant (JLS 5.1.2), used to fold CONST+CVT at lowering time
-uint64_t fold_cvt(uint64_t b, uint32_t from, uint32_t to) {
-    if (from == to) return b;
-    if (from == SG_T_INT) {
-        int32_t x = (int32_t)(uint32_t)b;
-        if (to == SG_T_LONG) return (uint64_t)(int64_t)x;
-        if (to == SG_T_FLOAT) { float f = (float)x; uint32_t u; memcpy(&u, &f, 4); return u; }
-        double d = (double)x; uint64_t u; memcpy(&u, &d, 8); return u;
-    }
-    if (from == SG_T_LONG) {
-        int64_t x = (int64_t)b;
-        if (to == SG_T_FLOAT) { float f = (float)x; uint32_t u; memcpy(&u, &f, 4); return u; }
-        double d = (double)x; uint64_t u; memcpy(&u, &d, 8); return u;
-    }
-    if (from == SG_T_FLOAT && to == SG_T_DOUBLE) {
-        uint32_t u = (uint32_t)b; float f; memcpy(&f, &u, 4); double d = (double)f; uint64_t o; memcpy(&o, &d, 8);
-        return o;
-    }
-    throw std::runtime_error("bad constant conversion");
-}
-
-// recognise `cmp (and cmp)*` over simple operands in a lowered program
-DPred to_pred(const DProg& f) {
-    DPred P{};
-    if (f.len == 0) return P;
-    uint32_t i = 0;
-    auto operand = [&](DOperand& o, uint32_t& type) -> bool {
-        if (i >= f.len) return false;
-        const DInst& I = f.ins[i];
-        if (I.op == SG_OP_VAR) {
-            o.kind = I.src == SGD_SRC_EV ? SGD_SRC_EV : I.src == SGD_SRC_CAP ? SGD_SRC_CAP : SGD_SRC_NULL;
-            o.idx = (uint8_t)I.arg;
-            o.from = I.t;
-            type = I.t;
-        } else if (I.op == SG_OP_CONST) {
-            o.kind = I.t2 ? SGD_SRC_NULL : SGD_SRC_CONST;
-            o.bits = I.imm;
-            o.from = I.t;
-            type = I.t;
-        } else {
-            return false;
-        }
-        i++;
-        if (i < f.len && f.ins[i].op == SG_OP_CVT) {
-            type = f.ins[i].t2;
-            i++;
-        }
-        return true;
-    };
-    while (i < f.len) {
-        if (P.n_atoms >= SGD_MAX_ATOMS) { P.use_prog = 1; return P; }
-        DAtom A{};
-        uint32_t lt = 0, rt = 0;
-        if (!operand(A.l, lt) || !operand(A.r, rt) || i >= f.len) { P.use_prog = 1; return P; }
-        const DInst& C = f.ins[i++];
-        if (C.op < SG_OP_EQ || C.op > SG_OP_LE || lt != rt || lt != C.t) { P.use_prog = 1; return P; }
-        A.op = C.op;
-        A.dom = C.t;
-        for (DOperand* o : {&A.l, &A.r})
-            if (o->kind == SGD_SRC_CONST) { o->bits = fold_cvt(o->bits, o->from, A.dom); o->from = A.dom; }
-        P.atoms[P.n_atoms++] = A;
-        if (P.n_atoms > 1) {
-            if (i >= f.len || f.ins[i].op != SG_OP_AND) { P.use_prog = 1; return P; }
-            i++;
-        }
-    }
-    return P;
-}
-
-DPredPacked pack_pred(const DPred& P) {
-    DPredPacked q{};
-    q.n = P.n_atoms;
-    q.prog = P.use_prog;
-    for (uint32_t a = 0; a < P.n_atoms && !P.use_prog; a++) {
-        const DAtom& A = P.atoms[a];
-        if (A.l.kind == SGD_SRC_CONST && A.r.kind == SGD_SRC_CONST) { q.prog = 1; break; }
-        q.code[a] = (uint32_t)(A.op - SG_OP_EQ) | ((uint32_t)A.dom << 4) | ((uint32_t)A.l.kind << 8) |
-                    ((uint32_t)A.l.from << 12) | ((uint32_t)A.l.idx << 16) | ((uint32_t)A.r.kind << 20) |
-                    ((uint32_t)A.r.from << 24) | ((uint32_t)A.r.idx << 28);
-        q.cbits[a] = A.l.kind == SGD_SRC_CONST ? A.l.bits : A.r.bits;
-    }
-    return q;
-}
-
 void build_plan(sg_engine* e, const void* ir, size_t len) {
     if (len < SG_IR_HDR_WORDS * 4 || len % 4) throw std::runtime_error("IR too short");
     e->ir.assign((const uint32_t*)ir, (const uint32_t*)ir + len / 4);
@@ -500,8 +437,6 @@ void build_plan(sg_engine* e, const void* ir, size_t len) {
         pl.cap_col.push_back((uint8_t)col_index(pl.evcols[pl.s0], attr));
         pl.cap_type.push_back((uint8_t)e->streams[pl.s0].types.at(attr));
     }
-    pl.p0 = to_pred(pl.f0);
-    pl.p1 = to_pred(pl.f1);
     for (size_t s = 0; s < nstreams; s++)
         for (uint32_t attr : pl.evcols[s])
             if (attr >= e->streams[s].types.size()) throw std::runtime_error("attribute index out of range");
@@ -519,14 +454,6 @@ void allocate(sg_engine* e) {
     e->p_capw = dalloc<uint32_t>(std::max<size_t>(1, e->n_capw) * C * K, o);
     e->p_capnull = dalloc<uint32_t>(C * K, o);
     HIP_OK(hipMemset(e->p_capnull, 0, C * K * 4));
-    if (e->dbg & 64) {
-        const size_t nw = ((size_t)K + SGD_BLOCK - 1) / SGD_BLOCK * (SGD_BLOCK / SGD_WAVE);
-        e->dbg_out = dalloc<unsigned long long>(nw * 8, o);
-        HIP_OK(hipMemset(e->dbg_out, 0, nw * 8 * 8));
-    }
-    e->d_prog = dalloc<DProg>(2, o);
-    HIP_OK(hipMemcpy(e->d_prog, &e->plan.f0, sizeof(DProg), hipMemcpyHostToDevice));
-    HIP_OK(hipMemcpy(e->d_prog + 1, &e->plan.f1, sizeof(DProg), hipMemcpyHostToDevice));
     e->b_ts = dalloc<int64_t>(B, o);
     e->b_key = dalloc<uint32_t>(B, o);
     size_t maxattr = 0;
@@ -554,7 +481,16 @@ void allocate(sg_engine* e) {
         e->sort_tmp_bytes = std::max(e->sort_tmp_bytes, tb);
     }
     e->sort_tmp = dalloc<uint8_t>(e->sort_tmp_bytes, o);
-    e->pay = dalloc<uint64_t>(4 * B, o);
+    {
+        uint32_t maxw = 1;  // payload words of the widest stream (+ null word)
+        for (int s : {e->plan.s0, e->plan.s1}) {
+            std::vector<uint32_t> ty;
+            for (uint32_t a : e->plan.evcols[s]) ty.push_back(e->streams[s].types[a]);
+            maxw = std::max(maxw, sgj_stride(sgj_col_words(ty) + 1));
+        }
+        e->pay_words = maxw;
+        e->pay = dalloc<uint32_t>((size_t)maxw * B, o);
+    }
     e->raw_e1 = dalloc<uint64_t>(M, o);
     e->raw_count = dalloc<unsigned long long>(1, o);
     e->t_cnt = dalloc<uint32_t>(B, o);
@@ -579,6 +515,58 @@ void allocate(sg_engine* e) {
     HIP_OK(hipDeviceSynchronize());
 }
 
+JitQuery make_jit_query(sg_engine* e) {
+    const Plan& pl = e->plan;
+    JitQuery q;
+    q.mode = pl.mode;
+    q.multi = pl.s0 == pl.s1;
+    q.within = pl.within >= 0;
+    q.reg_slots = e->reg_slots;
+    for (int r = 0; r < 2; r++) {
+        const int s = r == 0 ? pl.s0 : pl.s1;
+        for (uint32_t a : pl.evcols[s]) q.coltypes[r].push_back(e->streams[s].types[a]);
+    }
+    q.f0 = &pl.f0;
+    q.f1 = &pl.f1;
+    q.cap_col = pl.cap_col;
+    q.cap_type = pl.cap_type;
+    return q;
+}
+
+// the code object of one null variant (compiled on first use; cached across engines)
+sg_engine::Variant& variant(sg_engine* e, bool evnull, bool capnull) {
+    const int key = (evnull ? 1 : 0) | (capnull ? 2 : 0);
+    auto it = e->variants.find(key);
+    if (it != e->variants.end()) return it->second;
+    JitQuery q = e->jq;
+    q.evnull = evnull;
+    q.capnull = capnull;
+    std::vector<uint64_t> consts;
+    const std::string hdr = sgj_generate(q, consts);
+    std::vector<char> code;
+    std::string log;
+    if (!sgj_compile(hdr, code, log)) throw HipError("advance kernel JIT compilation failed: " + log);
+    sg_engine::Variant v;
+    HIP_OK(hipModuleLoadData(&v.mod, code.data()));
+    e->variants[key] = v;  // owned (unloaded by ~sg_engine) before any further call can throw
+    sg_engine::Variant& r = e->variants[key];
+    if (q.multi) {
+        HIP_OK(hipModuleGetFunction(&r.adv[0], r.mod, "k_adv_m"));
+        r.adv[1] = r.adv[0];
+    } else {
+        HIP_OK(hipModuleGetFunction(&r.adv[0], r.mod, "k_adv_s0"));
+        HIP_OK(hipModuleGetFunction(&r.adv[1], r.mod, "k_adv_s1"));
+    }
+    HIP_OK(hipModuleGetFunction(&r.pack[0], r.mod, "k_pack0"));
+    HIP_OK(hipModuleGetFunction(&r.pack[1], r.mod, "k_pack1"));
+    return r;
+}
+
+void launch(hipFunction_t f, uint32_t blocks, uint32_t threads, void* arg, hipStream_t stream) {
+    void* args[] = {arg};
+    HIP_OK(hipModuleLaunchKernel(f, blocks, 1, 1, threads, 1, 1, 0, stream, args, nullptr));
+}
+
 int push(sg_engine* e, const sg_batch* b) {
     const Plan& pl = e->plan;
     if (b->stream >= e->streams.size()) return fail(SG_ERR_INVALID, "stream index out of range");
@@ -593,6 +581,45 @@ int push(sg_engine* e, const sg_batch* b) {
     const bool is0 = (int)b->stream == pl.s0, is1 = (int)b->stream == pl.s1;
     if (!is0 && !is1) return SG_OK;  // stream not read by this query
     const uint32_t n = (uint32_t)b->n;
+    const int role = is0 ? 0 : 1;    // multi: both, kernel 0
+    const auto& cols = pl.evcols[b->stream];
+    const bool dev = b->mem == SG_MEM_DEVICE;
+    const hipMemcpyKind kind = dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+
+    // timestamps / key ids / the columns the filters read (host batches: H2D)
+    const int64_t* ts = b->ts;
+    if (!dev) {
+        HIP_OK(hipMemcpyAsync(e->b_ts, b->ts, (size_t)n * 8, kind, e->stream));
+        ts = e->b_ts;
+    }
+    PackParams pk{};
+    pk.n = n;
+    pk.ts = ts;
+    bool any_null = false;
+    std::vector<uint32_t> coltypes;
+    for (size_t c = 0; c < cols.size(); c++) {
+        const uint32_t attr = cols[c];
+        coltypes.push_back(types[attr]);
+        if (dev) {
+            pk.col[c] = b->cols[attr];
+            pk.nul[c] = b->nulls ? b->nulls[attr] : nullptr;
+        } else {
+            HIP_OK(hipMemcpyAsync(e->b_cols[c], b->cols[attr], (size_t)n * type_size(types[attr]), kind, e->stream));
+            pk.col[c] = e->b_cols[c];
+            pk.nul[c] = nullptr;
+            if (b->nulls && b->nulls[attr]) {
+                HIP_OK(hipMemcpyAsync(e->b_nulls[c], b->nulls[attr], n, kind, e->stream));
+                pk.nul[c] = e->b_nulls[c];
+            }
+        }
+        if (pk.nul[c]) any_null = true;
+    }
+    if (any_null) e->nullable = true;
+    sg_engine::Variant& v = variant(e, any_null, e->nullable);
+    const uint32_t words = sgj_col_words(coltypes) + (any_null ? 1u : 0u);
+    const uint32_t stride = sgj_stride(words);
+    if (stride > e->pay_words) throw HipError("payload stride above the allocated payload");
+    pk.payload = (uint32_t*)e->pay;
     if (!e->have_base) {
         e->poll_base = b->seq_base;
         e->have_base = true;
@@ -601,62 +628,10 @@ int push(sg_engine* e, const sg_batch* b) {
     e->st.events += b->n;
     e->st.batches++;
 
-    const auto& cols = pl.evcols[b->stream];
-    const bool dev = b->mem == SG_MEM_DEVICE;
-    const hipMemcpyKind kind = dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
-    P2Params p{};
-    p.n_keys = e->K;
-    p.cap = e->cap;
-    p.mode = (uint32_t)pl.mode;
-    p.multi = pl.s0 == pl.s1;
-    p.is_s0 = is0;
-    p.is_s1 = is1;
-    p.within = pl.within;
-    p.n = n;
-    p.seq_base = b->seq_base;
-    // timestamps / key ids / the columns the filters read
-    if (dev) {
-        p.ts = b->ts;
-    } else {
-        HIP_OK(hipMemcpyAsync(e->b_ts, b->ts, (size_t)n * 8, kind, e->stream));
-        p.ts = e->b_ts;
-    }
-    bool any_null = false;
-    p.n_evcols = (uint32_t)cols.size();
-    uint32_t words = 0;
-    for (size_t c = 0; c < cols.size(); c++) {
-        uint32_t attr = cols[c];
-        p.evtype[c] = (uint8_t)types[attr];
-        p.ev_word[c] = (uint8_t)words;
-        words += type_size(types[attr]) == 8 ? 2 : 1;
-        if (dev) {
-            p.evcol[c] = b->cols[attr];
-            p.evnull[c] = b->nulls ? b->nulls[attr] : nullptr;
-        } else {
-            HIP_OK(hipMemcpyAsync(e->b_cols[c], b->cols[attr], (size_t)n * type_size(types[attr]), kind, e->stream));
-            p.evcol[c] = e->b_cols[c];
-            p.evnull[c] = nullptr;
-            if (b->nulls && b->nulls[attr]) {
-                HIP_OK(hipMemcpyAsync(e->b_nulls[c], b->nulls[attr], n, kind, e->stream));
-                p.evnull[c] = e->b_nulls[c];
-            }
-        }
-        if (p.evnull[c]) any_null = true;
-    }
-    if (any_null) e->nullable = true;
-    p.n_evwords = words;
-    p.any_null = any_null;
-    // events staged per LDS pass: keep the workgroup's staging area near 40 KB
-    // staged event layout (payload order [idx][cols..][ts]); gather mode appends the null bits
-    p.pay_stride = (1 + words + 2 + 1) & ~1u;
-    p.lds_stride = p.pay_stride + (any_null ? 2 : 0);
-    p.chunk = std::max<uint32_t>(256, std::min<uint32_t>(4096, (20u * 1024u) / (4u * p.lds_stride)) & ~255u);
-    p.lds_slots = std::min<uint32_t>(e->cap, e->lds_slots);
-    p.dbg = e->dbg;
-    p.dbg_out = e->dbg_out;
-    // grouping by key
+    // ---- grouping by key: the batch as key-sorted payload elements + per-key segment bounds ----
     hipEvent_t g0 = nullptr, g1 = nullptr;
     if (e->timing) { g0 = e->ev(); e->mark(g0); }
+    const uint32_t pack_blocks = (n + 255) / 256;
     if (pl.partitioned) {
         const uint32_t* keys = b->key;
         if (!dev) {
@@ -666,41 +641,55 @@ int push(sg_engine* e, const sg_batch* b) {
             keys = e->b_key;
         }
         size_t tmp = e->sort_tmp_bytes;
-        if (!any_null && words >= 1 && words <= 4) {
-            // sort the events WITH their payload: the advance kernel then stages a contiguous,
-            // coalesced range per workgroup instead of gathering every event by index
+        if (words <= 4) {
+            // sort the events WITH their payload (packed on the fly by the first radix pass): the
+            // advance kernel then reads one contiguous run per key
             PackSrc ps{};
-            ps.ts = p.ts;
+            ps.ts = ts;
             uint32_t wi = 0;
             for (size_t c = 0; c < cols.size(); c++) {
-                const uint32_t ty = types[cols[c]];
+                const uint32_t ty = coltypes[c];
                 if (ty == SG_T_LONG || ty == SG_T_DOUBLE) {
-                    ps.p[wi] = p.evcol[c]; ps.kind[wi++] = 1;
-                    ps.p[wi] = p.evcol[c]; ps.kind[wi++] = 2;
+                    ps.p[wi] = pk.col[c]; ps.kind[wi++] = 1;
+                    ps.p[wi] = pk.col[c]; ps.kind[wi++] = 2;
                 } else {
-                    ps.p[wi] = p.evcol[c]; ps.kind[wi++] = ty == SG_T_BOOL ? 3 : 0;
+                    ps.p[wi] = pk.col[c]; ps.kind[wi++] = ty == SG_T_BOOL ? 3 : 0;
                 }
             }
-            HIP_OK(sort_payload_w((int)words, e->sort_tmp, tmp, keys, e->skeys, ps, e->pay, n, bits_for(e->K),
+            if (any_null) {
+                for (size_t c = 0; c < cols.size(); c++) ps.nul[c] = pk.nul[c];
+                ps.kind[wi++] = 4;
+            }
+            if (wi == 0) ps.kind[wi++] = 5;
+            HIP_OK(sort_payload_w((int)wi, e->sort_tmp, tmp, keys, e->skeys, ps, e->pay, n, bits_for(e->K),
                                   e->stream));
-            p.payload = (const uint32_t*)e->pay;
         } else {
             HIP_OK(rocprim::radix_sort_pairs(e->sort_tmp, tmp, keys, e->skeys, e->iota, e->sidx, n, 0,
                                              bits_for(e->K), e->stream));
+            pk.sidx = e->sidx;
+            launch(v.pack[role], pack_blocks, 256, &pk, e->stream);
         }
         HIP_OK(hipMemsetAsync(e->seg_begin, 0, (size_t)e->K * 4, e->stream));
         HIP_OK(hipMemsetAsync(e->seg_end, 0, (size_t)e->K * 4, e->stream));
         if (sgd_launch_bounds(e->skeys, n, e->K, e->seg_begin, e->seg_end, e->err, e->stream) != 0)
             throw HipError("k_seg_bounds launch failed");
-        p.sorted_idx = e->sidx;
     } else {
+        pk.sidx = nullptr;  // one key: arrival order
+        launch(v.pack[role], pack_blocks, 256, &pk, e->stream);
         const uint32_t z = 0;
         HIP_OK(hipMemcpyAsync(e->seg_begin, &z, 4, hipMemcpyHostToDevice, e->stream));
         HIP_OK(hipMemcpyAsync(e->seg_end, &n, 4, hipMemcpyHostToDevice, e->stream));
         HIP_OK(hipStreamSynchronize(e->stream));  // &n / &z are stack values
-        p.sorted_idx = e->iota;
     }
     if (e->timing) { g1 = e->ev(); e->mark(g1); e->spans.push_back({g0, g1, 0}); }
+
+    // ---- the NFA advance ----
+    P2Params p{};
+    p.n_keys = e->K;
+    p.cap = e->cap;
+    p.seq_base = b->seq_base;
+    p.within = pl.within;
+    p.payload = (const uint32_t*)e->pay;
     p.seg_begin = e->seg_begin;
     p.seg_end = e->seg_end;
     p.hdr = e->hdr;
@@ -708,33 +697,18 @@ int push(sg_engine* e, const sg_batch* b) {
     p.p_seq = e->p_seq;
     p.p_capw = e->p_capw;
     p.p_capnull = e->p_capnull;
-    p.n_caps = (uint32_t)pl.caps.size();
-    p.n_capw = e->n_capw;
-    p.nullable = e->nullable;
-    {
-        uint32_t w = 0;
-        for (size_t c = 0; c < pl.cap_col.size(); c++) {
-            p.cap_col[c] = pl.cap_col[c];
-            p.cap_type[c] = pl.cap_type[c];
-            p.cap_word[c] = (uint8_t)w;
-            w += (pl.cap_type[c] == SG_T_LONG || pl.cap_type[c] == SG_T_DOUBLE) ? 2 : 1;
-        }
-    }
-    p.q0 = pack_pred(pl.p0);
-    p.q1 = pack_pred(pl.p1);
     p.raw_e1 = e->raw_e1;
     p.raw_count = e->raw_count;
     p.raw_capacity = e->mcap;
     p.t_cnt = e->t_cnt;
     p.t_first = e->t_first;
-    HIP_OK(hipMemsetAsync(e->raw_count, 0, 8, e->stream));
     p.stats = e->stats;
     p.err = e->err;
-    p.f0g = e->d_prog;
-    p.f1g = e->d_prog + 1;
+    for (size_t i = 0; i < e->consts.size(); i++) p.cst[i] = e->consts[i];
+    HIP_OK(hipMemsetAsync(e->raw_count, 0, 8, e->stream));
     hipEvent_t a0 = nullptr, a1 = nullptr;
     if (e->timing) { a0 = e->ev(); e->mark(a0); }
-    if (sgd_launch_p2(p, e->stream) != 0) throw HipError("k_p2_advance launch failed");
+    launch(v.adv[role], (e->K + SGD_BLOCK - 1) / SGD_BLOCK, SGD_BLOCK, &p, e->stream);
     if (e->timing) { a1 = e->ev(); e->mark(a1); e->spans.push_back({a0, a1, 1}); }
     e->st.advance_launches++;
     // order this batch's matches by trigger (exclusive scan of per-event counts + scatter)
@@ -748,7 +722,7 @@ int push(sg_engine* e, const sg_batch* b) {
         sp.n = n;
         sp.seq_base = b->seq_base;
         sp.key = pl.partitioned ? (dev ? b->key : e->b_key) : nullptr;
-        sp.ts = p.ts;
+        sp.ts = ts;
         sp.t_cnt = e->t_cnt;
         sp.t_first = e->t_first;
         sp.t_off = e->t_off;
@@ -837,8 +811,8 @@ int sg_engine_create(const void* ir, size_t ir_len, const sg_config* cfg, sg_eng
         e->cfg = *cfg;
         e->device = cfg->device;
         e->timing = (cfg->flags & SG_CFG_TIMING) != 0;
-        if (const char* d = getenv("SGD_DBG")) e->dbg = (uint32_t)strtoul(d, nullptr, 0);
-        if (const char* d = getenv("SGD_LDS_SLOTS")) e->lds_slots = (uint32_t)strtoul(d, nullptr, 0);
+        if (const char* d = getenv("SGD_REG_SLOTS")) e->reg_slots = (uint32_t)strtoul(d, nullptr, 0);
+        if (e->reg_slots < 1 || e->reg_slots > SGD_MAX_REG) throw std::invalid_argument("SGD_REG_SLOTS out of [1, 16]");
         e->K = cfg->n_keys ? cfg->n_keys : 1;
         e->cap = cfg->partial_capacity ? cfg->partial_capacity : 64;
         e->maxb = cfg->max_batch ? cfg->max_batch : (1u << 20);
@@ -846,6 +820,8 @@ int sg_engine_create(const void* ir, size_t ir_len, const sg_config* cfg, sg_eng
         if (e->cap > SGD_MAX_CAP) throw std::invalid_argument("partial_capacity above 4095");
         if (e->mcap >= (1ull << 32)) throw std::invalid_argument("match_capacity must be < 2^32");
         build_plan(e, ir, ir_len);
+        e->jq = make_jit_query(e);
+        (void)sgj_generate(e->jq, e->consts);  // validates the filters, fixes the constant table
         if (!e->plan.partitioned && e->K != 1) e->K = 1;
         int ndev = 0;
         HIP_OK(hipGetDeviceCount(&ndev));
@@ -853,6 +829,7 @@ int sg_engine_create(const void* ir, size_t ir_len, const sg_config* cfg, sg_eng
         HIP_OK(hipSetDevice(cfg->device));
         HIP_OK(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
         allocate(e);
+        (void)variant(e, false, false);  // compile (or fetch) the advance kernel now: fail at creation
         *out = e;
         return SG_OK;
     } catch (const HipError& ex) {
@@ -867,21 +844,7 @@ int sg_engine_create(const void* ir, size_t ir_len, const sg_config* cfg, sg_eng
     }
 }
 
-void sg_engine_destroy(sg_engine* e) {
-    if (e && e->dbg_out) {  // profiling builds: per-section wave time of the last advance launch
-        const size_t nw = ((size_t)e->K + SGD_BLOCK - 1) / SGD_BLOCK * (SGD_BLOCK / SGD_WAVE);
-        std::vector<unsigned long long> h(nw * 8);
-        if (hipMemcpy(h.data(), e->dbg_out, h.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
-            double sum[8] = {0};
-            for (size_t w = 0; w < nw; w++)
-                for (int i = 0; i < 8; i++) sum[i] += (double)h[w * 8 + i];
-            fprintf(stderr, "[sgd stamps] mean cycles per wave:");
-            for (int i = 0; i < 8; i++) fprintf(stderr, " s%d=%.0f", i, sum[i] / nw);
-            fprintf(stderr, "\n");
-        }
-    }
-    delete e;
-}
+void sg_engine_destroy(sg_engine* e) { delete e; }
 
 int sg_push_batch(sg_engine* e, const sg_batch* b) {
     if (!e || !b) return fail(SG_ERR_INVALID, "null argument");
@@ -942,6 +905,7 @@ int sg_get_stats(sg_engine* e, sg_stats* out) {
         out->matches = s[SGD_ST_MATCHES];
         out->keys_touched = s[SGD_ST_KEYS];
         out->live_at_batch_start = s[SGD_ST_LIVE0];
+        out->window_spills = s[SGD_ST_SPILLS];
         // live partials now: sum of the headers' counts (host reduction; diagnostics only)
         std::vector<uint32_t> h(e->K);
         HIP_OK(hipMemcpy(h.data(), e->hdr, (size_t)e->K * 4, hipMemcpyDeviceToHost));
@@ -965,6 +929,40 @@ int sg_restore(sg_engine* e, const void* buf, size_t len) {
 int sg_free_buffer(void* buf) {
     free(buf);
     return SG_OK;
+}
+
+int sg_jit_check(const void* ir, size_t ir_len, uint32_t variant_flags, char* out, size_t out_len) {
+    if (!ir) return fail(SG_ERR_INVALID, "null argument");
+    sg_engine* e = nullptr;
+    int rc = SG_OK;
+    std::string text;
+    try {
+        e = new sg_engine();
+        e->device = -1;
+        if (const char* d = getenv("SGD_REG_SLOTS")) e->reg_slots = (uint32_t)strtoul(d, nullptr, 0);
+        build_plan(e, ir, ir_len);
+        JitQuery q = make_jit_query(e);
+        q.evnull = (variant_flags & 1u) != 0;
+        q.capnull = (variant_flags & 2u) != 0;
+        std::vector<uint64_t> consts;
+        text = sgj_generate(q, consts);
+        std::vector<char> code;
+        std::string log;
+        if (!sgj_compile(text, code, log)) {
+            text = log;
+            rc = fail(SG_ERR_DEVICE, "JIT compilation failed: " + log);
+        }
+    } catch (const std::exception& ex) {
+        text = ex.what();
+        rc = fail(SG_ERR_UNSUPPORTED, ex.what());
+    }
+    delete e;
+    if (out && out_len) {
+        const size_t m = std::min(out_len - 1, text.size());
+        memcpy(out, text.data(), m);
+        out[m] = 0;
+    }
+    return rc;
 }
 
 }  // extern "C"

@@ -56,7 +56,7 @@ class sg_stats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in ("events", "batches", "partials_scanned", "partials_created",
                                           "partials_live", "matches", "keys_touched",
                                           "live_at_batch_start", "group_ns", "advance_ns", "order_ns",
-                                          "advance_launches")]
+                                          "advance_launches", "window_spills")]
 
 
 @dataclass
@@ -87,6 +87,21 @@ def load_library(path):
 
 def load_hip_library():
     return load_library(HIP_LIBRARY)
+
+
+def jit_check(ir: bytes, variant_flags=0, lib=None):
+    """Generate and compile (hipRTC, gfx950, no device needed) the query-specialised advance kernel
+    of an IR blob.  Returns the generated query header; raises EngineError with the log on failure."""
+    lib = lib or load_hip_library()
+    f = lib.sg_jit_check
+    f.argtypes = [C.c_void_p, C.c_size_t, C.c_uint32, C.c_char_p, C.c_size_t]
+    buf = C.create_string_buffer(1 << 20)
+    irb = C.create_string_buffer(ir, len(ir))
+    rc = f(irb, len(ir), variant_flags, buf, len(buf))
+    if rc != SG_OK:
+        lib.sg_last_error.restype = C.c_char_p
+        raise EngineError(rc, lib.sg_last_error().decode(errors="replace"))
+    return buf.value.decode()
 
 
 def _np_ptr(a):

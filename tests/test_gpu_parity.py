@@ -101,8 +101,11 @@ def _push_both(gpu, ora, stream, seq_base, d, cols_names, ts=None):
         e.push(stream, seq_base, ts, cols, None, d["key"])
 
 
+@pytest.mark.parametrize("reg_slots", [8, 2])
 @pytest.mark.parametrize("shape", sorted(SHAPES))
-def test_gpu_random_streams_bit_exact(shape):
+def test_gpu_random_streams_bit_exact(shape, reg_slots, monkeypatch):
+    """reg_slots=2: most keys outgrow the register window, so the HBM-slab path is exercised too"""
+    monkeypatch.setenv("SGD_REG_SLOTS", str(reg_slots))
     n_keys, batch, nb = 2048, 40000, 4
     cq, gpu, ora = _engines(SHAPES[shape], n_keys, batch)
     seq = 0
@@ -122,10 +125,14 @@ def test_gpu_random_streams_bit_exact(shape):
     sg, so = gpu.stats(), ora.stats()
     assert sg["matches"] == so["matches"] and sg["matches"] > 0
     assert sg["partials_live"] == so["partials_live"]
+    if reg_slots == 2 and shape not in ("no_every", "every_both_within"):  # at most one live partial
+        assert sg["window_spills"] > 0
 
 
-def test_gpu_non_monotonic_timestamps():
+@pytest.mark.parametrize("reg_slots", [8, 3])
+def test_gpu_non_monotonic_timestamps(reg_slots, monkeypatch):
     """prefix-only expiry and the stable ts sort of staged partials (StreamPreStateProcessor.java:331-342)"""
+    monkeypatch.setenv("SGD_REG_SLOTS", str(reg_slots))
     n_keys, batch = 512, 30000
     cq, gpu, ora = _engines(SHAPES["two_streams"], n_keys, batch)
     rng = np.random.default_rng(5)
