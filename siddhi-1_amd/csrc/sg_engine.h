@@ -14,7 +14,7 @@
 #define SGD_MAX_REG 16     // register window (partials per lane) upper bound
 #define SGD_WAVE 64
 #define SGD_BLOCK 256      // lanes (= keys) per workgroup of the advance kernel
-#define SGD_RAW_CHUNK 2048 // raw match slots a wave reserves at a time
+#define SGD_RAW_CHUNK 256  // raw match slots a wave reserves at a time (the raw buffer has this much slack per wave)
 
 // ---- filters ------------------------------------------------------------------------------------
 // A filter's IR bytecode (siddhi_gpu_ir.h) is lowered to DProg (variables resolved to event

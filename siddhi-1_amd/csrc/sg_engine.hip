@@ -163,6 +163,7 @@ struct sg_engine {
     Plan plan;
     uint32_t K = 1, cap = 64, maxb = 0;
     uint64_t mcap = 0;
+    uint64_t raw_cap = 0;  // mcap + one reservation chunk of slack per advance-kernel wave
     std::vector<void*> owned;
 
     // state
@@ -491,7 +492,8 @@ void allocate(sg_engine* e) {
         e->pay_words = maxw;
         e->pay = dalloc<uint32_t>((size_t)maxw * B, o);
     }
-    e->raw_e1 = dalloc<uint64_t>(M, o);
+    e->raw_cap = M + ((size_t)(K + SGD_WAVE - 1) / SGD_WAVE) * SGD_RAW_CHUNK;
+    e->raw_e1 = dalloc<uint64_t>(e->raw_cap, o);
     e->raw_count = dalloc<unsigned long long>(1, o);
     e->t_cnt = dalloc<uint32_t>(B, o);
     e->t_first = dalloc<uint32_t>(B, o);
@@ -699,7 +701,7 @@ int push(sg_engine* e, const sg_batch* b) {
     p.p_capnull = e->p_capnull;
     p.raw_e1 = e->raw_e1;
     p.raw_count = e->raw_count;
-    p.raw_capacity = e->mcap;
+    p.raw_capacity = e->raw_cap;
     p.t_cnt = e->t_cnt;
     p.t_first = e->t_first;
     p.stats = e->stats;
@@ -818,7 +820,7 @@ int sg_engine_create(const void* ir, size_t ir_len, const sg_config* cfg, sg_eng
         e->maxb = cfg->max_batch ? cfg->max_batch : (1u << 20);
         e->mcap = cfg->match_capacity ? cfg->match_capacity : (uint64_t)e->maxb * 4;
         if (e->cap > SGD_MAX_CAP) throw std::invalid_argument("partial_capacity above 4095");
-        if (e->mcap >= (1ull << 32)) throw std::invalid_argument("match_capacity must be < 2^32");
+        if (e->mcap >= (1ull << 31)) throw std::invalid_argument("match_capacity must be < 2^31");
         build_plan(e, ir, ir_len);
         e->jq = make_jit_query(e);
         (void)sgj_generate(e->jq, e->consts);  // validates the filters, fixes the constant table
