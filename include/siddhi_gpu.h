@@ -48,6 +48,12 @@ extern "C" {
 #define SG_MEM_DEVICE 1u /* pointers are device (HBM) memory of the engine's device */
 
 #define SG_NULL_SEQ UINT64_MAX
+/* slot event created by an absent state when it fires (StreamEventFactory.newInstance():
+ * no attributes, ts -1; AbsentLogicalPreStateProcessor.java:153-166) */
+#define SG_BLANK_SEQ (UINT64_MAX - 1)
+/* trigger_seq of a match emitted by a timer (absent state fired by sg_advance_time, delivered at once:
+ * AbsentStreamPreStateProcessor.sendEvent, AbsentStreamPreStateProcessor.java:229-246) */
+#define SG_TIMER_SEQ UINT64_MAX
 
 /* engine configuration flags */
 #define SG_CFG_NO_ORDER 1u /* deliver matches per-key ordered only (skip the global trigger-seq order) */
@@ -116,6 +122,12 @@ typedef struct sg_stats {
 /* ir/ir_len: an IR blob (siddhi_gpu_ir.h) of one query */
 int sg_engine_create(const void* ir, size_t ir_len, const sg_config* cfg, sg_engine** out);
 int sg_push_batch(sg_engine* e, const sg_batch* b);
+/* The engine clock (TimestampGenerator.currentTime()).  Wall-clock apps (no @app:playback): now_ms is
+ * the wall clock; every per-key timer whose scheduled run time is <= now_ms runs, in time order
+ * (Scheduler.EventCaller, Scheduler.java:238-298).  Playback apps: now_ms is the event time set by
+ * InputHandler.send before the event is processed; timers whose queue head is <= now_ms run
+ * (Scheduler time-change listener, Scheduler.java:73-104).  Matches emitted by timers are polled
+ * like any other (trigger_seq = SG_TIMER_SEQ). */
 int sg_advance_time(sg_engine* e, int64_t now_ms);
 /* mem = SG_MEM_HOST copies matches to host memory; SG_MEM_DEVICE returns device pointers */
 int sg_poll_matches(sg_engine* e, uint32_t mem, sg_match_batch* out);

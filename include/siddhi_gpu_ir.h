@@ -37,6 +37,7 @@
  *
  *   node tree, prefix order:
  *     SG_N_STREAM : tag, slot, stream, filter_pc, filter_len, absent, for_lo, for_hi
+ *                   (absent = `not S[..] for T`: for = T in ms, -1 when a logical `not` has no `for`)
  *     SG_N_NEXT   : tag, <current>, <next>
  *     SG_N_EVERY  : tag, <child>
  *     SG_N_LOGICAL: tag, logical type (SG_L_AND | SG_L_OR), <element1>, <element2>
@@ -70,6 +71,7 @@
 #define SG_IR_SLOT_WORDS 2
 
 #define SG_IR_F_PARTITIONED 1u
+#define SG_IR_F_PLAYBACK 2u    /* @app:playback: the clock is event time (TimestampGeneratorImpl.java:77-122) */
 
 #define SG_COUNT_ANY 0x7fffffffu
 

@@ -28,6 +28,13 @@
  *                                       partition/PartitionStreamReceiver.java:148-272,
  *                                       partition/PartitionRuntimeImpl.java:346-367
  *   filter expression semantics         executor/condition/**, executor/math/** (see eval())
+ *   absent states (`not S[..] for T`)   AbsentStreamPreStateProcessor.java:67-308,
+ *                                       AbsentStreamPostStateProcessor.java:36-56,
+ *                                       AbsentLogicalPreStateProcessor.java:65-388,
+ *                                       AbsentLogicalPostStateProcessor.java:37-49
+ *   timers / clock                      util/Scheduler.java:65-368 (per-key FIFO queue; EventCaller in
+ *                                       wall-clock mode, time-change listener in playback mode),
+ *                                       util/timestamp/TimestampGeneratorImpl.java:77-122
  *
  * Memory: StateEvent / StreamEvent are intrusively reference counted (the Java originals are GC'd
  * objects that are shared between lists and chains; identity matters for the shared-alias
@@ -38,7 +45,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <list>
+#include <set>
+#include <tuple>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -185,10 +195,21 @@ struct KeyState {  // StreamPreState (+ Count extras) of ONE processor for ONE p
     bool initialized = false;
     bool successCondition = false;   // CountStreamPreState
     bool startStateReset = false;    // CountStreamPreState
+    // LogicalStreamPreState of the absent processors
+    int64_t lastScheduledTime = 0;   // AbsentStreamPreStateProcessor.java:312-318
+    int64_t lastArrivalTime = 0;     // AbsentLogicalPreStateProcessor.java:360-365
+    bool active = true;
+    bool started = false;            // StreamPreState.started (partitionCreated once per key)
+    // SchedulerState of this processor's Scheduler for this key (Scheduler.java:331-368)
+    std::deque<int64_t> toNotify;    // toNotifyQueue: FIFO, NOT sorted
+    bool running = false;            // an EventCaller is scheduled (wall-clock mode)
+    int64_t fireAt = 0;              // when that EventCaller runs
+    uint64_t order = 0;              // schedule order (ties of fireAt)
 };
 
 struct PostProc {
     int kind = P_STREAM;
+    bool absent = false;              // Absent{Stream,Logical}PostStateProcessor
     int stateId = 0;
     PreProc* nextStatePre = nullptr;
     PreProc* nextEveryStatePre = nullptr;
@@ -214,6 +235,8 @@ struct PostProc {
 struct PreProc {
     int id = 0;          // index in Engine::procs (state storage)
     int kind = P_STREAM;
+    bool absent = false;           // Absent{Stream,Logical}PreStateProcessor
+    int64_t waitingTime = -1;      // `for` time of the absent state
     int stateId = 0;
     bool isStart = false;
     int stateType = SG_Q_PATTERN;
@@ -254,6 +277,14 @@ struct PreProc {
     void startStateReset();
     void runChain(StateEvent* se);  // StreamPreStateProcessor.process(StateEvent)
     void processAndReturn(Ref<StreamEvent> ev, std::vector<SE>& ret);
+    // absent states
+    void notifyAt(int64_t t);                       // Scheduler.notifyAt (Scheduler.java:114-128)
+    void updateLastArrivalTime(int64_t ts);
+    void partitionCreated();
+    void processTimer(int64_t currentTime);         // Absent*PreStateProcessor.process(chunk)
+    void sendAbsentEvent(const SE& se);             // Absent*PreStateProcessor.sendEvent
+    bool partnerCanProceed(StateEvent* se);         // AbsentLogicalPreStateProcessor.java:391-422
+    void processAndReturnAbsentLogical(Ref<StreamEvent> ev);
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -354,7 +385,20 @@ struct Engine {
 
     sg_stats stats{};
 
+    // clock (TimestampGeneratorImpl): wall clock, or the last event time in playback mode
+    bool playback = false;
+    int64_t now = 0;
+    int64_t lastEventTs = 0;
+    uint64_t schedOrder = 0;
+    std::vector<PreProc*> startup;              // startupPreStateProcessors (absent pres, parse order)
+    // per scheduler (absent pre): keys whose queue is not empty, by head (playback listener)
+    std::vector<std::set<std::pair<int64_t, uint32_t>>> heads;   // [proc id]
+    // scheduled EventCallers (wall-clock mode): (fireAt, order, proc, key)
+    std::set<std::tuple<int64_t, uint64_t, int, uint32_t>> callers;
+
     KeyState& state(int proc) { return keyStates[curKey][proc]; }
+    void advanceTime(int64_t t);
+    void sendTimerEvents(PreProc* p);
 
     // ---- attribute access ----
     Val attr(uint64_t seq, uint32_t a) const {
@@ -375,7 +419,8 @@ KeyState& PreProc::st() { return eng->state(id); }
 void PreProc::init() {  // StreamPreStateProcessor.java:178-194
     KeyState& s = st();
     if (isStart && (!s.initialized || thisPost->nextEveryStatePre != nullptr ||
-                    (stateType == SG_Q_SEQUENCE && false /* next is absent: not supported yet */))) {
+                    (stateType == SG_Q_SEQUENCE && thisPost->nextStatePre != nullptr &&
+                     thisPost->nextStatePre->absent))) {
         SE se(new StateEvent(eng->nslots));
         addState(se);
         st().initialized = true;
@@ -384,13 +429,27 @@ void PreProc::init() {  // StreamPreStateProcessor.java:178-194
 
 void PreProc::addState(SE se) {
     KeyState& s = st();
-    if (kind == P_LOGICAL) {  // LogicalPreStateProcessor.java:52-72
+    if (absent && !s.active) return;  // Absent*PreStateProcessor.addState: 'every' not used, already fired
+    if (absent && kind == P_STREAM) {  // AbsentStreamPreStateProcessor.java:83-103
+        if (stateType == SG_Q_SEQUENCE) s.newAndEvery.clear();
+        s.newAndEvery.push_back(se);
+        if (!isStart) {
+            st().lastScheduledTime = se->ts + waitingTime;
+            notifyAt(st().lastScheduledTime);
+        }
+        return;
+    }
+    if (kind == P_LOGICAL) {  // LogicalPreStateProcessor.java:43-62
         if (isStart || stateType == SG_Q_SEQUENCE) {
             if (s.newAndEvery.empty()) s.newAndEvery.push_back(se);
             if (partner && partner->st().newAndEvery.empty()) partner->st().newAndEvery.push_back(se);
         } else {
             s.newAndEvery.push_back(se);
             if (partner) partner->st().newAndEvery.push_back(se);
+        }
+        if (absent && !isStart && waitingTime != -1) {  // AbsentLogicalPreStateProcessor.java:77-97
+            notifyAt(se->ts + waitingTime);
+            if (partner && partner->absent) partner->notifyAt(se->ts + partner->waitingTime);
         }
         return;
     }
@@ -408,7 +467,24 @@ void PreProc::addState(SE se) {
 void PreProc::addEveryState(const SE& se) {
     SE c = clone_state(se.get());
     c->type = CURRENT;
-    if (kind == P_LOGICAL) {  // LogicalPreStateProcessor.java:74-94
+    if (absent && kind == P_LOGICAL) {  // AbsentLogicalPreStateProcessor.java:99-118
+        if (c->slots[stateId]) c->ts = c->slots[stateId]->ts;
+        c->slots[stateId] = Ref<StreamEvent>();
+        c->slots[partner->stateId] = Ref<StreamEvent>();
+        st().newAndEvery.push_back(c);
+        partner->st().newAndEvery.push_back(c);
+        eng->stats.partials_created++;
+        return;
+    }
+    if (absent) {  // AbsentStreamPreStateProcessor.java:105-123
+        for (size_t i = stateId; i < c->slots.size(); i++) c->slots[i] = Ref<StreamEvent>();
+        st().newAndEvery.push_back(c);
+        st().lastScheduledTime = se->ts + waitingTime;
+        notifyAt(st().lastScheduledTime);
+        eng->stats.partials_created++;
+        return;
+    }
+    if (kind == P_LOGICAL) {  // LogicalPreStateProcessor.java:64-84
         c->slots[stateId] = Ref<StreamEvent>();
         for (size_t i = stateId; i < c->slots.size(); i++) c->slots[i] = Ref<StreamEvent>();
         st().newAndEvery.push_back(c);
@@ -524,6 +600,11 @@ void PreProc::runChain(StateEvent* se) {  // StreamPreStateProcessor.process(Sta
 
 void PreProc::processAndReturn(Ref<StreamEvent> ev, std::vector<SE>& ret) {
     KeyState& s = st();
+    if (absent) {
+        if (!s.active) return;
+        if (kind == P_LOGICAL) { processAndReturnAbsentLogical(ev); return; }
+    }
+    const size_t ret0 = ret.size();
     for (auto it = s.pending.begin(); it != s.pending.end();) {
         SE se = *it;
         eng->stats.partials_scanned++;
@@ -565,12 +646,54 @@ void PreProc::processAndReturn(Ref<StreamEvent> ev, std::vector<SE>& ret) {
         } else {
             se->slots[stateId] = Ref<StreamEvent>();
             if (stateType == SG_Q_SEQUENCE) {
-                it = s.pending.erase(it);
+                // removeOnNoStateChange: SEQUENCE, except absent (AbsentStreamPreStateProcessor.java:289-291)
+                if (kind == P_STREAM && absent) ++it;
+                else it = s.pending.erase(it);
                 if (kind == P_STREAM && thisPost->callbackPre) thisPost->callbackPre->startStateReset();
             } else {
                 ++it;
             }
         }
+    }
+    if (absent) ret.resize(ret0);  // AbsentStreamPreStateProcessor.processAndReturn: always empty (:265-283)
+}
+
+// AbsentLogicalPreStateProcessor.processAndReturn (AbsentLogicalPreStateProcessor.java:255-318)
+void PreProc::processAndReturnAbsentLogical(Ref<StreamEvent> ev) {
+    KeyState& s = st();
+    for (auto it = s.pending.begin(); it != s.pending.end();) {
+        SE se = *it;
+        eng->stats.partials_scanned++;
+        if (logicalType == SG_L_OR && se->slots[partner->stateId]) {
+            it = s.pending.erase(it);
+            continue;
+        }
+        Ref<StreamEvent> cur = se->slots[stateId];
+        se->slots[stateId] = Ref<StreamEvent>(new StreamEvent(ev->seq, ev->ts));
+        runChain(se.get());
+        if (waitingTime != -1 ||
+            (stateType == SG_Q_SEQUENCE && logicalType == SG_L_AND && thisPost->nextEveryStatePre != nullptr))
+            se->slots[stateId] = cur;  // reset to the original state after processing
+        bool removed = false;
+        if (thisLast->isEventReturned) {
+            thisLast->isEventReturned = false;
+            it = s.pending.erase(it);  // passed the filter: no longer an absent candidate
+            removed = true;
+            if (stateType == SG_Q_SEQUENCE) {
+                auto& pp = partner->st().pending;
+                for (auto jt = pp.begin(); jt != pp.end(); ++jt)
+                    if (*jt == se) { pp.erase(jt); break; }
+            }
+        }
+        if (!st().stateChanged) {
+            se->slots[stateId] = cur;
+            if (stateType == SG_Q_SEQUENCE) {
+                if (removed) throw std::runtime_error("iterator removed twice (IllegalStateException in the reference)");
+                it = s.pending.erase(it);
+                removed = true;
+            }
+        }
+        if (!removed) ++it;
     }
 }
 
@@ -596,6 +719,18 @@ void PostProc::processMinCountReached(StateEvent* se) {  // CountPostStateProces
 }
 
 void PostProc::process(StateEvent* se) {
+    if (absent) {
+        StreamEvent* ev = se->slots[stateId].get();
+        thisPre->stateChanged();
+        isEventReturned = true;  // the notification to the absent pre that the event was processed
+        if (kind == P_STREAM) {  // AbsentStreamPostStateProcessor.java:36-56
+            se->ts = ev->ts;
+            if (thisPre->isStart && nextEveryStatePre != nullptr && nextEveryStatePre == thisPre)
+                thisPre->addEveryState(SE(se));
+        }                        // AbsentLogicalPostStateProcessor.java:37-49
+        thisPre->updateLastArrivalTime(ev->ts);
+        return;
+    }
     if (kind == P_COUNT) {  // CountPostStateProcessor.java:39-66
         StreamEvent* s = se->slots[stateId].get();
         int n = 1;
@@ -616,7 +751,9 @@ void PostProc::process(StateEvent* se) {
     }
     if (kind == P_LOGICAL) {  // LogicalPostStateProcessor.java:59-83
         if (logicalType == SG_L_AND) {
-            if (se->slots[partnerPre->stateId]) streamProcess(se);
+            const bool go = partnerPre->absent ? partnerPre->partnerCanProceed(se)
+                                               : (bool)se->slots[partnerPre->stateId];
+            if (go) streamProcess(se);
             else thisPre->stateChanged();
         } else {
             streamProcess(se);
@@ -637,6 +774,239 @@ void PostProc::setNextStatePre(PreProc* p) {
 void PostProc::setNextEveryStatePre(PreProc* p) {
     nextEveryStatePre = p;
     if (kind == P_LOGICAL) partnerPost->nextEveryStatePre = p;
+}
+
+// ------------------------------------------------------------------------------------------------
+// absent states and their timers
+// ------------------------------------------------------------------------------------------------
+void PreProc::notifyAt(int64_t t) {  // Scheduler.notifyAt + schedule (Scheduler.java:114-156)
+    KeyState& s = st();
+    const bool wasEmpty = s.toNotify.empty();
+    s.toNotify.push_back(t);
+    if (wasEmpty) eng->heads[id].insert({t, eng->curKey});
+    if (!eng->playback && !s.running && s.toNotify.size() == 1) {
+        // EventCaller scheduled after (time - now), or at once when that is <= 0
+        s.running = true;
+        s.fireAt = std::max(t, eng->now);
+        s.order = ++eng->schedOrder;
+        eng->callers.insert({s.fireAt, s.order, id, eng->curKey});
+    }
+}
+
+void PreProc::updateLastArrivalTime(int64_t ts) {
+    KeyState& s = st();
+    if (kind == P_LOGICAL) {  // AbsentLogicalPreStateProcessor.java:65-74
+        s.lastArrivalTime = ts;
+        return;
+    }
+    s.lastScheduledTime = ts + waitingTime;  // AbsentStreamPreStateProcessor.java:70-81
+    notifyAt(s.lastScheduledTime);
+}
+
+// PartitionCreationListener.partitionCreated (AbsentStreamPreStateProcessor.java:290-308,
+// AbsentLogicalPreStateProcessor.java:370-389), called by StateStreamRuntime.initPartition :90-97
+void PreProc::partitionCreated() {
+    KeyState& s = st();
+    if (s.started) return;
+    s.started = true;
+    if (isStart && waitingTime != -1 && s.active) {
+        if (kind == P_STREAM) s.lastScheduledTime = eng->now + waitingTime;
+        notifyAt(eng->now + waitingTime);
+    }
+}
+
+// AbsentLogicalPreStateProcessor.partnerCanProceed (:391-422)
+bool PreProc::partnerCanProceed(StateEvent* se) {
+    KeyState& s = st();
+    if (stateType == SG_Q_SEQUENCE && thisPost->nextEveryStatePre == nullptr && s.lastArrivalTime > 0) return false;
+    if (waitingTime == -1) {
+        if (thisPost->nextEveryStatePre == nullptr) return !se->slots[stateId];
+        if (s.lastArrivalTime > 0) {
+            s.lastArrivalTime = 0;
+            init();
+            return false;
+        }
+        return true;
+    }
+    return (bool)se->slots[stateId];
+}
+
+// Absent*PreStateProcessor.sendEvent (AbsentStreamPreStateProcessor.java:229-246,
+// AbsentLogicalPreStateProcessor.java:228-247): the timer thread delivers the match at once
+void PreProc::sendAbsentEvent(const SE& se) {
+    if (thisPost->hasNext) eng->project(se.get());
+    if (thisPost->nextStatePre) thisPost->nextStatePre->addState(se);
+    if (thisPost->nextEveryStatePre) {
+        thisPost->nextEveryStatePre->addEveryState(se);
+    } else if (isStart) {
+        st().active = false;
+        if (kind == P_LOGICAL && logicalType == SG_L_OR && partner->absent) partner->st().active = false;
+    }
+    if (thisPost->callbackPre) thisPost->callbackPre->startStateReset();
+}
+
+// the TIMER event of this processor's scheduler for the current key, at `currentTime`
+void PreProc::processTimer(int64_t currentTime) {
+    KeyState& s = st();
+    if (!s.active) return;
+    std::vector<SE> ret;
+    if (kind == P_STREAM) {  // AbsentStreamPreStateProcessor.process (:151-227)
+        bool initialize = isStart && s.newAndEvery.empty() && s.pending.empty();
+        if (initialize && stateType == SG_Q_SEQUENCE && thisPost->nextEveryStatePre == nullptr &&
+            s.lastScheduledTime > 0)
+            initialize = false;
+        if (initialize) {
+            addState(SE(new StateEvent(eng->nslots)));
+        } else if (stateType == SG_Q_SEQUENCE && !s.newAndEvery.empty()) {
+            resetState();
+        }
+        updateState();
+        for (auto it = s.pending.begin(); it != s.pending.end();) {
+            SE se = *it;
+            eng->stats.partials_scanned++;
+            if (isExpired(se.get(), currentTime)) {
+                it = s.pending.erase(it);
+                if (withinEveryPre != nullptr && thisPost->nextEveryStatePre != this) {
+                    if (!thisPost->nextEveryStatePre) throw std::runtime_error("NullPointerException in the reference timer path");
+                    thisPost->nextEveryStatePre->addEveryState(se);
+                }
+                continue;
+            }
+            if ((se->ts == -1 && currentTime >= s.lastScheduledTime) ||
+                (se->ts != -1 && currentTime >= se->ts + waitingTime)) {
+                it = s.pending.erase(it);
+                se->ts = currentTime;
+                ret.push_back(se);
+                continue;
+            }
+            ++it;
+        }
+        if (withinEveryPre) withinEveryPre->updateState();
+        const bool notProcessed = ret.empty();
+        for (auto& se : ret) sendAbsentEvent(se);
+        KeyState& s2 = st();
+        const int64_t actual = eng->now;  // TimestampGenerator.currentTime()
+        if (actual > waitingTime + currentTime) s2.lastScheduledTime = actual + waitingTime;
+        if (notProcessed && s2.lastScheduledTime < currentTime) {
+            s2.lastScheduledTime = currentTime + waitingTime;
+            notifyAt(s2.lastScheduledTime);
+        }
+        return;
+    }
+    // AbsentLogicalPreStateProcessor.process (:121-209)
+    bool notProcessed = true;
+    if (currentTime >= s.lastArrivalTime + waitingTime) {
+        if (isStart && stateType == SG_Q_SEQUENCE && s.newAndEvery.empty() && s.pending.empty()) {
+            addState(SE(new StateEvent(eng->nslots)));
+        } else if (stateType == SG_Q_SEQUENCE && !s.newAndEvery.empty()) {
+            resetState();
+        }
+        updateState();
+        SE expired;
+        for (auto it = s.pending.begin(); it != s.pending.end();) {
+            SE se = *it;
+            eng->stats.partials_scanned++;
+            if (isExpired(se.get(), currentTime)) {
+                expired = se;
+                it = s.pending.erase(it);
+                continue;
+            }
+            StreamEvent* own = se->slots[stateId].get();
+            const bool passed = own ? currentTime >= own->ts + waitingTime : currentTime >= se->ts + waitingTime;
+            if (passed) {
+                it = s.pending.erase(it);
+                const bool partnerIn = (bool)se->slots[partner->stateId];
+                if (logicalType == SG_L_OR && !partnerIn) {
+                    add_event(se.get(), stateId, Ref<StreamEvent>(new StreamEvent(SG_BLANK_SEQ, -1)));
+                    ret.push_back(se);
+                } else if (logicalType == SG_L_AND && partnerIn) {
+                    ret.push_back(se);
+                } else if (logicalType == SG_L_AND && !partnerIn) {
+                    add_event(se.get(), stateId, Ref<StreamEvent>(new StreamEvent(SG_BLANK_SEQ, -1)));
+                }
+                continue;
+            }
+            ++it;
+        }
+        if (expired && withinEveryPre) {
+            withinEveryPre->addEveryState(expired);
+            withinEveryPre->updateState();
+        }
+        notProcessed = ret.empty();
+        for (auto& se : ret) {
+            se->ts = currentTime;
+            sendAbsentEvent(se);
+        }
+        st().lastArrivalTime = 0;
+    }
+    if (thisPost->nextEveryStatePre != nullptr || (notProcessed && isStart)) {
+        const int64_t nextBreak = st().lastArrivalTime == 0 ? eng->now + waitingTime : st().lastArrivalTime + waitingTime;
+        notifyAt(nextBreak);
+    }
+}
+
+// Scheduler.sendTimerEvents (Scheduler.java:172-210) for the current key
+void Engine::sendTimerEvents(PreProc* p) {
+    curTrigger = SG_TIMER_SEQ;
+    for (;;) {
+        KeyState& s = state(p->id);
+        if (s.toNotify.empty() || s.toNotify.front() > now) break;
+        const int64_t t = s.toNotify.front();
+        s.toNotify.pop_front();
+        heads[p->id].erase({t, curKey});
+        if (!s.toNotify.empty()) heads[p->id].insert({s.toNotify.front(), curKey});
+        p->processTimer(t);
+    }
+}
+
+void Engine::advanceTime(int64_t t) {
+    if (playback) {
+        // TimestampGeneratorImpl.setCurrentTimestamp -> each Scheduler's time-change listener, in
+        // registration order (Scheduler.java:73-104)
+        if (t < lastEventTs) return;
+        lastEventTs = t;
+        now = t;
+        for (PreProc* p : startup) {
+            std::vector<std::pair<int64_t, uint32_t>> due;
+            for (auto& h : heads[p->id]) {
+                if (h.first > t) break;
+                due.push_back(h);
+            }
+            // TreeMultimap<Long, SchedulerState> with SchedulerState.compareTo == 0 keeps ONE state per
+            // distinct due time; which one depends on Java HashMap order
+            for (size_t i = 1; i < due.size(); i++)
+                if (due[i].first == due[i - 1].first)
+                    throw std::runtime_error("two partition keys share a timer due time at one clock advance "
+                                             "(reference Scheduler collapse quirk, SURVEY A.10): input not supported");
+            const uint32_t save = curKey;
+            for (auto& d : due) {
+                curKey = d.second;
+                sendTimerEvents(p);
+            }
+            curKey = save;
+        }
+        return;
+    }
+    // wall clock: the EventCallers run in time order (Scheduler.EventCaller.run, Scheduler.java:264-298)
+    const uint32_t save = curKey;
+    while (!callers.empty() && std::get<0>(*callers.begin()) <= t) {
+        auto c = *callers.begin();
+        callers.erase(callers.begin());
+        now = std::max(now, std::get<0>(c));
+        PreProc* p = procs[std::get<2>(c)].get();
+        curKey = std::get<3>(c);
+        sendTimerEvents(p);
+        KeyState& s = state(p->id);
+        if (!s.toNotify.empty()) {
+            s.fireAt = std::max(s.toNotify.front(), now);
+            s.order = ++schedOrder;
+            callers.insert({s.fireAt, s.order, p->id, curKey});
+        } else {
+            s.running = false;
+        }
+    }
+    curKey = save;
+    if (t > now) now = t;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -913,14 +1283,23 @@ struct Builder {
         switch (tag) {
         case SG_N_STREAM: {  // StateInputStreamParser.java:167-225
             uint32_t slot = next(), stream = next(), fpc = next(), flen = next(), absent = next();
-            next(); next();  // for_ms
-            if (absent) throw std::runtime_error("absent states are not supported by the oracle yet");
-            if (!pre) pre = newPre(P_STREAM);
+            uint32_t flo = next(), fhi = next();
+            const int64_t forMs = (int64_t)((uint64_t)flo | ((uint64_t)fhi << 32));
+            if (!pre) {
+                pre = newPre(P_STREAM);
+                if (absent) {
+                    if (forMs < 0) throw std::runtime_error("absent stream state needs a 'for' time");
+                    e->startup.push_back(pre);  // startupPreStateProcessors (StateInputStreamParser.java:181-197)
+                }
+            }
+            pre->absent = absent != 0;
+            pre->waitingTime = absent ? forMs : -1;
             pre->stateId = (int)slot;
             pre->isStart = isStart;
             pre->filterPc = fpc;
             pre->filterLen = flen;
             if (!post) post = newPost(P_STREAM);
+            post->absent = absent != 0;
             post->stateId = (int)slot;
             post->thisPre = pre;
             pre->thisPost = post;
@@ -969,6 +1348,16 @@ struct Builder {
             lpost2->partnerPost = lpost1;
             lp1->partner = lp2;
             lp2->partner = lp1;
+            // AbsentLogicalPreStateProcessor pres join startupPreStateProcessors at creation, element 1
+            // first (StateInputStreamParser.java:289-320)
+            {
+                size_t q = pos;
+                const bool a1 = peekAbsent(q);
+                skip_at(q);
+                const bool a2 = peekAbsent(q);
+                if (a1) e->startup.push_back(lp1);
+                if (a2) e->startup.push_back(lp2);
+            }
             // element 1 is encoded first, but element 2 must be parsed (and slotted) first
             size_t save = pos;
             skip();               // element 1
@@ -1002,6 +1391,17 @@ struct Builder {
         }
         }
         throw std::runtime_error("bad node tag in IR");
+    }
+
+    bool peekAbsent(size_t q) const {  // the node at q is an absent stream state
+        return q < n && w[q] == SG_N_STREAM && q + 5 < n && w[q + 5] != 0;
+    }
+    void skip_at(size_t& q) {
+        size_t save = pos;
+        pos = q;
+        skip();
+        q = pos;
+        pos = save;
     }
 
     void skip() {
@@ -1049,6 +1449,7 @@ void build(Engine* e, const void* ir, size_t len) {
     e->within = (int64_t)((uint64_t)w[5] | ((uint64_t)w[6] << 32));
     uint32_t offStreams = w[7], offNodes = w[8], nNodes = w[9], offCode = w[10], nCode = w[11];
     e->partitioned = (w[12] & SG_IR_F_PARTITIONED) != 0;
+    e->playback = (w[12] & SG_IR_F_PLAYBACK) != 0;
     size_t nw = e->ir.size();
     if (offCode + nCode > nw || offNodes + nNodes > nw) throw std::runtime_error("IR offsets out of range");
     e->code = w + offCode;
@@ -1080,6 +1481,7 @@ void build(Engine* e, const void* ir, size_t len) {
         }
     }
     e->root->first->thisLast = e->root->last;
+    e->heads.resize(e->procs.size());
     // receiver kinds: Pattern/Sequence Multi when the stream appears more than once (:91-110)
     for (auto& r : e->receivers) {
         r.sequence = e->qtype == SG_Q_SEQUENCE;
@@ -1106,6 +1508,7 @@ void init_key(Engine* e, uint32_t key) {
         uint32_t save = e->curKey;
         e->curKey = key;
         e->root->init();
+        for (PreProc* p : e->startup) p->partitionCreated();  // StateStreamRuntime.initPartition :90-97
         e->curKey = save;
     }
 }
@@ -1129,7 +1532,7 @@ int sgo_engine_create(const void* ir, size_t ir_len, const sg_config* cfg, sgo_e
         auto* h = new sgo_engine();
         build(&h->e, ir, ir_len);
         (void)cfg;
-        if (!h->e.partitioned) init_key(&h->e, 0);  // unpartitioned: QueryRuntimeImpl.start seeds once
+        // unpartitioned: QueryRuntimeImpl.start seeds once, at the first sgo_advance_time / push
         *out = h;
         return SG_OK;
     } catch (const std::exception& ex) {
@@ -1153,6 +1556,7 @@ int sgo_push_batch(sgo_engine* h, const sg_batch* b) {
             e.haveSeq0 = true;
         }
         if (b->seq_base < e.seq0 + e.seqLoc.size()) return fail(SG_ERR_INVALID, "sequence numbers must increase");
+        if (!e.partitioned) init_key(&e, 0);
         // store rows
         uint32_t row0 = ss.cols.empty() ? 0 : (uint32_t)ss.cols[0].v.size();
         if (ss.cols.empty()) row0 = (uint32_t)(e.seqLoc.size());  // stream without attributes
@@ -1207,8 +1611,18 @@ int sgo_push_batch(sgo_engine* h, const sg_batch* b) {
 }
 
 int sgo_advance_time(sgo_engine* h, int64_t now) {
-    (void)h; (void)now;
-    return SG_OK;  // only absent states use the playback clock (not in the oracle yet)
+    if (!h) return fail(SG_ERR_INVALID, "null argument");
+    Engine& e = h->e;
+    try {
+        if (!e.partitioned && (e.keyInit.empty() || !e.keyInit[0])) {
+            if (!e.playback) e.now = std::max(e.now, now);  // start(): wall clock now
+            init_key(&e, 0);
+        }
+        e.advanceTime(now);
+        return SG_OK;
+    } catch (const std::exception& ex) {
+        return fail(SG_ERR_STATE, ex.what());
+    }
 }
 
 int sgo_poll_matches(sgo_engine* h, uint32_t mem, sg_match_batch* out) {

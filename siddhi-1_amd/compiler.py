@@ -27,6 +27,7 @@ SG_IR_MAGIC = 0x52494753
 SG_IR_VERSION = 1
 SG_IR_HDR_WORDS = 14
 SG_IR_F_PARTITIONED = 1
+SG_IR_F_PLAYBACK = 2
 SG_COUNT_ANY = 0x7FFFFFFF
 
 TYPE_CODE = {"STRING": 0, "INT": 1, "LONG": 2, "FLOAT": 3, "DOUBLE": 4, "BOOL": 5}
@@ -520,7 +521,9 @@ def compile_query(app: q.App, query: q.Query, strings) -> CompiledQuery:
     hdr = [SG_IR_MAGIC, SG_IR_VERSION, 0 if si.kind == "PATTERN" else 1, len(ctx.streams),
            len(ctx.slots), within & 0xFFFFFFFF, (within >> 32) & 0xFFFFFFFF,
            off_streams, off_nodes, len(nodes), off_code, len(em.code),
-           SG_IR_F_PARTITIONED if partition_keys else 0, off_slots]
+           (SG_IR_F_PARTITIONED if partition_keys else 0) |
+           (SG_IR_F_PLAYBACK if any(a.name.lower() == "app:playback" for a in app.annotations) else 0),
+           off_slots]
     words = hdr + stream_words + slot_words + nodes + em.code
     ir = struct.pack(f"<{len(words)}I", *[w & 0xFFFFFFFF for w in words])
 

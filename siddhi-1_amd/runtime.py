@@ -18,6 +18,7 @@ host (QuerySelector.processNoGroupBy, C/query/selector/QuerySelector.java:162-20
 """
 from __future__ import annotations
 
+import re
 import struct
 import time
 from typing import Callable, Dict, List, Optional
@@ -178,6 +179,10 @@ def _compare(op, dom, a, b):
 # ------------------------------------------------------------------------------------------------
 # host event store: payloads by arrival seq (strings never go to the device)
 # ------------------------------------------------------------------------------------------------
+TIMER_SEQ = 0xFFFFFFFFFFFFFFFF      # SG_TIMER_SEQ: trigger of a timer-emitted match
+BLANK_SEQ = 0xFFFFFFFFFFFFFFFE      # SG_BLANK_SEQ: the attribute-less event an absent state adds
+
+
 class _EventStore:
     def __init__(self):
         self.rows = []          # seq -> (stream name, ts, data tuple)
@@ -187,7 +192,14 @@ class _EventStore:
         return len(self.rows) - 1
 
     def get(self, seq):
+        if int(seq) == BLANK_SEQ:
+            return (None, -1, _NullRow())
         return self.rows[int(seq)]
+
+
+class _NullRow:
+    def __getitem__(self, i):
+        return None
 
 
 class StringDictionary:
@@ -284,7 +296,7 @@ class _QueryRuntime:
             chains = []
             for s in range(m.slot_seq.shape[1]):
                 ln = int(m.chain_len[i, s])
-                chains.append([int(x) for x in m.slot_seq[i, s, :ln]])
+                chains.append([int(x) for x in m.slot_seq[i, s, :ln]])   # BLANK_SEQ: absent-state event
             data = []
             for name, typ, t in self.cq.select:
                 v = self._eval(t, chains, store)
@@ -293,13 +305,15 @@ class _QueryRuntime:
         return out
 
     def dispatch(self, projected):
-        """Deliver in trigger order; one callback call per trigger event (ReturnEventHolder)."""
+        """Deliver in trigger order; one callback call per trigger event (ReturnEventHolder).  A match
+        emitted by a timer (absent state) is delivered on its own, at once
+        (AbsentStreamPreStateProcessor.sendEvent -> QuerySelector.process per StateEvent)."""
         if not projected:
             return
         groups = []
         cur = None
         for trig, ts, data in projected:
-            if cur is None or cur[0] != trig:
+            if cur is None or cur[0] != trig or trig == TIMER_SEQ:
                 cur = (trig, [])
                 groups.append(cur)
             cur[1].append(Event(ts, data))
@@ -318,17 +332,19 @@ class InputHandler:
         self.stream = stream
 
     def send(self, *args):
-        # send(Object[]) | send(long, Object[]) | send(Event) | send(Event[])
+        # send(Object[]) | send(long, Object[]) | send(Event) | send(Event[])   (InputHandler.java:51-97)
+        # In playback mode every form but send(Object[]) first sets the event clock (to the last
+        # event's timestamp for Event[]); send(Object[]) stamps the wall clock and leaves it alone.
         if len(args) == 2:
-            self.app_rt._send(self.stream, [(int(args[0]), list(args[1]))])
+            self.app_rt._send(self.stream, [(int(args[0]), list(args[1]))], explicit=True)
             return
         a = args[0]
         if isinstance(a, Event):
-            self.app_rt._send(self.stream, [(a.timestamp, a.data)])
+            self.app_rt._send(self.stream, [(a.timestamp, a.data)], explicit=True)
         elif isinstance(a, (list, tuple)) and a and isinstance(a[0], Event):
-            self.app_rt._send(self.stream, [(e.timestamp, e.data) for e in a])
+            self.app_rt._send(self.stream, [(e.timestamp, e.data) for e in a], explicit=True)
         else:
-            self.app_rt._send(self.stream, [(self.app_rt.current_time(), list(a))])
+            self.app_rt._send(self.stream, [(self.app_rt.wall_time(), list(a))], explicit=False)
 
 
 class SiddhiAppRuntime:
@@ -340,8 +356,14 @@ class SiddhiAppRuntime:
         self.stream_callbacks: Dict[str, List[StreamCallback]] = {}
         self.queries: List[_QueryRuntime] = []
         self.by_name: Dict[str, _QueryRuntime] = {}
-        self.playback = any(a.name.lower() == "app:playback" for a in self.app.annotations)
-        self._last_ts = None
+        pb = [a for a in self.app.annotations if a.name.lower() == "app:playback"]
+        self.playback = bool(pb)
+        # TimestampGeneratorImpl: lastEventTimestamp (playback clock) and the idle heartbeat
+        self._event_time = 0
+        self._idle = _time_ms(pb[0].get("idle.time")) if pb else None
+        self._increment = _time_ms(pb[0].get("increment")) if pb else None
+        self._last_sys = None
+        self._wall = None            # virtual wall clock (ms) of a test harness; None = real time
         self.key_dicts = {}
         for i, qq in enumerate(self.app.queries):
             cq = cp.compile_query(self.app, qq, self.strings)
@@ -370,7 +392,48 @@ class SiddhiAppRuntime:
             self.stream_callbacks.setdefault(name, []).append(cb)
 
     def start(self):
+        """SiddhiAppRuntimeImpl.start -> QueryRuntimeImpl.start -> initPartition (unpartitioned queries
+        seed their start states now; absent start states arm their timers)."""
         self.started = True
+        for qr in self.queries:
+            qr.engine.advance_time(self.current_time())
+            qr.dispatch(qr.project(qr.engine.poll(), self.store))
+
+    # -- clock -------------------------------------------------------------------------------------
+    def wall_time(self):
+        return self._wall if self._wall is not None else int(time.time() * 1000)
+
+    def set_wall_clock(self, ms):
+        """Test-harness hook: run on a virtual wall clock starting at `ms`."""
+        self._wall = int(ms)
+
+    def advance_wall_clock(self, ms):
+        """Test-harness hook: let virtual wall time pass until `ms` (what Thread.sleep does in the
+        reference tests): wall-clock timers fire (Scheduler.EventCaller), and in playback mode with
+        idle.time the heartbeat advances the event clock (TimestampGeneratorImpl.TimeInjector)."""
+        ms = int(ms)
+        if self.playback:
+            if self._idle is not None and self._idle >= 0 and self._last_sys is not None:
+                while self._last_sys + self._idle <= ms:
+                    self._wall = self._last_sys + self._idle
+                    self._set_event_time(self._event_time + (self._increment or 0))
+            self._wall = ms
+            return
+        self._wall = ms
+        if self.started:
+            self._fire_timers(ms)
+
+    def _fire_timers(self, now):
+        for qr in self.queries:
+            qr.engine.advance_time(now)
+            qr.dispatch(qr.project(qr.engine.poll(), self.store))
+
+    def _set_event_time(self, ts):
+        """TimestampGeneratorImpl.setCurrentTimestamp (playback)."""
+        if ts >= self._event_time:
+            self._event_time = ts
+            self._fire_timers(ts)
+            self._last_sys = self.wall_time()
 
     def shutdown(self):
         for qr in self.queries:
@@ -380,9 +443,8 @@ class SiddhiAppRuntime:
     add_callback = addCallback
 
     def current_time(self):
-        if self.playback and self._last_ts is not None:
-            return self._last_ts
-        return int(time.time() * 1000)
+        """TimestampGenerator.currentTime(): the event clock in playback mode, else the wall clock."""
+        return self._event_time if self.playback else self.wall_time()
 
     # internals ----------------------------------------------------------------------------------
     def _emit_stream(self, name, events):
@@ -412,16 +474,20 @@ class SiddhiAppRuntime:
             nulls.append(isnull if isnull.any() else None)
         return cols, nulls
 
-    def _send(self, stream, events):
+    def _send(self, stream, events, explicit=True):
         if stream not in self.app.streams:
             raise KeyError(stream)
         sd = self.app.streams[stream]
+        if self.playback:
+            if explicit and events:
+                self._set_event_time(events[-1][0])
+        elif self.started:
+            self._fire_timers(self.wall_time())
         seqs = []
         for ts, data in events:
             if len(data) != len(sd.attrs):
                 raise ValueError(f"event for {stream} has {len(data)} attributes, expected {len(sd.attrs)}")
             seqs.append(self.store.add(stream, ts, tuple(data)))
-            self._last_ts = ts
         for qr in self.queries:
             si = qr.cq.stream_index(stream)
             if si < 0:
@@ -460,6 +526,22 @@ class SiddhiAppRuntime:
                 start = end
             m = qr.engine.poll()
             qr.dispatch(qr.project(m, self.store))
+
+
+def _time_ms(v):
+    """'10 milliseconds' / '2 sec' / '1 min' -> ms (annotation time values)."""
+    if v is None:
+        return None
+    m = re.fullmatch(r"\s*(\d+)\s*([a-zA-Z]*)\s*", str(v))
+    if not m:
+        raise SiddhiAppCreationException(f"bad time value {v!r}")
+    n, u = int(m.group(1)), m.group(2).lower()
+    mult = {"": 1, "ms": 1, "millisec": 1, "millisecond": 1, "milliseconds": 1, "sec": 1000, "second": 1000,
+            "seconds": 1000, "min": 60000, "minute": 60000, "minutes": 60000, "hour": 3600000,
+            "hours": 3600000}
+    if u not in mult:
+        raise SiddhiAppCreationException(f"bad time unit in {v!r}")
+    return n * mult[u]
 
 
 class SiddhiManager:

@@ -553,6 +553,10 @@ class Parser:
             for s in (first, second):
                 if not isinstance(s, EStream):
                     raise SiddhiParserException("logical states combine plain stream states only")
+            if second.absent and not first.absent:
+                # the visitor puts the absent element first: State.logicalNotAnd(absent, present) /
+                # State.logicalOr(absent, present) (SiddhiQLBaseVisitorImpl.java:1019-1042)
+                first, second = second, first
             return ELogical(typ, first, second)
         return first
 
@@ -610,7 +614,7 @@ class Parser:
     def sequence_chain_top(self):
         # every_sequence_source_chain: EVERY? sequence_source ',' sequence_source_chain
         every = bool(self.accept("every"))
-        if every and self.at("("):
+        if self.at("("):
             self.expect("(")
             first = self.sequence_chain()
             self.expect(")")

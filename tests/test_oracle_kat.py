@@ -4,12 +4,14 @@ Each case is one @Test method of the reference test suite transcribed by tests/g
 (inputs + the expected outputs hard-coded in the Java test).  The oracle is run through the same
 host compiler / API mirror the product uses.
 """
+import os
+
 import pytest
 
 from kat_runner import load_cases, run_case
 from oracle_backend import oracle_manager
 
-FEATURES_UNSUPPORTED = {"absent"}   # `not ... for T` (timers) is not in the oracle yet
+FEATURES_UNSUPPORTED = set()
 
 # reference tests whose apps use constructs outside the pattern hot path (SURVEY §8f / out of scope);
 # they must fail at compile time with a clear message, never silently.
@@ -18,10 +20,16 @@ KNOWN_UNSUPPORTED = {
     "CountPatternTestCase::testQuery18": "aggregate count() in select (SURVEY §8f row f1)",
     "CountPatternTestCase::testQuery19": "aggregate count() in select (SURVEY §8f row f1)",
     "CountPatternTestCase::testQuery20": "aggregate count() in select (SURVEY §8f row f1)",
+    "CountPatternTestCase::testQuery14": "having + instanceOfFloat() in select (SURVEY §8f row f1)",
     "PatternPartitionTestCase::testPatternPartitionQuery30": "inner partition streams (#Stream)",
     "PatternPartitionTestCase::testPatternPartitionQuery32": "unpartitioned stream inside a partition",
     "PatternPartitionTestCase::testPatternPartitionQuery33": "non-pattern query in the app",
 }
+
+# faithful but slow: a playback app started at event time 0 whose `every not ... for 1 sec` timer
+# re-arms itself once per virtual second until it catches up with the first event's epoch-ms
+# timestamp (~1.5e9 timer events, also in the reference); minutes in the oracle.  SG_SLOW_KATS=1 runs them.
+SLOW = {"EveryAbsentSequenceTestCase::testQueryAbsent4_1", "EveryAbsentSequenceTestCase::testQueryAbsent4_2"}
 
 CASES = [(f, c) for f, c in load_cases() if "skip" not in c]
 
@@ -37,6 +45,8 @@ def test_oracle_matches_reference_kat(fc):
     if FEATURES_UNSUPPORTED & set(case.get("features", [])):
         pytest.skip("absent states are not restated yet")
     key = f"{f}::{case['name']}"
+    if key in SLOW and not os.environ.get("SG_SLOW_KATS"):
+        pytest.skip("slow (see SLOW); SG_SLOW_KATS=1 runs it")
     if key in KNOWN_UNSUPPORTED:
         from importlib import import_module
         sa = import_module("siddhi-1_amd")
