@@ -393,8 +393,9 @@ struct Engine {
     std::vector<PreProc*> startup;              // startupPreStateProcessors (absent pres, parse order)
     // per scheduler (absent pre): keys whose queue is not empty, by head (playback listener)
     std::vector<std::set<std::pair<int64_t, uint32_t>>> heads;   // [proc id]
-    // scheduled EventCallers (wall-clock mode): (fireAt, order, proc, key)
-    std::set<std::tuple<int64_t, uint64_t, int, uint32_t>> callers;
+    // scheduled EventCallers (wall-clock mode): (fireAt, key, order, proc).  Callers of different keys
+    // due at the same time run in key order (in the reference they race on the executor's threads).
+    std::set<std::tuple<int64_t, uint32_t, uint64_t, int>> callers;
 
     KeyState& state(int proc) { return keyStates[curKey][proc]; }
     void advanceTime(int64_t t);
@@ -789,7 +790,7 @@ void PreProc::notifyAt(int64_t t) {  // Scheduler.notifyAt + schedule (Scheduler
         s.running = true;
         s.fireAt = std::max(t, eng->now);
         s.order = ++eng->schedOrder;
-        eng->callers.insert({s.fireAt, s.order, id, eng->curKey});
+        eng->callers.insert({s.fireAt, eng->curKey, s.order, id});
     }
 }
 
@@ -993,14 +994,14 @@ void Engine::advanceTime(int64_t t) {
         auto c = *callers.begin();
         callers.erase(callers.begin());
         now = std::max(now, std::get<0>(c));
-        PreProc* p = procs[std::get<2>(c)].get();
-        curKey = std::get<3>(c);
+        PreProc* p = procs[std::get<3>(c)].get();
+        curKey = std::get<1>(c);
         sendTimerEvents(p);
         KeyState& s = state(p->id);
         if (!s.toNotify.empty()) {
             s.fireAt = std::max(s.toNotify.front(), now);
             s.order = ++schedOrder;
-            callers.insert({s.fireAt, s.order, p->id, curKey});
+            callers.insert({s.fireAt, curKey, s.order, p->id});
         } else {
             s.running = false;
         }

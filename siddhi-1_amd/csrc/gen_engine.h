@@ -1,0 +1,143 @@
+// gen_engine.h — the general NFA engine: every query shape of the IR (stream / next / every / logical /
+// count / absent states, PATTERN and SEQUENCE) on the device.  Shared by the host glue
+// (gen_engine.hip, host part) and the advance kernels (gen_engine.hip, device part).
+//
+// The processor graph that StateInputStreamParser builds (util/parser/StateInputStreamParser.java:76-408)
+// is lowered on the host into flat tables (GenProgram).  On the device one lane owns one partition key
+// and runs that key's processors over its events in arrival order.  All per-key state lives in HBM,
+// interleaved across keys (word w of key k at w * K + k) so that lanes reading the same field of
+// their keys issue one coalesced access:
+//   per processor  KeyState: flags, absent-state times, scheduler queue, pending and newAndEvery
+//                  lists (StreamPreStateProcessor.StreamPreState, StreamPreStateProcessor.java:435-498)
+//   StateEvent pool  partial matches (event/state/StateEvent.java:42-258), reference counted
+//   StreamEvent pool slot events with their attributes captured at creation
+//                  (event/stream/StreamEvent; count chains linked by `next`)
+#pragma once
+
+#include <stdint.h>
+
+#define GEN_MAXP 16      // processors per query
+#define GEN_MAXS 8       // input streams
+#define GEN_MAXSLOT 16   // state slots
+#define GEN_MAXA 16      // attributes per stream
+#define GEN_MAXCODE 1024 // filter bytecode words
+#define GEN_NONE (-1)
+#define GEN_NIL 0xffffu  // null pool index
+
+enum { GK_STREAM = 0, GK_COUNT = 1, GK_LOGICAL = 2 };
+
+// KeyState flag bits
+enum {
+    GF_CHANGED = 1u, GF_INIT = 2u, GF_SUCCESS = 4u, GF_SSRESET = 8u, GF_INACTIVE = 16u, GF_STARTED = 32u,
+    GF_RUNNING = 64u
+};
+
+struct GenPre {
+    int32_t kind, absent, stateId, isStart;
+    int64_t waiting;
+    int32_t withinEvery, thisPost, thisLast, countPost;
+    uint32_t fpc, flen;
+    int32_t minCount, maxCount, logicalType, partner;
+};
+
+struct GenPost {
+    int32_t kind, absent, stateId, thisPre;
+    int32_t nextStatePre, nextEveryStatePre, callbackPre, hasNext;
+    int32_t minCount, maxCount, logicalType, partnerPre, partnerPost, pad;
+};
+
+struct GenRecv {
+    int32_t multi, n, nStateProcs, pad;
+    int32_t procs[GEN_MAXP];        // nextProcessors (setup order); events visit them in reverse
+    int32_t stateProcs[GEN_MAXP];   // stateProcessorsForStream
+};
+
+struct GenProgram {
+    int32_t nprocs, nslots, qtype, playback, partitioned, nstreams;
+    int64_t within;
+    int32_t nStartIds, nInit, nReset, nUpdate, nAll, nStartup;
+    int32_t startIds[GEN_MAXSLOT];
+    int32_t initOrder[GEN_MAXP * 2], resetOrder[GEN_MAXP * 2], updateOrder[GEN_MAXP * 2];
+    int32_t allProcs[GEN_MAXP], startup[GEN_MAXP];
+    int32_t rootFirst, rootLast;
+    GenPre pre[GEN_MAXP];
+    GenPost post[GEN_MAXP];
+    GenRecv recv[GEN_MAXS];
+    int32_t slotStream[GEN_MAXSLOT];
+    int32_t nattr[GEN_MAXS];
+    int32_t attrType[GEN_MAXS][GEN_MAXA];
+    uint32_t ncode;
+    uint32_t code[GEN_MAXCODE];
+    // capacities and the per-key block layout (words)
+    uint32_t L, Q, STCAP, SECAP, NA, MC;  // list, timer queue, pools, attrs per event, max chain out
+    uint32_t ksWords;                       // words of one processor's KeyState
+    uint32_t offKS, offST, offSTfree, offSE, offSEfree, offDef, blockWords;
+    uint32_t stWords, seWords, DEF;
+};
+
+// KeyState field offsets inside a processor's record
+#define KS_FLAGS 0
+#define KS_LST 1    // lastScheduledTime (2 words)
+#define KS_LAT 3    // lastArrivalTime (2)
+#define KS_FIRE 5   // fireAt (2)
+#define KS_ORDER 7  // scheduler order (1)
+#define KS_QHEAD 8  // queue head index
+#define KS_QLEN 9
+#define KS_PLEN 10  // pending length
+#define KS_NLEN 11  // newAndEvery length
+#define KS_LISTS 12 // pending[L], newAndEvery[L], queue[Q] (2 words each)
+
+// StateEvent record: ts(2) type(1) rc(1) slots[nslots]
+#define ST_TS 0
+#define ST_TYPE 2
+#define ST_RC 3
+#define ST_SLOTS 4
+// StreamEvent record: seq(2) ts(2) next(1) rc(1) null(1) attrs[NA](2 each)
+#define SE_SEQ 0
+#define SE_TS 2
+#define SE_NEXT 4
+#define SE_RC 5
+#define SE_NULL 6
+#define SE_ATTR 7
+
+enum { GST_SCANNED = 0, GST_CREATED, GST_MATCHES, GST_KEYS, GST_N };
+enum { GERR_CAP = 1, GERR_MATCHCAP = 2, GERR_KEY = 4, GERR_COLLAPSE = 8, GERR_CHAIN = 16, GERR_REF = 32 };
+
+struct GenBatch {
+    uint32_t n, stream;
+    uint64_t seq_base;
+    const int64_t* ts;
+    const void* col[GEN_MAXA];
+    const uint8_t* nul[GEN_MAXA];
+    const uint32_t* sidx;      // key-sorted batch positions
+    const uint32_t* seg_begin; // [K]
+    const uint32_t* seg_end;
+};
+
+struct GenOut {
+    // raw matches: per match [trigger seq u64][ts i64][key u32][len[nslots] u32][seqs nslots*MC u64], as words
+    uint32_t* raw;
+    unsigned long long* raw_count;   // matches reserved
+    uint64_t raw_cap;                // in matches
+    uint32_t recWords;
+    // per batch event: matches it triggered and the first raw index (contiguous)
+    uint32_t* t_cnt;
+    uint32_t* t_first;
+    // timer matches: sort keys per raw match (k1 sched or 0, k2 due/fireAt, k3 key, raw index)
+    int64_t* tk2;
+    uint32_t* tk1;
+    uint32_t* tk3;
+    unsigned long long* nvalid;      // timer matches emitted by a sweep
+    unsigned long long* stats;
+    uint32_t* err;
+};
+
+struct GenArgs {
+    const GenProgram* G;
+    uint32_t* state;     // [blockWords][K] interleaved
+    uint32_t K;
+    GenBatch b;
+    GenOut o;
+    int64_t now;         // engine clock during a push; the advance target for a timer sweep
+    int64_t now0;        // the engine clock before a wall-clock timer sweep
+};

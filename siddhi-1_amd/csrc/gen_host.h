@@ -1,0 +1,22 @@
+// gen_host.h — host API of the general NFA engine (gen_host.hip), used by the C-ABI (sg_engine.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+#include "../../include/siddhi_gpu.h"
+
+struct GenEngine;
+struct GenProgram;
+
+// throws std::runtime_error (unsupported shape / allocation failure)
+GenProgram* gen_build_program(const uint32_t* ir, size_t nwords, uint32_t partial_capacity);
+GenEngine* gen_create(const uint32_t* ir, size_t nwords, const sg_config& cfg, hipStream_t stream);
+void gen_destroy(GenEngine* e);
+int gen_push(GenEngine* e, const sg_batch* b, std::string& msg);
+int gen_advance(GenEngine* e, int64_t now, std::string& msg);
+int gen_poll(GenEngine* e, uint32_t mem, sg_match_batch* out, std::string& msg);
+void gen_release(GenEngine* e);
+void gen_stats(GenEngine* e, sg_stats* out);
+void gen_synchronize(GenEngine* e);

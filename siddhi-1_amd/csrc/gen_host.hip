@@ -1,0 +1,809 @@
+// gen_host.hip — host side of the general NFA engine (gen_engine.h, gen_kernels.hip).
+//
+// Lowers the IR's state tree into GenProgram the way StateInputStreamParser.parse wires processors
+// (util/parser/StateInputStreamParser.java:148-408: Stream :167-225, Next :227-259, Every :261-287,
+// Logical :289-378, Count :380-403; then parseInputStream :76-146 for within / start states /
+// thisLast), allocates the per-key state in HBM and runs per push:
+//   key grouping (stable radix sort of key ids, per-key segments) -> k_gen_batch -> ordering
+// and per sg_advance_time: k_gen_timers -> ordering of the timer matches.
+#include <hip/hip_runtime.h>
+
+#include <rocprim/device/device_merge_sort.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
+
+#include <algorithm>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/siddhi_gpu.h"
+#include "../../include/siddhi_gpu_ir.h"
+#include "gen_engine.h"
+#include "gen_host.h"
+
+extern "C" __global__ void k_gen_batch(const GenArgs a);
+extern "C" __global__ void k_gen_timers(const GenArgs a);
+
+namespace {
+
+#define GH_OK(x)                                                                                        \
+    do {                                                                                                \
+        hipError_t e_ = (x);                                                                            \
+        if (e_ != hipSuccess) throw std::runtime_error(std::string(#x) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+// ---------------------------------------------------------------------------------------------
+// IR -> GenProgram (mirrors the reference parser's wiring)
+// ---------------------------------------------------------------------------------------------
+struct RT {  // InnerStateRuntime
+    int tag = 0, first = -1, last = -1, a = -1, b = -1, stream = -1;
+};
+
+struct Builder {
+    GenProgram& G;
+    const uint32_t* w;
+    size_t n, pos = 0;
+    std::vector<RT> rts;
+    int64_t forMsCur = -1;
+
+    uint32_t next() {
+        if (pos >= n) throw std::runtime_error("truncated IR node tree");
+        return w[pos++];
+    }
+    int newPre(int kind) {
+        if (G.nprocs >= GEN_MAXP) throw std::runtime_error("too many states for the device engine");
+        const int id = G.nprocs++;
+        GenPre& P = G.pre[id];
+        P = GenPre{};
+        P.kind = kind;
+        P.withinEvery = P.thisPost = P.thisLast = P.countPost = P.partner = GEN_NONE;
+        P.waiting = -1;
+        GenPost& Q = G.post[id];
+        Q = GenPost{};
+        Q.kind = kind;
+        Q.nextStatePre = Q.nextEveryStatePre = Q.callbackPre = Q.partnerPre = Q.partnerPost = Q.thisPre = GEN_NONE;
+        return id;  // pre and post share the index
+    }
+    int newRT(int tag) {
+        rts.push_back(RT{});
+        rts.back().tag = tag;
+        return (int)rts.size() - 1;
+    }
+    bool peekAbsent(size_t q) const { return q + 5 < n && w[q] == SG_N_STREAM && w[q + 5] != 0; }
+    void skip() {
+        const uint32_t tag = next();
+        switch (tag) {
+        case SG_N_STREAM: pos += 7; return;
+        case SG_N_NEXT: skip(); skip(); return;
+        case SG_N_EVERY: skip(); return;
+        case SG_N_LOGICAL: next(); skip(); skip(); return;
+        case SG_N_COUNT: next(); next(); skip(); return;
+        }
+        throw std::runtime_error("bad IR node tag");
+    }
+    void setNextStatePre(int post, int pre) {  // StreamPost/LogicalPost/CountPost.setNextStatePreProcessor
+        GenPost& Q = G.post[post];
+        Q.nextStatePre = pre;
+        if (Q.kind == GK_LOGICAL) G.post[Q.partnerPost].nextStatePre = pre;  // LogicalPostStateProcessor.java:117-120
+        if (Q.kind == GK_COUNT && G.pre[Q.thisPre].isStart && G.qtype == SG_Q_SEQUENCE && Q.minCount == 0)
+            G.post[G.pre[pre].thisPost].callbackPre = Q.thisPre;  // CountPostStateProcessor.java:82-88
+    }
+    void setNextEveryStatePre(int post, int pre) {
+        GenPost& Q = G.post[post];
+        Q.nextEveryStatePre = pre;
+        if (Q.kind == GK_LOGICAL) G.post[Q.partnerPost].nextEveryStatePre = pre;
+    }
+
+    int parse(int pre, std::vector<int>& preList, bool isStart) {
+        const uint32_t tag = next();
+        switch (tag) {
+        case SG_N_STREAM: {
+            const uint32_t slot = next(), stream = next(), fpc = next(), flen = next(), absent = next();
+            const uint32_t flo = next(), fhi = next();
+            const int64_t forMs = (int64_t)((uint64_t)flo | ((uint64_t)fhi << 32));
+            if (pre < 0) {
+                pre = newPre(GK_STREAM);
+                if (absent) {
+                    if (forMs < 0) throw std::runtime_error("absent stream state needs a 'for' time");
+                    G.startup[G.nStartup++] = pre;
+                }
+            }
+            GenPre& P = G.pre[pre];
+            P.absent = absent != 0;
+            P.waiting = absent ? forMs : -1;
+            P.stateId = (int)slot;
+            P.isStart = isStart;
+            P.fpc = fpc;
+            P.flen = flen;
+            GenPost& Q = G.post[pre];
+            Q.absent = absent != 0;
+            Q.stateId = (int)slot;
+            Q.thisPre = pre;
+            P.thisPost = pre;
+            P.thisLast = pre;
+            const int rt = newRT(SG_N_STREAM);
+            rts[rt].first = pre;
+            rts[rt].last = pre;
+            rts[rt].stream = (int)stream;
+            preList.push_back(pre);
+            return rt;
+        }
+        case SG_N_NEXT: {
+            const int cur = parse(pre, preList, isStart);
+            const int nx = parse(pre, preList, false);
+            setNextStatePre(rts[cur].last, rts[nx].first);
+            const int rt = newRT(SG_N_NEXT);
+            rts[rt].a = cur;
+            rts[rt].b = nx;
+            rts[rt].first = rts[cur].first;
+            rts[rt].last = rts[nx].last;
+            return rt;
+        }
+        case SG_N_EVERY: {
+            std::vector<int> withinEvery;
+            const int inner = parse(pre, withinEvery, isStart);
+            const int rt = newRT(SG_N_EVERY);
+            rts[rt].a = inner;
+            rts[rt].first = rts[inner].first;
+            rts[rt].last = rts[inner].last;
+            setNextEveryStatePre(rts[rt].last, rts[rt].first);
+            for (int p : withinEvery) G.pre[p].withinEvery = rts[rt].first;
+            preList.insert(preList.end(), withinEvery.begin(), withinEvery.end());
+            return rt;
+        }
+        case SG_N_LOGICAL: {
+            const uint32_t ltype = next();
+            const int lp1 = newPre(GK_LOGICAL), lp2 = newPre(GK_LOGICAL);
+            for (int x : {lp1, lp2}) {
+                G.pre[x].logicalType = (int)ltype;
+                G.post[x].logicalType = (int)ltype;
+            }
+            G.post[lp1].partnerPre = lp2;
+            G.post[lp2].partnerPre = lp1;
+            G.post[lp1].partnerPost = lp2;
+            G.post[lp2].partnerPost = lp1;
+            G.pre[lp1].partner = lp2;
+            G.pre[lp2].partner = lp1;
+            {  // absent logical pres join the startup list at creation, element 1 first
+                const size_t save = pos;
+                const bool a1 = peekAbsent(pos);
+                skip();
+                const bool a2 = peekAbsent(pos);
+                pos = save;
+                if (a1) G.startup[G.nStartup++] = lp1;
+                if (a2) G.startup[G.nStartup++] = lp2;
+            }
+            const size_t save = pos;
+            skip();  // element 1 is encoded first, element 2 is parsed (and slotted) first
+            const int rt2 = parse(lp2, preList, isStart);
+            const size_t after = pos;
+            pos = save;
+            const int rt1 = parse(lp1, preList, isStart);
+            pos = after;
+            const int rt = newRT(SG_N_LOGICAL);
+            rts[rt].a = rt1;
+            rts[rt].b = rt2;
+            rts[rt].first = rts[rt1].first;
+            rts[rt].last = rts[rt2].last;
+            return rt;
+        }
+        case SG_N_COUNT: {
+            const uint32_t mn = next(), mx = next();
+            const int cp = newPre(GK_COUNT);
+            GenPre& P = G.pre[cp];
+            P.minCount = (int)mn;
+            P.maxCount = mx == SG_COUNT_ANY ? 0x7fffffff : (int)mx;
+            G.post[cp].minCount = P.minCount;
+            G.post[cp].maxCount = P.maxCount;
+            P.countPost = cp;
+            const int inner = parse(cp, preList, isStart);
+            const int rt = newRT(SG_N_COUNT);
+            rts[rt].first = rts[inner].first;
+            rts[rt].last = rts[inner].last;
+            rts[rt].stream = rts[inner].stream;
+            return rt;
+        }
+        }
+        throw std::runtime_error("bad IR node tag");
+    }
+
+    // InnerStateRuntime init / reset / update / setQuerySelector / setup, flattened
+    void initOrder(int rt) {
+        const RT& r = rts[rt];
+        switch (r.tag) {
+        case SG_N_NEXT: initOrder(r.a); initOrder(r.b); return;
+        case SG_N_EVERY: initOrder(r.a); return;
+        case SG_N_LOGICAL: initOrder(r.b); initOrder(r.a); return;
+        default: G.initOrder[G.nInit++] = r.first;
+        }
+    }
+    void resetOrder(int rt) {
+        const RT& r = rts[rt];
+        switch (r.tag) {
+        case SG_N_NEXT: resetOrder(r.b); resetOrder(r.a); return;
+        case SG_N_LOGICAL: resetOrder(r.b); return;
+        default: G.resetOrder[G.nReset++] = r.first;  // Stream, Count and Every reset their first
+        }
+    }
+    void updateOrder(int rt) {
+        const RT& r = rts[rt];
+        switch (r.tag) {
+        case SG_N_NEXT: updateOrder(r.a); updateOrder(r.b); return;
+        case SG_N_LOGICAL: updateOrder(r.b); return;
+        default: G.updateOrder[G.nUpdate++] = r.first;
+        }
+    }
+    void setQuerySelector(int rt) {
+        const RT& r = rts[rt];
+        switch (r.tag) {
+        case SG_N_NEXT: setQuerySelector(r.b); return;
+        case SG_N_EVERY: setQuerySelector(r.a); return;
+        case SG_N_LOGICAL: setQuerySelector(r.b); setQuerySelector(r.a); return;
+        default: G.post[r.last].hasNext = 1;
+        }
+    }
+    void setup(int rt) {
+        const RT& r = rts[rt];
+        switch (r.tag) {
+        case SG_N_NEXT: setup(r.a); setup(r.b); return;
+        case SG_N_EVERY: setup(r.a); return;
+        case SG_N_LOGICAL: setup(r.b); setup(r.a); return;
+        default: {
+            if (r.stream < 0 || r.stream >= G.nstreams) throw std::runtime_error("IR stream index out of range");
+            GenRecv& R = G.recv[r.stream];
+            if (R.n >= GEN_MAXP) throw std::runtime_error("too many states on one stream");
+            R.procs[R.n++] = r.first;
+            R.stateProcs[R.nStateProcs++] = r.first;
+        }
+        }
+    }
+};
+
+uint32_t ceil32(uint32_t x) { return (x + 31) / 32; }
+
+}  // namespace
+
+GenProgram* gen_build_program(const uint32_t* w, size_t nw, uint32_t partialCap) {
+    auto* G = new GenProgram();
+    memset(G, 0, sizeof(*G));
+    try {
+        G->qtype = (int)w[2];
+        G->nstreams = (int)w[3];
+        G->nslots = (int)w[4];
+        G->within = (int64_t)((uint64_t)w[5] | ((uint64_t)w[6] << 32));
+        const uint32_t offS = w[7], offN = w[8], nN = w[9], offC = w[10], nC = w[11];
+        G->partitioned = (w[12] & SG_IR_F_PARTITIONED) != 0;
+        G->playback = (w[12] & SG_IR_F_PLAYBACK) != 0;
+        if (G->nstreams > GEN_MAXS || G->nslots > GEN_MAXSLOT) throw std::runtime_error("query too large for the device engine");
+        if (nC > GEN_MAXCODE) throw std::runtime_error("filters too long for the device engine");
+        if (offN + nN > nw || offC + nC > nw) throw std::runtime_error("IR offsets out of range");
+        size_t p = offS;
+        uint32_t maxAttr = 1;
+        for (int s = 0; s < G->nstreams; s++) {
+            const uint32_t na = w[p++];
+            if (na > GEN_MAXA) throw std::runtime_error("stream has too many attributes for the device engine");
+            G->nattr[s] = (int)na;
+            for (uint32_t a = 0; a < na; a++) G->attrType[s][a] = (int)w[p++];
+            maxAttr = std::max(maxAttr, na);
+        }
+        G->ncode = nC;
+        memcpy(G->code, w + offC, nC * 4);
+        Builder B{*G, w + offN, nN};
+        std::vector<int> preList;
+        const int root = B.parse(-1, preList, true);
+        if (B.pos != nN) throw std::runtime_error("IR node tree has trailing words");
+        G->nAll = (int)preList.size();
+        for (size_t i = 0; i < preList.size(); i++) G->allProcs[i] = preList[i];
+        B.setQuerySelector(root);
+        B.setup(root);
+        B.initOrder(root);
+        B.resetOrder(root);
+        B.updateOrder(root);
+        if (G->within != -1)
+            for (int x : preList)
+                if (G->pre[x].isStart) G->startIds[G->nStartIds++] = G->pre[x].stateId;
+        G->rootFirst = B.rts[root].first;
+        G->rootLast = B.rts[root].last;
+        G->pre[G->rootFirst].thisLast = G->rootLast;
+        for (int s = 0; s < G->nstreams; s++) G->recv[s].multi = G->recv[s].n > 1;
+        // capacities and the per-key block layout
+        uint32_t mc = 1;
+        for (int x = 0; x < G->nprocs; x++)
+            if (G->pre[x].kind == GK_COUNT) mc = std::max<uint32_t>(mc, G->pre[x].maxCount >= 0x7fffffff ? 16u : (uint32_t)G->pre[x].maxCount);
+        for (int x = 0; x < G->nprocs; x++)
+            if (G->pre[x].absent && G->pre[x].kind == GK_LOGICAL) mc = std::max<uint32_t>(mc, 2u);
+        G->MC = mc;
+        G->L = std::max<uint32_t>(4, partialCap);
+        G->Q = G->L + 8;
+        G->STCAP = std::min<uint32_t>(2 * G->L + 16, 0xfff0u);
+        G->SECAP = std::min<uint32_t>(G->STCAP * std::min<uint32_t>((uint32_t)G->nslots * mc, 8u), 0xfff0u);
+        G->NA = maxAttr;
+        G->DEF = G->L;
+        G->ksWords = KS_LISTS + 2 * G->L + 2 * G->Q;
+        G->stWords = ST_SLOTS + (uint32_t)G->nslots;
+        G->seWords = SE_ATTR + 2 * G->NA;
+        uint32_t off = 2;  // [0] key initialised, [1] scheduler order counter
+        G->offKS = off;
+        off += (uint32_t)G->nprocs * G->ksWords;
+        G->offST = off;
+        off += G->STCAP * G->stWords;
+        G->offSTfree = off;
+        off += ceil32(G->STCAP);
+        G->offSE = off;
+        off += G->SECAP * G->seWords;
+        G->offSEfree = off;
+        off += ceil32(G->SECAP);
+        G->offDef = off;
+        off += 1 + 2 * G->DEF;
+        G->blockWords = off;
+        return G;
+    } catch (...) {
+        delete G;
+        throw;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// device-side helpers of the engine
+// ---------------------------------------------------------------------------------------------
+__global__ void k_gen_bounds(const uint32_t* __restrict__ skeys, uint32_t n, uint32_t K, uint32_t* seg_begin,
+                             uint32_t* seg_end, uint32_t* err) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t k = skeys[i];
+    if (k >= K) { atomicOr(err, (uint32_t)GERR_KEY); return; }
+    if (i == 0 || skeys[i - 1] != k) seg_begin[k] = i;
+    if (i == n - 1 || skeys[i + 1] != k) seg_end[k] = i + 1;
+}
+
+struct OutBufs {
+    uint64_t* trig;
+    uint64_t* slot;
+    uint32_t* key;
+    int64_t* ts;
+    uint32_t* len;
+    unsigned long long* count;
+    uint64_t cap;
+    uint32_t nslots, MC, recWords;
+    uint32_t* err;
+};
+
+__device__ void write_out(const OutBufs& o, uint64_t d, const uint32_t* rec, bool timer) {
+    if (d >= o.cap) { atomicOr(o.err, (uint32_t)GERR_MATCHCAP); return; }
+    o.trig[d] = timer ? SG_TIMER_SEQ : ((uint64_t)rec[2] | ((uint64_t)rec[3] << 32));
+    o.ts[d] = (int64_t)((uint64_t)rec[4] | ((uint64_t)rec[5] << 32));
+    o.key[d] = rec[6];
+    const uint32_t* lens = rec + 7;
+    const uint32_t* seqs = lens + o.nslots;
+    for (uint32_t s = 0; s < o.nslots; s++) {
+        const uint32_t n = lens[s];
+        o.len[d * o.nslots + s] = n;
+        for (uint32_t c = 0; c < o.MC; c++) {
+            const uint64_t q = c < n ? ((uint64_t)seqs[2 * (s * o.MC + c)] | ((uint64_t)seqs[2 * (s * o.MC + c) + 1] << 32))
+                                     : SG_NULL_SEQ;
+            o.slot[(d * o.nslots + s) * o.MC + c] = q;
+        }
+    }
+}
+
+// batch matches: out_count + t_off[trigger] + rank
+__global__ void k_gen_scatter(const uint32_t* raw, const unsigned long long* raw_count, uint64_t raw_cap,
+                              const uint32_t* t_off, OutBufs o) {
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t n = *raw_count < raw_cap ? *raw_count : raw_cap;
+    if (r >= n) return;
+    const uint32_t* rec = raw + r * o.recWords;
+    if (rec[0] >= 0xfffffffeu) return;
+    write_out(o, *o.count + t_off[rec[0]] + rec[1], rec, false);
+}
+
+// timer matches in sorted order
+__global__ void k_gen_scatter_timers(const uint32_t* raw, const uint32_t* order, const unsigned long long* nvalid,
+                                     OutBufs o) {
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= *nvalid) return;
+    write_out(o, *o.count + r, raw + (uint64_t)order[r] * o.recWords, true);
+}
+
+__global__ void k_gen_bump(unsigned long long* count, const uint32_t* t_cnt, const uint32_t* t_off, uint32_t n,
+                           const unsigned long long* nvalid) {
+    if (nvalid) *count += *nvalid;
+    else *count += (unsigned long long)t_off[n - 1] + t_cnt[n - 1];
+}
+
+__global__ void k_gen_iota(uint32_t* x, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) x[i] = (uint32_t)i;
+}
+
+// live partial matches (StateEvents holding an event) in every list of every processor
+__global__ void k_gen_live(const GenProgram* G, const uint32_t* S, uint32_t K, unsigned long long* out) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= K) return;
+    unsigned long long live = 0;
+    for (int p = 0; p < G->nprocs; p++) {
+        const uint32_t ks = G->offKS + (uint32_t)p * G->ksWords;
+        for (int which = 0; which < 2; which++) {
+            const uint32_t n = S[(size_t)(ks + KS_PLEN + which) * K + k];
+            for (uint32_t i = 0; i < n; i++) {
+                const uint32_t se = S[(size_t)(ks + KS_LISTS + which * G->L + i) * K + k];
+                for (int s = 0; s < G->nslots; s++)
+                    if (S[(size_t)(G->offST + se * G->stWords + ST_SLOTS + s) * K + k] != GEN_NIL) { live++; break; }
+            }
+        }
+    }
+    if (live) atomicAdd(out, live);
+}
+
+struct TimerLess {
+    const uint32_t* k1;
+    const int64_t* k2;
+    const uint32_t* k3;
+    __device__ bool operator()(uint32_t a, uint32_t b) const {
+        if (k1[a] != k1[b]) return k1[a] < k1[b];
+        if (k2[a] != k2[b]) return k2[a] < k2[b];
+        if (k3[a] != k3[b]) return k3[a] < k3[b];
+        return a < b;
+    }
+};
+
+// ---------------------------------------------------------------------------------------------
+// the engine
+// ---------------------------------------------------------------------------------------------
+struct GenEngine {
+    GenProgram host{};
+    GenProgram* dprog = nullptr;
+    hipStream_t stream = nullptr;
+    uint32_t K = 1, maxb = 0;
+    uint64_t mcap = 0, rawCap = 0;
+    uint32_t recWords = 0;
+    std::vector<void*> owned;
+    uint32_t* state = nullptr;
+    // batch staging
+    int64_t* b_ts = nullptr;
+    uint32_t* b_key = nullptr;
+    std::vector<void*> b_cols;
+    std::vector<uint8_t*> b_nulls;
+    uint32_t *skeys = nullptr, *sidx = nullptr, *iota = nullptr, *seg_begin = nullptr, *seg_end = nullptr;
+    void* sort_tmp = nullptr;
+    size_t sort_tmp_bytes = 0;
+    // matches
+    uint32_t* raw = nullptr;
+    unsigned long long* raw_count = nullptr;
+    uint32_t *t_cnt = nullptr, *t_first = nullptr, *t_off = nullptr;
+    int64_t* tk2 = nullptr;
+    uint32_t *tk1 = nullptr, *tk3 = nullptr, *order_in = nullptr, *order_out = nullptr;
+    unsigned long long* nvalid = nullptr;
+    void* scan_tmp = nullptr;
+    size_t scan_tmp_bytes = 0;
+    void* msort_tmp = nullptr;
+    size_t msort_tmp_bytes = 0;
+    unsigned long long* stats = nullptr;
+    uint32_t* err = nullptr;
+    OutBufs out{};
+    std::vector<uint64_t> h_trig, h_slot;
+    std::vector<uint32_t> h_key, h_len;
+    std::vector<int64_t> h_ts;
+    bool held = false;
+    int64_t now = 0;        // TimestampGenerator.currentTime() as last set by sg_advance_time
+    int64_t lastEventTs = 0;
+    bool advanced = false;
+    sg_stats st{};
+
+    template <class T> T* dalloc(size_t n) {
+        void* p = nullptr;
+        GH_OK(hipMalloc(&p, std::max<size_t>(n, 1) * sizeof(T)));
+        owned.push_back(p);
+        return (T*)p;
+    }
+    ~GenEngine() {
+        if (stream) (void)hipStreamSynchronize(stream);
+        for (void* p : owned) (void)hipFree(p);
+    }
+
+    GenArgs args() const {
+        GenArgs a{};
+        a.G = dprog;
+        a.state = state;
+        a.K = K;
+        a.o.raw = raw;
+        a.o.raw_count = raw_count;
+        a.o.raw_cap = rawCap;
+        a.o.recWords = recWords;
+        a.o.t_cnt = t_cnt;
+        a.o.t_first = t_first;
+        a.o.tk1 = tk1;
+        a.o.tk2 = tk2;
+        a.o.tk3 = tk3;
+        a.o.nvalid = nvalid;
+        a.o.stats = stats;
+        a.o.err = err;
+        a.now = now;
+        a.now0 = now;
+        return a;
+    }
+};
+
+GenEngine* gen_create(const uint32_t* ir, size_t nw, const sg_config& cfg, hipStream_t stream) {
+    GenProgram* prog = gen_build_program(ir, nw, cfg.partial_capacity ? cfg.partial_capacity : 32);
+    auto* e = new GenEngine();
+    try {
+        e->host = *prog;
+        delete prog;
+        e->stream = stream;
+        e->K = e->host.partitioned ? (cfg.n_keys ? cfg.n_keys : 1) : 1;
+        e->maxb = cfg.max_batch ? cfg.max_batch : (1u << 20);
+        e->mcap = cfg.match_capacity ? cfg.match_capacity : (uint64_t)e->maxb * 4;
+        const GenProgram& G = e->host;
+        e->recWords = 7 + (uint32_t)G.nslots + 2 * (uint32_t)G.nslots * G.MC;
+        e->rawCap = e->mcap + (uint64_t)e->K * 16;
+        const size_t K = e->K, B = e->maxb;
+        e->dprog = e->dalloc<GenProgram>(1);
+        GH_OK(hipMemcpy(e->dprog, &e->host, sizeof(GenProgram), hipMemcpyHostToDevice));
+        e->state = e->dalloc<uint32_t>((size_t)G.blockWords * K);
+        GH_OK(hipMemset(e->state, 0, (size_t)G.blockWords * K * 4));
+        e->b_ts = e->dalloc<int64_t>(B);
+        e->b_key = e->dalloc<uint32_t>(B);
+        int maxa = 1;
+        for (int s = 0; s < G.nstreams; s++) maxa = std::max(maxa, G.nattr[s]);
+        for (int a = 0; a < maxa; a++) {
+            e->b_cols.push_back(e->dalloc<uint64_t>(B));
+            e->b_nulls.push_back(e->dalloc<uint8_t>(B));
+        }
+        e->skeys = e->dalloc<uint32_t>(B);
+        e->sidx = e->dalloc<uint32_t>(B);
+        e->iota = e->dalloc<uint32_t>(B);
+        hipLaunchKernelGGL(k_gen_iota, dim3((B + 255) / 256), dim3(256), 0, stream, e->iota, (uint64_t)B);
+        e->seg_begin = e->dalloc<uint32_t>(K);
+        e->seg_end = e->dalloc<uint32_t>(K);
+        GH_OK(rocprim::radix_sort_pairs(nullptr, e->sort_tmp_bytes, e->b_key, e->skeys, e->iota, e->sidx, (uint32_t)B,
+                                        0, 32, stream));
+        e->sort_tmp = e->dalloc<uint8_t>(e->sort_tmp_bytes);
+        e->raw = e->dalloc<uint32_t>(e->rawCap * e->recWords);
+        e->raw_count = e->dalloc<unsigned long long>(1);
+        e->t_cnt = e->dalloc<uint32_t>(B);
+        e->t_first = e->dalloc<uint32_t>(B);
+        e->t_off = e->dalloc<uint32_t>(B);
+        GH_OK(hipMemset(e->t_cnt, 0, B * 4));
+        e->tk1 = e->dalloc<uint32_t>(e->rawCap);
+        e->tk2 = e->dalloc<int64_t>(e->rawCap);
+        e->tk3 = e->dalloc<uint32_t>(e->rawCap);
+        e->order_in = e->dalloc<uint32_t>(e->rawCap);
+        e->order_out = e->dalloc<uint32_t>(e->rawCap);
+        e->nvalid = e->dalloc<unsigned long long>(1);
+        GH_OK(rocprim::exclusive_scan(nullptr, e->scan_tmp_bytes, e->t_cnt, e->t_off, 0u, (uint32_t)B,
+                                      rocprim::plus<uint32_t>(), stream));
+        e->scan_tmp = e->dalloc<uint8_t>(e->scan_tmp_bytes);
+        TimerLess lt{e->tk1, e->tk2, e->tk3};
+        GH_OK(rocprim::merge_sort(nullptr, e->msort_tmp_bytes, e->order_in, e->order_out, (size_t)e->rawCap, lt, stream));
+        e->msort_tmp = e->dalloc<uint8_t>(e->msort_tmp_bytes);
+        e->stats = e->dalloc<unsigned long long>(GST_N);
+        GH_OK(hipMemset(e->stats, 0, GST_N * 8));
+        e->err = e->dalloc<uint32_t>(1);
+        GH_OK(hipMemset(e->err, 0, 4));
+        const uint64_t M = e->mcap;
+        e->out.trig = e->dalloc<uint64_t>(M);
+        e->out.slot = e->dalloc<uint64_t>(M * G.nslots * G.MC);
+        e->out.key = e->dalloc<uint32_t>(M);
+        e->out.ts = e->dalloc<int64_t>(M);
+        e->out.len = e->dalloc<uint32_t>(M * G.nslots);
+        e->out.count = e->dalloc<unsigned long long>(1);
+        GH_OK(hipMemset(e->out.count, 0, 8));
+        e->out.cap = M;
+        e->out.nslots = (uint32_t)G.nslots;
+        e->out.MC = G.MC;
+        e->out.recWords = e->recWords;
+        e->out.err = e->err;
+        GH_OK(hipStreamSynchronize(stream));
+        return e;
+    } catch (...) {
+        delete e;
+        throw;
+    }
+}
+
+void gen_destroy(GenEngine* e) { delete e; }
+
+static size_t type_size(int t) {
+    switch (t) {
+    case SG_T_LONG: case SG_T_DOUBLE: return 8;
+    case SG_T_BOOL: return 1;
+    default: return 4;
+    }
+}
+
+static void launch_batch_or_timers(GenEngine* e, const GenArgs& a, bool timers) {
+    const uint32_t blocks = (e->K + 63) / 64;
+    if (timers) hipLaunchKernelGGL(k_gen_timers, dim3(blocks), dim3(64), 0, e->stream, a);
+    else hipLaunchKernelGGL(k_gen_batch, dim3(blocks), dim3(64), 0, e->stream, a);
+    GH_OK(hipGetLastError());
+}
+
+int gen_push(GenEngine* e, const sg_batch* b, std::string& msg) {
+    const GenProgram& G = e->host;
+    if (b->stream >= (uint32_t)G.nstreams) { msg = "stream index out of range"; return SG_ERR_INVALID; }
+    if (b->n_cols != (uint32_t)G.nattr[b->stream]) { msg = "column count does not match the stream"; return SG_ERR_INVALID; }
+    if (b->n == 0) return SG_OK;
+    if (b->n > e->maxb) { msg = "batch larger than max_batch"; return SG_ERR_INVALID; }
+    if (G.partitioned && !b->key) { msg = "partitioned query needs key ids"; return SG_ERR_INVALID; }
+    if (e->held) { msg = "release the polled matches before pushing"; return SG_ERR_STATE; }
+    const uint32_t n = (uint32_t)b->n;
+    const bool dev = b->mem == SG_MEM_DEVICE;
+    GenArgs a = e->args();
+    a.b.n = n;
+    a.b.stream = b->stream;
+    a.b.seq_base = b->seq_base;
+    a.b.ts = b->ts;
+    if (!dev) {
+        GH_OK(hipMemcpyAsync(e->b_ts, b->ts, (size_t)n * 8, hipMemcpyHostToDevice, e->stream));
+        a.b.ts = e->b_ts;
+    }
+    for (uint32_t c = 0; c < b->n_cols; c++) {
+        const int t = G.attrType[b->stream][c];
+        if (dev) {
+            a.b.col[c] = b->cols[c];
+            a.b.nul[c] = b->nulls ? b->nulls[c] : nullptr;
+        } else {
+            GH_OK(hipMemcpyAsync(e->b_cols[c], b->cols[c], (size_t)n * type_size(t), hipMemcpyHostToDevice, e->stream));
+            a.b.col[c] = e->b_cols[c];
+            a.b.nul[c] = nullptr;
+            if (b->nulls && b->nulls[c]) {
+                GH_OK(hipMemcpyAsync(e->b_nulls[c], b->nulls[c], n, hipMemcpyHostToDevice, e->stream));
+                a.b.nul[c] = e->b_nulls[c];
+            }
+        }
+    }
+    GH_OK(hipMemsetAsync(e->seg_begin, 0, (size_t)e->K * 4, e->stream));
+    GH_OK(hipMemsetAsync(e->seg_end, 0, (size_t)e->K * 4, e->stream));
+    if (G.partitioned) {
+        const uint32_t* keys = b->key;
+        if (!dev) {
+            for (uint32_t i = 0; i < n; i++)
+                if (b->key[i] >= e->K) { msg = "key id outside [0, n_keys)"; return SG_ERR_INVALID; }
+            GH_OK(hipMemcpyAsync(e->b_key, b->key, (size_t)n * 4, hipMemcpyHostToDevice, e->stream));
+            keys = e->b_key;
+        }
+        uint32_t bits = 1;
+        while (bits < 32 && (1ull << bits) < e->K) bits++;
+        size_t tmp = e->sort_tmp_bytes;
+        GH_OK(rocprim::radix_sort_pairs(e->sort_tmp, tmp, keys, e->skeys, e->iota, e->sidx, n, 0, bits, e->stream));
+        hipLaunchKernelGGL(k_gen_bounds, dim3((n + 255) / 256), dim3(256), 0, e->stream, e->skeys, n, e->K,
+                           e->seg_begin, e->seg_end, e->err);
+        a.b.sidx = e->sidx;
+    } else {
+        GH_OK(hipMemcpyAsync(e->seg_end, &n, 4, hipMemcpyHostToDevice, e->stream));
+        GH_OK(hipStreamSynchronize(e->stream));  // &n is a stack value
+        a.b.sidx = nullptr;
+    }
+    a.b.seg_begin = e->seg_begin;
+    a.b.seg_end = e->seg_end;
+    GH_OK(hipMemsetAsync(e->raw_count, 0, 8, e->stream));
+    launch_batch_or_timers(e, a, false);
+    // order: out_count + t_off[trigger] + rank
+    size_t tmp = e->scan_tmp_bytes;
+    GH_OK(rocprim::exclusive_scan(e->scan_tmp, tmp, e->t_cnt, e->t_off, 0u, n, rocprim::plus<uint32_t>(), e->stream));
+    const uint64_t maxRaw = e->rawCap;
+    hipLaunchKernelGGL(k_gen_scatter, dim3((unsigned)((maxRaw + 255) / 256)), dim3(256), 0, e->stream, e->raw,
+                       e->raw_count, e->rawCap, e->t_off, e->out);
+    hipLaunchKernelGGL(k_gen_bump, dim3(1), dim3(1), 0, e->stream, e->out.count, e->t_cnt, e->t_off, n,
+                       (const unsigned long long*)nullptr);
+    GH_OK(hipMemsetAsync(e->t_cnt, 0, (size_t)n * 4, e->stream));
+    GH_OK(hipGetLastError());
+    e->st.events += n;
+    e->st.batches++;
+    e->st.advance_launches++;
+    if (!dev) GH_OK(hipStreamSynchronize(e->stream));
+    return SG_OK;
+}
+
+int gen_advance(GenEngine* e, int64_t t, std::string& msg) {
+    const GenProgram& G = e->host;
+    if (G.playback) {
+        // TimestampGeneratorImpl.setCurrentTimestamp ignores a time earlier than the last one
+        if (e->advanced && t < e->lastEventTs) return SG_OK;
+        e->lastEventTs = t;
+    }
+    GenArgs a = e->args();
+    a.now = t;         // the advance target (playback: the event clock)
+    a.now0 = e->now;   // the clock before it (wall-clock callers run at their own times)
+    GH_OK(hipMemsetAsync(e->raw_count, 0, 8, e->stream));
+    GH_OK(hipMemsetAsync(e->nvalid, 0, 8, e->stream));
+    launch_batch_or_timers(e, a, true);
+    unsigned long long nr = 0;
+    GH_OK(hipMemcpyAsync(&nr, e->raw_count, 8, hipMemcpyDeviceToHost, e->stream));
+    GH_OK(hipStreamSynchronize(e->stream));
+    if (nr > 0) {
+        // the timer matches in the reference's order: playback by (listener, queue head), wall clock by
+        // (run time, key); within one key in emission order
+        const size_t n = (size_t)std::min<unsigned long long>(nr, e->rawCap);
+        hipLaunchKernelGGL(k_gen_iota, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, e->stream, e->order_in, (uint64_t)n);
+        size_t tmp = e->msort_tmp_bytes;
+        TimerLess lt{e->tk1, e->tk2, e->tk3};
+        GH_OK(rocprim::merge_sort(e->msort_tmp, tmp, e->order_in, e->order_out, n, lt, e->stream));
+        hipLaunchKernelGGL(k_gen_scatter_timers, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, e->stream, e->raw,
+                           e->order_out, e->nvalid, e->out);
+        hipLaunchKernelGGL(k_gen_bump, dim3(1), dim3(1), 0, e->stream, e->out.count, e->t_cnt, e->t_off, 1u,
+                           (const unsigned long long*)e->nvalid);
+        GH_OK(hipGetLastError());
+    }
+    if (G.playback || !e->advanced || t > e->now) e->now = t;
+    e->advanced = true;
+    (void)msg;
+    return SG_OK;
+}
+
+int gen_poll(GenEngine* e, uint32_t mem, sg_match_batch* out, std::string& msg) {
+    if (e->held) { msg = "previous matches not released"; return SG_ERR_STATE; }
+    unsigned long long n = 0;
+    uint32_t err = 0;
+    GH_OK(hipMemcpyAsync(&n, e->out.count, 8, hipMemcpyDeviceToHost, e->stream));
+    GH_OK(hipMemcpyAsync(&err, e->err, 4, hipMemcpyDeviceToHost, e->stream));
+    GH_OK(hipStreamSynchronize(e->stream));
+    if (err & GERR_KEY) { msg = "a batch carried key ids outside [0, n_keys)"; return SG_ERR_INVALID; }
+    if (err & GERR_CAP) { msg = "a partition key exceeded the engine's per-key capacity (partial_capacity)"; return SG_ERR_CAPACITY; }
+    if ((err & GERR_MATCHCAP) || n > e->mcap) { msg = "more matches than match_capacity between two polls"; return SG_ERR_CAPACITY; }
+    if (err & GERR_CHAIN) { msg = "a count state chain is longer than the output chain capacity"; return SG_ERR_CAPACITY; }
+    if (err & GERR_REF) { msg = "internal state error in the device engine"; return SG_ERR_STATE; }
+    const GenProgram& G = e->host;
+    const size_t ns = (size_t)G.nslots, mc = G.MC;
+    out->n = n;
+    out->n_slots = (uint32_t)ns;
+    out->max_chain = (uint32_t)mc;
+    out->reserved = 0;
+    if (mem == SG_MEM_DEVICE) {
+        out->trigger_seq = e->out.trig;
+        out->slot_seq = e->out.slot;
+        out->key = e->out.key;
+        out->ts = e->out.ts;
+        out->chain_len = e->out.len;
+        out->mem = SG_MEM_DEVICE;
+    } else {
+        e->h_trig.resize(n);
+        e->h_slot.resize(n * ns * mc);
+        e->h_key.resize(n);
+        e->h_ts.resize(n);
+        e->h_len.resize(n * ns);
+        if (n) {
+            GH_OK(hipMemcpyAsync(e->h_trig.data(), e->out.trig, n * 8, hipMemcpyDeviceToHost, e->stream));
+            GH_OK(hipMemcpyAsync(e->h_slot.data(), e->out.slot, n * ns * mc * 8, hipMemcpyDeviceToHost, e->stream));
+            GH_OK(hipMemcpyAsync(e->h_key.data(), e->out.key, n * 4, hipMemcpyDeviceToHost, e->stream));
+            GH_OK(hipMemcpyAsync(e->h_ts.data(), e->out.ts, n * 8, hipMemcpyDeviceToHost, e->stream));
+            GH_OK(hipMemcpyAsync(e->h_len.data(), e->out.len, n * ns * 4, hipMemcpyDeviceToHost, e->stream));
+            GH_OK(hipStreamSynchronize(e->stream));
+        }
+        out->trigger_seq = e->h_trig.data();
+        out->slot_seq = e->h_slot.data();
+        out->key = e->h_key.data();
+        out->ts = e->h_ts.data();
+        out->chain_len = e->h_len.data();
+        out->mem = SG_MEM_HOST;
+    }
+    GH_OK(hipMemsetAsync(e->out.count, 0, 8, e->stream));
+    e->held = true;
+    return SG_OK;
+}
+
+void gen_release(GenEngine* e) { e->held = false; }
+
+void gen_stats(GenEngine* e, sg_stats* out) {
+    unsigned long long s[GST_N];
+    GH_OK(hipMemcpyAsync(s, e->stats, sizeof(s), hipMemcpyDeviceToHost, e->stream));
+    unsigned long long* live = nullptr;
+    GH_OK(hipMallocAsync((void**)&live, 8, e->stream));
+    GH_OK(hipMemsetAsync(live, 0, 8, e->stream));
+    hipLaunchKernelGGL(k_gen_live, dim3((e->K + 255) / 256), dim3(256), 0, e->stream, e->dprog, e->state, e->K, live);
+    unsigned long long lv = 0;
+    GH_OK(hipMemcpyAsync(&lv, live, 8, hipMemcpyDeviceToHost, e->stream));
+    GH_OK(hipFreeAsync(live, e->stream));
+    GH_OK(hipStreamSynchronize(e->stream));
+    *out = e->st;
+    out->partials_scanned = s[GST_SCANNED];
+    out->partials_created = s[GST_CREATED];
+    out->matches = s[GST_MATCHES];
+    out->keys_touched = s[GST_KEYS];
+    out->partials_live = lv;
+}
+
+void gen_synchronize(GenEngine* e) { GH_OK(hipStreamSynchronize(e->stream)); }

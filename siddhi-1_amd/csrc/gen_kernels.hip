@@ -1,0 +1,1237 @@
+// gen_kernels.hip — device side of the general NFA engine (see gen_engine.h).
+//
+// One lane owns one partition key and runs the key's processor graph exactly as the reference does
+// for that key, over the key's events of the micro-batch in arrival order.  The processors are the
+// flat tables of GenProgram; their per-key state lives in HBM (interleaved by key).  Restated from
+// (paths under /root/reference/modules/siddhi-core/src/main/java/io/siddhi/core/):
+//   StreamPreStateProcessor.java:118-403     isExpired, init, addState, addEveryState, resetState,
+//                                            updateState, expireEvents, processAndReturn
+//   StreamPostStateProcessor.java:64-83      post processing of a passed filter
+//   CountPre/PostStateProcessor.java         `<m:n>` (chains appended to the SAME StateEvent objects)
+//   LogicalPre/PostStateProcessor.java       `and` / `or`
+//   Absent{Stream,Logical}{Pre,Post}StateProcessor.java   `not S for T` and its timers
+//   util/Scheduler.java:65-298               per-key FIFO timer queues
+//   query/input/*ProcessStreamReceiver.java  stabilize + reverse state order + deferred projection
+//   executor/condition/**, executor/math/**  filters with Java numerics (null, int wrap, /0 -> null)
+#include <hip/hip_runtime.h>
+
+#include "../../include/siddhi_gpu.h"
+#include "../../include/siddhi_gpu_ir.h"
+#include "gen_engine.h"
+
+namespace {
+
+struct GVal {
+    uint64_t b;
+    bool null;
+};
+
+// instruction length in words (siddhi_gpu_ir.h)
+__device__ __forceinline__ uint32_t op_len(uint32_t op) {
+    op &= 0xffu;
+    return (op == SG_OP_VAR || op == SG_OP_CONST) ? 3u : (op == SG_OP_ISNULL_EV ? 2u : 1u);
+}
+
+__device__ __forceinline__ float gf32(uint64_t b) { return __uint_as_float((uint32_t)b); }
+__device__ __forceinline__ double gf64(uint64_t b) { return __longlong_as_double((long long)b); }
+__device__ __forceinline__ uint64_t gbf32(float f) { return (uint64_t)__float_as_uint(f); }
+__device__ __forceinline__ uint64_t gbf64(double d) { return (uint64_t)__double_as_longlong(d); }
+
+struct Lane {
+    const GenProgram& G;
+    const GenArgs& A;
+    uint32_t* S;
+    uint32_t K, k;
+    int64_t now;
+    uint64_t trigSeq;       // seq of the event being processed (SG_TIMER_SEQ in a timer sweep)
+    uint32_t trigIdx;       // its batch position
+    uint32_t trigRank;      // matches emitted so far for this trigger
+    int64_t tk2;            // timer sort keys of the matches emitted now
+    uint32_t tk1;
+    bool ret[GEN_MAXP];     // StreamPostStateProcessor.isEventReturned (transient)
+    unsigned long long scanned, created, matches;
+    uint32_t err;
+    unsigned long long resBase;  // this lane's reserved raw match slots
+    uint32_t resLeft;
+
+    __device__ Lane(const GenArgs& a, uint32_t key)
+        : G(*a.G), A(a), S(a.state), K(a.K), k(key), now(a.now), trigSeq(SG_TIMER_SEQ), trigIdx(0), trigRank(0),
+          tk2(0), tk1(0), scanned(0), created(0), matches(0), err(0), resBase(0), resLeft(0) {
+        for (int i = 0; i < GEN_MAXP; i++) ret[i] = false;
+    }
+
+    // ---- HBM words of this key ----
+    __device__ __forceinline__ uint32_t& W(uint32_t w) const { return S[(size_t)w * K + k]; }
+    __device__ __forceinline__ int64_t R64(uint32_t w) const {
+        return (int64_t)((uint64_t)W(w) | ((uint64_t)W(w + 1) << 32));
+    }
+    __device__ __forceinline__ void W64(uint32_t w, int64_t v) const {
+        W(w) = (uint32_t)(uint64_t)v;
+        W(w + 1) = (uint32_t)((uint64_t)v >> 32);
+    }
+
+    // ---- KeyState of processor p ----
+    __device__ __forceinline__ uint32_t ks(int p) const { return G.offKS + (uint32_t)p * G.ksWords; }
+    __device__ __forceinline__ uint32_t flags(int p) const { return W(ks(p) + KS_FLAGS); }
+    __device__ __forceinline__ bool flag(int p, uint32_t f) const { return (flags(p) & f) != 0; }
+    __device__ __forceinline__ void setFlag(int p, uint32_t f, bool on) const {
+        uint32_t& x = W(ks(p) + KS_FLAGS);
+        x = on ? (x | f) : (x & ~f);
+    }
+    // lists: which 0 = pending, 1 = newAndEvery
+    __device__ __forceinline__ uint32_t& len(int p, int which) const { return W(ks(p) + KS_PLEN + which); }
+    __device__ __forceinline__ uint32_t& at(int p, int which, uint32_t i) const {
+        return W(ks(p) + KS_LISTS + (uint32_t)which * G.L + i);
+    }
+
+    // ---- StateEvent pool ----
+    __device__ __forceinline__ uint32_t stw(uint32_t se, uint32_t f) const { return G.offST + se * G.stWords + f; }
+    __device__ __forceinline__ int64_t stTs(uint32_t se) const { return R64(stw(se, ST_TS)); }
+    __device__ __forceinline__ void setStTs(uint32_t se, int64_t t) const { W64(stw(se, ST_TS), t); }
+    __device__ __forceinline__ uint32_t slot(uint32_t se, int s) const { return W(stw(se, ST_SLOTS + (uint32_t)s)); }
+    // ---- StreamEvent pool ----
+    __device__ __forceinline__ uint32_t sew(uint32_t e, uint32_t f) const { return G.offSE + e * G.seWords + f; }
+    __device__ __forceinline__ int64_t evTs(uint32_t e) const { return R64(sew(e, SE_TS)); }
+    __device__ __forceinline__ uint64_t evSeq(uint32_t e) const { return (uint64_t)R64(sew(e, SE_SEQ)); }
+    __device__ __forceinline__ uint32_t evNext(uint32_t e) const { return W(sew(e, SE_NEXT)); }
+
+    __device__ uint32_t alloc(uint32_t freeOff, uint32_t cap) {
+        const uint32_t nw = (cap + 31) / 32;
+        for (uint32_t w = 0; w < nw; w++) {
+            uint32_t x = W(freeOff + w);
+            if (x != 0xffffffffu) {
+                const uint32_t b = __ffs(~x) - 1;
+                const uint32_t idx = w * 32 + b;
+                if (idx >= cap) break;
+                W(freeOff + w) = x | (1u << b);
+                return idx;
+            }
+        }
+        err |= GERR_CAP;
+        return GEN_NIL;
+    }
+    __device__ void freeBit(uint32_t freeOff, uint32_t idx) const {
+        uint32_t& x = W(freeOff + idx / 32);
+        x &= ~(1u << (idx % 32));
+    }
+
+    __device__ void evIncref(uint32_t e) const {
+        if (e != GEN_NIL) W(sew(e, SE_RC)) += 1;
+    }
+    __device__ void evDecref(uint32_t e) {
+        while (e != GEN_NIL) {
+            uint32_t& rc = W(sew(e, SE_RC));
+            if (rc == 0) { err |= GERR_REF; return; }
+            if (--rc != 0) return;
+            const uint32_t nx = evNext(e);
+            freeBit(G.offSEfree, e);
+            e = nx;
+        }
+    }
+    __device__ uint32_t newEv(uint64_t seq, int64_t ts, uint32_t batchPos, bool blank) {
+        const uint32_t e = alloc(G.offSEfree, G.SECAP);
+        if (e == GEN_NIL) return e;
+        W64(sew(e, SE_SEQ), (int64_t)seq);
+        W64(sew(e, SE_TS), ts);
+        W(sew(e, SE_NEXT)) = GEN_NIL;
+        W(sew(e, SE_RC)) = 0;
+        uint32_t nb = 0;
+        if (!blank) {  // capture the event's attributes (the StreamEvent's data)
+            const int s = (int)A.b.stream;
+            const int na = G.nattr[s];
+            for (int a = 0; a < na; a++) {
+                uint64_t v = 0;
+                const void* c = A.b.col[a];
+                switch (G.attrType[s][a]) {
+                case SG_T_LONG: case SG_T_DOUBLE: v = ((const uint64_t*)c)[batchPos]; break;
+                case SG_T_BOOL: v = ((const uint8_t*)c)[batchPos] ? 1 : 0; break;
+                default: v = ((const uint32_t*)c)[batchPos];
+                }
+                W64(sew(e, SE_ATTR + 2 * (uint32_t)a), (int64_t)v);
+                if (A.b.nul[a] && A.b.nul[a][batchPos]) nb |= 1u << a;
+            }
+        } else {
+            nb = 0xffffffffu;  // StreamEventFactory.newInstance(): no data
+        }
+        W(sew(e, SE_NULL)) = nb;
+        return e;
+    }
+
+    __device__ void stIncref(uint32_t se) const {
+        if (se != GEN_NIL) W(stw(se, ST_RC)) += 1;
+    }
+    __device__ void stDecref(uint32_t se) {
+        if (se == GEN_NIL) return;
+        uint32_t& rc = W(stw(se, ST_RC));
+        if (rc == 0) { err |= GERR_REF; return; }
+        if (--rc != 0) return;
+        for (int s = 0; s < G.nslots; s++) evDecref(slot(se, s));
+        freeBit(G.offSTfree, se);
+    }
+    __device__ uint32_t newSt() {
+        const uint32_t se = alloc(G.offSTfree, G.STCAP);
+        if (se == GEN_NIL) return se;
+        W64(stw(se, ST_TS), -1);
+        W(stw(se, ST_TYPE)) = 0;
+        W(stw(se, ST_RC)) = 0;
+        for (int s = 0; s < G.nslots; s++) W(stw(se, ST_SLOTS + (uint32_t)s)) = GEN_NIL;
+        return se;
+    }
+    __device__ void setSlot(uint32_t se, int s, uint32_t e) {
+        evIncref(e);
+        uint32_t& w = W(stw(se, ST_SLOTS + (uint32_t)s));
+        const uint32_t old = w;
+        w = e;
+        evDecref(old);
+    }
+    // StateEventCloner.copyStateEvent: shallow copy of the slot references (StateEventCloner.java:48-60)
+    __device__ uint32_t cloneSt(uint32_t se) {
+        const uint32_t c = newSt();
+        if (c == GEN_NIL) return c;
+        for (int s = 0; s < G.nslots; s++) setSlot(c, s, slot(se, s));
+        W(stw(c, ST_TYPE)) = W(stw(se, ST_TYPE));
+        setStTs(c, stTs(se));
+        return c;
+    }
+    // StateEvent.getStreamEvent(int[]) for (slot, index-in-chain) (StateEvent.java:138-182)
+    __device__ uint32_t chainAt(uint32_t se, int s, int idx) const {
+        uint32_t e = slot(se, s);
+        if (e == GEN_NIL) return GEN_NIL;
+        if (idx >= 0) {
+            for (int i = 1; i <= idx; i++) {
+                e = evNext(e);
+                if (e == GEN_NIL) return GEN_NIL;
+            }
+            return e;
+        }
+        if (idx == -1) {
+            while (evNext(e) != GEN_NIL) e = evNext(e);
+            return e;
+        }
+        if (idx == -2) {
+            if (evNext(e) == GEN_NIL) return GEN_NIL;
+            while (evNext(evNext(e)) != GEN_NIL) e = evNext(e);
+            return e;
+        }
+        int n = 0;
+        for (uint32_t x = e; x != GEN_NIL; x = evNext(x)) n++;
+        const int index = n + idx;
+        if (index < 0) return GEN_NIL;
+        for (int i = 0; i < index; i++) e = evNext(e);
+        return e;
+    }
+    // StateEvent.addEvent / removeLastEvent (StateEvent.java:212-236)
+    __device__ void addEvent(uint32_t se, int s, uint32_t e) {
+        uint32_t x = slot(se, s);
+        if (x == GEN_NIL) { setSlot(se, s, e); return; }
+        while (evNext(x) != GEN_NIL) x = evNext(x);
+        evIncref(e);
+        W(sew(x, SE_NEXT)) = e;
+    }
+    __device__ void removeLastEvent(uint32_t se, int s) {
+        uint32_t x = slot(se, s);
+        if (x == GEN_NIL) return;
+        while (evNext(x) != GEN_NIL) {
+            const uint32_t nx = evNext(x);
+            if (evNext(nx) == GEN_NIL) {
+                W(sew(x, SE_NEXT)) = GEN_NIL;
+                evDecref(nx);
+                return;
+            }
+            x = nx;
+        }
+        setSlot(se, s, GEN_NIL);
+    }
+
+    // ---- lists of StateEvents ----
+    __device__ void push(int p, int which, uint32_t se) {
+        uint32_t& n = len(p, which);
+        if (n >= G.L) { err |= GERR_CAP; return; }
+        stIncref(se);
+        at(p, which, n) = se;
+        n++;
+    }
+    __device__ void erase(int p, int which, uint32_t i) {
+        uint32_t& n = len(p, which);
+        const uint32_t se = at(p, which, i);
+        for (uint32_t j = i + 1; j < n; j++) at(p, which, j - 1) = at(p, which, j);
+        n--;
+        stDecref(se);
+    }
+    __device__ void clearList(int p, int which) {
+        uint32_t& n = len(p, which);
+        const uint32_t m = n;
+        n = 0;
+        for (uint32_t j = 0; j < m; j++) stDecref(at(p, which, j));
+    }
+    __device__ bool removeValue(int p, int which, uint32_t se) {
+        const uint32_t n = len(p, which);
+        for (uint32_t j = 0; j < n; j++)
+            if (at(p, which, j) == se) { erase(p, which, j); return true; }
+        return false;
+    }
+    // eventTimeComparator (StreamPreStateProcessor.java:66-80): ts -1 last; List.sort is stable
+    __device__ bool tsBefore(uint32_t a, uint32_t b) const {
+        const int64_t ta = stTs(a), tb = stTs(b);
+        if (ta == -1) return false;
+        if (tb == -1) return true;
+        return ta < tb;
+    }
+    // newAndEvery sorted by ts, appended to pending, cleared
+    __device__ void promote(int p) {
+        const uint32_t n = len(p, 1);
+        for (uint32_t i = 1; i < n; i++) {  // stable insertion sort
+            const uint32_t x = at(p, 1, i);
+            uint32_t j = i;
+            while (j > 0 && tsBefore(x, at(p, 1, j - 1))) { at(p, 1, j) = at(p, 1, j - 1); j--; }
+            at(p, 1, j) = x;
+        }
+        uint32_t& pn = len(p, 0);
+        for (uint32_t i = 0; i < n; i++) {
+            if (pn >= G.L) { err |= GERR_CAP; break; }
+            at(p, 0, pn++) = at(p, 1, i);  // the reference moves: no count change
+        }
+        len(p, 1) = 0;
+    }
+
+    // ---- timers (Scheduler) ----
+    __device__ uint32_t qlen(int p) const { return W(ks(p) + KS_QLEN); }
+    __device__ int64_t qhead(int p) const {
+        const uint32_t h = W(ks(p) + KS_QHEAD);
+        return R64(ks(p) + KS_LISTS + 2 * G.L + 2 * h);
+    }
+    __device__ void qpop(int p) const {
+        uint32_t& h = W(ks(p) + KS_QHEAD);
+        h = (h + 1) % G.Q;
+        W(ks(p) + KS_QLEN) -= 1;
+    }
+    __device__ void notifyAt(int p, int64_t t) {  // Scheduler.notifyAt + schedule (Scheduler.java:114-156)
+        uint32_t& n = W(ks(p) + KS_QLEN);
+        if (n >= G.Q) { err |= GERR_CAP; return; }
+        const uint32_t pos = (W(ks(p) + KS_QHEAD) + n) % G.Q;
+        W64(ks(p) + KS_LISTS + 2 * G.L + 2 * pos, t);
+        n++;
+        if (!G.playback && !flag(p, GF_RUNNING) && n == 1) {
+            setFlag(p, GF_RUNNING, true);
+            W64(ks(p) + KS_FIRE, t > now ? t : now);
+            W(ks(p) + KS_ORDER) = ++W(1);
+        }
+    }
+
+    // ---- filters ----
+    __device__ GVal cvt(GVal v, int from, int to) const {
+        if (v.null) return v;
+        if (from == SG_T_INT) {
+            const int32_t x = (int32_t)(uint32_t)v.b;
+            if (to == SG_T_LONG) return {(uint64_t)(int64_t)x, false};
+            if (to == SG_T_FLOAT) return {gbf32((float)x), false};
+            if (to == SG_T_DOUBLE) return {gbf64((double)x), false};
+        } else if (from == SG_T_LONG) {
+            const int64_t x = (int64_t)v.b;
+            if (to == SG_T_FLOAT) return {gbf32((float)x), false};
+            if (to == SG_T_DOUBLE) return {gbf64((double)x), false};
+        } else if (from == SG_T_FLOAT && to == SG_T_DOUBLE) {
+            return {gbf64((double)gf32(v.b)), false};
+        }
+        return v;
+    }
+    __device__ GVal arith(int op, int t, GVal l, GVal r) const {
+        if (l.null || r.null) return {0, true};
+        switch (t) {
+        case SG_T_INT: {
+            const int32_t a = (int32_t)(uint32_t)l.b, b = (int32_t)(uint32_t)r.b;
+            const uint32_t ua = (uint32_t)a, ub = (uint32_t)b;
+            switch (op) {
+            case SG_OP_ADD: return {(uint64_t)(uint32_t)(ua + ub), false};
+            case SG_OP_SUB: return {(uint64_t)(uint32_t)(ua - ub), false};
+            case SG_OP_MUL: return {(uint64_t)(uint32_t)(ua * ub), false};
+            case SG_OP_DIV:
+                if (b == 0) return {0, true};
+                if (b == -1) return {(uint64_t)(uint32_t)(0u - ua), false};
+                return {(uint64_t)(uint32_t)(a / b), false};
+            default:
+                if (b == 0) return {0, true};
+                if (b == -1) return {0, false};
+                return {(uint64_t)(uint32_t)(a % b), false};
+            }
+        }
+        case SG_T_LONG: {
+            const int64_t a = (int64_t)l.b, b = (int64_t)r.b;
+            const uint64_t ua = (uint64_t)a, ub = (uint64_t)b;
+            switch (op) {
+            case SG_OP_ADD: return {ua + ub, false};
+            case SG_OP_SUB: return {ua - ub, false};
+            case SG_OP_MUL: return {ua * ub, false};
+            case SG_OP_DIV:
+                if (b == 0) return {0, true};
+                if (b == -1) return {0ull - ua, false};
+                return {(uint64_t)(a / b), false};
+            default:
+                if (b == 0) return {0, true};
+                if (b == -1) return {0, false};
+                return {(uint64_t)(a % b), false};
+            }
+        }
+        case SG_T_FLOAT: {
+            const float a = gf32(l.b), b = gf32(r.b);
+            switch (op) {
+            case SG_OP_ADD: return {gbf32(__fadd_rn(a, b)), false};
+            case SG_OP_SUB: return {gbf32(__fsub_rn(a, b)), false};
+            case SG_OP_MUL: return {gbf32(__fmul_rn(a, b)), false};
+            case SG_OP_DIV: if (b == 0.0f) return {0, true}; return {gbf32(__fdiv_rn(a, b)), false};
+            default: if (b == 0.0f) return {0, true}; return {gbf32(fmodf(a, b)), false};
+            }
+        }
+        default: {
+            const double a = gf64(l.b), b = gf64(r.b);
+            switch (op) {
+            case SG_OP_ADD: return {gbf64(__dadd_rn(a, b)), false};
+            case SG_OP_SUB: return {gbf64(__dsub_rn(a, b)), false};
+            case SG_OP_MUL: return {gbf64(__dmul_rn(a, b)), false};
+            case SG_OP_DIV: if (b == 0.0) return {0, true}; return {gbf64(__ddiv_rn(a, b)), false};
+            default: if (b == 0.0) return {0, true}; return {gbf64(fmod(a, b)), false};
+            }
+        }
+        }
+    }
+    template <class T> __device__ static bool cmpOp(int op, T a, T b) {
+        switch (op) {
+        case SG_OP_EQ: return a == b;
+        case SG_OP_NE: return a != b;
+        case SG_OP_GT: return a > b;
+        case SG_OP_GE: return a >= b;
+        case SG_OP_LT: return a < b;
+        default: return a <= b;
+        }
+    }
+    __device__ bool compare(int op, int dom, GVal l, GVal r) const {
+        if (l.null || r.null) return op == SG_OP_NE;  // CompareConditionExpressionExecutor.java:38-42
+        switch (dom) {
+        case SG_T_INT: return cmpOp(op, (int32_t)(uint32_t)l.b, (int32_t)(uint32_t)r.b);
+        case SG_T_LONG: return cmpOp(op, (int64_t)l.b, (int64_t)r.b);
+        case SG_T_FLOAT: return cmpOp(op, gf32(l.b), gf32(r.b));
+        case SG_T_DOUBLE: return cmpOp(op, gf64(l.b), gf64(r.b));
+        case SG_T_BOOL: return cmpOp(op, (uint32_t)(l.b & 1), (uint32_t)(r.b & 1));
+        default: return cmpOp(op, (uint32_t)l.b, (uint32_t)r.b);
+        }
+    }
+    // FilterProcessor.process: pass iff the condition is a non-null true (FilterProcessor.java:48-60)
+    __device__ bool eval(uint32_t se, uint32_t pc, uint32_t n) {
+        GVal stk[24];
+        int sp = 0;
+        const uint32_t end = pc + n;
+        while (pc < end) {
+            const uint32_t w = G.code[pc];
+            const uint32_t op = w & 0xff, a = (w >> 8) & 0xff, b = (w >> 16) & 0xff;
+            if (sp > 22) { err |= GERR_CAP; return false; }
+            switch (op) {
+            case SG_OP_VAR: {
+                const uint32_t e = chainAt(se, (int)b, (int32_t)G.code[pc + 2]);
+                const uint32_t at_ = G.code[pc + 1];
+                if (e == GEN_NIL) stk[sp++] = {0, true};
+                else stk[sp++] = {(uint64_t)R64(sew(e, SE_ATTR + 2 * at_)), ((W(sew(e, SE_NULL)) >> at_) & 1u) != 0};
+                break;
+            }
+            case SG_OP_CONST:
+                stk[sp++] = {(uint64_t)G.code[pc + 1] | ((uint64_t)G.code[pc + 2] << 32), b != 0};
+                break;
+            case SG_OP_CVT: stk[sp - 1] = cvt(stk[sp - 1], (int)a, (int)b); break;
+            case SG_OP_ADD: case SG_OP_SUB: case SG_OP_MUL: case SG_OP_DIV: case SG_OP_MOD:
+                stk[sp - 2] = arith((int)op, (int)a, stk[sp - 2], stk[sp - 1]);
+                sp--;
+                break;
+            case SG_OP_EQ: case SG_OP_NE: case SG_OP_GT: case SG_OP_GE: case SG_OP_LT: case SG_OP_LE:
+                stk[sp - 2] = {(uint64_t)compare((int)op, (int)a, stk[sp - 2], stk[sp - 1]), false};
+                sp--;
+                break;
+            case SG_OP_AND: {
+                const bool l = !stk[sp - 2].null && (stk[sp - 2].b & 1), r = !stk[sp - 1].null && (stk[sp - 1].b & 1);
+                stk[sp - 2] = {(uint64_t)(l && r), false};
+                sp--;
+                break;
+            }
+            case SG_OP_OR: {
+                const bool l = !stk[sp - 2].null && (stk[sp - 2].b & 1), r = !stk[sp - 1].null && (stk[sp - 1].b & 1);
+                stk[sp - 2] = {(uint64_t)(l || r), false};
+                sp--;
+                break;
+            }
+            case SG_OP_NOT: {
+                const bool t = !stk[sp - 1].null && (stk[sp - 1].b & 1);
+                stk[sp - 1] = {(uint64_t)(!t), false};
+                break;
+            }
+            case SG_OP_ISNULL: stk[sp - 1] = {(uint64_t)stk[sp - 1].null, false}; break;
+            case SG_OP_ISNULL_EV: {
+                const uint32_t e = chainAt(se, (int)b, (int32_t)G.code[pc + 1]);
+                stk[sp++] = {(uint64_t)(e == GEN_NIL), false};
+                break;
+            }
+            default: err |= GERR_REF; return false;
+            }
+            pc += op_len(op);
+        }
+        return sp > 0 && !stk[sp - 1].null && (stk[sp - 1].b & 1);
+    }
+
+    // ---- match output (QuerySelector input) ----
+    __device__ void project(uint32_t se) {
+        if (resLeft == 0) {
+            resBase = atomicAdd(A.o.raw_count, 16ull);
+            resLeft = 16;
+        }
+        const unsigned long long r = resBase++;
+        resLeft--;
+        matches++;
+        if (r >= A.o.raw_cap) { err |= GERR_MATCHCAP; return; }
+        uint32_t* rec = A.o.raw + r * A.o.recWords;
+        const bool timer = trigSeq == SG_TIMER_SEQ;
+        rec[0] = timer ? 0xfffffffeu : trigIdx;
+        rec[1] = timer ? 0u : trigRank++;
+        rec[2] = (uint32_t)trigSeq;
+        rec[3] = (uint32_t)(trigSeq >> 32);
+        const int64_t ts = stTs(se);
+        rec[4] = (uint32_t)(uint64_t)ts;
+        rec[5] = (uint32_t)((uint64_t)ts >> 32);
+        rec[6] = k;
+        uint32_t* lens = rec + 7;
+        uint32_t* seqs = lens + G.nslots;
+        for (int s = 0; s < G.nslots; s++) {
+            uint32_t n = 0;
+            for (uint32_t e = slot(se, s); e != GEN_NIL; e = evNext(e)) {
+                if (n >= G.MC) { err |= GERR_CHAIN; break; }
+                const uint64_t q = evSeq(e);
+                seqs[2 * (s * G.MC + n)] = (uint32_t)q;
+                seqs[2 * (s * G.MC + n) + 1] = (uint32_t)(q >> 32);
+                n++;
+            }
+            lens[s] = n;
+        }
+        if (timer) {
+            A.o.tk1[r] = tk1;
+            A.o.tk2[r] = tk2;
+            A.o.tk3[r] = k;
+            atomicAdd(A.o.nvalid, 1ull);
+        } else {
+            A.o.t_cnt[trigIdx] += 1;
+        }
+    }
+
+    // ---- StreamPreStateProcessor & co (per processor p, this key) ----
+    __device__ bool isExpired(uint32_t se, int64_t t) const {  // StreamPreStateProcessor.java:118-129
+        if (G.within == -1) return false;
+        for (int i = 0; i < G.nStartIds; i++) {
+            const uint32_t e = slot(se, G.startIds[i]);
+            if (e != GEN_NIL) {
+                const int64_t d = evTs(e) - t;
+                if ((d < 0 ? -d : d) > G.within) return true;
+            }
+        }
+        return false;
+    }
+
+    __device__ void init(int p) {  // StreamPreStateProcessor.java:178-194
+        const GenPre& P = G.pre[p];
+        const GenPost& Q = G.post[P.thisPost];
+        if (P.isStart && (!flag(p, GF_INIT) || Q.nextEveryStatePre != GEN_NONE ||
+                          (G.qtype == SG_Q_SEQUENCE && Q.nextStatePre != GEN_NONE && G.pre[Q.nextStatePre].absent))) {
+            const uint32_t se = newSt();
+            if (se == GEN_NIL) return;
+            stIncref(se);
+            addState(p, se);
+            stDecref(se);
+            setFlag(p, GF_INIT, true);
+        }
+    }
+
+    __device__ void addState(int p, uint32_t se) {
+        const GenPre& P = G.pre[p];
+        if (P.absent && flag(p, GF_INACTIVE)) return;
+        if (P.absent && P.kind == GK_STREAM) {  // AbsentStreamPreStateProcessor.java:83-103
+            if (G.qtype == SG_Q_SEQUENCE) clearList(p, 1);
+            push(p, 1, se);
+            if (!P.isStart) {
+                const int64_t t = stTs(se) + P.waiting;
+                W64(ks(p) + KS_LST, t);
+                notifyAt(p, t);
+            }
+            return;
+        }
+        if (P.kind == GK_LOGICAL) {  // LogicalPreStateProcessor.java:43-62
+            if (P.isStart || G.qtype == SG_Q_SEQUENCE) {
+                if (len(p, 1) == 0) push(p, 1, se);
+                if (P.partner != GEN_NONE && len(P.partner, 1) == 0) push(P.partner, 1, se);
+            } else {
+                push(p, 1, se);
+                if (P.partner != GEN_NONE) push(P.partner, 1, se);
+            }
+            if (P.absent && !P.isStart && P.waiting != -1) {  // AbsentLogicalPreStateProcessor.java:77-97
+                notifyAt(p, stTs(se) + P.waiting);
+                if (G.pre[P.partner].absent) notifyAt(P.partner, stTs(se) + G.pre[P.partner].waiting);
+            }
+            return;
+        }
+        // StreamPreStateProcessor.java:214-227, CountPreStateProcessor.java:114-128
+        if (G.qtype == SG_Q_SEQUENCE) {
+            if (len(p, 1) == 0) push(p, 1, se);
+        } else {
+            push(p, 1, se);
+        }
+        if (P.kind == GK_COUNT && P.minCount == 0 && slot(se, P.stateId) == GEN_NIL)  // :129-136
+            processMinCountReached(P.countPost, se);
+    }
+
+    __device__ void addEveryState(int p, uint32_t se) {
+        const GenPre& P = G.pre[p];
+        const uint32_t c = cloneSt(se);
+        if (c == GEN_NIL) return;
+        stIncref(c);
+        W(stw(c, ST_TYPE)) = 0;  // CURRENT
+        created++;
+        if (P.absent && P.kind == GK_LOGICAL) {  // AbsentLogicalPreStateProcessor.java:99-118
+            const uint32_t own = slot(c, P.stateId);
+            if (own != GEN_NIL) setStTs(c, evTs(own));
+            setSlot(c, P.stateId, GEN_NIL);
+            setSlot(c, G.pre[P.partner].stateId, GEN_NIL);
+            push(p, 1, c);
+            push(P.partner, 1, c);
+        } else if (P.absent) {  // AbsentStreamPreStateProcessor.java:105-123
+            for (int i = P.stateId; i < G.nslots; i++) setSlot(c, i, GEN_NIL);
+            push(p, 1, c);
+            const int64_t t = stTs(se) + P.waiting;
+            W64(ks(p) + KS_LST, t);
+            notifyAt(p, t);
+        } else if (P.kind == GK_LOGICAL) {  // LogicalPreStateProcessor.java:64-84
+            for (int i = P.stateId; i < G.nslots; i++) setSlot(c, i, GEN_NIL);
+            push(p, 1, c);
+            if (P.partner != GEN_NONE) {
+                setSlot(c, G.pre[P.partner].stateId, GEN_NIL);
+                push(P.partner, 1, c);
+            }
+        } else {  // StreamPreStateProcessor.java:229-247
+            for (int i = P.stateId; i < G.nslots; i++) setSlot(c, i, GEN_NIL);
+            push(p, 1, c);
+        }
+        stDecref(c);
+    }
+
+    __device__ bool seqHold(int p) const {  // SEQUENCE, no every, the next state still has pending partials
+        const GenPost& Q = G.post[G.pre[p].thisPost];
+        return G.qtype == SG_Q_SEQUENCE && Q.nextEveryStatePre == GEN_NONE && Q.nextStatePre != GEN_NONE &&
+               len(Q.nextStatePre, 0) != 0;
+    }
+
+    __device__ void resetState(int p) {
+        const GenPre& P = G.pre[p];
+        if (P.kind == GK_LOGICAL) {  // LogicalPreStateProcessor.java:86-108
+            if (P.logicalType == SG_L_OR || len(p, 0) == len(P.partner, 0)) {
+                clearList(p, 0);
+                clearList(P.partner, 0);
+                if (P.isStart && len(p, 1) == 0) {
+                    if (seqHold(p)) return;
+                    init(p);
+                }
+            }
+            return;
+        }
+        clearList(p, 0);  // StreamPreStateProcessor.java:287-305
+        if (P.isStart && len(p, 1) == 0) {
+            if (seqHold(p)) return;
+            init(p);
+        }
+    }
+
+    __device__ void updateState(int p) {
+        const GenPre& P = G.pre[p];
+        if (P.kind == GK_COUNT && flag(p, GF_SSRESET)) {  // CountPreStateProcessor.java:168-180
+            setFlag(p, GF_SSRESET, false);
+            init(p);
+        }
+        promote(p);
+        if (P.kind == GK_LOGICAL) promote(P.partner);  // LogicalPreStateProcessor.java:110-122
+    }
+
+    __device__ void expireEvents(int p, int64_t t) {  // StreamPreStateProcessor.java:325-361
+        uint32_t expired = GEN_NIL;
+        uint32_t i = 0;
+        while (i < len(p, 0)) {
+            const uint32_t se = at(p, 0, i);
+            if (!isExpired(se, t)) break;
+            if (W(stw(se, ST_TYPE)) != 1) {
+                W(stw(se, ST_TYPE)) = 1;
+                stIncref(se);
+                stDecref(expired);
+                expired = se;
+            }
+            erase(p, 0, i);
+        }
+        i = 0;
+        while (i < len(p, 1)) {
+            const uint32_t se = at(p, 1, i);
+            if (isExpired(se, t)) {
+                if (W(stw(se, ST_TYPE)) != 1) {
+                    W(stw(se, ST_TYPE)) = 1;
+                    stIncref(se);
+                    stDecref(expired);
+                    expired = se;
+                }
+                erase(p, 1, i);
+            } else {
+                i++;
+            }
+        }
+        const int we = G.pre[p].withinEvery;
+        if (expired != GEN_NIL && we != GEN_NONE) {
+            addEveryState(we, expired);
+            updateState(we);
+        }
+        stDecref(expired);
+    }
+
+    __device__ void startStateReset(int p) {  // CountPreStateProcessor.java:155-166
+        for (int depth = 0; depth < 2 * GEN_MAXP; depth++) {
+            setFlag(p, GF_SSRESET, true);
+            const GenPre& P = G.pre[p];
+            if (G.post[P.thisPost].callbackPre == GEN_NONE) return;
+            p = G.post[P.countPost].thisPre;
+        }
+        err |= GERR_REF;  // the reference overflows its stack here
+    }
+
+    __device__ void runChain(int p, uint32_t se) {  // StreamPreStateProcessor.process(StateEvent) :131-142
+        setFlag(p, GF_CHANGED, false);
+        const GenPre& P = G.pre[p];
+        if (P.flen == 0 || eval(se, P.fpc, P.flen)) postProcess(P.thisPost, se);
+    }
+
+    // ---- post processors ----
+    __device__ void streamProcess(int q, uint32_t se) {  // StreamPostStateProcessor.java:64-83
+        const GenPost& Q = G.post[q];
+        setFlag(Q.thisPre, GF_CHANGED, true);
+        setStTs(se, evTs(slot(se, Q.stateId)));
+        if (Q.hasNext) ret[q] = true;
+        stIncref(se);
+        if (Q.nextStatePre != GEN_NONE) addState(Q.nextStatePre, se);
+        if (Q.nextEveryStatePre != GEN_NONE) addEveryState(Q.nextEveryStatePre, se);
+        if (Q.callbackPre != GEN_NONE) startStateReset(Q.callbackPre);
+        stDecref(se);
+    }
+    __device__ void processMinCountReached(int q, uint32_t se) {  // CountPostStateProcessor.java:68-80
+        const GenPost& Q = G.post[q];
+        if (Q.hasNext) {
+            setFlag(Q.thisPre, GF_CHANGED, true);
+            ret[q] = true;
+        }
+        stIncref(se);
+        if (Q.nextStatePre != GEN_NONE) addState(Q.nextStatePre, se);
+        if (Q.nextEveryStatePre != GEN_NONE) addEveryState(Q.nextEveryStatePre, se);
+        stDecref(se);
+    }
+    __device__ void postProcess(int q, uint32_t se) {
+        const GenPost& Q = G.post[q];
+        if (Q.absent) {  // Absent{Stream,Logical}PostStateProcessor
+            const uint32_t ev = slot(se, Q.stateId);
+            setFlag(Q.thisPre, GF_CHANGED, true);
+            ret[q] = true;
+            if (Q.kind == GK_STREAM) {
+                setStTs(se, evTs(ev));
+                if (G.pre[Q.thisPre].isStart && Q.nextEveryStatePre == Q.thisPre) addEveryState(Q.thisPre, se);
+            }
+            updateLastArrivalTime(Q.thisPre, evTs(ev));
+            return;
+        }
+        if (Q.kind == GK_COUNT) {  // CountPostStateProcessor.java:39-66
+            uint32_t e = slot(se, Q.stateId);
+            int n = 1;
+            while (evNext(e) != GEN_NIL) { n++; e = evNext(e); }
+            setFlag(Q.thisPre, GF_SUCCESS, true);
+            setStTs(se, evTs(e));
+            if (n >= Q.minCount) {
+                if (G.qtype == SG_Q_SEQUENCE) {
+                    stIncref(se);
+                    if (Q.nextStatePre != GEN_NONE) addState(Q.nextStatePre, se);
+                    if (n != Q.maxCount) addState(Q.thisPre, se);
+                    stDecref(se);
+                } else if (n == Q.minCount) {
+                    processMinCountReached(q, se);
+                }
+                if (n == Q.maxCount) setFlag(Q.thisPre, GF_CHANGED, true);
+            }
+            return;
+        }
+        if (Q.kind == GK_LOGICAL) {  // LogicalPostStateProcessor.java:59-83
+            if (Q.logicalType == SG_L_AND) {
+                const GenPre& PP = G.pre[Q.partnerPre];
+                const bool go = PP.absent ? partnerCanProceed(Q.partnerPre, se) : slot(se, PP.stateId) != GEN_NIL;
+                if (go) streamProcess(q, se);
+                else setFlag(Q.thisPre, GF_CHANGED, true);
+            } else {
+                streamProcess(q, se);
+                if (G.post[Q.partnerPost].hasNext && G.pre[Q.thisPre].thisLast == Q.partnerPost) ret[Q.partnerPost] = true;
+            }
+            return;
+        }
+        streamProcess(q, se);
+    }
+
+    // ---- absent states ----
+    __device__ void updateLastArrivalTime(int p, int64_t ts) {
+        if (G.pre[p].kind == GK_LOGICAL) {  // AbsentLogicalPreStateProcessor.java:65-74
+            W64(ks(p) + KS_LAT, ts);
+            return;
+        }
+        const int64_t t = ts + G.pre[p].waiting;  // AbsentStreamPreStateProcessor.java:70-81
+        W64(ks(p) + KS_LST, t);
+        notifyAt(p, t);
+    }
+    __device__ void partitionCreated(int p) {  // AbsentStreamPreStateProcessor.java:290-308 (+ logical)
+        if (flag(p, GF_STARTED)) return;
+        setFlag(p, GF_STARTED, true);
+        const GenPre& P = G.pre[p];
+        if (P.isStart && P.waiting != -1 && !flag(p, GF_INACTIVE)) {
+            if (P.kind == GK_STREAM) W64(ks(p) + KS_LST, now + P.waiting);
+            notifyAt(p, now + P.waiting);
+        }
+    }
+    __device__ bool partnerCanProceed(int p, uint32_t se) {  // AbsentLogicalPreStateProcessor.java:391-422
+        const GenPre& P = G.pre[p];
+        const GenPost& Q = G.post[P.thisPost];
+        const int64_t lat = R64(ks(p) + KS_LAT);
+        if (G.qtype == SG_Q_SEQUENCE && Q.nextEveryStatePre == GEN_NONE && lat > 0) return false;
+        if (P.waiting == -1) {
+            if (Q.nextEveryStatePre == GEN_NONE) return slot(se, P.stateId) == GEN_NIL;
+            if (lat > 0) {
+                W64(ks(p) + KS_LAT, 0);
+                init(p);
+                return false;
+            }
+            return true;
+        }
+        return slot(se, P.stateId) != GEN_NIL;
+    }
+    __device__ void sendAbsentEvent(int p, uint32_t se) {  // Absent*PreStateProcessor.sendEvent
+        const GenPre& P = G.pre[p];
+        const GenPost& Q = G.post[P.thisPost];
+        if (Q.hasNext) project(se);
+        if (Q.nextStatePre != GEN_NONE) addState(Q.nextStatePre, se);
+        if (Q.nextEveryStatePre != GEN_NONE) {
+            addEveryState(Q.nextEveryStatePre, se);
+        } else if (P.isStart) {
+            setFlag(p, GF_INACTIVE, true);
+            if (P.kind == GK_LOGICAL && P.logicalType == SG_L_OR && G.pre[P.partner].absent)
+                setFlag(P.partner, GF_INACTIVE, true);
+        }
+        if (Q.callbackPre != GEN_NONE) startStateReset(Q.callbackPre);
+    }
+
+    // the TIMER event of processor p for this key at currentTime (Absent*PreStateProcessor.process)
+    __device__ void processTimer(int p, int64_t currentTime) {
+        const GenPre& P = G.pre[p];
+        const GenPost& Q = G.post[P.thisPost];
+        if (flag(p, GF_INACTIVE)) return;
+        uint32_t rl[64];
+        uint32_t nr = 0;
+        if (P.kind == GK_STREAM) {  // AbsentStreamPreStateProcessor.java:151-227
+            bool initialize = P.isStart && len(p, 1) == 0 && len(p, 0) == 0;
+            if (initialize && G.qtype == SG_Q_SEQUENCE && Q.nextEveryStatePre == GEN_NONE && R64(ks(p) + KS_LST) > 0)
+                initialize = false;
+            if (initialize) {
+                const uint32_t se = newSt();
+                if (se != GEN_NIL) { stIncref(se); addState(p, se); stDecref(se); }
+            } else if (G.qtype == SG_Q_SEQUENCE && len(p, 1) != 0) {
+                resetState(p);
+            }
+            updateState(p);
+            uint32_t i = 0;
+            while (i < len(p, 0)) {
+                const uint32_t se = at(p, 0, i);
+                scanned++;
+                if (isExpired(se, currentTime)) {
+                    stIncref(se);
+                    erase(p, 0, i);
+                    if (P.withinEvery != GEN_NONE && Q.nextEveryStatePre != p) {
+                        if (Q.nextEveryStatePre == GEN_NONE) err |= GERR_REF;
+                        else addEveryState(Q.nextEveryStatePre, se);
+                    }
+                    stDecref(se);
+                    continue;
+                }
+                const int64_t ts = stTs(se);
+                if ((ts == -1 && currentTime >= R64(ks(p) + KS_LST)) || (ts != -1 && currentTime >= ts + P.waiting)) {
+                    stIncref(se);
+                    erase(p, 0, i);
+                    setStTs(se, currentTime);
+                    if (nr < 64) rl[nr++] = se; else { err |= GERR_CAP; stDecref(se); }
+                    continue;
+                }
+                i++;
+            }
+            if (P.withinEvery != GEN_NONE) updateState(P.withinEvery);
+            const bool notProcessed = nr == 0;
+            for (uint32_t j = 0; j < nr; j++) { sendAbsentEvent(p, rl[j]); stDecref(rl[j]); }
+            if (now > P.waiting + currentTime) W64(ks(p) + KS_LST, now + P.waiting);
+            if (notProcessed && R64(ks(p) + KS_LST) < currentTime) {
+                W64(ks(p) + KS_LST, currentTime + P.waiting);
+                notifyAt(p, currentTime + P.waiting);
+            }
+            return;
+        }
+        // AbsentLogicalPreStateProcessor.java:121-209
+        bool notProcessed = true;
+        if (currentTime >= R64(ks(p) + KS_LAT) + P.waiting) {
+            if (P.isStart && G.qtype == SG_Q_SEQUENCE && len(p, 1) == 0 && len(p, 0) == 0) {
+                const uint32_t se = newSt();
+                if (se != GEN_NIL) { stIncref(se); addState(p, se); stDecref(se); }
+            } else if (G.qtype == SG_Q_SEQUENCE && len(p, 1) != 0) {
+                resetState(p);
+            }
+            updateState(p);
+            uint32_t expired = GEN_NIL;
+            uint32_t i = 0;
+            const int ps = G.pre[P.partner].stateId;
+            while (i < len(p, 0)) {
+                const uint32_t se = at(p, 0, i);
+                scanned++;
+                if (isExpired(se, currentTime)) {
+                    stIncref(se);
+                    stDecref(expired);
+                    expired = se;
+                    erase(p, 0, i);
+                    continue;
+                }
+                const uint32_t own = slot(se, P.stateId);
+                const bool passed = own != GEN_NIL ? currentTime >= evTs(own) + P.waiting : currentTime >= stTs(se) + P.waiting;
+                if (passed) {
+                    stIncref(se);
+                    erase(p, 0, i);
+                    const bool partnerIn = slot(se, ps) != GEN_NIL;
+                    bool keep = false;
+                    if (P.logicalType == SG_L_OR && !partnerIn) {
+                        const uint32_t b = newEv(SG_BLANK_SEQ, -1, 0, true);
+                        if (b != GEN_NIL) addEvent(se, P.stateId, b);
+                        keep = true;
+                    } else if (P.logicalType == SG_L_AND && partnerIn) {
+                        keep = true;
+                    } else if (P.logicalType == SG_L_AND && !partnerIn) {
+                        const uint32_t b = newEv(SG_BLANK_SEQ, -1, 0, true);
+                        if (b != GEN_NIL) addEvent(se, P.stateId, b);
+                    }
+                    if (keep && nr < 64) rl[nr++] = se;
+                    else { if (keep) err |= GERR_CAP; stDecref(se); }
+                    continue;
+                }
+                i++;
+            }
+            if (expired != GEN_NIL && P.withinEvery != GEN_NONE) {
+                addEveryState(P.withinEvery, expired);
+                updateState(P.withinEvery);
+            }
+            stDecref(expired);
+            notProcessed = nr == 0;
+            for (uint32_t j = 0; j < nr; j++) {
+                setStTs(rl[j], currentTime);
+                sendAbsentEvent(p, rl[j]);
+                stDecref(rl[j]);
+            }
+            W64(ks(p) + KS_LAT, 0);
+        }
+        if (Q.nextEveryStatePre != GEN_NONE || (notProcessed && P.isStart)) {
+            const int64_t lat = R64(ks(p) + KS_LAT);
+            notifyAt(p, lat == 0 ? now + P.waiting : lat + P.waiting);
+        }
+    }
+
+    // Scheduler.sendTimerEvents (Scheduler.java:172-210)
+    __device__ void sendTimerEvents(int p) {
+        for (int guard = 0; guard < (1 << 20); guard++) {
+            if (qlen(p) == 0) return;
+            const int64_t t = qhead(p);
+            if (t > now) return;
+            qpop(p);
+            processTimer(p, t);
+        }
+        err |= GERR_CAP;
+    }
+
+    // ---- processAndReturn ----
+    __device__ void processAndReturnAbsentLogical(int p, uint64_t seq, int64_t ts, uint32_t pos) {
+        const GenPre& P = G.pre[p];
+        const GenPost& Q = G.post[P.thisPost];
+        uint32_t i = 0;
+        while (i < len(p, 0)) {
+            const uint32_t se = at(p, 0, i);
+            scanned++;
+            if (P.logicalType == SG_L_OR && slot(se, G.pre[P.partner].stateId) != GEN_NIL) {
+                erase(p, 0, i);
+                continue;
+            }
+            stIncref(se);
+            const uint32_t cur = slot(se, P.stateId);
+            evIncref(cur);
+            const uint32_t e = newEv(seq, ts, pos, false);
+            setSlot(se, P.stateId, e);
+            runChain(p, se);
+            if (P.waiting != -1 ||
+                (G.qtype == SG_Q_SEQUENCE && P.logicalType == SG_L_AND && Q.nextEveryStatePre != GEN_NONE))
+                setSlot(se, P.stateId, cur);
+            bool removed = false;
+            if (ret[P.thisLast]) {
+                ret[P.thisLast] = false;
+                erase(p, 0, i);
+                removed = true;
+                if (G.qtype == SG_Q_SEQUENCE) removeValue(P.partner, 0, se);
+            }
+            if (!flag(p, GF_CHANGED)) {
+                setSlot(se, P.stateId, cur);
+                if (G.qtype == SG_Q_SEQUENCE) {
+                    if (removed) err |= GERR_REF;
+                    else { erase(p, 0, i); removed = true; }
+                }
+            }
+            evDecref(cur);
+            stDecref(se);
+            if (!removed) i++;
+        }
+    }
+
+    // matches returned to the receiver are appended to `outList` (state event refs held)
+    // (outList holds at most OUTCAP entries)
+    static constexpr uint32_t OUTCAP = 64;
+    __device__ void processAndReturn(int p, uint64_t seq, int64_t ts, uint32_t pos, uint32_t* outList, uint32_t& nOut) {
+        const GenPre& P = G.pre[p];
+        if (P.absent) {
+            if (flag(p, GF_INACTIVE)) return;
+            if (P.kind == GK_LOGICAL) { processAndReturnAbsentLogical(p, seq, ts, pos); return; }
+        }
+        const uint32_t out0 = nOut;
+        uint32_t i = 0;
+        while (i < len(p, 0)) {
+            const uint32_t se = at(p, 0, i);
+            scanned++;
+            if (P.kind == GK_COUNT) {  // CountPreStateProcessor.java:53-95
+                if ((G.nslots > P.stateId + 1 && slot(se, P.stateId + 1) != GEN_NIL) ||
+                    (G.nslots > P.stateId + 2 && slot(se, P.stateId + 2) != GEN_NIL)) {
+                    erase(p, 0, i);
+                    continue;
+                }
+                stIncref(se);
+                const uint32_t e = newEv(seq, ts, pos, false);
+                if (e != GEN_NIL) addEvent(se, P.stateId, e);
+                setFlag(p, GF_SUCCESS, false);
+                runChain(p, se);
+                if (ret[P.thisLast]) {
+                    ret[P.thisLast] = false;
+                    if (nOut < OUTCAP) { stIncref(se); outList[nOut++] = se; } else err |= GERR_CAP;
+                }
+                bool removed = false;
+                if (flag(p, GF_CHANGED)) { erase(p, 0, i); removed = true; }
+                if (!flag(p, GF_SUCCESS)) {
+                    removeLastEvent(se, P.stateId);
+                    if (G.qtype == SG_Q_SEQUENCE && !removed) { erase(p, 0, i); removed = true; }
+                }
+                stDecref(se);
+                if (!removed) i++;
+                continue;
+            }
+            if (P.kind == GK_LOGICAL && P.logicalType == SG_L_OR && slot(se, G.pre[P.partner].stateId) != GEN_NIL) {
+                erase(p, 0, i);  // LogicalPreStateProcessor.java:153-157
+                continue;
+            }
+            // StreamPreStateProcessor.java:371-397
+            stIncref(se);
+            const uint32_t e = newEv(seq, ts, pos, false);
+            setSlot(se, P.stateId, e);
+            runChain(p, se);
+            if (ret[P.thisLast]) {
+                ret[P.thisLast] = false;
+                if (nOut < OUTCAP) { stIncref(se); outList[nOut++] = se; } else err |= GERR_CAP;
+            }
+            bool removed = false;
+            if (flag(p, GF_CHANGED)) {
+                erase(p, 0, i);
+                removed = true;
+            } else {
+                setSlot(se, P.stateId, GEN_NIL);
+                if (G.qtype == SG_Q_SEQUENCE) {
+                    if (!(P.kind == GK_STREAM && P.absent)) { erase(p, 0, i); removed = true; }
+                    if (P.kind == GK_STREAM && G.post[P.thisPost].callbackPre != GEN_NONE)
+                        startStateReset(G.post[P.thisPost].callbackPre);
+                }
+            }
+            stDecref(se);
+            if (!removed) i++;
+        }
+        if (P.absent) {  // AbsentStreamPreStateProcessor.processAndReturn returns nothing (:265-283)
+            for (uint32_t j = out0; j < nOut; j++) stDecref(outList[j]);
+            nOut = out0;
+        }
+    }
+
+    // ---- receivers ----
+    __device__ void stabilize(const GenRecv& r, int64_t ts) {
+        for (int i = 0; i < G.nAll; i++) expireEvents(G.allProcs[i], ts);
+        if (G.qtype == SG_Q_SEQUENCE) {  // Sequence*ProcessStreamReceiver.stabilizeStates -> resetAndUpdate
+            for (int i = 0; i < G.nReset; i++) resetState(G.resetOrder[i]);
+            for (int i = 0; i < G.nUpdate; i++) updateState(G.updateOrder[i]);
+        } else if (r.multi) {  // PatternMultiProcessStreamReceiver.java:42-51
+            for (int i = 0; i < r.nStateProcs; i++) updateState(r.stateProcs[i]);
+        } else if (r.nStateProcs > 0) {  // PatternSingleProcessStreamReceiver.java:34-41
+            updateState(r.stateProcs[0]);
+        }
+    }
+
+    __device__ void initKey() {  // PartitionRuntimeImpl.initPartition -> StateStreamRuntime.initPartition
+        if (W(0) & 1u) return;
+        W(0) |= 1u;
+        for (int i = 0; i < G.nInit; i++) init(G.initOrder[i]);
+        for (int i = 0; i < G.nStartup; i++) partitionCreated(G.startup[i]);
+    }
+
+    __device__ uint32_t defBase() const { return G.offDef; }
+
+    // one event of this key (MultiProcessStreamReceiver / SingleProcessStreamReceiver semantics)
+    __device__ void processEvent(const GenRecv& r, uint32_t pos, bool chunkEnd) {
+        const uint64_t seq = A.b.seq_base + pos;
+        const int64_t ts = A.b.ts[pos];
+        stabilize(r, ts);
+        uint32_t& nd = W(defBase());
+        if (r.multi) {
+            trigSeq = seq;
+            trigIdx = pos;
+            trigRank = 0;
+            for (int j = r.n - 1; j >= 0; j--) {  // reverse declaration order, projected at once
+                uint32_t outl[64];
+                uint32_t no = 0;
+                processAndReturn(r.procs[j], seq, ts, pos, outl, no);
+                for (uint32_t x = 0; x < no; x++) { project(outl[x]); stDecref(outl[x]); }
+            }
+        } else {
+            // deferred until the end of the chunk (consecutive events of this key in the batch)
+            uint32_t outl[64];
+            uint32_t no = 0;
+            processAndReturn(r.procs[0], seq, ts, pos, outl, no);
+            for (uint32_t x = 0; x < no; x++) {
+                if (nd >= G.DEF) { err |= GERR_CAP; stDecref(outl[x]); continue; }
+                W(defBase() + 1 + 2 * nd) = outl[x];
+                W(defBase() + 2 + 2 * nd) = pos;
+                nd++;
+            }
+            if (chunkEnd) flushDeferred();
+        }
+    }
+    __device__ void flushDeferred() {
+        uint32_t& nd = W(defBase());
+        uint32_t lastPos = 0xffffffffu;
+        for (uint32_t x = 0; x < nd; x++) {
+            const uint32_t se = W(defBase() + 1 + 2 * x), pos = W(defBase() + 2 + 2 * x);
+            if (pos != lastPos) { trigRank = 0; lastPos = pos; }
+            trigIdx = pos;
+            trigSeq = A.b.seq_base + pos;
+            project(se);
+            stDecref(se);
+        }
+        nd = 0;
+    }
+};
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------------
+// batch: one lane per key walks its key-sorted events
+// ------------------------------------------------------------------------------------------------
+extern "C" __global__ void __launch_bounds__(64) k_gen_batch(const GenArgs a) {
+    const uint32_t key = blockIdx.x * blockDim.x + threadIdx.x;
+    if (key >= a.K) return;
+    const uint32_t b = a.b.seg_begin[key], e = a.b.seg_end[key];
+    if (b >= e) return;
+    Lane L(a, key);
+    L.initKey();
+    const GenRecv& r = a.G->recv[a.b.stream];
+    if (r.n > 0) {
+        for (uint32_t j = b; j < e; j++) {
+            const uint32_t pos = a.b.sidx ? a.b.sidx[j] : j;
+            const uint32_t nxt = (j + 1 < e) ? (a.b.sidx ? a.b.sidx[j + 1] : j + 1) : 0xffffffffu;
+            L.processEvent(r, pos, nxt != pos + 1);
+        }
+    }
+    if (L.err) atomicOr(a.o.err, L.err);
+    atomicAdd(&a.o.stats[GST_SCANNED], L.scanned);
+    atomicAdd(&a.o.stats[GST_CREATED], L.created);
+    atomicAdd(&a.o.stats[GST_MATCHES], L.matches);
+    atomicAdd(&a.o.stats[GST_KEYS], 1ull);
+    // unused reserved raw slots are marked empty
+    for (uint32_t x = 0; x < L.resLeft; x++) {
+        const unsigned long long rr = L.resBase + x;
+        if (rr < a.o.raw_cap) {
+            a.o.raw[rr * a.o.recWords] = 0xffffffffu;
+            a.o.tk1[rr] = 0xffffffffu;  // sorts after every real timer match
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// timer sweep to a.now (sg_advance_time): every key with due timers runs them in the reference order
+// ------------------------------------------------------------------------------------------------
+extern "C" __global__ void __launch_bounds__(64) k_gen_timers(const GenArgs a) {
+    const uint32_t key = blockIdx.x * blockDim.x + threadIdx.x;
+    if (key >= a.K) return;
+    Lane L(a, key);
+    const GenProgram& G = *a.G;
+    if (!(L.W(0) & 1u)) {
+        if (G.partitioned) return;  // a key is created by its first event
+        // unpartitioned: QueryRuntimeImpl.start seeds the query at the clock of start()
+        L.now = G.playback ? a.now0 : a.now;
+        L.initKey();
+    }
+    const int64_t T = a.now;
+    if (G.playback) {
+        // each Scheduler's time-change listener, in registration order (Scheduler.java:73-104); the
+        // listener's TreeMultimap orders the keys by their queue head at collection
+        L.now = T;
+        for (int i = 0; i < G.nStartup; i++) {
+            const int p = G.startup[i];
+            if (L.qlen(p) == 0 || L.qhead(p) > T) continue;
+            L.tk1 = (uint32_t)i;
+            L.tk2 = L.qhead(p);
+            L.sendTimerEvents(p);
+        }
+    } else {
+        L.now = a.now0;  // the engine clock before this advance
+        // EventCallers of this key in time order (Scheduler.EventCaller.run, Scheduler.java:264-298)
+        for (int guard = 0; guard < (1 << 20); guard++) {
+            int best = -1;
+            int64_t bf = 0;
+            uint32_t bo = 0;
+            for (int i = 0; i < G.nStartup; i++) {
+                const int p = G.startup[i];
+                if (!L.flag(p, GF_RUNNING)) continue;
+                const int64_t f = L.R64(L.ks(p) + KS_FIRE);
+                const uint32_t o = L.W(L.ks(p) + KS_ORDER);
+                if (f <= T && (best < 0 || f < bf || (f == bf && o < bo))) { best = G.startup[i]; bf = f; bo = o; }
+            }
+            if (best < 0) break;
+            if (bf > L.now) L.now = bf;
+            L.tk1 = 0;
+            L.tk2 = bf;  // callers of different keys due together run in key order
+            L.sendTimerEvents(best);
+            if (L.qlen(best) != 0) {
+                const int64_t h = L.qhead(best);
+                L.W64(L.ks(best) + KS_FIRE, h > L.now ? h : L.now);
+                L.W(L.ks(best) + KS_ORDER) = ++L.W(1);
+            } else {
+                L.setFlag(best, GF_RUNNING, false);
+            }
+        }
+    }
+    if (L.err) atomicOr(a.o.err, L.err);
+    if (L.scanned) atomicAdd(&a.o.stats[GST_SCANNED], L.scanned);
+    if (L.created) atomicAdd(&a.o.stats[GST_CREATED], L.created);
+    if (L.matches) atomicAdd(&a.o.stats[GST_MATCHES], L.matches);
+    for (uint32_t x = 0; x < L.resLeft; x++) {
+        const unsigned long long rr = L.resBase + x;
+        if (rr < a.o.raw_cap) {
+            a.o.raw[rr * a.o.recWords] = 0xffffffffu;
+            a.o.tk1[rr] = 0xffffffffu;  // sorts after every real timer match
+        }
+    }
+}

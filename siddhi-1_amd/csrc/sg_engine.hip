@@ -11,6 +11,9 @@
 //   3. k_p2_advance: one lane per key advances that key's NFA over its events in arrival order
 //      (query/input/stream/state/StreamPreStateProcessor.java:308-403 and friends)
 // and on poll orders the accumulated matches by trigger seq (stable: per-key emission order kept).
+//
+// Query shapes outside the specialised two-state kernel (count, logical, SEQUENCE, absent states,
+// longer chains) run on the general device engine (gen_host.hip / gen_kernels.hip).
 #include <hip/hip_runtime.h>
 
 #include <rocprim/device/device_radix_sort.hpp>
@@ -28,6 +31,8 @@
 
 #include "../../include/siddhi_gpu.h"
 #include "../../include/siddhi_gpu_ir.h"
+#include "gen_engine.h"
+#include "gen_host.h"
 #include "sg_engine.h"
 #include "sg_jit.h"
 
@@ -157,6 +162,7 @@ hipError_t sort_payload_w(int W, void* tmp, size_t& tmp_bytes, const uint32_t* k
 struct sg_engine {
     int device = 0;
     hipStream_t stream = nullptr;
+    GenEngine* gen = nullptr;  // the general engine, when the query is not a two-state pattern
     sg_config cfg{};
     std::vector<uint32_t> ir;
     std::vector<IRStream> streams;
@@ -259,6 +265,7 @@ struct sg_engine {
     ~sg_engine() {
         if (device >= 0) (void)hipSetDevice(device);
         if (stream) (void)hipStreamSynchronize(stream);
+        if (gen) gen_destroy(gen);
         for (auto& sp : spans) { (void)hipEventDestroy(sp.a); (void)hipEventDestroy(sp.b); }
         for (auto x : free_events) (void)hipEventDestroy(x);
         for (void* p : owned) (void)hipFree(p);
@@ -821,7 +828,30 @@ int sg_engine_create(const void* ir, size_t ir_len, const sg_config* cfg, sg_eng
         e->mcap = cfg->match_capacity ? cfg->match_capacity : (uint64_t)e->maxb * 4;
         if (e->cap > SGD_MAX_CAP) throw std::invalid_argument("partial_capacity above 4095");
         if (e->mcap >= (1ull << 31)) throw std::invalid_argument("match_capacity must be < 2^31");
-        build_plan(e, ir, ir_len);
+        if (ir_len < SG_IR_HDR_WORDS * 4 || ir_len % 4) throw std::invalid_argument("IR too short");
+        if (((const uint32_t*)ir)[0] != SG_IR_MAGIC || ((const uint32_t*)ir)[1] != SG_IR_VERSION)
+            throw std::invalid_argument("bad IR magic/version");
+        // every shape must lower onto the general engine (validates the IR); the specialised
+        // two-state kernel takes the shapes it covers
+        delete gen_build_program((const uint32_t*)ir, ir_len / 4, e->cap);
+        bool general = getenv("SG_FORCE_GENERAL") != nullptr;
+        if (!general) {
+            try {
+                build_plan(e, ir, ir_len);
+            } catch (const std::runtime_error&) {
+                general = true;
+            }
+        }
+        if (general) {
+            int ndev = 0;
+            HIP_OK(hipGetDeviceCount(&ndev));
+            if (cfg->device < 0 || cfg->device >= ndev) throw HipError("no such HIP device");
+            HIP_OK(hipSetDevice(cfg->device));
+            HIP_OK(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+            e->gen = gen_create((const uint32_t*)ir, ir_len / 4, *cfg, e->stream);
+            *out = e;
+            return SG_OK;
+        }
         e->jq = make_jit_query(e);
         (void)sgj_generate(e->jq, e->consts);  // validates the filters, fixes the constant table
         if (!e->plan.partitioned && e->K != 1) e->K = 1;
@@ -852,6 +882,11 @@ int sg_push_batch(sg_engine* e, const sg_batch* b) {
     if (!e || !b) return fail(SG_ERR_INVALID, "null argument");
     try {
         HIP_OK(hipSetDevice(e->device));
+        if (e->gen) {
+            std::string msg;
+            const int rc = gen_push(e->gen, b, msg);
+            return rc == SG_OK ? rc : fail(rc, msg);
+        }
         return push(e, b);
     } catch (const std::exception& ex) {
         return fail(SG_ERR_DEVICE, ex.what());
@@ -859,15 +894,27 @@ int sg_push_batch(sg_engine* e, const sg_batch* b) {
 }
 
 int sg_advance_time(sg_engine* e, int64_t now_ms) {
-    (void)now_ms;
     if (!e) return fail(SG_ERR_INVALID, "null argument");
-    return SG_OK;  // no absent (timer) states on the device yet; nothing is time driven
+    if (!e->gen) return SG_OK;  // the two-state kernel's shapes have no timers
+    try {
+        HIP_OK(hipSetDevice(e->device));
+        std::string msg;
+        const int rc = gen_advance(e->gen, now_ms, msg);
+        return rc == SG_OK ? rc : fail(rc, msg);
+    } catch (const std::exception& ex) {
+        return fail(SG_ERR_DEVICE, ex.what());
+    }
 }
 
 int sg_poll_matches(sg_engine* e, uint32_t mem, sg_match_batch* out) {
     if (!e || !out) return fail(SG_ERR_INVALID, "null argument");
     try {
         HIP_OK(hipSetDevice(e->device));
+        if (e->gen) {
+            std::string msg;
+            const int rc = gen_poll(e->gen, mem, out, msg);
+            return rc == SG_OK ? rc : fail(rc, msg);
+        }
         return poll(e, mem, out);
     } catch (const std::exception& ex) {
         return fail(SG_ERR_DEVICE, ex.what());
@@ -876,6 +923,7 @@ int sg_poll_matches(sg_engine* e, uint32_t mem, sg_match_batch* out) {
 
 int sg_release_matches(sg_engine* e, sg_match_batch* m) {
     if (!e) return fail(SG_ERR_INVALID, "null argument");
+    if (e->gen) gen_release(e->gen);
     e->held = false;
     if (m) memset(m, 0, sizeof(*m));
     return SG_OK;
@@ -897,6 +945,10 @@ int sg_get_stats(sg_engine* e, sg_stats* out) {
     if (!e || !out) return fail(SG_ERR_INVALID, "null argument");
     try {
         HIP_OK(hipSetDevice(e->device));
+        if (e->gen) {
+            gen_stats(e->gen, out);
+            return SG_OK;
+        }
         unsigned long long s[SGD_ST_N];
         HIP_OK(hipMemcpyAsync(s, e->stats, sizeof(s), hipMemcpyDeviceToHost, e->stream));
         HIP_OK(hipStreamSynchronize(e->stream));

@@ -33,12 +33,17 @@ def hip_manager(n_keys=1024):
     return sa.SiddhiManager(engine_factory=make, n_keys=n_keys)
 
 
-KATS = [(f, c) for f, c in load_cases() if "skip" not in c and "absent" not in c.get("features", [])]
+from test_oracle_kat import KNOWN_UNSUPPORTED, SLOW
+
+KATS = [(f, c) for f, c in load_cases() if "skip" not in c and f"{f}::{c['name']}" not in SLOW]
 
 
 @pytest.mark.parametrize("fc", KATS, ids=[f"{f}::{c['name']}" for f, c in KATS])
 def test_gpu_kat(fc):
+    """every transcribed reference KAT through the HIP engine (two-state kernel or general engine)"""
     f, case = fc
+    if f"{f}::{case['name']}" in KNOWN_UNSUPPORTED:
+        pytest.skip(KNOWN_UNSUPPORTED[f"{f}::{case['name']}"])
     try:
         ok, msg = run_case(case, hip_manager())
     except sa.EngineError as ex:
