@@ -311,10 +311,10 @@ GenProgram* gen_build_program(const uint32_t* w, size_t nw, uint32_t partialCap)
         // capacities and the per-key block layout
         uint32_t mc = 1;
         for (int x = 0; x < G->nprocs; x++)
-            if (G->pre[x].kind == GK_COUNT) mc = std::max<uint32_t>(mc, G->pre[x].maxCount >= 0x7fffffff ? 16u : (uint32_t)G->pre[x].maxCount);
+            if (G->pre[x].kind == GK_COUNT) mc = std::max<uint32_t>(mc, G->pre[x].maxCount >= 0x7fffffff ? 48u : (uint32_t)G->pre[x].maxCount);
         for (int x = 0; x < G->nprocs; x++)
             if (G->pre[x].absent && G->pre[x].kind == GK_LOGICAL) mc = std::max<uint32_t>(mc, 2u);
-        G->MC = mc;
+        G->MC = std::min<uint32_t>(mc, 64u);  // output chain capacity (longer chains fail loudly)
         G->L = std::max<uint32_t>(4, partialCap);
         G->Q = G->L + 8;
         G->STCAP = std::min<uint32_t>(2 * G->L + 16, 0xfff0u);

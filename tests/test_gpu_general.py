@@ -64,7 +64,7 @@ ABSENT = {
 }
 
 
-def _engines(query, n_keys, max_batch, cap=48, mcap=1 << 22):
+def _engines(query, n_keys, max_batch, cap=48, mcap=1 << 20):
     app = sa.parse_app(query)
     cq = sa.compile_query(app, app.queries[0], sa.StringDictionary())
     gpu = sa.NativeEngine(sa.load_hip_library(), "sg_", cq.ir, n_keys=n_keys, max_batch=max_batch,
