@@ -1,15 +1,22 @@
-"""Benchmark: partitioned 2-step pattern query on MI355X (BASELINE.json configs[1], "C2").
+"""Benchmark: partitioned pattern query on MI355X (BASELINE.json configs[1], "C2").
 
     every e1=StockStream[price > 20] -> e2=StockStream[price > e1.price] within 10 sec
-    partition with (symbol of StockStream), 1,048,576 synthetic keys
+    partition with (symbol of StockStream), 1,048,576 synthetic keys per GPU
 
-A step = one micro-batch of 2^24 synthetic stock ticks (already resident in HBM) pushed through the
-C-ABI (key grouping + NFA advance) and polled (matches ordered by trigger seq, left in HBM).
-`value` = input events/sec of the whole job (all ranks).  N > 1: one process per GPU, each rank owns
-a disjoint shard of 1,048,576 keys and its own arrival stream (weak scaling, no data-path
-collective).  The roofline object prices the NFA advance kernel with the algorithmic byte model of
-DESIGN.md over its HIP-event-timed duration; cpu_baseline times the CPU oracle (the
+A step = one micro-batch of 2^24 synthetic stock ticks per GPU (already resident in HBM) pushed
+through the C-ABI (key grouping + NFA advance) and polled (matches ordered by trigger seq, left in
+HBM).  `value` = input events/sec of the whole job (all ranks).
+
+N > 1: one process per GPU.  The global stream is arrival ordered; each rank holds a contiguous
+slice of every step (2^24 events) and the step first reshards it by key over RCCL (all_to_all of the
+packed events, siddhi-1_amd/reshard.py), then runs its engine on the 2^20 keys it owns
+(weak scaling: keys and events per GPU fixed).
+
+The roofline object prices the NFA advance kernel with the algorithmic byte model of DESIGN.md
+ over its HIP-event-timed duration.  cpu_baseline times the CPU oracle (the
 single-threaded restatement of the reference engine) on a bounded prefix of the same stream.
+At N=1 `other_configs` adds BASELINE configs[2] (C3, counting + logical sequence) and configs[3]
+(C4, absent state, playback clock) on the general device engine.
 """
 import argparse
 import importlib
@@ -60,15 +67,60 @@ def cpu_baseline(sa, synth, n_keys, batch, seconds):
                       f"unavailable on the box)"}
 
 
+def to_dev(torch, d, dev):
+    return {k: torch.from_numpy(v.view(np.int32) if v.dtype == np.uint32 else v).to(dev) for k, v in d.items()}
+
+
+def run_general(sa, synth, torch, dev, query, make_batch, n_keys, batch, steps, warmup, cap, playback=False):
+    """One of the general-engine configs: events/s over `steps` timed batches (HBM-resident)."""
+    app = sa.parse_app(query)
+    cq = sa.compile_query(app, app.queries[0], sa.StringDictionary())
+    eng = sa.NativeEngine(sa.load_hip_library(), "sg_", cq.ir, n_keys=n_keys, max_batch=batch,
+                          partial_capacity=cap, match_capacity=2 * batch, device=dev.index or 0)
+    bats = [to_dev(torch, make_batch(s), dev) for s in range(warmup + steps)]
+    lastts = [int(b["ts"][-1].item()) for b in bats]
+    torch.cuda.synchronize()
+
+    def step(s):
+        t = bats[s]
+        if playback:  # InputHandler.send(Event[]): the clock moves to the last event first (A.9)
+            eng.advance_time(lastts[s])
+            m = eng.poll_device()
+            eng.release(m)
+        eng.push(0, s * batch, (batch, t["ts"].data_ptr(), [t["symbol"].data_ptr(), t["price"].data_ptr(),
+                                                            t["volume"].data_ptr()], t["key"].data_ptr()),
+                 [0, 1, 2], mem=sa.native.SG_MEM_DEVICE)
+        m = eng.poll_device()
+        n = int(m.n)
+        eng.release(m)
+        return n
+
+    for s in range(warmup):
+        step(s)
+    eng.synchronize()
+    st0 = eng.stats()
+    t0 = time.perf_counter()
+    for s in range(warmup, warmup + steps):
+        step(s)
+    eng.synchronize()
+    el = time.perf_counter() - t0
+    d = delta(st0, eng.stats())
+    eng.close()
+    return {"value": batch * steps / el, "unit": "events/s", "ms_per_step": el / steps * 1e3,
+            "keys": n_keys, "batch_events": batch, "matches_per_step": d["matches"] / steps,
+            "partials_scanned_per_step": d["partials_scanned"] / steps, "engine": "general"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=1 << 24)
-    ap.add_argument("--keys", type=int, default=1 << 20)
+    ap.add_argument("--keys", type=int, default=1 << 20, help="keys per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-extra", action="store_true", help="skip the C3 / C4 lines")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -76,38 +128,56 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     dist = None
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
 
     sa = importlib.import_module("siddhi-1_amd")
     synth = importlib.import_module("siddhi-1_amd.synth")
+    reshard = importlib.import_module("siddhi-1_amd.reshard")
     app = sa.parse_app(synth.C2_QUERY)
     cq = sa.compile_query(app, app.queries[0], sa.StringDictionary())
     B, K = args.batch, args.keys
-    eng = sa.NativeEngine(sa.load_hip_library(), "sg_", cq.ir, n_keys=K, max_batch=B, partial_capacity=64,
-                          match_capacity=2 * B, device=local, flags=sa.native.SG_CFG_TIMING)
+    maxb = B if world == 1 else B + B // 8   # received counts vary around B after the reshard
+    eng = sa.NativeEngine(sa.load_hip_library(), "sg_", cq.ir, n_keys=K, max_batch=maxb, partial_capacity=64,
+                          match_capacity=2 * maxb, device=local, flags=sa.native.SG_CFG_TIMING)
 
-    # inputs resident in HBM before timing: one independent stream per rank (its own key shard)
+    # inputs resident in HBM before timing: this rank's slice of every step of the global
+    # arrival-ordered stream over world * K keys (events per ms scale with the job)
     total = args.warmup + args.steps
-    seed = synth.SEED + 7919 * rank
     batches = []
     for s in range(total):
-        d = synth.stock_ticks(s * B, B, K, seed=seed)
-        batches.append({k: torch.from_numpy(v.view(np.int32) if v.dtype == np.uint32 else v).to(dev)
-                        for k, v in d.items()})
+        base = s * world * B + rank * B
+        d = synth.stock_ticks(base, B, K * world, rate_per_ms=2000 * world)
+        t = to_dev(torch, d, dev)
+        if world > 1:
+            t["key"] = t["key"].to(torch.int64)
+            t["seq"] = torch.arange(base, base + B, dtype=torch.int64, device=dev)
+            del t["symbol"]
+        batches.append(t)
     torch.cuda.synchronize()
+    local_seq = [0]
 
     def step(s):
         t = batches[s]
-        eng.push(0, s * B, (B, t["ts"].data_ptr(), [t["symbol"].data_ptr(), t["price"].data_ptr(),
-                                                    t["volume"].data_ptr()], t["key"].data_ptr()),
-                 [0, 1, 2], mem=sa.native.SG_MEM_DEVICE)
+        if world > 1:
+            # RCCL all-to-all of the packed events to the GPUs owning their keys
+            g = reshard.reshard({"key": t["key"], "ts": t["ts"], "price": t["price"], "volume": t["volume"]},
+                                "key", world)
+            lk = reshard.local_key(g["key"], world).to(torch.int32)
+            n = lk.numel()
+            cols = (n, g["ts"].data_ptr(), [lk.data_ptr(), g["price"].data_ptr(), g["volume"].data_ptr()],
+                    lk.data_ptr())
+        else:
+            n = B
+            cols = (B, t["ts"].data_ptr(), [t["symbol"].data_ptr(), t["price"].data_ptr(), t["volume"].data_ptr()],
+                    t["key"].data_ptr())
+        eng.push(0, local_seq[0], cols, [0, 1, 2], mem=sa.native.SG_MEM_DEVICE)
+        local_seq[0] += n
         m = eng.poll_device()
         eng.release(m)
-        return int(m.n) if hasattr(m, "n") else 0
 
     for s in range(args.warmup):
         step(s)
@@ -153,11 +223,11 @@ def main():
         "data": "synthetic (splitmix64 stock ticks, seeded, HBM-resident)",
         "config": {"workload": "C2: every e1=StockStream[price>20] -> e2=StockStream[price>e1.price] "
                                "within 10 sec, partition with (symbol of StockStream)",
-                   "keys_per_gpu": K, "batch_events": B, "events_per_ms": 2000,
-                   "parallelism": f"key-sharded x{world}"},
+                   "keys_per_gpu": K, "batch_events_per_gpu": B, "events_per_ms": 2000 * world,
+                   "parallelism": f"key-sharded x{world}" + (" (RCCL all-to-all reshard per step)" if world > 1 else "")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "k_p2_advance", "alg_bytes_per_launch": alg,
+                     "kernel": "k_adv_m", "alg_bytes_per_launch": alg,
                      "kernel_ms_per_launch": adv_s * 1e3},
         "stages_ms_per_step": {"group": dst["group_ns"] / 1e6 / args.steps,
                                "advance": dst["advance_ns"] / 1e6 / args.steps,
@@ -165,11 +235,27 @@ def main():
         "work_per_step": {k: dst[k] / args.steps for k in ("matches", "partials_created", "partials_scanned",
                                                            "keys_touched", "live_at_batch_start")},
     }
+    eng.close()
+    del batches
+    torch.cuda.empty_cache()
+    if rank == 0 and world == 1 and not args.no_extra:
+        steps = max(3, args.steps // 4)
+        cb, c4b = 1 << 22, 1 << 20
+        out["other_configs"] = {
+            "C3": dict(run_general(sa, synth, torch, dev, synth.C3_QUERY,
+                                   lambda s: synth.stock_ticks(s * cb, cb, K), K, cb, steps, 1, 8),
+                       workload="C3: every e1=S[price>20]<2:5>, e2=S[price>e1[last].price] or e3=S[volume>1000] "
+                                "within 10 sec (SEQUENCE), 1,048,576 keys"),
+            "C4": dict(run_general(sa, synth, torch, dev, synth.C4_QUERY,
+                                   lambda s: synth.burst_ticks(s * (c4b // 64), c4b // 64, 4096, 64), 4096, c4b,
+                                   steps, 1, 1024, playback=True),
+                       workload="C4: every e1=S[price>20] -> not S[price>e1.price] for 30 sec within 60 sec, "
+                                "@app:playback, 4,096 keys, one key per ms in bursts of 64 events"),
+        }
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(sa, synth, K, B, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    eng.close()
     if dist:
         dist.destroy_process_group()
 

@@ -316,7 +316,7 @@ GenProgram* gen_build_program(const uint32_t* w, size_t nw, uint32_t partialCap)
             if (G->pre[x].absent && G->pre[x].kind == GK_LOGICAL) mc = std::max<uint32_t>(mc, 2u);
         G->MC = std::min<uint32_t>(mc, 64u);  // output chain capacity (longer chains fail loudly)
         G->L = std::max<uint32_t>(4, partialCap);
-        G->Q = G->L + 8;
+        G->Q = 4 * G->L + 16;  // timer queues: one entry per notifyAt until it falls due
         G->STCAP = std::min<uint32_t>(2 * G->L + 16, 0xfff0u);
         G->SECAP = std::min<uint32_t>(G->STCAP * std::min<uint32_t>((uint32_t)G->nslots * mc, 8u), 0xfff0u);
         G->NA = maxAttr;

@@ -36,6 +36,33 @@ select e1.symbol as symbol, e1.price as price1, e2.price as price2, e2.price - e
 insert into OutputStream;
 """
 
+# BASELINE configs[2] (C3): strict sequence with counting plus logical or (SiddhiQL counting syntax <m:n>)
+C3_QUERY = """
+define stream StockStream (symbol string, price float, volume int);
+partition with (symbol of StockStream)
+begin
+  @info(name = 'query1')
+  from every e1=StockStream[price > 20]<2:5>, e2=StockStream[price > e1[last].price] or e3=StockStream[volume > 1000]
+       within 10 sec
+  select e1[0].price as p0, e1[last].price as plast, e2.price as p2, e3.volume as v3
+  insert into OutputStream;
+end;
+"""
+
+# BASELINE configs[3] (C4): absent state with a long within, playback clock (SURVEY §8d)
+C4_QUERY = """
+@app:playback
+define stream StockStream (symbol string, price float, volume int);
+partition with (symbol of StockStream)
+begin
+  @info(name = 'query1')
+  from every e1=StockStream[price > 20] -> not StockStream[price > e1.price] for 30 sec
+       within 60 sec
+  select e1.symbol as symbol, e1.price as price
+  insert into OutputStream;
+end;
+"""
+
 T0 = 1_700_000_000_000
 SEED = 0x5EED5EED
 
@@ -67,4 +94,24 @@ def stock_ticks(start: int, n: int, n_keys: int, seed: int = SEED, rate_per_ms: 
     price = (10.0 + 30.0 * u).astype(np.float32)
     volume = (np.uint64(1) + h2 % np.uint64(2000)).astype(np.int32)
     ts = (np.int64(t0) + (i // np.uint64(rate_per_ms)).astype(np.int64)).astype(np.int64)
+    return {"key": key, "ts": ts, "symbol": key.copy(), "price": price, "volume": volume}
+
+
+def burst_ticks(start_ms: int, n_ms: int, n_keys: int, burst: int, seed: int = SEED, t0: int = T0):
+    """C4 input: millisecond t carries `burst` events of ONE key (key = h(t) % n_keys), timestamp
+    t0 + t.  Timer due times of different keys then never coincide, which keeps the reference's
+    Scheduler collapse quirk out of the input.  Stateless per event index."""
+    t = np.repeat(np.arange(start_ms, start_ms + n_ms, dtype=np.uint64), burst)
+    i = np.arange(start_ms * burst, (start_ms + n_ms) * burst, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        base = np.uint64(seed) * np.uint64(0x100000001B3) if seed else np.uint64(0)
+        hk = splitmix64(t * np.uint64(7) + base)
+        s = i * np.uint64(3) + base + np.uint64(0x51)
+        h1 = splitmix64(s + np.uint64(1))
+        h2 = splitmix64(s + np.uint64(2))
+    key = (hk % np.uint64(n_keys)).astype(np.uint32)
+    u = (h1 >> np.uint64(40)).astype(np.float64) / float(1 << 24)
+    price = (10.0 + 30.0 * u).astype(np.float32)
+    volume = (np.uint64(1) + h2 % np.uint64(2000)).astype(np.int32)
+    ts = (np.int64(t0) + t.astype(np.int64)).astype(np.int64)
     return {"key": key, "ts": ts, "symbol": key.copy(), "price": price, "volume": volume}
