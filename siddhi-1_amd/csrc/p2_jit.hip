@@ -352,11 +352,28 @@ __device__ __forceinline__ void glb_emit(const Slab& g, KeySt& s, const Ev& ev, 
 }
 
 // ---- the kernel ---------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t wave_min_u(uint32_t x) {
+    for (int off = 32; off > 0; off >>= 1) x = min(x, (uint32_t)__shfl_xor((int)x, off, SGD_WAVE));
+    return x;
+}
+__device__ __forceinline__ uint32_t wave_max_u(uint32_t x) {
+    for (int off = 32; off > 0; off >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, off, SGD_WAVE));
+    return x;
+}
+
 template <bool S0, bool S1>
 __device__ __forceinline__ void advance(const P2Params& p) {
     typedef typename SgSel<S0, SgEv0, SgEv1>::type Ev;
     constexpr int STRIDE = S0 ? SGQ_STRIDE0 : SGQ_STRIDE1;
+    // The 64 keys of a wave are consecutive, so their runs of the key-sorted payload form ONE
+    // contiguous range: the wave copies it into LDS with coalesced 16-B loads and the lanes then walk
+    // their own runs out of LDS (a lane-private walk through HBM touches every line 8x, once per
+    // iteration, and thrashes L2 at full occupancy).
+    constexpr uint32_t WPB = SGD_BLOCK / SGD_WAVE;
+    constexpr uint32_t CAPW = SGD_STAGE_BYTES / WPB / (STRIDE * 4);
+    __shared__ PayEl<STRIDE> stage[WPB][CAPW];
     const int lane = threadIdx.x & (SGD_WAVE - 1);
+    const uint32_t wv = threadIdx.x / SGD_WAVE;
     const uint32_t k = blockIdx.x * SGD_BLOCK + threadIdx.x;
     const uint32_t K = p.n_keys;
     uint32_t b = 0, e = 0, h = 0;
@@ -366,6 +383,13 @@ __device__ __forceinline__ void advance(const P2Params& p) {
     }
     const int nev = (int)(e - b);
     const int iters = wave_max(nev);
+    const uint32_t rlo = wave_min_u(nev > 0 ? b : 0xffffffffu);
+    const uint32_t rhi = wave_max_u(nev > 0 ? e : 0u);
+    const bool staged = iters > 0 && rhi - rlo <= CAPW;
+    if (staged) {
+        for (uint32_t i = (uint32_t)lane; i < rhi - rlo; i += SGD_WAVE) stage[wv][i] = load_pay<STRIDE>(p.payload, rlo + i);
+    }
+    __syncthreads();
     if (iters == 0) return;  // no key of this wave has an event in the batch (wave-uniform)
     if (nev > 0) h = p.hdr[k];
 
@@ -399,11 +423,12 @@ __device__ __forceinline__ void advance(const P2Params& p) {
     unsigned long long chunk_base = 0;  // this wave's reserved slots of the raw match buffer
     uint32_t chunk_left = 0;
     PayEl<STRIDE> cur, nxt;
-    if (nev > 0) cur = load_pay<STRIDE>(p.payload, b);
+    if (nev > 0) cur = staged ? stage[wv][b - rlo] : load_pay<STRIDE>(p.payload, b);
 
     for (int it = 0; it < iters; ++it) {
         const bool act = it < nev;
-        if (it + 1 < nev) nxt = load_pay<STRIDE>(p.payload, b + (uint32_t)it + 1);  // next event in flight
+        if (it + 1 < nev)  // next event in flight
+            nxt = staged ? stage[wv][b - rlo + (uint32_t)it + 1] : load_pay<STRIDE>(p.payload, b + (uint32_t)it + 1);
         Ev ev;
         int64_t ts = 0;
         uint32_t bi = 0;

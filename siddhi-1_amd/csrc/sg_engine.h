@@ -13,7 +13,8 @@
 #define SGD_MAX_CONST 32   // filter constants (kernel arguments, so equal-shaped queries share code)
 #define SGD_MAX_REG 16     // register window (partials per lane) upper bound
 #define SGD_WAVE 64
-#define SGD_BLOCK 256      // lanes (= keys) per workgroup of the advance kernel
+#define SGD_BLOCK 128      // lanes (= keys) per workgroup of the advance kernel
+#define SGD_STAGE_BYTES 49152  // LDS per workgroup staging the waves' payload runs
 #define SGD_RAW_CHUNK 256  // raw match slots a wave reserves at a time (the raw buffer has this much slack per wave)
 
 // ---- filters ------------------------------------------------------------------------------------
