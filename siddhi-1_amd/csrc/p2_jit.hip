@@ -109,6 +109,7 @@ __device__ __forceinline__ int64_t sg_i64(uint32_t lo, uint32_t hi) {
 }
 
 template <bool C, class A, class B> struct SgSel { typedef A type; };
+template <bool B> struct SgBool { static constexpr bool value = B; };
 template <class A, class B> struct SgSel<false, A, B> { typedef B type; };
 
 // the query: SGQ_* constants, SgEv0/SgEv1 + sgq_ev0/1 (payload decode), sgq_f0, sgq_f1,
@@ -117,7 +118,22 @@ template <class A, class B> struct SgSel<false, A, B> { typedef B type; };
 
 #define R SGQ_R
 
+// ablation knobs for tools/exp_c2.py (SG_JIT_EXTRA); 0 in every shipped configuration
+#ifndef SGX_NO_RAW
+#define SGX_NO_RAW 0
+#endif
+#ifndef SGX_NO_TDESC
+#define SGX_NO_TDESC 0
+#endif
+#ifndef SGX_NO_LOOP
+#define SGX_NO_LOOP 0
+#endif
+
 namespace {
+
+// a wave-uniform value moved to an SGPR: branches on it are scalar (s_cbranch_scc), so the two
+// sides of an if/else are disjoint paths for the compiler (no exec-masked sequencing of both)
+__device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 
 __device__ __forceinline__ int wave_max(int x) {
     for (int off = 32; off > 0; off >>= 1) x = max(x, __shfl_xor(x, off, SGD_WAVE));
@@ -127,18 +143,35 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long x) {
     for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, SGD_WAVE);
     return x;
 }
-// inclusive prefix sum over the wave (all 64 lanes must be active)
+// inclusive prefix sum over the wave (all 64 lanes must be active), in DPP lane moves (VALU only,
+// no LDS round trip): shifts within each 16-lane row, then row_bcast:15 / row_bcast:31
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, int lane) {
-    for (int off = 1; off < SGD_WAVE; off <<= 1) {
-        const uint32_t y = __shfl_up(x, off, SGD_WAVE);
-        if (lane >= off) x += y;
-    }
+    const int r = lane & 15;
+    uint32_t t;
+    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+    if (r >= 1) x += t;
+    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+    if (r >= 2) x += t;
+    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    if (r >= 4) x += t;
+    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    if (r >= 8) x += t;
+    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    if (lane & 16) x += t;
+    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    if (lane >= 32) x += t;
     return x;
 }
 
 template <int S> struct PayEl { uint32_t w[S]; };
 typedef uint32_t sg_u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t sg_u32x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(1))) void* sg_glb_ptr;
+typedef __attribute__((address_space(3))) void* sg_lds_ptr;
+
+// per-workgroup staging of the payload runs: SGD_BLOCK / 64 wave regions of p.stage_chunks 16-B
+// chunks each (dynamic LDS, sized by the host from the batch density)
+extern __shared__ sg_u32x4 sg_stage[];
 
 template <int S> __device__ __forceinline__ PayEl<S> load_pay(const uint32_t* __restrict__ base, uint32_t i) {
     PayEl<S> x;
@@ -154,6 +187,28 @@ template <int S> __device__ __forceinline__ PayEl<S> load_pay(const uint32_t* __
 #pragma unroll
         for (int q = 0; q < S / 2; ++q) {
             const sg_u32x2 v = __builtin_nontemporal_load(s + q);
+            x.w[2 * q] = v.x; x.w[2 * q + 1] = v.y;
+        }
+    }
+    return x;
+}
+
+// element i of a wave's payload run staged in LDS (base = element 0; 16-B aligned when the element
+// size is a multiple of 16 B, 8-B aligned otherwise)
+template <int S> __device__ __forceinline__ PayEl<S> lds_pay(const uint32_t* base, uint32_t i) {
+    PayEl<S> x;
+    if constexpr (S % 4 == 0) {
+        const sg_u32x4* s = (const sg_u32x4*)(base + (size_t)i * S);
+#pragma unroll
+        for (int q = 0; q < S / 4; ++q) {
+            const sg_u32x4 v = s[q];
+            x.w[4 * q] = v.x; x.w[4 * q + 1] = v.y; x.w[4 * q + 2] = v.z; x.w[4 * q + 3] = v.w;
+        }
+    } else {
+        const sg_u32x2* s = (const sg_u32x2*)(base + (size_t)i * S);
+#pragma unroll
+        for (int q = 0; q < S / 2; ++q) {
+            const sg_u32x2 v = s[q];
             x.w[2 * q] = v.x; x.w[2 * q + 1] = v.y;
         }
     }
@@ -197,6 +252,8 @@ struct Win {
     uint32_t live;  // slot holds a partial
     uint32_t stg;   // subset of live: staged (pre1's newAndEvery list), all above the pending slots
     uint32_t tail;  // appends go here (one past the highest live slot)
+    int64_t slast;  // ts of the last staged append
+    bool sbad;      // the staged slots may be out of ts order (promotion sorts them)
 
     __device__ __forceinline__ void copy_slot(int d, int s) {
         ts[d] = ts[s];
@@ -361,74 +418,161 @@ __device__ __forceinline__ uint32_t wave_max_u(uint32_t x) {
     return x;
 }
 
-template <bool S0, bool S1>
+// STG: the staged pass.  Every wave whose payload range fits its LDS region walks it there with the
+// keys' partials in the register window only; a key whose window could overflow at its next event
+// stops before that event and is resumed from there by the HBM pass (p.resume), and a wave whose
+// range does not fit is left whole to the HBM pass (p.deferred).  !STG: the HBM pass over those
+// waves and keys (payload read from HBM, register window spilling to the slab when full).  Two
+// kernels, so the staged walk carries no global load and no vmcnt wait behind the match stores.
+template <bool S0, bool S1, bool STG>
 __device__ __forceinline__ void advance(const P2Params& p) {
     typedef typename SgSel<S0, SgEv0, SgEv1>::type Ev;
     constexpr int STRIDE = S0 ? SGQ_STRIDE0 : SGQ_STRIDE1;
-    // The 64 keys of a wave are consecutive, so their runs of the key-sorted payload form ONE
-    // contiguous range: the wave copies it into LDS with coalesced 16-B loads and the lanes then walk
-    // their own runs out of LDS (a lane-private walk through HBM touches every line 8x, once per
-    // iteration, and thrashes L2 at full occupancy).
-    constexpr uint32_t WPB = SGD_BLOCK / SGD_WAVE;
-    constexpr uint32_t CAPW = SGD_STAGE_BYTES / WPB / (STRIDE * 4);
-    __shared__ PayEl<STRIDE> stage[WPB][CAPW];
+    constexpr uint32_t SB = STRIDE * 4;  // bytes per payload element
     const int lane = threadIdx.x & (SGD_WAVE - 1);
     const uint32_t wv = threadIdx.x / SGD_WAVE;
     const uint32_t k = blockIdx.x * SGD_BLOCK + threadIdx.x;
     const uint32_t K = p.n_keys;
-    uint32_t b = 0, e = 0, h = 0;
+    // round trip 1: the key's segment of the sorted batch and its header (independent loads)
+    const uint32_t wave_id = (blockIdx.x * SGD_BLOCK + threadIdx.x) / SGD_WAVE;
+    uint32_t b = 0, e = 0, h = 0, dfr = 0, rsm = SGD_NO_RESUME;
     if (k < K) {
         b = p.seg_begin[k];
         e = p.seg_end[k];
+        h = p.hdr[k];
+    }
+    bool count_key = true;  // this pass owns the key's keys_touched / live_at_batch_start counts
+    if constexpr (!STG) {
+        dfr = uni(p.deferred[wave_id]);  // 1: the whole wave; 2: the keys with a resume point
+        if (dfr == 0u) return;
+        if (dfr != 1u) {
+            count_key = false;
+            if (k < K) rsm = p.resume[k];
+            if (rsm != SGD_NO_RESUME) {
+                b += rsm;
+                p.resume[k] = SGD_NO_RESUME;
+            } else {
+                e = b;
+            }
+        }
     }
     const int nev = (int)(e - b);
-    const int iters = wave_max(nev);
-    const uint32_t rlo = wave_min_u(nev > 0 ? b : 0xffffffffu);
-    const uint32_t rhi = wave_max_u(nev > 0 ? e : 0u);
-    const bool staged = iters > 0 && rhi - rlo <= CAPW;
-    if (staged) {
-        for (uint32_t i = (uint32_t)lane; i < rhi - rlo; i += SGD_WAVE) stage[wv][i] = load_pay<STRIDE>(p.payload, rlo + i);
+    if (nev <= 0) h = 0;
+    int iters = (int)uni((uint32_t)wave_max(nev));
+    // The 64 keys of a wave are consecutive, so their runs of the key-sorted payload form ONE
+    // contiguous byte range: the wave copies it into its LDS region with 16-B global_load_lds (all
+    // copies in flight at once, no VGPRs) and the lanes then walk their own runs out of LDS (a
+    // lane-private walk through HBM touches every line ~8x, once per iteration, and thrashes L2).
+    const uint32_t rlo = uni(wave_min_u(nev > 0 ? b : 0xffffffffu));
+    const uint32_t rhi = uni(wave_max_u(nev > 0 ? e : 0u));
+    const uint64_t c_lo = (uint64_t)rlo * SB / 16u, c_hi = ((uint64_t)rhi * SB + 15u) / 16u;
+    uint32_t dval = 0;  // this wave's p.deferred entry (written last: no store ahead of the loads)
+    if constexpr (STG) {
+        const bool fits = c_hi - c_lo <= (uint64_t)p.stage_chunks;
+        dval = (iters > 0 && !fits) ? 1u : 0u;
+        if (!fits) iters = 0;  // the HBM pass takes this wave
     }
-    __syncthreads();
-    if (iters == 0) return;  // no key of this wave has an event in the batch (wave-uniform)
-    if (nev > 0) h = p.hdr[k];
+    sg_u32x4* wst = sg_stage + (size_t)wv * p.stage_chunks;
+    const uint32_t* lds_run = (const uint32_t*)wst + ((uint64_t)rlo * SB - c_lo * 16u) / 4u;  // element rlo
 
+    // round trip 2: the partials of the register window, the raw-slot reservation and the LDS copy,
+    // all in flight together (nothing below reads a result before the barrier)
     KeySt s{SGD_H_SPEND(h), SGD_H_SSTG(h), SGD_H_NPEND(h), SGD_H_NSTG(h), 0, 0, 0};
     if (nev > 0 && !SGD_H_INIT(h)) s.sstg = 1;  // PartitionRuntimeImpl.initPartition -> init(): one seed
     const uint32_t n0 = s.gnp + s.gns;
-    const unsigned long long st_live0 = (nev > 0) ? (unsigned long long)n0 : 0ull;
+    const unsigned long long st_live0 = (nev > 0 && count_key) ? (unsigned long long)n0 : 0ull;
     const Slab G{p.p_ts + k, p.p_seq + k, p.p_capw + k, p.p_capnull + k, K, (size_t)p.cap * K};
     bool hbm = n0 > (uint32_t)R;
+    // events of the run this pass walks (the staged pass may stop a key early: resume point `rs`)
+    int run = nev;
+    uint32_t rs = SGD_NO_RESUME;
+    if (STG && hbm && nev > 0) {  // more live partials than the window holds: all of it to the HBM pass
+        rs = 0;
+        run = 0;
+        hbm = false;
+    }
     bool overflow = false;
     unsigned long long spills = 0;
     const int64_t within = p.within;
+    constexpr bool GLB = !STG;  // only the HBM pass has the slab (spill) mode
 
     Win W;
     W.live = 0; W.stg = 0; W.tail = 0;
 #pragma unroll
     for (int j = 0; j < R; ++j) {
-        const bool ld = nev > 0 && !hbm && (uint32_t)j < n0;
+        const bool ld = run > 0 && !hbm && (uint32_t)j < n0;
         W.ts[j] = ld ? G.TS(j) : 0;
         W.seq[j] = ld ? G.SEQ(j) : 0;
 #pragma unroll
         for (int w = 0; w < SGQ_NCAPW; ++w) W.cw[j][w] = ld ? G.CAP(w, j) : 0u;
         W.cn[j] = (SGQ_CAPNULL && ld) ? G.NUL(j) : 0u;
     }
-    if (nev > 0 && !hbm) {
+    if (run > 0 && !hbm) {
         W.live = (1u << n0) - 1u;
         W.stg = W.live & ~((1u << s.gnp) - 1u);
         W.tail = n0;
     }
+    // staged partials carried over from the previous batch may be out of ts order (sorted at promotion)
+    W.sbad = s.gns > 1;
+    W.slast = 0;
 
-    unsigned long long chunk_base = 0;  // this wave's reserved slots of the raw match buffer
+    // Raw match slots.  Without `every` around the whole pattern a key holds at most one start seed,
+    // so each event creates at most one partial and each partial is matched at most once: the wave
+    // emits at most sum(n0 + nev) matches in this batch and reserves that many slots here, with one
+    // atomic (no atomic, hence no vmcnt wait behind the match stores, inside the walk).  Under
+    // `every (e1 -> e2)` seeds multiply; the wave then reserves chunks as it goes, the next chunk
+    // prefetched (lane 0 keeps its base until the switch).
+    constexpr bool BOUNDED = !(SGQ_MODE & SGD_P2_EVERY_BOTH);
+    unsigned long long chunk_base = 0, next_l0 = 0;
     uint32_t chunk_left = 0;
-    PayEl<STRIDE> cur, nxt;
-    if (nev > 0) cur = staged ? stage[wv][b - rlo] : load_pay<STRIDE>(p.payload, b);
+    bool have_next = false;
+    if constexpr (S1) {
+        if constexpr (BOUNDED) {
+            const uint32_t bound = nev > 0 ? n0 + (S0 ? (uint32_t)nev : 0u) : 0u;
+            const uint32_t wb = (uint32_t)wave_sum((unsigned long long)bound);
+            if (lane == 0 && wb) next_l0 = atomicAdd(p.raw_count, (unsigned long long)wb);
+            chunk_left = wb;
+        } else {
+            have_next = iters > 0;
+            if (have_next && lane == 0) next_l0 = atomicAdd(p.raw_count, (unsigned long long)SGD_RAW_CHUNK);
+        }
+    }
+    if (STG && iters > 0) {
+        const uint32_t nch = (uint32_t)(c_hi - c_lo);
+        const sg_u32x4* src = (const sg_u32x4*)p.payload + c_lo;
+        for (uint32_t c = 0; c < nch; c += SGD_WAVE)
+            if (c + (uint32_t)lane < nch)
+                __builtin_amdgcn_global_load_lds((sg_glb_ptr)(src + c + lane), (sg_lds_ptr)(wst + c), 16, 0, 0);
+    }
+    if constexpr (STG) __syncthreads();  // the LDS copies have landed
+    if (iters == 0) {  // no key of this wave has an event here (wave-uniform), or the HBM pass has it
+        if (STG && lane == 0) p.deferred[wave_id] = dval;
+        return;
+    }
+    // every prologue load has landed: an explicit full wait here clears the compiler's scoreboard, so
+    // the walk below carries no vmcnt waits for the window registers (which would also drain the
+    // match stores of every earlier iteration)
+    __builtin_amdgcn_s_waitcnt(0);
+    if (S1 && BOUNDED) chunk_base = __shfl(next_l0, 0, SGD_WAVE);
 
-    for (int it = 0; it < iters; ++it) {
-        const bool act = it < nev;
-        if (it + 1 < nev)  // next event in flight
-            nxt = staged ? stage[wv][b - rlo + (uint32_t)it + 1] : load_pay<STRIDE>(p.payload, b + (uint32_t)it + 1);
+    PayEl<STRIDE> cur, nxt;
+    if (run > 0) cur = STG ? lds_pay<STRIDE>(lds_run, b - rlo) : load_pay<STRIDE>(p.payload, b);
+
+    for (int it = 0; it < (SGX_NO_LOOP ? 0 : iters); ++it) {
+        bool act = it < run;
+        if constexpr (STG) {
+            // the partials this event can add: every start seed fires at most once (+1: the
+            // withinEvery re-arm of `every (e1 -> e2)`); stop here if the window could overflow
+            if (act && __popc(W.live) + s.spend + s.sstg + ((SGQ_MODE & SGD_P2_EVERY_BOTH) ? 1u : 0u) > (uint32_t)R) {
+                rs = (uint32_t)it;
+                run = it;
+                act = false;
+                spills++;
+            }
+        }
+        if (it + 1 < run)  // next event in flight
+            nxt = STG ? lds_pay<STRIDE>(lds_run, b - rlo + (uint32_t)it + 1)
+                      : load_pay<STRIDE>(p.payload, b + (uint32_t)it + 1);
         Ev ev;
         int64_t ts = 0;
         uint32_t bi = 0;
@@ -437,11 +581,13 @@ __device__ __forceinline__ void advance(const P2Params& p) {
             ts = sg_i64(cur.w[STRIDE - 2], cur.w[STRIDE - 1]);
             if constexpr (S0) ev = sgq_ev0(cur.w); else ev = sgq_ev1(cur.w);
             // ---- stabilize (receiver.stabilizeStates) ----
-            if (!hbm) {
+            if (!GLB || !hbm) {
                 if (SGQ_WITHIN && W.live) {
                     uint32_t X = 0;
 #pragma unroll
-                    for (int j = 0; j < R; ++j) X |= (expired(W.ts[j], ts, within) ? 1u : 0u) << j;
+                    for (int j = 0; j < R; ++j) {
+                        X |= (expired(W.ts[j], ts, within) ? 1u : 0u) << j;
+                    }
                     X &= W.live;
                     if (X) {
                         const uint32_t P = W.live & ~W.stg;
@@ -462,19 +608,11 @@ __device__ __forceinline__ void advance(const P2Params& p) {
                 }
                 if (S0) { s.spend += s.sstg; s.sstg = 0; }
                 if (S1 && W.stg) {
-                    // promotion: staged partials join the pending list sorted by ts (stable)
-                    bool bad = false, have = false;
-                    int64_t prev = 0;
-#pragma unroll
-                    for (int j = 0; j < R; ++j) {
-                        if ((W.stg >> j) & 1u) {
-                            bad |= have && ts_before(W.ts[j], prev);
-                            prev = W.ts[j];
-                            have = true;
-                        }
-                    }
-                    if (bad) W.sort_staged();
+                    // promotion: staged partials join the pending list sorted by ts (stable); the
+                    // appends tracked whether they arrived out of ts order
+                    if (W.sbad) W.sort_staged();
                     W.stg = 0;
+                    W.sbad = false;
                 }
             } else {
                 glb_stabilize<S0, S1>(G, s, ts, within);
@@ -485,11 +623,12 @@ __device__ __forceinline__ void advance(const P2Params& p) {
         uint64_t gmask = 0;
         if constexpr (S1) {
             if (act) {
-                if (!hbm) {
+                if (!GLB || !hbm) {
                     const uint32_t P = W.live & ~W.stg;
 #pragma unroll
-                    for (int j = 0; j < R; ++j)
+                    for (int j = 0; j < R; ++j) {
                         if (((P >> j) & 1u) && sgq_f1(ev, W.cw[j], W.cn[j], p)) H |= 1u << j;
+                    }
                     c1 = __popc(H);
                     s.scanned += __popc(P);
                 } else {
@@ -501,28 +640,33 @@ __device__ __forceinline__ void advance(const P2Params& p) {
         // wave-wide reservation of the emitted matches (one atomic per wave chunk of slots)
         if constexpr (S1) {
         const uint32_t incl = wave_incl_scan(c1, lane);
-        const uint32_t total = __shfl(incl, SGD_WAVE - 1, SGD_WAVE);
+        const uint32_t total = __builtin_amdgcn_readlane(incl, SGD_WAVE - 1);
         if (total) {
-            if (total > chunk_left) {
-                const uint32_t want = max(total, (uint32_t)SGD_RAW_CHUNK);
-                unsigned long long nb = 0;
-                if (lane == 0) nb = atomicAdd(p.raw_count, (unsigned long long)want);
-                chunk_base = __shfl(nb, 0, SGD_WAVE);
-                chunk_left = want;
+            if (!BOUNDED && total > chunk_left) {
+                if (have_next && total <= (uint32_t)SGD_RAW_CHUNK) {  // switch to the prefetched chunk
+                    chunk_base = __shfl(next_l0, 0, SGD_WAVE);
+                    chunk_left = SGD_RAW_CHUNK;
+                    have_next = false;
+                } else {
+                    const uint32_t want = max(total, (uint32_t)SGD_RAW_CHUNK);
+                    unsigned long long nb = 0;
+                    if (lane == 0) nb = atomicAdd(p.raw_count, (unsigned long long)want);
+                    chunk_base = __shfl(nb, 0, SGD_WAVE);
+                    chunk_left = want;
+                }
             }
             if (c1) {
                 unsigned long long pos = chunk_base + incl - c1;
                 if (pos + c1 <= p.raw_capacity) {
-                    p.t_cnt[bi] = c1;
-                    p.t_first[bi] = (uint32_t)pos;
+                    if (!SGX_NO_TDESC) p.t_desc[bi] = ((uint64_t)c1 << 32) | (uint64_t)(uint32_t)pos;  // count | first slot
                 } else {
                     atomicOr(p.err, (uint32_t)SGD_ERR_MATCH_CAP);
                 }
-                if (!hbm) {
+                if (!GLB || !hbm) {
 #pragma unroll
                     for (int j = 0; j < R; ++j) {
                         if ((H >> j) & 1u) {
-                            if (pos < p.raw_capacity) p.raw_e1[pos] = W.seq[j];
+                            if (!SGX_NO_RAW && pos < p.raw_capacity) p.raw_e1[pos] = W.seq[j];
                             pos++;
                         }
                     }
@@ -536,6 +680,10 @@ __device__ __forceinline__ void advance(const P2Params& p) {
             }
             chunk_base += total;
             chunk_left -= total;
+            if (!BOUNDED && !have_next && chunk_left < (uint32_t)SGD_RAW_CHUNK / 2) {  // prefetch the next chunk
+                if (lane == 0) next_l0 = atomicAdd(p.raw_count, (unsigned long long)SGD_RAW_CHUNK);
+                have_next = true;
+            }
         }
         }
         // ---- state 0: the start-state seeds ----
@@ -550,8 +698,9 @@ __device__ __forceinline__ void advance(const P2Params& p) {
                     sgq_capture(ev, cw, cn);
                     const uint64_t seq = p.seq_base + bi;
                     for (uint32_t q = 0; q < s.spend; ++q) {
-                        if (!hbm && W.tail >= (uint32_t)R) W.compact();
-                        if (!hbm && W.tail >= (uint32_t)R) {
+                        if ((!GLB || !hbm) && W.tail >= (uint32_t)R) W.compact();
+                        if (!GLB && W.tail >= (uint32_t)R) { overflow = true; break; }  // excluded by the stop rule
+                        if (GLB && !hbm && W.tail >= (uint32_t)R) {
                             // the window is full of live partials: move the list to the HBM slab
 #pragma unroll
                             for (int j = 0; j < R; ++j) {
@@ -566,7 +715,7 @@ __device__ __forceinline__ void advance(const P2Params& p) {
                             hbm = true;
                             spills++;
                         }
-                        if (!hbm) {
+                        if (!GLB || !hbm) {
                             const uint32_t t = W.tail;
 #pragma unroll
                             for (int j = 0; j < R; ++j) {
@@ -578,6 +727,8 @@ __device__ __forceinline__ void advance(const P2Params& p) {
                                     if (SGQ_CAPNULL) W.cn[j] = cn;
                                 }
                             }
+                            if (W.stg && ts_before(ts, W.slast)) W.sbad = true;
+                            W.slast = ts;
                             W.live |= 1u << t;
                             W.stg |= 1u << t;
                             W.tail = t + 1;
@@ -600,9 +751,14 @@ __device__ __forceinline__ void advance(const P2Params& p) {
         }
         cur = nxt;
     }
-    if (nev > 0) {
+    if (STG && rs != SGD_NO_RESUME) p.resume[k] = rs;
+    if constexpr (STG) {
+        const unsigned long long anyr = __ballot(rs != SGD_NO_RESUME);
+        if (lane == 0) p.deferred[wave_id] = anyr ? 2u : 0u;
+    }
+    if (run > 0) {
         uint32_t np, ns;
-        if (!hbm) {
+        if (!GLB || !hbm) {
             W.compact();
             const uint32_t n = W.tail;
 #pragma unroll
@@ -627,7 +783,8 @@ __device__ __forceinline__ void advance(const P2Params& p) {
     if (overflow) atomicOr(p.err, (uint32_t)SGD_ERR_PARTIAL_CAP);
     // exact work counters (wave-reduced, one atomic per wave and counter)
     const unsigned long long v0 = wave_sum(s.scanned), v1 = wave_sum(s.created), v2 = wave_sum(s.matches);
-    const unsigned long long v3 = wave_sum(nev > 0 ? 1ull : 0ull), v4 = wave_sum(st_live0), v5 = wave_sum(spills);
+    const unsigned long long v3 = wave_sum((nev > 0 && count_key) ? 1ull : 0ull), v4 = wave_sum(st_live0),
+                             v5 = wave_sum(spills);
     if (lane == 0) {
         if (v0) atomicAdd(&p.stats[SGD_ST_SCANNED], v0);
         if (v1) atomicAdd(&p.stats[SGD_ST_CREATED], v1);
@@ -663,11 +820,15 @@ __device__ __forceinline__ void pack(const PackParams& q) {
 #define SGQ_WAVES 2
 #endif
 #define SGQ_OCC __attribute__((amdgpu_waves_per_eu(SGQ_WAVES, 8)))
+// k_adv_*: the staged pass; k_adv_*_h: the HBM pass over the waves the staged pass deferred
 #if SGQ_MULTI
-extern "C" __global__ void __launch_bounds__(SGD_BLOCK) SGQ_OCC k_adv_m(const P2Params p) { advance<true, true>(p); }
+extern "C" __global__ void __launch_bounds__(SGD_BLOCK) SGQ_OCC k_adv_m(const P2Params p) { advance<true, true, true>(p); }
+extern "C" __global__ void __launch_bounds__(SGD_BLOCK) SGQ_OCC k_adv_m_h(const P2Params p) { advance<true, true, false>(p); }
 #else
-extern "C" __global__ void __launch_bounds__(SGD_BLOCK) SGQ_OCC k_adv_s0(const P2Params p) { advance<true, false>(p); }
-extern "C" __global__ void __launch_bounds__(SGD_BLOCK) SGQ_OCC k_adv_s1(const P2Params p) { advance<false, true>(p); }
+extern "C" __global__ void __launch_bounds__(SGD_BLOCK) SGQ_OCC k_adv_s0(const P2Params p) { advance<true, false, true>(p); }
+extern "C" __global__ void __launch_bounds__(SGD_BLOCK) SGQ_OCC k_adv_s1(const P2Params p) { advance<false, true, true>(p); }
+extern "C" __global__ void __launch_bounds__(SGD_BLOCK) SGQ_OCC k_adv_s0_h(const P2Params p) { advance<true, false, false>(p); }
+extern "C" __global__ void __launch_bounds__(SGD_BLOCK) SGQ_OCC k_adv_s1_h(const P2Params p) { advance<false, true, false>(p); }
 #endif
 extern "C" __global__ void __launch_bounds__(256) k_pack0(const PackParams q) { pack<SGQ_STRIDE0, 0>(q); }
 extern "C" __global__ void __launch_bounds__(256) k_pack1(const PackParams q) { pack<SGQ_STRIDE1, 1>(q); }

@@ -24,20 +24,22 @@ __global__ void __launch_bounds__(256) k_seg_bounds(const uint32_t* __restrict__
 }
 
 // ------------------------------------------------------------------------------------------------
-// match ordering: batch event t's matches go to out_count + t_off[t] (t_off = exclusive scan of
-// t_cnt), i.e. ascending trigger seq, then emission order — the reference's callback order
-// (MultiProcessStreamReceiver.java:119-121).  Resets t_cnt for the next batch.
+// match ordering: batch event t's matches go to out_count + t_off[t] (t_off = exclusive scan of the
+// per-event counts), i.e. ascending trigger seq, then emission order — the reference's callback order
+// (MultiProcessStreamReceiver.java:119-121).  Resets t_desc for the next batch.  chain_len is the
+// constant 1/1 of a two-state match and was written once at allocation.
 // ------------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_scatter(const ScatterParams s) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= s.n) return;
-    const uint32_t c = s.t_cnt[t];
+    const uint64_t d = s.t_desc[t];
+    const uint32_t c = (uint32_t)(d >> 32);
     const uint64_t base = *s.out_count;
     if (t == s.n - 1) *s.batch_total = (unsigned long long)s.t_off[t] + c;
     if (c == 0) return;
-    s.t_cnt[t] = 0;
+    s.t_desc[t] = 0;
     const uint64_t o = base + s.t_off[t];
-    const uint32_t f = s.t_first[t];
+    const uint32_t f = (uint32_t)d;
     const uint64_t trig = s.seq_base + t;
     const uint32_t key = s.key ? s.key[t] : 0u;
     const int64_t ts = s.ts[t];
@@ -46,14 +48,12 @@ __global__ void __launch_bounds__(256) k_scatter(const ScatterParams s) {
         return;
     }
     for (uint32_t r = 0; r < c; ++r) {
-        const uint64_t d = o + r;
-        s.o_trig[d] = trig;
-        s.o_slot[2 * d] = s.raw_e1[f + r];
-        s.o_slot[2 * d + 1] = trig;
-        s.o_key[d] = key;
-        s.o_ts[d] = ts;  // StreamPostStateProcessor.java:68: StateEvent ts = ts of the e2 event
-        s.o_len[2 * d] = 1;
-        s.o_len[2 * d + 1] = 1;
+        const uint64_t q = o + r;
+        s.o_trig[q] = trig;
+        s.o_slot[2 * q] = s.raw_e1[f + r];
+        s.o_slot[2 * q + 1] = trig;
+        s.o_key[q] = key;
+        s.o_ts[q] = ts;  // StreamPostStateProcessor.java:68: StateEvent ts = ts of the e2 event
     }
 }
 

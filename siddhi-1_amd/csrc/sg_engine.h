@@ -14,8 +14,8 @@
 #define SGD_MAX_REG 16     // register window (partials per lane) upper bound
 #define SGD_WAVE 64
 #define SGD_BLOCK 128      // lanes (= keys) per workgroup of the advance kernel
-#define SGD_STAGE_BYTES 49152  // LDS per workgroup staging the waves' payload runs
-#define SGD_RAW_CHUNK 256  // raw match slots a wave reserves at a time (the raw buffer has this much slack per wave)
+#define SGD_STAGE_MAX_BYTES 65536  // LDS per workgroup staging the waves' payload runs (upper bound)
+#define SGD_RAW_CHUNK 256  // raw match slots a wave reserves at a time (the raw buffer has 2 chunks of slack per wave)
 
 // ---- filters ------------------------------------------------------------------------------------
 // A filter's IR bytecode (siddhi_gpu_ir.h) is lowered to DProg (variables resolved to event
@@ -52,6 +52,7 @@ enum {
 #define SGD_H_MAKE(np, ns, sp, ss, in) \
     ((uint32_t)(np) | ((uint32_t)(ns) << 12) | ((uint32_t)(sp) << 24) | ((uint32_t)(ss) << 26) | ((uint32_t)(in) << 28))
 #define SGD_MAX_CAP 4095u
+#define SGD_NO_RESUME 0xffffffffu
 
 enum { SGD_ST_SCANNED = 0, SGD_ST_CREATED, SGD_ST_MATCHES, SGD_ST_KEYS, SGD_ST_LIVE0, SGD_ST_SPILLS, SGD_ST_N };
 
@@ -81,10 +82,16 @@ struct P2Params {
     uint64_t* raw_e1;
     unsigned long long* raw_count;
     uint64_t raw_capacity;
-    uint32_t* t_cnt;                   // [max_batch], zero outside the advance -> scatter window
-    uint32_t* t_first;                 // [max_batch]
+    uint64_t* t_desc;                  // [max_batch] count << 32 | first raw slot; zero outside the
+                                       // advance -> scatter window
     unsigned long long* stats;         // [SGD_ST_N]
     uint32_t* err;
+    uint32_t* deferred;                // [n_keys / 64] waves the staged pass left to the HBM pass:
+                                       // 1 = the whole wave, 2 = the keys with a resume point
+    uint32_t* resume;                  // [n_keys] event index (in the key's run) where the HBM pass
+                                       // resumes a key the staged pass stopped; SGD_NO_RESUME otherwise
+    uint32_t stage_chunks;             // LDS staging per wave, 16-B chunks (dynamic LDS = waves x this)
+    uint32_t pad;
     uint64_t cst[SGD_MAX_CONST];       // filter constants, already in their comparison domain
 };
 
@@ -109,9 +116,8 @@ struct ScatterParams {
     uint64_t seq_base;
     const uint32_t* key;       // batch key ids (NULL: unpartitioned -> key 0)
     const int64_t* ts;
-    uint32_t* t_cnt;
-    const uint32_t* t_first;
-    const uint32_t* t_off;     // exclusive scan of t_cnt
+    uint64_t* t_desc;          // count << 32 | first raw slot per batch event (reset here)
+    const uint32_t* t_off;     // exclusive scan of the counts
     const uint64_t* raw_e1;
     unsigned long long* out_count;
     unsigned long long* batch_total;
@@ -120,7 +126,6 @@ struct ScatterParams {
     uint64_t* o_slot;          // [n][2]
     uint32_t* o_key;
     int64_t* o_ts;
-    uint32_t* o_len;           // [n][2]
-    uint32_t* err;
+    uint32_t* err;             // (o_len is constant 1/1 for two-state matches: filled at allocation)
 };
 int sgd_launch_scatter(const ScatterParams& s, ihipStream_t* stream);

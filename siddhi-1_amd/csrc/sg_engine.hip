@@ -22,6 +22,7 @@
 #include <rocprim/iterator/transform_iterator.hpp>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <map>
 #include <cstring>
@@ -140,12 +141,30 @@ template <int W> struct PackFn {
     }
 };
 
+// 16-B payloads (one filter column): onesweep with 10-bit digits, so 2^11..2^20 keys sort in two
+// passes over the data instead of three (rocPRIM's gfx950 default for this pair size is 8 bits)
+using Pay16Config = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 6>, rocprim::kernel_config<1024, 6>, 10,
+                                        rocprim::block_radix_rank_algorithm::match>>;
+
 template <int W>
 hipError_t sort_payload(void* tmp, size_t& tmp_bytes, const uint32_t* keys, uint32_t* skeys, const PackSrc& src,
                         void* out, uint32_t n, uint32_t bits, hipStream_t stream) {
     auto it = rocprim::make_transform_iterator(rocprim::counting_iterator<uint32_t>(0), PackFn<W>{src});
+    if constexpr (W == 1) {
+        if (bits > 16 && bits <= 20)
+            return rocprim::radix_sort_pairs<Pay16Config>(tmp, tmp_bytes, keys, skeys, it, (Pay<W>*)out, n, 0u, bits,
+                                                           stream);
+    }
     return rocprim::radix_sort_pairs(tmp, tmp_bytes, keys, skeys, it, (Pay<W>*)out, n, 0u, bits, stream);
 }
+
+// the match count of a per-event descriptor (count << 32 | first raw slot)
+struct DescCount {
+    __host__ __device__ uint32_t operator()(uint64_t d) const { return (uint32_t)(d >> 32); }
+};
+inline auto desc_counts(const uint64_t* d) { return rocprim::make_transform_iterator(d, DescCount{}); }
 
 hipError_t sort_payload_w(int W, void* tmp, size_t& tmp_bytes, const uint32_t* keys, uint32_t* skeys,
                           const PackSrc& src, void* out, uint32_t n, uint32_t bits, hipStream_t stream) {
@@ -184,6 +203,7 @@ struct sg_engine {
     struct Variant {
         hipModule_t mod = nullptr;
         hipFunction_t adv[2] = {nullptr, nullptr};   // [0]: multi / state-0 stream, [1]: state-1 stream
+        hipFunction_t adv_h[2] = {nullptr, nullptr}; // the HBM pass over the waves the staged pass deferred
         hipFunction_t pack[2] = {nullptr, nullptr};
     };
     JitQuery jq;
@@ -206,8 +226,9 @@ struct sg_engine {
     // matches
     uint64_t* raw_e1 = nullptr;
     unsigned long long* raw_count = nullptr;
-    uint32_t* t_cnt = nullptr;
-    uint32_t* t_first = nullptr;
+    uint64_t* t_desc = nullptr;    // per batch event: match count << 32 | first raw slot
+    uint32_t* deferred = nullptr;  // per advance wave: left by the staged pass to the HBM pass
+    uint32_t* resume = nullptr;    // per key: where the HBM pass resumes a key the staged pass stopped
     uint32_t* t_off = nullptr;
     unsigned long long* out_count = nullptr;
     unsigned long long* batch_total = nullptr;
@@ -235,7 +256,8 @@ struct sg_engine {
     std::vector<Span> spans;
     std::vector<hipEvent_t> free_events;
     bool timing = false;
-    uint32_t reg_slots = 8;  // SGD_REG_SLOTS: partials per key held in registers by the advance kernel
+    uint32_t reg_slots = 12;  // SGD_REG_SLOTS: partials per key held in registers by the advance kernel
+    uint32_t stage_override = 0;  // SGD_STAGE_CHUNKS: fixed LDS staging per wave (tests force the HBM path)
     uint64_t spills = 0;
 
     hipEvent_t ev() {
@@ -485,8 +507,10 @@ void allocate(sg_engine* e) {
     for (int W = 1; W <= 4; ++W) {
         size_t tb = 0;
         PackSrc ps{};
-        HIP_OK(sort_payload_w(W, nullptr, tb, e->b_key, e->skeys, ps, nullptr, (uint32_t)B, 32, e->stream));
-        e->sort_tmp_bytes = std::max(e->sort_tmp_bytes, tb);
+        for (uint32_t bits : {20u, 32u}) {
+            HIP_OK(sort_payload_w(W, nullptr, tb, e->b_key, e->skeys, ps, nullptr, (uint32_t)B, bits, e->stream));
+            e->sort_tmp_bytes = std::max(e->sort_tmp_bytes, tb);
+        }
     }
     e->sort_tmp = dalloc<uint8_t>(e->sort_tmp_bytes, o);
     {
@@ -497,23 +521,28 @@ void allocate(sg_engine* e) {
             maxw = std::max(maxw, sgj_stride(sgj_col_words(ty) + 1));
         }
         e->pay_words = maxw;
-        e->pay = dalloc<uint32_t>((size_t)maxw * B, o);
+        e->pay = dalloc<uint32_t>((size_t)maxw * B + 4, o);  // + one 16-B chunk: the LDS copy rounds up
     }
-    e->raw_cap = M + ((size_t)(K + SGD_WAVE - 1) / SGD_WAVE) * SGD_RAW_CHUNK;
+    // raw match slots per batch: waves reserve at most sum(live partials + events) up front, or
+    // (every (e1 -> e2)) chunks of SGD_RAW_CHUNK with two chunks of slack per wave (p2_jit.hip)
+    e->raw_cap = std::max<uint64_t>(2 * (B + (uint64_t)K * C),
+                                    M + ((size_t)(K + SGD_WAVE - 1) / SGD_WAVE) * 2 * SGD_RAW_CHUNK);
     e->raw_e1 = dalloc<uint64_t>(e->raw_cap, o);
     e->raw_count = dalloc<unsigned long long>(1, o);
-    e->t_cnt = dalloc<uint32_t>(B, o);
-    e->t_first = dalloc<uint32_t>(B, o);
+    e->t_desc = dalloc<uint64_t>(B, o);
+    e->deferred = dalloc<uint32_t>((K + SGD_BLOCK - 1) / SGD_BLOCK * (SGD_BLOCK / SGD_WAVE), o);
+    e->resume = dalloc<uint32_t>(K, o);
+    HIP_OK(hipMemset(e->resume, 0xff, K * 4));  // SGD_NO_RESUME
     e->t_off = dalloc<uint32_t>(B, o);
     e->out_count = dalloc<unsigned long long>(1, o);
     e->batch_total = dalloc<unsigned long long>(1, o);
     e->stats = dalloc<unsigned long long>(SGD_ST_N, o);
     e->err = dalloc<uint32_t>(1, o);
-    HIP_OK(hipMemset(e->t_cnt, 0, B * 4));
+    HIP_OK(hipMemset(e->t_desc, 0, B * 8));
     HIP_OK(hipMemset(e->out_count, 0, 8));
     HIP_OK(hipMemset(e->stats, 0, SGD_ST_N * 8));
     HIP_OK(hipMemset(e->err, 0, 4));
-    HIP_OK(rocprim::exclusive_scan(nullptr, e->scan_tmp_bytes, e->t_cnt, e->t_off, 0u, (uint32_t)B,
+    HIP_OK(rocprim::exclusive_scan(nullptr, e->scan_tmp_bytes, desc_counts(e->t_desc), e->t_off, 0u, (uint32_t)B,
                                    rocprim::plus<uint32_t>(), e->stream));
     e->scan_tmp = dalloc<uint8_t>(e->scan_tmp_bytes, o);
     e->o_trig = dalloc<uint64_t>(M, o);
@@ -521,6 +550,7 @@ void allocate(sg_engine* e) {
     e->o_key = dalloc<uint32_t>(M, o);
     e->o_ts = dalloc<int64_t>(M, o);
     e->o_len = dalloc<uint32_t>(2 * M, o);
+    HIP_OK(hipMemsetD32((hipDeviceptr_t)e->o_len, 1, 2 * M));  // every two-state match: chain lengths 1, 1
     HIP_OK(hipDeviceSynchronize());
 }
 
@@ -561,19 +591,36 @@ sg_engine::Variant& variant(sg_engine* e, bool evnull, bool capnull) {
     sg_engine::Variant& r = e->variants[key];
     if (q.multi) {
         HIP_OK(hipModuleGetFunction(&r.adv[0], r.mod, "k_adv_m"));
+        HIP_OK(hipModuleGetFunction(&r.adv_h[0], r.mod, "k_adv_m_h"));
         r.adv[1] = r.adv[0];
+        r.adv_h[1] = r.adv_h[0];
     } else {
         HIP_OK(hipModuleGetFunction(&r.adv[0], r.mod, "k_adv_s0"));
         HIP_OK(hipModuleGetFunction(&r.adv[1], r.mod, "k_adv_s1"));
+        HIP_OK(hipModuleGetFunction(&r.adv_h[0], r.mod, "k_adv_s0_h"));
+        HIP_OK(hipModuleGetFunction(&r.adv_h[1], r.mod, "k_adv_s1_h"));
     }
     HIP_OK(hipModuleGetFunction(&r.pack[0], r.mod, "k_pack0"));
     HIP_OK(hipModuleGetFunction(&r.pack[1], r.mod, "k_pack1"));
     return r;
 }
 
-void launch(hipFunction_t f, uint32_t blocks, uint32_t threads, void* arg, hipStream_t stream) {
+void launch(hipFunction_t f, uint32_t blocks, uint32_t threads, void* arg, hipStream_t stream, uint32_t lds = 0) {
     void* args[] = {arg};
-    HIP_OK(hipModuleLaunchKernel(f, blocks, 1, 1, threads, 1, 1, 0, stream, args, nullptr));
+    HIP_OK(hipModuleLaunchKernel(f, blocks, 1, 1, threads, 1, 1, lds, stream, args, nullptr));
+}
+
+// LDS staging per advance-kernel wave, in 16-B chunks: the payload bytes of the wave's 64 keys at
+// this batch's density (n / K events per key) plus 4 standard deviations of a Poisson count, so that
+// practically every wave of a uniform key stream is staged (the rest read HBM directly, exactly);
+// a smaller region means more resident waves per CU (160 KB LDS).
+uint32_t stage_chunks_for(uint64_t n, uint64_t K, uint32_t stride_words) {
+    const uint32_t wpb = SGD_BLOCK / SGD_WAVE;
+    const double mean = (double)n * SGD_WAVE / (double)(K ? K : 1);
+    const double want = mean + 4.0 * std::sqrt(mean) + 32.0;
+    const double chunks = std::ceil(want * stride_words * 4.0 / 16.0) + 1.0;
+    const double hi = (double)SGD_STAGE_MAX_BYTES / wpb / 16.0;
+    return (uint32_t)std::max(64.0, std::min(chunks, hi));
 }
 
 int push(sg_engine* e, const sg_batch* b) {
@@ -709,15 +756,21 @@ int push(sg_engine* e, const sg_batch* b) {
     p.raw_e1 = e->raw_e1;
     p.raw_count = e->raw_count;
     p.raw_capacity = e->raw_cap;
-    p.t_cnt = e->t_cnt;
-    p.t_first = e->t_first;
+    p.t_desc = e->t_desc;
+    p.deferred = e->deferred;
+    p.resume = e->resume;
     p.stats = e->stats;
     p.err = e->err;
     for (size_t i = 0; i < e->consts.size(); i++) p.cst[i] = e->consts[i];
     HIP_OK(hipMemsetAsync(e->raw_count, 0, 8, e->stream));
     hipEvent_t a0 = nullptr, a1 = nullptr;
     if (e->timing) { a0 = e->ev(); e->mark(a0); }
-    launch(v.adv[role], (e->K + SGD_BLOCK - 1) / SGD_BLOCK, SGD_BLOCK, &p, e->stream);
+    {
+        p.stage_chunks = e->stage_override ? e->stage_override : stage_chunks_for(n, e->K, stride);
+        const uint32_t blocks = (e->K + SGD_BLOCK - 1) / SGD_BLOCK;
+        launch(v.adv[role], blocks, SGD_BLOCK, &p, e->stream, p.stage_chunks * 16u * (SGD_BLOCK / SGD_WAVE));
+        launch(v.adv_h[role], blocks, SGD_BLOCK, &p, e->stream);
+    }
     if (e->timing) { a1 = e->ev(); e->mark(a1); e->spans.push_back({a0, a1, 1}); }
     e->st.advance_launches++;
     // order this batch's matches by trigger (exclusive scan of per-event counts + scatter)
@@ -725,15 +778,14 @@ int push(sg_engine* e, const sg_batch* b) {
     if (e->timing) { o0 = e->ev(); e->mark(o0); }
     {
         size_t tmp = e->scan_tmp_bytes;
-        HIP_OK(rocprim::exclusive_scan(e->scan_tmp, tmp, e->t_cnt, e->t_off, 0u, n, rocprim::plus<uint32_t>(),
-                                       e->stream));
+        HIP_OK(rocprim::exclusive_scan(e->scan_tmp, tmp, desc_counts(e->t_desc), e->t_off, 0u, n,
+                                       rocprim::plus<uint32_t>(), e->stream));
         ScatterParams sp{};
         sp.n = n;
         sp.seq_base = b->seq_base;
         sp.key = pl.partitioned ? (dev ? b->key : e->b_key) : nullptr;
         sp.ts = ts;
-        sp.t_cnt = e->t_cnt;
-        sp.t_first = e->t_first;
+        sp.t_desc = e->t_desc;
         sp.t_off = e->t_off;
         sp.raw_e1 = e->raw_e1;
         sp.out_count = e->out_count;
@@ -743,7 +795,6 @@ int push(sg_engine* e, const sg_batch* b) {
         sp.o_slot = e->o_slot;
         sp.o_key = e->o_key;
         sp.o_ts = e->o_ts;
-        sp.o_len = e->o_len;
         sp.err = e->err;
         if (sgd_launch_scatter(sp, e->stream) != 0) throw HipError("k_scatter launch failed");
     }
@@ -822,6 +873,9 @@ int sg_engine_create(const void* ir, size_t ir_len, const sg_config* cfg, sg_eng
         e->timing = (cfg->flags & SG_CFG_TIMING) != 0;
         if (const char* d = getenv("SGD_REG_SLOTS")) e->reg_slots = (uint32_t)strtoul(d, nullptr, 0);
         if (e->reg_slots < 1 || e->reg_slots > SGD_MAX_REG) throw std::invalid_argument("SGD_REG_SLOTS out of [1, 16]");
+        if (const char* d = getenv("SGD_STAGE_CHUNKS")) e->stage_override = (uint32_t)strtoul(d, nullptr, 0);
+        if (e->stage_override * 16ull * (SGD_BLOCK / SGD_WAVE) > SGD_STAGE_MAX_BYTES)
+            throw std::invalid_argument("SGD_STAGE_CHUNKS above the LDS staging bound");
         e->K = cfg->n_keys ? cfg->n_keys : 1;
         e->cap = cfg->partial_capacity ? cfg->partial_capacity : 64;
         e->maxb = cfg->max_batch ? cfg->max_batch : (1u << 20);

@@ -274,7 +274,8 @@ uint64_t fnv1a(const void* d, size_t n, uint64_t h = 1469598103934665603ull) {
     return h;
 }
 
-const char* const kOpts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off"};
+const char* const kOpts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
+                             "-mllvm", "-amdgpu-atomic-optimizer-strategy=None"};
 
 std::string cache_dir() {
     if (const char* d = getenv("SG_JIT_CACHE")) return d;
@@ -334,6 +335,16 @@ std::string sgj_generate(const JitQuery& q, std::vector<uint64_t>& consts) {
     for (int s = 0; s < 2; s++)
         stride[s] = sgj_stride(sgj_col_words(q.coltypes[q.multi ? 0 : s]) + (q.evnull ? 1 : 0));
     o << "// generated by sg_jit.cpp: one two-state pattern query\n#pragma once\n";
+    // tuning experiments (tools/exp_c2.py): SG_JIT_EXTRA="NAME=VALUE,..." prepends #defines
+    if (const char* x = getenv("SG_JIT_EXTRA")) {
+        std::string defs(x), item;
+        std::istringstream ds(defs);
+        while (std::getline(ds, item, ',')) {
+            const size_t eq = item.find('=');
+            if (item.empty()) continue;
+            o << "#define " << (eq == std::string::npos ? item : item.substr(0, eq) + " " + item.substr(eq + 1)) << "\n";
+        }
+    }
     o << "#define SGQ_R " << q.reg_slots << "\n";
     o << "#define SGQ_MODE " << q.mode << "\n";
     o << "#define SGQ_MULTI " << (q.multi ? 1 : 0) << "\n";
@@ -374,6 +385,7 @@ bool sgj_compile(const std::string& qh, std::vector<char>& code, std::string& lo
     key += kJitEngineH;
     key += kJitIrH;
     for (const char* opt : kOpts) key += opt;
+    if (getenv("SG_JIT_ATOMIC_OPT")) key += "+atomicopt";
     std::lock_guard<std::mutex> lk(g_mu);
     auto it = g_cache.find(key);
     if (it != g_cache.end()) {
@@ -402,7 +414,9 @@ bool sgj_compile(const std::string& qh, std::vector<char>& code, std::string& lo
         log = "hiprtcCreateProgram failed";
         return false;
     }
-    const hiprtcResult rc = hiprtcCompileProgram(prog, (int)(sizeof(kOpts) / sizeof(kOpts[0])), kOpts);
+    std::vector<const char*> opts(kOpts, kOpts + sizeof(kOpts) / sizeof(kOpts[0]));
+    if (getenv("SG_JIT_ATOMIC_OPT")) opts.resize(opts.size() - 2);  // experiments: default atomic optimizer
+    const hiprtcResult rc = hiprtcCompileProgram(prog, (int)opts.size(), opts.data());
     size_t ls = 0;
     hiprtcGetProgramLogSize(prog, &ls);
     log.assign(ls, '\0');

@@ -17,7 +17,7 @@ struct JitQuery {
     int mode = 0;                         // SGD_P2_* bits
     bool multi = false;                   // both states read the same stream
     bool within = false;
-    uint32_t reg_slots = 8;               // SGQ_R
+    uint32_t reg_slots = 12;              // SGQ_R
     std::vector<uint32_t> coltypes[2];    // types of the filter columns of stream s0 / s1
     const DProg* f0 = nullptr;
     const DProg* f1 = nullptr;

@@ -111,11 +111,15 @@ def _push_both(gpu, ora, stream, seq_base, d, cols_names, ts=None):
         e.push(stream, seq_base, ts, cols, None, d["key"])
 
 
-@pytest.mark.parametrize("reg_slots", [8, 2])
+@pytest.mark.parametrize("reg_slots,stage", [(12, 0), (2, 0), (12, 64)])
 @pytest.mark.parametrize("shape", sorted(SHAPES))
-def test_gpu_random_streams_bit_exact(shape, reg_slots, monkeypatch):
-    """reg_slots=2: most keys outgrow the register window, so the HBM-slab path is exercised too"""
+def test_gpu_random_streams_bit_exact(shape, reg_slots, stage, monkeypatch):
+    """reg_slots=2: most keys outgrow the register window, so the HBM-slab path is exercised too;
+    stage=64: the LDS staging region is too small for any wave, so every lane reads its run of the
+    key-sorted batch from HBM directly"""
     monkeypatch.setenv("SGD_REG_SLOTS", str(reg_slots))
+    if stage:
+        monkeypatch.setenv("SGD_STAGE_CHUNKS", str(stage))
     n_keys, batch, nb = 2048, 40000, 4
     cq, gpu, ora = _engines(SHAPES[shape], n_keys, batch)
     seq = 0
@@ -139,7 +143,7 @@ def test_gpu_random_streams_bit_exact(shape, reg_slots, monkeypatch):
         assert sg["window_spills"] > 0
 
 
-@pytest.mark.parametrize("reg_slots", [8, 3])
+@pytest.mark.parametrize("reg_slots", [12, 3])
 def test_gpu_non_monotonic_timestamps(reg_slots, monkeypatch):
     """prefix-only expiry and the stable ts sort of staged partials (StreamPreStateProcessor.java:331-342)"""
     monkeypatch.setenv("SGD_REG_SLOTS", str(reg_slots))

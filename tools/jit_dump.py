@@ -30,7 +30,7 @@ def main():
     with open(os.path.join(out, "sgq_query.h"), "w") as f:
         f.write(sa.jit_check(cq.ir, flags))
     csrc = os.path.join(ROOT, "siddhi-1_amd", "csrc")
-    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
+    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-mllvm", "-amdgpu-atomic-optimizer-strategy=None",
            "--cuda-device-only", "-include", "hip/hip_runtime.h", "-c", "-I", out, "-I", csrc, "-I", os.path.join(ROOT, "include"),
            "-Rpass-analysis=kernel-resource-usage", "-save-temps=obj", "-o", os.path.join(out, "adv.o"),
            os.path.join(csrc, "p2_jit.hip")]
