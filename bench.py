@@ -205,7 +205,10 @@ def main():
     value = events_all / el
 
     launches = max(1, dst["advance_launches"])
-    adv_s = dst["advance_ns"] / 1e9 / launches
+    # the dominant kernel is the LDS-staged pass k_adv_m; the HBM pass (k_adv_m_h: waves whose payload
+    # range did not fit LDS, keys whose window could overflow) is timed separately and reported beside it
+    adv_s = (dst["advance_ns"] - dst["advance_hbm_ns"]) / 1e9 / launches
+    adv_h_s = dst["advance_hbm_ns"] / 1e9 / launches
     alg = algorithmic_bytes(dst) / launches
     achieved = alg / adv_s / 1e9 if adv_s > 0 else 0.0
     out = {
@@ -228,7 +231,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                      "kernel": "k_adv_m", "alg_bytes_per_launch": alg,
-                     "kernel_ms_per_launch": adv_s * 1e3},
+                     "kernel_ms_per_launch": adv_s * 1e3, "hbm_pass_ms_per_launch": adv_h_s * 1e3},
         "stages_ms_per_step": {"group": dst["group_ns"] / 1e6 / args.steps,
                                "advance": dst["advance_ns"] / 1e6 / args.steps,
                                "order": dst["order_ns"] / 1e6 / args.steps},
@@ -246,6 +249,10 @@ def main():
                                    lambda s: synth.stock_ticks(s * cb, cb, K), K, cb, steps, 1, 8),
                        workload="C3: every e1=S[price>20]<2:5>, e2=S[price>e1[last].price] or e3=S[volume>1000] "
                                 "within 10 sec (SEQUENCE), 1,048,576 keys"),
+            "C3_min1": dict(run_general(sa, synth, torch, dev, synth.C3_MIN1_QUERY,
+                                        lambda s: synth.stock_ticks(s * cb, cb, K), K, cb, steps, 1, 8),
+                            workload="C3 with e1<1:5> (C3 as written emits no match under the reference's "
+                                     "SEQUENCE reset semantics, DESIGN.md), 1,048,576 keys"),
             "C4": dict(run_general(sa, synth, torch, dev, synth.C4_QUERY,
                                    lambda s: synth.burst_ticks(s * (c4b // 64), c4b // 64, 4096, 64), 4096, c4b,
                                    steps, 1, 1024, playback=True),

@@ -117,6 +117,8 @@ typedef struct sg_stats {
     uint64_t order_ns;          /* SG_CFG_TIMING: device time of match ordering in polls */
     uint64_t advance_launches;  /* NFA advance kernel launches */
     uint64_t window_spills;     /* keys whose live partials outgrew the register window (moved to HBM) */
+    uint64_t advance_hbm_ns;    /* SG_CFG_TIMING: part of advance_ns spent in the HBM pass (waves and
+                                   keys the LDS-staged pass left to it) */
 } sg_stats;
 
 /* ir/ir_len: an IR blob (siddhi_gpu_ir.h) of one query */

@@ -276,6 +276,7 @@ struct sg_engine {
                 uint64_t ns = (uint64_t)((double)ms * 1e6);
                 if (s.stage == 0) st.group_ns += ns;
                 else if (s.stage == 1) st.advance_ns += ns;
+                else if (s.stage == 3) { st.advance_ns += ns; st.advance_hbm_ns += ns; }
                 else st.order_ns += ns;
             }
             free_events.push_back(s.a);
@@ -769,9 +770,10 @@ int push(sg_engine* e, const sg_batch* b) {
         p.stage_chunks = e->stage_override ? e->stage_override : stage_chunks_for(n, e->K, stride);
         const uint32_t blocks = (e->K + SGD_BLOCK - 1) / SGD_BLOCK;
         launch(v.adv[role], blocks, SGD_BLOCK, &p, e->stream, p.stage_chunks * 16u * (SGD_BLOCK / SGD_WAVE));
+        if (e->timing) { a1 = e->ev(); e->mark(a1); e->spans.push_back({a0, a1, 1}); a0 = e->ev(); e->mark(a0); }
         launch(v.adv_h[role], blocks, SGD_BLOCK, &p, e->stream);
+        if (e->timing) { a1 = e->ev(); e->mark(a1); e->spans.push_back({a0, a1, 3}); }
     }
-    if (e->timing) { a1 = e->ev(); e->mark(a1); e->spans.push_back({a0, a1, 1}); }
     e->st.advance_launches++;
     // order this batch's matches by trigger (exclusive scan of per-event counts + scatter)
     hipEvent_t o0 = nullptr, o1 = nullptr;

@@ -56,7 +56,7 @@ class sg_stats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in ("events", "batches", "partials_scanned", "partials_created",
                                           "partials_live", "matches", "keys_touched",
                                           "live_at_batch_start", "group_ns", "advance_ns", "order_ns",
-                                          "advance_launches", "window_spills")]
+                                          "advance_launches", "window_spills", "advance_hbm_ns")]
 
 
 @dataclass

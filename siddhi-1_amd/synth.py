@@ -49,6 +49,13 @@ begin
 end;
 """
 
+# C3 with <1:5>: under the reference's SEQUENCE semantics a start count state with min 2 is cleared by
+# StateStreamRuntime.resetAndUpdate (StateStreamRuntime.java:81-88 -> StreamPreStateProcessor.resetState,
+# StreamPreStateProcessor.java:288-305) before every event, and CountPostStateProcessor only re-adds the
+# partial once it holds min events (CountPostStateProcessor.java:39-66), so C3 as written never matches;
+# this variant is the same shape with matches, benchmarked beside it
+C3_MIN1_QUERY = C3_QUERY.replace("<2:5>", "<1:5>")
+
 # BASELINE configs[3] (C4): absent state with a long within, playback clock (SURVEY §8d)
 C4_QUERY = """
 @app:playback
