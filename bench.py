@@ -41,6 +41,20 @@ def algorithmic_bytes(st):
             + 16 * st["partials_created"] + 24 * st["matches"])
 
 
+def pmc_traffic():
+    """HBM bytes per launch of the advance kernel from the committed PMC summary (tools/pmc_summary.py),
+    only when it was measured on this exact kernel source; None otherwise."""
+    try:
+        import hashlib
+        t = json.load(open(os.path.join(ROOT, "tools", "pmc_traffic.json")))
+        src = open(os.path.join(ROOT, "siddhi-1_amd", "csrc", "p2_jit.hip"), "rb").read()
+        if t.get("kernel_src_sha1") == hashlib.sha1(src).hexdigest():
+            return t["traffic_bytes_per_launch"], t["profiles"]
+    except (OSError, ValueError, KeyError):
+        pass
+    return None, None
+
+
 def delta(a, b):
     return {k: b[k] - a[k] for k in a}
 
@@ -211,6 +225,7 @@ def main():
     adv_h_s = dst["advance_hbm_ns"] / 1e9 / launches
     alg = algorithmic_bytes(dst) / launches
     achieved = alg / adv_s / 1e9 if adv_s > 0 else 0.0
+    traffic, traffic_src = pmc_traffic()
     out = {
         "metric": "input events/sec, partitioned pattern query, 1/2/4/8 GPU; % of HBM roofline",
         "value": value,
@@ -229,7 +244,8 @@ def main():
                    "keys_per_gpu": K, "batch_events_per_gpu": B, "events_per_ms": 2000 * world,
                    "parallelism": f"key-sharded x{world}" + (" (RCCL all-to-all reshard per step)" if world > 1 else "")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes/launch",
+                     "traffic_source": traffic_src,
                      "kernel": "k_adv_m", "alg_bytes_per_launch": alg,
                      "kernel_ms_per_launch": adv_s * 1e3, "hbm_pass_ms_per_launch": adv_h_s * 1e3},
         "stages_ms_per_step": {"group": dst["group_ns"] / 1e6 / args.steps,
