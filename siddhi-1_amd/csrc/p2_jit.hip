@@ -128,6 +128,18 @@ template <class A, class B> struct SgSel<false, A, B> { typedef B type; };
 #ifndef SGX_NO_LOOP
 #define SGX_NO_LOOP 0
 #endif
+#ifndef SGX_MAX_IT
+#define SGX_MAX_IT 0x7fffffff
+#endif
+// SGX_PROF=1: s_memtime per walk phase, summed per wave into p.prof (tools/exp_c2.py prints it)
+#ifndef SGX_PROF
+#define SGX_PROF 0
+#endif
+#if SGX_PROF
+#define SGX_T(i) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); prof_acc[i] += t_ - prof_t; prof_t = t_; } while (0)
+#else
+#define SGX_T(i) do { } while (0)
+#endif
 
 namespace {
 
@@ -214,6 +226,9 @@ template <int S> __device__ __forceinline__ PayEl<S> lds_pay(const uint32_t* bas
     }
     return x;
 }
+
+#define SG_TS_LIM (1ll << 61)
+__device__ __forceinline__ bool ts_in_lim(int64_t t) { return t >= -SG_TS_LIM && t <= SG_TS_LIM; }
 
 __device__ __forceinline__ bool expired(int64_t pts, int64_t now, int64_t within) {
     const int64_t d = pts - now;  // StreamPreStateProcessor.isExpired: |slot0.ts - now| > within
@@ -517,24 +532,29 @@ __device__ __forceinline__ void advance(const P2Params& p) {
     W.slast = 0;
 
     // Raw match slots.  Without `every` around the whole pattern a key holds at most one start seed,
-    // so each event creates at most one partial and each partial is matched at most once: the wave
-    // emits at most sum(n0 + nev) matches in this batch and reserves that many slots here, with one
-    // atomic (no atomic, hence no vmcnt wait behind the match stores, inside the walk).  Under
-    // `every (e1 -> e2)` seeds multiply; the wave then reserves chunks as it goes, the next chunk
-    // prefetched (lane 0 keeps its base until the switch).
+    // so each event creates at most one partial and each partial is matched at most once: a lane
+    // emits at most n0 + nev matches in this batch.  In the staged pass n0 <= R (larger keys go to the
+    // HBM pass), so the wave's matches fit [rlo + w*64R, rhi + (w+1)*64R) of raw_e1 — disjoint from
+    // every other wave's range, found without any atomic (one device-wide counter hit by every wave
+    // serialises at the memory side and cost 0.8 ms per 2^24-event batch).  The HBM pass (few waves)
+    // and `every (e1 -> e2)` (seeds multiply: chunks reserved as the wave goes, the next one
+    // prefetched, lane 0 keeping its base until the switch) take slots above p.raw_static by atomics.
     constexpr bool BOUNDED = !(SGQ_MODE & SGD_P2_EVERY_BOTH);
     unsigned long long chunk_base = 0, next_l0 = 0;
     uint32_t chunk_left = 0;
     bool have_next = false;
     if constexpr (S1) {
-        if constexpr (BOUNDED) {
+        if constexpr (BOUNDED && STG) {
+            chunk_base = (unsigned long long)rlo + (unsigned long long)wave_id * (unsigned long long)(SGD_WAVE * R);
+        } else if constexpr (BOUNDED) {
             const uint32_t bound = nev > 0 ? n0 + (S0 ? (uint32_t)nev : 0u) : 0u;
             const uint32_t wb = (uint32_t)wave_sum((unsigned long long)bound);
-            if (lane == 0 && wb) next_l0 = atomicAdd(p.raw_count, (unsigned long long)wb);
+            if (lane == 0 && wb) next_l0 = p.raw_static + atomicAdd(p.raw_count, (unsigned long long)wb);
             chunk_left = wb;
         } else {
             have_next = iters > 0;
-            if (have_next && lane == 0) next_l0 = atomicAdd(p.raw_count, (unsigned long long)SGD_RAW_CHUNK);
+            if (have_next && lane == 0)
+                next_l0 = p.raw_static + atomicAdd(p.raw_count, (unsigned long long)SGD_RAW_CHUNK);
         }
     }
     if (STG && iters > 0) {
@@ -546,24 +566,50 @@ __device__ __forceinline__ void advance(const P2Params& p) {
     }
     if constexpr (STG) __syncthreads();  // the LDS copies have landed
     if (iters == 0) {  // no key of this wave has an event here (wave-uniform), or the HBM pass has it
-        if (STG && lane == 0) p.deferred[wave_id] = dval;
+        if (STG && lane == 0) {
+            p.deferred[wave_id] = dval;
+#pragma unroll
+            for (int i = 0; i < SGD_ST_N; ++i) p.wstats[(size_t)wave_id * SGD_ST_N + i] = 0;
+        }
         return;
     }
     // every prologue load has landed: an explicit full wait here clears the compiler's scoreboard, so
     // the walk below carries no vmcnt waits for the window registers (which would also drain the
     // match stores of every earlier iteration)
     __builtin_amdgcn_s_waitcnt(0);
-    if (S1 && BOUNDED) chunk_base = __shfl(next_l0, 0, SGD_WAVE);
+    if (S1 && BOUNDED && !STG) chunk_base = __shfl(next_l0, 0, SGD_WAVE);
+    if constexpr (STG && SGQ_WITHIN) {
+        // the staged walk tests expiry as `ts < now - within || ts > now + within`, exact when every
+        // timestamp and `within` lie in [-2^61, 2^61] (no 64-bit wrap anywhere, StreamPreStateProcessor
+        // .isExpired's long arithmetic included); a key outside that range goes to the HBM pass whole
+        bool far = within > SG_TS_LIM;
+#pragma unroll
+        for (int j = 0; j < R; ++j) far |= ((W.live >> j) & 1u) && !ts_in_lim(W.ts[j]);
+        if (run > 0 && far) {
+            rs = 0;
+            run = 0;
+            W.live = 0;
+            W.stg = 0;
+            W.tail = 0;
+        }
+    }
 
     PayEl<STRIDE> cur, nxt;
     if (run > 0) cur = STG ? lds_pay<STRIDE>(lds_run, b - rlo) : load_pay<STRIDE>(p.payload, b);
 
-    for (int it = 0; it < (SGX_NO_LOOP ? 0 : iters); ++it) {
+#if SGX_PROF
+    uint64_t prof_acc[5] = {0, 0, 0, 0, 0};
+    uint64_t prof_t = __builtin_amdgcn_s_memtime();
+#endif
+    for (int it = 0; it < (SGX_NO_LOOP ? 0 : min(iters, SGX_MAX_IT)); ++it) {
         bool act = it < run;
         if constexpr (STG) {
             // the partials this event can add: every start seed fires at most once (+1: the
-            // withinEvery re-arm of `every (e1 -> e2)`); stop here if the window could overflow
-            if (act && __popc(W.live) + s.spend + s.sstg + ((SGQ_MODE & SGD_P2_EVERY_BOTH) ? 1u : 0u) > (uint32_t)R) {
+            // withinEvery re-arm of `every (e1 -> e2)`); stop here if the window could overflow, or
+            // if the event's timestamp is outside the range of the band expiry test
+            const int64_t tsn = sg_i64(cur.w[STRIDE - 2], cur.w[STRIDE - 1]);
+            if (act && (__popc(W.live) + s.spend + s.sstg + ((SGQ_MODE & SGD_P2_EVERY_BOTH) ? 1u : 0u) > (uint32_t)R ||
+                        (SGQ_WITHIN && !ts_in_lim(tsn)))) {
                 rs = (uint32_t)it;
                 run = it;
                 act = false;
@@ -580,13 +626,18 @@ __device__ __forceinline__ void advance(const P2Params& p) {
             bi = cur.w[0];
             ts = sg_i64(cur.w[STRIDE - 2], cur.w[STRIDE - 1]);
             if constexpr (S0) ev = sgq_ev0(cur.w); else ev = sgq_ev1(cur.w);
+            SGX_T(0);
             // ---- stabilize (receiver.stabilizeStates) ----
             if (!GLB || !hbm) {
                 if (SGQ_WITHIN && W.live) {
                     uint32_t X = 0;
+                    if constexpr (STG) {  // band form (see the prologue): two compares per slot
+                        const int64_t lo = ts - within, hi = ts + within;
 #pragma unroll
-                    for (int j = 0; j < R; ++j) {
-                        X |= (expired(W.ts[j], ts, within) ? 1u : 0u) << j;
+                        for (int j = 0; j < R; ++j) X |= ((W.ts[j] < lo) | (W.ts[j] > hi) ? 1u : 0u) << j;
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < R; ++j) X |= (expired(W.ts[j], ts, within) ? 1u : 0u) << j;
                     }
                     X &= W.live;
                     if (X) {
@@ -618,6 +669,7 @@ __device__ __forceinline__ void advance(const P2Params& p) {
                 glb_stabilize<S0, S1>(G, s, ts, within);
             }
         }
+        SGX_T(1);
         // ---- state 1 first (reverse state order, PatternMultiProcessStreamReceiver.java:31-40) ----
         uint32_t c1 = 0, H = 0;
         uint64_t gmask = 0;
@@ -637,6 +689,7 @@ __device__ __forceinline__ void advance(const P2Params& p) {
                 }
             }
         }
+        SGX_T(2);
         // wave-wide reservation of the emitted matches (one atomic per wave chunk of slots)
         if constexpr (S1) {
         const uint32_t incl = wave_incl_scan(c1, lane);
@@ -650,7 +703,7 @@ __device__ __forceinline__ void advance(const P2Params& p) {
                 } else {
                     const uint32_t want = max(total, (uint32_t)SGD_RAW_CHUNK);
                     unsigned long long nb = 0;
-                    if (lane == 0) nb = atomicAdd(p.raw_count, (unsigned long long)want);
+                    if (lane == 0) nb = p.raw_static + atomicAdd(p.raw_count, (unsigned long long)want);
                     chunk_base = __shfl(nb, 0, SGD_WAVE);
                     chunk_left = want;
                 }
@@ -681,11 +734,12 @@ __device__ __forceinline__ void advance(const P2Params& p) {
             chunk_base += total;
             chunk_left -= total;
             if (!BOUNDED && !have_next && chunk_left < (uint32_t)SGD_RAW_CHUNK / 2) {  // prefetch the next chunk
-                if (lane == 0) next_l0 = atomicAdd(p.raw_count, (unsigned long long)SGD_RAW_CHUNK);
+                if (lane == 0) next_l0 = p.raw_static + atomicAdd(p.raw_count, (unsigned long long)SGD_RAW_CHUNK);
                 have_next = true;
             }
         }
         }
+        SGX_T(3);
         // ---- state 0: the start-state seeds ----
         if constexpr (S0) {
             if (act && s.spend > 0) {
@@ -750,7 +804,12 @@ __device__ __forceinline__ void advance(const P2Params& p) {
             }
         }
         cur = nxt;
+        SGX_T(4);
     }
+#if SGX_PROF
+    if (lane == 0 && p.prof)
+        for (int i = 0; i < 5; ++i) atomicAdd(&p.prof[i], (unsigned long long)prof_acc[i]);
+#endif
     if (STG && rs != SGD_NO_RESUME) p.resume[k] = rs;
     if constexpr (STG) {
         const unsigned long long anyr = __ballot(rs != SGD_NO_RESUME);
@@ -781,11 +840,21 @@ __device__ __forceinline__ void advance(const P2Params& p) {
         p.hdr[k] = SGD_H_MAKE(np, ns, min(s.spend, 3u), min(s.sstg, 3u), 1);
     }
     if (overflow) atomicOr(p.err, (uint32_t)SGD_ERR_PARTIAL_CAP);
-    // exact work counters (wave-reduced, one atomic per wave and counter)
+    // exact work counters, wave-reduced: the staged pass writes its wave's row of p.wstats (summed by
+    // k_stats_reduce: no device-wide atomics from every wave), the HBM pass adds to p.stats directly
     const unsigned long long v0 = wave_sum(s.scanned), v1 = wave_sum(s.created), v2 = wave_sum(s.matches);
     const unsigned long long v3 = wave_sum((nev > 0 && count_key) ? 1ull : 0ull), v4 = wave_sum(st_live0),
                              v5 = wave_sum(spills);
-    if (lane == 0) {
+    if (STG && lane == 0) {
+        unsigned long long* w = p.wstats + (size_t)wave_id * SGD_ST_N;
+        w[SGD_ST_SCANNED] = v0;
+        w[SGD_ST_CREATED] = v1;
+        w[SGD_ST_MATCHES] = v2;
+        w[SGD_ST_KEYS] = v3;
+        w[SGD_ST_LIVE0] = v4;
+        w[SGD_ST_SPILLS] = v5;
+    }
+    if (!STG && lane == 0) {
         if (v0) atomicAdd(&p.stats[SGD_ST_SCANNED], v0);
         if (v1) atomicAdd(&p.stats[SGD_ST_CREATED], v1);
         if (v2) atomicAdd(&p.stats[SGD_ST_MATCHES], v2);

@@ -61,6 +61,27 @@ __global__ void k_bump(unsigned long long* out_count, const unsigned long long* 
     *out_count += *batch_total;
 }
 
+// per-batch counters of the staged advance pass: one row per wave -> the cumulative totals
+__global__ void __launch_bounds__(1024) k_stats_reduce(const unsigned long long* __restrict__ wstats,
+                                                       uint32_t n_waves, unsigned long long* __restrict__ stats) {
+    __shared__ unsigned long long part[SGD_ST_N][16];
+    unsigned long long acc[SGD_ST_N];
+    for (int i = 0; i < SGD_ST_N; ++i) acc[i] = 0;
+    for (uint32_t w = threadIdx.x; w < n_waves; w += blockDim.x)
+        for (int i = 0; i < SGD_ST_N; ++i) acc[i] += wstats[(size_t)w * SGD_ST_N + i];
+    for (int i = 0; i < SGD_ST_N; ++i)
+        for (int off = 32; off > 0; off >>= 1) acc[i] += __shfl_xor(acc[i], off, 64);
+    const int wv = threadIdx.x / 64;
+    if ((threadIdx.x & 63) == 0)
+        for (int i = 0; i < SGD_ST_N; ++i) part[i][wv] = acc[i];
+    __syncthreads();
+    if (threadIdx.x < SGD_ST_N) {
+        unsigned long long t = 0;
+        for (int j = 0; j < (int)(blockDim.x / 64); ++j) t += part[threadIdx.x][j];
+        stats[threadIdx.x] += t;
+    }
+}
+
 // ------------------------------------------------------------------------------------------------
 // launch wrappers
 // ------------------------------------------------------------------------------------------------
@@ -69,6 +90,12 @@ int sgd_launch_bounds(const uint32_t* skeys, uint32_t n, uint32_t n_keys, uint32
     if (n == 0) return 0;
     hipLaunchKernelGGL(k_seg_bounds, dim3((n + 255) / 256), dim3(256), 0, stream, skeys, n, n_keys, seg_begin,
                        seg_end, err);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int sgd_launch_stats_reduce(const unsigned long long* wstats, uint32_t n_waves, unsigned long long* stats,
+                            ihipStream_t* stream) {
+    hipLaunchKernelGGL(k_stats_reduce, dim3(1), dim3(1024), 0, stream, wstats, n_waves, stats);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -84,12 +84,15 @@ struct P2Params {
     uint64_t raw_capacity;
     uint64_t* t_desc;                  // [max_batch] count << 32 | first raw slot; zero outside the
                                        // advance -> scatter window
-    unsigned long long* stats;         // [SGD_ST_N]
+    unsigned long long* stats;         // [SGD_ST_N] cumulative (HBM pass adds here directly)
+    unsigned long long* wstats;        // [n_keys / 64][SGD_ST_N] staged pass, this batch (k_stats_reduce)
+    uint64_t raw_static;               // raw_e1 slots [0, raw_static) belong to the staged pass's waves
     uint32_t* err;
     uint32_t* deferred;                // [n_keys / 64] waves the staged pass left to the HBM pass:
                                        // 1 = the whole wave, 2 = the keys with a resume point
     uint32_t* resume;                  // [n_keys] event index (in the key's run) where the HBM pass
                                        // resumes a key the staged pass stopped; SGD_NO_RESUME otherwise
+    unsigned long long* prof;          // SGX_PROF experiments only (NULL otherwise)
     uint32_t stage_chunks;             // LDS staging per wave, 16-B chunks (dynamic LDS = waves x this)
     uint32_t pad;
     uint64_t cst[SGD_MAX_CONST];       // filter constants, already in their comparison domain
@@ -129,3 +132,6 @@ struct ScatterParams {
     uint32_t* err;             // (o_len is constant 1/1 for two-state matches: filled at allocation)
 };
 int sgd_launch_scatter(const ScatterParams& s, ihipStream_t* stream);
+// sums the staged pass's per-wave counters of one batch into stats[SGD_ST_N]
+int sgd_launch_stats_reduce(const unsigned long long* wstats, uint32_t n_waves, unsigned long long* stats,
+                            ihipStream_t* stream);

@@ -226,8 +226,11 @@ struct sg_engine {
     // matches
     uint64_t* raw_e1 = nullptr;
     unsigned long long* raw_count = nullptr;
+    uint64_t raw_static = 0;       // raw slots owned by the staged pass's waves (no atomics)
+    unsigned long long* wstats = nullptr;  // per-wave counters of the staged pass (one batch)
     uint64_t* t_desc = nullptr;    // per batch event: match count << 32 | first raw slot
     uint32_t* deferred = nullptr;  // per advance wave: left by the staged pass to the HBM pass
+    unsigned long long* prof = nullptr;  // SG_PROF: walk-phase clocks of the staged pass (experiments)
     uint32_t* resume = nullptr;    // per key: where the HBM pass resumes a key the staged pass stopped
     uint32_t* t_off = nullptr;
     unsigned long long* out_count = nullptr;
@@ -288,6 +291,12 @@ struct sg_engine {
     ~sg_engine() {
         if (device >= 0) (void)hipSetDevice(device);
         if (stream) (void)hipStreamSynchronize(stream);
+        if (prof) {  // SG_PROF experiments: s_memtime ticks per walk phase, summed over waves
+            unsigned long long h[8] = {0};
+            if (hipMemcpy(h, prof, 64, hipMemcpyDeviceToHost) == hipSuccess)
+                fprintf(stderr, "SG_PROF phases: stop/decode %llu stabilize %llu f1 %llu emit %llu seed %llu\n",
+                        h[0], h[1], h[2], h[3], h[4]);
+        }
         if (gen) gen_destroy(gen);
         for (auto& sp : spans) { (void)hipEventDestroy(sp.a); (void)hipEventDestroy(sp.b); }
         for (auto x : free_events) (void)hipEventDestroy(x);
@@ -526,13 +535,22 @@ void allocate(sg_engine* e) {
     }
     // raw match slots per batch: waves reserve at most sum(live partials + events) up front, or
     // (every (e1 -> e2)) chunks of SGD_RAW_CHUNK with two chunks of slack per wave (p2_jit.hip)
-    e->raw_cap = std::max<uint64_t>(2 * (B + (uint64_t)K * C),
-                                    M + ((size_t)(K + SGD_WAVE - 1) / SGD_WAVE) * 2 * SGD_RAW_CHUNK);
+    // [0, raw_static): the staged pass's per-wave ranges (rlo + w*64R ..., p2_jit.hip); above: the
+    // atomically reserved slots of the HBM pass and of `every (e1 -> e2)`
+    const uint64_t nw = (K + SGD_WAVE - 1) / SGD_WAVE;
+    e->raw_static = (uint64_t)B + (nw + 1) * SGD_WAVE * e->reg_slots;
+    e->raw_cap = e->raw_static + std::max<uint64_t>(2 * (B + (uint64_t)K * C), M + nw * 2 * SGD_RAW_CHUNK);
+    if (e->raw_cap >= (1ull << 32)) throw std::invalid_argument("n_keys x partial_capacity too large for one engine");
+    e->wstats = dalloc<unsigned long long>(nw * SGD_ST_N, o);
     e->raw_e1 = dalloc<uint64_t>(e->raw_cap, o);
     e->raw_count = dalloc<unsigned long long>(1, o);
     e->t_desc = dalloc<uint64_t>(B, o);
     e->deferred = dalloc<uint32_t>((K + SGD_BLOCK - 1) / SGD_BLOCK * (SGD_BLOCK / SGD_WAVE), o);
     e->resume = dalloc<uint32_t>(K, o);
+    if (getenv("SG_PROF")) {
+        e->prof = dalloc<unsigned long long>(8, o);
+        HIP_OK(hipMemset(e->prof, 0, 64));
+    }
     HIP_OK(hipMemset(e->resume, 0xff, K * 4));  // SGD_NO_RESUME
     e->t_off = dalloc<uint32_t>(B, o);
     e->out_count = dalloc<unsigned long long>(1, o);
@@ -759,8 +777,11 @@ int push(sg_engine* e, const sg_batch* b) {
     p.raw_capacity = e->raw_cap;
     p.t_desc = e->t_desc;
     p.deferred = e->deferred;
+    p.prof = e->prof;
     p.resume = e->resume;
     p.stats = e->stats;
+    p.wstats = e->wstats;
+    p.raw_static = e->raw_static;
     p.err = e->err;
     for (size_t i = 0; i < e->consts.size(); i++) p.cst[i] = e->consts[i];
     HIP_OK(hipMemsetAsync(e->raw_count, 0, 8, e->stream));
@@ -773,6 +794,8 @@ int push(sg_engine* e, const sg_batch* b) {
         if (e->timing) { a1 = e->ev(); e->mark(a1); e->spans.push_back({a0, a1, 1}); a0 = e->ev(); e->mark(a0); }
         launch(v.adv_h[role], blocks, SGD_BLOCK, &p, e->stream);
         if (e->timing) { a1 = e->ev(); e->mark(a1); e->spans.push_back({a0, a1, 3}); }
+        if (sgd_launch_stats_reduce(e->wstats, blocks * (SGD_BLOCK / SGD_WAVE), e->stats, e->stream) != 0)
+            throw HipError("k_stats_reduce launch failed");
     }
     e->st.advance_launches++;
     // order this batch's matches by trigger (exclusive scan of per-event counts + scatter)
