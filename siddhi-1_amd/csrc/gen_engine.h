@@ -23,6 +23,8 @@
 #define GEN_MAXCODE 1024 // filter bytecode words
 #define GEN_NONE (-1)
 #define GEN_NIL 0xffffu  // null pool index
+#define GEN_RAWSEG 256   // raw-match reservation counters of a batch
+#define GEN_RESCHUNK 4   // raw matches a lane reserves at a time
 
 enum { GK_STREAM = 0, GK_COUNT = 1, GK_LOGICAL = 2 };
 
@@ -117,8 +119,14 @@ struct GenBatch {
 struct GenOut {
     // raw matches: per match [trigger seq u64][ts i64][key u32][len[nslots] u32][seqs nslots*MC u64], as words
     uint32_t* raw;
-    unsigned long long* raw_count;   // matches reserved
+    // matches reserved, per segment: a batch spreads its lanes' reservations over GEN_RAWSEG counters
+    // (segment = wave % nseg, slots [s * seg_cap, (s + 1) * seg_cap)); one device-wide counter hit by
+    // every lane serialises at the memory side.  Timer sweeps use one segment (their order sort reads
+    // a dense prefix).
+    unsigned long long* raw_count;
     uint64_t raw_cap;                // in matches
+    uint64_t seg_cap;
+    uint32_t nseg;
     uint32_t recWords;
     // per batch event: matches it triggered and the first raw index (contiguous)
     uint32_t* t_cnt;

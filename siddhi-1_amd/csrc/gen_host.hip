@@ -389,11 +389,13 @@ __device__ void write_out(const OutBufs& o, uint64_t d, const uint32_t* rec, boo
 }
 
 // batch matches: out_count + t_off[trigger] + rank
-__global__ void k_gen_scatter(const uint32_t* raw, const unsigned long long* raw_count, uint64_t raw_cap,
-                              const uint32_t* t_off, OutBufs o) {
+__global__ void k_gen_scatter(const uint32_t* raw, const unsigned long long* raw_count, uint64_t seg_cap,
+                              uint32_t nseg, const uint32_t* t_off, OutBufs o) {
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t n = *raw_count < raw_cap ? *raw_count : raw_cap;
-    if (r >= n) return;
+    const uint64_t sg = r / seg_cap;  // reservation segment (GenOut)
+    if (sg >= nseg) return;
+    const uint64_t n = raw_count[sg] < seg_cap ? raw_count[sg] : seg_cap;
+    if (r - sg * seg_cap >= n) return;
     const uint32_t* rec = raw + r * o.recWords;
     if (rec[0] >= 0xfffffffeu) return;
     write_out(o, *o.count + t_off[rec[0]] + rec[1], rec, false);
@@ -511,6 +513,8 @@ struct GenEngine {
         a.o.raw = raw;
         a.o.raw_count = raw_count;
         a.o.raw_cap = rawCap;
+        a.o.nseg = 1;
+        a.o.seg_cap = rawCap;
         a.o.recWords = recWords;
         a.o.t_cnt = t_cnt;
         a.o.t_first = t_first;
@@ -538,7 +542,9 @@ GenEngine* gen_create(const uint32_t* ir, size_t nw, const sg_config& cfg, hipSt
         e->mcap = cfg.match_capacity ? cfg.match_capacity : (uint64_t)e->maxb * 4;
         const GenProgram& G = e->host;
         e->recWords = 7 + (uint32_t)G.nslots + 2 * (uint32_t)G.nslots * G.MC;
-        e->rawCap = e->mcap + (uint64_t)e->K * 16;
+        // lanes reserve GEN_RESCHUNK slots at a time in one of GEN_RAWSEG segments: slack for every
+        // key's partly used chunks plus the segments' imbalance
+        e->rawCap = (e->mcap + (uint64_t)e->K * 2 * GEN_RESCHUNK + GEN_RAWSEG * 4096ull) / GEN_RAWSEG * GEN_RAWSEG;
         const size_t K = e->K, B = e->maxb;
         e->dprog = e->dalloc<GenProgram>(1);
         GH_OK(hipMemcpy(e->dprog, &e->host, sizeof(GenProgram), hipMemcpyHostToDevice));
@@ -562,7 +568,7 @@ GenEngine* gen_create(const uint32_t* ir, size_t nw, const sg_config& cfg, hipSt
                                         0, 32, stream));
         e->sort_tmp = e->dalloc<uint8_t>(e->sort_tmp_bytes);
         e->raw = e->dalloc<uint32_t>(e->rawCap * e->recWords);
-        e->raw_count = e->dalloc<unsigned long long>(1);
+        e->raw_count = e->dalloc<unsigned long long>(GEN_RAWSEG);
         e->t_cnt = e->dalloc<uint32_t>(B);
         e->t_first = e->dalloc<uint32_t>(B);
         e->t_off = e->dalloc<uint32_t>(B);
@@ -679,14 +685,16 @@ int gen_push(GenEngine* e, const sg_batch* b, std::string& msg) {
     }
     a.b.seg_begin = e->seg_begin;
     a.b.seg_end = e->seg_end;
-    GH_OK(hipMemsetAsync(e->raw_count, 0, 8, e->stream));
+    GH_OK(hipMemsetAsync(e->raw_count, 0, 8 * GEN_RAWSEG, e->stream));
+    a.o.nseg = GEN_RAWSEG;
+    a.o.seg_cap = e->rawCap / GEN_RAWSEG;
     launch_batch_or_timers(e, a, false);
     // order: out_count + t_off[trigger] + rank
     size_t tmp = e->scan_tmp_bytes;
     GH_OK(rocprim::exclusive_scan(e->scan_tmp, tmp, e->t_cnt, e->t_off, 0u, n, rocprim::plus<uint32_t>(), e->stream));
     const uint64_t maxRaw = e->rawCap;
     hipLaunchKernelGGL(k_gen_scatter, dim3((unsigned)((maxRaw + 255) / 256)), dim3(256), 0, e->stream, e->raw,
-                       e->raw_count, e->rawCap, e->t_off, e->out);
+                       e->raw_count, e->rawCap / GEN_RAWSEG, (uint32_t)GEN_RAWSEG, e->t_off, e->out);
     hipLaunchKernelGGL(k_gen_bump, dim3(1), dim3(1), 0, e->stream, e->out.count, e->t_cnt, e->t_off, n,
                        (const unsigned long long*)nullptr);
     GH_OK(hipMemsetAsync(e->t_cnt, 0, (size_t)n * 4, e->stream));
@@ -710,6 +718,8 @@ int gen_advance(GenEngine* e, int64_t t, std::string& msg) {
     a.now0 = e->now;   // the clock before it (wall-clock callers run at their own times)
     GH_OK(hipMemsetAsync(e->raw_count, 0, 8, e->stream));
     GH_OK(hipMemsetAsync(e->nvalid, 0, 8, e->stream));
+    a.o.nseg = 1;
+    a.o.seg_cap = e->rawCap;
     launch_batch_or_timers(e, a, true);
     unsigned long long nr = 0;
     GH_OK(hipMemcpyAsync(&nr, e->raw_count, 8, hipMemcpyDeviceToHost, e->stream));

@@ -52,11 +52,12 @@ struct Lane {
     unsigned long long scanned, created, matches;
     uint32_t err;
     unsigned long long resBase;  // this lane's reserved raw match slots
+    unsigned long long resEnd;   // end of its reservation segment
     uint32_t resLeft;
 
     __device__ Lane(const GenArgs& a, uint32_t key)
         : G(*a.G), A(a), S(a.state), K(a.K), k(key), now(a.now), trigSeq(SG_TIMER_SEQ), trigIdx(0), trigRank(0),
-          tk2(0), tk1(0), scanned(0), created(0), matches(0), err(0), resBase(0), resLeft(0) {
+          tk2(0), tk1(0), scanned(0), created(0), matches(0), err(0), resBase(0), resEnd(0), resLeft(0) {
         for (int i = 0; i < GEN_MAXP; i++) ret[i] = false;
     }
 
@@ -477,13 +478,15 @@ struct Lane {
     // ---- match output (QuerySelector input) ----
     __device__ void project(uint32_t se) {
         if (resLeft == 0) {
-            resBase = atomicAdd(A.o.raw_count, 16ull);
-            resLeft = 16;
+            const uint32_t sg = blockIdx.x % A.o.nseg;  // one wave per block
+            resBase = (unsigned long long)sg * A.o.seg_cap + atomicAdd(&A.o.raw_count[sg], (unsigned long long)GEN_RESCHUNK);
+            resEnd = (unsigned long long)(sg + 1) * A.o.seg_cap;
+            resLeft = GEN_RESCHUNK;
         }
         const unsigned long long r = resBase++;
         resLeft--;
         matches++;
-        if (r >= A.o.raw_cap) { err |= GERR_MATCHCAP; return; }
+        if (r >= resEnd) { err |= GERR_MATCHCAP; return; }
         uint32_t* rec = A.o.raw + r * A.o.recWords;
         const bool timer = trigSeq == SG_TIMER_SEQ;
         rec[0] = timer ? 0xfffffffeu : trigIdx;
@@ -1134,6 +1137,25 @@ struct Lane {
     }
 };
 
+// the lanes' work counters, reduced over the wave (all 64 lanes call this): one atomic per wave
+__device__ void gen_wave_stats(const GenArgs& a, unsigned long long sc, unsigned long long cr, unsigned long long ma,
+                               unsigned long long ky, uint32_t er) {
+    for (int off = 32; off > 0; off >>= 1) {
+        sc += __shfl_xor(sc, off, 64);
+        cr += __shfl_xor(cr, off, 64);
+        ma += __shfl_xor(ma, off, 64);
+        ky += __shfl_xor(ky, off, 64);
+        er |= (uint32_t)__shfl_xor((int)er, off, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if (er) atomicOr(a.o.err, er);
+        if (sc) atomicAdd(&a.o.stats[GST_SCANNED], sc);
+        if (cr) atomicAdd(&a.o.stats[GST_CREATED], cr);
+        if (ma) atomicAdd(&a.o.stats[GST_MATCHES], ma);
+        if (ky) atomicAdd(&a.o.stats[GST_KEYS], ky);
+    }
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------------------------------------
@@ -1141,40 +1163,43 @@ struct Lane {
 // ------------------------------------------------------------------------------------------------
 extern "C" __global__ void __launch_bounds__(64) k_gen_batch(const GenArgs a) {
     const uint32_t key = blockIdx.x * blockDim.x + threadIdx.x;
-    if (key >= a.K) return;
-    const uint32_t b = a.b.seg_begin[key], e = a.b.seg_end[key];
-    if (b >= e) return;
-    Lane L(a, key);
-    L.initKey();
-    const GenRecv& r = a.G->recv[a.b.stream];
-    if (r.n > 0) {
-        for (uint32_t j = b; j < e; j++) {
-            const uint32_t pos = a.b.sidx ? a.b.sidx[j] : j;
-            const uint32_t nxt = (j + 1 < e) ? (a.b.sidx ? a.b.sidx[j + 1] : j + 1) : 0xffffffffu;
-            L.processEvent(r, pos, nxt != pos + 1);
+    unsigned long long sc = 0, cr = 0, ma = 0, ky = 0;
+    uint32_t er = 0;
+    if (key < a.K && a.b.seg_begin[key] < a.b.seg_end[key]) {
+        const uint32_t b = a.b.seg_begin[key], e = a.b.seg_end[key];
+        Lane L(a, key);
+        L.initKey();
+        const GenRecv& r = a.G->recv[a.b.stream];
+        if (r.n > 0) {
+            for (uint32_t j = b; j < e; j++) {
+                const uint32_t pos = a.b.sidx ? a.b.sidx[j] : j;
+                const uint32_t nxt = (j + 1 < e) ? (a.b.sidx ? a.b.sidx[j + 1] : j + 1) : 0xffffffffu;
+                L.processEvent(r, pos, nxt != pos + 1);
+            }
         }
-    }
-    if (L.err) atomicOr(a.o.err, L.err);
-    atomicAdd(&a.o.stats[GST_SCANNED], L.scanned);
-    atomicAdd(&a.o.stats[GST_CREATED], L.created);
-    atomicAdd(&a.o.stats[GST_MATCHES], L.matches);
-    atomicAdd(&a.o.stats[GST_KEYS], 1ull);
-    // unused reserved raw slots are marked empty
-    for (uint32_t x = 0; x < L.resLeft; x++) {
-        const unsigned long long rr = L.resBase + x;
-        if (rr < a.o.raw_cap) {
-            a.o.raw[rr * a.o.recWords] = 0xffffffffu;
-            a.o.tk1[rr] = 0xffffffffu;  // sorts after every real timer match
+        // unused reserved raw slots are marked empty
+        for (uint32_t x = 0; x < L.resLeft; x++) {
+            const unsigned long long rr = L.resBase + x;
+            if (rr < L.resEnd) {
+                a.o.raw[rr * a.o.recWords] = 0xffffffffu;
+                a.o.tk1[rr] = 0xffffffffu;  // sorts after every real timer match
+            }
         }
+        er = L.err;
+        sc = L.scanned;
+        cr = L.created;
+        ma = L.matches;
+        ky = 1;
     }
+    gen_wave_stats(a, sc, cr, ma, ky, er);
 }
 
 // ------------------------------------------------------------------------------------------------
 // timer sweep to a.now (sg_advance_time): every key with due timers runs them in the reference order
 // ------------------------------------------------------------------------------------------------
-extern "C" __global__ void __launch_bounds__(64) k_gen_timers(const GenArgs a) {
-    const uint32_t key = blockIdx.x * blockDim.x + threadIdx.x;
-    if (key >= a.K) return;
+namespace {
+__device__ void gen_timers_key(const GenArgs& a, uint32_t key, unsigned long long& sc, unsigned long long& cr,
+                               unsigned long long& ma, uint32_t& er) {
     Lane L(a, key);
     const GenProgram& G = *a.G;
     if (!(L.W(0) & 1u)) {
@@ -1223,15 +1248,24 @@ extern "C" __global__ void __launch_bounds__(64) k_gen_timers(const GenArgs a) {
             }
         }
     }
-    if (L.err) atomicOr(a.o.err, L.err);
-    if (L.scanned) atomicAdd(&a.o.stats[GST_SCANNED], L.scanned);
-    if (L.created) atomicAdd(&a.o.stats[GST_CREATED], L.created);
-    if (L.matches) atomicAdd(&a.o.stats[GST_MATCHES], L.matches);
+    sc = L.scanned;
+    cr = L.created;
+    ma = L.matches;
+    er = L.err;
     for (uint32_t x = 0; x < L.resLeft; x++) {
         const unsigned long long rr = L.resBase + x;
-        if (rr < a.o.raw_cap) {
+        if (rr < L.resEnd) {
             a.o.raw[rr * a.o.recWords] = 0xffffffffu;
             a.o.tk1[rr] = 0xffffffffu;  // sorts after every real timer match
         }
     }
+}
+}  // namespace
+
+extern "C" __global__ void __launch_bounds__(64) k_gen_timers(const GenArgs a) {
+    const uint32_t key = blockIdx.x * blockDim.x + threadIdx.x;
+    unsigned long long sc = 0, cr = 0, ma = 0;
+    uint32_t er = 0;
+    if (key < a.K) gen_timers_key(a, key, sc, cr, ma, er);
+    gen_wave_stats(a, sc, cr, ma, 0, er);
 }
