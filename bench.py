@@ -167,23 +167,24 @@ def main():
         d = synth.stock_ticks(base, B, K * world, rate_per_ms=2000 * world)
         t = to_dev(torch, d, dev)
         if world > 1:
-            t["key"] = t["key"].to(torch.int64)
-            t["seq"] = torch.arange(base, base + B, dtype=torch.int64, device=dev)
             del t["symbol"]
         batches.append(t)
     torch.cuda.synchronize()
     local_seq = [0]
+    held = [None]
+    lib = sa.load_hip_library()
 
     def step(s):
         t = batches[s]
         if world > 1:
-            # RCCL all-to-all of the packed events to the GPUs owning their keys
-            g = reshard.reshard({"key": t["key"], "ts": t["ts"], "price": t["price"], "volume": t["volume"]},
-                                "key", world)
-            lk = reshard.local_key(g["key"], world).to(torch.int32)
-            n = lk.numel()
-            cols = (n, g["ts"].data_ptr(), [lk.data_ptr(), g["price"].data_ptr(), g["volume"].data_ptr()],
-                    lk.data_ptr())
+            # HIP stable pack by owning rank, RCCL all-to-all of the packed rows, unpack
+            g = reshard.reshard_device(lib, {"key": t["key"], "ts": t["ts"], "price": t["price"],
+                                             "volume": t["volume"]}, world)
+            held[0] = g  # keep the columns alive until the engine has read them
+            n = g["key"].numel()
+            cols = (n, g["ts"].data_ptr(), [g["key"].data_ptr(), g["price"].data_ptr(), g["volume"].data_ptr()],
+                    g["key"].data_ptr())
+            torch.cuda.current_stream(dev).synchronize()  # the engine's stream reads them next
         else:
             n = B
             cols = (B, t["ts"].data_ptr(), [t["symbol"].data_ptr(), t["price"].data_ptr(), t["volume"].data_ptr()],

@@ -143,6 +143,22 @@ void sg_engine_destroy(sg_engine* e);
 const char* sg_last_error(void);
 int sg_abi_version(void);
 
+/* Multi-GPU ingest (the reshard step in front of PartitionStreamReceiver, whose per-key
+ * state never crosses keys: PartitionStateHolder.java:43-49).  sg_shard_pack buckets one rank's slice
+ * of the arrival-ordered stream by owning rank (owner = key % world, local key = key / world) into
+ * packed rows {local key, ts lo, ts hi, col 0..n_cols-1} of 32-bit words, STABLE (arrival order kept
+ * per destination), destinations in rank order; dest_counts[world] (device, u64) receives the rows per
+ * destination.  All pointers are device memory of the current HIP device; work is queued on `stream`
+ * (a hipStream_t, NULL = default).  scratch: sg_shard_scratch_bytes(n, world) bytes of device memory.
+ * sg_shard_unpack turns received rows back into the SoA columns of a batch (cols_dev: a device
+ * array of n_cols column pointers). */
+int sg_shard_pack(uint64_t n, const uint32_t* key, const int64_t* ts, const uint32_t* const* cols, uint32_t n_cols,
+                  uint32_t world, uint32_t* rows, unsigned long long* dest_counts, void* scratch, size_t scratch_len,
+                  void* stream);
+size_t sg_shard_scratch_bytes(uint64_t n, uint32_t world);
+int sg_shard_unpack(uint64_t n, const uint32_t* rows, uint32_t n_cols, uint32_t* key, int64_t* ts,
+                    uint32_t* const* cols_dev, void* stream);
+
 /* Diagnostics (no device needed): generate and compile the query-specialised advance kernel of an IR
  * blob for gfx950.  variant_flags: bit 0 = batches carry null flags, bit 1 = captures carry null bits.
  * out (optional) receives the generated query header, or the compiler log on failure. */

@@ -1,0 +1,189 @@
+// shard_kernels.hip — multi-GPU ingest: bucket one rank's slice of the arrival-ordered
+// stream by the rank that owns each event's partition key, as packed rows ready for one RCCL
+// all_to_all, and unpack the received rows into the SoA columns sg_push_batch takes.
+//
+// Partition keys shard with no cross-key state (PartitionStateHolder.java:43-49,
+// PartitionStreamReceiver.send :262-272): owner = key % world, local key = key / world.  The pack is
+// a STABLE partition (arrival order kept within each destination), so a rank that receives the chunks
+// of all source ranks in rank order holds its keys' events in global arrival order — per key exactly
+// the order the reference processes them in.
+//
+// Layout: rows of W = 3 + n_cols 32-bit words {local key, ts lo, ts hi, col 0, ..}; the rows for
+// destination d are contiguous and in arrival order, destinations in rank order.
+//
+// Kernels (tiles of SH_TILE events, one workgroup each, SH_WAVES waves; wave w owns the contiguous
+// sub-range [w * SH_TILE / SH_WAVES, ...) of its tile, walked in rounds of 64 events):
+//   k_sh_count   per (destination, tile) counts, destination-major (so one exclusive scan gives every
+//                tile's first row per destination)
+//   k_sh_scatter stable rank per event by ballot per destination and round, rows written
+//   k_sh_unpack  rows -> SoA columns
+#include <hip/hip_runtime.h>
+
+#include <rocprim/device/device_scan.hpp>
+
+#include <cstdint>
+
+#include "../../include/siddhi_gpu.h"
+
+namespace {
+
+constexpr uint32_t SH_TILE = 4096;
+constexpr uint32_t SH_WAVES = 4;
+constexpr uint32_t SH_PER_WAVE = SH_TILE / SH_WAVES;  // 1024 = 16 rounds of 64
+constexpr uint32_t SH_MAX_WORLD = 64;
+constexpr uint32_t SH_MAX_COLS = 8;
+
+struct ShardArgs {
+    uint64_t n;
+    const uint32_t* key;   // global key ids
+    const int64_t* ts;
+    const uint32_t* col[SH_MAX_COLS];
+    uint32_t ncols;
+    uint32_t world;
+    uint32_t ntiles;
+    uint32_t* counts;      // [world][ntiles] (count pass) -> exclusive offsets (after the scan)
+    uint32_t* rows;        // [n][3 + ncols]
+};
+
+__global__ void __launch_bounds__(SH_WAVES * 64) k_sh_count(const ShardArgs a) {
+    __shared__ uint32_t c[SH_MAX_WORLD];
+    if (threadIdx.x < SH_MAX_WORLD) c[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t base = (uint64_t)blockIdx.x * SH_TILE;
+    for (uint32_t i = threadIdx.x; i < SH_TILE; i += blockDim.x) {
+        const uint64_t e = base + i;
+        if (e < a.n) atomicAdd(&c[a.key[e] % a.world], 1u);  // LDS atomics (order-free counts)
+    }
+    __syncthreads();
+    if (threadIdx.x < a.world) a.counts[(size_t)threadIdx.x * a.ntiles + blockIdx.x] = c[threadIdx.x];
+}
+
+__global__ void __launch_bounds__(SH_WAVES * 64) k_sh_scatter(const ShardArgs a) {
+    __shared__ uint32_t wtot[SH_WAVES][SH_MAX_WORLD];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x / 64;
+    const uint64_t wbase = (uint64_t)blockIdx.x * SH_TILE + (uint64_t)wv * SH_PER_WAVE;
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));  // the lanes below this one
+    // pass 1: this wave's count per destination (lane d keeps destination d's)
+    uint32_t mine = 0;
+    for (uint32_t r = 0; r < SH_PER_WAVE / 64; ++r) {
+        const uint64_t e = wbase + r * 64 + lane;
+        const uint32_t d = e < a.n ? a.key[e] % a.world : 0xffffffffu;
+        for (uint32_t dd = 0; dd < a.world; ++dd) {
+            const uint64_t m = __ballot(d == dd);
+            if (lane == dd) mine += (uint32_t)__popcll(m);
+        }
+    }
+    wtot[wv][lane] = mine;
+    __syncthreads();
+    // lane d: first row of destination d for this wave = the tile's offset + the tile's earlier waves
+    uint32_t base = 0;
+    if (lane < a.world) {
+        base = a.counts[(size_t)lane * a.ntiles + blockIdx.x];
+        for (uint32_t w2 = 0; w2 < wv; ++w2) base += wtot[w2][lane];
+    }
+    // pass 2: stable rank (arrival order = round, then lane) and the packed row
+    const uint32_t W = 3 + a.ncols;
+    for (uint32_t r = 0; r < SH_PER_WAVE / 64; ++r) {
+        const uint64_t e = wbase + r * 64 + lane;
+        const bool in = e < a.n;
+        const uint32_t k = in ? a.key[e] : 0u;
+        const uint32_t d = in ? k % a.world : 0xffffffffu;
+        uint32_t pos = 0;
+        for (uint32_t dd = 0; dd < a.world; ++dd) {
+            const uint64_t m = __ballot(d == dd);
+            const uint32_t bdd = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)dd);
+            if (d == dd) pos = bdd + (uint32_t)__popcll(m & lt);
+            if (lane == dd) base += (uint32_t)__popcll(m);
+        }
+        if (in) {
+            uint32_t* row = a.rows + (size_t)pos * W;
+            row[0] = k / a.world;
+            const uint64_t t = (uint64_t)a.ts[e];
+            row[1] = (uint32_t)t;
+            row[2] = (uint32_t)(t >> 32);
+            for (uint32_t c = 0; c < a.ncols; ++c) row[3 + c] = a.col[c][e];
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_sh_unpack(uint64_t n, const uint32_t* __restrict__ rows, uint32_t ncols,
+                                                   uint32_t* __restrict__ key, int64_t* __restrict__ ts,
+                                                   uint32_t* const* __restrict__ cols) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t W = 3 + ncols;
+    const uint32_t* row = rows + i * W;
+    key[i] = row[0];
+    ts[i] = (int64_t)((uint64_t)row[1] | ((uint64_t)row[2] << 32));
+    for (uint32_t c = 0; c < ncols; ++c) cols[c][i] = row[3 + c];
+}
+
+// destination totals from the scanned offsets (dest-major): total[d] = off[d+1][0] - off[d][0]
+__global__ void k_sh_totals(const uint32_t* off, const uint32_t* last_counts, uint32_t world, uint32_t ntiles,
+                            uint64_t n, unsigned long long* totals) {
+    const uint32_t d = threadIdx.x;
+    if (d >= world) return;
+    const uint64_t a = off[(size_t)d * ntiles];
+    const uint64_t b = (d + 1 < world) ? off[(size_t)(d + 1) * ntiles] : n;
+    totals[d] = b - a;
+    (void)last_counts;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sg_shard_pack(uint64_t n, const uint32_t* key, const int64_t* ts, const uint32_t* const* cols, uint32_t n_cols,
+                  uint32_t world, uint32_t* rows, unsigned long long* dest_counts, void* scratch, size_t scratch_len,
+                  void* stream) {
+    if (world == 0 || world > SH_MAX_WORLD || n_cols > SH_MAX_COLS || n >= (1ull << 32)) return SG_ERR_INVALID;
+    const hipStream_t s = (hipStream_t)stream;
+    ShardArgs a{};
+    a.n = n;
+    a.key = key;
+    a.ts = ts;
+    for (uint32_t c = 0; c < n_cols; ++c) a.col[c] = cols[c];
+    a.ncols = n_cols;
+    a.world = world;
+    a.ntiles = (uint32_t)((n + SH_TILE - 1) / SH_TILE);
+    const size_t ncnt = (size_t)world * a.ntiles;
+    size_t tmp = 0;
+    if (rocprim::exclusive_scan(nullptr, tmp, (uint32_t*)nullptr, (uint32_t*)nullptr, 0u, ncnt,
+                                rocprim::plus<uint32_t>(), s) != hipSuccess)
+        return SG_ERR_DEVICE;
+    const size_t need = 2 * ncnt * 4 + tmp + 256;
+    if (!scratch || scratch_len < need) return SG_ERR_CAPACITY;
+    uint32_t* cnt = (uint32_t*)scratch;
+    uint32_t* off = cnt + ncnt;
+    void* stmp = (void*)(((uintptr_t)(off + ncnt) + 255) & ~(uintptr_t)255);
+    if (n == 0) return hipMemsetAsync(dest_counts, 0, world * 8, s) == hipSuccess ? SG_OK : SG_ERR_DEVICE;
+    a.counts = cnt;
+    hipLaunchKernelGGL(k_sh_count, dim3(a.ntiles), dim3(SH_WAVES * 64), 0, s, a);
+    if (rocprim::exclusive_scan(stmp, tmp, cnt, off, 0u, ncnt, rocprim::plus<uint32_t>(), s) != hipSuccess)
+        return SG_ERR_DEVICE;
+    a.counts = off;
+    a.rows = rows;
+    hipLaunchKernelGGL(k_sh_scatter, dim3(a.ntiles), dim3(SH_WAVES * 64), 0, s, a);
+    hipLaunchKernelGGL(k_sh_totals, dim3(1), dim3(64), 0, s, off, cnt, world, a.ntiles, n, dest_counts);
+    return hipGetLastError() == hipSuccess ? SG_OK : SG_ERR_DEVICE;
+}
+
+size_t sg_shard_scratch_bytes(uint64_t n, uint32_t world) {
+    const uint32_t ntiles = (uint32_t)((n + SH_TILE - 1) / SH_TILE);
+    const size_t ncnt = (size_t)world * ntiles;
+    size_t tmp = 0;
+    (void)rocprim::exclusive_scan(nullptr, tmp, (uint32_t*)nullptr, (uint32_t*)nullptr, 0u, ncnt,
+                                  rocprim::plus<uint32_t>(), (hipStream_t)0);
+    return 2 * ncnt * 4 + tmp + 256;
+}
+
+int sg_shard_unpack(uint64_t n, const uint32_t* rows, uint32_t n_cols, uint32_t* key, int64_t* ts,
+                    uint32_t* const* cols_dev, void* stream) {
+    if (n_cols > SH_MAX_COLS) return SG_ERR_INVALID;
+    if (n == 0) return SG_OK;
+    hipLaunchKernelGGL(k_sh_unpack, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, n, rows,
+                       n_cols, key, ts, cols_dev);
+    return hipGetLastError() == hipSuccess ? SG_OK : SG_ERR_DEVICE;
+}
+
+}  // extern "C"

@@ -72,6 +72,57 @@ def reshard(cols: Dict[str, torch.Tensor], key_col: str, world: int, group=None)
     return res
 
 
+def reshard_device(lib, cols: Dict[str, torch.Tensor], world: int, group=None,
+                   exchange: bool = True) -> Dict[str, torch.Tensor]:
+    """The GPU path of `reshard` (RCCL): the HIP stable pack by owning rank (``sg_shard_pack``), one
+    all_to_all of the counts and one of the packed rows, and the unpack into SoA columns
+    (``sg_shard_unpack``).  ``cols``: "key" (global key id, int32/uint32), "ts" (int64) and 32-bit
+    attribute columns, all CUDA tensors of this rank's slice.  Returns "key" as the LOCAL key id
+    (key // world, int32), "ts" and the attribute columns, in global arrival order."""
+    import ctypes as C
+    key, ts = cols["key"].to(torch.int32).contiguous(), cols["ts"].contiguous()
+    names = [n for n in cols if n not in ("key", "ts")]
+    attrs = [cols[n].contiguous() for n in names]
+    if any(a.element_size() != 4 for a in attrs):
+        raise ValueError("reshard_device packs 32-bit attribute columns")
+    n, dev = key.numel(), key.device
+    W = 3 + len(attrs)
+    stream = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    lib.sg_shard_scratch_bytes.restype = C.c_size_t
+    lib.sg_shard_scratch_bytes.argtypes = [C.c_uint64, C.c_uint32]
+    scratch = torch.empty(int(lib.sg_shard_scratch_bytes(n, world)), dtype=torch.uint8, device=dev)
+    rows = torch.empty((max(n, 1), W), dtype=torch.int32, device=dev)
+    send = torch.empty(world, dtype=torch.int64, device=dev)
+    colp = (C.c_void_p * max(1, len(attrs)))(*[a.data_ptr() for a in attrs])
+    f = lib.sg_shard_pack
+    f.argtypes = [C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p,
+                  C.c_void_p, C.c_size_t, C.c_void_p]
+    rc = f(n, key.data_ptr(), ts.data_ptr(), colp, len(attrs), world, rows.data_ptr(), send.data_ptr(),
+           scratch.data_ptr(), scratch.numel(), stream)
+    if rc != 0:
+        raise RuntimeError(f"sg_shard_pack failed ({rc})")
+    if world == 1 or not exchange:
+        got = rows[:n]
+    else:
+        recv = torch.empty_like(send)
+        dist.all_to_all_single(recv, send, group=group)
+        sc, rc_ = send.tolist(), recv.tolist()
+        got = torch.empty((sum(rc_), W), dtype=torch.int32, device=dev)
+        dist.all_to_all_single(got.view(-1), rows[:n].reshape(-1), [c * W for c in rc_], [c * W for c in sc],
+                               group=group)
+    m = got.shape[0]
+    out = {"key": torch.empty(m, dtype=torch.int32, device=dev), "ts": torch.empty(m, dtype=torch.int64, device=dev)}
+    for nm, a in zip(names, attrs):
+        out[nm] = torch.empty(m, dtype=a.dtype, device=dev)
+    ptrs = torch.tensor([out[nm].data_ptr() for nm in names] or [0], dtype=torch.int64, device=dev)
+    g = lib.sg_shard_unpack
+    g.argtypes = [C.c_uint64, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    rc = g(m, got.data_ptr(), len(attrs), out["key"].data_ptr(), out["ts"].data_ptr(), ptrs.data_ptr(), stream)
+    if rc != 0:
+        raise RuntimeError(f"sg_shard_unpack failed ({rc})")
+    return out
+
+
 def merge_by_trigger(parts: List[Tuple[torch.Tensor, ...]]) -> torch.Tensor:
     """Host-side k-way merge order of per-rank match streams (each sorted by global trigger seq):
     returns the permutation of the concatenation that orders it by (trigger seq, rank, position) —
