@@ -8,9 +8,10 @@ through the C-ABI (key grouping + NFA advance) and polled (matches ordered by tr
 HBM).  `value` = input events/sec of the whole job (all ranks).
 
 N > 1: one process per GPU.  The global stream is arrival ordered; each rank holds a contiguous
-slice of every step (2^24 events) and the step first reshards it by key over RCCL (all_to_all of the
-packed events, siddhi-1_amd/reshard.py), then runs its engine on the 2^20 keys it owns
-(weak scaling: keys and events per GPU fixed).
+slice of every step (2^24 events); the slice is resharded by key (HIP stable pack by owning rank,
+RCCL all_to_all of the packed rows over xGMI, unpack: siddhi-1_amd/reshard.py) and each
+rank runs its engine on the 2^20 keys it owns (weak scaling: keys and events per GPU fixed).  Every
+timed step pushes one resharded slice and reshards the next one while the engine works on it.
 
 The roofline object prices the NFA advance kernel with the algorithmic byte model of DESIGN.md
  over its HIP-event-timed duration.  cpu_baseline times the CPU oracle (the
@@ -162,7 +163,8 @@ def main():
     # arrival-ordered stream over world * K keys (events per ms scale with the job)
     total = args.warmup + args.steps
     batches = []
-    for s in range(total):
+    # N > 1: one extra slice, so that every timed step also reshards the NEXT step's slice (below)
+    for s in range(total + (1 if world > 1 else 0)):
         base = s * world * B + rank * B
         d = synth.stock_ticks(base, B, K * world, rate_per_ms=2000 * world)
         t = to_dev(torch, d, dev)
@@ -171,26 +173,34 @@ def main():
         batches.append(t)
     torch.cuda.synchronize()
     local_seq = [0]
-    held = [None]
     lib = sa.load_hip_library()
 
-    def step(s):
+    def reshard_step(s):
+        # HIP stable pack by owning rank, RCCL all-to-all of the packed rows, unpack
         t = batches[s]
+        return reshard.reshard_device(lib, {"key": t["key"], "ts": t["ts"], "price": t["price"],
+                                            "volume": t["volume"]}, world)
+
+    nxt = [reshard_step(0) if world > 1 else None]
+
+    def step(s):
         if world > 1:
-            # HIP stable pack by owning rank, RCCL all-to-all of the packed rows, unpack
-            g = reshard.reshard_device(lib, {"key": t["key"], "ts": t["ts"], "price": t["price"],
-                                             "volume": t["volume"]}, world)
-            held[0] = g  # keep the columns alive until the engine has read them
+            g = nxt[0]
+            torch.cuda.current_stream(dev).synchronize()  # the engine's own stream reads these columns
             n = g["key"].numel()
             cols = (n, g["ts"].data_ptr(), [g["key"].data_ptr(), g["price"].data_ptr(), g["volume"].data_ptr()],
                     g["key"].data_ptr())
-            torch.cuda.current_stream(dev).synchronize()  # the engine's stream reads them next
         else:
+            t = batches[s]
             n = B
             cols = (B, t["ts"].data_ptr(), [t["symbol"].data_ptr(), t["price"].data_ptr(), t["volume"].data_ptr()],
                     t["key"].data_ptr())
         eng.push(0, local_seq[0], cols, [0, 1, 2], mem=sa.native.SG_MEM_DEVICE)
         local_seq[0] += n
+        if world > 1:
+            # the exchange of the next slice overlaps this step's engine work (own streams)
+            nxt[0] = reshard_step(s + 1)
+            del g
         m = eng.poll_device()
         eng.release(m)
 
