@@ -143,11 +143,18 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     dist = None
+    # test hooks for rehearsing the N > 1 path on one GPU: SG_BENCH_DEVICE pins every rank to one
+    # device, SG_BENCH_BACKEND=gloo exchanges through host memory (the driver's runs use neither)
+    local = int(os.environ.get("SG_BENCH_DEVICE", local))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("SG_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     sa = importlib.import_module("siddhi-1_amd")
     synth = importlib.import_module("siddhi-1_amd.synth")

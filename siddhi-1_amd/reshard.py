@@ -104,12 +104,16 @@ def reshard_device(lib, cols: Dict[str, torch.Tensor], world: int, group=None,
     if world == 1 or not exchange:
         got = rows[:n]
     else:
-        recv = torch.empty_like(send)
-        dist.all_to_all_single(recv, send, group=group)
+        host = dist.get_backend(group) == "gloo"  # rehearsal on one GPU: exchange through host memory
+        sd = send.cpu() if host else send
+        recv = torch.empty_like(sd)
+        dist.all_to_all_single(recv, sd, group=group)
         sc, rc_ = send.tolist(), recv.tolist()
-        got = torch.empty((sum(rc_), W), dtype=torch.int32, device=dev)
-        dist.all_to_all_single(got.view(-1), rows[:n].reshape(-1), [c * W for c in rc_], [c * W for c in sc],
-                               group=group)
+        src = rows[:n].reshape(-1)
+        src = src.cpu() if host else src
+        got = torch.empty((sum(rc_), W), dtype=torch.int32, device=src.device)
+        dist.all_to_all_single(got.view(-1), src, [c * W for c in rc_], [c * W for c in sc], group=group)
+        got = got.to(dev)
     m = got.shape[0]
     out = {"key": torch.empty(m, dtype=torch.int32, device=dev), "ts": torch.empty(m, dtype=torch.int64, device=dev)}
     for nm, a in zip(names, attrs):
