@@ -277,7 +277,7 @@ def main():
     torch.cuda.empty_cache()
     if rank == 0 and world == 1 and not args.no_extra:
         steps = max(3, args.steps // 4)
-        cb, c4b = 1 << 22, 1 << 20
+        cb, c4b = 1 << 22, 1 << 22
         out["other_configs"] = {
             "C3": dict(run_general(sa, synth, torch, dev, synth.C3_QUERY,
                                    lambda s: synth.stock_ticks(s * cb, cb, K), K, cb, steps, 1, 8),
@@ -288,10 +288,16 @@ def main():
                             workload="C3 with e1<1:5> (C3 as written emits no match under the reference's "
                                      "SEQUENCE reset semantics, DESIGN.md), 1,048,576 keys"),
             "C4": dict(run_general(sa, synth, torch, dev, synth.C4_QUERY,
-                                   lambda s: synth.burst_ticks(s * (c4b // 64), c4b // 64, 4096, 64), 4096, c4b,
-                                   steps, 1, 1024, playback=True),
+                                   lambda s: synth.burst_ticks(s * c4b, c4b, K, 1), K, c4b, steps, 1, 16,
+                                   playback=True),
                        workload="C4: every e1=S[price>20] -> not S[price>e1.price] for 30 sec within 60 sec, "
-                                "@app:playback, 4,096 keys, one key per ms in bursts of 64 events"),
+                                "@app:playback, 1,048,576 keys, one event per ms (distinct timer due times), "
+                                "4,194,304-event batches, the playback clock advanced per batch"),
+            "C4_deep": dict(run_general(sa, synth, torch, dev, synth.C4_QUERY,
+                                        lambda s: synth.burst_ticks(s * (c4b // 16), c4b // 16, K // 4, 16), K // 4,
+                                        c4b, steps, 1, 64, playback=True),
+                            workload="C4 with deeper per-key state: 262,144 keys, one key per ms in bursts of 16 "
+                                     "events (up to ~16 live partials per key)"),
         }
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(sa, synth, K, B, args.cpu_seconds)

@@ -12,6 +12,8 @@
 __global__ void __launch_bounds__(256) k_seg_bounds(const uint32_t* __restrict__ skeys, uint32_t n,
                                                     uint32_t n_keys, uint32_t* __restrict__ seg_begin,
                                                     uint32_t* __restrict__ seg_end, uint32_t* __restrict__ err) {
+    // every key gets its bounds written (keys without events get an empty [i, i) at the right spot),
+    // so no memset of the bound arrays is needed per batch
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     uint32_t k = skeys[i];
@@ -19,8 +21,18 @@ __global__ void __launch_bounds__(256) k_seg_bounds(const uint32_t* __restrict__
         atomicOr(err, (uint32_t)SGD_ERR_KEY_RANGE);
         return;
     }
-    if (i == 0 || skeys[i - 1] != k) seg_begin[k] = i;
-    if (i == n - 1 || skeys[i + 1] != k) seg_end[k] = i + 1;
+    const uint32_t prev = (i == 0) ? 0xffffffffu : skeys[i - 1];
+    if (prev != k) {
+        seg_begin[k] = i;
+        // keys between the previous run and this one (or before the first run) have no events
+        for (uint32_t g = (i == 0) ? 0u : prev + 1; g < k && g < n_keys; ++g) seg_begin[g] = seg_end[g] = i;
+    }
+    const uint32_t next = (i == n - 1) ? n_keys : skeys[i + 1];
+    if (next != k) {
+        seg_end[k] = i + 1;
+        if (i == n - 1)
+            for (uint32_t g = k + 1; g < n_keys; ++g) seg_begin[g] = seg_end[g] = n;
+    }
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -744,8 +744,6 @@ int push(sg_engine* e, const sg_batch* b) {
             pk.sidx = e->sidx;
             launch(v.pack[role], pack_blocks, 256, &pk, e->stream);
         }
-        HIP_OK(hipMemsetAsync(e->seg_begin, 0, (size_t)e->K * 4, e->stream));
-        HIP_OK(hipMemsetAsync(e->seg_end, 0, (size_t)e->K * 4, e->stream));
         if (sgd_launch_bounds(e->skeys, n, e->K, e->seg_begin, e->seg_end, e->err, e->stream) != 0)
             throw HipError("k_seg_bounds launch failed");
     } else {
