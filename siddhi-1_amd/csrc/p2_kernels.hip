@@ -3,6 +3,8 @@
 // query-specialised and compiled at engine creation (p2_jit.hip, sg_jit.cpp).
 #include <hip/hip_runtime.h>
 
+#include <rocprim/device/device_scan.hpp>
+
 #include "../../include/siddhi_gpu_ir.h"
 #include "sg_engine.h"
 
@@ -36,37 +38,84 @@ __global__ void __launch_bounds__(256) k_seg_bounds(const uint32_t* __restrict__
 }
 
 // ------------------------------------------------------------------------------------------------
-// match ordering: batch event t's matches go to out_count + t_off[t] (t_off = exclusive scan of the
-// per-event counts), i.e. ascending trigger seq, then emission order — the reference's callback order
-// (MultiProcessStreamReceiver.java:119-121).  Resets t_desc for the next batch.  chain_len is the
-// constant 1/1 of a two-state match and was written once at allocation.
+// match ordering: batch event t's matches go to out_count + (exclusive prefix of the per-event counts
+// over arrival order), i.e. ascending trigger seq, then emission order — the reference's callback
+// order (MultiProcessStreamReceiver.java:119-121).  Tiles of SGD_ORDER_TILE triggers: k_order_sums
+// (tile totals) -> exclusive scan of the totals -> k_order_scatter (row-by-row block scan of the
+// counts, 256 consecutive triggers per row so the lanes' output records are consecutive, and the
+// writes).  Resets t_desc for the next batch.  chain_len is the constant 1/1 of a two-state match and
+// was written once at allocation.
 // ------------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_scatter(const ScatterParams s) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= s.n) return;
-    const uint64_t d = s.t_desc[t];
-    const uint32_t c = (uint32_t)(d >> 32);
-    const uint64_t base = *s.out_count;
-    if (t == s.n - 1) *s.batch_total = (unsigned long long)s.t_off[t] + c;
-    if (c == 0) return;
-    s.t_desc[t] = 0;
-    const uint64_t o = base + s.t_off[t];
-    const uint32_t f = (uint32_t)d;
-    const uint64_t trig = s.seq_base + t;
-    const uint32_t key = s.key ? s.key[t] : 0u;
-    const int64_t ts = s.ts[t];
-    if (o + c > s.capacity) {
-        atomicOr(s.err, (uint32_t)SGD_ERR_MATCH_CAP);
-        return;
+__device__ __forceinline__ uint32_t ord_wave_incl_scan(uint32_t x, int lane) {
+    const int r = lane & 15;
+    uint32_t t;
+    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false); if (r >= 1) x += t;
+    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false); if (r >= 2) x += t;
+    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false); if (r >= 4) x += t;
+    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false); if (r >= 8) x += t;
+    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false); if (lane & 16) x += t;
+    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false); if (lane >= 32) x += t;
+    return x;
+}
+
+__global__ void __launch_bounds__(256) k_order_sums(const uint64_t* __restrict__ t_desc, uint32_t n,
+                                                    uint32_t* __restrict__ tile_sum) {
+    __shared__ uint32_t part[4];
+    const uint32_t base = blockIdx.x * SGD_ORDER_TILE;
+    uint32_t c = 0;
+    for (uint32_t j = 0; j < SGD_ORDER_TILE / 256; ++j) {
+        const uint32_t t = base + j * 256 + threadIdx.x;
+        if (t < n) c += (uint32_t)(t_desc[t] >> 32);
     }
-    for (uint32_t r = 0; r < c; ++r) {
-        const uint64_t q = o + r;
-        s.o_trig[q] = trig;
-        s.o_slot[2 * q] = s.raw_e1[f + r];
-        s.o_slot[2 * q + 1] = trig;
-        s.o_key[q] = key;
-        s.o_ts[q] = ts;  // StreamPostStateProcessor.java:68: StateEvent ts = ts of the e2 event
+    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) tile_sum[blockIdx.x] = part[0] + part[1] + part[2] + part[3];
+}
+
+__global__ void __launch_bounds__(256) k_order_scatter(const ScatterParams s, uint32_t ntiles) {
+    __shared__ uint32_t wtot[4];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t base = blockIdx.x * SGD_ORDER_TILE;
+    const uint64_t out0 = *s.out_count + s.tile_off[blockIdx.x];
+    uint32_t running = 0;
+    for (uint32_t j = 0; j < SGD_ORDER_TILE / 256; ++j) {
+        const uint32_t t = base + j * 256 + threadIdx.x;
+        const uint64_t d = t < s.n ? s.t_desc[t] : 0ull;
+        const uint32_t c = (uint32_t)(d >> 32);
+        const uint32_t incl = ord_wave_incl_scan(c, lane);
+        __syncthreads();  // the previous row's wtot reads are done
+        if (lane == 63) wtot[wv] = incl;
+        __syncthreads();
+        uint32_t before = 0, row = 0;
+        for (int w = 0; w < 4; ++w) {
+            const uint32_t x = wtot[w];
+            before += (w < wv) ? x : 0u;
+            row += x;
+        }
+        if (c) {
+            const uint64_t o = out0 + running + before + incl - c;
+            s.t_desc[t] = 0;
+            if (o + c > s.capacity) {
+                atomicOr(s.err, (uint32_t)SGD_ERR_MATCH_CAP);
+            } else {
+                const uint32_t f = (uint32_t)d;
+                const uint64_t trig = s.seq_base + t;
+                const uint32_t key = s.key ? s.key[t] : 0u;
+                const int64_t ts = s.ts[t];
+                for (uint32_t r = 0; r < c; ++r) {
+                    const uint64_t q = o + r;
+                    s.o_trig[q] = trig;
+                    s.o_slot[2 * q] = s.raw_e1[f + r];
+                    s.o_slot[2 * q + 1] = trig;
+                    s.o_key[q] = key;
+                    s.o_ts[q] = ts;  // StreamPostStateProcessor.java:68: StateEvent ts = ts of the e2 event
+                }
+            }
+        }
+        running += row;
     }
+    if (blockIdx.x == ntiles - 1 && threadIdx.x == 0) *s.batch_total = (unsigned long long)s.tile_off[blockIdx.x] + running;
 }
 
 __global__ void k_bump(unsigned long long* out_count, const unsigned long long* batch_total) {
@@ -111,9 +160,23 @@ int sgd_launch_stats_reduce(const unsigned long long* wstats, uint32_t n_waves, 
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int sgd_launch_scatter(const ScatterParams& s, ihipStream_t* stream) {
+size_t sgd_scatter_scan_bytes(uint32_t max_n) {
+    size_t tmp = 0;
+    const uint32_t nt = (max_n + SGD_ORDER_TILE - 1) / SGD_ORDER_TILE;
+    (void)rocprim::exclusive_scan(nullptr, tmp, (uint32_t*)nullptr, (uint32_t*)nullptr, 0u, nt,
+                                  rocprim::plus<uint32_t>(), (hipStream_t)0);
+    return tmp;
+}
+
+int sgd_launch_scatter(const ScatterParams& s, void* scan_tmp, size_t scan_bytes, ihipStream_t* stream) {
     if (s.n == 0) return 0;
-    hipLaunchKernelGGL(k_scatter, dim3((s.n + 255) / 256), dim3(256), 0, stream, s);
+    const uint32_t nt = (s.n + SGD_ORDER_TILE - 1) / SGD_ORDER_TILE;
+    hipLaunchKernelGGL(k_order_sums, dim3(nt), dim3(256), 0, stream, s.t_desc, s.n, s.tile_sum);
+    size_t tmp = scan_bytes;
+    if (rocprim::exclusive_scan(scan_tmp, tmp, s.tile_sum, s.tile_off, 0u, nt, rocprim::plus<uint32_t>(), stream) !=
+        hipSuccess)
+        return -1;
+    hipLaunchKernelGGL(k_order_scatter, dim3(nt), dim3(256), 0, stream, s, nt);
     hipLaunchKernelGGL(k_bump, dim3(1), dim3(1), 0, stream, s.out_count, s.batch_total);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -120,7 +120,8 @@ struct ScatterParams {
     const uint32_t* key;       // batch key ids (NULL: unpartitioned -> key 0)
     const int64_t* ts;
     uint64_t* t_desc;          // count << 32 | first raw slot per batch event (reset here)
-    const uint32_t* t_off;     // exclusive scan of the counts
+    uint32_t* tile_sum;        // [ceil(n / SGD_ORDER_TILE)] matches per tile of triggers
+    uint32_t* tile_off;        // exclusive scan of tile_sum
     const uint64_t* raw_e1;
     unsigned long long* out_count;
     unsigned long long* batch_total;
@@ -131,7 +132,11 @@ struct ScatterParams {
     int64_t* o_ts;
     uint32_t* err;             // (o_len is constant 1/1 for two-state matches: filled at allocation)
 };
-int sgd_launch_scatter(const ScatterParams& s, ihipStream_t* stream);
+#define SGD_ORDER_TILE 4096  // triggers per workgroup of the ordering kernels (256 threads x 16 rows)
+// ordering of one batch's matches: per-tile sums, their exclusive scan (scan_tmp: rocPRIM scratch of
+// scan_bytes), then the tile-local scan + scatter; also bumps out_count
+int sgd_launch_scatter(const ScatterParams& s, void* scan_tmp, size_t scan_bytes, ihipStream_t* stream);
+size_t sgd_scatter_scan_bytes(uint32_t max_n);
 // sums the staged pass's per-wave counters of one batch into stats[SGD_ST_N]
 int sgd_launch_stats_reduce(const unsigned long long* wstats, uint32_t n_waves, unsigned long long* stats,
                             ihipStream_t* stream);

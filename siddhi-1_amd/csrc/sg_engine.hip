@@ -160,11 +160,6 @@ hipError_t sort_payload(void* tmp, size_t& tmp_bytes, const uint32_t* keys, uint
     return rocprim::radix_sort_pairs(tmp, tmp_bytes, keys, skeys, it, (Pay<W>*)out, n, 0u, bits, stream);
 }
 
-// the match count of a per-event descriptor (count << 32 | first raw slot)
-struct DescCount {
-    __host__ __device__ uint32_t operator()(uint64_t d) const { return (uint32_t)(d >> 32); }
-};
-inline auto desc_counts(const uint64_t* d) { return rocprim::make_transform_iterator(d, DescCount{}); }
 
 hipError_t sort_payload_w(int W, void* tmp, size_t& tmp_bytes, const uint32_t* keys, uint32_t* skeys,
                           const PackSrc& src, void* out, uint32_t n, uint32_t bits, hipStream_t stream) {
@@ -232,7 +227,8 @@ struct sg_engine {
     uint32_t* deferred = nullptr;  // per advance wave: left by the staged pass to the HBM pass
     unsigned long long* prof = nullptr;  // SG_PROF: walk-phase clocks of the staged pass (experiments)
     uint32_t* resume = nullptr;    // per key: where the HBM pass resumes a key the staged pass stopped
-    uint32_t* t_off = nullptr;
+    uint32_t* tile_sum = nullptr;  // ordering: matches per tile of triggers, and its exclusive scan
+    uint32_t* tile_off = nullptr;
     unsigned long long* out_count = nullptr;
     unsigned long long* batch_total = nullptr;
     void* scan_tmp = nullptr;
@@ -552,7 +548,8 @@ void allocate(sg_engine* e) {
         HIP_OK(hipMemset(e->prof, 0, 64));
     }
     HIP_OK(hipMemset(e->resume, 0xff, K * 4));  // SGD_NO_RESUME
-    e->t_off = dalloc<uint32_t>(B, o);
+    e->tile_sum = dalloc<uint32_t>(B / SGD_ORDER_TILE + 1, o);
+    e->tile_off = dalloc<uint32_t>(B / SGD_ORDER_TILE + 1, o);
     e->out_count = dalloc<unsigned long long>(1, o);
     e->batch_total = dalloc<unsigned long long>(1, o);
     e->stats = dalloc<unsigned long long>(SGD_ST_N, o);
@@ -561,8 +558,7 @@ void allocate(sg_engine* e) {
     HIP_OK(hipMemset(e->out_count, 0, 8));
     HIP_OK(hipMemset(e->stats, 0, SGD_ST_N * 8));
     HIP_OK(hipMemset(e->err, 0, 4));
-    HIP_OK(rocprim::exclusive_scan(nullptr, e->scan_tmp_bytes, desc_counts(e->t_desc), e->t_off, 0u, (uint32_t)B,
-                                   rocprim::plus<uint32_t>(), e->stream));
+    e->scan_tmp_bytes = sgd_scatter_scan_bytes((uint32_t)B);
     e->scan_tmp = dalloc<uint8_t>(e->scan_tmp_bytes, o);
     e->o_trig = dalloc<uint64_t>(M, o);
     e->o_slot = dalloc<uint64_t>(2 * M, o);
@@ -800,16 +796,14 @@ int push(sg_engine* e, const sg_batch* b) {
     hipEvent_t o0 = nullptr, o1 = nullptr;
     if (e->timing) { o0 = e->ev(); e->mark(o0); }
     {
-        size_t tmp = e->scan_tmp_bytes;
-        HIP_OK(rocprim::exclusive_scan(e->scan_tmp, tmp, desc_counts(e->t_desc), e->t_off, 0u, n,
-                                       rocprim::plus<uint32_t>(), e->stream));
         ScatterParams sp{};
         sp.n = n;
         sp.seq_base = b->seq_base;
         sp.key = pl.partitioned ? (dev ? b->key : e->b_key) : nullptr;
         sp.ts = ts;
         sp.t_desc = e->t_desc;
-        sp.t_off = e->t_off;
+        sp.tile_sum = e->tile_sum;
+        sp.tile_off = e->tile_off;
         sp.raw_e1 = e->raw_e1;
         sp.out_count = e->out_count;
         sp.batch_total = e->batch_total;
@@ -819,7 +813,8 @@ int push(sg_engine* e, const sg_batch* b) {
         sp.o_key = e->o_key;
         sp.o_ts = e->o_ts;
         sp.err = e->err;
-        if (sgd_launch_scatter(sp, e->stream) != 0) throw HipError("k_scatter launch failed");
+        if (sgd_launch_scatter(sp, e->scan_tmp, e->scan_tmp_bytes, e->stream) != 0)
+            throw HipError("ordering launch failed");
     }
     if (e->timing) { o1 = e->ev(); e->mark(o1); e->spans.push_back({o0, o1, 2}); }
     if (!dev) HIP_OK(hipStreamSynchronize(e->stream));  // host buffers may be reused by the caller
