@@ -227,8 +227,13 @@ template <int S> __device__ __forceinline__ PayEl<S> lds_pay(const uint32_t* bas
     return x;
 }
 
-#define SG_TS_LIM (1ll << 61)
-__device__ __forceinline__ bool ts_in_lim(int64_t t) { return t >= -SG_TS_LIM && t <= SG_TS_LIM; }
+#define SG_OFF_LIM (1ll << 30)
+__device__ __forceinline__ bool off_ok(int64_t d) { return d >= -SG_OFF_LIM && d <= SG_OFF_LIM; }
+// t - base fits the staged pass's 32-bit offsets (no 64-bit wrap of the difference either)
+__device__ __forceinline__ bool ts_off_ok(int64_t t, int64_t base) {
+    int64_t d;
+    return !__builtin_sub_overflow(t, base, &d) && off_ok(d);
+}
 
 __device__ __forceinline__ bool expired(int64_t pts, int64_t now, int64_t within) {
     const int64_t d = pts - now;  // StreamPreStateProcessor.isExpired: |slot0.ts - now| > within
@@ -258,16 +263,22 @@ struct Slab {
     }
 };
 
-// the register window of one key: slot order = list order (pending slots before staged slots)
-struct Win {
-    int64_t ts[R];
-    uint64_t seq[R];
+// the register window of one key: slot order = list order (pending slots before staged slots).
+// OFF (the staged pass): timestamps and seqs are held as 32-bit offsets from a per-launch base (half
+// the registers and VALU of 64-bit values); ts -1 (eventTimeComparator's "unset") never occurs there
+// (such keys stop and go to the HBM pass), so the ts order is a plain compare.
+template <bool OFF> struct Win {
+    typedef typename SgSel<OFF, int32_t, int64_t>::type TS;
+    typedef typename SgSel<OFF, int32_t, uint64_t>::type SQ;
+    __device__ __forceinline__ static bool lt(TS a, TS b) { return OFF ? a < b : ts_before((int64_t)a, (int64_t)b); }
+    TS ts[R];
+    SQ seq[R];
     uint32_t cw[R][SGQ_NCAPW > 0 ? SGQ_NCAPW : 1];
     uint32_t cn[R];
     uint32_t live;  // slot holds a partial
     uint32_t stg;   // subset of live: staged (pre1's newAndEvery list), all above the pending slots
     uint32_t tail;  // appends go here (one past the highest live slot)
-    int64_t slast;  // ts of the last staged append
+    TS slast;       // ts of the last staged append
     bool sbad;      // the staged slots may be out of ts order (promotion sorts them)
 
     __device__ __forceinline__ void copy_slot(int d, int s) {
@@ -314,9 +325,9 @@ struct Win {
         for (int pass = 0; pass < R - 1; ++pass) {
 #pragma unroll
             for (int j = 0; j + 1 < R; ++j) {
-                if ((uint32_t)j >= lo && (uint32_t)(j + 1) < n && ts_before(ts[j + 1], ts[j])) {
-                    int64_t t = ts[j]; ts[j] = ts[j + 1]; ts[j + 1] = t;
-                    uint64_t q = seq[j]; seq[j] = seq[j + 1]; seq[j + 1] = q;
+                if ((uint32_t)j >= lo && (uint32_t)(j + 1) < n && lt(ts[j + 1], ts[j])) {
+                    TS t = ts[j]; ts[j] = ts[j + 1]; ts[j + 1] = t;
+                    SQ q = seq[j]; seq[j] = seq[j + 1]; seq[j + 1] = q;
 #pragma unroll
                     for (int w = 0; w < SGQ_NCAPW; ++w) { uint32_t c = cw[j][w]; cw[j][w] = cw[j + 1][w]; cw[j + 1][w] = c; }
                     if (SGQ_CAPNULL) { uint32_t c = cn[j]; cn[j] = cn[j + 1]; cn[j + 1] = c; }
@@ -511,13 +522,23 @@ __device__ __forceinline__ void advance(const P2Params& p) {
     const int64_t within = p.within;
     constexpr bool GLB = !STG;  // only the HBM pass has the slab (spill) mode
 
-    Win W;
+    // the staged pass's 32-bit offsets: ts from tbase (the batch's first key-sorted event), seq from
+    // the batch's seq_base; a key with a value out of range goes to the HBM pass (`far` below)
+    const int64_t tbase = STG ? sg_i64(p.payload[STRIDE - 2], p.payload[STRIDE - 1]) : 0;
+    const uint64_t sbase = STG ? p.seq_base : 0;
+    Win<STG> W;
+    typedef typename Win<STG>::TS WTS;
+    typedef typename Win<STG>::SQ WSQ;
+    bool far = false;
     W.live = 0; W.stg = 0; W.tail = 0;
 #pragma unroll
     for (int j = 0; j < R; ++j) {
         const bool ld = run > 0 && !hbm && (uint32_t)j < n0;
-        W.ts[j] = ld ? G.TS(j) : 0;
-        W.seq[j] = ld ? G.SEQ(j) : 0;
+        const int64_t t = ld ? G.TS(j) : 0;
+        const uint64_t q = ld ? G.SEQ(j) : 0;
+        if (STG && ld) far |= !ts_off_ok(t, tbase) || !off_ok((int64_t)(q - sbase)) || t == -1;
+        W.ts[j] = (WTS)(t - tbase);
+        W.seq[j] = (WSQ)(q - sbase);
 #pragma unroll
         for (int w = 0; w < SGQ_NCAPW; ++w) W.cw[j][w] = ld ? G.CAP(w, j) : 0u;
         W.cn[j] = (SGQ_CAPNULL && ld) ? G.NUL(j) : 0u;
@@ -578,13 +599,12 @@ __device__ __forceinline__ void advance(const P2Params& p) {
     // match stores of every earlier iteration)
     __builtin_amdgcn_s_waitcnt(0);
     if (S1 && BOUNDED && !STG) chunk_base = __shfl(next_l0, 0, SGD_WAVE);
-    if constexpr (STG && SGQ_WITHIN) {
-        // the staged walk tests expiry as `ts < now - within || ts > now + within`, exact when every
-        // timestamp and `within` lie in [-2^61, 2^61] (no 64-bit wrap anywhere, StreamPreStateProcessor
-        // .isExpired's long arithmetic included); a key outside that range goes to the HBM pass whole
-        bool far = within > SG_TS_LIM;
-#pragma unroll
-        for (int j = 0; j < R; ++j) far |= ((W.live >> j) & 1u) && !ts_in_lim(W.ts[j]);
+    if constexpr (STG) {
+        // the staged walk holds 32-bit offsets (|offset| <= 2^30) and tests expiry as
+        // `off < now - within || off > now + within`, exact in 32-bit arithmetic while 0 <= `within` < 2^30
+        // (StreamPreStateProcessor.isExpired's long arithmetic never wraps in that range, and off ± within
+        // stays inside int32); a key outside it goes to the HBM pass whole
+        if (SGQ_WITHIN && (within >= SG_OFF_LIM || within < 0)) far = true;
         if (run > 0 && far) {
             rs = 0;
             run = 0;
@@ -609,7 +629,7 @@ __device__ __forceinline__ void advance(const P2Params& p) {
             // if the event's timestamp is outside the range of the band expiry test
             const int64_t tsn = sg_i64(cur.w[STRIDE - 2], cur.w[STRIDE - 1]);
             if (act && (__popc(W.live) + s.spend + s.sstg + ((SGQ_MODE & SGD_P2_EVERY_BOTH) ? 1u : 0u) > (uint32_t)R ||
-                        (SGQ_WITHIN && !ts_in_lim(tsn)))) {
+                        !ts_off_ok(tsn, tbase) || tsn == -1 || cur.w[0] > 0x7fffffffu)) {
                 rs = (uint32_t)it;
                 run = it;
                 act = false;
@@ -631,13 +651,14 @@ __device__ __forceinline__ void advance(const P2Params& p) {
             if (!GLB || !hbm) {
                 if (SGQ_WITHIN && W.live) {
                     uint32_t X = 0;
-                    if constexpr (STG) {  // band form (see the prologue): two compares per slot
-                        const int64_t lo = ts - within, hi = ts + within;
+                    if constexpr (STG) {  // band form on the offsets (see the prologue): two compares per slot
+                        const int32_t tn = (int32_t)(ts - tbase), w32 = (int32_t)within;
+                        const int32_t lo = tn - w32, hi = tn + w32;
 #pragma unroll
                         for (int j = 0; j < R; ++j) X |= ((W.ts[j] < lo) | (W.ts[j] > hi) ? 1u : 0u) << j;
                     } else {
 #pragma unroll
-                        for (int j = 0; j < R; ++j) X |= (expired(W.ts[j], ts, within) ? 1u : 0u) << j;
+                        for (int j = 0; j < R; ++j) X |= (expired((int64_t)W.ts[j], ts, within) ? 1u : 0u) << j;
                     }
                     X &= W.live;
                     if (X) {
@@ -719,7 +740,7 @@ __device__ __forceinline__ void advance(const P2Params& p) {
 #pragma unroll
                     for (int j = 0; j < R; ++j) {
                         if ((H >> j) & 1u) {
-                            if (!SGX_NO_RAW && pos < p.raw_capacity) p.raw_e1[pos] = W.seq[j];
+                            if (!SGX_NO_RAW && pos < p.raw_capacity) p.raw_e1[pos] = sbase + (uint64_t)(int64_t)W.seq[j];
                             pos++;
                         }
                     }
@@ -758,8 +779,8 @@ __device__ __forceinline__ void advance(const P2Params& p) {
                             // the window is full of live partials: move the list to the HBM slab
 #pragma unroll
                             for (int j = 0; j < R; ++j) {
-                                G.TS(j) = W.ts[j];
-                                G.SEQ(j) = W.seq[j];
+                                G.TS(j) = tbase + (int64_t)W.ts[j];
+                                G.SEQ(j) = sbase + (uint64_t)(int64_t)W.seq[j];
 #pragma unroll
                                 for (int w = 0; w < SGQ_NCAPW; ++w) G.CAP(w, j) = W.cw[j][w];
                                 if (SGQ_CAPNULL) G.NUL(j) = W.cn[j];
@@ -774,15 +795,16 @@ __device__ __forceinline__ void advance(const P2Params& p) {
 #pragma unroll
                             for (int j = 0; j < R; ++j) {
                                 if ((uint32_t)j == t) {
-                                    W.ts[j] = ts;
-                                    W.seq[j] = seq;
+                                    W.ts[j] = (WTS)(ts - tbase);
+                                    W.seq[j] = (WSQ)(seq - sbase);
 #pragma unroll
                                     for (int w = 0; w < SGQ_NCAPW; ++w) W.cw[j][w] = cw[w];
                                     if (SGQ_CAPNULL) W.cn[j] = cn;
                                 }
                             }
-                            if (W.stg && ts_before(ts, W.slast)) W.sbad = true;
-                            W.slast = ts;
+                            const WTS to = (WTS)(ts - tbase);
+                            if (W.stg && Win<STG>::lt(to, W.slast)) W.sbad = true;
+                            W.slast = to;
                             W.live |= 1u << t;
                             W.stg |= 1u << t;
                             W.tail = t + 1;
@@ -807,8 +829,8 @@ __device__ __forceinline__ void advance(const P2Params& p) {
         SGX_T(4);
     }
 #if SGX_PROF
-    if (lane == 0 && p.prof)
-        for (int i = 0; i < 5; ++i) atomicAdd(&p.prof[i], (unsigned long long)prof_acc[i]);
+    if (lane == 0 && p.prof)  // one row per wave (no device-wide atomics), summed by the host
+        for (int i = 0; i < 5; ++i) p.prof[(size_t)wave_id * 8 + i] += prof_acc[i];
 #endif
     if (STG && rs != SGD_NO_RESUME) p.resume[k] = rs;
     if constexpr (STG) {
@@ -823,8 +845,8 @@ __device__ __forceinline__ void advance(const P2Params& p) {
 #pragma unroll
             for (int j = 0; j < R; ++j) {
                 if ((uint32_t)j < n) {
-                    G.TS(j) = W.ts[j];
-                    G.SEQ(j) = W.seq[j];
+                    G.TS(j) = tbase + (int64_t)W.ts[j];
+                    G.SEQ(j) = sbase + (uint64_t)(int64_t)W.seq[j];
 #pragma unroll
                     for (int w = 0; w < SGQ_NCAPW; ++w) G.CAP(w, j) = W.cw[j][w];
                     if (SGQ_CAPNULL) G.NUL(j) = W.cn[j];

@@ -226,6 +226,7 @@ struct sg_engine {
     uint64_t* t_desc = nullptr;    // per batch event: match count << 32 | first raw slot
     uint32_t* deferred = nullptr;  // per advance wave: left by the staged pass to the HBM pass
     unsigned long long* prof = nullptr;  // SG_PROF: walk-phase clocks of the staged pass (experiments)
+    size_t prof_rows = 0;
     uint32_t* resume = nullptr;    // per key: where the HBM pass resumes a key the staged pass stopped
     uint32_t* tile_sum = nullptr;  // ordering: matches per tile of triggers, and its exclusive scan
     uint32_t* tile_off = nullptr;
@@ -288,8 +289,12 @@ struct sg_engine {
         if (device >= 0) (void)hipSetDevice(device);
         if (stream) (void)hipStreamSynchronize(stream);
         if (prof) {  // SG_PROF experiments: s_memtime ticks per walk phase, summed over waves
+            std::vector<unsigned long long> rows(prof_rows * 8);
             unsigned long long h[8] = {0};
-            if (hipMemcpy(h, prof, 64, hipMemcpyDeviceToHost) == hipSuccess)
+            if (hipMemcpy(rows.data(), prof, rows.size() * 8, hipMemcpyDeviceToHost) == hipSuccess)
+                for (size_t r = 0; r < prof_rows; ++r)
+                    for (int i = 0; i < 8; ++i) h[i] += rows[r * 8 + i];
+            if (true)
                 fprintf(stderr, "SG_PROF phases: stop/decode %llu stabilize %llu f1 %llu emit %llu seed %llu\n",
                         h[0], h[1], h[2], h[3], h[4]);
         }
@@ -544,8 +549,9 @@ void allocate(sg_engine* e) {
     e->deferred = dalloc<uint32_t>((K + SGD_BLOCK - 1) / SGD_BLOCK * (SGD_BLOCK / SGD_WAVE), o);
     e->resume = dalloc<uint32_t>(K, o);
     if (getenv("SG_PROF")) {
-        e->prof = dalloc<unsigned long long>(8, o);
-        HIP_OK(hipMemset(e->prof, 0, 64));
+        e->prof = dalloc<unsigned long long>(nw * 8, o);
+        HIP_OK(hipMemset(e->prof, 0, nw * 64));
+        e->prof_rows = nw;
     }
     HIP_OK(hipMemset(e->resume, 0xff, K * 4));  // SGD_NO_RESUME
     e->tile_sum = dalloc<uint32_t>(B / SGD_ORDER_TILE + 1, o);

@@ -165,6 +165,32 @@ def test_gpu_non_monotonic_timestamps(reg_slots, monkeypatch):
         _same(gpu.poll(), ora.poll())
 
 
+@pytest.mark.parametrize("within", ["1 sec", "20 days"])
+def test_gpu_far_timestamps(within):
+    """the staged pass holds timestamps / seqs as 32-bit offsets from a per-batch base: keys with a
+    partial or an event more than 2^30 ms from the base, a ts of -1 (eventTimeComparator's unset) or
+    a `within` of 2^30 ms or more must leave the staged pass for the 64-bit HBM pass, bit-exact"""
+    q = (STOCK + "partition with (symbol of S) begin from every e1=S[price>20] -> e2=S[price>e1.price] "
+         f"within {within} select e1.price as a insert into O; end;")
+    n_keys, batch = 1024, 30000
+    cq, gpu, ora = _engines(q, n_keys, batch)
+    rng = np.random.default_rng(17)
+    seq = 0
+    for b in range(4):
+        d = synth.stock_ticks(seq, batch, n_keys, seed=40 + b, rate_per_ms=16)
+        ts = d["ts"].copy()
+        pick = rng.random(batch)
+        ts[pick < 0.01] += np.int64(1) << 33            # far future
+        ts[(pick >= 0.01) & (pick < 0.015)] -= np.int64(1) << 40   # far past
+        ts[(pick >= 0.015) & (pick < 0.018)] = -1
+        ts[(pick >= 0.018) & (pick < 0.019)] = np.int64(2**62)     # near the long range's edge
+        for e in (gpu, ora):
+            e.push(0, seq, ts, [d["symbol"], d["price"], d["volume"]], None, d["key"])
+        seq += batch
+        _same(gpu.poll(), ora.poll())
+    assert gpu.stats()["matches"] == ora.stats()["matches"] > 0
+
+
 def test_gpu_unpartitioned_single_key():
     q = STOCK + "from every e1=S[price>20] -> e2=S[price>e1.price] within 10 sec select e1.price as a insert into O;"
     cq, gpu, ora = _engines(q, 1, 20000)
