@@ -111,6 +111,9 @@ class CompiledQuery:
     query: q.Query
     element: object = None
     receiver_kinds: dict = field(default_factory=dict)
+    aggregators: list = field(default_factory=list)   # [_Typed("agg")] in QuerySelector order
+    group_by: list = field(default_factory=list)      # typed group-by expressions
+    having: object = None                             # typed having condition (may read output names)
 
     @property
     def partitioned(self):
@@ -228,29 +231,32 @@ class _Typed:
         self.__dict__.update(kw)
 
 
-def type_expr(ctx: _Ctx, e, resolve):
+def type_expr(ctx: _Ctx, e, resolve, funcs=None):
+    """funcs: typer of function calls (select / having only; filters on the device path take none)"""
     if isinstance(e, q.Const):
         if e.type == "OBJECT":
             return _Typed("const", "OBJECT", value=None)
         return _Typed("const", e.type, value=e.value)
     if isinstance(e, q.Var):
         rv = resolve(e)
+        if isinstance(rv, _Typed):   # a having clause naming an output attribute
+            return rv
         return _Typed("var", "OBJECT" if rv.multi_value else rv.type, var=rv)
     if isinstance(e, q.IsNullStream):
         # `e1 is null` inside a state query: the stream event itself (IsNullStreamConditionExpressionExecutor)
         v = resolve(q.Var("__stream__", e.stream, e.index))
         return _Typed("isnull_ev", "BOOL", slot=v.slot, chain=v.chain_index)
     if isinstance(e, q.IsNull):
-        inner = type_expr(ctx, e.expr, resolve)
+        inner = type_expr(ctx, e.expr, resolve, funcs)
         return _Typed("isnull", "BOOL", arg=inner)
     if isinstance(e, q.Not):
-        inner = type_expr(ctx, e.expr, resolve)
+        inner = type_expr(ctx, e.expr, resolve, funcs)
         if inner.type != "BOOL":
             raise SiddhiAppCreationException("NOT needs a BOOL operand")
         return _Typed("not", "BOOL", arg=inner)
     if isinstance(e, q.BinOp):
-        lt = type_expr(ctx, e.left, resolve)
-        rt = type_expr(ctx, e.right, resolve)
+        lt = type_expr(ctx, e.left, resolve, funcs)
+        rt = type_expr(ctx, e.right, resolve, funcs)
         if e.op in ("and", "or"):
             if lt.type != "BOOL" or rt.type != "BOOL":
                 raise SiddhiAppCreationException(f"{e.op.upper()} needs BOOL operands")
@@ -267,6 +273,8 @@ def type_expr(ctx: _Ctx, e, resolve):
             t = arith_type(lt.type, rt.type)
             return _Typed("arith", t, op=e.op, left=lt, right=rt)
     if isinstance(e, q.Func):
+        if funcs is not None:
+            return funcs(e)
         raise SiddhiAppCreationException(f"function {e.name}() is not supported on the pattern path")
     raise SiddhiAppCreationException(f"unsupported expression {e!r}")
 
@@ -453,11 +461,54 @@ def _stream_counts(el, acc):
     return acc
 
 
+NUMERIC = ("INT", "LONG", "FLOAT", "DOUBLE")
+INSTANCE_OF = {"instanceOfBoolean": "BOOL", "instanceOfDouble": "DOUBLE", "instanceOfFloat": "FLOAT",
+               "instanceOfInteger": "INT", "instanceOfLong": "LONG", "instanceOfString": "STRING"}
+
+
+def _type_select_func(ctx, f, resolve, funcs, aggs):
+    """Function calls of a select / having clause.  Aggregators follow
+    C/query/selector/attribute/aggregator/*AttributeAggregatorExecutor.java (return types from their
+    init: count/distinctCount LONG, sum LONG for int/long and DOUBLE for float/double, avg DOUBLE,
+    min/max the argument's type); instanceOf* follow C/executor/function/InstanceOf*FunctionExecutor.java
+    (true iff the value is a non-null instance of that type)."""
+    if f.namespace is not None:
+        raise SiddhiAppCreationException(f"function {f.namespace}:{f.name}() is not supported")
+    args = [type_expr(ctx, a, resolve, funcs) for a in f.args]
+    for a in args:
+        if _has_agg(a) and f.name not in INSTANCE_OF:
+            raise SiddhiAppCreationException(f"aggregator inside {f.name}()")
+    n = f.name
+    if n in INSTANCE_OF:
+        if len(args) != 1:
+            raise SiddhiAppCreationException(f"{n}() takes one argument")
+        return _Typed("instof", "BOOL", arg=args[0], want=INSTANCE_OF[n])
+    if n == "count" and len(args) <= 1:
+        t = "LONG"
+    elif n == "distinctCount" and len(args) == 1:
+        t = "LONG"
+    elif n in ("sum", "avg", "min", "max", "minForever", "maxForever") and len(args) == 1:
+        at = args[0].type
+        if at not in NUMERIC:
+            raise SiddhiAppCreationException(f"{n}() not supported for {at}")
+        t = {"sum": "LONG" if at in ("INT", "LONG") else "DOUBLE", "avg": "DOUBLE"}.get(n, at)
+    else:
+        raise SiddhiAppCreationException(f"function {n}() is not supported in select")
+    a = _Typed("agg", t, fn=n, arg=args[0] if args else None, idx=len(aggs))
+    aggs.append(a)
+    return a
+
+
+def _has_agg(t):
+    if t.kind == "agg":
+        return True
+    return any(_has_agg(getattr(t, k)) for k in ("left", "right", "arg")
+               if isinstance(getattr(t, k, None), _Typed))
+
+
 def compile_query(app: q.App, query: q.Query, strings) -> CompiledQuery:
     if not isinstance(query.input, q.StateInput):
         raise SiddhiAppCreationException("only pattern / sequence queries run on this engine")
-    if query.group_by or query.having is not None:
-        raise SiddhiAppCreationException("group by / having are not supported yet (SURVEY §8f row f1)")
     si = query.input
     ctx = _Ctx(app, app.streams, strings)
     _assign_slots(ctx, si.element)
@@ -478,9 +529,11 @@ def compile_query(app: q.App, query: q.Query, strings) -> CompiledQuery:
                 raise SiddhiAppCreationException(f"partition attribute {partition_keys[s.name]} "
                                                  f"not in {s.name}")
 
-    # select list (host-side projection) --------------------------------------------------------
+    # select list (host-side projection, QuerySelector) -----------------------------------------
     select = []
+    aggs: List[_Typed] = []
     resolve = lambda v: resolve_select_var(ctx, v)
+    funcs = lambda f: _type_select_func(ctx, f, resolve, funcs, aggs)
     if query.select is None:
         names = set()
         for s in ctx.slots:
@@ -491,9 +544,7 @@ def compile_query(app: q.App, query: q.Query, strings) -> CompiledQuery:
                 select.append((an, at, type_expr(ctx, q.Var(an), resolve)))
     else:
         for oa in query.select:
-            t = type_expr(ctx, oa.expr, resolve) if not isinstance(oa.expr, q.Func) else None
-            if t is None:
-                raise SiddhiAppCreationException(f"function {oa.expr.name}() in select is not supported yet")
+            t = type_expr(ctx, oa.expr, resolve, funcs)
             name = oa.rename
             if name is None:
                 if isinstance(oa.expr, q.Var):
@@ -501,6 +552,21 @@ def compile_query(app: q.App, query: q.Query, strings) -> CompiledQuery:
                 else:
                     raise SiddhiAppCreationException("select expressions need 'as <name>'")
             select.append((name, t.type, t))
+    group_by = [type_expr(ctx, g, resolve) for g in query.group_by]
+    having = None
+    if query.having is not None:
+        out_idx = {name: i for i, (name, _, _) in enumerate(select)}
+
+        def resolve_having(v):
+            # the output stream's attributes first (QueryParserHelper: having runs on the projected event)
+            if v.stream is None and v.index is None and v.attr in out_idx:
+                i = out_idx[v.attr]
+                return _Typed("out", select[i][1], idx=i)
+            return resolve(v)
+        hfuncs = lambda f: _type_select_func(ctx, f, resolve_having, hfuncs, aggs)
+        having = type_expr(ctx, query.having, resolve_having, hfuncs)
+        if having.type != "BOOL":
+            raise SiddhiAppCreationException("having needs a BOOL condition")
 
     # IR ---------------------------------------------------------------------------------------
     stream_words: List[int] = []
@@ -534,4 +600,5 @@ def compile_query(app: q.App, query: q.Query, strings) -> CompiledQuery:
         recv[s.name] = ("SEQUENCE" if si.kind == "SEQUENCE" else "PATTERN") + ("_MULTI" if multi else "_SINGLE")
 
     return CompiledQuery(query.name, si.kind, ir, list(ctx.streams), list(ctx.slots), si.within_ms,
-                         partition_keys, select, query.output_stream, query, si.element, recv)
+                         partition_keys, select, query.output_stream, query, si.element, recv,
+                         aggs, group_by, having)

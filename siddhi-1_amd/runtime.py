@@ -232,6 +232,11 @@ def java_string(v):
     return str(v)
 
 
+def _group_key(v):
+    """GroupByKeyGenerator.constructEventKey: the values' string forms joined (None -> "null")"""
+    return "null" if v is None else (v.item() if isinstance(v, np.generic) else v)
+
+
 # ------------------------------------------------------------------------------------------------
 # query runtime
 # ------------------------------------------------------------------------------------------------
@@ -243,6 +248,11 @@ class _QueryRuntime:
         self.n_keys = app_rt.n_keys if cq.partitioned else 1
         self.engine = engine_factory(cq.ir, self.n_keys)
         self.query_callbacks: List[QueryCallback] = []
+        # aggregator states: (partition key, group-by key) -> one state per aggregator
+        # (PartitionStateHolder over the group-by flow's states, C/util/snapshot/state/*StateHolder.java)
+        self._agg_states: Dict[tuple, list] = {}
+        self._cur_aggs = None
+        self._cur_out = None
 
     # -- projection (QuerySelector) --------------------------------------------------------------
     def _eval(self, t, chains, store):
@@ -281,6 +291,13 @@ class _QueryRuntime:
             return not (self._eval(t.arg, chains, store) is True)
         if k == "isnull":
             return self._eval(t.arg, chains, store) is None
+        if k == "agg":
+            return self._aggregate(t, chains, store)
+        if k == "instof":
+            v = self._eval(t.arg, chains, store)
+            return v is not None and t.arg.type == t.want
+        if k == "out":
+            return self._cur_out[t.idx]
         if k == "isnull_ev":
             chain = chains[t.slot]
             n = len(chain)
@@ -288,19 +305,74 @@ class _QueryRuntime:
             return not ((0 <= i < n) or (i < 0 and n + i >= 0 and n > 0))
         raise RuntimeError(k)
 
+    def _aggregate(self, t, chains, store):
+        """processAdd of one aggregator for a CURRENT event (AttributeAggregatorExecutor.java:60-100):
+        Count/Sum/Avg/Min/Max/DistinctCount*AttributeAggregatorExecutor.java, a null argument returns
+        the current value (distinctCount counts it)."""
+        st = self._cur_aggs[t.idx]
+        if st is None:
+            st = self._cur_aggs[t.idx] = {"n": 0, "v": None, "d": {}}
+        fn = t.fn
+        if fn == "count":
+            st["n"] += 1
+            return st["n"]
+        v = self._eval(t.arg, chains, store)
+        if fn == "distinctCount":
+            key = v.item() if isinstance(v, np.generic) else v
+            st["d"][key] = st["d"].get(key, 0) + 1
+            return len(st["d"])
+        if v is None:
+            if fn in ("sum", "avg"):
+                if st["n"] == 0:
+                    return None
+                return st["v"] if fn == "sum" else st["v"] / st["n"]
+            return st["v"]
+        if fn == "sum":
+            if t.type == "LONG":
+                st["v"] = _wrap64((st["v"] or 0) + int(v))
+            else:
+                st["v"] = (st["v"] or 0.0) + float(v)
+            st["n"] += 1
+            return st["v"]
+        if fn == "avg":
+            st["v"] = (st["v"] or 0.0) + float(v)
+            st["n"] += 1
+            return st["v"] / st["n"]
+        v = _to_type(v, t.type)
+        cur = st["v"]
+        if fn in ("min", "minForever"):
+            if cur is None or cur > v:
+                st["v"] = v
+        elif cur is None or cur < v:
+            st["v"] = v
+        return st["v"]
+
     def project(self, m, store):
+        """QuerySelector.process per emitted StateEvent (each reaches the selector in a chunk of its
+        own: StateMultiProcessStreamReceiver.java:59-65, SingleProcessStreamReceiver.java:71-77), so
+        processInBatch(No)GroupBy (QuerySelector.java:272-370) emits each match that passes `having`
+        with the aggregates updated through it."""
         out = []
-        strings = self.app_rt.strings
+        cq = self.cq
         n = len(m)
+        n_aggs = len(cq.aggregators)
         for i in range(n):
             chains = []
             for s in range(m.slot_seq.shape[1]):
                 ln = int(m.chain_len[i, s])
                 chains.append([int(x) for x in m.slot_seq[i, s, :ln]])   # BLANK_SEQ: absent-state event
+            if n_aggs:
+                pk = int(m.key[i]) if cq.partitioned else 0
+                gk = tuple(_group_key(self._eval(g, chains, store)) for g in cq.group_by)
+                self._cur_aggs = self._agg_states.setdefault((pk, gk), [None] * n_aggs)
             data = []
-            for name, typ, t in self.cq.select:
+            for name, typ, t in cq.select:
                 v = self._eval(t, chains, store)
                 data.append(v)
+            if cq.having is not None:
+                self._cur_out = data
+                if self._eval(cq.having, chains, store) is not True:
+                    continue
             out.append((int(m.trigger_seq[i]), int(m.ts[i]), data))
         return out
 

@@ -16,11 +16,6 @@ FEATURES_UNSUPPORTED = set()
 # reference tests whose apps use constructs outside the pattern hot path (SURVEY §8f / out of scope);
 # they must fail at compile time with a clear message, never silently.
 KNOWN_UNSUPPORTED = {
-    "CountPatternTestCase::testQuery17": "aggregate count() in select (SURVEY §8f row f1)",
-    "CountPatternTestCase::testQuery18": "aggregate count() in select (SURVEY §8f row f1)",
-    "CountPatternTestCase::testQuery19": "aggregate count() in select (SURVEY §8f row f1)",
-    "CountPatternTestCase::testQuery20": "aggregate count() in select (SURVEY §8f row f1)",
-    "CountPatternTestCase::testQuery14": "having + instanceOfFloat() in select (SURVEY §8f row f1)",
     "PatternPartitionTestCase::testPatternPartitionQuery30": "inner partition streams (#Stream)",
     "PatternPartitionTestCase::testPatternPartitionQuery32": "unpartitioned stream inside a partition",
     "PatternPartitionTestCase::testPatternPartitionQuery33": "non-pattern query in the app",

@@ -1,0 +1,67 @@
+"""Host QuerySelector over the match stream: aggregators, group by and having,
+per (partition key, group-by key) like the reference's partitioned state holders.  Expected values are
+worked by hand from QuerySelector.java:272-370 and the *AttributeAggregatorExecutor.java classes; the
+reference's own count()/having KATs (CountPatternTestCase testQuery14/17-20) run in
+test_oracle_kat.py / test_gpu_parity.py."""
+import importlib
+
+import pytest
+
+from oracle_backend import oracle_manager
+
+sa = importlib.import_module("siddhi-1_amd")
+
+STOCK = "define stream S (symbol string, price float, volume int);\n"
+EVENTS = [("A", 21.0, 10), ("B", 30.0, 5), ("A", 22.5, 20), ("A", 25.0, 1), ("B", 31.0, 7), ("A", 10.0, 3)]
+
+
+class _Collect(sa.StreamCallback):
+    def __init__(self):
+        self.events = []
+
+    def receive(self, events):
+        self.events += [list(e.data) for e in events]
+
+
+def _run(app):
+    rt = oracle_manager().createSiddhiAppRuntime(app)
+    cb = _Collect()
+    rt.addCallback("O", cb)
+    rt.start()
+    h = rt.getInputHandler("S")
+    for i, (s, p, v) in enumerate(EVENTS):
+        h.send(1000 + i, [s, p, v])
+    rt.shutdown()
+    return cb.events
+
+
+def test_partitioned_running_aggregates():
+    out = _run(STOCK + "partition with (symbol of S) begin "
+               "from every e1=S[price>20] -> e2=S[price>e1.price] select e1.symbol as symbol, count() as n, "
+               "sum(e2.volume) as v, avg(e2.price) as ap, min(e1.price) as lo, max(e2.price) as hi, "
+               "sum(e2.price) as sp, distinctCount(e1.price) as dc insert into O; end;")
+    assert out == [["A", 1, 20, 22.5, 21.0, 22.5, 22.5, 1],
+                   ["A", 2, 21, 23.75, 21.0, 25.0, 47.5, 2],
+                   ["B", 1, 7, 31.0, 30.0, 31.0, 31.0, 1]]
+    assert isinstance(out[0][1], int) and isinstance(out[0][2], int)   # count / sum(int) are LONG
+
+
+def test_group_by_having_unpartitioned():
+    out = _run(STOCK + "from every e1=S[price>20] -> e2=S[price>e1.price] "
+               "select e1.symbol as symbol, count() as n group by e1.symbol having n >= 2 insert into O;")
+    assert out == [["A", 2], ["A", 3]]
+
+
+def test_having_reads_inputs_and_outputs():
+    out = _run(STOCK + "from every e1=S[price>20] -> e2=S[price>e1.price] "
+               "select e1.symbol as symbol, e2.price - e1.price as d having d > 1.0f and e2.volume < 10 "
+               "insert into O;")
+    # (A21, B30) d 9; (A22.5, A25) d 2.5; (B30, B31) d == 1.0 fails `d > 1.0f`; (A25, B31) d 6
+    assert out == [["A", 9.0], ["A", 2.5], ["A", 6.0]]
+
+
+def test_unsupported_functions_fail_at_creation():
+    with pytest.raises(sa.SiddhiAppCreationException):
+        _run(STOCK + "from every e1=S[price>20] -> e2=S[price>e1.price] select foo(e1.price) as x insert into O;")
+    with pytest.raises(sa.SiddhiAppCreationException):
+        _run(STOCK + "from every e1=S[price>20] -> e2=S[price>e1.price] select sum(e1.symbol) as x insert into O;")
