@@ -9,7 +9,8 @@ The directory name is not a Python identifier; import it with
 ``importlib.import_module("siddhi-1_amd")``.
 """
 from .runtime import (Event, InputHandler, QueryCallback, SiddhiAppRuntime, SiddhiManager,  # noqa: F401
-                      StreamCallback, StringDictionary)
+                      StreamCallback, StringDictionary, InMemoryPersistenceStore,
+                      CannotRestoreSiddhiAppStateException, NoPersistenceStoreException)
 from .compiler import compile_query, SiddhiAppCreationException  # noqa: F401
 from .siddhiql import parse_app, SiddhiParserException  # noqa: F401
 from .native import NativeEngine, EngineError, load_hip_library, load_library, jit_check, HIP_LIBRARY  # noqa: F401

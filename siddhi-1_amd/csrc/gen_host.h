@@ -20,3 +20,9 @@ int gen_poll(GenEngine* e, uint32_t mem, sg_match_batch* out, std::string& msg);
 void gen_release(GenEngine* e);
 void gen_stats(GenEngine* e, sg_stats* out);
 void gen_synchronize(GenEngine* e);
+// device NFA state as a flat image (snapshot/restore, sg_engine.hip): the per-key state blocks plus the
+// clock fields.  gen_state_words = words of the block image (blockWords * K).
+struct GenClock { int64_t now, last_event_ts; uint32_t advanced, pad; };
+uint64_t gen_state_words(const GenEngine* e);
+int gen_snapshot(GenEngine* e, uint32_t* words, GenClock* clk, std::string& msg);
+int gen_restore(GenEngine* e, const uint32_t* words, const GenClock& clk, std::string& msg);

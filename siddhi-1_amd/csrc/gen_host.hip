@@ -483,6 +483,7 @@ struct GenEngine {
     void* msort_tmp = nullptr;
     size_t msort_tmp_bytes = 0;
     unsigned long long* stats = nullptr;
+    unsigned long long* live = nullptr;  // k_gen_live's sum (diagnostics)
     uint32_t* err = nullptr;
     OutBufs out{};
     std::vector<uint64_t> h_trig, h_slot;
@@ -586,6 +587,7 @@ GenEngine* gen_create(const uint32_t* ir, size_t nw, const sg_config& cfg, hipSt
         GH_OK(rocprim::merge_sort(nullptr, e->msort_tmp_bytes, e->order_in, e->order_out, (size_t)e->rawCap, lt, stream));
         e->msort_tmp = e->dalloc<uint8_t>(e->msort_tmp_bytes);
         e->stats = e->dalloc<unsigned long long>(GST_N);
+        e->live = e->dalloc<unsigned long long>(1);
         GH_OK(hipMemset(e->stats, 0, GST_N * 8));
         e->err = e->dalloc<uint32_t>(1);
         GH_OK(hipMemset(e->err, 0, 4));
@@ -800,13 +802,11 @@ void gen_release(GenEngine* e) { e->held = false; }
 void gen_stats(GenEngine* e, sg_stats* out) {
     unsigned long long s[GST_N];
     GH_OK(hipMemcpyAsync(s, e->stats, sizeof(s), hipMemcpyDeviceToHost, e->stream));
-    unsigned long long* live = nullptr;
-    GH_OK(hipMallocAsync((void**)&live, 8, e->stream));
+    unsigned long long* live = e->live;
     GH_OK(hipMemsetAsync(live, 0, 8, e->stream));
     hipLaunchKernelGGL(k_gen_live, dim3((e->K + 255) / 256), dim3(256), 0, e->stream, e->dprog, e->state, e->K, live);
     unsigned long long lv = 0;
     GH_OK(hipMemcpyAsync(&lv, live, 8, hipMemcpyDeviceToHost, e->stream));
-    GH_OK(hipFreeAsync(live, e->stream));
     GH_OK(hipStreamSynchronize(e->stream));
     *out = e->st;
     out->partials_scanned = s[GST_SCANNED];
@@ -817,3 +817,42 @@ void gen_stats(GenEngine* e, sg_stats* out) {
 }
 
 void gen_synchronize(GenEngine* e) { GH_OK(hipStreamSynchronize(e->stream)); }
+
+// Persistence of the device NFA state (the reference snapshots every pre-state
+// processor's pending / newAndEvery lists and absent-state flags per partition key,
+// StreamPreStateProcessor.java:450-469, CountPreStateProcessor.java:206-219,
+// AbsentStreamPreStateProcessor.java:328-341).  Here all of that, the per-key StateEvent/StreamEvent
+// pools and the timer queues live in the key-interleaved state blocks, so the image is the blocks plus
+// the engine clock.  Emitted matches are output, not state: both calls require that none are waiting
+// to be polled (the reference delivers callbacks before a snapshot completes).
+uint64_t gen_state_words(const GenEngine* e) { return (uint64_t)e->host.blockWords * e->K; }
+
+static bool gen_outputs_pending(GenEngine* e) {
+    unsigned long long n = 0;
+    GH_OK(hipMemcpyAsync(&n, e->out.count, 8, hipMemcpyDeviceToHost, e->stream));
+    GH_OK(hipStreamSynchronize(e->stream));
+    return n != 0;
+}
+
+int gen_snapshot(GenEngine* e, uint32_t* words, GenClock* clk, std::string& msg) {
+    if (e->held) { msg = "release the polled matches before a snapshot"; return SG_ERR_STATE; }
+    if (gen_outputs_pending(e)) { msg = "poll the emitted matches before a snapshot"; return SG_ERR_STATE; }
+    GH_OK(hipMemcpyAsync(words, e->state, gen_state_words(e) * 4, hipMemcpyDeviceToHost, e->stream));
+    GH_OK(hipStreamSynchronize(e->stream));
+    clk->now = e->now;
+    clk->last_event_ts = e->lastEventTs;
+    clk->advanced = e->advanced ? 1u : 0u;
+    clk->pad = 0;
+    return SG_OK;
+}
+
+int gen_restore(GenEngine* e, const uint32_t* words, const GenClock& clk, std::string& msg) {
+    if (e->held) { msg = "release the polled matches before a restore"; return SG_ERR_STATE; }
+    if (gen_outputs_pending(e)) { msg = "poll the emitted matches before a restore"; return SG_ERR_STATE; }
+    GH_OK(hipMemcpyAsync(e->state, words, gen_state_words(e) * 4, hipMemcpyHostToDevice, e->stream));
+    GH_OK(hipStreamSynchronize(e->stream));
+    e->now = clk.now;
+    e->lastEventTs = clk.last_event_ts;
+    e->advanced = clk.advanced != 0;
+    return SG_OK;
+}

@@ -11,29 +11,48 @@
 // ------------------------------------------------------------------------------------------------
 // segment bounds of the key-sorted batch: seg_begin[k], seg_end[k]
 // ------------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_seg_bounds(const uint32_t* __restrict__ skeys, uint32_t n,
-                                                    uint32_t n_keys, uint32_t* __restrict__ seg_begin,
-                                                    uint32_t* __restrict__ seg_end, uint32_t* __restrict__ err) {
-    // every key gets its bounds written (keys without events get an empty [i, i) at the right spot),
-    // so no memset of the bound arrays is needed per batch
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    uint32_t k = skeys[i];
+__device__ __forceinline__ void seg_bound_one(uint32_t i, uint32_t k, uint32_t prev, uint32_t next, uint32_t n,
+                                              uint32_t n_keys, uint32_t* __restrict__ seg_begin,
+                                              uint32_t* __restrict__ seg_end, uint32_t* __restrict__ err) {
     if (k >= n_keys) {  // key id outside [0, n_keys): reject the batch loudly, never write out of bounds
         atomicOr(err, (uint32_t)SGD_ERR_KEY_RANGE);
         return;
     }
-    const uint32_t prev = (i == 0) ? 0xffffffffu : skeys[i - 1];
     if (prev != k) {
         seg_begin[k] = i;
         // keys between the previous run and this one (or before the first run) have no events
         for (uint32_t g = (i == 0) ? 0u : prev + 1; g < k && g < n_keys; ++g) seg_begin[g] = seg_end[g] = i;
     }
-    const uint32_t next = (i == n - 1) ? n_keys : skeys[i + 1];
     if (next != k) {
         seg_end[k] = i + 1;
         if (i == n - 1)
             for (uint32_t g = k + 1; g < n_keys; ++g) seg_begin[g] = seg_end[g] = n;
+    }
+}
+
+// four sorted keys per thread (one 16-B load + the neighbours on either side)
+__global__ void __launch_bounds__(256) k_seg_bounds(const uint32_t* __restrict__ skeys, uint32_t n,
+                                                    uint32_t n_keys, uint32_t* __restrict__ seg_begin,
+                                                    uint32_t* __restrict__ seg_end, uint32_t* __restrict__ err) {
+    // every key gets its bounds written (keys without events get an empty [i, i) at the right spot),
+    // so no memset of the bound arrays is needed per batch
+    const uint32_t i0 = (blockIdx.x * blockDim.x + threadIdx.x) * 4u;
+    if (i0 >= n) return;
+    uint32_t k[6];  // k[0] = previous key, k[1..4] = this thread's keys, k[5] = next key
+    k[0] = (i0 == 0) ? 0xffffffffu : skeys[i0 - 1];
+    if (i0 + 4 <= n) {
+        const uint4 v = *reinterpret_cast<const uint4*>(skeys + i0);
+        k[1] = v.x; k[2] = v.y; k[3] = v.z; k[4] = v.w;
+    } else {
+        for (uint32_t q = 0; q < 4; ++q) k[q + 1] = (i0 + q < n) ? skeys[i0 + q] : 0u;
+    }
+    k[5] = (i0 + 4 < n) ? skeys[i0 + 4] : 0u;
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q) {
+        const uint32_t i = i0 + q;
+        if (i >= n) break;
+        const uint32_t next = (i == n - 1) ? n_keys : k[q + 2];
+        seg_bound_one(i, k[q + 1], (i == 0) ? 0xffffffffu : k[q], next, n, n_keys, seg_begin, seg_end, err);
     }
 }
 
@@ -74,42 +93,58 @@ __global__ void __launch_bounds__(256) k_order_sums(const uint64_t* __restrict__
 }
 
 __global__ void __launch_bounds__(256) k_order_scatter(const ScatterParams s, uint32_t ntiles) {
-    __shared__ uint32_t wtot[4];
+    // all rows' descriptors, keys and timestamps are loaded up front (independent loads in flight
+    // together), the 16 rows' wave scans are combined through one LDS round trip, then the writes
+    constexpr int ROWS = SGD_ORDER_TILE / 256;
+    __shared__ uint32_t wtot[ROWS][4];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t base = blockIdx.x * SGD_ORDER_TILE;
+    uint64_t d[ROWS];
+    uint32_t key[ROWS];
+    int64_t ts[ROWS];
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j) {
+        const uint32_t t = base + j * 256 + threadIdx.x;
+        const bool in = t < s.n;
+        d[j] = in ? s.t_desc[t] : 0ull;
+        key[j] = (in && s.key) ? s.key[t] : 0u;
+        ts[j] = in ? s.ts[t] : 0;
+    }
+    uint32_t incl[ROWS];
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j) {
+        incl[j] = ord_wave_incl_scan((uint32_t)(d[j] >> 32), lane);
+        if (lane == 63) wtot[j][wv] = incl[j];
+    }
+    __syncthreads();
     const uint64_t out0 = *s.out_count + s.tile_off[blockIdx.x];
     uint32_t running = 0;
-    for (uint32_t j = 0; j < SGD_ORDER_TILE / 256; ++j) {
-        const uint32_t t = base + j * 256 + threadIdx.x;
-        const uint64_t d = t < s.n ? s.t_desc[t] : 0ull;
-        const uint32_t c = (uint32_t)(d >> 32);
-        const uint32_t incl = ord_wave_incl_scan(c, lane);
-        __syncthreads();  // the previous row's wtot reads are done
-        if (lane == 63) wtot[wv] = incl;
-        __syncthreads();
+#pragma unroll
+    for (int j = 0; j < ROWS; ++j) {
         uint32_t before = 0, row = 0;
+#pragma unroll
         for (int w = 0; w < 4; ++w) {
-            const uint32_t x = wtot[w];
+            const uint32_t x = wtot[j][w];
             before += (w < wv) ? x : 0u;
             row += x;
         }
+        const uint32_t c = (uint32_t)(d[j] >> 32);
         if (c) {
-            const uint64_t o = out0 + running + before + incl - c;
+            const uint32_t t = base + j * 256 + threadIdx.x;
+            const uint64_t o = out0 + running + before + incl[j] - c;
             s.t_desc[t] = 0;
             if (o + c > s.capacity) {
                 atomicOr(s.err, (uint32_t)SGD_ERR_MATCH_CAP);
             } else {
-                const uint32_t f = (uint32_t)d;
+                const uint32_t f = (uint32_t)d[j];
                 const uint64_t trig = s.seq_base + t;
-                const uint32_t key = s.key ? s.key[t] : 0u;
-                const int64_t ts = s.ts[t];
                 for (uint32_t r = 0; r < c; ++r) {
                     const uint64_t q = o + r;
                     s.o_trig[q] = trig;
-                    s.o_slot[2 * q] = s.raw_e1[f + r];
-                    s.o_slot[2 * q + 1] = trig;
-                    s.o_key[q] = key;
-                    s.o_ts[q] = ts;  // StreamPostStateProcessor.java:68: StateEvent ts = ts of the e2 event
+                    // {e1 seq, e2 seq} as one 16-B store
+                    *reinterpret_cast<ulonglong2*>(s.o_slot + 2 * q) = make_ulonglong2(s.raw_e1[f + r], trig);
+                    s.o_key[q] = key[j];
+                    s.o_ts[q] = ts[j];  // StreamPostStateProcessor.java:68: StateEvent ts = ts of the e2 event
                 }
             }
         }
@@ -149,7 +184,7 @@ __global__ void __launch_bounds__(1024) k_stats_reduce(const unsigned long long*
 int sgd_launch_bounds(const uint32_t* skeys, uint32_t n, uint32_t n_keys, uint32_t* seg_begin, uint32_t* seg_end,
                       uint32_t* err, ihipStream_t* stream) {
     if (n == 0) return 0;
-    hipLaunchKernelGGL(k_seg_bounds, dim3((n + 255) / 256), dim3(256), 0, stream, skeys, n, n_keys, seg_begin,
+    hipLaunchKernelGGL(k_seg_bounds, dim3((n + 1023) / 1024), dim3(256), 0, stream, skeys, n, n_keys, seg_begin,
                        seg_end, err);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

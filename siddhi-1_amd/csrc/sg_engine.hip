@@ -179,6 +179,7 @@ struct sg_engine {
     GenEngine* gen = nullptr;  // the general engine, when the query is not a two-state pattern
     sg_config cfg{};
     std::vector<uint32_t> ir;
+    uint64_t ir_hash = 0;  // FNV-1a of the IR words: a snapshot restores only into the same query
     std::vector<IRStream> streams;
     Plan plan;
     uint32_t K = 1, cap = 64, maxb = 0;
@@ -912,6 +913,8 @@ int sg_engine_create(const void* ir, size_t ir_len, const sg_config* cfg, sg_eng
         // every shape must lower onto the general engine (validates the IR); the specialised
         // two-state kernel takes the shapes it covers
         delete gen_build_program((const uint32_t*)ir, ir_len / 4, e->cap);
+        e->ir_hash = 1469598103934665603ull;
+        for (size_t i = 0; i < ir_len / 4; i++) e->ir_hash = (e->ir_hash ^ ((const uint32_t*)ir)[i]) * 1099511628211ull;
         bool general = getenv("SG_FORCE_GENERAL") != nullptr;
         if (!general) {
             try {
@@ -1050,13 +1053,160 @@ int sg_get_stats(sg_engine* e, sg_stats* out) {
     }
 }
 
-int sg_snapshot(sg_engine* e, void** buf, size_t* len) {
-    (void)e; (void)buf; (void)len;
-    return fail(SG_ERR_UNSUPPORTED, "snapshot of device NFA state is SURVEY §8f row f3 (not built yet)");
+// ---- persistence -------------------------------------------------------------
+// The reference snapshots, per partition key, each pre-state processor's pending and newAndEvery lists
+// (StreamPreStateProcessor.StreamPreState.snapshot/restore, StreamPreStateProcessor.java:450-469) through
+// PartitionStateHolder (util/snapshot/state/PartitionStateHolder.java:43-80).  The device keeps exactly
+// that state in HBM, so the image is a header plus the state buffers:
+//   two-state kernel: hdr[K] (list counts, start-state seeds, init bit) and the first `rows` rows of
+//     every slab plane (partial j of key k at j*K + k; rows = the deepest key's pending + staged count)
+//   general kernel:  the interleaved per-key state blocks and the engine clock (gen_snapshot).
+// Matches are output, not state: a snapshot or restore with matches waiting to be polled fails with
+// SG_ERR_STATE (the reference has delivered its callbacks by the time a snapshot completes).  A
+// restore needs an engine created from the same IR with the same n_keys; the two-state image needs
+// partial_capacity >= rows, the general one the same partial_capacity (block layout).
+struct SnapHeader {
+    uint32_t magic;       // SG_SNAP_MAGIC
+    uint32_t version;
+    uint32_t kind;        // 1 = two-state kernel, 2 = general kernel
+    uint32_t K;
+    uint64_t ir_hash;
+    uint32_t cap;         // partial_capacity of the source engine
+    uint32_t rows;        // two-state: slab rows in the image
+    uint32_t n_capw;
+    uint32_t nullable;
+    uint64_t next_seq;    // sequence numbers must keep increasing across a restore
+    uint32_t have_base;
+    uint32_t pad;
+    GenClock clk;
+    uint64_t body_bytes;
+};
+#define SG_SNAP_MAGIC 0x4e534753u  // "SGSN"
+#define SG_SNAP_VERSION 1u
+
+static bool outputs_pending(sg_engine* e) {
+    unsigned long long n = 0;
+    HIP_OK(hipMemcpyAsync(&n, e->out_count, 8, hipMemcpyDeviceToHost, e->stream));
+    HIP_OK(hipStreamSynchronize(e->stream));
+    return n != 0;
 }
+
+int sg_snapshot(sg_engine* e, void** buf, size_t* len) {
+    if (!e || !buf || !len) return fail(SG_ERR_INVALID, "null argument");
+    try {
+        HIP_OK(hipSetDevice(e->device));
+        SnapHeader h{};
+        h.magic = SG_SNAP_MAGIC;
+        h.version = SG_SNAP_VERSION;
+        h.K = e->gen ? 0 : e->K;
+        h.ir_hash = e->ir_hash;
+        h.next_seq = e->next_seq;
+        h.have_base = e->have_base ? 1u : 0u;
+        if (e->gen) {
+            h.kind = 2;
+            const uint64_t words = gen_state_words(e->gen);
+            h.body_bytes = words * 4;
+            uint8_t* out = (uint8_t*)malloc(sizeof(h) + h.body_bytes);
+            if (!out) return fail(SG_ERR_CAPACITY, "snapshot buffer allocation failed");
+            std::string msg;
+            const int rc = gen_snapshot(e->gen, (uint32_t*)(out + sizeof(h)), &h.clk, msg);
+            if (rc != SG_OK) { free(out); return fail(rc, msg); }
+            h.cap = e->cap;
+            h.K = e->cfg.n_keys ? e->cfg.n_keys : 1;
+            memcpy(out, &h, sizeof(h));
+            *buf = out;
+            *len = sizeof(h) + h.body_bytes;
+            return SG_OK;
+        }
+        if (e->held) return fail(SG_ERR_STATE, "release the polled matches before a snapshot");
+        if (outputs_pending(e)) return fail(SG_ERR_STATE, "poll the emitted matches before a snapshot");
+        const size_t K = e->K;
+        std::vector<uint32_t> hdr(K);
+        HIP_OK(hipMemcpy(hdr.data(), e->hdr, K * 4, hipMemcpyDeviceToHost));
+        uint32_t rows = 0;
+        for (uint32_t x : hdr) rows = std::max(rows, (uint32_t)(SGD_H_NPEND(x) + SGD_H_NSTG(x)));
+        h.kind = 1;
+        h.cap = e->cap;
+        h.rows = rows;
+        h.n_capw = e->n_capw;
+        h.nullable = e->nullable ? 1u : 0u;
+        const size_t plane = (size_t)rows * K;  // elements per saved plane
+        h.body_bytes = K * 4 + plane * (8 + 8 + 4 * (size_t)e->n_capw + 4);
+        uint8_t* out = (uint8_t*)malloc(sizeof(h) + h.body_bytes);
+        if (!out) return fail(SG_ERR_CAPACITY, "snapshot buffer allocation failed");
+        uint8_t* q = out + sizeof(h);
+        memcpy(q, hdr.data(), K * 4);
+        q += K * 4;
+        HIP_OK(hipMemcpyAsync(q, e->p_ts, plane * 8, hipMemcpyDeviceToHost, e->stream));
+        q += plane * 8;
+        HIP_OK(hipMemcpyAsync(q, e->p_seq, plane * 8, hipMemcpyDeviceToHost, e->stream));
+        q += plane * 8;
+        for (uint32_t w = 0; w < e->n_capw; w++) {
+            HIP_OK(hipMemcpyAsync(q, e->p_capw + (size_t)w * e->cap * K, plane * 4, hipMemcpyDeviceToHost, e->stream));
+            q += plane * 4;
+        }
+        HIP_OK(hipMemcpyAsync(q, e->p_capnull, plane * 4, hipMemcpyDeviceToHost, e->stream));
+        HIP_OK(hipStreamSynchronize(e->stream));
+        memcpy(out, &h, sizeof(h));
+        *buf = out;
+        *len = sizeof(h) + h.body_bytes;
+        return SG_OK;
+    } catch (const std::exception& ex) {
+        return fail(SG_ERR_DEVICE, ex.what());
+    }
+}
+
 int sg_restore(sg_engine* e, const void* buf, size_t len) {
-    (void)e; (void)buf; (void)len;
-    return fail(SG_ERR_UNSUPPORTED, "restore of device NFA state is SURVEY §8f row f3 (not built yet)");
+    if (!e || !buf) return fail(SG_ERR_INVALID, "null argument");
+    SnapHeader h;
+    if (len < sizeof(h)) return fail(SG_ERR_INVALID, "snapshot too short");
+    memcpy(&h, buf, sizeof(h));
+    if (h.magic != SG_SNAP_MAGIC || h.version != SG_SNAP_VERSION) return fail(SG_ERR_INVALID, "not a snapshot of this engine version");
+    if (len != sizeof(h) + h.body_bytes) return fail(SG_ERR_INVALID, "snapshot length does not match its header");
+    if (h.ir_hash != e->ir_hash) return fail(SG_ERR_INVALID, "snapshot of a different query");
+    if (h.kind != (e->gen ? 2u : 1u)) return fail(SG_ERR_INVALID, "snapshot of a different engine kind");
+    const uint8_t* q = (const uint8_t*)buf + sizeof(h);
+    try {
+        HIP_OK(hipSetDevice(e->device));
+        if (e->gen) {
+            const uint64_t K = e->cfg.n_keys ? e->cfg.n_keys : 1;
+            const uint64_t words = gen_state_words(e->gen);
+            if (h.K != K || h.body_bytes != words * 4)
+                return fail(SG_ERR_INVALID, "snapshot taken with a different n_keys / partial_capacity");
+            std::string msg;
+            const int rc = gen_restore(e->gen, (const uint32_t*)q, h.clk, msg);
+            if (rc != SG_OK) return fail(rc, msg);
+        } else {
+            const size_t K = e->K;
+            if (h.K != K) return fail(SG_ERR_INVALID, "snapshot taken with a different n_keys");
+            if (h.rows > e->cap) return fail(SG_ERR_CAPACITY, "snapshot holds more partials per key than partial_capacity");
+            if (h.n_capw != e->n_capw) return fail(SG_ERR_INVALID, "snapshot capture layout differs");
+            const size_t plane = (size_t)h.rows * K;
+            if (h.body_bytes != K * 4 + plane * (8 + 8 + 4 * (size_t)h.n_capw + 4))
+                return fail(SG_ERR_INVALID, "snapshot body size does not match its header");
+            if (e->held) return fail(SG_ERR_STATE, "release the polled matches before a restore");
+            if (outputs_pending(e)) return fail(SG_ERR_STATE, "poll the emitted matches before a restore");
+            HIP_OK(hipMemcpyAsync(e->hdr, q, K * 4, hipMemcpyHostToDevice, e->stream));
+            q += K * 4;
+            HIP_OK(hipMemcpyAsync(e->p_ts, q, plane * 8, hipMemcpyHostToDevice, e->stream));
+            q += plane * 8;
+            HIP_OK(hipMemcpyAsync(e->p_seq, q, plane * 8, hipMemcpyHostToDevice, e->stream));
+            q += plane * 8;
+            for (uint32_t w = 0; w < h.n_capw; w++) {
+                HIP_OK(hipMemcpyAsync(e->p_capw + (size_t)w * e->cap * K, q, plane * 4, hipMemcpyHostToDevice, e->stream));
+                q += plane * 4;
+            }
+            HIP_OK(hipMemcpyAsync(e->p_capnull, q, plane * 4, hipMemcpyHostToDevice, e->stream));
+            HIP_OK(hipStreamSynchronize(e->stream));
+            if (h.nullable) e->nullable = true;
+        }
+        e->next_seq = h.next_seq;
+        e->have_base = h.have_base != 0;
+        e->poll_base = e->next_seq;
+        return SG_OK;
+    } catch (const std::exception& ex) {
+        return fail(SG_ERR_DEVICE, ex.what());
+    }
 }
 int sg_free_buffer(void* buf) {
     free(buf);

@@ -214,6 +214,24 @@ class NativeEngine:
         if self._sync is not None:
             self._check(self._sync(self.h))
 
+    def snapshot(self) -> bytes:
+        """Image of the device NFA state (sg_snapshot; poll the matches first)."""
+        f, free = getattr(self.lib, self.p + "snapshot"), self.lib.sg_free_buffer
+        f.argtypes = [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]
+        free.argtypes = [C.c_void_p]
+        buf, n = C.c_void_p(), C.c_size_t()
+        self._check(f(self.h, C.byref(buf), C.byref(n)))
+        try:
+            return C.string_at(buf, n.value)
+        finally:
+            free(buf)
+
+    def restore(self, image: bytes):
+        """Replace the engine's NFA state with a snapshot of an engine of the same query (sg_restore)."""
+        f = getattr(self.lib, self.p + "restore")
+        f.argtypes = [C.c_void_p, C.c_char_p, C.c_size_t]
+        self._check(f(self.h, image, len(image)))
+
     def stats(self):
         s = sg_stats()
         self._check(self._stats(self.h, C.byref(s)))

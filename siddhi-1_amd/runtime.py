@@ -18,6 +18,7 @@ host (QuerySelector.processNoGroupBy, C/query/selector/QuerySelector.java:162-20
 """
 from __future__ import annotations
 
+import json
 import re
 import struct
 import time
@@ -419,9 +420,96 @@ class InputHandler:
             self.app_rt._send(self.stream, [(self.app_rt.wall_time(), list(a))], explicit=False)
 
 
+# ------------------------------------------------------------------------------------------------
+# persistence (SiddhiAppRuntime.snapshot/restore, SnapshotService.java:91,334): the host's state
+# (event store rows the device partials still reference, dictionaries, clocks, aggregator states) as
+# tagged JSON, followed by one device image per query (sg_snapshot).  Exact for every value type the
+# path carries: floats travel as their hex form, numpy scalars keep their width.
+# ------------------------------------------------------------------------------------------------
+_SNAP_MAGIC = b"SGAP\x01\x00\x00\x00"
+
+
+def _enc(v):
+    if v is None or isinstance(v, (str, bool)):
+        return v if not isinstance(v, bool) else {"b": v}
+    if isinstance(v, np.floating):
+        return {"f%d" % v.dtype.itemsize: float(v).hex()}
+    if isinstance(v, np.integer):
+        return {"i%d" % v.dtype.itemsize: int(v)}
+    if isinstance(v, int):
+        return v
+    if isinstance(v, float):
+        return {"f": v.hex()}
+    if isinstance(v, tuple):
+        return {"t": [_enc(x) for x in v]}
+    if isinstance(v, list):
+        return [_enc(x) for x in v]
+    if isinstance(v, dict):
+        return {"d": [[_enc(k), _enc(x)] for k, x in v.items()]}
+    raise TypeError(f"cannot snapshot a value of type {type(v).__name__}")
+
+
+_NP_INT = {1: np.int8, 2: np.int16, 4: np.int32, 8: np.int64}
+
+
+def _dec(v):
+    if isinstance(v, list):
+        return [_dec(x) for x in v]
+    if not isinstance(v, dict):
+        return v
+    (tag, x), = v.items()
+    if tag == "b":
+        return bool(x)
+    if tag == "f":
+        return float.fromhex(x)
+    if tag == "f4":
+        return np.float32(float.fromhex(x))
+    if tag == "f8":
+        return np.float64(float.fromhex(x))
+    if tag[0] == "i":
+        return _NP_INT[int(tag[1:])](x)
+    if tag == "t":
+        return tuple(_dec(y) for y in x)
+    if tag == "d":
+        return {_dec(k): _dec(y) for k, y in x}
+    raise ValueError(f"bad snapshot tag {tag!r}")
+
+
+class InMemoryPersistenceStore:
+    """io.siddhi.core.util.persistence.InMemoryPersistenceStore: revisions per app name."""
+
+    def __init__(self):
+        self.revisions: Dict[str, List[bytes]] = {}
+
+    def save(self, app_name, revision, snapshot):
+        self.revisions.setdefault(app_name, []).append((revision, snapshot))
+
+    def load(self, app_name, revision):
+        for r, snap in self.revisions.get(app_name, []):
+            if r == revision:
+                return snap
+        return None
+
+    def getLastRevision(self, app_name):
+        revs = self.revisions.get(app_name)
+        return revs[-1][0] if revs else None
+
+
+class CannotRestoreSiddhiAppStateException(RuntimeError):
+    pass
+
+
+class NoPersistenceStoreException(RuntimeError):
+    pass
+
+
 class SiddhiAppRuntime:
-    def __init__(self, text, engine_factory, n_keys=1 << 16):
+    def __init__(self, text, engine_factory, n_keys=1 << 16, persistence_store=None):
         self.app = q.parse_app(text)
+        nm = [a for a in self.app.annotations if a.name.lower() == "app:name"]
+        self.name = (nm[0].elements[0][1] if nm and nm[0].elements else None) or "siddhi-app"
+        self.persistence_store = persistence_store
+        self._revision = 0
         self.n_keys = n_keys
         self.strings = StringDictionary()
         self.store = _EventStore()
@@ -506,6 +594,79 @@ class SiddhiAppRuntime:
             self._event_time = ts
             self._fire_timers(ts)
             self._last_sys = self.wall_time()
+
+    def snapshot(self) -> bytes:
+        """SiddhiAppRuntime.snapshot(): the app's pattern state as bytes (device NFA images included)."""
+        head = {
+            "app": self.name,
+            "strings": self.strings.strs,
+            "rows": [[st, int(ts), _enc(tuple(d))] for st, ts, d in self.store.rows],
+            "event_time": self._event_time,
+            "last_sys": self._last_sys,
+            "queries": [{"keys": list(qr.key_dict.keys()) if qr.key_dict is not None else None,
+                         "aggs": _enc(qr._agg_states)} for qr in self.queries],
+        }
+        js = json.dumps(head).encode()
+        parts = [_SNAP_MAGIC, struct.pack("<Q", len(js)), js]
+        for qr in self.queries:
+            img = qr.engine.snapshot()
+            parts += [struct.pack("<Q", len(img)), img]
+        return b"".join(parts)
+
+    def restore(self, snap: bytes):
+        """SiddhiAppRuntime.restore(byte[]): replace the app's pattern state with a snapshot taken from
+        a runtime of the same app text."""
+        try:
+            if snap[:8] != _SNAP_MAGIC:
+                raise ValueError("not a snapshot of this runtime")
+            (n,) = struct.unpack_from("<Q", snap, 8)
+            head = json.loads(snap[16:16 + n].decode())
+            if len(head["queries"]) != len(self.queries):
+                raise ValueError("snapshot of a different app")
+            off, imgs = 16 + n, []
+            for _ in self.queries:
+                (m,) = struct.unpack_from("<Q", snap, off)
+                imgs.append(snap[off + 8:off + 8 + m])
+                off += 8 + m
+            for qr, img in zip(self.queries, imgs):
+                qr.engine.restore(img)
+        except (ValueError, KeyError, struct.error) as ex:
+            raise CannotRestoreSiddhiAppStateException(f"Restoring of Siddhi app {self.name} failed: {ex}")
+        self.strings.strs = list(head["strings"])
+        self.strings.ids = {x: i for i, x in enumerate(self.strings.strs)}
+        self.store.rows = [(st, ts, _dec(d)) for st, ts, d in head["rows"]]
+        self._event_time = head["event_time"]
+        self._last_sys = head["last_sys"]
+        for qr, qs in zip(self.queries, head["queries"]):
+            if qr.key_dict is not None:
+                qr.key_dict.clear()
+                qr.key_dict.update({k: i for i, k in enumerate(qs["keys"])})
+            qr._agg_states = _dec(qs["aggs"])
+
+    def persist(self):
+        """SiddhiAppRuntime.persist(): snapshot into the manager's persistence store; returns the revision."""
+        if self.persistence_store is None:
+            raise NoPersistenceStoreException(f"No persistence store assigned for siddhi app {self.name}")
+        self._revision += 1
+        rev = f"{int(time.time() * 1000)}_{self.name}_{self._revision}"
+        self.persistence_store.save(self.name, rev, self.snapshot())
+        return rev
+
+    def restoreRevision(self, revision):
+        if self.persistence_store is None:
+            raise NoPersistenceStoreException(f"No persistence store assigned for siddhi app {self.name}")
+        snap = self.persistence_store.load(self.name, revision)
+        if snap is None:
+            raise CannotRestoreSiddhiAppStateException(f"no revision {revision} of {self.name}")
+        self.restore(snap)
+
+    def restoreLastRevision(self):
+        if self.persistence_store is None:
+            raise NoPersistenceStoreException(f"No persistence store assigned for siddhi app {self.name}")
+        rev = self.persistence_store.getLastRevision(self.name)
+        if rev is not None:
+            self.restoreRevision(rev)
+        return rev
 
     def shutdown(self):
         for qr in self.queries:
@@ -629,9 +790,13 @@ class SiddhiManager:
                                     partial_capacity=partial_capacity, device=device)
         self.engine_factory = engine_factory
         self.n_keys = n_keys
+        self.persistence_store = None
+
+    def setPersistenceStore(self, store):
+        self.persistence_store = store
 
     def createSiddhiAppRuntime(self, text) -> SiddhiAppRuntime:
-        return SiddhiAppRuntime(text, self.engine_factory, self.n_keys)
+        return SiddhiAppRuntime(text, self.engine_factory, self.n_keys, self.persistence_store)
 
     create_siddhi_app_runtime = createSiddhiAppRuntime
 

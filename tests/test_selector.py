@@ -65,3 +65,27 @@ def test_unsupported_functions_fail_at_creation():
         _run(STOCK + "from every e1=S[price>20] -> e2=S[price>e1.price] select foo(e1.price) as x insert into O;")
     with pytest.raises(sa.SiddhiAppCreationException):
         _run(STOCK + "from every e1=S[price>20] -> e2=S[price>e1.price] select sum(e1.symbol) as x insert into O;")
+
+
+# ------------------------------------------------------------------------------------------------
+# persistence host side (SiddhiAppRuntime.snapshot/persist; the device images are GPU tests in
+# test_gpu_snapshot.py)
+# ------------------------------------------------------------------------------------------------
+def test_snapshot_value_encoding_round_trips():
+    import numpy as np
+    rt = importlib.import_module("siddhi-1_amd.runtime")
+    vals = [None, True, False, 0, -(1 << 63), (1 << 64) - 1, 0.1, float("inf"), -0.0, np.float32(25.6),
+            np.float64(1e-300), np.int32(-7), np.int64(1 << 40), "WSO2", ("a", None, np.float32(1.5)),
+            {("k", "g"): [{"n": 1, "v": 2.5, "d": {np.float32(3.0): 2}}]}]
+    for v in vals:
+        w = rt._dec(rt._enc(v))
+        assert type(w) is type(v) and repr(w) == repr(v), (v, w)
+
+
+def test_persist_without_store_raises():
+    """PersistenceTestCase.persistenceTest3: persist() with no persistence store"""
+    r = oracle_manager().createSiddhiAppRuntime(STOCK + "from every e1=S[price>20] -> e2=S[price>e1.price] "
+                                                "select e1.price as a insert into O;")
+    with pytest.raises(sa.NoPersistenceStoreException):
+        r.persist()
+    r.shutdown()
