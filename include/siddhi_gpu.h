@@ -136,6 +136,16 @@ int sg_poll_matches(sg_engine* e, uint32_t mem, sg_match_batch* out);
 int sg_release_matches(sg_engine* e, sg_match_batch* m);
 int sg_get_stats(sg_engine* e, sg_stats* out);
 int sg_synchronize(sg_engine* e);
+/* Partition purge (@purge(enable, interval, idle.period) on a partition; PartitionRuntimeImpl.java:368-401
+ * removes idle keys and cleanGroupByStates() every state holder of the partition's queries, so the
+ * key's next event runs initPartition again).  The host tracks last-seen times and picks the idle
+ * keys; this resets their NFA state (pending / newAndEvery lists, count chains, absent-state flags and
+ * timers) to that of a key never seen.  keys: n key ids in host (SG_MEM_HOST) or device memory;
+ * ids outside [0, n_keys) fail with SG_ERR_INVALID. */
+int sg_reset_keys(sg_engine* e, const uint32_t* keys, uint64_t n, uint32_t mem);
+/* Persistence (SnapshotService.java:91,334 -> StreamPreStateProcessor.java:450-469 per key): an image
+ * of the device NFA state (library-owned until sg_free_buffer), restorable into an engine created from
+ * the same IR with the same n_keys.  Both fail with SG_ERR_STATE while matches wait to be polled. */
 int sg_snapshot(sg_engine* e, void** buf, size_t* len);
 int sg_restore(sg_engine* e, const void* buf, size_t len);
 int sg_free_buffer(void* buf);

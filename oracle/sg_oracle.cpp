@@ -1543,6 +1543,27 @@ int sgo_engine_create(const void* ir, size_t ir_len, const sg_config* cfg, sgo_e
 
 void sgo_engine_destroy(sgo_engine* h) { delete h; }
 
+// partition purge (PartitionRuntimeImpl.java:368-401): the key is removed from partitionKeys and every
+// state holder of the partition's queries drops its states (cleanGroupByStates), the schedulers' per-key
+// queues included; its next event runs initPartition again
+int sgo_reset_keys(sgo_engine* h, const uint32_t* keys, uint64_t n, uint32_t mem) {
+    if (!h || (!keys && n)) return fail(SG_ERR_INVALID, "null argument");
+    if (mem != SG_MEM_HOST) return fail(SG_ERR_INVALID, "oracle takes host key lists only");
+    Engine& e = h->e;
+    if (!e.partitioned) return SG_OK;
+    for (uint64_t i = 0; i < n; i++) {
+        const uint32_t k = keys[i];
+        if (k >= e.keyStates.size()) continue;  // never seen: nothing to drop
+        e.keyStates[k].clear();
+        e.keyInit[k] = 0;
+        for (auto& hs : e.heads)
+            for (auto it = hs.begin(); it != hs.end();) it = (it->second == k) ? hs.erase(it) : std::next(it);
+        for (auto it = e.callers.begin(); it != e.callers.end();)
+            it = (std::get<1>(*it) == k) ? e.callers.erase(it) : std::next(it);
+    }
+    return SG_OK;
+}
+
 int sgo_push_batch(sgo_engine* h, const sg_batch* b) {
     if (!h || !b) return fail(SG_ERR_INVALID, "null argument");
     Engine& e = h->e;

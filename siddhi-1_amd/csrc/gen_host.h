@@ -24,5 +24,8 @@ void gen_synchronize(GenEngine* e);
 // clock fields.  gen_state_words = words of the block image (blockWords * K).
 struct GenClock { int64_t now, last_event_ts; uint32_t advanced, pad; };
 uint64_t gen_state_words(const GenEngine* e);
+// partition purge: the listed keys' state blocks back to the never-seen (all-zero) state; keys is a
+// device array of n ids already range-checked by the caller
+int gen_reset_keys(GenEngine* e, const uint32_t* keys, uint32_t n, std::string& msg);
 int gen_snapshot(GenEngine* e, uint32_t* words, GenClock* clk, std::string& msg);
 int gen_restore(GenEngine* e, const uint32_t* words, const GenClock& clk, std::string& msg);

@@ -825,6 +825,25 @@ void gen_synchronize(GenEngine* e) { GH_OK(hipStreamSynchronize(e->stream)); }
 // pools and the timer queues live in the key-interleaved state blocks, so the image is the blocks plus
 // the engine clock.  Emitted matches are output, not state: both calls require that none are waiting
 // to be polled (the reference delivers callbacks before a snapshot completes).
+// one thread per (listed key, block word): word w of key k lives at w * K + k
+__global__ void __launch_bounds__(256) k_gen_reset(const uint32_t* __restrict__ keys, uint32_t n, uint32_t words,
+                                                   uint32_t K, uint32_t* __restrict__ state) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (uint64_t)n * words) return;
+    const uint32_t w = (uint32_t)(i / n), k = keys[i % n];
+    state[(size_t)w * K + k] = 0u;
+}
+
+int gen_reset_keys(GenEngine* e, const uint32_t* keys, uint32_t n, std::string& msg) {
+    (void)msg;
+    if (n == 0 || !e->host.partitioned) return SG_OK;
+    const uint64_t total = (uint64_t)n * e->host.blockWords;
+    hipLaunchKernelGGL(k_gen_reset, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, e->stream, keys, n,
+                       (uint32_t)e->host.blockWords, e->K, e->state);
+    GH_OK(hipGetLastError());
+    return SG_OK;
+}
+
 uint64_t gen_state_words(const GenEngine* e) { return (uint64_t)e->host.blockWords * e->K; }
 
 static bool gen_outputs_pending(GenEngine* e) {

@@ -153,6 +153,20 @@ __global__ void __launch_bounds__(256) k_order_scatter(const ScatterParams s, ui
     if (blockIdx.x == ntiles - 1 && threadIdx.x == 0) *s.batch_total = (unsigned long long)s.tile_off[blockIdx.x] + running;
 }
 
+// partition purge: the listed keys' headers go back to "never seen" (INIT clear, no partials); the
+// slab rows they held are dead once the counts are zero
+__global__ void __launch_bounds__(256) k_reset_keys(const uint32_t* __restrict__ keys, uint32_t n, uint32_t n_keys,
+                                                    uint32_t* __restrict__ hdr, uint32_t* __restrict__ err) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t k = keys[i];
+    if (k >= n_keys) {
+        atomicOr(err, (uint32_t)SGD_ERR_KEY_RANGE);
+        return;
+    }
+    hdr[k] = 0u;
+}
+
 __global__ void k_bump(unsigned long long* out_count, const unsigned long long* batch_total) {
     *out_count += *batch_total;
 }
@@ -186,6 +200,13 @@ int sgd_launch_bounds(const uint32_t* skeys, uint32_t n, uint32_t n_keys, uint32
     if (n == 0) return 0;
     hipLaunchKernelGGL(k_seg_bounds, dim3((n + 1023) / 1024), dim3(256), 0, stream, skeys, n, n_keys, seg_begin,
                        seg_end, err);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int sgd_launch_reset_keys(const uint32_t* keys, uint32_t n, uint32_t n_keys, uint32_t* hdr, uint32_t* err,
+                          ihipStream_t* stream) {
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(k_reset_keys, dim3((n + 255) / 256), dim3(256), 0, stream, keys, n, n_keys, hdr, err);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -137,6 +137,9 @@ struct ScatterParams {
 // scan_bytes), then the tile-local scan + scatter; also bumps out_count
 int sgd_launch_scatter(const ScatterParams& s, void* scan_tmp, size_t scan_bytes, ihipStream_t* stream);
 size_t sgd_scatter_scan_bytes(uint32_t max_n);
+// partition purge: hdr[keys[i]] = 0 (key range errors -> err)
+int sgd_launch_reset_keys(const uint32_t* keys, uint32_t n, uint32_t n_keys, uint32_t* hdr, uint32_t* err,
+                          ihipStream_t* stream);
 // sums the staged pass's per-wave counters of one batch into stats[SGD_ST_N]
 int sgd_launch_stats_reduce(const unsigned long long* wstats, uint32_t n_waves, unsigned long long* stats,
                             ihipStream_t* stream);

@@ -1053,6 +1053,46 @@ int sg_get_stats(sg_engine* e, sg_stats* out) {
     }
 }
 
+// ---- partition purge (PartitionRuntimeImpl.java:368-401) ----------------------------------------
+int sg_reset_keys(sg_engine* e, const uint32_t* keys, uint64_t n, uint32_t mem) {
+    if (!e || (!keys && n)) return fail(SG_ERR_INVALID, "null argument");
+    if (n == 0) return SG_OK;
+    if (n >= (1ull << 32)) return fail(SG_ERR_INVALID, "too many keys in one reset");
+    try {
+        HIP_OK(hipSetDevice(e->device));
+        if (e->held) return fail(SG_ERR_STATE, "release the polled matches before resetting keys");
+        const uint32_t K = e->gen ? (e->cfg.n_keys ? e->cfg.n_keys : 1) : e->K;
+        const uint32_t* dk = keys;
+        uint32_t* tmp = nullptr;
+        if (mem == SG_MEM_HOST) {
+            for (uint64_t i = 0; i < n; i++)
+                if (keys[i] >= K) return fail(SG_ERR_INVALID, "key id outside [0, n_keys)");
+            HIP_OK(hipMalloc(&tmp, n * 4));
+            HIP_OK(hipMemcpyAsync(tmp, keys, n * 4, hipMemcpyHostToDevice, e->stream));
+            dk = tmp;
+        }
+        int rc = SG_OK;
+        std::string msg;
+        if (e->gen) {
+            rc = gen_reset_keys(e->gen, dk, (uint32_t)n, msg);
+        } else if (e->plan.partitioned) {
+            if (sgd_launch_reset_keys(dk, (uint32_t)n, e->K, e->hdr, e->err, e->stream) != 0) rc = SG_ERR_DEVICE;
+            msg = "k_reset_keys launch failed";
+        }
+        HIP_OK(hipStreamSynchronize(e->stream));
+        if (tmp) HIP_OK(hipFree(tmp));
+        if (rc != SG_OK) return fail(rc, msg);
+        if (!e->gen) {
+            uint32_t err = 0;
+            HIP_OK(hipMemcpy(&err, e->err, 4, hipMemcpyDeviceToHost));
+            if (err & SGD_ERR_KEY_RANGE) return fail(SG_ERR_INVALID, "key id outside [0, n_keys)");
+        }
+        return SG_OK;
+    } catch (const std::exception& ex) {
+        return fail(SG_ERR_DEVICE, ex.what());
+    }
+}
+
 // ---- persistence -------------------------------------------------------------
 // The reference snapshots, per partition key, each pre-state processor's pending and newAndEvery lists
 // (StreamPreStateProcessor.StreamPreState.snapshot/restore, StreamPreStateProcessor.java:450-469) through

@@ -214,6 +214,13 @@ class NativeEngine:
         if self._sync is not None:
             self._check(self._sync(self.h))
 
+    def reset_keys(self, keys):
+        """Partition purge: the listed keys' NFA state back to never-seen (sg_reset_keys)."""
+        f = getattr(self.lib, self.p + "reset_keys")
+        f.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32]
+        k = np.ascontiguousarray(keys, dtype=np.uint32)
+        self._check(f(self.h, C.c_void_p(k.ctypes.data) if len(k) else None, len(k), SG_MEM_HOST))
+
     def snapshot(self) -> bytes:
         """Image of the device NFA state (sg_snapshot; poll the matches first)."""
         f, free = getattr(self.lib, self.p + "snapshot"), self.lib.sg_free_buffer

@@ -475,6 +475,54 @@ def _dec(v):
     raise ValueError(f"bad snapshot tag {tag!r}")
 
 
+class _Purge:
+    """@purge(enable, interval, idle.period) of one partition (PartitionRuntimeImpl.java:120-147 parse,
+    :346-401 run): every send records the partition key's last-seen time (TimestampGenerator.currentTime);
+    every `interval` of wall time the keys idle for more than `idle.period` are dropped from every query
+    of the partition (cleanGroupByStates), so their next event starts them afresh.  The reference runs
+    this on an executor thread at fixed delay; here it runs when the runtime's clock is read (sends and
+    the harness's wall-clock advances).  Key ids stay in the dictionary (the device state is reset)."""
+
+    @staticmethod
+    def _ann(p):
+        a = [x for x in p.annotations if x.name.lower() == "purge"]
+        return a[0] if a else None
+
+    @staticmethod
+    def enabled(p):
+        a = _Purge._ann(p)
+        if a is None:
+            return False
+        en = a.get("enable")
+        if en is None:
+            raise SiddhiAppCreationException("Annotation @purge is missing element 'enable'")
+        if en.lower() not in ("true", "false"):
+            raise SiddhiAppCreationException(f"Invalid value for enable: {en}. Please use 'true' or 'false'")
+        if a.get("idle.period") is None:
+            raise SiddhiAppCreationException("Annotation @purge is missing element 'idle.period'")
+        return en.lower() == "true"
+
+    def __init__(self, p, queries):
+        a = self._ann(p)
+        self.idle = _time_ms(a.get("idle.period"))
+        self.interval = _time_ms(a.get("interval")) if a.get("interval") is not None else 1000
+        self.queries = queries
+        self.last_seen: Dict[str, int] = {}
+        self.next_run = None
+
+    def run(self, now):
+        idle = [k for k, t in self.last_seen.items() if t + self.idle < now]
+        if not idle:
+            return []
+        kd = self.queries[0].key_dict if self.queries else {}
+        ids = [kd[k] for k in idle if k in kd]
+        for k in idle:
+            del self.last_seen[k]
+        for qr in self.queries:
+            qr.engine.reset_keys(ids)
+        return idle
+
+
 class InMemoryPersistenceStore:
     """io.siddhi.core.util.persistence.InMemoryPersistenceStore: revisions per app name."""
 
@@ -533,6 +581,9 @@ class SiddhiAppRuntime:
             qr = _QueryRuntime(self, cq, engine_factory, kd)
             self.queries.append(qr)
             self.by_name[qq.name or f"query{i + 1}"] = qr
+        self._purges = [_Purge(p, [qr for qr in self.queries if qr.cq.partitioned and
+                                   qr.key_dict is self.key_dicts.get(id(p))])
+                        for p in self.app.partitions if _Purge.enabled(p)]
         self.started = False
 
     # public API (camelCase as in the reference) -------------------------------------------------
@@ -555,6 +606,8 @@ class SiddhiAppRuntime:
         """SiddhiAppRuntimeImpl.start -> QueryRuntimeImpl.start -> initPartition (unpartitioned queries
         seed their start states now; absent start states arm their timers)."""
         self.started = True
+        for pg in self._purges:
+            pg.next_run = self.wall_time() + pg.interval
         for qr in self.queries:
             qr.engine.advance_time(self.current_time())
             qr.dispatch(qr.project(qr.engine.poll(), self.store))
@@ -572,6 +625,14 @@ class SiddhiAppRuntime:
         reference tests): wall-clock timers fire (Scheduler.EventCaller), and in playback mode with
         idle.time the heartbeat advances the event clock (TimestampGeneratorImpl.TimeInjector)."""
         ms = int(ms)
+        if self._purges and self.started:
+            for pg in self._purges:   # purge runs due before `ms`, each at its own wall time
+                if pg.next_run is None:
+                    pg.next_run = self.wall_time() + pg.interval
+                while pg.next_run <= ms:
+                    self._wall = pg.next_run
+                    pg.run(self.current_time())
+                    pg.next_run += pg.interval
         if self.playback:
             if self._idle is not None and self._idle >= 0 and self._last_sys is not None:
                 while self._last_sys + self._idle <= ms:
@@ -605,6 +666,7 @@ class SiddhiAppRuntime:
             "last_sys": self._last_sys,
             "queries": [{"keys": list(qr.key_dict.keys()) if qr.key_dict is not None else None,
                          "aggs": _enc(qr._agg_states)} for qr in self.queries],
+            "purge_last_seen": [pg.last_seen for pg in self._purges],
         }
         js = json.dumps(head).encode()
         parts = [_SNAP_MAGIC, struct.pack("<Q", len(js)), js]
@@ -642,6 +704,8 @@ class SiddhiAppRuntime:
                 qr.key_dict.clear()
                 qr.key_dict.update({k: i for i, k in enumerate(qs["keys"])})
             qr._agg_states = _dec(qs["aggs"])
+        for pg, seen in zip(self._purges, head.get("purge_last_seen", [])):
+            pg.last_seen = dict(seen)
 
     def persist(self):
         """SiddhiAppRuntime.persist(): snapshot into the manager's persistence store; returns the revision."""
@@ -707,9 +771,21 @@ class SiddhiAppRuntime:
             nulls.append(isnull if isnull.any() else None)
         return cols, nulls
 
+    def _run_purges(self):
+        if not self._purges or not self.started:
+            return
+        wall = self.wall_time()
+        for pg in self._purges:
+            if pg.next_run is None:
+                pg.next_run = wall + pg.interval
+            while wall >= pg.next_run:
+                pg.run(self.current_time())
+                pg.next_run += pg.interval
+
     def _send(self, stream, events, explicit=True):
         if stream not in self.app.streams:
             raise KeyError(stream)
+        self._run_purges()
         sd = self.app.streams[stream]
         if self.playback:
             if explicit and events:
@@ -734,10 +810,12 @@ class SiddhiAppRuntime:
                 ai = sd.attr_index(attr)
                 keys = []
                 keep = []
+                keys_str = []
                 for i, r in enumerate(rows):
                     ks = java_string(r[ai])
                     if ks is None:
                         continue          # PartitionStreamReceiver drops events whose key is null
+                    keys_str.append(ks)
                     kid = qr.key_dict.get(ks)
                     if kid is None:
                         kid = len(qr.key_dict)
@@ -746,6 +824,11 @@ class SiddhiAppRuntime:
                         qr.key_dict[ks] = kid
                     keys.append(kid)
                     keep.append(i)
+                for pg in self._purges:
+                    if qr in pg.queries:
+                        now = self.current_time()
+                        for k in keys_str:
+                            pg.last_seen[k] = now
             # contiguous seq runs (events dropped for a null key split the batch)
             start = 0
             while start < len(keep):

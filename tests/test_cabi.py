@@ -17,7 +17,8 @@ def declared():
 def test_header_declares_the_boundary():
     names = declared()
     for n in ("sg_engine_create", "sg_push_batch", "sg_advance_time", "sg_poll_matches",
-              "sg_release_matches", "sg_snapshot", "sg_restore", "sg_engine_destroy", "sg_last_error"):
+              "sg_release_matches", "sg_snapshot", "sg_restore", "sg_reset_keys", "sg_engine_destroy",
+              "sg_last_error"):
         assert n in names
 
 
@@ -32,7 +33,7 @@ def test_hip_library_exports_every_symbol():
 def test_oracle_exports_the_same_entry_points():
     lib = build_oracle()
     for n in ("engine_create", "push_batch", "poll_matches", "release_matches", "get_stats",
-              "engine_destroy", "last_error", "advance_time"):
+              "engine_destroy", "last_error", "advance_time", "reset_keys"):
         assert hasattr(lib, "sgo_" + n), n
 
 

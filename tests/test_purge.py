@@ -1,0 +1,113 @@
+"""Partition purge (@purge on a partition; PartitionRuntimeImpl.java:120-147, 346-401) on the oracle.
+
+Purging drops an idle key from every state holder of the partition's queries (cleanGroupByStates), so
+the key's next event starts afresh (initPartition).  Engine level (sg_reset_keys / sgo_reset_keys): a
+stream where keys P are reset between two batches gives, in the second batch, exactly the matches of
+a stream where P never sent anything before (their first-batch events moved to a key that stays
+silent afterwards).  Runtime level: the @purge annotation's interval / idle.period on a virtual wall
+clock.  The reference's purge KATs (CountPatternTestCase.testQuery26, AbsentWithEveryPatternTestCase
+testQuery8) finish before their purge task first runs, so they pin nothing beyond the plain pattern
+result; these checks are hand-worked ("parity unpinned" by a reference vector for the purge itself).
+The device side of the same property is in test_gpu_purge.py.
+"""
+import importlib
+
+import numpy as np
+import pytest
+
+from oracle_backend import build_oracle, oracle_manager
+
+sa = importlib.import_module("siddhi-1_amd")
+synth = importlib.import_module("siddhi-1_amd.synth")
+
+STOCK = "define stream S (symbol string, price float, volume int);\n"
+SHAPES = {
+    "two_state": STOCK + "partition with (symbol of S) begin from every e1=S[price>20] -> e2=S[price>e1.price] "
+                         "within 1 sec select e1.price as a insert into O; end;",
+    "count": STOCK + "partition with (symbol of S) begin from every e1=S[price>20]<2:5> -> "
+                     "e2=S[price>e1[last].price] within 1 sec select e1[0].price as a insert into O; end;",
+    "sequence": STOCK + "partition with (symbol of S) begin from every e1=S[price>20], e2=S[price>e1.price] "
+                        "select e1.price as a insert into O; end;",
+}
+
+
+def reset_property(shape, make, n_keys=256, batch=6000):
+    """returns (matches after reset, matches of the never-seen stream) for the second batch"""
+    app = sa.parse_app(SHAPES[shape])
+    cq = sa.compile_query(app, app.queries[0], sa.StringDictionary())
+    d1 = synth.stock_ticks(0, batch, n_keys - 1, seed=5, rate_per_ms=8)
+    d2 = synth.stock_ticks(batch, batch, n_keys - 1, seed=6, rate_per_ms=8)
+    purged = np.arange(0, n_keys - 1, 3, dtype=np.uint32)       # every third key
+    silent = np.uint32(n_keys - 1)                               # never appears in the second batch
+    a, b = make(cq.ir, n_keys), make(cq.ir, n_keys)
+    cols = lambda d: [d["symbol"], d["price"], d["volume"]]
+    a.push(0, 0, d1["ts"], cols(d1), None, d1["key"])
+    k1 = np.where(np.isin(d1["key"], purged), silent, d1["key"]).astype(np.uint32)
+    b.push(0, 0, d1["ts"], cols(d1), None, k1)
+    a.poll(), b.poll()
+    a.reset_keys(purged)
+    for e in (a, b):
+        e.push(0, batch, d2["ts"], cols(d2), None, d2["key"])
+    return a.poll(), b.poll()
+
+
+@pytest.mark.parametrize("shape", sorted(SHAPES))
+def test_oracle_reset_equals_never_seen(shape):
+    lib = build_oracle()
+    ma, mb = reset_property(shape, lambda ir, nk: sa.NativeEngine(lib, "sgo_", ir, n_keys=nk))
+    assert len(ma) == len(mb) > 0
+    assert np.array_equal(ma.trigger_seq, mb.trigger_seq)
+    assert np.array_equal(ma.slot_seq, mb.slot_seq)
+    assert np.array_equal(ma.key, mb.key)
+
+
+class _Collect(sa.StreamCallback):
+    def __init__(self):
+        self.events = []
+
+    def receive(self, events):
+        self.events += [list(e.data) for e in events]
+
+
+PURGE_APP = (STOCK + "@purge(enable='true', interval='1 sec', idle.period='2 sec') "
+             "partition with (symbol of S) begin from every e1=S[price>20] -> e2=S[price>e1.price] "
+             "select e1.symbol as s, e1.price as p1, e2.price as p2 insert into O; end;")
+
+
+def _run(app, steps):
+    rt = oracle_manager().createSiddhiAppRuntime(app)
+    cb = _Collect()
+    rt.addCallback("O", cb)
+    rt.set_wall_clock(1_000_000)
+    rt.start()
+    h = rt.getInputHandler("S")
+    for wall, ev in steps:
+        rt.advance_wall_clock(wall)
+        if ev is not None:
+            h.send(list(ev))
+    rt.shutdown()
+    return [[r[0], float(r[1]), float(r[2])] for r in cb.events]
+
+
+STEPS = [(1_000_000, ("A", 25.0, 1)), (1_000_100, ("B", 21.0, 1)),
+         (1_001_900, ("B", 19.0, 1)),          # keeps B alive (no new partial, no match)
+         (1_003_500, ("B", 22.0, 1)),          # purge at 1_003_000 dropped A (idle since 1_000_000), kept B
+         (1_005_000, ("A", 30.0, 1)),          # A starts afresh: no match
+         (1_005_100, ("B", 23.0, 1))]          # B seen at 1_003_500: kept by the purges up to 1_005_000
+
+
+def test_runtime_purge_drops_idle_keys():
+    got = _run(PURGE_APP, STEPS)
+    assert got == [["B", 21.0, 22.0], ["B", 22.0, 23.0]]
+
+
+def test_runtime_without_purge_keeps_state():
+    got = _run(PURGE_APP.replace("enable='true'", "enable='false'"), STEPS)
+    assert got == [["B", 21.0, 22.0], ["A", 25.0, 30.0], ["B", 22.0, 23.0]]
+
+
+def test_purge_annotation_errors():
+    with pytest.raises(sa.SiddhiAppCreationException):
+        oracle_manager().createSiddhiAppRuntime(PURGE_APP.replace("enable='true'", "enable='yes'"))
+    with pytest.raises(sa.SiddhiAppCreationException):
+        oracle_manager().createSiddhiAppRuntime(PURGE_APP.replace(", idle.period='2 sec'", ""))
