@@ -48,7 +48,7 @@ struct Lane {
     uint32_t trigRank;      // matches emitted so far for this trigger
     int64_t tk2;            // timer sort keys of the matches emitted now
     uint32_t tk1;
-    bool ret[GEN_MAXP];     // StreamPostStateProcessor.isEventReturned (transient)
+    uint32_t retm;          // StreamPostStateProcessor.isEventReturned per post processor (transient bits)
     unsigned long long scanned, created, matches;
     uint32_t err;
     unsigned long long resBase;  // this lane's reserved raw match slots
@@ -58,7 +58,7 @@ struct Lane {
     __device__ Lane(const GenArgs& a, uint32_t key)
         : G(*a.G), A(a), S(a.state), K(a.K), k(key), now(a.now), trigSeq(SG_TIMER_SEQ), trigIdx(0), trigRank(0),
           tk2(0), tk1(0), scanned(0), created(0), matches(0), err(0), resBase(0), resEnd(0), resLeft(0) {
-        for (int i = 0; i < GEN_MAXP; i++) ret[i] = false;
+        retm = 0;
     }
 
     // ---- HBM words of this key ----
@@ -547,9 +547,40 @@ struct Lane {
         }
     }
 
+    // addState with CountPreStateProcessor's min-count-0 forwarding (:129-136 -> processMinCountReached ->
+    // the next state's addState, and so on down a chain of <0:n> states) run as a loop over the chain:
+    // the continuations of processMinCountReached (its addEveryState and the reference drop) run after
+    // the innermost addState returns, innermost first, as the recursive calls would.  Keeping the call
+    // graph acyclic lets the compiler inline the whole processor graph (no call stack in scratch).
     __device__ void addState(int p, uint32_t se) {
+        int pend[GEN_MAXP];
+        int np = 0;
+        for (;;) {
+            if (addStateOne(p, se)) break;
+            const int q = G.pre[p].countPost;  // processMinCountReached(q, se), up to its addState
+            const GenPost& Q = G.post[q];
+            if (Q.hasNext) {
+                setFlag(Q.thisPre, GF_CHANGED, true);
+                retm |= 1u << q;
+            }
+            stIncref(se);
+            if (np >= GEN_MAXP) { err |= GERR_REF; stDecref(se); break; }
+            pend[np++] = q;
+            if (Q.nextStatePre == GEN_NONE) break;
+            p = Q.nextStatePre;
+        }
+        while (np > 0) {
+            const GenPost& Q = G.post[pend[--np]];
+            if (Q.nextEveryStatePre != GEN_NONE) addEveryState(Q.nextEveryStatePre, se);
+            stDecref(se);
+        }
+    }
+
+    // one StreamPre/CountPre/Logical/Absent addState; true when done, false when a count state with
+    // min 0 and an empty slot forwards the partial (processMinCountReached)
+    __device__ bool addStateOne(int p, uint32_t se) {
         const GenPre& P = G.pre[p];
-        if (P.absent && flag(p, GF_INACTIVE)) return;
+        if (P.absent && flag(p, GF_INACTIVE)) return true;
         if (P.absent && P.kind == GK_STREAM) {  // AbsentStreamPreStateProcessor.java:83-103
             if (G.qtype == SG_Q_SEQUENCE) clearList(p, 1);
             push(p, 1, se);
@@ -558,7 +589,7 @@ struct Lane {
                 W64(ks(p) + KS_LST, t);
                 notifyAt(p, t);
             }
-            return;
+            return true;
         }
         if (P.kind == GK_LOGICAL) {  // LogicalPreStateProcessor.java:43-62
             if (P.isStart || G.qtype == SG_Q_SEQUENCE) {
@@ -572,7 +603,7 @@ struct Lane {
                 notifyAt(p, stTs(se) + P.waiting);
                 if (G.pre[P.partner].absent) notifyAt(P.partner, stTs(se) + G.pre[P.partner].waiting);
             }
-            return;
+            return true;
         }
         // StreamPreStateProcessor.java:214-227, CountPreStateProcessor.java:114-128
         if (G.qtype == SG_Q_SEQUENCE) {
@@ -580,8 +611,7 @@ struct Lane {
         } else {
             push(p, 1, se);
         }
-        if (P.kind == GK_COUNT && P.minCount == 0 && slot(se, P.stateId) == GEN_NIL)  // :129-136
-            processMinCountReached(P.countPost, se);
+        return !(P.kind == GK_COUNT && P.minCount == 0 && slot(se, P.stateId) == GEN_NIL);  // :129-136
     }
 
     __device__ void addEveryState(int p, uint32_t se) {
@@ -712,7 +742,7 @@ struct Lane {
         const GenPost& Q = G.post[q];
         setFlag(Q.thisPre, GF_CHANGED, true);
         setStTs(se, evTs(slot(se, Q.stateId)));
-        if (Q.hasNext) ret[q] = true;
+        if (Q.hasNext) retm |= 1u << q;
         stIncref(se);
         if (Q.nextStatePre != GEN_NONE) addState(Q.nextStatePre, se);
         if (Q.nextEveryStatePre != GEN_NONE) addEveryState(Q.nextEveryStatePre, se);
@@ -723,7 +753,7 @@ struct Lane {
         const GenPost& Q = G.post[q];
         if (Q.hasNext) {
             setFlag(Q.thisPre, GF_CHANGED, true);
-            ret[q] = true;
+            retm |= 1u << q;
         }
         stIncref(se);
         if (Q.nextStatePre != GEN_NONE) addState(Q.nextStatePre, se);
@@ -735,7 +765,7 @@ struct Lane {
         if (Q.absent) {  // Absent{Stream,Logical}PostStateProcessor
             const uint32_t ev = slot(se, Q.stateId);
             setFlag(Q.thisPre, GF_CHANGED, true);
-            ret[q] = true;
+            retm |= 1u << q;
             if (Q.kind == GK_STREAM) {
                 setStTs(se, evTs(ev));
                 if (G.pre[Q.thisPre].isStart && Q.nextEveryStatePre == Q.thisPre) addEveryState(Q.thisPre, se);
@@ -770,7 +800,7 @@ struct Lane {
                 else setFlag(Q.thisPre, GF_CHANGED, true);
             } else {
                 streamProcess(q, se);
-                if (G.post[Q.partnerPost].hasNext && G.pre[Q.thisPre].thisLast == Q.partnerPost) ret[Q.partnerPost] = true;
+                if (G.post[Q.partnerPost].hasNext && G.pre[Q.thisPre].thisLast == Q.partnerPost) retm |= 1u << Q.partnerPost;
             }
             return;
         }
@@ -978,8 +1008,8 @@ struct Lane {
                 (G.qtype == SG_Q_SEQUENCE && P.logicalType == SG_L_AND && Q.nextEveryStatePre != GEN_NONE))
                 setSlot(se, P.stateId, cur);
             bool removed = false;
-            if (ret[P.thisLast]) {
-                ret[P.thisLast] = false;
+            if ((retm >> P.thisLast) & 1u) {
+                retm &= ~(1u << P.thisLast);
                 erase(p, 0, i);
                 removed = true;
                 if (G.qtype == SG_Q_SEQUENCE) removeValue(P.partner, 0, se);
@@ -1022,8 +1052,8 @@ struct Lane {
                 if (e != GEN_NIL) addEvent(se, P.stateId, e);
                 setFlag(p, GF_SUCCESS, false);
                 runChain(p, se);
-                if (ret[P.thisLast]) {
-                    ret[P.thisLast] = false;
+                if ((retm >> P.thisLast) & 1u) {
+                    retm &= ~(1u << P.thisLast);
                     if (nOut < OUTCAP) { stIncref(se); outList[nOut++] = se; } else err |= GERR_CAP;
                 }
                 bool removed = false;
@@ -1045,8 +1075,8 @@ struct Lane {
             const uint32_t e = newEv(seq, ts, pos, false);
             setSlot(se, P.stateId, e);
             runChain(p, se);
-            if (ret[P.thisLast]) {
-                ret[P.thisLast] = false;
+            if ((retm >> P.thisLast) & 1u) {
+                retm &= ~(1u << P.thisLast);
                 if (nOut < OUTCAP) { stIncref(se); outList[nOut++] = se; } else err |= GERR_CAP;
             }
             bool removed = false;
