@@ -23,8 +23,8 @@
 #include "gen_engine.h"
 #include "gen_host.h"
 
-extern "C" __global__ void k_gen_batch(const GenArgs a);
-extern "C" __global__ void k_gen_timers(const GenArgs a);
+extern "C" __global__ void k_gen_batch(const GenArgs* ap);
+extern "C" __global__ void k_gen_timers(const GenArgs* ap);
 
 namespace {
 
@@ -454,6 +454,8 @@ struct TimerLess {
 // ---------------------------------------------------------------------------------------------
 // the engine
 // ---------------------------------------------------------------------------------------------
+#define GEN_ARG_SLOTS 64
+
 struct GenEngine {
     GenProgram host{};
     GenProgram* dprog = nullptr;
@@ -484,6 +486,9 @@ struct GenEngine {
     size_t msort_tmp_bytes = 0;
     unsigned long long* stats = nullptr;
     unsigned long long* live = nullptr;  // k_gen_live's sum (diagnostics)
+    GenArgs* d_args = nullptr;           // kernel argument ring (device) and its pinned staging
+    GenArgs* h_args = nullptr;
+    uint64_t arg_next = 0;
     uint32_t* err = nullptr;
     OutBufs out{};
     std::vector<uint64_t> h_trig, h_slot;
@@ -504,6 +509,7 @@ struct GenEngine {
     ~GenEngine() {
         if (stream) (void)hipStreamSynchronize(stream);
         for (void* p : owned) (void)hipFree(p);
+        if (h_args) (void)hipHostFree(h_args);
     }
 
     GenArgs args() const {
@@ -588,6 +594,8 @@ GenEngine* gen_create(const uint32_t* ir, size_t nw, const sg_config& cfg, hipSt
         e->msort_tmp = e->dalloc<uint8_t>(e->msort_tmp_bytes);
         e->stats = e->dalloc<unsigned long long>(GST_N);
         e->live = e->dalloc<unsigned long long>(1);
+        e->d_args = e->dalloc<GenArgs>(GEN_ARG_SLOTS);
+        GH_OK(hipHostMalloc((void**)&e->h_args, sizeof(GenArgs) * GEN_ARG_SLOTS, hipHostMallocDefault));
         GH_OK(hipMemset(e->stats, 0, GST_N * 8));
         e->err = e->dalloc<uint32_t>(1);
         GH_OK(hipMemset(e->err, 0, 4));
@@ -622,10 +630,18 @@ static size_t type_size(int t) {
     }
 }
 
+// the kernels read their arguments from a device ring (GEN_ARG_SLOTS slots, staged through pinned host
+// memory on the engine's stream); a slot is rewritten only after the stream has drained the launches
+// that used it
 static void launch_batch_or_timers(GenEngine* e, const GenArgs& a, bool timers) {
     const uint32_t blocks = (e->K + 63) / 64;
-    if (timers) hipLaunchKernelGGL(k_gen_timers, dim3(blocks), dim3(64), 0, e->stream, a);
-    else hipLaunchKernelGGL(k_gen_batch, dim3(blocks), dim3(64), 0, e->stream, a);
+    const uint32_t slot = e->arg_next++ % GEN_ARG_SLOTS;
+    if (slot == 0 && e->arg_next > 1) GH_OK(hipStreamSynchronize(e->stream));
+    e->h_args[slot] = a;
+    GH_OK(hipMemcpyAsync(e->d_args + slot, e->h_args + slot, sizeof(GenArgs), hipMemcpyHostToDevice, e->stream));
+    const GenArgs* ap = e->d_args + slot;
+    if (timers) hipLaunchKernelGGL(k_gen_timers, dim3(blocks), dim3(64), 0, e->stream, ap);
+    else hipLaunchKernelGGL(k_gen_batch, dim3(blocks), dim3(64), 0, e->stream, ap);
     GH_OK(hipGetLastError());
 }
 

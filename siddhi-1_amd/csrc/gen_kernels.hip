@@ -418,61 +418,78 @@ struct Lane {
     }
     // FilterProcessor.process: pass iff the condition is a non-null true (FilterProcessor.java:48-60)
     __device__ bool eval(uint32_t se, uint32_t pc, uint32_t n) {
+        // the two top entries live in registers (t0 = top, t1 = below it); deeper ones in stk[]
+        // (stk[i] = entry i from the bottom), touched only by programs deeper than two
         GVal stk[24];
+        GVal t0{0, true}, t1{0, true};
         int sp = 0;
         const uint32_t end = pc + n;
         while (pc < end) {
             const uint32_t w = G.code[pc];
             const uint32_t op = w & 0xff, a = (w >> 8) & 0xff, b = (w >> 16) & 0xff;
             if (sp > 22) { err |= GERR_CAP; return false; }
+            GVal v;
+            bool push = false, binary = false;
             switch (op) {
             case SG_OP_VAR: {
                 const uint32_t e = chainAt(se, (int)b, (int32_t)G.code[pc + 2]);
                 const uint32_t at_ = G.code[pc + 1];
-                if (e == GEN_NIL) stk[sp++] = {0, true};
-                else stk[sp++] = {(uint64_t)R64(sew(e, SE_ATTR + 2 * at_)), ((W(sew(e, SE_NULL)) >> at_) & 1u) != 0};
+                if (e == GEN_NIL) v = {0, true};
+                else v = {(uint64_t)R64(sew(e, SE_ATTR + 2 * at_)), ((W(sew(e, SE_NULL)) >> at_) & 1u) != 0};
+                push = true;
                 break;
             }
             case SG_OP_CONST:
-                stk[sp++] = {(uint64_t)G.code[pc + 1] | ((uint64_t)G.code[pc + 2] << 32), b != 0};
+                v = {(uint64_t)G.code[pc + 1] | ((uint64_t)G.code[pc + 2] << 32), b != 0};
+                push = true;
                 break;
-            case SG_OP_CVT: stk[sp - 1] = cvt(stk[sp - 1], (int)a, (int)b); break;
+            case SG_OP_ISNULL_EV: {
+                const uint32_t e = chainAt(se, (int)b, (int32_t)G.code[pc + 1]);
+                v = {(uint64_t)(e == GEN_NIL), false};
+                push = true;
+                break;
+            }
+            case SG_OP_CVT: t0 = cvt(t0, (int)a, (int)b); break;
             case SG_OP_ADD: case SG_OP_SUB: case SG_OP_MUL: case SG_OP_DIV: case SG_OP_MOD:
-                stk[sp - 2] = arith((int)op, (int)a, stk[sp - 2], stk[sp - 1]);
-                sp--;
+                t0 = arith((int)op, (int)a, t1, t0);
+                binary = true;
                 break;
             case SG_OP_EQ: case SG_OP_NE: case SG_OP_GT: case SG_OP_GE: case SG_OP_LT: case SG_OP_LE:
-                stk[sp - 2] = {(uint64_t)compare((int)op, (int)a, stk[sp - 2], stk[sp - 1]), false};
-                sp--;
+                t0 = {(uint64_t)compare((int)op, (int)a, t1, t0), false};
+                binary = true;
                 break;
             case SG_OP_AND: {
-                const bool l = !stk[sp - 2].null && (stk[sp - 2].b & 1), r = !stk[sp - 1].null && (stk[sp - 1].b & 1);
-                stk[sp - 2] = {(uint64_t)(l && r), false};
-                sp--;
+                const bool l = !t1.null && (t1.b & 1), r = !t0.null && (t0.b & 1);
+                t0 = {(uint64_t)(l && r), false};
+                binary = true;
                 break;
             }
             case SG_OP_OR: {
-                const bool l = !stk[sp - 2].null && (stk[sp - 2].b & 1), r = !stk[sp - 1].null && (stk[sp - 1].b & 1);
-                stk[sp - 2] = {(uint64_t)(l || r), false};
-                sp--;
+                const bool l = !t1.null && (t1.b & 1), r = !t0.null && (t0.b & 1);
+                t0 = {(uint64_t)(l || r), false};
+                binary = true;
                 break;
             }
             case SG_OP_NOT: {
-                const bool t = !stk[sp - 1].null && (stk[sp - 1].b & 1);
-                stk[sp - 1] = {(uint64_t)(!t), false};
+                const bool t = !t0.null && (t0.b & 1);
+                t0 = {(uint64_t)(!t), false};
                 break;
             }
-            case SG_OP_ISNULL: stk[sp - 1] = {(uint64_t)stk[sp - 1].null, false}; break;
-            case SG_OP_ISNULL_EV: {
-                const uint32_t e = chainAt(se, (int)b, (int32_t)G.code[pc + 1]);
-                stk[sp++] = {(uint64_t)(e == GEN_NIL), false};
-                break;
-            }
+            case SG_OP_ISNULL: t0 = {(uint64_t)t0.null, false}; break;
             default: err |= GERR_REF; return false;
+            }
+            if (push) {
+                if (sp >= 2) stk[sp - 2] = t1;
+                t1 = t0;
+                t0 = v;
+                sp++;
+            } else if (binary) {  // two popped, one pushed: the entry below the operands moves up
+                if (sp >= 3) t1 = stk[sp - 3];
+                sp--;
             }
             pc += op_len(op);
         }
-        return sp > 0 && !stk[sp - 1].null && (stk[sp - 1].b & 1);
+        return sp > 0 && !t0.null && (t0.b & 1);
     }
 
     // ---- match output (QuerySelector input) ----
@@ -1191,7 +1208,11 @@ __device__ void gen_wave_stats(const GenArgs& a, unsigned long long sc, unsigned
 // ------------------------------------------------------------------------------------------------
 // batch: one lane per key walks its key-sorted events
 // ------------------------------------------------------------------------------------------------
-extern "C" __global__ void __launch_bounds__(64) k_gen_batch(const GenArgs a) {
+// The arguments live in device memory (written by the host before the launch): the lanes hold a
+// reference to them, and a reference to a by-value kernel argument would force a private copy of the
+// whole struct into every lane's scratch.
+extern "C" __global__ void __launch_bounds__(64) k_gen_batch(const GenArgs* __restrict__ ap) {
+    const GenArgs& a = *ap;
     const uint32_t key = blockIdx.x * blockDim.x + threadIdx.x;
     unsigned long long sc = 0, cr = 0, ma = 0, ky = 0;
     uint32_t er = 0;
@@ -1292,7 +1313,8 @@ __device__ void gen_timers_key(const GenArgs& a, uint32_t key, unsigned long lon
 }
 }  // namespace
 
-extern "C" __global__ void __launch_bounds__(64) k_gen_timers(const GenArgs a) {
+extern "C" __global__ void __launch_bounds__(64) k_gen_timers(const GenArgs* __restrict__ ap) {
+    const GenArgs& a = *ap;
     const uint32_t key = blockIdx.x * blockDim.x + threadIdx.x;
     unsigned long long sc = 0, cr = 0, ma = 0;
     uint32_t er = 0;
