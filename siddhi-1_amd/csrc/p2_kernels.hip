@@ -93,22 +93,24 @@ __global__ void __launch_bounds__(256) k_order_sums(const uint64_t* __restrict__
 }
 
 __global__ void __launch_bounds__(256) k_order_scatter(const ScatterParams s, uint32_t ntiles) {
-    // all rows' descriptors, keys and timestamps are loaded up front (independent loads in flight
-    // together), the 16 rows' wave scans are combined through one LDS round trip, then the writes
+    // Phase 1: all rows' descriptors are loaded up front, the 16 rows' wave scans combined through one
+    // LDS round trip: every trigger of the tile gets its tile-local output offset.  Phase 2 is
+    // output-major: each thread owns consecutive output records (coalesced stores); a window of
+    // WIN records at a time, each record's trigger found through an owner map in LDS.
     constexpr int ROWS = SGD_ORDER_TILE / 256;
+    constexpr uint32_t WIN = SGD_ORDER_TILE / 2;
     __shared__ uint32_t wtot[ROWS][4];
+    __shared__ uint32_t owner[WIN];          // window record -> tile-local trigger index
+    __shared__ uint32_t loc[SGD_ORDER_TILE]; // tile-local trigger -> its first record (tile-local)
+    __shared__ uint16_t cnt[SGD_ORDER_TILE]; // tile-local trigger -> its record count (<= SGD_MAX_CAP)
+    __shared__ uint32_t fst[SGD_ORDER_TILE]; // tile-local trigger -> its first raw slot
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t base = blockIdx.x * SGD_ORDER_TILE;
     uint64_t d[ROWS];
-    uint32_t key[ROWS];
-    int64_t ts[ROWS];
 #pragma unroll
     for (int j = 0; j < ROWS; ++j) {
         const uint32_t t = base + j * 256 + threadIdx.x;
-        const bool in = t < s.n;
-        d[j] = in ? s.t_desc[t] : 0ull;
-        key[j] = (in && s.key) ? s.key[t] : 0u;
-        ts[j] = in ? s.ts[t] : 0;
+        d[j] = t < s.n ? s.t_desc[t] : 0ull;
     }
     uint32_t incl[ROWS];
 #pragma unroll
@@ -117,7 +119,6 @@ __global__ void __launch_bounds__(256) k_order_scatter(const ScatterParams s, ui
         if (lane == 63) wtot[j][wv] = incl[j];
     }
     __syncthreads();
-    const uint64_t out0 = *s.out_count + s.tile_off[blockIdx.x];
     uint32_t running = 0;
 #pragma unroll
     for (int j = 0; j < ROWS; ++j) {
@@ -129,28 +130,45 @@ __global__ void __launch_bounds__(256) k_order_scatter(const ScatterParams s, ui
             row += x;
         }
         const uint32_t c = (uint32_t)(d[j] >> 32);
+        const uint32_t tl = j * 256 + threadIdx.x;
+        loc[tl] = running + before + incl[j] - c;
+        cnt[tl] = (uint16_t)c;
         if (c) {
-            const uint32_t t = base + j * 256 + threadIdx.x;
-            const uint64_t o = out0 + running + before + incl[j] - c;
-            s.t_desc[t] = 0;
-            if (o + c > s.capacity) {
-                atomicOr(s.err, (uint32_t)SGD_ERR_MATCH_CAP);
-            } else {
-                const uint32_t f = (uint32_t)d[j];
-                const uint64_t trig = s.seq_base + t;
-                for (uint32_t r = 0; r < c; ++r) {
-                    const uint64_t q = o + r;
-                    s.o_trig[q] = trig;
-                    // {e1 seq, e2 seq} as one 16-B store
-                    *reinterpret_cast<ulonglong2*>(s.o_slot + 2 * q) = make_ulonglong2(s.raw_e1[f + r], trig);
-                    s.o_key[q] = key[j];
-                    s.o_ts[q] = ts[j];  // StreamPostStateProcessor.java:68: StateEvent ts = ts of the e2 event
-                }
-            }
+            fst[tl] = (uint32_t)d[j];
+            s.t_desc[base + tl] = 0;
         }
         running += row;
     }
-    if (blockIdx.x == ntiles - 1 && threadIdx.x == 0) *s.batch_total = (unsigned long long)s.tile_off[blockIdx.x] + running;
+    const uint32_t total = running;  // records of this tile
+    const uint64_t out0 = *s.out_count + s.tile_off[blockIdx.x];
+    if (blockIdx.x == ntiles - 1 && threadIdx.x == 0) *s.batch_total = (unsigned long long)s.tile_off[blockIdx.x] + total;
+    if (out0 + total > s.capacity) {  // poll fails loudly; nothing is written past the buffers
+        if (threadIdx.x == 0 && total) atomicOr(s.err, (uint32_t)SGD_ERR_MATCH_CAP);
+        return;
+    }
+    for (uint32_t w0 = 0; w0 < total; w0 += WIN) {
+        const uint32_t w1 = min(total, w0 + WIN);
+#pragma unroll 1
+        for (int j = 0; j < ROWS; ++j) {
+            const uint32_t tl = j * 256 + threadIdx.x;
+            const uint32_t l0 = loc[tl], c = cnt[tl];
+            const uint32_t a = max(l0, w0), b = min(l0 + c, w1);
+            for (uint32_t r = a; r < b; ++r) owner[r - w0] = tl;
+        }
+        __syncthreads();
+        for (uint32_t q = w0 + threadIdx.x; q < w1; q += 256) {
+            const uint32_t tl = owner[q - w0];
+            const uint32_t t = base + tl;
+            const uint64_t trig = s.seq_base + t;
+            const uint64_t o = out0 + q;
+            s.o_trig[o] = trig;
+            // {e1 seq, e2 seq} as one 16-B store
+            *reinterpret_cast<ulonglong2*>(s.o_slot + 2 * o) = make_ulonglong2(s.raw_e1[fst[tl] + (q - loc[tl])], trig);
+            s.o_key[o] = s.key ? s.key[t] : 0u;
+            s.o_ts[o] = s.ts[t];  // StreamPostStateProcessor.java:68: StateEvent ts = ts of the e2 event
+        }
+        __syncthreads();  // the owner map is rebuilt for the next window
+    }
 }
 
 // partition purge: the listed keys' headers go back to "never seen" (INIT clear, no partials); the
