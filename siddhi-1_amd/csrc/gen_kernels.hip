@@ -1208,10 +1208,12 @@ __device__ void gen_wave_stats(const GenArgs& a, unsigned long long sc, unsigned
 // ------------------------------------------------------------------------------------------------
 // batch: one lane per key walks its key-sorted events
 // ------------------------------------------------------------------------------------------------
+// Occupancy: 6 waves/SIMD (80 VGPRs, some spilled to scratch) measured best for this latency-bound
+// kernel on C3/C4 (3 waves: C3 1.03e9 events/s, 5: 1.19e9, 6: 1.27e9; 8 waves spills 129 VGPRs).
 // The arguments live in device memory (written by the host before the launch): the lanes hold a
 // reference to them, and a reference to a by-value kernel argument would force a private copy of the
 // whole struct into every lane's scratch.
-extern "C" __global__ void __launch_bounds__(64) k_gen_batch(const GenArgs* __restrict__ ap) {
+extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6, 8))) k_gen_batch(const GenArgs* __restrict__ ap) {
     const GenArgs& a = *ap;
     const uint32_t key = blockIdx.x * blockDim.x + threadIdx.x;
     unsigned long long sc = 0, cr = 0, ma = 0, ky = 0;
@@ -1313,7 +1315,7 @@ __device__ void gen_timers_key(const GenArgs& a, uint32_t key, unsigned long lon
 }
 }  // namespace
 
-extern "C" __global__ void __launch_bounds__(64) k_gen_timers(const GenArgs* __restrict__ ap) {
+extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6, 8))) k_gen_timers(const GenArgs* __restrict__ ap) {
     const GenArgs& a = *ap;
     const uint32_t key = blockIdx.x * blockDim.x + threadIdx.x;
     unsigned long long sc = 0, cr = 0, ma = 0;
