@@ -169,6 +169,31 @@ size_t sg_shard_scratch_bytes(uint64_t n, uint32_t world);
 int sg_shard_unpack(uint64_t n, const uint32_t* rows, uint32_t n_cols, uint32_t* key, int64_t* ts,
                     uint32_t* const* cols_dev, void* stream);
 
+/* Partition-key dictionary (host ingest; no device needed).  Replaces the
+ * String-keyed partition map of PartitionStreamReceiver.receive (partition/PartitionStreamReceiver.java:
+ * 175-260), where ValuePartitionExecutor.execute (partition/executor/ValuePartitionExecutor.java:34-41)
+ * turns the key attribute into its String form and PartitionRuntimeImpl.initPartition
+ * (partition/PartitionRuntimeImpl.java:346-402) creates state the first time a key is seen.  Here each
+ * distinct key string gets a dense id in first-seen order (0, 1, 2, ...), the key_id that
+ * sg_batch.key carries.  Strings are UTF-8 bytes, batched Arrow-style: string i is
+ * bytes[offsets[i], offsets[i+1]) (offsets has n+1 entries).  valid (optional, n bytes): 0 marks a
+ * null key, which the reference drops (PartitionStreamReceiver.java:175-205); its id is SG_KEY_NULL.
+ * sg_dict_intern assigns ids to new strings; it is all-or-nothing: when the batch would take the
+ * dictionary past max_ids it fails with SG_ERR_CAPACITY and assigns nothing.  n_new (optional)
+ * receives how many strings were new.  sg_dict_lookup never inserts (absent: SG_KEY_NULL). */
+#define SG_KEY_NULL 0xFFFFFFFFu
+typedef struct sg_dict sg_dict;
+int sg_dict_create(uint32_t max_ids, uint64_t capacity_hint, sg_dict** out);
+int sg_dict_intern(sg_dict* d, const uint8_t* bytes, const uint64_t* offsets, const uint8_t* valid, uint64_t n,
+                   uint32_t* ids, uint64_t* n_new);
+int sg_dict_lookup(const sg_dict* d, const uint8_t* bytes, const uint64_t* offsets, const uint8_t* valid,
+                   uint64_t n, uint32_t* ids);
+uint32_t sg_dict_size(const sg_dict* d);
+/* the key string of an id (pointer valid until the next intern / clear) */
+int sg_dict_key(const sg_dict* d, uint32_t id, const uint8_t** ptr, uint64_t* len);
+int sg_dict_clear(sg_dict* d);
+void sg_dict_destroy(sg_dict* d);
+
 /* Diagnostics (no device needed): generate and compile the query-specialised advance kernel of an IR
  * blob for gfx950.  variant_flags: bit 0 = batches carry null flags, bit 1 = captures carry null bits.
  * out (optional) receives the generated query header, or the compiler log on failure. */

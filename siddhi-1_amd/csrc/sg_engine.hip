@@ -882,6 +882,9 @@ int poll(sg_engine* e, uint32_t mem, sg_match_batch* out) {
 
 }  // namespace
 
+// the other host-side translation units (sg_dict.cpp) report through the same sg_last_error
+int sg_set_error(int code, const char* msg) { return fail(code, msg); }
+
 extern "C" {
 
 const char* sg_last_error(void) { return g_err.c_str(); }

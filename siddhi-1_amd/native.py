@@ -108,6 +108,115 @@ def _np_ptr(a):
     return C.c_void_p(a.ctypes.data) if a is not None else None
 
 
+SG_KEY_NULL = 0xFFFFFFFF
+
+
+def pack_strings(strings):
+    """Arrow-style (bytes, offsets[n+1], valid) of a sequence of str/None (UTF-8, as Java's String
+    bytes for the dictionary's equality)."""
+    enc = [s.encode("utf-8") if s is not None else b"" for s in strings]
+    offsets = np.zeros(len(enc) + 1, dtype=np.uint64)
+    if enc:
+        np.cumsum([len(b) for b in enc], out=offsets[1:])
+    data = np.frombuffer(b"".join(enc) or b"\0", dtype=np.uint8)
+    valid = np.array([s is not None for s in strings], dtype=np.uint8)
+    return data, offsets, valid
+
+
+class KeyDictionary:
+    """Partition-key dictionary over sg_dict (include/siddhi_gpu.h): key String -> dense key_id in
+    first-seen order, the map PartitionStreamReceiver keeps per partition
+    (partition/PartitionStreamReceiver.java:175-260).  Behaves as the dict the host runtime used
+    (get / [] / in / len / keys / clear / update with first-seen ids) and adds the batched
+    `intern`, which is what ingest calls."""
+
+    def __init__(self, max_ids=(1 << 32) - 2, capacity_hint=0, lib=None):
+        self._lib = lib or load_hip_library()
+        L = self._lib
+        L.sg_dict_create.argtypes = [C.c_uint32, C.c_uint64, C.POINTER(C.c_void_p)]
+        L.sg_dict_intern.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p,
+                                     C.POINTER(C.c_uint64)]
+        L.sg_dict_lookup.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]
+        L.sg_dict_size.argtypes = [C.c_void_p]
+        L.sg_dict_size.restype = C.c_uint32
+        L.sg_dict_key.argtypes = [C.c_void_p, C.c_uint32, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]
+        L.sg_dict_clear.argtypes = [C.c_void_p]
+        L.sg_dict_destroy.argtypes = [C.c_void_p]
+        L.sg_dict_destroy.restype = None
+        L.sg_last_error.restype = C.c_char_p
+        h = C.c_void_p()
+        self._check(L.sg_dict_create(max_ids, capacity_hint, C.byref(h)))
+        self._h = h
+
+    def _check(self, rc):
+        if rc != SG_OK:
+            raise EngineError(rc, self._lib.sg_last_error().decode(errors="replace"))
+
+    def intern(self, strings):
+        """uint32 ids of a batch of key strings (None -> SG_KEY_NULL), new keys numbered in order of
+        first appearance; all-or-nothing (EngineError SG_ERR_CAPACITY past max_ids)."""
+        data, offsets, valid = pack_strings(strings)
+        ids = np.empty(len(offsets) - 1, dtype=np.uint32)
+        n_new = C.c_uint64()
+        self._check(self._lib.sg_dict_intern(self._h, _np_ptr(data), _np_ptr(offsets), _np_ptr(valid),
+                                             len(ids), _np_ptr(ids), C.byref(n_new)))
+        return ids
+
+    def lookup(self, strings):
+        data, offsets, valid = pack_strings(strings)
+        ids = np.empty(len(offsets) - 1, dtype=np.uint32)
+        self._check(self._lib.sg_dict_lookup(self._h, _np_ptr(data), _np_ptr(offsets), _np_ptr(valid),
+                                             len(ids), _np_ptr(ids)))
+        return ids
+
+    def key(self, i):
+        p, n = C.c_void_p(), C.c_uint64()
+        self._check(self._lib.sg_dict_key(self._h, i, C.byref(p), C.byref(n)))
+        return C.string_at(p, n.value).decode("utf-8") if n.value else ""
+
+    # the dict protocol of the host runtime --------------------------------------------------------
+    def __len__(self):
+        return int(self._lib.sg_dict_size(self._h))
+
+    def get(self, k, default=None):
+        i = int(self.lookup([k])[0])
+        return default if i == SG_KEY_NULL else i
+
+    def __getitem__(self, k):
+        i = self.get(k)
+        if i is None:
+            raise KeyError(k)
+        return i
+
+    def __contains__(self, k):
+        return self.get(k) is not None
+
+    def __setitem__(self, k, v):
+        if int(self.intern([k])[0]) != v:
+            raise ValueError("key ids are assigned in first-seen order")
+
+    def keys(self):
+        return [self.key(i) for i in range(len(self))]
+
+    def clear(self):
+        self._check(self._lib.sg_dict_clear(self._h))
+
+    def update(self, mapping):
+        for k, v in sorted(mapping.items(), key=lambda kv: kv[1]):
+            self[k] = v
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.sg_dict_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class NativeEngine:
     """One sg_engine (one compiled query on one device)."""
 

@@ -11,8 +11,8 @@
 
 Below the API, every pattern/sequence query is compiled to the engine IR and run by an engine
 behind the C-ABI (include/siddhi_gpu.h): the HIP engine by default.  Events are packed into columnar
-batches (one per `send` call and input stream), partition keys are mapped to dense ids by a host
-dictionary (keys are compared only by String.equals in ValuePartitionExecutor.java:34-41, so any
+batches (one per `send` call and input stream), partition keys are mapped to dense ids by the native
+key dictionary (sg_dict, one batched intern per send) (keys are compared only by String.equals in ValuePartitionExecutor.java:34-41, so any
 injective map preserves semantics), and emitted matches are projected through the select list on the
 host (QuerySelector.processNoGroupBy, C/query/selector/QuerySelector.java:162-206).
 """
@@ -28,7 +28,7 @@ import numpy as np
 
 from . import compiler as cp
 from . import siddhiql as q
-from .native import NativeEngine, load_hip_library
+from .native import SG_KEY_NULL, EngineError, KeyDictionary, NativeEngine, load_hip_library
 
 
 # ------------------------------------------------------------------------------------------------
@@ -577,7 +577,9 @@ class SiddhiAppRuntime:
             cq = cp.compile_query(self.app, qq, self.strings)
             kd = None
             if qq.partition is not None:
-                kd = self.key_dicts.setdefault(id(qq.partition), {})
+                kd = self.key_dicts.get(id(qq.partition))
+                if kd is None:  # the partition's String key -> key_id map, native (sg_dict)
+                    kd = self.key_dicts[id(qq.partition)] = KeyDictionary(max_ids=self.n_keys)
             qr = _QueryRuntime(self, cq, engine_factory, kd)
             self.queries.append(qr)
             self.by_name[qq.name or f"query{i + 1}"] = qr
@@ -808,22 +810,14 @@ class SiddhiAppRuntime:
             if qr.cq.partitioned:
                 attr = qr.cq.partition_keys[stream]
                 ai = sd.attr_index(attr)
-                keys = []
-                keep = []
-                keys_str = []
-                for i, r in enumerate(rows):
-                    ks = java_string(r[ai])
-                    if ks is None:
-                        continue          # PartitionStreamReceiver drops events whose key is null
-                    keys_str.append(ks)
-                    kid = qr.key_dict.get(ks)
-                    if kid is None:
-                        kid = len(qr.key_dict)
-                        if kid >= qr.n_keys:
-                            raise RuntimeError(f"more than {qr.n_keys} partition keys")
-                        qr.key_dict[ks] = kid
-                    keys.append(kid)
-                    keep.append(i)
+                # one batched intern per send (sg_dict); PartitionStreamReceiver drops null keys
+                try:
+                    kids = qr.key_dict.intern([java_string(r[ai]) for r in rows])
+                except EngineError as ex:
+                    raise RuntimeError(f"more than {qr.n_keys} partition keys") from ex
+                keep = [i for i in range(len(rows)) if kids[i] != SG_KEY_NULL]
+                keys = [int(kids[i]) for i in keep]
+                keys_str = [java_string(rows[i][ai]) for i in keep] if self._purges else []
                 for pg in self._purges:
                     if qr in pg.queries:
                         now = self.current_time()
