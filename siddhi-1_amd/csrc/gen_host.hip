@@ -645,6 +645,13 @@ static void launch_batch_or_timers(GenEngine* e, const GenArgs& a, bool timers) 
     GH_OK(hipGetLastError());
 }
 
+// largest key id of a host batch (branch-free, so it vectorises; range-checked after the H2D is queued)
+static uint32_t sgd_max_key(const uint32_t* k, uint32_t n) {
+    uint32_t m = 0;
+    for (uint32_t i = 0; i < n; i++) m = k[i] > m ? k[i] : m;
+    return m;
+}
+
 int gen_push(GenEngine* e, const sg_batch* b, std::string& msg) {
     const GenProgram& G = e->host;
     if (b->stream >= (uint32_t)G.nstreams) { msg = "stream index out of range"; return SG_ERR_INVALID; }
@@ -684,10 +691,14 @@ int gen_push(GenEngine* e, const sg_batch* b, std::string& msg) {
     if (G.partitioned) {
         const uint32_t* keys = b->key;
         if (!dev) {
-            for (uint32_t i = 0; i < n; i++)
-                if (b->key[i] >= e->K) { msg = "key id outside [0, n_keys)"; return SG_ERR_INVALID; }
+            // the copy is queued first, so the host range check overlaps the DMA (pinned batches)
             GH_OK(hipMemcpyAsync(e->b_key, b->key, (size_t)n * 4, hipMemcpyHostToDevice, e->stream));
             keys = e->b_key;
+            if (sgd_max_key(b->key, n) >= e->K) {
+                GH_OK(hipStreamSynchronize(e->stream));  // the queued copies read the caller's buffers
+                msg = "key id outside [0, n_keys)";
+                return SG_ERR_INVALID;
+            }
         }
         uint32_t bits = 1;
         while (bits < 32 && (1ull << bits) < e->K) bits++;

@@ -645,6 +645,13 @@ uint32_t stage_chunks_for(uint64_t n, uint64_t K, uint32_t stride_words) {
     return (uint32_t)std::max(64.0, std::min(chunks, hi));
 }
 
+// largest key id of a host batch (branch-free, so it vectorises; range-checked after the H2D is queued)
+static uint32_t sgd_max_key(const uint32_t* k, uint32_t n) {
+    uint32_t m = 0;
+    for (uint32_t i = 0; i < n; i++) m = k[i] > m ? k[i] : m;
+    return m;
+}
+
 int push(sg_engine* e, const sg_batch* b) {
     const Plan& pl = e->plan;
     if (b->stream >= e->streams.size()) return fail(SG_ERR_INVALID, "stream index out of range");
@@ -713,10 +720,13 @@ int push(sg_engine* e, const sg_batch* b) {
     if (pl.partitioned) {
         const uint32_t* keys = b->key;
         if (!dev) {
-            for (uint32_t i = 0; i < n; i++)
-                if (b->key[i] >= e->K) return fail(SG_ERR_INVALID, "key id outside [0, n_keys)");
+            // the copy is queued first, so the host range check overlaps the DMA (pinned batches)
             HIP_OK(hipMemcpyAsync(e->b_key, b->key, (size_t)n * 4, kind, e->stream));
             keys = e->b_key;
+            if (sgd_max_key(b->key, n) >= e->K) {
+                HIP_OK(hipStreamSynchronize(e->stream));  // the queued copies read the caller's buffers
+                return fail(SG_ERR_INVALID, "key id outside [0, n_keys)");
+            }
         }
         size_t tmp = e->sort_tmp_bytes;
         if (words <= 4) {
