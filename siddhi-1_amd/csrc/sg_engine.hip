@@ -557,12 +557,13 @@ void allocate(sg_engine* e) {
     HIP_OK(hipMemset(e->resume, 0xff, K * 4));  // SGD_NO_RESUME
     e->tile_sum = dalloc<uint32_t>(B / SGD_ORDER_TILE + 1, o);
     e->tile_off = dalloc<uint32_t>(B / SGD_ORDER_TILE + 1, o);
-    e->out_count = dalloc<unsigned long long>(1, o);
+    // the match count and the error word share 16 bytes, so poll reads both with one D2H copy
+    e->out_count = dalloc<unsigned long long>(2, o);
+    e->err = (uint32_t*)(e->out_count + 1);
     e->batch_total = dalloc<unsigned long long>(1, o);
     e->stats = dalloc<unsigned long long>(SGD_ST_N, o);
-    e->err = dalloc<uint32_t>(1, o);
     HIP_OK(hipMemset(e->t_desc, 0, B * 8));
-    HIP_OK(hipMemset(e->out_count, 0, 8));
+    HIP_OK(hipMemset(e->out_count, 0, 16));
     HIP_OK(hipMemset(e->stats, 0, SGD_ST_N * 8));
     HIP_OK(hipMemset(e->err, 0, 4));
     e->scan_tmp_bytes = sgd_scatter_scan_bytes((uint32_t)B);
@@ -840,11 +841,12 @@ int push(sg_engine* e, const sg_batch* b) {
 
 int poll(sg_engine* e, uint32_t mem, sg_match_batch* out) {
     if (e->held) return fail(SG_ERR_STATE, "previous matches not released");
-    unsigned long long n = 0;
-    uint32_t err = 0;
-    HIP_OK(hipMemcpyAsync(&n, e->out_count, 8, hipMemcpyDeviceToHost, e->stream));
-    HIP_OK(hipMemcpyAsync(&err, e->err, 4, hipMemcpyDeviceToHost, e->stream));
+    unsigned long long status[2] = {0ull, 0ull};  // {out_count, err} (adjacent on the device)
+    HIP_OK(hipMemcpyAsync(status, e->out_count, 16, hipMemcpyDeviceToHost, e->stream));
     HIP_OK(hipStreamSynchronize(e->stream));
+    const unsigned long long n = status[0];
+    uint32_t err = 0;
+    std::memcpy(&err, &status[1], 4);
     e->resolve_spans();
     if (err & SGD_ERR_KEY_RANGE) return fail(SG_ERR_INVALID, "a batch carried key ids outside [0, n_keys)");
     if (err & SGD_ERR_PARTIAL_CAP)
