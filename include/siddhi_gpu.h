@@ -188,8 +188,17 @@ int sg_dict_intern(sg_dict* d, const uint8_t* bytes, const uint64_t* offsets, co
                    uint32_t* ids, uint64_t* n_new);
 int sg_dict_lookup(const sg_dict* d, const uint8_t* bytes, const uint64_t* offsets, const uint8_t* valid,
                    uint64_t n, uint32_t* ids);
+/* Partition purge (PartitionRuntimeImpl.java:368-401 drops idle keys from its per-partition maps): the
+ * listed ids leave the dictionary and are handed out again, smallest first, to the next new keys (after
+ * sg_reset_keys has returned their device state to never-seen), so live ids stay below max_ids under key
+ * churn.  All-or-nothing: an id not in use (or listed twice) fails with SG_ERR_INVALID. */
+int sg_dict_remove(sg_dict* d, const uint32_t* ids, uint64_t n);
+/* bind key bytes to a given free id (restoring a snapshot's key map); ids skipped over become free */
+int sg_dict_put(sg_dict* d, uint32_t id, const uint8_t* bytes, uint64_t len);
+/* id bound: every id handed out so far is below it (removed ids included) */
 uint32_t sg_dict_size(const sg_dict* d);
-/* the key string of an id (pointer valid until the next intern / clear) */
+/* the key string of an id in use (pointer valid until the next intern / put / remove / clear); a removed
+ * id fails with SG_ERR_INVALID */
 int sg_dict_key(const sg_dict* d, uint32_t id, const uint8_t** ptr, uint64_t* len);
 int sg_dict_clear(sg_dict* d);
 void sg_dict_destroy(sg_dict* d);

@@ -140,12 +140,29 @@ struct GenOut {
     uint32_t* err;
 };
 
+// Timers (sg_advance_time).  Each key's next deadline (the earliest queue head of its absent
+// processors under the playback listener, the earliest caller fire time under the wall clock) is kept in
+// nd[K] by every kernel that changes the key's timers; an advance to T compacts the keys with
+// nd <= T into `due` and runs k_gen_timers over those only.  Under playback each due (key, listener)
+// also records its queue head in dpair_key / dpair_i (slot due index * nStartup + listener), so that
+// the host can detect two keys sharing a due time at one advance.
+#define GEN_NO_DEADLINE INT64_MAX
+#define GEN_PAIR_NONE 0xffffffffu
+struct GenTimers {
+    int64_t* nd;                     // [K] next deadline, GEN_NO_DEADLINE = none
+    uint32_t* due;                   // [K] keys due at this advance
+    unsigned long long* ndue;
+    unsigned long long* dpair_key;   // [K * nStartup] order-preserving u64 of the head, or UINT64_MAX
+    uint32_t* dpair_i;               // [K * nStartup] listener index, or GEN_PAIR_NONE
+};
+
 struct GenArgs {
     const GenProgram* G;
     uint32_t* state;     // [blockWords][K] interleaved
     uint32_t K;
     GenBatch b;
     GenOut o;
+    GenTimers t;
     int64_t now;         // engine clock during a push; the advance target for a timer sweep
     int64_t now0;        // the engine clock before a wall-clock timer sweep
 };

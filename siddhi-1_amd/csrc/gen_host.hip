@@ -25,6 +25,11 @@
 
 extern "C" __global__ void k_gen_batch(const GenArgs* ap);
 extern "C" __global__ void k_gen_timers(const GenArgs* ap);
+extern "C" __global__ void k_gen_deadlines(const GenArgs* ap);
+extern "C" __global__ void k_gen_due(const int64_t* nd, uint32_t K, int64_t now, uint32_t* due,
+                                     unsigned long long* ndue);
+extern "C" __global__ void k_gen_collapse(const unsigned long long* key, const uint32_t* li, uint64_t n,
+                                          uint32_t* err);
 
 namespace {
 
@@ -415,6 +420,17 @@ __global__ void k_gen_bump(unsigned long long* count, const uint32_t* t_cnt, con
     else *count += (unsigned long long)t_off[n - 1] + t_cnt[n - 1];
 }
 
+__global__ void k_gen_fill64(int64_t* x, uint64_t n, int64_t v) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) x[i] = v;
+}
+
+// purged keys have no timers
+__global__ void k_gen_nd_reset(const uint32_t* __restrict__ keys, uint32_t n, uint32_t K, int64_t* __restrict__ nd) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n && keys[i] < K) nd[keys[i]] = GEN_NO_DEADLINE;
+}
+
 __global__ void k_gen_iota(uint32_t* x, uint64_t n) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) x[i] = (uint32_t)i;
@@ -485,6 +501,13 @@ struct GenEngine {
     void* msort_tmp = nullptr;
     size_t msort_tmp_bytes = 0;
     unsigned long long* stats = nullptr;
+    // timers: per-key next deadline, the due-key list of an advance and its (due time, listener) pairs
+    GenTimers tm{};
+    uint64_t npairs_cap = 0;
+    unsigned long long* pair_key_s = nullptr;
+    uint32_t* pair_i_s = nullptr;
+    void* psort_tmp = nullptr;
+    size_t psort_tmp_bytes = 0;
     unsigned long long* live = nullptr;  // k_gen_live's sum (diagnostics)
     GenArgs* d_args = nullptr;           // kernel argument ring (device) and its pinned staging
     GenArgs* h_args = nullptr;
@@ -531,6 +554,7 @@ struct GenEngine {
         a.o.nvalid = nvalid;
         a.o.stats = stats;
         a.o.err = err;
+        a.t = tm;
         a.now = now;
         a.now0 = now;
         return a;
@@ -593,6 +617,23 @@ GenEngine* gen_create(const uint32_t* ir, size_t nw, const sg_config& cfg, hipSt
         GH_OK(rocprim::merge_sort(nullptr, e->msort_tmp_bytes, e->order_in, e->order_out, (size_t)e->rawCap, lt, stream));
         e->msort_tmp = e->dalloc<uint8_t>(e->msort_tmp_bytes);
         e->stats = e->dalloc<unsigned long long>(GST_N);
+        if (G.nStartup > 0) {
+            e->tm.nd = e->dalloc<int64_t>(K);
+            hipLaunchKernelGGL(k_gen_fill64, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, stream, e->tm.nd,
+                               (uint64_t)K, (int64_t)GEN_NO_DEADLINE);
+            e->tm.due = e->dalloc<uint32_t>(K);
+            e->tm.ndue = e->dalloc<unsigned long long>(1);
+            if (G.partitioned && G.playback) {
+                e->npairs_cap = (uint64_t)K * (uint64_t)G.nStartup;
+                e->tm.dpair_key = e->dalloc<unsigned long long>(e->npairs_cap);
+                e->tm.dpair_i = e->dalloc<uint32_t>(e->npairs_cap);
+                e->pair_key_s = e->dalloc<unsigned long long>(e->npairs_cap);
+                e->pair_i_s = e->dalloc<uint32_t>(e->npairs_cap);
+                GH_OK(rocprim::radix_sort_pairs(nullptr, e->psort_tmp_bytes, e->tm.dpair_key, e->pair_key_s,
+                                                e->tm.dpair_i, e->pair_i_s, (size_t)e->npairs_cap, 0, 64, stream));
+                e->psort_tmp = e->dalloc<uint8_t>(e->psort_tmp_bytes);
+            }
+        }
         e->live = e->dalloc<unsigned long long>(1);
         e->d_args = e->dalloc<GenArgs>(GEN_ARG_SLOTS);
         GH_OK(hipHostMalloc((void**)&e->h_args, sizeof(GenArgs) * GEN_ARG_SLOTS, hipHostMallocDefault));
@@ -633,14 +674,20 @@ static size_t type_size(int t) {
 // the kernels read their arguments from a device ring (GEN_ARG_SLOTS slots, staged through pinned host
 // memory on the engine's stream); a slot is rewritten only after the stream has drained the launches
 // that used it
-static void launch_batch_or_timers(GenEngine* e, const GenArgs& a, bool timers) {
+enum { GEN_L_BATCH = 0, GEN_L_TIMERS = 1, GEN_L_DEADLINES = 2 };
+// timer sweeps: a fixed grid of one-wave blocks striding over the due keys (their number is on the device)
+#define GEN_TIMER_BLOCKS 4096u
+static void launch_gen(GenEngine* e, const GenArgs& a, int which) {
     const uint32_t blocks = (e->K + 63) / 64;
     const uint32_t slot = e->arg_next++ % GEN_ARG_SLOTS;
     if (slot == 0 && e->arg_next > 1) GH_OK(hipStreamSynchronize(e->stream));
     e->h_args[slot] = a;
     GH_OK(hipMemcpyAsync(e->d_args + slot, e->h_args + slot, sizeof(GenArgs), hipMemcpyHostToDevice, e->stream));
     const GenArgs* ap = e->d_args + slot;
-    if (timers) hipLaunchKernelGGL(k_gen_timers, dim3(blocks), dim3(64), 0, e->stream, ap);
+    if (which == GEN_L_TIMERS)
+        hipLaunchKernelGGL(k_gen_timers, dim3(e->host.partitioned ? std::min(blocks, GEN_TIMER_BLOCKS) : 1u), dim3(64), 0,
+                           e->stream, ap);
+    else if (which == GEN_L_DEADLINES) hipLaunchKernelGGL(k_gen_deadlines, dim3(blocks), dim3(64), 0, e->stream, ap);
     else hipLaunchKernelGGL(k_gen_batch, dim3(blocks), dim3(64), 0, e->stream, ap);
     GH_OK(hipGetLastError());
 }
@@ -717,7 +764,7 @@ int gen_push(GenEngine* e, const sg_batch* b, std::string& msg) {
     GH_OK(hipMemsetAsync(e->raw_count, 0, 8 * GEN_RAWSEG, e->stream));
     a.o.nseg = GEN_RAWSEG;
     a.o.seg_cap = e->rawCap / GEN_RAWSEG;
-    launch_batch_or_timers(e, a, false);
+    launch_gen(e, a, GEN_L_BATCH);
     // order: out_count + t_off[trigger] + rank
     size_t tmp = e->scan_tmp_bytes;
     GH_OK(rocprim::exclusive_scan(e->scan_tmp, tmp, e->t_cnt, e->t_off, 0u, n, rocprim::plus<uint32_t>(), e->stream));
@@ -742,17 +789,42 @@ int gen_advance(GenEngine* e, int64_t t, std::string& msg) {
         if (e->advanced && t < e->lastEventTs) return SG_OK;
         e->lastEventTs = t;
     }
+    if (G.nStartup == 0) {  // no absent state: the query has no timers, only the clock moves
+        if (G.playback || !e->advanced || t > e->now) e->now = t;
+        e->advanced = true;
+        return SG_OK;
+    }
     GenArgs a = e->args();
     a.now = t;         // the advance target (playback: the event clock)
     a.now0 = e->now;   // the clock before it (wall-clock callers run at their own times)
     GH_OK(hipMemsetAsync(e->raw_count, 0, 8, e->stream));
     GH_OK(hipMemsetAsync(e->nvalid, 0, 8, e->stream));
+    GH_OK(hipMemsetAsync(e->tm.ndue, 0, 8, e->stream));
+    if (G.partitioned) {  // the keys with a deadline <= t: one pass over nd[K]
+        const uint32_t blocks = std::min<uint32_t>((e->K + 255) / 256, 2048u);
+        hipLaunchKernelGGL(k_gen_due, dim3(blocks), dim3(256), 0, e->stream, e->tm.nd, e->K, t, e->tm.due, e->tm.ndue);
+    }
     a.o.nseg = 1;
     a.o.seg_cap = e->rawCap;
-    launch_batch_or_timers(e, a, true);
-    unsigned long long nr = 0;
+    launch_gen(e, a, GEN_L_TIMERS);
+    unsigned long long nr = 0, ndue = 0;
     GH_OK(hipMemcpyAsync(&nr, e->raw_count, 8, hipMemcpyDeviceToHost, e->stream));
+    GH_OK(hipMemcpyAsync(&ndue, e->tm.ndue, 8, hipMemcpyDeviceToHost, e->stream));
     GH_OK(hipStreamSynchronize(e->stream));
+    bool check = false;
+    if (G.partitioned && G.playback && ndue * (uint64_t)G.nStartup >= 2) {
+        // the reference's listener collects the due (time, key) states in a
+        // TreeMultimap whose value comparator is always 0 (Scheduler.java:78-89, 364-367), so of several
+        // keys due at the same time only one (chosen by HashMap order) fires at this advance.  That
+        // input has no defined result: detect it and fail instead of diverging silently.
+        const size_t np = (size_t)(ndue * (uint64_t)G.nStartup);
+        size_t tmpb = e->psort_tmp_bytes;
+        GH_OK(rocprim::radix_sort_pairs(e->psort_tmp, tmpb, e->tm.dpair_key, e->pair_key_s, e->tm.dpair_i, e->pair_i_s,
+                                        np, 0, 64, e->stream));
+        hipLaunchKernelGGL(k_gen_collapse, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, e->stream, e->pair_key_s,
+                           e->pair_i_s, (uint64_t)np, e->err);
+        check = true;
+    }
     if (nr > 0) {
         // the timer matches in the reference's order: playback by (listener, queue head), wall clock by
         // (run time, key); within one key in emission order
@@ -769,7 +841,18 @@ int gen_advance(GenEngine* e, int64_t t, std::string& msg) {
     }
     if (G.playback || !e->advanced || t > e->now) e->now = t;
     e->advanced = true;
-    (void)msg;
+    if (check) {
+        uint32_t err = 0;
+        GH_OK(hipMemcpyAsync(&err, e->err, 4, hipMemcpyDeviceToHost, e->stream));
+        GH_OK(hipStreamSynchronize(e->stream));
+        if (err & GERR_COLLAPSE) {
+            const uint32_t rest = err & ~(uint32_t)GERR_COLLAPSE;
+            GH_OK(hipMemcpy(e->err, &rest, 4, hipMemcpyHostToDevice));
+            msg = "two partition keys share a timer due time at one clock advance (reference Scheduler collapse "
+                  "quirk, SURVEY A.10): input not supported";
+            return SG_ERR_UNSUPPORTED;
+        }
+    }
     return SG_OK;
 }
 
@@ -780,7 +863,13 @@ int gen_poll(GenEngine* e, uint32_t mem, sg_match_batch* out, std::string& msg) 
     GH_OK(hipMemcpyAsync(&n, e->out.count, 8, hipMemcpyDeviceToHost, e->stream));
     GH_OK(hipMemcpyAsync(&err, e->err, 4, hipMemcpyDeviceToHost, e->stream));
     GH_OK(hipStreamSynchronize(e->stream));
-    if (err & GERR_KEY) { msg = "a batch carried key ids outside [0, n_keys)"; return SG_ERR_INVALID; }
+    if (err & GERR_KEY) {
+        // reported once: the events with valid keys were processed, the others dropped
+        const uint32_t rest = err & ~(uint32_t)GERR_KEY;
+        GH_OK(hipMemcpy(e->err, &rest, 4, hipMemcpyHostToDevice));
+        msg = "a batch carried key ids outside [0, n_keys) (those events were dropped)";
+        return SG_ERR_INVALID;
+    }
     if (err & GERR_CAP) { msg = "a partition key exceeded the engine's per-key capacity (partial_capacity)"; return SG_ERR_CAPACITY; }
     if ((err & GERR_MATCHCAP) || n > e->mcap) { msg = "more matches than match_capacity between two polls"; return SG_ERR_CAPACITY; }
     if (err & GERR_CHAIN) { msg = "a count state chain is longer than the output chain capacity"; return SG_ERR_CAPACITY; }
@@ -858,7 +947,7 @@ __global__ void __launch_bounds__(256) k_gen_reset(const uint32_t* __restrict__ 
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (uint64_t)n * words) return;
     const uint32_t w = (uint32_t)(i / n), k = keys[i % n];
-    state[(size_t)w * K + k] = 0u;
+    if (k < K) state[(size_t)w * K + k] = 0u;  // ids were range-checked by sg_reset_keys; never write outside
 }
 
 int gen_reset_keys(GenEngine* e, const uint32_t* keys, uint32_t n, std::string& msg) {
@@ -867,6 +956,8 @@ int gen_reset_keys(GenEngine* e, const uint32_t* keys, uint32_t n, std::string& 
     const uint64_t total = (uint64_t)n * e->host.blockWords;
     hipLaunchKernelGGL(k_gen_reset, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, e->stream, keys, n,
                        (uint32_t)e->host.blockWords, e->K, e->state);
+    if (e->tm.nd)
+        hipLaunchKernelGGL(k_gen_nd_reset, dim3((n + 255) / 256), dim3(256), 0, e->stream, keys, n, e->K, e->tm.nd);
     GH_OK(hipGetLastError());
     return SG_OK;
 }
@@ -896,6 +987,7 @@ int gen_restore(GenEngine* e, const uint32_t* words, const GenClock& clk, std::s
     if (e->held) { msg = "release the polled matches before a restore"; return SG_ERR_STATE; }
     if (gen_outputs_pending(e)) { msg = "poll the emitted matches before a restore"; return SG_ERR_STATE; }
     GH_OK(hipMemcpyAsync(e->state, words, gen_state_words(e) * 4, hipMemcpyHostToDevice, e->stream));
+    if (e->tm.nd) launch_gen(e, e->args(), GEN_L_DEADLINES);  // the timers' due index from the restored state
     GH_OK(hipStreamSynchronize(e->stream));
     e->now = clk.now;
     e->lastEventTs = clk.last_event_ts;

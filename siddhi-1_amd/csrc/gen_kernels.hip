@@ -306,6 +306,24 @@ struct Lane {
         h = (h + 1) % G.Q;
         W(ks(p) + KS_QLEN) -= 1;
     }
+    // this key's next timer deadline (GenTimers): the earliest queue head of its absent processors
+    // (playback listener, Scheduler.java:73-104) or the earliest fire time of its running callers
+    // (wall clock, Scheduler.EventCaller, Scheduler.java:238-298)
+    __device__ int64_t nextDeadline() const {
+        int64_t best = GEN_NO_DEADLINE;
+        for (int i = 0; i < G.nStartup; i++) {
+            const int p = G.startup[i];
+            int64_t t = GEN_NO_DEADLINE;
+            if (G.playback) {
+                if (qlen(p) != 0) t = qhead(p);
+            } else if (flag(p, GF_RUNNING)) {
+                t = R64(ks(p) + KS_FIRE);
+            }
+            best = t < best ? t : best;
+        }
+        return best;
+    }
+
     __device__ void notifyAt(int p, int64_t t) {  // Scheduler.notifyAt + schedule (Scheduler.java:114-156)
         uint32_t& n = W(ks(p) + KS_QLEN);
         if (n >= G.Q) { err |= GERR_CAP; return; }
@@ -527,11 +545,10 @@ struct Lane {
             }
             lens[s] = n;
         }
-        if (timer) {
+        if (timer) {  // (nvalid: the timers kernel adds its waves' match counts)
             A.o.tk1[r] = tk1;
             A.o.tk2[r] = tk2;
             A.o.tk3[r] = k;
-            atomicAdd(A.o.nvalid, 1ull);
         } else {
             A.o.t_cnt[trigIdx] += 1;
         }
@@ -1238,6 +1255,7 @@ extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per
                 a.o.tk1[rr] = 0xffffffffu;  // sorts after every real timer match
             }
         }
+        if (a.G->nStartup > 0) a.t.nd[key] = L.nextDeadline();
         er = L.err;
         sc = L.scanned;
         cr = L.created;
@@ -1251,12 +1269,22 @@ extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per
 // timer sweep to a.now (sg_advance_time): every key with due timers runs them in the reference order
 // ------------------------------------------------------------------------------------------------
 namespace {
-__device__ void gen_timers_key(const GenArgs& a, uint32_t key, unsigned long long& sc, unsigned long long& cr,
-                               unsigned long long& ma, uint32_t& er) {
+__device__ __forceinline__ unsigned long long gen_ord64(int64_t t) { return (unsigned long long)t ^ (1ull << 63); }
+
+__device__ void gen_timers_key(const GenArgs& a, uint32_t key, uint64_t di, unsigned long long& sc,
+                               unsigned long long& cr, unsigned long long& ma, uint32_t& er) {
     Lane L(a, key);
     const GenProgram& G = *a.G;
     if (!(L.W(0) & 1u)) {
-        if (G.partitioned) return;  // a key is created by its first event
+        if (G.partitioned) {  // a key is created by its first event (not due: nd had no deadline)
+            if (G.playback)
+                for (int i = 0; i < G.nStartup; i++) {
+                    a.t.dpair_key[di * (uint64_t)G.nStartup + (uint64_t)i] = ~0ull;
+                    a.t.dpair_i[di * (uint64_t)G.nStartup + (uint64_t)i] = GEN_PAIR_NONE;
+                }
+            a.t.nd[key] = GEN_NO_DEADLINE;
+            return;
+        }
         // unpartitioned: QueryRuntimeImpl.start seeds the query at the clock of start()
         L.now = G.playback ? a.now0 : a.now;
         L.initKey();
@@ -1268,7 +1296,13 @@ __device__ void gen_timers_key(const GenArgs& a, uint32_t key, unsigned long lon
         L.now = T;
         for (int i = 0; i < G.nStartup; i++) {
             const int p = G.startup[i];
-            if (L.qlen(p) == 0 || L.qhead(p) > T) continue;
+            const bool due = L.qlen(p) != 0 && L.qhead(p) <= T;
+            if (G.partitioned) {  // the listener's collection of (due time, key): the A.10 check
+                const uint64_t slot = di * (uint64_t)G.nStartup + (uint64_t)i;
+                a.t.dpair_key[slot] = due ? gen_ord64(L.qhead(p)) : ~0ull;
+                a.t.dpair_i[slot] = due ? (uint32_t)i : GEN_PAIR_NONE;
+            }
+            if (!due) continue;
             L.tk1 = (uint32_t)i;
             L.tk2 = L.qhead(p);
             L.sendTimerEvents(p);
@@ -1301,10 +1335,11 @@ __device__ void gen_timers_key(const GenArgs& a, uint32_t key, unsigned long lon
             }
         }
     }
-    sc = L.scanned;
-    cr = L.created;
-    ma = L.matches;
-    er = L.err;
+    a.t.nd[key] = L.nextDeadline();
+    sc += L.scanned;
+    cr += L.created;
+    ma += L.matches;
+    er |= L.err;
     for (uint32_t x = 0; x < L.resLeft; x++) {
         const unsigned long long rr = L.resBase + x;
         if (rr < L.resEnd) {
@@ -1315,11 +1350,52 @@ __device__ void gen_timers_key(const GenArgs& a, uint32_t key, unsigned long lon
 }
 }  // namespace
 
-extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6, 8))) k_gen_timers(const GenArgs* __restrict__ ap) {
+// next deadline of every key from its state (after a restore)
+extern "C" __global__ void __launch_bounds__(64) k_gen_deadlines(const GenArgs* __restrict__ ap) {
     const GenArgs& a = *ap;
     const uint32_t key = blockIdx.x * blockDim.x + threadIdx.x;
+    if (key >= a.K) return;
+    Lane L(a, key);
+    a.t.nd[key] = (L.W(0) & 1u) ? L.nextDeadline() : GEN_NO_DEADLINE;
+}
+
+// the keys due at this advance (nd <= now): wave-ballot compaction into t.due
+extern "C" __global__ void __launch_bounds__(256) k_gen_due(const int64_t* __restrict__ nd, uint32_t K, int64_t now,
+                                                            uint32_t* __restrict__ due,
+                                                            unsigned long long* __restrict__ ndue) {
+    const int lane = threadIdx.x & 63;
+    for (uint32_t base = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < K; base += gridDim.x * blockDim.x) {
+        const uint32_t k = base + (uint32_t)lane;
+        const bool d = k < K && nd[k] <= now;
+        const unsigned long long m = __ballot(d);
+        if (!m) continue;
+        unsigned long long b0 = 0;
+        if (lane == 0) b0 = atomicAdd(ndue, (unsigned long long)__popcll(m));
+        b0 = __shfl(b0, 0, 64);
+        if (d) due[b0 + __popcll(m & ((1ull << lane) - 1ull))] = k;
+    }
+}
+
+// sorted (due time, listener) pairs of one advance: two equal ones = two keys share a due time (A.10)
+extern "C" __global__ void __launch_bounds__(256) k_gen_collapse(const unsigned long long* __restrict__ key,
+                                                                 const uint32_t* __restrict__ li, uint64_t n,
+                                                                 uint32_t* __restrict__ err) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j == 0 || j >= n || li[j] == GEN_PAIR_NONE || key[j] != key[j - 1]) return;
+    for (uint64_t m = j; m-- > 0 && key[m] == key[j];)
+        if (li[m] == li[j]) { atomicOr(err, (uint32_t)GERR_COLLAPSE); return; }
+}
+
+// timer sweep over the due keys (every key when unpartitioned: key 0, seeded at start())
+extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6, 8))) k_gen_timers(const GenArgs* __restrict__ ap) {
+    const GenArgs& a = *ap;
+    const uint64_t n = a.G->partitioned ? *a.t.ndue : 1ull;
     unsigned long long sc = 0, cr = 0, ma = 0;
     uint32_t er = 0;
-    if (key < a.K) gen_timers_key(a, key, sc, cr, ma, er);
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        gen_timers_key(a, a.G->partitioned ? a.t.due[i] : 0u, i, sc, cr, ma, er);
+    unsigned long long mw = ma;
+    for (int off = 32; off > 0; off >>= 1) mw += __shfl_xor(mw, off, 64);
+    if ((threadIdx.x & 63) == 0 && mw) atomicAdd(a.o.nvalid, mw);  // timer matches of this wave
     gen_wave_stats(a, sc, cr, ma, 0, er);
 }

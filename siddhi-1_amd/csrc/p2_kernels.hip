@@ -5,6 +5,8 @@
 
 #include <rocprim/device/device_scan.hpp>
 
+#include <algorithm>
+
 #include "../../include/siddhi_gpu_ir.h"
 #include "sg_engine.h"
 
@@ -185,6 +187,15 @@ __global__ void __launch_bounds__(256) k_reset_keys(const uint32_t* __restrict__
     hdr[k] = 0u;
 }
 
+// validation of a device array of key ids: *bad = 1 if any id is outside [0, n_keys) (*bad is cleared
+// by the wrapper first)
+__global__ void __launch_bounds__(256) k_check_keys(const uint32_t* __restrict__ keys, uint32_t n, uint32_t n_keys,
+                                                    uint32_t* __restrict__ bad) {
+    bool b = false;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) b |= keys[i] >= n_keys;
+    if (__any(b) && (threadIdx.x & 63) == 0) atomicOr(bad, 1u);
+}
+
 __global__ void k_bump(unsigned long long* out_count, const unsigned long long* batch_total) {
     *out_count += *batch_total;
 }
@@ -225,6 +236,14 @@ int sgd_launch_reset_keys(const uint32_t* keys, uint32_t n, uint32_t n_keys, uin
                           ihipStream_t* stream) {
     if (n == 0) return 0;
     hipLaunchKernelGGL(k_reset_keys, dim3((n + 255) / 256), dim3(256), 0, stream, keys, n, n_keys, hdr, err);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int sgd_launch_check_keys(const uint32_t* keys, uint32_t n, uint32_t n_keys, uint32_t* bad, ihipStream_t* stream) {
+    if (hipMemsetAsync(bad, 0, 4, stream) != hipSuccess) return -1;
+    if (n == 0) return 0;
+    const uint32_t blocks = std::min<uint32_t>((n + 255) / 256, 1024u);
+    hipLaunchKernelGGL(k_check_keys, dim3(blocks), dim3(256), 0, stream, keys, n, n_keys, bad);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -140,6 +140,8 @@ size_t sgd_scatter_scan_bytes(uint32_t max_n);
 // partition purge: hdr[keys[i]] = 0 (key range errors -> err)
 int sgd_launch_reset_keys(const uint32_t* keys, uint32_t n, uint32_t n_keys, uint32_t* hdr, uint32_t* err,
                           ihipStream_t* stream);
+// *bad = 1 iff some keys[i] >= n_keys (device ids of sg_reset_keys, checked before any reset)
+int sgd_launch_check_keys(const uint32_t* keys, uint32_t n, uint32_t n_keys, uint32_t* bad, ihipStream_t* stream);
 // sums the staged pass's per-wave counters of one batch into stats[SGD_ST_N]
 int sgd_launch_stats_reduce(const unsigned long long* wstats, uint32_t n_waves, unsigned long long* stats,
                             ihipStream_t* stream);

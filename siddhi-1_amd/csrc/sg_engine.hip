@@ -443,9 +443,9 @@ void build_plan(sg_engine* e, const void* ir, size_t len) {
     }
     size_t pos = 0;
     Node root = read_node(w + offN, nN, pos);
-    if (qtype != SG_Q_PATTERN)
-        throw std::runtime_error("HIP engine: SEQUENCE queries are not on the device yet (oracle only)");
-    if (nslots != 2) throw std::runtime_error("HIP engine: only two-state patterns run on the device so far");
+    // shapes outside the two-state kernel run on the general device engine (gen_host.hip)
+    if (qtype != SG_Q_PATTERN) throw std::runtime_error("SEQUENCE query: general device engine");
+    if (nslots != 2) throw std::runtime_error("not a two-state pattern: general device engine");
     const Node *a = nullptr, *b = nullptr;
     if (root.tag == SG_N_NEXT) {
         const Node& x = root.kids[0];
@@ -463,8 +463,8 @@ void build_plan(sg_engine* e, const void* ir, size_t len) {
         b = &root.kids[0].kids[1];
         pl.mode = SGD_P2_EVERY_BOTH;
     }
-    if (!a || !b) throw std::runtime_error("HIP engine: pattern shape not supported on the device yet");
-    if (a->absent || b->absent) throw std::runtime_error("HIP engine: absent states are not on the device yet");
+    if (!a || !b) throw std::runtime_error("pattern shape outside the two-state kernel: general device engine");
+    if (a->absent || b->absent) throw std::runtime_error("absent state: general device engine");
     pl.s0 = (int)a->stream;
     pl.s1 = (int)b->stream;
     pl.slot0 = a->slot;
@@ -700,12 +700,31 @@ int push(sg_engine* e, const sg_batch* b) {
         }
         if (pk.nul[c]) any_null = true;
     }
-    if (any_null) e->nullable = true;
-    sg_engine::Variant& v = variant(e, any_null, e->nullable);
+    // the engine state (sequence window, null variant, counters) changes only once the batch has
+    // passed validation: a rejected batch leaves the engine as it was, so the caller may fix it and
+    // push again at the same seq_base
+    const bool nullable = e->nullable || any_null;
+    sg_engine::Variant& v = variant(e, any_null, nullable);
     const uint32_t words = sgj_col_words(coltypes) + (any_null ? 1u : 0u);
     const uint32_t stride = sgj_stride(words);
     if (stride > e->pay_words) throw HipError("payload stride above the allocated payload");
     pk.payload = (uint32_t*)e->pay;
+
+    // ---- grouping by key: the batch as key-sorted payload elements + per-key segment bounds ----
+    hipEvent_t g0 = nullptr, g1 = nullptr;
+    const uint32_t pack_blocks = (n + 255) / 256;
+    const uint32_t* keys = b->key;
+    if (pl.partitioned && !dev) {
+        // the copy is queued first, so the host range check overlaps the DMA (pinned batches); the
+        // staging buffers it fills are not engine state
+        HIP_OK(hipMemcpyAsync(e->b_key, b->key, (size_t)n * 4, kind, e->stream));
+        keys = e->b_key;
+        if (sgd_max_key(b->key, n) >= e->K) {
+            HIP_OK(hipStreamSynchronize(e->stream));  // the queued copies read the caller's buffers
+            return fail(SG_ERR_INVALID, "key id outside [0, n_keys)");
+        }
+    }
+    e->nullable = nullable;
     if (!e->have_base) {
         e->poll_base = b->seq_base;
         e->have_base = true;
@@ -713,22 +732,8 @@ int push(sg_engine* e, const sg_batch* b) {
     e->next_seq = b->seq_base + b->n;
     e->st.events += b->n;
     e->st.batches++;
-
-    // ---- grouping by key: the batch as key-sorted payload elements + per-key segment bounds ----
-    hipEvent_t g0 = nullptr, g1 = nullptr;
     if (e->timing) { g0 = e->ev(); e->mark(g0); }
-    const uint32_t pack_blocks = (n + 255) / 256;
     if (pl.partitioned) {
-        const uint32_t* keys = b->key;
-        if (!dev) {
-            // the copy is queued first, so the host range check overlaps the DMA (pinned batches)
-            HIP_OK(hipMemcpyAsync(e->b_key, b->key, (size_t)n * 4, kind, e->stream));
-            keys = e->b_key;
-            if (sgd_max_key(b->key, n) >= e->K) {
-                HIP_OK(hipStreamSynchronize(e->stream));  // the queued copies read the caller's buffers
-                return fail(SG_ERR_INVALID, "key id outside [0, n_keys)");
-            }
-        }
         size_t tmp = e->sort_tmp_bytes;
         if (words <= 4) {
             // sort the events WITH their payload (packed on the fly by the first radix pass): the
@@ -848,7 +853,13 @@ int poll(sg_engine* e, uint32_t mem, sg_match_batch* out) {
     uint32_t err = 0;
     std::memcpy(&err, &status[1], 4);
     e->resolve_spans();
-    if (err & SGD_ERR_KEY_RANGE) return fail(SG_ERR_INVALID, "a batch carried key ids outside [0, n_keys)");
+    if (err & SGD_ERR_KEY_RANGE) {
+        // reported once: the events with valid keys were processed, the others dropped; the engine
+        // goes on (capacity errors below stay: partials were lost)
+        const uint32_t rest = err & ~(uint32_t)SGD_ERR_KEY_RANGE;
+        HIP_OK(hipMemcpy(e->err, &rest, 4, hipMemcpyHostToDevice));
+        return fail(SG_ERR_INVALID, "a batch carried key ids outside [0, n_keys) (those events were dropped)");
+    }
     if (err & SGD_ERR_PARTIAL_CAP)
         return fail(SG_ERR_CAPACITY, "a partition key exceeded partial_capacity live partial matches");
     if ((err & SGD_ERR_MATCH_CAP) || n > e->mcap)
@@ -1082,9 +1093,21 @@ int sg_reset_keys(sg_engine* e, const uint32_t* keys, uint64_t n, uint32_t mem) 
         if (mem == SG_MEM_HOST) {
             for (uint64_t i = 0; i < n; i++)
                 if (keys[i] >= K) return fail(SG_ERR_INVALID, "key id outside [0, n_keys)");
-            HIP_OK(hipMalloc(&tmp, n * 4));
+            HIP_OK(hipMalloc(&tmp, n * 4 + 4));
             HIP_OK(hipMemcpyAsync(tmp, keys, n * 4, hipMemcpyHostToDevice, e->stream));
             dk = tmp;
+        } else {
+            // device ids: validated before any state changes (all or nothing, as for host ids)
+            HIP_OK(hipMalloc(&tmp, 4));
+            if (sgd_launch_check_keys(dk, (uint32_t)n, K, tmp, e->stream) != 0)
+                throw HipError("k_check_keys launch failed");
+            uint32_t bad = 0;
+            HIP_OK(hipMemcpyAsync(&bad, tmp, 4, hipMemcpyDeviceToHost, e->stream));
+            HIP_OK(hipStreamSynchronize(e->stream));
+            if (bad) {
+                HIP_OK(hipFree(tmp));
+                return fail(SG_ERR_INVALID, "key id outside [0, n_keys)");
+            }
         }
         int rc = SG_OK;
         std::string msg;
@@ -1097,11 +1120,6 @@ int sg_reset_keys(sg_engine* e, const uint32_t* keys, uint64_t n, uint32_t mem) 
         HIP_OK(hipStreamSynchronize(e->stream));
         if (tmp) HIP_OK(hipFree(tmp));
         if (rc != SG_OK) return fail(rc, msg);
-        if (!e->gen) {
-            uint32_t err = 0;
-            HIP_OK(hipMemcpy(&err, e->err, 4, hipMemcpyDeviceToHost));
-            if (err & SGD_ERR_KEY_RANGE) return fail(SG_ERR_INVALID, "key id outside [0, n_keys)");
-        }
         return SG_OK;
     } catch (const std::exception& ex) {
         return fail(SG_ERR_DEVICE, ex.what());

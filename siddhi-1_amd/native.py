@@ -140,6 +140,8 @@ class KeyDictionary:
         L.sg_dict_size.argtypes = [C.c_void_p]
         L.sg_dict_size.restype = C.c_uint32
         L.sg_dict_key.argtypes = [C.c_void_p, C.c_uint32, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]
+        L.sg_dict_remove.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
+        L.sg_dict_put.argtypes = [C.c_void_p, C.c_uint32, C.c_char_p, C.c_uint64]
         L.sg_dict_clear.argtypes = [C.c_void_p]
         L.sg_dict_destroy.argtypes = [C.c_void_p]
         L.sg_dict_destroy.restype = None
@@ -174,6 +176,21 @@ class KeyDictionary:
         self._check(self._lib.sg_dict_key(self._h, i, C.byref(p), C.byref(n)))
         return C.string_at(p, n.value).decode("utf-8") if n.value else ""
 
+    def remove(self, ids):
+        """Partition purge: the ids leave the dictionary; later new keys reuse them, smallest first
+        (all-or-nothing; an id not in use raises EngineError SG_ERR_INVALID)."""
+        a = np.ascontiguousarray(ids, dtype=np.uint32)
+        self._check(self._lib.sg_dict_remove(self._h, _np_ptr(a) if len(a) else None, len(a)))
+
+    def put(self, i, k):
+        """Bind key string k to the free id i (snapshot restore)."""
+        b = k.encode("utf-8")
+        self._check(self._lib.sg_dict_put(self._h, i, b, len(b)))
+
+    def _live(self, i):
+        p, n = C.c_void_p(), C.c_uint64()
+        return self._lib.sg_dict_key(self._h, i, C.byref(p), C.byref(n)) == SG_OK
+
     # the dict protocol of the host runtime --------------------------------------------------------
     def __len__(self):
         return int(self._lib.sg_dict_size(self._h))
@@ -196,14 +213,16 @@ class KeyDictionary:
             raise ValueError("key ids are assigned in first-seen order")
 
     def keys(self):
-        return [self.key(i) for i in range(len(self))]
+        """key string per id below the id bound, None for a removed (free) id"""
+        return [self.key(i) if self._live(i) else None for i in range(len(self))]
 
     def clear(self):
         self._check(self._lib.sg_dict_clear(self._h))
 
     def update(self, mapping):
+        """bind every key -> id of mapping (ids in between stay free)"""
         for k, v in sorted(mapping.items(), key=lambda kv: kv[1]):
-            self[k] = v
+            self.put(int(v), k)
 
     def close(self):
         if getattr(self, "_h", None):

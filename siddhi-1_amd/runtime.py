@@ -481,7 +481,9 @@ class _Purge:
     every `interval` of wall time the keys idle for more than `idle.period` are dropped from every query
     of the partition (cleanGroupByStates), so their next event starts them afresh.  The reference runs
     this on an executor thread at fixed delay; here it runs when the runtime's clock is read (sends and
-    the harness's wall-clock advances).  Key ids stay in the dictionary (the device state is reset)."""
+    the harness's wall-clock advances).  The idle keys' device state is reset (sg_reset_keys) and their
+    ids leave the partition's key dictionary (sg_dict_remove), so new keys reuse them: the live keys, not
+    the keys ever seen, are bounded by n_keys, as the reference's maps are bounded by its purge."""
 
     @staticmethod
     def _ann(p):
@@ -518,8 +520,13 @@ class _Purge:
         ids = [kd[k] for k in idle if k in kd]
         for k in idle:
             del self.last_seen[k]
+        gone = set(ids)
         for qr in self.queries:
             qr.engine.reset_keys(ids)
+            # the selector's per-partition aggregator states go with the key (cleanGroupByStates)
+            qr._agg_states = {k: v for k, v in qr._agg_states.items() if k[0] not in gone}
+        if ids and self.queries:
+            kd.remove(ids)
         return idle
 
 
@@ -704,7 +711,7 @@ class SiddhiAppRuntime:
         for qr, qs in zip(self.queries, head["queries"]):
             if qr.key_dict is not None:
                 qr.key_dict.clear()
-                qr.key_dict.update({k: i for i, k in enumerate(qs["keys"])})
+                qr.key_dict.update({k: i for i, k in enumerate(qs["keys"]) if k is not None})
             qr._agg_states = _dec(qs["aggs"])
         for pg, seen in zip(self._purges, head.get("purge_last_seen", [])):
             pg.last_seen = dict(seen)

@@ -114,3 +114,63 @@ def test_runtime_partitions_through_the_native_dictionary():
     kd = rt.key_dicts[next(iter(rt.key_dicts))]
     assert isinstance(kd, native.KeyDictionary) and kd.keys() == ["A", "B"]
     assert sorted(got) == sorted([("A", 26.0), ("B", 31.0), ("B", 31.0)])
+
+
+def test_remove_recycles_ids_smallest_first_and_keeps_live_ids_bounded():
+    """@purge key churn (PartitionRuntimeImpl.java:368-401 drops idle keys from its maps): removed ids
+    are handed out again, smallest first, so max_ids bounds the LIVE keys, not the keys ever seen."""
+    kd = native.KeyDictionary(max_ids=4)
+    np.testing.assert_array_equal(kd.intern(["a", "b", "c", "d"]), [0, 1, 2, 3])
+    with pytest.raises(sa.EngineError):
+        kd.intern(["e"])
+    kd.remove([2, 0])
+    assert "a" not in kd and "c" not in kd and kd.keys() == [None, "b", None, "d"]
+    with pytest.raises(sa.EngineError):
+        kd.key(0)
+    np.testing.assert_array_equal(kd.intern(["e", "b", "f"]), [0, 1, 2])
+    with pytest.raises(sa.EngineError):     # full again; the failed batch changes nothing
+        kd.intern(["g", "h"])
+    assert kd.keys() == ["e", "b", "f", "d"]
+    with pytest.raises(sa.EngineError):
+        kd.remove([1, 1])                   # listed twice: all-or-nothing
+    with pytest.raises(sa.EngineError):
+        kd.remove([3, 7])                   # not in use
+    assert kd.keys() == ["e", "b", "f", "d"]
+
+
+def test_remove_rollback_and_put():
+    kd = native.KeyDictionary(max_ids=3)
+    kd.intern(["a", "b", "c"])
+    kd.remove([1])
+    with pytest.raises(sa.EngineError):     # "x" takes the free id 1, "y" would exceed max_ids
+        kd.intern(["x", "y"])
+    assert kd.keys() == ["a", None, "c"] and "x" not in kd
+    assert int(kd.intern(["y"])[0]) == 1
+    kd.clear()
+    kd.update({"p": 0, "r": 2})             # restore a key map with a hole
+    assert kd.keys() == ["p", None, "r"]
+    assert int(kd.intern(["q"])[0]) == 1
+
+
+def test_churn_many_keys_through_a_small_dictionary():
+    """100k distinct keys over time through a 1000-id dictionary, purging the oldest half whenever it
+    fills: ids stay below max_ids, every live key maps to its own id, removed keys are gone"""
+    rng = np.random.default_rng(3)
+    kd = native.KeyDictionary(max_ids=1000, capacity_hint=16)
+    live = {}
+    nxt = 0
+    while nxt < 100_000:
+        batch = [f"K{nxt + i}" for i in range(int(rng.integers(1, 200)))]
+        if len(live) + len(batch) > 1000:
+            old = sorted(live, key=lambda k: int(k[1:]))[: len(live) // 2]
+            kd.remove([live[k] for k in old])
+            for k in old:
+                del live[k]
+        ids = kd.intern(batch)
+        for k, i in zip(batch, ids):
+            live[k] = int(i)
+        nxt += len(batch)
+        assert max(live.values()) < 1000 and len(set(live.values())) == len(live)
+    for k, i in list(live.items())[::37]:
+        assert kd.key(i) == k and kd[k] == i
+    assert "K0" not in kd

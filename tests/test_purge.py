@@ -111,3 +111,35 @@ def test_purge_annotation_errors():
         oracle_manager().createSiddhiAppRuntime(PURGE_APP.replace("enable='true'", "enable='yes'"))
     with pytest.raises(sa.SiddhiAppCreationException):
         oracle_manager().createSiddhiAppRuntime(PURGE_APP.replace(", idle.period='2 sec'", ""))
+
+
+def test_runtime_purge_recycles_key_ids_under_churn():
+    """more distinct keys over time than n_keys: purged keys' ids are reused by new keys (sg_dict_remove),
+    and a reused id starts from the never-seen state (no partial or aggregate of the old key leaks)"""
+    app = (STOCK + "@purge(enable='true', interval='1 sec', idle.period='1 sec') "
+           "partition with (symbol of S) begin from every e1=S[price>20] -> e2=S[price>e1.price] "
+           "select e1.symbol as s, e1.price as p1, e2.price as p2, count() as c insert into O; end;")
+    lib = build_oracle()
+
+    def factory(ir, n_keys):
+        return sa.NativeEngine(lib, "sgo_", ir, n_keys=n_keys, max_batch=64, partial_capacity=16,
+                               match_capacity=1024)
+
+    rt = sa.SiddhiAppRuntime(app, factory, n_keys=4)
+    cb = _Collect()
+    rt.addCallback("O", cb)
+    rt.set_wall_clock(1_000_000)
+    rt.start()
+    h = rt.getInputHandler("S")
+    wall = 1_000_000
+    for gen in range(10):                 # 10 generations of 4 keys = 40 distinct keys through 4 ids
+        for k in range(4):
+            h.send([f"G{gen}K{k}", 25.0, 1])
+        for k in range(4):
+            h.send([f"G{gen}K{k}", 26.0, 1])
+        wall += 3000                      # every key of this generation goes idle and is purged
+        rt.advance_wall_clock(wall)
+    kd = next(iter(rt.key_dicts.values()))
+    assert len(kd) <= 4
+    # each key matched once (its own e1 -> e2), with a fresh count: nothing leaked across a reused id
+    assert sorted(cb.events) == sorted([[f"G{g}K{k}", 25.0, 26.0, 1] for g in range(10) for k in range(4)])
