@@ -273,9 +273,10 @@ def main():
     value = events_all / el
 
     launches = max(1, dst["advance_launches"])
-    # the dominant kernel is the LDS-staged pass k_adv_m; the HBM pass (k_adv_m_h: waves whose payload
-    # range did not fit LDS, keys whose window could overflow) is timed separately and reported beside it
-    adv_s = (dst["advance_ns"] - dst["advance_hbm_ns"]) / 1e9 / launches
+    # the dominant kernel is the NFA advance: the LDS-staged pass k_adv_m plus the HBM pass k_adv_m_h
+    # (waves whose payload range did not fit LDS, keys whose window could overflow); the algorithmic
+    # bytes cover every event of the batch, so they are priced over both passes' time
+    adv_s = dst["advance_ns"] / 1e9 / launches
     adv_h_s = dst["advance_hbm_ns"] / 1e9 / launches
     alg = algorithmic_bytes(dst) / launches
     achieved = alg / adv_s / 1e9 if adv_s > 0 else 0.0
@@ -300,7 +301,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes/launch",
                      "traffic_source": traffic_src,
-                     "kernel": "k_adv_m", "alg_bytes_per_launch": alg,
+                     "kernel": "k_adv_m + k_adv_m_h (NFA advance)", "alg_bytes_per_launch": alg,
                      "kernel_ms_per_launch": adv_s * 1e3, "hbm_pass_ms_per_launch": adv_h_s * 1e3},
         "stages_ms_per_step": {"group": dst["group_ns"] / 1e6 / args.steps,
                                "advance": dst["advance_ns"] / 1e6 / args.steps,

@@ -18,6 +18,10 @@ __device__ __forceinline__ void seg_bound_one(uint32_t i, uint32_t k, uint32_t p
                                               uint32_t* __restrict__ seg_end, uint32_t* __restrict__ err) {
     if (k >= n_keys) {  // key id outside [0, n_keys): reject the batch loudly, never write out of bounds
         atomicOr(err, (uint32_t)SGD_ERR_KEY_RANGE);
+        // such ids sort after every valid one: the first of them closes the bounds of the keys above
+        // the last valid run (no key keeps a stale segment of an earlier batch)
+        if (prev != k && (i == 0 || prev < n_keys))
+            for (uint32_t g = (i == 0) ? 0u : prev + 1; g < n_keys; ++g) seg_begin[g] = seg_end[g] = i;
         return;
     }
     if (prev != k) {

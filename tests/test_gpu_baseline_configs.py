@@ -217,8 +217,8 @@ def test_timers_distinct_due_times_across_many_keys_bit_exact():
     """many keys, advances that make only some keys due (due-key compaction picks exactly those), timers
     armed by batches and by earlier firings, checked against the oracle on every key"""
     q = ("@app:playback define stream S (symbol string, price float, volume int);\n"
-         "partition with (symbol of S) begin from every e1=S[price>20] -> not S[price>e1.price] for 50 ms "
-         "within 400 ms select e1.price as a insert into O; end;")
+         "partition with (symbol of S) begin from every e1=S[price>20] -> not S[price>e1.price] for 50 milliseconds "
+         "within 400 milliseconds select e1.price as a insert into O; end;")
     K = 4096
     gpu, ora = _engines(q, K, 1 << 14, 48, 1 << 20)
     rng = np.random.default_rng(12)
