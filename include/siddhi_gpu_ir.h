@@ -57,6 +57,8 @@
  *     SG_OP_AND, SG_OP_OR, SG_OP_NOT                      (never null; not(null) = true)
  *     SG_OP_ISNULL                                        (value is null)
  *     SG_OP_ISNULL_EV   b=slot  w1=chain index            (`e1 is null`: stream event absent)
+ *     SG_OP_IFELSE a=result type  pops cond, then, else   (ifThenElse(c, x, y): x iff c is a non-null
+ *                                                          true, else y; IfThenElseFunctionExecutor.java)
  *   A filter passes iff the program leaves a non-null true (FilterProcessor.java:48-60).
  */
 #ifndef SIDDHI_GPU_IR_H
@@ -115,7 +117,8 @@ enum sg_opcode {
     SG_OP_OR = 31,
     SG_OP_NOT = 32,
     SG_OP_ISNULL = 33,
-    SG_OP_ISNULL_EV = 34
+    SG_OP_ISNULL_EV = 34,
+    SG_OP_IFELSE = 40
 };
 
 /* instruction lengths in words */

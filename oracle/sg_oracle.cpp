@@ -1179,6 +1179,12 @@ bool Engine::eval(const StateEvent* se, uint32_t pc, uint32_t len) const {
             stk[sp++] = Val{(uint64_t)(ev == nullptr), false};
             break;
         }
+        case SG_OP_IFELSE: {  // IfThenElseFunctionExecutor.java:127-133, 148-159: Boolean.TRUE.equals(cond)
+            const bool c = !stk[sp - 3].null && (stk[sp - 3].b & 1);
+            stk[sp - 3] = c ? stk[sp - 2] : stk[sp - 1];
+            sp -= 2;
+            break;
+        }
         default: throw std::runtime_error("bad opcode");
         }
         pc += sg_op_len(op);

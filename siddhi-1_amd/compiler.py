@@ -40,6 +40,7 @@ OP_VAR, OP_CONST, OP_CVT = 1, 2, 3
 OP_ARITH = {"+": 10, "-": 11, "*": 12, "/": 13, "%": 14}
 OP_CMP = {"==": 20, "!=": 21, ">": 22, ">=": 23, "<": 24, "<=": 25}
 OP_AND, OP_OR, OP_NOT, OP_ISNULL, OP_ISNULL_EV = 30, 31, 32, 33, 34
+OP_IFELSE = 40
 
 NUMERIC = ("INT", "LONG", "FLOAT", "DOUBLE")
 _RANK = {"INT": 0, "LONG": 1, "FLOAT": 2, "DOUBLE": 3}
@@ -105,7 +106,8 @@ class CompiledQuery:
     streams: List[q.StreamDef]           # IR stream table order
     slots: List[SlotInfo]
     within_ms: Optional[int]
-    partition_keys: dict                 # stream name -> attr name (partitioned queries)
+    partition_keys: dict                 # stream name -> attr name (partitioned queries); None: the
+                                         # stream is not keyed, its events go to every known key
     select: list                         # [(name, type, expr-tree with ResolvedVar leaves)]
     output_stream: Optional[str]
     query: q.Query
@@ -244,7 +246,13 @@ def type_expr(ctx: _Ctx, e, resolve, funcs=None):
         return _Typed("var", "OBJECT" if rv.multi_value else rv.type, var=rv)
     if isinstance(e, q.IsNullStream):
         # `e1 is null` inside a state query: the stream event itself (IsNullStreamConditionExpressionExecutor)
-        v = resolve(q.Var("__stream__", e.stream, e.index))
+        try:
+            v = resolve(q.Var("__stream__", e.stream, e.index))
+        except SiddhiAppCreationException:
+            if e.index is not None:
+                raise
+            # not a stream reference: `<attribute> is null` (e.g. an output attribute in `having`)
+            return _Typed("isnull", "BOOL", arg=type_expr(ctx, q.Var(e.stream, None, None), resolve, funcs))
         return _Typed("isnull_ev", "BOOL", slot=v.slot, chain=v.chain_index)
     if isinstance(e, q.IsNull):
         inner = type_expr(ctx, e.expr, resolve, funcs)
@@ -272,6 +280,17 @@ def type_expr(ctx: _Ctx, e, resolve, funcs=None):
         if e.op in OP_ARITH:
             t = arith_type(lt.type, rt.type)
             return _Typed("arith", t, op=e.op, left=lt, right=rt)
+    if isinstance(e, q.Func) and e.namespace is None and e.name == "ifThenElse":
+        # IfThenElseFunctionExecutor.init (C/executor/function/IfThenElseFunctionExecutor.java:101-121):
+        # three arguments, a BOOL condition, then / else of the same type (the result type)
+        if len(e.args) != 3:
+            raise SiddhiAppCreationException("ifThenElse() needs 3 arguments")
+        c, x, y = (type_expr(ctx, a, resolve, funcs) for a in e.args)
+        if c.type != "BOOL":
+            raise SiddhiAppCreationException(f"ifThenElse() condition must be BOOL, not {c.type}")
+        if x.type != y.type:
+            raise SiddhiAppCreationException(f"ifThenElse() then / else types differ: {x.type} and {y.type}")
+        return _Typed("ifelse", x.type, cond=c, left=x, right=y)
     if isinstance(e, q.Func):
         if funcs is not None:
             return funcs(e)
@@ -340,6 +359,13 @@ class _Emitter:
             self.emit(t.left)
             self.emit(t.right)
             self.hdr(OP_AND if k == "and" else OP_OR)
+            return
+        if k == "ifelse":
+            self.emit(t.cond)
+            self.emit(t.left)
+            self.emit(t.right)
+            self.hdr(OP_IFELSE, TYPE_CODE[t.type])
+            self.cvt(t.type, want)
             return
         if k == "cmp":
             self.emit(t.left, t.dom)
@@ -523,8 +549,11 @@ def compile_query(app: q.App, query: q.Query, strings) -> CompiledQuery:
             partition_keys[stream] = attr
         for s in ctx.streams:
             if s.name not in partition_keys:
-                raise SiddhiAppCreationException(
-                    f"stream {s.name} of a partitioned pattern must be a partition-with stream")
+                # a stream the partition does not key: each of its events goes to every partition key
+                # known at that moment (PartitionStreamReceiver.receive with no partition executor ->
+                # send(ComplexEvent), C/partition/PartitionStreamReceiver.java:83-92, 275-283)
+                partition_keys[s.name] = None
+                continue
             if s.attr_index(partition_keys[s.name]) < 0:
                 raise SiddhiAppCreationException(f"partition attribute {partition_keys[s.name]} "
                                                  f"not in {s.name}")

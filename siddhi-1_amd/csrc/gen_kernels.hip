@@ -494,6 +494,14 @@ struct Lane {
                 break;
             }
             case SG_OP_ISNULL: t0 = {(uint64_t)t0.null, false}; break;
+            case SG_OP_IFELSE: {  // ifThenElse(cond, then, else): three popped, one pushed
+                const GVal c = sp >= 3 ? stk[sp - 3] : GVal{0, true};
+                t0 = (!c.null && (c.b & 1)) ? t1 : t0;
+                t1 = sp >= 4 ? stk[sp - 4] : GVal{0, true};
+                sp -= 2;
+                pc += op_len(op);
+                continue;
+            }
             default: err |= GERR_REF; return false;
             }
             if (push) {

@@ -292,6 +292,8 @@ class _QueryRuntime:
             return not (self._eval(t.arg, chains, store) is True)
         if k == "isnull":
             return self._eval(t.arg, chains, store) is None
+        if k == "ifelse":   # IfThenElseFunctionExecutor: Boolean.TRUE.equals(cond) ? then : else
+            return self._eval(t.left if self._eval(t.cond, chains, store) is True else t.right, chains, store)
         if k == "agg":
             return self._aggregate(t, chains, store)
         if k == "instof":
@@ -791,6 +793,24 @@ class SiddhiAppRuntime:
                 pg.run(self.current_time())
                 pg.next_run += pg.interval
 
+    def _send_broadcast(self, qr, si, sd, events):
+        """An event of a stream the partition does not key goes to every partition key known at that
+        moment, the whole chunk per key (PartitionStreamReceiver.receive -> send(ComplexEvent),
+        C/partition/PartitionStreamReceiver.java:83-92, 275-283; no initPartition: a key is created only by
+        its own streams).  The reference iterates a HashSet copy of the keys (unspecified order); here the
+        keys go in id order.  Each (key, event) copy is one engine event with its own arrival seq."""
+        ids = [i for i, k in enumerate(qr.key_dict.keys()) if k is not None]
+        if not ids or not events:
+            return
+        n = len(events)
+        seqs = [self.store.add(sd.name, ts, tuple(data)) for _ in ids for ts, data in events]
+        ts_all = np.array([e[0] for e in events] * len(ids), dtype=np.int64)
+        rows = [e[1] for e in events] * len(ids)
+        cols, nulls = self._columns(sd, rows)
+        kk = np.repeat(np.array(ids, dtype=np.uint32), n)
+        qr.engine.push(si, seqs[0], ts_all, cols, nulls, kk)
+        qr.dispatch(qr.project(qr.engine.poll(), self.store))
+
     def _send(self, stream, events, explicit=True):
         if stream not in self.app.streams:
             raise KeyError(stream)
@@ -814,6 +834,9 @@ class SiddhiAppRuntime:
             rows = [e[1] for e in events]
             keys = None
             keep = list(range(len(events)))
+            if qr.cq.partitioned and qr.cq.partition_keys[stream] is None:
+                self._send_broadcast(qr, si, sd, events)
+                continue
             if qr.cq.partitioned:
                 attr = qr.cq.partition_keys[stream]
                 ai = sd.attr_index(attr)

@@ -40,6 +40,9 @@ def same(exp, act):
     if exp is None or act is None:
         return exp is None and act is None
     t = exp["t"]
+    if t == "list":   # a count state's attribute over its chain (List / Object[] compared element-wise)
+        return isinstance(act, (list, tuple)) and len(act) == len(exp["v"]) and \
+            all(same(e, a) for e, a in zip(exp["v"], act))
     if t in ("float", "double"):
         a = np.float32(act) if t == "float" else float(act)
         e = np.float32(exp["v"]) if t == "float" else float(exp["v"])

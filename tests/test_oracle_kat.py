@@ -16,9 +16,9 @@ FEATURES_UNSUPPORTED = set()
 # reference tests whose apps use constructs outside the pattern hot path (SURVEY §8f / out of scope);
 # they must fail at compile time with a clear message, never silently.
 KNOWN_UNSUPPORTED = {
-    "PatternPartitionTestCase::testPatternPartitionQuery30": "inner partition streams (#Stream)",
-    "PatternPartitionTestCase::testPatternPartitionQuery32": "unpartitioned stream inside a partition",
-    "PatternPartitionTestCase::testPatternPartitionQuery33": "non-pattern query in the app",
+    "PatternPartitionTestCase::testPatternPartitionQuery32": "inner partition streams (#StockQuote) feeding "
+                                                             "a non-pattern query",
+    "PatternPartitionTestCase::testPatternPartitionQuery33": "non-pattern query (inner stream #Stream1) in the app",
 }
 
 # faithful but slow: a playback app started at event time 0 whose `every not ... for 1 sec` timer
