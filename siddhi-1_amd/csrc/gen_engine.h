@@ -16,6 +16,16 @@
 
 #include <stdint.h>
 
+// Per-key state layout.  GEN_AOS = 0: word w of key k at w * K + k (adjacent lanes = adjacent keys, a
+// converged wave's access to one field is one coalesced transaction); GEN_AOS = 1: each key's block is
+// contiguous (a lane's repeated accesses to its own key's header, lists and records share cache lines).
+#ifndef GEN_AOS
+#define GEN_AOS 0
+#endif
+__host__ __device__ inline size_t gen_at(uint32_t K, uint32_t blockWords, uint32_t k, uint32_t w) {
+    return GEN_AOS ? (size_t)k * blockWords + w : (size_t)w * K + k;
+}
+
 #define GEN_MAXP 16      // processors per query
 #define GEN_MAXS 8       // input streams
 #define GEN_MAXSLOT 16   // state slots

@@ -62,7 +62,11 @@ struct Lane {
     }
 
     // ---- HBM words of this key ----
+#if GEN_AOS
+    __device__ __forceinline__ uint32_t& W(uint32_t w) const { return S[(size_t)k * G.blockWords + w]; }
+#else
     __device__ __forceinline__ uint32_t& W(uint32_t w) const { return S[(size_t)w * K + k]; }
+#endif
     __device__ __forceinline__ int64_t R64(uint32_t w) const {
         return (int64_t)((uint64_t)W(w) | ((uint64_t)W(w + 1) << 32));
     }
@@ -1079,6 +1083,11 @@ struct Lane {
             if (P.kind == GK_LOGICAL) { processAndReturnAbsentLogical(p, seq, ts, pos); return; }
         }
         const uint32_t out0 = nOut;
+        // The reference clones the event into a fresh StreamEvent per pending partial
+        // (StreamPreStateProcessor.java:373).  A stream or logical state's slot event is never appended
+        // to (only count chains and absent-logical slots are), so one reference-counted copy per
+        // (event, processor) is indistinguishable and saves a record write per partial.
+        uint32_t shared = GEN_NIL;
         uint32_t i = 0;
         while (i < len(p, 0)) {
             const uint32_t se = at(p, 0, i);
@@ -1114,8 +1123,11 @@ struct Lane {
             }
             // StreamPreStateProcessor.java:371-397
             stIncref(se);
-            const uint32_t e = newEv(seq, ts, pos, false);
-            setSlot(se, P.stateId, e);
+            if (shared == GEN_NIL) {
+                shared = newEv(seq, ts, pos, false);
+                evIncref(shared);  // held until the loop ends
+            }
+            setSlot(se, P.stateId, shared);
             runChain(p, se);
             if ((retm >> P.thisLast) & 1u) {
                 retm &= ~(1u << P.thisLast);
@@ -1136,6 +1148,7 @@ struct Lane {
             stDecref(se);
             if (!removed) i++;
         }
+        evDecref(shared);
         if (P.absent) {  // AbsentStreamPreStateProcessor.processAndReturn returns nothing (:265-283)
             for (uint32_t j = out0; j < nOut; j++) stDecref(outList[j]);
             nOut = out0;

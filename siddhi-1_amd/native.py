@@ -24,6 +24,9 @@ ERRORS = {-1: "SG_ERR_INVALID", -2: "SG_ERR_UNSUPPORTED", -3: "SG_ERR_DEVICE",
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 HIP_LIBRARY = os.path.join(HERE, "lib", "libsiddhi_gpu.so")
+# experiments only (tools/): an alternative build of the same library (e.g. another state layout)
+if os.environ.get("SG_HIP_LIBRARY"):
+    HIP_LIBRARY = os.path.abspath(os.environ["SG_HIP_LIBRARY"])
 
 
 class EngineError(RuntimeError):
