@@ -1,17 +1,22 @@
-"""Benchmark: partitioned pattern query on MI355X (BASELINE.json configs[1], "C2").
+"""Benchmark: partitioned pattern query on MI355X (BASELINE.json configs[1] "C2" at N=1, configs[4] "C5"
+at N>1).
 
     every e1=StockStream[price > 20] -> e2=StockStream[price > e1.price] within 10 sec
-    partition with (symbol of StockStream), 1,048,576 synthetic keys per GPU
+    partition with (symbol of StockStream)
+    N = 1: 1,048,576 synthetic keys (C2);  N > 1: 2^23 keys per GPU (C5: 64M keys on 8 GPUs)
 
 A step = one micro-batch of 2^24 synthetic stock ticks per GPU (already resident in HBM) pushed
 through the C-ABI (key grouping + NFA advance) and polled (matches ordered by trigger seq, left in
 HBM).  `value` = input events/sec of the whole job (all ranks).
 
-N > 1: one process per GPU.  The global stream is arrival ordered; each rank holds a contiguous
-slice of every step (2^24 events); the slice is resharded by key (HIP stable pack by owning rank,
-RCCL all_to_all of the packed rows over xGMI, unpack: siddhi-1_amd/reshard.py) and each
-rank runs its engine on the 2^20 keys it owns (weak scaling: keys and events per GPU fixed).  Every
-timed step pushes one resharded slice and reshards the next one while the engine works on it.
+N > 1: one process per GPU.  The global stream is arrival ordered (16,000 events per ms at N=8); each
+rank holds a contiguous slice of every step (2^24 events); the slice is resharded by key without any
+host synchronisation (HIP stable pack into fixed-size destination blocks, one equal-split RCCL
+all_to_all over xGMI, unpack into a padded batch whose padding the engine drops as null-key events:
+siddhi-1_amd/reshard.py BlockResharder), and each rank runs its engine on the keys it owns
+(weak scaling: keys and events per GPU fixed).  The engine's stream waits for the exchange on the
+device (sg_wait_stream); every timed step pushes one resharded slice and reshards the next one while
+the engine works on it.
 
 The roofline object prices the NFA advance kernel with the algorithmic byte model of DESIGN.md
  over its HIP-event-timed duration.  cpu_baseline times the CPU oracle (the
@@ -168,7 +173,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=1 << 24)
-    ap.add_argument("--keys", type=int, default=1 << 20, help="keys per GPU")
+    ap.add_argument("--keys", type=int, default=None, help="keys per GPU (default: 2^20 at N=1 (C2), 2^23 at N>1 (C5))")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the C3 / C4 lines")
@@ -197,10 +202,16 @@ def main():
     reshard = importlib.import_module("siddhi-1_amd.reshard")
     app = sa.parse_app(synth.C2_QUERY)
     cq = sa.compile_query(app, app.queries[0], sa.StringDictionary())
-    B, K = args.batch, args.keys
-    maxb = B if world == 1 else B + B // 8   # received counts vary around B after the reshard
-    eng = sa.NativeEngine(sa.load_hip_library(), "sg_", cq.ir, n_keys=K, max_batch=maxb, partial_capacity=64,
-                          match_capacity=2 * maxb, device=local, flags=sa.native.SG_CFG_TIMING)
+    B = args.batch
+    K = args.keys or ((1 << 20) if world == 1 else (1 << 23))
+    lib = sa.load_hip_library()
+    rs = None
+    if world > 1:   # fixed-size destination blocks: the padded batch the engine receives per step
+        rs = reshard.BlockResharder(lib, B, world, ["price", "volume"], [torch.float32, torch.int32], dev)
+    maxb = B if world == 1 else world * rs.cap
+    flags = sa.native.SG_CFG_TIMING | (sa.native.SG_CFG_NULL_KEYS if world > 1 else 0)
+    eng = sa.NativeEngine(lib, "sg_", cq.ir, n_keys=K, max_batch=maxb, partial_capacity=64,
+                          match_capacity=2 * maxb, device=local, flags=flags)
 
     # inputs resident in HBM before timing: this rank's slice of every step of the global
     # arrival-ordered stream over world * K keys (events per ms scale with the job)
@@ -216,20 +227,22 @@ def main():
         batches.append(t)
     torch.cuda.synchronize()
     local_seq = [0]
-    lib = sa.load_hip_library()
+    import ctypes as C
+    lib.sg_wait_stream.argtypes = [C.c_void_p, C.c_void_p]
 
     def reshard_step(s):
-        # HIP stable pack by owning rank, RCCL all-to-all of the packed rows, unpack
+        # HIP stable pack into destination blocks, RCCL all-to-all, unpack (no host sync)
         t = batches[s]
-        return reshard.reshard_device(lib, {"key": t["key"], "ts": t["ts"], "price": t["price"],
-                                            "volume": t["volume"]}, world)
+        return rs({"key": t["key"], "ts": t["ts"], "price": t["price"], "volume": t["volume"]})
 
     nxt = [reshard_step(0) if world > 1 else None]
 
     def step(s):
         if world > 1:
             g = nxt[0]
-            torch.cuda.current_stream(dev).synchronize()  # the engine's own stream reads these columns
+            # the engine's stream waits for the exchange on the device (no host synchronisation)
+            if lib.sg_wait_stream(eng.h, C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)) != 0:
+                raise RuntimeError("sg_wait_stream failed")
             n = g["key"].numel()
             cols = (n, g["ts"].data_ptr(), [g["key"].data_ptr(), g["price"].data_ptr(), g["volume"].data_ptr()],
                     g["key"].data_ptr())
@@ -269,6 +282,8 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
     dst = delta(st0, st1)
+    if rs is not None:
+        rs.check()   # a destination block overflow would have dropped events: the run is invalid
     events_all = B * args.steps * world
     value = events_all / el
 
@@ -294,10 +309,12 @@ def main():
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (splitmix64 stock ticks, seeded, HBM-resident)",
-        "config": {"workload": "C2: every e1=StockStream[price>20] -> e2=StockStream[price>e1.price] "
-                               "within 10 sec, partition with (symbol of StockStream)",
+        "config": {"workload": ("C2" if world == 1 else "C5") + ": every e1=StockStream[price>20] -> "
+                               "e2=StockStream[price>e1.price] within 10 sec, partition with (symbol of StockStream), "
+                               f"{K * world} keys",
                    "keys_per_gpu": K, "batch_events_per_gpu": B, "events_per_ms": 2000 * world,
-                   "parallelism": f"key-sharded x{world}" + (" (RCCL all-to-all reshard per step)" if world > 1 else "")},
+                   "parallelism": f"key-sharded x{world}" + (" (RCCL all-to-all reshard per step, fixed blocks of "
+                                                             f"{rs.cap} rows per destination)" if world > 1 else "")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes/launch",
                      "traffic_source": traffic_src,

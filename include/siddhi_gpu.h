@@ -48,6 +48,7 @@ extern "C" {
 #define SG_MEM_DEVICE 1u /* pointers are device (HBM) memory of the engine's device */
 
 #define SG_NULL_SEQ UINT64_MAX
+#define SG_KEY_NULL 0xFFFFFFFFu /* partition key id of an event without a key (null key: dropped) */
 /* slot event created by an absent state when it fires (StreamEventFactory.newInstance():
  * no attributes, ts -1; AbsentLogicalPreStateProcessor.java:153-166) */
 #define SG_BLANK_SEQ (UINT64_MAX - 1)
@@ -58,6 +59,10 @@ extern "C" {
 /* engine configuration flags */
 #define SG_CFG_NO_ORDER 1u /* deliver matches per-key ordered only (skip the global trigger-seq order) */
 #define SG_CFG_TIMING 2u   /* record HIP events around every kernel stage (sg_stats *_ns fields) */
+/* batches may carry key == SG_KEY_NULL: such events are dropped, as PartitionStreamReceiver drops events
+ * whose partition key is null (PartitionStreamReceiver.java:175-205).  Used for fixed-size device batches
+ * with padding (the multi-GPU reshard).  Without the flag a SG_KEY_NULL key is out of range. */
+#define SG_CFG_NULL_KEYS 4u
 
 typedef struct sg_engine sg_engine;
 
@@ -136,6 +141,10 @@ int sg_poll_matches(sg_engine* e, uint32_t mem, sg_match_batch* out);
 int sg_release_matches(sg_engine* e, sg_match_batch* m);
 int sg_get_stats(sg_engine* e, sg_stats* out);
 int sg_synchronize(sg_engine* e);
+/* Device batches produced on another stream (a hipStream_t of the engine's device, NULL = the legacy
+ * default stream): the engine's later work waits for everything queued on `stream` so far, without a
+ * host synchronisation (the multi-GPU reshard hands its output over this way). */
+int sg_wait_stream(sg_engine* e, void* stream);
 /* Partition purge (@purge(enable, interval, idle.period) on a partition; PartitionRuntimeImpl.java:368-401
  * removes idle keys and cleanGroupByStates() every state holder of the partition's queries, so the
  * key's next event runs initPartition again).  The host tracks last-seen times and picks the idle
@@ -166,6 +175,14 @@ int sg_shard_pack(uint64_t n, const uint32_t* key, const int64_t* ts, const uint
                   uint32_t world, uint32_t* rows, unsigned long long* dest_counts, void* scratch, size_t scratch_len,
                   void* stream);
 size_t sg_shard_scratch_bytes(uint64_t n, uint32_t world);
+/* The same pack into fixed-size destination blocks, so that the exchange needs no host-side counts (one
+ * equal-split all_to_all, no device->host sync per step): destination d's rows go to
+ * rows[d * cap, d * cap + count_d), the rest of its block is padding rows whose local key is SG_KEY_NULL
+ * (an engine created with SG_CFG_NULL_KEYS drops them).  A destination with more than cap rows sets
+ * *overflow (device u32) and its extra rows are not written: the caller must fail the step. */
+int sg_shard_pack_blocks(uint64_t n, const uint32_t* key, const int64_t* ts, const uint32_t* const* cols,
+                         uint32_t n_cols, uint32_t world, uint32_t cap, uint32_t* rows, unsigned long long* dest_counts,
+                         uint32_t* overflow, void* scratch, size_t scratch_len, void* stream);
 int sg_shard_unpack(uint64_t n, const uint32_t* rows, uint32_t n_cols, uint32_t* key, int64_t* ts,
                     uint32_t* const* cols_dev, void* stream);
 
@@ -181,7 +198,6 @@ int sg_shard_unpack(uint64_t n, const uint32_t* rows, uint32_t n_cols, uint32_t*
  * sg_dict_intern assigns ids to new strings; it is all-or-nothing: when the batch would take the
  * dictionary past max_ids it fails with SG_ERR_CAPACITY and assigns nothing.  n_new (optional)
  * receives how many strings were new.  sg_dict_lookup never inserts (absent: SG_KEY_NULL). */
-#define SG_KEY_NULL 0xFFFFFFFFu
 typedef struct sg_dict sg_dict;
 int sg_dict_create(uint32_t max_ids, uint64_t capacity_hint, sg_dict** out);
 int sg_dict_intern(sg_dict* d, const uint8_t* bytes, const uint64_t* offsets, const uint8_t* valid, uint64_t n,

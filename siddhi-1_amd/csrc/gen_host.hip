@@ -353,12 +353,15 @@ GenProgram* gen_build_program(const uint32_t* w, size_t nw, uint32_t partialCap)
 // ---------------------------------------------------------------------------------------------
 // device-side helpers of the engine
 // ---------------------------------------------------------------------------------------------
-__global__ void k_gen_bounds(const uint32_t* __restrict__ skeys, uint32_t n, uint32_t K, uint32_t* seg_begin,
-                             uint32_t* seg_end, uint32_t* err) {
+__global__ void k_gen_bounds(const uint32_t* __restrict__ skeys, uint32_t n, uint32_t K, bool drop_null,
+                             uint32_t* seg_begin, uint32_t* seg_end, uint32_t* err) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint32_t k = skeys[i];
-    if (k >= K) { atomicOr(err, (uint32_t)GERR_KEY); return; }
+    if (k >= K) {  // SG_CFG_NULL_KEYS: SG_KEY_NULL events are dropped (null partition key)
+        if (!(drop_null && k == SG_KEY_NULL)) atomicOr(err, (uint32_t)GERR_KEY);
+        return;
+    }
     if (i == 0 || skeys[i - 1] != k) seg_begin[k] = i;
     if (i == n - 1 || skeys[i + 1] != k) seg_end[k] = i + 1;
 }
@@ -480,6 +483,7 @@ struct GenEngine {
     GenProgram* dprog = nullptr;
     hipStream_t stream = nullptr;
     uint32_t K = 1, maxb = 0;
+    bool null_keys = false;  // SG_CFG_NULL_KEYS
     uint64_t mcap = 0, rawCap = 0;
     uint32_t recWords = 0;
     std::vector<void*> owned;
@@ -572,6 +576,7 @@ GenEngine* gen_create(const uint32_t* ir, size_t nw, const sg_config& cfg, hipSt
         delete prog;
         e->stream = stream;
         e->K = e->host.partitioned ? (cfg.n_keys ? cfg.n_keys : 1) : 1;
+        e->null_keys = (cfg.flags & SG_CFG_NULL_KEYS) != 0;
         e->maxb = cfg.max_batch ? cfg.max_batch : (1u << 20);
         e->mcap = cfg.match_capacity ? cfg.match_capacity : (uint64_t)e->maxb * 4;
         const GenProgram& G = e->host;
@@ -696,9 +701,12 @@ static void launch_gen(GenEngine* e, const GenArgs& a, int which) {
 }
 
 // largest key id of a host batch (branch-free, so it vectorises; range-checked after the H2D is queued)
-static uint32_t sgd_max_key(const uint32_t* k, uint32_t n) {
+static uint32_t sgd_max_key(const uint32_t* k, uint32_t n, bool skip_null) {
     uint32_t m = 0;
-    for (uint32_t i = 0; i < n; i++) m = k[i] > m ? k[i] : m;
+    if (skip_null)
+        for (uint32_t i = 0; i < n; i++) m = (k[i] > m && k[i] != SG_KEY_NULL) ? k[i] : m;
+    else
+        for (uint32_t i = 0; i < n; i++) m = k[i] > m ? k[i] : m;
     return m;
 }
 
@@ -744,18 +752,18 @@ int gen_push(GenEngine* e, const sg_batch* b, std::string& msg) {
             // the copy is queued first, so the host range check overlaps the DMA (pinned batches)
             GH_OK(hipMemcpyAsync(e->b_key, b->key, (size_t)n * 4, hipMemcpyHostToDevice, e->stream));
             keys = e->b_key;
-            if (sgd_max_key(b->key, n) >= e->K) {
+            if (sgd_max_key(b->key, n, e->null_keys) >= e->K) {
                 GH_OK(hipStreamSynchronize(e->stream));  // the queued copies read the caller's buffers
                 msg = "key id outside [0, n_keys)";
                 return SG_ERR_INVALID;
             }
         }
-        uint32_t bits = 1;
-        while (bits < 32 && (1ull << bits) < e->K) bits++;
+        uint32_t bits = 1;  // SG_CFG_NULL_KEYS: one value more than the key range (SG_KEY_NULL sorts last)
+        while (bits < 32 && (1ull << bits) < (uint64_t)e->K + (e->null_keys ? 1u : 0u)) bits++;
         size_t tmp = e->sort_tmp_bytes;
         GH_OK(rocprim::radix_sort_pairs(e->sort_tmp, tmp, keys, e->skeys, e->iota, e->sidx, n, 0, bits, e->stream));
         hipLaunchKernelGGL(k_gen_bounds, dim3((n + 255) / 256), dim3(256), 0, e->stream, e->skeys, n, e->K,
-                           e->seg_begin, e->seg_end, e->err);
+                           e->null_keys, e->seg_begin, e->seg_end, e->err);
         a.b.sidx = e->sidx;
     } else {
         GH_OK(hipMemcpyAsync(e->seg_end, &n, 4, hipMemcpyHostToDevice, e->stream));

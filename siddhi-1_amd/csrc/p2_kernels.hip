@@ -14,10 +14,11 @@
 // segment bounds of the key-sorted batch: seg_begin[k], seg_end[k]
 // ------------------------------------------------------------------------------------------------
 __device__ __forceinline__ void seg_bound_one(uint32_t i, uint32_t k, uint32_t prev, uint32_t next, uint32_t n,
-                                              uint32_t n_keys, uint32_t* __restrict__ seg_begin,
+                                              uint32_t n_keys, bool drop_null, uint32_t* __restrict__ seg_begin,
                                               uint32_t* __restrict__ seg_end, uint32_t* __restrict__ err) {
     if (k >= n_keys) {  // key id outside [0, n_keys): reject the batch loudly, never write out of bounds
-        atomicOr(err, (uint32_t)SGD_ERR_KEY_RANGE);
+        // (SG_CFG_NULL_KEYS: an SG_KEY_NULL event is dropped, as the reference drops null-key events)
+        if (!(drop_null && k == 0xffffffffu)) atomicOr(err, (uint32_t)SGD_ERR_KEY_RANGE);
         // such ids sort after every valid one: the first of them closes the bounds of the keys above
         // the last valid run (no key keeps a stale segment of an earlier batch)
         if (prev != k && (i == 0 || prev < n_keys))
@@ -38,7 +39,7 @@ __device__ __forceinline__ void seg_bound_one(uint32_t i, uint32_t k, uint32_t p
 
 // four sorted keys per thread (one 16-B load + the neighbours on either side)
 __global__ void __launch_bounds__(256) k_seg_bounds(const uint32_t* __restrict__ skeys, uint32_t n,
-                                                    uint32_t n_keys, uint32_t* __restrict__ seg_begin,
+                                                    uint32_t n_keys, bool drop_null, uint32_t* __restrict__ seg_begin,
                                                     uint32_t* __restrict__ seg_end, uint32_t* __restrict__ err) {
     // every key gets its bounds written (keys without events get an empty [i, i) at the right spot),
     // so no memset of the bound arrays is needed per batch
@@ -58,7 +59,7 @@ __global__ void __launch_bounds__(256) k_seg_bounds(const uint32_t* __restrict__
         const uint32_t i = i0 + q;
         if (i >= n) break;
         const uint32_t next = (i == n - 1) ? n_keys : k[q + 2];
-        seg_bound_one(i, k[q + 1], (i == 0) ? 0xffffffffu : k[q], next, n, n_keys, seg_begin, seg_end, err);
+        seg_bound_one(i, k[q + 1], (i == 0) ? 0xffffffffu : k[q], next, n, n_keys, drop_null, seg_begin, seg_end, err);
     }
 }
 
@@ -228,11 +229,11 @@ __global__ void __launch_bounds__(1024) k_stats_reduce(const unsigned long long*
 // ------------------------------------------------------------------------------------------------
 // launch wrappers
 // ------------------------------------------------------------------------------------------------
-int sgd_launch_bounds(const uint32_t* skeys, uint32_t n, uint32_t n_keys, uint32_t* seg_begin, uint32_t* seg_end,
-                      uint32_t* err, ihipStream_t* stream) {
+int sgd_launch_bounds(const uint32_t* skeys, uint32_t n, uint32_t n_keys, bool drop_null, uint32_t* seg_begin,
+                      uint32_t* seg_end, uint32_t* err, ihipStream_t* stream) {
     if (n == 0) return 0;
-    hipLaunchKernelGGL(k_seg_bounds, dim3((n + 1023) / 1024), dim3(256), 0, stream, skeys, n, n_keys, seg_begin,
-                       seg_end, err);
+    hipLaunchKernelGGL(k_seg_bounds, dim3((n + 1023) / 1024), dim3(256), 0, stream, skeys, n, n_keys, drop_null,
+                       seg_begin, seg_end, err);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

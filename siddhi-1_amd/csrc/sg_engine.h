@@ -111,7 +111,7 @@ struct PackParams {
 
 // ahead-of-time launch wrappers (p2_kernels.hip)
 struct ihipStream_t;
-int sgd_launch_bounds(const uint32_t* sorted_keys, uint32_t n, uint32_t n_keys, uint32_t* seg_begin,
+int sgd_launch_bounds(const uint32_t* sorted_keys, uint32_t n, uint32_t n_keys, bool drop_null, uint32_t* seg_begin,
                       uint32_t* seg_end, uint32_t* err, ihipStream_t* stream);
 // ordered output of one batch: o_*[out_count + t_off[t] + r] for the r-th match of batch event t
 struct ScatterParams {

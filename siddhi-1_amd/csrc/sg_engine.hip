@@ -183,6 +183,8 @@ struct sg_engine {
     std::vector<IRStream> streams;
     Plan plan;
     uint32_t K = 1, cap = 64, maxb = 0;
+    uint32_t sort_bits = 1;   // key bits the grouping sorts on (SG_CFG_NULL_KEYS: SG_KEY_NULL sorts last)
+    bool null_keys = false;
     uint64_t mcap = 0;
     uint64_t raw_cap = 0;  // mcap + one reservation chunk of slack per advance-kernel wave
     std::vector<void*> owned;
@@ -646,10 +648,14 @@ uint32_t stage_chunks_for(uint64_t n, uint64_t K, uint32_t stride_words) {
     return (uint32_t)std::max(64.0, std::min(chunks, hi));
 }
 
-// largest key id of a host batch (branch-free, so it vectorises; range-checked after the H2D is queued)
-static uint32_t sgd_max_key(const uint32_t* k, uint32_t n) {
+// largest key id of a host batch (branch-free, so it vectorises; range-checked after the H2D is queued);
+// with SG_CFG_NULL_KEYS the dropped SG_KEY_NULL ids do not count
+static uint32_t sgd_max_key(const uint32_t* k, uint32_t n, bool skip_null) {
     uint32_t m = 0;
-    for (uint32_t i = 0; i < n; i++) m = k[i] > m ? k[i] : m;
+    if (skip_null)
+        for (uint32_t i = 0; i < n; i++) m = (k[i] > m && k[i] != SG_KEY_NULL) ? k[i] : m;
+    else
+        for (uint32_t i = 0; i < n; i++) m = k[i] > m ? k[i] : m;
     return m;
 }
 
@@ -719,7 +725,7 @@ int push(sg_engine* e, const sg_batch* b) {
         // staging buffers it fills are not engine state
         HIP_OK(hipMemcpyAsync(e->b_key, b->key, (size_t)n * 4, kind, e->stream));
         keys = e->b_key;
-        if (sgd_max_key(b->key, n) >= e->K) {
+        if (sgd_max_key(b->key, n, e->null_keys) >= e->K) {
             HIP_OK(hipStreamSynchronize(e->stream));  // the queued copies read the caller's buffers
             return fail(SG_ERR_INVALID, "key id outside [0, n_keys)");
         }
@@ -755,15 +761,15 @@ int push(sg_engine* e, const sg_batch* b) {
                 ps.kind[wi++] = 4;
             }
             if (wi == 0) ps.kind[wi++] = 5;
-            HIP_OK(sort_payload_w((int)wi, e->sort_tmp, tmp, keys, e->skeys, ps, e->pay, n, bits_for(e->K),
+            HIP_OK(sort_payload_w((int)wi, e->sort_tmp, tmp, keys, e->skeys, ps, e->pay, n, e->sort_bits,
                                   e->stream));
         } else {
             HIP_OK(rocprim::radix_sort_pairs(e->sort_tmp, tmp, keys, e->skeys, e->iota, e->sidx, n, 0,
-                                             bits_for(e->K), e->stream));
+                                             e->sort_bits, e->stream));
             pk.sidx = e->sidx;
             launch(v.pack[role], pack_blocks, 256, &pk, e->stream);
         }
-        if (sgd_launch_bounds(e->skeys, n, e->K, e->seg_begin, e->seg_end, e->err, e->stream) != 0)
+        if (sgd_launch_bounds(e->skeys, n, e->K, e->null_keys, e->seg_begin, e->seg_end, e->err, e->stream) != 0)
             throw HipError("k_seg_bounds launch failed");
     } else {
         pk.sidx = nullptr;  // one key: arrival order
@@ -928,6 +934,7 @@ int sg_engine_create(const void* ir, size_t ir_len, const sg_config* cfg, sg_eng
         if (e->stage_override * 16ull * (SGD_BLOCK / SGD_WAVE) > SGD_STAGE_MAX_BYTES)
             throw std::invalid_argument("SGD_STAGE_CHUNKS above the LDS staging bound");
         e->K = cfg->n_keys ? cfg->n_keys : 1;
+        e->null_keys = (cfg->flags & SG_CFG_NULL_KEYS) != 0;
         e->cap = cfg->partial_capacity ? cfg->partial_capacity : 64;
         e->maxb = cfg->max_batch ? cfg->max_batch : (1u << 20);
         e->mcap = cfg->match_capacity ? cfg->match_capacity : (uint64_t)e->maxb * 4;
@@ -962,6 +969,9 @@ int sg_engine_create(const void* ir, size_t ir_len, const sg_config* cfg, sg_eng
         e->jq = make_jit_query(e);
         (void)sgj_generate(e->jq, e->consts);  // validates the filters, fixes the constant table
         if (!e->plan.partitioned && e->K != 1) e->K = 1;
+        // the sort looks at the low sort_bits bits only: with SG_CFG_NULL_KEYS one more value than the
+        // key range, so that SG_KEY_NULL (all ones) sorts after every valid key
+        e->sort_bits = bits_for((uint64_t)e->K + (e->null_keys ? 1u : 0u));
         int ndev = 0;
         HIP_OK(hipGetDeviceCount(&ndev));
         if (cfg->device < 0 || cfg->device >= ndev) throw HipError("no such HIP device");
@@ -1008,6 +1018,20 @@ int sg_advance_time(sg_engine* e, int64_t now_ms) {
         std::string msg;
         const int rc = gen_advance(e->gen, now_ms, msg);
         return rc == SG_OK ? rc : fail(rc, msg);
+    } catch (const std::exception& ex) {
+        return fail(SG_ERR_DEVICE, ex.what());
+    }
+}
+
+int sg_wait_stream(sg_engine* e, void* stream) {
+    if (!e) return fail(SG_ERR_INVALID, "null argument");
+    try {
+        HIP_OK(hipSetDevice(e->device));
+        hipEvent_t x = e->ev();
+        HIP_OK(hipEventRecord(x, (hipStream_t)stream));
+        HIP_OK(hipStreamWaitEvent(e->stream, x, 0));
+        e->free_events.push_back(x);  // reusable once recorded again (a wait captures the recorded work)
+        return SG_OK;
     } catch (const std::exception& ex) {
         return fail(SG_ERR_DEVICE, ex.what());
     }

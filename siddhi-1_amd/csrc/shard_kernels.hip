@@ -42,7 +42,9 @@ struct ShardArgs {
     uint32_t world;
     uint32_t ntiles;
     uint32_t* counts;      // [world][ntiles] (count pass) -> exclusive offsets (after the scan)
-    uint32_t* rows;        // [n][3 + ncols]
+    uint32_t* rows;        // [n][3 + ncols], or [world][cap][3 + ncols] in block mode
+    uint32_t cap;          // block mode (> 0): destination d's rows at [d * cap, d * cap + count_d)
+    uint32_t* overflow;    // block mode: set when a destination receives more than cap rows
 };
 
 __global__ void __launch_bounds__(SH_WAVES * 64) k_sh_count(const ShardArgs a) {
@@ -95,6 +97,14 @@ __global__ void __launch_bounds__(SH_WAVES * 64) k_sh_scatter(const ShardArgs a)
             if (d == dd) pos = bdd + (uint32_t)__popcll(m & lt);
             if (lane == dd) base += (uint32_t)__popcll(m);
         }
+        if (in && a.cap) {  // block mode: the rank of the row within its destination, in d's block
+            const uint32_t r0 = pos - a.counts[(size_t)d * a.ntiles];
+            if (r0 >= a.cap) {
+                atomicOr(a.overflow, 1u);
+                continue;
+            }
+            pos = d * a.cap + r0;
+        }
         if (in) {
             uint32_t* row = a.rows + (size_t)pos * W;
             row[0] = k / a.world;
@@ -104,6 +114,19 @@ __global__ void __launch_bounds__(SH_WAVES * 64) k_sh_scatter(const ShardArgs a)
             for (uint32_t c = 0; c < a.ncols; ++c) row[3 + c] = a.col[c][e];
         }
     }
+}
+
+// block mode: the rows past each destination's count are padding (local key SG_KEY_NULL, dropped by an
+// engine created with SG_CFG_NULL_KEYS; ts and columns zero)
+__global__ void __launch_bounds__(256) k_sh_pad(uint32_t* __restrict__ rows, const unsigned long long* __restrict__ totals,
+                                                uint32_t world, uint32_t cap, uint32_t W) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (uint64_t)world * cap) return;
+    const uint32_t d = (uint32_t)(i / cap), r = (uint32_t)(i % cap);
+    if (r < totals[d]) return;
+    uint32_t* row = rows + i * W;
+    row[0] = SG_KEY_NULL;
+    for (uint32_t c = 1; c < W; ++c) row[c] = 0u;
 }
 
 __global__ void __launch_bounds__(256) k_sh_unpack(uint64_t n, const uint32_t* __restrict__ rows, uint32_t ncols,
@@ -133,9 +156,9 @@ __global__ void k_sh_totals(const uint32_t* off, const uint32_t* last_counts, ui
 
 extern "C" {
 
-int sg_shard_pack(uint64_t n, const uint32_t* key, const int64_t* ts, const uint32_t* const* cols, uint32_t n_cols,
-                  uint32_t world, uint32_t* rows, unsigned long long* dest_counts, void* scratch, size_t scratch_len,
-                  void* stream) {
+static int shard_pack(uint64_t n, const uint32_t* key, const int64_t* ts, const uint32_t* const* cols, uint32_t n_cols,
+                      uint32_t world, uint32_t cap, uint32_t* rows, unsigned long long* dest_counts, uint32_t* overflow,
+                      void* scratch, size_t scratch_len, void* stream) {
     if (world == 0 || world > SH_MAX_WORLD || n_cols > SH_MAX_COLS || n >= (1ull << 32)) return SG_ERR_INVALID;
     const hipStream_t s = (hipStream_t)stream;
     ShardArgs a{};
@@ -145,6 +168,8 @@ int sg_shard_pack(uint64_t n, const uint32_t* key, const int64_t* ts, const uint
     for (uint32_t c = 0; c < n_cols; ++c) a.col[c] = cols[c];
     a.ncols = n_cols;
     a.world = world;
+    a.cap = cap;
+    a.overflow = overflow;
     a.ntiles = (uint32_t)((n + SH_TILE - 1) / SH_TILE);
     const size_t ncnt = (size_t)world * a.ntiles;
     size_t tmp = 0;
@@ -156,7 +181,14 @@ int sg_shard_pack(uint64_t n, const uint32_t* key, const int64_t* ts, const uint
     uint32_t* cnt = (uint32_t*)scratch;
     uint32_t* off = cnt + ncnt;
     void* stmp = (void*)(((uintptr_t)(off + ncnt) + 255) & ~(uintptr_t)255);
-    if (n == 0) return hipMemsetAsync(dest_counts, 0, world * 8, s) == hipSuccess ? SG_OK : SG_ERR_DEVICE;
+    if (cap && hipMemsetAsync(overflow, 0, 4, s) != hipSuccess) return SG_ERR_DEVICE;
+    if (n == 0) {
+        if (hipMemsetAsync(dest_counts, 0, world * 8, s) != hipSuccess) return SG_ERR_DEVICE;
+        if (cap)
+            hipLaunchKernelGGL(k_sh_pad, dim3((unsigned)(((uint64_t)world * cap + 255) / 256)), dim3(256), 0, s, rows,
+                               dest_counts, world, cap, 3 + n_cols);
+        return hipGetLastError() == hipSuccess ? SG_OK : SG_ERR_DEVICE;
+    }
     a.counts = cnt;
     hipLaunchKernelGGL(k_sh_count, dim3(a.ntiles), dim3(SH_WAVES * 64), 0, s, a);
     if (rocprim::exclusive_scan(stmp, tmp, cnt, off, 0u, ncnt, rocprim::plus<uint32_t>(), s) != hipSuccess)
@@ -165,7 +197,23 @@ int sg_shard_pack(uint64_t n, const uint32_t* key, const int64_t* ts, const uint
     a.rows = rows;
     hipLaunchKernelGGL(k_sh_scatter, dim3(a.ntiles), dim3(SH_WAVES * 64), 0, s, a);
     hipLaunchKernelGGL(k_sh_totals, dim3(1), dim3(64), 0, s, off, cnt, world, a.ntiles, n, dest_counts);
+    if (cap)
+        hipLaunchKernelGGL(k_sh_pad, dim3((unsigned)(((uint64_t)world * cap + 255) / 256)), dim3(256), 0, s, rows,
+                           dest_counts, world, cap, 3 + n_cols);
     return hipGetLastError() == hipSuccess ? SG_OK : SG_ERR_DEVICE;
+}
+
+int sg_shard_pack(uint64_t n, const uint32_t* key, const int64_t* ts, const uint32_t* const* cols, uint32_t n_cols,
+                  uint32_t world, uint32_t* rows, unsigned long long* dest_counts, void* scratch, size_t scratch_len,
+                  void* stream) {
+    return shard_pack(n, key, ts, cols, n_cols, world, 0, rows, dest_counts, nullptr, scratch, scratch_len, stream);
+}
+
+int sg_shard_pack_blocks(uint64_t n, const uint32_t* key, const int64_t* ts, const uint32_t* const* cols,
+                         uint32_t n_cols, uint32_t world, uint32_t cap, uint32_t* rows, unsigned long long* dest_counts,
+                         uint32_t* overflow, void* scratch, size_t scratch_len, void* stream) {
+    if (cap == 0 || !overflow) return SG_ERR_INVALID;
+    return shard_pack(n, key, ts, cols, n_cols, world, cap, rows, dest_counts, overflow, scratch, scratch_len, stream);
 }
 
 size_t sg_shard_scratch_bytes(uint64_t n, uint32_t world) {

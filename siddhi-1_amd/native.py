@@ -18,6 +18,7 @@ SG_MEM_DEVICE = 1
 SG_NULL_SEQ = np.uint64(0xFFFFFFFFFFFFFFFF)
 SG_CFG_NO_ORDER = 1
 SG_CFG_TIMING = 2
+SG_CFG_NULL_KEYS = 4
 
 ERRORS = {-1: "SG_ERR_INVALID", -2: "SG_ERR_UNSUPPORTED", -3: "SG_ERR_DEVICE",
           -4: "SG_ERR_CAPACITY", -5: "SG_ERR_STATE"}

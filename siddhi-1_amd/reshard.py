@@ -127,6 +127,94 @@ def reshard_device(lib, cols: Dict[str, torch.Tensor], world: int, group=None,
     return out
 
 
+def block_capacity(n: int, world: int) -> int:
+    """Rows per destination block of `reshard_device_blocks` for a slice of n uniformly keyed events: the
+    mean n / world plus 8 standard deviations of its binomial count (overflow is detected, never silent)."""
+    m = n / world
+    return int(m + 8.0 * (m * (1.0 - 1.0 / world)) ** 0.5 + 256)
+
+
+class BlockResharder:
+    """`reshard_device` without any device->host synchronisation, for the per-step exchange of a
+    multi-GPU run: the pack fills fixed-size destination blocks of `cap` rows (``sg_shard_pack_blocks``;
+    the unused rows of a block are padding whose local key is SG_KEY_NULL), one equal-split all_to_all
+    moves them, and the received world * cap rows unpack into a padded batch in global arrival order.
+    The engine (created with SG_CFG_NULL_KEYS) drops the padding as the reference drops null-key events.
+    Buffers are allocated once (`slots` output sets, reused round-robin: the engine reads set s while
+    the next step is resharded into set s + 1).  A destination with more than cap rows raises the
+    device flag `overflow`; `check()` reads it once (the run is then invalid)."""
+
+    def __init__(self, lib, n: int, world: int, names, dtypes, device, cap=None, slots=2, group=None):
+        import ctypes as C
+        self.C, self.lib, self.n, self.world, self.group = C, lib, n, world, group
+        self.cap = cap or block_capacity(n, world)
+        self.names = list(names)
+        self.W = 3 + len(self.names)
+        self.dev = device
+        m = world * self.cap
+        lib.sg_shard_scratch_bytes.restype = C.c_size_t
+        lib.sg_shard_scratch_bytes.argtypes = [C.c_uint64, C.c_uint32]
+        self.scratch = torch.empty(int(lib.sg_shard_scratch_bytes(n, world)), dtype=torch.uint8, device=device)
+        self.send = torch.empty((m, self.W), dtype=torch.int32, device=device)
+        self.recv = torch.empty_like(self.send)
+        self.counts = torch.empty(world, dtype=torch.int64, device=device)
+        self.flag = torch.zeros(1, dtype=torch.int32, device=device)
+        self.overflow = torch.zeros(1, dtype=torch.int32, device=device)
+        self.host = world > 1 and dist.get_backend(group) == "gloo"  # one-GPU rehearsal through host memory
+        self.sets, self.ptrs = [], []
+        for _ in range(slots):
+            o = {"key": torch.empty(m, dtype=torch.int32, device=device),
+                 "ts": torch.empty(m, dtype=torch.int64, device=device)}
+            for nm, dt in zip(self.names, dtypes):
+                o[nm] = torch.empty(m, dtype=dt, device=device)
+            self.sets.append(o)
+            self.ptrs.append(torch.tensor([o[nm].data_ptr() for nm in self.names] or [0], dtype=torch.int64,
+                                          device=device))
+        self.next = 0
+        f = lib.sg_shard_pack_blocks
+        f.argtypes = [C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p,
+                      C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]
+        g = lib.sg_shard_unpack
+        g.argtypes = [C.c_uint64, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+
+    def __call__(self, cols: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+        """this rank's slice ("key": global key id, "ts", the attribute columns) -> the padded batch of the
+        keys this rank owns (local key ids), queued on the current stream"""
+        C = self.C
+        key, ts = cols["key"], cols["ts"]
+        attrs = [cols[nm] for nm in self.names]
+        stream = C.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)
+        colp = (C.c_void_p * max(1, len(attrs)))(*[a.data_ptr() for a in attrs])
+        rc = self.lib.sg_shard_pack_blocks(key.numel(), key.data_ptr(), ts.data_ptr(), colp, len(attrs), self.world,
+                                           self.cap, self.send.data_ptr(), self.counts.data_ptr(), self.flag.data_ptr(),
+                                           self.scratch.data_ptr(), self.scratch.numel(), stream)
+        if rc != 0:
+            raise RuntimeError(f"sg_shard_pack_blocks failed ({rc})")
+        self.overflow.bitwise_or_(self.flag)
+        rows = self.send
+        if self.world > 1:
+            if self.host:
+                got = torch.empty(self.send.numel(), dtype=torch.int32)
+                dist.all_to_all_single(got, self.send.view(-1).cpu(), group=self.group)
+                self.recv.view(-1).copy_(got)
+            else:
+                dist.all_to_all_single(self.recv.view(-1), self.send.view(-1), group=self.group)
+            rows = self.recv
+        o, p = self.sets[self.next], self.ptrs[self.next]
+        self.next = (self.next + 1) % len(self.sets)
+        m = self.world * self.cap
+        rc = self.lib.sg_shard_unpack(m, rows.data_ptr(), len(attrs), o["key"].data_ptr(), o["ts"].data_ptr(),
+                                      p.data_ptr(), stream)
+        if rc != 0:
+            raise RuntimeError(f"sg_shard_unpack failed ({rc})")
+        return o
+
+    def check(self):
+        if int(self.overflow.item()):
+            raise RuntimeError(f"a destination block overflowed its {self.cap} rows: the key distribution is "
+                               f"too skewed for this block size")
+
+
 def merge_by_trigger(parts: List[Tuple[torch.Tensor, ...]]) -> torch.Tensor:
     """Host-side k-way merge order of per-rank match streams (each sorted by global trigger seq):
     returns the permutation of the concatenation that orders it by (trigger seq, rank, position) —

@@ -888,13 +888,21 @@ class SiddhiManager:
     """io.siddhi.core.SiddhiManager (pattern path only)."""
 
     def __init__(self, engine_factory: Optional[Callable] = None, n_keys=1 << 16, device=0,
-                 partial_capacity=64, max_batch=1 << 16):
+                 partial_capacity=64, max_batch=1 << 16, devices=None):
+        """devices: several HIP devices -> every partitioned query runs on a ShardedEngine over them
+        (partition keys sharded across the GPUs, matches merged back in the single engine's order)."""
         if engine_factory is None:
             lib = load_hip_library()          # raises if the HIP engine is not built
+            if devices is not None and len(devices) > 1:
+                from .sharded import ShardedEngine
 
-            def engine_factory(ir, nk):
-                return NativeEngine(lib, "sg_", ir, n_keys=nk, max_batch=max_batch,
-                                    partial_capacity=partial_capacity, device=device)
+                def engine_factory(ir, nk):
+                    return ShardedEngine(lib, "sg_", ir, n_keys=nk, devices=tuple(devices), max_batch=max_batch,
+                                         partial_capacity=partial_capacity)
+            else:
+                def engine_factory(ir, nk):
+                    return NativeEngine(lib, "sg_", ir, n_keys=nk, max_batch=max_batch,
+                                        partial_capacity=partial_capacity, device=device)
         self.engine_factory = engine_factory
         self.n_keys = n_keys
         self.persistence_store = None
