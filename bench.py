@@ -65,12 +65,31 @@ def delta(a, b):
     return {k: b[k] - a[k] for k in a}
 
 
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(sa, synth, n_keys, batch, seconds):
-    """Single-thread CPU oracle on the first events of the same C2 stream (bounded by `seconds`)."""
+    """SURVEY §8(d) CPU legs, the CPU oracle (the C++ restatement of the reference engine; the reference
+    JVM is not runnable here or on the box) on the host cores of the GPU box:
+      (i)  faithful single thread on the first events of the same C2 stream (the reference serialises a
+           pattern query on one lock, so one core is its own parallelism for this query) -> `value`;
+      (ii) partition-parallel: T threads, keys sharded key % T, one oracle engine per thread over the
+           same prefix of the stream (an upper bound for any CPU engine; T = the box's CPU share);
+      (iii) C1 (BASELINE configs[0]): the unpartitioned query, one key, 1 event per ms, single thread.
+    Each leg is bounded to about `seconds` of CPU work."""
+    import threading
     from oracle_backend import build_oracle
+    lib = build_oracle()
     app = sa.parse_app(synth.C2_QUERY)
     cq = sa.compile_query(app, app.queries[0], sa.StringDictionary())
-    eng = sa.NativeEngine(build_oracle(), "sgo_", cq.ir, n_keys=n_keys)
+    eng = sa.NativeEngine(lib, "sgo_", cq.ir, n_keys=n_keys)
     chunk = 1 << 19
     done, busy = 0, 0.0
     while busy < seconds and done < batch * 4:
@@ -81,10 +100,60 @@ def cpu_baseline(sa, synth, n_keys, batch, seconds):
         busy += time.perf_counter() - t
         done += chunk
     eng.close()
-    return {"value": done / busy, "unit": "events/s", "cores": 1, "kind": "port",
-            "sample": f"first {done} events of the C2 stream ({n_keys} keys), CPU oracle "
-                      f"(faithful single-thread restatement of the reference engine; reference JVM "
-                      f"unavailable on the box)"}
+    single = done / busy
+    # (ii) partition-parallel over the box's CPU share (at most 16 threads on a one-GPU box)
+    T = max(1, min(16, os.cpu_count() or 1))
+    total = int(min(batch * 4, single * seconds * T * 0.7)) // (T * chunk) * (T * chunk) or T * chunk
+    d = synth.stock_ticks(0, total, n_keys)
+    own = d["key"] % np.uint32(T)
+    shards = []
+    for r in range(T):
+        idx = np.nonzero(own == r)[0]
+        shards.append({"ts": d["ts"][idx], "key": (d["key"][idx] // np.uint32(T)).astype(np.uint32),
+                       "cols": [d["symbol"][idx], d["price"][idx], d["volume"][idx]], "seq": idx.astype(np.uint64)})
+    del d
+    engs = [sa.NativeEngine(lib, "sgo_", cq.ir, n_keys=(n_keys + T - 1) // T) for _ in range(T)]
+
+    def work(r):
+        s, e = shards[r], engs[r]
+        n = len(s["ts"])
+        for a in range(0, n, chunk):   # local arrival seqs (the per-key order is the global one)
+            sl = slice(a, min(n, a + chunk))
+            e.push(0, a, s["ts"][sl], [c[sl] for c in s["cols"]], None, s["key"][sl])
+            e.poll()
+
+    th = [threading.Thread(target=work, args=(r,)) for r in range(T)]
+    t0 = time.perf_counter()
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    par = total / (time.perf_counter() - t0)
+    for e in engs:
+        e.close()
+    # (iii) C1: unpartitioned, one key, R = 1 event per ms (10,000 events per 10 s window)
+    app1 = sa.parse_app(synth.C1_QUERY)
+    cq1 = sa.compile_query(app1, app1.queries[0], sa.StringDictionary())
+    e1 = sa.NativeEngine(lib, "sgo_", cq1.ir, n_keys=1)
+    c1_done, c1_busy, c1_chunk = 0, 0.0, 1 << 16
+    while c1_busy < seconds / 2 and c1_done < 10_000_000:
+        d = synth.stock_ticks(c1_done, c1_chunk, 1, rate_per_ms=1)
+        t = time.perf_counter()
+        e1.push(0, c1_done, d["ts"], [d["symbol"], d["price"], d["volume"]])
+        e1.poll()
+        c1_busy += time.perf_counter() - t
+        c1_done += c1_chunk
+    e1.close()
+    return {"value": single, "unit": "events/s", "cores": 1, "kind": "port",
+            "sample": f"first {done} events of the C2 stream ({n_keys} keys), CPU oracle (faithful single-thread "
+                      f"restatement of the reference engine; reference JVM unavailable on the box)",
+            "cpu_model": cpu_model(), "nproc": os.cpu_count(),
+            "partition_parallel": {"value": par, "unit": "events/s", "threads": T,
+                                   "sample": f"first {total} events of the C2 stream, keys sharded key % {T}, one "
+                                             f"oracle engine per thread"},
+            "C1": {"value": c1_done / c1_busy, "unit": "events/s", "cores": 1,
+                   "sample": f"first {c1_done} events of the C1 stream (unpartitioned, 1 event per ms, "
+                             f"within 10 sec), single-thread oracle"}}
 
 
 def to_dev(torch, d, dev):
@@ -131,12 +200,24 @@ def run_general(sa, synth, torch, dev, query, make_batch, n_keys, batch, steps, 
             "partials_scanned_per_step": d["partials_scanned"] / steps, "engine": "general"}
 
 
+def take_all(eng, ready):
+    """poll + release device matches until none is left (a window that wraps the ring comes in two polls);
+    ready=True takes only the batches already complete"""
+    while True:
+        m = eng.poll_device(ready=ready)
+        n = int(m.n)
+        eng.release(m)
+        if n == 0:
+            return
+
+
 def pcie_inclusive(sa, synth, torch, dev, cq, n_keys, batch, steps):
     """C2 with the batches handed over in HOST memory (sg_batch.mem = SG_MEM_HOST, pinned buffers):
     the engine's H2D copies of ts / key / the filtered column are inside the timed region.  Reported
     beside `value` (which starts from HBM-resident inputs), never as it."""
     eng = sa.NativeEngine(sa.load_hip_library(), "sg_", cq.ir, n_keys=n_keys, max_batch=batch,
-                          partial_capacity=64, match_capacity=2 * batch, device=dev.index or 0)
+                          partial_capacity=64, match_capacity=2 * batch, device=dev.index or 0,
+                          flags=sa.native.SG_CFG_ASYNC_HOST)
     bats = []
     for s in range(steps + 1):
         d = synth.stock_ticks(s * batch, batch, n_keys)
@@ -146,25 +227,69 @@ def pcie_inclusive(sa, synth, torch, dev, cq, n_keys, batch, steps):
         pin["symbol"] = pin["symbol"].view(np.uint32)
         bats.append(pin)
 
-    def step(s):
+    def step(s):   # pinned host batch (kept until its matches are polled: SG_CFG_ASYNC_HOST)
         d = bats[s]
         eng.push(0, s * batch, d["ts"], [d["symbol"], d["price"], d["volume"]], None, d["key"])
-        m = eng.poll_device()
-        eng.release(m)
+        take_all(eng, True)
 
     step(0)
     eng.synchronize()
+    take_all(eng, False)
     t0 = time.perf_counter()
     for s in range(1, steps + 1):
         step(s)
     eng.synchronize()
+    take_all(eng, False)
     el = time.perf_counter() - t0
     eng.close()
     hbytes = batch * (8 + 4 + 4)   # ts, key id, price (the one column the filters read)
     return {"value": batch * steps / el, "unit": "events/s", "ms_per_step": el / steps * 1e3,
             "h2d_bytes_per_step": hbytes, "h2d_GBps": hbytes * steps / el / 1e9,
-            "what": "C2 from pinned host batches (SG_MEM_HOST): H2D of ts/key/price + grouping + advance + "
-                    "ordering per push, one synchronous push per step"}
+            "what": "C2 from pinned host batches (SG_MEM_HOST, SG_CFG_ASYNC_HOST): H2D of ts/key/price on the "
+                    "engine's grouping stream overlapping the previous batch's advance + ordering, ready polls"}
+
+
+def output_inclusive(sa, synth, torch, dev, n_keys, batch, steps):
+    """C2 with its select list projected on the device (sg_set_projection: e1.symbol, e1.price, e2.price,
+    e2.price - e1.price) and every step's matches + projected columns copied to host memory (the
+    callback-side cost the reference pays in QuerySelector + StreamCallback).  Beside `value`."""
+    cp = importlib.import_module("siddhi-1_amd.compiler")
+    strings = sa.StringDictionary()
+    app = sa.parse_app(synth.C2_QUERY)
+    cq = sa.compile_query(app, app.queries[0], strings)
+    eng = sa.NativeEngine(sa.load_hip_library(), "sg_", cq.ir, n_keys=n_keys, max_batch=batch, partial_capacity=64,
+                          match_capacity=2 * batch, device=dev.index or 0)
+    eng.set_projection(*cp.projection_program(cq, strings))
+    bats = [to_dev(torch, synth.stock_ticks(s * batch, batch, n_keys), dev) for s in range(steps + 1)]
+    torch.cuda.synchronize()
+
+    def step(s, ready=True):
+        t = bats[s]
+        eng.push(0, s * batch, (batch, t["ts"].data_ptr(), [t["symbol"].data_ptr(), t["price"].data_ptr(),
+                                                            t["volume"].data_ptr()], t["key"].data_ptr()),
+                 [0, 1, 2], mem=sa.native.SG_MEM_DEVICE)
+        # matches + projected select list to host memory (pinned staging) of the completed batches
+        return eng.poll(copy=False, ready=ready)
+
+    step(0, ready=False)
+    t0 = time.perf_counter()
+    n = 0
+    for s in range(1, steps + 1):
+        n += len(step(s))
+    eng.synchronize()
+    while True:   # the rest (a window that wraps the output ring comes in two parts)
+        k = len(eng.poll(copy=False))
+        n += k
+        if k == 0:
+            break
+    el = time.perf_counter() - t0
+    eng.close()
+    per = 8 + 4 + 8 + 16 + 8 + 4 * 9   # trigger, key, ts, 2 slot seqs, 2 chain lengths, 4 items (8 B + null)
+    return {"value": batch * steps / el, "unit": "events/s", "ms_per_step": el / steps * 1e3,
+            "matches_per_step": n / steps, "d2h_bytes_per_step": n / steps * per,
+            "d2h_GBps": n * per / el / 1e9,
+            "what": "C2 with the select list projected on the device and every step's matches + projected "
+                    "columns copied to host memory (sg_poll_matches + sg_get_projection to host)"}
 
 
 def main():
@@ -254,15 +379,23 @@ def main():
         eng.push(0, local_seq[0], cols, [0, 1, 2], mem=sa.native.SG_MEM_DEVICE)
         local_seq[0] += n
         if world > 1:
-            # the exchange of the next slice overlaps this step's engine work (own streams)
+            # the exchange of the next slice overlaps this step's engine work (own streams); the poll
+            # waits for the step, so the exchange buffers the engine reads are never overwritten early
             nxt[0] = reshard_step(s + 1)
             del g
-        m = eng.poll_device()
-        eng.release(m)
+            take_all(eng, False)
+        else:
+            # pipelined: the matches of the batches already complete; batch s's grouping runs while
+            # batch s-1 advances (the engine's two streams), no host round trip between batches
+            take_all(eng, True)
+
+    def drain():   # the matches of the batches still in flight
+        eng.synchronize()
+        take_all(eng, False)
 
     for s in range(args.warmup):
         step(s)
-    eng.synchronize()
+    drain()
     st0 = eng.stats()
     if dist:
         dist.barrier()
@@ -270,7 +403,7 @@ def main():
     t0 = time.perf_counter()
     for s in range(args.warmup, total):
         step(s)
-    eng.synchronize()
+    drain()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -355,6 +488,7 @@ def main():
         }
     if rank == 0 and world == 1 and not args.no_extra:
         out["pcie_inclusive"] = pcie_inclusive(sa, synth, torch, dev, cq, K, B, 4)
+        out["output_inclusive"] = output_inclusive(sa, synth, torch, dev, K, B, 4)
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(sa, synth, K, B, args.cpu_seconds)
     if rank == 0:

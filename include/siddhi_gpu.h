@@ -46,6 +46,9 @@ extern "C" {
 
 #define SG_MEM_HOST 0u   /* pointers are host memory */
 #define SG_MEM_DEVICE 1u /* pointers are device (HBM) memory of the engine's device */
+/* or-ed into sg_poll_matches' mem: return the matches of the batches whose processing is complete,
+ * without waiting for the batches still in flight (they come with a later poll, in order) */
+#define SG_POLL_READY 0x10u
 
 #define SG_NULL_SEQ UINT64_MAX
 #define SG_KEY_NULL 0xFFFFFFFFu /* partition key id of an event without a key (null key: dropped) */
@@ -63,6 +66,11 @@ extern "C" {
  * whose partition key is null (PartitionStreamReceiver.java:175-205).  Used for fixed-size device batches
  * with padding (the multi-GPU reshard).  Without the flag a SG_KEY_NULL key is out of range. */
 #define SG_CFG_NULL_KEYS 4u
+/* sg_push_batch with host (SG_MEM_HOST) pointers returns once its copies are queued; the caller keeps
+ * the host buffers unchanged until a blocking sg_poll_matches (without SG_POLL_READY), sg_synchronize,
+ * or a ready poll that returns that batch's matches (the reference's @async junction hands events over
+ * the same way).  Without the flag a host push returns after its copies. */
+#define SG_CFG_ASYNC_HOST 8u
 
 typedef struct sg_engine sg_engine;
 
@@ -107,6 +115,30 @@ typedef struct sg_match_batch {
     uint32_t reserved;
 } sg_match_batch;
 
+/* On-device projection: QuerySelector.processNoGroupBy (QuerySelector.java:162-206)
+ * evaluates the select list on each emitted StateEvent; for a select list of plain expressions (no
+ * aggregate, group by or having) the engine does it on the device when the match is emitted, with the
+ * Java numerics of the filters (float32 without FMA contraction, null propagation, /0 -> null).
+ * code: expression bytecode (siddhi_gpu_ir.h; SG_OP_VAR b = slot, w1 = attribute, w2 = chain index with
+ * the selector's default index 0); item i is code[item_pc[i], item_pc[i] + item_len[i]) of result type
+ * item_type[i] (SG_T_*).  part_attr[s]: the partition attribute of stream s, or -1 (every event of a match
+ * has the match's key, so a slot's partition attribute may be read from the trigger event).  Call once,
+ * before the first push; fails with SG_ERR_UNSUPPORTED for items the device cannot evaluate. */
+int sg_set_projection(sg_engine* e, const uint32_t* code, uint32_t code_words, const uint32_t* item_pc,
+                      const uint32_t* item_len, const uint32_t* item_type, uint32_t n_items, const int32_t* part_attr,
+                      uint32_t n_streams);
+/* The projected select list of the polled matches (valid from sg_poll_matches to sg_release_matches):
+ * value[i * n + m] are item i's bits for match m (int / float / string id / bool in the low 32 bits;
+ * long / double 64), null[i * n + m] = 1 when the value is null. */
+typedef struct sg_projection {
+    uint64_t n;
+    uint32_t n_items;
+    uint32_t mem;
+    const uint64_t* value;
+    const uint8_t* null;
+} sg_projection;
+int sg_get_projection(sg_engine* e, uint32_t mem, sg_projection* out);
+
 /* Exact work counters (the algorithmic-byte model of DESIGN.md is computed from these). */
 typedef struct sg_stats {
     uint64_t events;            /* events pushed */
@@ -136,7 +168,11 @@ int sg_push_batch(sg_engine* e, const sg_batch* b);
  * (Scheduler time-change listener, Scheduler.java:73-104).  Matches emitted by timers are polled
  * like any other (trigger_seq = SG_TIMER_SEQ). */
 int sg_advance_time(sg_engine* e, int64_t now_ms);
-/* mem = SG_MEM_HOST copies matches to host memory; SG_MEM_DEVICE returns device pointers */
+/* mem = SG_MEM_HOST copies matches to host memory; SG_MEM_DEVICE returns device pointers into the ring of
+ * match_capacity ordered records (a window that wraps the ring comes in two polls, the part up to the
+ * ring's end first); | SG_POLL_READY returns only what is complete (a pipelined caller pushes batch i + 1
+ * before polling batch i).  A push waits while two batches are in flight, so a caller that ready-polls
+ * after every push has at most three batches' matches pending in the ring. */
 int sg_poll_matches(sg_engine* e, uint32_t mem, sg_match_batch* out);
 int sg_release_matches(sg_engine* e, sg_match_batch* m);
 int sg_get_stats(sg_engine* e, sg_stats* out);

@@ -631,3 +631,33 @@ def compile_query(app: q.App, query: q.Query, strings) -> CompiledQuery:
     return CompiledQuery(query.name, si.kind, ir, list(ctx.streams), list(ctx.slots), si.within_ms,
                          partition_keys, select, query.output_stream, query, si.element, recv,
                          aggs, group_by, having)
+
+
+def _has_kind(t, kinds):
+    if t.kind in kinds:
+        return True
+    return any(_has_kind(getattr(t, k), kinds) for k in ("left", "right", "arg", "cond")
+               if isinstance(getattr(t, k, None), _Typed))
+
+
+def projection_program(cq: CompiledQuery, strings):
+    """The select list as device expression programs (sg_set_projection), or None when the selector must
+    run on the host: aggregators, group by / having (QuerySelector.processInBatch*, order-dependent
+    per-partition state), multi-valued count attributes (OBJECT lists), instanceOf checks.
+    Returns (code words, item pc, item len, item type codes, partition attribute per IR stream)."""
+    if cq.aggregators or cq.group_by or cq.having is not None:
+        return None
+    em = _Emitter(strings)
+    pcs, lens, types = [], [], []
+    for name, typ, t in cq.select:
+        if typ not in TYPE_CODE or _has_kind(t, ("agg", "instof", "out")):
+            return None
+        pcs.append(len(em.code))
+        em.emit(t)
+        lens.append(len(em.code) - pcs[-1])
+        types.append(TYPE_CODE[typ])
+    part = []
+    for s in cq.streams:
+        attr = cq.partition_keys.get(s.name) if cq.partitioned else None
+        part.append(s.attr_index(attr) if attr else -1)
+    return em.code, pcs, lens, types, part

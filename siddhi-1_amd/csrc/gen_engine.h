@@ -30,7 +30,8 @@ __host__ __device__ inline size_t gen_at(uint32_t K, uint32_t blockWords, uint32
 #define GEN_MAXS 8       // input streams
 #define GEN_MAXSLOT 16   // state slots
 #define GEN_MAXA 16      // attributes per stream
-#define GEN_MAXCODE 1024 // filter bytecode words
+#define GEN_MAXCODE 1024 // filter (+ projection) bytecode words
+#define GEN_MAXPROJ 32   // select-list items projected on the device
 #define GEN_NONE (-1)
 #define GEN_NIL 0xffffu  // null pool index
 #define GEN_RAWSEG 256   // raw-match reservation counters of a batch
@@ -85,6 +86,9 @@ struct GenProgram {
     uint32_t ksWords;                       // words of one processor's KeyState
     uint32_t offKS, offST, offSTfree, offSE, offSEfree, offDef, blockWords;
     uint32_t stWords, seWords, DEF;
+    // on-device projection of the select list (sg_set_projection): item i = code[projPc[i], +projLen[i])
+    uint32_t projN, projOff;              // items; their words in a raw match record (3 per item)
+    uint32_t projPc[GEN_MAXPROJ], projLen[GEN_MAXPROJ];
 };
 
 // KeyState field offsets inside a processor's record

@@ -22,6 +22,7 @@
 #include "../../include/siddhi_gpu_ir.h"
 #include "gen_engine.h"
 #include "gen_host.h"
+#include "pinned.h"
 
 extern "C" __global__ void k_gen_batch(const GenArgs* ap);
 extern "C" __global__ void k_gen_timers(const GenArgs* ap);
@@ -376,6 +377,9 @@ struct OutBufs {
     uint64_t cap;
     uint32_t nslots, MC, recWords;
     uint32_t* err;
+    uint64_t* pval;   // projection [projN][cap] value bits, [projN][cap] null flags
+    uint8_t* pnull;
+    uint32_t projN, projOff;
 };
 
 __device__ void write_out(const OutBufs& o, uint64_t d, const uint32_t* rec, bool timer) {
@@ -393,6 +397,11 @@ __device__ void write_out(const OutBufs& o, uint64_t d, const uint32_t* rec, boo
                                      : SG_NULL_SEQ;
             o.slot[(d * o.nslots + s) * o.MC + c] = q;
         }
+    }
+    for (uint32_t i = 0; i < o.projN; i++) {  // the select list projected at emission (Lane::project)
+        const uint32_t* pv = rec + o.projOff + 3 * i;
+        o.pval[(size_t)i * o.cap + d] = (uint64_t)pv[0] | ((uint64_t)pv[1] << 32);
+        o.pnull[(size_t)i * o.cap + d] = (uint8_t)pv[2];
     }
 }
 
@@ -521,10 +530,13 @@ struct GenEngine {
     uint64_t arg_next = 0;
     uint32_t* err = nullptr;
     OutBufs out{};
-    std::vector<uint64_t> h_trig, h_slot;
-    std::vector<uint32_t> h_key, h_len;
-    std::vector<int64_t> h_ts;
+    PinnedVec<uint64_t> h_trig, h_slot;
+    PinnedVec<uint32_t> h_key, h_len;
+    PinnedVec<int64_t> h_ts;
     bool held = false;
+    uint64_t polled = 0;    // matches of the held poll (sg_get_projection)
+    PinnedVec<uint64_t> h_pval;
+    PinnedVec<uint8_t> h_pnull;
     int64_t now = 0;        // TimestampGenerator.currentTime() as last set by sg_advance_time
     int64_t lastEventTs = 0;
     bool advanced = false;
@@ -921,6 +933,76 @@ int gen_poll(GenEngine* e, uint32_t mem, sg_match_batch* out, std::string& msg) 
     }
     GH_OK(hipMemsetAsync(e->out.count, 0, 8, e->stream));
     e->held = true;
+    e->polled = n;
+    return SG_OK;
+}
+
+int gen_set_projection(GenEngine* e, const uint32_t* code, uint32_t words, const uint32_t* pc, const uint32_t* len,
+                       uint32_t n, std::string& msg) {
+    GenProgram& G = e->host;
+    if (e->st.batches != 0 || e->held) { msg = "set the projection before the first push"; return SG_ERR_STATE; }
+    if (G.projN) { msg = "the projection is already set"; return SG_ERR_STATE; }
+    if (n > GEN_MAXPROJ) { msg = "too many select items for the device projection"; return SG_ERR_UNSUPPORTED; }
+    if (G.ncode + words > GEN_MAXCODE) { msg = "select list too long for the device projection"; return SG_ERR_UNSUPPORTED; }
+    for (uint32_t i = 0; i < n; i++)
+        if (pc[i] + len[i] > words) { msg = "projection item outside its code"; return SG_ERR_INVALID; }
+    for (uint32_t w = 0; w < words;) {  // every opcode known, every slot in range
+        const uint32_t op = code[w] & 0xffu, b = (code[w] >> 16) & 0xffu;
+        const bool known = op == SG_OP_VAR || op == SG_OP_CONST || op == SG_OP_CVT || op == SG_OP_ISNULL_EV ||
+                           (op >= SG_OP_ADD && op <= SG_OP_MOD) || (op >= SG_OP_EQ && op <= SG_OP_LE) ||
+                           (op >= SG_OP_AND && op <= SG_OP_ISNULL) || op == SG_OP_IFELSE;
+        if (!known) { msg = "unknown opcode in the projection"; return SG_ERR_INVALID; }
+        if ((op == SG_OP_VAR || op == SG_OP_ISNULL_EV) && b >= (uint32_t)G.nslots) {
+            msg = "projection reads a slot the query does not have";
+            return SG_ERR_INVALID;
+        }
+        w += (op == SG_OP_VAR || op == SG_OP_CONST) ? 3 : (op == SG_OP_ISNULL_EV ? 2 : 1);
+    }
+    memcpy(G.code + G.ncode, code, (size_t)words * 4);
+    for (uint32_t i = 0; i < n; i++) {
+        G.projPc[i] = G.ncode + pc[i];
+        G.projLen[i] = len[i];
+    }
+    G.ncode += words;
+    G.projN = n;
+    G.projOff = e->recWords;
+    e->recWords += 3 * n;
+    e->raw = e->dalloc<uint32_t>(e->rawCap * e->recWords);  // (the smaller record buffer is freed at destroy)
+    e->out.recWords = e->recWords;
+    e->out.pval = e->dalloc<uint64_t>(e->mcap * n);
+    e->out.pnull = e->dalloc<uint8_t>(e->mcap * n);
+    e->out.projN = n;
+    e->out.projOff = G.projOff;
+    GH_OK(hipMemcpy(e->dprog, &G, sizeof(GenProgram), hipMemcpyHostToDevice));
+    return SG_OK;
+}
+
+int gen_get_projection(GenEngine* e, uint32_t mem, sg_projection* out, std::string& msg) {
+    if (!e->held) { msg = "poll the matches first"; return SG_ERR_STATE; }
+    const uint32_t n = e->host.projN;
+    if (!n) { msg = "no projection set"; return SG_ERR_STATE; }
+    out->n = e->polled;
+    out->n_items = n;
+    if (mem == SG_MEM_DEVICE) {  // item i of match m at i * capacity + m
+        if (e->polled && n > 1) { msg = "device projection rows are capacity-strided: poll to host"; return SG_ERR_INVALID; }
+        out->value = e->out.pval;
+        out->null = e->out.pnull;
+        out->mem = SG_MEM_DEVICE;
+        return SG_OK;
+    }
+    const size_t m = (size_t)e->polled;
+    e->h_pval.resize(m * n);
+    e->h_pnull.resize(m * n);
+    for (uint32_t i = 0; i < n && m; i++) {
+        GH_OK(hipMemcpyAsync(e->h_pval.data() + i * m, e->out.pval + (size_t)i * e->mcap, m * 8, hipMemcpyDeviceToHost,
+                             e->stream));
+        GH_OK(hipMemcpyAsync(e->h_pnull.data() + i * m, e->out.pnull + (size_t)i * e->mcap, m, hipMemcpyDeviceToHost,
+                             e->stream));
+    }
+    GH_OK(hipStreamSynchronize(e->stream));
+    out->value = e->h_pval.data();
+    out->null = e->h_pnull.data();
+    out->mem = SG_MEM_HOST;
     return SG_OK;
 }
 

@@ -18,24 +18,10 @@
 #include "../../include/siddhi_gpu.h"
 #include "../../include/siddhi_gpu_ir.h"
 #include "gen_engine.h"
+#include "java_ops.h"
 
 namespace {
 
-struct GVal {
-    uint64_t b;
-    bool null;
-};
-
-// instruction length in words (siddhi_gpu_ir.h)
-__device__ __forceinline__ uint32_t op_len(uint32_t op) {
-    op &= 0xffu;
-    return (op == SG_OP_VAR || op == SG_OP_CONST) ? 3u : (op == SG_OP_ISNULL_EV ? 2u : 1u);
-}
-
-__device__ __forceinline__ float gf32(uint64_t b) { return __uint_as_float((uint32_t)b); }
-__device__ __forceinline__ double gf64(uint64_t b) { return __longlong_as_double((long long)b); }
-__device__ __forceinline__ uint64_t gbf32(float f) { return (uint64_t)__float_as_uint(f); }
-__device__ __forceinline__ uint64_t gbf64(double d) { return (uint64_t)__double_as_longlong(d); }
 
 struct Lane {
     const GenProgram& G;
@@ -341,185 +327,33 @@ struct Lane {
         }
     }
 
-    // ---- filters ----
-    __device__ GVal cvt(GVal v, int from, int to) const {
-        if (v.null) return v;
-        if (from == SG_T_INT) {
-            const int32_t x = (int32_t)(uint32_t)v.b;
-            if (to == SG_T_LONG) return {(uint64_t)(int64_t)x, false};
-            if (to == SG_T_FLOAT) return {gbf32((float)x), false};
-            if (to == SG_T_DOUBLE) return {gbf64((double)x), false};
-        } else if (from == SG_T_LONG) {
-            const int64_t x = (int64_t)v.b;
-            if (to == SG_T_FLOAT) return {gbf32((float)x), false};
-            if (to == SG_T_DOUBLE) return {gbf64((double)x), false};
-        } else if (from == SG_T_FLOAT && to == SG_T_DOUBLE) {
-            return {gbf64((double)gf32(v.b)), false};
-        }
-        return v;
-    }
-    __device__ GVal arith(int op, int t, GVal l, GVal r) const {
-        if (l.null || r.null) return {0, true};
-        switch (t) {
-        case SG_T_INT: {
-            const int32_t a = (int32_t)(uint32_t)l.b, b = (int32_t)(uint32_t)r.b;
-            const uint32_t ua = (uint32_t)a, ub = (uint32_t)b;
-            switch (op) {
-            case SG_OP_ADD: return {(uint64_t)(uint32_t)(ua + ub), false};
-            case SG_OP_SUB: return {(uint64_t)(uint32_t)(ua - ub), false};
-            case SG_OP_MUL: return {(uint64_t)(uint32_t)(ua * ub), false};
-            case SG_OP_DIV:
-                if (b == 0) return {0, true};
-                if (b == -1) return {(uint64_t)(uint32_t)(0u - ua), false};
-                return {(uint64_t)(uint32_t)(a / b), false};
-            default:
-                if (b == 0) return {0, true};
-                if (b == -1) return {0, false};
-                return {(uint64_t)(uint32_t)(a % b), false};
-            }
-        }
-        case SG_T_LONG: {
-            const int64_t a = (int64_t)l.b, b = (int64_t)r.b;
-            const uint64_t ua = (uint64_t)a, ub = (uint64_t)b;
-            switch (op) {
-            case SG_OP_ADD: return {ua + ub, false};
-            case SG_OP_SUB: return {ua - ub, false};
-            case SG_OP_MUL: return {ua * ub, false};
-            case SG_OP_DIV:
-                if (b == 0) return {0, true};
-                if (b == -1) return {0ull - ua, false};
-                return {(uint64_t)(a / b), false};
-            default:
-                if (b == 0) return {0, true};
-                if (b == -1) return {0, false};
-                return {(uint64_t)(a % b), false};
-            }
-        }
-        case SG_T_FLOAT: {
-            const float a = gf32(l.b), b = gf32(r.b);
-            switch (op) {
-            case SG_OP_ADD: return {gbf32(__fadd_rn(a, b)), false};
-            case SG_OP_SUB: return {gbf32(__fsub_rn(a, b)), false};
-            case SG_OP_MUL: return {gbf32(__fmul_rn(a, b)), false};
-            case SG_OP_DIV: if (b == 0.0f) return {0, true}; return {gbf32(__fdiv_rn(a, b)), false};
-            default: if (b == 0.0f) return {0, true}; return {gbf32(fmodf(a, b)), false};
-            }
-        }
-        default: {
-            const double a = gf64(l.b), b = gf64(r.b);
-            switch (op) {
-            case SG_OP_ADD: return {gbf64(__dadd_rn(a, b)), false};
-            case SG_OP_SUB: return {gbf64(__dsub_rn(a, b)), false};
-            case SG_OP_MUL: return {gbf64(__dmul_rn(a, b)), false};
-            case SG_OP_DIV: if (b == 0.0) return {0, true}; return {gbf64(__ddiv_rn(a, b)), false};
-            default: if (b == 0.0) return {0, true}; return {gbf64(fmod(a, b)), false};
-            }
-        }
-        }
-    }
-    template <class T> __device__ static bool cmpOp(int op, T a, T b) {
-        switch (op) {
-        case SG_OP_EQ: return a == b;
-        case SG_OP_NE: return a != b;
-        case SG_OP_GT: return a > b;
-        case SG_OP_GE: return a >= b;
-        case SG_OP_LT: return a < b;
-        default: return a <= b;
-        }
-    }
-    __device__ bool compare(int op, int dom, GVal l, GVal r) const {
-        if (l.null || r.null) return op == SG_OP_NE;  // CompareConditionExpressionExecutor.java:38-42
-        switch (dom) {
-        case SG_T_INT: return cmpOp(op, (int32_t)(uint32_t)l.b, (int32_t)(uint32_t)r.b);
-        case SG_T_LONG: return cmpOp(op, (int64_t)l.b, (int64_t)r.b);
-        case SG_T_FLOAT: return cmpOp(op, gf32(l.b), gf32(r.b));
-        case SG_T_DOUBLE: return cmpOp(op, gf64(l.b), gf64(r.b));
-        case SG_T_BOOL: return cmpOp(op, (uint32_t)(l.b & 1), (uint32_t)(r.b & 1));
-        default: return cmpOp(op, (uint32_t)l.b, (uint32_t)r.b);
-        }
+    // ---- filters (java_ops.h: Java value semantics of the expression bytecode) ----
+    // a value of the expression program: VAR reads slot s's event at chain index c (its captured attribute)
+    __device__ GVal evalv(uint32_t se, const uint32_t* code, uint32_t pc, uint32_t n) {
+        return jo_eval(code, pc, n, err,
+                       [&](uint32_t slot, uint32_t attr, int32_t chain) -> GVal {
+                           const uint32_t e = chainAt(se, (int)slot, chain);
+                           if (e == GEN_NIL) return GVal{0, true};
+                           return GVal{(uint64_t)R64(sew(e, SE_ATTR + 2 * attr)),
+                                       ((W(sew(e, SE_NULL)) >> attr) & 1u) != 0};
+                       },
+                       [&](uint32_t slot, int32_t chain) -> bool { return chainAt(se, (int)slot, chain) == GEN_NIL; });
     }
     // FilterProcessor.process: pass iff the condition is a non-null true (FilterProcessor.java:48-60)
     __device__ bool eval(uint32_t se, uint32_t pc, uint32_t n) {
-        // the two top entries live in registers (t0 = top, t1 = below it); deeper ones in stk[]
-        // (stk[i] = entry i from the bottom), touched only by programs deeper than two
-        GVal stk[24];
-        GVal t0{0, true}, t1{0, true};
-        int sp = 0;
-        const uint32_t end = pc + n;
-        while (pc < end) {
-            const uint32_t w = G.code[pc];
-            const uint32_t op = w & 0xff, a = (w >> 8) & 0xff, b = (w >> 16) & 0xff;
-            if (sp > 22) { err |= GERR_CAP; return false; }
-            GVal v;
-            bool push = false, binary = false;
-            switch (op) {
-            case SG_OP_VAR: {
-                const uint32_t e = chainAt(se, (int)b, (int32_t)G.code[pc + 2]);
-                const uint32_t at_ = G.code[pc + 1];
-                if (e == GEN_NIL) v = {0, true};
-                else v = {(uint64_t)R64(sew(e, SE_ATTR + 2 * at_)), ((W(sew(e, SE_NULL)) >> at_) & 1u) != 0};
-                push = true;
-                break;
-            }
-            case SG_OP_CONST:
-                v = {(uint64_t)G.code[pc + 1] | ((uint64_t)G.code[pc + 2] << 32), b != 0};
-                push = true;
-                break;
-            case SG_OP_ISNULL_EV: {
-                const uint32_t e = chainAt(se, (int)b, (int32_t)G.code[pc + 1]);
-                v = {(uint64_t)(e == GEN_NIL), false};
-                push = true;
-                break;
-            }
-            case SG_OP_CVT: t0 = cvt(t0, (int)a, (int)b); break;
-            case SG_OP_ADD: case SG_OP_SUB: case SG_OP_MUL: case SG_OP_DIV: case SG_OP_MOD:
-                t0 = arith((int)op, (int)a, t1, t0);
-                binary = true;
-                break;
-            case SG_OP_EQ: case SG_OP_NE: case SG_OP_GT: case SG_OP_GE: case SG_OP_LT: case SG_OP_LE:
-                t0 = {(uint64_t)compare((int)op, (int)a, t1, t0), false};
-                binary = true;
-                break;
-            case SG_OP_AND: {
-                const bool l = !t1.null && (t1.b & 1), r = !t0.null && (t0.b & 1);
-                t0 = {(uint64_t)(l && r), false};
-                binary = true;
-                break;
-            }
-            case SG_OP_OR: {
-                const bool l = !t1.null && (t1.b & 1), r = !t0.null && (t0.b & 1);
-                t0 = {(uint64_t)(l || r), false};
-                binary = true;
-                break;
-            }
-            case SG_OP_NOT: {
-                const bool t = !t0.null && (t0.b & 1);
-                t0 = {(uint64_t)(!t), false};
-                break;
-            }
-            case SG_OP_ISNULL: t0 = {(uint64_t)t0.null, false}; break;
-            case SG_OP_IFELSE: {  // ifThenElse(cond, then, else): three popped, one pushed
-                const GVal c = sp >= 3 ? stk[sp - 3] : GVal{0, true};
-                t0 = (!c.null && (c.b & 1)) ? t1 : t0;
-                t1 = sp >= 4 ? stk[sp - 4] : GVal{0, true};
-                sp -= 2;
-                pc += op_len(op);
-                continue;
-            }
-            default: err |= GERR_REF; return false;
-            }
-            if (push) {
-                if (sp >= 2) stk[sp - 2] = t1;
-                t1 = t0;
-                t0 = v;
-                sp++;
-            } else if (binary) {  // two popped, one pushed: the entry below the operands moves up
-                if (sp >= 3) t1 = stk[sp - 3];
-                sp--;
-            }
-            pc += op_len(op);
+        const GVal v = evalv(se, G.code, pc, n);
+        return !v.null && (v.b & 1);
+    }
+
+    // QuerySelector.processNoGroupBy (QuerySelector.java:162-206) at emission: the select list over the
+    // state event's slots, 3 words per item (value lo, hi, null)
+    __device__ __noinline__ void projectSelect(uint32_t se, uint32_t* pv) {
+        for (uint32_t i = 0; i < G.projN; i++) {
+            const GVal v = evalv(se, G.code, G.projPc[i], G.projLen[i]);
+            pv[3 * i] = (uint32_t)v.b;
+            pv[3 * i + 1] = (uint32_t)(v.b >> 32);
+            pv[3 * i + 2] = v.null ? 1u : 0u;
         }
-        return sp > 0 && !t0.null && (t0.b & 1);
     }
 
     // ---- match output (QuerySelector input) ----
@@ -557,6 +391,7 @@ struct Lane {
             }
             lens[s] = n;
         }
+        if (G.projN) projectSelect(se, rec + G.projOff);
         if (timer) {  // (nvalid: the timers kernel adds its waves' match counts)
             A.o.tk1[r] = tk1;
             A.o.tk2[r] = tk2;

@@ -424,7 +424,14 @@ __device__ __forceinline__ void glb_emit(const Slab& g, KeySt& s, const Ev& ev, 
     for (uint32_t j = 0; j < s.gnp; ++j) {
         const bool hit = (j < 64) ? ((mask >> j) & 1ull) != 0 : glb_hit(g, j, ev, p);
         if (hit) {
-            if (pos < p.raw_capacity) p.raw_e1[pos] = g.SEQ(j);
+            if (pos < p.raw_capacity) {
+                p.raw_e1[pos] = g.SEQ(j);
+#if SGQ_PROJ
+#pragma unroll
+                for (int w = 0; w < SGQ_NCAPW; ++w) p.raw_capw[(size_t)w * p.raw_capacity + pos] = g.CAP(w, j);
+                if (SGQ_CAPNULL) p.raw_capnull[pos] = g.NUL(j);
+#endif
+            }
             pos++;
         } else {
             if (w1 != j) g.move(w1, j);
@@ -740,7 +747,15 @@ __device__ __forceinline__ void advance(const P2Params& p) {
 #pragma unroll
                     for (int j = 0; j < R; ++j) {
                         if ((H >> j) & 1u) {
-                            if (!SGX_NO_RAW && pos < p.raw_capacity) p.raw_e1[pos] = sbase + (uint64_t)(int64_t)W.seq[j];
+                            if (!SGX_NO_RAW && pos < p.raw_capacity) {
+                                p.raw_e1[pos] = sbase + (uint64_t)(int64_t)W.seq[j];
+#if SGQ_PROJ
+#pragma unroll
+                                for (int w = 0; w < SGQ_NCAPW; ++w)
+                                    p.raw_capw[(size_t)w * p.raw_capacity + pos] = W.cw[j][w];
+                                if (SGQ_CAPNULL) p.raw_capnull[pos] = W.cn[j];
+#endif
+                            }
                             pos++;
                         }
                     }

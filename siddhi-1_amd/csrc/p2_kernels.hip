@@ -8,6 +8,7 @@
 #include <algorithm>
 
 #include "../../include/siddhi_gpu_ir.h"
+#include "java_ops.h"
 #include "sg_engine.h"
 
 // ------------------------------------------------------------------------------------------------
@@ -147,9 +148,9 @@ __global__ void __launch_bounds__(256) k_order_scatter(const ScatterParams s, ui
         running += row;
     }
     const uint32_t total = running;  // records of this tile
-    const uint64_t out0 = *s.out_count + s.tile_off[blockIdx.x];
+    const uint64_t out0 = *s.out_count + s.tile_off[blockIdx.x];   // monotonic record number
     if (blockIdx.x == ntiles - 1 && threadIdx.x == 0) *s.batch_total = (unsigned long long)s.tile_off[blockIdx.x] + total;
-    if (out0 + total > s.capacity) {  // poll fails loudly; nothing is written past the buffers
+    if (out0 + total - s.win_start > s.capacity) {  // the ring would overwrite unpolled records: fail loudly
         if (threadIdx.x == 0 && total) atomicOr(s.err, (uint32_t)SGD_ERR_MATCH_CAP);
         return;
     }
@@ -163,19 +164,73 @@ __global__ void __launch_bounds__(256) k_order_scatter(const ScatterParams s, ui
             for (uint32_t r = a; r < b; ++r) owner[r - w0] = tl;
         }
         __syncthreads();
+        const uint64_t ring0 = out0 % s.capacity;
         for (uint32_t q = w0 + threadIdx.x; q < w1; q += 256) {
             const uint32_t tl = owner[q - w0];
             const uint32_t t = base + tl;
             const uint64_t trig = s.seq_base + t;
-            const uint64_t o = out0 + q;
+            uint64_t o = ring0 + q;
+            if (o >= s.capacity) o -= s.capacity;
             s.o_trig[o] = trig;
             // {e1 seq, e2 seq} as one 16-B store
             *reinterpret_cast<ulonglong2*>(s.o_slot + 2 * o) = make_ulonglong2(s.raw_e1[fst[tl] + (q - loc[tl])], trig);
             s.o_key[o] = s.key ? s.key[t] : 0u;
             s.o_ts[o] = s.ts[t];  // StreamPostStateProcessor.java:68: StateEvent ts = ts of the e2 event
+            if (s.o_capw) {       // on-device projection: the partial's captures in output order
+                const uint64_t r = fst[tl] + (q - loc[tl]);
+                for (uint32_t w = 0; w < s.n_capw; ++w)
+                    s.o_capw[(size_t)w * s.capacity + o] = s.raw_capw[(size_t)w * s.raw_capacity + r];
+                s.o_capnull[o] = s.raw_capnull[r];
+            }
         }
         __syncthreads();  // the owner map is rebuilt for the next window
     }
+}
+
+// QuerySelector.processNoGroupBy (QuerySelector.java:162-206) on the device for the batch's matches,
+// output slots [out_count - batch_total, out_count): e1's attributes from the captures the partial
+// carried, e2's (the trigger's) from the batch columns; Java numerics from java_ops.h
+__global__ void __launch_bounds__(256) k_project(const ProjParams p) {
+    const uint64_t total = *p.batch_total, o0 = (*p.out_count - total) % p.capacity;
+    uint32_t err = 0;
+    if (total > p.capacity) return;  // (the ordering reported the overflow)
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t o = o0 + i;
+        if (o >= p.capacity) o -= p.capacity;
+        const uint64_t t = p.o_trig[o] - p.seq_base;
+        const uint32_t cn = p.o_capnull[o];
+        for (uint32_t it = 0; it < p.n_items; ++it) {
+            const GVal v = jo_eval(
+                p.code, p.item_pc[it], p.item_len[it], err,
+                [&](uint32_t src, uint32_t x, int32_t chain) -> GVal {
+                    if (!(chain == 0 || chain == -1)) return GVal{0, true};  // a single-event slot
+                    if (src == 0) {  // e1 capture x
+                        const uint32_t w = p.capw_off[x];
+                        uint64_t b = p.o_capw[(size_t)w * p.capacity + o];
+                        const uint32_t ty = p.cap_type[x];
+                        if (ty == SG_T_LONG || ty == SG_T_DOUBLE) b |= (uint64_t)p.o_capw[(size_t)(w + 1) * p.capacity + o] << 32;
+                        return GVal{b, ((cn >> x) & 1u) != 0};
+                    }
+                    const void* c = p.col[x];  // the trigger event's attribute x
+                    uint64_t b;
+                    switch (p.col_type[x]) {
+                    case SG_T_LONG: case SG_T_DOUBLE: b = ((const uint64_t*)c)[t]; break;
+                    case SG_T_BOOL: b = ((const uint8_t*)c)[t] ? 1u : 0u; break;
+                    default: b = ((const uint32_t*)c)[t];
+                    }
+                    return GVal{b, p.col_null[x] && p.col_null[x][t] != 0};
+                },
+                [&](uint32_t, int32_t chain) -> bool { return !(chain == 0 || chain == -1); });
+            p.pval[(size_t)it * p.capacity + o] = v.b;
+            p.pnull[(size_t)it * p.capacity + o] = v.null ? 1 : 0;
+        }
+    }
+    if (err) atomicOr(p.err, (uint32_t)SGD_ERR_PROJ);
+}
+
+int sgd_launch_project(const ProjParams& p, ihipStream_t* stream) {
+    hipLaunchKernelGGL(k_project, dim3(1024), dim3(256), 0, stream, p);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 // partition purge: the listed keys' headers go back to "never seen" (INIT clear, no partials); the

@@ -56,7 +56,7 @@ enum {
 
 enum { SGD_ST_SCANNED = 0, SGD_ST_CREATED, SGD_ST_MATCHES, SGD_ST_KEYS, SGD_ST_LIVE0, SGD_ST_SPILLS, SGD_ST_N };
 
-enum { SGD_ERR_PARTIAL_CAP = 1, SGD_ERR_MATCH_CAP = 2, SGD_ERR_KEY_RANGE = 4 };
+enum { SGD_ERR_PARTIAL_CAP = 1, SGD_ERR_MATCH_CAP = 2, SGD_ERR_KEY_RANGE = 4, SGD_ERR_PROJ = 8 };
 
 // Advance-kernel arguments.  Everything that shapes the code (pattern mode, stream roles, column
 // types, filter expressions, capture layout, register window) is compiled into the kernel; this
@@ -93,6 +93,8 @@ struct P2Params {
     uint32_t* resume;                  // [n_keys] event index (in the key's run) where the HBM pass
                                        // resumes a key the staged pass stopped; SGD_NO_RESUME otherwise
     unsigned long long* prof;          // SGX_PROF experiments only (NULL otherwise)
+    uint32_t* raw_capw;                // SGQ_PROJ: [n_capw][raw_capacity] the matched partial's captures
+    uint32_t* raw_capnull;             // SGQ_PROJ: [raw_capacity] their null bits
     uint32_t stage_chunks;             // LDS staging per wave, 16-B chunks (dynamic LDS = waves x this)
     uint32_t pad;
     uint64_t cst[SGD_MAX_CONST];       // filter constants, already in their comparison domain
@@ -113,7 +115,7 @@ struct PackParams {
 struct ihipStream_t;
 int sgd_launch_bounds(const uint32_t* sorted_keys, uint32_t n, uint32_t n_keys, bool drop_null, uint32_t* seg_begin,
                       uint32_t* seg_end, uint32_t* err, ihipStream_t* stream);
-// ordered output of one batch: o_*[out_count + t_off[t] + r] for the r-th match of batch event t
+// ordered output of one batch: o_*[(out_count + t_off[t] + r) % capacity] for the r-th match of batch event t
 struct ScatterParams {
     uint32_t n;
     uint64_t seq_base;
@@ -123,16 +125,52 @@ struct ScatterParams {
     uint32_t* tile_sum;        // [ceil(n / SGD_ORDER_TILE)] matches per tile of triggers
     uint32_t* tile_off;        // exclusive scan of tile_sum
     const uint64_t* raw_e1;
-    unsigned long long* out_count;
+    unsigned long long* out_count;     // matches ordered so far (monotonic; record r at r % capacity)
     unsigned long long* batch_total;
-    uint64_t capacity;
+    uint64_t capacity;                 // ring of output records
+    uint64_t win_start;                // matches handed out by polls so far (their records are free)
     uint64_t* o_trig;
     uint64_t* o_slot;          // [n][2]
     uint32_t* o_key;
     int64_t* o_ts;
     uint32_t* err;             // (o_len is constant 1/1 for two-state matches: filled at allocation)
+    // on-device projection: the matched partials' captures follow their matches into output order
+    const uint32_t* raw_capw;  // [n_capw][raw_capacity]
+    const uint32_t* raw_capnull;
+    uint64_t raw_capacity;
+    uint32_t* o_capw;          // [n_capw][capacity] (NULL: no projection)
+    uint32_t* o_capnull;
+    uint32_t n_capw;
 };
 #define SGD_ORDER_TILE 4096  // triggers per workgroup of the ordering kernels (256 threads x 16 rows)
+// On-device projection of the select list (sg_set_projection) for the two-state kernel: after the ordering
+// of a batch, item i of every match of the batch is evaluated (java_ops.h) over the match's e1 captures
+// (VAR b = 0, w1 = capture index) and its trigger event's batch columns (VAR b = 1, w1 = attribute).
+#define SGD_MAX_ATTR 16
+#define SGD_MAX_PROJ 32
+struct ProjParams {
+    const uint32_t* code;       // rewritten item bytecode
+    const uint32_t* item_pc;    // [n_items]
+    const uint32_t* item_len;
+    const uint32_t* capw_off;   // capture index -> first word
+    const uint32_t* cap_type;
+    uint32_t n_items;
+    uint32_t pad;
+    uint64_t seq_base;
+    const void* col[SGD_MAX_ATTR];       // trigger stream's columns by attribute (NULL: not read)
+    const uint8_t* col_null[SGD_MAX_ATTR];
+    uint32_t col_type[SGD_MAX_ATTR];
+    const uint64_t* o_trig;
+    const uint32_t* o_capw;
+    const uint32_t* o_capnull;
+    uint64_t capacity;
+    const unsigned long long* out_count;     // after the batch (k_bump ran)
+    const unsigned long long* batch_total;
+    uint64_t* pval;             // [n_items][capacity]
+    uint8_t* pnull;
+    uint32_t* err;
+};
+int sgd_launch_project(const ProjParams& p, ihipStream_t* stream);
 // ordering of one batch's matches: per-tile sums, their exclusive scan (scan_tmp: rocPRIM scratch of
 // scan_bytes), then the tile-local scan + scatter; also bumps out_count
 int sgd_launch_scatter(const ScatterParams& s, void* scan_tmp, size_t scan_bytes, ihipStream_t* stream);

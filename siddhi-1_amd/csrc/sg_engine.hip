@@ -34,6 +34,7 @@
 #include "../../include/siddhi_gpu_ir.h"
 #include "gen_engine.h"
 #include "gen_host.h"
+#include "pinned.h"
 #include "sg_engine.h"
 #include "sg_jit.h"
 
@@ -207,20 +208,43 @@ struct sg_engine {
     JitQuery jq;
     std::vector<uint64_t> consts;
     std::map<int, Variant> variants;  // key: evnull | capnull << 1
-    // batch staging
-    int64_t* b_ts = nullptr;
-    uint32_t* b_key = nullptr;
-    std::vector<void*> b_cols;      // per attr slot (max attrs over streams)
-    std::vector<uint8_t*> b_nulls;
-    uint32_t* skeys = nullptr;
-    uint32_t* sidx = nullptr;
-    uint32_t* seg_begin = nullptr;
-    uint32_t* seg_end = nullptr;
+    // Batch pipeline: batch i's H2D copies and key grouping run on `gstream` into buffer slot i % 2
+    // while batch i-1's advance, ordering and projection run on `stream`; a slot is reused once the
+    // batch two back has finished reading it (slot.free), the advance waits for its grouping
+    // (slot.grouped).  Per-key state, raw matches and the ordered output live on `stream` only.
+    hipStream_t gstream = nullptr;
+    hipStream_t pstream = nullptr;            // device->host copies of polls
+    struct Slot {
+        int64_t* b_ts = nullptr;            // host batches: staging of the copied columns
+        uint32_t* b_key = nullptr;
+        std::vector<void*> b_cols;          // per filter column
+        std::vector<uint8_t*> b_nulls;
+        std::vector<void*> b_pcols;         // per projection column
+        std::vector<uint8_t*> b_pnulls;
+        uint32_t* skeys = nullptr;
+        uint32_t* sidx = nullptr;
+        uint32_t* seg_begin = nullptr;
+        uint32_t* seg_end = nullptr;
+        void* pay = nullptr;                // key-sorted payload [max_batch] x pay_words
+        hipEvent_t grouped = nullptr, copied = nullptr, free_ev = nullptr;
+        bool used = false;
+    };
+    Slot slots[2];
+    uint64_t nbatch = 0;
     uint32_t* iota = nullptr;
     void* sort_tmp = nullptr;
     size_t sort_tmp_bytes = 0;
-    void* pay = nullptr;           // key-sorted payload [max_batch] x pay_words
     uint32_t pay_words = 0;
+    // per pushed batch, after its ordering: the {match count, error word} status block copied to pinned
+    // host memory and an event, so a poll finds the completed batches without waiting for the others
+    static constexpr uint32_t RING = 64;
+    unsigned long long* h_status = nullptr;   // pinned [RING][2]
+    hipEvent_t done_ev[RING] = {};
+    std::vector<uint32_t> inflight;            // ring indices of batches not yet seen complete, in order
+    uint64_t done_count = 0;                   // out_count after the newest completed batch
+    uint32_t done_err = 0;
+    uint64_t win = 0;                          // matches handed out so far (the poll window's start)
+    bool async_host = false;                   // SG_CFG_ASYNC_HOST
     // matches
     uint64_t* raw_e1 = nullptr;
     unsigned long long* raw_count = nullptr;
@@ -246,9 +270,9 @@ struct sg_engine {
     int64_t* o_ts = nullptr;
     uint32_t* o_len = nullptr;
     // host copies
-    std::vector<uint64_t> h_trig, h_slot;
-    std::vector<uint32_t> h_key, h_len;
-    std::vector<int64_t> h_ts;
+    PinnedVec<uint64_t> h_trig, h_slot;
+    PinnedVec<uint32_t> h_key, h_len;
+    PinnedVec<int64_t> h_ts;
     uint64_t poll_base = 0;
     bool have_base = false;
     uint64_t next_seq = 0;
@@ -259,6 +283,20 @@ struct sg_engine {
     std::vector<Span> spans;
     std::vector<hipEvent_t> free_events;
     bool timing = false;
+    // on-device projection of the select list (sg_set_projection)
+    uint32_t proj_n = 0;
+    std::vector<uint32_t> proj_attrs;     // trigger-stream attributes the projection reads
+    uint32_t* d_proj = nullptr;           // rewritten code | item pc | item len | capture word offsets | types
+    ProjParams pp{};
+    uint32_t* raw_capw = nullptr;
+    uint32_t* raw_capnull = nullptr;
+    uint32_t* o_capw = nullptr;
+    uint32_t* o_capnull = nullptr;
+    uint64_t* pval = nullptr;
+    uint8_t* pnull = nullptr;
+    uint64_t polled = 0;
+    PinnedVec<uint64_t> h_pval;
+    PinnedVec<uint8_t> h_pnull;
     uint32_t reg_slots = 12;  // SGD_REG_SLOTS: partials per key held in registers by the advance kernel
     uint32_t stage_override = 0;  // SGD_STAGE_CHUNKS: fixed LDS staging per wave (tests force the HBM path)
     uint64_t spills = 0;
@@ -269,8 +307,8 @@ struct sg_engine {
         if (hipEventCreate(&x) != hipSuccess) throw std::runtime_error("hipEventCreate failed");
         return x;
     }
-    void mark(hipEvent_t x) {
-        if (hipEventRecord(x, stream) != hipSuccess) throw std::runtime_error("hipEventRecord failed");
+    void mark(hipEvent_t x, hipStream_t s = nullptr) {
+        if (hipEventRecord(x, s ? s : stream) != hipSuccess) throw std::runtime_error("hipEventRecord failed");
     }
     void resolve_spans() {  // call after the stream is synchronised
         for (auto& s : spans) {
@@ -301,13 +339,22 @@ struct sg_engine {
                 fprintf(stderr, "SG_PROF phases: stop/decode %llu stabilize %llu f1 %llu emit %llu seed %llu\n",
                         h[0], h[1], h[2], h[3], h[4]);
         }
+        if (gstream) (void)hipStreamSynchronize(gstream);
         if (gen) gen_destroy(gen);
+        for (auto& sl : slots)
+            for (hipEvent_t x : {sl.grouped, sl.copied, sl.free_ev})
+                if (x) (void)hipEventDestroy(x);
+        for (hipEvent_t x : done_ev)
+            if (x) (void)hipEventDestroy(x);
+        if (h_status) (void)hipHostFree(h_status);
         for (auto& sp : spans) { (void)hipEventDestroy(sp.a); (void)hipEventDestroy(sp.b); }
         for (auto x : free_events) (void)hipEventDestroy(x);
         for (void* p : owned) (void)hipFree(p);
         for (auto& kv : variants)
             if (kv.second.mod) (void)hipModuleUnload(kv.second.mod);
         if (stream) (void)hipStreamDestroy(stream);
+        if (gstream) (void)hipStreamDestroy(gstream);
+        if (pstream) (void)hipStreamDestroy(pstream);
     }
 };
 
@@ -498,31 +545,39 @@ void allocate(sg_engine* e) {
     e->p_capw = dalloc<uint32_t>(std::max<size_t>(1, e->n_capw) * C * K, o);
     e->p_capnull = dalloc<uint32_t>(C * K, o);
     HIP_OK(hipMemset(e->p_capnull, 0, C * K * 4));
-    e->b_ts = dalloc<int64_t>(B, o);
-    e->b_key = dalloc<uint32_t>(B, o);
     size_t maxattr = 0;
     for (auto& s : e->streams) maxattr = std::max(maxattr, s.types.size());
-    for (size_t a = 0; a < maxattr; a++) {
-        e->b_cols.push_back(dalloc<uint64_t>(B, o));
-        e->b_nulls.push_back(dalloc<uint8_t>(B, o));
+    for (auto& sl : e->slots) {
+        sl.b_ts = dalloc<int64_t>(B, o);
+        sl.b_key = dalloc<uint32_t>(B, o);
+        for (size_t a = 0; a < maxattr; a++) {
+            sl.b_cols.push_back(dalloc<uint64_t>(B, o));
+            sl.b_nulls.push_back(dalloc<uint8_t>(B, o));
+        }
+        sl.skeys = dalloc<uint32_t>(B, o);
+        sl.sidx = dalloc<uint32_t>(B, o);
+        sl.seg_begin = dalloc<uint32_t>(K, o);
+        sl.seg_end = dalloc<uint32_t>(K, o);
+        HIP_OK(hipEventCreateWithFlags(&sl.grouped, hipEventDisableTiming));
+        HIP_OK(hipEventCreateWithFlags(&sl.copied, hipEventDisableTiming));
+        HIP_OK(hipEventCreateWithFlags(&sl.free_ev, hipEventDisableTiming));
     }
-    e->skeys = dalloc<uint32_t>(B, o);
-    e->sidx = dalloc<uint32_t>(B, o);
+    for (auto& x : e->done_ev) HIP_OK(hipEventCreateWithFlags(&x, hipEventDisableTiming));
+    HIP_OK(hipHostMalloc((void**)&e->h_status, sizeof(unsigned long long) * 2 * sg_engine::RING, hipHostMallocDefault));
     e->iota = dalloc<uint32_t>(B, o);
     {
         std::vector<uint32_t> h(B);
         for (size_t i = 0; i < B; i++) h[i] = (uint32_t)i;
         HIP_OK(hipMemcpy(e->iota, h.data(), B * 4, hipMemcpyHostToDevice));
     }
-    e->seg_begin = dalloc<uint32_t>(K, o);
-    e->seg_end = dalloc<uint32_t>(K, o);
-    HIP_OK(rocprim::radix_sort_pairs(nullptr, e->sort_tmp_bytes, e->b_key, e->skeys, e->iota, e->sidx,
-                                     (uint32_t)B, 0, 32, e->stream));
+    HIP_OK(rocprim::radix_sort_pairs(nullptr, e->sort_tmp_bytes, e->slots[0].b_key, e->slots[0].skeys, e->iota,
+                                     e->slots[0].sidx, (uint32_t)B, 0, 32, e->stream));
     for (int W = 1; W <= 4; ++W) {
         size_t tb = 0;
         PackSrc ps{};
         for (uint32_t bits : {20u, 32u}) {
-            HIP_OK(sort_payload_w(W, nullptr, tb, e->b_key, e->skeys, ps, nullptr, (uint32_t)B, bits, e->stream));
+            HIP_OK(sort_payload_w(W, nullptr, tb, e->slots[0].b_key, e->slots[0].skeys, ps, nullptr, (uint32_t)B, bits,
+                                  e->stream));
             e->sort_tmp_bytes = std::max(e->sort_tmp_bytes, tb);
         }
     }
@@ -535,7 +590,8 @@ void allocate(sg_engine* e) {
             maxw = std::max(maxw, sgj_stride(sgj_col_words(ty) + 1));
         }
         e->pay_words = maxw;
-        e->pay = dalloc<uint32_t>((size_t)maxw * B + 4, o);  // + one 16-B chunk: the LDS copy rounds up
+        for (auto& sl : e->slots)  // + one 16-B chunk: the LDS copy rounds up
+            sl.pay = dalloc<uint32_t>((size_t)maxw * B + 4, o);
     }
     // raw match slots per batch: waves reserve at most sum(live partials + events) up front, or
     // (every (e1 -> e2)) chunks of SGD_RAW_CHUNK with two chunks of slack per wave (p2_jit.hip)
@@ -659,6 +715,15 @@ static uint32_t sgd_max_key(const uint32_t* k, uint32_t n, bool skip_null) {
     return m;
 }
 
+// a batch is complete once its ordering ran: record its status block into the pinned ring
+static void drain_one(sg_engine* e) {  // wait for the oldest in-flight batch
+    const uint32_t ri = e->inflight.front();
+    HIP_OK(hipEventSynchronize(e->done_ev[ri]));
+    e->done_count = e->h_status[2 * ri];
+    e->done_err |= (uint32_t)e->h_status[2 * ri + 1];
+    e->inflight.erase(e->inflight.begin());
+}
+
 int push(sg_engine* e, const sg_batch* b) {
     const Plan& pl = e->plan;
     if (b->stream >= e->streams.size()) return fail(SG_ERR_INVALID, "stream index out of range");
@@ -677,12 +742,19 @@ int push(sg_engine* e, const sg_batch* b) {
     const auto& cols = pl.evcols[b->stream];
     const bool dev = b->mem == SG_MEM_DEVICE;
     const hipMemcpyKind kind = dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    sg_engine::Slot& sl = e->slots[e->nbatch & 1];
+    const hipStream_t gs = e->gstream;
+    // at most two batches in flight: batch i's copies + grouping overlap batch i - 1's advance, and the
+    // matches pending in the output ring stay within three batches (the caller polls between pushes)
+    while (e->inflight.size() >= 2) drain_one(e);
+    // the slot's buffers were last read by the batch two back (its advance, ordering, projection)
+    if (sl.used) HIP_OK(hipStreamWaitEvent(gs, sl.free_ev, 0));
 
-    // timestamps / key ids / the columns the filters read (host batches: H2D)
+    // timestamps / key ids / the columns the filters read (host batches: H2D on the grouping stream)
     const int64_t* ts = b->ts;
     if (!dev) {
-        HIP_OK(hipMemcpyAsync(e->b_ts, b->ts, (size_t)n * 8, kind, e->stream));
-        ts = e->b_ts;
+        HIP_OK(hipMemcpyAsync(sl.b_ts, b->ts, (size_t)n * 8, kind, gs));
+        ts = sl.b_ts;
     }
     PackParams pk{};
     pk.n = n;
@@ -696,15 +768,37 @@ int push(sg_engine* e, const sg_batch* b) {
             pk.col[c] = b->cols[attr];
             pk.nul[c] = b->nulls ? b->nulls[attr] : nullptr;
         } else {
-            HIP_OK(hipMemcpyAsync(e->b_cols[c], b->cols[attr], (size_t)n * type_size(types[attr]), kind, e->stream));
-            pk.col[c] = e->b_cols[c];
+            HIP_OK(hipMemcpyAsync(sl.b_cols[c], b->cols[attr], (size_t)n * type_size(types[attr]), kind, gs));
+            pk.col[c] = sl.b_cols[c];
             pk.nul[c] = nullptr;
             if (b->nulls && b->nulls[attr]) {
-                HIP_OK(hipMemcpyAsync(e->b_nulls[c], b->nulls[attr], n, kind, e->stream));
-                pk.nul[c] = e->b_nulls[c];
+                HIP_OK(hipMemcpyAsync(sl.b_nulls[c], b->nulls[attr], n, kind, gs));
+                pk.nul[c] = sl.b_nulls[c];
             }
         }
         if (pk.nul[c]) any_null = true;
+    }
+    // the projection's trigger columns (read after the ordering, on the main stream)
+    ProjParams q = e->pp;
+    const bool proj = e->proj_n && is1;
+    if (proj) {
+        q.seq_base = b->seq_base;
+        for (size_t j = 0; j < e->proj_attrs.size(); j++) {
+            const uint32_t a = e->proj_attrs[j];
+            if (dev) {
+                q.col[a] = b->cols[a];
+                q.col_null[a] = b->nulls ? b->nulls[a] : nullptr;
+            } else {
+                HIP_OK(hipMemcpyAsync(sl.b_pcols[j], b->cols[a], (size_t)n * type_size(types[a]), kind, gs));
+                q.col[a] = sl.b_pcols[j];
+                q.col_null[a] = nullptr;
+                if (b->nulls && b->nulls[a]) {
+                    HIP_OK(hipMemcpyAsync(sl.b_pnulls[j], b->nulls[a], n, kind, gs));
+                    q.col_null[a] = sl.b_pnulls[j];
+                }
+            }
+            q.col_type[a] = types[a];
+        }
     }
     // the engine state (sequence window, null variant, counters) changes only once the batch has
     // passed validation: a rejected batch leaves the engine as it was, so the caller may fix it and
@@ -714,7 +808,7 @@ int push(sg_engine* e, const sg_batch* b) {
     const uint32_t words = sgj_col_words(coltypes) + (any_null ? 1u : 0u);
     const uint32_t stride = sgj_stride(words);
     if (stride > e->pay_words) throw HipError("payload stride above the allocated payload");
-    pk.payload = (uint32_t*)e->pay;
+    pk.payload = (uint32_t*)sl.pay;
 
     // ---- grouping by key: the batch as key-sorted payload elements + per-key segment bounds ----
     hipEvent_t g0 = nullptr, g1 = nullptr;
@@ -723,13 +817,14 @@ int push(sg_engine* e, const sg_batch* b) {
     if (pl.partitioned && !dev) {
         // the copy is queued first, so the host range check overlaps the DMA (pinned batches); the
         // staging buffers it fills are not engine state
-        HIP_OK(hipMemcpyAsync(e->b_key, b->key, (size_t)n * 4, kind, e->stream));
-        keys = e->b_key;
+        HIP_OK(hipMemcpyAsync(sl.b_key, b->key, (size_t)n * 4, kind, gs));
+        keys = sl.b_key;
         if (sgd_max_key(b->key, n, e->null_keys) >= e->K) {
-            HIP_OK(hipStreamSynchronize(e->stream));  // the queued copies read the caller's buffers
+            HIP_OK(hipStreamSynchronize(gs));  // the queued copies read the caller's buffers
             return fail(SG_ERR_INVALID, "key id outside [0, n_keys)");
         }
     }
+    if (!dev) HIP_OK(hipEventRecord(sl.copied, gs));
     e->nullable = nullable;
     if (!e->have_base) {
         e->poll_base = b->seq_base;
@@ -738,7 +833,7 @@ int push(sg_engine* e, const sg_batch* b) {
     e->next_seq = b->seq_base + b->n;
     e->st.events += b->n;
     e->st.batches++;
-    if (e->timing) { g0 = e->ev(); e->mark(g0); }
+    if (e->timing) { g0 = e->ev(); e->mark(g0, gs); }
     if (pl.partitioned) {
         size_t tmp = e->sort_tmp_bytes;
         if (words <= 4) {
@@ -761,25 +856,24 @@ int push(sg_engine* e, const sg_batch* b) {
                 ps.kind[wi++] = 4;
             }
             if (wi == 0) ps.kind[wi++] = 5;
-            HIP_OK(sort_payload_w((int)wi, e->sort_tmp, tmp, keys, e->skeys, ps, e->pay, n, e->sort_bits,
-                                  e->stream));
+            HIP_OK(sort_payload_w((int)wi, e->sort_tmp, tmp, keys, sl.skeys, ps, sl.pay, n, e->sort_bits, gs));
         } else {
-            HIP_OK(rocprim::radix_sort_pairs(e->sort_tmp, tmp, keys, e->skeys, e->iota, e->sidx, n, 0,
-                                             e->sort_bits, e->stream));
-            pk.sidx = e->sidx;
-            launch(v.pack[role], pack_blocks, 256, &pk, e->stream);
+            HIP_OK(rocprim::radix_sort_pairs(e->sort_tmp, tmp, keys, sl.skeys, e->iota, sl.sidx, n, 0, e->sort_bits,
+                                             gs));
+            pk.sidx = sl.sidx;
+            launch(v.pack[role], pack_blocks, 256, &pk, gs);
         }
-        if (sgd_launch_bounds(e->skeys, n, e->K, e->null_keys, e->seg_begin, e->seg_end, e->err, e->stream) != 0)
+        if (sgd_launch_bounds(sl.skeys, n, e->K, e->null_keys, sl.seg_begin, sl.seg_end, e->err, gs) != 0)
             throw HipError("k_seg_bounds launch failed");
     } else {
         pk.sidx = nullptr;  // one key: arrival order
-        launch(v.pack[role], pack_blocks, 256, &pk, e->stream);
-        const uint32_t z = 0;
-        HIP_OK(hipMemcpyAsync(e->seg_begin, &z, 4, hipMemcpyHostToDevice, e->stream));
-        HIP_OK(hipMemcpyAsync(e->seg_end, &n, 4, hipMemcpyHostToDevice, e->stream));
-        HIP_OK(hipStreamSynchronize(e->stream));  // &n / &z are stack values
+        launch(v.pack[role], pack_blocks, 256, &pk, gs);
+        HIP_OK(hipMemsetD32Async((hipDeviceptr_t)sl.seg_begin, 0u, 1, gs));
+        HIP_OK(hipMemsetD32Async((hipDeviceptr_t)sl.seg_end, (int)n, 1, gs));
     }
-    if (e->timing) { g1 = e->ev(); e->mark(g1); e->spans.push_back({g0, g1, 0}); }
+    if (e->timing) { g1 = e->ev(); e->mark(g1, gs); e->spans.push_back({g0, g1, 0}); }
+    HIP_OK(hipEventRecord(sl.grouped, gs));
+    HIP_OK(hipStreamWaitEvent(e->stream, sl.grouped, 0));
 
     // ---- the NFA advance ----
     P2Params p{};
@@ -787,9 +881,9 @@ int push(sg_engine* e, const sg_batch* b) {
     p.cap = e->cap;
     p.seq_base = b->seq_base;
     p.within = pl.within;
-    p.payload = (const uint32_t*)e->pay;
-    p.seg_begin = e->seg_begin;
-    p.seg_end = e->seg_end;
+    p.payload = (const uint32_t*)sl.pay;
+    p.seg_begin = sl.seg_begin;
+    p.seg_end = sl.seg_end;
     p.hdr = e->hdr;
     p.p_ts = e->p_ts;
     p.p_seq = e->p_seq;
@@ -806,6 +900,8 @@ int push(sg_engine* e, const sg_batch* b) {
     p.wstats = e->wstats;
     p.raw_static = e->raw_static;
     p.err = e->err;
+    p.raw_capw = e->raw_capw;
+    p.raw_capnull = e->raw_capnull;
     for (size_t i = 0; i < e->consts.size(); i++) p.cst[i] = e->consts[i];
     HIP_OK(hipMemsetAsync(e->raw_count, 0, 8, e->stream));
     hipEvent_t a0 = nullptr, a1 = nullptr;
@@ -821,14 +917,15 @@ int push(sg_engine* e, const sg_batch* b) {
             throw HipError("k_stats_reduce launch failed");
     }
     e->st.advance_launches++;
-    // order this batch's matches by trigger (exclusive scan of per-event counts + scatter)
+    // order this batch's matches by trigger (exclusive scan of per-event counts + scatter) into the ring
+    // of match_capacity output records
     hipEvent_t o0 = nullptr, o1 = nullptr;
     if (e->timing) { o0 = e->ev(); e->mark(o0); }
     {
         ScatterParams sp{};
         sp.n = n;
         sp.seq_base = b->seq_base;
-        sp.key = pl.partitioned ? (dev ? b->key : e->b_key) : nullptr;
+        sp.key = pl.partitioned ? (dev ? b->key : sl.b_key) : nullptr;
         sp.ts = ts;
         sp.t_desc = e->t_desc;
         sp.tile_sum = e->tile_sum;
@@ -837,49 +934,98 @@ int push(sg_engine* e, const sg_batch* b) {
         sp.out_count = e->out_count;
         sp.batch_total = e->batch_total;
         sp.capacity = e->mcap;
+        sp.win_start = e->win;
         sp.o_trig = e->o_trig;
         sp.o_slot = e->o_slot;
         sp.o_key = e->o_key;
         sp.o_ts = e->o_ts;
         sp.err = e->err;
+        sp.raw_capw = e->raw_capw;
+        sp.raw_capnull = e->raw_capnull;
+        sp.raw_capacity = e->raw_cap;
+        sp.o_capw = proj ? e->o_capw : nullptr;
+        sp.o_capnull = e->o_capnull;
+        sp.n_capw = e->n_capw;
         if (sgd_launch_scatter(sp, e->scan_tmp, e->scan_tmp_bytes, e->stream) != 0)
             throw HipError("ordering launch failed");
+        if (proj && sgd_launch_project(q, e->stream) != 0) throw HipError("projection launch failed");
     }
     if (e->timing) { o1 = e->ev(); e->mark(o1); e->spans.push_back({o0, o1, 2}); }
-    if (!dev) HIP_OK(hipStreamSynchronize(e->stream));  // host buffers may be reused by the caller
+    // the slot is free again once this batch's kernels ran; its status goes to the pinned ring
+    HIP_OK(hipEventRecord(sl.free_ev, e->stream));
+    sl.used = true;
+    const uint32_t ri = (uint32_t)(e->nbatch % sg_engine::RING);
+    HIP_OK(hipMemcpyAsync(e->h_status + 2 * ri, e->out_count, 16, hipMemcpyDeviceToHost, e->stream));
+    HIP_OK(hipEventRecord(e->done_ev[ri], e->stream));
+    e->inflight.push_back(ri);
+    e->nbatch++;
+    // host buffers may be reused by the caller once their copies ran (SG_CFG_ASYNC_HOST: the caller keeps
+    // them until the next poll / synchronize instead)
+    if (!dev && !e->async_host) HIP_OK(hipEventSynchronize(sl.copied));
     return SG_OK;
 }
 
-int poll(sg_engine* e, uint32_t mem, sg_match_batch* out) {
-    if (e->held) return fail(SG_ERR_STATE, "previous matches not released");
-    unsigned long long status[2] = {0ull, 0ull};  // {out_count, err} (adjacent on the device)
-    HIP_OK(hipMemcpyAsync(status, e->out_count, 16, hipMemcpyDeviceToHost, e->stream));
+// every queued batch done (both streams), their status blocks taken
+static void sync_all(sg_engine* e) {
+    HIP_OK(hipStreamSynchronize(e->gstream));
     HIP_OK(hipStreamSynchronize(e->stream));
-    const unsigned long long n = status[0];
-    uint32_t err = 0;
-    std::memcpy(&err, &status[1], 4);
+    while (!e->inflight.empty()) drain_one(e);
     e->resolve_spans();
+}
+
+// n records of w bytes each from ring position start (of a ring of cap records) to contiguous host memory
+static void ring_to_host(void* dst, const void* ring, size_t w, uint64_t start, uint64_t n, uint64_t cap,
+                         hipStream_t st) {
+    const uint64_t a = std::min<uint64_t>(n, cap - start);
+    if (a) HIP_OK(hipMemcpyAsync(dst, (const char*)ring + start * w, a * w, hipMemcpyDeviceToHost, st));
+    if (n > a) HIP_OK(hipMemcpyAsync((char*)dst + a * w, ring, (n - a) * w, hipMemcpyDeviceToHost, st));
+}
+
+// SG_POLL_READY: the matches of the batches already complete (no wait); else of every pushed batch.
+// The ordered records form a ring of match_capacity entries: a host poll copies the whole window; a device
+// poll of a window that wraps hands it out in two polls (the part up to the ring's end first).
+int poll(sg_engine* e, uint32_t memflags, sg_match_batch* out) {
+    if (e->held) return fail(SG_ERR_STATE, "previous matches not released");
+    const bool ready = (memflags & SG_POLL_READY) != 0;
+    const uint32_t mem = memflags & ~(uint32_t)SG_POLL_READY;
+    if (ready) {
+        while (!e->inflight.empty() && hipEventQuery(e->done_ev[e->inflight.front()]) == hipSuccess) drain_one(e);
+        if (e->inflight.empty()) {
+            HIP_OK(hipStreamSynchronize(e->gstream));  // (idle by now: its work precedes the advances)
+            e->resolve_spans();
+        }
+    } else {
+        sync_all(e);
+    }
+    const uint32_t err = e->done_err;
     if (err & SGD_ERR_KEY_RANGE) {
         // reported once: the events with valid keys were processed, the others dropped; the engine
         // goes on (capacity errors below stay: partials were lost)
-        const uint32_t rest = err & ~(uint32_t)SGD_ERR_KEY_RANGE;
-        HIP_OK(hipMemcpy(e->err, &rest, 4, hipMemcpyHostToDevice));
+        sync_all(e);
+        uint32_t cur = 0;
+        HIP_OK(hipMemcpy(&cur, e->err, 4, hipMemcpyDeviceToHost));
+        cur &= ~(uint32_t)SGD_ERR_KEY_RANGE;
+        HIP_OK(hipMemcpy(e->err, &cur, 4, hipMemcpyHostToDevice));
+        e->done_err &= ~(uint32_t)SGD_ERR_KEY_RANGE;
         return fail(SG_ERR_INVALID, "a batch carried key ids outside [0, n_keys) (those events were dropped)");
     }
     if (err & SGD_ERR_PARTIAL_CAP)
         return fail(SG_ERR_CAPACITY, "a partition key exceeded partial_capacity live partial matches");
-    if ((err & SGD_ERR_MATCH_CAP) || n > e->mcap)
-        return fail(SG_ERR_CAPACITY, "more matches than match_capacity between two polls");
+    if (err & SGD_ERR_PROJ) return fail(SG_ERR_STATE, "malformed projection program");
+    if (err & SGD_ERR_MATCH_CAP) return fail(SG_ERR_CAPACITY, "more matches than match_capacity between two polls");
+    const uint64_t avail = e->done_count - e->win;
+    const uint64_t start = e->win % e->mcap;
+    const unsigned long long n = mem == SG_MEM_DEVICE ? std::min<uint64_t>(avail, e->mcap - start) : avail;
     out->n = n;
     out->n_slots = 2;
     out->max_chain = 1;
     out->reserved = 0;
     if (mem == SG_MEM_DEVICE) {
-        out->trigger_seq = e->o_trig;
-        out->slot_seq = e->o_slot;
-        out->key = e->o_key;
-        out->ts = e->o_ts;
-        out->chain_len = e->o_len;
+        out->trigger_seq = e->o_trig + start;
+        out->slot_seq = e->o_slot + 2 * start;
+        out->key = e->o_key + start;
+        out->ts = e->o_ts + start;
+        out->chain_len = e->o_len + 2 * start;
         out->mem = SG_MEM_DEVICE;
     } else {
         e->h_trig.resize(n);
@@ -887,13 +1033,13 @@ int poll(sg_engine* e, uint32_t mem, sg_match_batch* out) {
         e->h_key.resize(n);
         e->h_ts.resize(n);
         e->h_len.resize(2 * n);
-        if (n) {
-            HIP_OK(hipMemcpyAsync(e->h_trig.data(), e->o_trig, n * 8, hipMemcpyDeviceToHost, e->stream));
-            HIP_OK(hipMemcpyAsync(e->h_slot.data(), e->o_slot, 2 * n * 8, hipMemcpyDeviceToHost, e->stream));
-            HIP_OK(hipMemcpyAsync(e->h_key.data(), e->o_key, n * 4, hipMemcpyDeviceToHost, e->stream));
-            HIP_OK(hipMemcpyAsync(e->h_ts.data(), e->o_ts, n * 8, hipMemcpyDeviceToHost, e->stream));
-            HIP_OK(hipMemcpyAsync(e->h_len.data(), e->o_len, 2 * n * 4, hipMemcpyDeviceToHost, e->stream));
-            HIP_OK(hipStreamSynchronize(e->stream));
+        if (n) {  // (a separate stream would not see the records any sooner: they are complete)
+            ring_to_host(e->h_trig.data(), e->o_trig, 8, start, n, e->mcap, e->pstream);
+            ring_to_host(e->h_slot.data(), e->o_slot, 16, start, n, e->mcap, e->pstream);
+            ring_to_host(e->h_key.data(), e->o_key, 4, start, n, e->mcap, e->pstream);
+            ring_to_host(e->h_ts.data(), e->o_ts, 8, start, n, e->mcap, e->pstream);
+            ring_to_host(e->h_len.data(), e->o_len, 8, start, n, e->mcap, e->pstream);
+            HIP_OK(hipStreamSynchronize(e->pstream));
         }
         out->trigger_seq = e->h_trig.data();
         out->slot_seq = e->h_slot.data();
@@ -902,10 +1048,147 @@ int poll(sg_engine* e, uint32_t mem, sg_match_batch* out) {
         out->chain_len = e->h_len.data();
         out->mem = SG_MEM_HOST;
     }
-    // the window restarts after this poll (device pointers stay valid until the next push)
-    HIP_OK(hipMemsetAsync(e->out_count, 0, 8, e->stream));
     e->poll_base = e->next_seq;
     e->held = true;
+    e->polled = n;
+    return SG_OK;
+}
+
+// ---- on-device projection (two-state kernel) -------------------------------------------------------
+// VAR of e1 (slot0) becomes "capture c" (the partial carries the attribute; added to the capture list if
+// the filters do not capture it already), VAR of e2 (slot1) "trigger column a"; e1's partition attribute
+// in a single-stream query is read from the trigger (same key, so the same value).
+int set_projection(sg_engine* e, const uint32_t* code, uint32_t words, const uint32_t* pc, const uint32_t* len,
+                   const uint32_t* types, uint32_t n, const int32_t* part_attr, uint32_t n_streams) {
+    Plan& pl = e->plan;
+    if (e->have_base || e->held) return fail(SG_ERR_STATE, "set the projection before the first push");
+    if (e->proj_n) return fail(SG_ERR_STATE, "the projection is already set");
+    if (n == 0 || n > SGD_MAX_PROJ) return fail(SG_ERR_UNSUPPORTED, "select list size outside the device projection");
+    for (uint32_t i = 0; i < n; i++)
+        if (pc[i] + len[i] > words) return fail(SG_ERR_INVALID, "projection item outside its code");
+    std::vector<uint32_t> c(code, code + words);
+    std::vector<uint32_t> caps = pl.caps;
+    std::vector<uint32_t> attrs;
+    const int32_t part0 = (part_attr && (uint32_t)pl.s0 < n_streams) ? part_attr[pl.s0] : -1;
+    for (uint32_t w = 0; w < words;) {
+        const uint32_t op = c[w] & 0xffu, b = (c[w] >> 16) & 0xffu;
+        const bool known = op == SG_OP_VAR || op == SG_OP_CONST || op == SG_OP_CVT || op == SG_OP_ISNULL_EV ||
+                           (op >= SG_OP_ADD && op <= SG_OP_MOD) || (op >= SG_OP_EQ && op <= SG_OP_LE) ||
+                           (op >= SG_OP_AND && op <= SG_OP_ISNULL) || op == SG_OP_IFELSE;
+        if (!known) return fail(SG_ERR_INVALID, "unknown opcode in the projection");
+        if (op == SG_OP_VAR || op == SG_OP_ISNULL_EV) {
+            if (b != pl.slot0 && b != pl.slot1) return fail(SG_ERR_INVALID, "projection reads an unknown slot");
+        }
+        if (op == SG_OP_VAR) {
+            const uint32_t attr = c[w + 1];
+            uint32_t src, x;
+            if (b == pl.slot1 || (pl.s0 == pl.s1 && (int32_t)attr == part0)) {
+                if (attr >= e->streams[pl.s1].types.size() || attr >= SGD_MAX_ATTR)
+                    return fail(SG_ERR_UNSUPPORTED, "projection attribute outside the device projection");
+                src = 1;
+                x = attr;
+                if (std::find(attrs.begin(), attrs.end(), attr) == attrs.end()) attrs.push_back(attr);
+            } else {
+                if (attr >= e->streams[pl.s0].types.size()) return fail(SG_ERR_INVALID, "attribute out of range");
+                size_t ci = std::find(caps.begin(), caps.end(), attr) - caps.begin();
+                if (ci == caps.size()) {
+                    if (caps.size() >= SGD_MAX_CAPS) return fail(SG_ERR_UNSUPPORTED, "too many captured attributes");
+                    caps.push_back(attr);
+                }
+                src = 0;
+                x = (uint32_t)ci;
+            }
+            c[w] = (c[w] & ~(0xffu << 16)) | (src << 16);
+            c[w + 1] = x;
+        }
+        w += (op == SG_OP_VAR || op == SG_OP_CONST) ? 3 : (op == SG_OP_ISNULL_EV ? 2 : 1);
+    }
+    try {
+        // the new capture list: payload columns, capture layout, JIT code, slabs (empty: no push yet)
+        for (size_t i = pl.caps.size(); i < caps.size(); i++) {
+            pl.caps.push_back(caps[i]);
+            pl.cap_col.push_back((uint8_t)col_index(pl.evcols[pl.s0], caps[i]));
+            pl.cap_type.push_back((uint8_t)e->streams[pl.s0].types.at(caps[i]));
+        }
+        {
+            uint32_t maxw = 1;
+            for (int s : {pl.s0, pl.s1}) {
+                std::vector<uint32_t> ty;
+                for (uint32_t a : pl.evcols[s]) ty.push_back(e->streams[s].types[a]);
+                maxw = std::max(maxw, sgj_stride(sgj_col_words(ty) + 1));
+            }
+            if (maxw > e->pay_words) {
+                e->pay_words = maxw;
+                for (auto& sl : e->slots) sl.pay = dalloc<uint32_t>((size_t)maxw * e->maxb + 4, e->owned);
+            }
+        }
+        const size_t K = e->K, C = e->cap, M = e->mcap;
+        e->n_capw = 0;
+        std::vector<uint32_t> woff;
+        for (uint8_t t : pl.cap_type) {
+            woff.push_back(e->n_capw);
+            e->n_capw += (t == SG_T_LONG || t == SG_T_DOUBLE) ? 2 : 1;
+        }
+        e->p_capw = dalloc<uint32_t>(std::max<size_t>(1, e->n_capw) * C * K, e->owned);
+        e->p_capnull = dalloc<uint32_t>(C * K, e->owned);
+        HIP_OK(hipMemset(e->p_capnull, 0, C * K * 4));
+        e->raw_capw = dalloc<uint32_t>(std::max<size_t>(1, e->n_capw) * e->raw_cap, e->owned);
+        e->raw_capnull = dalloc<uint32_t>(e->raw_cap, e->owned);
+        HIP_OK(hipMemset(e->raw_capnull, 0, e->raw_cap * 4));
+        e->o_capw = dalloc<uint32_t>(std::max<size_t>(1, e->n_capw) * M, e->owned);
+        e->o_capnull = dalloc<uint32_t>(M, e->owned);
+        e->pval = dalloc<uint64_t>(n * M, e->owned);
+        e->pnull = dalloc<uint8_t>(n * M, e->owned);
+        for (auto& sl : e->slots)
+            for (size_t j = 0; j < attrs.size(); j++) {
+                sl.b_pcols.push_back(dalloc<uint64_t>(e->maxb, e->owned));
+                sl.b_pnulls.push_back(dalloc<uint8_t>(e->maxb, e->owned));
+            }
+        // device tables: code | item pc | item len | capture word offsets | capture types
+        std::vector<uint32_t> tab(c);
+        const size_t o_pc = tab.size();
+        tab.insert(tab.end(), pc, pc + n);
+        const size_t o_len = tab.size();
+        tab.insert(tab.end(), len, len + n);
+        const size_t o_off = tab.size();
+        tab.insert(tab.end(), woff.begin(), woff.end());
+        const size_t o_ty = tab.size();
+        for (uint8_t t : pl.cap_type) tab.push_back(t);
+        tab.push_back(0);
+        e->d_proj = dalloc<uint32_t>(tab.size(), e->owned);
+        HIP_OK(hipMemcpy(e->d_proj, tab.data(), tab.size() * 4, hipMemcpyHostToDevice));
+        ProjParams& q = e->pp;
+        q = ProjParams{};
+        q.code = e->d_proj;
+        q.item_pc = e->d_proj + o_pc;
+        q.item_len = e->d_proj + o_len;
+        q.capw_off = e->d_proj + o_off;
+        q.cap_type = e->d_proj + o_ty;
+        q.n_items = n;
+        q.o_trig = e->o_trig;
+        q.o_capw = e->o_capw;
+        q.o_capnull = e->o_capnull;
+        q.capacity = M;
+        q.out_count = e->out_count;
+        q.batch_total = e->batch_total;
+        q.pval = e->pval;
+        q.pnull = e->pnull;
+        q.err = e->err;
+        (void)types;
+        // recompile the advance kernel: matches now carry the partials' captures
+        for (auto& kv : e->variants)
+            if (kv.second.mod) (void)hipModuleUnload(kv.second.mod);
+        e->variants.clear();
+        e->jq = make_jit_query(e);
+        e->jq.proj = true;
+        e->consts.clear();
+        (void)sgj_generate(e->jq, e->consts);
+        (void)variant(e, false, false);
+        e->proj_attrs = attrs;
+        e->proj_n = n;
+    } catch (const std::exception& ex) {
+        return fail(SG_ERR_DEVICE, ex.what());
+    }
     return SG_OK;
 }
 
@@ -977,6 +1260,9 @@ int sg_engine_create(const void* ir, size_t ir_len, const sg_config* cfg, sg_eng
         if (cfg->device < 0 || cfg->device >= ndev) throw HipError("no such HIP device");
         HIP_OK(hipSetDevice(cfg->device));
         HIP_OK(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+        HIP_OK(hipStreamCreateWithFlags(&e->gstream, hipStreamNonBlocking));
+        HIP_OK(hipStreamCreateWithFlags(&e->pstream, hipStreamNonBlocking));
+        e->async_host = (cfg->flags & SG_CFG_ASYNC_HOST) != 0;
         allocate(e);
         (void)variant(e, false, false);  // compile (or fetch) the advance kernel now: fail at creation
         *out = e;
@@ -1023,6 +1309,62 @@ int sg_advance_time(sg_engine* e, int64_t now_ms) {
     }
 }
 
+int sg_set_projection(sg_engine* e, const uint32_t* code, uint32_t code_words, const uint32_t* item_pc,
+                      const uint32_t* item_len, const uint32_t* item_type, uint32_t n_items, const int32_t* part_attr,
+                      uint32_t n_streams) {
+    if (!e || !code || !item_pc || !item_len || !item_type) return fail(SG_ERR_INVALID, "null argument");
+    try {
+        HIP_OK(hipSetDevice(e->device));
+        if (e->gen) {
+            std::string msg;
+            const int rc = gen_set_projection(e->gen, code, code_words, item_pc, item_len, n_items, msg);
+            return rc == SG_OK ? rc : fail(rc, msg);
+        }
+        return set_projection(e, code, code_words, item_pc, item_len, item_type, n_items, part_attr, n_streams);
+    } catch (const std::exception& ex) {
+        return fail(SG_ERR_DEVICE, ex.what());
+    }
+}
+
+int sg_get_projection(sg_engine* e, uint32_t mem, sg_projection* out) {
+    if (!e || !out) return fail(SG_ERR_INVALID, "null argument");
+    try {
+        HIP_OK(hipSetDevice(e->device));
+        if (e->gen) {
+            std::string msg;
+            const int rc = gen_get_projection(e->gen, mem, out, msg);
+            return rc == SG_OK ? rc : fail(rc, msg);
+        }
+        if (!e->held) return fail(SG_ERR_STATE, "poll the matches first");
+        if (!e->proj_n) return fail(SG_ERR_STATE, "no projection set");
+        const uint32_t n = e->proj_n;
+        const size_t m = (size_t)e->polled;
+        const size_t start = (size_t)((e->win) % e->mcap);
+        out->n = m;
+        out->n_items = n;
+        if (mem == SG_MEM_DEVICE) {
+            if (m && n > 1) return fail(SG_ERR_INVALID, "device projection rows are capacity-strided: poll to host");
+            out->value = e->pval + start;
+            out->null = e->pnull + start;
+            out->mem = SG_MEM_DEVICE;
+            return SG_OK;
+        }
+        e->h_pval.resize(m * n);
+        e->h_pnull.resize(m * n);
+        for (uint32_t i = 0; i < n && m; i++) {
+            ring_to_host(e->h_pval.data() + i * m, e->pval + (size_t)i * e->mcap, 8, start, m, e->mcap, e->pstream);
+            ring_to_host(e->h_pnull.data() + i * m, e->pnull + (size_t)i * e->mcap, 1, start, m, e->mcap, e->pstream);
+        }
+        HIP_OK(hipStreamSynchronize(e->pstream));
+        out->value = e->h_pval.data();
+        out->null = e->h_pnull.data();
+        out->mem = SG_MEM_HOST;
+        return SG_OK;
+    } catch (const std::exception& ex) {
+        return fail(SG_ERR_DEVICE, ex.what());
+    }
+}
+
 int sg_wait_stream(sg_engine* e, void* stream) {
     if (!e) return fail(SG_ERR_INVALID, "null argument");
     try {
@@ -1041,9 +1383,9 @@ int sg_poll_matches(sg_engine* e, uint32_t mem, sg_match_batch* out) {
     if (!e || !out) return fail(SG_ERR_INVALID, "null argument");
     try {
         HIP_OK(hipSetDevice(e->device));
-        if (e->gen) {
+        if (e->gen) {  // (the general engine's polls always wait for every pushed batch)
             std::string msg;
-            const int rc = gen_poll(e->gen, mem, out, msg);
+            const int rc = gen_poll(e->gen, mem & ~(uint32_t)SG_POLL_READY, out, msg);
             return rc == SG_OK ? rc : fail(rc, msg);
         }
         return poll(e, mem, out);
@@ -1055,6 +1397,7 @@ int sg_poll_matches(sg_engine* e, uint32_t mem, sg_match_batch* out) {
 int sg_release_matches(sg_engine* e, sg_match_batch* m) {
     if (!e) return fail(SG_ERR_INVALID, "null argument");
     if (e->gen) gen_release(e->gen);
+    else if (e->held) e->win += e->polled;  // those ring records are free again
     e->held = false;
     if (m) memset(m, 0, sizeof(*m));
     return SG_OK;
@@ -1064,8 +1407,12 @@ int sg_synchronize(sg_engine* e) {
     if (!e) return fail(SG_ERR_INVALID, "null argument");
     try {
         HIP_OK(hipSetDevice(e->device));
-        HIP_OK(hipStreamSynchronize(e->stream));
-        e->resolve_spans();
+        if (e->gen) {
+            HIP_OK(hipStreamSynchronize(e->stream));
+            e->resolve_spans();
+        } else {
+            sync_all(e);
+        }
         return SG_OK;
     } catch (const std::exception& ex) {
         return fail(SG_ERR_DEVICE, ex.what());
@@ -1081,9 +1428,9 @@ int sg_get_stats(sg_engine* e, sg_stats* out) {
             return SG_OK;
         }
         unsigned long long s[SGD_ST_N];
+        sync_all(e);
         HIP_OK(hipMemcpyAsync(s, e->stats, sizeof(s), hipMemcpyDeviceToHost, e->stream));
         HIP_OK(hipStreamSynchronize(e->stream));
-        e->resolve_spans();
         *out = e->st;
         out->partials_scanned = s[SGD_ST_SCANNED];
         out->partials_created = s[SGD_ST_CREATED];
@@ -1182,10 +1529,8 @@ struct SnapHeader {
 #define SG_SNAP_VERSION 1u
 
 static bool outputs_pending(sg_engine* e) {
-    unsigned long long n = 0;
-    HIP_OK(hipMemcpyAsync(&n, e->out_count, 8, hipMemcpyDeviceToHost, e->stream));
-    HIP_OK(hipStreamSynchronize(e->stream));
-    return n != 0;
+    sync_all(e);
+    return e->done_count != e->win;
 }
 
 int sg_snapshot(sg_engine* e, void** buf, size_t* len) {

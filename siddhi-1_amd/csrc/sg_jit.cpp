@@ -351,6 +351,7 @@ std::string sgj_generate(const JitQuery& q, std::vector<uint64_t>& consts) {
     o << "#define SGQ_WITHIN " << (q.within ? 1 : 0) << "\n";
     o << "#define SGQ_NCAPW " << ncapw << "\n";
     o << "#define SGQ_CAPNULL " << (q.capnull ? 1 : 0) << "\n";
+    o << "#define SGQ_PROJ " << (q.proj ? 1 : 0) << "\n";
     o << "#define SGQ_STRIDE0 " << stride[0] << "\n";
     o << "#define SGQ_STRIDE1 " << stride[1] << "\n";
     for (int s = 0; s < ns; s++) gen_stream(o, s, q.coltypes[s], q.evnull);

@@ -25,6 +25,7 @@ struct JitQuery {
     std::vector<uint8_t> cap_type;
     bool evnull = false;                  // this variant's batches carry null flags
     bool capnull = false;                 // captures carry null bits
+    bool proj = false;                    // on-device projection: matches carry the partial's captures
 };
 
 // payload words of a stream: [batch position][column words][null word?][pad][ts lo, ts hi]

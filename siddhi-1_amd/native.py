@@ -9,12 +9,15 @@ from __future__ import annotations
 import ctypes as C
 import os
 from dataclasses import dataclass
+from typing import Optional
 
 import numpy as np
 
 SG_OK = 0
 SG_MEM_HOST = 0
 SG_MEM_DEVICE = 1
+SG_POLL_READY = 0x10
+SG_CFG_ASYNC_HOST = 8
 SG_NULL_SEQ = np.uint64(0xFFFFFFFFFFFFFFFF)
 SG_CFG_NO_ORDER = 1
 SG_CFG_TIMING = 2
@@ -63,14 +66,21 @@ class sg_stats(C.Structure):
                                           "advance_launches", "window_spills", "advance_hbm_ns")]
 
 
+class sg_projection(C.Structure):
+    _fields_ = [("n", C.c_uint64), ("n_items", C.c_uint32), ("mem", C.c_uint32), ("value", C.c_void_p),
+                ("null", C.c_void_p)]
+
+
 @dataclass
 class Matches:
-    """Host copy of one sg_match_batch."""
+    """Host copy of one sg_match_batch (+ the on-device projection of the select list, when set)."""
     trigger_seq: np.ndarray   # [n] uint64
     key: np.ndarray           # [n] uint32
     ts: np.ndarray            # [n] int64
     slot_seq: np.ndarray      # [n, n_slots, max_chain] uint64
     chain_len: np.ndarray     # [n, n_slots] uint32
+    proj_value: Optional[np.ndarray] = None   # [n_items, n] uint64 value bits
+    proj_null: Optional[np.ndarray] = None    # [n_items, n] uint8
 
     def __len__(self):
         return int(self.trigger_seq.shape[0])
@@ -275,6 +285,22 @@ class NativeEngine:
         self._check(self._create(self._ir, len(ir), C.byref(cfg), C.byref(h)))
         self.h = h
         self.n_keys = n_keys
+        self.proj_items = 0
+
+    def set_projection(self, code, item_pc, item_len, item_type, part_attr):
+        """On-device projection of the select list (sg_set_projection); raises EngineError when the
+        engine cannot evaluate it (SG_ERR_UNSUPPORTED: keep projecting on the host)."""
+        f = getattr(self.lib, self.p + "set_projection", None)
+        if f is None:   # (the CPU oracle projects on the host)
+            raise EngineError(-2, "this engine library has no on-device projection")
+        f.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
+                      C.c_void_p, C.c_uint32]
+        arr = lambda x, dt: np.ascontiguousarray(np.array(x, dtype=dt))
+        code, pc, ln, ty, pa = (arr(code, np.uint32), arr(item_pc, np.uint32), arr(item_len, np.uint32),
+                                arr(item_type, np.uint32), arr(part_attr, np.int32))
+        self._check(f(self.h, _np_ptr(code), len(code), _np_ptr(pc), _np_ptr(ln), _np_ptr(ty), len(pc), _np_ptr(pa),
+                      len(pa)))
+        self.proj_items = len(pc)
 
     def _check(self, rc):
         if rc != SG_OK:
@@ -312,9 +338,12 @@ class NativeEngine:
                          C.cast(colp, C.POINTER(C.c_void_p)), None, n_cols, SG_MEM_DEVICE)
             self._check(self._push(self.h, C.byref(b)))
 
-    def poll(self) -> Matches:
+    def poll(self, copy=True, ready=False) -> Matches:
+        """Matches emitted since the previous poll, in host memory.  copy=False returns views of the
+        engine's pinned staging, valid until the next poll of this engine (no host-side copy).
+        ready=True: only the matches of batches already complete (SG_POLL_READY, no wait)."""
         m = sg_match_batch()
-        self._check(self._poll(self.h, SG_MEM_HOST, C.byref(m)))
+        self._check(self._poll(self.h, SG_MEM_HOST | (SG_POLL_READY if ready else 0), C.byref(m)))
         n, ns, mc = int(m.n), int(m.n_slots), int(m.max_chain)
 
         def arr(ptr, dtype, shape):
@@ -322,18 +351,27 @@ class NativeEngine:
             if cnt == 0 or not ptr:
                 return np.zeros(shape, dtype=dtype)
             buf = (C.c_char * (cnt * np.dtype(dtype).itemsize)).from_address(ptr)
-            return np.frombuffer(buf, dtype=dtype).reshape(shape).copy()
+            a = np.frombuffer(buf, dtype=dtype).reshape(shape)
+            return a.copy() if copy else a
 
         out = Matches(arr(m.trigger_seq, np.uint64, (n,)), arr(m.key, np.uint32, (n,)),
                       arr(m.ts, np.int64, (n,)), arr(m.slot_seq, np.uint64, (n, ns, mc)),
                       arr(m.chain_len, np.uint32, (n, ns)))
+        if self.proj_items:
+            pr = sg_projection()
+            g = getattr(self.lib, self.p + "get_projection")
+            g.argtypes = [C.c_void_p, C.c_uint32, C.POINTER(sg_projection)]
+            self._check(g(self.h, SG_MEM_HOST, C.byref(pr)))
+            out.proj_value = arr(pr.value, np.uint64, (self.proj_items, n))
+            out.proj_null = arr(pr.null, np.uint8, (self.proj_items, n))
         self._check(self._release(self.h, C.byref(m)))
         return out
 
-    def poll_device(self):
-        """Matches stay in HBM; returns the raw sg_match_batch (caller must release())."""
+    def poll_device(self, ready=False):
+        """Matches stay in HBM; returns the raw sg_match_batch (caller must release()).
+        ready=True: only the batches already complete (SG_POLL_READY)."""
         m = sg_match_batch()
-        self._check(self._poll(self.h, SG_MEM_DEVICE, C.byref(m)))
+        self._check(self._poll(self.h, SG_MEM_DEVICE | (SG_POLL_READY if ready else 0), C.byref(m)))
         return m
 
     def release(self, m):

@@ -248,6 +248,15 @@ class _QueryRuntime:
         self.key_dict = key_dict
         self.n_keys = app_rt.n_keys if cq.partitioned else 1
         self.engine = engine_factory(cq.ir, self.n_keys)
+        # the select list on the device when it is plain expressions; else on the host
+        self.device_projection = False
+        prog = cp.projection_program(cq, app_rt.strings)
+        if prog is not None and hasattr(self.engine, "set_projection"):
+            try:
+                self.engine.set_projection(*prog)
+                self.device_projection = True
+            except EngineError:
+                self.device_projection = False
         self.query_callbacks: List[QueryCallback] = []
         # aggregator states: (partition key, group-by key) -> one state per aggregator
         # (PartitionStateHolder over the group-by flow's states, C/util/snapshot/state/*StateHolder.java)
@@ -350,7 +359,31 @@ class _QueryRuntime:
             st["v"] = v
         return st["v"]
 
+    def _decode(self, bits, null, typ):
+        """device projection bits of one item -> the Java-typed values (float -> np.float32)"""
+        if typ == "INT":
+            vals = bits.astype(np.uint32).view(np.int32).tolist()
+        elif typ == "LONG":
+            vals = bits.view(np.int64).tolist()
+        elif typ == "FLOAT":
+            vals = list(bits.astype(np.uint32).view(np.float32))
+        elif typ == "DOUBLE":
+            vals = bits.view(np.float64).tolist()
+        elif typ == "BOOL":
+            vals = [bool(x & 1) for x in bits.tolist()]
+        else:   # STRING: the host dictionary id
+            strs = self.app_rt.strings.strs
+            vals = [strs[int(x)] for x in bits.tolist()]
+        return [None if nl else v for v, nl in zip(vals, null.tolist())]
+
     def project(self, m, store):
+        if self.device_projection and m.proj_value is not None:
+            cols = [self._decode(m.proj_value[i], m.proj_null[i], typ) for i, (_, typ, _) in enumerate(self.cq.select)]
+            trig, ts = m.trigger_seq.tolist(), m.ts.tolist()
+            return [(trig[i], ts[i], [c[i] for c in cols]) for i in range(len(m))]
+        return self.project_host(m, store)
+
+    def project_host(self, m, store):
         """QuerySelector.process per emitted StateEvent (each reaches the selector in a chunk of its
         own: StateMultiProcessStreamReceiver.java:59-65, SingleProcessStreamReceiver.java:71-77), so
         processInBatch(No)GroupBy (QuerySelector.java:272-370) emits each match that passes `having`

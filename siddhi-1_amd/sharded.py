@@ -75,6 +75,9 @@ class ShardedEngine:
         return list(self.pool.map(fn, range(self.N)))
 
     # -- NativeEngine interface ------------------------------------------------------------------------
+    def set_projection(self, *prog):
+        for s in self.shards:
+            s.set_projection(*prog)
     def push(self, stream, seq_base, ts, cols, nulls=None, key=None, mem=SG_MEM_HOST):
         if mem != SG_MEM_HOST:
             raise ValueError("ShardedEngine takes host batches (the device path is bench.py's RCCL reshard)")
@@ -119,7 +122,7 @@ class ShardedEngine:
             slot[live] = self._map(r, slot[live])
             key = (m.key.astype(np.uint64) * np.uint64(self.N) + np.uint64(r)).astype(np.uint32) \
                 if self.N > 1 else m.key
-            parts.append(Matches(trig, key, m.ts.copy(), slot, m.chain_len.copy()))
+            parts.append(Matches(trig, key, m.ts.copy(), slot, m.chain_len.copy(), m.proj_value, m.proj_null))
         if not parts:
             return got[0] if got else Matches(np.zeros(0, np.uint64), np.zeros(0, np.uint32), np.zeros(0, np.int64),
                                              np.zeros((0, 1, 1), np.uint64), np.zeros((0, 1), np.uint32))
@@ -127,9 +130,13 @@ class ShardedEngine:
         for i, p in enumerate(parts):      # the chain dimension padded to the widest shard's
             if p.slot_seq.shape[2] < w:
                 pad = np.full(p.slot_seq.shape[:2] + (w - p.slot_seq.shape[2],), SG_NULL_SEQ, dtype=np.uint64)
-                parts[i] = Matches(p.trigger_seq, p.key, p.ts, np.concatenate([p.slot_seq, pad], axis=2), p.chain_len)
+                parts[i] = Matches(p.trigger_seq, p.key, p.ts, np.concatenate([p.slot_seq, pad], axis=2), p.chain_len,
+                                   p.proj_value, p.proj_null)
         cat = Matches(*[np.concatenate([getattr(p, f) for p in parts]) for f in
                         ("trigger_seq", "key", "ts", "slot_seq", "chain_len")])
+        if parts[0].proj_value is not None:
+            cat.proj_value = np.concatenate([p.proj_value for p in parts], axis=1)
+            cat.proj_null = np.concatenate([p.proj_null for p in parts], axis=1)
         pos = np.arange(len(cat.trigger_seq))
         timer = cat.trigger_seq == TIMER_SEQ
         # timer matches first (a poll after advance_time holds only those), by (fire time, key); batch
@@ -139,7 +146,8 @@ class ShardedEngine:
         k2 = np.where(timer, cat.key.astype(np.int64), 0)
         order = np.lexsort((pos, k2, k1, primary))
         return Matches(cat.trigger_seq[order], cat.key[order], cat.ts[order], cat.slot_seq[order],
-                       cat.chain_len[order])
+                       cat.chain_len[order], None if cat.proj_value is None else cat.proj_value[:, order],
+                       None if cat.proj_null is None else cat.proj_null[:, order])
 
     def advance_time(self, now):
         self._each(lambda r: self.shards[r].advance_time(now))
