@@ -462,6 +462,7 @@ __device__ __forceinline__ void advance(const P2Params& p) {
     typedef typename SgSel<S0, SgEv0, SgEv1>::type Ev;
     constexpr int STRIDE = S0 ? SGQ_STRIDE0 : SGQ_STRIDE1;
     constexpr uint32_t SB = STRIDE * 4;  // bytes per payload element
+    constexpr uint32_t NW = SGD_BLOCK / SGD_WAVE;
     const int lane = threadIdx.x & (SGD_WAVE - 1);
     const uint32_t wv = threadIdx.x / SGD_WAVE;
     const uint32_t k = blockIdx.x * SGD_BLOCK + threadIdx.x;
@@ -473,6 +474,24 @@ __device__ __forceinline__ void advance(const P2Params& p) {
         b = p.seg_begin[k];
         e = p.seg_end[k];
         h = p.hdr[k];
+    }
+    // The staged pass stages the workgroup's runs whole (its keys are consecutive, so their runs are one
+    // byte range of the sorted payload): the wave ranges meet in LDS, one barrier.  (Dealing keys to lanes
+    // by run length was measured: 22% fewer VALU instructions, no faster — the workgroup's LDS is held
+    // until its longest lane ends, so occupancy, not lane idling, bounds the walk.)
+    uint32_t blo = 0, bhi = 0, rlo = 0;  // the workgroup's payload range; the wave's first event
+    if constexpr (STG) {
+        __shared__ uint32_t s_lo[NW], s_hi[NW];
+        const uint32_t nv = e - b;
+        rlo = uni(wave_min_u(nv > 0 ? b : 0xffffffffu));
+        const uint32_t hi = uni(wave_max_u(nv > 0 ? e : 0u));
+        if (lane == 0) { s_lo[wv] = rlo; s_hi[wv] = hi; }
+        __syncthreads();
+        blo = 0xffffffffu;
+#pragma unroll
+        for (uint32_t w = 0; w < NW; ++w) { blo = min(blo, s_lo[w]); bhi = max(bhi, s_hi[w]); }
+        blo = uni(blo);
+        bhi = uni(bhi);
     }
     bool count_key = true;  // this pass owns the key's keys_touched / live_at_batch_start counts
     if constexpr (!STG) {
@@ -492,21 +511,20 @@ __device__ __forceinline__ void advance(const P2Params& p) {
     const int nev = (int)(e - b);
     if (nev <= 0) h = 0;
     int iters = (int)uni((uint32_t)wave_max(nev));
-    // The 64 keys of a wave are consecutive, so their runs of the key-sorted payload form ONE
-    // contiguous byte range: the wave copies it into its LDS region with 16-B global_load_lds (all
-    // copies in flight at once, no VGPRs) and the lanes then walk their own runs out of LDS (a
-    // lane-private walk through HBM touches every line ~8x, once per iteration, and thrashes L2).
-    const uint32_t rlo = uni(wave_min_u(nev > 0 ? b : 0xffffffffu));
-    const uint32_t rhi = uni(wave_max_u(nev > 0 ? e : 0u));
-    const uint64_t c_lo = (uint64_t)rlo * SB / 16u, c_hi = ((uint64_t)rhi * SB + 15u) / 16u;
-    uint32_t dval = 0;  // this wave's p.deferred entry (written last: no store ahead of the loads)
+    // The workgroup's keys are consecutive, so their runs of the key-sorted payload form ONE
+    // contiguous byte range: the waves copy it into LDS with 16-B global_load_lds (all copies in
+    // flight at once, no VGPRs) and the lanes then walk their own runs out of LDS (a lane-private walk
+    // through HBM touches every line ~8x, once per iteration, and thrashes L2).
+    const uint64_t c_lo = (uint64_t)blo * SB / 16u, c_hi = ((uint64_t)bhi * SB + 15u) / 16u;
+    bool fits = true;
     if constexpr (STG) {
-        const bool fits = c_hi - c_lo <= (uint64_t)p.stage_chunks;
-        dval = (iters > 0 && !fits) ? 1u : 0u;
-        if (!fits) iters = 0;  // the HBM pass takes this wave
+        fits = bhi <= blo || c_hi - c_lo <= (uint64_t)p.stage_chunks * NW;
+        // this wave's p.deferred entry: 1 = the HBM pass takes the whole workgroup (its range does not
+        // fit); keys stopped early raise it to 2 after the walk (written after the barrier below)
+        if (lane == 0) p.deferred[wave_id] = (!fits && bhi > blo) ? 1u : 0u;
+        if (!fits) iters = 0;
     }
-    sg_u32x4* wst = sg_stage + (size_t)wv * p.stage_chunks;
-    const uint32_t* lds_run = (const uint32_t*)wst + ((uint64_t)rlo * SB - c_lo * 16u) / 4u;  // element rlo
+    const uint32_t* lds_run = (const uint32_t*)sg_stage + ((uint64_t)blo * SB - c_lo * 16u) / 4u;  // element blo
 
     // round trip 2: the partials of the register window, the raw-slot reservation and the LDS copy,
     // all in flight together (nothing below reads a result before the barrier)
@@ -573,6 +591,8 @@ __device__ __forceinline__ void advance(const P2Params& p) {
     bool have_next = false;
     if constexpr (S1) {
         if constexpr (BOUNDED && STG) {
+            // the wave's events + 64 R window partials bound its matches: [rlo + w*64R, ...) is disjoint
+            // from every other wave's range
             chunk_base = (unsigned long long)rlo + (unsigned long long)wave_id * (unsigned long long)(SGD_WAVE * R);
         } else if constexpr (BOUNDED) {
             const uint32_t bound = nev > 0 ? n0 + (S0 ? (uint32_t)nev : 0u) : 0u;
@@ -585,17 +605,21 @@ __device__ __forceinline__ void advance(const P2Params& p) {
                 next_l0 = p.raw_static + atomicAdd(p.raw_count, (unsigned long long)SGD_RAW_CHUNK);
         }
     }
-    if (STG && iters > 0) {
+    if (STG && fits && bhi > blo) {
         const uint32_t nch = (uint32_t)(c_hi - c_lo);
         const sg_u32x4* src = (const sg_u32x4*)p.payload + c_lo;
-        for (uint32_t c = 0; c < nch; c += SGD_WAVE)
+        for (uint32_t c = wv * SGD_WAVE; c < nch; c += SGD_BLOCK)
             if (c + (uint32_t)lane < nch)
-                __builtin_amdgcn_global_load_lds((sg_glb_ptr)(src + c + lane), (sg_lds_ptr)(wst + c), 16, 0, 0);
+                __builtin_amdgcn_global_load_lds((sg_glb_ptr)(src + c + lane), (sg_lds_ptr)(sg_stage + c), 16, 0, 0);
     }
-    if constexpr (STG) __syncthreads();  // the LDS copies have landed
+    if constexpr (STG) {
+        // every wave's LDS copies have landed (a wave reads runs other waves copied: each waits for its
+        // own global_load_lds before the barrier)
+        __builtin_amdgcn_s_waitcnt(0);
+        __syncthreads();
+    }
     if (iters == 0) {  // no key of this wave has an event here (wave-uniform), or the HBM pass has it
         if (STG && lane == 0) {
-            p.deferred[wave_id] = dval;
 #pragma unroll
             for (int i = 0; i < SGD_ST_N; ++i) p.wstats[(size_t)wave_id * SGD_ST_N + i] = 0;
         }
@@ -622,7 +646,7 @@ __device__ __forceinline__ void advance(const P2Params& p) {
     }
 
     PayEl<STRIDE> cur, nxt;
-    if (run > 0) cur = STG ? lds_pay<STRIDE>(lds_run, b - rlo) : load_pay<STRIDE>(p.payload, b);
+    if (run > 0) cur = STG ? lds_pay<STRIDE>(lds_run, b - blo) : load_pay<STRIDE>(p.payload, b);
 
 #if SGX_PROF
     uint64_t prof_acc[5] = {0, 0, 0, 0, 0};
@@ -644,7 +668,7 @@ __device__ __forceinline__ void advance(const P2Params& p) {
             }
         }
         if (it + 1 < run)  // next event in flight
-            nxt = STG ? lds_pay<STRIDE>(lds_run, b - rlo + (uint32_t)it + 1)
+            nxt = STG ? lds_pay<STRIDE>(lds_run, b - blo + (uint32_t)it + 1)
                       : load_pay<STRIDE>(p.payload, b + (uint32_t)it + 1);
         Ev ev;
         int64_t ts = 0;
@@ -662,7 +686,7 @@ __device__ __forceinline__ void advance(const P2Params& p) {
                         const int32_t tn = (int32_t)(ts - tbase), w32 = (int32_t)within;
                         const int32_t lo = tn - w32, hi = tn + w32;
 #pragma unroll
-                        for (int j = 0; j < R; ++j) X |= ((W.ts[j] < lo) | (W.ts[j] > hi) ? 1u : 0u) << j;
+                        for (int j = 0; j < R; ++j) X |= (((W.ts[j] < lo) | (W.ts[j] > hi)) ? 1u : 0u) << j;
                     } else {
 #pragma unroll
                         for (int j = 0; j < R; ++j) X |= (expired((int64_t)W.ts[j], ts, within) ? 1u : 0u) << j;
@@ -847,10 +871,9 @@ __device__ __forceinline__ void advance(const P2Params& p) {
     if (lane == 0 && p.prof)  // one row per wave (no device-wide atomics), summed by the host
         for (int i = 0; i < 5; ++i) p.prof[(size_t)wave_id * 8 + i] += prof_acc[i];
 #endif
-    if (STG && rs != SGD_NO_RESUME) p.resume[k] = rs;
-    if constexpr (STG) {
-        const unsigned long long anyr = __ballot(rs != SGD_NO_RESUME);
-        if (lane == 0) p.deferred[wave_id] = anyr ? 2u : 0u;
+    if (STG && rs != SGD_NO_RESUME) {  // the HBM pass resumes the key
+        p.resume[k] = rs;
+        p.deferred[wave_id] = 2u;
     }
     if (run > 0) {
         uint32_t np, ns;

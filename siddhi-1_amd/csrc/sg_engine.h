@@ -13,8 +13,9 @@
 #define SGD_MAX_CONST 32   // filter constants (kernel arguments, so equal-shaped queries share code)
 #define SGD_MAX_REG 16     // register window (partials per lane) upper bound
 #define SGD_WAVE 64
-#define SGD_BLOCK 128      // lanes (= keys) per workgroup of the advance kernel
-#define SGD_STAGE_MAX_BYTES 65536  // LDS per workgroup staging the waves' payload runs (upper bound)
+#define SGD_BLOCK 256      // lanes (= keys) per workgroup of the advance kernel
+#define SGD_STAGE_MAX_BYTES 147456  // LDS per workgroup staging its keys' payload runs (upper bound; the
+                                    // static LDS of the lane dealing sits beside it in the 160 KB)
 #define SGD_RAW_CHUNK 256  // raw match slots a wave reserves at a time (the raw buffer has 2 chunks of slack per wave)
 
 // ---- filters ------------------------------------------------------------------------------------

@@ -597,7 +597,7 @@ void allocate(sg_engine* e) {
     // (every (e1 -> e2)) chunks of SGD_RAW_CHUNK with two chunks of slack per wave (p2_jit.hip)
     // [0, raw_static): the staged pass's per-wave ranges (rlo + w*64R ..., p2_jit.hip); above: the
     // atomically reserved slots of the HBM pass and of `every (e1 -> e2)`
-    const uint64_t nw = (K + SGD_WAVE - 1) / SGD_WAVE;
+    const uint64_t nw = (K + SGD_BLOCK - 1) / SGD_BLOCK * (SGD_BLOCK / SGD_WAVE);  // waves of one launch
     e->raw_static = (uint64_t)B + (nw + 1) * SGD_WAVE * e->reg_slots;
     e->raw_cap = e->raw_static + std::max<uint64_t>(2 * (B + (uint64_t)K * C), M + nw * 2 * SGD_RAW_CHUNK);
     if (e->raw_cap >= (1ull << 32)) throw std::invalid_argument("n_keys x partial_capacity too large for one engine");
@@ -691,16 +691,17 @@ void launch(hipFunction_t f, uint32_t blocks, uint32_t threads, void* arg, hipSt
     HIP_OK(hipModuleLaunchKernel(f, blocks, 1, 1, threads, 1, 1, lds, stream, args, nullptr));
 }
 
-// LDS staging per advance-kernel wave, in 16-B chunks: the payload bytes of the wave's 64 keys at
-// this batch's density (n / K events per key) plus 4 standard deviations of a Poisson count, so that
-// practically every wave of a uniform key stream is staged (the rest read HBM directly, exactly);
-// a smaller region means more resident waves per CU (160 KB LDS).
+// LDS staging per advance-kernel wave, in 16-B chunks (a workgroup stages its keys' runs in one region of
+// SGD_BLOCK / 64 times this): the payload bytes of the workgroup's keys at this batch's density (n / K
+// events per key) plus 4 standard deviations of a Poisson count, so that practically every workgroup of
+// a uniform key stream is staged (the rest read HBM directly, exactly); a smaller region means more
+// resident workgroups per CU (160 KB LDS).
 uint32_t stage_chunks_for(uint64_t n, uint64_t K, uint32_t stride_words) {
     const uint32_t wpb = SGD_BLOCK / SGD_WAVE;
-    const double mean = (double)n * SGD_WAVE / (double)(K ? K : 1);
+    const double mean = (double)n * SGD_BLOCK / (double)(K ? K : 1);
     const double want = mean + 4.0 * std::sqrt(mean) + 32.0;
-    const double chunks = std::ceil(want * stride_words * 4.0 / 16.0) + 1.0;
-    const double hi = (double)SGD_STAGE_MAX_BYTES / wpb / 16.0;
+    const double chunks = std::ceil((std::ceil(want * stride_words * 4.0 / 16.0) + 1.0) / wpb);
+    const double hi = std::floor((double)SGD_STAGE_MAX_BYTES / wpb / 16.0);
     return (uint32_t)std::max(64.0, std::min(chunks, hi));
 }
 

@@ -42,6 +42,15 @@ class Event:
         self.data = list(data) if data is not None else []
         self.is_expired = is_expired
 
+    @classmethod
+    def _of(cls, timestamp, data):
+        """an output event over a list the caller hands over (no copy)"""
+        e = cls.__new__(cls)
+        e.timestamp = timestamp
+        e.data = data
+        e.is_expired = False
+        return e
+
     def getData(self, i=None):
         return self.data if i is None else self.data[i]
 
@@ -192,6 +201,12 @@ class _EventStore:
         self.rows.append((stream, ts, data))
         return len(self.rows) - 1
 
+    def add_many(self, stream, ts, datas):
+        """consecutive seqs for a chunk of events; returns the first"""
+        base = len(self.rows)
+        self.rows.extend(zip([stream] * len(ts), ts, map(tuple, datas)))
+        return base
+
     def get(self, seq):
         if int(seq) == BLANK_SEQ:
             return (None, -1, _NullRow())
@@ -217,6 +232,19 @@ class StringDictionary:
             self.ids[s] = i
             self.strs.append(s)
         return i
+
+    def ids_of(self, vals):
+        """id_of over a column (one dict probe per value; new strings numbered in first-seen order)"""
+        g = self.ids.get
+        out = [g(v) for v in vals]
+        if None in out:
+            out = [self.id_of(v) if i is None else i for v, i in zip(vals, out)]
+        return out
+
+
+def java_strings(vals):
+    """java_string over a column (strings pass through as they are)"""
+    return [v if type(v) is str else java_string(v) for v in vals]
 
 
 def java_string(v):
@@ -424,7 +452,7 @@ class _QueryRuntime:
             if cur is None or cur[0] != trig or trig == TIMER_SEQ:
                 cur = (trig, [])
                 groups.append(cur)
-            cur[1].append(Event(ts, data))
+            cur[1].append(Event._of(ts, data))
         for _, evs in groups:
             if self.cq.output_stream is not None:
                 self.app_rt._emit_stream(self.cq.output_stream, evs)
@@ -792,10 +820,26 @@ class SiddhiAppRuntime:
         for cb in self.stream_callbacks.get(name, []):
             cb.receive(events)
 
+    _NP = {"INT": np.int32, "LONG": np.int64, "FLOAT": np.float32, "DOUBLE": np.float64}
+
     def _columns(self, sd: q.StreamDef, rows):
+        """rows -> one array per attribute (+ null bytes where the chunk has nulls).  A column without
+        nulls converts in one numpy call; the per-value path below handles nulls and the checks."""
         cols, nulls = [], []
+        by_attr = list(zip(*rows)) if rows else [()] * len(sd.attrs)
         for ai, (an, at) in enumerate(sd.attrs):
-            vals = [r[ai] for r in rows]
+            vals = by_attr[ai]
+            if at in self._NP and None not in vals:
+                try:
+                    cols.append(np.array(vals, dtype=self._NP[at]))
+                    nulls.append(None)
+                    continue
+                except (TypeError, ValueError, OverflowError):
+                    pass   # mixed Python types: the exact per-value conversion below
+            if at == "STRING" and None not in vals:
+                cols.append(np.array(self.strings.ids_of(vals), dtype=np.uint32))
+                nulls.append(None)
+                continue
             isnull = np.array([v is None for v in vals], dtype=np.uint8)
             if at == "STRING":
                 arr = np.array([self.strings.id_of(v) if v is not None else 0 for v in vals], dtype=np.uint32)
@@ -854,49 +898,51 @@ class SiddhiAppRuntime:
                 self._set_event_time(events[-1][0])
         elif self.started:
             self._fire_timers(self.wall_time())
-        seqs = []
-        for ts, data in events:
-            if len(data) != len(sd.attrs):
-                raise ValueError(f"event for {stream} has {len(data)} attributes, expected {len(sd.attrs)}")
-            seqs.append(self.store.add(stream, ts, tuple(data)))
+        na = len(sd.attrs)
+        rows = [e[1] for e in events]
+        for data in rows:
+            if len(data) != na:
+                raise ValueError(f"event for {stream} has {len(data)} attributes, expected {na}")
+        ts_all = np.fromiter((e[0] for e in events), dtype=np.int64, count=len(events))
+        base = self.store.add_many(stream, ts_all.tolist(), rows)
+        cols_all = None
         for qr in self.queries:
             si = qr.cq.stream_index(stream)
             if si < 0:
                 continue
-            ts_all = np.array([e[0] for e in events], dtype=np.int64)
-            rows = [e[1] for e in events]
-            keys = None
-            keep = list(range(len(events)))
             if qr.cq.partitioned and qr.cq.partition_keys[stream] is None:
                 self._send_broadcast(qr, si, sd, events)
                 continue
-            if qr.cq.partitioned:
-                attr = qr.cq.partition_keys[stream]
-                ai = sd.attr_index(attr)
+            if cols_all is None:
+                cols_all = self._columns(sd, rows)
+            cols, nulls = cols_all
+            if not qr.cq.partitioned:
+                qr.engine.push(si, base, ts_all, cols, nulls, None)
+            else:
+                ai = sd.attr_index(qr.cq.partition_keys[stream])
                 # one batched intern per send (sg_dict); PartitionStreamReceiver drops null keys
                 try:
-                    kids = qr.key_dict.intern([java_string(r[ai]) for r in rows])
+                    kids = np.asarray(qr.key_dict.intern(java_strings([r[ai] for r in rows])), dtype=np.uint32)
                 except EngineError as ex:
                     raise RuntimeError(f"more than {qr.n_keys} partition keys") from ex
-                keep = [i for i in range(len(rows)) if kids[i] != SG_KEY_NULL]
-                keys = [int(kids[i]) for i in keep]
-                keys_str = [java_string(rows[i][ai]) for i in keep] if self._purges else []
-                for pg in self._purges:
-                    if qr in pg.queries:
-                        now = self.current_time()
-                        for k in keys_str:
-                            pg.last_seen[k] = now
-            # contiguous seq runs (events dropped for a null key split the batch)
-            start = 0
-            while start < len(keep):
-                end = start + 1
-                while end < len(keep) and keep[end] == keep[end - 1] + 1:
-                    end += 1
-                idx = keep[start:end]
-                cols, nulls = self._columns(sd, [rows[i] for i in idx])
-                kk = np.array(keys[start:end], dtype=np.uint32) if keys is not None else None
-                qr.engine.push(si, seqs[idx[0]], ts_all[idx], cols, nulls, kk)
-                start = end
+                keep = np.nonzero(kids != SG_KEY_NULL)[0]
+                if self._purges:
+                    now = self.current_time()
+                    for pg in self._purges:
+                        if qr in pg.queries:
+                            for i in keep.tolist():
+                                pg.last_seen[java_string(rows[i][ai])] = now
+                if len(keep) == len(rows):
+                    qr.engine.push(si, base, ts_all, cols, nulls, kids)
+                else:
+                    # contiguous seq runs (events dropped for a null key split the batch)
+                    cut = np.nonzero(np.diff(keep) != 1)[0] + 1
+                    for idx in np.split(keep, cut):
+                        if len(idx) == 0:
+                            continue
+                        lo, hi = int(idx[0]), int(idx[-1]) + 1
+                        qr.engine.push(si, base + lo, ts_all[lo:hi], [c[lo:hi] for c in cols],
+                                       [x[lo:hi] if x is not None else None for x in nulls], kids[lo:hi])
             m = qr.engine.poll()
             qr.dispatch(qr.project(m, self.store))
 

@@ -49,8 +49,12 @@ def main():
             eng.push(0, s * B, (B, t["ts"].data_ptr(), [t["symbol"].data_ptr(), t["price"].data_ptr(),
                                                         t["volume"].data_ptr()], t["key"].data_ptr()),
                      [0, 1, 2], mem=sa.native.SG_MEM_DEVICE)
-            m = eng.poll_device()
-            eng.release(m)
+            while True:   # a window that wraps the output ring comes in two polls
+                m = eng.poll_device()
+                n_m = int(m.n)
+                eng.release(m)
+                if n_m == 0:
+                    break
             if s == 0:
                 eng.synchronize()
                 st0 = eng.stats()
