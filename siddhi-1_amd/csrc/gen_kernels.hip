@@ -22,11 +22,20 @@
 
 namespace {
 
+// Address spaces made explicit: the per-key state and the batch columns are global memory
+// (address_space 1: global_load/store, whose waits are counted per kind, instead of flat accesses
+// that every wait must drain completely); the program tables are constant memory (address_space 4:
+// scalar loads wherever the index is wave-uniform).
+typedef __attribute__((address_space(1))) uint32_t gu32;
+typedef __attribute__((address_space(4))) const GenProgram cGenProgram;
+template <class T> __device__ __forceinline__ __attribute__((address_space(1))) T* gp(T* p) {
+    return (__attribute__((address_space(1))) T*)p;
+}
 
 struct Lane {
-    const GenProgram& G;
+    const cGenProgram& G;
     const GenArgs& A;
-    uint32_t* S;
+    gu32* S;
     uint32_t K, k;
     int64_t now;
     uint64_t trigSeq;       // seq of the event being processed (SG_TIMER_SEQ in a timer sweep)
@@ -42,21 +51,21 @@ struct Lane {
     uint32_t resLeft;
 
     __device__ Lane(const GenArgs& a, uint32_t key)
-        : G(*a.G), A(a), S(a.state), K(a.K), k(key), now(a.now), trigSeq(SG_TIMER_SEQ), trigIdx(0), trigRank(0),
+        : G(*(cGenProgram*)a.G), A(a), S(gp(a.state)), K(a.K), k(key), now(a.now), trigSeq(SG_TIMER_SEQ), trigIdx(0), trigRank(0),
           tk2(0), tk1(0), scanned(0), created(0), matches(0), err(0), resBase(0), resEnd(0), resLeft(0) {
         retm = 0;
     }
 
     // ---- HBM words of this key ----
 #if GEN_AOS
-    __device__ __forceinline__ uint32_t& W(uint32_t w) const { return S[(size_t)k * G.blockWords + w]; }
+    __device__ __forceinline__ gu32& W(uint32_t w) const { return S[(size_t)k * G.blockWords + w]; }
 #else
-    __device__ __forceinline__ uint32_t& W(uint32_t w) const { return S[(size_t)w * K + k]; }
+    __device__ __forceinline__ gu32& W(uint32_t w) const { return S[(size_t)w * K + k]; }
 #endif
-    __device__ __forceinline__ int64_t R64(uint32_t w) const {
+    __device__ __forceinline__ int64_t R64(uint32_t w) const __restrict__ {
         return (int64_t)((uint64_t)W(w) | ((uint64_t)W(w + 1) << 32));
     }
-    __device__ __forceinline__ void W64(uint32_t w, int64_t v) const {
+    __device__ __forceinline__ void W64(uint32_t w, int64_t v) const __restrict__ {
         W(w) = (uint32_t)(uint64_t)v;
         W(w + 1) = (uint32_t)((uint64_t)v >> 32);
     }
@@ -65,13 +74,13 @@ struct Lane {
     __device__ __forceinline__ uint32_t ks(int p) const { return G.offKS + (uint32_t)p * G.ksWords; }
     __device__ __forceinline__ uint32_t flags(int p) const { return W(ks(p) + KS_FLAGS); }
     __device__ __forceinline__ bool flag(int p, uint32_t f) const { return (flags(p) & f) != 0; }
-    __device__ __forceinline__ void setFlag(int p, uint32_t f, bool on) const {
-        uint32_t& x = W(ks(p) + KS_FLAGS);
+    __device__ __forceinline__ void setFlag(int p, uint32_t f, bool on) const __restrict__ {
+        gu32& x = W(ks(p) + KS_FLAGS);
         x = on ? (x | f) : (x & ~f);
     }
     // lists: which 0 = pending, 1 = newAndEvery
-    __device__ __forceinline__ uint32_t& len(int p, int which) const { return W(ks(p) + KS_PLEN + which); }
-    __device__ __forceinline__ uint32_t& at(int p, int which, uint32_t i) const {
+    __device__ __forceinline__ gu32& len(int p, int which) const { return W(ks(p) + KS_PLEN + which); }
+    __device__ __forceinline__ gu32& at(int p, int which, uint32_t i) const __restrict__ {
         return W(ks(p) + KS_LISTS + (uint32_t)which * G.L + i);
     }
 
@@ -86,7 +95,7 @@ struct Lane {
     __device__ __forceinline__ uint64_t evSeq(uint32_t e) const { return (uint64_t)R64(sew(e, SE_SEQ)); }
     __device__ __forceinline__ uint32_t evNext(uint32_t e) const { return W(sew(e, SE_NEXT)); }
 
-    __device__ uint32_t alloc(uint32_t freeOff, uint32_t cap) {
+    __device__ uint32_t alloc(uint32_t freeOff, uint32_t cap) __restrict__ {
         const uint32_t nw = (cap + 31) / 32;
         for (uint32_t w = 0; w < nw; w++) {
             uint32_t x = W(freeOff + w);
@@ -101,17 +110,17 @@ struct Lane {
         err |= GERR_CAP;
         return GEN_NIL;
     }
-    __device__ void freeBit(uint32_t freeOff, uint32_t idx) const {
-        uint32_t& x = W(freeOff + idx / 32);
+    __device__ void freeBit(uint32_t freeOff, uint32_t idx) const __restrict__ {
+        gu32& x = W(freeOff + idx / 32);
         x &= ~(1u << (idx % 32));
     }
 
-    __device__ void evIncref(uint32_t e) const {
+    __device__ void evIncref(uint32_t e) const __restrict__ {
         if (e != GEN_NIL) W(sew(e, SE_RC)) += 1;
     }
-    __device__ void evDecref(uint32_t e) {
+    __device__ void evDecref(uint32_t e) __restrict__ {
         while (e != GEN_NIL) {
-            uint32_t& rc = W(sew(e, SE_RC));
+            gu32& rc = W(sew(e, SE_RC));
             if (rc == 0) { err |= GERR_REF; return; }
             if (--rc != 0) return;
             const uint32_t nx = evNext(e);
@@ -119,7 +128,7 @@ struct Lane {
             e = nx;
         }
     }
-    __device__ uint32_t newEv(uint64_t seq, int64_t ts, uint32_t batchPos, bool blank) {
+    __device__ uint32_t newEv(uint64_t seq, int64_t ts, uint32_t batchPos, bool blank) __restrict__ {
         const uint32_t e = alloc(G.offSEfree, G.SECAP);
         if (e == GEN_NIL) return e;
         W64(sew(e, SE_SEQ), (int64_t)seq);
@@ -134,12 +143,12 @@ struct Lane {
                 uint64_t v = 0;
                 const void* c = A.b.col[a];
                 switch (G.attrType[s][a]) {
-                case SG_T_LONG: case SG_T_DOUBLE: v = ((const uint64_t*)c)[batchPos]; break;
-                case SG_T_BOOL: v = ((const uint8_t*)c)[batchPos] ? 1 : 0; break;
-                default: v = ((const uint32_t*)c)[batchPos];
+                case SG_T_LONG: case SG_T_DOUBLE: v = gp((const uint64_t*)c)[batchPos]; break;
+                case SG_T_BOOL: v = gp((const uint8_t*)c)[batchPos] ? 1 : 0; break;
+                default: v = gp((const uint32_t*)c)[batchPos];
                 }
                 W64(sew(e, SE_ATTR + 2 * (uint32_t)a), (int64_t)v);
-                if (A.b.nul[a] && A.b.nul[a][batchPos]) nb |= 1u << a;
+                if (A.b.nul[a] && gp(A.b.nul[a])[batchPos]) nb |= 1u << a;
             }
         } else {
             nb = 0xffffffffu;  // StreamEventFactory.newInstance(): no data
@@ -148,18 +157,18 @@ struct Lane {
         return e;
     }
 
-    __device__ void stIncref(uint32_t se) const {
+    __device__ void stIncref(uint32_t se) const __restrict__ {
         if (se != GEN_NIL) W(stw(se, ST_RC)) += 1;
     }
-    __device__ void stDecref(uint32_t se) {
+    __device__ void stDecref(uint32_t se) __restrict__ {
         if (se == GEN_NIL) return;
-        uint32_t& rc = W(stw(se, ST_RC));
+        gu32& rc = W(stw(se, ST_RC));
         if (rc == 0) { err |= GERR_REF; return; }
         if (--rc != 0) return;
         for (int s = 0; s < G.nslots; s++) evDecref(slot(se, s));
         freeBit(G.offSTfree, se);
     }
-    __device__ uint32_t newSt() {
+    __device__ uint32_t newSt() __restrict__ {
         const uint32_t se = alloc(G.offSTfree, G.STCAP);
         if (se == GEN_NIL) return se;
         W64(stw(se, ST_TS), -1);
@@ -168,15 +177,15 @@ struct Lane {
         for (int s = 0; s < G.nslots; s++) W(stw(se, ST_SLOTS + (uint32_t)s)) = GEN_NIL;
         return se;
     }
-    __device__ void setSlot(uint32_t se, int s, uint32_t e) {
+    __device__ void setSlot(uint32_t se, int s, uint32_t e) __restrict__ {
         evIncref(e);
-        uint32_t& w = W(stw(se, ST_SLOTS + (uint32_t)s));
+        gu32& w = W(stw(se, ST_SLOTS + (uint32_t)s));
         const uint32_t old = w;
         w = e;
         evDecref(old);
     }
     // StateEventCloner.copyStateEvent: shallow copy of the slot references (StateEventCloner.java:48-60)
-    __device__ uint32_t cloneSt(uint32_t se) {
+    __device__ uint32_t cloneSt(uint32_t se) __restrict__ {
         const uint32_t c = newSt();
         if (c == GEN_NIL) return c;
         for (int s = 0; s < G.nslots; s++) setSlot(c, s, slot(se, s));
@@ -185,7 +194,7 @@ struct Lane {
         return c;
     }
     // StateEvent.getStreamEvent(int[]) for (slot, index-in-chain) (StateEvent.java:138-182)
-    __device__ uint32_t chainAt(uint32_t se, int s, int idx) const {
+    __device__ uint32_t chainAt(uint32_t se, int s, int idx) const __restrict__ {
         uint32_t e = slot(se, s);
         if (e == GEN_NIL) return GEN_NIL;
         if (idx >= 0) {
@@ -212,14 +221,14 @@ struct Lane {
         return e;
     }
     // StateEvent.addEvent / removeLastEvent (StateEvent.java:212-236)
-    __device__ void addEvent(uint32_t se, int s, uint32_t e) {
+    __device__ void addEvent(uint32_t se, int s, uint32_t e) __restrict__ {
         uint32_t x = slot(se, s);
         if (x == GEN_NIL) { setSlot(se, s, e); return; }
         while (evNext(x) != GEN_NIL) x = evNext(x);
         evIncref(e);
         W(sew(x, SE_NEXT)) = e;
     }
-    __device__ void removeLastEvent(uint32_t se, int s) {
+    __device__ void removeLastEvent(uint32_t se, int s) __restrict__ {
         uint32_t x = slot(se, s);
         if (x == GEN_NIL) return;
         while (evNext(x) != GEN_NIL) {
@@ -235,41 +244,41 @@ struct Lane {
     }
 
     // ---- lists of StateEvents ----
-    __device__ void push(int p, int which, uint32_t se) {
-        uint32_t& n = len(p, which);
+    __device__ void push(int p, int which, uint32_t se) __restrict__ {
+        gu32& n = len(p, which);
         if (n >= G.L) { err |= GERR_CAP; return; }
         stIncref(se);
         at(p, which, n) = se;
         n++;
     }
-    __device__ void erase(int p, int which, uint32_t i) {
-        uint32_t& n = len(p, which);
+    __device__ void erase(int p, int which, uint32_t i) __restrict__ {
+        gu32& n = len(p, which);
         const uint32_t se = at(p, which, i);
         for (uint32_t j = i + 1; j < n; j++) at(p, which, j - 1) = at(p, which, j);
         n--;
         stDecref(se);
     }
-    __device__ void clearList(int p, int which) {
-        uint32_t& n = len(p, which);
+    __device__ void clearList(int p, int which) __restrict__ {
+        gu32& n = len(p, which);
         const uint32_t m = n;
         n = 0;
         for (uint32_t j = 0; j < m; j++) stDecref(at(p, which, j));
     }
-    __device__ bool removeValue(int p, int which, uint32_t se) {
+    __device__ bool removeValue(int p, int which, uint32_t se) __restrict__ {
         const uint32_t n = len(p, which);
         for (uint32_t j = 0; j < n; j++)
             if (at(p, which, j) == se) { erase(p, which, j); return true; }
         return false;
     }
     // eventTimeComparator (StreamPreStateProcessor.java:66-80): ts -1 last; List.sort is stable
-    __device__ bool tsBefore(uint32_t a, uint32_t b) const {
+    __device__ bool tsBefore(uint32_t a, uint32_t b) const __restrict__ {
         const int64_t ta = stTs(a), tb = stTs(b);
         if (ta == -1) return false;
         if (tb == -1) return true;
         return ta < tb;
     }
     // newAndEvery sorted by ts, appended to pending, cleared
-    __device__ void promote(int p) {
+    __device__ void promote(int p) __restrict__ {
         const uint32_t n = len(p, 1);
         for (uint32_t i = 1; i < n; i++) {  // stable insertion sort
             const uint32_t x = at(p, 1, i);
@@ -277,7 +286,7 @@ struct Lane {
             while (j > 0 && tsBefore(x, at(p, 1, j - 1))) { at(p, 1, j) = at(p, 1, j - 1); j--; }
             at(p, 1, j) = x;
         }
-        uint32_t& pn = len(p, 0);
+        gu32& pn = len(p, 0);
         for (uint32_t i = 0; i < n; i++) {
             if (pn >= G.L) { err |= GERR_CAP; break; }
             at(p, 0, pn++) = at(p, 1, i);  // the reference moves: no count change
@@ -287,19 +296,19 @@ struct Lane {
 
     // ---- timers (Scheduler) ----
     __device__ uint32_t qlen(int p) const { return W(ks(p) + KS_QLEN); }
-    __device__ int64_t qhead(int p) const {
+    __device__ int64_t qhead(int p) const __restrict__ {
         const uint32_t h = W(ks(p) + KS_QHEAD);
         return R64(ks(p) + KS_LISTS + 2 * G.L + 2 * h);
     }
-    __device__ void qpop(int p) const {
-        uint32_t& h = W(ks(p) + KS_QHEAD);
+    __device__ void qpop(int p) const __restrict__ {
+        gu32& h = W(ks(p) + KS_QHEAD);
         h = (h + 1) % G.Q;
         W(ks(p) + KS_QLEN) -= 1;
     }
     // this key's next timer deadline (GenTimers): the earliest queue head of its absent processors
     // (playback listener, Scheduler.java:73-104) or the earliest fire time of its running callers
     // (wall clock, Scheduler.EventCaller, Scheduler.java:238-298)
-    __device__ int64_t nextDeadline() const {
+    __device__ int64_t nextDeadline() const __restrict__ {
         int64_t best = GEN_NO_DEADLINE;
         for (int i = 0; i < G.nStartup; i++) {
             const int p = G.startup[i];
@@ -314,8 +323,8 @@ struct Lane {
         return best;
     }
 
-    __device__ void notifyAt(int p, int64_t t) {  // Scheduler.notifyAt + schedule (Scheduler.java:114-156)
-        uint32_t& n = W(ks(p) + KS_QLEN);
+    __device__ void notifyAt(int p, int64_t t) __restrict__ {  // Scheduler.notifyAt + schedule (Scheduler.java:114-156)
+        gu32& n = W(ks(p) + KS_QLEN);
         if (n >= G.Q) { err |= GERR_CAP; return; }
         const uint32_t pos = (W(ks(p) + KS_QHEAD) + n) % G.Q;
         W64(ks(p) + KS_LISTS + 2 * G.L + 2 * pos, t);
@@ -329,7 +338,7 @@ struct Lane {
 
     // ---- filters (java_ops.h: Java value semantics of the expression bytecode) ----
     // a value of the expression program: VAR reads slot s's event at chain index c (its captured attribute)
-    __device__ GVal evalv(uint32_t se, const uint32_t* code, uint32_t pc, uint32_t n) {
+    template <class CodePtr> __device__ GVal evalv(uint32_t se, CodePtr code, uint32_t pc, uint32_t n) __restrict__ {
         return jo_eval(code, pc, n, err,
                        [&](uint32_t slot, uint32_t attr, int32_t chain) -> GVal {
                            const uint32_t e = chainAt(se, (int)slot, chain);
@@ -340,14 +349,14 @@ struct Lane {
                        [&](uint32_t slot, int32_t chain) -> bool { return chainAt(se, (int)slot, chain) == GEN_NIL; });
     }
     // FilterProcessor.process: pass iff the condition is a non-null true (FilterProcessor.java:48-60)
-    __device__ bool eval(uint32_t se, uint32_t pc, uint32_t n) {
+    __device__ bool eval(uint32_t se, uint32_t pc, uint32_t n) __restrict__ {
         const GVal v = evalv(se, G.code, pc, n);
         return !v.null && (v.b & 1);
     }
 
     // QuerySelector.processNoGroupBy (QuerySelector.java:162-206) at emission: the select list over the
     // state event's slots, 3 words per item (value lo, hi, null)
-    __device__ __noinline__ void projectSelect(uint32_t se, uint32_t* pv) {
+    __device__ __noinline__ void projectSelect(uint32_t se, gu32* pv) __restrict__ {
         for (uint32_t i = 0; i < G.projN; i++) {
             const GVal v = evalv(se, G.code, G.projPc[i], G.projLen[i]);
             pv[3 * i] = (uint32_t)v.b;
@@ -357,7 +366,7 @@ struct Lane {
     }
 
     // ---- match output (QuerySelector input) ----
-    __device__ void project(uint32_t se) {
+    __device__ void project(uint32_t se) __restrict__ {
         if (resLeft == 0) {
             const uint32_t sg = blockIdx.x % A.o.nseg;  // one wave per block
             resBase = (unsigned long long)sg * A.o.seg_cap + atomicAdd(&A.o.raw_count[sg], (unsigned long long)GEN_RESCHUNK);
@@ -368,7 +377,7 @@ struct Lane {
         resLeft--;
         matches++;
         if (r >= resEnd) { err |= GERR_MATCHCAP; return; }
-        uint32_t* rec = A.o.raw + r * A.o.recWords;
+        gu32* rec = gp(A.o.raw) + r * A.o.recWords;
         const bool timer = trigSeq == SG_TIMER_SEQ;
         rec[0] = timer ? 0xfffffffeu : trigIdx;
         rec[1] = timer ? 0u : trigRank++;
@@ -378,8 +387,8 @@ struct Lane {
         rec[4] = (uint32_t)(uint64_t)ts;
         rec[5] = (uint32_t)((uint64_t)ts >> 32);
         rec[6] = k;
-        uint32_t* lens = rec + 7;
-        uint32_t* seqs = lens + G.nslots;
+        gu32* lens = rec + 7;
+        gu32* seqs = lens + G.nslots;
         for (int s = 0; s < G.nslots; s++) {
             uint32_t n = 0;
             for (uint32_t e = slot(se, s); e != GEN_NIL; e = evNext(e)) {
@@ -393,16 +402,16 @@ struct Lane {
         }
         if (G.projN) projectSelect(se, rec + G.projOff);
         if (timer) {  // (nvalid: the timers kernel adds its waves' match counts)
-            A.o.tk1[r] = tk1;
-            A.o.tk2[r] = tk2;
-            A.o.tk3[r] = k;
+            gp(A.o.tk1)[r] = tk1;
+            gp(A.o.tk2)[r] = tk2;
+            gp(A.o.tk3)[r] = k;
         } else {
-            A.o.t_cnt[trigIdx] += 1;
+            gp(A.o.t_cnt)[trigIdx] += 1;
         }
     }
 
     // ---- StreamPreStateProcessor & co (per processor p, this key) ----
-    __device__ bool isExpired(uint32_t se, int64_t t) const {  // StreamPreStateProcessor.java:118-129
+    __device__ bool isExpired(uint32_t se, int64_t t) const __restrict__ {  // StreamPreStateProcessor.java:118-129
         if (G.within == -1) return false;
         for (int i = 0; i < G.nStartIds; i++) {
             const uint32_t e = slot(se, G.startIds[i]);
@@ -414,9 +423,9 @@ struct Lane {
         return false;
     }
 
-    __device__ void init(int p) {  // StreamPreStateProcessor.java:178-194
-        const GenPre& P = G.pre[p];
-        const GenPost& Q = G.post[P.thisPost];
+    __device__ void init(int p) __restrict__ {  // StreamPreStateProcessor.java:178-194
+        const auto& P = G.pre[p];
+        const auto& Q = G.post[P.thisPost];
         if (P.isStart && (!flag(p, GF_INIT) || Q.nextEveryStatePre != GEN_NONE ||
                           (G.qtype == SG_Q_SEQUENCE && Q.nextStatePre != GEN_NONE && G.pre[Q.nextStatePre].absent))) {
             const uint32_t se = newSt();
@@ -433,13 +442,13 @@ struct Lane {
     // the continuations of processMinCountReached (its addEveryState and the reference drop) run after
     // the innermost addState returns, innermost first, as the recursive calls would.  Keeping the call
     // graph acyclic lets the compiler inline the whole processor graph (no call stack in scratch).
-    __device__ void addState(int p, uint32_t se) {
+    __device__ void addState(int p, uint32_t se) __restrict__ {
         int pend[GEN_MAXP];
         int np = 0;
         for (;;) {
             if (addStateOne(p, se)) break;
             const int q = G.pre[p].countPost;  // processMinCountReached(q, se), up to its addState
-            const GenPost& Q = G.post[q];
+            const auto& Q = G.post[q];
             if (Q.hasNext) {
                 setFlag(Q.thisPre, GF_CHANGED, true);
                 retm |= 1u << q;
@@ -451,7 +460,7 @@ struct Lane {
             p = Q.nextStatePre;
         }
         while (np > 0) {
-            const GenPost& Q = G.post[pend[--np]];
+            const auto& Q = G.post[pend[--np]];
             if (Q.nextEveryStatePre != GEN_NONE) addEveryState(Q.nextEveryStatePre, se);
             stDecref(se);
         }
@@ -459,8 +468,8 @@ struct Lane {
 
     // one StreamPre/CountPre/Logical/Absent addState; true when done, false when a count state with
     // min 0 and an empty slot forwards the partial (processMinCountReached)
-    __device__ bool addStateOne(int p, uint32_t se) {
-        const GenPre& P = G.pre[p];
+    __device__ bool addStateOne(int p, uint32_t se) __restrict__ {
+        const auto& P = G.pre[p];
         if (P.absent && flag(p, GF_INACTIVE)) return true;
         if (P.absent && P.kind == GK_STREAM) {  // AbsentStreamPreStateProcessor.java:83-103
             if (G.qtype == SG_Q_SEQUENCE) clearList(p, 1);
@@ -495,8 +504,8 @@ struct Lane {
         return !(P.kind == GK_COUNT && P.minCount == 0 && slot(se, P.stateId) == GEN_NIL);  // :129-136
     }
 
-    __device__ void addEveryState(int p, uint32_t se) {
-        const GenPre& P = G.pre[p];
+    __device__ void addEveryState(int p, uint32_t se) __restrict__ {
+        const auto& P = G.pre[p];
         const uint32_t c = cloneSt(se);
         if (c == GEN_NIL) return;
         stIncref(c);
@@ -529,14 +538,14 @@ struct Lane {
         stDecref(c);
     }
 
-    __device__ bool seqHold(int p) const {  // SEQUENCE, no every, the next state still has pending partials
-        const GenPost& Q = G.post[G.pre[p].thisPost];
+    __device__ bool seqHold(int p) const __restrict__ {  // SEQUENCE, no every, the next state still has pending partials
+        const auto& Q = G.post[G.pre[p].thisPost];
         return G.qtype == SG_Q_SEQUENCE && Q.nextEveryStatePre == GEN_NONE && Q.nextStatePre != GEN_NONE &&
                len(Q.nextStatePre, 0) != 0;
     }
 
-    __device__ void resetState(int p) {
-        const GenPre& P = G.pre[p];
+    __device__ void resetState(int p) __restrict__ {
+        const auto& P = G.pre[p];
         if (P.kind == GK_LOGICAL) {  // LogicalPreStateProcessor.java:86-108
             if (P.logicalType == SG_L_OR || len(p, 0) == len(P.partner, 0)) {
                 clearList(p, 0);
@@ -555,8 +564,8 @@ struct Lane {
         }
     }
 
-    __device__ void updateState(int p) {
-        const GenPre& P = G.pre[p];
+    __device__ void updateState(int p) __restrict__ {
+        const auto& P = G.pre[p];
         if (P.kind == GK_COUNT && flag(p, GF_SSRESET)) {  // CountPreStateProcessor.java:168-180
             setFlag(p, GF_SSRESET, false);
             init(p);
@@ -565,10 +574,13 @@ struct Lane {
         if (P.kind == GK_LOGICAL) promote(P.partner);  // LogicalPreStateProcessor.java:110-122
     }
 
-    __device__ void expireEvents(int p, int64_t t) {  // StreamPreStateProcessor.java:325-361
+    // One pass per list: the expired entries are dropped (their references released in list order, as
+    // the reference's iterator.remove() calls do) and the survivors moved down once (no per-erase shift).
+    __device__ void expireEvents(int p, int64_t t) __restrict__ {  // StreamPreStateProcessor.java:325-361
         uint32_t expired = GEN_NIL;
+        const uint32_t n0 = len(p, 0);
         uint32_t i = 0;
-        while (i < len(p, 0)) {
+        for (; i < n0; i++) {  // a prefix of the pending list (:331-343)
             const uint32_t se = at(p, 0, i);
             if (!isExpired(se, t)) break;
             if (W(stw(se, ST_TYPE)) != 1) {
@@ -577,10 +589,15 @@ struct Lane {
                 stDecref(expired);
                 expired = se;
             }
-            erase(p, 0, i);
+            stDecref(se);
         }
-        i = 0;
-        while (i < len(p, 1)) {
+        if (i > 0) {
+            for (uint32_t j = i; j < n0; j++) at(p, 0, j - i) = at(p, 0, j);
+            len(p, 0) = n0 - i;
+        }
+        const uint32_t n1 = len(p, 1);
+        uint32_t w = 0;
+        for (i = 0; i < n1; i++) {  // any entry of newAndEvery (:345-357)
             const uint32_t se = at(p, 1, i);
             if (isExpired(se, t)) {
                 if (W(stw(se, ST_TYPE)) != 1) {
@@ -589,11 +606,13 @@ struct Lane {
                     stDecref(expired);
                     expired = se;
                 }
-                erase(p, 1, i);
+                stDecref(se);
             } else {
-                i++;
+                if (w != i) at(p, 1, w) = se;
+                w++;
             }
         }
+        if (w != n1) len(p, 1) = w;
         const int we = G.pre[p].withinEvery;
         if (expired != GEN_NIL && we != GEN_NONE) {
             addEveryState(we, expired);
@@ -602,25 +621,25 @@ struct Lane {
         stDecref(expired);
     }
 
-    __device__ void startStateReset(int p) {  // CountPreStateProcessor.java:155-166
+    __device__ void startStateReset(int p) __restrict__ {  // CountPreStateProcessor.java:155-166
         for (int depth = 0; depth < 2 * GEN_MAXP; depth++) {
             setFlag(p, GF_SSRESET, true);
-            const GenPre& P = G.pre[p];
+            const auto& P = G.pre[p];
             if (G.post[P.thisPost].callbackPre == GEN_NONE) return;
             p = G.post[P.countPost].thisPre;
         }
         err |= GERR_REF;  // the reference overflows its stack here
     }
 
-    __device__ void runChain(int p, uint32_t se) {  // StreamPreStateProcessor.process(StateEvent) :131-142
+    __device__ void runChain(int p, uint32_t se) __restrict__ {  // StreamPreStateProcessor.process(StateEvent) :131-142
         setFlag(p, GF_CHANGED, false);
-        const GenPre& P = G.pre[p];
+        const auto& P = G.pre[p];
         if (P.flen == 0 || eval(se, P.fpc, P.flen)) postProcess(P.thisPost, se);
     }
 
     // ---- post processors ----
-    __device__ void streamProcess(int q, uint32_t se) {  // StreamPostStateProcessor.java:64-83
-        const GenPost& Q = G.post[q];
+    __device__ void streamProcess(int q, uint32_t se) __restrict__ {  // StreamPostStateProcessor.java:64-83
+        const auto& Q = G.post[q];
         setFlag(Q.thisPre, GF_CHANGED, true);
         setStTs(se, evTs(slot(se, Q.stateId)));
         if (Q.hasNext) retm |= 1u << q;
@@ -630,8 +649,8 @@ struct Lane {
         if (Q.callbackPre != GEN_NONE) startStateReset(Q.callbackPre);
         stDecref(se);
     }
-    __device__ void processMinCountReached(int q, uint32_t se) {  // CountPostStateProcessor.java:68-80
-        const GenPost& Q = G.post[q];
+    __device__ void processMinCountReached(int q, uint32_t se) __restrict__ {  // CountPostStateProcessor.java:68-80
+        const auto& Q = G.post[q];
         if (Q.hasNext) {
             setFlag(Q.thisPre, GF_CHANGED, true);
             retm |= 1u << q;
@@ -641,8 +660,8 @@ struct Lane {
         if (Q.nextEveryStatePre != GEN_NONE) addEveryState(Q.nextEveryStatePre, se);
         stDecref(se);
     }
-    __device__ void postProcess(int q, uint32_t se) {
-        const GenPost& Q = G.post[q];
+    __device__ void postProcess(int q, uint32_t se) __restrict__ {
+        const auto& Q = G.post[q];
         if (Q.absent) {  // Absent{Stream,Logical}PostStateProcessor
             const uint32_t ev = slot(se, Q.stateId);
             setFlag(Q.thisPre, GF_CHANGED, true);
@@ -675,7 +694,7 @@ struct Lane {
         }
         if (Q.kind == GK_LOGICAL) {  // LogicalPostStateProcessor.java:59-83
             if (Q.logicalType == SG_L_AND) {
-                const GenPre& PP = G.pre[Q.partnerPre];
+                const auto& PP = G.pre[Q.partnerPre];
                 const bool go = PP.absent ? partnerCanProceed(Q.partnerPre, se) : slot(se, PP.stateId) != GEN_NIL;
                 if (go) streamProcess(q, se);
                 else setFlag(Q.thisPre, GF_CHANGED, true);
@@ -689,7 +708,7 @@ struct Lane {
     }
 
     // ---- absent states ----
-    __device__ void updateLastArrivalTime(int p, int64_t ts) {
+    __device__ void updateLastArrivalTime(int p, int64_t ts) __restrict__ {
         if (G.pre[p].kind == GK_LOGICAL) {  // AbsentLogicalPreStateProcessor.java:65-74
             W64(ks(p) + KS_LAT, ts);
             return;
@@ -698,18 +717,18 @@ struct Lane {
         W64(ks(p) + KS_LST, t);
         notifyAt(p, t);
     }
-    __device__ void partitionCreated(int p) {  // AbsentStreamPreStateProcessor.java:290-308 (+ logical)
+    __device__ void partitionCreated(int p) __restrict__ {  // AbsentStreamPreStateProcessor.java:290-308 (+ logical)
         if (flag(p, GF_STARTED)) return;
         setFlag(p, GF_STARTED, true);
-        const GenPre& P = G.pre[p];
+        const auto& P = G.pre[p];
         if (P.isStart && P.waiting != -1 && !flag(p, GF_INACTIVE)) {
             if (P.kind == GK_STREAM) W64(ks(p) + KS_LST, now + P.waiting);
             notifyAt(p, now + P.waiting);
         }
     }
-    __device__ bool partnerCanProceed(int p, uint32_t se) {  // AbsentLogicalPreStateProcessor.java:391-422
-        const GenPre& P = G.pre[p];
-        const GenPost& Q = G.post[P.thisPost];
+    __device__ bool partnerCanProceed(int p, uint32_t se) __restrict__ {  // AbsentLogicalPreStateProcessor.java:391-422
+        const auto& P = G.pre[p];
+        const auto& Q = G.post[P.thisPost];
         const int64_t lat = R64(ks(p) + KS_LAT);
         if (G.qtype == SG_Q_SEQUENCE && Q.nextEveryStatePre == GEN_NONE && lat > 0) return false;
         if (P.waiting == -1) {
@@ -723,9 +742,9 @@ struct Lane {
         }
         return slot(se, P.stateId) != GEN_NIL;
     }
-    __device__ void sendAbsentEvent(int p, uint32_t se) {  // Absent*PreStateProcessor.sendEvent
-        const GenPre& P = G.pre[p];
-        const GenPost& Q = G.post[P.thisPost];
+    __device__ void sendAbsentEvent(int p, uint32_t se) __restrict__ {  // Absent*PreStateProcessor.sendEvent
+        const auto& P = G.pre[p];
+        const auto& Q = G.post[P.thisPost];
         if (Q.hasNext) project(se);
         if (Q.nextStatePre != GEN_NONE) addState(Q.nextStatePre, se);
         if (Q.nextEveryStatePre != GEN_NONE) {
@@ -739,9 +758,9 @@ struct Lane {
     }
 
     // the TIMER event of processor p for this key at currentTime (Absent*PreStateProcessor.process)
-    __device__ void processTimer(int p, int64_t currentTime) {
-        const GenPre& P = G.pre[p];
-        const GenPost& Q = G.post[P.thisPost];
+    __device__ void processTimer(int p, int64_t currentTime) __restrict__ {
+        const auto& P = G.pre[p];
+        const auto& Q = G.post[P.thisPost];
         if (flag(p, GF_INACTIVE)) return;
         uint32_t rl[64];
         uint32_t nr = 0;
@@ -856,7 +875,7 @@ struct Lane {
     }
 
     // Scheduler.sendTimerEvents (Scheduler.java:172-210)
-    __device__ void sendTimerEvents(int p) {
+    __device__ void sendTimerEvents(int p) __restrict__ {
         for (int guard = 0; guard < (1 << 20); guard++) {
             if (qlen(p) == 0) return;
             const int64_t t = qhead(p);
@@ -868,9 +887,9 @@ struct Lane {
     }
 
     // ---- processAndReturn ----
-    __device__ void processAndReturnAbsentLogical(int p, uint64_t seq, int64_t ts, uint32_t pos) {
-        const GenPre& P = G.pre[p];
-        const GenPost& Q = G.post[P.thisPost];
+    __device__ void processAndReturnAbsentLogical(int p, uint64_t seq, int64_t ts, uint32_t pos) __restrict__ {
+        const auto& P = G.pre[p];
+        const auto& Q = G.post[P.thisPost];
         uint32_t i = 0;
         while (i < len(p, 0)) {
             const uint32_t se = at(p, 0, i);
@@ -911,8 +930,8 @@ struct Lane {
     // matches returned to the receiver are appended to `outList` (state event refs held)
     // (outList holds at most OUTCAP entries)
     static constexpr uint32_t OUTCAP = 64;
-    __device__ void processAndReturn(int p, uint64_t seq, int64_t ts, uint32_t pos, uint32_t* outList, uint32_t& nOut) {
-        const GenPre& P = G.pre[p];
+    __device__ void processAndReturn(int p, uint64_t seq, int64_t ts, uint32_t pos, uint32_t* outList, uint32_t& nOut) __restrict__ {
+        const auto& P = G.pre[p];
         if (P.absent) {
             if (flag(p, GF_INACTIVE)) return;
             if (P.kind == GK_LOGICAL) { processAndReturnAbsentLogical(p, seq, ts, pos); return; }
@@ -923,14 +942,19 @@ struct Lane {
         // to (only count chains and absent-logical slots are), so one reference-counted copy per
         // (event, processor) is indistinguishable and saves a record write per partial.
         uint32_t shared = GEN_NIL;
-        uint32_t i = 0;
-        while (i < len(p, 0)) {
+        // one pass over the pending list: a dropped entry's reference is released where the reference's
+        // iterator.remove() runs, the survivors move down once (nothing else touches this list meanwhile:
+        // the processors the chain reaches append to newAndEvery lists only)
+        const uint32_t n0 = len(p, 0);
+        uint32_t w = 0;
+        for (uint32_t i = 0; i < n0; i++) {
             const uint32_t se = at(p, 0, i);
             scanned++;
+            bool removed = false;
             if (P.kind == GK_COUNT) {  // CountPreStateProcessor.java:53-95
                 if ((G.nslots > P.stateId + 1 && slot(se, P.stateId + 1) != GEN_NIL) ||
                     (G.nslots > P.stateId + 2 && slot(se, P.stateId + 2) != GEN_NIL)) {
-                    erase(p, 0, i);
+                    stDecref(se);
                     continue;
                 }
                 stIncref(se);
@@ -942,18 +966,17 @@ struct Lane {
                     retm &= ~(1u << P.thisLast);
                     if (nOut < OUTCAP) { stIncref(se); outList[nOut++] = se; } else err |= GERR_CAP;
                 }
-                bool removed = false;
-                if (flag(p, GF_CHANGED)) { erase(p, 0, i); removed = true; }
+                if (flag(p, GF_CHANGED)) { stDecref(se); removed = true; }
                 if (!flag(p, GF_SUCCESS)) {
                     removeLastEvent(se, P.stateId);
-                    if (G.qtype == SG_Q_SEQUENCE && !removed) { erase(p, 0, i); removed = true; }
+                    if (G.qtype == SG_Q_SEQUENCE && !removed) { stDecref(se); removed = true; }
                 }
                 stDecref(se);
-                if (!removed) i++;
+                if (!removed) { if (w != i) at(p, 0, w) = se; w++; }
                 continue;
             }
             if (P.kind == GK_LOGICAL && P.logicalType == SG_L_OR && slot(se, G.pre[P.partner].stateId) != GEN_NIL) {
-                erase(p, 0, i);  // LogicalPreStateProcessor.java:153-157
+                stDecref(se);  // LogicalPreStateProcessor.java:153-157
                 continue;
             }
             // StreamPreStateProcessor.java:371-397
@@ -968,21 +991,21 @@ struct Lane {
                 retm &= ~(1u << P.thisLast);
                 if (nOut < OUTCAP) { stIncref(se); outList[nOut++] = se; } else err |= GERR_CAP;
             }
-            bool removed = false;
             if (flag(p, GF_CHANGED)) {
-                erase(p, 0, i);
+                stDecref(se);
                 removed = true;
             } else {
                 setSlot(se, P.stateId, GEN_NIL);
                 if (G.qtype == SG_Q_SEQUENCE) {
-                    if (!(P.kind == GK_STREAM && P.absent)) { erase(p, 0, i); removed = true; }
+                    if (!(P.kind == GK_STREAM && P.absent)) { stDecref(se); removed = true; }
                     if (P.kind == GK_STREAM && G.post[P.thisPost].callbackPre != GEN_NONE)
                         startStateReset(G.post[P.thisPost].callbackPre);
                 }
             }
             stDecref(se);
-            if (!removed) i++;
+            if (!removed) { if (w != i) at(p, 0, w) = se; w++; }
         }
+        if (w != n0) len(p, 0) = w;
         evDecref(shared);
         if (P.absent) {  // AbsentStreamPreStateProcessor.processAndReturn returns nothing (:265-283)
             for (uint32_t j = out0; j < nOut; j++) stDecref(outList[j]);
@@ -991,7 +1014,7 @@ struct Lane {
     }
 
     // ---- receivers ----
-    __device__ void stabilize(const GenRecv& r, int64_t ts) {
+    __device__ void stabilize(const __attribute__((address_space(4))) GenRecv& r, int64_t ts) __restrict__ {
         for (int i = 0; i < G.nAll; i++) expireEvents(G.allProcs[i], ts);
         if (G.qtype == SG_Q_SEQUENCE) {  // Sequence*ProcessStreamReceiver.stabilizeStates -> resetAndUpdate
             for (int i = 0; i < G.nReset; i++) resetState(G.resetOrder[i]);
@@ -1003,7 +1026,7 @@ struct Lane {
         }
     }
 
-    __device__ void initKey() {  // PartitionRuntimeImpl.initPartition -> StateStreamRuntime.initPartition
+    __device__ void initKey() __restrict__ {  // PartitionRuntimeImpl.initPartition -> StateStreamRuntime.initPartition
         if (W(0) & 1u) return;
         W(0) |= 1u;
         for (int i = 0; i < G.nInit; i++) init(G.initOrder[i]);
@@ -1013,11 +1036,11 @@ struct Lane {
     __device__ uint32_t defBase() const { return G.offDef; }
 
     // one event of this key (MultiProcessStreamReceiver / SingleProcessStreamReceiver semantics)
-    __device__ void processEvent(const GenRecv& r, uint32_t pos, bool chunkEnd) {
+    __device__ void processEvent(const __attribute__((address_space(4))) GenRecv& r, uint32_t pos, bool chunkEnd) __restrict__ {
         const uint64_t seq = A.b.seq_base + pos;
-        const int64_t ts = A.b.ts[pos];
+        const int64_t ts = gp(A.b.ts)[pos];
         stabilize(r, ts);
-        uint32_t& nd = W(defBase());
+        gu32& nd = W(defBase());
         if (r.multi) {
             trigSeq = seq;
             trigIdx = pos;
@@ -1042,8 +1065,8 @@ struct Lane {
             if (chunkEnd) flushDeferred();
         }
     }
-    __device__ void flushDeferred() {
-        uint32_t& nd = W(defBase());
+    __device__ void flushDeferred() __restrict__ {
+        gu32& nd = W(defBase());
         uint32_t lastPos = 0xffffffffu;
         for (uint32_t x = 0; x < nd; x++) {
             const uint32_t se = W(defBase() + 1 + 2 * x), pos = W(defBase() + 2 + 2 * x);
@@ -1091,15 +1114,15 @@ extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per
     const uint32_t key = blockIdx.x * blockDim.x + threadIdx.x;
     unsigned long long sc = 0, cr = 0, ma = 0, ky = 0;
     uint32_t er = 0;
-    if (key < a.K && a.b.seg_begin[key] < a.b.seg_end[key]) {
-        const uint32_t b = a.b.seg_begin[key], e = a.b.seg_end[key];
+    if (key < a.K && gp(a.b.seg_begin)[key] < gp(a.b.seg_end)[key]) {
+        const uint32_t b = gp(a.b.seg_begin)[key], e = gp(a.b.seg_end)[key];
         Lane L(a, key);
         L.initKey();
-        const GenRecv& r = a.G->recv[a.b.stream];
+        const auto& r = L.G.recv[a.b.stream];
         if (r.n > 0) {
             for (uint32_t j = b; j < e; j++) {
-                const uint32_t pos = a.b.sidx ? a.b.sidx[j] : j;
-                const uint32_t nxt = (j + 1 < e) ? (a.b.sidx ? a.b.sidx[j + 1] : j + 1) : 0xffffffffu;
+                const uint32_t pos = a.b.sidx ? gp(a.b.sidx)[j] : j;
+                const uint32_t nxt = (j + 1 < e) ? (a.b.sidx ? gp(a.b.sidx)[j + 1] : j + 1) : 0xffffffffu;
                 L.processEvent(r, pos, nxt != pos + 1);
             }
         }
@@ -1107,11 +1130,11 @@ extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per
         for (uint32_t x = 0; x < L.resLeft; x++) {
             const unsigned long long rr = L.resBase + x;
             if (rr < L.resEnd) {
-                a.o.raw[rr * a.o.recWords] = 0xffffffffu;
-                a.o.tk1[rr] = 0xffffffffu;  // sorts after every real timer match
+                gp(a.o.raw)[rr * a.o.recWords] = 0xffffffffu;
+                gp(a.o.tk1)[rr] = 0xffffffffu;  // sorts after every real timer match
             }
         }
-        if (a.G->nStartup > 0) a.t.nd[key] = L.nextDeadline();
+        if (a.G->nStartup > 0) gp(a.t.nd)[key] = L.nextDeadline();
         er = L.err;
         sc = L.scanned;
         cr = L.created;
@@ -1130,7 +1153,7 @@ __device__ __forceinline__ unsigned long long gen_ord64(int64_t t) { return (uns
 __device__ void gen_timers_key(const GenArgs& a, uint32_t key, uint64_t di, unsigned long long& sc,
                                unsigned long long& cr, unsigned long long& ma, uint32_t& er) {
     Lane L(a, key);
-    const GenProgram& G = *a.G;
+    const cGenProgram& G = *(cGenProgram*)a.G;
     if (!(L.W(0) & 1u)) {
         if (G.partitioned) {  // a key is created by its first event (not due: nd had no deadline)
             if (G.playback)
@@ -1199,8 +1222,8 @@ __device__ void gen_timers_key(const GenArgs& a, uint32_t key, uint64_t di, unsi
     for (uint32_t x = 0; x < L.resLeft; x++) {
         const unsigned long long rr = L.resBase + x;
         if (rr < L.resEnd) {
-            a.o.raw[rr * a.o.recWords] = 0xffffffffu;
-            a.o.tk1[rr] = 0xffffffffu;  // sorts after every real timer match
+            gp(a.o.raw)[rr * a.o.recWords] = 0xffffffffu;
+            gp(a.o.tk1)[rr] = 0xffffffffu;  // sorts after every real timer match
         }
     }
 }

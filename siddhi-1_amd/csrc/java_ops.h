@@ -131,8 +131,8 @@ __device__ __forceinline__ bool jo_compare(int op, int dom, GVal l, GVal r) {
 // evnull(slot, chain) -> bool (`e1 is null`).  The two top entries live in registers (t0 = top, t1 =
 // below it); deeper ones in stk[] (stk[i] = entry i from the bottom), touched only by programs deeper
 // than two.  Malformed code sets err bit 32 (GERR_REF) / 1 (stack too deep) and yields null.
-template <class VarFn, class EvNullFn>
-__device__ __forceinline__ GVal jo_eval(const uint32_t* code, uint32_t pc, uint32_t n, uint32_t& err, VarFn var,
+template <class CodePtr, class VarFn, class EvNullFn>
+__device__ __forceinline__ GVal jo_eval(CodePtr code, uint32_t pc, uint32_t n, uint32_t& err, VarFn var,
                                         EvNullFn evnull) {
     GVal stk[24];
     GVal t0{0, true}, t1{0, true};
