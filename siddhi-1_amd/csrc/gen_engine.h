@@ -16,14 +16,18 @@
 
 #include <stdint.h>
 
-// Per-key state layout.  GEN_AOS = 0: word w of key k at w * K + k (adjacent lanes = adjacent keys, a
-// converged wave's access to one field is one coalesced transaction); GEN_AOS = 1: each key's block is
-// contiguous (a lane's repeated accesses to its own key's header, lists and records share cache lines).
-#ifndef GEN_AOS
-#define GEN_AOS 0
+// Per-key state layout.  GEN_SPLIT = 0 (shipped): every word interleaved across keys, word w of key k at
+// w * K + k, so a converged wave's access to one field is one coalesced transaction.  GEN_SPLIT = 1: the
+// KeyState records (words [0, split), split = offST) interleaved, the StateEvent / StreamEvent pools and
+// the deferred list contiguous per key (a record's words share cache lines).  Measured on C3_min1 / C4 /
+// C4_deep: the split layout runs 0.69x / 0.73x / 0.78x — the kernel is bound by memory transactions, and
+// per-key records turn each wave access into 64 of them.
+#ifndef GEN_SPLIT
+#define GEN_SPLIT 0
 #endif
-__host__ __device__ inline size_t gen_at(uint32_t K, uint32_t blockWords, uint32_t k, uint32_t w) {
-    return GEN_AOS ? (size_t)k * blockWords + w : (size_t)w * K + k;
+__host__ __device__ inline size_t gen_at(uint32_t K, uint32_t blockWords, uint32_t split, uint32_t k, uint32_t w) {
+    if (!GEN_SPLIT || w < split) return (size_t)w * K + k;
+    return (size_t)split * K + (size_t)k * (blockWords - split) + (w - split);
 }
 
 #define GEN_MAXP 16      // processors per query

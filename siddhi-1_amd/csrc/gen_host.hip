@@ -456,11 +456,11 @@ __global__ void k_gen_live(const GenProgram* G, const uint32_t* S, uint32_t K, u
     for (int p = 0; p < G->nprocs; p++) {
         const uint32_t ks = G->offKS + (uint32_t)p * G->ksWords;
         for (int which = 0; which < 2; which++) {
-            const uint32_t n = S[gen_at(K, G->blockWords, k, ks + KS_PLEN + which)];
+            const uint32_t n = S[gen_at(K, G->blockWords, G->offST, k, ks + KS_PLEN + which)];
             for (uint32_t i = 0; i < n; i++) {
-                const uint32_t se = S[gen_at(K, G->blockWords, k, ks + KS_LISTS + which * G->L + i)];
+                const uint32_t se = S[gen_at(K, G->blockWords, G->offST, k, ks + KS_LISTS + which * G->L + i)];
                 for (int s = 0; s < G->nslots; s++)
-                    if (S[gen_at(K, G->blockWords, k, G->offST + se * G->stWords + ST_SLOTS + s)] != GEN_NIL) {
+                    if (S[gen_at(K, G->blockWords, G->offST, k, G->offST + se * G->stWords + ST_SLOTS + s)] != GEN_NIL) {
                         live++;
                         break;
                     }
@@ -1034,13 +1034,13 @@ void gen_synchronize(GenEngine* e) { GH_OK(hipStreamSynchronize(e->stream)); }
 // pools and the timer queues live in the key-interleaved state blocks, so the image is the blocks plus
 // the engine clock.  Emitted matches are output, not state: both calls require that none are waiting
 // to be polled (the reference delivers callbacks before a snapshot completes).
-// one thread per (listed key, block word): word w of key k lives at gen_at(K, words, k, w)
+// one thread per (listed key, block word): word w of key k lives at gen_at(K, words, split, k, w)
 __global__ void __launch_bounds__(256) k_gen_reset(const uint32_t* __restrict__ keys, uint32_t n, uint32_t words,
-                                                   uint32_t K, uint32_t* __restrict__ state) {
+                                                   uint32_t split, uint32_t K, uint32_t* __restrict__ state) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (uint64_t)n * words) return;
     const uint32_t w = (uint32_t)(i / n), k = keys[i % n];
-    if (k < K) state[gen_at(K, words, k, w)] = 0u;  // ids were range-checked by sg_reset_keys; never write outside
+    if (k < K) state[gen_at(K, words, split, k, w)] = 0u;  // ids were range-checked by sg_reset_keys; never write outside
 }
 
 int gen_reset_keys(GenEngine* e, const uint32_t* keys, uint32_t n, std::string& msg) {
@@ -1048,7 +1048,7 @@ int gen_reset_keys(GenEngine* e, const uint32_t* keys, uint32_t n, std::string& 
     if (n == 0 || !e->host.partitioned) return SG_OK;
     const uint64_t total = (uint64_t)n * e->host.blockWords;
     hipLaunchKernelGGL(k_gen_reset, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, e->stream, keys, n,
-                       (uint32_t)e->host.blockWords, e->K, e->state);
+                       (uint32_t)e->host.blockWords, (uint32_t)e->host.offST, e->K, e->state);
     if (e->tm.nd)
         hipLaunchKernelGGL(k_gen_nd_reset, dim3((n + 255) / 256), dim3(256), 0, e->stream, keys, n, e->K, e->tm.nd);
     GH_OK(hipGetLastError());

@@ -36,6 +36,8 @@ struct Lane {
     const cGenProgram& G;
     const GenArgs& A;
     gu32* S;
+    gu32* pool;             // this key's pool words (gen_at)
+    uint32_t split;
     uint32_t K, k;
     int64_t now;
     uint64_t trigSeq;       // seq of the event being processed (SG_TIMER_SEQ in a timer sweep)
@@ -54,14 +56,16 @@ struct Lane {
         : G(*(cGenProgram*)a.G), A(a), S(gp(a.state)), K(a.K), k(key), now(a.now), trigSeq(SG_TIMER_SEQ), trigIdx(0), trigRank(0),
           tk2(0), tk1(0), scanned(0), created(0), matches(0), err(0), resBase(0), resEnd(0), resLeft(0) {
         retm = 0;
+        split = G.offST;
+        pool = S + (size_t)split * K + (size_t)k * (G.blockWords - split);
     }
 
     // ---- HBM words of this key ----
-#if GEN_AOS
-    __device__ __forceinline__ gu32& W(uint32_t w) const { return S[(size_t)k * G.blockWords + w]; }
-#else
-    __device__ __forceinline__ gu32& W(uint32_t w) const { return S[(size_t)w * K + k]; }
-#endif
+    // (gen_engine.h gen_at: KeyState words interleaved across keys, pool words contiguous per key)
+    __device__ __forceinline__ gu32& W(uint32_t w) const {
+        if (!GEN_SPLIT || w < split) return S[(size_t)w * K + k];
+        return pool[w - split];
+    }
     __device__ __forceinline__ int64_t R64(uint32_t w) const __restrict__ {
         return (int64_t)((uint64_t)W(w) | ((uint64_t)W(w + 1) << 32));
     }
@@ -1104,12 +1108,16 @@ __device__ void gen_wave_stats(const GenArgs& a, unsigned long long sc, unsigned
 // ------------------------------------------------------------------------------------------------
 // batch: one lane per key walks its key-sorted events
 // ------------------------------------------------------------------------------------------------
-// Occupancy: 6 waves/SIMD (80 VGPRs, some spilled to scratch) measured best for this latency-bound
-// kernel on C3/C4 (3 waves: C3 1.03e9 events/s, 5: 1.19e9, 6: 1.27e9; 8 waves spills 129 VGPRs).
+// Occupancy: GEN_WAVES waves/SIMD (above) for this latency-bound kernel.
 // The arguments live in device memory (written by the host before the launch): the lanes hold a
 // reference to them, and a reference to a by-value kernel argument would force a private copy of the
 // whole struct into every lane's scratch.
-extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6, 8))) k_gen_batch(const GenArgs* __restrict__ ap) {
+// occupancy (waves per SIMD): measured C3_min1 / C4 / C4_deep at 2, 3, 4, 6, 8: 4 best (fewer spills
+// at 128 VGPRs outweigh the waves lost)
+#ifndef GEN_WAVES
+#define GEN_WAVES 4
+#endif
+extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GEN_WAVES, 8))) k_gen_batch(const GenArgs* __restrict__ ap) {
     const GenArgs& a = *ap;
     const uint32_t key = blockIdx.x * blockDim.x + threadIdx.x;
     unsigned long long sc = 0, cr = 0, ma = 0, ky = 0;
@@ -1266,7 +1274,7 @@ extern "C" __global__ void __launch_bounds__(256) k_gen_collapse(const unsigned 
 }
 
 // timer sweep over the due keys (every key when unpartitioned: key 0, seeded at start())
-extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6, 8))) k_gen_timers(const GenArgs* __restrict__ ap) {
+extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GEN_WAVES, 8))) k_gen_timers(const GenArgs* __restrict__ ap) {
     const GenArgs& a = *ap;
     const uint64_t n = a.G->partitioned ? *a.t.ndue : 1ull;
     unsigned long long sc = 0, cr = 0, ma = 0;
