@@ -131,6 +131,10 @@ template <class A, class B> struct SgSel<false, A, B> { typedef B type; };
 #ifndef SGX_MAX_IT
 #define SGX_MAX_IT 0x7fffffff
 #endif
+// SGX_GLB_WALK=1: the staged pass walks the payload in HBM (one element ahead) instead of LDS
+#ifndef SGX_GLB_WALK
+#define SGX_GLB_WALK 0
+#endif
 // SGX_PROF=1: s_memtime per walk phase, summed per wave into p.prof (tools/exp_c2.py prints it)
 #ifndef SGX_PROF
 #define SGX_PROF 0
@@ -518,7 +522,7 @@ __device__ __forceinline__ void advance(const P2Params& p) {
     const uint64_t c_lo = (uint64_t)blo * SB / 16u, c_hi = ((uint64_t)bhi * SB + 15u) / 16u;
     bool fits = true;
     if constexpr (STG) {
-        fits = bhi <= blo || c_hi - c_lo <= (uint64_t)p.stage_chunks * NW;
+        fits = SGX_GLB_WALK || bhi <= blo || c_hi - c_lo <= (uint64_t)p.stage_chunks * NW;
         // this wave's p.deferred entry: 1 = the HBM pass takes the whole workgroup (its range does not
         // fit); keys stopped early raise it to 2 after the walk (written after the barrier below)
         if (lane == 0) p.deferred[wave_id] = (!fits && bhi > blo) ? 1u : 0u;
@@ -605,7 +609,7 @@ __device__ __forceinline__ void advance(const P2Params& p) {
                 next_l0 = p.raw_static + atomicAdd(p.raw_count, (unsigned long long)SGD_RAW_CHUNK);
         }
     }
-    if (STG && fits && bhi > blo) {
+    if (!SGX_GLB_WALK && STG && fits && bhi > blo) {
         const uint32_t nch = (uint32_t)(c_hi - c_lo);
         const sg_u32x4* src = (const sg_u32x4*)p.payload + c_lo;
         for (uint32_t c = wv * SGD_WAVE; c < nch; c += SGD_BLOCK)
@@ -646,7 +650,7 @@ __device__ __forceinline__ void advance(const P2Params& p) {
     }
 
     PayEl<STRIDE> cur, nxt;
-    if (run > 0) cur = STG ? lds_pay<STRIDE>(lds_run, b - blo) : load_pay<STRIDE>(p.payload, b);
+    if (run > 0) cur = (STG && !SGX_GLB_WALK) ? lds_pay<STRIDE>(lds_run, b - blo) : load_pay<STRIDE>(p.payload, b);
 
 #if SGX_PROF
     uint64_t prof_acc[5] = {0, 0, 0, 0, 0};
@@ -668,7 +672,7 @@ __device__ __forceinline__ void advance(const P2Params& p) {
             }
         }
         if (it + 1 < run)  // next event in flight
-            nxt = STG ? lds_pay<STRIDE>(lds_run, b - blo + (uint32_t)it + 1)
+            nxt = (STG && !SGX_GLB_WALK) ? lds_pay<STRIDE>(lds_run, b - blo + (uint32_t)it + 1)
                       : load_pay<STRIDE>(p.payload, b + (uint32_t)it + 1);
         Ev ev;
         int64_t ts = 0;
