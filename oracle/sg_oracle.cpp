@@ -57,6 +57,7 @@
 
 #include "../include/siddhi_gpu.h"
 #include "../include/siddhi_gpu_ir.h"
+#include "../siddhi-1_amd/csrc/state_doc.h"   // the state document's format (sgo_state_export/import)
 
 namespace {
 
@@ -370,6 +371,9 @@ struct Engine {
     // event store
     std::vector<StreamStore> streams;
     std::vector<EvLoc> seqLoc;
+    // events that entered through sgo_state_import (before this engine's first push): seq -> attribute
+    // value bits + null bits
+    std::unordered_map<uint64_t, std::pair<std::vector<uint64_t>, uint32_t>> importedAttrs;
     uint64_t seq0 = 0;
     bool haveSeq0 = false;
 
@@ -389,6 +393,7 @@ struct Engine {
     bool playback = false;
     int64_t now = 0;
     int64_t lastEventTs = 0;
+    bool clockSet = false;                      // an event or a time advance has reached the engine
     uint64_t schedOrder = 0;
     std::vector<PreProc*> startup;              // startupPreStateProcessors (absent pres, parse order)
     // per scheduler (absent pre): keys whose queue is not empty, by head (playback listener)
@@ -402,7 +407,16 @@ struct Engine {
     void sendTimerEvents(PreProc* p);
 
     // ---- attribute access ----
+    bool stored(uint64_t seq) const {
+        return haveSeq0 && seq >= seq0 && seq - seq0 < seqLoc.size() && seqLoc[seq - seq0].stream != UINT32_MAX;
+    }
     Val attr(uint64_t seq, uint32_t a) const {
+        if (!stored(seq)) {
+            auto it = importedAttrs.find(seq);
+            if (it == importedAttrs.end() || a >= it->second.first.size())
+                throw std::runtime_error("attributes of an event not in the store");
+            return Val{it->second.first[a], ((it->second.second >> a) & 1u) != 0};
+        }
         const EvLoc& l = seqLoc[seq - seq0];
         const Column& c = streams[l.stream].cols[a];
         return Val{c.v[l.row], c.null.empty() ? false : (bool)c.null[l.row]};
@@ -1583,6 +1597,7 @@ int sgo_push_batch(sgo_engine* h, const sg_batch* b) {
             e.seq0 = b->seq_base;
             e.haveSeq0 = true;
         }
+        e.clockSet = true;
         if (b->seq_base < e.seq0 + e.seqLoc.size()) return fail(SG_ERR_INVALID, "sequence numbers must increase");
         if (!e.partitioned) init_key(&e, 0);
         // store rows
@@ -1642,6 +1657,7 @@ int sgo_advance_time(sgo_engine* h, int64_t now) {
     if (!h) return fail(SG_ERR_INVALID, "null argument");
     Engine& e = h->e;
     try {
+        e.clockSet = true;
         if (!e.partitioned && (e.keyInit.empty() || !e.keyInit[0])) {
             if (!e.playback) e.now = std::max(e.now, now);  // start(): wall clock now
             init_key(&e, 0);
@@ -1694,6 +1710,175 @@ int sgo_release_matches(sgo_engine* h, sg_match_batch* m) {
     (void)h;
     if (m) memset(m, 0, sizeof(*m));
     return SG_OK;
+}
+
+// ---- the per-key state in the reference's per-state-processor form (state_doc.h) ----------------------
+// StreamPreState.snapshot (StreamPreStateProcessor.java:450-469) + Count / Absent extras + the
+// Scheduler's toNotifyQueue, per initialised key
+int sgo_state_export(sgo_engine* h, void** buf, size_t* len) {
+    if (!h || !buf || !len) return fail(SG_ERR_INVALID, "null argument");
+    Engine& e = h->e;
+    try {
+        SdDoc d;
+        d.n_procs = (uint32_t)e.procs.size();
+        d.n_slots = (uint32_t)e.nslots;
+        for (const auto& p : e.procs) d.desc.push_back(SdProcDesc{(uint32_t)p->kind, p->absent ? 1u : 0u, (uint32_t)p->stateId});
+        d.now = e.now;
+        d.last_event_ts = e.lastEventTs;
+        d.clock_flags = e.clockSet ? 1u : 0u;
+        for (uint32_t k = 0; k < e.keyInit.size(); k++) {
+            if (!e.keyInit[k]) continue;
+            SdKeyBuilder<const StateEvent*, const StreamEvent*> B;
+            B.k.key = k;
+            auto visit_ev = [&](const StreamEvent* ev) -> uint32_t {
+                bool fresh;
+                const uint32_t i = B.stream(ev, fresh);
+                if (!fresh) return i;
+                SdStream s;
+                s.seq = ev->seq;
+                s.ts = ev->ts;
+                if (ev->seq == SG_BLANK_SEQ) {
+                    s.null_bits = 0xffffffffu;
+                } else if (e.stored(ev->seq)) {
+                    const EvLoc& l = e.seqLoc[ev->seq - e.seq0];
+                    const StreamStore& ss = e.streams[l.stream];
+                    for (uint32_t a = 0; a < ss.cols.size(); a++) {
+                        const Val v = e.attr(ev->seq, a);
+                        s.attr.push_back(v.b);
+                        if (v.null) s.null_bits |= 1u << a;
+                    }
+                    s.present = ss.cols.size() >= 32 ? 0xffffffffu : ((1u << ss.cols.size()) - 1u);
+                } else {
+                    auto it = e.importedAttrs.find(ev->seq);
+                    if (it != e.importedAttrs.end()) {
+                        s.attr = it->second.first;
+                        s.null_bits = it->second.second;
+                        s.present = s.attr.size() >= 32 ? 0xffffffffu : ((1u << s.attr.size()) - 1u);
+                    }
+                }
+                B.k.streams[i] = s;
+                return i;
+            };
+            auto visit_st = [&](const StateEvent* se) -> uint32_t {
+                bool fresh;
+                const uint32_t i = B.state(se, fresh);
+                if (!fresh) return i;
+                SdState st;
+                st.ts = se->ts;
+                st.type = se->type == EXPIRED ? 1u : 0u;
+                st.chains.resize(e.nslots);
+                for (int sl = 0; sl < e.nslots; sl++)
+                    for (const StreamEvent* ev = se->slots[sl].get(); ev; ev = ev->next.get())
+                        st.chains[sl].push_back(visit_ev(ev));
+                B.k.states[i] = st;
+                return i;
+            };
+            for (size_t p = 0; p < e.procs.size(); p++) {
+                const KeyState& ks = e.keyStates[k][p];
+                SdProc P;
+                P.flags = (ks.initialized ? (uint32_t)SD_INITIALIZED : 0u) | (ks.started ? (uint32_t)SD_STARTED : 0u) |
+                          (ks.successCondition ? (uint32_t)SD_SUCCESS : 0u) |
+                          (ks.startStateReset ? (uint32_t)SD_SSRESET : 0u) | (ks.active ? (uint32_t)SD_ACTIVE : 0u);
+                P.last_scheduled = ks.lastScheduledTime;
+                P.last_arrival = ks.lastArrivalTime;
+                for (const SE& se : ks.pending) P.pending.push_back(visit_st(se.get()));
+                for (const SE& se : ks.newAndEvery) P.newev.push_back(visit_st(se.get()));
+                P.queue.assign(ks.toNotify.begin(), ks.toNotify.end());
+                P.running = ks.running ? 1u : 0u;
+                P.fire_at = ks.running ? ks.fireAt : 0;
+                P.order = ks.order;
+                B.k.procs.push_back(P);
+            }
+            sd_rank_orders(B.k);
+            d.keys.push_back(std::move(B.k));
+        }
+        std::vector<uint8_t> bytes = sd_write(d);
+        void* out = malloc(bytes.size());
+        if (!out) return fail(SG_ERR_CAPACITY, "state document allocation failed");
+        memcpy(out, bytes.data(), bytes.size());
+        *buf = out;
+        *len = bytes.size();
+        return SG_OK;
+    } catch (const std::exception& ex) {
+        return fail(SG_ERR_STATE, ex.what());
+    }
+}
+
+int sgo_free_buffer(void* buf) {
+    free(buf);
+    return SG_OK;
+}
+
+// replaces the whole NFA state (keys absent from the document become never-seen); the document's events
+// keep their attributes for the filters and projections that read them later
+int sgo_state_import(sgo_engine* h, const void* buf, size_t len) {
+    if (!h || !buf) return fail(SG_ERR_INVALID, "null argument");
+    Engine& e = h->e;
+    try {
+        const SdDoc d = sd_read(buf, len);
+        bool same = d.n_procs == e.procs.size() && d.n_slots == (uint32_t)e.nslots;
+        for (size_t p = 0; same && p < e.procs.size(); p++)
+            same = d.desc[p] == SdProcDesc{(uint32_t)e.procs[p]->kind, e.procs[p]->absent ? 1u : 0u,
+                                           (uint32_t)e.procs[p]->stateId};
+        if (!same) return fail(SG_ERR_INVALID, "state document of a different query shape");
+        for (auto& ks : e.keyStates) ks.clear();
+        std::fill(e.keyInit.begin(), e.keyInit.end(), 0);
+        for (auto& hs : e.heads) hs.clear();
+        e.callers.clear();
+        e.now = d.now;
+        e.lastEventTs = d.last_event_ts;
+        e.clockSet = (d.clock_flags & 1u) != 0;
+        uint64_t maxRank = 0;
+        for (const SdKey& k : d.keys) {
+            if (e.partitioned ? false : k.key != 0) return fail(SG_ERR_INVALID, "unpartitioned query with a key other than 0");
+            ensure_key(&e, k.key);
+            e.keyInit[k.key] = 1;
+            std::vector<Ref<StreamEvent>> evs;
+            for (const SdStream& s : k.streams) {
+                evs.emplace_back(new StreamEvent(s.seq, s.ts));
+                if (s.seq != SG_BLANK_SEQ && !e.stored(s.seq)) e.importedAttrs[s.seq] = {s.attr, s.null_bits};
+            }
+            std::vector<SE> sts;
+            for (const SdState& st : k.states) {
+                SE se(new StateEvent(e.nslots));
+                se->ts = st.ts;
+                se->type = st.type ? EXPIRED : CURRENT;
+                for (int sl = 0; sl < e.nslots; sl++) {
+                    const auto& c = st.chains[sl];
+                    if (c.empty()) continue;
+                    se->slots[sl] = evs[c[0]];
+                    for (size_t i = 0; i + 1 < c.size(); i++) evs[c[i]]->next = evs[c[i + 1]];
+                }
+                sts.push_back(se);
+            }
+            for (size_t p = 0; p < e.procs.size(); p++) {
+                const SdProc& P = k.procs[p];
+                KeyState& ks = e.keyStates[k.key][p];
+                ks.initialized = (P.flags & SD_INITIALIZED) != 0;
+                ks.started = (P.flags & SD_STARTED) != 0;
+                ks.successCondition = (P.flags & SD_SUCCESS) != 0;
+                ks.startStateReset = (P.flags & SD_SSRESET) != 0;
+                ks.active = (P.flags & SD_ACTIVE) != 0;
+                ks.lastScheduledTime = P.last_scheduled;
+                ks.lastArrivalTime = P.last_arrival;
+                for (uint32_t x : P.pending) ks.pending.push_back(sts[x]);
+                for (uint32_t x : P.newev) ks.newAndEvery.push_back(sts[x]);
+                ks.toNotify.assign(P.queue.begin(), P.queue.end());
+                if (!ks.toNotify.empty()) e.heads[p].insert({ks.toNotify.front(), k.key});
+                ks.running = P.running != 0;
+                if (ks.running) {
+                    ks.fireAt = P.fire_at;
+                    ks.order = e.schedOrder + P.order;
+                    maxRank = std::max<uint64_t>(maxRank, P.order);
+                    e.callers.insert({ks.fireAt, k.key, ks.order, (int)p});
+                }
+            }
+        }
+        e.schedOrder += maxRank;
+        return SG_OK;
+    } catch (const std::exception& ex) {
+        return fail(SG_ERR_INVALID, ex.what());
+    }
 }
 
 int sgo_get_stats(sgo_engine* h, sg_stats* out) {

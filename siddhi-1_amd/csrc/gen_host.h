@@ -33,3 +33,7 @@ uint64_t gen_state_words(const GenEngine* e);
 int gen_reset_keys(GenEngine* e, const uint32_t* keys, uint32_t n, std::string& msg);
 int gen_snapshot(GenEngine* e, uint32_t* words, GenClock* clk, std::string& msg);
 int gen_restore(GenEngine* e, const uint32_t* words, const GenClock& clk, std::string& msg);
+// the state in the reference's per-state-processor form (state_doc.h)
+struct SdDoc;
+int gen_state_export(GenEngine* e, SdDoc& d, std::string& msg);
+int gen_state_import(GenEngine* e, const SdDoc& d, std::string& msg);

@@ -13,6 +13,7 @@
 #include <rocprim/device/device_scan.hpp>
 
 #include <algorithm>
+#include <functional>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -23,6 +24,7 @@
 #include "gen_engine.h"
 #include "gen_host.h"
 #include "pinned.h"
+#include "state_doc.h"
 
 extern "C" __global__ void k_gen_batch(const GenArgs* ap);
 extern "C" __global__ void k_gen_timers(const GenArgs* ap);
@@ -1086,4 +1088,197 @@ int gen_restore(GenEngine* e, const uint32_t* words, const GenClock& clk, std::s
     e->lastEventTs = clk.last_event_ts;
     e->advanced = clk.advanced != 0;
     return SG_OK;
+}
+
+// ---- the per-key state in the reference's per-state-processor form (state_doc.h) -----------------------
+// Decoded from / encoded into the interleaved state blocks on the host (word w of key k at w * K + k):
+// every initialised key's processors (flags, absent-state times, pending / newAndEvery lists, timer queue,
+// wall-clock caller) with the StateEvents and StreamEvents the lists reach.  Import replaces the whole
+// state (keys absent from the document become never-seen) and recomputes the refcounts and free bitmaps
+// from the references the document holds.
+int gen_state_export(GenEngine* e, SdDoc& d, std::string& msg) {
+    const GenProgram& G = e->host;
+    const uint64_t K = e->K;
+    std::vector<uint32_t> S(gen_state_words(e));
+    GenClock clk{};
+    const int rc = gen_snapshot(e, S.data(), &clk, msg);
+    if (rc != SG_OK) return rc;
+    auto W = [&](uint32_t k, uint32_t w) -> uint32_t { return S[(size_t)w * K + k]; };
+    auto R64 = [&](uint32_t k, uint32_t w) -> int64_t {
+        return (int64_t)((uint64_t)W(k, w) | ((uint64_t)W(k, w + 1) << 32));
+    };
+    d.n_procs = (uint32_t)G.nprocs;
+    d.n_slots = (uint32_t)G.nslots;
+    for (int p = 0; p < G.nprocs; p++)
+        d.desc.push_back(SdProcDesc{(uint32_t)G.pre[p].kind, G.pre[p].absent ? 1u : 0u, (uint32_t)G.pre[p].stateId});
+    d.now = clk.now;
+    d.last_event_ts = clk.last_event_ts;
+    d.clock_flags = clk.advanced ? 1u : 0u;
+    for (uint32_t k = 0; k < K; k++) {
+        if (!(W(k, 0) & 1u)) continue;
+        SdKeyBuilder<uint32_t, uint32_t> B;
+        B.k.key = k;
+        std::function<uint32_t(uint32_t, int)> visit_ev = [&](uint32_t ev, int slot) -> uint32_t {
+            bool fresh;
+            const uint32_t i = B.stream(ev, fresh);
+            if (!fresh) return i;
+            const uint32_t base = G.offSE + ev * G.seWords;
+            SdStream x;
+            x.seq = (uint64_t)R64(k, base + SE_SEQ);
+            x.ts = R64(k, base + SE_TS);
+            x.null_bits = W(k, base + SE_NULL);
+            if (x.null_bits != 0xffffffffu) {
+                const int na = G.nattr[G.slotStream[slot]];
+                for (int a = 0; a < na; a++) x.attr.push_back((uint64_t)R64(k, base + SE_ATTR + 2 * (uint32_t)a));
+                x.present = na >= 32 ? 0xffffffffu : ((1u << na) - 1u);
+                x.null_bits &= x.present;
+            }
+            B.k.streams[i] = x;
+            return i;
+        };
+        auto visit_st = [&](uint32_t st) -> uint32_t {
+            bool fresh;
+            const uint32_t i = B.state(st, fresh);
+            if (!fresh) return i;
+            const uint32_t base = G.offST + st * G.stWords;
+            SdState x;
+            x.ts = R64(k, base + ST_TS);
+            x.type = W(k, base + ST_TYPE);
+            x.chains.resize(G.nslots);
+            for (int sl = 0; sl < G.nslots; sl++) {
+                uint32_t ev = W(k, base + ST_SLOTS + (uint32_t)sl);
+                for (uint32_t guard = 0; ev != GEN_NIL && guard <= G.SECAP; guard++) {
+                    x.chains[sl].push_back(visit_ev(ev, sl));
+                    ev = W(k, G.offSE + ev * G.seWords + SE_NEXT);
+                }
+            }
+            B.k.states[i] = x;
+            return i;
+        };
+        for (int p = 0; p < G.nprocs; p++) {
+            const uint32_t ks = G.offKS + (uint32_t)p * G.ksWords;
+            const uint32_t f = W(k, ks + KS_FLAGS);
+            SdProc P;
+            P.flags = ((f & GF_INIT) ? (uint32_t)SD_INITIALIZED : 0u) | ((f & GF_STARTED) ? (uint32_t)SD_STARTED : 0u) |
+                      ((f & GF_SUCCESS) ? (uint32_t)SD_SUCCESS : 0u) | ((f & GF_SSRESET) ? (uint32_t)SD_SSRESET : 0u) |
+                      ((f & GF_INACTIVE) ? 0u : (uint32_t)SD_ACTIVE);
+            P.last_scheduled = R64(k, ks + KS_LST);
+            P.last_arrival = R64(k, ks + KS_LAT);
+            for (int which = 0; which < 2; which++) {
+                const uint32_t n = W(k, ks + KS_PLEN + (uint32_t)which);
+                for (uint32_t i = 0; i < n && i < G.L; i++) {
+                    const uint32_t st = visit_st(W(k, ks + KS_LISTS + (uint32_t)which * G.L + i));
+                    (which ? P.newev : P.pending).push_back(st);
+                }
+            }
+            const uint32_t h = W(k, ks + KS_QHEAD), q = W(k, ks + KS_QLEN);
+            for (uint32_t i = 0; i < q && i < G.Q; i++) P.queue.push_back(R64(k, ks + KS_LISTS + 2 * G.L + 2 * ((h + i) % G.Q)));
+            P.running = (f & GF_RUNNING) ? 1u : 0u;
+            P.fire_at = P.running ? R64(k, ks + KS_FIRE) : 0;
+            P.order = W(k, ks + KS_ORDER);
+            B.k.procs.push_back(P);
+        }
+        sd_rank_orders(B.k);
+        d.keys.push_back(std::move(B.k));
+    }
+    return SG_OK;
+}
+
+int gen_state_import(GenEngine* e, const SdDoc& d, std::string& msg) {
+    const GenProgram& G = e->host;
+    const uint64_t K = e->K;
+    bool same = d.n_procs == (uint32_t)G.nprocs && d.n_slots == (uint32_t)G.nslots;
+    for (int p = 0; same && p < G.nprocs; p++)
+        same = d.desc[p] == SdProcDesc{(uint32_t)G.pre[p].kind, G.pre[p].absent ? 1u : 0u, (uint32_t)G.pre[p].stateId};
+    if (!same) {
+        msg = "state document of a different query shape";
+        return SG_ERR_INVALID;
+    }
+    std::vector<uint32_t> S(gen_state_words(e), 0u);
+    auto W = [&](uint32_t k, uint32_t w) -> uint32_t& { return S[(size_t)w * K + k]; };
+    auto W64 = [&](uint32_t k, uint32_t w, int64_t v) {
+        W(k, w) = (uint32_t)(uint64_t)v;
+        W(k, w + 1) = (uint32_t)((uint64_t)v >> 32);
+    };
+    for (const SdKey& x : d.keys) {
+        if (x.key >= K) { msg = "state document key id outside [0, n_keys)"; return SG_ERR_INVALID; }
+        if (x.states.size() > G.STCAP || x.streams.size() > G.SECAP) {
+            msg = "state document holds more partial matches per key than partial_capacity allows";
+            return SG_ERR_CAPACITY;
+        }
+        const uint32_t k = x.key;
+        W(k, 0) = 1u;
+        // references: a StateEvent is held by each list entry; a StreamEvent by each slot head and by the
+        // event before it in a count chain
+        std::vector<uint32_t> st_rc(x.states.size(), 0), ev_rc(x.streams.size(), 0);
+        std::vector<uint32_t> next(x.streams.size(), GEN_NIL);
+        std::vector<uint8_t> linked(x.streams.size(), 0);
+        for (const SdState& st : x.states)
+            for (const auto& c : st.chains) {
+                if (c.empty()) continue;
+                ev_rc[c[0]]++;
+                for (size_t i = 0; i + 1 < c.size(); i++) {
+                    if (next[c[i]] == GEN_NIL) next[c[i]] = c[i + 1];
+                    else if (next[c[i]] != c[i + 1]) { msg = "state document chains disagree"; return SG_ERR_INVALID; }
+                    if (!linked[c[i + 1]]) { linked[c[i + 1]] = 1; ev_rc[c[i + 1]]++; }
+                }
+            }
+        uint32_t maxOrder = 0;
+        for (int p = 0; p < G.nprocs; p++) {
+            const SdProc& P = x.procs[p];
+            const uint32_t ks = G.offKS + (uint32_t)p * G.ksWords;
+            if (P.pending.size() > G.L || P.newev.size() > G.L || P.queue.size() > G.Q) {
+                msg = "state document list longer than this engine's capacity";
+                return SG_ERR_CAPACITY;
+            }
+            uint32_t f = 0;
+            if (P.flags & SD_INITIALIZED) f |= GF_INIT;
+            if (P.flags & SD_STARTED) f |= GF_STARTED;
+            if (P.flags & SD_SUCCESS) f |= GF_SUCCESS;
+            if (P.flags & SD_SSRESET) f |= GF_SSRESET;
+            if (!(P.flags & SD_ACTIVE)) f |= GF_INACTIVE;
+            if (P.running) f |= GF_RUNNING;
+            W(k, ks + KS_FLAGS) = f;
+            W64(k, ks + KS_LST, P.last_scheduled);
+            W64(k, ks + KS_LAT, P.last_arrival);
+            W64(k, ks + KS_FIRE, P.running ? P.fire_at : 0);
+            W(k, ks + KS_ORDER) = (uint32_t)P.order;
+            maxOrder = std::max(maxOrder, (uint32_t)P.order);
+            W(k, ks + KS_QHEAD) = 0;
+            W(k, ks + KS_QLEN) = (uint32_t)P.queue.size();
+            for (size_t i = 0; i < P.queue.size(); i++) W64(k, ks + KS_LISTS + 2 * G.L + 2 * (uint32_t)i, P.queue[i]);
+            for (int which = 0; which < 2; which++) {
+                const auto& l = which ? P.newev : P.pending;
+                W(k, ks + KS_PLEN + (uint32_t)which) = (uint32_t)l.size();
+                for (size_t i = 0; i < l.size(); i++) {
+                    W(k, ks + KS_LISTS + (uint32_t)which * G.L + (uint32_t)i) = l[i];
+                    st_rc[l[i]]++;
+                }
+            }
+        }
+        W(k, 1) = maxOrder;  // the key's scheduler order counter
+        for (size_t i = 0; i < x.states.size(); i++) {
+            const SdState& st = x.states[i];
+            const uint32_t base = G.offST + (uint32_t)i * G.stWords;
+            W64(k, base + ST_TS, st.ts);
+            W(k, base + ST_TYPE) = st.type;
+            W(k, base + ST_RC) = st_rc[i];
+            for (int sl = 0; sl < G.nslots; sl++)
+                W(k, base + ST_SLOTS + (uint32_t)sl) = st.chains[sl].empty() ? GEN_NIL : st.chains[sl][0];
+            W(k, G.offSTfree + (uint32_t)i / 32) |= 1u << (i % 32);
+        }
+        for (size_t i = 0; i < x.streams.size(); i++) {
+            const SdStream& ev = x.streams[i];
+            const uint32_t base = G.offSE + (uint32_t)i * G.seWords;
+            W64(k, base + SE_SEQ, (int64_t)ev.seq);
+            W64(k, base + SE_TS, ev.ts);
+            W(k, base + SE_NEXT) = next[i];
+            W(k, base + SE_RC) = ev_rc[i];
+            W(k, base + SE_NULL) = ev.null_bits;
+            for (size_t a = 0; a < ev.attr.size() && a < G.NA; a++) W64(k, base + SE_ATTR + 2 * (uint32_t)a, (int64_t)ev.attr[a]);
+            W(k, G.offSEfree + (uint32_t)i / 32) |= 1u << (i % 32);
+        }
+    }
+    GenClock clk{d.now, d.last_event_ts, (uint32_t)(d.clock_flags & 1u), 0};
+    return gen_restore(e, S.data(), clk, msg);
 }

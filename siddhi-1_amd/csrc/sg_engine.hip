@@ -35,6 +35,7 @@
 #include "gen_engine.h"
 #include "gen_host.h"
 #include "pinned.h"
+#include "state_doc.h"
 #include "sg_engine.h"
 #include "sg_jit.h"
 
@@ -1654,6 +1655,193 @@ int sg_restore(sg_engine* e, const void* buf, size_t len) {
 int sg_free_buffer(void* buf) {
     free(buf);
     return SG_OK;
+}
+
+// ---- the per-key state in the reference's per-state-processor form (state_doc.h) -----------------------
+// Two-state kernel: processor 0 is e1's pre-state (its pending / newAndEvery lists hold the start-state
+// seeds: StateEvents with no slot filled, counted in the key header), processor 1 is e2's (its lists are
+// the partials: one StateEvent per slab row, slot0 = the e1 StreamEvent with the attributes the partial
+// captured; the other attributes are not on the device and are marked absent in `present`).  A seed's
+// timestamp is not kept (it does not affect matching) and is written as -1.
+static int twostate_export(sg_engine* e, SdDoc& d) {
+    const Plan& pl = e->plan;
+    const size_t K = e->K;
+    if (e->held) return fail(SG_ERR_STATE, "release the polled matches before exporting the state");
+    if (outputs_pending(e)) return fail(SG_ERR_STATE, "poll the emitted matches before exporting the state");
+    std::vector<uint32_t> hdr(K);
+    HIP_OK(hipMemcpy(hdr.data(), e->hdr, K * 4, hipMemcpyDeviceToHost));
+    uint32_t rows = 0;
+    for (uint32_t x : hdr) rows = std::max(rows, (uint32_t)(SGD_H_NPEND(x) + SGD_H_NSTG(x)));
+    const size_t plane = (size_t)rows * K;
+    std::vector<int64_t> ts(plane);
+    std::vector<uint64_t> seq(plane);
+    std::vector<uint32_t> capw((size_t)e->n_capw * plane), capn(plane);
+    if (plane) {
+        HIP_OK(hipMemcpy(ts.data(), e->p_ts, plane * 8, hipMemcpyDeviceToHost));
+        HIP_OK(hipMemcpy(seq.data(), e->p_seq, plane * 8, hipMemcpyDeviceToHost));
+        for (uint32_t w = 0; w < e->n_capw; w++)
+            HIP_OK(hipMemcpy(capw.data() + w * plane, e->p_capw + (size_t)w * e->cap * K, plane * 4, hipMemcpyDeviceToHost));
+        HIP_OK(hipMemcpy(capn.data(), e->p_capnull, plane * 4, hipMemcpyDeviceToHost));
+    }
+    const uint32_t na = (uint32_t)e->streams[pl.s0].types.size();
+    d.n_procs = 2;
+    d.n_slots = 2;
+    d.desc = {SdProcDesc{0, 0, pl.slot0}, SdProcDesc{0, 0, pl.slot1}};
+    for (uint32_t k = 0; k < K; k++) {
+        const uint32_t h = hdr[k];
+        if (!SGD_H_INIT(h)) continue;
+        SdKey x;
+        x.key = k;
+        x.procs.resize(2);
+        for (auto& P : x.procs) P.flags = SD_ACTIVE;
+        x.procs[0].flags |= SD_INITIALIZED;  // the start state's init() ran with the key's first event
+        auto seed = [&]() {
+            SdState st;
+            st.chains.resize(2);
+            x.states.push_back(st);
+            return (uint32_t)x.states.size() - 1;
+        };
+        for (uint32_t i = 0; i < SGD_H_SPEND(h); i++) x.procs[0].pending.push_back(seed());
+        for (uint32_t i = 0; i < SGD_H_SSTG(h); i++) x.procs[0].newev.push_back(seed());
+        const uint32_t np = SGD_H_NPEND(h), ns = SGD_H_NSTG(h);
+        for (uint32_t j = 0; j < np + ns; j++) {
+            const size_t r = (size_t)j * K + k;
+            SdStream ev;
+            ev.seq = seq[r];
+            ev.ts = ts[r];
+            ev.attr.assign(na, 0);
+            uint32_t w = 0;
+            for (size_t c = 0; c < pl.caps.size(); c++) {
+                const uint32_t a = pl.caps[c], t = pl.cap_type[c];
+                uint64_t v = capw[(size_t)w * plane + r];
+                if (t == SG_T_LONG || t == SG_T_DOUBLE) v |= (uint64_t)capw[(size_t)(w + 1) * plane + r] << 32;
+                w += (t == SG_T_LONG || t == SG_T_DOUBLE) ? 2 : 1;
+                ev.attr[a] = v;
+                ev.present |= 1u << a;
+                if ((capn[r] >> c) & 1u) ev.null_bits |= 1u << a;
+            }
+            x.streams.push_back(ev);
+            SdState st;
+            st.ts = ts[r];
+            st.chains.resize(2);
+            st.chains[pl.slot0].push_back((uint32_t)x.streams.size() - 1);
+            x.states.push_back(st);
+            (j < np ? x.procs[1].pending : x.procs[1].newev).push_back((uint32_t)x.states.size() - 1);
+        }
+        d.keys.push_back(std::move(x));
+    }
+    return SG_OK;
+}
+
+static int twostate_import(sg_engine* e, const SdDoc& d) {
+    const Plan& pl = e->plan;
+    const size_t K = e->K;
+    if (d.n_procs != 2 || d.n_slots != 2 || !(d.desc[0] == SdProcDesc{0, 0, pl.slot0}) ||
+        !(d.desc[1] == SdProcDesc{0, 0, pl.slot1}))
+        return fail(SG_ERR_INVALID, "state document of a different query shape");
+    if (e->held) return fail(SG_ERR_STATE, "release the polled matches before a state import");
+    if (outputs_pending(e)) return fail(SG_ERR_STATE, "poll the emitted matches before a state import");
+    uint32_t rows = 0;
+    for (const SdKey& x : d.keys) rows = std::max<uint32_t>(rows, (uint32_t)(x.procs[1].pending.size() + x.procs[1].newev.size()));
+    if (rows > e->cap) return fail(SG_ERR_CAPACITY, "state document holds more partials per key than partial_capacity");
+    const size_t plane = (size_t)rows * K;
+    std::vector<uint32_t> hdr(K, 0u);
+    std::vector<int64_t> ts(plane, 0);
+    std::vector<uint64_t> seq(plane, 0);
+    std::vector<uint32_t> capw((size_t)e->n_capw * plane, 0u), capn(plane, 0u);
+    bool nulls = false;
+    for (const SdKey& x : d.keys) {
+        if (x.key >= K) return fail(SG_ERR_INVALID, "state document key id outside [0, n_keys)");
+        for (int p = 0; p < 1; p++)
+            for (const auto* l : {&x.procs[0].pending, &x.procs[0].newev})
+                for (uint32_t si : *l)
+                    for (const auto& c : x.states[si].chains)
+                        if (!c.empty()) return fail(SG_ERR_UNSUPPORTED, "a start-state list entry holds an event");
+        const size_t spend = x.procs[0].pending.size(), sstg = x.procs[0].newev.size();
+        if (spend > 3 || sstg > 3) return fail(SG_ERR_UNSUPPORTED, "more than 3 start-state seeds in one list");
+        const size_t np = x.procs[1].pending.size(), ns = x.procs[1].newev.size();
+        const bool init = (x.procs[0].flags & SD_INITIALIZED) != 0 || spend + sstg + np + ns > 0;
+        hdr[x.key] = SGD_H_MAKE(np, ns, spend, sstg, init ? 1 : 0);
+        for (size_t j = 0; j < np + ns; j++) {
+            const SdState& st = x.states[j < np ? x.procs[1].pending[j] : x.procs[1].newev[j - np]];
+            for (uint32_t sl = 0; sl < 2; sl++)
+                if ((sl == pl.slot0) != (st.chains[sl].size() == 1) || st.chains[sl].size() > 1)
+                    return fail(SG_ERR_UNSUPPORTED, "a partial that is not one e1 event");
+            const SdStream& ev = x.streams[st.chains[pl.slot0][0]];
+            const size_t r = j * K + x.key;
+            ts[r] = ev.ts;
+            seq[r] = ev.seq;
+            uint32_t w = 0;
+            for (size_t c = 0; c < pl.caps.size(); c++) {
+                const uint32_t a = pl.caps[c], t = pl.cap_type[c];
+                if (a >= ev.attr.size() || !((ev.present >> a) & 1u))
+                    return fail(SG_ERR_INVALID, "a partial's event lacks an attribute the query reads");
+                capw[(size_t)w * plane + r] = (uint32_t)ev.attr[a];
+                if (t == SG_T_LONG || t == SG_T_DOUBLE) capw[(size_t)(w + 1) * plane + r] = (uint32_t)(ev.attr[a] >> 32);
+                w += (t == SG_T_LONG || t == SG_T_DOUBLE) ? 2 : 1;
+                if ((ev.null_bits >> a) & 1u) {
+                    capn[r] |= 1u << c;
+                    nulls = true;
+                }
+            }
+        }
+    }
+    HIP_OK(hipMemcpy(e->hdr, hdr.data(), K * 4, hipMemcpyHostToDevice));
+    if (plane) {
+        HIP_OK(hipMemcpy(e->p_ts, ts.data(), plane * 8, hipMemcpyHostToDevice));
+        HIP_OK(hipMemcpy(e->p_seq, seq.data(), plane * 8, hipMemcpyHostToDevice));
+        for (uint32_t w = 0; w < e->n_capw; w++)
+            HIP_OK(hipMemcpy(e->p_capw + (size_t)w * e->cap * K, capw.data() + w * plane, plane * 4, hipMemcpyHostToDevice));
+        HIP_OK(hipMemcpy(e->p_capnull, capn.data(), plane * 4, hipMemcpyHostToDevice));
+    }
+    if (nulls) e->nullable = true;
+    return SG_OK;
+}
+
+int sg_state_export(sg_engine* e, void** buf, size_t* len) {
+    if (!e || !buf || !len) return fail(SG_ERR_INVALID, "null argument");
+    try {
+        HIP_OK(hipSetDevice(e->device));
+        SdDoc d;
+        if (e->gen) {
+            std::string msg;
+            const int rc = gen_state_export(e->gen, d, msg);
+            if (rc != SG_OK) return fail(rc, msg);
+        } else {
+            const int rc = twostate_export(e, d);
+            if (rc != SG_OK) return rc;
+        }
+        std::vector<uint8_t> bytes = sd_write(d);
+        void* out = malloc(bytes.size());
+        if (!out) return fail(SG_ERR_CAPACITY, "state document allocation failed");
+        memcpy(out, bytes.data(), bytes.size());
+        *buf = out;
+        *len = bytes.size();
+        return SG_OK;
+    } catch (const std::exception& ex) {
+        return fail(SG_ERR_DEVICE, ex.what());
+    }
+}
+
+int sg_state_import(sg_engine* e, const void* buf, size_t len) {
+    if (!e || !buf) return fail(SG_ERR_INVALID, "null argument");
+    SdDoc d;
+    try {
+        d = sd_read(buf, len);
+    } catch (const std::exception& ex) {
+        return fail(SG_ERR_INVALID, ex.what());
+    }
+    try {
+        HIP_OK(hipSetDevice(e->device));
+        if (e->gen) {
+            std::string msg;
+            const int rc = gen_state_import(e->gen, d, msg);
+            return rc == SG_OK ? rc : fail(rc, msg);
+        }
+        return twostate_import(e, d);
+    } catch (const std::exception& ex) {
+        return fail(SG_ERR_DEVICE, ex.what());
+    }
 }
 
 int sg_jit_check(const void* ir, size_t ir_len, uint32_t variant_flags, char* out, size_t out_len) {

@@ -409,6 +409,24 @@ class NativeEngine:
         f.argtypes = [C.c_void_p, C.c_char_p, C.c_size_t]
         self._check(f(self.h, image, len(image)))
 
+    def state_export(self) -> bytes:
+        """The NFA state in the reference's per-state-processor form (sg_state_export, state_doc.py)."""
+        f, free = getattr(self.lib, self.p + "state_export"), getattr(self.lib, self.p + "free_buffer")
+        f.argtypes = [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]
+        free.argtypes = [C.c_void_p]
+        buf, n = C.c_void_p(), C.c_size_t()
+        self._check(f(self.h, C.byref(buf), C.byref(n)))
+        try:
+            return C.string_at(buf, n.value)
+        finally:
+            free(buf)
+
+    def state_import(self, doc: bytes):
+        """Replace the NFA state with a state document of any engine of the same query (sg_state_import)."""
+        f = getattr(self.lib, self.p + "state_import")
+        f.argtypes = [C.c_void_p, C.c_char_p, C.c_size_t]
+        self._check(f(self.h, doc, len(doc)))
+
     def stats(self):
         s = sg_stats()
         self._check(self._stats(self.h, C.byref(s)))

@@ -733,7 +733,7 @@ class SiddhiAppRuntime:
         head = {
             "app": self.name,
             "strings": self.strings.strs,
-            "rows": [[st, int(ts), _enc(tuple(d))] for st, ts, d in self.store.rows],
+            "rows": [None if r is None else [r[0], int(r[1]), _enc(tuple(r[2]))] for r in self.store.rows],
             "event_time": self._event_time,
             "last_sys": self._last_sys,
             "queries": [{"keys": list(qr.key_dict.keys()) if qr.key_dict is not None else None,
@@ -768,7 +768,7 @@ class SiddhiAppRuntime:
             raise CannotRestoreSiddhiAppStateException(f"Restoring of Siddhi app {self.name} failed: {ex}")
         self.strings.strs = list(head["strings"])
         self.strings.ids = {x: i for i, x in enumerate(self.strings.strs)}
-        self.store.rows = [(st, ts, _dec(d)) for st, ts, d in head["rows"]]
+        self.store.rows = [None if r is None else (r[0], r[1], _dec(r[2])) for r in head["rows"]]
         self._event_time = head["event_time"]
         self._last_sys = head["last_sys"]
         for qr, qs in zip(self.queries, head["queries"]):
@@ -778,6 +778,72 @@ class SiddhiAppRuntime:
             qr._agg_states = _dec(qs["aggs"])
         for pg, seen in zip(self._purges, head.get("purge_last_seen", [])):
             pg.last_seen = dict(seen)
+
+    # -- the pattern state in the reference's per-state-processor form (state_doc.py) --------------------
+    def snapshot_states(self):
+        """{query name: {partition key: {element id: StreamPreState map}}} — PartitionStateHolder's map
+        (PartitionStateHolder.java:37-80) of every pattern query, each processor's map as
+        StreamPreState.snapshot() writes it (StreamPreStateProcessor.java:450-469, + Count / Absent extras and
+        the Scheduler's toNotifyQueue), StateEvent / StreamEvent objects shared as the engine shares them and
+        each StreamEvent's data from the host event store."""
+        sd = _state_doc()
+        out = {}
+        for name, qr in self.by_name.items():
+            doc = sd.parse(qr.engine.state_export())
+            keys = qr.key_dict.keys() if qr.key_dict is not None else None
+            slots = qr.cq.slots
+
+            def data(ds, sl):
+                if ds.seq == BLANK_SEQ or ds.seq >= len(self.store.rows) or self.store.rows[ds.seq] is None:
+                    return None
+                return list(self.store.rows[ds.seq][2])
+
+            out[name] = sd.to_reference_map(doc, key_name=(lambda k, keys=keys: keys[k]) if keys is not None else
+                                            (lambda k: ""), event_data=data,
+                                            slot_name=lambda sl, slots=slots: slots[sl].ref or slots[sl].stream,
+                                            slot_stream=lambda sl, slots=slots: slots[sl].stream)
+        return out
+
+    def restore_states(self, states):
+        """Replace the pattern queries' state with a map of snapshot_states()'s form (from this runtime, a
+        runtime of the same app, or built by hand).  The StreamEvents' data enter the event store at their
+        seqs, the partition keys the key dictionary."""
+        sd = _state_doc()
+        for name, qr in self.by_name.items():
+            m = states.get(name, {})
+            slots = qr.cq.slots
+            n_slots = len(slots)
+            probe = sd.parse(qr.engine.state_export())
+            touched = []
+
+            def bits(ev):
+                if ev.data is None:
+                    return [], 0xFFFFFFFF, 0
+                sdef = self.app.streams[ev.stream]
+                cols, nulls = self._columns(sdef, [tuple(ev.data)])
+                vals = [int(np.asarray(c).view(np.uint32 if c.dtype.itemsize == 4 else
+                                               (np.uint64 if c.dtype.itemsize == 8 else np.uint8))[0]) for c in cols]
+                nb = 0
+                for a, x in enumerate(nulls):
+                    if x is not None and x[0]:
+                        nb |= 1 << a
+                touched.append(ev)
+                return vals, nb, (1 << len(vals)) - 1
+
+            def key_id(pk):
+                if qr.key_dict is None:
+                    return 0
+                return int(qr.key_dict.intern([pk])[0])
+
+            doc = sd.from_reference_map(m, probe.desc, n_slots, key_id=key_id, event_bits=bits,
+                                        slot_name=lambda sl: slots[sl].ref or slots[sl].stream,
+                                        now=probe.now, last_event_ts=probe.last_event_ts,
+                                        clock_flags=probe.clock_flags)
+            qr.engine.state_import(sd.write(doc))
+            for ev in touched:   # the events the partials hold, for the host projection of later matches
+                while len(self.store.rows) <= ev.seq:
+                    self.store.rows.append(None)
+                self.store.rows[ev.seq] = (ev.stream, int(ev.timestamp), tuple(ev.data))
 
     def persist(self):
         """SiddhiAppRuntime.persist(): snapshot into the manager's persistence store; returns the revision."""
@@ -945,6 +1011,11 @@ class SiddhiAppRuntime:
                                        [x[lo:hi] if x is not None else None for x in nulls], kids[lo:hi])
             m = qr.engine.poll()
             qr.dispatch(qr.project(m, self.store))
+
+
+def _state_doc():
+    from . import state_doc
+    return state_doc
 
 
 def _time_ms(v):

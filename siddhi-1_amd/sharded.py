@@ -199,6 +199,44 @@ class ShardedEngine:
         self.gmap = [np.concatenate([m, np.zeros(1024, np.uint64)]) for m in maps]
         self.next_local = nxt
 
+    def state_export(self) -> bytes:
+        """one state document over every shard (state_doc.py): keys and event seqs mapped to global ids"""
+        from . import state_doc as sd
+        docs = [sd.parse(b) for b in self._each(lambda r: self.shards[r].state_export())]
+        out = sd.StateDoc(docs[0].n_procs, docs[0].n_slots, docs[0].desc, docs[0].now, docs[0].last_event_ts,
+                          max(d.clock_flags for d in docs))
+        for r, d in enumerate(docs):
+            for k in d.keys:
+                if self.N > 1:
+                    k.key = k.key * self.N + r
+                for ev in k.streams:
+                    if ev.seq < int(BLANK_SEQ):
+                        ev.seq = int(self.gmap[r][ev.seq])
+                out.keys.append(k)
+        out.keys.sort(key=lambda k: k.key)
+        return sd.write(out)
+
+    def state_import(self, doc: bytes):
+        """split a state document by owner shard; its events get fresh local seqs mapped to their global ones"""
+        from . import state_doc as sd
+        d = sd.parse(doc)
+        parts = [sd.StateDoc(d.n_procs, d.n_slots, d.desc, d.now, d.last_event_ts, d.clock_flags) for _ in range(self.N)]
+        for k in d.keys:
+            if k.key >= self.n_keys:
+                raise ValueError("state document key id outside [0, n_keys)")
+            r = k.key % self.N
+            k.key //= self.N
+            parts[r].keys.append(k)
+        for r, p in enumerate(parts):
+            glob = sorted({ev.seq for k in p.keys for ev in k.streams if ev.seq < int(BLANK_SEQ)})
+            base = self._append(r, np.array(glob, dtype=np.uint64))
+            local = {g: base + i for i, g in enumerate(glob)}
+            for k in p.keys:
+                for ev in k.streams:
+                    if ev.seq < int(BLANK_SEQ):
+                        ev.seq = local[ev.seq]
+        self._each(lambda r: self.shards[r].state_import(sd.write(parts[r])))
+
     def close(self):
         for s in self.shards:
             s.close()

@@ -1,0 +1,274 @@
+"""The NFA state in the reference's per-state-processor form (sg_state_export / sg_state_import,
+siddhi-1_amd/state_doc.py) on the CPU oracle.
+
+The reference persists, per partition key, each pre-state processor's StreamPreState map
+(StreamPreStateProcessor.java:450-469 + Count / Absent extras + the Scheduler's toNotifyQueue).  Checked
+here: an oracle exported after some batches and imported into a fresh oracle exports the same bytes and
+continues exactly as the uninterrupted one (every pattern / sequence / count / logical / absent shape,
+timers included); the document codec and the nested reference map round-trip; malformed documents are
+refused.  The device engines against the oracle: tests/test_gpu_state_doc.py.
+"""
+import importlib
+
+import numpy as np
+import pytest
+
+from oracle_backend import build_oracle
+from test_gpu_general import ABSENT, GENERAL, _burst_stream
+from test_gpu_parity import SHAPES
+
+sa = importlib.import_module("siddhi-1_amd")
+synth = importlib.import_module("siddhi-1_amd.synth")
+sd = importlib.import_module("siddhi-1_amd.state_doc")
+
+BATCH_SHAPES = dict(SHAPES)
+BATCH_SHAPES.update({f"gen_{k}": v for k, v in GENERAL.items()})
+
+
+def _oracle(q, n_keys):
+    app = sa.parse_app(q)
+    cq = sa.compile_query(app, app.queries[0], sa.StringDictionary())
+    return cq, sa.NativeEngine(build_oracle(), "sgo_", cq.ir, n_keys=n_keys)
+
+
+def _feed(e, cq, q, seq, d):
+    cols = [d["symbol"], d["price"], d["volume"]]
+    if "S1" in q:   # two streams: the first half of the batch on S1, the rest on S2
+        half = len(d["ts"]) // 2
+        wide = "price double" in q   # S2 (symbol string, price double, volume long)
+        for s, lo, hi in ((cq.stream_index("S1"), 0, half), (cq.stream_index("S2"), half, len(d["ts"]))):
+            cs = [c[lo:hi] for c in cols]
+            if wide and s == cq.stream_index("S2"):
+                cs = [cs[0], cs[1].astype(np.float64), cs[2].astype(np.int64)]
+            e.push(s, seq + lo, d["ts"][lo:hi], cs, None, d["key"][lo:hi])
+    else:
+        e.push(0, seq, d["ts"], cols, None, d["key"])
+
+
+def _same(a, b):
+    assert len(a) == len(b)
+    for f in ("trigger_seq", "key", "ts", "chain_len"):
+        assert np.array_equal(getattr(a, f), getattr(b, f)), f
+    w = min(a.slot_seq.shape[2], b.slot_seq.shape[2])
+    assert np.array_equal(a.slot_seq[:, :, :w], b.slot_seq[:, :, :w])
+
+
+@pytest.mark.parametrize("shape", sorted(BATCH_SHAPES))
+def test_oracle_export_import_continues_exactly(shape):
+    q = BATCH_SHAPES[shape]
+    n_keys, batch = 256, 6000
+    data = [(b * batch, synth.stock_ticks(b * batch, batch, n_keys, seed=70 + b, rate_per_ms=16)) for b in range(4)]
+    cq, ref = _oracle(q, n_keys)
+    want = []
+    for seq, d in data:
+        _feed(ref, cq, q, seq, d)
+        want.append(ref.poll())
+    cq, a = _oracle(q, n_keys)
+    for seq, d in data[:2]:
+        _feed(a, cq, q, seq, d)
+        a.poll()
+    doc = a.state_export()
+    parsed = sd.parse(doc)
+    assert sd.write(parsed) == doc                 # the codec is exact
+    assert len(parsed.keys) > 0
+    cq, b = _oracle(q, n_keys)
+    b.state_import(doc)
+    assert b.state_export() == doc                 # same logical state, same bytes
+    assert b.stats()["partials_live"] == a.stats()["partials_live"]
+    for i, (seq, d) in enumerate(data[2:], start=2):
+        _feed(b, cq, q, seq, d)
+        _same(b.poll(), want[i])
+    assert sum(len(m) for m in want) > 0 or shape == "gen_c3"   # C3 emits nothing, in the reference too
+
+
+@pytest.mark.parametrize("shape", sorted(ABSENT))
+def test_oracle_export_import_with_timers(shape):
+    q = ABSENT[shape]
+    n_keys = 64
+    d = _burst_stream(900, n_keys, seed=13)
+    ts = d["ts"]
+    bounds = np.concatenate([[0], np.nonzero(np.diff(ts))[0] + 1, [len(ts)]])
+    cut = len(bounds) // 2
+
+    def drive(e, cq, lo_i, hi_i, out):
+        two = "S1" in q
+        for i in range(lo_i, hi_i):
+            lo, hi = int(bounds[i]), int(bounds[i + 1])
+            e.advance_time(int(ts[lo]))
+            out.append(e.poll())
+            stream = (cq.stream_index("S1") if (i % 3) else cq.stream_index("S2")) if two else 0
+            e.push(stream, lo, ts[lo:hi], [d["symbol"][lo:hi], d["price"][lo:hi], d["volume"][lo:hi]], None,
+                   d["key"][lo:hi])
+            out.append(e.poll())
+
+    cq, ref = _oracle(q, n_keys)
+    ref.advance_time(int(ts[0]) - 5)
+    want = [ref.poll()]
+    drive(ref, cq, 0, len(bounds) - 1, want)
+    ref.advance_time(int(ts[-1]) + 1000)
+    want.append(ref.poll())
+
+    cq, a = _oracle(q, n_keys)
+    a.advance_time(int(ts[0]) - 5)
+    got = [a.poll()]
+    drive(a, cq, 0, cut, got)
+    doc = a.state_export()
+    parsed = sd.parse(doc)
+    assert any(p.queue for k in parsed.keys for p in k.procs)    # armed timers are in the document
+    cq, b = _oracle(q, n_keys)
+    b.state_import(doc)
+    assert b.state_export() == doc
+    drive(b, cq, cut, len(bounds) - 1, got)
+    b.advance_time(int(ts[-1]) + 1000)
+    got.append(b.poll())
+    assert len(got) == len(want)
+    for x, y in zip(got, want):
+        _same(x, y)
+    assert sum(len(m) for m in want) > 0
+
+
+@pytest.mark.parametrize("shape", ["gen_count_pattern", "gen_logical_and", "c2_every_within"])
+def test_reference_map_round_trip(shape):
+    """document -> nested reference map (shared StateEvent / StreamEvent objects) -> document"""
+    q = BATCH_SHAPES[shape]
+    cq, e = _oracle(q, 128)
+    d = synth.stock_ticks(0, 4000, 128, seed=5, rate_per_ms=16)
+    _feed(e, cq, q, 0, d)
+    e.poll()
+    raw = e.state_export()
+    doc = sd.parse(raw)
+    m = sd.to_reference_map(doc)
+    names = sd.proc_names(doc.desc)
+    assert len(set(names)) == len(names)
+    for pk, states in m.items():
+        for name in names:
+            st = states[name]
+            assert set(st) >= {"FirstEvent", "PendingStateEventList", "NewAndEveryStateEventList",
+                               "Initialized", "Started"}
+            for se in st["PendingStateEventList"] + st["NewAndEveryStateEventList"]:
+                assert isinstance(se, sd.StateEventState)
+    by_seq = {(k.key, s.seq): s for k in doc.keys for s in k.streams}
+    key_of = {}
+    for k in doc.keys:
+        key_of[str(k.key)] = k.key
+
+    def bits(ev):
+        return ev.data, 0, (1 << len(ev.data)) - 1 if ev.data else 0
+
+    back = sd.from_reference_map(m, doc.desc, doc.n_slots, key_id=int, event_bits=bits, now=doc.now,
+                                 last_event_ts=doc.last_event_ts, clock_flags=doc.clock_flags)
+    assert sd.logical(back, seed_ts=True) == sd.logical(doc, seed_ts=True)
+    # the map keeps the document's object sharing: re-importing it gives the same engine state
+    cq, f = _oracle(q, 128)
+    for k in back.keys:
+        for s in k.streams:
+            s.null_bits = by_seq[(k.key, s.seq)].null_bits
+            s.present = by_seq[(k.key, s.seq)].present
+    f.state_import(sd.write(back))
+    assert f.state_export() == raw
+
+
+def test_import_refuses_malformed_documents():
+    q = SHAPES["c2_every_within"]
+    cq, e = _oracle(q, 64)
+    d = synth.stock_ticks(0, 2000, 64, seed=3, rate_per_ms=8)
+    _feed(e, cq, q, 0, d)
+    e.poll()
+    doc = e.state_export()
+    cq, f = _oracle(q, 64)
+    with pytest.raises(sa.EngineError):
+        f.state_import(doc[:-3])                      # truncated
+    with pytest.raises(sa.EngineError):
+        f.state_import(b"XXXX" + doc[4:])             # not a document
+    cq3, g = _oracle(GENERAL["three_states"], 64)
+    with pytest.raises(sa.EngineError):
+        g.state_import(doc)                           # another query shape
+
+
+# ---- through the runtime API and across shards ----------------------------------------------------------
+RT_APP = """
+define stream S (symbol string, price float, volume int);
+partition with (symbol of S)
+begin
+  @info(name = 'q')
+  from every e1=S[price > 20] -> e2=S[price > e1.price] within 10 sec
+  select e1.symbol as symbol, e1.price as p1, e2.price as p2 insert into O;
+end;
+"""
+
+
+def _runtime(app=RT_APP):
+    from oracle_backend import oracle_factory
+    m = sa.SiddhiManager(engine_factory=oracle_factory(), n_keys=64)
+    rt = m.createSiddhiAppRuntime(app)
+    got = []
+    rt.addCallback("q", lambda ts, i, r: got.extend([list(e.data) for e in i]))
+    rt.start()
+    return rt, got
+
+
+def test_runtime_snapshot_states_is_the_reference_map():
+    rt, got = _runtime()
+    rt.getInputHandler("S").send([sa.Event(1000, ["IBM", 25.0, 10]), sa.Event(1001, ["WSO2", 30.0, 5]),
+                                  sa.Event(1002, ["IBM", 21.0, 7])])
+    st = rt.snapshot_states()["q"]
+    assert set(st) == {"IBM", "WSO2"}                    # partition keys as the partition's String values
+    ibm = st["IBM"]
+    e1, e2 = ibm["StreamPreStateProcessor:e1"], ibm["StreamPreStateProcessor:e2"]
+    assert e1["Initialized"] and not e2["Initialized"]   # init() ran for the start state only
+    # every e1: the start state's clone waits in newAndEvery; both IBM partials wait for e2, the second one
+    # still in newAndEvery (promoted at the next event)
+    assert len(e1["PendingStateEventList"]) == 0 and len(e1["NewAndEveryStateEventList"]) == 1
+    pend, new = e2["PendingStateEventList"], e2["NewAndEveryStateEventList"]
+    assert [s.chain(0)[0].data for s in pend + new] == [["IBM", 25.0, 10], ["IBM", 21.0, 7]]
+    assert [s.timestamp for s in pend + new] == [1000, 1002]
+
+    rt2, got2 = _runtime()
+    rt2.restore_states(rt.snapshot_states())
+    for r in (rt, rt2):
+        r.getInputHandler("S").send([sa.Event(1003, ["IBM", 26.0, 1]), sa.Event(1004, ["WSO2", 31.0, 2])])
+    assert got == got2 and len(got) == 3
+
+
+def test_runtime_restore_states_from_a_hand_built_map():
+    """a map written by hand (as a reference user's persisted state would be) drives the engine"""
+    rt, got = _runtime()
+    rt.getInputHandler("S").send([sa.Event(1000, ["IBM", 25.0, 10])])
+    m = rt.snapshot_states()
+    ev = sd.StreamEventState(10**6, 999, ["ORCL", 22.5, 3], stream="S")
+    partial = sd.StateEventState(999, 0, [ev, None])
+    m["q"]["ORCL"] = {"StreamPreStateProcessor:e1": {"PendingStateEventList": [],
+                                                     "NewAndEveryStateEventList": [sd.StateEventState(999, 0, [None, None])],
+                                                     "Initialized": True, "Started": False},
+                      "StreamPreStateProcessor:e2": {"PendingStateEventList": [partial],
+                                                     "NewAndEveryStateEventList": [],
+                                                     "Initialized": False, "Started": False}}
+    rt2, got2 = _runtime()
+    rt2.restore_states(m)
+    rt2.getInputHandler("S").send([sa.Event(1005, ["ORCL", 23.0, 1])])
+    assert got2 == [["ORCL", np.float32(22.5), np.float32(23.0)]]
+
+
+@pytest.mark.parametrize("shape", ["c2_every_within", "gen_count_pattern", "gen_logical_or"])
+def test_sharded_state_document_equals_single_engine(shape):
+    q = BATCH_SHAPES[shape]
+    n_keys, batch = 300, 6000
+    app = sa.parse_app(q)
+    cq = sa.compile_query(app, app.queries[0], sa.StringDictionary())
+    lib = build_oracle()
+    one = sa.NativeEngine(lib, "sgo_", cq.ir, n_keys=n_keys)
+    shd = sa.ShardedEngine(lib, "sgo_", cq.ir, n_keys=n_keys, devices=(0, 1, 2))
+    data = [(b * batch, synth.stock_ticks(b * batch, batch, n_keys, seed=30 + b, rate_per_ms=16)) for b in range(4)]
+    for seq, d in data[:2]:
+        for e in (one, shd):
+            _feed(e, cq, q, seq, d)
+        _same(one.poll(), shd.poll())
+    d1, d3 = sd.parse(one.state_export()), sd.parse(shd.state_export())
+    assert sd.logical(d1) == sd.logical(d3)
+    # the single engine's document split across three fresh shards continues exactly
+    shd2 = sa.ShardedEngine(lib, "sgo_", cq.ir, n_keys=n_keys, devices=(0, 1, 2))
+    shd2.state_import(one.state_export())
+    for seq, d in data[2:]:
+        for e in (one, shd2):
+            _feed(e, cq, q, seq, d)
+        _same(one.poll(), shd2.poll())
