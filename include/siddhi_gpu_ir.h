@@ -98,6 +98,24 @@ enum sg_node_tag {
 
 enum sg_logical_type { SG_L_AND = 1, SG_L_OR = 2 };
 
+/* Projection programs (sg_set_projection): item_type = result type code | aggregator << 8 | role bits.
+ * Items come in QuerySelector order: first one item per aggregator (its argument program; empty for
+ * count()), then the select list, then at most one `having` condition.  Inside the select items and
+ * `having`, VAR b = SG_PROJ_SLOT_AGG reads aggregator w1's current value and b = SG_PROJ_SLOT_OUT reads
+ * select item w1 of the same output row (`having` over output attributes, QuerySelector.java:120-160). */
+enum sg_proj_agg {
+    SG_AGG_NONE = 0,
+    SG_AGG_COUNT = 1, /* CountAttributeAggregatorExecutor: LONG, every event */
+    SG_AGG_SUM = 2,   /* SumAttributeAggregatorExecutor: LONG for int/long arguments, DOUBLE otherwise */
+    SG_AGG_AVG = 3,   /* AvgAttributeAggregatorExecutor: DOUBLE sum / count */
+    SG_AGG_MIN = 4,   /* Min(Forever)AttributeAggregatorExecutor: the argument's type */
+    SG_AGG_MAX = 5    /* Max(Forever)AttributeAggregatorExecutor */
+};
+#define SG_PROJ_AGG_ITEM 0x10000u  /* item_type bit: this item is an aggregator's argument */
+#define SG_PROJ_HAVING 0x20000u    /* item_type bit: this item is the `having` condition (BOOL) */
+#define SG_PROJ_SLOT_AGG 0xFDu
+#define SG_PROJ_SLOT_OUT 0xFEu
+
 enum sg_opcode {
     SG_OP_VAR = 1,
     SG_OP_CONST = 2,

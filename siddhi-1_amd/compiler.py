@@ -31,6 +31,10 @@ SG_IR_F_PLAYBACK = 2
 SG_COUNT_ANY = 0x7FFFFFFF
 
 TYPE_CODE = {"STRING": 0, "INT": 1, "LONG": 2, "FLOAT": 3, "DOUBLE": 4, "BOOL": 5}
+# projection roles (include/siddhi_gpu_ir.h)
+AGG_CODE = {"count": 1, "sum": 2, "avg": 3, "min": 4, "max": 5, "minForever": 4, "maxForever": 5}
+PROJ_AGG_ITEM, PROJ_HAVING = 0x10000, 0x20000
+PROJ_SLOT_AGG, PROJ_SLOT_OUT = 0xFD, 0xFE
 CODE_TYPE = {v: k for k, v in TYPE_CODE.items()}
 
 N_STREAM, N_NEXT, N_EVERY, N_LOGICAL, N_COUNT = 1, 2, 3, 4, 5
@@ -343,6 +347,16 @@ class _Emitter:
             self.w(v.attr_idx, v.chain_index)
             self.cvt(v.type, want)
             return
+        if k == "agg":   # the aggregator's current value (SG_PROJ_SLOT_AGG, after its processAdd)
+            self.hdr(OP_VAR, TYPE_CODE[t.type], PROJ_SLOT_AGG)
+            self.w(t.idx, 0)
+            self.cvt(t.type, want)
+            return
+        if k == "out":   # select item `idx` of the same output row (having over output attributes)
+            self.hdr(OP_VAR, TYPE_CODE[t.type], PROJ_SLOT_OUT)
+            self.w(t.idx, 0)
+            self.cvt(t.type, want)
+            return
         if k == "isnull_ev":
             self.hdr(OP_ISNULL_EV, 0, t.slot)
             self.w(t.chain)
@@ -641,21 +655,38 @@ def _has_kind(t, kinds):
 
 
 def projection_program(cq: CompiledQuery, strings):
-    """The select list as device expression programs (sg_set_projection), or None when the selector must
-    run on the host: aggregators, group by / having (QuerySelector.processInBatch*, order-dependent
-    per-partition state), multi-valued count attributes (OBJECT lists), instanceOf checks.
+    """The selector as device expression programs (sg_set_projection), or None when it must run on the
+    host: group by (per-group aggregator states), distinctCount, multi-valued count attributes (OBJECT
+    lists), instanceOf checks.  Items in QuerySelector order (siddhi_gpu_ir.h): one argument program per
+    aggregator (empty for count()), the select list (reading aggregator values through
+    SG_PROJ_SLOT_AGG), then `having` (reading output attributes through SG_PROJ_SLOT_OUT).
     Returns (code words, item pc, item len, item type codes, partition attribute per IR stream)."""
-    if cq.aggregators or cq.group_by or cq.having is not None:
+    if cq.group_by:
         return None
     em = _Emitter(strings)
     pcs, lens, types = [], [], []
-    for name, typ, t in cq.select:
-        if typ not in TYPE_CODE or _has_kind(t, ("agg", "instof", "out")):
-            return None
+
+    def item(t, code):
         pcs.append(len(em.code))
-        em.emit(t)
+        if t is not None:
+            em.emit(t)
         lens.append(len(em.code) - pcs[-1])
-        types.append(TYPE_CODE[typ])
+        types.append(code)
+
+    for a in cq.aggregators:
+        if a.fn not in AGG_CODE or (a.arg is not None and (a.arg.type not in TYPE_CODE or
+                                                           _has_kind(a.arg, ("agg", "instof", "out")))):
+            return None
+        at = a.arg.type if a.arg is not None else "LONG"
+        item(a.arg, TYPE_CODE[at] | (AGG_CODE[a.fn] << 8) | PROJ_AGG_ITEM)
+    for name, typ, t in cq.select:
+        if typ not in TYPE_CODE or _has_kind(t, ("instof", "out")):
+            return None
+        item(t, TYPE_CODE[typ])
+    if cq.having is not None:
+        if _has_kind(cq.having, ("instof",)):
+            return None
+        item(cq.having, TYPE_CODE["BOOL"] | PROJ_HAVING)
     part = []
     for s in cq.streams:
         attr = cq.partition_keys.get(s.name) if cq.partitioned else None

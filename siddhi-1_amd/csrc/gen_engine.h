@@ -35,7 +35,8 @@ __host__ __device__ inline size_t gen_at(uint32_t K, uint32_t blockWords, uint32
 #define GEN_MAXSLOT 16   // state slots
 #define GEN_MAXA 16      // attributes per stream
 #define GEN_MAXCODE 1024 // filter (+ projection) bytecode words
-#define GEN_MAXPROJ 32   // select-list items projected on the device
+#define GEN_MAXPROJ 32   // selector items projected on the device (aggregator arguments + select + having)
+#define GEN_MAXAGG 16    // aggregators of the selector on the device
 #define GEN_NONE (-1)
 #define GEN_NIL 0xffffu  // null pool index
 #define GEN_RAWSEG 256   // raw-match reservation counters of a batch
@@ -90,9 +91,13 @@ struct GenProgram {
     uint32_t ksWords;                       // words of one processor's KeyState
     uint32_t offKS, offST, offSTfree, offSE, offSEfree, offDef, blockWords;
     uint32_t stWords, seWords, DEF;
-    // on-device projection of the select list (sg_set_projection): item i = code[projPc[i], +projLen[i])
-    uint32_t projN, projOff;              // items; their words in a raw match record (3 per item)
-    uint32_t projPc[GEN_MAXPROJ], projLen[GEN_MAXPROJ];
+    // on-device projection of the select list (sg_set_projection): item i = code[projPc[i], +projLen[i]);
+    // items [0, projAgg) are aggregator arguments (siddhi_gpu_ir.h), the rest the select list and the optional
+    // `having`, whose values go to the raw match record (3 words each from projOff)
+    uint32_t projN, projOff;
+    uint32_t projAgg;                     // aggregators; their per-key state: 5 words each from offAgg
+    uint32_t offAgg;                      //   (count lo/hi, value lo/hi, has-value)
+    uint32_t projPc[GEN_MAXPROJ], projLen[GEN_MAXPROJ], projType[GEN_MAXPROJ];
 };
 
 // KeyState field offsets inside a processor's record

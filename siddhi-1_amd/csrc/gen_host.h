@@ -19,7 +19,7 @@ int gen_advance(GenEngine* e, int64_t now, std::string& msg);
 int gen_poll(GenEngine* e, uint32_t mem, sg_match_batch* out, std::string& msg);
 // on-device projection of the select list (sg_set_projection / sg_get_projection)
 int gen_set_projection(GenEngine* e, const uint32_t* code, uint32_t words, const uint32_t* pc, const uint32_t* len,
-                       uint32_t n, std::string& msg);
+                       const uint32_t* types, uint32_t n, std::string& msg);
 int gen_get_projection(GenEngine* e, uint32_t mem, sg_projection* out, std::string& msg);
 void gen_release(GenEngine* e);
 void gen_stats(GenEngine* e, sg_stats* out);

@@ -940,40 +940,73 @@ int gen_poll(GenEngine* e, uint32_t mem, sg_match_batch* out, std::string& msg) 
 }
 
 int gen_set_projection(GenEngine* e, const uint32_t* code, uint32_t words, const uint32_t* pc, const uint32_t* len,
-                       uint32_t n, std::string& msg) {
+                       const uint32_t* types, uint32_t n, std::string& msg) {
     GenProgram& G = e->host;
     if (e->st.batches != 0 || e->held) { msg = "set the projection before the first push"; return SG_ERR_STATE; }
     if (G.projN) { msg = "the projection is already set"; return SG_ERR_STATE; }
     if (n > GEN_MAXPROJ) { msg = "too many select items for the device projection"; return SG_ERR_UNSUPPORTED; }
     if (G.ncode + words > GEN_MAXCODE) { msg = "select list too long for the device projection"; return SG_ERR_UNSUPPORTED; }
-    for (uint32_t i = 0; i < n; i++)
+    // roles (siddhi_gpu_ir.h): aggregator arguments, then the select list, then at most one `having`
+    uint32_t A = 0, S = 0, H = 0;
+    for (uint32_t i = 0; i < n; i++) {
         if (pc[i] + len[i] > words) { msg = "projection item outside its code"; return SG_ERR_INVALID; }
-    for (uint32_t w = 0; w < words;) {  // every opcode known, every slot in range
-        const uint32_t op = code[w] & 0xffu, b = (code[w] >> 16) & 0xffu;
-        const bool known = op == SG_OP_VAR || op == SG_OP_CONST || op == SG_OP_CVT || op == SG_OP_ISNULL_EV ||
-                           (op >= SG_OP_ADD && op <= SG_OP_MOD) || (op >= SG_OP_EQ && op <= SG_OP_LE) ||
-                           (op >= SG_OP_AND && op <= SG_OP_ISNULL) || op == SG_OP_IFELSE;
-        if (!known) { msg = "unknown opcode in the projection"; return SG_ERR_INVALID; }
-        if ((op == SG_OP_VAR || op == SG_OP_ISNULL_EV) && b >= (uint32_t)G.nslots) {
-            msg = "projection reads a slot the query does not have";
-            return SG_ERR_INVALID;
+        if (types[i] & SG_PROJ_AGG_ITEM) {
+            const uint32_t fn = (types[i] >> 8) & 0xffu;
+            if (S || H || fn < SG_AGG_COUNT || fn > SG_AGG_MAX) { msg = "malformed aggregator item"; return SG_ERR_INVALID; }
+            A++;
+        } else if (types[i] & SG_PROJ_HAVING) {
+            if (H) { msg = "more than one having item"; return SG_ERR_INVALID; }
+            H = 1;
+        } else {
+            if (H) { msg = "select items after the having item"; return SG_ERR_INVALID; }
+            S++;
         }
-        w += (op == SG_OP_VAR || op == SG_OP_CONST) ? 3 : (op == SG_OP_ISNULL_EV ? 2 : 1);
+    }
+    if (A > GEN_MAXAGG) { msg = "too many aggregators for the device projection"; return SG_ERR_UNSUPPORTED; }
+    for (uint32_t i = 0; i < n; i++) {  // every opcode known, every slot in range
+        for (uint32_t w = pc[i]; w < pc[i] + len[i];) {
+            const uint32_t op = code[w] & 0xffu, b = (code[w] >> 16) & 0xffu;
+            const bool known = op == SG_OP_VAR || op == SG_OP_CONST || op == SG_OP_CVT || op == SG_OP_ISNULL_EV ||
+                               (op >= SG_OP_ADD && op <= SG_OP_MOD) || (op >= SG_OP_EQ && op <= SG_OP_LE) ||
+                               (op >= SG_OP_AND && op <= SG_OP_ISNULL) || op == SG_OP_IFELSE;
+            if (!known) { msg = "unknown opcode in the projection"; return SG_ERR_INVALID; }
+            const uint32_t ow = (op == SG_OP_VAR || op == SG_OP_CONST) ? 3 : (op == SG_OP_ISNULL_EV ? 2 : 1);
+            if (w + ow > pc[i] + len[i]) { msg = "projection item truncated"; return SG_ERR_INVALID; }
+            if (op == SG_OP_VAR && (b == SG_PROJ_SLOT_AGG || b == SG_PROJ_SLOT_OUT)) {
+                const uint32_t x = code[w + 1];
+                if (b == SG_PROJ_SLOT_AGG ? (i < A || x >= A) : (!(H && i == n - 1) || x >= S)) {
+                    msg = "projection reads an aggregator or output item it cannot see";
+                    return SG_ERR_INVALID;
+                }
+            } else if ((op == SG_OP_VAR || op == SG_OP_ISNULL_EV) && b >= (uint32_t)G.nslots) {
+                msg = "projection reads a slot the query does not have";
+                return SG_ERR_INVALID;
+            }
+            w += ow;
+        }
     }
     memcpy(G.code + G.ncode, code, (size_t)words * 4);
     for (uint32_t i = 0; i < n; i++) {
         G.projPc[i] = G.ncode + pc[i];
         G.projLen[i] = len[i];
+        G.projType[i] = types[i];
     }
     G.ncode += words;
     G.projN = n;
+    G.projAgg = A;
     G.projOff = e->recWords;
-    e->recWords += 3 * n;
+    e->recWords += 3 * (S + H);
+    if (A) {  // the aggregators' per-key state joins the key blocks (no push yet: all zero)
+        G.offAgg = G.blockWords;
+        G.blockWords += 5 * A;
+        e->state = e->dalloc<uint32_t>((size_t)G.blockWords * e->K);
+        GH_OK(hipMemset(e->state, 0, (size_t)G.blockWords * e->K * 4));
+    }
     e->raw = e->dalloc<uint32_t>(e->rawCap * e->recWords);  // (the smaller record buffer is freed at destroy)
     e->out.recWords = e->recWords;
-    e->out.pval = e->dalloc<uint64_t>(e->mcap * n);
-    e->out.pnull = e->dalloc<uint8_t>(e->mcap * n);
-    e->out.projN = n;
+    e->out.pval = e->dalloc<uint64_t>(e->mcap * (S + H));
+    e->out.pnull = e->dalloc<uint8_t>(e->mcap * (S + H));
+    e->out.projN = S + H;
     e->out.projOff = G.projOff;
     GH_OK(hipMemcpy(e->dprog, &G, sizeof(GenProgram), hipMemcpyHostToDevice));
     return SG_OK;
@@ -981,8 +1014,8 @@ int gen_set_projection(GenEngine* e, const uint32_t* code, uint32_t words, const
 
 int gen_get_projection(GenEngine* e, uint32_t mem, sg_projection* out, std::string& msg) {
     if (!e->held) { msg = "poll the matches first"; return SG_ERR_STATE; }
-    const uint32_t n = e->host.projN;
-    if (!n) { msg = "no projection set"; return SG_ERR_STATE; }
+    const uint32_t n = e->out.projN;   // output items: select list + having
+    if (!e->host.projN) { msg = "no projection set"; return SG_ERR_STATE; }
     out->n = e->polled;
     out->n_items = n;
     if (mem == SG_MEM_DEVICE) {  // item i of match m at i * capacity + m

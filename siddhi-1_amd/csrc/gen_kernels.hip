@@ -358,14 +358,40 @@ struct Lane {
         return !v.null && (v.b & 1);
     }
 
-    // QuerySelector.processNoGroupBy (QuerySelector.java:162-206) at emission: the select list over the
-    // state event's slots, 3 words per item (value lo, hi, null)
+    // QuerySelector.processNoGroupBy (QuerySelector.java:162-206) at emission, in this key's output order:
+    // each aggregator's processAdd over its argument (java_ops.h jo_agg, per-key state in the block), then
+    // the select list (reading the aggregators' values) and `having` (reading the output row), 3 words per
+    // output item (value lo, hi, null)
     __device__ __noinline__ void projectSelect(uint32_t se, gu32* pv) __restrict__ {
-        for (uint32_t i = 0; i < G.projN; i++) {
-            const GVal v = evalv(se, G.code, G.projPc[i], G.projLen[i]);
-            pv[3 * i] = (uint32_t)v.b;
-            pv[3 * i + 1] = (uint32_t)(v.b >> 32);
-            pv[3 * i + 2] = v.null ? 1u : 0u;
+        GVal aggres[GEN_MAXAGG];
+        for (uint32_t a = 0; a < G.projAgg; a++) {
+            const GVal arg = G.projLen[a] ? evalv(se, G.code, G.projPc[a], G.projLen[a]) : GVal{0, true};
+            const uint32_t base = G.offAgg + 5 * a;
+            int64_t n = R64(base);
+            uint64_t v = (uint64_t)R64(base + 2);
+            bool has = W(base + 4) != 0;
+            aggres[a] = jo_agg((G.projType[a] >> 8) & 0xffu, (int)(G.projType[a] & 0xffu), arg, n, v, has);
+            W64(base, n);
+            W64(base + 2, (int64_t)v);
+            W(base + 4) = has ? 1u : 0u;
+        }
+        for (uint32_t i = G.projAgg; i < G.projN; i++) {
+            const GVal v = jo_eval(G.code, G.projPc[i], G.projLen[i], err,
+                                   [&](uint32_t slot, uint32_t attr, int32_t chain) -> GVal {
+                                       if (slot == SG_PROJ_SLOT_AGG) return attr < GEN_MAXAGG ? aggres[attr] : GVal{0, true};
+                                       if (slot == SG_PROJ_SLOT_OUT)
+                                           return GVal{(uint64_t)pv[3 * attr] | ((uint64_t)pv[3 * attr + 1] << 32),
+                                                       pv[3 * attr + 2] != 0};
+                                       const uint32_t e = chainAt(se, (int)slot, chain);
+                                       if (e == GEN_NIL) return GVal{0, true};
+                                       return GVal{(uint64_t)R64(sew(e, SE_ATTR + 2 * attr)),
+                                                   ((W(sew(e, SE_NULL)) >> attr) & 1u) != 0};
+                                   },
+                                   [&](uint32_t slot, int32_t chain) -> bool { return chainAt(se, (int)slot, chain) == GEN_NIL; });
+            const uint32_t j = i - G.projAgg;
+            pv[3 * j] = (uint32_t)v.b;
+            pv[3 * j + 1] = (uint32_t)(v.b >> 32);
+            pv[3 * j + 2] = v.null ? 1u : 0u;
         }
     }
 

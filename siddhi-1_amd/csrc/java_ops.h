@@ -207,3 +207,71 @@ __device__ __forceinline__ GVal jo_eval(CodePtr code, uint32_t pc, uint32_t n, u
     }
     return sp > 0 ? t0 : GVal{0, true};
 }
+
+// One aggregator's processAdd for a CURRENT event of one partition key (AttributeAggregatorExecutor.java:
+// 60-100 over Count / Sum / Avg / Min / Max*AttributeAggregatorExecutor.java): `arg` of type `at`, the
+// per-key state (n events added, v value bits, has = a value exists); returns the aggregator's value after
+// the event.  A null argument leaves the state and returns the current value (null before any value).
+// Sums add in arrival order from 0 / 0.0, like the reference's running sums.
+__device__ __forceinline__ GVal jo_agg(uint32_t fn, int at, GVal arg, int64_t& n, uint64_t& v, bool& has) {
+    if (fn == SG_AGG_COUNT) {
+        n += 1;
+        return {(uint64_t)n, false};
+    }
+    const bool wide_int = at == SG_T_INT || at == SG_T_LONG;
+    if (fn == SG_AGG_SUM || fn == SG_AGG_AVG) {
+        if (!arg.null) {
+            if (fn == SG_AGG_SUM && wide_int) {
+                const int64_t x = at == SG_T_INT ? (int64_t)(int32_t)(uint32_t)arg.b : (int64_t)arg.b;
+                v = (uint64_t)((has ? (int64_t)v : 0) + x);   // two's-complement wrap, as long addition
+            } else {
+                double x = 0.0;
+                switch (at) {
+                case SG_T_INT: x = (double)(int32_t)(uint32_t)arg.b; break;
+                case SG_T_LONG: x = (double)(int64_t)arg.b; break;
+                case SG_T_FLOAT: x = (double)gf32(arg.b); break;
+                default: x = gf64(arg.b);
+                }
+                v = gbf64(__dadd_rn(has ? gf64(v) : 0.0, x));
+            }
+            has = true;
+            n += 1;
+        }
+        if (!has) return {0, true};
+        if (fn == SG_AGG_SUM) return {v, false};
+        return {gbf64(__ddiv_rn(gf64(v), (double)n)), false};
+    }
+    // min / max in the argument's domain
+    if (!arg.null) {
+        bool take = !has;
+        if (!take) {
+            switch (at) {
+            case SG_T_INT: {
+                const int32_t c = (int32_t)(uint32_t)v, x = (int32_t)(uint32_t)arg.b;
+                take = fn == SG_AGG_MIN ? c > x : c < x;
+                break;
+            }
+            case SG_T_LONG: {
+                const int64_t c = (int64_t)v, x = (int64_t)arg.b;
+                take = fn == SG_AGG_MIN ? c > x : c < x;
+                break;
+            }
+            case SG_T_FLOAT: {
+                const float c = gf32(v), x = gf32(arg.b);
+                take = fn == SG_AGG_MIN ? c > x : c < x;
+                break;
+            }
+            default: {
+                const double c = gf64(v), x = gf64(arg.b);
+                take = fn == SG_AGG_MIN ? c > x : c < x;
+            }
+            }
+        }
+        if (take) {
+            v = arg.b;
+            has = true;
+        }
+        n += 1;
+    }
+    return has ? GVal{v, false} : GVal{0, true};
+}

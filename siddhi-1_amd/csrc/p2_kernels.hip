@@ -141,6 +141,10 @@ __global__ void __launch_bounds__(256) k_order_scatter(const ScatterParams s, ui
         const uint32_t tl = j * 256 + threadIdx.x;
         loc[tl] = running + before + incl[j] - c;
         cnt[tl] = (uint16_t)c;
+        if (s.out_first && base + tl < s.n) {  // aggregators: where each trigger's records start
+            const uint64_t r = (*s.out_count + s.tile_off[blockIdx.x] + loc[tl]) % s.capacity;
+            s.out_first[base + tl] = c ? (((uint64_t)c << 32) | r) : 0ull;
+        }
         if (c) {
             fst[tl] = (uint32_t)d[j];
             s.t_desc[base + tl] = 0;
@@ -194,15 +198,24 @@ __global__ void __launch_bounds__(256) k_project(const ProjParams p) {
     const uint64_t total = *p.batch_total, o0 = (*p.out_count - total) % p.capacity;
     uint32_t err = 0;
     if (total > p.capacity) return;  // (the ordering reported the overflow)
+    const uint32_t it0 = p.phase == 0 ? 0u : p.n_agg, it1 = p.phase == 0 ? p.n_agg : p.n_items;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
         uint64_t o = o0 + i;
         if (o >= p.capacity) o -= p.capacity;
         const uint64_t t = p.o_trig[o] - p.seq_base;
         const uint32_t cn = p.o_capnull[o];
-        for (uint32_t it = 0; it < p.n_items; ++it) {
+        for (uint32_t it = it0; it < it1; ++it) {
             const GVal v = jo_eval(
                 p.code, p.item_pc[it], p.item_len[it], err,
                 [&](uint32_t src, uint32_t x, int32_t chain) -> GVal {
+                    if (src == 2) {  // select item x of this row (evaluated before `having`)
+                        const size_t r = (size_t)x * p.capacity + o;
+                        return GVal{p.pval[r], p.pnull[r] != 0};
+                    }
+                    if (src == 3) {  // aggregator x after this row's event (k_agg)
+                        const size_t r = (size_t)x * p.capacity + o;
+                        return GVal{p.aggv[r], p.aggnull[r] != 0};
+                    }
                     if (!(chain == 0 || chain == -1)) return GVal{0, true};  // a single-event slot
                     if (src == 0) {  // e1 capture x
                         const uint32_t w = p.capw_off[x];
@@ -221,15 +234,85 @@ __global__ void __launch_bounds__(256) k_project(const ProjParams p) {
                     return GVal{b, p.col_null[x] && p.col_null[x][t] != 0};
                 },
                 [&](uint32_t, int32_t chain) -> bool { return !(chain == 0 || chain == -1); });
-            p.pval[(size_t)it * p.capacity + o] = v.b;
-            p.pnull[(size_t)it * p.capacity + o] = v.null ? 1 : 0;
+            if (p.phase == 0) {
+                p.aggv[(size_t)it * p.capacity + o] = v.b;
+                p.aggnull[(size_t)it * p.capacity + o] = v.null ? 1 : 0;
+            } else {
+                p.pval[(size_t)(it - p.n_agg) * p.capacity + o] = v.b;
+                p.pnull[(size_t)(it - p.n_agg) * p.capacity + o] = v.null ? 1 : 0;
+            }
         }
     }
     if (err) atomicOr(p.err, (uint32_t)SGD_ERR_PROJ);
 }
 
+// The aggregators of QuerySelector.processNoGroupBy (QuerySelector.java:162-206) run per partition key
+// over the key's matches in output order: one thread per key walks its batch events in arrival order
+// (the key's run of the grouped payload) and each event's records in emission order, applying processAdd
+// (java_ops.h jo_agg) to the argument phase 0 wrote and leaving the aggregator's value in its place.  The
+// state (count, value, has-value) persists per key across batches.
+__global__ void __launch_bounds__(256) k_agg(const AggParams a) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= a.K) return;
+    const uint32_t b = a.seg_begin[k], e = a.seg_end[k];
+    if (b >= e) return;
+    for (uint32_t f = 0; f < a.n_agg; ++f) {
+        const size_t si = (size_t)f * a.K + k;
+        int64_t n = a.st_n[si];
+        uint64_t v = a.st_v[si];
+        bool has = a.st_has[si] != 0;
+        const uint32_t ty = a.agg_type[f];
+        const uint32_t fn = (ty >> 8) & 0xffu;
+        const int at = (int)(ty & 0xffu);
+        bool touched = false;
+        for (uint32_t j = b; j < e; ++j) {
+            const uint32_t t = a.payload[(size_t)j * a.stride];
+            const uint64_t d = a.out_first[t];
+            const uint32_t c = (uint32_t)(d >> 32);
+            uint64_t r = (uint32_t)d;
+            for (uint32_t q = 0; q < c; ++q) {
+                const size_t x = (size_t)f * a.capacity + r;
+                const GVal res = jo_agg(fn, at, GVal{a.aggv[x], a.aggnull[x] != 0}, n, v, has);
+                a.aggv[x] = res.b;
+                a.aggnull[x] = res.null ? 1 : 0;
+                touched = true;
+                if (++r == a.capacity) r = 0;
+            }
+        }
+        if (touched) {
+            a.st_n[si] = n;
+            a.st_v[si] = v;
+            a.st_has[si] = has ? 1 : 0;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_reset_agg(const uint32_t* __restrict__ keys, uint32_t n, uint32_t K,
+                                                   uint32_t n_agg, int64_t* st_n, uint64_t* st_v, uint8_t* st_has) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || keys[i] >= K) return;
+    for (uint32_t f = 0; f < n_agg; ++f) {
+        const size_t si = (size_t)f * K + keys[i];
+        st_n[si] = 0;
+        st_v[si] = 0;
+        st_has[si] = 0;
+    }
+}
+
 int sgd_launch_project(const ProjParams& p, ihipStream_t* stream) {
     hipLaunchKernelGGL(k_project, dim3(1024), dim3(256), 0, stream, p);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int sgd_launch_agg(const AggParams& a, ihipStream_t* stream) {
+    hipLaunchKernelGGL(k_agg, dim3((a.K + 255) / 256), dim3(256), 0, stream, a);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int sgd_launch_reset_agg(const uint32_t* keys, uint32_t n, uint32_t K, uint32_t n_agg, int64_t* st_n, uint64_t* st_v,
+                         uint8_t* st_has, ihipStream_t* stream) {
+    if (n == 0 || n_agg == 0) return 0;
+    hipLaunchKernelGGL(k_reset_agg, dim3((n + 255) / 256), dim3(256), 0, stream, keys, n, K, n_agg, st_n, st_v, st_has);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -142,6 +142,8 @@ struct ScatterParams {
     uint32_t* o_capw;          // [n_capw][capacity] (NULL: no projection)
     uint32_t* o_capnull;
     uint32_t n_capw;
+    uint64_t* out_first;       // aggregators: per batch event, count << 32 | ring position of its first
+                               // record (0: no match); NULL otherwise
 };
 #define SGD_ORDER_TILE 4096  // triggers per workgroup of the ordering kernels (256 threads x 16 rows)
 // On-device projection of the select list (sg_set_projection) for the two-state kernel: after the ordering
@@ -149,6 +151,11 @@ struct ScatterParams {
 // (VAR b = 0, w1 = capture index) and its trigger event's batch columns (VAR b = 1, w1 = attribute).
 #define SGD_MAX_ATTR 16
 #define SGD_MAX_PROJ 32
+#define SGD_MAX_AGG 16
+// Items (siddhi_gpu_ir.h): [0, n_agg) aggregator arguments, then n_sel select items, then the optional
+// `having`.  Phase 0 evaluates the aggregator arguments into aggv; k_agg turns them into the aggregators'
+// values per key in output order; phase 1 evaluates the select items and `having` into pval (VAR src 2 =
+// select item x of the row, src 3 = aggregator x).
 struct ProjParams {
     const uint32_t* code;       // rewritten item bytecode
     const uint32_t* item_pc;    // [n_items]
@@ -167,10 +174,36 @@ struct ProjParams {
     uint64_t capacity;
     const unsigned long long* out_count;     // after the batch (k_bump ran)
     const unsigned long long* batch_total;
-    uint64_t* pval;             // [n_items][capacity]
+    uint64_t* pval;             // [n_items - n_agg][capacity]
     uint8_t* pnull;
     uint32_t* err;
+    uint32_t phase;             // 0: aggregator arguments -> aggv; 1: select + having -> pval
+    uint32_t n_agg;
+    uint64_t* aggv;             // [n_agg][capacity]: argument, then (k_agg) the aggregator's value
+    uint8_t* aggnull;
 };
+// per-key aggregator state in output order (QuerySelector + the aggregators' PartitionStateHolder): one
+// thread per key walks its batch events in arrival order and their matches in emission order
+struct AggParams {
+    uint32_t K, n_agg;
+    const uint32_t* seg_begin;
+    const uint32_t* seg_end;
+    const uint32_t* payload;    // element j's word 0 = its batch position
+    uint32_t stride;            // payload words per element
+    uint32_t pad;
+    const uint64_t* out_first;
+    uint64_t capacity;
+    const uint32_t* agg_type;   // item type of each aggregator (arg type | fn << 8)
+    uint64_t* aggv;
+    uint8_t* aggnull;
+    int64_t* st_n;              // [n_agg][K]
+    uint64_t* st_v;
+    uint8_t* st_has;
+};
+int sgd_launch_agg(const AggParams& a, ihipStream_t* stream);
+// partition purge of the aggregator states of the listed (range-checked) keys
+int sgd_launch_reset_agg(const uint32_t* keys, uint32_t n, uint32_t K, uint32_t n_agg, int64_t* st_n, uint64_t* st_v,
+                         uint8_t* st_has, ihipStream_t* stream);
 int sgd_launch_project(const ProjParams& p, ihipStream_t* stream);
 // ordering of one batch's matches: per-tile sums, their exclusive scan (scan_tmp: rocPRIM scratch of
 // scan_bytes), then the tile-local scan + scatter; also bumps out_count

@@ -78,6 +78,8 @@ struct Plan {
     DProg f0{}, f1{};
 };
 
+uint32_t op_words(uint32_t op) { return (op == SG_OP_VAR || op == SG_OP_CONST) ? 3u : (op == SG_OP_ISNULL_EV ? 2u : 1u); }
+
 uint32_t bits_for(uint64_t n) {
     uint32_t b = 1;
     while (b < 64 && (1ull << b) < n) b++;
@@ -295,6 +297,16 @@ struct sg_engine {
     uint32_t* o_capnull = nullptr;
     uint64_t* pval = nullptr;
     uint8_t* pnull = nullptr;
+    uint32_t proj_out = 0;                // output items: select list + having
+    // aggregators of the selector (QuerySelector + their per-key states, PartitionStateHolder)
+    uint32_t n_agg = 0;
+    const uint32_t* d_agg_type = nullptr;
+    uint64_t* aggv = nullptr;             // [n_agg][mcap] argument, then value, per output record
+    uint8_t* aggnull = nullptr;
+    int64_t* agg_n = nullptr;             // [n_agg][K] per-key state
+    uint64_t* agg_v = nullptr;
+    uint8_t* agg_has = nullptr;
+    uint64_t* out_first = nullptr;        // [max_batch] per batch event: its records (ScatterParams)
     uint64_t polled = 0;
     PinnedVec<uint64_t> h_pval;
     PinnedVec<uint8_t> h_pnull;
@@ -948,9 +960,33 @@ int push(sg_engine* e, const sg_batch* b) {
         sp.o_capw = proj ? e->o_capw : nullptr;
         sp.o_capnull = e->o_capnull;
         sp.n_capw = e->n_capw;
+        sp.out_first = (proj && e->n_agg) ? e->out_first : nullptr;
         if (sgd_launch_scatter(sp, e->scan_tmp, e->scan_tmp_bytes, e->stream) != 0)
             throw HipError("ordering launch failed");
-        if (proj && sgd_launch_project(q, e->stream) != 0) throw HipError("projection launch failed");
+        if (proj) {
+            if (e->n_agg) {  // aggregator arguments, then their per-key values in output order
+                q.phase = 0;
+                if (sgd_launch_project(q, e->stream) != 0) throw HipError("projection launch failed");
+                AggParams ag{};
+                ag.K = pl.partitioned ? e->K : 1u;
+                ag.n_agg = e->n_agg;
+                ag.seg_begin = sl.seg_begin;
+                ag.seg_end = sl.seg_end;
+                ag.payload = (const uint32_t*)sl.pay;
+                ag.stride = stride;
+                ag.out_first = e->out_first;
+                ag.capacity = e->mcap;
+                ag.agg_type = e->d_agg_type;
+                ag.aggv = e->aggv;
+                ag.aggnull = e->aggnull;
+                ag.st_n = e->agg_n;
+                ag.st_v = e->agg_v;
+                ag.st_has = e->agg_has;
+                if (sgd_launch_agg(ag, e->stream) != 0) throw HipError("aggregator launch failed");
+            }
+            q.phase = 1;
+            if (sgd_launch_project(q, e->stream) != 0) throw HipError("projection launch failed");
+        }
     }
     if (e->timing) { o1 = e->ev(); e->mark(o1); e->spans.push_back({o0, o1, 2}); }
     // the slot is free again once this batch's kernels ran; its status goes to the pinned ring
@@ -1068,42 +1104,71 @@ int set_projection(sg_engine* e, const uint32_t* code, uint32_t words, const uin
     if (n == 0 || n > SGD_MAX_PROJ) return fail(SG_ERR_UNSUPPORTED, "select list size outside the device projection");
     for (uint32_t i = 0; i < n; i++)
         if (pc[i] + len[i] > words) return fail(SG_ERR_INVALID, "projection item outside its code");
+    // roles (siddhi_gpu_ir.h): aggregator arguments, then the select list, then at most one `having`
+    uint32_t A = 0, S = 0, H = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        if (types[i] & SG_PROJ_AGG_ITEM) {
+            if (S || H) return fail(SG_ERR_INVALID, "aggregator items must come first");
+            const uint32_t fn = (types[i] >> 8) & 0xffu;
+            if (fn < SG_AGG_COUNT || fn > SG_AGG_MAX) return fail(SG_ERR_INVALID, "unknown aggregator");
+            A++;
+        } else if (types[i] & SG_PROJ_HAVING) {
+            if (H) return fail(SG_ERR_INVALID, "more than one having item");
+            H = 1;
+        } else {
+            if (H) return fail(SG_ERR_INVALID, "select items after the having item");
+            S++;
+        }
+    }
+    if (A > SGD_MAX_AGG) return fail(SG_ERR_UNSUPPORTED, "too many aggregators for the device projection");
     std::vector<uint32_t> c(code, code + words);
     std::vector<uint32_t> caps = pl.caps;
     std::vector<uint32_t> attrs;
     const int32_t part0 = (part_attr && (uint32_t)pl.s0 < n_streams) ? part_attr[pl.s0] : -1;
-    for (uint32_t w = 0; w < words;) {
-        const uint32_t op = c[w] & 0xffu, b = (c[w] >> 16) & 0xffu;
-        const bool known = op == SG_OP_VAR || op == SG_OP_CONST || op == SG_OP_CVT || op == SG_OP_ISNULL_EV ||
-                           (op >= SG_OP_ADD && op <= SG_OP_MOD) || (op >= SG_OP_EQ && op <= SG_OP_LE) ||
-                           (op >= SG_OP_AND && op <= SG_OP_ISNULL) || op == SG_OP_IFELSE;
-        if (!known) return fail(SG_ERR_INVALID, "unknown opcode in the projection");
-        if (op == SG_OP_VAR || op == SG_OP_ISNULL_EV) {
-            if (b != pl.slot0 && b != pl.slot1) return fail(SG_ERR_INVALID, "projection reads an unknown slot");
-        }
-        if (op == SG_OP_VAR) {
-            const uint32_t attr = c[w + 1];
-            uint32_t src, x;
-            if (b == pl.slot1 || (pl.s0 == pl.s1 && (int32_t)attr == part0)) {
-                if (attr >= e->streams[pl.s1].types.size() || attr >= SGD_MAX_ATTR)
-                    return fail(SG_ERR_UNSUPPORTED, "projection attribute outside the device projection");
-                src = 1;
-                x = attr;
-                if (std::find(attrs.begin(), attrs.end(), attr) == attrs.end()) attrs.push_back(attr);
-            } else {
-                if (attr >= e->streams[pl.s0].types.size()) return fail(SG_ERR_INVALID, "attribute out of range");
-                size_t ci = std::find(caps.begin(), caps.end(), attr) - caps.begin();
-                if (ci == caps.size()) {
-                    if (caps.size() >= SGD_MAX_CAPS) return fail(SG_ERR_UNSUPPORTED, "too many captured attributes");
-                    caps.push_back(attr);
-                }
-                src = 0;
-                x = (uint32_t)ci;
+    for (uint32_t i = 0; i < n; i++) {
+        const bool is_agg = i < A, is_having = H && i == n - 1;
+        for (uint32_t w = pc[i]; w < pc[i] + len[i];) {
+            const uint32_t op = c[w] & 0xffu, b = (c[w] >> 16) & 0xffu;
+            const bool known = op == SG_OP_VAR || op == SG_OP_CONST || op == SG_OP_CVT || op == SG_OP_ISNULL_EV ||
+                               (op >= SG_OP_ADD && op <= SG_OP_MOD) || (op >= SG_OP_EQ && op <= SG_OP_LE) ||
+                               (op >= SG_OP_AND && op <= SG_OP_ISNULL) || op == SG_OP_IFELSE;
+            if (!known) return fail(SG_ERR_INVALID, "unknown opcode in the projection");
+            if (w + op_words(op) > pc[i] + len[i]) return fail(SG_ERR_INVALID, "projection item truncated");
+            if (op == SG_OP_VAR && (b == SG_PROJ_SLOT_AGG || b == SG_PROJ_SLOT_OUT)) {
+                const uint32_t x = c[w + 1];
+                if (b == SG_PROJ_SLOT_AGG ? (is_agg || x >= A) : (!is_having || x >= S))
+                    return fail(SG_ERR_INVALID, "projection reads an aggregator or output item it cannot see");
+                c[w] = (c[w] & ~(0xffu << 16)) | ((b == SG_PROJ_SLOT_AGG ? 3u : 2u) << 16);
+                w += 3;
+                continue;
             }
-            c[w] = (c[w] & ~(0xffu << 16)) | (src << 16);
-            c[w + 1] = x;
+            if (op == SG_OP_VAR || op == SG_OP_ISNULL_EV) {
+                if (b != pl.slot0 && b != pl.slot1) return fail(SG_ERR_INVALID, "projection reads an unknown slot");
+            }
+            if (op == SG_OP_VAR) {
+                const uint32_t attr = c[w + 1];
+                uint32_t src, x;
+                if (b == pl.slot1 || (pl.s0 == pl.s1 && (int32_t)attr == part0)) {
+                    if (attr >= e->streams[pl.s1].types.size() || attr >= SGD_MAX_ATTR)
+                        return fail(SG_ERR_UNSUPPORTED, "projection attribute outside the device projection");
+                    src = 1;
+                    x = attr;
+                    if (std::find(attrs.begin(), attrs.end(), attr) == attrs.end()) attrs.push_back(attr);
+                } else {
+                    if (attr >= e->streams[pl.s0].types.size()) return fail(SG_ERR_INVALID, "attribute out of range");
+                    size_t ci = std::find(caps.begin(), caps.end(), attr) - caps.begin();
+                    if (ci == caps.size()) {
+                        if (caps.size() >= SGD_MAX_CAPS) return fail(SG_ERR_UNSUPPORTED, "too many captured attributes");
+                        caps.push_back(attr);
+                    }
+                    src = 0;
+                    x = (uint32_t)ci;
+                }
+                c[w] = (c[w] & ~(0xffu << 16)) | (src << 16);
+                c[w + 1] = x;
+            }
+            w += op_words(op);
         }
-        w += (op == SG_OP_VAR || op == SG_OP_CONST) ? 3 : (op == SG_OP_ISNULL_EV ? 2 : 1);
     }
     try {
         // the new capture list: payload columns, capture layout, JIT code, slabs (empty: no push yet)
@@ -1139,8 +1204,19 @@ int set_projection(sg_engine* e, const uint32_t* code, uint32_t words, const uin
         HIP_OK(hipMemset(e->raw_capnull, 0, e->raw_cap * 4));
         e->o_capw = dalloc<uint32_t>(std::max<size_t>(1, e->n_capw) * M, e->owned);
         e->o_capnull = dalloc<uint32_t>(M, e->owned);
-        e->pval = dalloc<uint64_t>(n * M, e->owned);
-        e->pnull = dalloc<uint8_t>(n * M, e->owned);
+        e->pval = dalloc<uint64_t>((size_t)(S + H) * M, e->owned);
+        e->pnull = dalloc<uint8_t>((size_t)(S + H) * M, e->owned);
+        if (A) {
+            e->aggv = dalloc<uint64_t>((size_t)A * M, e->owned);
+            e->aggnull = dalloc<uint8_t>((size_t)A * M, e->owned);
+            e->agg_n = dalloc<int64_t>((size_t)A * K, e->owned);
+            e->agg_v = dalloc<uint64_t>((size_t)A * K, e->owned);
+            e->agg_has = dalloc<uint8_t>((size_t)A * K, e->owned);
+            HIP_OK(hipMemset(e->agg_n, 0, (size_t)A * K * 8));
+            HIP_OK(hipMemset(e->agg_v, 0, (size_t)A * K * 8));
+            HIP_OK(hipMemset(e->agg_has, 0, (size_t)A * K));
+            e->out_first = dalloc<uint64_t>(e->maxb, e->owned);
+        }
         for (auto& sl : e->slots)
             for (size_t j = 0; j < attrs.size(); j++) {
                 sl.b_pcols.push_back(dalloc<uint64_t>(e->maxb, e->owned));
@@ -1156,6 +1232,9 @@ int set_projection(sg_engine* e, const uint32_t* code, uint32_t words, const uin
         tab.insert(tab.end(), woff.begin(), woff.end());
         const size_t o_ty = tab.size();
         for (uint8_t t : pl.cap_type) tab.push_back(t);
+        tab.push_back(0);
+        const size_t o_at = tab.size();
+        tab.insert(tab.end(), types, types + A);
         tab.push_back(0);
         e->d_proj = dalloc<uint32_t>(tab.size(), e->owned);
         HIP_OK(hipMemcpy(e->d_proj, tab.data(), tab.size() * 4, hipMemcpyHostToDevice));
@@ -1176,7 +1255,10 @@ int set_projection(sg_engine* e, const uint32_t* code, uint32_t words, const uin
         q.pval = e->pval;
         q.pnull = e->pnull;
         q.err = e->err;
-        (void)types;
+        q.n_agg = A;
+        q.aggv = e->aggv;
+        q.aggnull = e->aggnull;
+        e->d_agg_type = e->d_proj + o_at;
         // recompile the advance kernel: matches now carry the partials' captures
         for (auto& kv : e->variants)
             if (kv.second.mod) (void)hipModuleUnload(kv.second.mod);
@@ -1188,6 +1270,8 @@ int set_projection(sg_engine* e, const uint32_t* code, uint32_t words, const uin
         (void)variant(e, false, false);
         e->proj_attrs = attrs;
         e->proj_n = n;
+        e->proj_out = S + H;
+        e->n_agg = A;
     } catch (const std::exception& ex) {
         return fail(SG_ERR_DEVICE, ex.what());
     }
@@ -1319,7 +1403,7 @@ int sg_set_projection(sg_engine* e, const uint32_t* code, uint32_t code_words, c
         HIP_OK(hipSetDevice(e->device));
         if (e->gen) {
             std::string msg;
-            const int rc = gen_set_projection(e->gen, code, code_words, item_pc, item_len, n_items, msg);
+            const int rc = gen_set_projection(e->gen, code, code_words, item_pc, item_len, item_type, n_items, msg);
             return rc == SG_OK ? rc : fail(rc, msg);
         }
         return set_projection(e, code, code_words, item_pc, item_len, item_type, n_items, part_attr, n_streams);
@@ -1339,7 +1423,7 @@ int sg_get_projection(sg_engine* e, uint32_t mem, sg_projection* out) {
         }
         if (!e->held) return fail(SG_ERR_STATE, "poll the matches first");
         if (!e->proj_n) return fail(SG_ERR_STATE, "no projection set");
-        const uint32_t n = e->proj_n;
+        const uint32_t n = e->proj_out;   // select items + having (the aggregators feed them)
         const size_t m = (size_t)e->polled;
         const size_t start = (size_t)((e->win) % e->mcap);
         out->n = m;
@@ -1488,6 +1572,8 @@ int sg_reset_keys(sg_engine* e, const uint32_t* keys, uint64_t n, uint32_t mem) 
             rc = gen_reset_keys(e->gen, dk, (uint32_t)n, msg);
         } else if (e->plan.partitioned) {
             if (sgd_launch_reset_keys(dk, (uint32_t)n, e->K, e->hdr, e->err, e->stream) != 0) rc = SG_ERR_DEVICE;
+            if (sgd_launch_reset_agg(dk, (uint32_t)n, e->K, e->n_agg, e->agg_n, e->agg_v, e->agg_has, e->stream) != 0)
+                rc = SG_ERR_DEVICE;
             msg = "k_reset_keys launch failed";
         }
         HIP_OK(hipStreamSynchronize(e->stream));
@@ -1523,12 +1609,12 @@ struct SnapHeader {
     uint32_t nullable;
     uint64_t next_seq;    // sequence numbers must keep increasing across a restore
     uint32_t have_base;
-    uint32_t pad;
+    uint32_t n_agg;       // two-state: per-key aggregator states in the image (selector aggregators)
     GenClock clk;
     uint64_t body_bytes;
 };
 #define SG_SNAP_MAGIC 0x4e534753u  // "SGSN"
-#define SG_SNAP_VERSION 1u
+#define SG_SNAP_VERSION 2u
 
 static bool outputs_pending(sg_engine* e) {
     sync_all(e);
@@ -1574,8 +1660,9 @@ int sg_snapshot(sg_engine* e, void** buf, size_t* len) {
         h.rows = rows;
         h.n_capw = e->n_capw;
         h.nullable = e->nullable ? 1u : 0u;
+        h.n_agg = e->n_agg;
         const size_t plane = (size_t)rows * K;  // elements per saved plane
-        h.body_bytes = K * 4 + plane * (8 + 8 + 4 * (size_t)e->n_capw + 4);
+        h.body_bytes = K * 4 + plane * (8 + 8 + 4 * (size_t)e->n_capw + 4) + (size_t)e->n_agg * K * 17;
         uint8_t* out = (uint8_t*)malloc(sizeof(h) + h.body_bytes);
         if (!out) return fail(SG_ERR_CAPACITY, "snapshot buffer allocation failed");
         uint8_t* q = out + sizeof(h);
@@ -1590,6 +1677,13 @@ int sg_snapshot(sg_engine* e, void** buf, size_t* len) {
             q += plane * 4;
         }
         HIP_OK(hipMemcpyAsync(q, e->p_capnull, plane * 4, hipMemcpyDeviceToHost, e->stream));
+        q += plane * 4;
+        if (e->n_agg) {
+            const size_t na = (size_t)e->n_agg * K;
+            HIP_OK(hipMemcpyAsync(q, e->agg_n, na * 8, hipMemcpyDeviceToHost, e->stream));
+            HIP_OK(hipMemcpyAsync(q + na * 8, e->agg_v, na * 8, hipMemcpyDeviceToHost, e->stream));
+            HIP_OK(hipMemcpyAsync(q + na * 16, e->agg_has, na, hipMemcpyDeviceToHost, e->stream));
+        }
         HIP_OK(hipStreamSynchronize(e->stream));
         memcpy(out, &h, sizeof(h));
         *buf = out;
@@ -1625,8 +1719,9 @@ int sg_restore(sg_engine* e, const void* buf, size_t len) {
             if (h.K != K) return fail(SG_ERR_INVALID, "snapshot taken with a different n_keys");
             if (h.rows > e->cap) return fail(SG_ERR_CAPACITY, "snapshot holds more partials per key than partial_capacity");
             if (h.n_capw != e->n_capw) return fail(SG_ERR_INVALID, "snapshot capture layout differs");
+            if (h.n_agg != e->n_agg) return fail(SG_ERR_INVALID, "snapshot aggregator layout differs");
             const size_t plane = (size_t)h.rows * K;
-            if (h.body_bytes != K * 4 + plane * (8 + 8 + 4 * (size_t)h.n_capw + 4))
+            if (h.body_bytes != K * 4 + plane * (8 + 8 + 4 * (size_t)h.n_capw + 4) + (size_t)h.n_agg * K * 17)
                 return fail(SG_ERR_INVALID, "snapshot body size does not match its header");
             if (e->held) return fail(SG_ERR_STATE, "release the polled matches before a restore");
             if (outputs_pending(e)) return fail(SG_ERR_STATE, "poll the emitted matches before a restore");
@@ -1641,6 +1736,13 @@ int sg_restore(sg_engine* e, const void* buf, size_t len) {
                 q += plane * 4;
             }
             HIP_OK(hipMemcpyAsync(e->p_capnull, q, plane * 4, hipMemcpyHostToDevice, e->stream));
+            q += plane * 4;
+            if (e->n_agg) {
+                const size_t na = (size_t)e->n_agg * K;
+                HIP_OK(hipMemcpyAsync(e->agg_n, q, na * 8, hipMemcpyHostToDevice, e->stream));
+                HIP_OK(hipMemcpyAsync(e->agg_v, q + na * 8, na * 8, hipMemcpyHostToDevice, e->stream));
+                HIP_OK(hipMemcpyAsync(e->agg_has, q + na * 16, na, hipMemcpyHostToDevice, e->stream));
+            }
             HIP_OK(hipStreamSynchronize(e->stream));
             if (h.nullable) e->nullable = true;
         }

@@ -300,7 +300,8 @@ class NativeEngine:
                                 arr(item_type, np.uint32), arr(part_attr, np.int32))
         self._check(f(self.h, _np_ptr(code), len(code), _np_ptr(pc), _np_ptr(ln), _np_ptr(ty), len(pc), _np_ptr(pa),
                       len(pa)))
-        self.proj_items = len(pc)
+        # output items: the select list and `having` (the aggregator-argument items feed them)
+        self.proj_items = int(np.sum((ty & 0x10000) == 0))
 
     def _check(self, rc):
         if rc != SG_OK:

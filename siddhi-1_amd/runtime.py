@@ -406,9 +406,14 @@ class _QueryRuntime:
 
     def project(self, m, store):
         if self.device_projection and m.proj_value is not None:
-            cols = [self._decode(m.proj_value[i], m.proj_null[i], typ) for i, (_, typ, _) in enumerate(self.cq.select)]
+            sel = self.cq.select
+            cols = [self._decode(m.proj_value[i], m.proj_null[i], typ) for i, (_, typ, _) in enumerate(sel)]
             trig, ts = m.trigger_seq.tolist(), m.ts.tolist()
-            return [(trig[i], ts[i], [c[i] for c in cols]) for i in range(len(m))]
+            keep = range(len(m))
+            if self.cq.having is not None:   # the device evaluated `having` per row: only a non-null true passes
+                h, hn = m.proj_value[len(sel)], m.proj_null[len(sel)]
+                keep = np.nonzero((hn == 0) & ((h & 1) == 1))[0].tolist()
+            return [(trig[i], ts[i], [c[i] for c in cols]) for i in keep]
         return self.project_host(m, store)
 
     def project_host(self, m, store):

@@ -101,3 +101,130 @@ def test_device_projection_equals_host(name):
     host = run(app, False, nulls=(name == "arith_nulls"))
     assert len(dev) == len(host) and len(dev) > 0
     assert bits(dev) == bits(host)
+
+
+# aggregators and `having` on the device (QuerySelector.processNoGroupBy with AttributeAggregatorExecutors,
+# QuerySelector.java:162-206): per-partition-key running states updated in emission order, select items
+# reading them, `having` over the output attributes
+AGG_APPS = {
+    "agg_c2": (STOCK + "partition with (symbol of S) begin @info(name='query1') "
+               "from every e1=S[price>20] -> e2=S[price>e1.price] within 1 sec "
+               "select e1.symbol as s, sum(e2.price) as total, count() as n, avg(e1.price) as a, "
+               "max(e2.volume) as mx, min(e1.price) as mn, e2.price - e1.price as d "
+               "having n > 1 insert into O; end;"),
+    "agg_having_expr": (STOCK + "partition with (symbol of S) begin @info(name='query1') "
+                        "from every e1=S[price>20] -> e2=S[price>e1.price] within 1 sec "
+                        "select sum(e2.volume) as sv, max(e1.price) as mp, count() as n "
+                        "having sv > 2000 and mp < 60.0 or n % 4 == 0 insert into O; end;"),
+    "agg_two_streams": ("define stream S1 (symbol string, price float, volume int);\n"
+                        "define stream S2 (symbol string, price double, volume long);\n"
+                        "partition with (symbol of S1, symbol of S2) begin @info(name='query1') "
+                        "from every e1=S1[price>20] -> e2=S2[price>e1.price] within 1 sec "
+                        "select e1.symbol as s, sum(e2.volume * 1000000000000L) as big, avg(e2.price) as a, "
+                        "min(e2.volume) as mn, sum(e1.volume) as sv, count() as n insert into O; end;"),
+    "agg_nulls": (STOCK + "partition with (symbol of S) begin @info(name='query1') "
+                  "from every e1=S[price>25] -> e2=S[price>e1.price] within 1 sec "
+                  "select sum(e2.volume) as sv, avg(e1.volume) as av, min(e2.volume) as mn, max(e1.volume) as mx, "
+                  "count() as n, sum(e2.price * 1.0) as sp having sv is null or sv > 100 insert into O; end;"),
+    "agg_count_pattern": (STOCK + "partition with (symbol of S) begin @info(name='query1') "
+                          "from every e1=S[price>20]<2:5> -> e2=S[price>e1[last].price] within 1 sec "
+                          "select sum(e1[0].price) as s0, max(e1[last].volume) as mv, count() as n, "
+                          "avg(e2.price - e1[0].price) as ad having n > 2 insert into O; end;"),
+    "agg_sequence": (STOCK + "partition with (symbol of S) begin @info(name='query1') "
+                     "from every e1=S[price>20], e2=S[price>e1.price] "
+                     "select e1.symbol as s, count() as n, sum(e2.price) as t, min(e2.price - e1.price) as md "
+                     "insert into O; end;"),
+}
+
+
+@pytest.mark.parametrize("name", sorted(AGG_APPS))
+def test_device_aggregates_equal_host(name):
+    app = AGG_APPS[name]
+    nulls = name == "agg_nulls"
+    dev = run(app, True, nulls=nulls)
+    host = run(app, False, nulls=nulls)
+    assert len(dev) == len(host) and len(dev) > 0
+    assert bits(dev) == bits(host)
+
+
+def _runtime(app, n_keys=512):
+    lib = sa.load_hip_library()
+    return sa.SiddhiAppRuntime(app, lambda ir, nk: sa.NativeEngine(lib, "sg_", ir, n_keys=nk, max_batch=1 << 14,
+                                                                   partial_capacity=64, match_capacity=1 << 20),
+                               n_keys=n_keys)
+
+
+def _feed_rt(rt, batches):
+    h = rt.getInputHandler("S")
+    for seq, d in batches:
+        h.send([sa.Event(int(d["ts"][i]), [f"K{int(d['key'][i])}", float(d["price"][i]), int(d["volume"][i])])
+                for i in range(len(d["ts"]))])
+
+
+@pytest.mark.parametrize("name", ["agg_c2", "agg_count_pattern"])
+def test_device_aggregates_snapshot_restore(name):
+    """the aggregator states travel with the engine image (SiddhiAppRuntime.snapshot / restore): a runtime
+    restored after batch 2 continues with the same running sums and counts as the uninterrupted one"""
+    app = AGG_APPS[name]
+    n_keys, n = 512, 6000
+    batches = [(b * n, synth.stock_ticks(b * n, n, n_keys, seed=70 + b, rate_per_ms=8)) for b in range(4)]
+    want = []
+    rt = _runtime(app, n_keys)
+    assert rt.queries[0].device_projection
+    rt.addCallback("query1", lambda ts, cur, exp: want.extend((e.timestamp, tuple(e.data)) for e in cur or []))
+    rt.start()
+    _feed_rt(rt, batches)
+    rt.shutdown()
+    got = []
+    a = _runtime(app, n_keys)
+    a.addCallback("query1", lambda ts, cur, exp: got.extend((e.timestamp, tuple(e.data)) for e in cur or []))
+    a.start()
+    _feed_rt(a, batches[:2])
+    image = a.snapshot()
+    a.shutdown()
+    b = _runtime(app, n_keys)
+    b.addCallback("query1", lambda ts, cur, exp: got.extend((e.timestamp, tuple(e.data)) for e in cur or []))
+    b.start()
+    b.restore(image)
+    _feed_rt(b, batches[2:])
+    b.shutdown()
+    assert len(want) > 0 and bits(got) == bits(want)
+
+
+def test_device_aggregates_purged_with_key():
+    """a purged key's aggregator state goes with it (cleanGroupByStates): reused key ids start counting
+    afresh on the device (as test_purge.test_runtime_purge_recycles_key_ids_under_churn on the oracle)"""
+    app = (STOCK + "@purge(enable='true', interval='1 sec', idle.period='1 sec') "
+           "partition with (symbol of S) begin from every e1=S[price>20] -> e2=S[price>e1.price] "
+           "select e1.symbol as s, e1.price as p1, e2.price as p2, count() as c, sum(e2.volume) as sv "
+           "insert into O; end;")
+    lib = sa.load_hip_library()
+    rt = sa.SiddhiAppRuntime(app, lambda ir, nk: sa.NativeEngine(lib, "sg_", ir, n_keys=nk, max_batch=64,
+                                                                 partial_capacity=16, match_capacity=1024),
+                             n_keys=4)
+    assert rt.queries[0].device_projection
+    rows = []
+
+    class CB(sa.StreamCallback):
+        def receive(self, events):
+            rows.extend(list(e.data) for e in events)
+
+    rt.addCallback("O", CB())
+    rt.set_wall_clock(1_000_000)
+    rt.start()
+    h = rt.getInputHandler("S")
+    wall = 1_000_000
+    for gen in range(10):
+        for k in range(4):
+            h.send([f"G{gen}K{k}", 25.0, 1])
+        for k in range(4):
+            h.send([f"G{gen}K{k}", 26.0, 5])
+            h.send([f"G{gen}K{k}", 27.0, 7])
+        wall += 3000
+        rt.advance_wall_clock(wall)
+    rt.shutdown()
+    want = []
+    for g in range(10):
+        for k in range(4):
+            want += [[f"G{g}K{k}", 25.0, 26.0, 1, 5], [f"G{g}K{k}", 26.0, 27.0, 2, 12]]
+    assert sorted([r[0], float(r[1]), float(r[2]), r[3], r[4]] for r in rows) == sorted(want)
