@@ -160,15 +160,39 @@ def to_dev(torch, d, dev):
     return {k: torch.from_numpy(v.view(np.int32) if v.dtype == np.uint32 else v).to(dev) for k, v in d.items()}
 
 
-def run_general(sa, synth, torch, dev, query, make_batch, n_keys, batch, steps, warmup, cap, playback=False):
-    """One of the general-engine configs: events/s over `steps` timed batches (HBM-resident)."""
+def run_general(sa, synth, torch, dev, query, make_batch, n_keys, batch, steps, warmup, cap, playback=False,
+                extra_in=0):
+    """One of the general-engine configs: events/s over `steps` timed batches (HBM-resident), then the
+    same batches again with SG_CFG_TIMING for the roofline of the NFA kernels (k_gen_batch + the timer
+    sweeps): the §8d byte model over their exact counters (extra_in: bytes per event of referenced
+    attributes beyond key/price/ts) / their HIP-event time.  The timing run also counts the touched keys'
+    live partials before each batch, so it is kept apart from `value`."""
     app = sa.parse_app(query)
     cq = sa.compile_query(app, app.queries[0], sa.StringDictionary())
-    eng = sa.NativeEngine(sa.load_hip_library(), "sg_", cq.ir, n_keys=n_keys, max_batch=batch,
-                          partial_capacity=cap, match_capacity=2 * batch, device=dev.index or 0)
     bats = [to_dev(torch, make_batch(s), dev) for s in range(warmup + steps)]
     lastts = [int(b["ts"][-1].item()) for b in bats]
     torch.cuda.synchronize()
+    res = _run_general(sa, cq, bats, lastts, n_keys, batch, steps, warmup, cap, playback, 0, dev)
+    tm = _run_general(sa, cq, bats, lastts, n_keys, batch, steps, warmup, cap, playback,
+                      sa.native.SG_CFG_TIMING, dev)["delta"]
+    d = res.pop("delta")
+    bytes_ = algorithmic_bytes(tm) + extra_in * tm["events"]
+    sec = tm["advance_ns"] / 1e9
+    gbs = bytes_ / sec / 1e9 if sec > 0 else 0.0
+    res["roofline"] = {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                       "frac": gbs / HBM_PEAK_GBS, "traffic": None,
+                       "kernel": "k_gen_batch + k_gen_timers (NFA advance, general engine)",
+                       "alg_bytes_per_step": bytes_ / steps, "kernel_ms_per_step": sec * 1e3 / steps,
+                       "alg_bytes_per_event": bytes_ / max(1, tm["events"]),
+                       "counters_per_step": {k: tm[k] / steps for k in ("keys_touched", "live_at_batch_start",
+                                                                       "partials_created", "matches")}}
+    assert d["matches"] == tm["matches"] and d["partials_created"] == tm["partials_created"]
+    return res
+
+
+def _run_general(sa, cq, bats, lastts, n_keys, batch, steps, warmup, cap, playback, flags, dev):
+    eng = sa.NativeEngine(sa.load_hip_library(), "sg_", cq.ir, n_keys=n_keys, max_batch=batch,
+                          partial_capacity=cap, match_capacity=2 * batch, device=dev.index or 0, flags=flags)
 
     def step(s):
         t = bats[s]
@@ -197,7 +221,7 @@ def run_general(sa, synth, torch, dev, query, make_batch, n_keys, batch, steps, 
     eng.close()
     return {"value": batch * steps / el, "unit": "events/s", "ms_per_step": el / steps * 1e3,
             "keys": n_keys, "batch_events": batch, "matches_per_step": d["matches"] / steps,
-            "partials_scanned_per_step": d["partials_scanned"] / steps, "engine": "general"}
+            "partials_scanned_per_step": d["partials_scanned"] / steps, "engine": "general", "delta": d}
 
 
 def take_all(eng, ready):
@@ -531,11 +555,11 @@ def main():
         cb, c4b = 1 << 22, 1 << 22
         out["other_configs"] = {
             "C3": dict(run_general(sa, synth, torch, dev, synth.C3_QUERY,
-                                   lambda s: synth.stock_ticks(s * cb, cb, K), K, cb, steps, 1, 8),
+                                   lambda s: synth.stock_ticks(s * cb, cb, K), K, cb, steps, 1, 8, extra_in=4),
                        workload="C3: every e1=S[price>20]<2:5>, e2=S[price>e1[last].price] or e3=S[volume>1000] "
                                 "within 10 sec (SEQUENCE), 1,048,576 keys"),
             "C3_min1": dict(run_general(sa, synth, torch, dev, synth.C3_MIN1_QUERY,
-                                        lambda s: synth.stock_ticks(s * cb, cb, K), K, cb, steps, 1, 8),
+                                        lambda s: synth.stock_ticks(s * cb, cb, K), K, cb, steps, 1, 8, extra_in=4),
                             workload="C3 with e1<1:5> (C3 as written emits no match under the reference's "
                                      "SEQUENCE reset semantics, DESIGN.md), 1,048,576 keys"),
             "C4": dict(run_general(sa, synth, torch, dev, synth.C4_QUERY,

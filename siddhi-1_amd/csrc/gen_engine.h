@@ -125,7 +125,7 @@ struct GenProgram {
 #define SE_NULL 6
 #define SE_ATTR 7
 
-enum { GST_SCANNED = 0, GST_CREATED, GST_MATCHES, GST_KEYS, GST_N };
+enum { GST_SCANNED = 0, GST_CREATED, GST_MATCHES, GST_KEYS, GST_LIVE0, GST_N };  // GST_LIVE0: SG_CFG_TIMING only
 enum { GERR_CAP = 1, GERR_MATCHCAP = 2, GERR_KEY = 4, GERR_COLLAPSE = 8, GERR_CHAIN = 16, GERR_REF = 32 };
 
 struct GenBatch {

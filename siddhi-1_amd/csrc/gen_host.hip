@@ -450,10 +450,13 @@ __global__ void k_gen_iota(uint32_t* x, uint64_t n) {
     if (i < n) x[i] = (uint32_t)i;
 }
 
-// live partial matches (StateEvents holding an event) in every list of every processor
-__global__ void k_gen_live(const GenProgram* G, const uint32_t* S, uint32_t K, unsigned long long* out) {
+// live partial matches (StateEvents holding an event) in every list of every processor; with seg_begin /
+// seg_end, of the keys the batch touches only (sg_stats.live_at_batch_start, before the batch kernel)
+__global__ void k_gen_live(const GenProgram* G, const uint32_t* S, uint32_t K, unsigned long long* out,
+                           const uint32_t* seg_begin = nullptr, const uint32_t* seg_end = nullptr) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= K) return;
+    if (seg_begin && seg_begin[k] >= seg_end[k]) return;
     unsigned long long live = 0;
     for (int p = 0; p < G->nprocs; p++) {
         const uint32_t ks = G->offKS + (uint32_t)p * G->ksWords;
@@ -543,6 +546,17 @@ struct GenEngine {
     int64_t lastEventTs = 0;
     bool advanced = false;
     sg_stats st{};
+    // SG_CFG_TIMING: HIP events around the NFA kernels (batch + timer sweeps: advance_ns) and the
+    // grouping (group_ns), resolved by gen_stats; the touched keys' live partials counted before each batch
+    bool timing = false;
+    struct Span { hipEvent_t a, b; int which; };
+    std::vector<Span> spans;
+    hipEvent_t ev() {
+        hipEvent_t x;
+        GH_OK(hipEventCreate(&x));
+        GH_OK(hipEventRecord(x, stream));
+        return x;
+    }
 
     template <class T> T* dalloc(size_t n) {
         void* p = nullptr;
@@ -552,6 +566,7 @@ struct GenEngine {
     }
     ~GenEngine() {
         if (stream) (void)hipStreamSynchronize(stream);
+        for (auto& x : spans) { (void)hipEventDestroy(x.a); (void)hipEventDestroy(x.b); }
         for (void* p : owned) (void)hipFree(p);
         if (h_args) (void)hipHostFree(h_args);
     }
@@ -591,6 +606,7 @@ GenEngine* gen_create(const uint32_t* ir, size_t nw, const sg_config& cfg, hipSt
         e->stream = stream;
         e->K = e->host.partitioned ? (cfg.n_keys ? cfg.n_keys : 1) : 1;
         e->null_keys = (cfg.flags & SG_CFG_NULL_KEYS) != 0;
+        e->timing = (cfg.flags & SG_CFG_TIMING) != 0;
         e->maxb = cfg.max_batch ? cfg.max_batch : (1u << 20);
         e->mcap = cfg.match_capacity ? cfg.match_capacity : (uint64_t)e->maxb * 4;
         const GenProgram& G = e->host;
@@ -602,7 +618,7 @@ GenEngine* gen_create(const uint32_t* ir, size_t nw, const sg_config& cfg, hipSt
         e->dprog = e->dalloc<GenProgram>(1);
         GH_OK(hipMemcpy(e->dprog, &e->host, sizeof(GenProgram), hipMemcpyHostToDevice));
         e->state = e->dalloc<uint32_t>((size_t)G.blockWords * K);
-        GH_OK(hipMemset(e->state, 0, (size_t)G.blockWords * K * 4));
+        GH_OK(hipMemsetAsync(e->state, 0, (size_t)G.blockWords * K * 4, stream));
         e->b_ts = e->dalloc<int64_t>(B);
         e->b_key = e->dalloc<uint32_t>(B);
         int maxa = 1;
@@ -625,7 +641,7 @@ GenEngine* gen_create(const uint32_t* ir, size_t nw, const sg_config& cfg, hipSt
         e->t_cnt = e->dalloc<uint32_t>(B);
         e->t_first = e->dalloc<uint32_t>(B);
         e->t_off = e->dalloc<uint32_t>(B);
-        GH_OK(hipMemset(e->t_cnt, 0, B * 4));
+        GH_OK(hipMemsetAsync(e->t_cnt, 0, B * 4, stream));
         e->tk1 = e->dalloc<uint32_t>(e->rawCap);
         e->tk2 = e->dalloc<int64_t>(e->rawCap);
         e->tk3 = e->dalloc<uint32_t>(e->rawCap);
@@ -659,9 +675,9 @@ GenEngine* gen_create(const uint32_t* ir, size_t nw, const sg_config& cfg, hipSt
         e->live = e->dalloc<unsigned long long>(1);
         e->d_args = e->dalloc<GenArgs>(GEN_ARG_SLOTS);
         GH_OK(hipHostMalloc((void**)&e->h_args, sizeof(GenArgs) * GEN_ARG_SLOTS, hipHostMallocDefault));
-        GH_OK(hipMemset(e->stats, 0, GST_N * 8));
+        GH_OK(hipMemsetAsync(e->stats, 0, GST_N * 8, stream));
         e->err = e->dalloc<uint32_t>(1);
-        GH_OK(hipMemset(e->err, 0, 4));
+        GH_OK(hipMemsetAsync(e->err, 0, 4, stream));
         const uint64_t M = e->mcap;
         e->out.trig = e->dalloc<uint64_t>(M);
         e->out.slot = e->dalloc<uint64_t>(M * G.nslots * G.MC);
@@ -669,13 +685,13 @@ GenEngine* gen_create(const uint32_t* ir, size_t nw, const sg_config& cfg, hipSt
         e->out.ts = e->dalloc<int64_t>(M);
         e->out.len = e->dalloc<uint32_t>(M * G.nslots);
         e->out.count = e->dalloc<unsigned long long>(1);
-        GH_OK(hipMemset(e->out.count, 0, 8));
+        GH_OK(hipMemsetAsync(e->out.count, 0, 8, stream));
         e->out.cap = M;
         e->out.nslots = (uint32_t)G.nslots;
         e->out.MC = G.MC;
         e->out.recWords = e->recWords;
         e->out.err = e->err;
-        GH_OK(hipStreamSynchronize(stream));
+        GH_OK(hipStreamSynchronize(stream));  // the zeroed state and counters are in place before a push
         return e;
     } catch (...) {
         delete e;
@@ -706,12 +722,14 @@ static void launch_gen(GenEngine* e, const GenArgs& a, int which) {
     e->h_args[slot] = a;
     GH_OK(hipMemcpyAsync(e->d_args + slot, e->h_args + slot, sizeof(GenArgs), hipMemcpyHostToDevice, e->stream));
     const GenArgs* ap = e->d_args + slot;
+    hipEvent_t t0 = (e->timing && which != GEN_L_DEADLINES) ? e->ev() : nullptr;
     if (which == GEN_L_TIMERS)
         hipLaunchKernelGGL(k_gen_timers, dim3(e->host.partitioned ? std::min(blocks, GEN_TIMER_BLOCKS) : 1u), dim3(64), 0,
                            e->stream, ap);
     else if (which == GEN_L_DEADLINES) hipLaunchKernelGGL(k_gen_deadlines, dim3(blocks), dim3(64), 0, e->stream, ap);
     else hipLaunchKernelGGL(k_gen_batch, dim3(blocks), dim3(64), 0, e->stream, ap);
     GH_OK(hipGetLastError());
+    if (t0) e->spans.push_back({t0, e->ev(), 1});
 }
 
 // largest key id of a host batch (branch-free, so it vectorises; range-checked after the H2D is queued)
@@ -772,12 +790,14 @@ int gen_push(GenEngine* e, const sg_batch* b, std::string& msg) {
                 return SG_ERR_INVALID;
             }
         }
+        hipEvent_t g0 = e->timing ? e->ev() : nullptr;
         uint32_t bits = 1;  // SG_CFG_NULL_KEYS: one value more than the key range (SG_KEY_NULL sorts last)
         while (bits < 32 && (1ull << bits) < (uint64_t)e->K + (e->null_keys ? 1u : 0u)) bits++;
         size_t tmp = e->sort_tmp_bytes;
         GH_OK(rocprim::radix_sort_pairs(e->sort_tmp, tmp, keys, e->skeys, e->iota, e->sidx, n, 0, bits, e->stream));
         hipLaunchKernelGGL(k_gen_bounds, dim3((n + 255) / 256), dim3(256), 0, e->stream, e->skeys, n, e->K,
                            e->null_keys, e->seg_begin, e->seg_end, e->err);
+        if (g0) e->spans.push_back({g0, e->ev(), 0});
         a.b.sidx = e->sidx;
     } else {
         GH_OK(hipMemcpyAsync(e->seg_end, &n, 4, hipMemcpyHostToDevice, e->stream));
@@ -789,6 +809,9 @@ int gen_push(GenEngine* e, const sg_batch* b, std::string& msg) {
     GH_OK(hipMemsetAsync(e->raw_count, 0, 8 * GEN_RAWSEG, e->stream));
     a.o.nseg = GEN_RAWSEG;
     a.o.seg_cap = e->rawCap / GEN_RAWSEG;
+    if (e->timing)  // sg_stats.live_at_batch_start (outside the batch kernel's span)
+        hipLaunchKernelGGL(k_gen_live, dim3((e->K + 255) / 256), dim3(256), 0, e->stream, e->dprog, e->state, e->K,
+                           e->stats + GST_LIVE0, e->seg_begin, e->seg_end);
     launch_gen(e, a, GEN_L_BATCH);
     // order: out_count + t_off[trigger] + rank
     size_t tmp = e->scan_tmp_bytes;
@@ -1000,7 +1023,7 @@ int gen_set_projection(GenEngine* e, const uint32_t* code, uint32_t words, const
         G.offAgg = G.blockWords;
         G.blockWords += 5 * A;
         e->state = e->dalloc<uint32_t>((size_t)G.blockWords * e->K);
-        GH_OK(hipMemset(e->state, 0, (size_t)G.blockWords * e->K * 4));
+        GH_OK(hipMemsetAsync(e->state, 0, (size_t)G.blockWords * e->K * 4, e->stream));
     }
     e->raw = e->dalloc<uint32_t>(e->rawCap * e->recWords);  // (the smaller record buffer is freed at destroy)
     e->out.recWords = e->recWords;
@@ -1008,6 +1031,7 @@ int gen_set_projection(GenEngine* e, const uint32_t* code, uint32_t words, const
     e->out.pnull = e->dalloc<uint8_t>(e->mcap * (S + H));
     e->out.projN = S + H;
     e->out.projOff = G.projOff;
+    GH_OK(hipStreamSynchronize(e->stream));  // no kernel reads the program while it changes
     GH_OK(hipMemcpy(e->dprog, &G, sizeof(GenProgram), hipMemcpyHostToDevice));
     return SG_OK;
 }
@@ -1052,7 +1076,16 @@ void gen_stats(GenEngine* e, sg_stats* out) {
     unsigned long long lv = 0;
     GH_OK(hipMemcpyAsync(&lv, live, 8, hipMemcpyDeviceToHost, e->stream));
     GH_OK(hipStreamSynchronize(e->stream));
+    for (auto& x : e->spans) {
+        float ms = 0.f;
+        GH_OK(hipEventElapsedTime(&ms, x.a, x.b));
+        (x.which == 0 ? e->st.group_ns : e->st.advance_ns) += (uint64_t)((double)ms * 1e6);
+        (void)hipEventDestroy(x.a);
+        (void)hipEventDestroy(x.b);
+    }
+    e->spans.clear();
     *out = e->st;
+    out->live_at_batch_start = s[GST_LIVE0];
     out->partials_scanned = s[GST_SCANNED];
     out->partials_created = s[GST_CREATED];
     out->matches = s[GST_MATCHES];

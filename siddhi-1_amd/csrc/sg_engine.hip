@@ -550,14 +550,14 @@ void allocate(sg_engine* e) {
     const size_t K = e->K, C = e->cap, B = e->maxb, M = e->mcap;
     auto& o = e->owned;
     e->hdr = dalloc<uint32_t>(K, o);
-    HIP_OK(hipMemset(e->hdr, 0, K * 4));
+    HIP_OK(hipMemsetAsync(e->hdr, 0, K * 4, e->stream));
     e->p_ts = dalloc<int64_t>(C * K, o);
     e->p_seq = dalloc<uint64_t>(C * K, o);
     e->n_capw = 0;
     for (uint8_t t : e->plan.cap_type) e->n_capw += (t == SG_T_LONG || t == SG_T_DOUBLE) ? 2 : 1;
     e->p_capw = dalloc<uint32_t>(std::max<size_t>(1, e->n_capw) * C * K, o);
     e->p_capnull = dalloc<uint32_t>(C * K, o);
-    HIP_OK(hipMemset(e->p_capnull, 0, C * K * 4));
+    HIP_OK(hipMemsetAsync(e->p_capnull, 0, C * K * 4, e->stream));
     size_t maxattr = 0;
     for (auto& s : e->streams) maxattr = std::max(maxattr, s.types.size());
     for (auto& sl : e->slots) {
@@ -622,10 +622,10 @@ void allocate(sg_engine* e) {
     e->resume = dalloc<uint32_t>(K, o);
     if (getenv("SG_PROF")) {
         e->prof = dalloc<unsigned long long>(nw * 8, o);
-        HIP_OK(hipMemset(e->prof, 0, nw * 64));
+        HIP_OK(hipMemsetAsync(e->prof, 0, nw * 64, e->stream));
         e->prof_rows = nw;
     }
-    HIP_OK(hipMemset(e->resume, 0xff, K * 4));  // SGD_NO_RESUME
+    HIP_OK(hipMemsetAsync(e->resume, 0xff, K * 4, e->stream));  // SGD_NO_RESUME
     e->tile_sum = dalloc<uint32_t>(B / SGD_ORDER_TILE + 1, o);
     e->tile_off = dalloc<uint32_t>(B / SGD_ORDER_TILE + 1, o);
     // the match count and the error word share 16 bytes, so poll reads both with one D2H copy
@@ -633,10 +633,10 @@ void allocate(sg_engine* e) {
     e->err = (uint32_t*)(e->out_count + 1);
     e->batch_total = dalloc<unsigned long long>(1, o);
     e->stats = dalloc<unsigned long long>(SGD_ST_N, o);
-    HIP_OK(hipMemset(e->t_desc, 0, B * 8));
-    HIP_OK(hipMemset(e->out_count, 0, 16));
-    HIP_OK(hipMemset(e->stats, 0, SGD_ST_N * 8));
-    HIP_OK(hipMemset(e->err, 0, 4));
+    HIP_OK(hipMemsetAsync(e->t_desc, 0, B * 8, e->stream));
+    HIP_OK(hipMemsetAsync(e->out_count, 0, 16, e->stream));
+    HIP_OK(hipMemsetAsync(e->stats, 0, SGD_ST_N * 8, e->stream));
+    HIP_OK(hipMemsetAsync(e->err, 0, 4, e->stream));
     e->scan_tmp_bytes = sgd_scatter_scan_bytes((uint32_t)B);
     e->scan_tmp = dalloc<uint8_t>(e->scan_tmp_bytes, o);
     e->o_trig = dalloc<uint64_t>(M, o);
@@ -1198,10 +1198,10 @@ int set_projection(sg_engine* e, const uint32_t* code, uint32_t words, const uin
         }
         e->p_capw = dalloc<uint32_t>(std::max<size_t>(1, e->n_capw) * C * K, e->owned);
         e->p_capnull = dalloc<uint32_t>(C * K, e->owned);
-        HIP_OK(hipMemset(e->p_capnull, 0, C * K * 4));
+        HIP_OK(hipMemsetAsync(e->p_capnull, 0, C * K * 4, e->stream));
         e->raw_capw = dalloc<uint32_t>(std::max<size_t>(1, e->n_capw) * e->raw_cap, e->owned);
         e->raw_capnull = dalloc<uint32_t>(e->raw_cap, e->owned);
-        HIP_OK(hipMemset(e->raw_capnull, 0, e->raw_cap * 4));
+        HIP_OK(hipMemsetAsync(e->raw_capnull, 0, e->raw_cap * 4, e->stream));
         e->o_capw = dalloc<uint32_t>(std::max<size_t>(1, e->n_capw) * M, e->owned);
         e->o_capnull = dalloc<uint32_t>(M, e->owned);
         e->pval = dalloc<uint64_t>((size_t)(S + H) * M, e->owned);
@@ -1212,9 +1212,9 @@ int set_projection(sg_engine* e, const uint32_t* code, uint32_t words, const uin
             e->agg_n = dalloc<int64_t>((size_t)A * K, e->owned);
             e->agg_v = dalloc<uint64_t>((size_t)A * K, e->owned);
             e->agg_has = dalloc<uint8_t>((size_t)A * K, e->owned);
-            HIP_OK(hipMemset(e->agg_n, 0, (size_t)A * K * 8));
-            HIP_OK(hipMemset(e->agg_v, 0, (size_t)A * K * 8));
-            HIP_OK(hipMemset(e->agg_has, 0, (size_t)A * K));
+            HIP_OK(hipMemsetAsync(e->agg_n, 0, (size_t)A * K * 8, e->stream));
+            HIP_OK(hipMemsetAsync(e->agg_v, 0, (size_t)A * K * 8, e->stream));
+            HIP_OK(hipMemsetAsync(e->agg_has, 0, (size_t)A * K, e->stream));
             e->out_first = dalloc<uint64_t>(e->maxb, e->owned);
         }
         for (auto& sl : e->slots)

@@ -1,9 +1,12 @@
 """General-engine configs of bench.py (C3_min1, C4, C4_deep) at their bench sizes, fewer steps: one JSON
 line per config.  SG_HIP_LIBRARY selects an alternative build of the engine (layout experiments)."""
+import faulthandler
 import importlib
 import json
 import os
 import sys
+
+faulthandler.dump_traceback_later(int(os.environ.get("SG_EXP_WATCHDOG", "150")), exit=True)
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -25,6 +28,7 @@ cfg = {
                 True),
 }
 for name in which:
+    print("config", name, flush=True)
     q, mk, keys, b, cap, pb = cfg[name]
     r = bench.run_general(sa, synth, torch, dev, q, mk, keys, b, steps, 1, cap, playback=pb)
     print(json.dumps(dict(r, config=name, lib=os.environ.get("SG_HIP_LIBRARY", "default"))), flush=True)
