@@ -1308,6 +1308,8 @@ int sg_engine_create(const void* ir, size_t ir_len, const sg_config* cfg, sg_eng
         e->maxb = cfg->max_batch ? cfg->max_batch : (1u << 20);
         e->mcap = cfg->match_capacity ? cfg->match_capacity : (uint64_t)e->maxb * 4;
         if (e->cap > SGD_MAX_CAP) throw std::invalid_argument("partial_capacity above 4095");
+        // the register window never holds more partials than the key's slab can take when it spills
+        if (e->reg_slots > e->cap) e->reg_slots = e->cap;
         if (e->mcap >= (1ull << 31)) throw std::invalid_argument("match_capacity must be < 2^31");
         if (ir_len < SG_IR_HDR_WORDS * 4 || ir_len % 4) throw std::invalid_argument("IR too short");
         if (((const uint32_t*)ir)[0] != SG_IR_MAGIC || ((const uint32_t*)ir)[1] != SG_IR_VERSION)
