@@ -161,6 +161,7 @@ struct GenOut {
     unsigned long long* nvalid;      // timer matches emitted by a sweep
     unsigned long long* stats;
     uint32_t* err;
+    unsigned long long* prof;        // GENX_PROF builds: shader-clock cycles per walk phase (summed over waves)
 };
 
 // Timers (sg_advance_time).  Each key's next deadline (the earliest queue head of its absent

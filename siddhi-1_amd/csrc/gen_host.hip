@@ -13,6 +13,8 @@
 #include <rocprim/device/device_scan.hpp>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <functional>
 #include <cstring>
 #include <stdexcept>
@@ -549,6 +551,7 @@ struct GenEngine {
     // SG_CFG_TIMING: HIP events around the NFA kernels (batch + timer sweeps: advance_ns) and the
     // grouping (group_ns), resolved by gen_stats; the touched keys' live partials counted before each batch
     bool timing = false;
+    unsigned long long* prof = nullptr;  // SG_GEN_PROF with a GENX_PROF build: walk-phase cycles, printed at destroy
     struct Span { hipEvent_t a, b; int which; };
     std::vector<Span> spans;
     hipEvent_t ev() {
@@ -566,6 +569,12 @@ struct GenEngine {
     }
     ~GenEngine() {
         if (stream) (void)hipStreamSynchronize(stream);
+        if (prof) {
+            unsigned long long h[8] = {};
+            if (hipMemcpy(h, prof, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess)
+                fprintf(stderr, "gen prof (cycles summed over waves): start %llu stabilize %llu process %llu "
+                        "project %llu end %llu timers %llu waves %llu\n", h[0], h[1], h[2], h[3], h[4], h[5], h[6]);
+        }
         for (auto& x : spans) { (void)hipEventDestroy(x.a); (void)hipEventDestroy(x.b); }
         for (void* p : owned) (void)hipFree(p);
         if (h_args) (void)hipHostFree(h_args);
@@ -590,6 +599,7 @@ struct GenEngine {
         a.o.nvalid = nvalid;
         a.o.stats = stats;
         a.o.err = err;
+        a.o.prof = prof;
         a.t = tm;
         a.now = now;
         a.now0 = now;
@@ -607,6 +617,10 @@ GenEngine* gen_create(const uint32_t* ir, size_t nw, const sg_config& cfg, hipSt
         e->K = e->host.partitioned ? (cfg.n_keys ? cfg.n_keys : 1) : 1;
         e->null_keys = (cfg.flags & SG_CFG_NULL_KEYS) != 0;
         e->timing = (cfg.flags & SG_CFG_TIMING) != 0;
+        if (getenv("SG_GEN_PROF")) {
+            e->prof = e->dalloc<unsigned long long>(8);
+            GH_OK(hipMemsetAsync(e->prof, 0, 64, stream));
+        }
         e->maxb = cfg.max_batch ? cfg.max_batch : (1u << 20);
         e->mcap = cfg.match_capacity ? cfg.match_capacity : (uint64_t)e->maxb * 4;
         const GenProgram& G = e->host;

@@ -20,6 +20,18 @@
 #include "gen_engine.h"
 #include "java_ops.h"
 
+// GENX_PROF=1 (experiment builds only): s_memtime per walk phase of each wave, summed into A.o.prof:
+// 0 key start (bounds, initKey), 1 stabilize, 2 processAndReturn, 3 projection / deferral,
+// 4 key end (flush, reservations, deadline), 5 timer sweeps, 6 waves
+#ifndef GENX_PROF
+#define GENX_PROF 0
+#endif
+#if GENX_PROF
+#define GENX_T(i) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); prof[i] += t_ - prof_t; prof_t = t_; } while (0)
+#else
+#define GENX_T(i) do { } while (0)
+#endif
+
 namespace {
 
 // Address spaces made explicit: the per-key state and the batch columns are global memory
@@ -51,6 +63,10 @@ struct Lane {
     unsigned long long resBase;  // this lane's reserved raw match slots
     unsigned long long resEnd;   // end of its reservation segment
     uint32_t resLeft;
+#if GENX_PROF
+    uint64_t prof[7] = {0, 0, 0, 0, 0, 0, 0};
+    uint64_t prof_t = __builtin_amdgcn_s_memtime();
+#endif
 
     __device__ Lane(const GenArgs& a, uint32_t key)
         : G(*(cGenProgram*)a.G), A(a), S(gp(a.state)), K(a.K), k(key), now(a.now), trigSeq(SG_TIMER_SEQ), trigIdx(0), trigRank(0),
@@ -1069,7 +1085,9 @@ struct Lane {
     __device__ void processEvent(const __attribute__((address_space(4))) GenRecv& r, uint32_t pos, bool chunkEnd) __restrict__ {
         const uint64_t seq = A.b.seq_base + pos;
         const int64_t ts = gp(A.b.ts)[pos];
+        GENX_T(4);
         stabilize(r, ts);
+        GENX_T(1);
         gu32& nd = W(defBase());
         if (r.multi) {
             trigSeq = seq;
@@ -1079,13 +1097,16 @@ struct Lane {
                 uint32_t outl[64];
                 uint32_t no = 0;
                 processAndReturn(r.procs[j], seq, ts, pos, outl, no);
+                GENX_T(2);
                 for (uint32_t x = 0; x < no; x++) { project(outl[x]); stDecref(outl[x]); }
+                GENX_T(3);
             }
         } else {
             // deferred until the end of the chunk (consecutive events of this key in the batch)
             uint32_t outl[64];
             uint32_t no = 0;
             processAndReturn(r.procs[0], seq, ts, pos, outl, no);
+            GENX_T(2);
             for (uint32_t x = 0; x < no; x++) {
                 if (nd >= G.DEF) { err |= GERR_CAP; stDecref(outl[x]); continue; }
                 W(defBase() + 1 + 2 * nd) = outl[x];
@@ -1093,6 +1114,7 @@ struct Lane {
                 nd++;
             }
             if (chunkEnd) flushDeferred();
+            GENX_T(3);
         }
     }
     __device__ void flushDeferred() __restrict__ {
@@ -1152,6 +1174,9 @@ extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per
         const uint32_t b = gp(a.b.seg_begin)[key], e = gp(a.b.seg_end)[key];
         Lane L(a, key);
         L.initKey();
+#if GENX_PROF
+        { const uint64_t t_ = __builtin_amdgcn_s_memtime(); L.prof[0] += t_ - L.prof_t; L.prof_t = t_; }
+#endif
         const auto& r = L.G.recv[a.b.stream];
         if (r.n > 0) {
             for (uint32_t j = b; j < e; j++) {
@@ -1174,7 +1199,15 @@ extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per
         cr = L.created;
         ma = L.matches;
         ky = 1;
+#if GENX_PROF
+        { const uint64_t t_ = __builtin_amdgcn_s_memtime(); L.prof[4] += t_ - L.prof_t; L.prof_t = t_; }
+        if (a.o.prof && (threadIdx.x & 63) == __builtin_amdgcn_readfirstlane(threadIdx.x & 63))
+            for (int i = 0; i < 5; i++) atomicAdd(&a.o.prof[i], (unsigned long long)L.prof[i]);
+#endif
     }
+#if GENX_PROF
+    if (a.o.prof && (threadIdx.x & 63) == 0) atomicAdd(&a.o.prof[6], 1ull);
+#endif
     gen_wave_stats(a, sc, cr, ma, ky, er);
 }
 
@@ -1302,11 +1335,17 @@ extern "C" __global__ void __launch_bounds__(256) k_gen_collapse(const unsigned 
 // timer sweep over the due keys (every key when unpartitioned: key 0, seeded at start())
 extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GEN_WAVES, 8))) k_gen_timers(const GenArgs* __restrict__ ap) {
     const GenArgs& a = *ap;
+#if GENX_PROF
+    const uint64_t t0_ = __builtin_amdgcn_s_memtime();
+#endif
     const uint64_t n = a.G->partitioned ? *a.t.ndue : 1ull;
     unsigned long long sc = 0, cr = 0, ma = 0;
     uint32_t er = 0;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
         gen_timers_key(a, a.G->partitioned ? a.t.due[i] : 0u, i, sc, cr, ma, er);
+#if GENX_PROF
+    if (a.o.prof && (threadIdx.x & 63) == 0) atomicAdd(&a.o.prof[5], (unsigned long long)(__builtin_amdgcn_s_memtime() - t0_));
+#endif
     unsigned long long mw = ma;
     for (int off = 32; off > 0; off >>= 1) mw += __shfl_xor(mw, off, 64);
     if ((threadIdx.x & 63) == 0 && mw) atomicAdd(a.o.nvalid, mw);  // timer matches of this wave
