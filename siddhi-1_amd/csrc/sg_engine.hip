@@ -34,6 +34,8 @@
 #include "../../include/siddhi_gpu_ir.h"
 #include "gen_engine.h"
 #include "gen_host.h"
+#include "grp.h"
+#include "pack.h"
 #include "pinned.h"
 #include "state_doc.h"
 #include "sg_engine.h"
@@ -102,48 +104,6 @@ size_t type_size(uint32_t t) {
     }
 }
 
-// key-sorted event payload: batch position, the filter columns (32-bit words), timestamp
-template <int W> struct alignas(8) Pay {
-    uint32_t idx;
-    uint32_t w[W];
-    int64_t ts;
-};
-static_assert(sizeof(Pay<1>) == 16 && sizeof(Pay<2>) == 24 && sizeof(Pay<3>) == 24 && sizeof(Pay<4>) == 32,
-              "payload layout: ts in the last 8 bytes");
-
-struct PackSrc {
-    const void* p[4];
-    uint8_t kind[4];  // 0: 32-bit column, 1: low / 2: high word of a 64-bit column, 3: bool byte,
-                      // 4: null bits of the columns, 5: zero
-    const uint8_t* nul[SGD_MAX_EVCOLS];
-    const int64_t* ts;
-};
-
-template <int W> struct PackFn {
-    PackSrc s;
-    __host__ __device__ Pay<W> operator()(uint32_t i) const {
-        Pay<W> o;
-        o.idx = i;
-        o.ts = s.ts[i];
-        for (int w = 0; w < W; ++w) {
-            switch (s.kind[w]) {
-            case 0: o.w[w] = ((const uint32_t*)s.p[w])[i]; break;
-            case 1: o.w[w] = (uint32_t)((const uint64_t*)s.p[w])[i]; break;
-            case 2: o.w[w] = (uint32_t)(((const uint64_t*)s.p[w])[i] >> 32); break;
-            case 3: o.w[w] = ((const uint8_t*)s.p[w])[i] ? 1u : 0u; break;
-            case 4: {
-                uint32_t nb = 0;
-                for (int c = 0; c < SGD_MAX_EVCOLS; ++c)
-                    if (s.nul[c]) nb |= (s.nul[c][i] != 0 ? 1u : 0u) << c;
-                o.w[w] = nb;
-                break;
-            }
-            default: o.w[w] = 0u;
-            }
-        }
-        return o;
-    }
-};
 
 // 16-B payloads (one filter column): onesweep with 10-bit digits, so 2^11..2^20 keys sort in two
 // passes over the data instead of three (rocPRIM's gfx950 default for this pair size is 8 bits)
@@ -237,6 +197,14 @@ struct sg_engine {
     uint32_t* iota = nullptr;
     void* sort_tmp = nullptr;
     size_t sort_tmp_bytes = 0;
+    // tile grouping (grp_kernels.hip; K <= 2^20, max_batch <= 2^24, payload <= 4 words): shared by the
+    // slots (both slots' groupings run on gstream, one after the other)
+    bool tile_grp = false;
+    uint32_t* g_mat = nullptr;
+    uint32_t* g_mscan = nullptr;
+    void* g_tpay = nullptr;
+    void* g_scan_tmp = nullptr;
+    size_t g_scan_tmp_bytes = 0;
     uint32_t pay_words = 0;
     // per pushed batch, after its ordering: the {match count, error word} status block copied to pinned
     // host memory and an event, so a poll finds the completed batches without waiting for the others
@@ -605,6 +573,17 @@ void allocate(sg_engine* e) {
         e->pay_words = maxw;
         for (auto& sl : e->slots)  // + one 16-B chunk: the LDS copy rounds up
             sl.pay = dalloc<uint32_t>((size_t)maxw * B + 4, o);
+        // the tile grouping is opt-in (SG_GROUP_TILES=1): measured slower than the radix sort on C2
+        e->tile_grp = e->plan.partitioned && sgd_group_tiles_ok(K, B, 1) && getenv("SG_GROUP_TILES");
+        if (e->tile_grp) {
+            const uint64_t nt = (K + SGD_BLOCK - 1) / SGD_BLOCK, nb = (B + SGD_GRP_BLOCK_EVENTS - 1) / SGD_GRP_BLOCK_EVENTS;
+            e->g_mat = dalloc<uint32_t>(nt * nb + 1, o);
+            e->g_mscan = dalloc<uint32_t>(nt * nb + 1, o);
+            e->g_tpay = dalloc<uint32_t>((size_t)maxw * B + 4, o);
+            e->g_scan_tmp_bytes = sgd_group_scan_bytes(nt * nb + 1);
+            if (!e->g_scan_tmp_bytes) throw HipError("tile grouping: scan storage query failed");
+            e->g_scan_tmp = dalloc<uint8_t>(e->g_scan_tmp_bytes, o);
+        }
     }
     // raw match slots per batch: waves reserve at most sum(live partials + events) up front, or
     // (every (e1 -> e2)) chunks of SGD_RAW_CHUNK with two chunks of slack per wave (p2_jit.hip)
@@ -870,6 +849,30 @@ int push(sg_engine* e, const sg_batch* b) {
                 ps.kind[wi++] = 4;
             }
             if (wi == 0) ps.kind[wi++] = 5;
+            if (e->tile_grp && sgd_group_tiles_ok(e->K, n, wi)) {
+                // by key tile, then by key inside each tile in LDS (grp_kernels.hip): the same key-sorted
+                // payload and per-key bounds as the radix sort below
+                GrpArgs ga{};
+                ga.n = n;
+                ga.K = e->K;
+                ga.n_tiles = (e->K + SGD_BLOCK - 1) / SGD_BLOCK;
+                ga.nblk = (n + SGD_GRP_BLOCK_EVENTS - 1) / SGD_GRP_BLOCK_EVENTS;
+                ga.drop_null = e->null_keys ? 1u : 0u;
+                ga.tile_lds = sgd_group_tile_lds(n, e->K, wi);
+                if (const char* x = getenv("SG_GRP_EXP")) ga.exp = (uint32_t)strtoul(x, nullptr, 0);
+                ga.keys = keys;
+                ga.mat = e->g_mat;
+                ga.mscan = e->g_mscan;
+                ga.tpay = e->g_tpay;
+                ga.pay = sl.pay;
+                ga.seg_begin = sl.seg_begin;
+                ga.seg_end = sl.seg_end;
+                ga.err = e->err;
+                ga.scan_tmp = e->g_scan_tmp;
+                ga.scan_tmp_bytes = e->g_scan_tmp_bytes;
+                HIP_OK(sgd_group_tiles(ga, ps, (int)wi, gs));
+                goto grouped;
+            }
             HIP_OK(sort_payload_w((int)wi, e->sort_tmp, tmp, keys, sl.skeys, ps, sl.pay, n, e->sort_bits, gs));
         } else {
             HIP_OK(rocprim::radix_sort_pairs(e->sort_tmp, tmp, keys, sl.skeys, e->iota, sl.sidx, n, 0, e->sort_bits,
@@ -879,6 +882,7 @@ int push(sg_engine* e, const sg_batch* b) {
         }
         if (sgd_launch_bounds(sl.skeys, n, e->K, e->null_keys, sl.seg_begin, sl.seg_end, e->err, gs) != 0)
             throw HipError("k_seg_bounds launch failed");
+    grouped:;
     } else {
         pk.sidx = nullptr;  // one key: arrival order
         launch(v.pack[role], pack_blocks, 256, &pk, gs);
