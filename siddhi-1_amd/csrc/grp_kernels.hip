@@ -223,21 +223,21 @@ template <int W> __global__ void __launch_bounds__(GT_W * 64) k_grp_tile(const G
     for (uint32_t j0 = lo; j0 < hi; j0 += 64) {  // wave-uniform
         const uint32_t j = j0 + lane;
         const bool v = j < hi;
-        constexpr uint32_t Q = SB / 8;  // the element as 8-B words (Pay is 8-B aligned)
-        uint2 el[Q];
+        constexpr uint32_t Q = SB / 4;  // the element as 4-B words
+        uint32_t el[Q];
         if (v) {
-            const uint2* ep = (const uint2*)(e + j);
+            const uint32_t* ep = (const uint32_t*)(e + j);
 #pragma unroll
             for (uint32_t q = 0; q < Q; ++q) el[q] = ep[q];
         }
-        const uint32_t s = v ? (el[0].x >> 24) : 0u;
+        const uint32_t s = v ? (el[0] >> 24) : 0u;
         const uint64_t m = match_any<8>(s, __ballot(v));
         if (v) {
             const uint32_t before = lane_rank(m);
             const uint32_t base = cnt[w][s];
             if (before == 0) cnt[w][s] = base + (uint32_t)__popcll(m);
-            el[0].x &= 0xffffffu;
-            uint2* op = (uint2*)(out + base + before);
+            el[0] &= 0xffffffu;
+            uint32_t* op = (uint32_t*)(out + base + before);
 #pragma unroll
             for (uint32_t q = 0; q < Q; ++q) op[q] = el[q];
         }
@@ -273,7 +273,7 @@ size_t sgd_group_scan_bytes(uint64_t max_entries) {
 // LDS region of the tile sort: the tile's payload bytes at this density (n / K events per key, 256 keys)
 // plus 4 standard deviations of the Poisson count (larger tiles are ranked from HBM, exactly)
 uint32_t sgd_group_tile_lds(uint64_t n, uint64_t K, uint32_t words) {
-    const uint32_t sb = words == 1 ? 16u : (words <= 3 ? 24u : 32u);
+    const uint32_t sb = 4u * (words + 2u);  // sizeof(Pay<words>)
     const double mean = (double)n * 256.0 / (double)(K ? K : 1);
     const double want = (mean + 4.0 * std::sqrt(mean) + 32.0) * sb + 32.0;
     const double lim = 148.0 * 1024.0;  // beside the 8 KB of counters

@@ -191,7 +191,10 @@ extern __shared__ sg_u32x4 sg_stage[];
 
 template <int S> __device__ __forceinline__ PayEl<S> load_pay(const uint32_t* __restrict__ base, uint32_t i) {
     PayEl<S> x;
-    if constexpr (S % 4 == 0) {
+    if constexpr (S % 2 != 0) {  // 4-B aligned elements
+#pragma unroll
+        for (int q = 0; q < S; ++q) x.w[q] = __builtin_nontemporal_load(base + (size_t)i * S + q);
+    } else if constexpr (S % 4 == 0) {
         const sg_u32x4* s = (const sg_u32x4*)(base + (size_t)i * S);
 #pragma unroll
         for (int q = 0; q < S / 4; ++q) {
@@ -210,10 +213,13 @@ template <int S> __device__ __forceinline__ PayEl<S> load_pay(const uint32_t* __
 }
 
 // element i of a wave's payload run staged in LDS (base = element 0; 16-B aligned when the element
-// size is a multiple of 16 B, 8-B aligned otherwise)
+// size is a multiple of 16 B, 8-B aligned when it is a multiple of 8 B, 4-B aligned otherwise)
 template <int S> __device__ __forceinline__ PayEl<S> lds_pay(const uint32_t* base, uint32_t i) {
     PayEl<S> x;
-    if constexpr (S % 4 == 0) {
+    if constexpr (S % 2 != 0) {  // 4-B aligned elements
+#pragma unroll
+        for (int q = 0; q < S; ++q) x.w[q] = base[(size_t)i * S + q];
+    } else if constexpr (S % 4 == 0) {
         const sg_u32x4* s = (const sg_u32x4*)(base + (size_t)i * S);
 #pragma unroll
         for (int q = 0; q < S / 4; ++q) {
@@ -231,7 +237,14 @@ template <int S> __device__ __forceinline__ PayEl<S> lds_pay(const uint32_t* bas
     return x;
 }
 
-#define SG_OFF_LIM (1ll << 30)
+#define SG_OFF_LIM SGD_TS_LIM
+// the payload's timestamp word (pack.h sgd_ts_off): ts - base, or SGD_TS_FAR when that does not fit
+__device__ __forceinline__ int32_t ts_off32(int64_t t, int64_t base) {
+    if (t == -1) return SGD_TS_FAR;
+    const int64_t x = (int64_t)((uint64_t)t - (uint64_t)base);
+    const bool wrapped = ((t ^ base) < 0) && ((x ^ t) < 0);
+    return (wrapped || x < -SGD_TS_LIM || x > SGD_TS_LIM) ? SGD_TS_FAR : (int32_t)x;
+}
 __device__ __forceinline__ bool off_ok(int64_t d) { return d >= -SG_OFF_LIM && d <= SG_OFF_LIM; }
 // t - base fits the staged pass's 32-bit offsets (no 64-bit wrap of the difference either)
 __device__ __forceinline__ bool ts_off_ok(int64_t t, int64_t base) {
@@ -551,9 +564,11 @@ __device__ __forceinline__ void advance(const P2Params& p) {
     const int64_t within = p.within;
     constexpr bool GLB = !STG;  // only the HBM pass has the slab (spill) mode
 
-    // the staged pass's 32-bit offsets: ts from tbase (the batch's first key-sorted event), seq from
-    // the batch's seq_base; a key with a value out of range goes to the HBM pass (`far` below)
-    const int64_t tbase = STG ? sg_i64(p.payload[STRIDE - 2], p.payload[STRIDE - 1]) : 0;
+    // the payload's timestamps are 32-bit offsets from obase, the batch's first timestamp (pack.h); the
+    // staged pass keeps the window's timestamps as offsets from the same base (tbase) and seqs from the
+    // batch's seq_base; a key with a value out of range goes to the HBM pass (`far` below)
+    const int64_t obase = p.ts_col[0];
+    const int64_t tbase = STG ? obase : 0;
     const uint64_t sbase = STG ? p.seq_base : 0;
     Win<STG> W;
     typedef typename Win<STG>::TS WTS;
@@ -662,9 +677,8 @@ __device__ __forceinline__ void advance(const P2Params& p) {
             // the partials this event can add: every start seed fires at most once (+1: the
             // withinEvery re-arm of `every (e1 -> e2)`); stop here if the window could overflow, or
             // if the event's timestamp is outside the range of the band expiry test
-            const int64_t tsn = sg_i64(cur.w[STRIDE - 2], cur.w[STRIDE - 1]);
             if (act && (__popc(W.live) + s.spend + s.sstg + ((SGQ_MODE & SGD_P2_EVERY_BOTH) ? 1u : 0u) > (uint32_t)R ||
-                        !ts_off_ok(tsn, tbase) || tsn == -1 || cur.w[0] > 0x7fffffffu)) {
+                        (int32_t)cur.w[STRIDE - 1] == SGD_TS_FAR || cur.w[0] > 0x7fffffffu)) {
                 rs = (uint32_t)it;
                 run = it;
                 act = false;
@@ -679,7 +693,8 @@ __device__ __forceinline__ void advance(const P2Params& p) {
         uint32_t bi = 0;
         if (act) {
             bi = cur.w[0];
-            ts = sg_i64(cur.w[STRIDE - 2], cur.w[STRIDE - 1]);
+            const int32_t toff = (int32_t)cur.w[STRIDE - 1];
+            ts = (STG || toff != SGD_TS_FAR) ? obase + (int64_t)toff : p.ts_col[bi];
             if constexpr (S0) ev = sgq_ev0(cur.w); else ev = sgq_ev1(cur.w);
             SGX_T(0);
             // ---- stabilize (receiver.stabilizeStates) ----
@@ -687,7 +702,7 @@ __device__ __forceinline__ void advance(const P2Params& p) {
                 if (SGQ_WITHIN && W.live) {
                     uint32_t X = 0;
                     if constexpr (STG) {  // band form on the offsets (see the prologue): two compares per slot
-                        const int32_t tn = (int32_t)(ts - tbase), w32 = (int32_t)within;
+                        const int32_t tn = toff, w32 = (int32_t)within;
                         const int32_t lo = tn - w32, hi = tn + w32;
 #pragma unroll
                         for (int j = 0; j < R; ++j) X |= (((W.ts[j] < lo) | (W.ts[j] > hi)) ? 1u : 0u) << j;
@@ -938,12 +953,10 @@ __device__ __forceinline__ void pack(const PackParams& q) {
     for (int w = 0; w < STRIDE; ++w) x.w[w] = 0;
     x.w[0] = j;
     if constexpr (WHICH == 0) sgq_pack0(q, j, x.w); else sgq_pack1(q, j, x.w);
-    const uint64_t t = (uint64_t)q.ts[j];
-    x.w[STRIDE - 2] = (uint32_t)t;
-    x.w[STRIDE - 1] = (uint32_t)(t >> 32);
-    uint2* d = (uint2*)(q.payload + (size_t)i * STRIDE);
+    x.w[STRIDE - 1] = (uint32_t)ts_off32(q.ts[j], q.ts[0]);
+    uint32_t* d = q.payload + (size_t)i * STRIDE;
 #pragma unroll
-    for (int w = 0; w < STRIDE / 2; ++w) d[w] = make_uint2(x.w[2 * w], x.w[2 * w + 1]);
+    for (int w = 0; w < STRIDE; ++w) d[w] = x.w[w];
 }
 
 }  // namespace

@@ -7,14 +7,24 @@
 
 #include "sg_engine.h"
 
-// key-sorted event payload: batch position, the filter columns (32-bit words), timestamp
-template <int W> struct alignas(8) Pay {
+// key-sorted event payload: batch position, the filter columns (32-bit words), timestamp as a 32-bit
+// offset from the batch's first timestamp (SGD_TS_FAR when it does not fit)
+template <int W> struct Pay {
     uint32_t idx;
     uint32_t w[W];
-    int64_t ts;
+    int32_t ts;
 };
-static_assert(sizeof(Pay<1>) == 16 && sizeof(Pay<2>) == 24 && sizeof(Pay<3>) == 24 && sizeof(Pay<4>) == 32,
-              "payload layout: ts in the last 8 bytes");
+static_assert(sizeof(Pay<1>) == 12 && sizeof(Pay<2>) == 16 && sizeof(Pay<3>) == 20 && sizeof(Pay<4>) == 24,
+              "payload layout: 4-B words, the ts offset last");
+
+__host__ __device__ __forceinline__ int32_t sgd_ts_off(int64_t t, int64_t base) {
+    if (t == -1) return SGD_TS_FAR;
+    const uint64_t d = (uint64_t)t - (uint64_t)base;  // two's-complement difference
+    const int64_t x = (int64_t)d;
+    // exact only when t - base does not wrap: same signs or the difference keeps the sign of t - base
+    const bool wrapped = ((t ^ base) < 0) && ((x ^ t) < 0);
+    return (wrapped || x < -SGD_TS_LIM || x > SGD_TS_LIM) ? SGD_TS_FAR : (int32_t)x;
+}
 
 struct PackSrc {
     const void* p[4];
@@ -29,7 +39,7 @@ template <int W> struct PackFn {
     __host__ __device__ Pay<W> operator()(uint32_t i) const {
         Pay<W> o;
         o.idx = i;
-        o.ts = s.ts[i];
+        o.ts = sgd_ts_off(s.ts[i], s.ts[0]);
         for (int w = 0; w < W; ++w) {
             switch (s.kind[w]) {
             case 0: o.w[w] = ((const uint32_t*)s.p[w])[i]; break;

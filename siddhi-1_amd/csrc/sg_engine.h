@@ -16,6 +16,11 @@
 #define SGD_BLOCK 256      // lanes (= keys) per workgroup of the advance kernel
 #define SGD_STAGE_MAX_BYTES 147456  // LDS per workgroup staging its keys' payload runs (upper bound; the
                                     // static LDS of the lane dealing sits beside it in the 160 KB)
+// key-sorted payload timestamps are 32-bit offsets from the batch's first (arrival-order) timestamp;
+// an event whose offset does not fit [-2^30, 2^30] (or whose ts is -1) carries SGD_TS_FAR and the
+// advance kernel reads its full timestamp from the batch's ts column
+#define SGD_TS_FAR ((int32_t)0x80000000)
+#define SGD_TS_LIM (1ll << 30)
 #define SGD_RAW_CHUNK 256  // raw match slots a wave reserves at a time (the raw buffer has 2 chunks of slack per wave)
 
 // ---- filters ------------------------------------------------------------------------------------
@@ -69,6 +74,7 @@ struct P2Params {
     int64_t within;                    // -1 = none
     // key-sorted batch: element i = [batch position][filter column words..][null bits?][ts lo, hi]
     const uint32_t* payload;
+    const int64_t* ts_col;             // the batch's timestamps in arrival order (ts_col[0]: the offsets' base)
     const uint32_t* seg_begin;         // [n_keys]
     const uint32_t* seg_end;           // [n_keys]
     // per-key state (SoA, partial j of key k at j * n_keys + k)

@@ -105,11 +105,13 @@ size_t type_size(uint32_t t) {
 }
 
 
-// 16-B payloads (one filter column): onesweep with 10-bit digits, so 2^11..2^20 keys sort in two
-// passes over the data instead of three (rocPRIM's gfx950 default for this pair size is 8 bits)
+// 12-B payloads (one filter column): onesweep with 10-bit digits, so 2^11..2^20 keys sort in two
+// passes over the data instead of three (rocPRIM's gfx950 default for this pair size is 8 bits);
+// 1024 x 16 items per block measured fastest for 2^24 events (tools/sweep/sort_sweep12.hip: 0.460 ms
+// against 0.538 at 1024 x 6 and 0.650 for the default configuration)
 using Pay16Config = rocprim::radix_sort_config<
     rocprim::default_config, rocprim::default_config,
-    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 6>, rocprim::kernel_config<1024, 6>, 10,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 16>, rocprim::kernel_config<1024, 16>, 10,
                                         rocprim::block_radix_rank_algorithm::match>>;
 
 template <int W>
@@ -900,6 +902,7 @@ int push(sg_engine* e, const sg_batch* b) {
     p.seq_base = b->seq_base;
     p.within = pl.within;
     p.payload = (const uint32_t*)sl.pay;
+    p.ts_col = ts;
     p.seg_begin = sl.seg_begin;
     p.seg_end = sl.seg_end;
     p.hdr = e->hdr;

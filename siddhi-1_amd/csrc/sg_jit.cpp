@@ -302,7 +302,7 @@ uint32_t sgj_col_words(const std::vector<uint32_t>& types) {
 
 uint32_t sgj_stride(uint32_t words) {
     const uint32_t w = words ? words : 1;
-    return ((w + 2) & ~1u) + 2;  // == sizeof(Pay<w>) / 4 of the sorted-payload path (sg_engine.hip)
+    return w + 2;  // == sizeof(Pay<w>) / 4 of the sorted-payload path (pack.h): position, words, ts offset
 }
 
 uint64_t sgj_fold_cvt(uint64_t b, uint32_t from, uint32_t to) {
