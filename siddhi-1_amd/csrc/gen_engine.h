@@ -189,4 +189,6 @@ struct GenArgs {
     GenTimers t;
     int64_t now;         // engine clock during a push; the advance target for a timer sweep
     int64_t now0;        // the engine clock before a wall-clock timer sweep
+    uint32_t kpl;        // k_gen_batch: keys per lane (lane l of block b walks keys (b*kpl + j)*64 + l)
+    uint32_t pad;
 };

@@ -729,8 +729,18 @@ static size_t type_size(int t) {
 enum { GEN_L_BATCH = 0, GEN_L_TIMERS = 1, GEN_L_DEADLINES = 2 };
 // timer sweeps: a fixed grid of one-wave blocks striding over the due keys (their number is on the device)
 #define GEN_TIMER_BLOCKS 4096u
-static void launch_gen(GenEngine* e, const GenArgs& a, int which) {
+// keys per lane of k_gen_batch: 1 (GEN_KPL=n, experiments: n keys per lane).  Measured on C3/C3_min1/C4 at
+// 2^20 keys with 4 keys per lane (one resident wave per slot, a lane's runs averaging out): 2-7 % slower
+// than one key per lane — the kernel is bound by its memory transactions, not by idle lanes
+static uint32_t gen_kpl(uint32_t K) {
+    (void)K;
+    if (const char* x = getenv("GEN_KPL")) return std::max(1u, (uint32_t)strtoul(x, nullptr, 0));
+    return 1u;
+}
+
+static void launch_gen(GenEngine* e, GenArgs a, int which) {
     const uint32_t blocks = (e->K + 63) / 64;
+    a.kpl = gen_kpl(e->K);
     const uint32_t slot = e->arg_next++ % GEN_ARG_SLOTS;
     if (slot == 0 && e->arg_next > 1) GH_OK(hipStreamSynchronize(e->stream));
     e->h_args[slot] = a;
@@ -741,7 +751,7 @@ static void launch_gen(GenEngine* e, const GenArgs& a, int which) {
         hipLaunchKernelGGL(k_gen_timers, dim3(e->host.partitioned ? std::min(blocks, GEN_TIMER_BLOCKS) : 1u), dim3(64), 0,
                            e->stream, ap);
     else if (which == GEN_L_DEADLINES) hipLaunchKernelGGL(k_gen_deadlines, dim3(blocks), dim3(64), 0, e->stream, ap);
-    else hipLaunchKernelGGL(k_gen_batch, dim3(blocks), dim3(64), 0, e->stream, ap);
+    else hipLaunchKernelGGL(k_gen_batch, dim3((e->K + 64u * a.kpl - 1) / (64u * a.kpl)), dim3(64), 0, e->stream, ap);
     GH_OK(hipGetLastError());
     if (t0) e->spans.push_back({t0, e->ev(), 1});
 }

@@ -75,6 +75,16 @@ struct Lane {
         split = G.offST;
         pool = S + (size_t)split * K + (size_t)k * (G.blockWords - split);
     }
+    // the next key of this lane (k_gen_batch walks several keys per lane; the work counters, the error
+    // bits and the raw-slot reservation carry over)
+    __device__ void retarget(uint32_t key) __restrict__ {
+        k = key;
+        pool = S + (size_t)split * K + (size_t)k * (G.blockWords - split);
+        trigSeq = SG_TIMER_SEQ;
+        trigIdx = 0;
+        trigRank = 0;
+        retm = 0;
+    }
 
     // ---- HBM words of this key ----
     // (gen_engine.h gen_at: KeyState words interleaved across keys, pool words contiguous per key)
@@ -1165,26 +1175,54 @@ __device__ void gen_wave_stats(const GenArgs& a, unsigned long long sc, unsigned
 #ifndef GEN_WAVES
 #define GEN_WAVES 4
 #endif
+// Several keys per lane (a.kpl, sized by the host so that the grid is about one resident wave per slot):
+// lane l of block b walks keys (b*kpl + j)*64 + l for j = 0..kpl-1, one flat loop whose every step is
+// either one event or the switch to the lane's next key, so a wave runs for the longest SUM of its lanes'
+// runs instead of the sum over j of the longest run (Poisson runs of a few events per key: one key per
+// lane leaves half of every wave's lane-steps idle).  A wave's 64 lanes still touch 64
+// consecutive keys of one row of the interleaved state at each j.
 extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GEN_WAVES, 8))) k_gen_batch(const GenArgs* __restrict__ ap) {
     const GenArgs& a = *ap;
-    const uint32_t key = blockIdx.x * blockDim.x + threadIdx.x;
-    unsigned long long sc = 0, cr = 0, ma = 0, ky = 0;
-    uint32_t er = 0;
-    if (key < a.K && gp(a.b.seg_begin)[key] < gp(a.b.seg_end)[key]) {
-        const uint32_t b = gp(a.b.seg_begin)[key], e = gp(a.b.seg_end)[key];
-        Lane L(a, key);
-        L.initKey();
-#if GENX_PROF
-        { const uint64_t t_ = __builtin_amdgcn_s_memtime(); L.prof[0] += t_ - L.prof_t; L.prof_t = t_; }
-#endif
-        const auto& r = L.G.recv[a.b.stream];
-        if (r.n > 0) {
-            for (uint32_t j = b; j < e; j++) {
-                const uint32_t pos = a.b.sidx ? gp(a.b.sidx)[j] : j;
-                const uint32_t nxt = (j + 1 < e) ? (a.b.sidx ? gp(a.b.sidx)[j + 1] : j + 1) : 0xffffffffu;
-                L.processEvent(r, pos, nxt != pos + 1);
+    const uint32_t kpl = a.kpl ? a.kpl : 1u;
+    const uint32_t k0 = blockIdx.x * kpl * 64u + threadIdx.x;
+    const auto& r = ((const cGenProgram*)a.G)->recv[a.b.stream];
+    Lane L(a, k0);
+    uint32_t j = 0, i = 0, e = 0;
+    bool open = false, any = false;
+    unsigned long long ky = 0;
+    for (;;) {
+        if (!open) {
+            uint32_t key = 0;
+            for (; j < kpl; j++) {  // the lane's next key with events in this batch
+                key = k0 + j * 64u;
+                if (key < a.K && gp(a.b.seg_begin)[key] < gp(a.b.seg_end)[key]) break;
             }
+            if (j >= kpl) break;
+            i = gp(a.b.seg_begin)[key];
+            e = gp(a.b.seg_end)[key];
+            L.retarget(key);
+            L.initKey();
+            open = true;
+            any = true;
+#if GENX_PROF
+            { const uint64_t t_ = __builtin_amdgcn_s_memtime(); L.prof[0] += t_ - L.prof_t; L.prof_t = t_; }
+#endif
+            if (r.n == 0) i = e;
         }
+        if (i < e) {
+            const uint32_t pos = a.b.sidx ? gp(a.b.sidx)[i] : i;
+            const uint32_t nxt = (i + 1 < e) ? (a.b.sidx ? gp(a.b.sidx)[i + 1] : i + 1) : 0xffffffffu;
+            L.processEvent(r, pos, nxt != pos + 1);
+            i++;
+        }
+        if (i >= e) {  // the key's run is done
+            if (a.G->nStartup > 0) gp(a.t.nd)[L.k] = L.nextDeadline();
+            ky++;
+            open = false;
+            j++;
+        }
+    }
+    if (any) {
         // unused reserved raw slots are marked empty
         for (uint32_t x = 0; x < L.resLeft; x++) {
             const unsigned long long rr = L.resBase + x;
@@ -1193,22 +1231,16 @@ extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per
                 gp(a.o.tk1)[rr] = 0xffffffffu;  // sorts after every real timer match
             }
         }
-        if (a.G->nStartup > 0) gp(a.t.nd)[key] = L.nextDeadline();
-        er = L.err;
-        sc = L.scanned;
-        cr = L.created;
-        ma = L.matches;
-        ky = 1;
 #if GENX_PROF
         { const uint64_t t_ = __builtin_amdgcn_s_memtime(); L.prof[4] += t_ - L.prof_t; L.prof_t = t_; }
         if (a.o.prof && (threadIdx.x & 63) == __builtin_amdgcn_readfirstlane(threadIdx.x & 63))
-            for (int i = 0; i < 5; i++) atomicAdd(&a.o.prof[i], (unsigned long long)L.prof[i]);
+            for (int q = 0; q < 5; q++) atomicAdd(&a.o.prof[q], (unsigned long long)L.prof[q]);
 #endif
     }
 #if GENX_PROF
     if (a.o.prof && (threadIdx.x & 63) == 0) atomicAdd(&a.o.prof[6], 1ull);
 #endif
-    gen_wave_stats(a, sc, cr, ma, ky, er);
+    gen_wave_stats(a, L.scanned, L.created, L.matches, ky, L.err);
 }
 
 // ------------------------------------------------------------------------------------------------
