@@ -343,13 +343,16 @@ __global__ void k_bump(unsigned long long* out_count, const unsigned long long* 
     *out_count += *batch_total;
 }
 
-// per-batch counters of the staged advance pass: one row per wave -> the cumulative totals
-__global__ void __launch_bounds__(1024) k_stats_reduce(const unsigned long long* __restrict__ wstats,
-                                                       uint32_t n_waves, unsigned long long* __restrict__ stats) {
-    __shared__ unsigned long long part[SGD_ST_N][16];
+// per-batch counters of the staged advance pass: one row per wave -> the cumulative totals (blocks stride
+// over the rows; one atomic per counter per block)
+__global__ void __launch_bounds__(256) k_stats_reduce(const unsigned long long* __restrict__ wstats,
+                                                      uint32_t n_waves, unsigned long long* __restrict__ stats,
+                                                      unsigned long long* __restrict__ raw_count) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) *raw_count = 0;  // the next advance's atomic slot counter
+    __shared__ unsigned long long part[SGD_ST_N][4];
     unsigned long long acc[SGD_ST_N];
     for (int i = 0; i < SGD_ST_N; ++i) acc[i] = 0;
-    for (uint32_t w = threadIdx.x; w < n_waves; w += blockDim.x)
+    for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < n_waves; w += gridDim.x * blockDim.x)
         for (int i = 0; i < SGD_ST_N; ++i) acc[i] += wstats[(size_t)w * SGD_ST_N + i];
     for (int i = 0; i < SGD_ST_N; ++i)
         for (int off = 32; off > 0; off >>= 1) acc[i] += __shfl_xor(acc[i], off, 64);
@@ -358,9 +361,8 @@ __global__ void __launch_bounds__(1024) k_stats_reduce(const unsigned long long*
         for (int i = 0; i < SGD_ST_N; ++i) part[i][wv] = acc[i];
     __syncthreads();
     if (threadIdx.x < SGD_ST_N) {
-        unsigned long long t = 0;
-        for (int j = 0; j < (int)(blockDim.x / 64); ++j) t += part[threadIdx.x][j];
-        stats[threadIdx.x] += t;
+        const unsigned long long t = part[threadIdx.x][0] + part[threadIdx.x][1] + part[threadIdx.x][2] + part[threadIdx.x][3];
+        if (t) atomicAdd(&stats[threadIdx.x], t);
     }
 }
 
@@ -391,8 +393,9 @@ int sgd_launch_check_keys(const uint32_t* keys, uint32_t n, uint32_t n_keys, uin
 }
 
 int sgd_launch_stats_reduce(const unsigned long long* wstats, uint32_t n_waves, unsigned long long* stats,
-                            ihipStream_t* stream) {
-    hipLaunchKernelGGL(k_stats_reduce, dim3(1), dim3(1024), 0, stream, wstats, n_waves, stats);
+                            unsigned long long* raw_count, ihipStream_t* stream) {
+    const uint32_t blocks = std::max(1u, std::min(64u, (n_waves + 255u) / 256u));
+    hipLaunchKernelGGL(k_stats_reduce, dim3(blocks), dim3(256), 0, stream, wstats, n_waves, stats, raw_count);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

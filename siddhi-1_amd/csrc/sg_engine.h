@@ -222,4 +222,4 @@ int sgd_launch_reset_keys(const uint32_t* keys, uint32_t n, uint32_t n_keys, uin
 int sgd_launch_check_keys(const uint32_t* keys, uint32_t n, uint32_t n_keys, uint32_t* bad, ihipStream_t* stream);
 // sums the staged pass's per-wave counters of one batch into stats[SGD_ST_N]
 int sgd_launch_stats_reduce(const unsigned long long* wstats, uint32_t n_waves, unsigned long long* stats,
-                            ihipStream_t* stream);
+                            unsigned long long* raw_count, ihipStream_t* stream);

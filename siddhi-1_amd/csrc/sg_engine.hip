@@ -597,7 +597,8 @@ void allocate(sg_engine* e) {
     if (e->raw_cap >= (1ull << 32)) throw std::invalid_argument("n_keys x partial_capacity too large for one engine");
     e->wstats = dalloc<unsigned long long>(nw * SGD_ST_N, o);
     e->raw_e1 = dalloc<uint64_t>(e->raw_cap, o);
-    e->raw_count = dalloc<unsigned long long>(1, o);
+    e->raw_count = dalloc<unsigned long long>(1, o);  // zeroed here, then by k_stats_reduce after every advance
+    HIP_OK(hipMemsetAsync(e->raw_count, 0, 8, e->stream));
     e->t_desc = dalloc<uint64_t>(B, o);
     e->deferred = dalloc<uint32_t>((K + SGD_BLOCK - 1) / SGD_BLOCK * (SGD_BLOCK / SGD_WAVE), o);
     e->resume = dalloc<uint32_t>(K, o);
@@ -924,7 +925,6 @@ int push(sg_engine* e, const sg_batch* b) {
     p.raw_capw = e->raw_capw;
     p.raw_capnull = e->raw_capnull;
     for (size_t i = 0; i < e->consts.size(); i++) p.cst[i] = e->consts[i];
-    HIP_OK(hipMemsetAsync(e->raw_count, 0, 8, e->stream));
     hipEvent_t a0 = nullptr, a1 = nullptr;
     if (e->timing) { a0 = e->ev(); e->mark(a0); }
     {
@@ -934,7 +934,7 @@ int push(sg_engine* e, const sg_batch* b) {
         if (e->timing) { a1 = e->ev(); e->mark(a1); e->spans.push_back({a0, a1, 1}); a0 = e->ev(); e->mark(a0); }
         launch(v.adv_h[role], blocks, SGD_BLOCK, &p, e->stream);
         if (e->timing) { a1 = e->ev(); e->mark(a1); e->spans.push_back({a0, a1, 3}); }
-        if (sgd_launch_stats_reduce(e->wstats, blocks * (SGD_BLOCK / SGD_WAVE), e->stats, e->stream) != 0)
+        if (sgd_launch_stats_reduce(e->wstats, blocks * (SGD_BLOCK / SGD_WAVE), e->stats, e->raw_count, e->stream) != 0)
             throw HipError("k_stats_reduce launch failed");
     }
     e->st.advance_launches++;
