@@ -285,7 +285,7 @@ def output_inclusive(sa, synth, torch, dev, n_keys, batch, steps):
                           match_capacity=2 * batch, device=dev.index or 0)
     eng.set_projection(*cp.projection_program(cq, strings))
     W = 3   # warmup steps: the pinned host staging grows to the largest window before the timed region
-    bats = [to_dev(torch, synth.stock_ticks(s * batch, batch, n_keys), dev) for s in range(steps + W)]
+    bats = [synth.stock_ticks_torch(torch, s * batch, batch, n_keys, dev) for s in range(steps + W)]
     torch.cuda.synchronize()
 
     def step(s, ready=True):
@@ -363,7 +363,8 @@ def api_inclusive(sa, synth, n_keys, chunk, chunks):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    # 64 steps of 2^24 events: 1.07e9 events per run (>= 1e9)
+    ap.add_argument("--steps", type=int, default=64)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=1 << 24)
     ap.add_argument("--keys", type=int, default=None, help="keys per GPU (default: 2^20 at N=1 (C2), 2^23 at N>1 (C5))")
@@ -415,8 +416,8 @@ def main():
     ISO = 3
     for s in range(total + (1 if world > 1 else ISO)):
         base = s * world * B + rank * B
-        d = synth.stock_ticks(base, B, K * world, rate_per_ms=2000 * world)
-        t = to_dev(torch, d, dev)
+        # generated on the device, bit-identical to synth.stock_ticks (tests/test_synth.py)
+        t = synth.stock_ticks_torch(torch, base, B, K * world, dev, rate_per_ms=2000 * world)
         if world > 1:
             del t["symbol"]
         batches.append(t)

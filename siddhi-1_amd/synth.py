@@ -104,6 +104,46 @@ def stock_ticks(start: int, n: int, n_keys: int, seed: int = SEED, rate_per_ms: 
     return {"key": key, "ts": ts, "symbol": key.copy(), "price": price, "volume": volume}
 
 
+def _i64(u: int) -> int:
+    """a uint64 constant as the int64 with the same bits (torch has no uint64 arithmetic)"""
+    return u - (1 << 64) if u >= (1 << 63) else u
+
+
+def _srl(torch, x, n: int):
+    """logical right shift of int64 bit patterns"""
+    return (x >> n) & ((1 << (64 - n)) - 1)
+
+
+def splitmix64_torch(torch, x):
+    """splitmix64 over int64 tensors holding uint64 bit patterns (wrapping multiplication)"""
+    z = x + _i64(0x9E3779B97F4A7C15)
+    z = (z ^ _srl(torch, z, 30)) * _i64(0xBF58476D1CE4E5B9)
+    z = (z ^ _srl(torch, z, 27)) * _i64(0x94D049BB133111EB)
+    return z ^ _srl(torch, z, 31)
+
+
+def stock_ticks_torch(torch, start: int, n: int, n_keys: int, device, seed: int = SEED, rate_per_ms: int = 2000,
+                      t0: int = T0):
+    """stock_ticks generated on `device` (bit-identical values; n_keys a power of two): dict of tensors key,
+    symbol (int32 bit patterns of the uint32 ids), ts (int64), price (float32), volume (int32).  The bench
+    builds its HBM-resident batches with it (the numpy generator takes seconds per 2^24-event batch)."""
+    if n_keys & (n_keys - 1):
+        raise ValueError("stock_ticks_torch: n_keys must be a power of two")
+    i = torch.arange(start, start + n, dtype=torch.int64, device=device)
+    base = _i64((seed * 0x100000001B3) & ((1 << 64) - 1)) if seed else 0
+    s = i * 3 + base
+    h0 = splitmix64_torch(torch, s)
+    h1 = splitmix64_torch(torch, s + 1)
+    h2 = splitmix64_torch(torch, s + 2)
+    key = (h0 & (n_keys - 1)).to(torch.int32)
+    u = _srl(torch, h1, 40).to(torch.float64) / float(1 << 24)
+    price = (10.0 + 30.0 * u).to(torch.float32)
+    # h2 mod 2000 of the unsigned value: 2 * ((h2 >>> 1) mod 1000) + (h2 & 1)
+    volume = (1 + 2 * (_srl(torch, h2, 1) % 1000) + (h2 & 1)).to(torch.int32)
+    ts = t0 + torch.div(i, rate_per_ms, rounding_mode="floor")
+    return {"key": key, "ts": ts, "symbol": key.clone(), "price": price, "volume": volume}
+
+
 def burst_ticks(start_ms: int, n_ms: int, n_keys: int, burst: int, seed: int = SEED, t0: int = T0):
     """C4 input: millisecond t carries `burst` events of ONE key (key = h(t) % n_keys), timestamp
     t0 + t.  Timer due times of different keys then never coincide, which keeps the reference's
