@@ -150,6 +150,7 @@ struct ScatterParams {
     uint32_t n_capw;
     uint64_t* out_first;       // aggregators: per batch event, count << 32 | ring position of its first
                                // record (0: no match); NULL otherwise
+    uint32_t exp;              // SG_ORDER_EXP ablations (timing experiments only, wrong results), 0 otherwise
 };
 #define SGD_ORDER_TILE 4096  // triggers per workgroup of the ordering kernels (256 threads x 16 rows)
 // On-device projection of the select list (sg_set_projection) for the two-state kernel: after the ordering

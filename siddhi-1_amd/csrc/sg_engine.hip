@@ -968,6 +968,7 @@ int push(sg_engine* e, const sg_batch* b) {
         sp.o_capnull = e->o_capnull;
         sp.n_capw = e->n_capw;
         sp.out_first = (proj && e->n_agg) ? e->out_first : nullptr;
+        if (const char* x = getenv("SG_ORDER_EXP")) sp.exp = (uint32_t)strtoul(x, nullptr, 0);
         if (sgd_launch_scatter(sp, e->scan_tmp, e->scan_tmp_bytes, e->stream) != 0)
             throw HipError("ordering launch failed");
         if (proj) {

@@ -191,6 +191,27 @@ def test_gpu_far_timestamps(within):
     assert gpu.stats()["matches"] == ora.stats()["matches"] > 0
 
 
+@pytest.mark.parametrize("first", ["unset", "far_past", "far_future"])
+def test_gpu_batch_base_timestamp_far(first):
+    """the payload's 32-bit timestamps are offsets from the batch's FIRST (arrival-order) timestamp: when
+    that one is -1 or far from the rest, every other event of the batch is out of offset range and runs
+    on the 64-bit path (the HBM pass reads the ts column), bit-exact"""
+    q = (STOCK + "partition with (symbol of S) begin from every e1=S[price>20] -> e2=S[price>e1.price] "
+         "within 1 sec select e1.price as a insert into O; end;")
+    n_keys, batch = 512, 20000
+    cq, gpu, ora = _engines(q, n_keys, batch)
+    seq = 0
+    for b in range(3):
+        d = synth.stock_ticks(seq, batch, n_keys, seed=70 + b, rate_per_ms=16)
+        ts = d["ts"].copy()
+        ts[0] = {"unset": -1, "far_past": ts[1] - (np.int64(1) << 31), "far_future": ts[1] + (np.int64(1) << 35)}[first]
+        for e in (gpu, ora):
+            e.push(0, seq, ts, [d["symbol"], d["price"], d["volume"]], None, d["key"])
+        seq += batch
+        _same(gpu.poll(), ora.poll())
+    assert gpu.stats()["matches"] == ora.stats()["matches"] > 0
+
+
 def test_gpu_unpartitioned_single_key():
     q = STOCK + "from every e1=S[price>20] -> e2=S[price>e1.price] within 10 sec select e1.price as a insert into O;"
     cq, gpu, ora = _engines(q, 1, 20000)

@@ -21,18 +21,18 @@ template <unsigned B, unsigned I, unsigned BITS, rocprim::block_radix_rank_algor
 using Cfg = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
     rocprim::radix_sort_onesweep_config<rocprim::kernel_config<B, I>, rocprim::kernel_config<B, I>, BITS, ALG>>;
 
-template <class C>
+template <class C, unsigned KB = 20>
 void run(const char* name, const uint32_t* keys, uint32_t* skeys, const uint32_t* price, const int64_t* ts, Pay* out,
          uint32_t n) {
     auto it = rocprim::make_transform_iterator(rocprim::counting_iterator<uint32_t>(0), Fn{price, ts});
     size_t tmpb = 0;
-    CK(rocprim::radix_sort_pairs<C>(nullptr, tmpb, keys, skeys, it, out, n, 0u, 20u, 0));
+    CK(rocprim::radix_sort_pairs<C>(nullptr, tmpb, keys, skeys, it, out, n, 0u, KB, 0));
     void* tmp; CK(hipMalloc(&tmp, tmpb));
     hipEvent_t a, b; CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
-    for (int i = 0; i < 3; i++) CK(rocprim::radix_sort_pairs<C>(tmp, tmpb, keys, skeys, it, out, n, 0u, 20u, 0));
+    for (int i = 0; i < 3; i++) CK(rocprim::radix_sort_pairs<C>(tmp, tmpb, keys, skeys, it, out, n, 0u, KB, 0));
     const int R = 20;
     CK(hipEventRecord(a, 0));
-    for (int i = 0; i < R; i++) CK(rocprim::radix_sort_pairs<C>(tmp, tmpb, keys, skeys, it, out, n, 0u, 20u, 0));
+    for (int i = 0; i < R; i++) CK(rocprim::radix_sort_pairs<C>(tmp, tmpb, keys, skeys, it, out, n, 0u, KB, 0));
     CK(hipEventRecord(b, 0)); CK(hipEventSynchronize(b));
     float ms; CK(hipEventElapsedTime(&ms, a, b));
     std::vector<uint32_t> hk(n); std::vector<Pay> hp(n);
@@ -53,12 +53,14 @@ int main() {
     CK(hipMemcpy(keys, hk.data(), n * 4, hipMemcpyHostToDevice)); CK(hipMemcpy(price, hpz.data(), n * 4, hipMemcpyHostToDevice));
     CK(hipMemcpy(ts, ht.data(), n * 8, hipMemcpyHostToDevice));
     using M = rocprim::block_radix_rank_algorithm;
-    run<Cfg<1024, 10, 10, M::match>>("1024x10 b10 match", keys, skeys, price, ts, out, n);
-    run<Cfg<1024, 11, 10, M::match>>("1024x11 b10 match", keys, skeys, price, ts, out, n);
-    run<Cfg<1024, 14, 10, M::match>>("1024x14 b10 match", keys, skeys, price, ts, out, n);
     run<Cfg<1024, 16, 10, M::match>>("1024x16 b10 match", keys, skeys, price, ts, out, n);
-    run<Cfg<768, 12, 10, M::match>>("768x12 b10 match", keys, skeys, price, ts, out, n);
-    run<Cfg<768, 16, 10, M::match>>("768x16 b10 match", keys, skeys, price, ts, out, n);
-    run<rocprim::default_config>("default", keys, skeys, price, ts, out, n);
+    // 2^23 keys (C5 per GPU): three passes either way
+    for (uint32_t i = 0; i < n; i++) hk[i] = (uint32_t)(((uint64_t)hk[i] * 2654435761u + i) % (1u << 23));
+    CK(hipMemcpy(keys, hk.data(), n * 4, hipMemcpyHostToDevice));
+    run<rocprim::default_config, 23>("default, 23-bit", keys, skeys, price, ts, out, n);
+    run<Cfg<1024, 16, 8, M::match>, 23>("1024x16 b8, 23-bit", keys, skeys, price, ts, out, n);
+    run<Cfg<1024, 16, 10, M::match>, 23>("1024x16 b10, 23-bit", keys, skeys, price, ts, out, n);
+    run<Cfg<1024, 10, 8, M::match>, 23>("1024x10 b8, 23-bit", keys, skeys, price, ts, out, n);
+    run<Cfg<1024, 8, 11, M::match>, 23>("1024x8 b11, 23-bit", keys, skeys, price, ts, out, n);
     return 0;
 }
