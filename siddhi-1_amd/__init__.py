@@ -8,7 +8,8 @@ ctypes binding of the HIP engine library (lib/libsiddhi_gpu.so, built from csrc/
 The directory name is not a Python identifier; import it with
 ``importlib.import_module("siddhi-1_amd")``.
 """
-from .runtime import (Event, InputHandler, QueryCallback, SiddhiAppRuntime, SiddhiManager,  # noqa: F401
+from .runtime import (Event, InputHandler, QueryCallback, ColumnarQueryCallback, SiddhiAppRuntime,  # noqa: F401
+                      SiddhiManager,
                       StreamCallback, StringDictionary, InMemoryPersistenceStore,
                       CannotRestoreSiddhiAppStateException, NoPersistenceStoreException)
 from .compiler import compile_query, SiddhiAppCreationException  # noqa: F401

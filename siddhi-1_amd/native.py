@@ -127,7 +127,24 @@ SG_KEY_NULL = 0xFFFFFFFF
 
 def pack_strings(strings):
     """Arrow-style (bytes, offsets[n+1], valid) of a sequence of str/None (UTF-8, as Java's String
-    bytes for the dictionary's equality)."""
+    bytes for the dictionary's equality).  A numpy bytes array ('S', UTF-8, no nulls) packs without a
+    per-value Python loop (numpy drops trailing NUL characters of fixed-width strings)."""
+    if isinstance(strings, np.ndarray) and strings.dtype.kind == "U":
+        strings = strings.tolist()   # (one encode per value below: faster than np.char.encode)
+    if isinstance(strings, np.ndarray) and strings.dtype.kind == "S":
+        enc = strings
+        n, w = len(enc), enc.dtype.itemsize
+        lens = np.char.str_len(enc).astype(np.uint64) if n else np.zeros(0, dtype=np.uint64)
+        offsets = np.zeros(n + 1, dtype=np.uint64)
+        np.cumsum(lens, out=offsets[1:])
+        if n and w:
+            mat = np.ascontiguousarray(enc).view(np.uint8).reshape(n, w)
+            data = mat[np.arange(w, dtype=np.uint64)[None, :] < lens[:, None]]
+        else:
+            data = np.zeros(0, dtype=np.uint8)
+        if data.size == 0:
+            data = np.zeros(1, dtype=np.uint8)
+        return np.ascontiguousarray(data), offsets, np.ones(n, dtype=np.uint8)
     enc = [s.encode("utf-8") if s is not None else b"" for s in strings]
     offsets = np.zeros(len(enc) + 1, dtype=np.uint64)
     if enc:

@@ -74,6 +74,18 @@ class QueryCallback:
         raise NotImplementedError
 
 
+class ColumnarQueryCallback:
+    """Columnar counterpart of QueryCallback (an addition to the reference API, for callers that take
+    the output as arrays): receive_columns(timestamps, columns, trigger_seq) once per delivery with every
+    match of it in QueryCallback's order — the rows QueryCallback.receive would get, one call per trigger
+    there, concatenated.  `columns` maps each select item's name to a numpy array (STRING items: object
+    arrays; null values: masked arrays, or None in object arrays); trigger_seq is the arrival sequence
+    number of each row's triggering event (SG_TIMER_SEQ for a timer-emitted match)."""
+
+    def receive_columns(self, timestamps, columns, trigger_seq):
+        raise NotImplementedError
+
+
 class _FnStreamCallback(StreamCallback):
     def __init__(self, fn):
         self.fn = fn
@@ -194,23 +206,61 @@ BLANK_SEQ = 0xFFFFFFFFFFFFFFFE      # SG_BLANK_SEQ: the attribute-less event an 
 
 
 class _EventStore:
+    """seq -> (stream name, ts, data tuple).  Columnar sends (InputHandler.send_columns) append their
+    arrays as they are; their rows are built only when something reads them (host projection, state
+    documents, snapshots)."""
+
     def __init__(self):
-        self.rows = []          # seq -> (stream name, ts, data tuple)
+        self._rows = []
+        self._pending = []      # (stream, ts array, column arrays) after _rows, in seq order
+        self._pending_n = 0
+
+    @property
+    def rows(self):
+        self._flush()
+        return self._rows
+
+    @rows.setter
+    def rows(self, v):
+        self._pending, self._pending_n = [], 0
+        self._rows = v
+
+    def __len__(self):
+        return len(self._rows) + self._pending_n
+
+    def _flush(self):
+        for stream, ts, cols in self._pending:
+            vals = [c.tolist() if not np.ma.isMaskedArray(c) else
+                    [None if m else x for x, m in zip(c.data.tolist(), np.ma.getmaskarray(c).tolist())]
+                    for c in cols]
+            self._rows.extend(zip([stream] * len(ts), ts.tolist(), zip(*vals) if vals else [()] * len(ts)))
+        self._pending, self._pending_n = [], 0
 
     def add(self, stream, ts, data):
-        self.rows.append((stream, ts, data))
-        return len(self.rows) - 1
+        self._flush()
+        self._rows.append((stream, ts, data))
+        return len(self._rows) - 1
 
     def add_many(self, stream, ts, datas):
         """consecutive seqs for a chunk of events; returns the first"""
-        base = len(self.rows)
-        self.rows.extend(zip([stream] * len(ts), ts, map(tuple, datas)))
+        self._flush()
+        base = len(self._rows)
+        self._rows.extend(zip([stream] * len(ts), ts, map(tuple, datas)))
+        return base
+
+    def add_columns(self, stream, ts, cols):
+        """consecutive seqs for a columnar chunk (kept as arrays until a row is read); returns the first"""
+        base = len(self)
+        self._pending.append((stream, ts, cols))
+        self._pending_n += len(ts)
         return base
 
     def get(self, seq):
         if int(seq) == BLANK_SEQ:
             return (None, -1, _NullRow())
-        return self.rows[int(seq)]
+        if self._pending:
+            self._flush()
+        return self._rows[int(seq)]
 
 
 class _NullRow:
@@ -232,6 +282,14 @@ class StringDictionary:
             self.ids[s] = i
             self.strs.append(s)
         return i
+
+    def array(self):
+        """the strings as a numpy object array indexed by id (+ None at index len: a null's slot),
+        extended as the dictionary grows"""
+        a = getattr(self, "_arr", None)
+        if a is None or len(a) != len(self.strs) + 1:
+            a = self._arr = np.array(self.strs + [None], dtype=object)
+        return a
 
     def ids_of(self, vals):
         """id_of over a column (one dict probe per value; new strings numbered in first-seen order)"""
@@ -286,6 +344,7 @@ class _QueryRuntime:
             except EngineError:
                 self.device_projection = False
         self.query_callbacks: List[QueryCallback] = []
+        self.columnar_callbacks: List[ColumnarQueryCallback] = []
         # aggregator states: (partition key, group-by key) -> one state per aggregator
         # (PartitionStateHolder over the group-by flow's states, C/util/snapshot/state/*StateHolder.java)
         self._agg_states: Dict[tuple, list] = {}
@@ -445,6 +504,79 @@ class _QueryRuntime:
             out.append((int(m.trigger_seq[i]), int(m.ts[i]), data))
         return out
 
+    _NPT = {"INT": np.int32, "LONG": np.int64, "FLOAT": np.float32, "DOUBLE": np.float64, "BOOL": np.bool_}
+
+    def _decode_array(self, bits, null, typ):
+        """device projection bits of one item -> a typed numpy array (masked where null)"""
+        if typ == "INT":
+            vals = bits.astype(np.uint32).view(np.int32)
+        elif typ == "LONG":
+            vals = bits.view(np.int64)
+        elif typ == "FLOAT":
+            vals = bits.astype(np.uint32).view(np.float32)
+        elif typ == "DOUBLE":
+            vals = bits.view(np.float64)
+        elif typ == "BOOL":
+            vals = (bits & 1).astype(np.bool_)
+        else:   # STRING: the host dictionary id
+            strs = self.app_rt.strings.array()
+            ids = np.where(null != 0, len(strs) - 1, bits.astype(np.int64))
+            return strs[ids]
+        return np.ma.MaskedArray(vals, mask=null != 0) if null.any() else vals
+
+    def project_columns(self, m, store):
+        """(timestamps, {name: array}, trigger_seq) of the matches, `having` applied (device projection);
+        the row projection transposed otherwise"""
+        sel = self.cq.select
+        if self.device_projection and m.proj_value is not None:
+            keep = None
+            if self.cq.having is not None:
+                h, hn = m.proj_value[len(sel)], m.proj_null[len(sel)]
+                keep = np.nonzero((hn == 0) & ((h & 1) == 1))[0]
+            cols = {}
+            for i, (name, typ, _) in enumerate(sel):
+                v, nl = m.proj_value[i], m.proj_null[i]
+                if keep is not None:
+                    v, nl = v[keep], nl[keep]
+                cols[name] = self._decode_array(v, nl, typ)
+            ts, trig = (m.ts, m.trigger_seq) if keep is None else (m.ts[keep], m.trigger_seq[keep])
+            return np.asarray(ts, dtype=np.int64), cols, np.asarray(trig, dtype=np.uint64)
+        return self._rows_to_columns(self.project_host(m, store))
+
+    def _rows_to_columns(self, rows):
+        sel = self.cq.select
+        cols = {}
+        for i, (name, typ, _) in enumerate(sel):
+            vals = [r[2][i] for r in rows]
+            if typ in self._NPT and None not in vals:
+                cols[name] = np.array(vals, dtype=self._NPT[typ])
+            elif typ in self._NPT:
+                cols[name] = np.ma.MaskedArray(np.array([0 if v is None else v for v in vals], dtype=self._NPT[typ]),
+                                               mask=[v is None for v in vals])
+            else:
+                cols[name] = np.array(vals, dtype=object)
+        return (np.array([r[1] for r in rows], dtype=np.int64), cols,
+                np.array([r[0] for r in rows], dtype=np.uint64))
+
+    def deliver(self, m, store):
+        """the matches of one poll to the callbacks / the output stream (QuerySelector -> OutputCallback).
+        Rows are built only for row listeners (QueryCallbacks, StreamCallbacks of the output stream) and
+        for the host selector's aggregator states; a device projection nobody reads as rows stays arrays."""
+        out = self.cq.output_stream
+        listen = bool(self.query_callbacks) or bool(out is not None and self.app_rt.stream_callbacks.get(out))
+        rows = None
+        if listen or (not self.device_projection and not self.columnar_callbacks):
+            rows = self.project(m, store)
+            if listen:
+                self.dispatch(rows)
+        if self.columnar_callbacks and len(m):
+            # host projection updates aggregator states: project once, transpose the rows
+            cols = self._rows_to_columns(rows) if rows is not None and not self.device_projection \
+                else self.project_columns(m, store)
+            if len(cols[0]):
+                for cb in self.columnar_callbacks:
+                    cb.receive_columns(*cols)
+
     def dispatch(self, projected):
         """Deliver in trigger order; one callback call per trigger event (ReturnEventHolder).  A match
         emitted by a timer (absent state) is delivered on its own, at once
@@ -486,6 +618,13 @@ class InputHandler:
             self.app_rt._send(self.stream, [(e.timestamp, e.data) for e in a], explicit=True)
         else:
             self.app_rt._send(self.stream, [(self.app_rt.wall_time(), list(a))], explicit=False)
+
+    def send_columns(self, timestamps, columns):
+        """Columnar send (an addition to the reference API): the events (timestamps[i], [c[i] for c in
+        columns]) — what send(Event[]) would take, without the Event objects.  `columns` holds one array
+        per attribute in the stream's order (or a dict by attribute name): numpy arrays for numbers
+        (masked arrays for nulls), numpy str/bytes arrays or sequences of str/None for STRING."""
+        self.app_rt._send_columns(self.stream, timestamps, columns)
 
 
 # ------------------------------------------------------------------------------------------------
@@ -670,6 +809,11 @@ class SiddhiAppRuntime:
         return InputHandler(self, stream)
 
     def addCallback(self, name, cb):
+        if isinstance(cb, ColumnarQueryCallback):
+            if name not in self.by_name:
+                raise KeyError(f"query {name} does not exist")
+            self.by_name[name].columnar_callbacks.append(cb)
+            return
         if callable(cb) and not isinstance(cb, (StreamCallback, QueryCallback)):
             cb = _FnStreamCallback(cb) if name not in self.by_name else _FnQueryCallback(cb)
         if isinstance(cb, QueryCallback):
@@ -687,7 +831,7 @@ class SiddhiAppRuntime:
             pg.next_run = self.wall_time() + pg.interval
         for qr in self.queries:
             qr.engine.advance_time(self.current_time())
-            qr.dispatch(qr.project(qr.engine.poll(), self.store))
+            qr.deliver(qr.engine.poll(), self.store)
 
     # -- clock -------------------------------------------------------------------------------------
     def wall_time(self):
@@ -724,7 +868,7 @@ class SiddhiAppRuntime:
     def _fire_timers(self, now):
         for qr in self.queries:
             qr.engine.advance_time(now)
-            qr.dispatch(qr.project(qr.engine.poll(), self.store))
+            qr.deliver(qr.engine.poll(), self.store)
 
     def _set_event_time(self, ts):
         """TimestampGeneratorImpl.setCurrentTimestamp (playback)."""
@@ -957,7 +1101,7 @@ class SiddhiAppRuntime:
         cols, nulls = self._columns(sd, rows)
         kk = np.repeat(np.array(ids, dtype=np.uint32), n)
         qr.engine.push(si, seqs[0], ts_all, cols, nulls, kk)
-        qr.dispatch(qr.project(qr.engine.poll(), self.store))
+        qr.deliver(qr.engine.poll(), self.store)
 
     def _send(self, stream, events, explicit=True):
         if stream not in self.app.streams:
@@ -1014,8 +1158,139 @@ class SiddhiAppRuntime:
                         lo, hi = int(idx[0]), int(idx[-1]) + 1
                         qr.engine.push(si, base + lo, ts_all[lo:hi], [c[lo:hi] for c in cols],
                                        [x[lo:hi] if x is not None else None for x in nulls], kids[lo:hi])
-            m = qr.engine.poll()
-            qr.dispatch(qr.project(m, self.store))
+            qr.deliver(qr.engine.poll(), self.store)
+
+
+    def _send_columns(self, stream, timestamps, columns):
+        """InputHandler.send_columns: _send's path (send(Event[]) semantics) on arrays"""
+        if stream not in self.app.streams:
+            raise KeyError(stream)
+        sd = self.app.streams[stream]
+        na = len(sd.attrs)
+        if isinstance(columns, dict):
+            columns = [columns[an] for an, _ in sd.attrs]
+        if len(columns) != na:
+            raise ValueError(f"{len(columns)} columns for {stream}, expected {na}")
+        ts_all = np.ascontiguousarray(timestamps, dtype=np.int64)
+        n = len(ts_all)
+        cols_in = [c if isinstance(c, np.ndarray) or _is_categorical(c) else np.array(c, dtype=object)
+                   for c in columns]
+        for c in cols_in:
+            if len(c) != n:
+                raise ValueError(f"column of {len(c)} values for {n} timestamps")
+        if n == 0:
+            return
+        if self._purges or any(qr.cq.partitioned and qr.cq.partition_keys.get(stream, 0) is None
+                               and qr.cq.stream_index(stream) >= 0 for qr in self.queries):
+            # per-key bookkeeping of @purge and the broadcast of an unkeyed stream work on rows
+            vals = [c.tolist() if not np.ma.isMaskedArray(c) else
+                    [None if m else x for x, m in zip(c.data.tolist(), np.ma.getmaskarray(c).tolist())]
+                    for c in cols_in]
+            self._send(stream, list(zip(ts_all.tolist(), [list(r) for r in zip(*vals)])), explicit=True)
+            return
+        self._run_purges()
+        if self.playback:
+            self._set_event_time(int(ts_all[-1]))
+        elif self.started:
+            self._fire_timers(self.wall_time())
+        base = self.store.add_columns(stream, ts_all, cols_in)
+        cols_all = None
+        for qr in self.queries:
+            si = qr.cq.stream_index(stream)
+            if si < 0:
+                continue
+            if cols_all is None:
+                cols_all = self._columns_np(sd, cols_in)
+            cols, nulls = cols_all
+            if not qr.cq.partitioned:
+                qr.engine.push(si, base, ts_all, cols, nulls, None)
+            else:
+                ai = sd.attr_index(qr.cq.partition_keys[stream])
+                kc = cols_in[ai]
+                try:
+                    if _is_categorical(kc):   # one intern per distinct category (cached while unchanged)
+                        codes = np.asarray(kc.codes)
+                        cid = self._category_ids(kc.categories, ("key", id(qr.key_dict)),
+                                                 lambda cats: qr.key_dict.intern(java_strings(cats)))
+                        kids = np.where(codes < 0, np.uint32(SG_KEY_NULL),
+                                        cid[np.where(codes < 0, 0, codes)] if len(cid) else np.uint32(SG_KEY_NULL))
+                        kids = np.asarray(kids, dtype=np.uint32)
+                    else:
+                        keyvals = kc if kc.dtype.kind == "S" else java_strings(kc.tolist())
+                        kids = np.asarray(qr.key_dict.intern(keyvals), dtype=np.uint32)
+                except EngineError as ex:
+                    raise RuntimeError(f"more than {qr.n_keys} partition keys") from ex
+                keep = np.nonzero(kids != SG_KEY_NULL)[0]
+                if len(keep) == n:
+                    qr.engine.push(si, base, ts_all, cols, nulls, kids)
+                else:
+                    cut = np.nonzero(np.diff(keep) != 1)[0] + 1
+                    for idx in np.split(keep, cut):
+                        if len(idx) == 0:
+                            continue
+                        lo, hi = int(idx[0]), int(idx[-1]) + 1
+                        qr.engine.push(si, base + lo, ts_all[lo:hi], [c[lo:hi] for c in cols],
+                                       [x[lo:hi] if x is not None else None for x in nulls], kids[lo:hi])
+            qr.deliver(qr.engine.poll(), self.store)
+
+    def _category_ids(self, categories, what, make):
+        """ids of a categorical column's categories (`make` over their strings), cached per categories
+        object while it is alive and unchanged (a caller reusing one set of categories interns once; an
+        app with @purge, which releases key ids, never gets here: its sends take the row path)."""
+        cache = self.__dict__.setdefault("_cat_cache", {})
+        ent = cache.get((id(categories), what))
+        if ent is not None and ent[0] is categories and ent[1] == len(categories):
+            return ent[2]
+        cats = [None if v is None else (v.decode("utf-8") if isinstance(v, bytes) else str(v))
+                for v in list(categories)]
+        ids = np.asarray(make(cats), dtype=np.uint32)
+        cache[(id(categories), what)] = (categories, len(categories), ids)
+        return ids
+
+    def _columns_np(self, sd, cols_in):
+        """_columns over arrays: numeric arrays convert in one call, masked arrays give the null bytes,
+        STRING arrays map to dictionary ids (one probe per distinct value); object arrays (mixed Python
+        values, None) take _columns' per-value path"""
+        cols, nulls = [], []
+        for (an, at), c in zip(sd.attrs, cols_in):
+            if at == "STRING" and _is_categorical(c):
+                codes = np.asarray(c.codes)
+                ids = self._category_ids(c.categories, "attr", lambda cats: self.strings.ids_of(cats))
+                cols.append(ids[np.where(codes < 0, 0, codes)] if len(ids) else np.zeros(len(codes), np.uint32))
+                nulls.append((codes < 0).astype(np.uint8) if (codes < 0).any() else None)
+                continue
+            if at == "STRING" and c.dtype.kind in "SU":
+                vals = c.tolist() if c.dtype.kind == "U" else [x.decode("utf-8") for x in c.tolist()]
+                cols.append(np.asarray(self.strings.ids_of(vals), dtype=np.uint32))
+                nulls.append(None)
+                continue
+            if at in self._NP and c.dtype.kind in "biuf":
+                if np.ma.isMaskedArray(c):
+                    m = np.ma.getmaskarray(c)
+                    cols.append(np.ascontiguousarray(c.filled(0), dtype=self._NP[at]))
+                    nulls.append(m.astype(np.uint8) if m.any() else None)
+                else:
+                    cols.append(np.ascontiguousarray(c, dtype=self._NP[at]))
+                    nulls.append(None)
+                continue
+            vals = c.tolist() if not np.ma.isMaskedArray(c) else \
+                [None if m else x for x, m in zip(c.data.tolist(), np.ma.getmaskarray(c).tolist())]
+            one_c, one_n = self._columns(_OneAttr(an, at), [(v,) for v in vals])
+            cols.append(one_c[0])
+            nulls.append(one_n[0])
+        return cols, nulls
+
+
+def _is_categorical(c):
+    """a dictionary-encoded column (pandas.Categorical or anything with .codes / .categories)"""
+    return hasattr(c, "codes") and hasattr(c, "categories")
+
+
+class _OneAttr:
+    """a one-attribute stream definition for _columns' per-value path"""
+
+    def __init__(self, name, typ):
+        self.attrs = [(name, typ)]
 
 
 def _state_doc():
