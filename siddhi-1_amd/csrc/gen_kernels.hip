@@ -1365,7 +1365,11 @@ extern "C" __global__ void __launch_bounds__(256) k_gen_collapse(const unsigned 
 }
 
 // timer sweep over the due keys (every key when unpartitioned: key 0, seeded at start())
-extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GEN_WAVES, 8))) k_gen_timers(const GenArgs* __restrict__ ap) {
+// occupancy of the timer sweep (waves per SIMD), separate from the batch kernel's
+#ifndef GEN_TWAVES
+#define GEN_TWAVES GEN_WAVES
+#endif
+extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GEN_TWAVES, 8))) k_gen_timers(const GenArgs* __restrict__ ap) {
     const GenArgs& a = *ap;
 #if GENX_PROF
     const uint64_t t0_ = __builtin_amdgcn_s_memtime();

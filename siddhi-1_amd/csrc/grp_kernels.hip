@@ -62,14 +62,15 @@ __global__ void __launch_bounds__(1024) k_grp_hist(const GrpArgs a) {
 #pragma unroll
     for (uint32_t c = 0; c < GRP_KPT; ++c) {  // every load in flight at once
         const uint32_t i = i0 + c * 1024;
-        k[c] = i < a.n ? a.keys[i] : 0xfffffffeu;
+        k[c] = i < a.n ? a.keys[i] : 0u;
     }
     __syncthreads();
     bool bad = false;
 #pragma unroll
     for (uint32_t c = 0; c < GRP_KPT; ++c) {
+        if (i0 + c * 1024 >= a.n) continue;
         if (key_ok(k[c], a.K)) atomicAdd(&cnt[k[c] >> 8], 1u);
-        else if (k[c] != 0xfffffffeu && !(a.drop_null && k[c] == 0xffffffffu)) bad = true;
+        else if (!(a.drop_null && k[c] == 0xffffffffu)) bad = true;
     }
     // an out-of-range id is reported (the batch's other events go on), never written anywhere
     if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(a.err, (uint32_t)SGD_ERR_KEY_RANGE);
