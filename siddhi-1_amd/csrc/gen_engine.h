@@ -25,8 +25,16 @@
 #ifndef GEN_SPLIT
 #define GEN_SPLIT 0
 #endif
+// GEN_GRAN_LOG2 = g (experiments): granules of 2^g consecutive words of one key interleaved across keys,
+// word w of key k at ((w >> g) * K + k) << g | (w & (2^g - 1)); 0 (shipped) = one word per granule
+#ifndef GEN_GRAN_LOG2
+#define GEN_GRAN_LOG2 0
+#endif
+__host__ __device__ inline size_t gen_il(uint32_t K, uint32_t k, uint32_t w) {
+    return ((((size_t)(w >> GEN_GRAN_LOG2)) * K + k) << GEN_GRAN_LOG2) | (w & ((1u << GEN_GRAN_LOG2) - 1u));
+}
 __host__ __device__ inline size_t gen_at(uint32_t K, uint32_t blockWords, uint32_t split, uint32_t k, uint32_t w) {
-    if (!GEN_SPLIT || w < split) return (size_t)w * K + k;
+    if (!GEN_SPLIT || w < split) return gen_il(K, k, w);
     return (size_t)split * K + (size_t)k * (blockWords - split) + (w - split);
 }
 

@@ -347,7 +347,7 @@ GenProgram* gen_build_program(const uint32_t* w, size_t nw, uint32_t partialCap)
         off += ceil32(G->SECAP);
         G->offDef = off;
         off += 1 + 2 * G->DEF;
-        G->blockWords = off;
+        G->blockWords = (off + (1u << GEN_GRAN_LOG2) - 1u) & ~((1u << GEN_GRAN_LOG2) - 1u);  // whole granules
         return G;
     } catch (...) {
         delete G;
@@ -1045,7 +1045,7 @@ int gen_set_projection(GenEngine* e, const uint32_t* code, uint32_t words, const
     e->recWords += 3 * (S + H);
     if (A) {  // the aggregators' per-key state joins the key blocks (no push yet: all zero)
         G.offAgg = G.blockWords;
-        G.blockWords += 5 * A;
+        G.blockWords = (G.blockWords + 5 * A + (1u << GEN_GRAN_LOG2) - 1u) & ~((1u << GEN_GRAN_LOG2) - 1u);
         e->state = e->dalloc<uint32_t>((size_t)G.blockWords * e->K);
         GH_OK(hipMemsetAsync(e->state, 0, (size_t)G.blockWords * e->K * 4, e->stream));
     }
@@ -1193,7 +1193,7 @@ int gen_state_export(GenEngine* e, SdDoc& d, std::string& msg) {
     GenClock clk{};
     const int rc = gen_snapshot(e, S.data(), &clk, msg);
     if (rc != SG_OK) return rc;
-    auto W = [&](uint32_t k, uint32_t w) -> uint32_t { return S[(size_t)w * K + k]; };
+    auto W = [&](uint32_t k, uint32_t w) -> uint32_t { return S[gen_il(K, k, w)]; };
     auto R64 = [&](uint32_t k, uint32_t w) -> int64_t {
         return (int64_t)((uint64_t)W(k, w) | ((uint64_t)W(k, w + 1) << 32));
     };
@@ -1285,7 +1285,7 @@ int gen_state_import(GenEngine* e, const SdDoc& d, std::string& msg) {
         return SG_ERR_INVALID;
     }
     std::vector<uint32_t> S(gen_state_words(e), 0u);
-    auto W = [&](uint32_t k, uint32_t w) -> uint32_t& { return S[(size_t)w * K + k]; };
+    auto W = [&](uint32_t k, uint32_t w) -> uint32_t& { return S[gen_il(K, k, w)]; };
     auto W64 = [&](uint32_t k, uint32_t w, int64_t v) {
         W(k, w) = (uint32_t)(uint64_t)v;
         W(k, w + 1) = (uint32_t)((uint64_t)v >> 32);

@@ -89,7 +89,7 @@ struct Lane {
     // ---- HBM words of this key ----
     // (gen_engine.h gen_at: KeyState words interleaved across keys, pool words contiguous per key)
     __device__ __forceinline__ gu32& W(uint32_t w) const {
-        if (!GEN_SPLIT || w < split) return S[(size_t)w * K + k];
+        if (!GEN_SPLIT || w < split) return S[gen_il(K, k, w)];
         return pool[w - split];
     }
     __device__ __forceinline__ int64_t R64(uint32_t w) const __restrict__ {
