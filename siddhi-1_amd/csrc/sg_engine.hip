@@ -1355,8 +1355,12 @@ int sg_engine_create(const void* ir, size_t ir_len, const sg_config* cfg, sg_eng
         HIP_OK(hipGetDeviceCount(&ndev));
         if (cfg->device < 0 || cfg->device >= ndev) throw HipError("no such HIP device");
         HIP_OK(hipSetDevice(cfg->device));
-        HIP_OK(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
-        HIP_OK(hipStreamCreateWithFlags(&e->gstream, hipStreamNonBlocking));
+        // SG_STREAM_PRIO (experiments): "g" = the grouping stream at the higher priority, "m" = the main one
+        const char* pr = getenv("SG_STREAM_PRIO");
+        int plo = 0, phi = 0;
+        HIP_OK(hipDeviceGetStreamPriorityRange(&plo, &phi));
+        HIP_OK(hipStreamCreateWithPriority(&e->stream, hipStreamNonBlocking, (pr && pr[0] == 'm') ? phi : plo));
+        HIP_OK(hipStreamCreateWithPriority(&e->gstream, hipStreamNonBlocking, (pr && pr[0] == 'g') ? phi : plo));
         HIP_OK(hipStreamCreateWithFlags(&e->pstream, hipStreamNonBlocking));
         e->async_host = (cfg->flags & SG_CFG_ASYNC_HOST) != 0;
         allocate(e);
