@@ -1244,6 +1244,8 @@ class SiddhiAppRuntime:
         cats = [None if v is None else (v.decode("utf-8") if isinstance(v, bytes) else str(v))
                 for v in list(categories)]
         ids = np.asarray(make(cats), dtype=np.uint32)
+        if len(cache) >= 16:   # callers building new categories per send: keep the cache bounded
+            cache.clear()
         cache[(id(categories), what)] = (categories, len(categories), ids)
         return ids
 
