@@ -246,16 +246,18 @@ def test_gpu_capacity_overflow_fails_loudly():
 
 
 @pytest.mark.slow
-def test_gpu_baseline_size_key_subset_and_properties():
-    """C2 at BASELINE size: 1,048,576 keys, two 2^24-event batches.  Oracle on keys % 64 == 0."""
-    n_keys, batch = 1 << 20, 1 << 24
+@pytest.mark.parametrize("n_keys,mod", [(1 << 20, 64), (1 << 23, 512)], ids=["C2", "C5_per_gpu"])
+def test_gpu_baseline_size_key_subset_and_properties(n_keys, mod):
+    """C2 at BASELINE size: 1,048,576 keys, two 2^24-event batches; and C5's per-GPU shape (2^23 keys:
+    the three-pass 23-bit grouping).  Oracle on keys % mod == 0."""
+    batch = 1 << 24
     cq, gpu, ora = _engines(synth.C2_QUERY, n_keys, batch, mcap=1 << 24)
     seq = 0
     for b in range(2):
         d = synth.stock_ticks(seq, batch, n_keys)
         gpu.push(0, seq, d["ts"], [d["symbol"], d["price"], d["volume"]], None, d["key"])
         mg = gpu.poll()
-        sub = (d["key"] % 64) == 0
+        sub = (d["key"] % mod) == 0
         idx = np.nonzero(sub)[0]
         # the oracle sees the subset with the same arrival seqs (runs of consecutive positions)
         starts = np.concatenate([[0], np.nonzero(np.diff(idx) != 1)[0] + 1])
@@ -265,8 +267,8 @@ def test_gpu_baseline_size_key_subset_and_properties():
             ora.push(0, seq + int(sl[0]), d["ts"][sl], [d["symbol"][sl], d["price"][sl], d["volume"][sl]],
                      None, d["key"][sl])
         mo = ora.poll()
-        keep = (mg.key % 64) == 0
-        assert int(keep.sum()) == len(mo)
+        keep = (mg.key % mod) == 0
+        assert int(keep.sum()) == len(mo) and len(mo) > 0
         assert np.array_equal(mg.trigger_seq[keep], mo.trigger_seq)
         assert np.array_equal(mg.slot_seq[keep], mo.slot_seq)
         # size-independent properties of every match
