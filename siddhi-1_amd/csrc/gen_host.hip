@@ -120,6 +120,8 @@ struct Builder {
                     G.startup[G.nStartup++] = pre;
                 }
             }
+            if (slot >= GEN_MAXSLOT || stream >= GEN_MAXS) throw std::runtime_error("IR slot or stream index out of range");
+            G.slotStream[slot] = (int)stream;  // the stream of the events this slot holds (their attribute types)
             GenPre& P = G.pre[pre];
             P.absent = absent != 0;
             P.waiting = absent ? forMs : -1;
@@ -1218,8 +1220,13 @@ int gen_state_export(GenEngine* e, SdDoc& d, std::string& msg) {
             x.ts = R64(k, base + SE_TS);
             x.null_bits = W(k, base + SE_NULL);
             if (x.null_bits != 0xffffffffu) {
-                const int na = G.nattr[G.slotStream[slot]];
-                for (int a = 0; a < na; a++) x.attr.push_back((uint64_t)R64(k, base + SE_ATTR + 2 * (uint32_t)a));
+                const int st = G.slotStream[slot];
+                const int na = G.nattr[st];
+                for (int a = 0; a < na; a++) {  // (32-bit types: the low word; the kernel leaves the high one)
+                    const int32_t t = G.attrType[st][a];
+                    const uint32_t w = base + SE_ATTR + 2 * (uint32_t)a;
+                    x.attr.push_back((t == SG_T_LONG || t == SG_T_DOUBLE) ? (uint64_t)R64(k, w) : (uint64_t)W(k, w));
+                }
                 x.present = na >= 32 ? 0xffffffffu : ((1u << na) - 1u);
                 x.null_bits &= x.present;
             }

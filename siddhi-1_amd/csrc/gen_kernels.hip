@@ -124,6 +124,12 @@ struct Lane {
     __device__ __forceinline__ int64_t evTs(uint32_t e) const { return R64(sew(e, SE_TS)); }
     __device__ __forceinline__ uint64_t evSeq(uint32_t e) const { return (uint64_t)R64(sew(e, SE_SEQ)); }
     __device__ __forceinline__ uint32_t evNext(uint32_t e) const { return W(sew(e, SE_NEXT)); }
+    // attribute `attr` of StreamEvent e, an event of slot `slot`'s stream (32-bit types: the low word only)
+    __device__ __forceinline__ uint64_t attrWord(uint32_t e, uint32_t slot, uint32_t attr) const {
+        const uint32_t w = sew(e, SE_ATTR + 2 * attr);
+        const int32_t t = G.attrType[G.slotStream[slot]][attr];
+        return (t == SG_T_LONG || t == SG_T_DOUBLE) ? (uint64_t)R64(w) : (uint64_t)W(w);
+    }
 
     __device__ uint32_t alloc(uint32_t freeOff, uint32_t cap) __restrict__ {
         const uint32_t nw = (cap + 31) / 32;
@@ -170,14 +176,14 @@ struct Lane {
             const int s = (int)A.b.stream;
             const int na = G.nattr[s];
             for (int a = 0; a < na; a++) {
-                uint64_t v = 0;
+                // two words per attribute; the high word is written (and read, attrWord) only for long/double
                 const void* c = A.b.col[a];
+                const uint32_t w = sew(e, SE_ATTR + 2 * (uint32_t)a);
                 switch (G.attrType[s][a]) {
-                case SG_T_LONG: case SG_T_DOUBLE: v = gp((const uint64_t*)c)[batchPos]; break;
-                case SG_T_BOOL: v = gp((const uint8_t*)c)[batchPos] ? 1 : 0; break;
-                default: v = gp((const uint32_t*)c)[batchPos];
+                case SG_T_LONG: case SG_T_DOUBLE: W64(w, (int64_t)gp((const uint64_t*)c)[batchPos]); break;
+                case SG_T_BOOL: W(w) = gp((const uint8_t*)c)[batchPos] ? 1u : 0u; break;
+                default: W(w) = gp((const uint32_t*)c)[batchPos];
                 }
-                W64(sew(e, SE_ATTR + 2 * (uint32_t)a), (int64_t)v);
                 if (A.b.nul[a] && gp(A.b.nul[a])[batchPos]) nb |= 1u << a;
             }
         } else {
@@ -373,8 +379,7 @@ struct Lane {
                        [&](uint32_t slot, uint32_t attr, int32_t chain) -> GVal {
                            const uint32_t e = chainAt(se, (int)slot, chain);
                            if (e == GEN_NIL) return GVal{0, true};
-                           return GVal{(uint64_t)R64(sew(e, SE_ATTR + 2 * attr)),
-                                       ((W(sew(e, SE_NULL)) >> attr) & 1u) != 0};
+                           return GVal{attrWord(e, slot, attr), ((W(sew(e, SE_NULL)) >> attr) & 1u) != 0};
                        },
                        [&](uint32_t slot, int32_t chain) -> bool { return chainAt(se, (int)slot, chain) == GEN_NIL; });
     }
@@ -410,8 +415,7 @@ struct Lane {
                                                        pv[3 * attr + 2] != 0};
                                        const uint32_t e = chainAt(se, (int)slot, chain);
                                        if (e == GEN_NIL) return GVal{0, true};
-                                       return GVal{(uint64_t)R64(sew(e, SE_ATTR + 2 * attr)),
-                                                   ((W(sew(e, SE_NULL)) >> attr) & 1u) != 0};
+                                       return GVal{attrWord(e, slot, attr), ((W(sew(e, SE_NULL)) >> attr) & 1u) != 0};
                                    },
                                    [&](uint32_t slot, int32_t chain) -> bool { return chainAt(se, (int)slot, chain) == GEN_NIL; });
             const uint32_t j = i - G.projAgg;

@@ -144,3 +144,29 @@ def test_cross_engine_import_with_timers(shape):
     for x, y in zip(got, want):
         _same(x, y)
     assert sum(len(m) for m in want) > 0
+
+
+def test_gpu_state_two_streams_of_different_arity():
+    """a general-engine query over two streams with different attribute lists (S1: symbol, price, volume;
+    S3: symbol, price double): each slot's StreamEvents carry their own stream's attributes (the slot ->
+    stream map of the device program), in the matches and in the exported state (== the oracle's)"""
+    q = ("define stream S1 (symbol string, price float, volume int);\n"
+         "define stream S3 (symbol string, price double);\n"
+         "partition with (symbol of S1, symbol of S3) begin "
+         "from every e1=S1[price>20], e2=S3[price>e1.price] within 1 sec "
+         "select e1.price as a, e2.price as b insert into O; end;")
+    n_keys, batch = 256, 6000
+    cq, g = _gpu(q, n_keys, batch)
+    _, o = _oracle(q, n_keys)
+    for seq, d in _data(n_keys, batch, 3, seed=120):
+        half = batch // 2
+        for e in (g, o):
+            e.push(cq.stream_index("S1"), seq, d["ts"][:half], [d["symbol"][:half], d["price"][:half],
+                                                                 d["volume"][:half]], None, d["key"][:half])
+            e.push(cq.stream_index("S3"), seq + half, d["ts"][half:], [d["symbol"][half:],
+                                                                       d["price"][half:].astype(np.float64)],
+                   None, d["key"][half:])
+        _same(g.poll(), o.poll())
+    dg, do = sd.parse(g.state_export()), sd.parse(o.state_export())
+    assert len(dg.keys) == len(do.keys) > 0
+    assert sd.logical(dg) == sd.logical(do)
