@@ -474,18 +474,20 @@ __device__ __forceinline__ uint32_t wave_max_u(uint32_t x) {
 // range does not fit is left whole to the HBM pass (p.deferred).  !STG: the HBM pass over those
 // waves and keys (payload read from HBM, register window spilling to the slab when full).  Two
 // kernels, so the staged walk carries no global load and no vmcnt wait behind the match stores.
+// gid: the lane's global index (key): blockIdx.x * SGD_BLOCK + threadIdx.x in the staged pass; the HBM pass
+// runs one wave per work-group over the list of deferred waves (gid = wave * 64 + lane)
 template <bool S0, bool S1, bool STG>
-__device__ __forceinline__ void advance(const P2Params& p) {
+__device__ __forceinline__ void advance(const P2Params& p, const uint32_t gid) {
     typedef typename SgSel<S0, SgEv0, SgEv1>::type Ev;
     constexpr int STRIDE = S0 ? SGQ_STRIDE0 : SGQ_STRIDE1;
     constexpr uint32_t SB = STRIDE * 4;  // bytes per payload element
     constexpr uint32_t NW = SGD_BLOCK / SGD_WAVE;
     const int lane = threadIdx.x & (SGD_WAVE - 1);
     const uint32_t wv = threadIdx.x / SGD_WAVE;
-    const uint32_t k = blockIdx.x * SGD_BLOCK + threadIdx.x;
+    const uint32_t k = gid;
     const uint32_t K = p.n_keys;
     // round trip 1: the key's segment of the sorted batch and its header (independent loads)
-    const uint32_t wave_id = (blockIdx.x * SGD_BLOCK + threadIdx.x) / SGD_WAVE;
+    const uint32_t wave_id = gid / SGD_WAVE;
     uint32_t b = 0, e = 0, h = 0, dfr = 0, rsm = SGD_NO_RESUME;
     if (k < K) {
         b = p.seg_begin[k];
@@ -539,6 +541,7 @@ __device__ __forceinline__ void advance(const P2Params& p) {
         // this wave's p.deferred entry: 1 = the HBM pass takes the whole workgroup (its range does not
         // fit); keys stopped early raise it to 2 after the walk (written after the barrier below)
         if (lane == 0) p.deferred[wave_id] = (!fits && bhi > blo) ? 1u : 0u;
+        if (!fits && bhi > blo && lane == 0) p.dlist[atomicAdd(p.dlist_n, 1u)] = wave_id;  // the HBM pass's list
         if (!fits) iters = 0;
     }
     const uint32_t* lds_run = (const uint32_t*)sg_stage + ((uint64_t)blo * SB - c_lo * 16u) / 4u;  // element blo
@@ -894,6 +897,9 @@ __device__ __forceinline__ void advance(const P2Params& p) {
         p.resume[k] = rs;
         p.deferred[wave_id] = 2u;
     }
+    if constexpr (STG) {  // a wave with resumed keys joins the HBM pass's list (once)
+        if (__ballot(rs != SGD_NO_RESUME) != 0ull && lane == 0) p.dlist[atomicAdd(p.dlist_n, 1u)] = wave_id;
+    }
     if (run > 0) {
         uint32_t np, ns;
         if (!GLB || !hbm) {
@@ -967,14 +973,25 @@ __device__ __forceinline__ void pack(const PackParams& q) {
 #endif
 #define SGQ_OCC __attribute__((amdgpu_waves_per_eu(SGQ_WAVES, 8)))
 // k_adv_*: the staged pass; k_adv_*_h: the HBM pass over the waves the staged pass deferred
+// the HBM pass: one wave per work-group, striding over the waves the staged pass listed (p.dlist: the
+// workgroups whose range did not fit LDS, the waves with resumed keys), so a batch with few of them
+// costs few work-groups
+template <bool S0, bool S1> __device__ __forceinline__ void hbm_pass(const P2Params& p) {
+    const uint32_t n = __builtin_amdgcn_readfirstlane(*p.dlist_n);
+    for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+        const uint32_t w = __builtin_amdgcn_readfirstlane(p.dlist[i]);
+        advance<S0, S1, false>(p, w * SGD_WAVE + threadIdx.x);
+    }
+}
+#define SG_GID (blockIdx.x * SGD_BLOCK + threadIdx.x)
 #if SGQ_MULTI
-extern "C" __global__ void __launch_bounds__(SGD_BLOCK) SGQ_OCC k_adv_m(const P2Params p) { advance<true, true, true>(p); }
-extern "C" __global__ void __launch_bounds__(SGD_BLOCK) SGQ_OCC k_adv_m_h(const P2Params p) { advance<true, true, false>(p); }
+extern "C" __global__ void __launch_bounds__(SGD_BLOCK) SGQ_OCC k_adv_m(const P2Params p) { advance<true, true, true>(p, SG_GID); }
+extern "C" __global__ void __launch_bounds__(SGD_WAVE) SGQ_OCC k_adv_m_h(const P2Params p) { hbm_pass<true, true>(p); }
 #else
-extern "C" __global__ void __launch_bounds__(SGD_BLOCK) SGQ_OCC k_adv_s0(const P2Params p) { advance<true, false, true>(p); }
-extern "C" __global__ void __launch_bounds__(SGD_BLOCK) SGQ_OCC k_adv_s1(const P2Params p) { advance<false, true, true>(p); }
-extern "C" __global__ void __launch_bounds__(SGD_BLOCK) SGQ_OCC k_adv_s0_h(const P2Params p) { advance<true, false, false>(p); }
-extern "C" __global__ void __launch_bounds__(SGD_BLOCK) SGQ_OCC k_adv_s1_h(const P2Params p) { advance<false, true, false>(p); }
+extern "C" __global__ void __launch_bounds__(SGD_BLOCK) SGQ_OCC k_adv_s0(const P2Params p) { advance<true, false, true>(p, SG_GID); }
+extern "C" __global__ void __launch_bounds__(SGD_BLOCK) SGQ_OCC k_adv_s1(const P2Params p) { advance<false, true, true>(p, SG_GID); }
+extern "C" __global__ void __launch_bounds__(SGD_WAVE) SGQ_OCC k_adv_s0_h(const P2Params p) { hbm_pass<true, false>(p); }
+extern "C" __global__ void __launch_bounds__(SGD_WAVE) SGQ_OCC k_adv_s1_h(const P2Params p) { hbm_pass<false, true>(p); }
 #endif
 extern "C" __global__ void __launch_bounds__(256) k_pack0(const PackParams q) { pack<SGQ_STRIDE0, 0>(q); }
 extern "C" __global__ void __launch_bounds__(256) k_pack1(const PackParams q) { pack<SGQ_STRIDE1, 1>(q); }

@@ -348,8 +348,12 @@ __global__ void k_bump(unsigned long long* out_count, const unsigned long long* 
 // over the rows; one atomic per counter per block)
 __global__ void __launch_bounds__(256) k_stats_reduce(const unsigned long long* __restrict__ wstats,
                                                       uint32_t n_waves, unsigned long long* __restrict__ stats,
-                                                      unsigned long long* __restrict__ raw_count) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) *raw_count = 0;  // the next advance's atomic slot counter
+                                                      unsigned long long* __restrict__ raw_count,
+                                                      uint32_t* __restrict__ dlist_n) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // the next advance's atomic slot counter and HBM-pass list
+        *raw_count = 0;
+        *dlist_n = 0;
+    }
     __shared__ unsigned long long part[SGD_ST_N][4];
     unsigned long long acc[SGD_ST_N];
     for (int i = 0; i < SGD_ST_N; ++i) acc[i] = 0;
@@ -394,9 +398,9 @@ int sgd_launch_check_keys(const uint32_t* keys, uint32_t n, uint32_t n_keys, uin
 }
 
 int sgd_launch_stats_reduce(const unsigned long long* wstats, uint32_t n_waves, unsigned long long* stats,
-                            unsigned long long* raw_count, ihipStream_t* stream) {
+                            unsigned long long* raw_count, uint32_t* dlist_n, ihipStream_t* stream) {
     const uint32_t blocks = std::max(1u, std::min(64u, (n_waves + 255u) / 256u));
-    hipLaunchKernelGGL(k_stats_reduce, dim3(blocks), dim3(256), 0, stream, wstats, n_waves, stats, raw_count);
+    hipLaunchKernelGGL(k_stats_reduce, dim3(blocks), dim3(256), 0, stream, wstats, n_waves, stats, raw_count, dlist_n);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

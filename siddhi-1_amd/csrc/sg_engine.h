@@ -97,6 +97,8 @@ struct P2Params {
     uint32_t* err;
     uint32_t* deferred;                // [n_keys / 64] waves the staged pass left to the HBM pass:
                                        // 1 = the whole wave, 2 = the keys with a resume point
+    uint32_t* dlist;                   // [n_keys / 64] the waves the HBM pass takes (appended by the staged pass)
+    uint32_t* dlist_n;                 // their number (reset after the batch by k_stats_reduce)
     uint32_t* resume;                  // [n_keys] event index (in the key's run) where the HBM pass
                                        // resumes a key the staged pass stopped; SGD_NO_RESUME otherwise
     unsigned long long* prof;          // SGX_PROF experiments only (NULL otherwise)
@@ -223,4 +225,4 @@ int sgd_launch_reset_keys(const uint32_t* keys, uint32_t n, uint32_t n_keys, uin
 int sgd_launch_check_keys(const uint32_t* keys, uint32_t n, uint32_t n_keys, uint32_t* bad, ihipStream_t* stream);
 // sums the staged pass's per-wave counters of one batch into stats[SGD_ST_N]
 int sgd_launch_stats_reduce(const unsigned long long* wstats, uint32_t n_waves, unsigned long long* stats,
-                            unsigned long long* raw_count, ihipStream_t* stream);
+                            unsigned long long* raw_count, uint32_t* dlist_n, ihipStream_t* stream);

@@ -228,6 +228,8 @@ struct sg_engine {
     unsigned long long* prof = nullptr;  // SG_PROF: walk-phase clocks of the staged pass (experiments)
     size_t prof_rows = 0;
     uint32_t* resume = nullptr;    // per key: where the HBM pass resumes a key the staged pass stopped
+    uint32_t* dlist = nullptr;     // the waves the HBM pass takes, and their number
+    uint32_t* dlist_n = nullptr;
     uint32_t* tile_sum = nullptr;  // ordering: matches per tile of triggers, and its exclusive scan
     uint32_t* tile_off = nullptr;
     unsigned long long* out_count = nullptr;
@@ -602,6 +604,9 @@ void allocate(sg_engine* e) {
     e->t_desc = dalloc<uint64_t>(B, o);
     e->deferred = dalloc<uint32_t>((K + SGD_BLOCK - 1) / SGD_BLOCK * (SGD_BLOCK / SGD_WAVE), o);
     e->resume = dalloc<uint32_t>(K, o);
+    e->dlist = dalloc<uint32_t>((K + SGD_BLOCK - 1) / SGD_BLOCK * (SGD_BLOCK / SGD_WAVE), o);
+    e->dlist_n = dalloc<uint32_t>(1, o);  // zeroed here, then by k_stats_reduce after every advance
+    HIP_OK(hipMemsetAsync(e->dlist_n, 0, 4, e->stream));
     if (getenv("SG_PROF")) {
         e->prof = dalloc<unsigned long long>(nw * 8, o);
         HIP_OK(hipMemsetAsync(e->prof, 0, nw * 64, e->stream));
@@ -918,6 +923,8 @@ int push(sg_engine* e, const sg_batch* b) {
     p.deferred = e->deferred;
     p.prof = e->prof;
     p.resume = e->resume;
+    p.dlist = e->dlist;
+    p.dlist_n = e->dlist_n;
     p.stats = e->stats;
     p.wstats = e->wstats;
     p.raw_static = e->raw_static;
@@ -932,9 +939,10 @@ int push(sg_engine* e, const sg_batch* b) {
         const uint32_t blocks = (e->K + SGD_BLOCK - 1) / SGD_BLOCK;
         launch(v.adv[role], blocks, SGD_BLOCK, &p, e->stream, p.stage_chunks * 16u * (SGD_BLOCK / SGD_WAVE));
         if (e->timing) { a1 = e->ev(); e->mark(a1); e->spans.push_back({a0, a1, 1}); a0 = e->ev(); e->mark(a0); }
-        launch(v.adv_h[role], blocks, SGD_BLOCK, &p, e->stream);
+        // one wave per work-group over the listed waves (a fixed grid: the list's length is on the device)
+        launch(v.adv_h[role], std::min<uint32_t>(blocks * (SGD_BLOCK / SGD_WAVE), 2048u), SGD_WAVE, &p, e->stream);
         if (e->timing) { a1 = e->ev(); e->mark(a1); e->spans.push_back({a0, a1, 3}); }
-        if (sgd_launch_stats_reduce(e->wstats, blocks * (SGD_BLOCK / SGD_WAVE), e->stats, e->raw_count, e->stream) != 0)
+        if (sgd_launch_stats_reduce(e->wstats, blocks * (SGD_BLOCK / SGD_WAVE), e->stats, e->raw_count, e->dlist_n, e->stream) != 0)
             throw HipError("k_stats_reduce launch failed");
     }
     e->st.advance_launches++;
