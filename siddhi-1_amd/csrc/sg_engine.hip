@@ -228,6 +228,7 @@ struct sg_engine {
     unsigned long long* prof = nullptr;  // SG_PROF: walk-phase clocks of the staged pass (experiments)
     size_t prof_rows = 0;
     uint32_t* resume = nullptr;    // per key: where the HBM pass resumes a key the staged pass stopped
+    uint32_t hbm_grid = 2048;      // work-groups of the HBM pass (SG_HBM_GRID: experiments)
     uint32_t* dlist = nullptr;     // the waves the HBM pass takes, and their number
     uint32_t* dlist_n = nullptr;
     uint32_t* tile_sum = nullptr;  // ordering: matches per tile of triggers, and its exclusive scan
@@ -606,6 +607,7 @@ void allocate(sg_engine* e) {
     e->resume = dalloc<uint32_t>(K, o);
     e->dlist = dalloc<uint32_t>((K + SGD_BLOCK - 1) / SGD_BLOCK * (SGD_BLOCK / SGD_WAVE), o);
     e->dlist_n = dalloc<uint32_t>(1, o);  // zeroed here, then by k_stats_reduce after every advance
+    if (const char* x = getenv("SG_HBM_GRID")) e->hbm_grid = std::max(1u, (uint32_t)strtoul(x, nullptr, 0));
     HIP_OK(hipMemsetAsync(e->dlist_n, 0, 4, e->stream));
     if (getenv("SG_PROF")) {
         e->prof = dalloc<unsigned long long>(nw * 8, o);
@@ -940,7 +942,7 @@ int push(sg_engine* e, const sg_batch* b) {
         launch(v.adv[role], blocks, SGD_BLOCK, &p, e->stream, p.stage_chunks * 16u * (SGD_BLOCK / SGD_WAVE));
         if (e->timing) { a1 = e->ev(); e->mark(a1); e->spans.push_back({a0, a1, 1}); a0 = e->ev(); e->mark(a0); }
         // one wave per work-group over the listed waves (a fixed grid: the list's length is on the device)
-        launch(v.adv_h[role], std::min<uint32_t>(blocks * (SGD_BLOCK / SGD_WAVE), 2048u), SGD_WAVE, &p, e->stream);
+        launch(v.adv_h[role], std::min<uint32_t>(blocks * (SGD_BLOCK / SGD_WAVE), e->hbm_grid), SGD_WAVE, &p, e->stream);
         if (e->timing) { a1 = e->ev(); e->mark(a1); e->spans.push_back({a0, a1, 3}); }
         if (sgd_launch_stats_reduce(e->wstats, blocks * (SGD_BLOCK / SGD_WAVE), e->stats, e->raw_count, e->dlist_n, e->stream) != 0)
             throw HipError("k_stats_reduce launch failed");
