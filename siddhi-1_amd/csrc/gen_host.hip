@@ -1293,6 +1293,16 @@ int gen_state_import(GenEngine* e, const SdDoc& d, std::string& msg) {
     }
     std::vector<uint32_t> S(gen_state_words(e), 0u);
     auto W = [&](uint32_t k, uint32_t w) -> uint32_t& { return S[gen_il(K, k, w)]; };
+    if (G.projAgg) {
+        // the device aggregators' running values (QuerySelector state, not pattern state: the document
+        // does not carry them) stay as they are, as the two-state engine's import leaves its aggregators
+        std::vector<uint32_t> cur(gen_state_words(e));
+        GenClock c0{};
+        const int rc = gen_snapshot(e, cur.data(), &c0, msg);
+        if (rc != SG_OK) return rc;
+        for (uint32_t w = G.offAgg; w < G.offAgg + 5 * G.projAgg; w++)
+            for (uint64_t k = 0; k < K; k++) S[gen_il(K, (uint32_t)k, w)] = cur[gen_il(K, (uint32_t)k, w)];
+    }
     auto W64 = [&](uint32_t k, uint32_t w, int64_t v) {
         W(k, w) = (uint32_t)(uint64_t)v;
         W(k, w + 1) = (uint32_t)((uint64_t)v >> 32);

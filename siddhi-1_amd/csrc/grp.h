@@ -22,6 +22,16 @@
 #define SGD_GRP_TILE_WAVES 8                                 // tile sort workgroup: 512 lanes
 #define SGD_GRP_MAX_BATCH (1u << 24)                         // the tile sort carries key & 255 in idx bits 24..31
 
+// Ablation knobs that deliberately produce wrong results (timing experiments) exist only in builds made
+// with EXTRA=-DSG_EXPERIMENTS; in the shipped library SG_EXP(x) is the constant 0 and their code is gone.
+#ifndef SG_EXP
+#ifdef SG_EXPERIMENTS
+#define SG_EXP(x) (x)
+#else
+#define SG_EXP(x) 0u
+#endif
+#endif
+
 struct GrpArgs {
     uint32_t n;          // events in the batch
     uint32_t K;          // n_keys
@@ -29,7 +39,7 @@ struct GrpArgs {
     uint32_t nblk;       // ceil(n / SGD_GRP_BLOCK_EVENTS)
     uint32_t drop_null;  // SG_CFG_NULL_KEYS
     uint32_t tile_lds;   // dynamic LDS of the tile sort (bytes); larger tiles are split from HBM
-    uint32_t exp;        // SG_GRP_EXP ablations (wrong results; timing experiments only), 0 otherwise
+    uint32_t exp;        // grouping ablations (EXTRA=-DSG_EXPERIMENTS builds only: wrong results), 0 otherwise
     uint32_t pad;
     const uint32_t* keys;
     uint32_t* mat;       // [n_tiles * nblk + 1]

@@ -110,7 +110,7 @@ template <int W> __global__ void __launch_bounds__(1024) k_grp_scatter(const Grp
         const bool v = key_ok(k, a.K);
         const uint64_t act = __ballot(v);
         uint32_t r = 0;
-        if (act && !(a.exp & 2)) {  // wave-uniform
+        if (act && !(SG_EXP(a.exp) & 2)) {  // wave-uniform
             const uint64_t m = match_any<12>(k >> 8, act);
             if (v) {
                 const uint32_t t = k >> 8;
@@ -151,7 +151,7 @@ template <int W> __global__ void __launch_bounds__(1024) k_grp_scatter(const Grp
                 const uint32_t k = pk[c] & 0xfffffu, t = k >> 8;
                 // the tile sort's split key rides in the position's top byte
                 el[q].idx = (i0 + c * 64) | ((k & 255u) << 24);
-                out[(a.exp & 1) ? i0 + c * 64 : boff[t] + mine[t] + (pk[c] >> 20)] = el[q];
+                out[(SG_EXP(a.exp) & 1) ? i0 + c * 64 : boff[t] + mine[t] + (pk[c] >> 20)] = el[q];
             }
         }
     }

@@ -118,7 +118,7 @@ template <class A, class B> struct SgSel<false, A, B> { typedef B type; };
 
 #define R SGQ_R
 
-// ablation knobs for tools/exp_c2.py (SG_JIT_EXTRA); 0 in every shipped configuration
+// ablation knobs for tools/exp_c2.py (JIT-time defines, experiment builds only); 0 in every shipped configuration
 #ifndef SGX_NO_RAW
 #define SGX_NO_RAW 0
 #endif

@@ -177,7 +177,7 @@ __global__ void __launch_bounds__(256) k_order_scatter(const ScatterParams s, ui
             if (o >= s.capacity) o -= s.capacity;
             s.o_trig[o] = trig;
             // {e1 seq, e2 seq} as one 16-B store
-            const uint64_t e1 = (s.exp & 1) ? 0ull : s.raw_e1[fst[tl] + (q - loc[tl])];
+            const uint64_t e1 = (SG_EXP(s.exp) & 1) ? 0ull : s.raw_e1[fst[tl] + (q - loc[tl])];
             *reinterpret_cast<ulonglong2*>(s.o_slot + 2 * o) = make_ulonglong2(e1, trig);
             s.o_key[o] = s.key ? s.key[t] : 0u;
             s.o_ts[o] = s.ts[t];  // StreamPostStateProcessor.java:68: StateEvent ts = ts of the e2 event

@@ -6,6 +6,16 @@
 
 #include <stdint.h>
 
+// Ablation knobs that deliberately produce wrong results (timing experiments) exist only in builds made
+// with EXTRA=-DSG_EXPERIMENTS; in the shipped library SG_EXP(x) is the constant 0 and their code is gone.
+#ifndef SG_EXP
+#ifdef SG_EXPERIMENTS
+#define SG_EXP(x) (x)
+#else
+#define SG_EXP(x) 0u
+#endif
+#endif
+
 #define SGD_MAX_PROG 64    // filter program length (instructions)
 #define SGD_MAX_STACK 16   // filter evaluation stack depth
 #define SGD_MAX_EVCOLS 8   // event columns a query's filters read (per stream)
@@ -152,7 +162,7 @@ struct ScatterParams {
     uint32_t n_capw;
     uint64_t* out_first;       // aggregators: per batch event, count << 32 | ring position of its first
                                // record (0: no match); NULL otherwise
-    uint32_t exp;              // SG_ORDER_EXP ablations (timing experiments only, wrong results), 0 otherwise
+    uint32_t exp;              // ordering ablations (EXTRA=-DSG_EXPERIMENTS builds only: wrong results), 0 otherwise
 };
 #define SGD_ORDER_TILE 4096  // triggers per workgroup of the ordering kernels (256 threads x 16 rows)
 // On-device projection of the select list (sg_set_projection) for the two-state kernel: after the ordering

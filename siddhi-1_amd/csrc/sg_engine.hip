@@ -869,7 +869,9 @@ int push(sg_engine* e, const sg_batch* b) {
                 ga.nblk = (n + SGD_GRP_BLOCK_EVENTS - 1) / SGD_GRP_BLOCK_EVENTS;
                 ga.drop_null = e->null_keys ? 1u : 0u;
                 ga.tile_lds = sgd_group_tile_lds(n, e->K, wi);
+#ifdef SG_EXPERIMENTS
                 if (const char* x = getenv("SG_GRP_EXP")) ga.exp = (uint32_t)strtoul(x, nullptr, 0);
+#endif
                 ga.keys = keys;
                 ga.mat = e->g_mat;
                 ga.mscan = e->g_mscan;
@@ -978,7 +980,9 @@ int push(sg_engine* e, const sg_batch* b) {
         sp.o_capnull = e->o_capnull;
         sp.n_capw = e->n_capw;
         sp.out_first = (proj && e->n_agg) ? e->out_first : nullptr;
+#ifdef SG_EXPERIMENTS
         if (const char* x = getenv("SG_ORDER_EXP")) sp.exp = (uint32_t)strtoul(x, nullptr, 0);
+#endif
         if (sgd_launch_scatter(sp, e->scan_tmp, e->scan_tmp_bytes, e->stream) != 0)
             throw HipError("ordering launch failed");
         if (proj) {

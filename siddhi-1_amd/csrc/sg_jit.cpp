@@ -336,6 +336,7 @@ std::string sgj_generate(const JitQuery& q, std::vector<uint64_t>& consts) {
         stride[s] = sgj_stride(sgj_col_words(q.coltypes[q.multi ? 0 : s]) + (q.evnull ? 1 : 0));
     o << "// generated by sg_jit.cpp: one two-state pattern query\n#pragma once\n";
     // tuning experiments (tools/exp_c2.py): SG_JIT_EXTRA="NAME=VALUE,..." prepends #defines
+#ifdef SG_EXPERIMENTS
     if (const char* x = getenv("SG_JIT_EXTRA")) {
         std::string defs(x), item;
         std::istringstream ds(defs);
@@ -345,6 +346,7 @@ std::string sgj_generate(const JitQuery& q, std::vector<uint64_t>& consts) {
             o << "#define " << (eq == std::string::npos ? item : item.substr(0, eq) + " " + item.substr(eq + 1)) << "\n";
         }
     }
+#endif
     o << "#define SGQ_R " << q.reg_slots << "\n";
     o << "#define SGQ_MODE " << q.mode << "\n";
     o << "#define SGQ_MULTI " << (q.multi ? 1 : 0) << "\n";

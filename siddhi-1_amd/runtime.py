@@ -287,8 +287,9 @@ class StringDictionary:
         """the strings as a numpy object array indexed by id (+ None at index len: a null's slot),
         extended as the dictionary grows"""
         a = getattr(self, "_arr", None)
-        if a is None or len(a) != len(self.strs) + 1:
+        if a is None or len(a) != len(self.strs) + 1 or getattr(self, "_arr_of", None) is not self.strs:
             a = self._arr = np.array(self.strs + [None], dtype=object)
+            self._arr_of = self.strs   # (a restore that swaps in another list of the same length rebuilds)
         return a
 
     def ids_of(self, vals):
@@ -298,6 +299,15 @@ class StringDictionary:
         if None in out:
             out = [self.id_of(v) if i is None else i for v, i in zip(vals, out)]
         return out
+
+
+def _decode_bytes_column(c):
+    """a numpy bytes ('S') column as str values (UTF-8), masks kept; any other column as it is"""
+    if not isinstance(c, np.ndarray) or c.dtype.kind != "S":
+        return c
+    if np.ma.isMaskedArray(c):
+        return np.ma.array(np.char.decode(np.asarray(c.data), "utf-8"), mask=np.ma.getmaskarray(c))
+    return np.char.decode(c, "utf-8")
 
 
 def java_strings(vals):
@@ -917,6 +927,7 @@ class SiddhiAppRuntime:
             raise CannotRestoreSiddhiAppStateException(f"Restoring of Siddhi app {self.name} failed: {ex}")
         self.strings.strs = list(head["strings"])
         self.strings.ids = {x: i for i, x in enumerate(self.strings.strs)}
+        self._invalidate_caches()
         self.store.rows = [None if r is None else (r[0], r[1], _dec(r[2])) for r in head["rows"]]
         self._event_time = head["event_time"]
         self._last_sys = head["last_sys"]
@@ -1180,12 +1191,16 @@ class SiddhiAppRuntime:
                 raise ValueError(f"column of {len(c)} values for {n} timestamps")
         if n == 0:
             return
+        # numpy bytes ('S') STRING columns: UTF-8 bytes are interned as they are (the key dictionary packs
+        # them without a per-value loop), but the event store and the row path hold str values, as a
+        # send(Event[]) of the same strings would
+        cols_rows = [_decode_bytes_column(c) for c in cols_in]
         if self._purges or any(qr.cq.partitioned and qr.cq.partition_keys.get(stream, 0) is None
                                and qr.cq.stream_index(stream) >= 0 for qr in self.queries):
             # per-key bookkeeping of @purge and the broadcast of an unkeyed stream work on rows
             vals = [c.tolist() if not np.ma.isMaskedArray(c) else
                     [None if m else x for x, m in zip(c.data.tolist(), np.ma.getmaskarray(c).tolist())]
-                    for c in cols_in]
+                    for c in cols_rows]
             self._send(stream, list(zip(ts_all.tolist(), [list(r) for r in zip(*vals)])), explicit=True)
             return
         self._run_purges()
@@ -1193,7 +1208,7 @@ class SiddhiAppRuntime:
             self._set_event_time(int(ts_all[-1]))
         elif self.started:
             self._fire_timers(self.wall_time())
-        base = self.store.add_columns(stream, ts_all, cols_in)
+        base = self.store.add_columns(stream, ts_all, cols_rows)
         cols_all = None
         for qr in self.queries:
             si = qr.cq.stream_index(stream)
@@ -1232,6 +1247,12 @@ class SiddhiAppRuntime:
                         qr.engine.push(si, base + lo, ts_all[lo:hi], [c[lo:hi] for c in cols],
                                        [x[lo:hi] if x is not None else None for x in nulls], kids[lo:hi])
             qr.deliver(qr.engine.poll(), self.store)
+
+    def _invalidate_caches(self):
+        """drop what was derived from the dictionaries (categorical id maps, the id -> string array): a
+        restore replaces the dictionaries, and an id map built before it would push stale ids"""
+        self.__dict__.pop("_cat_cache", None)
+        self.strings.__dict__.pop("_arr", None)
 
     def _category_ids(self, categories, what, make):
         """ids of a categorical column's categories (`make` over their strings), cached per categories

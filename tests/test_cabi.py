@@ -45,3 +45,12 @@ def test_engine_create_rejects_garbage_ir():
         assert "magic" in str(ex) or "IR" in str(ex)
     else:
         raise AssertionError("garbage IR accepted")
+
+
+def test_no_result_changing_knobs_in_the_shipped_library():
+    """the ablation knobs that produce wrong results (ordering / grouping ablations, JIT-time defines) are
+    compiled only into EXTRA=-DSG_EXPERIMENTS builds: the shipped library does not read them"""
+    path = os.path.join(ROOT, "siddhi-1_amd", "lib", "libsiddhi_gpu.so")
+    blob = open(path, "rb").read()
+    for name in (b"SG_ORDER_EXP", b"SG_GRP_EXP", b"SG_JIT_EXTRA"):
+        assert name not in blob, name

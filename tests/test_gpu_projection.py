@@ -228,3 +228,26 @@ def test_device_aggregates_purged_with_key():
         for k in range(4):
             want += [[f"G{g}K{k}", 25.0, 26.0, 1, 5], [f"G{g}K{k}", 26.0, 27.0, 2, 12]]
     assert sorted([r[0], float(r[1]), float(r[2]), r[3], r[4]] for r in rows) == sorted(want)
+
+
+@pytest.mark.parametrize("name", ["agg_c2", "agg_count_pattern"])
+def test_device_aggregates_survive_state_import(name):
+    """restore_states (sg_state_import) replaces the pattern state only: the selector's running aggregates
+    keep counting from where they were, on the two-state kernel and on the general kernel alike"""
+    app = AGG_APPS[name]
+    n_keys, n = 512, 6000
+    batches = [(b * n, synth.stock_ticks(b * n, n, n_keys, seed=80 + b, rate_per_ms=8)) for b in range(4)]
+    runs = []
+    for reimport in (False, True):
+        rows = []
+        rt = _runtime(app, n_keys)
+        assert rt.queries[0].device_projection
+        rt.addCallback("query1", lambda ts, cur, exp: rows.extend((e.timestamp, tuple(e.data)) for e in cur or []))
+        rt.start()
+        _feed_rt(rt, batches[:2])
+        if reimport:
+            rt.restore_states(rt.snapshot_states())
+        _feed_rt(rt, batches[2:])
+        rt.shutdown()
+        runs.append(rows)
+    assert len(runs[0]) > 0 and bits(runs[1]) == bits(runs[0])
