@@ -1,0 +1,700 @@
+// abs_kernels.hip — register-window kernels for the absent-tail pattern
+//
+//     [every] e1=S[f0] -> not S[f1(e1)] for T [within W]      (PATTERN, partitioned, @app:playback)
+//
+// (BASELINE configs[3], "C4").  The general kernels (gen_kernels.hip) interpret the processor graph with
+// every partial match in the key-interleaved state blocks of HBM: each partial a key creates costs ~40
+// word stores to the StateEvent / StreamEvent pools even when it dies a few events later.  These kernels
+// run the same two processors on the same state with one lane per key, but hold the key's lists in
+// registers for the whole walk:
+//   start processor p0   its seed (pending or staged: at most one), the seed's timestamp
+//   absent processor p1  a window of ABS_R partials {e1 ts, e1 seq, e1's attribute words, null bits}
+//                        in list order (pending slots, then staged), lastScheduledTime, the timer queue's
+//                        head / length (entries appended straight to the HBM ring)
+// and write the lists back once per key, in a canonical layout of the general blocks (StateEvent 0 = the
+// seed, StateEvent 1 + j / StreamEvent j = partial j, free bitmaps rebuilt).  The state stays the general
+// engine's state: snapshots, state documents, purge and the general kernels read it unchanged.  A key this
+// path cannot hold (a shared or foreign-shaped list, more than ABS_R partials, a queue about to fill) is
+// handed to the general kernel from the event where it stops (k_gen_batch GEN_M_KEYLIST) or for its whole
+// timer sweep (k_gen_timers over the list), so the results stay exactly the general engine's.
+//
+// Semantics restated from (paths under /root/reference/modules/siddhi-core/src/main/java/io/siddhi/core/):
+//   query/input/stream/state/StreamPreStateProcessor.java:118-129 isExpired, :214-247 addState /
+//       addEveryState, :308-323 updateState (stable sort by ts, -1 last), :325-361 expireEvents,
+//       :364-403 processAndReturn
+//   query/input/stream/state/StreamPostStateProcessor.java:64-83 (the start state's post processing)
+//   query/input/stream/state/AbsentStreamPreStateProcessor.java:80-103 addState (schedules ts + T),
+//       :150-227 process (the TIMER event), :256-274 processAndReturn (returns nothing)
+//   query/input/stream/state/AbsentStreamPostStateProcessor.java:36-56 (a matching event kills the partial
+//       and reschedules at its ts + T)
+//   query/input/stream/state/receiver/PatternMultiProcessStreamReceiver.java:31-51 (stabilize, then the
+//       later state first)
+//   util/Scheduler.java:114-128 notifyAt, :172-210 sendTimerEvents
+#include <hip/hip_runtime.h>
+
+#include "../../include/siddhi_gpu.h"
+#include "../../include/siddhi_gpu_ir.h"
+#include "gen_engine.h"
+#include "java_ops.h"
+
+namespace {
+
+typedef __attribute__((address_space(1))) uint32_t gu32;
+typedef __attribute__((address_space(4))) const GenProgram cGenProgram;
+template <class T> __device__ __forceinline__ __attribute__((address_space(1))) T* gp(T* p) {
+    return (__attribute__((address_space(1))) T*)p;
+}
+
+__device__ __forceinline__ bool ts_before(int64_t a, int64_t b) { return (a != -1) && (b == -1 || a < b); }
+
+template <int NW> struct AbsEv {
+    int64_t ts;
+    uint64_t seq;
+    uint32_t w[NW];
+    uint32_t nb;
+};
+
+// one key's absent-tail state during a walk (see the file comment)
+template <int NW> struct AbsKey {
+    const cGenProgram& G;
+    gu32* S;
+    uint32_t K, k;
+    uint32_t ks0, ks1;  // KeyState word offsets of p0 / p1
+    int stream, slot0, slot1;
+    // window: slots [0, n) live, [0, np) pending, [np, n) staged (newAndEvery)
+    int64_t ts[ABS_R];
+    uint64_t seq[ABS_R];
+    uint32_t w[ABS_R][NW];
+    uint32_t nb[ABS_R];
+    uint32_t n, np;
+    bool sbad;            // the staged slots may be out of ts order (promotion sorts them)
+    uint32_t seedPend, seedStg;
+    int64_t seedPendTs, seedStgTs;
+    uint32_t f0, f1;      // the processors' flag words
+    int64_t lst;          // p1 lastScheduledTime
+    uint32_t qh, ql;      // p1 timer queue head index / length
+    int64_t qhv;          // the head entry (valid while ql > 0)
+    uint32_t err;
+    unsigned long long scanned, created, matches;
+
+    __device__ AbsKey(const GenProgram* g, uint32_t* state, uint32_t K_, uint32_t key)
+        : G(*(cGenProgram*)g), S(gp(state)), K(K_), k(key), n(0), np(0), sbad(false), seedPend(0), seedStg(0),
+          seedPendTs(-1), seedStgTs(-1), f0(0), f1(0), lst(0), qh(0), ql(0), qhv(0), err(0), scanned(0), created(0),
+          matches(0) {
+        ks0 = G.offKS + (uint32_t)G.absP0 * G.ksWords;
+        ks1 = G.offKS + (uint32_t)G.absP1 * G.ksWords;
+        stream = G.slotStream[G.pre[G.absP0].stateId];
+        slot0 = G.pre[G.absP0].stateId;
+        slot1 = G.pre[G.absP1].stateId;
+    }
+
+    __device__ __forceinline__ gu32& W(uint32_t w_) const { return S[gen_il(K, k, w_)]; }
+    __device__ __forceinline__ int64_t R64(uint32_t w_) const {
+        return (int64_t)((uint64_t)W(w_) | ((uint64_t)W(w_ + 1) << 32));
+    }
+    __device__ __forceinline__ void W64(uint32_t w_, int64_t v) const {
+        W(w_) = (uint32_t)(uint64_t)v;
+        W(w_ + 1) = (uint32_t)((uint64_t)v >> 32);
+    }
+    __device__ __forceinline__ uint32_t qword(uint32_t i) const { return ks1 + KS_LISTS + 2 * G.L + 2 * i; }
+
+    // ---- load: false = this key's lists are not of the shape the window holds (the general kernel takes it)
+    __device__ __forceinline__ bool load() {
+        if (!(W(0) & 1u)) {  // PartitionRuntimeImpl.initPartition: p0.init() stages one seed; p1.partitionCreated()
+            seedStg = 1;
+            seedStgTs = -1;
+            f0 = GF_INIT;
+            f1 = GF_STARTED;
+            return true;
+        }
+        f0 = W(ks0 + KS_FLAGS);
+        f1 = W(ks1 + KS_FLAGS);
+        if ((f0 | f1) & (GF_INACTIVE | GF_RUNNING)) return false;
+        const uint32_t p0n = W(ks0 + KS_PLEN), s0n = W(ks0 + KS_NLEN);
+        if (p0n + s0n > 1u) return false;
+        if (p0n + s0n == 1u) {
+            const uint32_t st = W(ks0 + KS_LISTS + (p0n ? 0u : G.L));
+            if (st >= G.STCAP) return false;
+            const uint32_t b = G.offST + st * G.stWords;
+            if (W(b + ST_TYPE) != 0u || W(b + ST_RC) != 1u) return false;
+            for (int s = 0; s < G.nslots; s++)
+                if (W(b + ST_SLOTS + (uint32_t)s) != GEN_NIL) return false;
+            const int64_t t = R64(b + ST_TS);
+            if (p0n) { seedPend = 1; seedPendTs = t; } else { seedStg = 1; seedStgTs = t; }
+        }
+        np = W(ks1 + KS_PLEN);
+        const uint32_t ns = W(ks1 + KS_NLEN);
+        if (np + ns > (uint32_t)ABS_R) return false;
+        n = np + ns;
+        bool ok = true;
+        int64_t prev = 0;
+#pragma unroll
+        for (int j = 0; j < ABS_R; ++j) {
+            ts[j] = 0;
+            seq[j] = 0;
+#pragma unroll
+            for (int q = 0; q < NW; ++q) w[j][q] = 0;
+            nb[j] = 0;
+            if ((uint32_t)j < n) {
+                const uint32_t st = W(ks1 + KS_LISTS + ((uint32_t)j < np ? (uint32_t)j : G.L + (uint32_t)j - np));
+                ok = ok && st < G.STCAP;
+                const uint32_t b = G.offST + (st < G.STCAP ? st : 0u) * G.stWords;
+                const uint32_t e = W(b + ST_SLOTS + (uint32_t)slot0);
+                ok = ok && W(b + ST_TYPE) == 0u && W(b + ST_RC) == 1u && e < G.SECAP &&
+                     W(b + ST_SLOTS + (uint32_t)slot1) == GEN_NIL;
+                const uint32_t eb = G.offSE + (e < G.SECAP ? e : 0u) * G.seWords;
+                const int64_t t = R64(b + ST_TS);
+                ok = ok && W(eb + SE_NEXT) == GEN_NIL && W(eb + SE_RC) == 1u && R64(eb + SE_TS) == t;
+                ts[j] = t;
+                seq[j] = (uint64_t)R64(eb + SE_SEQ);
+                nb[j] = W(eb + SE_NULL);
+                const int na = G.nattr[stream];
+                for (int a = 0; a < na; a++) {
+                    const int ty = G.attrType[stream][a];
+                    const bool wide = ty == SG_T_LONG || ty == SG_T_DOUBLE;
+                    const uint32_t o = G.absOff[a];
+                    const uint32_t lo = W(eb + SE_ATTR + 2 * (uint32_t)a);
+                    const uint32_t hi = wide ? W(eb + SE_ATTR + 2 * (uint32_t)a + 1) : 0u;
+#pragma unroll
+                    for (int q = 0; q < NW; ++q) {
+                        if ((uint32_t)q == o) w[j][q] = lo;
+                        if (wide && (uint32_t)q == o + 1) w[j][q] = hi;
+                    }
+                }
+                if ((uint32_t)j > np && ts_before(t, prev)) sbad = true;
+                prev = t;
+            }
+        }
+        if (!ok) return false;
+        lst = R64(ks1 + KS_LST);
+        qh = W(ks1 + KS_QHEAD);
+        ql = W(ks1 + KS_QLEN);
+        if (qh >= G.Q || ql > G.Q) return false;
+        if (ql) qhv = R64(qword(qh));
+        return true;
+    }
+
+    // ---- store: the lists in the canonical layout (StateEvent 0 = the seed, 1 + j = partial j over
+    // StreamEvent j), free bitmaps rebuilt, the queue header
+    __device__ __forceinline__ void store() const {
+        W(0) = 1u;
+        W(ks0 + KS_FLAGS) = f0;
+        W(ks0 + KS_PLEN) = seedPend;
+        W(ks0 + KS_NLEN) = seedStg;
+        if (seedPend) W(ks0 + KS_LISTS) = 0u;
+        if (seedStg) W(ks0 + KS_LISTS + G.L) = 0u;
+        if (seedPend | seedStg) {
+            const uint32_t b = G.offST;
+            W64(b + ST_TS, seedPend ? seedPendTs : seedStgTs);
+            W(b + ST_TYPE) = 0u;
+            W(b + ST_RC) = 1u;
+            for (int s = 0; s < G.nslots; s++) W(b + ST_SLOTS + (uint32_t)s) = GEN_NIL;
+        }
+        W(ks1 + KS_FLAGS) = f1;
+        W64(ks1 + KS_LST, lst);
+        W(ks1 + KS_QHEAD) = qh;
+        W(ks1 + KS_QLEN) = ql;
+        W(ks1 + KS_PLEN) = np;
+        W(ks1 + KS_NLEN) = n - np;
+        const int na = G.nattr[stream];
+#pragma unroll
+        for (int j = 0; j < ABS_R; ++j) {
+            if ((uint32_t)j < n) {
+                W(ks1 + KS_LISTS + ((uint32_t)j < np ? (uint32_t)j : G.L + (uint32_t)j - np)) = 1u + (uint32_t)j;
+                const uint32_t b = G.offST + (1u + (uint32_t)j) * G.stWords;
+                W64(b + ST_TS, ts[j]);
+                W(b + ST_TYPE) = 0u;
+                W(b + ST_RC) = 1u;
+                for (int s = 0; s < G.nslots; s++) W(b + ST_SLOTS + (uint32_t)s) = s == slot0 ? (uint32_t)j : GEN_NIL;
+                const uint32_t eb = G.offSE + (uint32_t)j * G.seWords;
+                W64(eb + SE_SEQ, (int64_t)seq[j]);
+                W64(eb + SE_TS, ts[j]);
+                W(eb + SE_NEXT) = GEN_NIL;
+                W(eb + SE_RC) = 1u;
+                W(eb + SE_NULL) = nb[j];
+                for (int a = 0; a < na; a++) {
+                    const int ty = G.attrType[stream][a];
+                    const bool wide = ty == SG_T_LONG || ty == SG_T_DOUBLE;
+                    const uint32_t o = G.absOff[a];
+                    uint32_t lo = 0, hi = 0;
+#pragma unroll
+                    for (int q = 0; q < NW; ++q) {
+                        if ((uint32_t)q == o) lo = w[j][q];
+                        if ((uint32_t)q == o + 1) hi = w[j][q];
+                    }
+                    W(eb + SE_ATTR + 2 * (uint32_t)a) = lo;
+                    if (wide) W(eb + SE_ATTR + 2 * (uint32_t)a + 1) = hi;
+                }
+            }
+        }
+        // free bitmaps: StateEvents {0 if a seed} + [1, 1 + n), StreamEvents [0, n)
+        const uint32_t stBits = (seedPend | seedStg) ? 1u : 0u;
+        for (uint32_t x = 0; x < (G.STCAP + 31) / 32; x++) {
+            uint32_t m = 0;
+            if (x == 0) m = stBits | (n >= 31u ? 0xfffffffeu : (((1u << n) - 1u) << 1));
+            else if (n + 1 > 32 * x) m = (n + 1 >= 32 * (x + 1)) ? 0xffffffffu : ((1u << (n + 1 - 32 * x)) - 1u);
+            W(G.offSTfree + x) = m;
+        }
+        for (uint32_t x = 0; x < (G.SECAP + 31) / 32; x++) {
+            uint32_t m = 0;
+            if (n > 32 * x) m = (n >= 32 * (x + 1)) ? 0xffffffffu : ((1u << (n - 32 * x)) - 1u);
+            W(G.offSEfree + x) = m;
+        }
+    }
+
+    __device__ __forceinline__ int64_t deadline() const { return ql ? qhv : GEN_NO_DEADLINE; }
+
+    // Scheduler.notifyAt under playback (Scheduler.java:114-128): append to the key's queue
+    __device__ __forceinline__ void notifyAt(int64_t t) {
+        if (ql >= G.Q) { err |= GERR_CAP; return; }
+        const uint32_t pos = (qh + ql) % G.Q;
+        W64(qword(pos), t);
+        if (ql == 0) qhv = t;
+        ql++;
+    }
+    __device__ __forceinline__ void qpop() {
+        qh = (qh + 1) % G.Q;
+        ql--;
+        if (ql) qhv = R64(qword(qh));
+    }
+
+    // ---- the window ----
+    __device__ __forceinline__ void copy_slot(int d, int s) {
+        ts[d] = ts[s];
+        seq[d] = seq[s];
+#pragma unroll
+        for (int q = 0; q < NW; ++q) w[d][q] = w[s][q];
+        nb[d] = nb[s];
+    }
+    // drop the slots whose bit is set in `drop`, keeping the order of the rest: every kept slot moves down
+    // by the number of dropped slots below it, in log2(ABS_R) collision-free steps (static register indices)
+    __device__ __forceinline__ void remove(uint32_t drop) {
+        drop &= (n >= 32u ? 0xffffffffu : ((1u << n) - 1u));
+        if (!drop) return;
+        const uint32_t keep = ((n >= 32u ? 0xffffffffu : ((1u << n) - 1u))) & ~drop;
+        uint32_t d[ABS_R];
+#pragma unroll
+        for (int j = 0; j < ABS_R; ++j) d[j] = __popc(drop & ((1u << j) - 1u));
+        uint32_t cur = keep;
+#pragma unroll
+        for (int s = 0; (1 << s) < ABS_R; ++s) {
+            const int sh = 1 << s;
+#pragma unroll
+            for (int j = sh; j < ABS_R; ++j) {
+                if (((cur >> j) & 1u) && ((d[j] >> s) & 1u)) {
+                    copy_slot(j - sh, j);
+                    d[j - sh] = d[j];
+                    cur = (cur & ~(1u << j)) | (1u << (j - sh));
+                }
+            }
+        }
+        const uint32_t lowMask = np >= 32u ? 0xffffffffu : ((1u << np) - 1u);
+        np -= __popc(drop & lowMask);
+        n -= __popc(drop);
+    }
+    // updateState: the staged slots join the pending list, stable-sorted by ts (eventTimeComparator)
+    __device__ __forceinline__ void promote() {
+        if (n > np && sbad) {
+#pragma unroll
+            for (int pass = 0; pass < ABS_R - 1; ++pass) {
+#pragma unroll
+                for (int j = 0; j + 1 < ABS_R; ++j) {
+                    if ((uint32_t)j >= np && (uint32_t)(j + 1) < n && ts_before(ts[j + 1], ts[j])) {
+                        int64_t t = ts[j]; ts[j] = ts[j + 1]; ts[j + 1] = t;
+                        uint64_t q = seq[j]; seq[j] = seq[j + 1]; seq[j + 1] = q;
+#pragma unroll
+                        for (int x = 0; x < NW; ++x) { uint32_t c = w[j][x]; w[j][x] = w[j + 1][x]; w[j + 1][x] = c; }
+                        uint32_t c = nb[j]; nb[j] = nb[j + 1]; nb[j + 1] = c;
+                    }
+                }
+            }
+        }
+        np = n;
+        sbad = false;
+    }
+    // StreamPreStateProcessor.expireEvents on p1: the expired prefix of pending, any expired staged slot
+    // (p0's seed holds no event and never expires; p1 has no withinEvery processor: gen_host abs_shape)
+    __device__ __forceinline__ void expire(int64_t now) {
+        if (G.within == -1 || n == 0) return;
+        uint32_t X = 0;
+#pragma unroll
+        for (int j = 0; j < ABS_R; ++j) {
+            const int64_t dd = ts[j] - now;
+            if ((uint32_t)j < n && (dd < 0 ? -dd : dd) > G.within) X |= 1u << j;
+        }
+        if (!X) return;
+        const uint32_t P = np >= 32u ? 0xffffffffu : ((1u << np) - 1u);
+        const uint32_t f = P & ~X;  // the first pending partial that survives ends the prefix
+        const uint32_t pre = f ? (P & X & ((f & (0u - f)) - 1u)) : (P & X);
+        remove(pre | (X & ~P));
+    }
+
+    // ---- values for the filters (java_ops.h jo_eval) ----
+    __device__ __forceinline__ GVal attr(const uint32_t (&ww)[NW], uint32_t nbits, uint32_t a) const {
+        const int ty = G.attrType[stream][a];
+        const uint32_t o = G.absOff[a];
+        uint32_t lo = 0, hi = 0;
+#pragma unroll
+        for (int q = 0; q < NW; ++q) {
+            if ((uint32_t)q == o) lo = ww[q];
+            if ((uint32_t)q == o + 1) hi = ww[q];
+        }
+        const uint64_t b = (ty == SG_T_LONG || ty == SG_T_DOUBLE) ? ((uint64_t)lo | ((uint64_t)hi << 32)) : (uint64_t)lo;
+        return GVal{b, ((nbits >> a) & 1u) != 0};
+    }
+    // f0 on the seed: slot0 = the event, every other slot empty
+    __device__ __forceinline__ bool evalF0(const AbsEv<NW>& ev) {
+        const auto& P = G.pre[G.absP0];
+        if (P.flen == 0) return true;
+        const GVal v = jo_eval<false>(G.code, P.fpc, P.flen, err,
+                               [&](uint32_t s, uint32_t a, int32_t c) -> GVal {
+                                   if ((int)s == slot0 && (c == 0 || c == -1)) return attr(ev.w, ev.nb, a);
+                                   return GVal{0, true};
+                               },
+                               [&](uint32_t s, int32_t c) -> bool { return !((int)s == slot0 && (c == 0 || c == -1)); });
+        return !v.null && (v.b & 1);
+    }
+    // f1 on a partial whose e1 words are `pw` / `pn`: slot0 = its e1, slot1 = the event
+    __device__ __forceinline__ bool evalF1(const AbsEv<NW>& ev, const uint32_t (&pw)[NW], uint32_t pn) {
+        const auto& P = G.pre[G.absP1];
+        if (P.flen == 0) return true;
+        const GVal v = jo_eval<false>(G.code, P.fpc, P.flen, err,
+                                      [&](uint32_t s, uint32_t a, int32_t c) -> GVal {
+                                          if (c != 0 && c != -1) return GVal{0, true};
+                                          if ((int)s == slot1) return attr(ev.w, ev.nb, a);
+                                          if ((int)s == slot0) return attr(pw, pn, a);
+                                          return GVal{0, true};
+                                      },
+                                      [&](uint32_t s, int32_t c) -> bool {
+                                          return !(((int)s == slot0 || (int)s == slot1) && (c == 0 || c == -1));
+                                      });
+        return !v.null && (v.b & 1);
+    }
+    // p1.processAndReturn: f1 over the pending partials in list order; the ones it passes die (one
+    // interpreted evaluation per partial: slot j's words are selected into registers first)
+    __device__ __forceinline__ uint32_t killScan(const AbsEv<NW>& ev) {
+        uint32_t kill = 0;
+        for (uint32_t j = 0; j < np; j++) {
+            uint32_t pw[NW], pn = 0;
+#pragma unroll
+            for (int q = 0; q < NW; ++q) pw[q] = 0;
+#pragma unroll
+            for (int x = 0; x < ABS_R; ++x) {
+                if ((uint32_t)x == j) {
+#pragma unroll
+                    for (int q = 0; q < NW; ++q) pw[q] = w[x][q];
+                    pn = nb[x];
+                }
+            }
+            scanned++;
+            if (evalF1(ev, pw, pn)) {  // AbsentStreamPostStateProcessor.process: the partial dies
+                kill |= 1u << j;
+                lst = ev.ts + G.pre[G.absP1].waiting;  // updateLastArrivalTime
+                notifyAt(lst);
+            }
+        }
+        return kill;
+    }
+
+    // one event of this key (PatternMultiProcessStreamReceiver: stabilize, then p1, then p0)
+    __device__ __forceinline__ void event(const AbsEv<NW>& ev) {
+        expire(ev.ts);
+        seedPend += seedStg;  // updateState(p0): the seed moves to pending
+        if (seedStg) seedPendTs = seedStgTs;
+        seedStg = 0;
+        promote();            // updateState(p1)
+        // p1.processAndReturn: a partial whose f1 passes is removed (and reschedules), the rest stay
+        remove(killScan(ev));
+        // p0.processAndReturn over its seed
+        if (seedPend) {
+            scanned++;
+            if (evalF0(ev)) {
+                // StreamPostStateProcessor: the seed becomes the partial (ts = e1.ts) -> p1.addState
+                // (staged; schedules e1.ts + T); `every`: p0.addEveryState (a new seed, staged, same ts)
+                const uint32_t t = n;
+#pragma unroll
+                for (int j = 0; j < ABS_R; ++j) {
+                    if ((uint32_t)j == t) {
+                        ts[j] = ev.ts;
+                        seq[j] = ev.seq;
+#pragma unroll
+                        for (int q = 0; q < NW; ++q) w[j][q] = ev.w[q];
+                        nb[j] = ev.nb;
+                    }
+                }
+                if (n > np) {  // a staged append out of ts order: promotion sorts
+                    int64_t last = 0;
+#pragma unroll
+                    for (int j = 0; j < ABS_R; ++j) if ((uint32_t)j + 1 == t) last = ts[j];
+                    if (ts_before(ev.ts, last)) sbad = true;
+                }
+                n++;
+                lst = ev.ts + G.pre[G.absP1].waiting;
+                notifyAt(lst);
+                seedPend = 0;
+                if (G.absEvery) {
+                    seedStg = 1;
+                    seedStgTs = ev.ts;
+                    created++;
+                }
+            }
+        }
+    }
+
+    // AbsentStreamPreStateProcessor.process for the TIMER event at currentTime = t (the clock is `now`)
+    __device__ __forceinline__ void timer(int64_t t, int64_t now, const GenArgs& a, uint32_t listener, int64_t tk2,
+                          unsigned long long& resBase, unsigned long long& resEnd, uint32_t& resLeft) {
+        promote();  // this.updateState()
+        const int64_t waiting = G.pre[G.absP1].waiting;
+        uint32_t drop = 0, emit = 0;
+#pragma unroll
+        for (int j = 0; j < ABS_R; ++j) {
+            if ((uint32_t)j < np) {
+                scanned++;
+                const int64_t dd = ts[j] - t;
+                if (G.within != -1 && (dd < 0 ? -dd : dd) > G.within) {
+                    drop |= 1u << j;
+                } else if ((ts[j] == -1 && t >= lst) || (ts[j] != -1 && t >= ts[j] + waiting)) {
+                    drop |= 1u << j;
+                    emit |= 1u << j;
+                }
+            }
+        }
+        // sendEvent in list order: the selector gets each (slot0 = e1, ts = currentTime)
+#pragma unroll
+        for (int j = 0; j < ABS_R; ++j) {
+            if ((emit >> j) & 1u) project(seq[j], t, a, listener, tk2, resBase, resEnd, resLeft);
+        }
+        remove(drop);
+        if (now > waiting + t) lst = now + waiting;
+        if (emit == 0 && lst < t) {
+            lst = t + waiting;
+            notifyAt(t + waiting);
+        }
+    }
+
+    // Lane::project for a timer match: [timer mark][rank][trigger seq][ts][key][chain lengths][seqs]
+    __device__ __forceinline__ void project(uint64_t e1seq, int64_t t, const GenArgs& a, uint32_t listener, int64_t tk2,
+                            unsigned long long& resBase, unsigned long long& resEnd, uint32_t& resLeft) {
+        if (resLeft == 0) {
+            resBase = atomicAdd(&a.o.raw_count[0], (unsigned long long)GEN_RESCHUNK);
+            resEnd = a.o.seg_cap;
+            resLeft = GEN_RESCHUNK;
+        }
+        const unsigned long long r = resBase++;
+        resLeft--;
+        matches++;
+        if (r >= resEnd) { err |= GERR_MATCHCAP; return; }
+        gu32* rec = gp(a.o.raw) + r * a.o.recWords;
+        rec[0] = 0xfffffffeu;
+        rec[1] = 0u;
+        rec[2] = 0xffffffffu;  // SG_TIMER_SEQ
+        rec[3] = 0xffffffffu;
+        rec[4] = (uint32_t)(uint64_t)t;
+        rec[5] = (uint32_t)((uint64_t)t >> 32);
+        rec[6] = k;
+        gu32* lens = rec + 7;
+        gu32* seqs = lens + G.nslots;
+        for (int s = 0; s < G.nslots; s++) {
+            lens[s] = s == slot0 ? 1u : 0u;
+            if (s == slot0) {
+                seqs[2 * (s * G.MC)] = (uint32_t)e1seq;
+                seqs[2 * (s * G.MC) + 1] = (uint32_t)(e1seq >> 32);
+            }
+        }
+        gp(a.o.tk1)[r] = listener;
+        gp(a.o.tk2)[r] = tk2;
+        gp(a.o.tk3)[r] = k;
+    }
+};
+
+// the lanes' work counters, reduced over the wave (all 64 lanes call this): one atomic per wave
+__device__ void abs_wave_stats(const GenArgs& a, unsigned long long sc, unsigned long long cr, unsigned long long ma,
+                               unsigned long long ky, uint32_t er, unsigned long long fb) {
+    for (int off = 32; off > 0; off >>= 1) {
+        fb += __shfl_xor(fb, off, 64);
+        sc += __shfl_xor(sc, off, 64);
+        cr += __shfl_xor(cr, off, 64);
+        ma += __shfl_xor(ma, off, 64);
+        ky += __shfl_xor(ky, off, 64);
+        er |= (uint32_t)__shfl_xor((int)er, off, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if (er) atomicOr(a.o.err, er);
+        if (sc) atomicAdd(&a.o.stats[GST_SCANNED], sc);
+        if (cr) atomicAdd(&a.o.stats[GST_CREATED], cr);
+        if (ma) atomicAdd(&a.o.stats[GST_MATCHES], ma);
+        if (ky) atomicAdd(&a.o.stats[GST_KEYS], ky);
+        if (fb) atomicAdd(&a.o.stats[GST_SPILLS], fb);
+    }
+}
+
+// hand a key to the general kernels (wave-aggregated append to the fallback list)
+__device__ __forceinline__ void abs_fallback(const GenArgs& a, bool mine, uint32_t key, uint32_t start) {
+    const unsigned long long m = __ballot(mine);
+    if (!m) return;
+    const int lane = threadIdx.x & 63;
+    unsigned long long b0 = 0;
+    if (lane == __ffsll((long long)m) - 1) b0 = atomicAdd(a.fb_n, (unsigned long long)__popcll(m));
+    b0 = __shfl(b0, __ffsll((long long)m) - 1, 64);
+    if (mine) {
+        gp(a.fb_list)[b0 + __popcll(m & ((1ull << lane) - 1ull))] = key;
+        if (a.fb_start) gp(a.fb_start)[key] = start;
+    }
+}
+
+template <int NW> __device__ void abs_gather(const GenArgs& a, const cGenProgram& G, uint32_t pos, AbsEv<NW>& ev) {
+    const int s = (int)a.b.stream;
+    const int na = G.nattr[s];
+    ev.nb = 0;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) ev.w[q] = 0;
+    for (int at = 0; at < na; at++) {
+        const int ty = G.attrType[s][at];
+        const void* c = a.b.col[at];
+        uint32_t lo = 0, hi = 0;
+        if (ty == SG_T_LONG || ty == SG_T_DOUBLE) {
+            const uint64_t v = gp((const uint64_t*)c)[pos];
+            lo = (uint32_t)v;
+            hi = (uint32_t)(v >> 32);
+        } else if (ty == SG_T_BOOL) {
+            lo = gp((const uint8_t*)c)[pos] ? 1u : 0u;
+        } else {
+            lo = gp((const uint32_t*)c)[pos];
+        }
+        const uint32_t o = G.absOff[at];
+#pragma unroll
+        for (int q = 0; q < NW; ++q) {
+            if ((uint32_t)q == o) ev.w[q] = lo;
+            if ((ty == SG_T_LONG || ty == SG_T_DOUBLE) && (uint32_t)q == o + 1) ev.w[q] = hi;
+        }
+        if (a.b.nul[at] && gp(a.b.nul[at])[pos]) ev.nb |= 1u << at;
+    }
+}
+
+// ---- batch: one lane per key walks its events of the key-sorted batch ----
+template <int NW> __device__ void abs_batch(const GenArgs& a) {
+    const cGenProgram& G = *(cGenProgram*)a.G;
+    const uint32_t key = blockIdx.x * 64u + threadIdx.x;
+    uint32_t b = 0, e = 0;
+    if (key < a.K) {
+        b = gp(a.b.seg_begin)[key];
+        e = gp(a.b.seg_end)[key];
+    }
+    AbsKey<NW> L(a.G, a.state, a.K, key < a.K ? key : 0u);
+    bool walk = b < e;
+    bool fb = false;
+    uint32_t stop = b;
+    if (walk && !L.load()) {  // not this path's shape: the general kernel walks the whole run
+        fb = true;
+        walk = false;
+    }
+    unsigned long long ky = 0;
+    if (walk) {
+        uint32_t i = b;
+        for (; i < e; i++) {
+            // at most n + 1 appends to the queue and one new partial per event: stop before an event that
+            // could overflow the window or the queue (the general kernel continues from it)
+            if (L.n + 1u > (uint32_t)ABS_R || L.ql + L.n + 1u > G.Q) break;
+            const uint32_t pos = a.b.sidx ? gp(a.b.sidx)[i] : i;
+            AbsEv<NW> ev;
+            ev.ts = gp(a.b.ts)[pos];
+            ev.seq = a.b.seq_base + pos;
+            abs_gather<NW>(a, G, pos, ev);
+            L.event(ev);
+        }
+        L.store();
+        if (i < e) {
+            fb = true;
+            stop = i;
+        } else {
+            gp(a.t.nd)[key] = L.deadline();
+            ky = 1;
+        }
+    }
+    abs_fallback(a, fb, key, stop);
+    abs_wave_stats(a, L.scanned, L.created, 0ull, ky, L.err, fb ? 1ull : 0ull);
+}
+
+__device__ __forceinline__ unsigned long long abs_ord64(int64_t t) { return (unsigned long long)t ^ (1ull << 63); }
+
+// ---- timer sweep to a.now over the due keys (k_gen_due) ----
+template <int NW> __device__ void abs_timers(const GenArgs& a) {
+    const cGenProgram& G = *(cGenProgram*)a.G;
+    const uint64_t nd = *a.t.ndue;
+    unsigned long long sc = 0, cr = 0, ma = 0, nfb = 0;
+    uint32_t er = 0;
+    const uint32_t li = (uint32_t)G.absListener;
+    for (uint64_t base = (uint64_t)blockIdx.x * 64u; base < nd; base += (uint64_t)gridDim.x * 64u) {
+        const uint64_t di = base + threadIdx.x;
+        const bool act = di < nd;
+        const uint32_t key = act ? gp(a.t.due)[di] : 0u;
+        AbsKey<NW> L(a.G, a.state, a.K, key);
+        bool fb = false;
+        if (act) {
+            if (!(L.W(0) & 1u)) {  // a key is created by its first event (not due)
+                gp(a.t.dpair_key)[di] = ~0ull;
+                gp(a.t.dpair_i)[di] = GEN_PAIR_NONE;
+                gp(a.t.nd)[key] = GEN_NO_DEADLINE;
+            } else {
+                // the listener's collection of (due time, key) from the queue head (the A.10 check)
+                const uint32_t qh = L.W(L.ks1 + KS_QHEAD), ql = L.W(L.ks1 + KS_QLEN);
+                const int64_t h = ql ? L.R64(L.qword(qh < G.Q ? qh : 0u)) : 0;
+                const bool due = ql != 0 && h <= a.now;
+                gp(a.t.dpair_key)[di] = due ? abs_ord64(h) : ~0ull;
+                gp(a.t.dpair_i)[di] = due ? li : GEN_PAIR_NONE;
+                if (!L.load()) {
+                    fb = true;
+                } else {
+                    unsigned long long resBase = 0, resEnd = 0;
+                    uint32_t resLeft = 0;
+                    const int64_t tk2 = L.qhv;
+                    for (int guard = 0; guard < (1 << 20); guard++) {  // Scheduler.sendTimerEvents
+                        if (L.ql == 0 || L.qhv > a.now) break;
+                        const int64_t t = L.qhv;
+                        L.qpop();
+                        L.timer(t, a.now, a, li, tk2, resBase, resEnd, resLeft);
+                    }
+                    L.store();
+                    gp(a.t.nd)[key] = L.deadline();
+                    for (uint32_t x = 0; x < resLeft; x++) {  // unused reserved raw slots
+                        const unsigned long long rr = resBase + x;
+                        if (rr < resEnd) {
+                            gp(a.o.raw)[rr * a.o.recWords] = 0xffffffffu;
+                            gp(a.o.tk1)[rr] = 0xffffffffu;
+                        }
+                    }
+                }
+            }
+        }
+        abs_fallback(a, fb, key, 0u);
+        nfb += fb ? 1ull : 0ull;
+        sc += L.scanned;
+        cr += L.created;
+        ma += L.matches;
+        er |= L.err;
+    }
+    unsigned long long mw = ma;
+    for (int off = 32; off > 0; off >>= 1) mw += __shfl_xor(mw, off, 64);
+    if ((threadIdx.x & 63) == 0 && mw) atomicAdd(a.o.nvalid, mw);
+    abs_wave_stats(a, sc, cr, ma, 0ull, er, nfb);
+}
+
+}  // namespace
+
+// One kernel per captured-word count (NW = the stream's attributes as 32-bit words, long / double 2 each).
+#define ABS_KERNELS(NW)                                                                                             \
+    extern "C" __global__ void __launch_bounds__(64) k_abs_batch_##NW(const GenArgs* __restrict__ ap) {           \
+        abs_batch<NW>(*ap);                                                                                         \
+    }                                                                                                               \
+    extern "C" __global__ void __launch_bounds__(64) k_abs_timers_##NW(const GenArgs* __restrict__ ap) {          \
+        abs_timers<NW>(*ap);                                                                                        \
+    }
+ABS_KERNELS(1)
+ABS_KERNELS(2)
+ABS_KERNELS(3)
+ABS_KERNELS(4)
+ABS_KERNELS(5)
+ABS_KERNELS(6)
+ABS_KERNELS(7)
+ABS_KERNELS(8)

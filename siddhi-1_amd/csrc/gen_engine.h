@@ -49,6 +49,8 @@ __host__ __device__ inline size_t gen_at(uint32_t K, uint32_t blockWords, uint32
 #define GEN_NIL 0xffffu  // null pool index
 #define GEN_RAWSEG 256   // raw-match reservation counters of a batch
 #define GEN_RESCHUNK 4   // raw matches a lane reserves at a time
+#define ABS_R 8          // abs_kernels.hip: partials a key's register window holds
+#define ABS_MAXNW 8      // abs_kernels.hip: attribute words of an event it captures
 
 enum { GK_STREAM = 0, GK_COUNT = 1, GK_LOGICAL = 2 };
 
@@ -106,6 +108,13 @@ struct GenProgram {
     uint32_t projAgg;                     // aggregators; their per-key state: 5 words each from offAgg
     uint32_t offAgg;                      //   (count lo/hi, value lo/hi, has-value)
     uint32_t projPc[GEN_MAXPROJ], projLen[GEN_MAXPROJ], projType[GEN_MAXPROJ];
+    // the absent-tail shape `[every] e1=S[f0] -> not S[f1] for T [within W]` (PATTERN, partitioned, playback,
+    // one stream), which runs on the register-window kernels of abs_kernels.hip (gen_host.hip abs_shape):
+    // absP0 / absP1 the start and absent processors, absEvery: `every` re-arms the start seed, absNW the
+    // words an event's attributes take (2 for long / double), absOff[a] attribute a's first word
+    int32_t absOk, absP0, absP1, absEvery, absListener;
+    uint32_t absNW;
+    uint32_t absOff[GEN_MAXA];
 };
 
 // KeyState field offsets inside a processor's record
@@ -133,7 +142,9 @@ struct GenProgram {
 #define SE_NULL 6
 #define SE_ATTR 7
 
-enum { GST_SCANNED = 0, GST_CREATED, GST_MATCHES, GST_KEYS, GST_LIVE0, GST_N };  // GST_LIVE0: SG_CFG_TIMING only
+// GST_LIVE0: SG_CFG_TIMING only; GST_SPILLS: keys the register-window kernels (abs_kernels.hip) handed to the
+// general kernels (sg_stats.window_spills)
+enum { GST_SCANNED = 0, GST_CREATED, GST_MATCHES, GST_KEYS, GST_LIVE0, GST_SPILLS, GST_N };
 enum { GERR_CAP = 1, GERR_MATCHCAP = 2, GERR_KEY = 4, GERR_COLLAPSE = 8, GERR_CHAIN = 16, GERR_REF = 32 };
 
 struct GenBatch {
@@ -198,5 +209,13 @@ struct GenArgs {
     int64_t now;         // engine clock during a push; the advance target for a timer sweep
     int64_t now0;        // the engine clock before a wall-clock timer sweep
     uint32_t kpl;        // k_gen_batch: keys per lane (lane l of block b walks keys (b*kpl + j)*64 + l)
-    uint32_t pad;
+    uint32_t mode;       // GEN_M_* below
+    // keys the register-window kernels (abs_kernels.hip) hand to the general kernels: the list, its
+    // length and, for a batch, the index of the key's first event still to walk (absolute, into sidx)
+    uint32_t* fb_list;
+    unsigned long long* fb_n;
+    uint32_t* fb_start;
 };
+// GenArgs.mode
+#define GEN_M_KEYLIST 1u   // k_gen_batch: lane i walks key fb_list[i] from fb_start[key]
+#define GEN_M_NOPAIRS 2u   // k_gen_timers over fb_list: the collapse pairs were recorded by k_abs_timers

@@ -29,6 +29,15 @@
 #include "state_doc.h"
 
 extern "C" __global__ void k_gen_batch(const GenArgs* ap);
+#define ABS_DECL(NW) extern "C" __global__ void k_abs_batch_##NW(const GenArgs* ap); \
+                     extern "C" __global__ void k_abs_timers_##NW(const GenArgs* ap);
+ABS_DECL(1) ABS_DECL(2) ABS_DECL(3) ABS_DECL(4) ABS_DECL(5) ABS_DECL(6) ABS_DECL(7) ABS_DECL(8)
+typedef void (*AbsKernel)(const GenArgs*);
+static const AbsKernel kAbsBatch[ABS_MAXNW + 1] = {nullptr, k_abs_batch_1, k_abs_batch_2, k_abs_batch_3, k_abs_batch_4,
+                                                   k_abs_batch_5, k_abs_batch_6, k_abs_batch_7, k_abs_batch_8};
+static const AbsKernel kAbsTimers[ABS_MAXNW + 1] = {nullptr, k_abs_timers_1, k_abs_timers_2, k_abs_timers_3,
+                                                    k_abs_timers_4, k_abs_timers_5, k_abs_timers_6, k_abs_timers_7,
+                                                    k_abs_timers_8};
 extern "C" __global__ void k_gen_timers(const GenArgs* ap);
 extern "C" __global__ void k_gen_deadlines(const GenArgs* ap);
 extern "C" __global__ void k_gen_due(const int64_t* nd, uint32_t K, int64_t now, uint32_t* due,
@@ -275,6 +284,62 @@ struct Builder {
 
 uint32_t ceil32(uint32_t x) { return (x + 31) / 32; }
 
+// deepest stack a filter program reaches; -1 when it uses ifThenElse (abs_kernels.hip evaluates programs
+// at most two deep without a stack array)
+int prog_depth(const uint32_t* code, uint32_t pc, uint32_t n) {
+    int sp = 0, mx = 0;
+    for (uint32_t end = pc + n; pc < end;) {
+        const uint32_t op = code[pc] & 0xffu;
+        switch (op) {
+        case SG_OP_VAR: case SG_OP_CONST: case SG_OP_ISNULL_EV: sp++; break;
+        case SG_OP_CVT: case SG_OP_NOT: case SG_OP_ISNULL: break;
+        case SG_OP_IFELSE: return -1;
+        default: sp--;
+        }
+        mx = std::max(mx, sp);
+        pc += (uint32_t)sg_op_len(op);
+    }
+    return mx;
+}
+
+// the absent-tail shape of abs_kernels.hip: `[every] e1=S[f0] -> not S[f1] for T [within W]` with the
+// processors wired exactly as the kernels restate them (anything else stays on the general kernels)
+void abs_shape(GenProgram& G) {
+    G.absOk = 0;
+    if (G.qtype != SG_Q_PATTERN || !G.partitioned || !G.playback || G.nstreams != 1 || G.nprocs != 2 || G.nslots != 2)
+        return;
+    const GenPre &P0 = G.pre[0], &P1 = G.pre[1];
+    const GenPost &Q0 = G.post[0], &Q1 = G.post[1];
+    if (P0.kind != GK_STREAM || P0.absent || !P0.isStart || P1.kind != GK_STREAM || !P1.absent || P1.isStart) return;
+    if (P1.waiting < 0 || P1.withinEvery != GEN_NONE || (P0.withinEvery != GEN_NONE && P0.withinEvery != 0)) return;
+    if (Q0.nextStatePre != 1 || (Q0.nextEveryStatePre != GEN_NONE && Q0.nextEveryStatePre != 0) ||
+        Q0.callbackPre != GEN_NONE || Q0.hasNext)
+        return;
+    if (Q1.nextStatePre != GEN_NONE || Q1.nextEveryStatePre != GEN_NONE || Q1.callbackPre != GEN_NONE || !Q1.hasNext)
+        return;
+    const GenRecv& R = G.recv[0];
+    if (R.n != 2 || R.procs[0] != 0 || R.procs[1] != 1 || R.nStateProcs != 2 || R.stateProcs[0] != 0 ||
+        R.stateProcs[1] != 1)
+        return;
+    if (G.nStartup != 1 || G.startup[0] != 1 || G.MC != 1 || P0.stateId == P1.stateId) return;
+    if (G.slotStream[P0.stateId] != 0 || G.slotStream[P1.stateId] != 0) return;
+    if (prog_depth(G.code, P0.fpc, P0.flen) < 0 || prog_depth(G.code, P0.fpc, P0.flen) > 2 ||
+        prog_depth(G.code, P1.fpc, P1.flen) < 0 || prog_depth(G.code, P1.fpc, P1.flen) > 2)
+        return;
+    uint32_t o = 0;
+    for (int a = 0; a < G.nattr[0]; a++) {
+        G.absOff[a] = o;
+        o += (G.attrType[0][a] == SG_T_LONG || G.attrType[0][a] == SG_T_DOUBLE) ? 2u : 1u;
+    }
+    if (o == 0 || o > ABS_MAXNW) return;
+    G.absNW = o;
+    G.absP0 = 0;
+    G.absP1 = 1;
+    G.absEvery = Q0.nextEveryStatePre == 0 ? 1 : 0;
+    G.absListener = 0;
+    G.absOk = getenv("SG_NO_ABS") ? 0 : 1;  // (SG_NO_ABS: A/B timing against the general kernels; same results)
+}
+
 }  // namespace
 
 GenProgram* gen_build_program(const uint32_t* w, size_t nw, uint32_t partialCap) {
@@ -350,6 +415,7 @@ GenProgram* gen_build_program(const uint32_t* w, size_t nw, uint32_t partialCap)
         G->offDef = off;
         off += 1 + 2 * G->DEF;
         G->blockWords = (off + (1u << GEN_GRAN_LOG2) - 1u) & ~((1u << GEN_GRAN_LOG2) - 1u);  // whole granules
+        abs_shape(*G);
         return G;
     } catch (...) {
         delete G;
@@ -534,6 +600,9 @@ struct GenEngine {
     void* psort_tmp = nullptr;
     size_t psort_tmp_bytes = 0;
     unsigned long long* live = nullptr;  // k_gen_live's sum (diagnostics)
+    // keys the register-window kernels (abs_kernels.hip) hand to the general kernels
+    uint32_t *fb_list = nullptr, *fb_start = nullptr;
+    unsigned long long* fb_n = nullptr;
     GenArgs* d_args = nullptr;           // kernel argument ring (device) and its pinned staging
     GenArgs* h_args = nullptr;
     uint64_t arg_next = 0;
@@ -689,6 +758,11 @@ GenEngine* gen_create(const uint32_t* ir, size_t nw, const sg_config& cfg, hipSt
             }
         }
         e->live = e->dalloc<unsigned long long>(1);
+        if (G.absOk) {
+            e->fb_list = e->dalloc<uint32_t>(K);
+            e->fb_start = e->dalloc<uint32_t>(K);
+            e->fb_n = e->dalloc<unsigned long long>(1);
+        }
         e->d_args = e->dalloc<GenArgs>(GEN_ARG_SLOTS);
         GH_OK(hipHostMalloc((void**)&e->h_args, sizeof(GenArgs) * GEN_ARG_SLOTS, hipHostMallocDefault));
         GH_OK(hipMemsetAsync(e->stats, 0, GST_N * 8, stream));
@@ -728,7 +802,9 @@ static size_t type_size(int t) {
 // the kernels read their arguments from a device ring (GEN_ARG_SLOTS slots, staged through pinned host
 // memory on the engine's stream); a slot is rewritten only after the stream has drained the launches
 // that used it
-enum { GEN_L_BATCH = 0, GEN_L_TIMERS = 1, GEN_L_DEADLINES = 2 };
+enum { GEN_L_BATCH = 0, GEN_L_TIMERS = 1, GEN_L_DEADLINES = 2, GEN_L_ABS_BATCH = 3, GEN_L_ABS_TIMERS = 4 };
+// the general kernels over the keys a register-window kernel handed over: a fixed grid striding the list
+#define GEN_FB_BLOCKS 1024u
 // timer sweeps: a fixed grid of one-wave blocks striding over the due keys (their number is on the device)
 #define GEN_TIMER_BLOCKS 4096u
 // keys per lane of k_gen_batch: 1 (GEN_KPL=n, experiments: n keys per lane).  Measured on C3/C3_min1/C4 at
@@ -740,6 +816,10 @@ static uint32_t gen_kpl(uint32_t K) {
     return 1u;
 }
 
+// the register-window kernels of abs_kernels.hip run this query (the shape, and no device projection: the
+// selector items are evaluated by the general kernel's projectSelect)
+static bool abs_on(const GenEngine* e) { return e->host.absOk && e->host.projN == 0 && e->fb_list; }
+
 static void launch_gen(GenEngine* e, GenArgs a, int which) {
     const uint32_t blocks = (e->K + 63) / 64;
     a.kpl = gen_kpl(e->K);
@@ -749,11 +829,16 @@ static void launch_gen(GenEngine* e, GenArgs a, int which) {
     GH_OK(hipMemcpyAsync(e->d_args + slot, e->h_args + slot, sizeof(GenArgs), hipMemcpyHostToDevice, e->stream));
     const GenArgs* ap = e->d_args + slot;
     hipEvent_t t0 = (e->timing && which != GEN_L_DEADLINES) ? e->ev() : nullptr;
+    const bool fb = (a.mode & (GEN_M_KEYLIST | GEN_M_NOPAIRS)) != 0;
     if (which == GEN_L_TIMERS)
-        hipLaunchKernelGGL(k_gen_timers, dim3(e->host.partitioned ? std::min(blocks, GEN_TIMER_BLOCKS) : 1u), dim3(64), 0,
-                           e->stream, ap);
+        hipLaunchKernelGGL(k_gen_timers, dim3(fb ? GEN_FB_BLOCKS : e->host.partitioned ? std::min(blocks, GEN_TIMER_BLOCKS) : 1u),
+                           dim3(64), 0, e->stream, ap);
     else if (which == GEN_L_DEADLINES) hipLaunchKernelGGL(k_gen_deadlines, dim3(blocks), dim3(64), 0, e->stream, ap);
-    else hipLaunchKernelGGL(k_gen_batch, dim3((e->K + 64u * a.kpl - 1) / (64u * a.kpl)), dim3(64), 0, e->stream, ap);
+    else if (which == GEN_L_ABS_BATCH) hipLaunchKernelGGL(kAbsBatch[e->host.absNW], dim3(blocks), dim3(64), 0, e->stream, ap);
+    else if (which == GEN_L_ABS_TIMERS)
+        hipLaunchKernelGGL(kAbsTimers[e->host.absNW], dim3(std::min(blocks, GEN_TIMER_BLOCKS)), dim3(64), 0, e->stream, ap);
+    else hipLaunchKernelGGL(k_gen_batch, dim3(fb ? GEN_FB_BLOCKS : (e->K + 64u * a.kpl - 1) / (64u * a.kpl)), dim3(64), 0,
+                            e->stream, ap);
     GH_OK(hipGetLastError());
     if (t0) e->spans.push_back({t0, e->ev(), 1});
 }
@@ -838,6 +923,24 @@ int gen_push(GenEngine* e, const sg_batch* b, std::string& msg) {
     if (e->timing)  // sg_stats.live_at_batch_start (outside the batch kernel's span)
         hipLaunchKernelGGL(k_gen_live, dim3((e->K + 255) / 256), dim3(256), 0, e->stream, e->dprog, e->state, e->K,
                            e->stats + GST_LIVE0, e->seg_begin, e->seg_end);
+    if (abs_on(e)) {
+        // the register-window kernel, then the general kernel over the keys it handed over; this shape
+        // emits nothing on events (an absent state's processAndReturn returns nothing; its matches come
+        // from the timers), so there is no batch ordering
+        GH_OK(hipMemsetAsync(e->fb_n, 0, 8, e->stream));
+        a.fb_list = e->fb_list;
+        a.fb_n = e->fb_n;
+        a.fb_start = e->fb_start;
+        launch_gen(e, a, GEN_L_ABS_BATCH);
+        a.mode = GEN_M_KEYLIST;
+        launch_gen(e, a, GEN_L_BATCH);
+        GH_OK(hipGetLastError());
+        e->st.events += n;
+        e->st.batches++;
+        e->st.advance_launches++;
+        if (!dev) GH_OK(hipStreamSynchronize(e->stream));
+        return SG_OK;
+    }
     launch_gen(e, a, GEN_L_BATCH);
     // order: out_count + t_off[trigger] + rank
     size_t tmp = e->scan_tmp_bytes;
@@ -880,7 +983,19 @@ int gen_advance(GenEngine* e, int64_t t, std::string& msg) {
     }
     a.o.nseg = 1;
     a.o.seg_cap = e->rawCap;
-    launch_gen(e, a, GEN_L_TIMERS);
+    if (abs_on(e)) {  // the register-window sweep, then the general sweep over the keys it handed over
+        GH_OK(hipMemsetAsync(e->fb_n, 0, 8, e->stream));
+        a.fb_list = e->fb_list;
+        a.fb_n = e->fb_n;
+        a.fb_start = nullptr;
+        launch_gen(e, a, GEN_L_ABS_TIMERS);
+        a.mode = GEN_M_NOPAIRS;
+        a.t.due = e->fb_list;
+        a.t.ndue = e->fb_n;
+        launch_gen(e, a, GEN_L_TIMERS);
+    } else {
+        launch_gen(e, a, GEN_L_TIMERS);
+    }
     unsigned long long nr = 0, ndue = 0;
     GH_OK(hipMemcpyAsync(&nr, e->raw_count, 8, hipMemcpyDeviceToHost, e->stream));
     GH_OK(hipMemcpyAsync(&ndue, e->tm.ndue, 8, hipMemcpyDeviceToHost, e->stream));
@@ -1116,6 +1231,7 @@ void gen_stats(GenEngine* e, sg_stats* out) {
     out->partials_created = s[GST_CREATED];
     out->matches = s[GST_MATCHES];
     out->keys_touched = s[GST_KEYS];
+    out->window_spills = s[GST_SPILLS];
     out->partials_live = lv;
 }
 

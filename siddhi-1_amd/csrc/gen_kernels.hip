@@ -1197,13 +1197,22 @@ extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per
     for (;;) {
         if (!open) {
             uint32_t key = 0;
-            for (; j < kpl; j++) {  // the lane's next key with events in this batch
-                key = k0 + j * 64u;
-                if (key < a.K && gp(a.b.seg_begin)[key] < gp(a.b.seg_end)[key]) break;
+            if (a.mode & GEN_M_KEYLIST) {  // the keys the register-window kernel handed over, from their resume index
+                // (a fixed grid striding over the list: the list length is known on the device only)
+                const unsigned long long li = ((unsigned long long)j * gridDim.x + blockIdx.x) * 64u + threadIdx.x;
+                if (li >= *a.fb_n) break;
+                key = gp(a.fb_list)[li];
+                i = gp(a.fb_start)[key];
+                e = gp(a.b.seg_end)[key];
+            } else {
+                for (; j < kpl; j++) {  // the lane's next key with events in this batch
+                    key = k0 + j * 64u;
+                    if (key < a.K && gp(a.b.seg_begin)[key] < gp(a.b.seg_end)[key]) break;
+                }
+                if (j >= kpl) break;
+                i = gp(a.b.seg_begin)[key];
+                e = gp(a.b.seg_end)[key];
             }
-            if (j >= kpl) break;
-            i = gp(a.b.seg_begin)[key];
-            e = gp(a.b.seg_end)[key];
             L.retarget(key);
             L.initKey();
             open = true;
@@ -1259,7 +1268,7 @@ __device__ void gen_timers_key(const GenArgs& a, uint32_t key, uint64_t di, unsi
     const cGenProgram& G = *(cGenProgram*)a.G;
     if (!(L.W(0) & 1u)) {
         if (G.partitioned) {  // a key is created by its first event (not due: nd had no deadline)
-            if (G.playback)
+            if (G.playback && !(a.mode & GEN_M_NOPAIRS))
                 for (int i = 0; i < G.nStartup; i++) {
                     a.t.dpair_key[di * (uint64_t)G.nStartup + (uint64_t)i] = ~0ull;
                     a.t.dpair_i[di * (uint64_t)G.nStartup + (uint64_t)i] = GEN_PAIR_NONE;
@@ -1279,7 +1288,7 @@ __device__ void gen_timers_key(const GenArgs& a, uint32_t key, uint64_t di, unsi
         for (int i = 0; i < G.nStartup; i++) {
             const int p = G.startup[i];
             const bool due = L.qlen(p) != 0 && L.qhead(p) <= T;
-            if (G.partitioned) {  // the listener's collection of (due time, key): the A.10 check
+            if (G.partitioned && !(a.mode & GEN_M_NOPAIRS)) {  // the listener's collection of (due time, key): the A.10 check
                 const uint64_t slot = di * (uint64_t)G.nStartup + (uint64_t)i;
                 a.t.dpair_key[slot] = due ? gen_ord64(L.qhead(p)) : ~0ull;
                 a.t.dpair_i[slot] = due ? (uint32_t)i : GEN_PAIR_NONE;

@@ -131,17 +131,19 @@ __device__ __forceinline__ bool jo_compare(int op, int dom, GVal l, GVal r) {
 // evnull(slot, chain) -> bool (`e1 is null`).  The two top entries live in registers (t0 = top, t1 =
 // below it); deeper ones in stk[] (stk[i] = entry i from the bottom), touched only by programs deeper
 // than two.  Malformed code sets err bit 32 (GERR_REF) / 1 (stack too deep) and yields null.
-template <class CodePtr, class VarFn, class EvNullFn>
+// DEEP = false: programs at most two entries deep (checked on the host, jo_depth): no stack array at all,
+// so a kernel that only evaluates such programs keeps every value in registers (no scratch)
+template <bool DEEP = true, class CodePtr, class VarFn, class EvNullFn>
 __device__ __forceinline__ GVal jo_eval(CodePtr code, uint32_t pc, uint32_t n, uint32_t& err, VarFn var,
                                         EvNullFn evnull) {
-    GVal stk[24];
+    GVal stk[DEEP ? 24 : 1];
     GVal t0{0, true}, t1{0, true};
     int sp = 0;
     const uint32_t end = pc + n;
     while (pc < end) {
         const uint32_t w = code[pc];
         const uint32_t op = w & 0xff, a = (w >> 8) & 0xff, b = (w >> 16) & 0xff;
-        if (sp > 22) { err |= 1u; return GVal{0, true}; }
+        if (sp > (DEEP ? 22 : 2)) { err |= 1u; return GVal{0, true}; }
         GVal v;
         bool push = false, binary = false;
         switch (op) {
@@ -185,6 +187,7 @@ __device__ __forceinline__ GVal jo_eval(CodePtr code, uint32_t pc, uint32_t n, u
         }
         case SG_OP_ISNULL: t0 = {(uint64_t)t0.null, false}; break;
         case SG_OP_IFELSE: {  // ifThenElse(cond, then, else): three popped, one pushed
+            if constexpr (!DEEP) { err |= 1u; return GVal{0, true}; }
             const GVal c = sp >= 3 ? stk[sp - 3] : GVal{0, true};
             t0 = (!c.null && (c.b & 1)) ? t1 : t0;
             t1 = sp >= 4 ? stk[sp - 4] : GVal{0, true};
@@ -195,12 +198,19 @@ __device__ __forceinline__ GVal jo_eval(CodePtr code, uint32_t pc, uint32_t n, u
         default: err |= 32u; return GVal{0, true};
         }
         if (push) {
-            if (sp >= 2) stk[sp - 2] = t1;
+            if constexpr (DEEP) {
+                if (sp >= 2) stk[sp - 2] = t1;
+            } else if (sp >= 2) {
+                err |= 1u;
+                return GVal{0, true};
+            }
             t1 = t0;
             t0 = v;
             sp++;
         } else if (binary) {  // two popped, one pushed: the entry below the operands moves up
-            if (sp >= 3) t1 = stk[sp - 3];
+            if constexpr (DEEP) {
+                if (sp >= 3) t1 = stk[sp - 3];
+            }
             sp--;
         }
         pc += op_len(op);

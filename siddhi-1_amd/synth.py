@@ -162,3 +162,26 @@ def burst_ticks(start_ms: int, n_ms: int, n_keys: int, burst: int, seed: int = S
     volume = (np.uint64(1) + h2 % np.uint64(2000)).astype(np.int32)
     ts = (np.int64(t0) + t.astype(np.int64)).astype(np.int64)
     return {"key": key, "ts": ts, "symbol": key.copy(), "price": price, "volume": volume}
+
+
+def absent_deep_ticks(start_ms: int, n_ms: int, n_keys: int, burst: int, seed: int = SEED, t0: int = T0,
+                      period_ms: int = 600_000):
+    """Deep absent state (C4 with hundreds of live partials per key): as burst_ticks, millisecond t carries
+    `burst` events of ONE key (distinct timer due times across keys), but each key's
+    price falls steadily along a sawtooth of `period_ms` (key-specific phase) and, inside a burst, with the
+    event index: `not S[price > e1.price]` then almost never fires on an event, so every partial lives until
+    its `for` timer (or `within` expiry), and each key's sawtooth jump kills its whole list at once."""
+    t = np.repeat(np.arange(start_ms, start_ms + n_ms, dtype=np.uint64), burst)
+    j = np.tile(np.arange(burst, dtype=np.float64), n_ms)
+    i = np.arange(start_ms * burst, (start_ms + n_ms) * burst, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        base = np.uint64(seed) * np.uint64(0x100000001B3) if seed else np.uint64(0)
+        hk = splitmix64(t * np.uint64(7) + base)
+        h2 = splitmix64(i * np.uint64(3) + base + np.uint64(0x53))
+    key = (hk % np.uint64(n_keys)).astype(np.uint32)
+    phase = (splitmix64(key.astype(np.uint64) + base) % np.uint64(period_ms)).astype(np.float64)
+    frac = ((t.astype(np.float64) + phase) % period_ms) / period_ms
+    price = (21.0 + 60.0 * (1.0 - frac) - 1e-3 * j).astype(np.float32)
+    volume = (np.uint64(1) + h2 % np.uint64(2000)).astype(np.int32)
+    ts = (np.int64(t0) + t.astype(np.int64)).astype(np.int64)
+    return {"key": key, "ts": ts, "symbol": key.copy(), "price": price, "volume": volume}

@@ -1,0 +1,248 @@
+"""The register-window kernels of the absent-tail shape (csrc/abs_kernels.hip; BASELINE configs[3], "C4")
+against the CPU oracle and against the general kernels they shortcut (SG_NO_ABS=1), bit-exact:
+
+    [every] e1=S[f0] -> not S[f1(e1)] for T [within W]      (@app:playback, partitioned)
+
+* match records (timer matches: trigger seq, key, fire time, e1's seq), the work counters and the live
+  partials after every batch, the exported state documents (the kernels write the general engine's
+  state blocks in a canonical layout: the document must not notice);
+* keys the window cannot hold (more than ABS_R live partials, a timer queue about to fill, state imported
+  in a foreign layout) are handed to the general kernels mid-run (sg_stats.window_spills counts them) and
+  the results stay the same;
+* deep cross-batch state: 2048 keys with hundreds of live partials each carried
+  across 2^16-event pushes at the 30 s / 60 s windows of C4, every key checked against the oracle.
+"""
+import importlib
+
+import numpy as np
+import pytest
+
+from oracle_backend import build_oracle
+from test_gpu_general import _burst_stream
+from test_gpu_parity import _same
+
+sa = importlib.import_module("siddhi-1_amd")
+synth = importlib.import_module("siddhi-1_amd.synth")
+sd = importlib.import_module("siddhi-1_amd.state_doc")
+
+pytestmark = pytest.mark.gpu
+
+STOCK = "define stream S (symbol string, price float, volume int);\n"
+WIDE = "define stream S (symbol string, price double, volume long);\n"
+
+
+def query(every=True, within="within 60 milliseconds", for_="30 milliseconds", schema=STOCK, f0="price>20",
+          f1="price>e1.price"):
+    return ("@app:playback " + schema + "partition with (symbol of S) begin "
+            f"from {'every ' if every else ''}e1=S[{f0}] -> not S[{f1}] for {for_} {within} "
+            "select e1.price as a insert into O; end;")
+
+
+SHAPES = {
+    "c4": query(),
+    "no_within": query(within=""),
+    "no_every": query(every=False),
+    "short_for": query(for_="3 milliseconds", within="within 5 milliseconds"),
+    "wide_types": query(schema=WIDE, f1="price > e1.price + 0.5"),
+    "volume_filter": query(f0="volume > 500", f1="volume > e1.volume"),
+}
+
+
+def _engine(q, n_keys, batch, cap, general, monkeypatch):
+    app = sa.parse_app(q)
+    cq = sa.compile_query(app, app.queries[0], sa.StringDictionary())
+    if general:
+        monkeypatch.setenv("SG_NO_ABS", "1")
+    e = sa.NativeEngine(sa.load_hip_library(), "sg_", cq.ir, n_keys=n_keys, max_batch=batch, partial_capacity=cap,
+                        match_capacity=1 << 20)
+    monkeypatch.delenv("SG_NO_ABS", raising=False)
+    return cq, e
+
+
+def _oracle(q, n_keys):
+    app = sa.parse_app(q)
+    cq = sa.compile_query(app, app.queries[0], sa.StringDictionary())
+    return sa.NativeEngine(build_oracle(), "sgo_", cq.ir, n_keys=n_keys)
+
+
+def _cols(d, wide):
+    if wide:
+        return [d["symbol"], d["price"].astype(np.float64), d["volume"].astype(np.int64)]
+    return [d["symbol"], d["price"], d["volume"]]
+
+
+def _drive(engines, d, chunks, wide=False, start=None):
+    """push the stream in `chunks` (index bounds); before each chunk the playback clock moves to the chunk's
+    last timestamp (InputHandler.send(Event[])); polls after every call, compared across engines"""
+    ts = d["ts"]
+    if start is not None:
+        for e in engines:
+            e.advance_time(start)
+    total = 0
+    for lo, hi in chunks:
+        sl = slice(lo, hi)
+        for what in ("advance", "push"):
+            for e in engines:
+                if what == "advance":
+                    e.advance_time(int(ts[hi - 1]))
+                else:
+                    e.push(0, lo, ts[sl], [c[sl] for c in _cols(d, wide)], None, d["key"][sl])
+            ms = [e.poll() for e in engines]
+            for m in ms[1:]:
+                _same(ms[0], m)
+            total += len(ms[0])
+    return total
+
+
+def _stats_equal(a, b, keys=("matches", "partials_live")):
+    """the oracle and the device agree on matches and live partials; the two device paths on every counter"""
+    sa_, sb = a.stats(), b.stats()
+    for k in keys:
+        assert sa_[k] == sb[k], (k, sa_[k], sb[k])
+
+
+ALL = ("matches", "partials_created", "partials_scanned", "keys_touched", "partials_live")
+
+
+def _chunks(n, size):
+    return [(i, min(n, i + size)) for i in range(0, n, size)]
+
+
+@pytest.mark.parametrize("shape", sorted(SHAPES))
+def test_absent_window_equals_oracle_and_general(shape, monkeypatch):
+    """bursty streams (one key per millisecond, several events per burst), batches spanning many
+    milliseconds, the clock advanced per batch: device (register window) == device (general kernels) ==
+    oracle, matches, counters and state documents"""
+    q = SHAPES[shape]
+    n_keys = 64
+    d = _burst_stream(3000, n_keys, seed=11, max_burst=5)
+    n = len(d["ts"])
+    _, fast = _engine(q, n_keys, 4096, 48, False, monkeypatch)
+    _, gen = _engine(q, n_keys, 4096, 48, True, monkeypatch)
+    ora = _oracle(q, n_keys)
+    wide = "double" in q
+    total = _drive([fast, gen, ora], d, _chunks(n, 700), wide=wide, start=int(d["ts"][0]) - 3)
+    for e in (fast, gen, ora):
+        e.advance_time(int(d["ts"][-1]) + 10_000)
+    ms = [e.poll() for e in (fast, gen, ora)]
+    _same(ms[0], ms[1])
+    _same(ms[0], ms[2])
+    total += len(ms[0])
+    assert total > 0
+    _stats_equal(fast, ora)
+    _stats_equal(fast, gen, ALL)
+    assert sd.logical(sd.parse(fast.state_export()), seed_ts=True) == sd.logical(sd.parse(ora.state_export()),
+                                                                                 seed_ts=True)
+
+
+def test_absent_window_per_timestamp_sends(monkeypatch):
+    """one send per distinct timestamp (the clock moves before every send): timers fire between the
+    events of one key, the kills and the timer firings interleave at millisecond grain"""
+    q = SHAPES["c4"]
+    n_keys = 32
+    d = _burst_stream(2500, n_keys, seed=5, max_burst=4)
+    ts = d["ts"]
+    bounds = np.concatenate([[0], np.nonzero(np.diff(ts))[0] + 1, [len(ts)]])
+    _, fast = _engine(q, n_keys, 4096, 48, False, monkeypatch)
+    ora = _oracle(q, n_keys)
+    chunks = [(int(bounds[i]), int(bounds[i + 1])) for i in range(len(bounds) - 1)]
+    total = _drive([fast, ora], d, chunks, start=int(ts[0]) - 5)
+    assert total > 0
+    _stats_equal(fast, ora)
+    assert sd.logical(sd.parse(fast.state_export()), seed_ts=True) == sd.logical(sd.parse(ora.state_export()),
+                                                                                 seed_ts=True)
+
+
+def test_absent_window_overflow_hands_keys_to_general(monkeypatch):
+    """falling prices: no partial is killed, keys hold far more live partials than the register window
+    (and timer queues near their capacity): the kernel hands those keys to the general kernel from the
+    event where the window would overflow; results equal the oracle's"""
+    q = query(for_="400 milliseconds", within="within 800 milliseconds")
+    n_keys = 16
+    d = synth.absent_deep_ticks(0, 4000, n_keys, 3, t0=1_000_000, period_ms=3000)
+    n = len(d["ts"])
+    _, fast = _engine(q, n_keys, 4096, 256, False, monkeypatch)
+    ora = _oracle(q, n_keys)
+    total = _drive([fast, ora], d, _chunks(n, 1500), start=int(d["ts"][0]) - 1)
+    assert total > 0
+    _stats_equal(fast, ora)
+    assert fast.stats()["window_spills"] > 0   # the register-window kernel ran and handed keys over
+    assert sd.logical(sd.parse(fast.state_export()), seed_ts=True) == sd.logical(sd.parse(ora.state_export()),
+                                                                                 seed_ts=True)
+
+
+def test_absent_window_after_foreign_import(monkeypatch):
+    """state imported from an oracle document (the general layout, pool slots in any order) continues
+    exactly as the oracle does: the window loads foreign layouts or hands them over"""
+    q = SHAPES["c4"]
+    n_keys = 48
+    d = _burst_stream(3000, n_keys, seed=23, max_burst=5)
+    n = len(d["ts"])
+    half = n // 2
+    ora = _oracle(q, n_keys)
+    _drive([ora], d, _chunks(half, 600), start=int(d["ts"][0]) - 3)
+    doc = ora.state_export()
+    _, fast = _engine(q, n_keys, 4096, 48, False, monkeypatch)
+    fast.state_import(doc)
+    rest = [(lo, hi) for lo, hi in _chunks(n, 600) if lo >= half] or [(half, n)]
+    if rest[0][0] != half:
+        rest.insert(0, (half, rest[0][0]))
+    total = _drive([fast, ora], d, rest)
+    assert total > 0
+    assert sd.logical(sd.parse(fast.state_export()), seed_ts=True) == sd.logical(sd.parse(ora.state_export()),
+                                                                                 seed_ts=True)
+
+
+def test_absent_window_out_of_order_timestamps(monkeypatch):
+    """timestamps that go backwards inside a batch (staged partials out of ts order: promotion sorts them;
+    the playback clock ignores an earlier time)"""
+    q = SHAPES["c4"]
+    n_keys = 32
+    d = _burst_stream(2000, n_keys, seed=3, max_burst=3)
+    rng = np.random.default_rng(4)
+    jitter = rng.integers(-4, 5, len(d["ts"]))
+    d["ts"] = d["ts"] + jitter
+    n = len(d["ts"])
+    _, fast = _engine(q, n_keys, 4096, 48, False, monkeypatch)
+    _, gen = _engine(q, n_keys, 4096, 48, True, monkeypatch)
+    ora = _oracle(q, n_keys)
+    total = _drive([fast, gen, ora], d, _chunks(n, 500), start=int(d["ts"].min()) - 5)
+    assert total > 0
+    _stats_equal(fast, ora)
+
+
+def test_absent_deep_state_across_pushes(monkeypatch):
+    """C4's windows (for 30 sec, within 60 sec) over 2048 keys at the C4_deep rate (16
+    events per millisecond, one key per millisecond), pushed 2^16 events (4.1 s of event time) at a time:
+    hundreds of live partials per key survive into every later push's walk; every match of every key
+    equals the oracle's, and the live partials at batch start are counted"""
+    q = synth.C4_QUERY
+    n_keys, burst = 2048, 16
+    push = 1 << 16
+    ms_per_push = push // burst
+    app = sa.parse_app(q)
+    cq = sa.compile_query(app, app.queries[0], sa.StringDictionary())
+    gpu = sa.NativeEngine(sa.load_hip_library(), "sg_", cq.ir, n_keys=n_keys, max_batch=push, partial_capacity=512,
+                          match_capacity=1 << 21, flags=sa.native.SG_CFG_TIMING)
+    ora = sa.NativeEngine(build_oracle(), "sgo_", cq.ir, n_keys=n_keys)
+    total = 0
+    n_push = 14   # 57 s of event time: the live lists fill over the first 30 s, then fire and refill
+    live0 = []
+    for p in range(n_push):
+        d = synth.absent_deep_ticks(p * ms_per_push, ms_per_push, n_keys, burst)
+        before = gpu.stats()
+        for e in (gpu, ora):
+            e.advance_time(int(d["ts"][-1]))
+        mg, mo = gpu.poll(), ora.poll()
+        _same(mg, mo)
+        total += len(mg)
+        for e in (gpu, ora):
+            e.push(0, p * push, d["ts"], [d["symbol"], d["price"], d["volume"]], None, d["key"])
+        mg, mo = gpu.poll(), ora.poll()
+        _same(mg, mo)
+        after = gpu.stats()
+        live0.append((after["live_at_batch_start"] - before["live_at_batch_start"]) /
+                     max(1, after["keys_touched"] - before["keys_touched"]))
+    assert total > 0
+    assert max(live0) >= 100, live0    # hundreds of live partials per touched key carried into a push
+    assert gpu.stats()["partials_live"] == ora.stats()["partials_live"]
