@@ -75,6 +75,23 @@ def cpu_model():
     return "unknown"
 
 
+def cpu_quota():
+    """CPUs this process may use: the cgroup v2 quota (cpu.max), the affinity mask, whichever is smaller"""
+    q = None
+    try:
+        lim, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if lim != "max":
+            q = float(lim) / float(per)
+    except (OSError, ValueError):
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+        q = min(q, aff) if q else aff
+    except (AttributeError, OSError):
+        pass
+    return q
+
+
 def cpu_baseline(sa, synth, n_keys, batch, seconds):
     """SURVEY §8(d) CPU legs, the CPU oracle (the C++ restatement of the reference engine; the reference
     JVM is not runnable here or on the box) on the host cores of the GPU box:
@@ -101,26 +118,33 @@ def cpu_baseline(sa, synth, n_keys, batch, seconds):
         done += chunk
     eng.close()
     single = done / busy
-    # (ii) partition-parallel over the box's CPU share (at most 16 threads on a one-GPU box)
-    T = max(1, min(16, os.cpu_count() or 1))
-    total = int(min(batch * 4, single * seconds * T * 0.7)) // (T * chunk) * (T * chunk) or T * chunk
+    # (ii) partition-parallel over the box's CPU share: the cgroup CPU quota when there is one, else
+    # OMP_NUM_THREADS (set to the GPU's share on the GPU boxes), else nproc.  One oracle engine per thread;
+    # the chunks are cut contiguous before the timed region, so each thread's loop is two foreign calls per
+    # chunk (ctypes drops the GIL around them) and the threads share nothing but the allocator.
+    quota = cpu_quota()
+    T = max(1, int(quota) if quota else int(os.environ.get("OMP_NUM_THREADS", 0)) or (os.cpu_count() or 1))
+    total = int(min(batch * 4, single * seconds * T * 0.5)) // (T * chunk) * (T * chunk) or T * chunk
     d = synth.stock_ticks(0, total, n_keys)
     own = d["key"] % np.uint32(T)
     shards = []
     for r in range(T):
         idx = np.nonzero(own == r)[0]
-        shards.append({"ts": d["ts"][idx], "key": (d["key"][idx] // np.uint32(T)).astype(np.uint32),
-                       "cols": [d["symbol"][idx], d["price"][idx], d["volume"][idx]], "seq": idx.astype(np.uint64)})
+        ts, key = d["ts"][idx], (d["key"][idx] // np.uint32(T)).astype(np.uint32)
+        cols = [d["symbol"][idx], d["price"][idx], d["volume"][idx]]
+        shards.append([(a, np.ascontiguousarray(ts[a:a + chunk]), [np.ascontiguousarray(c[a:a + chunk]) for c in cols],
+                        np.ascontiguousarray(key[a:a + chunk])) for a in range(0, len(idx), chunk)])
     del d
     engs = [sa.NativeEngine(lib, "sgo_", cq.ir, n_keys=(n_keys + T - 1) // T) for _ in range(T)]
+    busy = [0.0] * T
 
     def work(r):
-        s, e = shards[r], engs[r]
-        n = len(s["ts"])
-        for a in range(0, n, chunk):   # local arrival seqs (the per-key order is the global one)
-            sl = slice(a, min(n, a + chunk))
-            e.push(0, a, s["ts"][sl], [c[sl] for c in s["cols"]], None, s["key"][sl])
-            e.poll()
+        e = engs[r]
+        t = time.perf_counter()
+        for a, ts, cols, key in shards[r]:   # local arrival seqs (the per-key order is the global one)
+            e.push(0, a, ts, cols, None, key)
+            e.discard()
+        busy[r] = time.perf_counter() - t
 
     th = [threading.Thread(target=work, args=(r,)) for r in range(T)]
     t0 = time.perf_counter()
@@ -148,7 +172,9 @@ def cpu_baseline(sa, synth, n_keys, batch, seconds):
             "sample": f"first {done} events of the C2 stream ({n_keys} keys), CPU oracle (faithful single-thread "
                       f"restatement of the reference engine; reference JVM unavailable on the box)",
             "cpu_model": cpu_model(), "nproc": os.cpu_count(),
-            "partition_parallel": {"value": par, "unit": "events/s", "threads": T,
+            "partition_parallel": {"value": par, "unit": "events/s", "threads": T, "cpu_quota": quota,
+                                   "per_thread_scaling": par / single / T,
+                                   "thread_busy_s": [round(b, 3) for b in busy],
                                    "sample": f"first {total} events of the C2 stream, keys sharded key % {T}, one "
                                              f"oracle engine per thread"},
             "C1": {"value": c1_done / c1_busy, "unit": "events/s", "cores": 1,

@@ -1049,7 +1049,11 @@ struct Lane {
             runChain(p, se);
             if ((retm >> P.thisLast) & 1u) {
                 retm &= ~(1u << P.thisLast);
-                if (nOut < OUTCAP) { stIncref(se); outList[nOut++] = se; } else err |= GERR_CAP;
+                // (an absent state returns nothing, :265-283: its partials are not collected at all, so
+                // one event may kill any number of them)
+                if (!P.absent) {
+                    if (nOut < OUTCAP) { stIncref(se); outList[nOut++] = se; } else err |= GERR_CAP;
+                }
             }
             if (flag(p, GF_CHANGED)) {
                 stDecref(se);

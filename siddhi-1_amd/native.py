@@ -392,6 +392,15 @@ class NativeEngine:
         self._check(self._poll(self.h, SG_MEM_DEVICE | (SG_POLL_READY if ready else 0), C.byref(m)))
         return m
 
+    def discard(self):
+        """poll to host memory and release at once, without building arrays (a caller that only needs the
+        engine to hand its matches out, e.g. a throughput loop)"""
+        m = sg_match_batch()
+        self._check(self._poll(self.h, SG_MEM_HOST, C.byref(m)))
+        n = int(m.n)
+        self._check(self._release(self.h, C.byref(m)))
+        return n
+
     def release(self, m):
         self._check(self._release(self.h, C.byref(m)))
 
