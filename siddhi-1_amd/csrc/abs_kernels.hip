@@ -54,8 +54,10 @@ template <int NW> struct AbsEv {
     uint32_t nb;
 };
 
-// one key's absent-tail state during a walk (see the file comment)
-template <int NW> struct AbsKey {
+// one key's absent-tail state during a walk (see the file comment); TM: the timer sweep, which also keeps
+// the first ABS_QP entries of the timer queue in registers (the pops of one sweep need no dependent loads)
+#define ABS_QP 4
+template <int NW, bool TM> struct AbsKey {
     const cGenProgram& G;
     gu32* S;
     uint32_t K, k;
@@ -74,12 +76,14 @@ template <int NW> struct AbsKey {
     int64_t lst;          // p1 lastScheduledTime
     uint32_t qh, ql;      // p1 timer queue head index / length
     int64_t qhv;          // the head entry (valid while ql > 0)
+    int64_t qbuf[ABS_QP]; // TM: queue entries [qh, qh + qb)
+    uint32_t qb;
     uint32_t err;
     unsigned long long scanned, created, matches;
 
     __device__ AbsKey(const GenProgram* g, uint32_t* state, uint32_t K_, uint32_t key)
         : G(*(cGenProgram*)g), S(gp(state)), K(K_), k(key), n(0), np(0), sbad(false), seedPend(0), seedStg(0),
-          seedPendTs(-1), seedStgTs(-1), f0(0), f1(0), lst(0), qh(0), ql(0), qhv(0), err(0), scanned(0), created(0),
+          seedPendTs(-1), seedStgTs(-1), f0(0), f1(0), lst(0), qh(0), ql(0), qhv(0), qb(0), err(0), scanned(0), created(0),
           matches(0) {
         ks0 = G.offKS + (uint32_t)G.absP0 * G.ksWords;
         ks1 = G.offKS + (uint32_t)G.absP1 * G.ksWords;
@@ -170,8 +174,23 @@ template <int NW> struct AbsKey {
         qh = W(ks1 + KS_QHEAD);
         ql = W(ks1 + KS_QLEN);
         if (qh >= G.Q || ql > G.Q) return false;
-        if (ql) qhv = R64(qword(qh));
+        if constexpr (TM) {
+            qfill();
+        } else {
+            if (ql) qhv = R64(qword(qh));
+        }
         return true;
+    }
+    // TM: (re)load the buffered queue entries (independent loads, all in flight together)
+    __device__ __forceinline__ void qfill() {
+        qb = ql < (uint32_t)ABS_QP ? ql : (uint32_t)ABS_QP;
+#pragma unroll
+        for (int i = 0; i < ABS_QP; ++i) {
+            uint32_t pos = qh + (uint32_t)i;
+            pos = pos >= G.Q ? pos - G.Q : pos;
+            qbuf[i] = (uint32_t)i < qb ? R64(qword(pos)) : 0;
+        }
+        qhv = qbuf[0];
     }
 
     // ---- store: the lists in the canonical layout (StateEvent 0 = the seed, 1 + j = partial j over
@@ -249,13 +268,29 @@ template <int NW> struct AbsKey {
         if (ql >= G.Q) { err |= GERR_CAP; return; }
         const uint32_t pos = (qh + ql) % G.Q;
         W64(qword(pos), t);
+        if constexpr (TM) {
+            if (qb == ql && qb < (uint32_t)ABS_QP) {  // the buffer holds the whole queue: append there too
+#pragma unroll
+                for (int i = 0; i < ABS_QP; ++i)
+                    if ((uint32_t)i == qb) qbuf[i] = t;
+                qb++;
+            }
+        }
         if (ql == 0) qhv = t;
         ql++;
     }
     __device__ __forceinline__ void qpop() {
         qh = (qh + 1) % G.Q;
         ql--;
-        if (ql) qhv = R64(qword(qh));
+        if constexpr (TM) {
+#pragma unroll
+            for (int i = 0; i + 1 < ABS_QP; ++i) qbuf[i] = qbuf[i + 1];
+            qb--;
+            if (qb == 0 && ql) qfill();
+            qhv = qbuf[0];
+        } else {
+            if (ql) qhv = R64(qword(qh));
+        }
     }
 
     // ---- the window ----
@@ -483,11 +518,11 @@ template <int NW> struct AbsKey {
         }
         const unsigned long long r = resBase++;
         resLeft--;
-        matches++;
+        const uint32_t rank = (uint32_t)matches++;
         if (r >= resEnd) { err |= GERR_MATCHCAP; return; }
         gu32* rec = gp(a.o.raw) + r * a.o.recWords;
         rec[0] = 0xfffffffeu;
-        rec[1] = 0u;
+        rec[1] = rank;  // its rank in this key's sweep (the matches are ordered through the sorted due keys)
         rec[2] = 0xffffffffu;  // SG_TIMER_SEQ
         rec[3] = 0xffffffffu;
         rec[4] = (uint32_t)(uint64_t)t;
@@ -581,7 +616,7 @@ template <int NW> __device__ void abs_batch(const GenArgs& a) {
         b = gp(a.b.seg_begin)[key];
         e = gp(a.b.seg_end)[key];
     }
-    AbsKey<NW> L(a.G, a.state, a.K, key < a.K ? key : 0u);
+    AbsKey<NW, false> L(a.G, a.state, a.K, key < a.K ? key : 0u);
     bool walk = b < e;
     bool fb = false;
     uint32_t stop = b;
@@ -629,12 +664,13 @@ template <int NW> __device__ void abs_timers(const GenArgs& a) {
         const uint64_t di = base + threadIdx.x;
         const bool act = di < nd;
         const uint32_t key = act ? gp(a.t.due)[di] : 0u;
-        AbsKey<NW> L(a.G, a.state, a.K, key);
+        AbsKey<NW, true> L(a.G, a.state, a.K, key);
         bool fb = false;
         if (act) {
             if (!(L.W(0) & 1u)) {  // a key is created by its first event (not due)
                 gp(a.t.dpair_key)[di] = ~0ull;
                 gp(a.t.dpair_i)[di] = GEN_PAIR_NONE;
+                if (a.t.dpair_kid) gp(a.t.dpair_kid)[di] = GEN_PAIR_NONE;
                 gp(a.t.nd)[key] = GEN_NO_DEADLINE;
             } else {
                 // the listener's collection of (due time, key) from the queue head (the A.10 check)
@@ -643,6 +679,7 @@ template <int NW> __device__ void abs_timers(const GenArgs& a) {
                 const bool due = ql != 0 && h <= a.now;
                 gp(a.t.dpair_key)[di] = due ? abs_ord64(h) : ~0ull;
                 gp(a.t.dpair_i)[di] = due ? li : GEN_PAIR_NONE;
+                if (a.t.dpair_kid) gp(a.t.dpair_kid)[di] = due ? key : GEN_PAIR_NONE;
                 if (!L.load()) {
                     fb = true;
                 } else {
@@ -657,6 +694,7 @@ template <int NW> __device__ void abs_timers(const GenArgs& a) {
                     }
                     L.store();
                     gp(a.t.nd)[key] = L.deadline();
+                    if (a.t.kcnt) gp(a.t.kcnt)[key] = (uint32_t)L.matches;
                     for (uint32_t x = 0; x < resLeft; x++) {  // unused reserved raw slots
                         const unsigned long long rr = resBase + x;
                         if (rr < resEnd) {

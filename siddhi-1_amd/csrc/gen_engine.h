@@ -197,6 +197,11 @@ struct GenTimers {
     unsigned long long* ndue;
     unsigned long long* dpair_key;   // [K * nStartup] order-preserving u64 of the head, or UINT64_MAX
     uint32_t* dpair_i;               // [K * nStartup] listener index, or GEN_PAIR_NONE
+    // one listener (nStartup == 1, partitioned, playback): the timer matches are ordered through the due
+    // keys sorted by head (gen_host.hip timer_order_keys) instead of a sort of the matches: the key of each
+    // due slot and each due key's match count of the sweep (records carry their rank within the key)
+    uint32_t* dpair_kid;             // [K] key of due slot di, or NULL
+    uint32_t* kcnt;                  // [K] matches of the key at this sweep, or NULL
 };
 
 struct GenArgs {

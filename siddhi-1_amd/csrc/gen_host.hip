@@ -545,6 +545,58 @@ __global__ void k_gen_live(const GenProgram* G, const uint32_t* S, uint32_t K, u
     if (live) atomicAdd(out, live);
 }
 
+// ---- timer matches ordered through the due keys (one listener: GenTimers.kcnt / dpair_kid) ----
+// sort key of due slot di: 1 + (T - head) (descending = head ascending; 0 = not due, sorted last); a lag
+// that does not fit 32 bits sets *ovf (the host then takes the 64-bit pair sort)
+__global__ void __launch_bounds__(256) k_timer_rel(const unsigned long long* __restrict__ dkey,
+                                                   const unsigned long long* __restrict__ ndue, int64_t T,
+                                                   uint32_t* __restrict__ rel, unsigned long long* __restrict__ ctr) {
+    __shared__ unsigned long long bmax[4];
+    const uint64_t di = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    unsigned long long r = 0;
+    if (di < *ndue) {
+        const unsigned long long h = dkey[di];
+        if (h != ~0ull) {
+            const int64_t head = (int64_t)(h ^ (1ull << 63));
+            r = (unsigned long long)(T - head) + 1ull;
+            if (T < head || r >= 0xffffffffull) { ctr[1] = 1ull; r = 0; }
+        }
+        rel[di] = (uint32_t)r;
+    }
+    for (int off = 32; off > 0; off >>= 1) r = max(r, (unsigned long long)__shfl_xor(r, off, 64));
+    if ((threadIdx.x & 63) == 0) bmax[threadIdx.x / 64] = r;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned long long m = max(max(bmax[0], bmax[1]), max(bmax[2], bmax[3]));
+        if (m) atomicMax(&ctr[0], m);
+    }
+}
+// two due keys sharing a head time (adjacent after the sort): the reference's collapse quirk (A.10)
+__global__ void k_timer_collapse(const uint32_t* __restrict__ srel, uint64_t n, uint32_t* __restrict__ err) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j == 0 || j >= n || srel[j] == 0u) return;
+    if (srel[j] == srel[j - 1]) atomicOr(err, (uint32_t)GERR_COLLAPSE);
+}
+__global__ void k_timer_cnt(const uint32_t* __restrict__ skid, uint64_t n, const uint32_t* __restrict__ kcnt,
+                            uint32_t* __restrict__ c) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < n) c[j] = skid[j] == GEN_PAIR_NONE ? 0u : kcnt[skid[j]];
+}
+__global__ void k_timer_off(const uint32_t* __restrict__ skid, uint64_t n, const uint32_t* __restrict__ off,
+                            uint32_t* __restrict__ koff) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < n && skid[j] != GEN_PAIR_NONE) koff[skid[j]] = off[j];
+}
+// each timer match to count + (its key's offset in head order) + (its rank in the key's sweep)
+__global__ void k_timer_scatter(const uint32_t* raw, const unsigned long long* raw_count, const uint32_t* koff,
+                                OutBufs o) {
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= *raw_count) return;
+    const uint32_t* rec = raw + r * o.recWords;
+    if (rec[0] != 0xfffffffeu) return;
+    write_out(o, *o.count + koff[rec[6]] + rec[1], rec, true);
+}
+
 struct TimerLess {
     const uint32_t* k1;
     const int64_t* k2;
@@ -603,6 +655,14 @@ struct GenEngine {
     // keys the register-window kernels (abs_kernels.hip) hand to the general kernels
     uint32_t *fb_list = nullptr, *fb_start = nullptr;
     unsigned long long* fb_n = nullptr;
+    // timer matches ordered through the due keys (keyorder: partitioned, playback, one listener)
+    bool keyorder = false;
+    uint32_t *rel = nullptr, *srel = nullptr, *skid = nullptr, *kc = nullptr, *koff_s = nullptr, *koff = nullptr;
+    unsigned long long* ctr = nullptr;  // [0] max sort key, [1] lag overflow
+    void* ksort_tmp = nullptr;
+    size_t ksort_tmp_bytes = 0;
+    void* kscan_tmp = nullptr;
+    size_t kscan_tmp_bytes = 0;
     GenArgs* d_args = nullptr;           // kernel argument ring (device) and its pinned staging
     GenArgs* h_args = nullptr;
     uint64_t arg_next = 0;
@@ -755,6 +815,24 @@ GenEngine* gen_create(const uint32_t* ir, size_t nw, const sg_config& cfg, hipSt
                 GH_OK(rocprim::radix_sort_pairs(nullptr, e->psort_tmp_bytes, e->tm.dpair_key, e->pair_key_s,
                                                 e->tm.dpair_i, e->pair_i_s, (size_t)e->npairs_cap, 0, 64, stream));
                 e->psort_tmp = e->dalloc<uint8_t>(e->psort_tmp_bytes);
+                if (G.nStartup == 1) {
+                    e->keyorder = true;
+                    e->tm.dpair_kid = e->dalloc<uint32_t>(K);
+                    e->tm.kcnt = e->dalloc<uint32_t>(K);
+                    e->rel = e->dalloc<uint32_t>(K);
+                    e->srel = e->dalloc<uint32_t>(K);
+                    e->skid = e->dalloc<uint32_t>(K);
+                    e->kc = e->dalloc<uint32_t>(K);
+                    e->koff_s = e->dalloc<uint32_t>(K);
+                    e->koff = e->dalloc<uint32_t>(K);
+                    e->ctr = e->dalloc<unsigned long long>(2);
+                    GH_OK(rocprim::radix_sort_pairs_desc(nullptr, e->ksort_tmp_bytes, e->rel, e->srel, e->tm.dpair_kid,
+                                                         e->skid, (size_t)K, 0, 32, stream));
+                    e->ksort_tmp = e->dalloc<uint8_t>(e->ksort_tmp_bytes);
+                    GH_OK(rocprim::exclusive_scan(nullptr, e->kscan_tmp_bytes, e->kc, e->koff_s, 0u, (size_t)K,
+                                                  rocprim::plus<uint32_t>(), stream));
+                    e->kscan_tmp = e->dalloc<uint8_t>(e->kscan_tmp_bytes);
+                }
             }
         }
         e->live = e->dalloc<unsigned long long>(1);
@@ -835,8 +913,8 @@ static void launch_gen(GenEngine* e, GenArgs a, int which) {
                            dim3(64), 0, e->stream, ap);
     else if (which == GEN_L_DEADLINES) hipLaunchKernelGGL(k_gen_deadlines, dim3(blocks), dim3(64), 0, e->stream, ap);
     else if (which == GEN_L_ABS_BATCH) hipLaunchKernelGGL(kAbsBatch[e->host.absNW], dim3(blocks), dim3(64), 0, e->stream, ap);
-    else if (which == GEN_L_ABS_TIMERS)
-        hipLaunchKernelGGL(kAbsTimers[e->host.absNW], dim3(std::min(blocks, GEN_TIMER_BLOCKS)), dim3(64), 0, e->stream, ap);
+    else if (which == GEN_L_ABS_TIMERS)  // one lane per possible due key (the count is on the device)
+        hipLaunchKernelGGL(kAbsTimers[e->host.absNW], dim3(blocks), dim3(64), 0, e->stream, ap);
     else hipLaunchKernelGGL(k_gen_batch, dim3(fb ? GEN_FB_BLOCKS : (e->K + 64u * a.kpl - 1) / (64u * a.kpl)), dim3(64), 0,
                             e->stream, ap);
     GH_OK(hipGetLastError());
@@ -978,7 +1056,7 @@ int gen_advance(GenEngine* e, int64_t t, std::string& msg) {
     GH_OK(hipMemsetAsync(e->nvalid, 0, 8, e->stream));
     GH_OK(hipMemsetAsync(e->tm.ndue, 0, 8, e->stream));
     if (G.partitioned) {  // the keys with a deadline <= t: one pass over nd[K]
-        const uint32_t blocks = std::min<uint32_t>((e->K + 255) / 256, 2048u);
+        const uint32_t blocks = std::min<uint32_t>((e->K + 4095) / 4096, 1024u);
         hipLaunchKernelGGL(k_gen_due, dim3(blocks), dim3(256), 0, e->stream, e->tm.nd, e->K, t, e->tm.due, e->tm.ndue);
     }
     a.o.nseg = 1;
@@ -996,12 +1074,46 @@ int gen_advance(GenEngine* e, int64_t t, std::string& msg) {
     } else {
         launch_gen(e, a, GEN_L_TIMERS);
     }
-    unsigned long long nr = 0, ndue = 0;
+    if (e->keyorder) {  // the sort keys of the due slots (no host round trip: the count is on the device)
+        GH_OK(hipMemsetAsync(e->ctr, 0, 16, e->stream));
+        hipLaunchKernelGGL(k_timer_rel, dim3((e->K + 255) / 256), dim3(256), 0, e->stream, e->tm.dpair_key, e->tm.ndue,
+                           t, e->rel, e->ctr);
+    }
+    unsigned long long nr = 0, ndue = 0, kctr[2] = {0, 0};
     GH_OK(hipMemcpyAsync(&nr, e->raw_count, 8, hipMemcpyDeviceToHost, e->stream));
     GH_OK(hipMemcpyAsync(&ndue, e->tm.ndue, 8, hipMemcpyDeviceToHost, e->stream));
+    if (e->keyorder) GH_OK(hipMemcpyAsync(kctr, e->ctr, 16, hipMemcpyDeviceToHost, e->stream));
     GH_OK(hipStreamSynchronize(e->stream));
     bool check = false;
-    if (G.partitioned && G.playback && ndue * (uint64_t)G.nStartup >= 2) {
+    if (e->keyorder && !kctr[1] && ndue >= 1) {
+        // one listener: the due keys sorted by queue head (TreeMultimap order of the listener's collection,
+        // Scheduler.java:78-99) give the output order of their timer matches (each key's in emission
+        // order) and, where two heads are equal, the A.10 collapse below
+        const size_t n = (size_t)ndue;
+        int bits = 1;
+        while (bits < 32 && (kctr[0] >> bits) != 0) bits++;
+        size_t tmp = e->ksort_tmp_bytes;
+        GH_OK(rocprim::radix_sort_pairs_desc(e->ksort_tmp, tmp, e->rel, e->srel, e->tm.dpair_kid, e->skid, n, 0, bits,
+                                             e->stream));
+        const dim3 g((unsigned)((n + 255) / 256));
+        if (n >= 2) {
+            hipLaunchKernelGGL(k_timer_collapse, g, dim3(256), 0, e->stream, e->srel, (uint64_t)n, e->err);
+            check = true;
+        }
+        if (nr > 0) {
+            hipLaunchKernelGGL(k_timer_cnt, g, dim3(256), 0, e->stream, e->skid, (uint64_t)n, e->tm.kcnt, e->kc);
+            size_t st = e->kscan_tmp_bytes;
+            GH_OK(rocprim::exclusive_scan(e->kscan_tmp, st, e->kc, e->koff_s, 0u, n, rocprim::plus<uint32_t>(), e->stream));
+            hipLaunchKernelGGL(k_timer_off, g, dim3(256), 0, e->stream, e->skid, (uint64_t)n, e->koff_s, e->koff);
+            const size_t m = (size_t)std::min<unsigned long long>(nr, e->rawCap);
+            hipLaunchKernelGGL(k_timer_scatter, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, e->stream, e->raw,
+                               e->raw_count, e->koff, e->out);
+            hipLaunchKernelGGL(k_gen_bump, dim3(1), dim3(1), 0, e->stream, e->out.count, e->t_cnt, e->t_off, 1u,
+                               (const unsigned long long*)e->nvalid);
+            GH_OK(hipGetLastError());
+        }
+        nr = 0;  // ordered
+    } else if (G.partitioned && G.playback && ndue * (uint64_t)G.nStartup >= 2) {
         // the reference's listener collects the due (time, key) states in a
         // TreeMultimap whose value comparator is always 0 (Scheduler.java:78-89, 364-367), so of several
         // keys due at the same time only one (chosen by HashMap order) fires at this advance.  That

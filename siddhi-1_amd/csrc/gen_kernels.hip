@@ -440,7 +440,7 @@ struct Lane {
         gu32* rec = gp(A.o.raw) + r * A.o.recWords;
         const bool timer = trigSeq == SG_TIMER_SEQ;
         rec[0] = timer ? 0xfffffffeu : trigIdx;
-        rec[1] = timer ? 0u : trigRank++;
+        rec[1] = trigRank++;  // a timer match: its rank in this key's sweep (gen_host.hip timer ordering)
         rec[2] = (uint32_t)trigSeq;
         rec[3] = (uint32_t)(trigSeq >> 32);
         const int64_t ts = stTs(se);
@@ -1276,6 +1276,7 @@ __device__ void gen_timers_key(const GenArgs& a, uint32_t key, uint64_t di, unsi
                 for (int i = 0; i < G.nStartup; i++) {
                     a.t.dpair_key[di * (uint64_t)G.nStartup + (uint64_t)i] = ~0ull;
                     a.t.dpair_i[di * (uint64_t)G.nStartup + (uint64_t)i] = GEN_PAIR_NONE;
+                    if (a.t.dpair_kid) a.t.dpair_kid[di * (uint64_t)G.nStartup + (uint64_t)i] = GEN_PAIR_NONE;
                 }
             a.t.nd[key] = GEN_NO_DEADLINE;
             return;
@@ -1296,6 +1297,7 @@ __device__ void gen_timers_key(const GenArgs& a, uint32_t key, uint64_t di, unsi
                 const uint64_t slot = di * (uint64_t)G.nStartup + (uint64_t)i;
                 a.t.dpair_key[slot] = due ? gen_ord64(L.qhead(p)) : ~0ull;
                 a.t.dpair_i[slot] = due ? (uint32_t)i : GEN_PAIR_NONE;
+                if (a.t.dpair_kid) a.t.dpair_kid[slot] = due ? key : GEN_PAIR_NONE;
             }
             if (!due) continue;
             L.tk1 = (uint32_t)i;
@@ -1331,6 +1333,7 @@ __device__ void gen_timers_key(const GenArgs& a, uint32_t key, uint64_t di, unsi
         }
     }
     a.t.nd[key] = L.nextDeadline();
+    if (a.t.kcnt) a.t.kcnt[key] = (uint32_t)L.matches;
     sc += L.scanned;
     cr += L.created;
     ma += L.matches;
@@ -1354,20 +1357,49 @@ extern "C" __global__ void __launch_bounds__(64) k_gen_deadlines(const GenArgs* 
     a.t.nd[key] = (L.W(0) & 1u) ? L.nextDeadline() : GEN_NO_DEADLINE;
 }
 
-// the keys due at this advance (nd <= now): wave-ballot compaction into t.due
-extern "C" __global__ void __launch_bounds__(256) k_gen_due(const int64_t* __restrict__ nd, uint32_t K, int64_t now,
-                                                            uint32_t* __restrict__ due,
-                                                            unsigned long long* __restrict__ ndue) {
+// the keys due at this advance (nd <= now), compacted into t.due: each block takes a contiguous range of
+// keys, counts its due keys (wave ballots combined in LDS) and reserves its output range with ONE atomic
+// (one atomic per wave serialised ~16K atomics on one counter at 2^20 keys: 150-200 us)
+#define GEN_DUE_BLOCK 256
+extern "C" __global__ void __launch_bounds__(GEN_DUE_BLOCK) k_gen_due(const int64_t* __restrict__ nd, uint32_t K,
+                                                                      int64_t now, uint32_t* __restrict__ due,
+                                                                      unsigned long long* __restrict__ ndue) {
+    constexpr uint32_t NW = GEN_DUE_BLOCK / 64;
+    __shared__ uint32_t wcnt[NW];
+    __shared__ unsigned long long bbase;
     const int lane = threadIdx.x & 63;
-    for (uint32_t base = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < K; base += gridDim.x * blockDim.x) {
-        const uint32_t k = base + (uint32_t)lane;
-        const bool d = k < K && nd[k] <= now;
+    const uint32_t wv = threadIdx.x / 64;
+    const uint32_t per = (K + gridDim.x - 1) / gridDim.x;              // keys of this block
+    const uint32_t lo = min(K, blockIdx.x * per), hi = min(K, lo + per);
+    const uint32_t step = GEN_DUE_BLOCK;
+    // pass 1: count
+    uint32_t mine = 0;
+    for (uint32_t k = lo + threadIdx.x; k < hi; k += step) mine += nd[k] <= now ? 1u : 0u;
+    for (int off = 32; off > 0; off >>= 1) mine += (uint32_t)__shfl_xor((int)mine, off, 64);
+    if (lane == 0) wcnt[wv] = mine;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (uint32_t w = 0; w < NW; w++) t += wcnt[w];
+        bbase = t ? atomicAdd(ndue, (unsigned long long)t) : 0ull;
+    }
+    __syncthreads();
+    // pass 2: write, in key order inside the block (ballot prefix per wave row, a running offset per row)
+    unsigned long long pos = bbase;
+    for (uint32_t base = lo; base < hi; base += step) {
+        const uint32_t k = base + threadIdx.x;
+        const bool d = k < hi && nd[k] <= now;
         const unsigned long long m = __ballot(d);
-        if (!m) continue;
-        unsigned long long b0 = 0;
-        if (lane == 0) b0 = atomicAdd(ndue, (unsigned long long)__popcll(m));
-        b0 = __shfl(b0, 0, 64);
-        if (d) due[b0 + __popcll(m & ((1ull << lane) - 1ull))] = k;
+        if (lane == 0) wcnt[wv] = (uint32_t)__popcll(m);
+        __syncthreads();
+        uint32_t before = 0, row = 0;
+        for (uint32_t w = 0; w < NW; w++) {
+            before += w < wv ? wcnt[w] : 0u;
+            row += wcnt[w];
+        }
+        if (d) due[pos + before + __popcll(m & ((1ull << lane) - 1ull))] = k;
+        pos += row;
+        __syncthreads();
     }
 }
 

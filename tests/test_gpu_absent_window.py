@@ -199,10 +199,11 @@ def test_absent_window_out_of_order_timestamps(monkeypatch):
     q = SHAPES["c4"]
     n_keys = 32
     d = _burst_stream(2000, n_keys, seed=3, max_burst=3)
-    rng = np.random.default_rng(4)
-    jitter = rng.integers(-4, 5, len(d["ts"]))
-    d["ts"] = d["ts"] + jitter
+    # arrival order reversed inside blocks of 7 events: timestamps go backwards, while every millisecond
+    # still belongs to one key (distinct due times across keys)
     n = len(d["ts"])
+    perm = np.concatenate([np.arange(i, min(n, i + 7))[::-1] for i in range(0, n, 7)])
+    d = {k: v[perm] for k, v in d.items()}
     _, fast = _engine(q, n_keys, 4096, 48, False, monkeypatch)
     _, gen = _engine(q, n_keys, 4096, 48, True, monkeypatch)
     ora = _oracle(q, n_keys)
