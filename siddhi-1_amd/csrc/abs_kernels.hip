@@ -36,6 +36,7 @@
 #include "../../include/siddhi_gpu_ir.h"
 #include "gen_engine.h"
 #include "java_ops.h"
+#include "sg_engine.h"
 
 namespace {
 
@@ -267,28 +268,23 @@ template <int NW, bool TM> struct AbsKey {
     __device__ __forceinline__ void notifyAt(int64_t t) {
         if (ql >= G.Q) { err |= GERR_CAP; return; }
         const uint32_t pos = (qh + ql) % G.Q;
-        W64(qword(pos), t);
-        if constexpr (TM) {
-            if (qb == ql && qb < (uint32_t)ABS_QP) {  // the buffer holds the whole queue: append there too
-#pragma unroll
-                for (int i = 0; i < ABS_QP; ++i)
-                    if ((uint32_t)i == qb) qbuf[i] = t;
-                qb++;
-            }
-        }
+        W64(qword(pos), t);  // (TM: the buffer stays a prefix of the queue; a pop past it reloads)
         if (ql == 0) qhv = t;
         ql++;
     }
     __device__ __forceinline__ void qpop() {
-        qh = (qh + 1) % G.Q;
-        ql--;
         if constexpr (TM) {
+            if (qb == 0) qfill();
+            qh = (qh + 1) % G.Q;
+            ql--;
 #pragma unroll
             for (int i = 0; i + 1 < ABS_QP; ++i) qbuf[i] = qbuf[i + 1];
             qb--;
             if (qb == 0 && ql) qfill();
-            qhv = qbuf[0];
+            if (ql) qhv = qbuf[0];
         } else {
+            qh = (qh + 1) % G.Q;
+            ql--;
             if (ql) qhv = R64(qword(qh));
         }
     }
@@ -496,9 +492,13 @@ template <int NW, bool TM> struct AbsKey {
             }
         }
         // sendEvent in list order: the selector gets each (slot0 = e1, ts = currentTime)
+        for (uint32_t m = emit; m; m &= m - 1u) {
+            const uint32_t j = (uint32_t)__ffs(m) - 1u;
+            uint64_t q = 0;
 #pragma unroll
-        for (int j = 0; j < ABS_R; ++j) {
-            if ((emit >> j) & 1u) project(seq[j], t, a, listener, tk2, resBase, resEnd, resLeft);
+            for (int x = 0; x < ABS_R; ++x)
+                if ((uint32_t)x == j) q = seq[x];
+            project(q, t, a, listener, tk2, resBase, resEnd, resLeft);
         }
         remove(drop);
         if (now > waiting + t) lst = now + waiting;
@@ -607,6 +607,29 @@ template <int NW> __device__ void abs_gather(const GenArgs& a, const cGenProgram
     }
 }
 
+// event i of the key-sorted payload (pack.h Pay<W>): the batch position, the attribute words in attribute
+// order (= the window's word layout), the null bits when present, the timestamp offset from ts[0]
+template <int NW> __device__ __forceinline__ void abs_pay(const GenArgs& a, uint32_t i, int64_t tbase, AbsEv<NW>& ev) {
+    constexpr int MW = NW + 3;
+    const uint32_t st = a.b.payStride;
+    const gu32* p = gp(a.b.pay) + (size_t)i * st;
+    uint32_t x[MW];
+#pragma unroll
+    for (int q = 0; q < MW; ++q) x[q] = (uint32_t)q < st ? p[q] : 0u;
+    const uint32_t pos = x[0];
+#pragma unroll
+    for (int q = 0; q < NW; ++q) ev.w[q] = x[1 + q];
+    uint32_t toff = 0, nb = 0;
+#pragma unroll
+    for (int q = 1; q < MW; ++q) {
+        if ((uint32_t)q == st - 1) toff = x[q];
+        if (a.b.payNull && (uint32_t)q == st - 2) nb = x[q];
+    }
+    ev.nb = nb;
+    ev.ts = (int32_t)toff == SGD_TS_FAR ? gp(a.b.ts)[pos] : tbase + (int64_t)(int32_t)toff;
+    ev.seq = a.b.seq_base + pos;
+}
+
 // ---- batch: one lane per key walks its events of the key-sorted batch ----
 template <int NW> __device__ void abs_batch(const GenArgs& a) {
     const cGenProgram& G = *(cGenProgram*)a.G;
@@ -625,17 +648,22 @@ template <int NW> __device__ void abs_batch(const GenArgs& a) {
         walk = false;
     }
     unsigned long long ky = 0;
+    const int64_t tbase = a.b.pay ? gp(a.b.ts)[0] : 0;  // the payload's ts offsets are from the batch's first ts
     if (walk) {
         uint32_t i = b;
         for (; i < e; i++) {
             // at most n + 1 appends to the queue and one new partial per event: stop before an event that
             // could overflow the window or the queue (the general kernel continues from it)
             if (L.n + 1u > (uint32_t)ABS_R || L.ql + L.n + 1u > G.Q) break;
-            const uint32_t pos = a.b.sidx ? gp(a.b.sidx)[i] : i;
             AbsEv<NW> ev;
-            ev.ts = gp(a.b.ts)[pos];
-            ev.seq = a.b.seq_base + pos;
-            abs_gather<NW>(a, G, pos, ev);
+            if (a.b.pay) {
+                abs_pay<NW>(a, i, tbase, ev);
+            } else {
+                const uint32_t pos = a.b.sidx ? gp(a.b.sidx)[i] : i;
+                ev.ts = gp(a.b.ts)[pos];
+                ev.seq = a.b.seq_base + pos;
+                abs_gather<NW>(a, G, pos, ev);
+            }
             L.event(ev);
         }
         L.store();

@@ -153,9 +153,17 @@ struct GenBatch {
     const int64_t* ts;
     const void* col[GEN_MAXA];
     const uint8_t* nul[GEN_MAXA];
-    const uint32_t* sidx;      // key-sorted batch positions
+    const uint32_t* sidx;      // key-sorted batch positions: sorted element i's at sidx[i * sidxStride]
     const uint32_t* seg_begin; // [K]
     const uint32_t* seg_end;
+    // the key-sorted payload (pack.h Pay<W>: batch position, the attribute words in attribute order, the
+    // null bits when payNull, the ts offset from ts[0] or SGD_TS_FAR), or NULL: then the kernels read the
+    // columns at sidx positions
+    const uint32_t* pay;
+    uint32_t payStride;        // words per element (W + 2)
+    uint32_t payNull;
+    uint32_t sidxStride;       // 0 = 1
+    uint32_t pad;
 };
 
 struct GenOut {

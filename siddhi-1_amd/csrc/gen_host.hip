@@ -24,6 +24,7 @@
 #include "../../include/siddhi_gpu.h"
 #include "../../include/siddhi_gpu_ir.h"
 #include "gen_engine.h"
+#include "pack.h"
 #include "gen_host.h"
 #include "pinned.h"
 #include "state_doc.h"
@@ -655,6 +656,9 @@ struct GenEngine {
     // keys the register-window kernels (abs_kernels.hip) hand to the general kernels
     uint32_t *fb_list = nullptr, *fb_start = nullptr;
     unsigned long long* fb_n = nullptr;
+    uint32_t* pay = nullptr;   // the key-sorted payload of the register-window kernel (pack.h Pay<W>)
+    void* paysort_tmp = nullptr;
+    size_t paysort_tmp_bytes = 0;
     // timer matches ordered through the due keys (keyorder: partitioned, playback, one listener)
     bool keyorder = false;
     uint32_t *rel = nullptr, *srel = nullptr, *skid = nullptr, *kc = nullptr, *koff_s = nullptr, *koff = nullptr;
@@ -840,6 +844,14 @@ GenEngine* gen_create(const uint32_t* ir, size_t nw, const sg_config& cfg, hipSt
             e->fb_list = e->dalloc<uint32_t>(K);
             e->fb_start = e->dalloc<uint32_t>(K);
             e->fb_n = e->dalloc<unsigned long long>(1);
+            e->pay = e->dalloc<uint32_t>(B * 6);  // Pay<4>: 6 words
+            PackSrc ps{};
+            for (int w = 1; w <= 4; w++) {
+                size_t tb = 0;
+                GH_OK(sgd_sort_payload(w, nullptr, tb, e->b_key, e->skeys, ps, nullptr, (uint32_t)B, 32, stream));
+                e->paysort_tmp_bytes = std::max(e->paysort_tmp_bytes, tb);
+            }
+            e->paysort_tmp = e->dalloc<uint8_t>(e->paysort_tmp_bytes);
         }
         e->d_args = e->dalloc<GenArgs>(GEN_ARG_SLOTS);
         GH_OK(hipHostMalloc((void**)&e->h_args, sizeof(GenArgs) * GEN_ARG_SLOTS, hipHostMallocDefault));
@@ -982,12 +994,54 @@ int gen_push(GenEngine* e, const sg_batch* b, std::string& msg) {
         hipEvent_t g0 = e->timing ? e->ev() : nullptr;
         uint32_t bits = 1;  // SG_CFG_NULL_KEYS: one value more than the key range (SG_KEY_NULL sorts last)
         while (bits < 32 && (1ull << bits) < (uint64_t)e->K + (e->null_keys ? 1u : 0u)) bits++;
-        size_t tmp = e->sort_tmp_bytes;
-        GH_OK(rocprim::radix_sort_pairs(e->sort_tmp, tmp, keys, e->skeys, e->iota, e->sidx, n, 0, bits, e->stream));
+        // the register-window kernel's grouping carries the events' words through the sort (gathered in
+        // arrival order in the first pass, so each key's events end up contiguous, instead of a random
+        // gather per event in the walk); other engines sort batch positions
+        PackSrc ps{};
+        uint32_t W = 0;
+        bool nul = false;
+        if (abs_on(e)) {
+            const int st = (int)b->stream;
+            for (int c = 0; c < G.nattr[st] && W <= 4; c++) {
+                const int t = G.attrType[st][c];
+                const void* col = a.b.col[c];
+                if (t == SG_T_LONG || t == SG_T_DOUBLE) {
+                    if (W + 2 > 4) { W = 5; break; }
+                    ps.p[W] = col; ps.kind[W++] = 1;
+                    ps.p[W] = col; ps.kind[W++] = 2;
+                } else {
+                    if (W + 1 > 4) { W = 5; break; }
+                    ps.p[W] = col;
+                    ps.kind[W++] = t == SG_T_BOOL ? 3 : 0;
+                }
+                if (a.b.nul[c]) {
+                    nul = true;
+                    if (c < SGD_MAX_EVCOLS) ps.nul[c] = a.b.nul[c];
+                    else W = 5;
+                }
+            }
+            if (nul && W <= 4) {
+                if (W + 1 > 4) W = 5;
+                else { ps.p[W] = nullptr; ps.kind[W++] = 4; }
+            }
+            ps.ts = a.b.ts;
+        }
+        if (abs_on(e) && W >= 1 && W <= 4) {
+            size_t tmp = e->paysort_tmp_bytes;
+            GH_OK(sgd_sort_payload((int)W, e->paysort_tmp, tmp, keys, e->skeys, ps, e->pay, n, bits, e->stream));
+            a.b.pay = e->pay;
+            a.b.payStride = W + 2;
+            a.b.payNull = nul ? 1u : 0u;
+            a.b.sidx = e->pay;  // (the general kernel over handed-over keys reads the positions from it)
+            a.b.sidxStride = W + 2;
+        } else {
+            size_t tmp = e->sort_tmp_bytes;
+            GH_OK(rocprim::radix_sort_pairs(e->sort_tmp, tmp, keys, e->skeys, e->iota, e->sidx, n, 0, bits, e->stream));
+            a.b.sidx = e->sidx;
+        }
         hipLaunchKernelGGL(k_gen_bounds, dim3((n + 255) / 256), dim3(256), 0, e->stream, e->skeys, n, e->K,
                            e->null_keys, e->seg_begin, e->seg_end, e->err);
         if (g0) e->spans.push_back({g0, e->ev(), 0});
-        a.b.sidx = e->sidx;
     } else {
         GH_OK(hipMemcpyAsync(e->seg_end, &n, 4, hipMemcpyHostToDevice, e->stream));
         GH_OK(hipStreamSynchronize(e->stream));  // &n is a stack value

@@ -1227,8 +1227,9 @@ extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per
             if (r.n == 0) i = e;
         }
         if (i < e) {
-            const uint32_t pos = a.b.sidx ? gp(a.b.sidx)[i] : i;
-            const uint32_t nxt = (i + 1 < e) ? (a.b.sidx ? gp(a.b.sidx)[i + 1] : i + 1) : 0xffffffffu;
+            const size_t ss = a.b.sidxStride ? a.b.sidxStride : 1u;
+            const uint32_t pos = a.b.sidx ? gp(a.b.sidx)[i * ss] : i;
+            const uint32_t nxt = (i + 1 < e) ? (a.b.sidx ? gp(a.b.sidx)[(i + 1) * ss] : i + 1) : 0xffffffffu;
             L.processEvent(r, pos, nxt != pos + 1);
             i++;
         }

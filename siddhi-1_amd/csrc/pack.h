@@ -59,3 +59,8 @@ template <int W> struct PackFn {
         return o;
     }
 };
+
+// the key-sorted payload grouping (sg_engine.hip): radix sort of the key ids carrying Pay<W> (W = 1..4)
+// gathered from the SoA columns by PackFn in the first pass; tmp == nullptr queries tmp_bytes
+hipError_t sgd_sort_payload(int W, void* tmp, size_t& tmp_bytes, const uint32_t* keys, uint32_t* skeys,
+                            const PackSrc& src, void* out, uint32_t n, uint32_t bits, hipStream_t stream);

@@ -105,6 +105,9 @@ size_t type_size(uint32_t t) {
 }
 
 
+
+}  // namespace
+
 // 12-B payloads (one filter column): onesweep with 10-bit digits, so 2^11..2^20 keys sort in two
 // passes over the data instead of three (rocPRIM's gfx950 default for this pair size is 8 bits);
 // 1024 x 16 items per block measured fastest for 2^24 events (tools/sweep/sort_sweep12.hip: 0.460 ms
@@ -127,7 +130,7 @@ hipError_t sort_payload(void* tmp, size_t& tmp_bytes, const uint32_t* keys, uint
 }
 
 
-hipError_t sort_payload_w(int W, void* tmp, size_t& tmp_bytes, const uint32_t* keys, uint32_t* skeys,
+hipError_t sgd_sort_payload(int W, void* tmp, size_t& tmp_bytes, const uint32_t* keys, uint32_t* skeys,
                           const PackSrc& src, void* out, uint32_t n, uint32_t bits, hipStream_t stream) {
     switch (W) {
     case 1: return sort_payload<1>(tmp, tmp_bytes, keys, skeys, src, out, n, bits, stream);
@@ -137,7 +140,6 @@ hipError_t sort_payload_w(int W, void* tmp, size_t& tmp_bytes, const uint32_t* k
     }
 }
 
-}  // namespace
 
 struct sg_engine {
     int device = 0;
@@ -562,7 +564,7 @@ void allocate(sg_engine* e) {
         size_t tb = 0;
         PackSrc ps{};
         for (uint32_t bits : {20u, 32u}) {
-            HIP_OK(sort_payload_w(W, nullptr, tb, e->slots[0].b_key, e->slots[0].skeys, ps, nullptr, (uint32_t)B, bits,
+            HIP_OK(sgd_sort_payload(W, nullptr, tb, e->slots[0].b_key, e->slots[0].skeys, ps, nullptr, (uint32_t)B, bits,
                                   e->stream));
             e->sort_tmp_bytes = std::max(e->sort_tmp_bytes, tb);
         }
@@ -885,7 +887,7 @@ int push(sg_engine* e, const sg_batch* b) {
                 HIP_OK(sgd_group_tiles(ga, ps, (int)wi, gs));
                 goto grouped;
             }
-            HIP_OK(sort_payload_w((int)wi, e->sort_tmp, tmp, keys, sl.skeys, ps, sl.pay, n, e->sort_bits, gs));
+            HIP_OK(sgd_sort_payload((int)wi, e->sort_tmp, tmp, keys, sl.skeys, ps, sl.pay, n, e->sort_bits, gs));
         } else {
             HIP_OK(rocprim::radix_sort_pairs(e->sort_tmp, tmp, keys, sl.skeys, e->iota, sl.sidx, n, 0, e->sort_bits,
                                              gs));
