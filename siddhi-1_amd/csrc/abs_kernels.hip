@@ -473,8 +473,7 @@ template <int NW, bool TM> struct AbsKey {
     }
 
     // AbsentStreamPreStateProcessor.process for the TIMER event at currentTime = t (the clock is `now`)
-    __device__ __forceinline__ void timer(int64_t t, int64_t now, const GenArgs& a, uint32_t listener, int64_t tk2,
-                          unsigned long long& resBase, unsigned long long& resEnd, uint32_t& resLeft) {
+    __device__ __forceinline__ void timer(int64_t t, int64_t now, const GenArgs& a) {
         promote();  // this.updateState()
         const int64_t waiting = G.pre[G.absP1].waiting;
         uint32_t drop = 0, emit = 0;
@@ -498,7 +497,7 @@ template <int NW, bool TM> struct AbsKey {
 #pragma unroll
             for (int x = 0; x < ABS_R; ++x)
                 if ((uint32_t)x == j) q = seq[x];
-            project(q, t, a, listener, tk2, resBase, resEnd, resLeft);
+            project(q, t, a);
         }
         remove(drop);
         if (now > waiting + t) lst = now + waiting;
@@ -508,42 +507,19 @@ template <int NW, bool TM> struct AbsKey {
         }
     }
 
-    // Lane::project for a timer match: [timer mark][rank][trigger seq][ts][key][chain lengths][seqs]
-    __device__ __forceinline__ void project(uint64_t e1seq, int64_t t, const GenArgs& a, uint32_t listener, int64_t tk2,
-                            unsigned long long& resBase, unsigned long long& resEnd, uint32_t& resLeft) {
-        if (resLeft == 0) {
-            resBase = atomicAdd(&a.o.raw_count[0], (unsigned long long)GEN_RESCHUNK);
-            resEnd = a.o.seg_cap;
-            resLeft = GEN_RESCHUNK;
-        }
-        const unsigned long long r = resBase++;
-        resLeft--;
+    // a timer match (QuerySelector input: slot0 = e1, ts = the fire time) staged at its rank in this key's
+    // sweep (gen_host.hip k_timer_scatter_abs writes it out in the due keys' head order): no atomics
+    __device__ __forceinline__ void project(uint64_t e1seq, int64_t t, const GenArgs& a) {
         const uint32_t rank = (uint32_t)matches++;
-        if (r >= resEnd) { err |= GERR_MATCHCAP; return; }
-        gu32* rec = gp(a.o.raw) + r * a.o.recWords;
-        rec[0] = 0xfffffffeu;
-        rec[1] = rank;  // its rank in this key's sweep (the matches are ordered through the sorted due keys)
-        rec[2] = 0xffffffffu;  // SG_TIMER_SEQ
-        rec[3] = 0xffffffffu;
-        rec[4] = (uint32_t)(uint64_t)t;
-        rec[5] = (uint32_t)((uint64_t)t >> 32);
-        rec[6] = k;
-        gu32* lens = rec + 7;
-        gu32* seqs = lens + G.nslots;
-        for (int s = 0; s < G.nslots; s++) {
-            lens[s] = s == slot0 ? 1u : 0u;
-            if (s == slot0) {
-                seqs[2 * (s * G.MC)] = (uint32_t)e1seq;
-                seqs[2 * (s * G.MC) + 1] = (uint32_t)(e1seq >> 32);
-            }
-        }
-        gp(a.o.tk1)[r] = listener;
-        gp(a.o.tk2)[r] = tk2;
-        gp(a.o.tk3)[r] = k;
+        if (rank >= (uint32_t)ABS_R) { err |= GERR_REF; return; }  // (a sweep emits only partials it loaded)
+        auto st = gp(a.t.tstage);
+        st[(size_t)rank * K + k] = e1seq;
+        st[(size_t)(ABS_R + rank) * K + k] = (unsigned long long)t;
     }
 };
 
 // the lanes' work counters, reduced over the wave (all 64 lanes call this): one atomic per wave
+// (the wave's row of a.o.wstats: every wave writes its row, k_gen_stats_reduce sums them afterwards)
 __device__ void abs_wave_stats(const GenArgs& a, unsigned long long sc, unsigned long long cr, unsigned long long ma,
                                unsigned long long ky, uint32_t er, unsigned long long fb) {
     for (int off = 32; off > 0; off >>= 1) {
@@ -556,11 +532,13 @@ __device__ void abs_wave_stats(const GenArgs& a, unsigned long long sc, unsigned
     }
     if ((threadIdx.x & 63) == 0) {
         if (er) atomicOr(a.o.err, er);
-        if (sc) atomicAdd(&a.o.stats[GST_SCANNED], sc);
-        if (cr) atomicAdd(&a.o.stats[GST_CREATED], cr);
-        if (ma) atomicAdd(&a.o.stats[GST_MATCHES], ma);
-        if (ky) atomicAdd(&a.o.stats[GST_KEYS], ky);
-        if (fb) atomicAdd(&a.o.stats[GST_SPILLS], fb);
+        auto w = gp(a.o.wstats) + (size_t)blockIdx.x * GST_N;
+        w[GST_SCANNED] = sc;
+        w[GST_CREATED] = cr;
+        w[GST_MATCHES] = ma;
+        w[GST_KEYS] = ky;
+        w[GST_LIVE0] = 0;
+        w[GST_SPILLS] = fb;
     }
 }
 
@@ -688,6 +666,7 @@ template <int NW> __device__ void abs_timers(const GenArgs& a) {
     unsigned long long sc = 0, cr = 0, ma = 0, nfb = 0;
     uint32_t er = 0;
     const uint32_t li = (uint32_t)G.absListener;
+    // (one lane per due slot: the grid covers every key, each wave at most one pass)
     for (uint64_t base = (uint64_t)blockIdx.x * 64u; base < nd; base += (uint64_t)gridDim.x * 64u) {
         const uint64_t di = base + threadIdx.x;
         const bool act = di < nd;
@@ -711,25 +690,15 @@ template <int NW> __device__ void abs_timers(const GenArgs& a) {
                 if (!L.load()) {
                     fb = true;
                 } else {
-                    unsigned long long resBase = 0, resEnd = 0;
-                    uint32_t resLeft = 0;
-                    const int64_t tk2 = L.qhv;
                     for (int guard = 0; guard < (1 << 20); guard++) {  // Scheduler.sendTimerEvents
                         if (L.ql == 0 || L.qhv > a.now) break;
                         const int64_t t = L.qhv;
                         L.qpop();
-                        L.timer(t, a.now, a, li, tk2, resBase, resEnd, resLeft);
+                        L.timer(t, a.now, a);
                     }
                     L.store();
                     gp(a.t.nd)[key] = L.deadline();
-                    if (a.t.kcnt) gp(a.t.kcnt)[key] = (uint32_t)L.matches;
-                    for (uint32_t x = 0; x < resLeft; x++) {  // unused reserved raw slots
-                        const unsigned long long rr = resBase + x;
-                        if (rr < resEnd) {
-                            gp(a.o.raw)[rr * a.o.recWords] = 0xffffffffu;
-                            gp(a.o.tk1)[rr] = 0xffffffffu;
-                        }
-                    }
+                    gp(a.t.kcnt)[key] = (uint32_t)L.matches | GEN_KCNT_STAGED;
                 }
             }
         }
@@ -740,9 +709,6 @@ template <int NW> __device__ void abs_timers(const GenArgs& a) {
         ma += L.matches;
         er |= L.err;
     }
-    unsigned long long mw = ma;
-    for (int off = 32; off > 0; off >>= 1) mw += __shfl_xor(mw, off, 64);
-    if ((threadIdx.x & 63) == 0 && mw) atomicAdd(a.o.nvalid, mw);
     abs_wave_stats(a, sc, cr, ma, 0ull, er, nfb);
 }
 

@@ -187,6 +187,9 @@ struct GenOut {
     uint32_t* tk3;
     unsigned long long* nvalid;      // timer matches emitted by a sweep
     unsigned long long* stats;
+    // per-wave counter rows [wave][GST_N] of the register-window kernels (summed by k_gen_stats_reduce:
+    // one device-wide atomic per wave and counter serialised ~16K atomics per counter at 2^20 keys)
+    unsigned long long* wstats;
     uint32_t* err;
     unsigned long long* prof;        // GENX_PROF builds: shader-clock cycles per walk phase (summed over waves)
 };
@@ -209,8 +212,13 @@ struct GenTimers {
     // keys sorted by head (gen_host.hip timer_order_keys) instead of a sort of the matches: the key of each
     // due slot and each due key's match count of the sweep (records carry their rank within the key)
     uint32_t* dpair_kid;             // [K] key of due slot di, or NULL
-    uint32_t* kcnt;                  // [K] matches of the key at this sweep, or NULL
+    uint32_t* kcnt;                  // [K] matches of the key at this sweep, or NULL; | GEN_KCNT_STAGED when
+                                     //     k_abs_timers left them in tstage (not in the raw records)
+    // k_abs_timers: a key's (e1 seq, fire time) per match of the sweep, rank-major ([rank][K] seqs, then
+    // [rank][K] times): at most ABS_R per key (a sweep only emits partials that were live at its start)
+    unsigned long long* tstage;
 };
+#define GEN_KCNT_STAGED 0x80000000u
 
 struct GenArgs {
     const GenProgram* G;

@@ -578,10 +578,56 @@ __global__ void k_timer_collapse(const uint32_t* __restrict__ srel, uint64_t n, 
     if (j == 0 || j >= n || srel[j] == 0u) return;
     if (srel[j] == srel[j - 1]) atomicOr(err, (uint32_t)GERR_COLLAPSE);
 }
+__global__ void k_timer_collapse64(const unsigned long long* __restrict__ skey, uint64_t n, uint32_t* __restrict__ err) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j == 0 || j >= n || skey[j] == ~0ull) return;
+    if (skey[j] == skey[j - 1]) atomicOr(err, (uint32_t)GERR_COLLAPSE);
+}
 __global__ void k_timer_cnt(const uint32_t* __restrict__ skid, uint64_t n, const uint32_t* __restrict__ kcnt,
                             uint32_t* __restrict__ c) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j < n) c[j] = skid[j] == GEN_PAIR_NONE ? 0u : kcnt[skid[j]];
+    if (j < n) c[j] = skid[j] == GEN_PAIR_NONE ? 0u : (kcnt[skid[j]] & ~GEN_KCNT_STAGED);
+}
+// the matches k_abs_timers staged per key, to count + (the key's offset in head order) + rank
+__global__ void k_timer_scatter_abs(const uint32_t* __restrict__ skid, uint64_t n, const uint32_t* __restrict__ kcnt,
+                                    const uint32_t* __restrict__ koff, const unsigned long long* __restrict__ tstage,
+                                    uint32_t K, uint32_t slot0, OutBufs o) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n || skid[j] == GEN_PAIR_NONE) return;
+    const uint32_t key = skid[j];
+    const uint32_t c = kcnt[key];
+    if (!(c & GEN_KCNT_STAGED)) return;
+    const uint64_t base = *o.count + koff[key];
+    for (uint32_t r = 0; r < (c & ~GEN_KCNT_STAGED); r++) {
+        const uint64_t d = base + r;
+        if (d >= o.cap) { atomicOr(o.err, (uint32_t)GERR_MATCHCAP); return; }
+        o.trig[d] = SG_TIMER_SEQ;
+        o.ts[d] = (int64_t)tstage[(size_t)(ABS_R + r) * K + key];
+        o.key[d] = key;
+        for (uint32_t s = 0; s < o.nslots; s++) {
+            o.len[d * o.nslots + s] = s == slot0 ? 1u : 0u;
+            for (uint32_t q = 0; q < o.MC; q++)
+                o.slot[(d * o.nslots + s) * o.MC + q] = (s == slot0 && q == 0) ? tstage[(size_t)r * K + key] : SG_NULL_SEQ;
+        }
+    }
+}
+__global__ void k_timer_bump(unsigned long long* count, const uint32_t* c, const uint32_t* off, uint64_t n) {
+    *count += (unsigned long long)off[n - 1] + c[n - 1];
+}
+// the register-window kernels' per-wave counter rows into the engine counters (one block per counter)
+__global__ void __launch_bounds__(256) k_gen_stats_reduce(const unsigned long long* __restrict__ w, uint32_t rows,
+                                                          unsigned long long* __restrict__ stats) {
+    __shared__ unsigned long long part[4];
+    const uint32_t c = blockIdx.x;
+    unsigned long long x = 0;
+    for (uint32_t r = threadIdx.x; r < rows; r += blockDim.x) x += w[(size_t)r * GST_N + c];
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x / 64] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned long long t = part[0] + part[1] + part[2] + part[3];
+        if (t) stats[c] += t;
+    }
 }
 __global__ void k_timer_off(const uint32_t* __restrict__ skid, uint64_t n, const uint32_t* __restrict__ off,
                             uint32_t* __restrict__ koff) {
@@ -657,6 +703,8 @@ struct GenEngine {
     uint32_t *fb_list = nullptr, *fb_start = nullptr;
     unsigned long long* fb_n = nullptr;
     uint32_t* pay = nullptr;   // the key-sorted payload of the register-window kernel (pack.h Pay<W>)
+    unsigned long long* wstats = nullptr;  // its per-wave counter rows
+    unsigned long long* tstage = nullptr;  // its staged timer matches
     void* paysort_tmp = nullptr;
     size_t paysort_tmp_bytes = 0;
     // timer matches ordered through the due keys (keyorder: partitioned, playback, one listener)
@@ -733,6 +781,7 @@ struct GenEngine {
         a.o.tk3 = tk3;
         a.o.nvalid = nvalid;
         a.o.stats = stats;
+        a.o.wstats = wstats;
         a.o.err = err;
         a.o.prof = prof;
         a.t = tm;
@@ -845,6 +894,11 @@ GenEngine* gen_create(const uint32_t* ir, size_t nw, const sg_config& cfg, hipSt
             e->fb_start = e->dalloc<uint32_t>(K);
             e->fb_n = e->dalloc<unsigned long long>(1);
             e->pay = e->dalloc<uint32_t>(B * 6);  // Pay<4>: 6 words
+            e->wstats = e->dalloc<unsigned long long>((size_t)((K + 63) / 64) * GST_N);
+            if (G.playback && G.partitioned && G.nStartup == 1) {
+                e->tstage = e->dalloc<unsigned long long>((size_t)K * ABS_R * 2);
+                e->tm.tstage = e->tstage;
+            }
             PackSrc ps{};
             for (int w = 1; w <= 4; w++) {
                 size_t tb = 0;
@@ -908,7 +962,9 @@ static uint32_t gen_kpl(uint32_t K) {
 
 // the register-window kernels of abs_kernels.hip run this query (the shape, and no device projection: the
 // selector items are evaluated by the general kernel's projectSelect)
-static bool abs_on(const GenEngine* e) { return e->host.absOk && e->host.projN == 0 && e->fb_list; }
+static bool abs_on(const GenEngine* e) {
+    return e->host.absOk && e->host.projN == 0 && e->fb_list && e->tstage && e->keyorder;
+}
 
 static void launch_gen(GenEngine* e, GenArgs a, int which) {
     const uint32_t blocks = (e->K + 63) / 64;
@@ -924,9 +980,12 @@ static void launch_gen(GenEngine* e, GenArgs a, int which) {
         hipLaunchKernelGGL(k_gen_timers, dim3(fb ? GEN_FB_BLOCKS : e->host.partitioned ? std::min(blocks, GEN_TIMER_BLOCKS) : 1u),
                            dim3(64), 0, e->stream, ap);
     else if (which == GEN_L_DEADLINES) hipLaunchKernelGGL(k_gen_deadlines, dim3(blocks), dim3(64), 0, e->stream, ap);
-    else if (which == GEN_L_ABS_BATCH) hipLaunchKernelGGL(kAbsBatch[e->host.absNW], dim3(blocks), dim3(64), 0, e->stream, ap);
-    else if (which == GEN_L_ABS_TIMERS)  // one lane per possible due key (the count is on the device)
-        hipLaunchKernelGGL(kAbsTimers[e->host.absNW], dim3(blocks), dim3(64), 0, e->stream, ap);
+    else if (which == GEN_L_ABS_BATCH || which == GEN_L_ABS_TIMERS) {
+        // one lane per key / possible due slot (the due count is on the device); then the waves' counter rows
+        hipLaunchKernelGGL(which == GEN_L_ABS_BATCH ? kAbsBatch[e->host.absNW] : kAbsTimers[e->host.absNW], dim3(blocks),
+                           dim3(64), 0, e->stream, ap);
+        hipLaunchKernelGGL(k_gen_stats_reduce, dim3(GST_N), dim3(256), 0, e->stream, e->wstats, blocks, e->stats);
+    }
     else hipLaunchKernelGGL(k_gen_batch, dim3(fb ? GEN_FB_BLOCKS : (e->K + 64u * a.kpl - 1) / (64u * a.kpl)), dim3(64), 0,
                             e->stream, ap);
     GH_OK(hipGetLastError());
@@ -1139,33 +1198,42 @@ int gen_advance(GenEngine* e, int64_t t, std::string& msg) {
     if (e->keyorder) GH_OK(hipMemcpyAsync(kctr, e->ctr, 16, hipMemcpyDeviceToHost, e->stream));
     GH_OK(hipStreamSynchronize(e->stream));
     bool check = false;
-    if (e->keyorder && !kctr[1] && ndue >= 1) {
+    if (e->keyorder && ndue >= 1) {
         // one listener: the due keys sorted by queue head (TreeMultimap order of the listener's collection,
         // Scheduler.java:78-99) give the output order of their timer matches (each key's in emission
-        // order) and, where two heads are equal, the A.10 collapse below
+        // order) and, where two heads are equal, the A.10 collapse below.  Sort keys: 32-bit lags from the
+        // advance target when they fit (descending), else the 64-bit heads.
         const size_t n = (size_t)ndue;
-        int bits = 1;
-        while (bits < 32 && (kctr[0] >> bits) != 0) bits++;
-        size_t tmp = e->ksort_tmp_bytes;
-        GH_OK(rocprim::radix_sort_pairs_desc(e->ksort_tmp, tmp, e->rel, e->srel, e->tm.dpair_kid, e->skid, n, 0, bits,
-                                             e->stream));
         const dim3 g((unsigned)((n + 255) / 256));
-        if (n >= 2) {
-            hipLaunchKernelGGL(k_timer_collapse, g, dim3(256), 0, e->stream, e->srel, (uint64_t)n, e->err);
-            check = true;
+        if (!kctr[1]) {
+            int bits = 1;
+            while (bits < 32 && (kctr[0] >> bits) != 0) bits++;
+            size_t tmp = e->ksort_tmp_bytes;
+            GH_OK(rocprim::radix_sort_pairs_desc(e->ksort_tmp, tmp, e->rel, e->srel, e->tm.dpair_kid, e->skid, n, 0,
+                                                 bits, e->stream));
+            if (n >= 2) hipLaunchKernelGGL(k_timer_collapse, g, dim3(256), 0, e->stream, e->srel, (uint64_t)n, e->err);
+        } else {
+            size_t tmpb = e->psort_tmp_bytes;
+            GH_OK(rocprim::radix_sort_pairs(e->psort_tmp, tmpb, e->tm.dpair_key, e->pair_key_s, e->tm.dpair_kid, e->skid,
+                                            n, 0, 64, e->stream));
+            if (n >= 2) hipLaunchKernelGGL(k_timer_collapse64, g, dim3(256), 0, e->stream, e->pair_key_s, (uint64_t)n,
+                                           e->err);
         }
-        if (nr > 0) {
-            hipLaunchKernelGGL(k_timer_cnt, g, dim3(256), 0, e->stream, e->skid, (uint64_t)n, e->tm.kcnt, e->kc);
-            size_t st = e->kscan_tmp_bytes;
-            GH_OK(rocprim::exclusive_scan(e->kscan_tmp, st, e->kc, e->koff_s, 0u, n, rocprim::plus<uint32_t>(), e->stream));
-            hipLaunchKernelGGL(k_timer_off, g, dim3(256), 0, e->stream, e->skid, (uint64_t)n, e->koff_s, e->koff);
+        check = n >= 2;
+        hipLaunchKernelGGL(k_timer_cnt, g, dim3(256), 0, e->stream, e->skid, (uint64_t)n, e->tm.kcnt, e->kc);
+        size_t st = e->kscan_tmp_bytes;
+        GH_OK(rocprim::exclusive_scan(e->kscan_tmp, st, e->kc, e->koff_s, 0u, n, rocprim::plus<uint32_t>(), e->stream));
+        hipLaunchKernelGGL(k_timer_off, g, dim3(256), 0, e->stream, e->skid, (uint64_t)n, e->koff_s, e->koff);
+        if (nr > 0) {  // matches of the general kernels (raw records)
             const size_t m = (size_t)std::min<unsigned long long>(nr, e->rawCap);
             hipLaunchKernelGGL(k_timer_scatter, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, e->stream, e->raw,
                                e->raw_count, e->koff, e->out);
-            hipLaunchKernelGGL(k_gen_bump, dim3(1), dim3(1), 0, e->stream, e->out.count, e->t_cnt, e->t_off, 1u,
-                               (const unsigned long long*)e->nvalid);
-            GH_OK(hipGetLastError());
         }
+        if (e->tstage)  // matches k_abs_timers staged
+            hipLaunchKernelGGL(k_timer_scatter_abs, g, dim3(256), 0, e->stream, e->skid, (uint64_t)n, e->tm.kcnt,
+                               e->koff, e->tstage, e->K, (uint32_t)G.pre[G.absP0].stateId, e->out);
+        hipLaunchKernelGGL(k_timer_bump, dim3(1), dim3(1), 0, e->stream, e->out.count, e->kc, e->koff_s, (uint64_t)n);
+        GH_OK(hipGetLastError());
         nr = 0;  // ordered
     } else if (G.partitioned && G.playback && ndue * (uint64_t)G.nStartup >= 2) {
         // the reference's listener collects the due (time, key) states in a
