@@ -547,29 +547,80 @@ __global__ void k_gen_live(const GenProgram* G, const uint32_t* S, uint32_t K, u
 }
 
 // ---- timer matches ordered through the due keys (one listener: GenTimers.kcnt / dpair_kid) ----
-// sort key of due slot di: 1 + (T - head) (descending = head ascending; 0 = not due, sorted last); a lag
-// that does not fit 32 bits sets *ovf (the host then takes the 64-bit pair sort)
-__global__ void __launch_bounds__(256) k_timer_rel(const unsigned long long* __restrict__ dkey,
-                                                   const unsigned long long* __restrict__ ndue, int64_t T,
-                                                   uint32_t* __restrict__ rel, unsigned long long* __restrict__ ctr) {
-    __shared__ unsigned long long bmax[4];
-    const uint64_t di = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    unsigned long long r = 0;
-    if (di < *ndue) {
-        const unsigned long long h = dkey[di];
-        if (h != ~0ull) {
-            const int64_t head = (int64_t)(h ^ (1ull << 63));
-            r = (unsigned long long)(T - head) + 1ull;
-            if (T < head || r >= 0xffffffffull) { ctr[1] = 1ull; r = 0; }
+// ctr: [0] largest sort key, [1] a lag that does not fit 32 bits, [2] keys with matches, [3] two due keys
+// share a head time (the reference's collapse quirk)
+#define GEN_TPREP_BLOCK 1024
+__device__ __forceinline__ uint64_t gen_hmix(uint64_t x) {
+    x ^= x >> 33;
+    x *= 0xff51afd7ed558ccdull;
+    x ^= x >> 33;
+    return x;
+}
+// per due slot: the head into an exact hash set (a second equal head = the A.10 collapse), and the keys
+// that emitted matches into a compact list with their sort key 1 + (T - head) (descending = head order;
+// the 64-bit head too, for lags beyond 32 bits).  One atomic per block for the list.
+__global__ void __launch_bounds__(GEN_TPREP_BLOCK) k_timer_prep(
+        const unsigned long long* __restrict__ dkey, const uint32_t* __restrict__ dkid,
+        const unsigned long long* __restrict__ ndue, int64_t T, const uint32_t* __restrict__ kcnt,
+        unsigned long long* __restrict__ ht, uint64_t htmask, uint32_t* __restrict__ rel_c,
+        uint32_t* __restrict__ kid_c, unsigned long long* __restrict__ hkey_c, unsigned long long* __restrict__ ctr) {
+    constexpr uint32_t NW = GEN_TPREP_BLOCK / 64;
+    __shared__ uint32_t wcnt[NW];
+    __shared__ unsigned long long bbase, bmax[NW];
+    const int lane = threadIdx.x & 63;
+    const uint32_t wv = threadIdx.x / 64;
+    const uint64_t n = *ndue;
+    unsigned long long mx = 0;
+    for (uint64_t base = (uint64_t)blockIdx.x * GEN_TPREP_BLOCK; base < n; base += (uint64_t)gridDim.x * GEN_TPREP_BLOCK) {
+        const uint64_t di = base + threadIdx.x;
+        bool has = false;
+        uint32_t r32 = 0, kid = GEN_PAIR_NONE;
+        unsigned long long h = ~0ull;
+        if (di < n) {
+            h = dkey[di];
+            kid = dkid[di];
+            if (h != ~0ull && kid != GEN_PAIR_NONE) {
+                uint64_t p = gen_hmix(h) & htmask;
+                for (uint64_t probe = 0; probe <= htmask; probe++) {
+                    const unsigned long long prev = atomicCAS(&ht[p], ~0ull, h);
+                    if (prev == ~0ull) break;
+                    if (prev == h) { ctr[3] = 1ull; break; }
+                    p = (p + 1) & htmask;
+                }
+                const int64_t head = (int64_t)(h ^ (1ull << 63));
+                unsigned long long r = (unsigned long long)(T - head) + 1ull;
+                if (T < head || r >= 0xffffffffull) { ctr[1] = 1ull; r = 0; }
+                r32 = (uint32_t)r;
+                mx = max(mx, r);
+                has = (kcnt[kid] & ~GEN_KCNT_STAGED) != 0u;
+            }
         }
-        rel[di] = (uint32_t)r;
+        const unsigned long long m = __ballot(has);
+        if (lane == 0) wcnt[wv] = (uint32_t)__popcll(m);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t t = 0;
+            for (uint32_t w = 0; w < NW; w++) t += wcnt[w];
+            bbase = t ? atomicAdd(&ctr[2], (unsigned long long)t) : 0ull;
+        }
+        __syncthreads();
+        if (has) {
+            uint32_t before = 0;
+            for (uint32_t w = 0; w < wv; w++) before += wcnt[w];
+            const unsigned long long o = bbase + before + __popcll(m & ((1ull << lane) - 1ull));
+            rel_c[o] = r32;
+            kid_c[o] = kid;
+            hkey_c[o] = h;
+        }
+        __syncthreads();
     }
-    for (int off = 32; off > 0; off >>= 1) r = max(r, (unsigned long long)__shfl_xor(r, off, 64));
-    if ((threadIdx.x & 63) == 0) bmax[threadIdx.x / 64] = r;
+    for (int off = 32; off > 0; off >>= 1) mx = max(mx, (unsigned long long)__shfl_xor(mx, off, 64));
+    if (lane == 0) bmax[wv] = mx;
     __syncthreads();
     if (threadIdx.x == 0) {
-        const unsigned long long m = max(max(bmax[0], bmax[1]), max(bmax[2], bmax[3]));
-        if (m) atomicMax(&ctr[0], m);
+        unsigned long long t = 0;
+        for (uint32_t w = 0; w < NW; w++) t = max(t, bmax[w]);
+        if (t) atomicMax(&ctr[0], t);
     }
 }
 // two due keys sharing a head time (adjacent after the sort): the reference's collapse quirk (A.10)
@@ -644,6 +695,10 @@ __global__ void k_timer_scatter(const uint32_t* raw, const unsigned long long* r
     write_out(o, *o.count + koff[rec[6]] + rec[1], rec, true);
 }
 
+// the due keys' sort: onesweep at every size (rocPRIM's default merge-sorts up to 2^20 items: ~20 passes)
+using KeySortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                                 rocprim::default_config, 4096>;
+
 struct TimerLess {
     const uint32_t* k1;
     const int64_t* k2;
@@ -710,7 +765,11 @@ struct GenEngine {
     // timer matches ordered through the due keys (keyorder: partitioned, playback, one listener)
     bool keyorder = false;
     uint32_t *rel = nullptr, *srel = nullptr, *skid = nullptr, *kc = nullptr, *koff_s = nullptr, *koff = nullptr;
-    unsigned long long* ctr = nullptr;  // [0] max sort key, [1] lag overflow
+    uint32_t* kid_c = nullptr;
+    unsigned long long *hkey_c = nullptr, *hkey_s = nullptr;
+    unsigned long long* ht = nullptr;   // the due heads' hash set (A.10 check), 2^k >= 2 K slots
+    uint64_t htmask = 0;
+    unsigned long long* ctr = nullptr;  // k_timer_prep's counters
     void* ksort_tmp = nullptr;
     size_t ksort_tmp_bytes = 0;
     void* kscan_tmp = nullptr;
@@ -878,9 +937,20 @@ GenEngine* gen_create(const uint32_t* ir, size_t nw, const sg_config& cfg, hipSt
                     e->kc = e->dalloc<uint32_t>(K);
                     e->koff_s = e->dalloc<uint32_t>(K);
                     e->koff = e->dalloc<uint32_t>(K);
-                    e->ctr = e->dalloc<unsigned long long>(2);
-                    GH_OK(rocprim::radix_sort_pairs_desc(nullptr, e->ksort_tmp_bytes, e->rel, e->srel, e->tm.dpair_kid,
-                                                         e->skid, (size_t)K, 0, 32, stream));
+                    e->ctr = e->dalloc<unsigned long long>(4);
+                    e->kid_c = e->dalloc<uint32_t>(K);
+                    e->hkey_c = e->dalloc<unsigned long long>(K);
+                    e->hkey_s = e->dalloc<unsigned long long>(K);
+                    uint64_t hs = 1024;
+                    while (hs < 2 * (uint64_t)K) hs <<= 1;
+                    e->ht = e->dalloc<unsigned long long>(hs);
+                    e->htmask = hs - 1;
+                    size_t t1 = 0, t2 = 0;
+                    GH_OK(rocprim::radix_sort_pairs_desc<KeySortConfig>(nullptr, t1, e->rel, e->srel, e->kid_c, e->skid,
+                                                                        (size_t)K, 0, 32, stream));
+                    GH_OK(rocprim::radix_sort_pairs<KeySortConfig>(nullptr, t2, e->hkey_c, e->hkey_s, e->kid_c, e->skid,
+                                                                   (size_t)K, 0, 64, stream));
+                    e->ksort_tmp_bytes = std::max(t1, t2);
                     e->ksort_tmp = e->dalloc<uint8_t>(e->ksort_tmp_bytes);
                     GH_OK(rocprim::exclusive_scan(nullptr, e->kscan_tmp_bytes, e->kc, e->koff_s, 0u, (size_t)K,
                                                   rocprim::plus<uint32_t>(), stream));
@@ -900,11 +970,12 @@ GenEngine* gen_create(const uint32_t* ir, size_t nw, const sg_config& cfg, hipSt
                 e->tm.tstage = e->tstage;
             }
             PackSrc ps{};
-            for (int w = 1; w <= 4; w++) {
-                size_t tb = 0;
-                GH_OK(sgd_sort_payload(w, nullptr, tb, e->b_key, e->skeys, ps, nullptr, (uint32_t)B, 32, stream));
-                e->paysort_tmp_bytes = std::max(e->paysort_tmp_bytes, tb);
-            }
+            for (int w = 1; w <= 4; w++)
+                for (uint32_t bq : {16u, 20u, 32u}) {  // (the configurations differ by key width)
+                    size_t tb = 0;
+                    GH_OK(sgd_sort_payload(w, nullptr, tb, e->b_key, e->skeys, ps, nullptr, (uint32_t)B, bq, stream));
+                    e->paysort_tmp_bytes = std::max(e->paysort_tmp_bytes, tb);
+                }
             e->paysort_tmp = e->dalloc<uint8_t>(e->paysort_tmp_bytes);
         }
         e->d_args = e->dalloc<GenArgs>(GEN_ARG_SLOTS);
@@ -1187,55 +1258,59 @@ int gen_advance(GenEngine* e, int64_t t, std::string& msg) {
     } else {
         launch_gen(e, a, GEN_L_TIMERS);
     }
-    if (e->keyorder) {  // the sort keys of the due slots (no host round trip: the count is on the device)
-        GH_OK(hipMemsetAsync(e->ctr, 0, 16, e->stream));
-        hipLaunchKernelGGL(k_timer_rel, dim3((e->K + 255) / 256), dim3(256), 0, e->stream, e->tm.dpair_key, e->tm.ndue,
-                           t, e->rel, e->ctr);
+    if (e->keyorder) {  // the A.10 check and the keys with matches, before the one host round trip
+        GH_OK(hipMemsetAsync(e->ctr, 0, 32, e->stream));
+        GH_OK(hipMemsetAsync(e->ht, 0xff, (e->htmask + 1) * 8, e->stream));
+        const uint32_t blocks = std::min<uint32_t>((e->K + GEN_TPREP_BLOCK - 1) / GEN_TPREP_BLOCK, 1024u);
+        hipLaunchKernelGGL(k_timer_prep, dim3(blocks), dim3(GEN_TPREP_BLOCK), 0, e->stream, e->tm.dpair_key,
+                           e->tm.dpair_kid, e->tm.ndue, t, e->tm.kcnt, e->ht, e->htmask, e->rel, e->kid_c, e->hkey_c,
+                           e->ctr);
     }
-    unsigned long long nr = 0, ndue = 0, kctr[2] = {0, 0};
+    unsigned long long nr = 0, ndue = 0, kctr[4] = {0, 0, 0, 0};
     GH_OK(hipMemcpyAsync(&nr, e->raw_count, 8, hipMemcpyDeviceToHost, e->stream));
     GH_OK(hipMemcpyAsync(&ndue, e->tm.ndue, 8, hipMemcpyDeviceToHost, e->stream));
-    if (e->keyorder) GH_OK(hipMemcpyAsync(kctr, e->ctr, 16, hipMemcpyDeviceToHost, e->stream));
+    if (e->keyorder) GH_OK(hipMemcpyAsync(kctr, e->ctr, 32, hipMemcpyDeviceToHost, e->stream));
     GH_OK(hipStreamSynchronize(e->stream));
     bool check = false;
-    if (e->keyorder && ndue >= 1) {
-        // one listener: the due keys sorted by queue head (TreeMultimap order of the listener's collection,
-        // Scheduler.java:78-99) give the output order of their timer matches (each key's in emission
-        // order) and, where two heads are equal, the A.10 collapse below.  Sort keys: 32-bit lags from the
-        // advance target when they fit (descending), else the 64-bit heads.
-        const size_t n = (size_t)ndue;
-        const dim3 g((unsigned)((n + 255) / 256));
-        if (!kctr[1]) {
-            int bits = 1;
-            while (bits < 32 && (kctr[0] >> bits) != 0) bits++;
-            size_t tmp = e->ksort_tmp_bytes;
-            GH_OK(rocprim::radix_sort_pairs_desc(e->ksort_tmp, tmp, e->rel, e->srel, e->tm.dpair_kid, e->skid, n, 0,
-                                                 bits, e->stream));
-            if (n >= 2) hipLaunchKernelGGL(k_timer_collapse, g, dim3(256), 0, e->stream, e->srel, (uint64_t)n, e->err);
-        } else {
-            size_t tmpb = e->psort_tmp_bytes;
-            GH_OK(rocprim::radix_sort_pairs(e->psort_tmp, tmpb, e->tm.dpair_key, e->pair_key_s, e->tm.dpair_kid, e->skid,
-                                            n, 0, 64, e->stream));
-            if (n >= 2) hipLaunchKernelGGL(k_timer_collapse64, g, dim3(256), 0, e->stream, e->pair_key_s, (uint64_t)n,
-                                           e->err);
+    bool collapse = false;
+    if (e->keyorder) {
+        // one listener: the keys that emitted sorted by queue head (TreeMultimap order of the listener's
+        // collection, Scheduler.java:78-99) give the output order of their timer matches (each key's in
+        // emission order).  Sort keys: 32-bit lags from the advance target when they fit (descending),
+        // else the 64-bit heads.
+        collapse = kctr[3] != 0;
+        const size_t n = (size_t)kctr[2];
+        if (n >= 1) {
+            const dim3 g((unsigned)((n + 255) / 256));
+            if (!kctr[1]) {
+                int bits = 1;
+                while (bits < 32 && (kctr[0] >> bits) != 0) bits++;
+                size_t tmp = e->ksort_tmp_bytes;
+                GH_OK(rocprim::radix_sort_pairs_desc<KeySortConfig>(e->ksort_tmp, tmp, e->rel, e->srel, e->kid_c, e->skid,
+                                                                    n, 0, bits, e->stream));
+            } else {
+                size_t tmp = e->ksort_tmp_bytes;
+                GH_OK(rocprim::radix_sort_pairs<KeySortConfig>(e->ksort_tmp, tmp, e->hkey_c, e->hkey_s, e->kid_c, e->skid,
+                                                               n, 0, 64, e->stream));
+            }
+            hipLaunchKernelGGL(k_timer_cnt, g, dim3(256), 0, e->stream, e->skid, (uint64_t)n, e->tm.kcnt, e->kc);
+            size_t st = e->kscan_tmp_bytes;
+            GH_OK(rocprim::exclusive_scan(e->kscan_tmp, st, e->kc, e->koff_s, 0u, n, rocprim::plus<uint32_t>(), e->stream));
+            hipLaunchKernelGGL(k_timer_off, g, dim3(256), 0, e->stream, e->skid, (uint64_t)n, e->koff_s, e->koff);
+            if (nr > 0) {  // matches of the general kernels (raw records)
+                const size_t m = (size_t)std::min<unsigned long long>(nr, e->rawCap);
+                hipLaunchKernelGGL(k_timer_scatter, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, e->stream, e->raw,
+                                   e->raw_count, e->koff, e->out);
+            }
+            if (e->tstage)  // matches k_abs_timers staged
+                hipLaunchKernelGGL(k_timer_scatter_abs, g, dim3(256), 0, e->stream, e->skid, (uint64_t)n, e->tm.kcnt,
+                                   e->koff, e->tstage, e->K, (uint32_t)G.pre[G.absP0].stateId, e->out);
+            hipLaunchKernelGGL(k_timer_bump, dim3(1), dim3(1), 0, e->stream, e->out.count, e->kc, e->koff_s, (uint64_t)n);
+            GH_OK(hipGetLastError());
         }
-        check = n >= 2;
-        hipLaunchKernelGGL(k_timer_cnt, g, dim3(256), 0, e->stream, e->skid, (uint64_t)n, e->tm.kcnt, e->kc);
-        size_t st = e->kscan_tmp_bytes;
-        GH_OK(rocprim::exclusive_scan(e->kscan_tmp, st, e->kc, e->koff_s, 0u, n, rocprim::plus<uint32_t>(), e->stream));
-        hipLaunchKernelGGL(k_timer_off, g, dim3(256), 0, e->stream, e->skid, (uint64_t)n, e->koff_s, e->koff);
-        if (nr > 0) {  // matches of the general kernels (raw records)
-            const size_t m = (size_t)std::min<unsigned long long>(nr, e->rawCap);
-            hipLaunchKernelGGL(k_timer_scatter, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, e->stream, e->raw,
-                               e->raw_count, e->koff, e->out);
-        }
-        if (e->tstage)  // matches k_abs_timers staged
-            hipLaunchKernelGGL(k_timer_scatter_abs, g, dim3(256), 0, e->stream, e->skid, (uint64_t)n, e->tm.kcnt,
-                               e->koff, e->tstage, e->K, (uint32_t)G.pre[G.absP0].stateId, e->out);
-        hipLaunchKernelGGL(k_timer_bump, dim3(1), dim3(1), 0, e->stream, e->out.count, e->kc, e->koff_s, (uint64_t)n);
-        GH_OK(hipGetLastError());
         nr = 0;  // ordered
-    } else if (G.partitioned && G.playback && ndue * (uint64_t)G.nStartup >= 2) {
+    }
+    if (!e->keyorder && G.partitioned && G.playback && ndue * (uint64_t)G.nStartup >= 2) {
         // the reference's listener collects the due (time, key) states in a
         // TreeMultimap whose value comparator is always 0 (Scheduler.java:78-89, 364-367), so of several
         // keys due at the same time only one (chosen by HashMap order) fires at this advance.  That
@@ -1264,6 +1339,11 @@ int gen_advance(GenEngine* e, int64_t t, std::string& msg) {
     }
     if (G.playback || !e->advanced || t > e->now) e->now = t;
     e->advanced = true;
+    if (collapse) {
+        msg = "two partition keys share a timer due time at one clock advance (reference Scheduler collapse "
+              "quirk, SURVEY A.10): input not supported";
+        return SG_ERR_UNSUPPORTED;
+    }
     if (check) {
         uint32_t err = 0;
         GH_OK(hipMemcpyAsync(&err, e->err, 4, hipMemcpyDeviceToHost, e->stream));

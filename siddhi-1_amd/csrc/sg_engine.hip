@@ -117,6 +117,13 @@ using Pay16Config = rocprim::radix_sort_config<
     rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 16>, rocprim::kernel_config<1024, 16>, 10,
                                         rocprim::block_radix_rank_algorithm::match>>;
 
+// wider payloads (16-24 B): rocPRIM's default onesweep for them takes 4-bit digits (5 passes over 2^20 keys);
+// 10-bit digits with 512 x 8 items per block keep the block's LDS within 160 KB and sort 20 key bits in 2
+using PayWideConfig = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<512, 8>, rocprim::kernel_config<512, 8>, 10,
+                                        rocprim::block_radix_rank_algorithm::match>>;
+
 template <int W>
 hipError_t sort_payload(void* tmp, size_t& tmp_bytes, const uint32_t* keys, uint32_t* skeys, const PackSrc& src,
                         void* out, uint32_t n, uint32_t bits, hipStream_t stream) {
@@ -125,6 +132,10 @@ hipError_t sort_payload(void* tmp, size_t& tmp_bytes, const uint32_t* keys, uint
         if (bits > 16 && bits <= 20)
             return rocprim::radix_sort_pairs<Pay16Config>(tmp, tmp_bytes, keys, skeys, it, (Pay<W>*)out, n, 0u, bits,
                                                            stream);
+    } else {
+        if (bits > 10 && bits <= 20)
+            return rocprim::radix_sort_pairs<PayWideConfig>(tmp, tmp_bytes, keys, skeys, it, (Pay<W>*)out, n, 0u, bits,
+                                                             stream);
     }
     return rocprim::radix_sort_pairs(tmp, tmp_bytes, keys, skeys, it, (Pay<W>*)out, n, 0u, bits, stream);
 }
