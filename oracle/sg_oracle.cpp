@@ -1671,7 +1671,8 @@ int sgo_advance_time(sgo_engine* h, int64_t now) {
 
 int sgo_poll_matches(sgo_engine* h, uint32_t mem, sg_match_batch* out) {
     if (!h || !out) return fail(SG_ERR_INVALID, "null argument");
-    if (mem != SG_MEM_HOST) return fail(SG_ERR_INVALID, "oracle returns host memory only");
+    // (SG_POLL_READY: every batch of the oracle is complete when its push returns)
+    if ((mem & ~SG_POLL_READY) != SG_MEM_HOST) return fail(SG_ERR_INVALID, "oracle returns host memory only");
     Engine& e = h->e;
     uint32_t maxc = 1;
     for (auto& m : e.matches)

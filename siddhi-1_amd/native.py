@@ -195,6 +195,39 @@ class KeyDictionary:
                                              len(ids), _np_ptr(ids), C.byref(n_new)))
         return ids
 
+    def intern_string_ids(self, sids, isnull, strings):
+        """intern over a STRING column given as the host string dictionary's ids (`strings`, a runtime
+        StringDictionary; isnull: the null bytes or None): ids seen before map through a cache (string id ->
+        key id, one gather per batch), the others are interned in order of first appearance.  The cache
+        follows this dictionary: remove / clear / put / update drop it, and so must a caller that replaces
+        `strings`' ids (drop_string_cache)."""
+        sids = np.asarray(sids, dtype=np.uint32)
+        c = self.__dict__.get("_scache")
+        if c is None or c[0] is not strings:
+            c = self._scache = (strings, np.full(max(1024, 2 * len(strings.strs)), 0xFFFFFFFE, dtype=np.uint32))
+        tab = c[1]
+        if len(tab) < len(strings.strs):
+            grown = np.full(2 * len(strings.strs), 0xFFFFFFFE, dtype=np.uint32)
+            grown[:len(tab)] = tab
+            tab = grown
+            self._scache = (strings, tab)
+        kids = tab[sids]
+        miss = kids == 0xFFFFFFFE
+        if isnull is not None:
+            miss &= isnull == 0
+        if miss.any():
+            u, first = np.unique(sids[miss], return_index=True)
+            u = u[np.argsort(first, kind="stable")]   # first-seen order within the batch
+            strs = strings.strs
+            tab[u] = self.intern([strs[i] for i in u.tolist()])
+            kids = tab[sids]
+        if isnull is not None and isnull.any():
+            kids = np.where(isnull != 0, np.uint32(SG_KEY_NULL), kids).astype(np.uint32)
+        return kids
+
+    def drop_string_cache(self):
+        self.__dict__.pop("_scache", None)
+
     def lookup(self, strings):
         data, offsets, valid = pack_strings(strings)
         ids = np.empty(len(offsets) - 1, dtype=np.uint32)
@@ -211,11 +244,13 @@ class KeyDictionary:
         """Partition purge: the ids leave the dictionary; later new keys reuse them, smallest first
         (all-or-nothing; an id not in use raises EngineError SG_ERR_INVALID)."""
         a = np.ascontiguousarray(ids, dtype=np.uint32)
+        self.drop_string_cache()
         self._check(self._lib.sg_dict_remove(self._h, _np_ptr(a) if len(a) else None, len(a)))
 
     def put(self, i, k):
         """Bind key string k to the free id i (snapshot restore)."""
         b = k.encode("utf-8")
+        self.drop_string_cache()
         self._check(self._lib.sg_dict_put(self._h, i, b, len(b)))
 
     def _live(self, i):
@@ -248,6 +283,7 @@ class KeyDictionary:
         return [self.key(i) if self._live(i) else None for i in range(len(self))]
 
     def clear(self):
+        self.drop_string_cache()
         self._check(self._lib.sg_dict_clear(self._h))
 
     def update(self, mapping):

@@ -18,6 +18,10 @@ host (QuerySelector.processNoGroupBy, C/query/selector/QuerySelector.java:162-20
 """
 from __future__ import annotations
 
+import functools
+import gc
+import inspect
+import itertools
 import json
 import re
 import struct
@@ -31,11 +35,29 @@ from . import siddhiql as q
 from .native import SG_KEY_NULL, EngineError, KeyDictionary, NativeEngine, load_hip_library
 
 
+def _no_gc(fn):
+    """run fn with Python's cyclic garbage collector paused: a send allocates one list / tuple / Event per
+    event and per match (none of them in a cycle), and with many live objects in the caller (Event
+    batches) each generation-2 collection those allocations trigger walks all of them — measured 2.8x of
+    the host time of a 65,536-event send(Event[]) (tools/api_host_prof.py)"""
+    @functools.wraps(fn)
+    def run(*a, **kw):
+        if not gc.isenabled():
+            return fn(*a, **kw)
+        gc.disable()
+        try:
+            return fn(*a, **kw)
+        finally:
+            gc.enable()
+    return run
+
+
 # ------------------------------------------------------------------------------------------------
 # public value types
 # ------------------------------------------------------------------------------------------------
 class Event:
     """io.siddhi.core.event.Event"""
+    __slots__ = ("timestamp", "data", "is_expired")
 
     def __init__(self, timestamp=-1, data=None, is_expired=False):
         self.timestamp = timestamp
@@ -62,6 +84,16 @@ class Event:
 
     def __repr__(self):
         return f"Event{{timestamp={self.timestamp}, data={self.data}, isExpired={self.is_expired}}}"
+
+
+class _OutEvent(Event):
+    """an output Event built over a data list the runtime hands over (no copy), constructed by map()"""
+    __slots__ = ()
+
+    def __init__(self, timestamp, data):
+        self.timestamp = timestamp
+        self.data = data
+        self.is_expired = False
 
 
 class StreamCallback:
@@ -229,7 +261,10 @@ class _EventStore:
         return len(self._rows) + self._pending_n
 
     def _flush(self):
-        for stream, ts, cols in self._pending:
+        for stream, ts, cols, rows in self._pending:
+            if rows is not None:   # a row chunk (send(Event[])): the data lists as sent
+                self._rows.extend(zip([stream] * len(ts), ts, map(tuple, rows)))
+                continue
             vals = [c.tolist() if not np.ma.isMaskedArray(c) else
                     [None if m else x for x, m in zip(c.data.tolist(), np.ma.getmaskarray(c).tolist())]
                     for c in cols]
@@ -242,16 +277,17 @@ class _EventStore:
         return len(self._rows) - 1
 
     def add_many(self, stream, ts, datas):
-        """consecutive seqs for a chunk of events; returns the first"""
-        self._flush()
-        base = len(self._rows)
-        self._rows.extend(zip([stream] * len(ts), ts, map(tuple, datas)))
+        """consecutive seqs for a chunk of events (ts: list of ints, datas: their data lists, kept as they
+        are until a row is read, as the reference keeps the sent Event's data); returns the first"""
+        base = len(self)
+        self._pending.append((stream, ts, None, datas))
+        self._pending_n += len(ts)
         return base
 
     def add_columns(self, stream, ts, cols):
         """consecutive seqs for a columnar chunk (kept as arrays until a row is read); returns the first"""
         base = len(self)
-        self._pending.append((stream, ts, cols))
+        self._pending.append((stream, ts, cols, None))
         self._pending_n += len(ts)
         return base
 
@@ -294,10 +330,16 @@ class StringDictionary:
 
     def ids_of(self, vals):
         """id_of over a column (one dict probe per value; new strings numbered in first-seen order)"""
-        g = self.ids.get
-        out = [g(v) for v in vals]
-        if None in out:
-            out = [self.id_of(v) if i is None else i for v, i in zip(vals, out)]
+        ids = self.ids
+        try:
+            return [ids[v] for v in vals]
+        except KeyError:
+            pass
+        n0 = len(ids)
+        sd = ids.setdefault
+        out = [sd(v, len(ids)) for v in vals]   # (a new string gets the next id, in first-seen order)
+        if len(ids) > n0:
+            self.strs.extend(reversed(list(itertools.islice(reversed(ids), len(ids) - n0))))
         return out
 
 
@@ -344,6 +386,10 @@ class _QueryRuntime:
         self.key_dict = key_dict
         self.n_keys = app_rt.n_keys if cq.partitioned else 1
         self.engine = engine_factory(cq.ir, self.n_keys)
+        try:   # engines that can hand out only the complete batches (sg_poll_matches | SG_POLL_READY)
+            self.ready_polls = "ready" in inspect.signature(self.engine.poll).parameters
+        except (TypeError, ValueError):
+            self.ready_polls = False
         # the select list on the device when it is plain expressions; else on the host
         self.device_projection = False
         prog = cp.projection_program(cq, app_rt.strings)
@@ -478,11 +524,12 @@ class _QueryRuntime:
             sel = self.cq.select
             cols = [self._decode(m.proj_value[i], m.proj_null[i], typ) for i, (_, typ, _) in enumerate(sel)]
             trig, ts = m.trigger_seq.tolist(), m.ts.tolist()
-            keep = range(len(m))
+            data = list(map(list, zip(*cols))) if cols else [[] for _ in trig]
             if self.cq.having is not None:   # the device evaluated `having` per row: only a non-null true passes
                 h, hn = m.proj_value[len(sel)], m.proj_null[len(sel)]
                 keep = np.nonzero((hn == 0) & ((h & 1) == 1))[0].tolist()
-            return [(trig[i], ts[i], [c[i] for c in cols]) for i in keep]
+                return [(trig[i], ts[i], data[i]) for i in keep]
+            return list(zip(trig, ts, data))
         return self.project_host(m, store)
 
     def project_host(self, m, store):
@@ -593,17 +640,26 @@ class _QueryRuntime:
         (AbsentStreamPreStateProcessor.sendEvent -> QuerySelector.process per StateEvent)."""
         if not projected:
             return
-        groups = []
-        cur = None
-        for trig, ts, data in projected:
-            if cur is None or cur[0] != trig or trig == TIMER_SEQ:
-                cur = (trig, [])
-                groups.append(cur)
-            cur[1].append(Event._of(ts, data))
-        for _, evs in groups:
-            if self.cq.output_stream is not None:
-                self.app_rt._emit_stream(self.cq.output_stream, evs)
-            for cb in self.query_callbacks:
+        trig, ts, data = zip(*projected)
+        events = list(map(_OutEvent, ts, data))
+        n = len(events)
+        t = np.fromiter(trig, dtype=np.uint64, count=n)
+        # a new callback call where the trigger changes; every timer match on its own
+        cut = (np.flatnonzero((t[1:] != t[:-1]) | (t[1:] == np.uint64(TIMER_SEQ))) + 1).tolist()
+        out, qcbs = self.cq.output_stream, self.query_callbacks
+        scbs = self.app_rt.stream_callbacks.get(out) if out is not None else None
+        if len(cut) == n - 1 and len(qcbs) == 1 and not scbs:   # one match per trigger, one QueryCallback
+            rcv = qcbs[0].receive
+            for e in events:
+                rcv(e.timestamp, [e], None)
+            return
+        a = 0
+        for b in cut + [n]:
+            evs = events[a:b]
+            a = b
+            if scbs:
+                self.app_rt._emit_stream(out, evs)
+            for cb in qcbs:
                 cb.receive(evs[-1].timestamp, evs, None)
 
 
@@ -618,16 +674,17 @@ class InputHandler:
         # send(Object[]) | send(long, Object[]) | send(Event) | send(Event[])   (InputHandler.java:51-97)
         # In playback mode every form but send(Object[]) first sets the event clock (to the last
         # event's timestamp for Event[]); send(Object[]) stamps the wall clock and leaves it alone.
+        rt = self.app_rt
         if len(args) == 2:
-            self.app_rt._send(self.stream, [(int(args[0]), list(args[1]))], explicit=True)
+            rt._send_rows(self.stream, [int(args[0])], [list(args[1])], True)
             return
         a = args[0]
         if isinstance(a, Event):
-            self.app_rt._send(self.stream, [(a.timestamp, a.data)], explicit=True)
+            rt._send_rows(self.stream, [a.timestamp], [a.data], True)
         elif isinstance(a, (list, tuple)) and a and isinstance(a[0], Event):
-            self.app_rt._send(self.stream, [(e.timestamp, e.data) for e in a], explicit=True)
+            rt._send_rows(self.stream, [e.timestamp for e in a], [e.data for e in a], True)
         else:
-            self.app_rt._send(self.stream, [(self.app_rt.wall_time(), list(a))], explicit=False)
+            rt._send_rows(self.stream, [rt.wall_time()], [list(a)], False)
 
     def send_columns(self, timestamps, columns):
         """Columnar send (an addition to the reference API): the events (timestamps[i], [c[i] for c in
@@ -810,6 +867,17 @@ class SiddhiAppRuntime:
         self._purges = [_Purge(p, [qr for qr in self.queries if qr.cq.partitioned and
                                    qr.key_dict is self.key_dicts.get(id(p))])
                         for p in self.app.partitions if _Purge.enabled(p)]
+        # @async streams (StreamJunction.java:104-135): their sends are buffered and handed to the engines in
+        # batches, the matches collected by ready polls (see _AsyncConfig)
+        self._async = {name: _AsyncConfig.of(sd) for name, sd in self.app.streams.items()
+                       if _AsyncConfig.annotation(sd) is not None}
+        # timers (absent states) or @purge make the clock and the per-send bookkeeping part of the output:
+        # sends on @async streams then go through one by one, as on a synchronous junction
+        self._async_merge = not self._purges and not any(_has_absent(qr.cq.query) for qr in self.queries)
+        self._abuf = []          # buffered sends of @async streams in arrival order: (stream, events, explicit)
+        self._abuf_n = 0
+        self._abuf_max = 0
+        self._inflight = []      # queries whose engines may hold batches not yet polled (ready polls)
         self.started = False
 
     # public API (camelCase as in the reference) -------------------------------------------------
@@ -836,6 +904,7 @@ class SiddhiAppRuntime:
     def start(self):
         """SiddhiAppRuntimeImpl.start -> QueryRuntimeImpl.start -> initPartition (unpartitioned queries
         seed their start states now; absent start states arm their timers)."""
+        self._drain()
         self.started = True
         for pg in self._purges:
             pg.next_run = self.wall_time() + pg.interval
@@ -856,6 +925,7 @@ class SiddhiAppRuntime:
         reference tests): wall-clock timers fire (Scheduler.EventCaller), and in playback mode with
         idle.time the heartbeat advances the event clock (TimestampGeneratorImpl.TimeInjector)."""
         ms = int(ms)
+        self._drain()   # (a test's sleep: the @async consumer has caught up)
         if self._purges and self.started:
             for pg in self._purges:   # purge runs due before `ms`, each at its own wall time
                 if pg.next_run is None:
@@ -875,20 +945,24 @@ class SiddhiAppRuntime:
         if self.started:
             self._fire_timers(ms)
 
-    def _fire_timers(self, now):
+    def _fire_timers(self, now, poll=True):
+        """the engines' clocks to `now`; poll=False (an @async batch of an app without timers): the clock
+        only, the matches stay for the ready polls"""
         for qr in self.queries:
             qr.engine.advance_time(now)
-            qr.deliver(qr.engine.poll(), self.store)
+            if poll:
+                qr.deliver(qr.engine.poll(), self.store)
 
-    def _set_event_time(self, ts):
+    def _set_event_time(self, ts, poll=True):
         """TimestampGeneratorImpl.setCurrentTimestamp (playback)."""
         if ts >= self._event_time:
             self._event_time = ts
-            self._fire_timers(ts)
+            self._fire_timers(ts, poll)
             self._last_sys = self.wall_time()
 
     def snapshot(self) -> bytes:
         """SiddhiAppRuntime.snapshot(): the app's pattern state as bytes (device NFA images included)."""
+        self._drain()
         head = {
             "app": self.name,
             "strings": self.strings.strs,
@@ -909,6 +983,7 @@ class SiddhiAppRuntime:
     def restore(self, snap: bytes):
         """SiddhiAppRuntime.restore(byte[]): replace the app's pattern state with a snapshot taken from
         a runtime of the same app text."""
+        self._drain()
         try:
             if snap[:8] != _SNAP_MAGIC:
                 raise ValueError("not a snapshot of this runtime")
@@ -946,6 +1021,7 @@ class SiddhiAppRuntime:
         StreamPreState.snapshot() writes it (StreamPreStateProcessor.java:450-469, + Count / Absent extras and
         the Scheduler's toNotifyQueue), StateEvent / StreamEvent objects shared as the engine shares them and
         each StreamEvent's data from the host event store."""
+        self._drain()
         sd = _state_doc()
         out = {}
         for name, qr in self.by_name.items():
@@ -968,6 +1044,7 @@ class SiddhiAppRuntime:
         """Replace the pattern queries' state with a map of snapshot_states()'s form (from this runtime, a
         runtime of the same app, or built by hand).  The StreamEvents' data enter the event store at their
         seqs, the partition keys the key dictionary."""
+        self._drain()
         sd = _state_doc()
         for name, qr in self.by_name.items():
             m = states.get(name, {})
@@ -1031,8 +1108,13 @@ class SiddhiAppRuntime:
         return rev
 
     def shutdown(self):
-        for qr in self.queries:
-            qr.engine.close()
+        """SiddhiAppRuntime.shutdown: the @async junctions drain (StreamJunction.stopProcessing ->
+        Disruptor.shutdown waits for the buffered events), then the engines close"""
+        try:
+            self._drain()
+        finally:
+            for qr in self.queries:
+                qr.engine.close()
 
     get_input_handler = getInputHandler
     add_callback = addCallback
@@ -1055,13 +1137,17 @@ class SiddhiAppRuntime:
         by_attr = list(zip(*rows)) if rows else [()] * len(sd.attrs)
         for ai, (an, at) in enumerate(sd.attrs):
             vals = by_attr[ai]
-            if at in self._NP and None not in vals:
+            if at in self._NP:
+                # one numpy call; a None raises for the integer types and becomes NaN for the float types
+                # (only then the values are checked one by one)
                 try:
-                    cols.append(np.array(vals, dtype=self._NP[at]))
-                    nulls.append(None)
-                    continue
+                    arr = np.array(vals, dtype=self._NP[at])
+                    if at in ("INT", "LONG") or not np.isnan(arr).any() or None not in vals:
+                        cols.append(arr)
+                        nulls.append(None)
+                        continue
                 except (TypeError, ValueError, OverflowError):
-                    pass   # mixed Python types: the exact per-value conversion below
+                    pass   # nulls or mixed Python types: the exact per-value conversion below
             if at == "STRING" and None not in vals:
                 cols.append(np.array(self.strings.ids_of(vals), dtype=np.uint32))
                 nulls.append(None)
@@ -1115,29 +1201,96 @@ class SiddhiAppRuntime:
         qr.deliver(qr.engine.poll(), self.store)
 
     def _send(self, stream, events, explicit=True):
-        if stream not in self.app.streams:
+        """events: [(timestamp, data list)]"""
+        self._send_rows(stream, [e[0] for e in events], [e[1] for e in events], explicit)
+
+    @_no_gc
+    def _send_rows(self, stream, ts, rows, explicit=True):
+        """one send of len(ts) events: ts[i] the timestamp, rows[i] the data list (InputHandler.send)"""
+        sd = self.app.streams.get(stream)
+        if sd is None:
             raise KeyError(stream)
+        na = len(sd.attrs)
+        lens = set(map(len, rows))
+        if lens and lens != {na}:
+            bad = next(x for x in lens if x != na)
+            raise ValueError(f"event for {stream} has {bad} attributes, expected {na}")
+        cfg = self._async.get(stream)
+        if cfg is not None and self._async_merge:
+            # @async junction: InputHandler.send returns once the events are in the ring; the consumer
+            # hands them on in batches of up to batch.size.max (StreamHandler.java:58-85)
+            self._abuf.append((stream, ts, rows, explicit))
+            self._abuf_n += len(ts)
+            if self._abuf_n >= cfg.batch:
+                self._flush_async()
+            return
+        self._drain()
+        self._send_now(stream, ts, rows, explicit, False)
+
+    # -- @async junctions --------------------------------------------------------------------------
+    def _flush_async(self):
+        """the buffered @async sends to the engines: consecutive sends of one stream merged into batches of
+        up to batch.size.max events (a single larger send stays whole), in arrival order; their matches are
+        collected by ready polls (the batches still in flight come with a later poll or the drain)"""
+        buf, self._abuf, self._abuf_n = self._abuf, [], 0
+        i = 0
+        while i < len(buf):
+            stream, ts, rows, explicit = buf[i]
+            cap = self._async[stream].batch
+            j = i + 1
+            if j < len(buf) and buf[j][0] == stream and buf[j][3] == explicit and len(ts) < cap:
+                ts, rows = list(ts), list(rows)
+                while j < len(buf) and buf[j][0] == stream and buf[j][3] == explicit and \
+                        len(ts) + len(buf[j][1]) <= cap:
+                    ts.extend(buf[j][1])
+                    rows.extend(buf[j][2])
+                    j += 1
+            self._send_now(stream, ts, rows, explicit, True)
+            i = j
+
+    @_no_gc
+    def _drain(self):
+        """every buffered @async send processed and every match delivered (the synchronous operations —
+        a send on a synchronous stream, timers, snapshots, shutdown — see the state after all earlier sends)"""
+        if self._abuf:
+            self._flush_async()
+        if self._inflight:
+            qs, self._inflight = self._inflight, []
+            for qr in qs:
+                qr.deliver(qr.engine.poll(), self.store)
+
+    def _collect(self, qr, pipelined):
+        """the matches of qr's engine after a push: all of them (a synchronous send), or only those of the
+        batches already complete (an @async batch: SG_POLL_READY, no wait for the batch just pushed)"""
+        if pipelined and qr.ready_polls:
+            qr.deliver(qr.engine.poll(ready=True), self.store)
+            if qr not in self._inflight:
+                self._inflight.append(qr)
+        else:
+            qr.deliver(qr.engine.poll(), self.store)
+
+    def flush(self):
+        """Deliver everything sent so far (the @async streams' buffered events included).  Not in the
+        reference API, where the consumer threads drain the rings on their own."""
+        self._drain()
+
+    def _send_now(self, stream, ts, rows, explicit, pipelined):
         self._run_purges()
         sd = self.app.streams[stream]
         if self.playback:
-            if explicit and events:
-                self._set_event_time(events[-1][0])
+            if explicit and ts:
+                self._set_event_time(ts[-1], poll=not pipelined)
         elif self.started:
-            self._fire_timers(self.wall_time())
-        na = len(sd.attrs)
-        rows = [e[1] for e in events]
-        for data in rows:
-            if len(data) != na:
-                raise ValueError(f"event for {stream} has {len(data)} attributes, expected {na}")
-        ts_all = np.fromiter((e[0] for e in events), dtype=np.int64, count=len(events))
-        base = self.store.add_many(stream, ts_all.tolist(), rows)
+            self._fire_timers(self.wall_time(), poll=not pipelined)
+        ts_all = np.array(ts, dtype=np.int64)
+        base = self.store.add_many(stream, ts, rows)
         cols_all = None
         for qr in self.queries:
             si = qr.cq.stream_index(stream)
             if si < 0:
                 continue
             if qr.cq.partitioned and qr.cq.partition_keys[stream] is None:
-                self._send_broadcast(qr, si, sd, events)
+                self._send_broadcast(qr, si, sd, list(zip(ts, rows)))
                 continue
             if cols_all is None:
                 cols_all = self._columns(sd, rows)
@@ -1146,9 +1299,13 @@ class SiddhiAppRuntime:
                 qr.engine.push(si, base, ts_all, cols, nulls, None)
             else:
                 ai = sd.attr_index(qr.cq.partition_keys[stream])
-                # one batched intern per send (sg_dict); PartitionStreamReceiver drops null keys
+                # one batched intern per send (sg_dict); PartitionStreamReceiver drops null keys.  A STRING
+                # key is the attribute's string id already: ids seen before map through a cache
                 try:
-                    kids = np.asarray(qr.key_dict.intern(java_strings([r[ai] for r in rows])), dtype=np.uint32)
+                    if sd.attrs[ai][1] == "STRING":
+                        kids = qr.key_dict.intern_string_ids(cols[ai], nulls[ai], self.strings)
+                    else:
+                        kids = np.asarray(qr.key_dict.intern(java_strings([r[ai] for r in rows])), dtype=np.uint32)
                 except EngineError as ex:
                     raise RuntimeError(f"more than {qr.n_keys} partition keys") from ex
                 keep = np.nonzero(kids != SG_KEY_NULL)[0]
@@ -1169,9 +1326,9 @@ class SiddhiAppRuntime:
                         lo, hi = int(idx[0]), int(idx[-1]) + 1
                         qr.engine.push(si, base + lo, ts_all[lo:hi], [c[lo:hi] for c in cols],
                                        [x[lo:hi] if x is not None else None for x in nulls], kids[lo:hi])
-            qr.deliver(qr.engine.poll(), self.store)
+            self._collect(qr, pipelined)
 
-
+    @_no_gc
     def _send_columns(self, stream, timestamps, columns):
         """InputHandler.send_columns: _send's path (send(Event[]) semantics) on arrays"""
         if stream not in self.app.streams:
@@ -1191,6 +1348,12 @@ class SiddhiAppRuntime:
                 raise ValueError(f"column of {len(c)} values for {n} timestamps")
         if n == 0:
             return
+        pipelined = stream in self._async and self._async_merge
+        if pipelined:
+            if self._abuf:   # (the events buffered before this send go first)
+                self._flush_async()
+        else:
+            self._drain()
         # numpy bytes ('S') STRING columns: UTF-8 bytes are interned as they are (the key dictionary packs
         # them without a per-value loop), but the event store and the row path hold str values, as a
         # send(Event[]) of the same strings would
@@ -1205,9 +1368,9 @@ class SiddhiAppRuntime:
             return
         self._run_purges()
         if self.playback:
-            self._set_event_time(int(ts_all[-1]))
+            self._set_event_time(int(ts_all[-1]), poll=not pipelined)
         elif self.started:
-            self._fire_timers(self.wall_time())
+            self._fire_timers(self.wall_time(), poll=not pipelined)
         base = self.store.add_columns(stream, ts_all, cols_rows)
         cols_all = None
         for qr in self.queries:
@@ -1246,13 +1409,16 @@ class SiddhiAppRuntime:
                         lo, hi = int(idx[0]), int(idx[-1]) + 1
                         qr.engine.push(si, base + lo, ts_all[lo:hi], [c[lo:hi] for c in cols],
                                        [x[lo:hi] if x is not None else None for x in nulls], kids[lo:hi])
-            qr.deliver(qr.engine.poll(), self.store)
+            self._collect(qr, pipelined)
 
     def _invalidate_caches(self):
-        """drop what was derived from the dictionaries (categorical id maps, the id -> string array): a
-        restore replaces the dictionaries, and an id map built before it would push stale ids"""
+        """drop what was derived from the dictionaries (categorical id maps, the id -> string array, the
+        string id -> key id maps): a restore replaces the dictionaries, and an id map built before it would
+        push stale ids"""
         self.__dict__.pop("_cat_cache", None)
         self.strings.__dict__.pop("_arr", None)
+        for kd in self.key_dicts.values():
+            kd.drop_string_cache()
 
     def _category_ids(self, categories, what, make):
         """ids of a categorical column's categories (`make` over their strings), cached per categories
@@ -1302,6 +1468,68 @@ class SiddhiAppRuntime:
             cols.append(one_c[0])
             nulls.append(one_n[0])
         return cols, nulls
+
+
+class _AsyncConfig:
+    """@async(buffer.size='N', workers='W', batch.size.max='B') of a stream definition (StreamJunction.java:
+    104-135; defaults: buffer.size SiddhiConstants.DEFAULT_EVENT_BUFFER_SIZE = 1024, batch.size.max = the
+    buffer size).  The reference puts each sent event into a Disruptor ring and its StreamHandler consumers
+    hand the events on in chunks of up to batch.size.max (StreamHandler.java:58-85); here the runtime buffers
+    the sends and pushes them as one columnar batch per batch.size.max events, and the engines' matches of a
+    batch are delivered by a later ready poll (sg_poll_matches | SG_POLL_READY) — the host packs batch i + 1
+    while the device runs batch i.  workers > 1 makes the reference's output order nondeterministic
+    (SURVEY A.13); the runtime keeps one consumer, so the output is the synchronous junction's."""
+
+    def __init__(self, buffer_size, workers, batch):
+        self.buffer_size, self.workers, self.batch = buffer_size, workers, batch
+
+    @staticmethod
+    def annotation(sd):
+        for a in getattr(sd, "annotations", None) or []:
+            if a.name.lower() == "async":
+                return a
+        return None
+
+    @classmethod
+    def of(cls, sd):
+        a = cls.annotation(sd)
+
+        def num(key):
+            v = a.get(key)
+            if v is None:
+                return None
+            try:
+                return int(str(v).strip())
+            except ValueError:
+                raise SiddhiAppCreationException(f"Annotation element '{key}' of stream {sd.name} is not an "
+                                                 f"integer: '{v}'")
+        buf = num("buffer.size")
+        buf = 1024 if buf is None else buf
+        workers = num("workers")
+        if workers is not None and workers <= 0:
+            raise SiddhiAppCreationException(f"Annotation element 'workers' cannot be negative or zero, but found, "
+                                             f"'{workers}'.")
+        batch = num("batch.size.max")
+        if batch is not None and batch <= 0:
+            raise SiddhiAppCreationException(f"Annotation element 'batch.size.max' cannot be negative or zero, but "
+                                             f"found, '{batch}'.")
+        if buf <= 0:
+            raise SiddhiAppCreationException(f"Annotation element 'buffer.size' must be positive, found '{buf}'.")
+        return cls(buf, workers or 1, batch if batch is not None else buf)
+
+
+def _has_absent(node, seen=None):
+    """does a query's input tree hold an absent (`not ... for`) state (timers)?"""
+    seen = set() if seen is None else seen
+    if node is None or id(node) in seen or isinstance(node, (str, bytes, int, float, bool)):
+        return False
+    seen.add(id(node))
+    if getattr(node, "absent", False) is True:
+        return True
+    if isinstance(node, (list, tuple)):
+        return any(_has_absent(x, seen) for x in node)
+    d = getattr(node, "__dict__", None)
+    return bool(d) and any(_has_absent(v, seen) for v in d.values())
 
 
 def _is_categorical(c):
