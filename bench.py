@@ -386,6 +386,45 @@ def api_inclusive(sa, synth, n_keys, chunk, chunks):
                     "(host Python runtime + HIP engine), bounded sample"}
 
 
+def api_async(sa, synth, n_keys, n, batch_max=1 << 16):
+    """C2 through the product API with the input stream declared
+    @async(buffer.size, batch.size.max) and one InputHandler.send(Event) per event (the reference's usual
+    producer loop; StreamJunction.java:280-317 + StreamHandler.java:58-85): the runtime buffers the sends,
+    pushes batch.size.max-event batches and delivers the callbacks from ready polls, so the host packs the
+    next batch while the device runs the last one.  Event objects are built before the timed region."""
+    mgr = sa.SiddhiManager(n_keys=n_keys, max_batch=batch_max)
+    rt = mgr.createSiddhiAppRuntime(f"@async(buffer.size='{batch_max}', batch.size.max='{batch_max}')\n" +
+                                    synth.C2_QUERY)
+    got = [0, 0]
+
+    class Count(sa.QueryCallback):
+        def receive(self, timestamp, in_events, remove_events):
+            got[0] += 1
+            got[1] += len(in_events)
+
+    rt.addCallback("query1", Count())
+    rt.start()
+    ih = rt.getInputHandler("StockStream")
+    names = [f"S{k}" for k in range(n_keys)]
+    d = synth.stock_ticks(0, n + batch_max, n_keys)
+    evs = [sa.Event(t, [names[k], p, v]) for t, k, p, v in
+           zip(d["ts"].tolist(), d["key"].tolist(), d["price"].tolist(), d["volume"].tolist())]
+    for e in evs[:batch_max]:   # (warm-up: engine creation, the JIT'd kernel, the key dictionary)
+        ih.send(e)
+    rt.flush()
+    t0 = time.perf_counter()
+    for e in evs[batch_max:]:
+        ih.send(e)
+    rt.flush()
+    el = time.perf_counter() - t0
+    rt.shutdown()
+    return {"value": n / el, "unit": "events/s", "events": n, "batch_size_max": batch_max, "keys": n_keys,
+            "callbacks": got[0], "matches": got[1], "device_projection": bool(rt.queries[0].device_projection),
+            "what": "C2 through SiddhiManager with @async(batch.size.max) on the input stream, one "
+                    "InputHandler.send(Event) per event, QueryCallback per trigger (host runtime + HIP engine, "
+                    "ready polls), bounded sample"}
+
+
 def api_columnar(sa, synth, n_keys, chunk, chunks):
     """C2 through the columnar host API end to end (SiddhiManager -> InputHandler.send_columns with the
     symbol column dictionary-encoded (pandas.Categorical over the 2^20 key names) -> the HIP engine ->
@@ -645,6 +684,7 @@ def main():
         out["pcie_inclusive"] = pcie_inclusive(sa, synth, torch, dev, cq, K, B, 4)
         out["output_inclusive"] = output_inclusive(sa, synth, torch, dev, K, B, 6)
         out["api_inclusive"] = api_inclusive(sa, synth, 1 << 16, 1 << 16, 16)
+        out["api_async"] = api_async(sa, synth, 1 << 16, 1 << 20)
         out["api_columnar"] = api_columnar(sa, synth, 1 << 20, 1 << 20, 8)
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(sa, synth, K, B, args.cpu_seconds)

@@ -680,7 +680,7 @@ class InputHandler:
             return
         a = args[0]
         if isinstance(a, Event):
-            rt._send_rows(self.stream, [a.timestamp], [a.data], True)
+            rt._send_one(self.stream, a.timestamp, a.data)
         elif isinstance(a, (list, tuple)) and a and isinstance(a[0], Event):
             rt._send_rows(self.stream, [e.timestamp for e in a], [e.data for e in a], True)
         else:
@@ -1204,49 +1204,74 @@ class SiddhiAppRuntime:
         """events: [(timestamp, data list)]"""
         self._send_rows(stream, [e[0] for e in events], [e[1] for e in events], explicit)
 
-    @_no_gc
     def _send_rows(self, stream, ts, rows, explicit=True):
         """one send of len(ts) events: ts[i] the timestamp, rows[i] the data list (InputHandler.send)"""
         sd = self.app.streams.get(stream)
         if sd is None:
             raise KeyError(stream)
         na = len(sd.attrs)
-        lens = set(map(len, rows))
-        if lens and lens != {na}:
-            bad = next(x for x in lens if x != na)
-            raise ValueError(f"event for {stream} has {bad} attributes, expected {na}")
+        if len(rows) == 1:
+            if len(rows[0]) != na:
+                raise ValueError(f"event for {stream} has {len(rows[0])} attributes, expected {na}")
+        else:
+            lens = set(map(len, rows))
+            if lens and lens != {na}:
+                bad = next(x for x in lens if x != na)
+                raise ValueError(f"event for {stream} has {bad} attributes, expected {na}")
         cfg = self._async.get(stream)
         if cfg is not None and self._async_merge:
             # @async junction: InputHandler.send returns once the events are in the ring; the consumer
-            # hands them on in batches of up to batch.size.max (StreamHandler.java:58-85)
-            self._abuf.append((stream, ts, rows, explicit))
+            # hands them on in batches of up to batch.size.max (StreamHandler.java:58-85).  The buffer is a
+            # list of segments [stream, explicit, timestamps, data lists], one per run of sends of one stream
+            b = self._abuf
+            if b and b[-1][0] == stream and b[-1][1] == explicit:
+                b[-1][2].extend(ts)
+                b[-1][3].extend(rows)
+            else:
+                b.append([stream, explicit, list(ts), list(rows)])
             self._abuf_n += len(ts)
             if self._abuf_n >= cfg.batch:
                 self._flush_async()
             return
+        self._send_sync(stream, ts, rows, explicit)
+
+    def _send_one(self, stream, ts, data):
+        """InputHandler.send(Event): one event, explicit timestamp (no per-event container on an @async
+        stream: the timestamp and the data list join the buffer's current segment)"""
+        cfg = self._async.get(stream)
+        b = self._abuf
+        if cfg is not None and self._async_merge and b and b[-1][0] == stream and b[-1][1] is True and \
+                len(data) == len(self.app.streams[stream].attrs):
+            b[-1][2].append(ts)
+            b[-1][3].append(data)
+            self._abuf_n += 1
+            if self._abuf_n >= cfg.batch:
+                self._flush_async()
+            return
+        self._send_rows(stream, [ts], [data], True)
+
+    @_no_gc
+    def _send_sync(self, stream, ts, rows, explicit):
         self._drain()
         self._send_now(stream, ts, rows, explicit, False)
 
     # -- @async junctions --------------------------------------------------------------------------
+    @_no_gc
     def _flush_async(self):
         """the buffered @async sends to the engines: consecutive sends of one stream merged into batches of
-        up to batch.size.max events (a single larger send stays whole), in arrival order; their matches are
+        up to batch.size.max events, in arrival order; their matches are
         collected by ready polls (the batches still in flight come with a later poll or the drain)"""
         buf, self._abuf, self._abuf_n = self._abuf, [], 0
-        i = 0
-        while i < len(buf):
-            stream, ts, rows, explicit = buf[i]
+        for stream, explicit, ts, rows in buf:
+            # batches of up to batch.size.max events (the engine's order is by arrival seq, so where a
+            # batch ends does not change the matches or their order; the clock is not part of an app
+            # that merges)
             cap = self._async[stream].batch
-            j = i + 1
-            if j < len(buf) and buf[j][0] == stream and buf[j][3] == explicit and len(ts) < cap:
-                ts, rows = list(ts), list(rows)
-                while j < len(buf) and buf[j][0] == stream and buf[j][3] == explicit and \
-                        len(ts) + len(buf[j][1]) <= cap:
-                    ts.extend(buf[j][1])
-                    rows.extend(buf[j][2])
-                    j += 1
-            self._send_now(stream, ts, rows, explicit, True)
-            i = j
+            if len(ts) <= cap:
+                self._send_now(stream, ts, rows, explicit, True)
+                continue
+            for a in range(0, len(ts), cap):
+                self._send_now(stream, ts[a:a + cap], rows[a:a + cap], explicit, True)
 
     @_no_gc
     def _drain(self):
