@@ -1,4 +1,5 @@
-"""Profile of the columnar host API leg (bench.api_columnar) under cProfile: where a send's host time goes."""
+"""Host API legs of bench.py (api_inclusive, api_async, api_columnar) timed, then each again under
+cProfile: where a send's host time goes on the GPU box."""
 import cProfile
 import importlib
 import os
@@ -11,9 +12,19 @@ import bench  # noqa: E402
 
 sa = importlib.import_module("siddhi-1_amd")
 synth = importlib.import_module("siddhi-1_amd.synth")
-pr = cProfile.Profile()
-pr.enable()
-r = bench.api_columnar(sa, synth, 1 << 20, 1 << 20, 4)
-pr.disable()
-print({k: v for k, v in r.items() if k != "what"})
-pstats.Stats(pr).sort_stats("cumulative").print_stats(28)
+legs = {
+    "api_inclusive": lambda: bench.api_inclusive(sa, synth, 1 << 16, 1 << 16, 16),
+    "api_async": lambda: bench.api_async(sa, synth, 1 << 16, 1 << 20),
+    "api_columnar": lambda: bench.api_columnar(sa, synth, 1 << 20, 1 << 20, 8),
+}
+want = sys.argv[1:] or list(legs)
+for name in want:
+    r = legs[name]()
+    print(name, {k: v for k, v in r.items() if k != "what"}, flush=True)
+for name in want:
+    pr = cProfile.Profile()
+    pr.enable()
+    r = legs[name]()
+    pr.disable()
+    print(f"== {name} under cProfile: {r['value']:.4g} events/s", flush=True)
+    pstats.Stats(pr).sort_stats("tottime").print_stats(25)
