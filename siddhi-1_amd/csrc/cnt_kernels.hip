@@ -1,0 +1,494 @@
+// cnt_kernels.hip — register-window kernel for the counting sequence shape
+//
+//     every e1=S[f0]<m:n>, e2=S[fA] or e3=S[fB] [within W]          (SEQUENCE, partitioned, 1 <= m, n <= CNT_R)
+//
+// (BASELINE configs[2], "C3" / "C3_min1").  The general kernel (gen_kernels.hip) runs this query through the
+// processor graph with every StateEvent / StreamEvent in the key-interleaved pools of HBM: a count partial
+// that grows by one event costs ~25 word accesses to distinct rows (pool bitmaps, records, list entries,
+// refcounts) per processor visit.  Under SEQUENCE semantics a key of this shape holds at most ONE partial
+// between events (StateStreamRuntime.resetAndUpdate clears every pending list before each event, and the
+// SEQUENCE addState keeps at most one staged entry per processor), so one lane per key keeps that partial —
+// the count chain e1 (up to CNT_R events: seq, ts, attribute words, null bits), its list memberships and the
+// three processors' flag words — in registers for the key's whole run of the batch, and writes the lists back
+// once, in a canonical layout of the general blocks (StateEvent 0 = the partial over StreamEvents 0..len-1
+// linked by `next`, StateEvent 1 = a staged start seed, free bitmaps rebuilt).  The state stays the general
+// engine's: snapshots, state documents, purge and the general kernel read it unchanged; a key whose stored
+// lists are not of this canonical shape (e.g. imported from a document of another shape's history) is handed
+// to the general kernel for its whole run (k_gen_batch GEN_M_KEYLIST), so the results stay exactly the
+// general engine's.
+//
+// What one event of a key does (restated from the reference, paths under
+// /root/reference/modules/siddhi-core/src/main/java/io/siddhi/core/query/input/stream/state/):
+//   receiver/SequenceMultiProcessStreamReceiver.java:39-50 stabilizeStates -> StateStreamRuntime.java:81-88
+//       resetAndUpdate, then the states in reverse order (pA, pB, p0), each projected at once
+//   StreamPreStateProcessor.java:118-129 isExpired, :325-361 expireEvents (+ :354-357 withinEvery clone),
+//       :287-305 resetState (+ :178-194 init: `every` stages a fresh seed), :308-323 updateState
+//   LogicalPreStateProcessor.java:43-62 addState (SEQUENCE: one entry, both partners), :96-124 resetState,
+//       :126-140 updateState, :143-180 processAndReturn (a partial whose partner slot is filled is dropped)
+//   LogicalPostStateProcessor.java:59-83 (OR: StreamPostStateProcessor + the partner's event-returned flag)
+//   CountPreStateProcessor.java:53-95 processAndReturn (a partial whose e2 / e3 slot is filled is dropped;
+//       the event appended to the chain, removed again when the filter fails; SEQUENCE drops a failed one)
+//   CountPostStateProcessor.java:39-66 (SEQUENCE: n >= m -> next state's addState; n != max -> own addState;
+//       n == max -> stateChanged)
+#include <hip/hip_runtime.h>
+
+#include "../../include/siddhi_gpu.h"
+#include "../../include/siddhi_gpu_ir.h"
+#include "gen_engine.h"
+#include "java_ops.h"
+#include "sg_engine.h"
+#include "reg_common.h"
+
+namespace {
+
+template <int NW> struct CntKey {
+    const cGenProgram& G;
+    const GenArgs& A;
+    gu32* S;
+    uint32_t K, k;
+    int p0, pA, pB;           // processors (an event visits pA, pB, p0)
+    int s0, sA, sB;           // their slots
+    uint32_t ks0, ksA, ksB;   // KeyState word offsets
+    int32_t mn, mx;           // count bounds
+    // the partial X: e1's chain [0, n) (n = 0: no partial), X's timestamp and its list memberships
+    int64_t ts[CNT_R];
+    uint64_t seq[CNT_R];
+    uint32_t w[CNT_R][NW];
+    uint32_t nb[CNT_R];
+    uint32_t n;
+    int64_t xts;
+    bool inP0p, inP0n, inL;   // X in p0.pending / p0.newAndEvery / both logical newAndEvery lists
+    bool seedN;               // a blank start seed staged in p0.newAndEvery
+    uint32_t f0, fA, fB;      // the processors' flag words
+    uint32_t err;
+    unsigned long long scanned, created, matches;
+    // this lane's reserved raw match slots (as the general kernel's Lane::project)
+    unsigned long long resBase, resEnd;
+    uint32_t resLeft;
+    uint32_t trigRank;
+
+    __device__ CntKey(const GenArgs& a, uint32_t key)
+        : G(*(cGenProgram*)a.G), A(a), S(gp(a.state)), K(a.K), k(key), n(0), xts(-1), inP0p(false), inP0n(false),
+          inL(false), seedN(false), f0(0), fA(0), fB(0), err(0), scanned(0), created(0), matches(0), resBase(0),
+          resEnd(0), resLeft(0), trigRank(0) {
+        p0 = G.cntP0;
+        pA = G.cntPA;
+        pB = G.cntPB;
+        s0 = G.pre[p0].stateId;
+        sA = G.pre[pA].stateId;
+        sB = G.pre[pB].stateId;
+        ks0 = G.offKS + (uint32_t)p0 * G.ksWords;
+        ksA = G.offKS + (uint32_t)pA * G.ksWords;
+        ksB = G.offKS + (uint32_t)pB * G.ksWords;
+        mn = G.pre[p0].minCount;
+        mx = G.pre[p0].maxCount;
+    }
+    __device__ void retarget(uint32_t key) {
+        k = key;
+        n = 0;
+        xts = -1;
+        inP0p = inP0n = inL = seedN = false;
+        f0 = fA = fB = 0;
+    }
+
+    __device__ __forceinline__ gu32& W(uint32_t w_) const { return S[gen_il(K, k, w_)]; }
+    __device__ __forceinline__ int64_t R64(uint32_t w_) const {
+        return (int64_t)((uint64_t)W(w_) | ((uint64_t)W(w_ + 1) << 32));
+    }
+    __device__ __forceinline__ void W64(uint32_t w_, int64_t v) const {
+        W(w_) = (uint32_t)(uint64_t)v;
+        W(w_ + 1) = (uint32_t)((uint64_t)v >> 32);
+    }
+    __device__ __forceinline__ uint32_t stw(uint32_t se, uint32_t f) const { return G.offST + se * G.stWords + f; }
+    __device__ __forceinline__ uint32_t sew(uint32_t e, uint32_t f) const { return G.offSE + e * G.seWords + f; }
+
+    // ---- load: false = the stored lists are not of this kernel's canonical shape (the general kernel
+    // takes the key's run)
+    __device__ bool load() {
+        if (!(W(0) & 1u)) {  // PartitionRuntimeImpl.initPartition: p0.init() stages one seed
+            seedN = true;
+            f0 = GF_INIT;
+            return true;
+        }
+        f0 = W(ks0 + KS_FLAGS);
+        fA = W(ksA + KS_FLAGS);
+        fB = W(ksB + KS_FLAGS);
+        const uint32_t p0p = W(ks0 + KS_PLEN), p0n = W(ks0 + KS_NLEN);
+        const uint32_t Ap = W(ksA + KS_PLEN), An = W(ksA + KS_NLEN), Bp = W(ksB + KS_PLEN), Bn = W(ksB + KS_NLEN);
+        if (Ap != 0u || Bp != 0u || p0p > 1u || p0n > 1u || An > 1u || An != Bn) return false;
+        // (memberships computed as values and assigned once: branches that store to different members
+        // make the compiler select a member address, which keeps the whole key object in scratch)
+        uint32_t xi = GEN_NIL;
+        const bool l = An != 0u;
+        if (l) {
+            xi = W(ksA + KS_LISTS + G.L);
+            if (W(ksB + KS_LISTS + G.L) != xi) return false;
+        }
+        const bool pp = p0p != 0u;
+        if (pp) {
+            const uint32_t y = W(ks0 + KS_LISTS);
+            if (xi != GEN_NIL && y != xi) return false;
+            xi = y;
+        }
+        bool pn = false, sd = false;
+        if (p0n) {
+            const uint32_t y = W(ks0 + KS_LISTS + G.L);
+            const bool blank = y < G.STCAP && W(stw(y, ST_TYPE)) == 0u && W(stw(y, ST_RC)) == 1u &&
+                               R64(stw(y, ST_TS)) == -1 && W(stw(y, ST_SLOTS + (uint32_t)s0)) == GEN_NIL &&
+                               W(stw(y, ST_SLOTS + (uint32_t)sA)) == GEN_NIL && W(stw(y, ST_SLOTS + (uint32_t)sB)) == GEN_NIL;
+            sd = y != xi && blank && !pp;  // (a staged seed: only before the key's first event)
+            pn = !sd;
+            if (pn && xi != GEN_NIL && y != xi) return false;
+            xi = pn ? y : xi;
+        }
+        inL = l;
+        inP0p = pp;
+        inP0n = pn;
+        seedN = sd;
+        if (xi == GEN_NIL) return true;
+        if (xi >= G.STCAP) return false;
+        const uint32_t rc = (inP0p ? 1u : 0u) + (inP0n ? 1u : 0u) + (inL ? 2u : 0u);
+        if (W(stw(xi, ST_TYPE)) != 0u || W(stw(xi, ST_RC)) != rc) return false;
+        if (W(stw(xi, ST_SLOTS + (uint32_t)sA)) != GEN_NIL || W(stw(xi, ST_SLOTS + (uint32_t)sB)) != GEN_NIL) return false;
+        xts = R64(stw(xi, ST_TS));
+        uint32_t e = W(stw(xi, ST_SLOTS + (uint32_t)s0));
+#pragma unroll
+        for (int j = 0; j < CNT_R; ++j) {
+            ts[j] = 0;
+            seq[j] = 0;
+#pragma unroll
+            for (int q = 0; q < NW; ++q) w[j][q] = 0;
+            nb[j] = 0;
+        }
+        uint32_t len = 0;
+        while (e != GEN_NIL) {
+            if (e >= G.SECAP || len >= (uint32_t)mx || len >= (uint32_t)CNT_R || W(sew(e, SE_RC)) != 1u) return false;
+            const int64_t t = R64(sew(e, SE_TS));
+            const uint64_t q = (uint64_t)R64(sew(e, SE_SEQ));
+            const uint32_t nbits = W(sew(e, SE_NULL));
+            uint32_t ww[NW];
+#pragma unroll
+            for (int x = 0; x < NW; ++x) ww[x] = W(sew(e, G.absWordAt[x]));
+#pragma unroll
+            for (int j = 0; j < CNT_R; ++j) {  // (selects: a conditional store at j == len becomes an indexed one)
+                const bool here = (uint32_t)j == len;
+                ts[j] = here ? t : ts[j];
+                seq[j] = here ? q : seq[j];
+                nb[j] = here ? nbits : nb[j];
+#pragma unroll
+                for (int x = 0; x < NW; ++x) w[j][x] = here ? ww[x] : w[j][x];
+            }
+            len++;
+            e = W(sew(e, SE_NEXT));
+        }
+        if (len == 0u) return false;
+        n = len;
+        return true;
+    }
+
+    // ---- store: the lists in the canonical layout, free bitmaps rebuilt
+    __device__ void store() const {
+        W(0) = 1u;
+        W(ks0 + KS_FLAGS) = f0;
+        W(ksA + KS_FLAGS) = fA;
+        W(ksB + KS_FLAGS) = fB;
+        const bool x = n > 0u;
+        const uint32_t seedIdx = x ? 1u : 0u;
+        W(ks0 + KS_PLEN) = (x && inP0p) ? 1u : 0u;
+        W(ks0 + KS_NLEN) = ((x && inP0n) || seedN) ? 1u : 0u;
+        if (x && inP0p) W(ks0 + KS_LISTS) = 0u;
+        if (x && inP0n) W(ks0 + KS_LISTS + G.L) = 0u;
+        else if (seedN) W(ks0 + KS_LISTS + G.L) = seedIdx;
+        W(ksA + KS_PLEN) = 0u;
+        W(ksB + KS_PLEN) = 0u;
+        W(ksA + KS_NLEN) = (x && inL) ? 1u : 0u;
+        W(ksB + KS_NLEN) = (x && inL) ? 1u : 0u;
+        if (x && inL) {
+            W(ksA + KS_LISTS + G.L) = 0u;
+            W(ksB + KS_LISTS + G.L) = 0u;
+        }
+        if (x) {
+            const uint32_t b = G.offST;
+            W64(b + ST_TS, xts);
+            W(b + ST_TYPE) = 0u;
+            W(b + ST_RC) = (inP0p ? 1u : 0u) + (inP0n ? 1u : 0u) + (inL ? 2u : 0u);
+            for (int s = 0; s < G.nslots; s++) W(b + ST_SLOTS + (uint32_t)s) = s == s0 ? 0u : GEN_NIL;
+#pragma unroll
+            for (int j = 0; j < CNT_R; ++j) {
+                if ((uint32_t)j < n) {
+                    const uint32_t eb = G.offSE + (uint32_t)j * G.seWords;
+                    W64(eb + SE_SEQ, (int64_t)seq[j]);
+                    W64(eb + SE_TS, ts[j]);
+                    W(eb + SE_NEXT) = (uint32_t)j + 1u < n ? (uint32_t)j + 1u : GEN_NIL;
+                    W(eb + SE_RC) = 1u;
+                    W(eb + SE_NULL) = nb[j];
+#pragma unroll
+                    for (int q = 0; q < NW; ++q) W(eb + G.absWordAt[q]) = w[j][q];
+                }
+            }
+        }
+        if (seedN) {
+            const uint32_t b = G.offST + seedIdx * G.stWords;
+            W64(b + ST_TS, -1);
+            W(b + ST_TYPE) = 0u;
+            W(b + ST_RC) = 1u;
+            for (int s = 0; s < G.nslots; s++) W(b + ST_SLOTS + (uint32_t)s) = GEN_NIL;
+        }
+        // free bitmaps: StateEvents [0, x + seed), StreamEvents [0, n)
+        const uint32_t nst = (x ? 1u : 0u) + (seedN ? 1u : 0u);
+        for (uint32_t q = 0; q < (G.STCAP + 31) / 32; q++) W(G.offSTfree + q) = q == 0 ? ((1u << nst) - 1u) : 0u;
+        for (uint32_t q = 0; q < (G.SECAP + 31) / 32; q++) {
+            uint32_t m = 0;
+            if (n > 32 * q) m = (n >= 32 * (q + 1)) ? 0xffffffffu : ((1u << (n - 32 * q)) - 1u);
+            W(G.offSEfree + q) = m;
+        }
+        W(G.offDef) = 0u;
+    }
+
+    // ---- filter values (java_ops.h jo_eval): e1's chain at index c (StateEvent.getStreamEvent, the general
+    // kernel's chainAt: c >= 0 the c-th, -1 the last, -2 the one before it, else len + c)
+    __device__ __forceinline__ int chainIdx(int32_t c, uint32_t len) const {
+        if (c >= 0) return c < (int32_t)len ? c : -1;
+        if (c == -1) return len ? (int)len - 1 : -1;
+        if (c == -2) return len >= 2u ? (int)len - 2 : -1;
+        const int i = (int)len + c;
+        return i >= 0 ? i : -1;
+    }
+    __device__ __forceinline__ GVal word(const uint32_t (&ww)[NW], uint32_t nbits, uint32_t a) const {
+        const int ty = G.attrType[0][a];
+        const uint32_t o = G.absOff[a];
+        uint32_t lo = 0, hi = 0;
+#pragma unroll
+        for (int q = 0; q < NW; ++q) {
+            if ((uint32_t)q == o) lo = ww[q];
+            if ((uint32_t)q == o + 1) hi = ww[q];
+        }
+        const uint64_t b = (ty == SG_T_LONG || ty == SG_T_DOUBLE) ? ((uint64_t)lo | ((uint64_t)hi << 32)) : (uint64_t)lo;
+        return GVal{b, ((nbits >> a) & 1u) != 0};
+    }
+    __device__ __forceinline__ GVal chainAttr(int idx, uint32_t a) const {
+        // the word of attribute a of chain entry idx, selected without indexing the register arrays
+        const int ty = G.attrType[0][a];
+        const uint32_t o = G.absOff[a];
+        uint32_t lo = 0, hi = 0, nbits = 0;
+#pragma unroll
+        for (int j = 0; j < CNT_R; ++j) {
+            const bool here = j == idx;
+#pragma unroll
+            for (int q = 0; q < NW; ++q) {
+                lo = (here && (uint32_t)q == o) ? w[j][q] : lo;
+                hi = (here && (uint32_t)q == o + 1) ? w[j][q] : hi;
+            }
+            nbits = here ? nb[j] : nbits;
+        }
+        const uint64_t b = (ty == SG_T_LONG || ty == SG_T_DOUBLE) ? ((uint64_t)lo | ((uint64_t)hi << 32)) : (uint64_t)lo;
+        return GVal{b, ((nbits >> a) & 1u) != 0};
+    }
+    // filter of processor p on X: slot s0 = the chain [0, len), slot `evSlot` = the event alone (or none)
+    __device__ bool evalOn(int p, uint32_t len, int evSlot, const AbsEv<NW>& ev) {
+        const auto& P = G.pre[p];
+        if (P.flen == 0) return true;
+        const GVal v = jo_eval<false>(
+            G.code, P.fpc, P.flen, err,
+            [&](uint32_t s, uint32_t a, int32_t c) -> GVal {
+                if ((int)s == s0) {
+                    const int i = chainIdx(c, len);
+                    return i < 0 ? GVal{0, true} : chainAttr(i, a);
+                }
+                if ((int)s == evSlot && chainIdx(c, 1u) == 0) return word(ev.w, ev.nb, a);
+                return GVal{0, true};
+            },
+            [&](uint32_t s, int32_t c) -> bool {
+                if ((int)s == s0) return chainIdx(c, len) < 0;
+                if ((int)s == evSlot) return chainIdx(c, 1u) != 0;
+                return true;
+            });
+        return !v.null && (v.b & 1);
+    }
+
+    // ---- a match (QuerySelector input): X with e1's chain and the event in `evSlot` (Lane::project's record)
+    __device__ void project(const AbsEv<NW>& ev, uint32_t pos, int evSlot) {
+        if (resLeft == 0) {
+            const uint32_t sg = blockIdx.x % A.o.nseg;
+            resBase = (unsigned long long)sg * A.o.seg_cap + atomicAdd(&A.o.raw_count[sg], (unsigned long long)GEN_RESCHUNK);
+            resEnd = (unsigned long long)(sg + 1) * A.o.seg_cap;
+            resLeft = GEN_RESCHUNK;
+        }
+        const unsigned long long r = resBase++;
+        resLeft--;
+        matches++;
+        if (r >= resEnd) { err |= GERR_MATCHCAP; return; }
+        gu32* rec = gp(A.o.raw) + r * A.o.recWords;
+        rec[0] = pos;
+        rec[1] = trigRank++;
+        rec[2] = (uint32_t)ev.seq;
+        rec[3] = (uint32_t)(ev.seq >> 32);
+        rec[4] = (uint32_t)(uint64_t)xts;
+        rec[5] = (uint32_t)((uint64_t)xts >> 32);
+        rec[6] = k;
+        gu32* lens = rec + 7;
+        gu32* seqs = lens + G.nslots;
+        for (int s = 0; s < G.nslots; s++) lens[s] = s == s0 ? n : (s == evSlot ? 1u : 0u);
+#pragma unroll
+        for (int j = 0; j < CNT_R; ++j) {
+            if ((uint32_t)j < n) {
+                seqs[2 * (s0 * G.MC + j)] = (uint32_t)seq[j];
+                seqs[2 * (s0 * G.MC + j) + 1] = (uint32_t)(seq[j] >> 32);
+            }
+        }
+        seqs[2 * (evSlot * G.MC)] = (uint32_t)ev.seq;
+        seqs[2 * (evSlot * G.MC) + 1] = (uint32_t)(ev.seq >> 32);
+        gp(A.o.t_cnt)[pos] += 1;
+    }
+
+    // ---- one event of this key (SequenceMultiProcessStreamReceiver: stabilize, then pA, pB, p0)
+    __device__ void event(const AbsEv<NW>& ev, uint32_t pos) {
+        trigRank = 0;
+        // expireEvents over p0, pA, pB: X expires as a whole (one isExpired per StateEvent); found in p0's
+        // lists first, it is cloned into p0.newAndEvery by withinEvery and promoted — a clone the reset below
+        // drops again (only the creation counter sees it)
+        if (G.within != -1 && n > 0u) {
+            const int64_t d = ts[0] - ev.ts;
+            if ((d < 0 ? -d : d) > G.within) {
+                if ((inP0p || inP0n) && G.cntWE) created++;
+                n = 0;
+                inP0p = inP0n = inL = false;
+            }
+        }
+        // resetAndUpdate: the logical pair's pending lists clear (empty between events), p0's pending clears;
+        // p0 with nothing staged inits (`every`: a fresh seed); then p0's and the pair's staged entries are promoted
+        inP0p = false;
+        if (!(inP0n && n > 0u) && !seedN) {
+            seedN = true;
+            f0 |= GF_INIT;
+        }
+        const bool xP0 = inP0n && n > 0u, sP0 = seedN && !xP0, xL = inL && n > 0u;
+        inP0n = false;
+        seedN = false;
+        inL = false;
+        if (!xP0 && !xL) n = 0;  // a partial only p0's pending held dies at the reset
+        // pA, then pB: X in both pending lists (the partner's filled slot drops it from the second)
+        bool matched = false;
+        if (xL) {
+            scanned++;
+            fA &= ~(uint32_t)GF_CHANGED;
+            if (evalOn(pA, n, sA, ev)) {
+                fA |= GF_CHANGED;
+                xts = ev.ts;
+                project(ev, pos, sA);
+                matched = true;
+            }
+            scanned++;
+            if (!matched) {
+                fB &= ~(uint32_t)GF_CHANGED;
+                if (evalOn(pB, n, sB, ev)) {
+                    fB |= GF_CHANGED;
+                    xts = ev.ts;
+                    project(ev, pos, sB);
+                    matched = true;
+                }
+            }
+        }
+        // p0: X (its e2 / e3 slot filled: dropped; else the event joins the chain) or the seed
+        if (xP0 || sP0) {
+            scanned++;
+            if (xP0 && matched) {
+                n = 0;
+            } else {
+                if (sP0) n = 0;  // X (if any) was the pair's alone and has left it: the seed starts a chain
+                if (n >= (uint32_t)CNT_R) { err |= GERR_CHAIN; return; }
+#pragma unroll
+                for (int j = 0; j < CNT_R; ++j) {
+                    const bool here = (uint32_t)j == n;
+                    ts[j] = here ? ev.ts : ts[j];
+                    seq[j] = here ? ev.seq : seq[j];
+                    nb[j] = here ? ev.nb : nb[j];
+#pragma unroll
+                    for (int q = 0; q < NW; ++q) w[j][q] = here ? ev.w[q] : w[j][q];
+                }
+                const uint32_t len = n + 1u;
+                f0 &= ~(uint32_t)(GF_SUCCESS | GF_CHANGED);
+                if (evalOn(p0, len, -1, ev)) {  // CountPostStateProcessor
+                    f0 |= GF_SUCCESS;
+                    xts = ev.ts;
+                    n = len;
+                    if ((int32_t)len >= mn) {
+                        inL = true;
+                        if ((int32_t)len != mx) inP0n = true;
+                    }
+                    if ((int32_t)len == mx) f0 |= GF_CHANGED;
+                    inP0p = (f0 & GF_CHANGED) == 0u;
+                } else {
+                    // removeLastEvent, and SEQUENCE drops the partial from pending (a seed goes with it)
+                    if (sP0) n = 0;
+                }
+            }
+        } else if (matched) {
+            n = 0;
+        }
+        if (!inP0p && !inP0n && !inL) n = 0;
+    }
+};
+
+// ---- batch: one lane per key walks its events of the key-sorted batch ----
+template <int NW> __device__ void cnt_batch(const GenArgs& a) {
+    const uint32_t key = blockIdx.x * 64u + threadIdx.x;
+    uint32_t b = 0, e = 0;
+    if (key < a.K) {
+        b = gp(a.b.seg_begin)[key];
+        e = gp(a.b.seg_end)[key];
+    }
+    CntKey<NW> L(a, key < a.K ? key : 0u);
+    bool walk = b < e;
+    bool fb = false;
+    if (walk && !L.load()) {  // not this kernel's canonical state: the general kernel walks the whole run
+        fb = true;
+        walk = false;
+    }
+    unsigned long long ky = 0;
+    const int64_t tbase = a.b.pay ? gp(a.b.ts)[0] : 0;  // the payload's ts offsets are from the batch's first ts
+    if (walk) {
+        for (uint32_t i = b; i < e; i++) {
+            AbsEv<NW> ev;
+            uint32_t pos;
+            if (a.b.pay) {
+                abs_pay<NW>(a, i, tbase, ev);
+                pos = (uint32_t)(ev.seq - a.b.seq_base);
+            } else {
+                pos = a.b.sidx ? gp(a.b.sidx)[i] : i;
+                ev.ts = gp(a.b.ts)[pos];
+                ev.seq = a.b.seq_base + pos;
+                abs_gather<NW>(a, *(cGenProgram*)a.G, pos, ev);
+            }
+            L.event(ev, pos);
+        }
+        L.store();
+        ky = 1;
+    }
+    // unused reserved raw slots are marked empty (k_gen_scatter skips them)
+    for (uint32_t x = 0; x < L.resLeft; x++) {
+        const unsigned long long rr = L.resBase + x;
+        if (rr < L.resEnd) {
+            gp(a.o.raw)[rr * a.o.recWords] = 0xffffffffu;
+            gp(a.o.tk1)[rr] = 0xffffffffu;
+        }
+    }
+    abs_fallback(a, fb, key, b);
+    abs_wave_stats(a, L.scanned, L.created, L.matches, ky, L.err, fb ? 1ull : 0ull);
+}
+
+}  // namespace
+
+// One kernel per captured-word count (NW = the stream's attributes as 32-bit words, long / double 2 each).
+#define CNT_KERNELS(NW)                                                                                             \
+    extern "C" __global__ void __launch_bounds__(64) k_cnt_batch_##NW(const GenArgs* __restrict__ ap) {           \
+        cnt_batch<NW>(*ap);                                                                                         \
+    }
+CNT_KERNELS(1)
+CNT_KERNELS(2)
+CNT_KERNELS(3)
+CNT_KERNELS(4)
+CNT_KERNELS(5)
+CNT_KERNELS(6)
+CNT_KERNELS(7)
+CNT_KERNELS(8)

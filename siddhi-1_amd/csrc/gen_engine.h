@@ -51,6 +51,7 @@ __host__ __device__ inline size_t gen_at(uint32_t K, uint32_t blockWords, uint32
 #define GEN_RESCHUNK 4   // raw matches a lane reserves at a time
 #define ABS_R 8          // abs_kernels.hip: partials a key's register window holds
 #define ABS_MAXNW 8      // abs_kernels.hip: attribute words of an event it captures
+#define CNT_R 8          // cnt_kernels.hip: events a count chain in registers holds (the shape's max count)
 
 enum { GK_STREAM = 0, GK_COUNT = 1, GK_LOGICAL = 2 };
 
@@ -115,6 +116,13 @@ struct GenProgram {
     int32_t absOk, absP0, absP1, absEvery, absListener;
     uint32_t absNW;
     uint32_t absOff[GEN_MAXA];
+    // the counting sequence shape `every e1=S[f0]<m:n>, e2=S[fA] or e3=S[fB] [within W]` (SEQUENCE,
+    // partitioned, one stream), which runs on the register-window kernel of cnt_kernels.hip (gen_host.hip
+    // cnt_shape): cntP0 the count processor, cntPA / cntPB the logical OR pair in the order an event visits
+    // them (the receiver's reverse order), cntWE: p0's withinEvery is p0 itself (an expired partial of p0's
+    // lists is cloned into it, StreamPreStateProcessor.java:354-357); absNW / absOff give the word layout
+    int32_t cntOk, cntP0, cntPA, cntPB, cntWE;
+    uint32_t absWordAt[ABS_MAXNW];  // the StreamEvent record word (SE_ATTR + ...) of each captured word
 };
 
 // KeyState field offsets inside a processor's record

@@ -36,6 +36,10 @@ ABS_DECL(1) ABS_DECL(2) ABS_DECL(3) ABS_DECL(4) ABS_DECL(5) ABS_DECL(6) ABS_DECL
 typedef void (*AbsKernel)(const GenArgs*);
 static const AbsKernel kAbsBatch[ABS_MAXNW + 1] = {nullptr, k_abs_batch_1, k_abs_batch_2, k_abs_batch_3, k_abs_batch_4,
                                                    k_abs_batch_5, k_abs_batch_6, k_abs_batch_7, k_abs_batch_8};
+#define CNT_DECL(NW) extern "C" __global__ void k_cnt_batch_##NW(const GenArgs* ap);
+CNT_DECL(1) CNT_DECL(2) CNT_DECL(3) CNT_DECL(4) CNT_DECL(5) CNT_DECL(6) CNT_DECL(7) CNT_DECL(8)
+static const AbsKernel kCntBatch[ABS_MAXNW + 1] = {nullptr, k_cnt_batch_1, k_cnt_batch_2, k_cnt_batch_3, k_cnt_batch_4,
+                                                   k_cnt_batch_5, k_cnt_batch_6, k_cnt_batch_7, k_cnt_batch_8};
 static const AbsKernel kAbsTimers[ABS_MAXNW + 1] = {nullptr, k_abs_timers_1, k_abs_timers_2, k_abs_timers_3,
                                                     k_abs_timers_4, k_abs_timers_5, k_abs_timers_6, k_abs_timers_7,
                                                     k_abs_timers_8};
@@ -303,6 +307,73 @@ int prog_depth(const uint32_t* code, uint32_t pc, uint32_t n) {
     return mx;
 }
 
+// a filter the register-window kernels evaluate without a stack (jo_eval<false>)
+bool shallow(const GenProgram& G, const GenPre& P) {
+    const int d = prog_depth(G.code, P.fpc, P.flen);
+    return d >= 0 && d <= 2;
+}
+
+// the register-window kernels' word layout of stream 0's event (absOff / absNW: long and double take two words)
+bool reg_layout(GenProgram& G) {
+    uint32_t o = 0;
+    for (int a = 0; a < G.nattr[0]; a++) {
+        G.absOff[a] = o;
+        const bool wide = G.attrType[0][a] == SG_T_LONG || G.attrType[0][a] == SG_T_DOUBLE;
+        if (o < ABS_MAXNW) G.absWordAt[o] = SE_ATTR + 2 * (uint32_t)a;
+        if (wide && o + 1 < ABS_MAXNW) G.absWordAt[o + 1] = SE_ATTR + 2 * (uint32_t)a + 1;
+        o += wide ? 2u : 1u;
+    }
+    if (o == 0 || o > ABS_MAXNW) return false;
+    G.absNW = o;
+    return true;
+}
+
+// the counting sequence shape of cnt_kernels.hip:
+//     every e1=S[f0]<m:n>, e2=S[fA] or e3=S[fB] [within W]      (SEQUENCE, partitioned, one stream)
+// with the processors wired as StateInputStreamParser wires that query (a count state inside `every`, its
+// post processor feeding a logical OR pair whose post processors reach the selector); 1 <= m, n <= CNT_R.
+// Anything else stays on the general kernels.
+void cnt_shape(GenProgram& G) {
+    G.cntOk = 0;
+    if (G.qtype != SG_Q_SEQUENCE || !G.partitioned || G.nstreams != 1 || G.nprocs != 3 || G.nslots != 3 ||
+        G.nStartup != 0)
+        return;
+    const GenRecv& R = G.recv[0];
+    if (R.n != 3 || R.nStateProcs != 3) return;
+    const int p0 = R.procs[0], pA = R.procs[2], pB = R.procs[1];  // an event visits procs[2], [1], [0]
+    const GenPre &P0 = G.pre[p0], &PA = G.pre[pA], &PB = G.pre[pB];
+    const GenPost &Q0 = G.post[p0], &QA = G.post[pA], &QB = G.post[pB];
+    if (P0.kind != GK_COUNT || P0.absent || !P0.isStart || P0.minCount < 1 || P0.maxCount > CNT_R ||
+        P0.minCount > P0.maxCount || P0.countPost != p0)
+        return;
+    if (PA.kind != GK_LOGICAL || PB.kind != GK_LOGICAL || PA.absent || PB.absent || PA.isStart || PB.isStart ||
+        PA.logicalType != SG_L_OR || PB.logicalType != SG_L_OR || PA.partner != pB || PB.partner != pA)
+        return;
+    if (Q0.nextStatePre != pA && Q0.nextStatePre != pB) return;
+    if (Q0.nextEveryStatePre != p0 || Q0.callbackPre != GEN_NONE || Q0.hasNext) return;
+    for (const GenPost* Q : {&QA, &QB})
+        if (Q->nextStatePre != GEN_NONE || Q->nextEveryStatePre != GEN_NONE || Q->callbackPre != GEN_NONE || !Q->hasNext)
+            return;
+    if (PA.withinEvery != GEN_NONE || PB.withinEvery != GEN_NONE || (P0.withinEvery != GEN_NONE && P0.withinEvery != p0))
+        return;
+    // expiry visits p0 first (its expired partial is the one withinEvery clones)
+    if (G.nAll != 3 || G.allProcs[0] != p0) return;
+    if (G.within != -1 && (G.nStartIds != 1 || G.startIds[0] != P0.stateId)) return;
+    if (G.slotStream[P0.stateId] != 0 || G.slotStream[PA.stateId] != 0 || G.slotStream[PB.stateId] != 0) return;
+    if (P0.stateId == PA.stateId || P0.stateId == PB.stateId || PA.stateId == PB.stateId) return;
+    // CountPreStateProcessor drops a partial once slot stateId + 1 or + 2 is filled (:97-103): the logical
+    // pair's slots
+    const int s1 = P0.stateId + 1, s2 = P0.stateId + 2;
+    if (!((PA.stateId == s1 && PB.stateId == s2) || (PA.stateId == s2 && PB.stateId == s1))) return;
+    if ((uint32_t)P0.maxCount > G.MC) return;
+    if (!shallow(G, P0) || !shallow(G, PA) || !shallow(G, PB) || !reg_layout(G)) return;
+    G.cntP0 = p0;
+    G.cntPA = pA;
+    G.cntPB = pB;
+    G.cntWE = P0.withinEvery == p0 ? 1 : 0;
+    G.cntOk = getenv("SG_NO_CNT") ? 0 : 1;  // (SG_NO_CNT: A/B timing against the general kernels; same results)
+}
+
 // the absent-tail shape of abs_kernels.hip: `[every] e1=S[f0] -> not S[f1] for T [within W]` with the
 // processors wired exactly as the kernels restate them (anything else stays on the general kernels)
 void abs_shape(GenProgram& G) {
@@ -324,16 +395,7 @@ void abs_shape(GenProgram& G) {
         return;
     if (G.nStartup != 1 || G.startup[0] != 1 || G.MC != 1 || P0.stateId == P1.stateId) return;
     if (G.slotStream[P0.stateId] != 0 || G.slotStream[P1.stateId] != 0) return;
-    if (prog_depth(G.code, P0.fpc, P0.flen) < 0 || prog_depth(G.code, P0.fpc, P0.flen) > 2 ||
-        prog_depth(G.code, P1.fpc, P1.flen) < 0 || prog_depth(G.code, P1.fpc, P1.flen) > 2)
-        return;
-    uint32_t o = 0;
-    for (int a = 0; a < G.nattr[0]; a++) {
-        G.absOff[a] = o;
-        o += (G.attrType[0][a] == SG_T_LONG || G.attrType[0][a] == SG_T_DOUBLE) ? 2u : 1u;
-    }
-    if (o == 0 || o > ABS_MAXNW) return;
-    G.absNW = o;
+    if (!shallow(G, P0) || !shallow(G, P1) || !reg_layout(G)) return;
     G.absP0 = 0;
     G.absP1 = 1;
     G.absEvery = Q0.nextEveryStatePre == 0 ? 1 : 0;
@@ -417,6 +479,7 @@ GenProgram* gen_build_program(const uint32_t* w, size_t nw, uint32_t partialCap)
         off += 1 + 2 * G->DEF;
         G->blockWords = (off + (1u << GEN_GRAN_LOG2) - 1u) & ~((1u << GEN_GRAN_LOG2) - 1u);  // whole granules
         abs_shape(*G);
+        cnt_shape(*G);
         return G;
     } catch (...) {
         delete G;
@@ -959,7 +1022,7 @@ GenEngine* gen_create(const uint32_t* ir, size_t nw, const sg_config& cfg, hipSt
             }
         }
         e->live = e->dalloc<unsigned long long>(1);
-        if (G.absOk) {
+        if (G.absOk || G.cntOk) {
             e->fb_list = e->dalloc<uint32_t>(K);
             e->fb_start = e->dalloc<uint32_t>(K);
             e->fb_n = e->dalloc<unsigned long long>(1);
@@ -1017,7 +1080,7 @@ static size_t type_size(int t) {
 // the kernels read their arguments from a device ring (GEN_ARG_SLOTS slots, staged through pinned host
 // memory on the engine's stream); a slot is rewritten only after the stream has drained the launches
 // that used it
-enum { GEN_L_BATCH = 0, GEN_L_TIMERS = 1, GEN_L_DEADLINES = 2, GEN_L_ABS_BATCH = 3, GEN_L_ABS_TIMERS = 4 };
+enum { GEN_L_BATCH = 0, GEN_L_TIMERS = 1, GEN_L_DEADLINES = 2, GEN_L_ABS_BATCH = 3, GEN_L_ABS_TIMERS = 4, GEN_L_CNT_BATCH = 5 };
 // the general kernels over the keys a register-window kernel handed over: a fixed grid striding the list
 #define GEN_FB_BLOCKS 1024u
 // timer sweeps: a fixed grid of one-wave blocks striding over the due keys (their number is on the device)
@@ -1036,6 +1099,8 @@ static uint32_t gen_kpl(uint32_t K) {
 static bool abs_on(const GenEngine* e) {
     return e->host.absOk && e->host.projN == 0 && e->fb_list && e->tstage && e->keyorder;
 }
+// the register-window kernel of cnt_kernels.hip runs this query (the shape, no device projection)
+static bool cnt_on(const GenEngine* e) { return e->host.cntOk && e->host.projN == 0 && e->fb_list; }
 
 static void launch_gen(GenEngine* e, GenArgs a, int which) {
     const uint32_t blocks = (e->K + 63) / 64;
@@ -1051,10 +1116,12 @@ static void launch_gen(GenEngine* e, GenArgs a, int which) {
         hipLaunchKernelGGL(k_gen_timers, dim3(fb ? GEN_FB_BLOCKS : e->host.partitioned ? std::min(blocks, GEN_TIMER_BLOCKS) : 1u),
                            dim3(64), 0, e->stream, ap);
     else if (which == GEN_L_DEADLINES) hipLaunchKernelGGL(k_gen_deadlines, dim3(blocks), dim3(64), 0, e->stream, ap);
-    else if (which == GEN_L_ABS_BATCH || which == GEN_L_ABS_TIMERS) {
+    else if (which == GEN_L_ABS_BATCH || which == GEN_L_ABS_TIMERS || which == GEN_L_CNT_BATCH) {
         // one lane per key / possible due slot (the due count is on the device); then the waves' counter rows
-        hipLaunchKernelGGL(which == GEN_L_ABS_BATCH ? kAbsBatch[e->host.absNW] : kAbsTimers[e->host.absNW], dim3(blocks),
-                           dim3(64), 0, e->stream, ap);
+        hipLaunchKernelGGL(which == GEN_L_ABS_BATCH   ? kAbsBatch[e->host.absNW]
+                           : which == GEN_L_CNT_BATCH ? kCntBatch[e->host.absNW]
+                                                      : kAbsTimers[e->host.absNW],
+                           dim3(blocks), dim3(64), 0, e->stream, ap);
         hipLaunchKernelGGL(k_gen_stats_reduce, dim3(GST_N), dim3(256), 0, e->stream, e->wstats, blocks, e->stats);
     }
     else hipLaunchKernelGGL(k_gen_batch, dim3(fb ? GEN_FB_BLOCKS : (e->K + 64u * a.kpl - 1) / (64u * a.kpl)), dim3(64), 0,
@@ -1130,7 +1197,7 @@ int gen_push(GenEngine* e, const sg_batch* b, std::string& msg) {
         PackSrc ps{};
         uint32_t W = 0;
         bool nul = false;
-        if (abs_on(e)) {
+        if (abs_on(e) || cnt_on(e)) {
             const int st = (int)b->stream;
             for (int c = 0; c < G.nattr[st] && W <= 4; c++) {
                 const int t = G.attrType[st][c];
@@ -1156,7 +1223,7 @@ int gen_push(GenEngine* e, const sg_batch* b, std::string& msg) {
             }
             ps.ts = a.b.ts;
         }
-        if (abs_on(e) && W >= 1 && W <= 4) {
+        if ((abs_on(e) || cnt_on(e)) && W >= 1 && W <= 4) {
             size_t tmp = e->paysort_tmp_bytes;
             GH_OK(sgd_sort_payload((int)W, e->paysort_tmp, tmp, keys, e->skeys, ps, e->pay, n, bits, e->stream));
             a.b.pay = e->pay;
@@ -1202,6 +1269,16 @@ int gen_push(GenEngine* e, const sg_batch* b, std::string& msg) {
         e->st.advance_launches++;
         if (!dev) GH_OK(hipStreamSynchronize(e->stream));
         return SG_OK;
+    }
+    if (cnt_on(e)) {
+        // the register-window kernel, then the general kernel over the keys it handed over (whole runs);
+        // both write raw records + per-trigger counts, ordered below
+        GH_OK(hipMemsetAsync(e->fb_n, 0, 8, e->stream));
+        a.fb_list = e->fb_list;
+        a.fb_n = e->fb_n;
+        a.fb_start = e->fb_start;
+        launch_gen(e, a, GEN_L_CNT_BATCH);
+        a.mode = GEN_M_KEYLIST;
     }
     launch_gen(e, a, GEN_L_BATCH);
     // order: out_count + t_off[trigger] + rank
