@@ -82,6 +82,16 @@ typedef struct sg_config {
     uint32_t partial_capacity; /* max live partial matches per key */
     uint32_t flags;            /* SG_CFG_* */
     uint64_t match_capacity;   /* max matches held between two polls */
+    /* Multi-GPU fan-out inside the engine (replaces the per-key routing of
+     * PartitionStreamReceiver.java:262-272 across processes): n_devices > 1 HIP devices listed in devices[]
+     * (device above is then ignored).  A partitioned query's keys are sharded key % n_devices (local id
+     * key / n_devices) over one engine per device; every entry point keeps its meaning for the whole key
+     * range, polls merge the shards' matches into the single engine's order and return host memory
+     * (sg_sharded.cpp).  0 or 1: one device.  A caller built against the header without these two fields
+     * passes the smaller struct_size and gets one device. */
+    uint32_t n_devices;
+    uint32_t reserved;
+    const int32_t* devices;
 } sg_config;
 
 /* One micro-batch of events of ONE input stream, in arrival order (columnar / SoA). */

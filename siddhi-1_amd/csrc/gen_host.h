@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <string>
+#include <vector>
 
 #include "../../include/siddhi_gpu.h"
 
@@ -24,6 +25,12 @@ int gen_get_projection(GenEngine* e, uint32_t mem, sg_projection* out, std::stri
 void gen_release(GenEngine* e);
 void gen_stats(GenEngine* e, sg_stats* out);
 void gen_synchronize(GenEngine* e);
+// the multi-device fan-out (sg_sharded.cpp) merges the shards' timer matches in the single engine's order:
+// with keep = true every advance records, for each key that emitted, its queue head at that advance (the
+// listener's TreeMultimap order, Scheduler.java:78-99), in the key order the engine emitted them.
+// false = the engine does not order timer matches by key heads (not partitioned playback with one listener)
+bool gen_keep_timer_heads(GenEngine* e, bool keep);
+void gen_timer_heads(const GenEngine* e, std::vector<uint32_t>& keys, std::vector<int64_t>& heads);
 // device NFA state as a flat image (snapshot/restore, sg_engine.hip): the per-key state blocks plus the
 // clock fields.  gen_state_words = words of the block image (blockWords * K).
 struct GenClock { int64_t now, last_event_ts; uint32_t advanced, pad; };

@@ -780,6 +780,10 @@ struct TimerLess {
 #define GEN_ARG_SLOTS 64
 
 struct GenEngine {
+    // gen_keep_timer_heads: the last advance's emitting keys in head order and their heads (host copies)
+    bool keep_heads = false;
+    std::vector<uint32_t> head_keys;
+    std::vector<int64_t> head_t;
     GenProgram host{};
     GenProgram* dprog = nullptr;
     hipStream_t stream = nullptr;
@@ -1298,8 +1302,20 @@ int gen_push(GenEngine* e, const sg_batch* b, std::string& msg) {
     return SG_OK;
 }
 
+bool gen_keep_timer_heads(GenEngine* e, bool keep) {
+    e->keep_heads = keep && e->keyorder;
+    return e->keyorder;
+}
+
+void gen_timer_heads(const GenEngine* e, std::vector<uint32_t>& keys, std::vector<int64_t>& heads) {
+    keys = e->head_keys;
+    heads = e->head_t;
+}
+
 int gen_advance(GenEngine* e, int64_t t, std::string& msg) {
     const GenProgram& G = e->host;
+    e->head_keys.clear();
+    e->head_t.clear();
     if (G.playback) {
         // TimestampGeneratorImpl.setCurrentTimestamp ignores a time earlier than the last one
         if (e->advanced && t < e->lastEventTs) return SG_OK;
@@ -1369,6 +1385,18 @@ int gen_advance(GenEngine* e, int64_t t, std::string& msg) {
                 size_t tmp = e->ksort_tmp_bytes;
                 GH_OK(rocprim::radix_sort_pairs<KeySortConfig>(e->ksort_tmp, tmp, e->hkey_c, e->hkey_s, e->kid_c, e->skid,
                                                                n, 0, 64, e->stream));
+            }
+            if (e->keep_heads) {  // (the sorted keys and their heads, for the multi-device merge)
+                std::vector<uint32_t> rel(n);
+                std::vector<unsigned long long> hk(n);
+                e->head_keys.resize(n);
+                GH_OK(hipMemcpyAsync(e->head_keys.data(), e->skid, n * 4, hipMemcpyDeviceToHost, e->stream));
+                if (!kctr[1]) GH_OK(hipMemcpyAsync(rel.data(), e->srel, n * 4, hipMemcpyDeviceToHost, e->stream));
+                else GH_OK(hipMemcpyAsync(hk.data(), e->hkey_s, n * 8, hipMemcpyDeviceToHost, e->stream));
+                GH_OK(hipStreamSynchronize(e->stream));
+                e->head_t.resize(n);
+                for (size_t i = 0; i < n; i++)
+                    e->head_t[i] = !kctr[1] ? t + 1 - (int64_t)rel[i] : (int64_t)(hk[i] ^ (1ull << 63));
             }
             hipLaunchKernelGGL(k_timer_cnt, g, dim3(256), 0, e->stream, e->skid, (uint64_t)n, e->tm.kcnt, e->kc);
             size_t st = e->kscan_tmp_bytes;

@@ -37,6 +37,7 @@
 #include "grp.h"
 #include "pack.h"
 #include "pinned.h"
+#include "sg_sharded.h"
 #include "state_doc.h"
 #include "sg_engine.h"
 #include "sg_jit.h"
@@ -153,6 +154,7 @@ hipError_t sgd_sort_payload(int W, void* tmp, size_t& tmp_bytes, const uint32_t*
 
 
 struct sg_engine {
+    ShardEngine* shard = nullptr;   // n_devices > 1: the multi-device fan-out (sg_sharded.cpp) behind this handle
     int device = 0;
     hipStream_t stream = nullptr;
     GenEngine* gen = nullptr;  // the general engine, when the query is not a two-state pattern
@@ -1318,6 +1320,13 @@ int set_projection(sg_engine* e, const uint32_t* code, uint32_t words, const uin
 // the other host-side translation units (sg_dict.cpp) report through the same sg_last_error
 int sg_set_error(int code, const char* msg) { return fail(code, msg); }
 
+bool sg_internal_keep_heads(sg_engine* e) { return e && e->gen ? gen_keep_timer_heads(e->gen, true) : false; }
+void sg_internal_heads(sg_engine* e, std::vector<uint32_t>& keys, std::vector<int64_t>& heads) {
+    keys.clear();
+    heads.clear();
+    if (e && e->gen) gen_timer_heads(e->gen, keys, heads);
+}
+
 extern "C" {
 
 const char* sg_last_error(void) { return g_err.c_str(); }
@@ -1325,7 +1334,27 @@ int sg_abi_version(void) { return SG_ABI_VERSION; }
 
 int sg_engine_create(const void* ir, size_t ir_len, const sg_config* cfg, sg_engine** out) {
     if (!ir || !out || !cfg) return fail(SG_ERR_INVALID, "null argument");
-    if (cfg->struct_size < sizeof(sg_config)) return fail(SG_ERR_INVALID, "sg_config too small");
+    // (the fields before n_devices are the round-2 sg_config: such a caller gets one device)
+    if (cfg->struct_size < offsetof(sg_config, n_devices)) return fail(SG_ERR_INVALID, "sg_config too small");
+    sg_config full{};
+    memcpy(&full, cfg, std::min<size_t>(cfg->struct_size, sizeof(sg_config)));
+    full.struct_size = sizeof(sg_config);
+    if (cfg->struct_size < sizeof(sg_config)) {
+        full.n_devices = 1;
+        full.devices = nullptr;
+    }
+    cfg = &full;
+    if (cfg->n_devices > 1) {
+        if (!cfg->devices) return fail(SG_ERR_INVALID, "n_devices > 1 needs the devices list");
+        int rc = SG_OK;
+        ShardEngine* sh = shd_create(ir, ir_len, cfg, &rc);
+        if (!sh) return rc;
+        sg_engine* e = new sg_engine();
+        e->shard = sh;
+        e->cfg = *cfg;
+        *out = e;
+        return SG_OK;
+    }
     sg_engine* e = nullptr;
     try {
         e = new sg_engine();
@@ -1406,10 +1435,17 @@ int sg_engine_create(const void* ir, size_t ir_len, const sg_config* cfg, sg_eng
     }
 }
 
-void sg_engine_destroy(sg_engine* e) { delete e; }
+void sg_engine_destroy(sg_engine* e) {
+    if (e && e->shard) {
+        shd_destroy(e->shard);
+        e->shard = nullptr;
+    }
+    delete e;
+}
 
 int sg_push_batch(sg_engine* e, const sg_batch* b) {
     if (!e || !b) return fail(SG_ERR_INVALID, "null argument");
+    if (e->shard) return shd_push(e->shard, b);
     try {
         HIP_OK(hipSetDevice(e->device));
         if (e->gen) {
@@ -1425,6 +1461,7 @@ int sg_push_batch(sg_engine* e, const sg_batch* b) {
 
 int sg_advance_time(sg_engine* e, int64_t now_ms) {
     if (!e) return fail(SG_ERR_INVALID, "null argument");
+    if (e->shard) return shd_advance(e->shard, now_ms);
     if (!e->gen) return SG_OK;  // the two-state kernel's shapes have no timers
     try {
         HIP_OK(hipSetDevice(e->device));
@@ -1440,6 +1477,8 @@ int sg_set_projection(sg_engine* e, const uint32_t* code, uint32_t code_words, c
                       const uint32_t* item_len, const uint32_t* item_type, uint32_t n_items, const int32_t* part_attr,
                       uint32_t n_streams) {
     if (!e || !code || !item_pc || !item_len || !item_type) return fail(SG_ERR_INVALID, "null argument");
+    if (e->shard)
+        return shd_set_projection(e->shard, code, code_words, item_pc, item_len, item_type, n_items, part_attr, n_streams);
     try {
         HIP_OK(hipSetDevice(e->device));
         if (e->gen) {
@@ -1455,6 +1494,7 @@ int sg_set_projection(sg_engine* e, const uint32_t* code, uint32_t code_words, c
 
 int sg_get_projection(sg_engine* e, uint32_t mem, sg_projection* out) {
     if (!e || !out) return fail(SG_ERR_INVALID, "null argument");
+    if (e->shard) return shd_get_projection(e->shard, mem, out);
     try {
         HIP_OK(hipSetDevice(e->device));
         if (e->gen) {
@@ -1494,6 +1534,7 @@ int sg_get_projection(sg_engine* e, uint32_t mem, sg_projection* out) {
 
 int sg_wait_stream(sg_engine* e, void* stream) {
     if (!e) return fail(SG_ERR_INVALID, "null argument");
+    if (e->shard) return shd_wait_stream(e->shard, stream);
     try {
         HIP_OK(hipSetDevice(e->device));
         hipEvent_t x = e->ev();
@@ -1508,6 +1549,7 @@ int sg_wait_stream(sg_engine* e, void* stream) {
 
 int sg_poll_matches(sg_engine* e, uint32_t mem, sg_match_batch* out) {
     if (!e || !out) return fail(SG_ERR_INVALID, "null argument");
+    if (e->shard) return shd_poll(e->shard, mem, out);
     try {
         HIP_OK(hipSetDevice(e->device));
         if (e->gen) {  // (the general engine's polls always wait for every pushed batch)
@@ -1523,6 +1565,7 @@ int sg_poll_matches(sg_engine* e, uint32_t mem, sg_match_batch* out) {
 
 int sg_release_matches(sg_engine* e, sg_match_batch* m) {
     if (!e) return fail(SG_ERR_INVALID, "null argument");
+    if (e->shard) return shd_release(e->shard, m);
     if (e->gen) gen_release(e->gen);
     else if (e->held) e->win += e->polled;  // those ring records are free again
     e->held = false;
@@ -1532,6 +1575,7 @@ int sg_release_matches(sg_engine* e, sg_match_batch* m) {
 
 int sg_synchronize(sg_engine* e) {
     if (!e) return fail(SG_ERR_INVALID, "null argument");
+    if (e->shard) return shd_synchronize(e->shard);
     try {
         HIP_OK(hipSetDevice(e->device));
         if (e->gen) {
@@ -1548,6 +1592,7 @@ int sg_synchronize(sg_engine* e) {
 
 int sg_get_stats(sg_engine* e, sg_stats* out) {
     if (!e || !out) return fail(SG_ERR_INVALID, "null argument");
+    if (e->shard) return shd_stats(e->shard, out);
     try {
         HIP_OK(hipSetDevice(e->device));
         if (e->gen) {
@@ -1581,6 +1626,7 @@ int sg_get_stats(sg_engine* e, sg_stats* out) {
 int sg_reset_keys(sg_engine* e, const uint32_t* keys, uint64_t n, uint32_t mem) {
     if (!e || (!keys && n)) return fail(SG_ERR_INVALID, "null argument");
     if (n == 0) return SG_OK;
+    if (e->shard) return shd_reset_keys(e->shard, keys, n, mem);
     if (n >= (1ull << 32)) return fail(SG_ERR_INVALID, "too many keys in one reset");
     try {
         HIP_OK(hipSetDevice(e->device));
@@ -1664,6 +1710,7 @@ static bool outputs_pending(sg_engine* e) {
 
 int sg_snapshot(sg_engine* e, void** buf, size_t* len) {
     if (!e || !buf || !len) return fail(SG_ERR_INVALID, "null argument");
+    if (e->shard) return shd_snapshot(e->shard, buf, len);
     try {
         HIP_OK(hipSetDevice(e->device));
         SnapHeader h{};
@@ -1737,6 +1784,7 @@ int sg_snapshot(sg_engine* e, void** buf, size_t* len) {
 
 int sg_restore(sg_engine* e, const void* buf, size_t len) {
     if (!e || !buf) return fail(SG_ERR_INVALID, "null argument");
+    if (e->shard) return shd_restore(e->shard, buf, len);
     SnapHeader h;
     if (len < sizeof(h)) return fail(SG_ERR_INVALID, "snapshot too short");
     memcpy(&h, buf, sizeof(h));
@@ -1943,6 +1991,7 @@ static int twostate_import(sg_engine* e, const SdDoc& d) {
 
 int sg_state_export(sg_engine* e, void** buf, size_t* len) {
     if (!e || !buf || !len) return fail(SG_ERR_INVALID, "null argument");
+    if (e->shard) return shd_state_export(e->shard, buf, len);
     try {
         HIP_OK(hipSetDevice(e->device));
         SdDoc d;
@@ -1968,6 +2017,7 @@ int sg_state_export(sg_engine* e, void** buf, size_t* len) {
 
 int sg_state_import(sg_engine* e, const void* buf, size_t len) {
     if (!e || !buf) return fail(SG_ERR_INVALID, "null argument");
+    if (e->shard) return shd_state_import(e->shard, buf, len);
     SdDoc d;
     try {
         d = sd_read(buf, len);

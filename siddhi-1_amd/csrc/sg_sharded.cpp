@@ -1,0 +1,751 @@
+// sg_sharded.cpp — multi-device fan-out inside one engine (SURVEY §8b "Multi-GPU fan-out is internal to one
+// engine", §8e).  An sg_engine created with sg_config.n_devices > 1 owns one engine per listed device and
+// forwards every entry point here, so a caller bound to siddhi_gpu.h (the JNI shim of INTEGRATION.md) drives
+// several GPUs through the same handle.
+//
+// Partition keys shard because no processor reads another key's state (PartitionStateHolder.java:43-49;
+// PartitionStreamReceiver.java:262-272 routes each event to its key's runtime).  Key ids are dense in first-seen
+// order, so consecutive ids are unrelated keys: shard r = key % N owns a key and sees it as local id key / N,
+// dense in [0, ceil(n_keys / N)).  A batch is split stably by owner (per key the arrival order is kept); each
+// shard numbers its events with its own arrival seqs (dense: 0, 1, 2, ...) and this engine keeps the map back to
+// the global seqs, so polls return global trigger / slot seqs and global key ids, merged into the single
+// engine's order: batch matches by (trigger seq, emission order) — all matches of one trigger come from the shard
+// owning the trigger's key — and the timer matches of an advance key by key in the order of the keys' queue
+// heads (the Scheduler listener's TreeMultimap order, Scheduler.java:78-99: each shard reports its emitting keys'
+// heads; two keys sharing a due time, on one shard or across two, is the collapse the single engine refuses,
+// SURVEY A.10), or by (fire time, key) for the engines that do not order by heads.  Matches are collected from
+// the shards before and right after every advance, so batch and timer matches keep the single engine's
+// interleaving.  The playback / wall clock is global: every shard gets the same advance_time sequence.  An unpartitioned query
+// (n_keys == 1) does not shard: one key's NFA is sequential, it runs on the first device.
+//
+// Shards are driven concurrently, one host thread per device per call (each sub-engine is used by one thread at
+// a time, as siddhi_gpu.h requires).  Device batches are staged to host memory and split there; polls return
+// host memory only (the bench's multi-GPU path reshards on the devices with RCCL instead, bench.py).
+#include "sg_sharded.h"
+
+#include <string.h>
+
+#include <algorithm>
+#include <functional>
+#include <future>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include <hip/hip_runtime.h>
+
+#include "../../include/siddhi_gpu_ir.h"
+#include "state_doc.h"
+
+namespace {
+
+struct ShardError : std::runtime_error {
+    int code;
+    ShardError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+size_t tsize(uint32_t t) {
+    switch (t) {
+    case SG_T_LONG: case SG_T_DOUBLE: return 8;
+    case SG_T_BOOL: return 1;
+    default: return 4;
+    }
+}
+
+const uint64_t kMagic = 0x3148534753ull;  // "SGSH1"
+
+}  // namespace
+
+struct ShardEngine {
+    uint32_t N = 1, K = 1, KL = 1;   // shards, global / local key ranges
+    bool null_keys = false;
+    std::vector<sg_engine*> sh;
+    std::vector<std::vector<uint32_t>> attr_types;   // per stream of the IR
+    std::vector<std::vector<uint64_t>> gmap;         // per shard: global seq of each local seq
+    // matches in host memory, in the single engine's order: `pend` collects them as the shards produce them
+    // (batch matches before every advance, timer matches right after it), a poll hands `pend` out as `out`
+    struct Out {
+        uint64_t n = 0;
+        uint32_t ns = 0, mc = 1, ni = 0;
+        std::vector<uint64_t> trig, slot, pval;
+        std::vector<uint32_t> key, len;
+        std::vector<int64_t> ts;
+        std::vector<uint8_t> pnull;
+    };
+    Out pend, out;
+    bool held = false;
+    bool proj = false;
+    bool heads = false;   // every shard orders its timer matches by the keys' queue heads (and reports them)
+
+    // run fn(r) for every shard, concurrently when there are several; the first failure is rethrown here
+    void each(const std::function<int(uint32_t)>& fn) {
+        std::vector<int> rc(N, SG_OK);
+        std::vector<std::string> msg(N);
+        auto run = [&](uint32_t r) {
+            try {
+                rc[r] = fn(r);
+                if (rc[r] != SG_OK) msg[r] = sg_last_error();   // (the error text is per thread)
+            } catch (const ShardError& ex) {
+                rc[r] = ex.code;
+                msg[r] = ex.what();
+            } catch (const std::exception& ex) {
+                rc[r] = SG_ERR_DEVICE;
+                msg[r] = ex.what();
+            }
+        };
+        if (N == 1) {
+            run(0);
+        } else {
+            std::vector<std::future<void>> fs;
+            for (uint32_t r = 1; r < N; r++) fs.push_back(std::async(std::launch::async, run, r));
+            run(0);
+            for (auto& f : fs) f.get();
+        }
+        for (uint32_t r = 0; r < N; r++)
+            if (rc[r] != SG_OK) throw ShardError(rc[r], "shard " + std::to_string(r) + ": " + msg[r]);
+    }
+
+    uint64_t map_seq(uint32_t r, uint64_t local) const {
+        if (local >= SG_BLANK_SEQ) return local;   // null / blank / timer markers pass through
+        if (local >= gmap[r].size()) throw ShardError(SG_ERR_DEVICE, "shard seq outside its map");
+        return gmap[r][local];
+    }
+};
+
+namespace {
+
+int fail_from(const std::exception& ex) {
+    if (auto* s = dynamic_cast<const ShardError*>(&ex)) return sg_set_error(s->code, s->what());
+    return sg_set_error(SG_ERR_DEVICE, ex.what());
+}
+
+void parse_streams(ShardEngine* s, const uint32_t* w, size_t nw) {
+    if (nw < SG_IR_HDR_WORDS) throw ShardError(SG_ERR_INVALID, "IR too short");
+    const uint32_t ns = w[3];
+    size_t p = w[7];
+    for (uint32_t i = 0; i < ns; i++) {
+        if (p >= nw) throw ShardError(SG_ERR_INVALID, "IR stream table out of range");
+        const uint32_t na = w[p++];
+        if (p + na > nw) throw ShardError(SG_ERR_INVALID, "IR stream table out of range");
+        s->attr_types.emplace_back(w + p, w + p + na);
+        p += na;
+    }
+}
+
+// the staged host copy of a batch (device batches are copied first)
+struct HostBatch {
+    std::vector<std::vector<uint8_t>> store;
+    const int64_t* ts = nullptr;
+    const uint32_t* key = nullptr;
+    std::vector<const void*> cols;
+    std::vector<const uint8_t*> nulls;
+};
+
+HostBatch stage(const ShardEngine* s, const sg_batch* b) {
+    HostBatch h;
+    const uint64_t n = b->n;
+    h.cols.assign(b->n_cols, nullptr);
+    h.nulls.assign(b->n_cols, nullptr);
+    if (b->mem == SG_MEM_HOST) {
+        h.ts = b->ts;
+        h.key = b->key;
+        for (uint32_t c = 0; c < b->n_cols; c++) {
+            h.cols[c] = b->cols[c];
+            h.nulls[c] = b->nulls ? b->nulls[c] : nullptr;
+        }
+        return h;
+    }
+    auto copy = [&](const void* src, size_t bytes) -> const void* {
+        h.store.emplace_back(bytes);
+        if (bytes && hipMemcpy(h.store.back().data(), src, bytes, hipMemcpyDeviceToHost) != hipSuccess)
+            throw ShardError(SG_ERR_DEVICE, "staging a device batch failed");
+        return h.store.back().data();
+    };
+    h.ts = (const int64_t*)copy(b->ts, n * 8);
+    if (b->key) h.key = (const uint32_t*)copy(b->key, n * 4);
+    const auto& ty = s->attr_types[b->stream];
+    for (uint32_t c = 0; c < b->n_cols; c++) {
+        h.cols[c] = copy(b->cols[c], n * tsize(ty[c]));
+        if (b->nulls && b->nulls[c]) h.nulls[c] = (const uint8_t*)copy(b->nulls[c], n);
+    }
+    return h;
+}
+
+}  // namespace
+
+ShardEngine* shd_create(const void* ir, size_t ir_len, const sg_config* cfg, int* rc) {
+    std::unique_ptr<ShardEngine> s(new ShardEngine());
+    try {
+        parse_streams(s.get(), (const uint32_t*)ir, ir_len / 4);
+        s->K = cfg->n_keys ? cfg->n_keys : 1;
+        s->N = s->K > 1 ? cfg->n_devices : 1;
+        s->KL = (s->K + s->N - 1) / s->N;
+        s->null_keys = (cfg->flags & SG_CFG_NULL_KEYS) != 0;
+        s->gmap.resize(s->N);
+        s->sh.assign(s->N, nullptr);
+        for (uint32_t r = 0; r < s->N; r++) {
+            sg_config c = *cfg;
+            c.struct_size = sizeof(sg_config);
+            c.device = cfg->devices[r];
+            c.n_keys = s->K > 1 ? s->KL : 1;
+            c.n_devices = 1;
+            c.devices = nullptr;
+            const int e = sg_engine_create(ir, ir_len, &c, &s->sh[r]);
+            if (e != SG_OK) throw ShardError(e, std::string("shard ") + std::to_string(r) + ": " + sg_last_error());
+        }
+        s->heads = true;
+        for (uint32_t r = 0; r < s->N; r++) s->heads = sg_internal_keep_heads(s->sh[r]) && s->heads;
+        *rc = SG_OK;
+        return s.release();
+    } catch (const std::exception& ex) {
+        for (sg_engine* e : s->sh)
+            if (e) sg_engine_destroy(e);
+        s->sh.clear();
+        *rc = fail_from(ex);
+        return nullptr;
+    }
+}
+
+void shd_destroy(ShardEngine* s) {
+    if (!s) return;
+    for (sg_engine* e : s->sh)
+        if (e) sg_engine_destroy(e);
+    delete s;
+}
+
+int shd_push(ShardEngine* s, const sg_batch* b) {
+    try {
+        if (s->held) throw ShardError(SG_ERR_STATE, "release the polled matches before pushing");
+        if (b->stream >= s->attr_types.size()) throw ShardError(SG_ERR_INVALID, "stream index out of range");
+        if (b->n_cols != s->attr_types[b->stream].size())
+            throw ShardError(SG_ERR_INVALID, "column count does not match the stream");
+        if (b->n == 0) return SG_OK;
+        const uint64_t n = b->n;
+        if (s->N == 1) {   // (unpartitioned, or one device): the shard takes the batch as it is
+            sg_batch c = *b;
+            c.seq_base = s->gmap[0].size();
+            std::vector<uint64_t>& m = s->gmap[0];
+            const size_t m0 = m.size();
+            m.resize(m0 + n);
+            for (uint64_t i = 0; i < n; i++) m[m0 + i] = b->seq_base + i;
+            const int rc = sg_push_batch(s->sh[0], &c);
+            if (rc != SG_OK) {
+                m.resize(m0);
+                return rc;
+            }
+            return SG_OK;
+        }
+        if (!b->key) throw ShardError(SG_ERR_INVALID, "partitioned query needs key ids");
+        HostBatch h = stage(s, b);
+        const uint32_t N = s->N;
+        // owner of every event (null keys: dropped with SG_CFG_NULL_KEYS, else an error), per-shard counts
+        std::vector<uint32_t> cnt(N, 0);
+        for (uint64_t i = 0; i < n; i++) {
+            const uint32_t k = h.key[i];
+            if (k >= s->K) {
+                if (s->null_keys && k == SG_KEY_NULL) continue;
+                throw ShardError(SG_ERR_INVALID, "key id outside [0, n_keys)");
+            }
+            cnt[k % N]++;
+        }
+        const auto& ty = s->attr_types[b->stream];
+        const uint32_t nc = b->n_cols;
+        // per shard: the sub-batch columns (stable: arrival order within the shard)
+        struct Sub {
+            std::vector<int64_t> ts;
+            std::vector<uint32_t> key;
+            std::vector<std::vector<uint8_t>> cols, nulls;
+            std::vector<uint64_t> glob;
+        };
+        std::vector<Sub> sub(N);
+        for (uint32_t r = 0; r < N; r++) {
+            sub[r].ts.reserve(cnt[r]);
+            sub[r].key.reserve(cnt[r]);
+            sub[r].glob.reserve(cnt[r]);
+            sub[r].cols.resize(nc);
+            sub[r].nulls.resize(nc);
+            for (uint32_t c = 0; c < nc; c++) {
+                sub[r].cols[c].reserve((size_t)cnt[r] * tsize(ty[c]));
+                if (h.nulls[c]) sub[r].nulls[c].reserve(cnt[r]);
+            }
+        }
+        for (uint64_t i = 0; i < n; i++) {
+            const uint32_t k = h.key[i];
+            if (k >= s->K) continue;
+            Sub& u = sub[k % N];
+            u.ts.push_back(h.ts[i]);
+            u.key.push_back(k / N);
+            u.glob.push_back(b->seq_base + i);
+            for (uint32_t c = 0; c < nc; c++) {
+                const size_t sz = tsize(ty[c]);
+                const uint8_t* src = (const uint8_t*)h.cols[c] + i * sz;
+                u.cols[c].insert(u.cols[c].end(), src, src + sz);
+                if (h.nulls[c]) u.nulls[c].push_back(h.nulls[c][i]);
+            }
+        }
+        s->each([&](uint32_t r) -> int {
+            Sub& u = sub[r];
+            if (u.ts.empty()) return SG_OK;
+            std::vector<const void*> cp(nc);
+            std::vector<const uint8_t*> np(nc, nullptr);
+            bool anyNull = false;
+            for (uint32_t c = 0; c < nc; c++) {
+                cp[c] = u.cols[c].data();
+                if (h.nulls[c]) {
+                    np[c] = u.nulls[c].data();
+                    anyNull = true;
+                }
+            }
+            std::vector<uint64_t>& m = s->gmap[r];
+            sg_batch c{};
+            c.struct_size = sizeof(sg_batch);
+            c.stream = b->stream;
+            c.n = u.ts.size();
+            c.seq_base = m.size();
+            c.key = u.key.data();
+            c.ts = u.ts.data();
+            c.cols = cp.data();
+            c.nulls = anyNull ? np.data() : nullptr;
+            c.n_cols = nc;
+            c.mem = SG_MEM_HOST;
+            const int rc = sg_push_batch(s->sh[r], &c);
+            if (rc == SG_OK) m.insert(m.end(), u.glob.begin(), u.glob.end());
+            return rc;
+        });
+        return SG_OK;
+    } catch (const std::exception& ex) {
+        return fail_from(ex);
+    }
+}
+
+int shd_set_projection(ShardEngine* s, const uint32_t* code, uint32_t code_words, const uint32_t* item_pc,
+                       const uint32_t* item_len, const uint32_t* item_type, uint32_t n_items, const int32_t* part_attr,
+                       uint32_t n_streams) {
+    try {
+        s->each([&](uint32_t r) {
+            return sg_set_projection(s->sh[r], code, code_words, item_pc, item_len, item_type, n_items, part_attr,
+                                     n_streams);
+        });
+        s->proj = true;
+        return SG_OK;
+    } catch (const std::exception& ex) {
+        return fail_from(ex);
+    }
+}
+
+namespace {
+
+// every shard's matches since its last poll, mapped to global seqs / keys, merged and appended to s->pend:
+// timers = false: batch matches, by (trigger seq, the shard's emission order) — all matches of one trigger come
+// from the shard owning the trigger's key; timers = true: the timer matches of one advance, key by key in the
+// order of the keys' queue heads (each shard emitted its keys in that order; two shards' keys sharing a head is
+// the Scheduler collapse the single engine refuses), or by (fire time, key) for an engine that does
+// not order by heads
+void collect(ShardEngine* s, bool timers) {
+    const uint32_t N = s->N;
+    std::vector<ShardEngine::Out> parts(N);
+    std::vector<std::vector<uint32_t>> hk(N);
+    std::vector<std::vector<int64_t>> ht(N);
+    s->each([&](uint32_t r) -> int {
+        sg_match_batch m{};
+        int rc = sg_poll_matches(s->sh[r], SG_MEM_HOST, &m);
+        if (rc != SG_OK) return rc;
+        ShardEngine::Out& p = parts[r];
+        p.n = m.n;
+        p.ns = m.n_slots;
+        p.mc = m.max_chain ? m.max_chain : 1;
+        p.trig.resize(p.n);
+        p.key.resize(p.n);
+        p.ts.resize(p.n);
+        p.len.assign(m.chain_len, m.chain_len + p.n * p.ns);
+        p.slot.resize(p.n * p.ns * p.mc);
+        for (uint64_t i = 0; i < p.n; i++) {
+            p.trig[i] = m.trigger_seq[i] == SG_TIMER_SEQ ? SG_TIMER_SEQ : s->map_seq(r, m.trigger_seq[i]);
+            p.key[i] = N > 1 ? m.key[i] * N + r : m.key[i];
+            p.ts[i] = m.ts[i];
+        }
+        for (size_t j = 0; j < p.slot.size(); j++) p.slot[j] = s->map_seq(r, m.slot_seq[j]);
+        if (s->proj) {
+            sg_projection pr{};
+            rc = sg_get_projection(s->sh[r], SG_MEM_HOST, &pr);
+            if (rc != SG_OK) return rc;
+            p.ni = pr.n_items;
+            p.pval.assign(pr.value, pr.value + (size_t)pr.n_items * p.n);
+            p.pnull.assign(pr.null, pr.null + (size_t)pr.n_items * p.n);
+        }
+        if (timers && s->heads) sg_internal_heads(s->sh[r], hk[r], ht[r]);
+        return sg_release_matches(s->sh[r], &m);
+    });
+    struct Ref {
+        uint32_t r;
+        uint64_t i;
+        int64_t head;
+    };
+    std::vector<Ref> ord;
+    uint64_t total = 0;
+    for (uint32_t r = 0; r < N; r++) total += parts[r].n;
+    if (total == 0) return;
+    ord.reserve(total);
+    for (uint32_t r = 0; r < N; r++) {
+        const ShardEngine::Out& p = parts[r];
+        if (timers && s->heads) {
+            // the shard's output is its emitting keys' matches, key after key in head order (hk / ht)
+            size_t g = 0;
+            for (uint64_t i = 0; i < p.n; i++) {
+                const uint32_t lk = N > 1 ? p.key[i] / N : p.key[i];
+                if (i > 0 && p.key[i] != p.key[i - 1]) g++;
+                while (g < hk[r].size() && hk[r][g] != lk) g++;
+                if (g >= hk[r].size()) throw ShardError(SG_ERR_DEVICE, "timer match of a key without a recorded head");
+                ord.push_back({r, i, ht[r][g]});
+            }
+        } else {
+            for (uint64_t i = 0; i < p.n; i++) ord.push_back({r, i, 0});
+        }
+    }
+    std::stable_sort(ord.begin(), ord.end(), [&](const Ref& a, const Ref& b) {
+        const ShardEngine::Out &A = parts[a.r], &B = parts[b.r];
+        const bool ta = A.trig[a.i] == SG_TIMER_SEQ, tb = B.trig[b.i] == SG_TIMER_SEQ;
+        if (ta != tb) return ta;
+        if (ta && s->heads) return a.head < b.head;
+        if (ta) {
+            if (A.ts[a.i] != B.ts[b.i]) return A.ts[a.i] < B.ts[b.i];
+            return A.key[a.i] < B.key[b.i];
+        }
+        return A.trig[a.i] < B.trig[b.i];
+    });
+    if (timers && s->heads)
+        for (size_t x = 1; x < ord.size(); x++)
+            if (ord[x].r != ord[x - 1].r && ord[x].head == ord[x - 1].head)
+                throw ShardError(SG_ERR_UNSUPPORTED,
+                                 "two partition keys share a timer due time at one clock advance (reference Scheduler "
+                                 "collapse quirk, SURVEY A.10): input not supported");
+    // append to pend (the chain dimension grows to the widest shard's)
+    ShardEngine::Out& o = s->pend;
+    uint32_t mc = std::max(o.n ? o.mc : 1u, 1u), ns = 0, ni = o.n ? o.ni : 0;
+    for (const auto& p : parts)
+        if (p.n) {
+            mc = std::max(mc, p.mc);
+            ns = p.ns;
+            ni = std::max(ni, p.ni);
+        }
+    if (o.n && o.ns != ns) throw ShardError(SG_ERR_DEVICE, "shards disagree on the slot count");
+    if (o.n && mc != o.mc) {  // re-pad what is pending
+        std::vector<uint64_t> sl(o.n * ns * mc, SG_NULL_SEQ);
+        for (uint64_t q = 0; q < o.n * ns; q++)
+            for (uint32_t c = 0; c < o.mc; c++) sl[q * mc + c] = o.slot[q * o.mc + c];
+        o.slot.swap(sl);
+    }
+    if (o.n && ni != o.ni) {  // (the item count is the projection's: the same for every shard)
+        throw ShardError(SG_ERR_DEVICE, "shards disagree on the projected items");
+    }
+    const uint64_t n0 = o.n, n1 = n0 + total;
+    o.ns = ns;
+    o.mc = mc;
+    o.ni = ni;
+    o.trig.resize(n1);
+    o.key.resize(n1);
+    o.ts.resize(n1);
+    o.len.resize(n1 * ns, 0);
+    o.slot.resize(n1 * ns * mc, SG_NULL_SEQ);
+    // projection: item-major over the pending rows -> rebuilt with the new row count
+    std::vector<uint64_t> pv((size_t)ni * n1, 0);
+    std::vector<uint8_t> pn((size_t)ni * n1, 0);
+    for (uint32_t it = 0; it < ni && n0; it++)
+        for (uint64_t q = 0; q < n0; q++) {
+            pv[(size_t)it * n1 + q] = o.pval[(size_t)it * n0 + q];
+            pn[(size_t)it * n1 + q] = o.pnull[(size_t)it * n0 + q];
+        }
+    for (uint64_t x = 0; x < total; x++) {
+        const ShardEngine::Out& p = parts[ord[x].r];
+        const uint64_t i = ord[x].i, d = n0 + x;
+        o.trig[d] = p.trig[i];
+        o.key[d] = p.key[i];
+        o.ts[d] = p.ts[i];
+        for (uint32_t sl = 0; sl < ns; sl++) {
+            o.len[d * ns + sl] = p.len[i * ns + sl];
+            for (uint32_t c = 0; c < p.mc; c++) o.slot[(d * ns + sl) * mc + c] = p.slot[(i * ns + sl) * p.mc + c];
+        }
+        for (uint32_t it = 0; it < p.ni; it++) {
+            pv[(size_t)it * n1 + d] = p.pval[(size_t)it * p.n + i];
+            pn[(size_t)it * n1 + d] = p.pnull[(size_t)it * p.n + i];
+        }
+    }
+    o.pval.swap(pv);
+    o.pnull.swap(pn);
+    o.n = n1;
+}
+
+}  // namespace
+
+int shd_advance(ShardEngine* s, int64_t now) {
+    try {
+        if (s->held) throw ShardError(SG_ERR_STATE, "release the polled matches first");
+        collect(s, false);   // the batch matches so far come before this advance's timer matches
+        s->each([&](uint32_t r) { return sg_advance_time(s->sh[r], now); });
+        collect(s, true);
+        return SG_OK;
+    } catch (const std::exception& ex) {
+        return fail_from(ex);
+    }
+}
+
+int shd_poll(ShardEngine* s, uint32_t mem, sg_match_batch* out) {
+    try {
+        if ((mem & ~(uint32_t)SG_POLL_READY) != SG_MEM_HOST)
+            throw ShardError(SG_ERR_INVALID, "a multi-device engine returns matches in host memory");
+        if (s->held) throw ShardError(SG_ERR_STATE, "release the polled matches first");
+        collect(s, false);
+        s->out = std::move(s->pend);
+        s->pend = ShardEngine::Out();
+        const ShardEngine::Out& o = s->out;
+        out->n = o.n;
+        out->n_slots = o.n ? o.ns : 0;
+        out->max_chain = o.n ? o.mc : 1;
+        out->trigger_seq = o.trig.data();
+        out->key = o.key.data();
+        out->ts = o.ts.data();
+        out->slot_seq = o.slot.data();
+        out->chain_len = o.len.data();
+        out->mem = SG_MEM_HOST;
+        out->reserved = 0;
+        s->held = true;
+        return SG_OK;
+    } catch (const std::exception& ex) {
+        return fail_from(ex);
+    }
+}
+
+int shd_get_projection(ShardEngine* s, uint32_t mem, sg_projection* out) {
+    if (!s->held) return sg_set_error(SG_ERR_STATE, "poll the matches first");
+    if (!s->proj) return sg_set_error(SG_ERR_STATE, "no projection set");
+    if (mem != SG_MEM_HOST) return sg_set_error(SG_ERR_INVALID, "a multi-device engine returns host memory");
+    out->n = s->out.n;
+    out->n_items = s->out.ni;
+    out->mem = SG_MEM_HOST;
+    out->value = s->out.pval.data();
+    out->null = s->out.pnull.data();
+    return SG_OK;
+}
+
+int shd_release(ShardEngine* s, sg_match_batch* m) {
+    s->held = false;
+    s->out = ShardEngine::Out();
+    if (m) memset(m, 0, sizeof(*m));
+    return SG_OK;
+}
+
+int shd_synchronize(ShardEngine* s) {
+    try {
+        s->each([&](uint32_t r) { return sg_synchronize(s->sh[r]); });
+        return SG_OK;
+    } catch (const std::exception& ex) {
+        return fail_from(ex);
+    }
+}
+
+int shd_stats(ShardEngine* s, sg_stats* out) {
+    try {
+        std::vector<sg_stats> st(s->N);
+        s->each([&](uint32_t r) { return sg_get_stats(s->sh[r], &st[r]); });
+        memset(out, 0, sizeof(*out));
+        uint64_t* o = (uint64_t*)out;
+        for (const sg_stats& x : st)
+            for (size_t i = 0; i < sizeof(sg_stats) / 8; i++) o[i] += ((const uint64_t*)&x)[i];
+        // (events / batches: every event reaches exactly one shard, so the sums are the engine's; batches count
+        // each shard's sub-batches)
+        return SG_OK;
+    } catch (const std::exception& ex) {
+        return fail_from(ex);
+    }
+}
+
+int shd_reset_keys(ShardEngine* s, const uint32_t* keys, uint64_t n, uint32_t mem) {
+    try {
+        if (n == 0) return SG_OK;
+        std::vector<uint32_t> h(n);
+        if (mem == SG_MEM_HOST) {
+            memcpy(h.data(), keys, n * 4);
+        } else if (hipMemcpy(h.data(), keys, n * 4, hipMemcpyDeviceToHost) != hipSuccess) {
+            throw ShardError(SG_ERR_DEVICE, "copying the key ids failed");
+        }
+        for (uint32_t k : h)
+            if (k >= s->K) throw ShardError(SG_ERR_INVALID, "key id outside [0, n_keys)");
+        std::vector<std::vector<uint32_t>> per(s->N);
+        for (uint32_t k : h) per[k % s->N].push_back(k / s->N);
+        s->each([&](uint32_t r) {
+            return per[r].empty() ? SG_OK : sg_reset_keys(s->sh[r], per[r].data(), per[r].size(), SG_MEM_HOST);
+        });
+        return SG_OK;
+    } catch (const std::exception& ex) {
+        return fail_from(ex);
+    }
+}
+
+// image: magic u64, N u32, pad u32 | per shard: u64 image bytes, u64 map entries, image, map (u64 each)
+int shd_snapshot(ShardEngine* s, void** buf, size_t* len) {
+    try {
+        if (s->pend.n || s->held) throw ShardError(SG_ERR_STATE, "poll the matches first");
+        std::vector<void*> img(s->N, nullptr);
+        std::vector<size_t> il(s->N, 0);
+        s->each([&](uint32_t r) { return sg_snapshot(s->sh[r], &img[r], &il[r]); });
+        size_t total = 16;
+        for (uint32_t r = 0; r < s->N; r++) total += 16 + il[r] + 8 * s->gmap[r].size();
+        uint8_t* o = (uint8_t*)malloc(total);
+        if (!o) throw ShardError(SG_ERR_CAPACITY, "out of host memory");
+        size_t off = 0;
+        auto put = [&](const void* p, size_t b) { memcpy(o + off, p, b); off += b; };
+        const uint32_t hdr[2] = {s->N, 0};
+        put(&kMagic, 8);
+        put(hdr, 8);
+        for (uint32_t r = 0; r < s->N; r++) {
+            const uint64_t a[2] = {il[r], s->gmap[r].size()};
+            put(a, 16);
+            put(img[r], il[r]);
+            put(s->gmap[r].data(), 8 * s->gmap[r].size());
+            sg_free_buffer(img[r]);
+        }
+        *buf = o;
+        *len = total;
+        return SG_OK;
+    } catch (const std::exception& ex) {
+        return fail_from(ex);
+    }
+}
+
+int shd_restore(ShardEngine* s, const void* buf, size_t len) {
+    try {
+        const uint8_t* p = (const uint8_t*)buf;
+        size_t off = 0;
+        auto need = [&](size_t b) {
+            if (off + b > len) throw ShardError(SG_ERR_INVALID, "sharded snapshot truncated");
+        };
+        need(16);
+        uint64_t magic;
+        uint32_t hdr[2];
+        memcpy(&magic, p, 8);
+        memcpy(hdr, p + 8, 8);
+        off = 16;
+        if (magic != kMagic) throw ShardError(SG_ERR_INVALID, "not a snapshot of a multi-device engine");
+        if (hdr[0] != s->N) throw ShardError(SG_ERR_INVALID, "snapshot of a different shard count");
+        std::vector<const uint8_t*> img(s->N);
+        std::vector<size_t> il(s->N);
+        std::vector<std::vector<uint64_t>> maps(s->N);
+        for (uint32_t r = 0; r < s->N; r++) {
+            need(16);
+            uint64_t a[2];
+            memcpy(a, p + off, 16);
+            off += 16;
+            need(a[0]);
+            img[r] = p + off;
+            il[r] = a[0];
+            off += a[0];
+            if (a[1] > (len - off) / 8) throw ShardError(SG_ERR_INVALID, "sharded snapshot truncated");
+            maps[r].resize(a[1]);
+            memcpy(maps[r].data(), p + off, 8 * a[1]);
+            off += 8 * a[1];
+        }
+        s->each([&](uint32_t r) { return sg_restore(s->sh[r], img[r], il[r]); });
+        s->gmap = std::move(maps);
+        return SG_OK;
+    } catch (const std::exception& ex) {
+        return fail_from(ex);
+    }
+}
+
+// one document over every shard: keys and event seqs mapped to global ids, keys in id order
+int shd_state_export(ShardEngine* s, void** buf, size_t* len) {
+    try {
+        if (s->pend.n || s->held) throw ShardError(SG_ERR_STATE, "poll the matches first");
+        std::vector<SdDoc> docs(s->N);
+        s->each([&](uint32_t r) -> int {
+            void* b = nullptr;
+            size_t l = 0;
+            const int rc = sg_state_export(s->sh[r], &b, &l);
+            if (rc != SG_OK) return rc;
+            try {
+                docs[r] = sd_read(b, l);
+            } catch (...) {
+                sg_free_buffer(b);
+                throw;
+            }
+            sg_free_buffer(b);
+            return SG_OK;
+        });
+        SdDoc out;
+        out.n_procs = docs[0].n_procs;
+        out.n_slots = docs[0].n_slots;
+        out.desc = docs[0].desc;
+        out.now = docs[0].now;
+        out.last_event_ts = docs[0].last_event_ts;
+        for (uint32_t r = 0; r < s->N; r++) {
+            out.clock_flags = std::max(out.clock_flags, docs[r].clock_flags);
+            for (SdKey& k : docs[r].keys) {
+                if (s->N > 1) k.key = k.key * s->N + r;
+                for (SdStream& ev : k.streams) ev.seq = s->map_seq(r, ev.seq);
+                out.keys.push_back(std::move(k));
+            }
+        }
+        std::stable_sort(out.keys.begin(), out.keys.end(), [](const SdKey& a, const SdKey& b) { return a.key < b.key; });
+        const std::vector<uint8_t> bytes = sd_write(out);
+        void* o = malloc(bytes.size());
+        if (!o) throw ShardError(SG_ERR_CAPACITY, "out of host memory");
+        memcpy(o, bytes.data(), bytes.size());
+        *buf = o;
+        *len = bytes.size();
+        return SG_OK;
+    } catch (const std::exception& ex) {
+        return fail_from(ex);
+    }
+}
+
+// split a document by owner shard; its events get fresh local seqs mapped to their global ones
+int shd_state_import(ShardEngine* s, const void* buf, size_t len) {
+    try {
+        SdDoc d = sd_read(buf, len);
+        std::vector<SdDoc> parts(s->N);
+        for (SdDoc& p : parts) {
+            p.n_procs = d.n_procs;
+            p.n_slots = d.n_slots;
+            p.desc = d.desc;
+            p.now = d.now;
+            p.last_event_ts = d.last_event_ts;
+            p.clock_flags = d.clock_flags;
+        }
+        for (SdKey& k : d.keys) {
+            if (k.key >= s->K) throw ShardError(SG_ERR_INVALID, "state document key id outside [0, n_keys)");
+            const uint32_t r = k.key % s->N;
+            k.key /= s->N;
+            parts[r].keys.push_back(std::move(k));
+        }
+        std::vector<std::vector<uint64_t>> add(s->N);
+        for (uint32_t r = 0; r < s->N; r++) {
+            std::vector<uint64_t> glob;
+            for (const SdKey& k : parts[r].keys)
+                for (const SdStream& ev : k.streams)
+                    if (ev.seq < SG_BLANK_SEQ) glob.push_back(ev.seq);
+            std::sort(glob.begin(), glob.end());
+            glob.erase(std::unique(glob.begin(), glob.end()), glob.end());
+            const uint64_t base = s->gmap[r].size();
+            for (SdKey& k : parts[r].keys)
+                for (SdStream& ev : k.streams)
+                    if (ev.seq < SG_BLANK_SEQ)
+                        ev.seq = base + (uint64_t)(std::lower_bound(glob.begin(), glob.end(), ev.seq) - glob.begin());
+            add[r] = std::move(glob);
+        }
+        s->each([&](uint32_t r) -> int {
+            const std::vector<uint8_t> bytes = sd_write(parts[r]);
+            return sg_state_import(s->sh[r], bytes.data(), bytes.size());
+        });
+        for (uint32_t r = 0; r < s->N; r++) s->gmap[r].insert(s->gmap[r].end(), add[r].begin(), add[r].end());
+        return SG_OK;
+    } catch (const std::exception& ex) {
+        return fail_from(ex);
+    }
+}
+
+int shd_wait_stream(ShardEngine* s, void* stream) {
+    (void)s;
+    (void)stream;
+    return sg_set_error(SG_ERR_UNSUPPORTED, "sg_wait_stream: a multi-device engine stages device batches on the host");
+}

@@ -42,7 +42,8 @@ class EngineError(RuntimeError):
 class sg_config(C.Structure):
     _fields_ = [("struct_size", C.c_uint32), ("device", C.c_int32), ("n_keys", C.c_uint32),
                 ("max_batch", C.c_uint32), ("partial_capacity", C.c_uint32), ("flags", C.c_uint32),
-                ("match_capacity", C.c_uint64)]
+                ("match_capacity", C.c_uint64), ("n_devices", C.c_uint32), ("reserved", C.c_uint32),
+                ("devices", C.POINTER(C.c_int32))]
 
 
 class sg_batch(C.Structure):
@@ -307,7 +308,9 @@ class NativeEngine:
     """One sg_engine (one compiled query on one device)."""
 
     def __init__(self, lib, prefix, ir: bytes, n_keys=1, max_batch=1 << 16, partial_capacity=64,
-                 match_capacity=1 << 20, device=0, flags=0):
+                 match_capacity=1 << 20, device=0, flags=0, devices=None):
+        """devices: several HIP device ordinals -> the engine's own multi-device fan-out (sg_config.n_devices,
+        sg_sharded.cpp): keys sharded key % len(devices), one engine per device behind this one handle"""
         self.lib = lib
         self.p = prefix
         f = lambda n: getattr(lib, prefix + n)
@@ -331,8 +334,10 @@ class NativeEngine:
         self._sync = getattr(lib, prefix + "synchronize", None)
         if self._sync is not None:
             self._sync.argtypes = [C.c_void_p]
-        cfg = sg_config(C.sizeof(sg_config), device, n_keys, max_batch, partial_capacity, flags,
-                        match_capacity)
+        devs = list(devices) if devices is not None else [device]
+        self._devs = (C.c_int32 * len(devs))(*devs)
+        cfg = sg_config(C.sizeof(sg_config), devs[0], n_keys, max_batch, partial_capacity, flags,
+                        match_capacity, len(devs), 0, self._devs)
         self._ir = C.create_string_buffer(ir, len(ir))
         h = C.c_void_p()
         self._check(self._create(self._ir, len(ir), C.byref(cfg), C.byref(h)))

@@ -1595,16 +1595,16 @@ class SiddhiManager:
 
     def __init__(self, engine_factory: Optional[Callable] = None, n_keys=1 << 16, device=0,
                  partial_capacity=64, max_batch=1 << 16, devices=None):
-        """devices: several HIP devices -> every partitioned query runs on a ShardedEngine over them
-        (partition keys sharded across the GPUs, matches merged back in the single engine's order)."""
+        """devices: several HIP devices -> every partitioned query runs on the engine's multi-device fan-out
+        over them (sg_config.n_devices: partition keys sharded across the GPUs, matches merged back in the single
+        engine's order; sg_sharded.cpp)."""
         if engine_factory is None:
             lib = load_hip_library()          # raises if the HIP engine is not built
             if devices is not None and len(devices) > 1:
-                from .sharded import ShardedEngine
-
+                # the engine's own multi-device fan-out behind one C-ABI handle (sg_config.n_devices)
                 def engine_factory(ir, nk):
-                    return ShardedEngine(lib, "sg_", ir, n_keys=nk, devices=tuple(devices), max_batch=max_batch,
-                                         partial_capacity=partial_capacity)
+                    return NativeEngine(lib, "sg_", ir, n_keys=nk, max_batch=max_batch,
+                                        partial_capacity=partial_capacity, devices=tuple(devices))
             else:
                 def engine_factory(ir, nk):
                     return NativeEngine(lib, "sg_", ir, n_keys=nk, max_batch=max_batch,

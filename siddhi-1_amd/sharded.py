@@ -1,5 +1,9 @@
-"""Multi-device fan-out inside one engine ("Multi-GPU fan-out is internal to one engine";
-§8e: partition keys shard, one exchange step, output merged back by trigger seq).
+"""Multi-device fan-out over N engines of any backend, in Python.
+
+The product's multi-device path is the C-ABI's own fan-out (sg_config.n_devices, csrc/sg_sharded.cpp: one
+sg_engine handle over one engine per device, what a JNI shim bound to siddhi_gpu.h gets; SiddhiManager(devices=..)
+uses it).  This module restates the same splitting / seq mapping / merge over NativeEngine objects so that
+the CPU tests can run it over the oracle (tests/test_sharded.py) and the GPU tests can compare both.
 
 `ShardedEngine` has the interface of `NativeEngine` (push / poll / advance_time / reset_keys / snapshot /
 restore / stats) and drives one engine per device.  Partition key ids are dense (first-seen order of the

@@ -1,6 +1,7 @@
-"""ShardedEngine over HIP engines (two shards on device 0, or one per device when the box has more)
-against one HIP engine, bit-exact, incl. purge, snapshot/restore and playback timers; the runtime API
-with SiddhiManager(devices=...)."""
+"""Multi-device fan-out against one HIP engine, bit-exact, incl. purge, snapshot/restore and playback timers:
+the C-ABI's own fan-out (sg_config.n_devices, csrc/sg_sharded.cpp: one handle, driven only through
+siddhi_gpu.h by ctypes) and the Python ShardedEngine, two shards on device 0 (or one per device when the box
+has more); state documents across the fan-out; the runtime API with SiddhiManager(devices=...)."""
 import importlib
 
 import pytest
@@ -21,6 +22,94 @@ def _devices():
 @pytest.mark.parametrize("shape", sorted(SHAPES))
 def test_sharded_hip_equals_single(shape):
     run_property(shape, sa.load_hip_library(), "sg_", devices=_devices())
+
+
+@pytest.mark.parametrize("shape", sorted(SHAPES))
+def test_cabi_fanout_equals_single(shape):
+    """the fan-out behind the C-ABI (one sg_engine over two devices' engines) equals the
+    single engine for every shape, purge, snapshot / restore and timers included"""
+    run_property(shape, sa.load_hip_library(), "sg_", devices=_devices(), cabi=True)
+
+
+@pytest.mark.parametrize("shape", ["two_state", "count", "absent_playback"])
+def test_cabi_fanout_state_documents(shape):
+    """sg_state_export of the fan-out is the single engine's document (global key ids and seqs); importing
+    it into a fresh fan-out and into a single engine continues identically"""
+    import numpy as np
+    from test_gpu_parity import _same
+    synth = importlib.import_module("siddhi-1_amd.synth")
+    sd = importlib.import_module("siddhi-1_amd.state_doc")
+    app = sa.parse_app(SHAPES[shape])
+    cq = sa.compile_query(app, app.queries[0], sa.StringDictionary())
+    K = 257
+    lib = sa.load_hip_library()
+    mk = lambda devs=None: sa.NativeEngine(lib, "sg_", cq.ir, n_keys=K, max_batch=1 << 14, partial_capacity=64,
+                                           match_capacity=1 << 20, devices=devs)
+    one, fan = mk(), mk(_devices())
+    playback = "playback" in SHAPES[shape]
+    streams = []
+    if playback:   # bursts of one key per millisecond, 64 keys: partials die by their timers (distinct due times)
+        from test_gpu_general import _burst_stream
+        full = _burst_stream(4000, 64, seed=31, max_burst=4)
+        n = len(full["ts"])
+        # short sends (the clock moves per send, and a send(Event[]) spanning many windows expires its
+        # partials before their timers can fire)
+        for a in range(0, n, 200):
+            streams.append((a, {k: v[a:a + 200] for k, v in full.items()}))
+    else:
+        seq = 0
+        for b in range(4):
+            streams.append((seq, synth.stock_ticks(seq, 4000, K, seed=90 + b, rate_per_ms=4)))
+            seq += 4000
+    half = len(streams) // 2
+    for seq0, d in streams[:half]:
+        for e in (one, fan):
+            if playback:
+                e.advance_time(int(d["ts"][-1]))
+            e.push(0, seq0, d["ts"], [d["symbol"], d["price"], d["volume"]], None, d["key"])
+        _same(one.poll(), fan.poll())
+    doc1, docf = one.state_export(), fan.state_export()
+    assert sd.logical(sd.parse(doc1), seed_ts=True) == sd.logical(sd.parse(docf), seed_ts=True)
+    fan2, one2 = mk(_devices()), mk()
+    fan2.state_import(doc1)
+    one2.state_import(docf)
+    total = 0
+    for seq0, d in streams[half:]:
+        for e in (one, fan2, one2):
+            if playback:
+                e.advance_time(int(d["ts"][-1]))
+            e.push(0, seq0, d["ts"], [d["symbol"], d["price"], d["volume"]], None, d["key"])
+        ms = [e.poll() for e in (one, fan2, one2)]
+        _same(ms[0], ms[1])
+        _same(ms[0], ms[2])
+        total += len(ms[0])
+    assert total > 0
+
+
+def test_cabi_fanout_runtime_api():
+    """SiddhiManager(devices=...) runs a partitioned query on the C-ABI fan-out: the callbacks equal a
+    one-device runtime's"""
+    synth = importlib.import_module("siddhi-1_amd.synth")
+    app = SHAPES["two_state"]
+    out = []
+    for devs in (None, _devices()):
+        mgr = sa.SiddhiManager(n_keys=512, max_batch=1 << 14, devices=devs)
+        rt = mgr.createSiddhiAppRuntime(app)
+        got = []
+        q = rt.queries[0]
+        rt.addCallback(list(rt.by_name)[0], lambda ts, ins, rem: got.extend((e.timestamp, tuple(e.data)) for e in ins))
+        rt.start()
+        h = rt.getInputHandler("S")
+        d = synth.stock_ticks(0, 6000, 97, seed=4, rate_per_ms=4)
+        ev = [sa.Event(t, [f"K{k}", p, v]) for t, k, p, v in zip(d["ts"].tolist(), d["key"].tolist(),
+                                                                 d["price"].tolist(), d["volume"].tolist())]
+        for i in range(0, len(ev), 1000):
+            h.send(ev[i:i + 1000])
+        rt.shutdown()
+        if devs is not None:
+            assert isinstance(q.engine, sa.NativeEngine) and len(q.engine._devs) > 1
+        out.append(got)
+    assert len(out[0]) > 0 and out[0] == out[1]
 
 
 def test_null_keys_are_dropped():

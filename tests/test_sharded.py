@@ -28,15 +28,23 @@ def same(a, b):
     assert np.array_equal(a.slot_seq[:, :, :w], b.slot_seq[:, :, :w])
 
 
-def run_property(shape, lib, prefix, devices):
+def run_property(shape, lib, prefix, devices, cabi=False):
+    """cabi: the sharded engine is the C-ABI's own fan-out (sg_config.n_devices, one handle), else the Python
+    ShardedEngine over N engines"""
     app = sa.parse_app(SHAPES[shape])
     cq = sa.compile_query(app, app.queries[0], sa.StringDictionary())
     K = 300
     mk = lambda: sa.NativeEngine(lib, prefix, cq.ir, n_keys=K, max_batch=1 << 14, partial_capacity=64,
                                  match_capacity=1 << 20)
     one = mk()
-    shd = sa.ShardedEngine(lib, prefix, cq.ir, n_keys=K, devices=devices, max_batch=1 << 14, partial_capacity=64,
-                           match_capacity=1 << 20)
+
+    def mk_sharded():
+        if cabi:
+            return sa.NativeEngine(lib, prefix, cq.ir, n_keys=K, max_batch=1 << 14, partial_capacity=64,
+                                   match_capacity=1 << 20, devices=devices)
+        return sa.ShardedEngine(lib, prefix, cq.ir, n_keys=K, devices=devices, max_batch=1 << 14,
+                                partial_capacity=64, match_capacity=1 << 20)
+    shd = mk_sharded()
     playback = "playback" in SHAPES[shape]
     seq, total = 0, 0
     for b in range(4):
@@ -57,8 +65,7 @@ def run_property(shape, lib, prefix, devices):
             if hasattr(lib, prefix + "snapshot"):   # (the oracle has no snapshot)
                 img = shd.snapshot()
                 shd.close()
-                shd = sa.ShardedEngine(lib, prefix, cq.ir, n_keys=K, devices=devices, max_batch=1 << 14,
-                                       partial_capacity=64, match_capacity=1 << 20)
+                shd = mk_sharded()
                 shd.restore(img)
         for e in (one, shd):
             e.push(0, seq, d["ts"], [d["symbol"], d["price"], d["volume"]], None, d["key"])
