@@ -679,7 +679,18 @@ def main():
                                         c4b, steps, 1, 64, playback=True),
                             workload="C4 with deeper per-key state: 262,144 keys, one key per ms in bursts of 16 "
                                      "events (up to ~16 live partials per key)"),
+            # hundreds of live absent partials per key carried across pushes (C4's 30 s / 60 s
+            # windows, 2,048 keys, a burst of 16 events per ms with falling prices so that partials die by their
+            # timers, 2^16-event pushes = 4.1 s of event time; 8 warmup pushes fill the lists)
+            "C4_deep_state": dict(run_general(sa, synth, torch, dev, synth.C4_QUERY,
+                                              lambda s: synth.absent_deep_ticks(s * 4096, 4096, 2048, 16), 2048,
+                                              1 << 16, 16, 8, 512, playback=True),
+                                  workload="C4 deep cross-batch state: 2,048 keys, bursts of 16 events per ms, "
+                                           "2^16-event pushes, hundreds of live partials per key at every push"),
         }
+        ds = out["other_configs"]["C4_deep_state"]["roofline"]["counters_per_step"]
+        out["other_configs"]["C4_deep_state"]["live_per_touched_key_at_batch_start"] = \
+            ds["live_at_batch_start"] / max(1.0, ds["keys_touched"])
     if rank == 0 and world == 1 and not args.no_extra:
         out["pcie_inclusive"] = pcie_inclusive(sa, synth, torch, dev, cq, K, B, 4)
         out["output_inclusive"] = output_inclusive(sa, synth, torch, dev, K, B, 6)

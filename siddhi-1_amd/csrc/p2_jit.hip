@@ -132,6 +132,12 @@ template <class A, class B> struct SgSel<false, A, B> { typedef B type; };
 #define SGX_MAX_IT 0x7fffffff
 #endif
 // SGX_GLB_WALK=1: the staged pass walks the payload in HBM (one element ahead) instead of LDS
+// SGX_BRANCHLESS (1, shipped): the window scan evaluates the filter on every slot and masks with the pending
+// set (no exec-mask branch per slot), and the matches are stored by a wave loop over the set bits of the
+// hit mask (slot words picked by selects) instead of one predicated region per slot; 0: the per-slot branches
+#ifndef SGX_BRANCHLESS
+#define SGX_BRANCHLESS 1
+#endif
 #ifndef SGX_GLB_WALK
 #define SGX_GLB_WALK 0
 #endif
@@ -751,9 +757,15 @@ __device__ __forceinline__ void advance(const P2Params& p, const uint32_t gid) {
             if (act) {
                 if (!GLB || !hbm) {
                     const uint32_t P = W.live & ~W.stg;
+                    if (SGX_BRANCHLESS) {
 #pragma unroll
-                    for (int j = 0; j < R; ++j) {
-                        if (((P >> j) & 1u) && sgq_f1(ev, W.cw[j], W.cn[j], p)) H |= 1u << j;
+                        for (int j = 0; j < R; ++j) H |= (sgq_f1(ev, W.cw[j], W.cn[j], p) ? 1u : 0u) << j;
+                        H &= P;
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < R; ++j) {
+                            if (((P >> j) & 1u) && sgq_f1(ev, W.cw[j], W.cn[j], p)) H |= 1u << j;
+                        }
                     }
                     c1 = __popc(H);
                     s.scanned += __popc(P);
@@ -789,7 +801,42 @@ __device__ __forceinline__ void advance(const P2Params& p, const uint32_t gid) {
                 } else {
                     atomicOr(p.err, (uint32_t)SGD_ERR_MATCH_CAP);
                 }
-                if (!GLB || !hbm) {
+                if ((!GLB || !hbm) && SGX_BRANCHLESS) {
+                    // the hit slots in slot order: one trip per set bit of the wave's widest mask
+                    for (uint32_t m = H; __builtin_amdgcn_read_exec() & __ballot(m != 0u);) {
+                        if (m) {
+                            const int jj = __ffs(m) - 1;
+                            m &= m - 1u;
+                            WSQ sq = 0;
+#if SGQ_PROJ
+                            uint32_t cw[SGQ_NCAPW > 0 ? SGQ_NCAPW : 1], cn = 0;
+#pragma unroll
+                            for (int w = 0; w < SGQ_NCAPW; ++w) cw[w] = 0;
+#endif
+#pragma unroll
+                            for (int j = 0; j < R; ++j) {
+                                const bool here = j == jj;
+                                sq = here ? W.seq[j] : sq;
+#if SGQ_PROJ
+#pragma unroll
+                                for (int w = 0; w < SGQ_NCAPW; ++w) cw[w] = here ? W.cw[j][w] : cw[w];
+                                if (SGQ_CAPNULL) cn = here ? W.cn[j] : cn;
+#endif
+                            }
+                            if (!SGX_NO_RAW && pos < p.raw_capacity) {
+                                p.raw_e1[pos] = sbase + (uint64_t)(int64_t)sq;
+#if SGQ_PROJ
+#pragma unroll
+                                for (int w = 0; w < SGQ_NCAPW; ++w) p.raw_capw[(size_t)w * p.raw_capacity + pos] = cw[w];
+                                if (SGQ_CAPNULL) p.raw_capnull[pos] = cn;
+#endif
+                            }
+                            pos++;
+                        }
+                    }
+                    W.live &= ~H;
+                    W.fix_tail();
+                } else if (!GLB || !hbm) {
 #pragma unroll
                     for (int j = 0; j < R; ++j) {
                         if ((H >> j) & 1u) {

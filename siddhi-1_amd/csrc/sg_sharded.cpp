@@ -77,6 +77,7 @@ struct ShardEngine {
     bool held = false;
     bool proj = false;
     bool heads = false;   // every shard orders its timer matches by the keys' queue heads (and reports them)
+    uint32_t nslots = 0, mchain = 1;  // the shards' slot count / chain width (reported by every poll, even empty)
 
     // run fn(r) for every shard, concurrently when there are several; the first failure is rethrown here
     void each(const std::function<int(uint32_t)>& fn) {
@@ -384,7 +385,11 @@ void collect(ShardEngine* s, bool timers) {
     };
     std::vector<Ref> ord;
     uint64_t total = 0;
-    for (uint32_t r = 0; r < N; r++) total += parts[r].n;
+    for (uint32_t r = 0; r < N; r++) {
+        total += parts[r].n;
+        if (parts[r].ns) s->nslots = parts[r].ns;
+        s->mchain = std::max(s->mchain, parts[r].mc);
+    }
     if (total == 0) return;
     ord.reserve(total);
     for (uint32_t r = 0; r < N; r++) {
@@ -500,8 +505,8 @@ int shd_poll(ShardEngine* s, uint32_t mem, sg_match_batch* out) {
         s->pend = ShardEngine::Out();
         const ShardEngine::Out& o = s->out;
         out->n = o.n;
-        out->n_slots = o.n ? o.ns : 0;
-        out->max_chain = o.n ? o.mc : 1;
+        out->n_slots = o.n ? o.ns : s->nslots;
+        out->max_chain = o.n ? o.mc : s->mchain;
         out->trigger_seq = o.trig.data();
         out->key = o.key.data();
         out->ts = o.ts.data();

@@ -26,9 +26,12 @@ cfg = {
     "C4": (synth.C4_QUERY, lambda s: synth.burst_ticks(s * cb, cb, K, 1), K, cb, 16, True),
     "C4_deep": (synth.C4_QUERY, lambda s: synth.burst_ticks(s * (cb // 16), cb // 16, K // 4, 16), K // 4, cb, 64,
                 True),
+    "C4_deep_state": (synth.C4_QUERY, lambda s: synth.absent_deep_ticks(s * 4096, 4096, 2048, 16), 2048, 1 << 16, 512,
+                      True),
 }
 for name in which:
     print("config", name, flush=True)
     q, mk, keys, b, cap, pb = cfg[name]
-    r = bench.run_general(sa, synth, torch, dev, q, mk, keys, b, steps, 1, cap, playback=pb)
+    r = bench.run_general(sa, synth, torch, dev, q, mk, keys, b, steps, 8 if name == "C4_deep_state" else 1, cap,
+                          playback=pb)
     print(json.dumps(dict(r, config=name, lib=os.environ.get("SG_HIP_LIBRARY", "default"))), flush=True)
