@@ -339,6 +339,7 @@ template <int NW> struct CntKey {
         seqs[2 * (evSlot * G.MC)] = (uint32_t)ev.seq;
         seqs[2 * (evSlot * G.MC) + 1] = (uint32_t)(ev.seq >> 32);
         gp(A.o.t_cnt)[pos] += 1;
+        if (A.mode & GEN_M_TFIRST) gp(A.o.t_first)[pos] = (uint32_t)r;
     }
 
     // ---- one event of this key (SequenceMultiProcessStreamReceiver: stabilize, then pA, pB, p0)

@@ -554,6 +554,16 @@ __global__ void k_gen_scatter(const uint32_t* raw, const unsigned long long* raw
     write_out(o, *o.count + t_off[rec[0]] + rec[1], rec, false);
 }
 
+// batch matches when every trigger has at most one (GEN_M_TFIRST): output-major, one thread per trigger
+// event — the output writes of a wave are consecutive, the raw records are gathered
+__global__ void k_gen_gather1(const uint32_t* __restrict__ raw, const uint32_t* __restrict__ t_cnt,
+                              const uint32_t* __restrict__ t_off, const uint32_t* __restrict__ t_first, uint32_t n,
+                              OutBufs o) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || t_cnt[i] == 0u) return;
+    write_out(o, *o.count + t_off[i], raw + (uint64_t)t_first[i] * o.recWords, false);
+}
+
 // timer matches in sorted order
 __global__ void k_gen_scatter_timers(const uint32_t* raw, const uint32_t* order, const unsigned long long* nvalid,
                                      OutBufs o) {
@@ -1281,16 +1291,21 @@ int gen_push(GenEngine* e, const sg_batch* b, std::string& msg) {
         a.fb_list = e->fb_list;
         a.fb_n = e->fb_n;
         a.fb_start = e->fb_start;
+        a.mode = GEN_M_TFIRST;   // (this shape emits at most one match per event)
         launch_gen(e, a, GEN_L_CNT_BATCH);
-        a.mode = GEN_M_KEYLIST;
+        a.mode = GEN_M_KEYLIST | GEN_M_TFIRST;
     }
     launch_gen(e, a, GEN_L_BATCH);
     // order: out_count + t_off[trigger] + rank
     size_t tmp = e->scan_tmp_bytes;
     GH_OK(rocprim::exclusive_scan(e->scan_tmp, tmp, e->t_cnt, e->t_off, 0u, n, rocprim::plus<uint32_t>(), e->stream));
     const uint64_t maxRaw = e->rawCap;
-    hipLaunchKernelGGL(k_gen_scatter, dim3((unsigned)((maxRaw + 255) / 256)), dim3(256), 0, e->stream, e->raw,
-                       e->raw_count, e->rawCap / GEN_RAWSEG, (uint32_t)GEN_RAWSEG, e->t_off, e->out);
+    if (a.mode & GEN_M_TFIRST)
+        hipLaunchKernelGGL(k_gen_gather1, dim3((n + 255) / 256), dim3(256), 0, e->stream, e->raw, e->t_cnt, e->t_off,
+                           e->t_first, n, e->out);
+    else
+        hipLaunchKernelGGL(k_gen_scatter, dim3((unsigned)((maxRaw + 255) / 256)), dim3(256), 0, e->stream, e->raw,
+                           e->raw_count, e->rawCap / GEN_RAWSEG, (uint32_t)GEN_RAWSEG, e->t_off, e->out);
     hipLaunchKernelGGL(k_gen_bump, dim3(1), dim3(1), 0, e->stream, e->out.count, e->t_cnt, e->t_off, n,
                        (const unsigned long long*)nullptr);
     GH_OK(hipMemsetAsync(e->t_cnt, 0, (size_t)n * 4, e->stream));

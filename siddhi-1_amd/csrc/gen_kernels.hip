@@ -467,6 +467,7 @@ struct Lane {
             gp(A.o.tk3)[r] = k;
         } else {
             gp(A.o.t_cnt)[trigIdx] += 1;
+            if (A.mode & GEN_M_TFIRST) gp(A.o.t_first)[trigIdx] = (uint32_t)r;
         }
     }
 
