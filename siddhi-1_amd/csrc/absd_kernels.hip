@@ -1,0 +1,645 @@
+// absd_kernels.hip — wave-per-key kernels for the absent-tail shape with deep per-key state
+//
+//     [every] e1=S[f0] -> not S[f1] for T [within W]          (PATTERN, partitioned, @app:playback)
+//
+// (BASELINE configs[3], "deep partial-match state in HBM").  The register-window kernels (abs_kernels.hip) hold
+// at most ABS_R partials per key in one lane's registers and hand a key with more to the next stage.  With
+// hundreds of live partials per key, one lane per key leaves the GPU idle (a few thousand lanes) and walks each
+// key's list serially; here ONE WAVE owns a key: its pending / newAndEvery lists live in the wave's LDS slice
+// (list order, SoA: ts, e1 seq, null bits, the event's attribute words), and every list operation is
+// data-parallel over the 64 lanes — the `within` expiry of the pending prefix and of any staged partial, the
+// kill scan of `not S[f1]` over every pending partial, the timer's expiry / emission test — each followed by an
+// order-preserving compaction (wave ballot + prefix count, chunk by chunk in place).  The key's scalar state
+// (start seed, flag words, lastScheduledTime, timer queue head / length) is wave-uniform.  State is read from
+// and written back to the general engine's blocks in the canonical layout of abs_kernels.hip (StateEvent 0 =
+// the seed, 1 + j / StreamEvent j = partial j), so every other component reads it unchanged; a key whose lists
+// are not of that shape, or whose next event could overflow the lists or the timer queue, goes on to the
+// general kernels (k_gen_batch / k_gen_timers over the second hand-over list).
+//
+// The keys come from the register-window kernels' hand-over list (those whose lists outgrew ABS_R or were not
+// canonical); a fixed grid of one-wave work-groups strides over it.
+//
+// Semantics restated from (paths under /root/reference/modules/siddhi-core/src/main/java/io/siddhi/core/):
+//   query/input/stream/state/StreamPreStateProcessor.java:118-129 isExpired, :308-323 updateState (stable sort
+//       by ts, -1 last), :325-361 expireEvents (the expired prefix of pending, any staged)
+//   query/input/stream/state/AbsentStreamPreStateProcessor.java:80-103 addState (schedules ts + T), :150-227
+//       process (the TIMER event: expired partials dropped, due ones sent in list order), :256-274
+//       processAndReturn (returns nothing)
+//   query/input/stream/state/AbsentStreamPostStateProcessor.java:36-56 (a matching event kills the partial and
+//       reschedules at its ts + T)
+//   util/Scheduler.java:114-128 notifyAt, :172-210 sendTimerEvents
+#include <hip/hip_runtime.h>
+
+#include "../../include/siddhi_gpu.h"
+#include "../../include/siddhi_gpu_ir.h"
+#include "gen_engine.h"
+#include "java_ops.h"
+#include "sg_engine.h"
+#include "reg_common.h"
+
+namespace {
+
+template <int NW> struct DEnt {
+    int64_t ts;
+    uint64_t seq;
+    uint32_t nb;
+    uint32_t w[NW];
+};
+
+// one key's absent-tail state, one wave (every member is wave-uniform except where noted)
+template <int NW> struct DeepKey {
+    const cGenProgram& G;
+    const GenArgs& A;
+    gu32* S;
+    uint32_t K, k, C;
+    uint32_t ks0, ks1;
+    int slot0, slot1;
+    int lane;
+    // the lists in LDS: entries [0, n) in list order, [0, np) pending, [np, n) staged
+    int64_t* lts;
+    uint64_t* lseq;
+    uint32_t* lnb;
+    uint32_t* lw;    // [NW][C]
+    uint32_t n, np;
+    bool sbad;
+    uint32_t seedPend, seedStg;
+    int64_t seedPendTs, seedStgTs;
+    uint32_t f0, f1;
+    int64_t lst;
+    uint32_t qh, ql;
+    uint32_t err;
+    unsigned long long scanned, created, matches;
+    uint32_t rank;   // timer matches of this key's sweep so far
+
+    __device__ DeepKey(const GenArgs& a, uint8_t* smem, uint32_t key)
+        : G(*(cGenProgram*)a.G), A(a), S(gp(a.state)), K(a.K), k(key), n(0), np(0), sbad(false), seedPend(0),
+          seedStg(0), seedPendTs(-1), seedStgTs(-1), f0(0), f1(0), lst(0), qh(0), ql(0), err(0), scanned(0),
+          created(0), matches(0), rank(0) {
+        C = G.L;
+        ks0 = G.offKS + (uint32_t)G.absP0 * G.ksWords;
+        ks1 = G.offKS + (uint32_t)G.absP1 * G.ksWords;
+        slot0 = G.pre[G.absP0].stateId;
+        slot1 = G.pre[G.absP1].stateId;
+        lane = (int)(threadIdx.x & 63);
+        lts = (int64_t*)smem;
+        lseq = (uint64_t*)(smem + 8 * (size_t)C);
+        lnb = (uint32_t*)(smem + 16 * (size_t)C);
+        lw = (uint32_t*)(smem + 20 * (size_t)C);
+    }
+
+    __device__ __forceinline__ gu32& W(uint32_t w_) const { return S[gen_il(K, k, w_)]; }
+    __device__ __forceinline__ int64_t R64(uint32_t w_) const {
+        return (int64_t)((uint64_t)W(w_) | ((uint64_t)W(w_ + 1) << 32));
+    }
+    __device__ __forceinline__ void W64(uint32_t w_, int64_t v) const {
+        W(w_) = (uint32_t)(uint64_t)v;
+        W(w_ + 1) = (uint32_t)((uint64_t)v >> 32);
+    }
+    __device__ __forceinline__ uint32_t qword(uint32_t i) const { return ks1 + KS_LISTS + 2 * G.L + 2 * i; }
+    __device__ __forceinline__ bool wany(bool x) const { return __ballot(x) != 0ull; }
+
+    __device__ __forceinline__ void get(uint32_t i, DEnt<NW>& e) const {
+        e.ts = lts[i];
+        e.seq = lseq[i];
+        e.nb = lnb[i];
+#pragma unroll
+        for (int q = 0; q < NW; ++q) e.w[q] = lw[(size_t)q * C + i];
+    }
+    __device__ __forceinline__ void put(uint32_t i, const DEnt<NW>& e) const {
+        lts[i] = e.ts;
+        lseq[i] = e.seq;
+        lnb[i] = e.nb;
+#pragma unroll
+        for (int q = 0; q < NW; ++q) lw[(size_t)q * C + i] = e.w[q];
+    }
+
+    // ---- load: false = not this kernel's shape (the general kernels take the key)
+    __device__ bool load() {
+        if (!(W(0) & 1u)) {
+            seedStg = 1;
+            seedStgTs = -1;
+            f0 = GF_INIT;
+            f1 = GF_STARTED;
+            return true;
+        }
+        f0 = W(ks0 + KS_FLAGS);
+        f1 = W(ks1 + KS_FLAGS);
+        if ((f0 | f1) & (GF_INACTIVE | GF_RUNNING)) return false;
+        const uint32_t p0n = W(ks0 + KS_PLEN), s0n = W(ks0 + KS_NLEN);
+        if (p0n + s0n > 1u) return false;
+        if (p0n + s0n == 1u) {
+            const uint32_t st = W(ks0 + KS_LISTS + (p0n ? 0u : G.L));
+            if (st >= G.STCAP) return false;
+            const uint32_t b = G.offST + st * G.stWords;
+            if (W(b + ST_TYPE) != 0u || W(b + ST_RC) != 1u) return false;
+            for (int s = 0; s < G.nslots; s++)
+                if (W(b + ST_SLOTS + (uint32_t)s) != GEN_NIL) return false;
+            const int64_t t = R64(b + ST_TS);
+            if (p0n) { seedPend = 1; seedPendTs = t; } else { seedStg = 1; seedStgTs = t; }
+        }
+        np = W(ks1 + KS_PLEN);
+        const uint32_t ns = W(ks1 + KS_NLEN);
+        if (np > G.L || ns > G.L || np + ns > C) return false;
+        n = np + ns;
+        bool ok = true, bad = false;
+        for (uint32_t c = 0; c < n; c += 64) {
+            const uint32_t i = c + (uint32_t)lane;
+            if (i < n) {
+                const uint32_t st = W(ks1 + KS_LISTS + (i < np ? i : G.L + i - np));
+                ok = ok && st < G.STCAP;
+                const uint32_t b = G.offST + (st < G.STCAP ? st : 0u) * G.stWords;
+                const uint32_t e = W(b + ST_SLOTS + (uint32_t)slot0);
+                ok = ok && W(b + ST_TYPE) == 0u && W(b + ST_RC) == 1u && e < G.SECAP &&
+                     W(b + ST_SLOTS + (uint32_t)slot1) == GEN_NIL;
+                const uint32_t eb = G.offSE + (e < G.SECAP ? e : 0u) * G.seWords;
+                const int64_t t = R64(b + ST_TS);
+                ok = ok && W(eb + SE_NEXT) == GEN_NIL && W(eb + SE_RC) == 1u && R64(eb + SE_TS) == t;
+                DEnt<NW> x;
+                x.ts = t;
+                x.seq = (uint64_t)R64(eb + SE_SEQ);
+                x.nb = W(eb + SE_NULL);
+#pragma unroll
+                for (int q = 0; q < NW; ++q) x.w[q] = W(eb + G.absWordAt[q]);
+                put(i, x);
+            }
+        }
+        if (!wany(!ok)) {
+            __builtin_amdgcn_s_waitcnt(0);
+            __builtin_amdgcn_wave_barrier();
+            // staged partials out of ts order (promotion sorts them)
+            for (uint32_t c = np + 1; c < n; c += 64) {
+                const uint32_t i = c + (uint32_t)lane;
+                if (i < n && ts_before(lts[i], lts[i - 1])) bad = true;
+            }
+            sbad = wany(bad);
+        } else {
+            return false;
+        }
+        lst = R64(ks1 + KS_LST);
+        qh = W(ks1 + KS_QHEAD);
+        ql = W(ks1 + KS_QLEN);
+        if (qh >= G.Q || ql > G.Q) return false;
+        return true;
+    }
+
+    // ---- store: the canonical layout (StateEvent 0 = the seed, 1 + j = partial j over StreamEvent j)
+    __device__ void store() const {
+        for (uint32_t c = 0; c < n; c += 64) {
+            const uint32_t j = c + (uint32_t)lane;
+            if (j < n) {
+                DEnt<NW> x;
+                get(j, x);
+                W(ks1 + KS_LISTS + (j < np ? j : G.L + j - np)) = 1u + j;
+                const uint32_t b = G.offST + (1u + j) * G.stWords;
+                W64(b + ST_TS, x.ts);
+                W(b + ST_TYPE) = 0u;
+                W(b + ST_RC) = 1u;
+                for (int s = 0; s < G.nslots; s++) W(b + ST_SLOTS + (uint32_t)s) = s == slot0 ? j : GEN_NIL;
+                const uint32_t eb = G.offSE + j * G.seWords;
+                W64(eb + SE_SEQ, (int64_t)x.seq);
+                W64(eb + SE_TS, x.ts);
+                W(eb + SE_NEXT) = GEN_NIL;
+                W(eb + SE_RC) = 1u;
+                W(eb + SE_NULL) = x.nb;
+#pragma unroll
+                for (int q = 0; q < NW; ++q) W(eb + G.absWordAt[q]) = x.w[q];
+            }
+        }
+        // free bitmaps: StateEvents {0 if a seed} + [1, 1 + n), StreamEvents [0, n)
+        const uint32_t stBits = (seedPend | seedStg) ? 1u : 0u;
+        for (uint32_t x = (uint32_t)lane; x < (G.STCAP + 31) / 32; x += 64) {
+            uint32_t m = 0;
+            const uint32_t lo = 32 * x;  // StateEvent bits lo..lo+31: index s set when s == 0 && seed, or 1 <= s <= n
+            for (int bit = 0; bit < 32; bit++) {
+                const uint32_t sidx = lo + (uint32_t)bit;
+                if ((sidx == 0 && stBits) || (sidx >= 1 && sidx <= n)) m |= 1u << bit;
+            }
+            W(G.offSTfree + x) = m;
+        }
+        for (uint32_t x = (uint32_t)lane; x < (G.SECAP + 31) / 32; x += 64) {
+            uint32_t m = 0;
+            if (n > 32 * x) m = (n >= 32 * (x + 1)) ? 0xffffffffu : ((1u << (n - 32 * x)) - 1u);
+            W(G.offSEfree + x) = m;
+        }
+        if (lane == 0) {
+            W(0) = 1u;
+            W(ks0 + KS_FLAGS) = f0;
+            W(ks0 + KS_PLEN) = seedPend;
+            W(ks0 + KS_NLEN) = seedStg;
+            if (seedPend) W(ks0 + KS_LISTS) = 0u;
+            if (seedStg) W(ks0 + KS_LISTS + G.L) = 0u;
+            if (seedPend | seedStg) {
+                const uint32_t b = G.offST;
+                W64(b + ST_TS, seedPend ? seedPendTs : seedStgTs);
+                W(b + ST_TYPE) = 0u;
+                W(b + ST_RC) = 1u;
+                for (int s = 0; s < G.nslots; s++) W(b + ST_SLOTS + (uint32_t)s) = GEN_NIL;
+            }
+            W(ks1 + KS_FLAGS) = f1;
+            W64(ks1 + KS_LST, lst);
+            W(ks1 + KS_QHEAD) = qh;
+            W(ks1 + KS_QLEN) = ql;
+            W(ks1 + KS_PLEN) = np;
+            W(ks1 + KS_NLEN) = n - np;
+        }
+    }
+
+    // a queue entry (other lanes of this wave may have written it in this walk: every store has completed
+    // (s_waitcnt) and the load goes to L2, bypassing the non-coherent vector L1)
+    __device__ __forceinline__ int64_t qread(uint32_t i) const {
+        __builtin_amdgcn_s_waitcnt(0);
+        const size_t a0 = gen_il(K, k, qword(i)), a1 = gen_il(K, k, qword(i) + 1);
+        const uint32_t lo = __hip_atomic_load((uint32_t*)&S[a0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t hi = __hip_atomic_load((uint32_t*)&S[a1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return (int64_t)((uint64_t)lo | ((uint64_t)hi << 32));
+    }
+    __device__ __forceinline__ int64_t deadline() const { return ql ? qread(qh) : GEN_NO_DEADLINE; }
+
+    // Scheduler.notifyAt under playback, `cnt` times at t (lanes [0, cnt) write one entry each)
+    __device__ __forceinline__ void notifyAt(int64_t t, uint32_t cnt) {
+        if (ql + cnt > G.Q) { err |= GERR_CAP; return; }
+        for (uint32_t c = 0; c < cnt; c += 64) {
+            const uint32_t i = c + (uint32_t)lane;
+            if (i < cnt) {
+                uint32_t pos = qh + ql + i;
+                while (pos >= G.Q) pos -= G.Q;
+                W64(qword(pos), t);
+            }
+        }
+        ql += cnt;
+    }
+
+    // ---- values for the filters ----
+    __device__ __forceinline__ GVal attr(const uint32_t (&ww)[NW], uint32_t nbits, uint32_t a) const {
+        const int ty = G.attrType[0][a];
+        const uint32_t o = G.absOff[a];
+        uint32_t lo = 0, hi = 0;
+#pragma unroll
+        for (int q = 0; q < NW; ++q) {
+            if ((uint32_t)q == o) lo = ww[q];
+            if ((uint32_t)q == o + 1) hi = ww[q];
+        }
+        const uint64_t b = (ty == SG_T_LONG || ty == SG_T_DOUBLE) ? ((uint64_t)lo | ((uint64_t)hi << 32)) : (uint64_t)lo;
+        return GVal{b, ((nbits >> a) & 1u) != 0};
+    }
+    __device__ bool evalF0(const AbsEv<NW>& ev) {
+        const auto& P = G.pre[G.absP0];
+        if (P.flen == 0) return true;
+        const GVal v = jo_eval<false>(G.code, P.fpc, P.flen, err,
+                                      [&](uint32_t s, uint32_t a, int32_t c) -> GVal {
+                                          if ((int)s == slot0 && (c == 0 || c == -1)) return attr(ev.w, ev.nb, a);
+                                          return GVal{0, true};
+                                      },
+                                      [&](uint32_t s, int32_t c) -> bool { return !((int)s == slot0 && (c == 0 || c == -1)); });
+        return !v.null && (v.b & 1);
+    }
+    __device__ bool evalF1(const AbsEv<NW>& ev, const DEnt<NW>& x) {
+        const auto& P = G.pre[G.absP1];
+        if (P.flen == 0) return true;
+        const GVal v = jo_eval<false>(G.code, P.fpc, P.flen, err,
+                                      [&](uint32_t s, uint32_t a, int32_t c) -> GVal {
+                                          if (c != 0 && c != -1) return GVal{0, true};
+                                          if ((int)s == slot1) return attr(ev.w, ev.nb, a);
+                                          if ((int)s == slot0) return attr(x.w, x.nb, a);
+                                          return GVal{0, true};
+                                      },
+                                      [&](uint32_t s, int32_t c) -> bool {
+                                          return !(((int)s == slot0 || (int)s == slot1) && (c == 0 || c == -1));
+                                      });
+        return !v.null && (v.b & 1);
+    }
+
+    // ---- the order-preserving compaction: decide(i, entry) -> keep, chunk by chunk in place (a kept entry
+    // only moves down, below every entry not yet read); np becomes the kept count of [0, np)
+    template <class F> __device__ __forceinline__ void compact(F decide) {
+        uint32_t w = 0, keptPend = 0;
+        const unsigned long long below = (1ull << lane) - 1ull;
+        for (uint32_t c = 0; c < n; c += 64) {
+            const uint32_t i = c + (uint32_t)lane;
+            DEnt<NW> x{};
+            bool keep = false;
+            if (i < n) {
+                get(i, x);
+                keep = decide(i, x);
+            }
+            const unsigned long long m = __ballot(keep);
+            const unsigned long long mp = __ballot(keep && i < np);
+            __builtin_amdgcn_s_waitcnt(0);
+            __builtin_amdgcn_wave_barrier();
+            if (keep) put(w + (uint32_t)__popcll(m & below), x);
+            w += (uint32_t)__popcll(m);
+            keptPend += (uint32_t)__popcll(mp);
+            __builtin_amdgcn_s_waitcnt(0);
+            __builtin_amdgcn_wave_barrier();
+        }
+        n = w;
+        np = keptPend;
+    }
+
+    // updateState: the staged entries join the pending list stable-sorted by ts (eventTimeComparator); an
+    // out-of-order append is rare: lane 0 sorts the staged range in LDS
+    __device__ void promote() {
+        if (n > np && sbad) {
+            if (lane == 0) {
+                for (uint32_t i = np + 1; i < n; i++) {
+                    DEnt<NW> x;
+                    get(i, x);
+                    uint32_t j = i;
+                    while (j > np) {
+                        DEnt<NW> y;
+                        get(j - 1, y);
+                        if (!ts_before(x.ts, y.ts)) break;
+                        put(j, y);
+                        j--;
+                    }
+                    put(j, x);
+                }
+            }
+            __builtin_amdgcn_s_waitcnt(0);
+            __builtin_amdgcn_wave_barrier();
+        }
+        np = n;
+        sbad = false;
+    }
+
+    __device__ __forceinline__ bool expiredAt(int64_t ts, int64_t now) const {
+        const int64_t d = ts - now;
+        return (d < 0 ? -d : d) > G.within;
+    }
+
+    // StreamPreStateProcessor.expireEvents on p1: the expired prefix of pending, any expired staged entry
+    __device__ void expire(int64_t now) {
+        if (G.within == -1 || n == 0) return;
+        // the first pending entry that survives ends the prefix
+        uint32_t f = np;
+        for (uint32_t c = 0; c < np; c += 64) {
+            const uint32_t i = c + (uint32_t)lane;
+            const unsigned long long m = __ballot(i < np && !expiredAt(lts[i], now));
+            if (m) {
+                f = c + (uint32_t)(__ffsll((long long)m) - 1);
+                break;
+            }
+        }
+        bool anyStaged = false;
+        for (uint32_t c = np; c < n; c += 64) {
+            const uint32_t i = c + (uint32_t)lane;
+            anyStaged = anyStaged || (i < n && expiredAt(lts[i], now));
+        }
+        if (f == 0 && !wany(anyStaged)) return;
+        compact([&](uint32_t i, const DEnt<NW>& x) { return i < np ? i >= f : !expiredAt(x.ts, now); });
+    }
+
+    // one event of this key (PatternMultiProcessStreamReceiver: stabilize, then p1, then p0)
+    __device__ void event(const AbsEv<NW>& ev) {
+        expire(ev.ts);
+        seedPend += seedStg;
+        if (seedStg) seedPendTs = seedStgTs;
+        seedStg = 0;
+        promote();
+        // p1.processAndReturn: every pending partial whose f1 passes dies and reschedules (each kill sets
+        // lastScheduledTime = ev.ts + T and notifies at it, AbsentStreamPostStateProcessor.java:36-56)
+        scanned += np;
+        uint32_t kills = 0;
+        for (uint32_t c = 0; c < np; c += 64) {
+            const uint32_t i = c + (uint32_t)lane;
+            bool kl = false;
+            if (i < np) {
+                DEnt<NW> x;
+                get(i, x);
+                kl = evalF1(ev, x);
+            }
+            kills += (uint32_t)__popcll(__ballot(kl));
+        }
+        if (kills) {
+            const int64_t t = ev.ts + G.pre[G.absP1].waiting;
+            lst = t;
+            notifyAt(t, kills);
+            compact([&](uint32_t i, const DEnt<NW>& x) { return !(i < np && evalF1(ev, x)); });
+        }
+        // p0.processAndReturn over its seed
+        if (seedPend) {
+            scanned++;
+            if (evalF0(ev)) {
+                if (lane == 0) {
+                    DEnt<NW> x;
+                    x.ts = ev.ts;
+                    x.seq = ev.seq;
+                    x.nb = ev.nb;
+#pragma unroll
+                    for (int q = 0; q < NW; ++q) x.w[q] = ev.w[q];
+                    put(n, x);
+                }
+                if (n > np && n > 0 && ts_before(ev.ts, lts[n - 1])) sbad = true;
+                __builtin_amdgcn_s_waitcnt(0);
+                __builtin_amdgcn_wave_barrier();
+                n++;
+                lst = ev.ts + G.pre[G.absP1].waiting;
+                notifyAt(lst, 1u);
+                seedPend = 0;
+                if (G.absEvery) {
+                    seedStg = 1;
+                    seedStgTs = ev.ts;
+                    created++;
+                }
+            }
+        }
+    }
+
+    // a timer match: a raw record of the general engine (trigger = timer, rank within this key's sweep)
+    __device__ void project(uint64_t base, uint32_t r, uint64_t e1seq, int64_t t) {
+        const unsigned long long slot = base + r;
+        if (slot >= A.o.seg_cap) { err |= GERR_MATCHCAP; return; }
+        gu32* rec = gp(A.o.raw) + slot * A.o.recWords;
+        rec[0] = 0xfffffffeu;
+        rec[1] = rank + r;
+        rec[2] = 0xffffffffu;
+        rec[3] = 0xffffffffu;
+        rec[4] = (uint32_t)(uint64_t)t;
+        rec[5] = (uint32_t)((uint64_t)t >> 32);
+        rec[6] = k;
+        gu32* lens = rec + 7;
+        gu32* seqs = lens + G.nslots;
+        for (int s = 0; s < G.nslots; s++) lens[s] = s == slot0 ? 1u : 0u;
+        seqs[2 * (slot0 * G.MC)] = (uint32_t)e1seq;
+        seqs[2 * (slot0 * G.MC) + 1] = (uint32_t)(e1seq >> 32);
+        gp(A.o.tk1)[slot] = (uint32_t)G.absListener;
+        gp(A.o.tk2)[slot] = t;
+        gp(A.o.tk3)[slot] = k;
+    }
+
+    // AbsentStreamPreStateProcessor.process for the TIMER event at currentTime = t (the clock is `now`)
+    __device__ void timer(int64_t t, int64_t now) {
+        promote();
+        const int64_t waiting = G.pre[G.absP1].waiting;
+        scanned += np;
+        auto due = [&](const DEnt<NW>& x) {
+            return (x.ts == -1 && t >= lst) || (x.ts != -1 && t >= x.ts + waiting);
+        };
+        auto gone = [&](const DEnt<NW>& x) { return G.within != -1 && expiredAt(x.ts, t); };
+        // the emitted partials in list order (sendEvent per partial: slot0 = e1, ts = currentTime)
+        uint32_t emits = 0, drops = 0;
+        for (uint32_t c = 0; c < np; c += 64) {
+            const uint32_t i = c + (uint32_t)lane;
+            bool em = false, dr = false;
+            if (i < np) {
+                DEnt<NW> x;
+                get(i, x);
+                dr = gone(x);
+                em = !dr && due(x);
+            }
+            emits += (uint32_t)__popcll(__ballot(em));
+            drops += (uint32_t)__popcll(__ballot(dr || em));
+        }
+        if (emits) {
+            unsigned long long base = 0;
+            if (lane == 0) base = atomicAdd(&A.o.raw_count[0], (unsigned long long)emits);
+            base = __shfl(base, 0, 64);
+            uint32_t r = 0;
+            const unsigned long long below = (1ull << lane) - 1ull;
+            for (uint32_t c = 0; c < np; c += 64) {
+                const uint32_t i = c + (uint32_t)lane;
+                bool em = false;
+                DEnt<NW> x{};
+                if (i < np) {
+                    get(i, x);
+                    em = !gone(x) && due(x);
+                }
+                const unsigned long long m = __ballot(em);
+                if (em) project(base, r + (uint32_t)__popcll(m & below), x.seq, t);
+                r += (uint32_t)__popcll(m);
+            }
+            rank += emits;
+            matches += emits;
+        }
+        if (drops) compact([&](uint32_t i, const DEnt<NW>& x) { return !(i < np && (gone(x) || due(x))); });
+        if (now > waiting + t) lst = now + waiting;
+        if (emits == 0 && lst < t) {
+            lst = t + waiting;
+            notifyAt(t + waiting, 1u);
+        }
+    }
+};
+
+// a wave-aggregated append to the second hand-over list (the general kernels take these keys)
+__device__ __forceinline__ void absd_handover(const GenArgs& a, uint32_t key, uint32_t start) {
+    if ((threadIdx.x & 63) == 0) {
+        const unsigned long long i = atomicAdd(a.fb2_n, 1ull);
+        gp(a.fb2_list)[i] = key;
+        if (a.fb2_start) gp(a.fb2_start)[key] = start;
+    }
+}
+
+__device__ void absd_stats(const GenArgs& a, unsigned long long sc, unsigned long long cr, unsigned long long ma,
+                           unsigned long long ky, uint32_t er, unsigned long long fb) {
+    if ((threadIdx.x & 63) == 0) {  // (a few waves: device-wide atomics are cheap here)
+        if (er) atomicOr(a.o.err, er);
+        if (sc) atomicAdd(&a.o.stats[GST_SCANNED], sc);
+        if (cr) atomicAdd(&a.o.stats[GST_CREATED], cr);
+        if (ma) atomicAdd(&a.o.stats[GST_MATCHES], ma);
+        if (ky) atomicAdd(&a.o.stats[GST_KEYS], ky);
+        if (fb) atomicAdd(&a.o.stats[GST_SPILLS], fb);
+    }
+}
+
+// ---- batch: one wave per handed-over key walks its events from where the register window stopped ----
+template <int NW> __device__ void absd_batch(const GenArgs& a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const cGenProgram& G = *(cGenProgram*)a.G;
+    unsigned long long sc = 0, cr = 0, ky = 0, fb = 0;
+    uint32_t er = 0;
+    const uint64_t nfb = *a.fb_n;
+    const int64_t tbase = a.b.pay ? gp(a.b.ts)[0] : 0;
+    for (uint64_t li = blockIdx.x; li < nfb; li += gridDim.x) {
+        const uint32_t key = __builtin_amdgcn_readfirstlane(gp(a.fb_list)[li]);
+        const uint32_t b = __builtin_amdgcn_readfirstlane(gp(a.fb_start)[key]);
+        const uint32_t e = __builtin_amdgcn_readfirstlane(gp(a.b.seg_end)[key]);
+        DeepKey<NW> L(a, smem, key);
+        if (!L.load()) {
+            absd_handover(a, key, b);
+            fb++;
+            continue;
+        }
+        uint32_t i = b;
+        for (; i < e; i++) {
+            // at most one new partial and n + 1 queue entries per event: stop before an event that could overflow
+            if (L.n + 1u > L.C || L.ql + L.n + 1u > G.Q) break;
+            AbsEv<NW> ev;
+            if (a.b.pay) {
+                abs_pay<NW>(a, i, tbase, ev);
+            } else {
+                const uint32_t pos = a.b.sidx ? gp(a.b.sidx)[i] : i;
+                ev.ts = gp(a.b.ts)[pos];
+                ev.seq = a.b.seq_base + pos;
+                abs_gather<NW>(a, G, pos, ev);
+            }
+            L.event(ev);
+        }
+        L.store();
+        if (i < e) {
+            absd_handover(a, key, i);
+            fb++;
+        } else {
+            if ((threadIdx.x & 63) == 0) gp(a.t.nd)[key] = L.deadline();
+            ky++;
+        }
+        sc += L.scanned;
+        cr += L.created;
+        er |= L.err;
+    }
+    absd_stats(a, sc, cr, 0ull, ky, er, fb);
+}
+
+// ---- timer sweep: one wave per handed-over due key ----
+template <int NW> __device__ void absd_timers(const GenArgs& a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const cGenProgram& G = *(cGenProgram*)a.G;
+    unsigned long long sc = 0, cr = 0, ma = 0, fb = 0;
+    uint32_t er = 0;
+    const uint64_t nfb = *a.fb_n;
+    for (uint64_t li = blockIdx.x; li < nfb; li += gridDim.x) {
+        const uint32_t key = __builtin_amdgcn_readfirstlane(gp(a.fb_list)[li]);
+        DeepKey<NW> L(a, smem, key);
+        if (!L.load()) {
+            absd_handover(a, key, 0u);
+            fb++;
+            continue;
+        }
+        for (int guard = 0; guard < (1 << 20); guard++) {  // Scheduler.sendTimerEvents
+            if (L.ql == 0) break;
+            const int64_t t = L.qread(L.qh);
+            if (t > a.now) break;
+            L.qh = L.qh + 1u == G.Q ? 0u : L.qh + 1u;
+            L.ql--;
+            L.timer(t, a.now);
+        }
+        L.store();
+        if ((threadIdx.x & 63) == 0) {
+            gp(a.t.nd)[key] = L.deadline();
+            if (a.t.kcnt) gp(a.t.kcnt)[key] = L.rank;
+        }
+        sc += L.scanned;
+        ma += L.matches;
+        er |= L.err;
+    }
+    if ((threadIdx.x & 63) == 0 && ma) atomicAdd(a.o.nvalid, ma);
+    absd_stats(a, sc, cr, ma, 0ull, er, fb);
+}
+
+}  // namespace
+
+// One kernel per captured-word count (NW), one wave per work-group, dynamic LDS = the key's lists.
+#define ABSD_KERNELS(NW)                                                                                            \
+    extern "C" __global__ void __launch_bounds__(64) k_absd_batch_##NW(const GenArgs* __restrict__ ap) {          \
+        absd_batch<NW>(*ap);                                                                                        \
+    }                                                                                                               \
+    extern "C" __global__ void __launch_bounds__(64) k_absd_timers_##NW(const GenArgs* __restrict__ ap) {         \
+        absd_timers<NW>(*ap);                                                                                       \
+    }
+ABSD_KERNELS(1)
+ABSD_KERNELS(2)
+ABSD_KERNELS(3)
+ABSD_KERNELS(4)
+ABSD_KERNELS(5)
+ABSD_KERNELS(6)
+ABSD_KERNELS(7)
+ABSD_KERNELS(8)

@@ -244,6 +244,10 @@ struct GenArgs {
     uint32_t* fb_list;
     unsigned long long* fb_n;
     uint32_t* fb_start;
+    // the wave-per-key kernels (absd_kernels.hip) take fb_list and hand what they cannot hold on in this one
+    uint32_t* fb2_list;
+    unsigned long long* fb2_n;
+    uint32_t* fb2_start;
 };
 // GenArgs.mode
 #define GEN_M_KEYLIST 1u   // k_gen_batch: lane i walks key fb_list[i] from fb_start[key]

@@ -36,6 +36,15 @@ ABS_DECL(1) ABS_DECL(2) ABS_DECL(3) ABS_DECL(4) ABS_DECL(5) ABS_DECL(6) ABS_DECL
 typedef void (*AbsKernel)(const GenArgs*);
 static const AbsKernel kAbsBatch[ABS_MAXNW + 1] = {nullptr, k_abs_batch_1, k_abs_batch_2, k_abs_batch_3, k_abs_batch_4,
                                                    k_abs_batch_5, k_abs_batch_6, k_abs_batch_7, k_abs_batch_8};
+#define ABSD_DECL(NW) extern "C" __global__ void k_absd_batch_##NW(const GenArgs* ap); \
+                      extern "C" __global__ void k_absd_timers_##NW(const GenArgs* ap);
+ABSD_DECL(1) ABSD_DECL(2) ABSD_DECL(3) ABSD_DECL(4) ABSD_DECL(5) ABSD_DECL(6) ABSD_DECL(7) ABSD_DECL(8)
+static const AbsKernel kAbsdBatch[ABS_MAXNW + 1] = {nullptr, k_absd_batch_1, k_absd_batch_2, k_absd_batch_3,
+                                                    k_absd_batch_4, k_absd_batch_5, k_absd_batch_6, k_absd_batch_7,
+                                                    k_absd_batch_8};
+static const AbsKernel kAbsdTimers[ABS_MAXNW + 1] = {nullptr, k_absd_timers_1, k_absd_timers_2, k_absd_timers_3,
+                                                     k_absd_timers_4, k_absd_timers_5, k_absd_timers_6, k_absd_timers_7,
+                                                     k_absd_timers_8};
 #define CNT_DECL(NW) extern "C" __global__ void k_cnt_batch_##NW(const GenArgs* ap);
 CNT_DECL(1) CNT_DECL(2) CNT_DECL(3) CNT_DECL(4) CNT_DECL(5) CNT_DECL(6) CNT_DECL(7) CNT_DECL(8)
 static const AbsKernel kCntBatch[ABS_MAXNW + 1] = {nullptr, k_cnt_batch_1, k_cnt_batch_2, k_cnt_batch_3, k_cnt_batch_4,
@@ -833,6 +842,8 @@ struct GenEngine {
     unsigned long long* live = nullptr;  // k_gen_live's sum (diagnostics)
     // keys the register-window kernels (abs_kernels.hip) hand to the general kernels
     uint32_t *fb_list = nullptr, *fb_start = nullptr;
+    uint32_t *fb2_list = nullptr, *fb2_start = nullptr;  // the wave-per-key kernels' hand-over (absd_kernels.hip)
+    unsigned long long* fb2_n = nullptr;
     unsigned long long* fb_n = nullptr;
     uint32_t* pay = nullptr;   // the key-sorted payload of the register-window kernel (pack.h Pay<W>)
     unsigned long long* wstats = nullptr;  // its per-wave counter rows
@@ -1040,6 +1051,11 @@ GenEngine* gen_create(const uint32_t* ir, size_t nw, const sg_config& cfg, hipSt
             e->fb_list = e->dalloc<uint32_t>(K);
             e->fb_start = e->dalloc<uint32_t>(K);
             e->fb_n = e->dalloc<unsigned long long>(1);
+            if (G.absOk && !getenv("SG_NO_ABSD")) {
+                e->fb2_list = e->dalloc<uint32_t>(K);
+                e->fb2_start = e->dalloc<uint32_t>(K);
+                e->fb2_n = e->dalloc<unsigned long long>(1);
+            }
             e->pay = e->dalloc<uint32_t>(B * 6);  // Pay<4>: 6 words
             e->wstats = e->dalloc<unsigned long long>((size_t)((K + 63) / 64) * GST_N);
             if (G.playback && G.partitioned && G.nStartup == 1) {
@@ -1094,7 +1110,8 @@ static size_t type_size(int t) {
 // the kernels read their arguments from a device ring (GEN_ARG_SLOTS slots, staged through pinned host
 // memory on the engine's stream); a slot is rewritten only after the stream has drained the launches
 // that used it
-enum { GEN_L_BATCH = 0, GEN_L_TIMERS = 1, GEN_L_DEADLINES = 2, GEN_L_ABS_BATCH = 3, GEN_L_ABS_TIMERS = 4, GEN_L_CNT_BATCH = 5 };
+enum { GEN_L_BATCH = 0, GEN_L_TIMERS = 1, GEN_L_DEADLINES = 2, GEN_L_ABS_BATCH = 3, GEN_L_ABS_TIMERS = 4, GEN_L_CNT_BATCH = 5,
+       GEN_L_ABSD_BATCH = 6, GEN_L_ABSD_TIMERS = 7 };
 // the general kernels over the keys a register-window kernel handed over: a fixed grid striding the list
 #define GEN_FB_BLOCKS 1024u
 // timer sweeps: a fixed grid of one-wave blocks striding over the due keys (their number is on the device)
@@ -1113,6 +1130,12 @@ static uint32_t gen_kpl(uint32_t K) {
 static bool abs_on(const GenEngine* e) {
     return e->host.absOk && e->host.projN == 0 && e->fb_list && e->tstage && e->keyorder;
 }
+// the wave-per-key kernels of absd_kernels.hip take the keys the register window hands over (their LDS slice:
+// one key's lists, partial_capacity entries of 20 + 4 NW bytes, within 64 KB); SG_NO_ABSD: A/B against the
+// general kernels (same results)
+static size_t absd_lds(const GenEngine* e) { return (size_t)e->host.L * (20u + 4u * e->host.absNW); }
+static bool absd_on(const GenEngine* e) { return e->fb2_list && absd_lds(e) <= 65536; }
+
 // the register-window kernel of cnt_kernels.hip runs this query (the shape, no device projection)
 static bool cnt_on(const GenEngine* e) { return e->host.cntOk && e->host.projN == 0 && e->fb_list; }
 
@@ -1130,6 +1153,11 @@ static void launch_gen(GenEngine* e, GenArgs a, int which) {
         hipLaunchKernelGGL(k_gen_timers, dim3(fb ? GEN_FB_BLOCKS : e->host.partitioned ? std::min(blocks, GEN_TIMER_BLOCKS) : 1u),
                            dim3(64), 0, e->stream, ap);
     else if (which == GEN_L_DEADLINES) hipLaunchKernelGGL(k_gen_deadlines, dim3(blocks), dim3(64), 0, e->stream, ap);
+    else if (which == GEN_L_ABSD_BATCH || which == GEN_L_ABSD_TIMERS) {
+        // one wave per handed-over key (a fixed grid striding over the list, whose length is on the device)
+        hipLaunchKernelGGL(which == GEN_L_ABSD_BATCH ? kAbsdBatch[e->host.absNW] : kAbsdTimers[e->host.absNW],
+                           dim3(GEN_FB_BLOCKS), dim3(64), (unsigned)absd_lds(e), e->stream, ap);
+    }
     else if (which == GEN_L_ABS_BATCH || which == GEN_L_ABS_TIMERS || which == GEN_L_CNT_BATCH) {
         // one lane per key / possible due slot (the due count is on the device); then the waves' counter rows
         hipLaunchKernelGGL(which == GEN_L_ABS_BATCH   ? kAbsBatch[e->host.absNW]
@@ -1275,6 +1303,16 @@ int gen_push(GenEngine* e, const sg_batch* b, std::string& msg) {
         a.fb_n = e->fb_n;
         a.fb_start = e->fb_start;
         launch_gen(e, a, GEN_L_ABS_BATCH);
+        if (absd_on(e)) {  // the deep keys, one wave each; what they cannot hold goes on to the general kernel
+            GH_OK(hipMemsetAsync(e->fb2_n, 0, 8, e->stream));
+            a.fb2_list = e->fb2_list;
+            a.fb2_n = e->fb2_n;
+            a.fb2_start = e->fb2_start;
+            launch_gen(e, a, GEN_L_ABSD_BATCH);
+            a.fb_list = e->fb2_list;
+            a.fb_n = e->fb2_n;
+            a.fb_start = e->fb2_start;
+        }
         a.mode = GEN_M_KEYLIST;
         launch_gen(e, a, GEN_L_BATCH);
         GH_OK(hipGetLastError());
@@ -1362,6 +1400,15 @@ int gen_advance(GenEngine* e, int64_t t, std::string& msg) {
         a.mode = GEN_M_NOPAIRS;
         a.t.due = e->fb_list;
         a.t.ndue = e->fb_n;
+        if (absd_on(e)) {
+            GH_OK(hipMemsetAsync(e->fb2_n, 0, 8, e->stream));
+            a.fb2_list = e->fb2_list;
+            a.fb2_n = e->fb2_n;
+            a.fb2_start = nullptr;
+            launch_gen(e, a, GEN_L_ABSD_TIMERS);
+            a.t.due = e->fb2_list;
+            a.t.ndue = e->fb2_n;
+        }
         launch_gen(e, a, GEN_L_TIMERS);
     } else {
         launch_gen(e, a, GEN_L_TIMERS);
