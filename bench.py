@@ -435,18 +435,21 @@ def api_async(sa, synth, n_keys, n, batch_max=1 << 16):
                     "ready polls), bounded sample"}
 
 
-def api_columnar(sa, synth, n_keys, chunk, chunks):
+def api_columnar(sa, synth, n_keys, chunk, chunks, strings="object"):
     """C2 through the columnar host API end to end (SiddhiManager -> InputHandler.send_columns with the
     symbol column dictionary-encoded (pandas.Categorical over the 2^20 key names) -> the HIP engine ->
     ColumnarQueryCallback with the projected select list as arrays).  Columns are built before the timed
     region; key interning, push, poll, projection decode and the callbacks are inside it.  A bounded
-    sample, beside `value`."""
+    sample, beside `value`.  strings="categorical": the callback takes its STRING items dictionary-encoded
+    too (ColumnarQueryCallback.string_columns) instead of as str objects."""
     import pandas as pd
     mgr = sa.SiddhiManager(n_keys=n_keys, max_batch=chunk)
     rt = mgr.createSiddhiAppRuntime(synth.C2_QUERY)
     got = [0, 0]
 
     class Count(sa.ColumnarQueryCallback):
+        string_columns = strings
+
         def receive_columns(self, timestamps, columns, trigger_seq):
             got[0] += 1
             got[1] += len(timestamps)
@@ -469,6 +472,7 @@ def api_columnar(sa, synth, n_keys, chunk, chunks):
     return {"value": chunk * chunks / el, "unit": "events/s", "events": chunk * chunks, "chunk": chunk,
             "keys": n_keys, "callbacks": got[0], "matches": got[1],
             "device_projection": bool(rt.queries[0].device_projection),
+            "string_columns": strings,
             "what": "C2 through SiddhiManager / InputHandler.send_columns (dictionary-encoded symbols) / "
                     "ColumnarQueryCallback, one send per chunk (host runtime + HIP engine), bounded sample"}
 
@@ -707,6 +711,7 @@ def main():
         out["api_inclusive"] = api_inclusive(sa, synth, 1 << 16, 1 << 16, 16)
         out["api_async"] = api_async(sa, synth, 1 << 16, 1 << 20)
         out["api_columnar"] = api_columnar(sa, synth, 1 << 20, 1 << 20, 8)
+        out["api_columnar_cat"] = api_columnar(sa, synth, 1 << 20, 1 << 20, 8, strings="categorical")
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(sa, synth, K, B, args.cpu_seconds)
     if rank == 0:

@@ -112,7 +112,13 @@ class ColumnarQueryCallback:
     match of it in QueryCallback's order — the rows QueryCallback.receive would get, one call per trigger
     there, concatenated.  `columns` maps each select item's name to a numpy array (STRING items: object
     arrays; null values: masked arrays, or None in object arrays); trigger_seq is the arrival sequence
-    number of each row's triggering event (SG_TIMER_SEQ for a timer-emitted match)."""
+    number of each row's triggering event (SG_TIMER_SEQ for a timer-emitted match).
+
+    string_columns = "categorical" (a class or instance attribute) delivers STRING items as
+    pandas.Categorical over the app's string dictionary instead: the codes only, no per-value string
+    objects (null: code -1) — send_columns' dictionary-encoded input, mirrored on the output."""
+
+    string_columns = "object"
 
     def receive_columns(self, timestamps, columns, trigger_seq):
         raise NotImplementedError
@@ -328,6 +334,16 @@ class StringDictionary:
             self._arr_of = self.strs   # (a restore that swaps in another list of the same length rebuilds)
         return a
 
+    def categorical_dtype(self, need):
+        """a pandas CategoricalDtype whose categories are the first >= `need` strings by id (code = id),
+        rebuilt only when an id beyond the cached one is asked for (or a restore swapped the list)"""
+        c = getattr(self, "_cat", None)
+        if c is None or c[0] < need or c[1] is not self.strs:
+            import pandas as pd
+            n = len(self.strs)
+            c = self._cat = (n, self.strs, pd.CategoricalDtype(pd.Index(self.strs[:n], dtype=object)))
+        return c[2]
+
     def ids_of(self, vals):
         """id_of over a column (one dict probe per value; new strings numbered in first-seen order)"""
         ids = self.ids
@@ -387,9 +403,11 @@ class _QueryRuntime:
         self.n_keys = app_rt.n_keys if cq.partitioned else 1
         self.engine = engine_factory(cq.ir, self.n_keys)
         try:   # engines that can hand out only the complete batches (sg_poll_matches | SG_POLL_READY)
-            self.ready_polls = "ready" in inspect.signature(self.engine.poll).parameters
+            params = inspect.signature(self.engine.poll).parameters
+            self.ready_polls = "ready" in params
+            self._view_polls = "copy" in params   # poll(copy=False): views of the engine's staging
         except (TypeError, ValueError):
-            self.ready_polls = False
+            self.ready_polls = self._view_polls = False
         # the select list on the device when it is plain expressions; else on the host
         self.device_projection = False
         prog = cp.projection_program(cq, app_rt.strings)
@@ -563,27 +581,38 @@ class _QueryRuntime:
 
     _NPT = {"INT": np.int32, "LONG": np.int64, "FLOAT": np.float32, "DOUBLE": np.float64, "BOOL": np.bool_}
 
-    def _decode_array(self, bits, null, typ):
-        """device projection bits of one item -> a typed numpy array (masked where null)"""
+    def _decode_array(self, bits, null, typ, strings="object"):
+        """device projection bits of one item -> a typed numpy array (masked where null); STRING items as
+        str objects, or (strings="categorical") as a pandas.Categorical of the dictionary ids"""
         if typ == "INT":
             vals = bits.astype(np.uint32).view(np.int32)
         elif typ == "LONG":
-            vals = bits.view(np.int64)
+            vals = bits.view(np.int64).copy()   # (bits may be a view of the engine's staging)
         elif typ == "FLOAT":
             vals = bits.astype(np.uint32).view(np.float32)
         elif typ == "DOUBLE":
-            vals = bits.view(np.float64)
+            vals = bits.view(np.float64).copy()
         elif typ == "BOOL":
             vals = (bits & 1).astype(np.bool_)
         else:   # STRING: the host dictionary id
+            if strings == "categorical":
+                import pandas as pd
+                sd = self.app_rt.strings
+                codes = bits.astype(np.int32 if len(sd.strs) < (1 << 31) else np.int64)
+                has_null = bool(null.any())
+                if has_null:
+                    codes[null != 0] = -1
+                dt = sd.categorical_dtype(int(codes.max()) + 1 if len(codes) else 0)
+                return pd.Categorical.from_codes(codes, dtype=dt, validate=False)
             strs = self.app_rt.strings.array()
-            ids = np.where(null != 0, len(strs) - 1, bits.astype(np.int64))
-            return strs[ids]
+            if not null.any():
+                return strs[bits]
+            return strs[np.where(null != 0, len(strs) - 1, bits.astype(np.int64))]
         return np.ma.MaskedArray(vals, mask=null != 0) if null.any() else vals
 
-    def project_columns(self, m, store):
+    def project_columns(self, m, store, strings="object"):
         """(timestamps, {name: array}, trigger_seq) of the matches, `having` applied (device projection);
-        the row projection transposed otherwise"""
+        the row projection transposed otherwise (strings: ColumnarQueryCallback.string_columns)"""
         sel = self.cq.select
         if self.device_projection and m.proj_value is not None:
             keep = None
@@ -595,12 +624,13 @@ class _QueryRuntime:
                 v, nl = m.proj_value[i], m.proj_null[i]
                 if keep is not None:
                     v, nl = v[keep], nl[keep]
-                cols[name] = self._decode_array(v, nl, typ)
+                cols[name] = self._decode_array(v, nl, typ, strings)
             ts, trig = (m.ts, m.trigger_seq) if keep is None else (m.ts[keep], m.trigger_seq[keep])
-            return np.asarray(ts, dtype=np.int64), cols, np.asarray(trig, dtype=np.uint64)
-        return self._rows_to_columns(self.project_host(m, store))
+            # (copies: the poll may have handed out views of the engine's staging)
+            return np.array(ts, dtype=np.int64), cols, np.array(trig, dtype=np.uint64)
+        return self._rows_to_columns(self.project_host(m, store), strings)
 
-    def _rows_to_columns(self, rows):
+    def _rows_to_columns(self, rows, strings="object"):
         sel = self.cq.select
         cols = {}
         for i, (name, typ, _) in enumerate(sel):
@@ -610,28 +640,48 @@ class _QueryRuntime:
             elif typ in self._NPT:
                 cols[name] = np.ma.MaskedArray(np.array([0 if v is None else v for v in vals], dtype=self._NPT[typ]),
                                                mask=[v is None for v in vals])
+            elif strings == "categorical" and typ == "STRING":
+                import pandas as pd
+                cols[name] = pd.Categorical(vals)
             else:
                 cols[name] = np.array(vals, dtype=object)
         return (np.array([r[1] for r in rows], dtype=np.int64), cols,
                 np.array([r[0] for r in rows], dtype=np.uint64))
 
+    def _rows_needed(self):
+        out = self.cq.output_stream
+        listen = bool(self.query_callbacks) or bool(out is not None and self.app_rt.stream_callbacks.get(out))
+        return listen, listen or (not self.device_projection and not self.columnar_callbacks)
+
+    def poll(self, ready=False):
+        """this query's matches (ready: only those of complete batches).  When nobody reads rows and the
+        select list runs on the device, the poll hands out views of the engine's staging instead of
+        copies: project_columns copies only what the callbacks get (never the slot chains)."""
+        kw = {"ready": True} if ready else {}
+        if self._view_polls and not self._rows_needed()[1]:
+            return self.engine.poll(copy=False, **kw)
+        return self.engine.poll(**kw)
+
     def deliver(self, m, store):
         """the matches of one poll to the callbacks / the output stream (QuerySelector -> OutputCallback).
         Rows are built only for row listeners (QueryCallbacks, StreamCallbacks of the output stream) and
         for the host selector's aggregator states; a device projection nobody reads as rows stays arrays."""
-        out = self.cq.output_stream
-        listen = bool(self.query_callbacks) or bool(out is not None and self.app_rt.stream_callbacks.get(out))
+        listen, need_rows = self._rows_needed()
         rows = None
-        if listen or (not self.device_projection and not self.columnar_callbacks):
+        if need_rows:
             rows = self.project(m, store)
             if listen:
                 self.dispatch(rows)
         if self.columnar_callbacks and len(m):
             # host projection updates aggregator states: project once, transpose the rows
-            cols = self._rows_to_columns(rows) if rows is not None and not self.device_projection \
-                else self.project_columns(m, store)
-            if len(cols[0]):
-                for cb in self.columnar_callbacks:
+            made = {}
+            for cb in self.columnar_callbacks:
+                mode = "categorical" if getattr(cb, "string_columns", "object") == "categorical" else "object"
+                cols = made.get(mode)
+                if cols is None:
+                    cols = made[mode] = self._rows_to_columns(rows, mode) \
+                        if rows is not None and not self.device_projection else self.project_columns(m, store, mode)
+                if len(cols[0]):
                     cb.receive_columns(*cols)
 
     def dispatch(self, projected):
@@ -910,7 +960,7 @@ class SiddhiAppRuntime:
             pg.next_run = self.wall_time() + pg.interval
         for qr in self.queries:
             qr.engine.advance_time(self.current_time())
-            qr.deliver(qr.engine.poll(), self.store)
+            qr.deliver(qr.poll(), self.store)
 
     # -- clock -------------------------------------------------------------------------------------
     def wall_time(self):
@@ -951,7 +1001,7 @@ class SiddhiAppRuntime:
         for qr in self.queries:
             qr.engine.advance_time(now)
             if poll:
-                qr.deliver(qr.engine.poll(), self.store)
+                qr.deliver(qr.poll(), self.store)
 
     def _set_event_time(self, ts, poll=True):
         """TimestampGeneratorImpl.setCurrentTimestamp (playback)."""
@@ -1198,7 +1248,7 @@ class SiddhiAppRuntime:
         cols, nulls = self._columns(sd, rows)
         kk = np.repeat(np.array(ids, dtype=np.uint32), n)
         qr.engine.push(si, seqs[0], ts_all, cols, nulls, kk)
-        qr.deliver(qr.engine.poll(), self.store)
+        qr.deliver(qr.poll(), self.store)
 
     def _send(self, stream, events, explicit=True):
         """events: [(timestamp, data list)]"""
@@ -1282,17 +1332,17 @@ class SiddhiAppRuntime:
         if self._inflight:
             qs, self._inflight = self._inflight, []
             for qr in qs:
-                qr.deliver(qr.engine.poll(), self.store)
+                qr.deliver(qr.poll(), self.store)
 
     def _collect(self, qr, pipelined):
         """the matches of qr's engine after a push: all of them (a synchronous send), or only those of the
         batches already complete (an @async batch: SG_POLL_READY, no wait for the batch just pushed)"""
         if pipelined and qr.ready_polls:
-            qr.deliver(qr.engine.poll(ready=True), self.store)
+            qr.deliver(qr.poll(ready=True), self.store)
             if qr not in self._inflight:
                 self._inflight.append(qr)
         else:
-            qr.deliver(qr.engine.poll(), self.store)
+            qr.deliver(qr.poll(), self.store)
 
     def flush(self):
         """Deliver everything sent so far (the @async streams' buffered events included).  Not in the
@@ -1415,18 +1465,22 @@ class SiddhiAppRuntime:
                         codes = np.asarray(kc.codes)
                         cid = self._category_ids(kc.categories, ("key", id(qr.key_dict)),
                                                  lambda cats: qr.key_dict.intern(java_strings(cats)))
-                        kids = np.where(codes < 0, np.uint32(SG_KEY_NULL),
-                                        cid[np.where(codes < 0, 0, codes)] if len(cid) else np.uint32(SG_KEY_NULL))
+                        neg = codes < 0
+                        if not neg.any() and len(cid):
+                            kids = self._map_codes(codes, cid)   # (the common case: no null key)
+                        else:
+                            kids = np.where(neg, np.uint32(SG_KEY_NULL),
+                                            cid[np.where(neg, 0, codes)] if len(cid) else np.uint32(SG_KEY_NULL))
                         kids = np.asarray(kids, dtype=np.uint32)
                     else:
                         keyvals = kc if kc.dtype.kind == "S" else java_strings(kc.tolist())
                         kids = np.asarray(qr.key_dict.intern(keyvals), dtype=np.uint32)
                 except EngineError as ex:
                     raise RuntimeError(f"more than {qr.n_keys} partition keys") from ex
-                keep = np.nonzero(kids != SG_KEY_NULL)[0]
-                if len(keep) == n:
+                if not (kids == np.uint32(SG_KEY_NULL)).any():
                     qr.engine.push(si, base, ts_all, cols, nulls, kids)
                 else:
+                    keep = np.nonzero(kids != SG_KEY_NULL)[0]
                     cut = np.nonzero(np.diff(keep) != 1)[0] + 1
                     for idx in np.split(keep, cut):
                         if len(idx) == 0:
@@ -1442,6 +1496,7 @@ class SiddhiAppRuntime:
         push stale ids"""
         self.__dict__.pop("_cat_cache", None)
         self.strings.__dict__.pop("_arr", None)
+        self.strings.__dict__.pop("_cat", None)
         for kd in self.key_dicts.values():
             kd.drop_string_cache()
 
@@ -1456,10 +1511,25 @@ class SiddhiAppRuntime:
         cats = [None if v is None else (v.decode("utf-8") if isinstance(v, bytes) else str(v))
                 for v in list(categories)]
         ids = np.asarray(make(cats), dtype=np.uint32)
+        # categories interned in order onto fresh ids map affinely (ids[i] = ids[0] + i): flag it so a send
+        # maps its codes with one sequential add instead of a random gather over the id table
+        if len(ids) and int(ids[-1]) - int(ids[0]) == len(ids) - 1 and \
+                bool((np.diff(ids.astype(np.int64)) == 1).all()):
+            ids = _AffineIds(ids)
         if len(cache) >= 16:   # callers building new categories per send: keep the cache bounded
             cache.clear()
         cache[(id(categories), what)] = (categories, len(categories), ids)
         return ids
+
+    @staticmethod
+    def _map_codes(codes, ids):
+        """ids[codes] for non-negative categorical codes"""
+        if isinstance(ids, _AffineIds):
+            out = codes.astype(np.uint32)
+            if ids.base0:
+                out += np.uint32(ids.base0)
+            return out
+        return ids[codes]
 
     def _columns_np(self, sd, cols_in):
         """_columns over arrays: numeric arrays convert in one call, masked arrays give the null bytes,
@@ -1470,8 +1540,13 @@ class SiddhiAppRuntime:
             if at == "STRING" and _is_categorical(c):
                 codes = np.asarray(c.codes)
                 ids = self._category_ids(c.categories, "attr", lambda cats: self.strings.ids_of(cats))
-                cols.append(ids[np.where(codes < 0, 0, codes)] if len(ids) else np.zeros(len(codes), np.uint32))
-                nulls.append((codes < 0).astype(np.uint8) if (codes < 0).any() else None)
+                neg = codes < 0
+                if not neg.any():
+                    cols.append(self._map_codes(codes, ids) if len(ids) else np.zeros(len(codes), np.uint32))
+                    nulls.append(None)
+                    continue
+                cols.append(ids[np.where(neg, 0, codes)] if len(ids) else np.zeros(len(codes), np.uint32))
+                nulls.append(neg.astype(np.uint8))
                 continue
             if at == "STRING" and c.dtype.kind in "SU":
                 vals = c.tolist() if c.dtype.kind == "U" else [x.decode("utf-8") for x in c.tolist()]
@@ -1560,6 +1635,18 @@ def _has_absent(node, seen=None):
 def _is_categorical(c):
     """a dictionary-encoded column (pandas.Categorical or anything with .codes / .categories)"""
     return hasattr(c, "codes") and hasattr(c, "categories")
+
+
+class _AffineIds(np.ndarray):
+    """a category id table that is a contiguous run (ids[i] = base0 + i)"""
+
+    def __new__(cls, ids):
+        obj = np.asarray(ids, dtype=np.uint32).view(cls)
+        obj.base0 = int(ids[0])
+        return obj
+
+    def __array_finalize__(self, obj):
+        self.base0 = getattr(obj, "base0", 0)
 
 
 class _OneAttr:

@@ -40,10 +40,19 @@ class Cols(sa.ColumnarQueryCallback):
             c = columns[nm]
             if np.ma.isMaskedArray(c):
                 vals.append([None if m else x for x, m in zip(c.data.tolist(), np.ma.getmaskarray(c).tolist())])
+            elif type(c).__name__ == "Categorical":   # string_columns = "categorical"
+                assert self.string_columns == "categorical"
+                cats = list(c.categories)
+                vals.append([None if k < 0 else cats[k] for k in np.asarray(c.codes).tolist()])
             else:
                 vals.append(c.tolist())
         assert len(trigger_seq) == len(timestamps)
         self.rows += list(zip(timestamps.tolist(), map(tuple, zip(*vals))))
+
+
+class CatCols(Cols):
+    """STRING items delivered dictionary-encoded (pandas.Categorical)"""
+    string_columns = "categorical"
 
 
 def _norm(rows):
@@ -201,6 +210,53 @@ def test_categorical_columns():
     ref, _, _ = _run(C2, chunks, columnar=False)
     _, got, _ = _run(C2, chunks, columnar=True)
     assert len(ref) > 0 and _norm(got) == _norm(ref)
+
+
+def test_categorical_id_maps_affine_and_gathered():
+    """category sets whose ids form one contiguous run map codes with an add (from id 0, and from a later
+    base once other keys hold the first ids); a reordered / overlapping set takes the gather: all three
+    give send(Event[])'s callbacks"""
+    pd = pytest.importorskip("pandas")
+    sets = [pd.Index([f"K{k}" for k in range(23)]),                 # fresh ids 0..22: affine, base 0
+            pd.Index([f"K{k}" for k in reversed(range(23))]),       # same keys reversed: gathered
+            pd.Index([f"N{k}" for k in range(23)])]                 # fresh ids 23..45: affine, base 23
+    chunks = []
+    base = 0
+    for s, cats in enumerate(sets):
+        d = synth.stock_ticks(base, 1500, 23, seed=30 + s, rate_per_ms=4)
+        codes = d["key"].astype(np.int64)
+        col = pd.Categorical.from_codes(codes, categories=cats)
+        syms = [cats[c] for c in codes.tolist()]
+        events = [sa.Event(t, [k, p, v]) for t, k, p, v in
+                  zip(d["ts"].tolist(), syms, d["price"].tolist(), d["volume"].tolist())]
+        chunks.append((d["ts"], [col, d["price"], d["volume"]], events))
+        base += 1500
+    ref, _, _ = _run(C2, chunks, columnar=False)
+    _, got, _ = _run(C2, chunks, columnar=True)
+    assert len(ref) > 0 and _norm(got) == _norm(ref)
+
+
+def test_categorical_string_output():
+    """ColumnarQueryCallback.string_columns = "categorical": STRING items arrive as pandas.Categorical
+    (null: code -1) with the values the object-array callback gets, beside it on the same query"""
+    pytest.importorskip("pandas")
+    app = ("define stream S (symbol string, price float, venue string);\n"
+           "partition with (symbol of S) begin @info(name = 'q') from every e1=S[price>20] -> "
+           "e2=S[price>e1.price] within 1 sec select e1.symbol as sym, e2.venue as venue, "
+           "e2.price - e1.price as d insert into O; end;")
+    rt = oracle_manager().createSiddhiAppRuntime(app)
+    obj, cat = Cols(), CatCols()
+    rt.addCallback("q", obj)
+    rt.addCallback("q", cat)
+    rt.start()
+    h = rt.getInputHandler("S")
+    for b in range(3):
+        ts, colv, _ = _stream(1500, 23, seed=40 + b)
+        venue = np.array([None if v % 7 == 0 else f"V{v % 5}" for v in colv[2].tolist()], dtype=object)
+        h.send_columns(ts + b * 10_000, [colv[0], colv[1], venue])
+    rt.shutdown()
+    assert len(obj.rows) > 0 and cat.rows == obj.rows and cat.calls == obj.calls
+    assert any(r[1][1] is None for r in obj.rows) and any(r[1][1] is not None for r in obj.rows)
 
 
 @pytest.mark.parametrize("purge", [False, True])

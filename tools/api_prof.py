@@ -16,6 +16,7 @@ legs = {
     "api_inclusive": lambda: bench.api_inclusive(sa, synth, 1 << 16, 1 << 16, 16),
     "api_async": lambda: bench.api_async(sa, synth, 1 << 16, 1 << 20),
     "api_columnar": lambda: bench.api_columnar(sa, synth, 1 << 20, 1 << 20, 8),
+    "api_columnar_cat": lambda: bench.api_columnar(sa, synth, 1 << 20, 1 << 20, 8, strings="categorical"),
 }
 want = sys.argv[1:] or list(legs)
 for name in want:
@@ -28,3 +29,4 @@ for name in want:
     pr.disable()
     print(f"== {name} under cProfile: {r['value']:.4g} events/s", flush=True)
     pstats.Stats(pr).sort_stats("tottime").print_stats(25)
+    pstats.Stats(pr).sort_stats("cumtime").print_stats("runtime.py|native.py|bench.py", 25)
