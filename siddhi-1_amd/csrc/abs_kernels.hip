@@ -11,8 +11,11 @@
 //   absent processor p1  a window of ABS_R partials {e1 ts, e1 seq, e1's attribute words, null bits}
 //                        in list order (pending slots, then staged), lastScheduledTime, the timer queue's
 //                        head / length (entries appended straight to the HBM ring)
-// and write the lists back once per key, in a canonical layout of the general blocks (StateEvent 0 = the
-// seed, StateEvent 1 + j / StreamEvent j = partial j, free bitmaps rebuilt).  The state stays the general
+// and write the lists back once per key into the general blocks: StateEvent 0 = the seed, and each partial
+// keeps the pool entry it was created in (StreamEvent e, StateEvent 1 + e) for its whole life, so a
+// write-back stores the list words, the header, word 0 of the free bitmaps and only the records of the
+// partials created in this walk (a key loaded in another layout is rewritten whole, partial j at entry j).
+// The state stays the general
 // engine's state: snapshots, state documents, purge and the general kernels read it unchanged.  A key this
 // path cannot hold (a shared or foreign-shaped list, more than ABS_R partials, a queue about to fill) is
 // handed to the general kernel from the event where it stops (k_gen_batch GEN_M_KEYLIST) or for its whole
@@ -56,6 +59,15 @@ template <int NW, bool TM> struct AbsKey {
     uint32_t w[ABS_R][NW];
     uint32_t nb[ABS_R];
     uint32_t n, np;
+    uint32_t px[ABS_R];   // slot j's pool entry: StreamEvent px[j], StateEvent 1 + px[j]
+    uint32_t used;        // the pool entries in use (bit e)
+    uint32_t dpool;       // the pool entries whose records this walk wrote into registers (stored)
+    bool canon;           // loaded in this layout: only the new records and bitmap word 0 need storing
+    uint32_t hw0;         // pool entries [0, hw0) hold their constant words (GEN_W0_POOLC, as loaded)
+    uint32_t used0;       // the entries of the partials as loaded (checked: their constant words are in place)
+    bool seed0;           // a seed was loaded (at StateEvent 0), with timestamp seedTs0
+    int64_t seedTs0;
+    uint32_t h0[8];       // the header words as loaded (canon: only the changed ones are stored)
     bool sbad;            // the staged slots may be out of ts order (promotion sorts them)
     uint32_t seedPend, seedStg;
     int64_t seedPendTs, seedStgTs;
@@ -69,7 +81,8 @@ template <int NW, bool TM> struct AbsKey {
     unsigned long long scanned, created, matches;
 
     __device__ AbsKey(const GenProgram* g, uint32_t* state, uint32_t K_, uint32_t key)
-        : G(*(cGenProgram*)g), S(gp(state)), K(K_), k(key), n(0), np(0), sbad(false), seedPend(0), seedStg(0),
+        : G(*(cGenProgram*)g), S(gp(state)), K(K_), k(key), n(0), np(0), used(0), dpool(0), canon(false),
+          hw0(0), used0(0), seed0(false), seedTs0(0), sbad(false), seedPend(0), seedStg(0),
           seedPendTs(-1), seedStgTs(-1), f0(0), f1(0), lst(0), qh(0), ql(0), qhv(0), qb(0), err(0), scanned(0), created(0),
           matches(0) {
         ks0 = G.offKS + (uint32_t)G.absP0 * G.ksWords;
@@ -91,13 +104,17 @@ template <int NW, bool TM> struct AbsKey {
 
     // ---- load: false = this key's lists are not of the shape the window holds (the general kernel takes it)
     __device__ __forceinline__ bool load() {
-        if (!(W(0) & 1u)) {  // PartitionRuntimeImpl.initPartition: p0.init() stages one seed; p1.partitionCreated()
+#pragma unroll
+        for (int j = 0; j < ABS_R; ++j) px[j] = (uint32_t)j;
+        const uint32_t w0 = W(0);
+        if (!(w0 & 1u)) {  // PartitionRuntimeImpl.initPartition: p0.init() stages one seed; p1.partitionCreated()
             seedStg = 1;
             seedStgTs = -1;
             f0 = GF_INIT;
             f1 = GF_STARTED;
-            return true;
+            return true;     // (canon = false: the zeroed block is written whole)
         }
+        canon = true;
         f0 = W(ks0 + KS_FLAGS);
         f1 = W(ks1 + KS_FLAGS);
         if ((f0 | f1) & (GF_INACTIVE | GF_RUNNING)) return false;
@@ -112,10 +129,14 @@ template <int NW, bool TM> struct AbsKey {
                 if (W(b + ST_SLOTS + (uint32_t)s) != GEN_NIL) return false;
             const int64_t t = R64(b + ST_TS);
             if (p0n) { seedPend = 1; seedPendTs = t; } else { seedStg = 1; seedStgTs = t; }
+            canon = canon && st == 0u;
+            seed0 = true;
+            seedTs0 = t;
         }
         np = W(ks1 + KS_PLEN);
         const uint32_t ns = W(ks1 + KS_NLEN);
         if (np + ns > (uint32_t)ABS_R) return false;
+        const uint32_t lim = pool_lim();
         n = np + ns;
         bool ok = true;
         int64_t prev = 0;
@@ -137,30 +158,50 @@ template <int NW, bool TM> struct AbsKey {
                 const int64_t t = R64(b + ST_TS);
                 ok = ok && W(eb + SE_NEXT) == GEN_NIL && W(eb + SE_RC) == 1u && R64(eb + SE_TS) == t;
                 ts[j] = t;
-                seq[j] = (uint64_t)R64(eb + SE_SEQ);
-                nb[j] = W(eb + SE_NULL);
-                const int na = G.nattr[stream];
-                for (int a = 0; a < na; a++) {
-                    const int ty = G.attrType[stream][a];
-                    const bool wide = ty == SG_T_LONG || ty == SG_T_DOUBLE;
-                    const uint32_t o = G.absOff[a];
-                    const uint32_t lo = W(eb + SE_ATTR + 2 * (uint32_t)a);
-                    const uint32_t hi = wide ? W(eb + SE_ATTR + 2 * (uint32_t)a + 1) : 0u;
-#pragma unroll
-                    for (int q = 0; q < NW; ++q) {
-                        if ((uint32_t)q == o) w[j][q] = lo;
-                        if (wide && (uint32_t)q == o + 1) w[j][q] = hi;
-                    }
-                }
+                canon = canon && st == 1u + e && e < lim;
+                px[j] = e < G.SECAP ? e : 0u;
+                used |= e < 32u ? 1u << e : 0u;
                 if ((uint32_t)j > np && ts_before(t, prev)) sbad = true;
                 prev = t;
             }
         }
         if (!ok) return false;
+        // the partials' payload: the timer sweep of a key in this layout reads none of it (a timer tests
+        // timestamps; an emitted partial's seq is read when it fires, and no record is rewritten)
+        if (!TM || !canon) {
+#pragma unroll
+            for (int j = 0; j < ABS_R; ++j) {
+                if ((uint32_t)j < n) {
+                    const uint32_t eb = G.offSE + px[j] * G.seWords;
+                    seq[j] = (uint64_t)R64(eb + SE_SEQ);
+                    nb[j] = W(eb + SE_NULL);
+                    const int na = G.nattr[stream];
+                    for (int a = 0; a < na; a++) {
+                        const int ty = G.attrType[stream][a];
+                        const bool wide = ty == SG_T_LONG || ty == SG_T_DOUBLE;
+                        const uint32_t o = G.absOff[a];
+                        const uint32_t lo = W(eb + SE_ATTR + 2 * (uint32_t)a);
+                        const uint32_t hi = wide ? W(eb + SE_ATTR + 2 * (uint32_t)a + 1) : 0u;
+#pragma unroll
+                        for (int q = 0; q < NW; ++q) {
+                            if ((uint32_t)q == o) w[j][q] = lo;
+                            if (wide && (uint32_t)q == o + 1) w[j][q] = hi;
+                        }
+                    }
+                }
+            }
+        }
+        hw0 = (canon && (w0 & GEN_W0_POOLC)) ? (w0 >> 2) & 63u : 0u;
+        used0 = used;
+        if (!canon) {  // rewritten whole at the store, partial j at entry j
+#pragma unroll
+            for (int j = 0; j < ABS_R; ++j) px[j] = (uint32_t)j;
+        }
         lst = R64(ks1 + KS_LST);
         qh = W(ks1 + KS_QHEAD);
         ql = W(ks1 + KS_QLEN);
         if (qh >= G.Q || ql > G.Q) return false;
+        hdr(h0);
         if constexpr (TM) {
             qfill();
         } else {
@@ -180,10 +221,135 @@ template <int NW, bool TM> struct AbsKey {
         qhv = qbuf[0];
     }
 
-    // ---- store: the lists in the canonical layout (StateEvent 0 = the seed, 1 + j = partial j over
-    // StreamEvent j), free bitmaps rebuilt, the queue header
+    // the pool entries a partial may take: e < 31 (StateEvent 1 + e in bitmap word 0) and inside both pools
+    __device__ __forceinline__ uint32_t pool_lim() const {
+        uint32_t l = 31u;
+        l = G.SECAP < l ? G.SECAP : l;
+        l = G.STCAP - 1u < l ? G.STCAP - 1u : l;
+        return l;
+    }
+    // the partials the window may hold: its slots, and pool entries for all of them
+    __device__ __forceinline__ uint32_t cap_n() const {
+        const uint32_t l = pool_lim();
+        return l < (uint32_t)ABS_R ? l : (uint32_t)ABS_R;
+    }
+    // a pool entry for a new partial (the lowest free one: n < cap_n() <= pool_lim entries are in use)
+    __device__ __forceinline__ uint32_t alloc() {
+        const uint32_t lim = pool_lim();
+        const uint32_t fr = ~used & (lim >= 32u ? 0xffffffffu : ((1u << lim) - 1u));
+        // (branch-free: a branch that updates one member or another becomes a select of member addresses,
+        // which puts the struct in scratch)
+        const uint32_t e = fr ? (uint32_t)__ffs(fr) - 1u : 0u;
+        const uint32_t bit = fr ? 1u << e : 0u;
+        err |= fr ? 0u : (uint32_t)GERR_REF;
+        used |= bit;
+        dpool |= bit;
+        return e;
+    }
+
+    // ---- store: the header, the list words, the records of the partials this walk created (every record
+    // when the key was loaded in another layout), the free bitmaps (word 0; all words then)
     __device__ __forceinline__ void store() const {
-        W(0) = 1u;
+        if (!canon) {
+            store_all();
+            return;
+        }
+        uint32_t h[8];
+        hdr(h);
+        const uint32_t at[8] = {ks0 + KS_FLAGS, ks0 + KS_PLEN, ks0 + KS_NLEN, ks1 + KS_FLAGS, ks1 + KS_LST,
+                                ks1 + KS_LST + 1, ks1 + KS_QHEAD, ks1 + KS_QLEN};
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            if (h[i] != h0[i]) W(at[i]) = h[i];
+        if (seedPend && !h0[1]) W(ks0 + KS_LISTS) = 0u;
+        if (seedStg && !h0[2]) W(ks0 + KS_LISTS + G.L) = 0u;
+        uint32_t cw = 0;   // entries whose records (constant words included) this store writes
+        const int64_t sts = seedPend ? seedPendTs : seedStgTs;
+        if ((seedPend | seedStg) && (!seed0 || sts != seedTs0)) {
+            const uint32_t b = G.offST;
+            W64(b + ST_TS, sts);
+            if (!seed0) {
+                W(b + ST_TYPE) = 0u;
+                W(b + ST_RC) = 1u;
+                for (int s = 0; s < G.nslots; s++) W(b + ST_SLOTS + (uint32_t)s) = GEN_NIL;
+            }
+        }
+        W(ks1 + KS_PLEN) = np;
+        W(ks1 + KS_NLEN) = n - np;
+        for (uint32_t j = 0; j < n; j++) {   // (slot j's registers picked by selects: no dynamic indexing)
+            uint32_t e = 0, pn = 0, pw[NW];
+            int64_t t = 0;
+            uint64_t q = 0;
+#pragma unroll
+            for (int x = 0; x < NW; ++x) pw[x] = 0;
+#pragma unroll
+            for (int y = 0; y < ABS_R; ++y) {
+                if ((uint32_t)y == j) {
+                    e = px[y]; t = ts[y]; q = seq[y]; pn = nb[y];
+#pragma unroll
+                    for (int x = 0; x < NW; ++x) pw[x] = w[y][x];
+                }
+            }
+            W(ks1 + KS_LISTS + (j < np ? j : G.L + j - np)) = 1u + e;
+            if ((dpool >> e) & 1u) {
+                put_record(e, t, q, pn, pw);
+                cw |= 1u << e;
+            }
+        }
+        // the entries whose constant words are now known in place: below hw0, the partials loaded, the records
+        // just written; the new mark is the run of them from entry 0
+        const uint32_t V = (hw0 >= 32u ? 0xffffffffu : ((1u << hw0) - 1u)) | used0 | cw;
+        const uint32_t hw = ~V ? (uint32_t)__ffs(~V) - 1u : 32u;
+        if (hw != hw0) W(0) = 1u | GEN_W0_POOLC | (hw << 2);
+        W(G.offSTfree) = ((seedPend | seedStg) ? 1u : 0u) | (used << 1);
+        W(G.offSEfree) = used;
+    }
+    // pool entry e's constant words (a partial of this shape: StateEvent 1 + e of type 0 holding StreamEvent e
+    // in slot0, both referenced once, no chain)
+    __device__ __forceinline__ void put_consts(uint32_t e) const {
+        const uint32_t b = G.offST + (1u + e) * G.stWords;
+        const uint32_t eb = G.offSE + e * G.seWords;
+        W(b + ST_TYPE) = 0u;
+        W(b + ST_RC) = 1u;
+        for (int s = 0; s < G.nslots; s++) W(b + ST_SLOTS + (uint32_t)s) = s == slot0 ? e : GEN_NIL;
+        W(eb + SE_NEXT) = GEN_NIL;
+        W(eb + SE_RC) = 1u;
+    }
+    // the header words store() compares: p0 flags / pending / staged seed counts, p1 flags, lastScheduledTime,
+    // the timer queue's head and length
+    __device__ __forceinline__ void hdr(uint32_t (&h)[8]) const {
+        h[0] = f0; h[1] = seedPend; h[2] = seedStg; h[3] = f1;
+        h[4] = (uint32_t)(uint64_t)lst; h[5] = (uint32_t)((uint64_t)lst >> 32); h[6] = qh; h[7] = ql;
+    }
+    // a partial's StateEvent / StreamEvent records at its pool entry e
+    __device__ __forceinline__ void put_record(uint32_t e, int64_t t, uint64_t q, uint32_t pn,
+                                               const uint32_t (&pw)[NW]) const {
+        const uint32_t b = G.offST + (1u + e) * G.stWords;
+        const uint32_t eb = G.offSE + e * G.seWords;
+        W64(b + ST_TS, t);
+        if (e >= hw0) put_consts(e);
+        W64(eb + SE_SEQ, (int64_t)q);
+        W64(eb + SE_TS, t);
+        W(eb + SE_NULL) = pn;
+        const int na = G.nattr[stream];
+        for (int a = 0; a < na; a++) {
+            const int ty = G.attrType[stream][a];
+            const bool wide = ty == SG_T_LONG || ty == SG_T_DOUBLE;
+            const uint32_t o = G.absOff[a];
+            uint32_t lo = 0, hi = 0;
+#pragma unroll
+            for (int x = 0; x < NW; ++x) {
+                if ((uint32_t)x == o) lo = pw[x];
+                if ((uint32_t)x == o + 1) hi = pw[x];
+            }
+            W(eb + SE_ATTR + 2 * (uint32_t)a) = lo;
+            if (wide) W(eb + SE_ATTR + 2 * (uint32_t)a + 1) = hi;
+        }
+    }
+    // a key loaded in another layout (or created here): every record, partial j at entry j (px[j] = j: the
+    // window's entries were assigned in slot order), the constant words of the free entries, every bitmap word
+    __device__ __forceinline__ void store_all() const {
+        W(0) = 1u | GEN_W0_POOLC | (n << 2);  // (entries [0, n) written below)
         W(ks0 + KS_FLAGS) = f0;
         W(ks0 + KS_PLEN) = seedPend;
         W(ks0 + KS_NLEN) = seedStg;
@@ -277,6 +443,7 @@ template <int NW, bool TM> struct AbsKey {
 
     // ---- the window ----
     __device__ __forceinline__ void copy_slot(int d, int s) {
+        px[d] = px[s];
         ts[d] = ts[s];
         seq[d] = seq[s];
 #pragma unroll
@@ -289,6 +456,11 @@ template <int NW, bool TM> struct AbsKey {
         drop &= (n >= 32u ? 0xffffffffu : ((1u << n) - 1u));
         if (!drop) return;
         const uint32_t keep = ((n >= 32u ? 0xffffffffu : ((1u << n) - 1u))) & ~drop;
+        if (canon) {  // the dropped partials' pool entries are free again
+#pragma unroll
+            for (int j = 0; j < ABS_R; ++j)
+                if ((drop >> j) & 1u) used &= ~(1u << px[j]);
+        }
         uint32_t d[ABS_R];
 #pragma unroll
         for (int j = 0; j < ABS_R; ++j) d[j] = __popc(drop & ((1u << j) - 1u));
@@ -322,6 +494,7 @@ template <int NW, bool TM> struct AbsKey {
 #pragma unroll
                         for (int x = 0; x < NW; ++x) { uint32_t c = w[j][x]; w[j][x] = w[j + 1][x]; w[j + 1][x] = c; }
                         uint32_t c = nb[j]; nb[j] = nb[j + 1]; nb[j + 1] = c;
+                        c = px[j]; px[j] = px[j + 1]; px[j + 1] = c;
                     }
                 }
             }
@@ -429,9 +602,11 @@ template <int NW, bool TM> struct AbsKey {
                 // StreamPostStateProcessor: the seed becomes the partial (ts = e1.ts) -> p1.addState
                 // (staged; schedules e1.ts + T); `every`: p0.addEveryState (a new seed, staged, same ts)
                 const uint32_t t = n;
+                const uint32_t e = canon ? alloc() : t;   // (store_all writes partial j at entry j)
 #pragma unroll
                 for (int j = 0; j < ABS_R; ++j) {
                     if ((uint32_t)j == t) {
+                        px[j] = e;
                         ts[j] = ev.ts;
                         seq[j] = ev.seq;
 #pragma unroll
@@ -480,9 +655,11 @@ template <int NW, bool TM> struct AbsKey {
         for (uint32_t m = emit; m; m &= m - 1u) {
             const uint32_t j = (uint32_t)__ffs(m) - 1u;
             uint64_t q = 0;
+            uint32_t e = 0;
 #pragma unroll
             for (int x = 0; x < ABS_R; ++x)
-                if ((uint32_t)x == j) q = seq[x];
+                if ((uint32_t)x == j) { q = seq[x]; e = px[x]; }
+            if (TM && canon) q = (uint64_t)R64(G.offSE + e * G.seWords + SE_SEQ);  // (not loaded: see load)
             project(q, t, a);
         }
         remove(drop);
@@ -528,7 +705,7 @@ template <int NW> __device__ void abs_batch(const GenArgs& a) {
         for (; i < e; i++) {
             // at most n + 1 appends to the queue and one new partial per event: stop before an event that
             // could overflow the window or the queue (the general kernel continues from it)
-            if (L.n + 1u > (uint32_t)ABS_R || L.ql + L.n + 1u > G.Q) break;
+            if (L.n + 1u > L.cap_n() || L.ql + L.n + 1u > G.Q) break;
             AbsEv<NW> ev;
             if (a.b.pay) {
                 abs_pay<NW>(a, i, tbase, ev);

@@ -49,6 +49,10 @@ __host__ __device__ inline size_t gen_at(uint32_t K, uint32_t blockWords, uint32
 #define GEN_NIL 0xffffu  // null pool index
 #define GEN_RAWSEG 256   // raw-match reservation counters of a batch
 #define GEN_RESCHUNK 4   // raw matches a lane reserves at a time
+// a key block's word 0: bit 0 = initialised; GEN_W0_POOLC = abs_kernels.hip's layout with the constant words
+// (type, refcounts, slot links) of pool entries [0, bits 2..7) in place, so its stores skip them (cleared by
+// every other kernel that writes the block)
+#define GEN_W0_POOLC 2u
 #define ABS_R 8          // abs_kernels.hip: partials a key's register window holds
 #define ABS_MAXNW 8      // abs_kernels.hip: attribute words of an event it captures
 #define CNT_R 8          // cnt_kernels.hip: events a count chain in registers holds (the shape's max count)

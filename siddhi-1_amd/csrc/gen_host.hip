@@ -587,6 +587,51 @@ __global__ void k_gen_bump(unsigned long long* count, const uint32_t* t_cnt, con
     else *count += (unsigned long long)t_off[n - 1] + t_cnt[n - 1];
 }
 
+// the per-batch / per-advance resets of the engine's counters and per-key bounds in one launch (a
+// hipMemsetAsync each was a fill kernel of its own: ~26 per C4 step)
+#define GEN_CLEAR_JOBS 8
+struct GenClear {
+    uint32_t n;
+    uint32_t v[GEN_CLEAR_JOBS];      // the 32-bit fill value
+    uint64_t words[GEN_CLEAR_JOBS];  // 32-bit words
+    uint32_t* p[GEN_CLEAR_JOBS];     // 16-B aligned (device allocations)
+};
+__global__ void __launch_bounds__(256) k_gen_clear(const GenClear c) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, st = (uint64_t)gridDim.x * blockDim.x;
+    for (uint32_t q = 0; q < c.n; ++q) {
+        const uint32_t v = c.v[q];
+        const uint64_t n4 = c.words[q] >> 2;
+        uint4* p4 = (uint4*)c.p[q];
+        for (uint64_t k = i; k < n4; k += st) p4[k] = make_uint4(v, v, v, v);
+        for (uint64_t k = n4 * 4 + i; k < c.words[q]; k += st) c.p[q][k] = v;
+    }
+}
+struct GenClearList {
+    GenClear c{};
+    uint64_t most = 0;
+    void add(void* p, uint64_t bytes, uint32_t v = 0u) {
+        c.p[c.n] = (uint32_t*)p;
+        c.words[c.n] = bytes / 4;
+        c.v[c.n++] = v;
+        most = std::max<uint64_t>(most, bytes / 4);
+    }
+    hipError_t launch(hipStream_t s) const {
+        if (!c.n) return hipSuccess;
+        const uint64_t blocks = std::min<uint64_t>(std::max<uint64_t>((most / 4 + 255) / 256, 1), 2048);
+        hipLaunchKernelGGL(k_gen_clear, dim3((unsigned)blocks), dim3(256), 0, s, c);
+        return hipGetLastError();
+    }
+};
+
+// the slots k_timer_prep filled in the due heads' hash set back to empty (instead of refilling the whole
+// 2 K-slot table before every advance)
+__global__ void k_ht_clear(const uint32_t* __restrict__ ins, const unsigned long long* __restrict__ ndue,
+                           unsigned long long* __restrict__ ht) {
+    const uint64_t n = *ndue;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        if (ins[i] != 0xffffffffu) ht[ins[i]] = ~0ull;
+}
+
 __global__ void k_gen_fill64(int64_t* x, uint64_t n, int64_t v) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) x[i] = v;
@@ -644,7 +689,7 @@ __device__ __forceinline__ uint64_t gen_hmix(uint64_t x) {
 __global__ void __launch_bounds__(GEN_TPREP_BLOCK) k_timer_prep(
         const unsigned long long* __restrict__ dkey, const uint32_t* __restrict__ dkid,
         const unsigned long long* __restrict__ ndue, int64_t T, const uint32_t* __restrict__ kcnt,
-        unsigned long long* __restrict__ ht, uint64_t htmask, uint32_t* __restrict__ rel_c,
+        unsigned long long* __restrict__ ht, uint64_t htmask, uint32_t* __restrict__ ht_ins, uint32_t* __restrict__ rel_c,
         uint32_t* __restrict__ kid_c, unsigned long long* __restrict__ hkey_c, unsigned long long* __restrict__ ctr) {
     constexpr uint32_t NW = GEN_TPREP_BLOCK / 64;
     __shared__ uint32_t wcnt[NW];
@@ -661,11 +706,12 @@ __global__ void __launch_bounds__(GEN_TPREP_BLOCK) k_timer_prep(
         if (di < n) {
             h = dkey[di];
             kid = dkid[di];
+            uint32_t ins = 0xffffffffu;   // the slot this entry filled (k_ht_clear empties it)
             if (h != ~0ull && kid != GEN_PAIR_NONE) {
                 uint64_t p = gen_hmix(h) & htmask;
                 for (uint64_t probe = 0; probe <= htmask; probe++) {
                     const unsigned long long prev = atomicCAS(&ht[p], ~0ull, h);
-                    if (prev == ~0ull) break;
+                    if (prev == ~0ull) { ins = (uint32_t)p; break; }
                     if (prev == h) { ctr[3] = 1ull; break; }
                     p = (p + 1) & htmask;
                 }
@@ -676,6 +722,7 @@ __global__ void __launch_bounds__(GEN_TPREP_BLOCK) k_timer_prep(
                 mx = max(mx, r);
                 has = (kcnt[kid] & ~GEN_KCNT_STAGED) != 0u;
             }
+            ht_ins[di] = ins;
         }
         const unsigned long long m = __ballot(has);
         if (lane == 0) wcnt[wv] = (uint32_t)__popcll(m);
@@ -858,6 +905,7 @@ struct GenEngine {
     unsigned long long* ht = nullptr;   // the due heads' hash set (A.10 check), 2^k >= 2 K slots
     uint64_t htmask = 0;
     unsigned long long* ctr = nullptr;  // k_timer_prep's counters
+    uint32_t* ht_ins = nullptr;         // [npairs_cap] the hash slot each due entry filled
     void* ksort_tmp = nullptr;
     size_t ksort_tmp_bytes = 0;
     void* kscan_tmp = nullptr;
@@ -1033,6 +1081,8 @@ GenEngine* gen_create(const uint32_t* ir, size_t nw, const sg_config& cfg, hipSt
                     while (hs < 2 * (uint64_t)K) hs <<= 1;
                     e->ht = e->dalloc<unsigned long long>(hs);
                     e->htmask = hs - 1;
+                    e->ht_ins = e->dalloc<uint32_t>(std::max<uint64_t>(e->npairs_cap, 1));
+                    GH_OK(hipMemsetAsync(e->ht, 0xff, hs * 8, stream));   // empty; kept empty by k_ht_clear
                     size_t t1 = 0, t2 = 0;
                     GH_OK(rocprim::radix_sort_pairs_desc<KeySortConfig>(nullptr, t1, e->rel, e->srel, e->kid_c, e->skid,
                                                                         (size_t)K, 0, 32, stream));
@@ -1216,8 +1266,15 @@ int gen_push(GenEngine* e, const sg_batch* b, std::string& msg) {
             }
         }
     }
-    GH_OK(hipMemsetAsync(e->seg_begin, 0, (size_t)e->K * 4, e->stream));
-    GH_OK(hipMemsetAsync(e->seg_end, 0, (size_t)e->K * 4, e->stream));
+    {   // per-key bounds, the raw-record counters and the hand-over lists' counts: one launch
+        GenClearList cl;
+        cl.add(e->seg_begin, (size_t)e->K * 4);
+        cl.add(e->seg_end, (size_t)e->K * 4);
+        cl.add(e->raw_count, 8 * GEN_RAWSEG);
+        if (abs_on(e) || cnt_on(e)) cl.add(e->fb_n, 8);
+        if (abs_on(e) && absd_on(e)) cl.add(e->fb2_n, 8);
+        GH_OK(cl.launch(e->stream));
+    }
     if (G.partitioned) {
         const uint32_t* keys = b->key;
         if (!dev) {
@@ -1288,7 +1345,6 @@ int gen_push(GenEngine* e, const sg_batch* b, std::string& msg) {
     }
     a.b.seg_begin = e->seg_begin;
     a.b.seg_end = e->seg_end;
-    GH_OK(hipMemsetAsync(e->raw_count, 0, 8 * GEN_RAWSEG, e->stream));
     a.o.nseg = GEN_RAWSEG;
     a.o.seg_cap = e->rawCap / GEN_RAWSEG;
     if (e->timing)  // sg_stats.live_at_batch_start (outside the batch kernel's span)
@@ -1298,13 +1354,11 @@ int gen_push(GenEngine* e, const sg_batch* b, std::string& msg) {
         // the register-window kernel, then the general kernel over the keys it handed over; this shape
         // emits nothing on events (an absent state's processAndReturn returns nothing; its matches come
         // from the timers), so there is no batch ordering
-        GH_OK(hipMemsetAsync(e->fb_n, 0, 8, e->stream));
         a.fb_list = e->fb_list;
         a.fb_n = e->fb_n;
         a.fb_start = e->fb_start;
         launch_gen(e, a, GEN_L_ABS_BATCH);
         if (absd_on(e)) {  // the deep keys, one wave each; what they cannot hold goes on to the general kernel
-            GH_OK(hipMemsetAsync(e->fb2_n, 0, 8, e->stream));
             a.fb2_list = e->fb2_list;
             a.fb2_n = e->fb2_n;
             a.fb2_start = e->fb2_start;
@@ -1325,7 +1379,6 @@ int gen_push(GenEngine* e, const sg_batch* b, std::string& msg) {
     if (cnt_on(e)) {
         // the register-window kernel, then the general kernel over the keys it handed over (whole runs);
         // both write raw records + per-trigger counts, ordered below
-        GH_OK(hipMemsetAsync(e->fb_n, 0, 8, e->stream));
         a.fb_list = e->fb_list;
         a.fb_n = e->fb_n;
         a.fb_start = e->fb_start;
@@ -1346,8 +1399,11 @@ int gen_push(GenEngine* e, const sg_batch* b, std::string& msg) {
                            e->raw_count, e->rawCap / GEN_RAWSEG, (uint32_t)GEN_RAWSEG, e->t_off, e->out);
     hipLaunchKernelGGL(k_gen_bump, dim3(1), dim3(1), 0, e->stream, e->out.count, e->t_cnt, e->t_off, n,
                        (const unsigned long long*)nullptr);
-    GH_OK(hipMemsetAsync(e->t_cnt, 0, (size_t)n * 4, e->stream));
-    GH_OK(hipGetLastError());
+    {
+        GenClearList cl;   // (the per-trigger counts back to zero for the next batch)
+        cl.add(e->t_cnt, (size_t)n * 4);
+        GH_OK(cl.launch(e->stream));
+    }
     e->st.events += n;
     e->st.batches++;
     e->st.advance_launches++;
@@ -1382,9 +1438,16 @@ int gen_advance(GenEngine* e, int64_t t, std::string& msg) {
     GenArgs a = e->args();
     a.now = t;         // the advance target (playback: the event clock)
     a.now0 = e->now;   // the clock before it (wall-clock callers run at their own times)
-    GH_OK(hipMemsetAsync(e->raw_count, 0, 8, e->stream));
-    GH_OK(hipMemsetAsync(e->nvalid, 0, 8, e->stream));
-    GH_OK(hipMemsetAsync(e->tm.ndue, 0, 8, e->stream));
+    {
+        GenClearList cl;
+        cl.add(e->raw_count, 8);
+        cl.add(e->nvalid, 8);
+        cl.add(e->tm.ndue, 8);
+        if (abs_on(e)) cl.add(e->fb_n, 8);
+        if (abs_on(e) && absd_on(e)) cl.add(e->fb2_n, 8);
+        if (e->keyorder) cl.add(e->ctr, 32);
+        GH_OK(cl.launch(e->stream));
+    }
     if (G.partitioned) {  // the keys with a deadline <= t: one pass over nd[K]
         const uint32_t blocks = std::min<uint32_t>((e->K + 4095) / 4096, 1024u);
         hipLaunchKernelGGL(k_gen_due, dim3(blocks), dim3(256), 0, e->stream, e->tm.nd, e->K, t, e->tm.due, e->tm.ndue);
@@ -1392,7 +1455,6 @@ int gen_advance(GenEngine* e, int64_t t, std::string& msg) {
     a.o.nseg = 1;
     a.o.seg_cap = e->rawCap;
     if (abs_on(e)) {  // the register-window sweep, then the general sweep over the keys it handed over
-        GH_OK(hipMemsetAsync(e->fb_n, 0, 8, e->stream));
         a.fb_list = e->fb_list;
         a.fb_n = e->fb_n;
         a.fb_start = nullptr;
@@ -1401,7 +1463,6 @@ int gen_advance(GenEngine* e, int64_t t, std::string& msg) {
         a.t.due = e->fb_list;
         a.t.ndue = e->fb_n;
         if (absd_on(e)) {
-            GH_OK(hipMemsetAsync(e->fb2_n, 0, 8, e->stream));
             a.fb2_list = e->fb2_list;
             a.fb2_n = e->fb2_n;
             a.fb2_start = nullptr;
@@ -1414,12 +1475,11 @@ int gen_advance(GenEngine* e, int64_t t, std::string& msg) {
         launch_gen(e, a, GEN_L_TIMERS);
     }
     if (e->keyorder) {  // the A.10 check and the keys with matches, before the one host round trip
-        GH_OK(hipMemsetAsync(e->ctr, 0, 32, e->stream));
-        GH_OK(hipMemsetAsync(e->ht, 0xff, (e->htmask + 1) * 8, e->stream));
         const uint32_t blocks = std::min<uint32_t>((e->K + GEN_TPREP_BLOCK - 1) / GEN_TPREP_BLOCK, 1024u);
         hipLaunchKernelGGL(k_timer_prep, dim3(blocks), dim3(GEN_TPREP_BLOCK), 0, e->stream, e->tm.dpair_key,
-                           e->tm.dpair_kid, e->tm.ndue, t, e->tm.kcnt, e->ht, e->htmask, e->rel, e->kid_c, e->hkey_c,
-                           e->ctr);
+                           e->tm.dpair_kid, e->tm.ndue, t, e->tm.kcnt, e->ht, e->htmask, e->ht_ins, e->rel, e->kid_c,
+                           e->hkey_c, e->ctr);
+        hipLaunchKernelGGL(k_ht_clear, dim3(blocks), dim3(GEN_TPREP_BLOCK), 0, e->stream, e->ht_ins, e->tm.ndue, e->ht);
     }
     unsigned long long nr = 0, ndue = 0, kctr[4] = {0, 0, 0, 0};
     GH_OK(hipMemcpyAsync(&nr, e->raw_count, 8, hipMemcpyDeviceToHost, e->stream));

@@ -1092,8 +1092,12 @@ struct Lane {
     }
 
     __device__ void initKey() __restrict__ {  // PartitionRuntimeImpl.initPartition -> StateStreamRuntime.initPartition
-        if (W(0) & 1u) return;
-        W(0) |= 1u;
+        const uint32_t w0 = W(0);
+        if (w0 & 1u) {
+            if (w0 & GEN_W0_POOLC) W(0) = 1u;  // (this kernel's allocations do not keep abs_kernels' pool words)
+            return;
+        }
+        W(0) = 1u;
         for (int i = 0; i < G.nInit; i++) init(G.initOrder[i]);
         for (int i = 0; i < G.nStartup; i++) partitionCreated(G.startup[i]);
     }
@@ -1286,6 +1290,8 @@ __device__ void gen_timers_key(const GenArgs& a, uint32_t key, uint64_t di, unsi
         // unpartitioned: QueryRuntimeImpl.start seeds the query at the clock of start()
         L.now = G.playback ? a.now0 : a.now;
         L.initKey();
+    } else if (L.W(0) & GEN_W0_POOLC) {
+        L.W(0) = 1u;  // (see initKey)
     }
     const int64_t T = a.now;
     if (G.playback) {

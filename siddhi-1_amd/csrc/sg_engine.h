@@ -23,7 +23,9 @@
 #define SGD_MAX_CONST 32   // filter constants (kernel arguments, so equal-shaped queries share code)
 #define SGD_MAX_REG 16     // register window (partials per lane) upper bound
 #define SGD_WAVE 64
+#ifndef SGD_BLOCK
 #define SGD_BLOCK 256      // lanes (= keys) per workgroup of the advance kernel
+#endif
 #define SGD_STAGE_MAX_BYTES 147456  // LDS per workgroup staging its keys' payload runs (upper bound; the
                                     // static LDS of the lane dealing sits beside it in the 160 KB)
 // key-sorted payload timestamps are 32-bit offsets from the batch's first (arrival-order) timestamp;

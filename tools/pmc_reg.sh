@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 export SG_EXP_STEPS=3
 mkdir -p gpurun_out/pmc_reg
-for cfg in C4 C3_min1; do
+for cfg in ${PMC_CFGS:-C4 C3_min1}; do
   timeout -s KILL 200 rocprofv3 --kernel-trace --stats -d gpurun_out/pmc_reg/${cfg}_trace -o run --output-format csv \
       -- python3 tools/exp_gen.py $cfg > gpurun_out/pmc_reg/${cfg}_trace.log 2>&1 || { echo "trace $cfg failed"; tail -5 gpurun_out/pmc_reg/${cfg}_trace.log; exit 1; }
   echo "trace $cfg ok"
