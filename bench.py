@@ -76,17 +76,31 @@ def cpu_model():
 
 
 def distinct_cores(n):
-    """up to n CPUs of this process's affinity mask on distinct physical cores (one SMT sibling each), or
-    [] when the mask does not hold n such cores"""
+    """up to n CPUs of this process's affinity mask, spread over the L3 caches first (round-robin over the
+    L3 domains: the oracle's per-shard state is tens of MB, and threads that share an L3 evict each other's)
+    and on distinct physical cores (one SMT sibling each); [] when the mask does not hold n such cores"""
+    def rd(path):
+        with open(path) as f:
+            return f.read().strip()
     try:
-        seen, out = set(), []
+        seen, groups = set(), {}
         for c in sorted(os.sched_getaffinity(0)):
-            base = f"/sys/devices/system/cpu/cpu{c}/topology/"
-            core = (open(base + "physical_package_id").read().strip(), open(base + "core_id").read().strip())
-            if core not in seen:
-                seen.add(core)
-                out.append(c)
-        return out[:n] if len(out) >= n else []
+            base = f"/sys/devices/system/cpu/cpu{c}/"
+            core = (rd(base + "topology/physical_package_id"), rd(base + "topology/core_id"))
+            if core in seen:
+                continue
+            seen.add(core)
+            try:
+                l3 = rd(base + "cache/index3/id")
+            except OSError:
+                l3 = core[0]
+            groups.setdefault((core[0], l3), []).append(c)
+        out, lists = [], [g for _, g in sorted(groups.items())]
+        while len(out) < n and any(lists):
+            for g in lists:
+                if g and len(out) < n:
+                    out.append(g.pop(0))
+        return out if len(out) >= n else []
     except (AttributeError, OSError):
         return []
 
@@ -140,10 +154,11 @@ def cpu_baseline(sa, synth, n_keys, batch, seconds):
     # chunk (ctypes drops the GIL around them) and the threads share nothing but the allocator.
     quota = cpu_quota()
     T = max(1, int(quota) if quota else int(os.environ.get("OMP_NUM_THREADS", 0)) or (os.cpu_count() or 1))
+    T = int(os.environ.get("SG_CPU_THREADS", T))   # (tools/cpu_leg.py: scaling sweeps)
     total = int(min(batch * 4, single * seconds * T * 0.5)) // (T * chunk) * (T * chunk) or T * chunk
     d = synth.stock_ticks(0, total, n_keys)
-    # S = 4T key shards (key % S), one oracle engine each; the T threads take whole shards from a shared queue
-    # (a shard's chunks run in order on one thread), so a slow core does not hold the others back
+    # S = 4T key shards (key % S), one oracle engine each, four per thread (a shard's chunks run in order on
+    # its thread)
     S = 4 * T
     own = d["key"] % np.uint32(S)
     # each shard's events in two halves: the first half runs untimed (the engines' state reaches its
@@ -177,23 +192,19 @@ def cpu_baseline(sa, synth, n_keys, batch, seconds):
     e0.close()
     engs = [sa.NativeEngine(lib, "sgo_", cq.ir, n_keys=(n_keys + S - 1) // S) for _ in range(S)]
     busy = [0.0] * T
-    # each thread on a physical core of its own: the quota counts CPUs, and two threads on SMT siblings of
-    # one core share its caches and pipelines (the oracle's walk is memory-latency bound)
+    # each thread on a physical core of its own, spread over the L3 domains: the quota counts CPUs, two
+    # threads on SMT siblings share a core, and threads sharing an L3 thrash it (a shard's state is tens of
+    # MB at 2^20 keys: one thread alone has the whole L3)
     pins = distinct_cores(T)
 
     def phase(half):
-        queue = list(range(S))
-        qlock = threading.Lock()
-
+        # thread r owns shards r, r + T, ... in both halves: an engine's memory is allocated and freed by
+        # one thread (glibc's per-thread arenas; a free of another arena's block takes that arena's lock)
         def work(r):
             if pins:
                 os.sched_setaffinity(0, {pins[r]})   # (the calling thread)
             t = time.perf_counter()
-            while True:
-                with qlock:
-                    if not queue:
-                        break
-                    sh = queue.pop(0)
+            for sh in range(r, S, T):
                 run_shard(engs[sh], shards[sh][half])
             busy[r] = time.perf_counter() - t
 
@@ -233,7 +244,7 @@ def cpu_baseline(sa, synth, n_keys, batch, seconds):
                                    "vs_single_prefix": par / single / T,
                                    "thread_busy_s": [round(b, 3) for b in busy],
                                    "sample": f"first {total} events of the C2 stream, keys sharded key % {S} (4 shards "
-                                             f"per thread, taken from a shared queue), one oracle engine per shard; "
+                                             f"per thread, the same ones in both halves), one oracle engine per shard; "
                                              f"each shard's first half untimed, its second half ({timed} events) timed"},
             "C1": {"value": c1_done / c1_busy, "unit": "events/s", "cores": 1,
                    "sample": f"first {c1_done} events of the C1 stream (unpartitioned, 1 event per ms, "
