@@ -789,11 +789,11 @@ template <int NW> __device__ void abs_timers(const GenArgs& a) {
 
 // One kernel per captured-word count (NW = the stream's attributes as 32-bit words, long / double 2 each).
 #define ABS_KERNELS(NW)                                                                                             \
-    extern "C" __global__ void __launch_bounds__(64) k_abs_batch_##NW(const GenArgs* __restrict__ ap) {           \
-        abs_batch<NW>(*ap);                                                                                         \
+    extern "C" __global__ void __launch_bounds__(64) k_abs_batch_##NW(const GenArgs ap) {           \
+        abs_batch<NW>(ap);                                                                                         \
     }                                                                                                               \
-    extern "C" __global__ void __launch_bounds__(64) k_abs_timers_##NW(const GenArgs* __restrict__ ap) {          \
-        abs_timers<NW>(*ap);                                                                                        \
+    extern "C" __global__ void __launch_bounds__(64) k_abs_timers_##NW(const GenArgs ap) {          \
+        abs_timers<NW>(ap);                                                                                        \
     }
 ABS_KERNELS(1)
 ABS_KERNELS(2)

@@ -629,11 +629,11 @@ template <int NW> __device__ void absd_timers(const GenArgs& a) {
 
 // One kernel per captured-word count (NW), one wave per work-group, dynamic LDS = the key's lists.
 #define ABSD_KERNELS(NW)                                                                                            \
-    extern "C" __global__ void __launch_bounds__(64) k_absd_batch_##NW(const GenArgs* __restrict__ ap) {          \
-        absd_batch<NW>(*ap);                                                                                        \
+    extern "C" __global__ void __launch_bounds__(64) k_absd_batch_##NW(const GenArgs ap) {          \
+        absd_batch<NW>(ap);                                                                                        \
     }                                                                                                               \
-    extern "C" __global__ void __launch_bounds__(64) k_absd_timers_##NW(const GenArgs* __restrict__ ap) {         \
-        absd_timers<NW>(*ap);                                                                                       \
+    extern "C" __global__ void __launch_bounds__(64) k_absd_timers_##NW(const GenArgs ap) {         \
+        absd_timers<NW>(ap);                                                                                       \
     }
 ABSD_KERNELS(1)
 ABSD_KERNELS(2)

@@ -482,8 +482,8 @@ template <int NW> __device__ void cnt_batch(const GenArgs& a) {
 
 // One kernel per captured-word count (NW = the stream's attributes as 32-bit words, long / double 2 each).
 #define CNT_KERNELS(NW)                                                                                             \
-    extern "C" __global__ void __launch_bounds__(64) k_cnt_batch_##NW(const GenArgs* __restrict__ ap) {           \
-        cnt_batch<NW>(*ap);                                                                                         \
+    extern "C" __global__ void __launch_bounds__(64) k_cnt_batch_##NW(const GenArgs ap) {           \
+        cnt_batch<NW>(ap);                                                                                         \
     }
 CNT_KERNELS(1)
 CNT_KERNELS(2)

@@ -29,15 +29,15 @@
 #include "pinned.h"
 #include "state_doc.h"
 
-extern "C" __global__ void k_gen_batch(const GenArgs* ap);
-#define ABS_DECL(NW) extern "C" __global__ void k_abs_batch_##NW(const GenArgs* ap); \
-                     extern "C" __global__ void k_abs_timers_##NW(const GenArgs* ap);
+extern "C" __global__ void k_gen_batch(const GenArgs ap);
+#define ABS_DECL(NW) extern "C" __global__ void k_abs_batch_##NW(const GenArgs ap); \
+                     extern "C" __global__ void k_abs_timers_##NW(const GenArgs ap);
 ABS_DECL(1) ABS_DECL(2) ABS_DECL(3) ABS_DECL(4) ABS_DECL(5) ABS_DECL(6) ABS_DECL(7) ABS_DECL(8)
-typedef void (*AbsKernel)(const GenArgs*);
+typedef void (*AbsKernel)(const GenArgs);
 static const AbsKernel kAbsBatch[ABS_MAXNW + 1] = {nullptr, k_abs_batch_1, k_abs_batch_2, k_abs_batch_3, k_abs_batch_4,
                                                    k_abs_batch_5, k_abs_batch_6, k_abs_batch_7, k_abs_batch_8};
-#define ABSD_DECL(NW) extern "C" __global__ void k_absd_batch_##NW(const GenArgs* ap); \
-                      extern "C" __global__ void k_absd_timers_##NW(const GenArgs* ap);
+#define ABSD_DECL(NW) extern "C" __global__ void k_absd_batch_##NW(const GenArgs ap); \
+                      extern "C" __global__ void k_absd_timers_##NW(const GenArgs ap);
 ABSD_DECL(1) ABSD_DECL(2) ABSD_DECL(3) ABSD_DECL(4) ABSD_DECL(5) ABSD_DECL(6) ABSD_DECL(7) ABSD_DECL(8)
 static const AbsKernel kAbsdBatch[ABS_MAXNW + 1] = {nullptr, k_absd_batch_1, k_absd_batch_2, k_absd_batch_3,
                                                     k_absd_batch_4, k_absd_batch_5, k_absd_batch_6, k_absd_batch_7,
@@ -45,15 +45,15 @@ static const AbsKernel kAbsdBatch[ABS_MAXNW + 1] = {nullptr, k_absd_batch_1, k_a
 static const AbsKernel kAbsdTimers[ABS_MAXNW + 1] = {nullptr, k_absd_timers_1, k_absd_timers_2, k_absd_timers_3,
                                                      k_absd_timers_4, k_absd_timers_5, k_absd_timers_6, k_absd_timers_7,
                                                      k_absd_timers_8};
-#define CNT_DECL(NW) extern "C" __global__ void k_cnt_batch_##NW(const GenArgs* ap);
+#define CNT_DECL(NW) extern "C" __global__ void k_cnt_batch_##NW(const GenArgs ap);
 CNT_DECL(1) CNT_DECL(2) CNT_DECL(3) CNT_DECL(4) CNT_DECL(5) CNT_DECL(6) CNT_DECL(7) CNT_DECL(8)
 static const AbsKernel kCntBatch[ABS_MAXNW + 1] = {nullptr, k_cnt_batch_1, k_cnt_batch_2, k_cnt_batch_3, k_cnt_batch_4,
                                                    k_cnt_batch_5, k_cnt_batch_6, k_cnt_batch_7, k_cnt_batch_8};
 static const AbsKernel kAbsTimers[ABS_MAXNW + 1] = {nullptr, k_abs_timers_1, k_abs_timers_2, k_abs_timers_3,
                                                     k_abs_timers_4, k_abs_timers_5, k_abs_timers_6, k_abs_timers_7,
                                                     k_abs_timers_8};
-extern "C" __global__ void k_gen_timers(const GenArgs* ap);
-extern "C" __global__ void k_gen_deadlines(const GenArgs* ap);
+extern "C" __global__ void k_gen_timers(const GenArgs ap);
+extern "C" __global__ void k_gen_deadlines(const GenArgs ap);
 extern "C" __global__ void k_gen_due(const int64_t* nd, uint32_t K, int64_t now, uint32_t* due,
                                      unsigned long long* ndue);
 extern "C" __global__ void k_gen_collapse(const unsigned long long* key, const uint32_t* li, uint64_t n,
@@ -798,15 +798,18 @@ __global__ void k_timer_bump(unsigned long long* count, const uint32_t* c, const
 __global__ void __launch_bounds__(256) k_gen_stats_reduce(const unsigned long long* __restrict__ w, uint32_t rows,
                                                           unsigned long long* __restrict__ stats) {
     __shared__ unsigned long long part[4];
+    // block (c, y): counter c over rows y, y + gridDim.y, ... (a few loads per lane in flight instead of a
+    // 64-deep dependent loop in one block per counter)
     const uint32_t c = blockIdx.x;
     unsigned long long x = 0;
-    for (uint32_t r = threadIdx.x; r < rows; r += blockDim.x) x += w[(size_t)r * GST_N + c];
+    for (uint32_t r = blockIdx.y * blockDim.x + threadIdx.x; r < rows; r += gridDim.y * blockDim.x)
+        x += w[(size_t)r * GST_N + c];
     for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
     if ((threadIdx.x & 63) == 0) part[threadIdx.x / 64] = x;
     __syncthreads();
     if (threadIdx.x == 0) {
         const unsigned long long t = part[0] + part[1] + part[2] + part[3];
-        if (t) stats[c] += t;
+        if (t) atomicAdd(&stats[c], t);
     }
 }
 __global__ void k_timer_off(const uint32_t* __restrict__ skid, uint64_t n, const uint32_t* __restrict__ off,
@@ -843,8 +846,6 @@ struct TimerLess {
 // ---------------------------------------------------------------------------------------------
 // the engine
 // ---------------------------------------------------------------------------------------------
-#define GEN_ARG_SLOTS 64
-
 struct GenEngine {
     // gen_keep_timer_heads: the last advance's emitting keys in head order and their heads (host copies)
     bool keep_heads = false;
@@ -910,9 +911,6 @@ struct GenEngine {
     size_t ksort_tmp_bytes = 0;
     void* kscan_tmp = nullptr;
     size_t kscan_tmp_bytes = 0;
-    GenArgs* d_args = nullptr;           // kernel argument ring (device) and its pinned staging
-    GenArgs* h_args = nullptr;
-    uint64_t arg_next = 0;
     uint32_t* err = nullptr;
     OutBufs out{};
     PinnedVec<uint64_t> h_trig, h_slot;
@@ -955,7 +953,6 @@ struct GenEngine {
         }
         for (auto& x : spans) { (void)hipEventDestroy(x.a); (void)hipEventDestroy(x.b); }
         for (void* p : owned) (void)hipFree(p);
-        if (h_args) (void)hipHostFree(h_args);
     }
 
     GenArgs args() const {
@@ -1121,8 +1118,6 @@ GenEngine* gen_create(const uint32_t* ir, size_t nw, const sg_config& cfg, hipSt
                 }
             e->paysort_tmp = e->dalloc<uint8_t>(e->paysort_tmp_bytes);
         }
-        e->d_args = e->dalloc<GenArgs>(GEN_ARG_SLOTS);
-        GH_OK(hipHostMalloc((void**)&e->h_args, sizeof(GenArgs) * GEN_ARG_SLOTS, hipHostMallocDefault));
         GH_OK(hipMemsetAsync(e->stats, 0, GST_N * 8, stream));
         e->err = e->dalloc<uint32_t>(1);
         GH_OK(hipMemsetAsync(e->err, 0, 4, stream));
@@ -1157,9 +1152,7 @@ static size_t type_size(int t) {
     }
 }
 
-// the kernels read their arguments from a device ring (GEN_ARG_SLOTS slots, staged through pinned host
-// memory on the engine's stream); a slot is rewritten only after the stream has drained the launches
-// that used it
+// the kernels take GenArgs (608 B) by value in their kernel arguments
 enum { GEN_L_BATCH = 0, GEN_L_TIMERS = 1, GEN_L_DEADLINES = 2, GEN_L_ABS_BATCH = 3, GEN_L_ABS_TIMERS = 4, GEN_L_CNT_BATCH = 5,
        GEN_L_ABSD_BATCH = 6, GEN_L_ABSD_TIMERS = 7 };
 // the general kernels over the keys a register-window kernel handed over: a fixed grid striding the list
@@ -1192,11 +1185,7 @@ static bool cnt_on(const GenEngine* e) { return e->host.cntOk && e->host.projN =
 static void launch_gen(GenEngine* e, GenArgs a, int which) {
     const uint32_t blocks = (e->K + 63) / 64;
     a.kpl = gen_kpl(e->K);
-    const uint32_t slot = e->arg_next++ % GEN_ARG_SLOTS;
-    if (slot == 0 && e->arg_next > 1) GH_OK(hipStreamSynchronize(e->stream));
-    e->h_args[slot] = a;
-    GH_OK(hipMemcpyAsync(e->d_args + slot, e->h_args + slot, sizeof(GenArgs), hipMemcpyHostToDevice, e->stream));
-    const GenArgs* ap = e->d_args + slot;
+    const GenArgs& ap = a;   // (by value in the kernel arguments: no upload per launch)
     hipEvent_t t0 = (e->timing && which != GEN_L_DEADLINES) ? e->ev() : nullptr;
     const bool fb = (a.mode & (GEN_M_KEYLIST | GEN_M_NOPAIRS)) != 0;
     if (which == GEN_L_TIMERS)
@@ -1214,7 +1203,8 @@ static void launch_gen(GenEngine* e, GenArgs a, int which) {
                            : which == GEN_L_CNT_BATCH ? kCntBatch[e->host.absNW]
                                                       : kAbsTimers[e->host.absNW],
                            dim3(blocks), dim3(64), 0, e->stream, ap);
-        hipLaunchKernelGGL(k_gen_stats_reduce, dim3(GST_N), dim3(256), 0, e->stream, e->wstats, blocks, e->stats);
+        hipLaunchKernelGGL(k_gen_stats_reduce, dim3(GST_N, std::min<uint32_t>((blocks + 1023) / 1024, 16u)), dim3(256),
+                           0, e->stream, e->wstats, blocks, e->stats);
     }
     else hipLaunchKernelGGL(k_gen_batch, dim3(fb ? GEN_FB_BLOCKS : (e->K + 64u * a.kpl - 1) / (64u * a.kpl)), dim3(64), 0,
                             e->stream, ap);

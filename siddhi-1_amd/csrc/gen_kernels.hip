@@ -1194,8 +1194,8 @@ __device__ void gen_wave_stats(const GenArgs& a, unsigned long long sc, unsigned
 // runs instead of the sum over j of the longest run (Poisson runs of a few events per key: one key per
 // lane leaves half of every wave's lane-steps idle).  A wave's 64 lanes still touch 64
 // consecutive keys of one row of the interleaved state at each j.
-extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GEN_WAVES, 8))) k_gen_batch(const GenArgs* __restrict__ ap) {
-    const GenArgs& a = *ap;
+extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GEN_WAVES, 8))) k_gen_batch(const GenArgs ap) {
+    const GenArgs& a = ap;
     const uint32_t kpl = a.kpl ? a.kpl : 1u;
     const uint32_t k0 = blockIdx.x * kpl * 64u + threadIdx.x;
     const auto& r = ((const cGenProgram*)a.G)->recv[a.b.stream];
@@ -1357,8 +1357,8 @@ __device__ void gen_timers_key(const GenArgs& a, uint32_t key, uint64_t di, unsi
 }  // namespace
 
 // next deadline of every key from its state (after a restore)
-extern "C" __global__ void __launch_bounds__(64) k_gen_deadlines(const GenArgs* __restrict__ ap) {
-    const GenArgs& a = *ap;
+extern "C" __global__ void __launch_bounds__(64) k_gen_deadlines(const GenArgs ap) {
+    const GenArgs& a = ap;
     const uint32_t key = blockIdx.x * blockDim.x + threadIdx.x;
     if (key >= a.K) return;
     Lane L(a, key);
@@ -1426,8 +1426,8 @@ extern "C" __global__ void __launch_bounds__(256) k_gen_collapse(const unsigned 
 #ifndef GEN_TWAVES
 #define GEN_TWAVES GEN_WAVES
 #endif
-extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GEN_TWAVES, 8))) k_gen_timers(const GenArgs* __restrict__ ap) {
-    const GenArgs& a = *ap;
+extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GEN_TWAVES, 8))) k_gen_timers(const GenArgs ap) {
+    const GenArgs& a = ap;
 #if GENX_PROF
     const uint64_t t0_ = __builtin_amdgcn_s_memtime();
 #endif
