@@ -565,12 +565,55 @@ __global__ void k_gen_scatter(const uint32_t* raw, const unsigned long long* raw
 
 // batch matches when every trigger has at most one (GEN_M_TFIRST): output-major, one thread per trigger
 // event — the output writes of a wave are consecutive, the raw records are gathered
-__global__ void k_gen_gather1(const uint32_t* __restrict__ raw, const uint32_t* __restrict__ t_cnt,
-                              const uint32_t* __restrict__ t_off, const uint32_t* __restrict__ t_first, uint32_t n,
-                              OutBufs o) {
+// The matches of a wave's 64 triggers are consecutive output records (t_off is the scan of 0/1 counts), so
+// the slot chains ([n][n_slots][max_chain] u64: 192 B per match at C3_min1) and chain lengths are written by
+// the whole wave over its contiguous output range — lane j stores element j, j + 64, ... of the range,
+// reading the record word it needs (records found through an LDS table) — instead of one lane storing its
+// match's 192 B with 64 lanes' stores 192 B apart
+__global__ void __launch_bounds__(256) k_gen_gather1(const uint32_t* __restrict__ raw, const uint32_t* __restrict__ t_cnt,
+                                                     const uint32_t* __restrict__ t_off,
+                                                     const uint32_t* __restrict__ t_first, uint32_t n, OutBufs o) {
+    __shared__ uint32_t rb[4][64];   // per wave: the record index of its q-th match
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n || t_cnt[i] == 0u) return;
-    write_out(o, *o.count + t_off[i], raw + (uint64_t)t_first[i] * o.recWords, false);
+    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const bool has = i < n && t_cnt[i] != 0u;
+    const uint64_t bm = __ballot(has);
+    if (!bm) return;   // (wave-uniform)
+    const uint32_t m = (uint32_t)__popcll(bm);
+    const uint32_t first = (uint32_t)__ffsll((unsigned long long)bm) - 1u;
+    const uint64_t d0 = *o.count + __shfl(i < n ? t_off[i] : 0u, (int)first, 64);
+    if (d0 + m > o.cap) {   // (the capacity check of write_out, per wave)
+        if (lane == 0) atomicOr(o.err, (uint32_t)GERR_MATCHCAP);
+        return;
+    }
+    const uint32_t* rec = has ? raw + (uint64_t)t_first[i] * o.recWords : raw;
+    if (has) {
+        const uint32_t q = __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
+        rb[w][q] = t_first[i];
+        const uint64_t d = d0 + q;
+        o.trig[d] = (uint64_t)rec[2] | ((uint64_t)rec[3] << 32);
+        o.ts[d] = (int64_t)((uint64_t)rec[4] | ((uint64_t)rec[5] << 32));
+        o.key[d] = rec[6];
+        for (uint32_t x = 0; x < o.projN; x++) {
+            const uint32_t* pv = rec + o.projOff + 3 * x;
+            o.pval[(size_t)x * o.cap + d] = (uint64_t)pv[0] | ((uint64_t)pv[1] << 32);
+            o.pnull[(size_t)x * o.cap + d] = (uint8_t)pv[2];
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint32_t ns = o.nslots, mc = o.MC, per = ns * mc;
+    for (uint32_t x = lane; x < m * ns; x += 64) {   // chain lengths
+        const uint32_t* r = raw + (uint64_t)rb[w][x / ns] * o.recWords;
+        o.len[d0 * ns + x] = r[7 + x % ns];
+    }
+    for (uint32_t x = lane; x < m * per; x += 64) {  // slot chains
+        const uint32_t q = x / per, y = x % per, sl = y / mc, c = y % mc;
+        const uint32_t* r = raw + (uint64_t)rb[w][q] * o.recWords;
+        const uint32_t* seqs = r + 7 + ns;
+        o.slot[d0 * per + x] = c < r[7 + sl] ? ((uint64_t)seqs[2 * y] | ((uint64_t)seqs[2 * y + 1] << 32)) : SG_NULL_SEQ;
+    }
 }
 
 // timer matches in sorted order
