@@ -181,21 +181,37 @@ def cpu_baseline(sa, synth, n_keys, batch, seconds):
             e.push(0, a, ts, cols, None, key)
             e.discard()
 
-    # one thread alone on shard 0 (its own engine): the per-thread rate of this same sample.  The
-    # single-thread `value` above runs the stream's first seconds, before the 10 s windows fill, and is
-    # faster per event than the steady state here, so scaling is measured against this instead
-    e0 = sa.NativeEngine(lib, "sgo_", cq.ir, n_keys=(n_keys + S - 1) // S)
-    run_shard(e0, shards[0][0])
-    t = time.perf_counter()
-    run_shard(e0, shards[0][1])
-    alone = sum(len(x[1]) for x in shards[0][1]) / (time.perf_counter() - t)
-    e0.close()
-    engs = [sa.NativeEngine(lib, "sgo_", cq.ir, n_keys=(n_keys + S - 1) // S) for _ in range(S)]
-    busy = [0.0] * T
     # each thread on a physical core of its own, spread over the L3 domains: the quota counts CPUs, two
     # threads on SMT siblings share a core, and threads sharing an L3 thrash it (a shard's state is tens of
-    # MB at 2^20 keys: one thread alone has the whole L3)
+    # MB at 2^20 keys: one thread alone has the whole L3).  Every engine is created by the thread that runs
+    # it, so its memory is first touched on that core's NUMA node.
     pins = distinct_cores(T)
+    engs = [None] * S
+
+    def make(sh):
+        engs[sh] = sa.NativeEngine(lib, "sgo_", cq.ir, n_keys=(n_keys + S - 1) // S)
+        return engs[sh]
+
+    # one thread alone on shard 0 (its own engine, on the first pinned core): the per-thread rate of this
+    # same sample.  The single-thread `value` above runs the stream's first seconds, before the 10 s windows
+    # fill, and is faster per event than the steady state here, so scaling is measured against this instead
+    alone = [0.0]
+
+    def solo():
+        if pins:
+            os.sched_setaffinity(0, {pins[0]})
+        e0 = sa.NativeEngine(lib, "sgo_", cq.ir, n_keys=(n_keys + S - 1) // S)
+        run_shard(e0, shards[0][0])
+        t = time.perf_counter()
+        run_shard(e0, shards[0][1])
+        alone[0] = sum(len(x[1]) for x in shards[0][1]) / (time.perf_counter() - t)
+        e0.close()
+
+    th0 = threading.Thread(target=solo)
+    th0.start()
+    th0.join()
+    alone = alone[0]
+    busy = [0.0] * T
 
     def phase(half):
         # thread r owns shards r, r + T, ... in both halves: an engine's memory is allocated and freed by
@@ -205,7 +221,7 @@ def cpu_baseline(sa, synth, n_keys, batch, seconds):
                 os.sched_setaffinity(0, {pins[r]})   # (the calling thread)
             t = time.perf_counter()
             for sh in range(r, S, T):
-                run_shard(engs[sh], shards[sh][half])
+                run_shard(engs[sh] if half else make(sh), shards[sh][half])
             busy[r] = time.perf_counter() - t
 
         th = [threading.Thread(target=work, args=(r,)) for r in range(T)]
