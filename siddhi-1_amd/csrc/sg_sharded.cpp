@@ -252,39 +252,52 @@ int shd_push(ShardEngine* s, const sg_batch* b) {
         }
         const auto& ty = s->attr_types[b->stream];
         const uint32_t nc = b->n_cols;
-        // per shard: the sub-batch columns (stable: arrival order within the shard)
+        // per shard: the positions of its events (stable: arrival order within the shard), then each column
+        // gathered through them with typed loads (one pass per column, no per-byte appends)
         struct Sub {
+            std::vector<uint32_t> pos;
             std::vector<int64_t> ts;
             std::vector<uint32_t> key;
             std::vector<std::vector<uint8_t>> cols, nulls;
             std::vector<uint64_t> glob;
         };
         std::vector<Sub> sub(N);
-        for (uint32_t r = 0; r < N; r++) {
-            sub[r].ts.reserve(cnt[r]);
-            sub[r].key.reserve(cnt[r]);
-            sub[r].glob.reserve(cnt[r]);
-            sub[r].cols.resize(nc);
-            sub[r].nulls.resize(nc);
-            for (uint32_t c = 0; c < nc; c++) {
-                sub[r].cols[c].reserve((size_t)cnt[r] * tsize(ty[c]));
-                if (h.nulls[c]) sub[r].nulls[c].reserve(cnt[r]);
-            }
-        }
+        for (uint32_t r = 0; r < N; r++) sub[r].pos.reserve(cnt[r]);
         for (uint64_t i = 0; i < n; i++) {
             const uint32_t k = h.key[i];
-            if (k >= s->K) continue;
-            Sub& u = sub[k % N];
-            u.ts.push_back(h.ts[i]);
-            u.key.push_back(k / N);
-            u.glob.push_back(b->seq_base + i);
-            for (uint32_t c = 0; c < nc; c++) {
-                const size_t sz = tsize(ty[c]);
-                const uint8_t* src = (const uint8_t*)h.cols[c] + i * sz;
-                u.cols[c].insert(u.cols[c].end(), src, src + sz);
-                if (h.nulls[c]) u.nulls[c].push_back(h.nulls[c][i]);
-            }
+            if (k < s->K) sub[k % N].pos.push_back((uint32_t)i);
         }
+        auto gather = [](const void* src, size_t sz, const std::vector<uint32_t>& pos, std::vector<uint8_t>& out) {
+            out.resize(pos.size() * sz);
+            switch (sz) {
+            case 8: { const uint64_t* a = (const uint64_t*)src; uint64_t* o = (uint64_t*)out.data();
+                      for (size_t j = 0; j < pos.size(); j++) o[j] = a[pos[j]]; break; }
+            case 4: { const uint32_t* a = (const uint32_t*)src; uint32_t* o = (uint32_t*)out.data();
+                      for (size_t j = 0; j < pos.size(); j++) o[j] = a[pos[j]]; break; }
+            default: { const uint8_t* a = (const uint8_t*)src;
+                       for (size_t j = 0; j < pos.size(); j++) memcpy(out.data() + j * sz, a + (size_t)pos[j] * sz, sz); }
+            }
+        };
+        s->each([&](uint32_t r) -> int {   // (the gathers of different shards run side by side)
+            Sub& u = sub[r];
+            const size_t m = u.pos.size();
+            u.ts.resize(m);
+            u.key.resize(m);
+            u.glob.resize(m);
+            for (size_t j = 0; j < m; j++) {
+                const uint32_t i = u.pos[j];
+                u.ts[j] = h.ts[i];
+                u.key[j] = h.key[i] / N;
+                u.glob[j] = b->seq_base + i;
+            }
+            u.cols.resize(nc);
+            u.nulls.resize(nc);
+            for (uint32_t c = 0; c < nc; c++) {
+                gather(h.cols[c], tsize(ty[c]), u.pos, u.cols[c]);
+                if (h.nulls[c]) gather(h.nulls[c], 1, u.pos, u.nulls[c]);
+            }
+            return SG_OK;
+        });
         s->each([&](uint32_t r) -> int {
             Sub& u = sub[r];
             if (u.ts.empty()) return SG_OK;
