@@ -47,7 +47,9 @@ namespace {
 // one key's absent-tail state during a walk (see the file comment); TM: the timer sweep, which also keeps
 // the first ABS_QP entries of the timer queue in registers (the pops of one sweep need no dependent loads)
 #define ABS_QP 4
-template <int NW, bool TM> struct AbsKey {
+// FF: the filters are decoded compares (GenPre.ff; a kernel variant of its own, so the interpreter's registers
+// are not allocated beside them)
+template <int NW, bool TM, bool FF = false> struct AbsKey {
     const cGenProgram& G;
     gu32* S;
     uint32_t K, k;
@@ -536,25 +538,27 @@ template <int NW, bool TM> struct AbsKey {
     __device__ __forceinline__ bool evalF0(const AbsEv<NW>& ev) {
         const auto& P = G.pre[G.absP0];
         if (P.flen == 0) return true;
-        const GVal v = jo_eval<false>(G.code, P.fpc, P.flen, err,
-                               [&](uint32_t s, uint32_t a, int32_t c) -> GVal {
+        auto var_ = [&](uint32_t s, uint32_t a, int32_t c) -> GVal {
                                    if ((int)s == slot0 && (c == 0 || c == -1)) return attr(ev.w, ev.nb, a);
                                    return GVal{0, true};
-                               },
-                               [&](uint32_t s, int32_t c) -> bool { return !((int)s == slot0 && (c == 0 || c == -1)); });
+                               };
+        if constexpr (FF) return jo_fast(P.ff, var_);   // (gen_engine.h JoFast)
+        const GVal v = jo_eval<false>(G.code, P.fpc, P.flen, err, var_,
+                                      [&](uint32_t s, int32_t c) -> bool { return !((int)s == slot0 && (c == 0 || c == -1)); });
         return !v.null && (v.b & 1);
     }
     // f1 on a partial whose e1 words are `pw` / `pn`: slot0 = its e1, slot1 = the event
     __device__ __forceinline__ bool evalF1(const AbsEv<NW>& ev, const uint32_t (&pw)[NW], uint32_t pn) {
         const auto& P = G.pre[G.absP1];
         if (P.flen == 0) return true;
-        const GVal v = jo_eval<false>(G.code, P.fpc, P.flen, err,
-                                      [&](uint32_t s, uint32_t a, int32_t c) -> GVal {
+        auto var_ = [&](uint32_t s, uint32_t a, int32_t c) -> GVal {
                                           if (c != 0 && c != -1) return GVal{0, true};
                                           if ((int)s == slot1) return attr(ev.w, ev.nb, a);
                                           if ((int)s == slot0) return attr(pw, pn, a);
                                           return GVal{0, true};
-                                      },
+                                      };
+        if constexpr (FF) return jo_fast(P.ff, var_);   // (gen_engine.h JoFast)
+        const GVal v = jo_eval<false>(G.code, P.fpc, P.flen, err, var_,
                                       [&](uint32_t s, int32_t c) -> bool {
                                           return !(((int)s == slot0 || (int)s == slot1) && (c == 0 || c == -1));
                                       });
@@ -682,7 +686,7 @@ template <int NW, bool TM> struct AbsKey {
 };
 
 // ---- batch: one lane per key walks its events of the key-sorted batch ----
-template <int NW> __device__ void abs_batch(const GenArgs& a) {
+template <int NW, bool FF> __device__ void abs_batch(const GenArgs& a) {
     const cGenProgram& G = *(cGenProgram*)a.G;
     const uint32_t key = blockIdx.x * 64u + threadIdx.x;
     uint32_t b = 0, e = 0;
@@ -690,7 +694,7 @@ template <int NW> __device__ void abs_batch(const GenArgs& a) {
         b = gp(a.b.seg_begin)[key];
         e = gp(a.b.seg_end)[key];
     }
-    AbsKey<NW, false> L(a.G, a.state, a.K, key < a.K ? key : 0u);
+    AbsKey<NW, false, FF> L(a.G, a.state, a.K, key < a.K ? key : 0u);
     bool walk = b < e;
     bool fb = false;
     uint32_t stop = b;
@@ -790,7 +794,10 @@ template <int NW> __device__ void abs_timers(const GenArgs& a) {
 // One kernel per captured-word count (NW = the stream's attributes as 32-bit words, long / double 2 each).
 #define ABS_KERNELS(NW)                                                                                             \
     extern "C" __global__ void __launch_bounds__(64) k_abs_batch_##NW(const GenArgs ap) {           \
-        abs_batch<NW>(ap);                                                                                         \
+        abs_batch<NW, false>(ap);                                                                                  \
+    }                                                                                                               \
+    extern "C" __global__ void __launch_bounds__(64) k_abs_batchf_##NW(const GenArgs ap) {          \
+        abs_batch<NW, true>(ap);                                                                                   \
     }                                                                                                               \
     extern "C" __global__ void __launch_bounds__(64) k_abs_timers_##NW(const GenArgs ap) {          \
         abs_timers<NW>(ap);                                                                                        \

@@ -285,24 +285,26 @@ template <int NW> struct DeepKey {
     __device__ bool evalF0(const AbsEv<NW>& ev) {
         const auto& P = G.pre[G.absP0];
         if (P.flen == 0) return true;
-        const GVal v = jo_eval<false>(G.code, P.fpc, P.flen, err,
-                                      [&](uint32_t s, uint32_t a, int32_t c) -> GVal {
+        auto var_ = [&](uint32_t s, uint32_t a, int32_t c) -> GVal {
                                           if ((int)s == slot0 && (c == 0 || c == -1)) return attr(ev.w, ev.nb, a);
                                           return GVal{0, true};
-                                      },
+                                      };
+        if (P.ff.on) return jo_fast(P.ff, var_);   // (gen_engine.h JoFast)
+        const GVal v = jo_eval<false>(G.code, P.fpc, P.flen, err, var_,
                                       [&](uint32_t s, int32_t c) -> bool { return !((int)s == slot0 && (c == 0 || c == -1)); });
         return !v.null && (v.b & 1);
     }
     __device__ bool evalF1(const AbsEv<NW>& ev, const DEnt<NW>& x) {
         const auto& P = G.pre[G.absP1];
         if (P.flen == 0) return true;
-        const GVal v = jo_eval<false>(G.code, P.fpc, P.flen, err,
-                                      [&](uint32_t s, uint32_t a, int32_t c) -> GVal {
+        auto var_ = [&](uint32_t s, uint32_t a, int32_t c) -> GVal {
                                           if (c != 0 && c != -1) return GVal{0, true};
                                           if ((int)s == slot1) return attr(ev.w, ev.nb, a);
                                           if ((int)s == slot0) return attr(x.w, x.nb, a);
                                           return GVal{0, true};
-                                      },
+                                      };
+        if (P.ff.on) return jo_fast(P.ff, var_);   // (gen_engine.h JoFast)
+        const GVal v = jo_eval<false>(G.code, P.fpc, P.flen, err, var_,
                                       [&](uint32_t s, int32_t c) -> bool {
                                           return !(((int)s == slot0 || (int)s == slot1) && (c == 0 || c == -1));
                                       });

@@ -288,17 +288,17 @@ template <int NW> struct CntKey {
     __device__ bool evalOn(int p, uint32_t len, int evSlot, const AbsEv<NW>& ev) {
         const auto& P = G.pre[p];
         if (P.flen == 0) return true;
-        const GVal v = jo_eval<false>(
-            G.code, P.fpc, P.flen, err,
-            [&](uint32_t s, uint32_t a, int32_t c) -> GVal {
+        auto var_ = [&](uint32_t s, uint32_t a, int32_t c) -> GVal {
                 if ((int)s == s0) {
                     const int i = chainIdx(c, len);
                     return i < 0 ? GVal{0, true} : chainAttr(i, a);
                 }
                 if ((int)s == evSlot && chainIdx(c, 1u) == 0) return word(ev.w, ev.nb, a);
                 return GVal{0, true};
-            },
-            [&](uint32_t s, int32_t c) -> bool {
+            };
+        if (P.ff.on) return jo_fast(P.ff, var_);   // (gen_engine.h JoFast)
+        const GVal v = jo_eval<false>(G.code, P.fpc, P.flen, err, var_,
+                                      [&](uint32_t s, int32_t c) -> bool {
                 if ((int)s == s0) return chainIdx(c, len) < 0;
                 if ((int)s == evSlot) return chainIdx(c, 1u) != 0;
                 return true;

@@ -65,12 +65,24 @@ enum {
     GF_RUNNING = 64u
 };
 
+// A filter program of the form `operand CMP operand` (an attribute or a constant on each side, each widened
+// to the compare domain), decoded once on the host (gen_host.hip jo_fast_decode) and evaluated by
+// java_ops.h jo_fast without the interpreter: the common shapes `price > 20`, `price > e1.price`.
+struct JoFast {
+    uint32_t on, op, dom, pad;
+    uint32_t isConst[2], from[2], slot[2], attr[2];
+    int32_t chain[2];
+    uint64_t cbits[2];  // constants, already in the compare domain
+    uint32_t cnull[2], pad2[2];
+};
+
 struct GenPre {
     int32_t kind, absent, stateId, isStart;
     int64_t waiting;
     int32_t withinEvery, thisPost, thisLast, countPost;
     uint32_t fpc, flen;
     int32_t minCount, maxCount, logicalType, partner;
+    JoFast ff;   // the filter as one decoded compare (java_ops.h), when it has that form (ff.on)
 };
 
 struct GenPost {

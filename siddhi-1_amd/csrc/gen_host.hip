@@ -31,11 +31,15 @@
 
 extern "C" __global__ void k_gen_batch(const GenArgs ap);
 #define ABS_DECL(NW) extern "C" __global__ void k_abs_batch_##NW(const GenArgs ap); \
+                     extern "C" __global__ void k_abs_batchf_##NW(const GenArgs ap); \
                      extern "C" __global__ void k_abs_timers_##NW(const GenArgs ap);
 ABS_DECL(1) ABS_DECL(2) ABS_DECL(3) ABS_DECL(4) ABS_DECL(5) ABS_DECL(6) ABS_DECL(7) ABS_DECL(8)
 typedef void (*AbsKernel)(const GenArgs);
 static const AbsKernel kAbsBatch[ABS_MAXNW + 1] = {nullptr, k_abs_batch_1, k_abs_batch_2, k_abs_batch_3, k_abs_batch_4,
                                                    k_abs_batch_5, k_abs_batch_6, k_abs_batch_7, k_abs_batch_8};
+static const AbsKernel kAbsBatchF[ABS_MAXNW + 1] = {nullptr, k_abs_batchf_1, k_abs_batchf_2, k_abs_batchf_3,
+                                                    k_abs_batchf_4, k_abs_batchf_5, k_abs_batchf_6, k_abs_batchf_7,
+                                                    k_abs_batchf_8};
 #define ABSD_DECL(NW) extern "C" __global__ void k_absd_batch_##NW(const GenArgs ap); \
                       extern "C" __global__ void k_absd_timers_##NW(const GenArgs ap);
 ABSD_DECL(1) ABSD_DECL(2) ABSD_DECL(3) ABSD_DECL(4) ABSD_DECL(5) ABSD_DECL(6) ABSD_DECL(7) ABSD_DECL(8)
@@ -385,6 +389,71 @@ void cnt_shape(GenProgram& G) {
 
 // the absent-tail shape of abs_kernels.hip: `[every] e1=S[f0] -> not S[f1] for T [within W]` with the
 // processors wired exactly as the kernels restate them (anything else stays on the general kernels)
+// A filter program `operand [CVT] operand [CVT] CMP` (include/siddhi_gpu_ir.h encodings) as a JoFast, each
+// operand an attribute or a constant ending in the compare domain; constants widened here as java_ops.h
+// jo_cvt would widen them (JLS 5.1.2, round to nearest).  Any other program: on = 0 (the interpreter runs it).
+static uint64_t jo_host_cvt(uint64_t b, uint32_t from, uint32_t to) {
+    auto f32 = [](float f) { uint32_t u; memcpy(&u, &f, 4); return (uint64_t)u; };
+    auto f64 = [](double d) { uint64_t u; memcpy(&u, &d, 8); return u; };
+    if (from == to) return b;
+    if (from == SG_T_INT) {
+        const int32_t x = (int32_t)(uint32_t)b;
+        if (to == SG_T_LONG) return (uint64_t)(int64_t)x;
+        if (to == SG_T_FLOAT) return f32((float)x);
+        if (to == SG_T_DOUBLE) return f64((double)x);
+    } else if (from == SG_T_LONG) {
+        const int64_t x = (int64_t)b;
+        if (to == SG_T_FLOAT) return f32((float)x);
+        if (to == SG_T_DOUBLE) return f64((double)x);
+    } else if (from == SG_T_FLOAT && to == SG_T_DOUBLE) {
+        float f;
+        const uint32_t u = (uint32_t)b;
+        memcpy(&f, &u, 4);
+        return f64((double)f);
+    }
+    return b;
+}
+JoFast jo_fast_decode(const uint32_t* code, uint32_t pc, uint32_t n) {
+    JoFast f{};
+    if (n == 0) return f;
+    const uint32_t end = pc + n;
+    uint32_t fin[2] = {0, 0};
+    for (int i = 0; i < 2; ++i) {
+        if (pc + 3 > end) return JoFast{};
+        const uint32_t w = code[pc], op = w & 0xffu, a = (w >> 8) & 0xffu, b = (w >> 16) & 0xffu;
+        if (op == SG_OP_VAR) {
+            f.isConst[i] = 0;
+            f.from[i] = a;
+            f.slot[i] = b;
+            f.attr[i] = code[pc + 1];
+            f.chain[i] = (int32_t)code[pc + 2];
+        } else if (op == SG_OP_CONST) {
+            f.isConst[i] = 1;
+            f.from[i] = a;
+            f.cbits[i] = (uint64_t)code[pc + 1] | ((uint64_t)code[pc + 2] << 32);
+            f.cnull[i] = b != 0u;
+        } else {
+            return JoFast{};
+        }
+        pc += 3;
+        fin[i] = f.from[i];
+        if (pc < end && (code[pc] & 0xffu) == SG_OP_CVT) {
+            if (((code[pc] >> 8) & 0xffu) != fin[i]) return JoFast{};
+            fin[i] = (code[pc] >> 16) & 0xffu;
+            pc += 1;
+        }
+    }
+    if (pc + 1 != end) return JoFast{};
+    const uint32_t op = code[pc] & 0xffu, dom = (code[pc] >> 8) & 0xffu;
+    if (op < SG_OP_EQ || op > SG_OP_LE || fin[0] != dom || fin[1] != dom) return JoFast{};
+    f.op = op;
+    f.dom = dom;
+    for (int i = 0; i < 2; ++i)
+        if (f.isConst[i] && !f.cnull[i]) f.cbits[i] = jo_host_cvt(f.cbits[i], f.from[i], dom);
+    f.on = 1;
+    return f;
+}
+
 void abs_shape(GenProgram& G) {
     G.absOk = 0;
     if (G.qtype != SG_Q_PATTERN || !G.partitioned || !G.playback || G.nstreams != 1 || G.nprocs != 2 || G.nslots != 2)
@@ -487,6 +556,7 @@ GenProgram* gen_build_program(const uint32_t* w, size_t nw, uint32_t partialCap)
         G->offDef = off;
         off += 1 + 2 * G->DEF;
         G->blockWords = (off + (1u << GEN_GRAN_LOG2) - 1u) & ~((1u << GEN_GRAN_LOG2) - 1u);  // whole granules
+        for (int x = 0; x < G->nprocs; x++) G->pre[x].ff = jo_fast_decode(G->code, G->pre[x].fpc, G->pre[x].flen);
         abs_shape(*G);
         cnt_shape(*G);
         return G;
@@ -1242,7 +1312,11 @@ static void launch_gen(GenEngine* e, GenArgs a, int which) {
     }
     else if (which == GEN_L_ABS_BATCH || which == GEN_L_ABS_TIMERS || which == GEN_L_CNT_BATCH) {
         // one lane per key / possible due slot (the due count is on the device); then the waves' counter rows
-        hipLaunchKernelGGL(which == GEN_L_ABS_BATCH   ? kAbsBatch[e->host.absNW]
+        // (the absent kernel's variant for decoded-compare filters when both of its filters are)
+        const GenPre& f0 = e->host.pre[e->host.absP0];
+        const GenPre& f1 = e->host.pre[e->host.absP1];
+        const bool ff = (f0.flen == 0 || f0.ff.on) && (f1.flen == 0 || f1.ff.on);
+        hipLaunchKernelGGL(which == GEN_L_ABS_BATCH   ? (ff ? kAbsBatchF[e->host.absNW] : kAbsBatch[e->host.absNW])
                            : which == GEN_L_CNT_BATCH ? kCntBatch[e->host.absNW]
                                                       : kAbsTimers[e->host.absNW],
                            dim3(blocks), dim3(64), 0, e->stream, ap);

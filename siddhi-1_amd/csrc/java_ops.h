@@ -127,6 +127,19 @@ __device__ __forceinline__ bool jo_compare(int op, int dom, GVal l, GVal r) {
     }
 }
 
+// A filter program of the form `operand CMP operand` (operands: an attribute, or a constant, each widened
+// to the compare domain), decoded once on the host (gen_host.hip jo_fast_decode) and evaluated without the
+// interpreter's loop and dispatch: the common shapes `price > 20`, `price > e1.price`.
+// (F: gen_engine.h JoFast)
+template <class F, class VarFn> __device__ __forceinline__ bool jo_fast(const F& f, VarFn var) {
+    GVal o[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+        o[i] = f.isConst[i] ? GVal{f.cbits[i], f.cnull[i] != 0u}
+                            : jo_cvt(var(f.slot[i], f.attr[i], f.chain[i]), (int)f.from[i], (int)f.dom);
+    return jo_compare((int)f.op, (int)f.dom, o[0], o[1]);
+}
+
 // The value of one expression program code[pc, pc + n).  Leaves: var(slot, attr, chain) -> GVal and
 // evnull(slot, chain) -> bool (`e1 is null`).  The two top entries live in registers (t0 = top, t1 =
 // below it); deeper ones in stk[] (stk[i] = entry i from the bottom), touched only by programs deeper
