@@ -389,6 +389,15 @@ struct Lane {
         return !v.null && (v.b & 1);
     }
 
+    // a filter decoded on the host into one compare (gen_engine.h JoFast): the same reads, no interpreter
+    template <class F> __device__ bool evalFast(uint32_t se, const F& f) __restrict__ {
+        return jo_fast(f, [&](uint32_t slot, uint32_t attr, int32_t chain) -> GVal {
+            const uint32_t e = chainAt(se, (int)slot, chain);
+            if (e == GEN_NIL) return GVal{0, true};
+            return GVal{attrWord(e, slot, attr), ((W(sew(e, SE_NULL)) >> attr) & 1u) != 0};
+        });
+    }
+
     // QuerySelector.processNoGroupBy (QuerySelector.java:162-206) at emission, in this key's output order:
     // each aggregator's processAdd over its argument (java_ops.h jo_agg, per-key state in the block), then
     // the select list (reading the aggregators' values) and `having` (reading the output row), 3 words per
@@ -695,7 +704,7 @@ struct Lane {
     __device__ void runChain(int p, uint32_t se) __restrict__ {  // StreamPreStateProcessor.process(StateEvent) :131-142
         setFlag(p, GF_CHANGED, false);
         const auto& P = G.pre[p];
-        if (P.flen == 0 || eval(se, P.fpc, P.flen)) postProcess(P.thisPost, se);
+        if (P.flen == 0 || (P.ff.on ? evalFast(se, P.ff) : eval(se, P.fpc, P.flen))) postProcess(P.thisPost, se);
     }
 
     // ---- post processors ----
