@@ -47,6 +47,23 @@ def algorithmic_bytes(st):
             + 16 * st["partials_created"] + 24 * st["matches"])
 
 
+def pmc_traffic_general(cfg):
+    """NFA-kernel HBM bytes per pushed batch of a general-engine config from the committed PMC summary
+    (tools/pmc_general_summary.py), only when it was measured on these exact kernel sources; (None, None)
+    otherwise"""
+    try:
+        import hashlib
+        t = json.load(open(os.path.join(ROOT, "tools", "pmc_traffic_general.json")))
+        h = hashlib.sha1()
+        for f in t["sources"]:
+            h.update(open(os.path.join(ROOT, "siddhi-1_amd", "csrc", f), "rb").read())
+        if t.get("kernel_src_sha1") == h.hexdigest() and cfg in t["configs"]:
+            return t["configs"][cfg]["traffic_bytes_per_step"], t["profiles"]
+    except (OSError, ValueError, KeyError):
+        pass
+    return None, None
+
+
 def pmc_traffic():
     """HBM bytes per launch of the advance kernel from the committed PMC summary (tools/pmc_summary.py),
     only when it was measured on this exact kernel source; None otherwise."""
@@ -267,12 +284,142 @@ def cpu_baseline(sa, synth, n_keys, batch, seconds):
                              f"within 10 sec), single-thread oracle"}}
 
 
+def cpu_general(sa, query, make_batch, n_keys, batch, warm, playback, seconds, label):
+    """SURVEY §8(d) CPU legs of one general-engine config (BASELINE configs[2] / [3]), the CPU oracle on the GPU
+    box's host cores over the SAME stream the GPU leg runs: its batches in order, each pushed with the playback
+    clock first advanced to the batch's last event (as the GPU leg and InputHandler.send(Event[]) do), in chunks
+    (one advance per batch, so chunking changes nothing).  The GPU leg's warm-up batches run untimed first, then
+    the timed events, each part bounded by time:
+      (i)  single thread (the reference runs a partitioned pattern query under one lock) -> `value`;
+      (ii) partition-parallel over the box's CPU share: keys sharded key % 4T, four oracle engines per pinned
+           thread, each shard's events of the same batches (the same clock advances), the same untimed /
+           timed split; an upper bound for any CPU engine."""
+    import threading
+    from oracle_backend import build_oracle
+    lib = build_oracle()
+    app = sa.parse_app(query)
+    cq = sa.compile_query(app, app.queries[0], sa.StringDictionary())
+    chunk = 1 << 18
+    cache = {}
+
+    def get(b):
+        if b not in cache:
+            cache.clear()
+            cache[b] = make_batch(b)
+        return cache[b]
+
+    def cols(d, sl):
+        return [d["symbol"][sl], d["price"][sl], d["volume"][sl]]
+
+    # (i) single thread: untimed warm-up (the GPU leg's warm-up batches, at most seconds / 3), then timed
+    eng = sa.NativeEngine(lib, "sgo_", cq.ir, n_keys=n_keys)
+    pos, busy, t_warm, done = 0, 0.0, 0.0, 0
+    advanced = -1
+    while True:
+        b, off = divmod(pos, batch)
+        d = get(b)
+        warmup = b < warm and t_warm < seconds / 3
+        if not warmup and busy >= seconds:
+            break
+        hi = min(batch, off + chunk)
+        t = time.perf_counter()
+        if playback and advanced != b:
+            eng.advance_time(int(d["ts"][-1]))
+            eng.discard()
+            advanced = b
+        sl = slice(off, hi)
+        eng.push(0, pos, d["ts"][sl], cols(d, sl), None, d["key"][sl])
+        eng.discard()
+        el = time.perf_counter() - t
+        if warmup:
+            t_warm += el
+        else:
+            busy += el
+            done += hi - off
+        pos += hi - off
+    eng.close()
+    t0_ev = pos - done
+    single = done / busy
+    # (ii) partition-parallel: the same untimed prefix [0, t0_ev), then a timed range sized for ~seconds / 2
+    quota = cpu_quota()
+    T = max(1, int(quota) if quota else int(os.environ.get("OMP_NUM_THREADS", 0)) or (os.cpu_count() or 1))
+    T = int(os.environ.get("SG_CPU_THREADS", T))
+    S = 4 * T
+    n_timed = max(chunk, int(single * T * 0.5 * seconds / 2))
+    end = t0_ev + n_timed
+    pins = distinct_cores(T)
+    parts = [[[], []] for _ in range(S)]   # per shard: (untimed, timed) lists of (batch, seq base, arrays)
+    for b in range(0, (end + batch - 1) // batch):
+        d = get(b)
+        lo, hi = b * batch, min((b + 1) * batch, end)
+        last = int(d["ts"][-1])
+        own = d["key"][: hi - lo] % np.uint32(S)
+        for half, (a, z) in enumerate(((lo, min(hi, t0_ev)), (max(lo, t0_ev), hi))):
+            if a >= z:
+                continue
+            for r in range(S):
+                idx = np.nonzero(own[a - lo:z - lo] == r)[0] + (a - lo)
+                parts[r][half].append((last, a, np.ascontiguousarray(d["ts"][idx]),
+                                       [np.ascontiguousarray(c[idx]) for c in cols(d, slice(None))],
+                                       (d["key"][idx] // np.uint32(S)).astype(np.uint32)))
+    cache.clear()
+    engs = [None] * S
+    busy_t = [0.0] * T
+
+    def run(e, lst):
+        last_adv = None
+        for last, a, ts, cs, key in lst:   # local arrival seqs (the per-key order is the global one)
+            if playback and last != last_adv:
+                e.advance_time(last)
+                e.discard()
+                last_adv = last
+            if len(ts):
+                e.push(0, e._sg_next, ts, cs, None, key)
+                e._sg_next += len(ts)
+                e.discard()
+
+    def phase(half):
+        def work(r):
+            if pins:
+                os.sched_setaffinity(0, {pins[r]})
+            t = time.perf_counter()
+            for sh in range(r, S, T):
+                if half == 0:
+                    engs[sh] = sa.NativeEngine(lib, "sgo_", cq.ir, n_keys=(n_keys + S - 1) // S)
+                    engs[sh]._sg_next = 0
+                run(engs[sh], parts[sh][half])
+            busy_t[r] = time.perf_counter() - t
+        th = [threading.Thread(target=work, args=(r,)) for r in range(T)]
+        t0 = time.perf_counter()
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        return time.perf_counter() - t0
+
+    phase(0)
+    par = n_timed / phase(1)
+    for e in engs:
+        e.close()
+    return {"value": single, "unit": "events/s", "cores": 1, "kind": "port",
+            "sample": f"events [{t0_ev}, {t0_ev + done}) of the {label} stream after [0, {t0_ev}) untimed "
+                      f"({warm} warm-up batch(es) of the GPU leg, capped), CPU oracle single thread, pushed in the GPU "
+                      f"leg's batches (playback clock per batch)" if playback else
+                      f"events [{t0_ev}, {t0_ev + done}) of the {label} stream after [0, {t0_ev}) untimed, CPU oracle "
+                      f"single thread",
+            "partition_parallel": {"value": par, "unit": "events/s", "threads": T, "cpu_quota": quota,
+                                   "pinned_cpus": pins, "per_thread_vs_single": par / single / T,
+                                   "thread_busy_s": [round(x, 3) for x in busy_t],
+                                   "sample": f"events [{t0_ev}, {end}) after the same untimed prefix, keys sharded "
+                                             f"key % {S}, four oracle engines per thread"}}
+
+
 def to_dev(torch, d, dev):
     return {k: torch.from_numpy(v.view(np.int32) if v.dtype == np.uint32 else v).to(dev) for k, v in d.items()}
 
 
 def run_general(sa, synth, torch, dev, query, make_batch, n_keys, batch, steps, warmup, cap, playback=False,
-                extra_in=0):
+                extra_in=0, label=None):
     """One of the general-engine configs: events/s over `steps` timed batches (HBM-resident), then the
     same batches again with SG_CFG_TIMING for the roofline of the NFA kernels (k_gen_batch + the timer
     sweeps): the §8d byte model over their exact counters (extra_in: bytes per event of referenced
@@ -290,9 +437,12 @@ def run_general(sa, synth, torch, dev, query, make_batch, n_keys, batch, steps, 
     bytes_ = algorithmic_bytes(tm) + extra_in * tm["events"]
     sec = tm["advance_ns"] / 1e9
     gbs = bytes_ / sec / 1e9 if sec > 0 else 0.0
+    traffic, tsrc = pmc_traffic_general(label) if label else (None, None)
     res["roofline"] = {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                       "frac": gbs / HBM_PEAK_GBS, "traffic": None,
-                       "kernel": "k_gen_batch + k_gen_timers (NFA advance, general engine)",
+                       "frac": gbs / HBM_PEAK_GBS, "traffic": traffic, "traffic_unit": "bytes/step",
+                       "traffic_source": tsrc,
+                       "traffic_per_alg_byte": traffic / (bytes_ / steps) if traffic else None,
+                       "kernel": res.pop("kernels"),
                        "alg_bytes_per_step": bytes_ / steps, "kernel_ms_per_step": sec * 1e3 / steps,
                        "alg_bytes_per_event": bytes_ / max(1, tm["events"]),
                        "counters_per_step": {k: tm[k] / steps for k in ("keys_touched", "live_at_batch_start",
@@ -329,10 +479,12 @@ def _run_general(sa, cq, bats, lastts, n_keys, batch, steps, warmup, cap, playba
     eng.synchronize()
     el = time.perf_counter() - t0
     d = delta(st0, eng.stats())
+    kernels = eng.describe()
     eng.close()
     return {"value": batch * steps / el, "unit": "events/s", "ms_per_step": el / steps * 1e3,
             "keys": n_keys, "batch_events": batch, "matches_per_step": d["matches"] / steps,
-            "partials_scanned_per_step": d["partials_scanned"] / steps, "engine": "general", "delta": d}
+            "partials_scanned_per_step": d["partials_scanned"] / steps, "engine": "general", "delta": d,
+            "kernels": kernels}
 
 
 def take_all(eng, ready):
@@ -747,36 +899,39 @@ def main():
     torch.cuda.empty_cache()
     if rank == 0 and world == 1 and not args.no_extra:
         steps = max(3, args.steps // 4)
-        cb, c4b = 1 << 22, 1 << 22
-        out["other_configs"] = {
-            "C3": dict(run_general(sa, synth, torch, dev, synth.C3_QUERY,
-                                   lambda s: synth.stock_ticks(s * cb, cb, K), K, cb, steps, 1, 8, extra_in=4),
-                       workload="C3: every e1=S[price>20]<2:5>, e2=S[price>e1[last].price] or e3=S[volume>1000] "
-                                "within 10 sec (SEQUENCE), 1,048,576 keys"),
-            "C3_min1": dict(run_general(sa, synth, torch, dev, synth.C3_MIN1_QUERY,
-                                        lambda s: synth.stock_ticks(s * cb, cb, K), K, cb, steps, 1, 8, extra_in=4),
-                            workload="C3 with e1<1:5> (C3 as written emits no match under the reference's "
-                                     "SEQUENCE reset semantics, DESIGN.md), 1,048,576 keys"),
-            "C4": dict(run_general(sa, synth, torch, dev, synth.C4_QUERY,
-                                   lambda s: synth.burst_ticks(s * c4b, c4b, K, 1), K, c4b, steps, 1, 16,
-                                   playback=True),
-                       workload="C4: every e1=S[price>20] -> not S[price>e1.price] for 30 sec within 60 sec, "
-                                "@app:playback, 1,048,576 keys, one event per ms (distinct timer due times), "
-                                "4,194,304-event batches, the playback clock advanced per batch"),
-            "C4_deep": dict(run_general(sa, synth, torch, dev, synth.C4_QUERY,
-                                        lambda s: synth.burst_ticks(s * (c4b // 16), c4b // 16, K // 4, 16), K // 4,
-                                        c4b, steps, 1, 64, playback=True),
-                            workload="C4 with deeper per-key state: 262,144 keys, one key per ms in bursts of 16 "
-                                     "events (up to ~16 live partials per key)"),
+        cb = 1 << 22
+        # name: (query, batch maker, keys, batch events, warm-up batches, partial capacity, playback, extra bytes
+        #        per event of referenced attributes, workload)
+        gcfg = {
+            "C3": (synth.C3_QUERY, lambda s: synth.stock_ticks(s * cb, cb, K), K, cb, 1, 8, False, 4,
+                   "C3: every e1=S[price>20]<2:5>, e2=S[price>e1[last].price] or e3=S[volume>1000] within 10 sec "
+                   "(SEQUENCE), 1,048,576 keys"),
+            "C3_min1": (synth.C3_MIN1_QUERY, lambda s: synth.stock_ticks(s * cb, cb, K), K, cb, 1, 8, False, 4,
+                        "C3 with e1<1:5> (C3 as written emits no match under the reference's SEQUENCE reset "
+                        "semantics, DESIGN.md), 1,048,576 keys"),
+            "C4": (synth.C4_QUERY, lambda s: synth.burst_ticks(s * cb, cb, K, 1), K, cb, 1, 16, True, 0,
+                   "C4: every e1=S[price>20] -> not S[price>e1.price] for 30 sec within 60 sec, @app:playback, "
+                   "1,048,576 keys, one event per ms (distinct timer due times), 4,194,304-event batches, the "
+                   "playback clock advanced per batch"),
+            "C4_deep": (synth.C4_QUERY, lambda s: synth.burst_ticks(s * (cb // 16), cb // 16, K // 4, 16), K // 4, cb,
+                        1, 64, True, 0,
+                        "C4 with deeper per-key state: 262,144 keys, one key per ms in bursts of 16 events (up to "
+                        "~16 live partials per key)"),
             # hundreds of live absent partials per key carried across pushes (C4's 30 s / 60 s
             # windows, 2,048 keys, a burst of 16 events per ms with falling prices so that partials die by their
             # timers, 2^16-event pushes = 4.1 s of event time; 8 warmup pushes fill the lists)
-            "C4_deep_state": dict(run_general(sa, synth, torch, dev, synth.C4_QUERY,
-                                              lambda s: synth.absent_deep_ticks(s * 4096, 4096, 2048, 16), 2048,
-                                              1 << 16, 16, 8, 512, playback=True),
-                                  workload="C4 deep cross-batch state: 2,048 keys, bursts of 16 events per ms, "
-                                           "2^16-event pushes, hundreds of live partials per key at every push"),
+            "C4_deep_state": (synth.C4_QUERY, lambda s: synth.absent_deep_ticks(s * 4096, 4096, 2048, 16), 2048,
+                              1 << 16, 8, 512, True, 0,
+                              "C4 deep cross-batch state: 2,048 keys, bursts of 16 events per ms, 2^16-event pushes, "
+                              "hundreds of live partials per key at every push"),
         }
+        out["other_configs"] = {}
+        for name, (q, mk, keys, bsz, warm, cap, pb, extra, wl) in gcfg.items():
+            r = dict(run_general(sa, synth, torch, dev, q, mk, keys, bsz, 16 if name == "C4_deep_state" else steps,
+                                 warm, cap, playback=pb, extra_in=extra, label=name), workload=wl)
+            if not args.no_cpu:
+                r["cpu_baseline"] = cpu_general(sa, q, mk, keys, bsz, warm, pb, args.cpu_seconds / 3, name)
+            out["other_configs"][name] = r
         ds = out["other_configs"]["C4_deep_state"]["roofline"]["counters_per_step"]
         out["other_configs"]["C4_deep_state"]["live_per_touched_key_at_batch_start"] = \
             ds["live_at_batch_start"] / max(1.0, ds["keys_touched"])

@@ -88,7 +88,11 @@ typedef struct sg_config {
      * key / n_devices) over one engine per device; every entry point keeps its meaning for the whole key
      * range, polls merge the shards' matches into the single engine's order and return host memory
      * (sg_sharded.cpp).  0 or 1: one device.  A caller built against the header without these two fields
-     * passes the smaller struct_size and gets one device. */
+     * passes the smaller struct_size and gets one device.  A device batch is split on the device it lives on
+     * and reaches other devices by peer copies (never staged to host).  A call that fails after some shards
+     * took their part (a push one shard refused, an advance or poll one shard failed) leaves the shards out of
+     * step: every later push / advance / poll then fails with SG_ERR_STATE until sg_restore or
+     * sg_state_import. */
     uint32_t n_devices;
     uint32_t reserved;
     const int32_t* devices;
@@ -166,6 +170,10 @@ typedef struct sg_stats {
     uint64_t window_spills;     /* keys whose live partials outgrew the register window (moved to HBM) */
     uint64_t advance_hbm_ns;    /* SG_CFG_TIMING: part of advance_ns spent in the HBM pass (waves and
                                    keys the LDS-staged pass left to it) */
+    uint64_t host_staged_bytes; /* multi-device engine: batch bytes it copied to host memory (device
+                                   batches are split on the device: 0) */
+    uint64_t seq_map_entries;   /* multi-device engine: local -> global seq map entries it holds (trimmed
+                                   below the oldest seq a live partial references after each poll) */
 } sg_stats;
 
 /* ir/ir_len: an IR blob (siddhi_gpu_ir.h) of one query */
@@ -186,6 +194,10 @@ int sg_advance_time(sg_engine* e, int64_t now_ms);
 int sg_poll_matches(sg_engine* e, uint32_t mem, sg_match_batch* out);
 int sg_release_matches(sg_engine* e, sg_match_batch* m);
 int sg_get_stats(sg_engine* e, sg_stats* out);
+/* Diagnostics: the kernels this engine dispatches per push and per clock advance, in launch order, as a
+ * NUL-terminated line of text truncated to out_len (no reference counterpart: the query plan a profiler's
+ * kernel names map to, as EXPLAIN would print it). */
+int sg_engine_describe(sg_engine* e, char* out, size_t out_len);
 int sg_synchronize(sg_engine* e);
 /* Device batches produced on another stream (a hipStream_t of the engine's device, NULL = the legacy
  * default stream): the engine's later work waits for everything queued on `stream` so far, without a

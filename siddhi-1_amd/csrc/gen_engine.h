@@ -205,6 +205,7 @@ struct GenOut {
     // per batch event: matches it triggered and the first raw index (contiguous)
     uint32_t* t_cnt;
     uint32_t* t_first;
+    uint32_t* t_multi;   // GEN_M_TFIRST: set when a trigger emitted more than one match (the ordering scatters)
     // timer matches: sort keys per raw match (k1 sched or 0, k2 due/fireAt, k3 key, raw index)
     int64_t* tk2;
     uint32_t* tk1;

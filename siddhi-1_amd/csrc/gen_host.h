@@ -25,6 +25,9 @@ int gen_get_projection(GenEngine* e, uint32_t mem, sg_projection* out, std::stri
 void gen_release(GenEngine* e);
 void gen_stats(GenEngine* e, sg_stats* out);
 void gen_synchronize(GenEngine* e);
+std::string gen_describe(const GenEngine* e);
+// the smallest event seq a live partial references (UINT64_MAX: none); synchronises the engine's stream
+uint64_t gen_min_seq(GenEngine* e);
 // the multi-device fan-out (sg_sharded.cpp) merges the shards' timer matches in the single engine's order:
 // with keep = true every advance records, for each key that emitted, its queue head at that advance (the
 // listener's TreeMultimap order, Scheduler.java:78-99), in the key order the engine emitted them.

@@ -620,17 +620,20 @@ __device__ void write_out(const OutBufs& o, uint64_t d, const uint32_t* rec, boo
     }
 }
 
-// batch matches: out_count + t_off[trigger] + rank
+// batch matches: out_count + t_off[trigger] + rank (a grid-stride loop over the reserved raw slots); with
+// `only_if` (the GEN_M_TFIRST ordering's t_multi flag) the launch does nothing unless the flag is set
 __global__ void k_gen_scatter(const uint32_t* raw, const unsigned long long* raw_count, uint64_t seg_cap,
-                              uint32_t nseg, const uint32_t* t_off, OutBufs o) {
-    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t sg = r / seg_cap;  // reservation segment (GenOut)
-    if (sg >= nseg) return;
-    const uint64_t n = raw_count[sg] < seg_cap ? raw_count[sg] : seg_cap;
-    if (r - sg * seg_cap >= n) return;
-    const uint32_t* rec = raw + r * o.recWords;
-    if (rec[0] >= 0xfffffffeu) return;
-    write_out(o, *o.count + t_off[rec[0]] + rec[1], rec, false);
+                              uint32_t nseg, const uint32_t* t_off, OutBufs o, const uint32_t* only_if) {
+    if (only_if && *only_if == 0u) return;
+    for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < seg_cap * nseg;
+         r += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t sg = r / seg_cap;  // reservation segment (GenOut)
+        const uint64_t n = raw_count[sg] < seg_cap ? raw_count[sg] : seg_cap;
+        if (r - sg * seg_cap >= n) continue;
+        const uint32_t* rec = raw + r * o.recWords;
+        if (rec[0] >= 0xfffffffeu) continue;
+        write_out(o, *o.count + t_off[rec[0]] + rec[1], rec, false);
+    }
 }
 
 // batch matches when every trigger has at most one (GEN_M_TFIRST): output-major, one thread per trigger
@@ -642,8 +645,10 @@ __global__ void k_gen_scatter(const uint32_t* raw, const unsigned long long* raw
 // match's 192 B with 64 lanes' stores 192 B apart
 __global__ void __launch_bounds__(256) k_gen_gather1(const uint32_t* __restrict__ raw, const uint32_t* __restrict__ t_cnt,
                                                      const uint32_t* __restrict__ t_off,
-                                                     const uint32_t* __restrict__ t_first, uint32_t n, OutBufs o) {
+                                                     const uint32_t* __restrict__ t_first, uint32_t n, OutBufs o,
+                                                     const uint32_t* __restrict__ t_multi) {
     __shared__ uint32_t rb[4][64];   // per wave: the record index of its q-th match
+    if (*t_multi) return;            // (k_gen_scatter places the records)
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const bool has = i < n && t_cnt[i] != 0u;
@@ -784,6 +789,40 @@ __global__ void k_gen_live(const GenProgram* G, const uint32_t* S, uint32_t K, u
         }
     }
     if (live) atomicAdd(out, live);
+}
+
+// the smallest event seq any live partial still references: every StreamEvent a list's StateEvent reaches
+// (count chains followed), over every initialised key (the multi-device engine trims its seq maps below it)
+__global__ void k_gen_min_seq(const GenProgram* G, const uint32_t* S, uint32_t K, unsigned long long* out) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    unsigned long long m = ~0ull;
+    if (k < K && (S[gen_at(K, G->blockWords, G->offST, k, 0)] & 1u)) {
+        auto W = [&](uint32_t w) { return S[gen_at(K, G->blockWords, G->offST, k, w)]; };
+        for (int p = 0; p < G->nprocs; p++) {
+            const uint32_t ks = G->offKS + (uint32_t)p * G->ksWords;
+            for (int which = 0; which < 2; which++) {
+                const uint32_t n = W(ks + KS_PLEN + which);
+                for (uint32_t i = 0; i < n && i < G->L; i++) {
+                    const uint32_t se = W(ks + KS_LISTS + which * G->L + i);
+                    for (int sl = 0; sl < G->nslots; sl++) {
+                        uint32_t ev = W(G->offST + se * G->stWords + ST_SLOTS + sl);
+                        for (uint32_t guard = 0; ev != GEN_NIL && guard <= G->SECAP; guard++) {
+                            const uint32_t b = G->offSE + ev * G->seWords;
+                            const unsigned long long q = (unsigned long long)W(b + SE_SEQ) |
+                                                         ((unsigned long long)W(b + SE_SEQ + 1) << 32);
+                            m = q < m ? q : m;
+                            ev = W(b + SE_NEXT);
+                        }
+                    }
+                }
+            }
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long o = __shfl_xor(m, off, 64);
+        m = o < m ? o : m;
+    }
+    if ((threadIdx.x & 63) == 0 && m != ~0ull) atomicMin(out, m);
 }
 
 // ---- timer matches ordered through the due keys (one listener: GenTimers.kcnt / dpair_kid) ----
@@ -985,6 +1024,7 @@ struct GenEngine {
     uint32_t* raw = nullptr;
     unsigned long long* raw_count = nullptr;
     uint32_t *t_cnt = nullptr, *t_first = nullptr, *t_off = nullptr;
+    uint32_t* t_multi = nullptr;          // GenOut.t_multi
     int64_t* tk2 = nullptr;
     uint32_t *tk1 = nullptr, *tk3 = nullptr, *order_in = nullptr, *order_out = nullptr;
     unsigned long long* nvalid = nullptr;
@@ -1001,6 +1041,7 @@ struct GenEngine {
     void* psort_tmp = nullptr;
     size_t psort_tmp_bytes = 0;
     unsigned long long* live = nullptr;  // k_gen_live's sum (diagnostics)
+    unsigned long long* minseq = nullptr;  // k_gen_min_seq's result
     // keys the register-window kernels (abs_kernels.hip) hand to the general kernels
     uint32_t *fb_list = nullptr, *fb_start = nullptr;
     uint32_t *fb2_list = nullptr, *fb2_start = nullptr;  // the wave-per-key kernels' hand-over (absd_kernels.hip)
@@ -1081,6 +1122,7 @@ struct GenEngine {
         a.o.recWords = recWords;
         a.o.t_cnt = t_cnt;
         a.o.t_first = t_first;
+        a.o.t_multi = t_multi;
         a.o.tk1 = tk1;
         a.o.tk2 = tk2;
         a.o.tk3 = tk3;
@@ -1144,7 +1186,9 @@ GenEngine* gen_create(const uint32_t* ir, size_t nw, const sg_config& cfg, hipSt
         e->t_cnt = e->dalloc<uint32_t>(B);
         e->t_first = e->dalloc<uint32_t>(B);
         e->t_off = e->dalloc<uint32_t>(B);
+        e->t_multi = e->dalloc<uint32_t>(1);
         GH_OK(hipMemsetAsync(e->t_cnt, 0, B * 4, stream));
+        GH_OK(hipMemsetAsync(e->t_multi, 0, 4, stream));
         e->tk1 = e->dalloc<uint32_t>(e->rawCap);
         e->tk2 = e->dalloc<int64_t>(e->rawCap);
         e->tk3 = e->dalloc<uint32_t>(e->rawCap);
@@ -1378,6 +1422,7 @@ int gen_push(GenEngine* e, const sg_batch* b, std::string& msg) {
         cl.add(e->seg_begin, (size_t)e->K * 4);
         cl.add(e->seg_end, (size_t)e->K * 4);
         cl.add(e->raw_count, 8 * GEN_RAWSEG);
+        cl.add(e->t_multi, 4);
         if (abs_on(e) || cnt_on(e)) cl.add(e->fb_n, 8);
         if (abs_on(e) && absd_on(e)) cl.add(e->fb2_n, 8);
         GH_OK(cl.launch(e->stream));
@@ -1498,12 +1543,19 @@ int gen_push(GenEngine* e, const sg_batch* b, std::string& msg) {
     size_t tmp = e->scan_tmp_bytes;
     GH_OK(rocprim::exclusive_scan(e->scan_tmp, tmp, e->t_cnt, e->t_off, 0u, n, rocprim::plus<uint32_t>(), e->stream));
     const uint64_t maxRaw = e->rawCap;
-    if (a.mode & GEN_M_TFIRST)
+    if (a.mode & GEN_M_TFIRST) {
+        // output-major gather of the one match per trigger; a trigger of a handed-over key that emitted several
+        // (t_multi, set on the device) turns it off and every record is placed by (t_off, rank) instead
         hipLaunchKernelGGL(k_gen_gather1, dim3((n + 255) / 256), dim3(256), 0, e->stream, e->raw, e->t_cnt, e->t_off,
-                           e->t_first, n, e->out);
-    else
-        hipLaunchKernelGGL(k_gen_scatter, dim3((unsigned)((maxRaw + 255) / 256)), dim3(256), 0, e->stream, e->raw,
-                           e->raw_count, e->rawCap / GEN_RAWSEG, (uint32_t)GEN_RAWSEG, e->t_off, e->out);
+                           e->t_first, n, e->out, (const uint32_t*)e->t_multi);
+        hipLaunchKernelGGL(k_gen_scatter, dim3((unsigned)std::min<uint64_t>((maxRaw + 255) / 256, 4096)), dim3(256), 0,
+                           e->stream, e->raw, e->raw_count, e->rawCap / GEN_RAWSEG, (uint32_t)GEN_RAWSEG, e->t_off, e->out,
+                           (const uint32_t*)e->t_multi);
+    } else {
+        hipLaunchKernelGGL(k_gen_scatter, dim3((unsigned)std::min<uint64_t>((maxRaw + 255) / 256, 4096)), dim3(256), 0,
+                           e->stream, e->raw, e->raw_count, e->rawCap / GEN_RAWSEG, (uint32_t)GEN_RAWSEG, e->t_off, e->out,
+                           (const uint32_t*)nullptr);
+    }
     hipLaunchKernelGGL(k_gen_bump, dim3(1), dim3(1), 0, e->stream, e->out.count, e->t_cnt, e->t_off, n,
                        (const unsigned long long*)nullptr);
     {
@@ -1881,6 +1933,43 @@ void gen_stats(GenEngine* e, sg_stats* out) {
     out->keys_touched = s[GST_KEYS];
     out->window_spills = s[GST_SPILLS];
     out->partials_live = lv;
+}
+
+uint64_t gen_min_seq(GenEngine* e) {
+    if (!e->minseq) e->minseq = e->dalloc<unsigned long long>(1);
+    unsigned long long* m = e->minseq;
+    unsigned long long h = ~0ull;
+    GH_OK(hipMemcpyAsync(m, &h, 8, hipMemcpyHostToDevice, e->stream));
+    hipLaunchKernelGGL(k_gen_min_seq, dim3((e->K + 255) / 256), dim3(256), 0, e->stream, e->dprog, e->state, e->K, m);
+    GH_OK(hipMemcpyAsync(&h, m, 8, hipMemcpyDeviceToHost, e->stream));
+    GH_OK(hipStreamSynchronize(e->stream));
+    return h;
+}
+
+// the kernels a push and an advance dispatch (sg_engine_describe), in launch order
+std::string gen_describe(const GenEngine* e) {
+    const GenProgram& G = e->host;
+    const std::string nw = std::to_string(G.absNW);
+    std::string push, adv;
+    if (abs_on(e)) {
+        const GenPre& f0 = G.pre[G.absP0];
+        const GenPre& f1 = G.pre[G.absP1];
+        const bool ff = (f0.flen == 0 || f0.ff.on) && (f1.flen == 0 || f1.ff.on);
+        push = (ff ? "k_abs_batchf_" : "k_abs_batch_") + nw + " (register window, lane per key)";
+        adv = "k_abs_timers_" + nw + " (register window)";
+        if (absd_on(e)) {
+            push += " + k_absd_batch_" + nw + " (deep keys, wave per key)";
+            adv += " + k_absd_timers_" + nw + " (deep keys)";
+        }
+        push += " + k_gen_batch (keys handed over)";
+        adv += " + k_gen_timers (keys handed over)";
+    } else if (cnt_on(e)) {
+        push = "k_cnt_batch_" + nw + " (register window, lane per key) + k_gen_batch (keys handed over)";
+    } else {
+        push = "k_gen_batch (general interpreter, lane per key)";
+        if (G.nStartup > 0) adv = "k_gen_timers (general interpreter)";
+    }
+    return "push: " + push + (adv.empty() ? std::string() : "; advance: " + adv);
 }
 
 void gen_synchronize(GenEngine* e) { GH_OK(hipStreamSynchronize(e->stream)); }

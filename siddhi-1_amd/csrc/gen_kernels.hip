@@ -475,8 +475,15 @@ struct Lane {
             gp(A.o.tk2)[r] = tk2;
             gp(A.o.tk3)[r] = k;
         } else {
-            gp(A.o.t_cnt)[trigIdx] += 1;
-            if (A.mode & GEN_M_TFIRST) gp(A.o.t_first)[trigIdx] = (uint32_t)r;
+            const uint32_t c0 = gp(A.o.t_cnt)[trigIdx];
+            gp(A.o.t_cnt)[trigIdx] = c0 + 1u;
+            if (A.mode & GEN_M_TFIRST) {
+                gp(A.o.t_first)[trigIdx] = (uint32_t)r;
+                // a second match of one trigger (a key handed over in a non-canonical state, e.g. imported,
+                // can hold several partials): t_first keeps one record only, so the ordering must place
+                // every record by (t_off, rank) instead (gen_host.hip: k_gen_scatter when t_multi is set)
+                if (c0) *gp(A.o.t_multi) = 1u;
+            }
         }
     }
 
@@ -1205,6 +1212,9 @@ __device__ void gen_wave_stats(const GenArgs& a, unsigned long long sc, unsigned
 // consecutive keys of one row of the interleaved state at each j.
 extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GEN_WAVES, 8))) k_gen_batch(const GenArgs ap) {
     const GenArgs& a = ap;
+    // a hand-over launch (a fixed grid over a list whose length only the device knows) whose waves have no
+    // key leave before the lane object exists: building it (it lives in scratch) wrote ~50 MB per empty launch
+    if ((a.mode & GEN_M_KEYLIST) && (unsigned long long)blockIdx.x * 64u >= *a.fb_n) return;
     const uint32_t kpl = a.kpl ? a.kpl : 1u;
     const uint32_t k0 = blockIdx.x * kpl * 64u + threadIdx.x;
     const auto& r = ((const cGenProgram*)a.G)->recv[a.b.stream];
@@ -1441,6 +1451,7 @@ extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per
     const uint64_t t0_ = __builtin_amdgcn_s_memtime();
 #endif
     const uint64_t n = a.G->partitioned ? *a.t.ndue : 1ull;
+    if ((uint64_t)blockIdx.x * blockDim.x >= n) return;   // (waves with no due key: nothing to count)
     unsigned long long sc = 0, cr = 0, ma = 0;
     uint32_t er = 0;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)

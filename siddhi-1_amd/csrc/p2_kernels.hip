@@ -371,6 +371,27 @@ __global__ void __launch_bounds__(256) k_stats_reduce(const unsigned long long* 
     }
 }
 
+// the smallest e1 seq a live partial holds (pending + staged rows of every key; the multi-device engine trims
+// its seq maps below it)
+__global__ void __launch_bounds__(256) k_min_seq(const uint32_t* __restrict__ hdr, const uint64_t* __restrict__ p_seq,
+                                                 uint32_t n_keys, unsigned long long* out) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    unsigned long long m = ~0ull;
+    if (k < n_keys) {
+        const uint32_t h = hdr[k];
+        const uint32_t c = SGD_H_NPEND(h) + SGD_H_NSTG(h);
+        for (uint32_t j = 0; j < c; j++) {
+            const unsigned long long q = p_seq[(size_t)j * n_keys + k];
+            m = q < m ? q : m;
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long o = __shfl_xor(m, off, 64);
+        m = o < m ? o : m;
+    }
+    if ((threadIdx.x & 63) == 0 && m != ~0ull) atomicMin(out, m);
+}
+
 // ------------------------------------------------------------------------------------------------
 // launch wrappers
 // ------------------------------------------------------------------------------------------------
@@ -422,5 +443,11 @@ int sgd_launch_scatter(const ScatterParams& s, void* scan_tmp, size_t scan_bytes
         return -1;
     hipLaunchKernelGGL(k_order_scatter, dim3(nt), dim3(256), 0, stream, s, nt);
     hipLaunchKernelGGL(k_bump, dim3(1), dim3(1), 0, stream, s.out_count, s.batch_total);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int sgd_launch_min_seq(const uint32_t* hdr, const uint64_t* p_seq, uint32_t n_keys, unsigned long long* out,
+                       ihipStream_t* stream) {
+    hipLaunchKernelGGL(k_min_seq, dim3((n_keys + 255) / 256), dim3(256), 0, stream, hdr, p_seq, n_keys, out);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

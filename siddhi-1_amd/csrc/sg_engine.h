@@ -235,6 +235,8 @@ int sgd_launch_reset_keys(const uint32_t* keys, uint32_t n, uint32_t n_keys, uin
                           ihipStream_t* stream);
 // *bad = 1 iff some keys[i] >= n_keys (device ids of sg_reset_keys, checked before any reset)
 int sgd_launch_check_keys(const uint32_t* keys, uint32_t n, uint32_t n_keys, uint32_t* bad, ihipStream_t* stream);
+int sgd_launch_min_seq(const uint32_t* hdr, const uint64_t* p_seq, uint32_t n_keys, unsigned long long* out,
+                       ihipStream_t* stream);
 // sums the staged pass's per-wave counters of one batch into stats[SGD_ST_N]
 int sgd_launch_stats_reduce(const unsigned long long* wstats, uint32_t n_waves, unsigned long long* stats,
                             unsigned long long* raw_count, uint32_t* dlist_n, ihipStream_t* stream);

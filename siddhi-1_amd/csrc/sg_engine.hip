@@ -1320,6 +1320,28 @@ int set_projection(sg_engine* e, const uint32_t* code, uint32_t words, const uin
 // the other host-side translation units (sg_dict.cpp) report through the same sg_last_error
 int sg_set_error(int code, const char* msg) { return fail(code, msg); }
 
+// the multi-device engine (sg_sharded.cpp): the smallest event seq a live partial references (UINT64_MAX: none),
+// after every queued batch; and an event recorded behind everything queued so far (its reads of a pushed device
+// batch included: the two-state engine's grouping stream joins the main stream before the advance)
+uint64_t sg_internal_min_seq(sg_engine* e) {
+    HIP_OK(hipSetDevice(e->device));
+    if (e->gen) return gen_min_seq(e->gen);
+    sync_all(e);
+    unsigned long long h = ~0ull;
+    unsigned long long* m = nullptr;
+    HIP_OK(hipMalloc(&m, 8));
+    HIP_OK(hipMemcpyAsync(m, &h, 8, hipMemcpyHostToDevice, e->stream));
+    if (sgd_launch_min_seq(e->hdr, e->p_seq, e->K, m, e->stream) != 0) throw HipError("k_min_seq launch failed");
+    HIP_OK(hipMemcpyAsync(&h, m, 8, hipMemcpyDeviceToHost, e->stream));
+    HIP_OK(hipStreamSynchronize(e->stream));
+    HIP_OK(hipFree(m));
+    return h;
+}
+void sg_internal_record(sg_engine* e, hipEvent_t ev) {
+    HIP_OK(hipSetDevice(e->device));
+    HIP_OK(hipEventRecord(ev, e->stream));
+}
+
 bool sg_internal_keep_heads(sg_engine* e) { return e && e->gen ? gen_keep_timer_heads(e->gen, true) : false; }
 void sg_internal_heads(sg_engine* e, std::vector<uint32_t>& keys, std::vector<int64_t>& heads) {
     keys.clear();
@@ -1540,6 +1562,8 @@ int sg_wait_stream(sg_engine* e, void* stream) {
         hipEvent_t x = e->ev();
         HIP_OK(hipEventRecord(x, (hipStream_t)stream));
         HIP_OK(hipStreamWaitEvent(e->stream, x, 0));
+        // the two-state engine reads a pushed batch first on its grouping stream (copies + sort): it waits too
+        if (e->gstream) HIP_OK(hipStreamWaitEvent(e->gstream, x, 0));
         e->free_events.push_back(x);  // reusable once recorded again (a wait captures the recorded work)
         return SG_OK;
     } catch (const std::exception& ex) {
@@ -1620,6 +1644,27 @@ int sg_get_stats(sg_engine* e, sg_stats* out) {
     } catch (const std::exception& ex) {
         return fail(SG_ERR_DEVICE, ex.what());
     }
+}
+
+int sg_engine_describe(sg_engine* e, char* out, size_t out_len) {
+    if (!e || (!out && out_len)) return fail(SG_ERR_INVALID, "null argument");
+    std::string d;
+    sg_engine* one = e->shard ? shd_first(e->shard) : e;
+    if (one->gen) {
+        d = gen_describe(one->gen);
+    } else {
+        d = std::string("push: ") + (one->tile_grp ? "k_grp_hist + k_grp_scatter + k_grp_tile" : "rocPRIM onesweep radix sort") +
+            " + k_seg_bounds (grouping, stream 2); k_adv_m (NFA advance, LDS-staged, lane per key) + k_adv_m_h "
+            "(NFA advance, HBM pass) + k_stats_reduce; k_order_sums + scan + k_order_scatter (ordering)";
+        if (one->proj_n) d += " + k_project" + std::string(one->n_agg ? " + k_agg" : "");
+    }
+    if (e->shard) d = std::to_string(shd_count(e->shard)) + " shards, each " + d;
+    if (out_len) {
+        const size_t n = std::min(out_len - 1, d.size());
+        memcpy(out, d.data(), n);
+        out[n] = 0;
+    }
+    return SG_OK;
 }
 
 // ---- partition purge (PartitionRuntimeImpl.java:368-401) ----------------------------------------

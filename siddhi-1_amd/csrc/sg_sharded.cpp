@@ -19,8 +19,19 @@
 // (n_keys == 1) does not shard: one key's NFA is sequential, it runs on the first device.
 //
 // Shards are driven concurrently, one host thread per device per call (each sub-engine is used by one thread at
-// a time, as siddhi_gpu.h requires).  Device batches are staged to host memory and split there; polls return
-// host memory only (the bench's multi-GPU path reshards on the devices with RCCL instead, bench.py).
+// a time, as siddhi_gpu.h requires).  A device batch stays on the devices: it is split by owner on the device it
+// was handed over on (shard_kernels.hip fan_split: stable, one destination-major copy of each column), a shard on
+// another device gets its part by a peer copy, and each shard's engine waits for that work on the device
+// (sg_wait_stream) — only the per-shard counts and the 4-B batch position of every event (the seq map) come to
+// the host.  Host batches are split on the host.  Polls return host memory.
+//
+// Seq maps are bounded by live state, not by stream length: after a poll (every shard drained: no match is
+// pending on any device), a shard whose map has grown past its threshold reports the smallest seq a live partial
+// of it still references (sg_internal_min_seq) and its map drops every entry below (SeqMap.trim).
+//
+// A call that fails part-way (one shard took a sub-batch, another refused it; a poll that lost one shard's
+// matches) leaves the shards out of step: the engine then refuses every call but sg_restore / sg_state_import /
+// the read-only ones with SG_ERR_STATE (siddhi_gpu.h).
 #include "sg_sharded.h"
 
 #include <string.h>
@@ -53,16 +64,116 @@ size_t tsize(uint32_t t) {
     }
 }
 
-const uint64_t kMagic = 0x3148534753ull;  // "SGSH1"
+const uint64_t kMagic = 0x3248534753ull;  // "SGSH2" (v2: seq maps with their base)
 
 }  // namespace
+
+// a shard's local -> global seq map: local seq base + i maps to v[i]; entries below `base` were trimmed (no live
+// partial and no pending match references them)
+struct SeqMap {
+    uint64_t base = 0;
+    std::vector<uint64_t> v;
+    uint64_t trim_at = 1u << 20;   // the size at which the next trim check runs (doubles with the live span)
+    uint64_t end() const { return base + v.size(); }
+    void trim(uint64_t keep_from) {
+        if (keep_from <= base) return;
+        const uint64_t d = std::min<uint64_t>(keep_from - base, v.size());
+        v.erase(v.begin(), v.begin() + (ptrdiff_t)d);
+        base += d;
+    }
+};
 
 struct ShardEngine {
     uint32_t N = 1, K = 1, KL = 1;   // shards, global / local key ranges
     bool null_keys = false;
     std::vector<sg_engine*> sh;
     std::vector<std::vector<uint32_t>> attr_types;   // per stream of the IR
-    std::vector<std::vector<uint64_t>> gmap;         // per shard: global seq of each local seq
+    std::vector<int> dev;                            // per shard: its HIP device
+    std::vector<SeqMap> gmap;                        // per shard: global seq of each local seq
+    bool failed = false;                             // a call failed part-way (shards out of step)
+    uint64_t staged_bytes = 0;                       // batch bytes copied to host memory (host splits of device batches: none)
+    uint64_t trims = 0;
+    // device batches: split on their own device (fan_split), two buffer sets used alternately; set j's events
+    // done[r] (on shard r's device) are recorded behind what reads set j for shard r — the shard's push, or the
+    // peer copy of its part — and the next split into set j waits for them on the device
+    struct DevSplit {
+        int device = -1;
+        hipStream_t stream = nullptr;
+        size_t scratch_len = 0;
+        uint32_t* totals = nullptr;   // [N] device
+        uint32_t* err = nullptr;
+        uint32_t* h_totals = nullptr; // pinned [N + 1] (err last)
+        uint32_t* h_opos = nullptr;   // pinned [max_batch]
+        struct Set {
+            void* scratch = nullptr;
+            int64_t* ts = nullptr;
+            uint32_t* key = nullptr;
+            uint32_t* opos = nullptr;
+            std::vector<void*> cols;
+            std::vector<uint8_t*> nulls;
+            std::vector<hipEvent_t> done;  // per shard (created on dev[r])
+            std::vector<char> armed;
+        } set[2];
+        uint32_t next = 0;
+    };
+    // a shard's staging on its own device for parts split on another device
+    struct Peer {
+        hipStream_t stream = nullptr;
+        struct Set {
+            int64_t* ts = nullptr;
+            uint32_t* key = nullptr;
+            std::vector<void*> cols;
+            std::vector<uint8_t*> nulls;
+            hipEvent_t done = nullptr;     // recorded behind the shard's push from this set
+            bool armed = false;
+        } set[2];
+        uint32_t next = 0;
+    };
+    std::vector<DevSplit> splits;   // by source device ordinal (lazily)
+    std::vector<Peer> peers;        // per shard (lazily)
+    bool force_peer = false;        // SG_FAN_PEER_COPY (tests): peer-copy every part, even on the source device
+    uint64_t max_batch = 0;
+    size_t max_attrs = 1;
+
+    ~ShardEngine() { free_device_buffers(); }
+    void free_device_buffers() {
+        for (size_t r = 0; r < peers.size(); r++) {
+            Peer& q = peers[r];
+            if (!q.stream) continue;
+            (void)hipSetDevice(dev[r]);
+            (void)hipStreamSynchronize(q.stream);
+            for (auto& st : q.set) {
+                if (st.done) (void)hipEventDestroy(st.done);
+                for (void* x : {(void*)st.ts, (void*)st.key}) if (x) (void)hipFree(x);
+                for (void* x : st.cols) if (x) (void)hipFree(x);
+                for (void* x : st.nulls) if (x) (void)hipFree(x);
+            }
+            (void)hipStreamDestroy(q.stream);
+        }
+        peers.clear();
+        for (DevSplit& p : splits) {
+            if (p.device < 0) continue;
+            (void)hipSetDevice(p.device);
+            if (p.stream) (void)hipStreamSynchronize(p.stream);
+            for (auto& st : p.set) {
+                for (size_t r = 0; r < st.done.size(); r++)
+                    if (st.done[r]) {
+                        (void)hipSetDevice(dev[r]);
+                        (void)hipEventDestroy(st.done[r]);
+                    }
+                (void)hipSetDevice(p.device);
+                for (void* x : {st.scratch, (void*)st.ts, (void*)st.key, (void*)st.opos}) if (x) (void)hipFree(x);
+                for (void* x : st.cols) if (x) (void)hipFree(x);
+                for (void* x : st.nulls) if (x) (void)hipFree(x);
+            }
+            for (void* x : {(void*)p.totals, (void*)p.err}) if (x) (void)hipFree(x);
+            if (p.h_totals) (void)hipHostFree(p.h_totals);
+            if (p.h_opos) (void)hipHostFree(p.h_opos);
+            if (p.stream) (void)hipStreamDestroy(p.stream);
+        }
+        splits.clear();
+    }
+
     // matches in host memory, in the single engine's order: `pend` collects them as the shards produce them
     // (batch matches before every advance, timer matches right after it), a poll hands `pend` out as `out`
     struct Out {
@@ -107,10 +218,12 @@ struct ShardEngine {
             if (rc[r] != SG_OK) throw ShardError(rc[r], "shard " + std::to_string(r) + ": " + msg[r]);
     }
 
+
     uint64_t map_seq(uint32_t r, uint64_t local) const {
         if (local >= SG_BLANK_SEQ) return local;   // null / blank / timer markers pass through
-        if (local >= gmap[r].size()) throw ShardError(SG_ERR_DEVICE, "shard seq outside its map");
-        return gmap[r][local];
+        const SeqMap& m = gmap[r];
+        if (local < m.base || local >= m.end()) throw ShardError(SG_ERR_DEVICE, "shard seq outside its map");
+        return m.v[local - m.base];
     }
 };
 
@@ -159,6 +272,7 @@ HostBatch stage(const ShardEngine* s, const sg_batch* b) {
     }
     auto copy = [&](const void* src, size_t bytes) -> const void* {
         h.store.emplace_back(bytes);
+        const_cast<ShardEngine*>(s)->staged_bytes += bytes;
         if (bytes && hipMemcpy(h.store.back().data(), src, bytes, hipMemcpyDeviceToHost) != hipSuccess)
             throw ShardError(SG_ERR_DEVICE, "staging a device batch failed");
         return h.store.back().data();
@@ -185,10 +299,14 @@ ShardEngine* shd_create(const void* ir, size_t ir_len, const sg_config* cfg, int
         s->null_keys = (cfg->flags & SG_CFG_NULL_KEYS) != 0;
         s->gmap.resize(s->N);
         s->sh.assign(s->N, nullptr);
+        s->max_batch = cfg->max_batch ? cfg->max_batch : (1u << 20);
+        for (const auto& t : s->attr_types) s->max_attrs = std::max(s->max_attrs, t.size());
+        s->force_peer = getenv("SG_FAN_PEER_COPY") != nullptr;
+        for (uint32_t r = 0; r < s->N; r++) s->dev.push_back(cfg->devices ? cfg->devices[r] : cfg->device);
         for (uint32_t r = 0; r < s->N; r++) {
             sg_config c = *cfg;
             c.struct_size = sizeof(sg_config);
-            c.device = cfg->devices[r];
+            c.device = s->dev[r];
             c.n_keys = s->K > 1 ? s->KL : 1;
             c.n_devices = 1;
             c.devices = nullptr;
@@ -215,8 +333,204 @@ void shd_destroy(ShardEngine* s) {
     delete s;
 }
 
+namespace {
+
+#define FAN_OK(x)                                                                                         \
+    do {                                                                                                  \
+        const hipError_t e_ = (x);                                                                        \
+        if (e_ != hipSuccess) throw ShardError(SG_ERR_DEVICE, std::string(#x) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+template <class T> T* fan_alloc(size_t n) {
+    void* p = nullptr;
+    FAN_OK(hipMalloc(&p, std::max<size_t>(n, 1) * sizeof(T)));
+    return (T*)p;
+}
+
+ShardEngine::DevSplit& split_for(ShardEngine* s, int device) {
+    if ((size_t)device >= s->splits.size()) s->splits.resize(device + 1);
+    ShardEngine::DevSplit& p = s->splits[device];
+    if (p.device >= 0) return p;
+    FAN_OK(hipSetDevice(device));
+    p.device = device;
+    const size_t B = s->max_batch;
+    FAN_OK(hipStreamCreateWithFlags(&p.stream, hipStreamNonBlocking));
+    p.scratch_len = fan_split_scratch_bytes(B, s->N);
+    p.totals = fan_alloc<uint32_t>(s->N + 1);
+    p.err = p.totals + s->N;
+    FAN_OK(hipHostMalloc((void**)&p.h_totals, (s->N + 1) * 4, hipHostMallocDefault));
+    FAN_OK(hipHostMalloc((void**)&p.h_opos, B * 4, hipHostMallocDefault));
+    for (auto& st : p.set) {
+        st.scratch = fan_alloc<uint8_t>(p.scratch_len);
+        st.ts = fan_alloc<int64_t>(B);
+        st.key = fan_alloc<uint32_t>(B);
+        st.opos = fan_alloc<uint32_t>(B);
+        for (size_t c = 0; c < s->max_attrs; c++) {
+            st.cols.push_back(fan_alloc<uint64_t>(B));
+            st.nulls.push_back(fan_alloc<uint8_t>(B));
+        }
+        st.done.assign(s->N, nullptr);
+        st.armed.assign(s->N, 0);
+        for (uint32_t r = 0; r < s->N; r++) {
+            FAN_OK(hipSetDevice(s->dev[r]));
+            FAN_OK(hipEventCreateWithFlags(&st.done[r], hipEventDisableTiming));
+        }
+        FAN_OK(hipSetDevice(device));
+    }
+    return p;
+}
+
+ShardEngine::Peer& peer_for(ShardEngine* s, uint32_t r) {
+    ShardEngine::Peer& q = s->peers[r];
+    if (q.stream) return q;
+    FAN_OK(hipSetDevice(s->dev[r]));
+    const size_t B = s->max_batch;
+    FAN_OK(hipStreamCreateWithFlags(&q.stream, hipStreamNonBlocking));
+    for (auto& st : q.set) {
+        st.ts = fan_alloc<int64_t>(B);
+        st.key = fan_alloc<uint32_t>(B);
+        for (size_t c = 0; c < s->max_attrs; c++) {
+            st.cols.push_back(fan_alloc<uint64_t>(B));
+            st.nulls.push_back(fan_alloc<uint8_t>(B));
+        }
+        FAN_OK(hipEventCreateWithFlags(&st.done, hipEventDisableTiming));
+    }
+    return q;
+}
+
+// a device batch, split on its device: the shards' parts pushed as device batches (peer-copied to shards on
+// other devices), each shard's engine waiting for its part on the device; only the per-shard counts and the
+// batch position of every event (the seq maps) are copied to the host
+void push_device(ShardEngine* s, const sg_batch* b) {
+    hipPointerAttribute_t at{};
+    FAN_OK(hipPointerGetAttributes(&at, b->ts));
+    const int src = at.device;
+    const uint32_t N = s->N;
+    const uint64_t n = b->n;
+    if (n > s->max_batch) throw ShardError(SG_ERR_INVALID, "batch larger than max_batch");
+    const auto& ty = s->attr_types[b->stream];
+    const uint32_t nc = b->n_cols;
+    ShardEngine::DevSplit& p = split_for(s, src);
+    const uint32_t j = p.next;
+    auto& st = p.set[j];
+    FAN_OK(hipSetDevice(src));
+    for (uint32_t r = 0; r < N; r++)   // this set's previous readers are done (on the device)
+        if (st.armed[r]) FAN_OK(hipStreamWaitEvent(p.stream, st.done[r], 0));
+    std::vector<const void*> cols(nc);
+    std::vector<uint32_t> cb(nc);
+    std::vector<const uint8_t*> nul(nc, nullptr);
+    bool anyNull = false;
+    for (uint32_t c = 0; c < nc; c++) {
+        cols[c] = b->cols[c];
+        cb[c] = (uint32_t)tsize(ty[c]);
+        if (b->nulls && b->nulls[c]) {
+            nul[c] = b->nulls[c];
+            anyNull = true;
+        }
+    }
+    std::vector<void*> ocols(st.cols.begin(), st.cols.begin() + nc);
+    std::vector<uint8_t*> onul(st.nulls.begin(), st.nulls.begin() + nc);
+    const int rc = fan_split(n, b->key, s->K, N, s->null_keys, b->ts, cols.data(), cb.data(), nul.data(), nc, st.ts,
+                             ocols.data(), onul.data(), st.opos, st.key, p.totals, p.err, st.scratch, p.scratch_len,
+                             p.stream);
+    if (rc != SG_OK) throw ShardError(rc, "device split of the batch failed");
+    FAN_OK(hipMemcpyAsync(p.h_totals, p.totals, (N + 1) * 4, hipMemcpyDeviceToHost, p.stream));
+    FAN_OK(hipMemcpyAsync(p.h_opos, st.opos, n * 4, hipMemcpyDeviceToHost, p.stream));
+    FAN_OK(hipStreamSynchronize(p.stream));
+    if (p.h_totals[N]) throw ShardError(SG_ERR_INVALID, "key id outside [0, n_keys)");
+    // validated: nothing has changed yet (a rejected batch leaves every shard as it was)
+    std::vector<uint64_t> off(N + 1, 0);
+    for (uint32_t r = 0; r < N; r++) off[r + 1] = off[r] + p.h_totals[r];
+    hipEvent_t split_done = nullptr;
+    FAN_OK(hipEventCreateWithFlags(&split_done, hipEventDisableTiming));
+    FAN_OK(hipEventRecord(split_done, p.stream));
+    p.next ^= 1u;
+    if (s->peers.empty()) s->peers.resize(N);   // (before the shard threads: peer_for touches only peers[r])
+    std::vector<char> pushed(N, 0);
+    try {
+        s->each([&](uint32_t r) -> int {
+            const uint64_t m = off[r + 1] - off[r];
+            if (m == 0) return SG_OK;
+            FAN_OK(hipSetDevice(s->dev[r]));
+            sg_batch c{};
+            c.struct_size = sizeof(sg_batch);
+            c.stream = b->stream;
+            c.n = m;
+            c.seq_base = s->gmap[r].end();
+            c.n_cols = nc;
+            c.mem = SG_MEM_DEVICE;
+            std::vector<const void*> cp(nc);
+            std::vector<const uint8_t*> np(nc, nullptr);
+            const bool copy = s->force_peer || s->dev[r] != src;
+            ShardEngine::Peer::Set* ps = nullptr;
+            hipStream_t wait_on = p.stream;
+            if (copy) {   // the part to the shard's device (a peer copy; on one device a device-to-device copy)
+                ShardEngine::Peer& q = peer_for(s, r);
+                ps = &q.set[q.next];
+                q.next ^= 1u;
+                if (ps->armed) FAN_OK(hipStreamWaitEvent(q.stream, ps->done, 0));
+                FAN_OK(hipStreamWaitEvent(q.stream, split_done, 0));
+                FAN_OK(hipMemcpyPeerAsync(ps->ts, s->dev[r], st.ts + off[r], src, m * 8, q.stream));
+                FAN_OK(hipMemcpyPeerAsync(ps->key, s->dev[r], st.key + off[r], src, m * 4, q.stream));
+                for (uint32_t c2 = 0; c2 < nc; c2++) {
+                    FAN_OK(hipMemcpyPeerAsync(ps->cols[c2], s->dev[r], (const uint8_t*)st.cols[c2] + off[r] * cb[c2], src,
+                                              m * cb[c2], q.stream));
+                    if (nul[c2])
+                        FAN_OK(hipMemcpyPeerAsync(ps->nulls[c2], s->dev[r], st.nulls[c2] + off[r], src, m, q.stream));
+                }
+                // the split set may be reused once the copies ran
+                FAN_OK(hipEventRecord(st.done[r], q.stream));
+                st.armed[r] = 1;
+                c.ts = ps->ts;
+                c.key = ps->key;
+                for (uint32_t c2 = 0; c2 < nc; c2++) {
+                    cp[c2] = ps->cols[c2];
+                    np[c2] = nul[c2] ? ps->nulls[c2] : nullptr;
+                }
+                wait_on = q.stream;
+            } else {
+                c.ts = st.ts + off[r];
+                c.key = st.key + off[r];
+                for (uint32_t c2 = 0; c2 < nc; c2++) {
+                    cp[c2] = (const uint8_t*)st.cols[c2] + off[r] * cb[c2];
+                    np[c2] = nul[c2] ? st.nulls[c2] + off[r] : nullptr;
+                }
+            }
+            c.cols = cp.data();
+            c.nulls = anyNull ? np.data() : nullptr;
+            int rc2 = sg_wait_stream(s->sh[r], wait_on);
+            if (rc2 != SG_OK) return rc2;
+            rc2 = sg_push_batch(s->sh[r], &c);
+            if (rc2 != SG_OK) return rc2;
+            pushed[r] = 1;
+            // what reads the part is queued: the buffers it lives in are free once the shard's engine ran it
+            if (copy) {
+                sg_internal_record(s->sh[r], ps->done);
+                ps->armed = true;
+            } else {
+                sg_internal_record(s->sh[r], st.done[r]);
+                st.armed[r] = 1;
+            }
+            SeqMap& g = s->gmap[r];
+            const size_t g0 = g.v.size();
+            g.v.resize(g0 + m);
+            for (uint64_t i = 0; i < m; i++) g.v[g0 + i] = b->seq_base + p.h_opos[off[r] + i];
+            return SG_OK;
+        });
+    } catch (...) {
+        (void)hipEventDestroy(split_done);
+        for (uint32_t r = 0; r < N; r++)
+            if (pushed[r]) s->failed = true;   // some shards took their part: the engine is out of step
+        throw;
+    }
+    (void)hipEventDestroy(split_done);
+}
+
+}  // namespace
+
 int shd_push(ShardEngine* s, const sg_batch* b) {
     try {
+        if (s->failed) throw ShardError(SG_ERR_STATE, "a previous call failed part-way: restore a snapshot first");
         if (s->held) throw ShardError(SG_ERR_STATE, "release the polled matches before pushing");
         if (b->stream >= s->attr_types.size()) throw ShardError(SG_ERR_INVALID, "stream index out of range");
         if (b->n_cols != s->attr_types[b->stream].size())
@@ -225,19 +539,20 @@ int shd_push(ShardEngine* s, const sg_batch* b) {
         const uint64_t n = b->n;
         if (s->N == 1) {   // (unpartitioned, or one device): the shard takes the batch as it is
             sg_batch c = *b;
-            c.seq_base = s->gmap[0].size();
-            std::vector<uint64_t>& m = s->gmap[0];
-            const size_t m0 = m.size();
-            m.resize(m0 + n);
-            for (uint64_t i = 0; i < n; i++) m[m0 + i] = b->seq_base + i;
+            SeqMap& m = s->gmap[0];
+            c.seq_base = m.end();
             const int rc = sg_push_batch(s->sh[0], &c);
-            if (rc != SG_OK) {
-                m.resize(m0);
-                return rc;
-            }
+            if (rc != SG_OK) return rc;
+            const size_t m0 = m.v.size();
+            m.v.resize(m0 + n);
+            for (uint64_t i = 0; i < n; i++) m.v[m0 + i] = b->seq_base + i;
             return SG_OK;
         }
         if (!b->key) throw ShardError(SG_ERR_INVALID, "partitioned query needs key ids");
+        if (b->mem == SG_MEM_DEVICE) {
+            push_device(s, b);
+            return SG_OK;
+        }
         HostBatch h = stage(s, b);
         const uint32_t N = s->N;
         // owner of every event (null keys: dropped with SG_CFG_NULL_KEYS, else an error), per-shard counts
@@ -298,35 +613,45 @@ int shd_push(ShardEngine* s, const sg_batch* b) {
             }
             return SG_OK;
         });
-        s->each([&](uint32_t r) -> int {
-            Sub& u = sub[r];
-            if (u.ts.empty()) return SG_OK;
-            std::vector<const void*> cp(nc);
-            std::vector<const uint8_t*> np(nc, nullptr);
-            bool anyNull = false;
-            for (uint32_t c = 0; c < nc; c++) {
-                cp[c] = u.cols[c].data();
-                if (h.nulls[c]) {
-                    np[c] = u.nulls[c].data();
-                    anyNull = true;
+        std::vector<char> pushed(N, 0);
+        try {
+            s->each([&](uint32_t r) -> int {
+                Sub& u = sub[r];
+                if (u.ts.empty()) return SG_OK;
+                std::vector<const void*> cp(nc);
+                std::vector<const uint8_t*> np(nc, nullptr);
+                bool anyNull = false;
+                for (uint32_t c = 0; c < nc; c++) {
+                    cp[c] = u.cols[c].data();
+                    if (h.nulls[c]) {
+                        np[c] = u.nulls[c].data();
+                        anyNull = true;
+                    }
                 }
-            }
-            std::vector<uint64_t>& m = s->gmap[r];
-            sg_batch c{};
-            c.struct_size = sizeof(sg_batch);
-            c.stream = b->stream;
-            c.n = u.ts.size();
-            c.seq_base = m.size();
-            c.key = u.key.data();
-            c.ts = u.ts.data();
-            c.cols = cp.data();
-            c.nulls = anyNull ? np.data() : nullptr;
-            c.n_cols = nc;
-            c.mem = SG_MEM_HOST;
-            const int rc = sg_push_batch(s->sh[r], &c);
-            if (rc == SG_OK) m.insert(m.end(), u.glob.begin(), u.glob.end());
-            return rc;
-        });
+                SeqMap& m = s->gmap[r];
+                sg_batch c{};
+                c.struct_size = sizeof(sg_batch);
+                c.stream = b->stream;
+                c.n = u.ts.size();
+                c.seq_base = m.end();
+                c.key = u.key.data();
+                c.ts = u.ts.data();
+                c.cols = cp.data();
+                c.nulls = anyNull ? np.data() : nullptr;
+                c.n_cols = nc;
+                c.mem = SG_MEM_HOST;
+                const int rc = sg_push_batch(s->sh[r], &c);
+                if (rc == SG_OK) {
+                    pushed[r] = 1;
+                    m.v.insert(m.v.end(), u.glob.begin(), u.glob.end());
+                }
+                return rc;
+            });
+        } catch (...) {
+            for (uint32_t r = 0; r < N; r++)
+                if (pushed[r]) s->failed = true;
+            throw;
+        }
         return SG_OK;
     } catch (const std::exception& ex) {
         return fail_from(ex);
@@ -498,22 +823,61 @@ void collect(ShardEngine* s, bool timers) {
 
 int shd_advance(ShardEngine* s, int64_t now) {
     try {
+        if (s->failed) throw ShardError(SG_ERR_STATE, "a previous call failed part-way: restore a snapshot first");
         if (s->held) throw ShardError(SG_ERR_STATE, "release the polled matches first");
         collect(s, false);   // the batch matches so far come before this advance's timer matches
-        s->each([&](uint32_t r) { return sg_advance_time(s->sh[r], now); });
-        collect(s, true);
+        try {
+            s->each([&](uint32_t r) { return sg_advance_time(s->sh[r], now); });
+            collect(s, true);
+        } catch (...) {
+            s->failed = true;   // some shards may have advanced (and emitted) while another failed
+            throw;
+        }
         return SG_OK;
     } catch (const std::exception& ex) {
         return fail_from(ex);
     }
 }
 
+namespace {
+
+// every shard drained (no pending match on any device): a shard whose seq map has grown past its threshold
+// drops the entries below the smallest seq its live partials reference; the threshold follows the live span
+void trim_maps(ShardEngine* s) {
+    std::vector<char> due(s->N, 0);
+    bool any = false;
+    for (uint32_t r = 0; r < s->N; r++)
+        if (s->gmap[r].v.size() >= s->gmap[r].trim_at) due[r] = any = 1;
+    if (!any) return;
+    std::vector<uint64_t> lo(s->N, 0);
+    s->each([&](uint32_t r) -> int {
+        if (due[r]) lo[r] = sg_internal_min_seq(s->sh[r]);
+        return SG_OK;
+    });
+    for (uint32_t r = 0; r < s->N; r++) {
+        if (!due[r]) continue;
+        SeqMap& m = s->gmap[r];
+        m.trim(std::min(lo[r], m.end()));
+        m.trim_at = std::max<uint64_t>(1u << 20, 2 * m.v.size());
+        s->trims++;
+    }
+}
+
+}  // namespace
+
 int shd_poll(ShardEngine* s, uint32_t mem, sg_match_batch* out) {
     try {
         if ((mem & ~(uint32_t)SG_POLL_READY) != SG_MEM_HOST)
             throw ShardError(SG_ERR_INVALID, "a multi-device engine returns matches in host memory");
+        if (s->failed) throw ShardError(SG_ERR_STATE, "a previous call failed part-way: restore a snapshot first");
         if (s->held) throw ShardError(SG_ERR_STATE, "release the polled matches first");
-        collect(s, false);
+        try {
+            collect(s, false);
+        } catch (...) {
+            s->failed = true;   // shards that released their matches before another failed lost them
+            throw;
+        }
+        trim_maps(s);
         s->out = std::move(s->pend);
         s->pend = ShardEngine::Out();
         const ShardEngine::Out& o = s->out;
@@ -572,6 +936,9 @@ int shd_stats(ShardEngine* s, sg_stats* out) {
             for (size_t i = 0; i < sizeof(sg_stats) / 8; i++) o[i] += ((const uint64_t*)&x)[i];
         // (events / batches: every event reaches exactly one shard, so the sums are the engine's; batches count
         // each shard's sub-batches)
+        out->host_staged_bytes = s->staged_bytes;
+        out->seq_map_entries = 0;
+        for (const SeqMap& m : s->gmap) out->seq_map_entries += m.v.size();
         return SG_OK;
     } catch (const std::exception& ex) {
         return fail_from(ex);
@@ -600,7 +967,7 @@ int shd_reset_keys(ShardEngine* s, const uint32_t* keys, uint64_t n, uint32_t me
     }
 }
 
-// image: magic u64, N u32, pad u32 | per shard: u64 image bytes, u64 map entries, image, map (u64 each)
+// image: magic u64, N u32, pad u32 | per shard: u64 image bytes, u64 map base, u64 map entries, image, map (u64 each)
 int shd_snapshot(ShardEngine* s, void** buf, size_t* len) {
     try {
         if (s->pend.n || s->held) throw ShardError(SG_ERR_STATE, "poll the matches first");
@@ -608,7 +975,7 @@ int shd_snapshot(ShardEngine* s, void** buf, size_t* len) {
         std::vector<size_t> il(s->N, 0);
         s->each([&](uint32_t r) { return sg_snapshot(s->sh[r], &img[r], &il[r]); });
         size_t total = 16;
-        for (uint32_t r = 0; r < s->N; r++) total += 16 + il[r] + 8 * s->gmap[r].size();
+        for (uint32_t r = 0; r < s->N; r++) total += 24 + il[r] + 8 * s->gmap[r].v.size();
         uint8_t* o = (uint8_t*)malloc(total);
         if (!o) throw ShardError(SG_ERR_CAPACITY, "out of host memory");
         size_t off = 0;
@@ -617,10 +984,10 @@ int shd_snapshot(ShardEngine* s, void** buf, size_t* len) {
         put(&kMagic, 8);
         put(hdr, 8);
         for (uint32_t r = 0; r < s->N; r++) {
-            const uint64_t a[2] = {il[r], s->gmap[r].size()};
-            put(a, 16);
+            const uint64_t a[3] = {il[r], s->gmap[r].base, s->gmap[r].v.size()};
+            put(a, 24);
             put(img[r], il[r]);
-            put(s->gmap[r].data(), 8 * s->gmap[r].size());
+            put(s->gmap[r].v.data(), 8 * s->gmap[r].v.size());
             sg_free_buffer(img[r]);
         }
         *buf = o;
@@ -648,23 +1015,27 @@ int shd_restore(ShardEngine* s, const void* buf, size_t len) {
         if (hdr[0] != s->N) throw ShardError(SG_ERR_INVALID, "snapshot of a different shard count");
         std::vector<const uint8_t*> img(s->N);
         std::vector<size_t> il(s->N);
-        std::vector<std::vector<uint64_t>> maps(s->N);
+        std::vector<SeqMap> maps(s->N);
         for (uint32_t r = 0; r < s->N; r++) {
-            need(16);
-            uint64_t a[2];
-            memcpy(a, p + off, 16);
-            off += 16;
+            need(24);
+            uint64_t a[3];
+            memcpy(a, p + off, 24);
+            off += 24;
             need(a[0]);
             img[r] = p + off;
             il[r] = a[0];
             off += a[0];
-            if (a[1] > (len - off) / 8) throw ShardError(SG_ERR_INVALID, "sharded snapshot truncated");
-            maps[r].resize(a[1]);
-            memcpy(maps[r].data(), p + off, 8 * a[1]);
-            off += 8 * a[1];
+            if (a[2] > (len - off) / 8) throw ShardError(SG_ERR_INVALID, "sharded snapshot truncated");
+            maps[r].base = a[1];
+            maps[r].v.resize(a[2]);
+            memcpy(maps[r].v.data(), p + off, 8 * a[2]);
+            maps[r].trim_at = std::max<uint64_t>(1u << 20, 2 * a[2]);
+            off += 8 * a[2];
         }
         s->each([&](uint32_t r) { return sg_restore(s->sh[r], img[r], il[r]); });
         s->gmap = std::move(maps);
+        s->failed = false;
+        s->pend = ShardEngine::Out();
         return SG_OK;
     } catch (const std::exception& ex) {
         return fail_from(ex);
@@ -744,7 +1115,7 @@ int shd_state_import(ShardEngine* s, const void* buf, size_t len) {
                     if (ev.seq < SG_BLANK_SEQ) glob.push_back(ev.seq);
             std::sort(glob.begin(), glob.end());
             glob.erase(std::unique(glob.begin(), glob.end()), glob.end());
-            const uint64_t base = s->gmap[r].size();
+            const uint64_t base = s->gmap[r].end();
             for (SdKey& k : parts[r].keys)
                 for (SdStream& ev : k.streams)
                     if (ev.seq < SG_BLANK_SEQ)
@@ -755,7 +1126,8 @@ int shd_state_import(ShardEngine* s, const void* buf, size_t len) {
             const std::vector<uint8_t> bytes = sd_write(parts[r]);
             return sg_state_import(s->sh[r], bytes.data(), bytes.size());
         });
-        for (uint32_t r = 0; r < s->N; r++) s->gmap[r].insert(s->gmap[r].end(), add[r].begin(), add[r].end());
+        for (uint32_t r = 0; r < s->N; r++) s->gmap[r].v.insert(s->gmap[r].v.end(), add[r].begin(), add[r].end());
+        s->failed = false;
         return SG_OK;
     } catch (const std::exception& ex) {
         return fail_from(ex);
@@ -767,3 +1139,6 @@ int shd_wait_stream(ShardEngine* s, void* stream) {
     (void)stream;
     return sg_set_error(SG_ERR_UNSUPPORTED, "sg_wait_stream: a multi-device engine stages device batches on the host");
 }
+
+sg_engine* shd_first(ShardEngine* s) { return s->sh[0]; }
+uint32_t shd_count(const ShardEngine* s) { return s->N; }

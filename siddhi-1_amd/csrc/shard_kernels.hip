@@ -24,6 +24,7 @@
 #include <cstdint>
 
 #include "../../include/siddhi_gpu.h"
+#include "sg_sharded.h"
 
 namespace {
 
@@ -152,6 +153,109 @@ __global__ void k_sh_totals(const uint32_t* off, const uint32_t* last_counts, ui
     (void)last_counts;
 }
 
+// ---- the multi-device engine's split of a device batch (sg_sharded.cpp): SoA in, SoA out ----
+// The batch stays on the device it was handed over on: every event gets its owner shard (key % world; local
+// key key / world) and its stable rank within the owner (arrival order kept, as k_sh_scatter), and each column
+// is scattered into one destination-major copy of the batch, shard r's events contiguous at [off_r, off_r +
+// count_r).  opos[j] = the batch position of output row j (the shard's local -> global seq map, 4 B per event:
+// the only thing copied to the host besides the per-shard counts).  Keys outside [0, K) set *err (an
+// SG_KEY_NULL with null_keys is dropped instead).
+struct FanArgs {
+    uint64_t n;
+    const uint32_t* key;
+    uint32_t K, world, ntiles, null_keys;
+    uint32_t* counts;   // [world][ntiles] counts, then (scanned) first output row per (shard, tile)
+    uint32_t* pos;      // [n] output row of event i (0xffffffff: dropped)
+    uint32_t* opos;     // [n] batch position of output row j
+    uint32_t* okey;     // [n] local key of output row j
+    uint32_t* err;
+};
+
+__device__ __forceinline__ uint32_t fan_owner(const FanArgs& a, uint64_t e) {
+    if (e >= a.n) return 0xffffffffu;
+    const uint32_t k = a.key[e];
+    if (k < a.K) return k % a.world;
+    if (!(a.null_keys && k == SG_KEY_NULL)) atomicOr(a.err, 1u);
+    return 0xffffffffu;
+}
+
+__global__ void __launch_bounds__(SH_WAVES * 64) k_fan_count(const FanArgs a) {
+    __shared__ uint32_t c[SH_MAX_WORLD];
+    if (threadIdx.x < SH_MAX_WORLD) c[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t base = (uint64_t)blockIdx.x * SH_TILE;
+    for (uint32_t i = threadIdx.x; i < SH_TILE; i += blockDim.x) {
+        const uint32_t d = fan_owner(a, base + i);
+        if (d != 0xffffffffu) atomicAdd(&c[d], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < a.world) a.counts[(size_t)threadIdx.x * a.ntiles + blockIdx.x] = c[threadIdx.x];
+}
+
+__global__ void __launch_bounds__(SH_WAVES * 64) k_fan_rank(const FanArgs a) {
+    __shared__ uint32_t wtot[SH_WAVES][SH_MAX_WORLD];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x / 64;
+    const uint64_t wbase = (uint64_t)blockIdx.x * SH_TILE + (uint64_t)wv * SH_PER_WAVE;
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    uint32_t mine = 0;
+    for (uint32_t r = 0; r < SH_PER_WAVE / 64; ++r) {
+        const uint64_t e = wbase + r * 64 + lane;
+        const uint32_t d = e < a.n ? (a.key[e] < a.K ? a.key[e] % a.world : 0xffffffffu) : 0xffffffffu;
+        for (uint32_t dd = 0; dd < a.world; ++dd) {
+            const uint64_t m = __ballot(d == dd);
+            if (lane == dd) mine += (uint32_t)__popcll(m);
+        }
+    }
+    wtot[wv][lane] = mine;
+    __syncthreads();
+    uint32_t base = 0;
+    if (lane < a.world) {
+        base = a.counts[(size_t)lane * a.ntiles + blockIdx.x];
+        for (uint32_t w2 = 0; w2 < wv; ++w2) base += wtot[w2][lane];
+    }
+    for (uint32_t r = 0; r < SH_PER_WAVE / 64; ++r) {
+        const uint64_t e = wbase + r * 64 + lane;
+        const bool in = e < a.n;
+        const uint32_t k = in ? a.key[e] : 0u;
+        const uint32_t d = (in && k < a.K) ? k % a.world : 0xffffffffu;
+        uint32_t p = 0xffffffffu;
+        for (uint32_t dd = 0; dd < a.world; ++dd) {
+            const uint64_t m = __ballot(d == dd);
+            const uint32_t bdd = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)dd);
+            if (d == dd) p = bdd + (uint32_t)__popcll(m & lt);
+            if (lane == dd) base += (uint32_t)__popcll(m);
+        }
+        if (in) {
+            a.pos[e] = p;
+            if (p != 0xffffffffu) {
+                a.opos[p] = (uint32_t)e;
+                a.okey[p] = k / a.world;
+            }
+        }
+    }
+}
+
+// one column: out[pos[e]] = in[e] (W = 1, 4 or 8 bytes)
+template <typename T>
+__global__ void __launch_bounds__(256) k_fan_col(uint64_t n, const uint32_t* __restrict__ pos, const T* __restrict__ in,
+                                                 T* __restrict__ out) {
+    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n) return;
+    const uint32_t p = pos[e];
+    if (p != 0xffffffffu) out[p] = in[e];
+}
+
+// per-shard totals from the scanned offsets (shard-major): total[d] = off[d + 1][0] - off[d][0]
+__global__ void k_fan_totals(const uint32_t* off, uint32_t world, uint32_t ntiles, const uint32_t* last_cnt,
+                             uint32_t* totals) {
+    const uint32_t d = threadIdx.x;
+    if (d >= world) return;
+    const uint32_t a = off[(size_t)d * ntiles];
+    const uint32_t b = (d + 1 < world) ? off[(size_t)(d + 1) * ntiles]
+                                       : off[(size_t)d * ntiles + ntiles - 1] + last_cnt[(size_t)d * ntiles + ntiles - 1];
+    totals[d] = b - a;
+}
+
 }  // namespace
 
 extern "C" {
@@ -215,6 +319,70 @@ int sg_shard_pack_blocks(uint64_t n, const uint32_t* key, const int64_t* ts, con
     if (cap == 0 || !overflow) return SG_ERR_INVALID;
     return shard_pack(n, key, ts, cols, n_cols, world, cap, rows, dest_counts, overflow, scratch, scratch_len, stream);
 }
+
+}  // extern "C"
+
+// sg_sharded.h: split one device batch by owner shard on the stream's device (all buffers on that device;
+// scratch from fan_split_scratch_bytes).  Queues the work only: totals / opos / err are valid once `stream` is.
+int fan_split(uint64_t n, const uint32_t* key, uint32_t K, uint32_t world, bool null_keys, const int64_t* ts,
+              const void* const* cols, const uint32_t* col_bytes, const uint8_t* const* nulls, uint32_t ncols,
+              int64_t* out_ts, void* const* out_cols, uint8_t* const* out_nulls, uint32_t* opos, uint32_t* okey,
+              uint32_t* totals, uint32_t* err, void* scratch, size_t scratch_len, hipStream_t s) {
+    if (world == 0 || world > SH_MAX_WORLD || n >= (1ull << 32)) return SG_ERR_INVALID;
+    FanArgs a{};
+    a.n = n;
+    a.key = key;
+    a.K = K;
+    a.world = world;
+    a.null_keys = null_keys ? 1u : 0u;
+    a.ntiles = (uint32_t)((n + SH_TILE - 1) / SH_TILE);
+    const size_t ncnt = (size_t)world * a.ntiles;
+    size_t tmp = 0;
+    if (rocprim::exclusive_scan(nullptr, tmp, (uint32_t*)nullptr, (uint32_t*)nullptr, 0u, ncnt,
+                                rocprim::plus<uint32_t>(), s) != hipSuccess)
+        return SG_ERR_DEVICE;
+    const size_t need = 2 * ncnt * 4 + (size_t)n * 4 + tmp + 512;
+    if (!scratch || scratch_len < need) return SG_ERR_CAPACITY;
+    uint32_t* cnt = (uint32_t*)scratch;
+    uint32_t* off = cnt + ncnt;
+    a.pos = off + ncnt;
+    void* stmp = (void*)(((uintptr_t)(a.pos + n) + 255) & ~(uintptr_t)255);
+    a.opos = opos;
+    a.okey = okey;
+    a.err = err;
+    if (hipMemsetAsync(err, 0, 4, s) != hipSuccess) return SG_ERR_DEVICE;
+    a.counts = cnt;
+    hipLaunchKernelGGL(k_fan_count, dim3(a.ntiles), dim3(SH_WAVES * 64), 0, s, a);
+    if (rocprim::exclusive_scan(stmp, tmp, cnt, off, 0u, ncnt, rocprim::plus<uint32_t>(), s) != hipSuccess)
+        return SG_ERR_DEVICE;
+    a.counts = off;
+    hipLaunchKernelGGL(k_fan_rank, dim3(a.ntiles), dim3(SH_WAVES * 64), 0, s, a);
+    hipLaunchKernelGGL(k_fan_totals, dim3(1), dim3(64), 0, s, off, world, a.ntiles, cnt, totals);
+    const dim3 g((unsigned)((n + 255) / 256)), b(256);
+    hipLaunchKernelGGL(k_fan_col<uint64_t>, g, b, 0, s, n, a.pos, (const uint64_t*)ts, (uint64_t*)out_ts);
+    for (uint32_t c = 0; c < ncols; ++c) {
+        if (col_bytes[c] == 8)
+            hipLaunchKernelGGL(k_fan_col<uint64_t>, g, b, 0, s, n, a.pos, (const uint64_t*)cols[c], (uint64_t*)out_cols[c]);
+        else if (col_bytes[c] == 4)
+            hipLaunchKernelGGL(k_fan_col<uint32_t>, g, b, 0, s, n, a.pos, (const uint32_t*)cols[c], (uint32_t*)out_cols[c]);
+        else
+            hipLaunchKernelGGL(k_fan_col<uint8_t>, g, b, 0, s, n, a.pos, (const uint8_t*)cols[c], (uint8_t*)out_cols[c]);
+        if (nulls && nulls[c])
+            hipLaunchKernelGGL(k_fan_col<uint8_t>, g, b, 0, s, n, a.pos, nulls[c], out_nulls[c]);
+    }
+    return hipGetLastError() == hipSuccess ? SG_OK : SG_ERR_DEVICE;
+}
+
+size_t fan_split_scratch_bytes(uint64_t n, uint32_t world) {
+    const uint32_t ntiles = (uint32_t)((n + SH_TILE - 1) / SH_TILE);
+    const size_t ncnt = (size_t)world * ntiles;
+    size_t tmp = 0;
+    (void)rocprim::exclusive_scan(nullptr, tmp, (uint32_t*)nullptr, (uint32_t*)nullptr, 0u, ncnt,
+                                  rocprim::plus<uint32_t>(), (hipStream_t)0);
+    return 2 * ncnt * 4 + (size_t)n * 4 + tmp + 512;
+}
+
+extern "C" {
 
 size_t sg_shard_scratch_bytes(uint64_t n, uint32_t world) {
     const uint32_t ntiles = (uint32_t)((n + SH_TILE - 1) / SH_TILE);

@@ -64,7 +64,8 @@ class sg_stats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in ("events", "batches", "partials_scanned", "partials_created",
                                           "partials_live", "matches", "keys_touched",
                                           "live_at_batch_start", "group_ns", "advance_ns", "order_ns",
-                                          "advance_launches", "window_spills", "advance_hbm_ns")]
+                                          "advance_launches", "window_spills", "advance_hbm_ns",
+                                          "host_staged_bytes", "seq_map_entries")]
 
 
 class sg_projection(C.Structure):
@@ -499,6 +500,17 @@ class NativeEngine:
         s = sg_stats()
         self._check(self._stats(self.h, C.byref(s)))
         return {n: int(getattr(s, n)) for n, _ in sg_stats._fields_}
+
+    def describe(self):
+        """the kernels this engine dispatches per push / advance (sg_engine_describe); None when the library
+        has no such entry (the CPU oracle)"""
+        fn = getattr(self.lib, self.p + "engine_describe", None)
+        if fn is None:
+            return None
+        fn.argtypes = [C.c_void_p, C.c_char_p, C.c_size_t]
+        buf = C.create_string_buffer(1024)
+        self._check(fn(self.h, buf, 1024))
+        return buf.value.decode()
 
     def close(self):
         if getattr(self, "h", None):

@@ -729,10 +729,13 @@ class InputHandler:
             rt._send_rows(self.stream, [int(args[0])], [list(args[1])], True)
             return
         a = args[0]
+        # the data is copied at send time, as the junction copies every sent Event into its own
+        # (StreamJunction.java:196, 220, 242 copyFrom; :266 arraycopy): a caller that reuses or mutates a
+        # data list after send does not change what the engine processes or what a callback reads
         if isinstance(a, Event):
-            rt._send_one(self.stream, a.timestamp, a.data)
+            rt._send_one(self.stream, a.timestamp, tuple(a.data))
         elif isinstance(a, (list, tuple)) and a and isinstance(a[0], Event):
-            rt._send_rows(self.stream, [e.timestamp for e in a], [e.data for e in a], True)
+            rt._send_rows(self.stream, [e.timestamp for e in a], [tuple(e.data) for e in a], True)
         else:
             rt._send_rows(self.stream, [rt.wall_time()], [list(a)], False)
 
@@ -1312,16 +1315,24 @@ class SiddhiAppRuntime:
         up to batch.size.max events, in arrival order; their matches are
         collected by ready polls (the batches still in flight come with a later poll or the drain)"""
         buf, self._abuf, self._abuf_n = self._abuf, [], 0
-        for stream, explicit, ts, rows in buf:
+        for i, (stream, explicit, ts, rows) in enumerate(buf):
             # batches of up to batch.size.max events (the engine's order is by arrival seq, so where a
             # batch ends does not change the matches or their order; the clock is not part of an app
             # that merges)
             cap = self._async[stream].batch
-            if len(ts) <= cap:
-                self._send_now(stream, ts, rows, explicit, True)
-                continue
             for a in range(0, len(ts), cap):
-                self._send_now(stream, ts[a:a + cap], rows[a:a + cap], explicit, True)
+                try:
+                    if a == 0 and len(ts) <= cap:
+                        self._send_now(stream, ts, rows, explicit, True)
+                    else:
+                        self._send_now(stream, ts[a:a + cap], rows[a:a + cap], explicit, True)
+                except BaseException:
+                    # the failing batch is reported; the sends buffered after it stay buffered (in arrival
+                    # order, ahead of any buffered since) for the next flush instead of being dropped
+                    rest = ([[stream, explicit, ts[a + cap:], rows[a + cap:]]] if a + cap < len(ts) else []) + buf[i + 1:]
+                    self._abuf = rest + self._abuf
+                    self._abuf_n = sum(len(x[2]) for x in self._abuf)
+                    raise
 
     @_no_gc
     def _drain(self):

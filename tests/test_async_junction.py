@@ -159,3 +159,33 @@ def test_async_buffer_drained_by_snapshot_and_shutdown():
     rt2.flush()
     assert cb2.calls == ref[n_after_snap:]
     rt2.shutdown()
+
+
+@pytest.mark.parametrize("async_", [False, True])
+def test_send_copies_the_event_data(async_):
+    # the junction copies a sent Event's data (StreamJunction.java:196/220/242 copyFrom, :266 arraycopy):
+    # a caller that reuses one data list for every send gets the matches of the values it sent, and the
+    # callbacks' rows are those values, on synchronous and @async streams alike
+    evs = _events(2000, 29, seed=5)
+    ref, _ = _run(STOCK + Q_C2, [("S", e) for e in evs])
+    head = ASYNC.format(buf=4096, bm=700) if async_ else ""
+    rt = oracle_manager().createSiddhiAppRuntime(head + STOCK + Q_C2)
+    cb = Calls()
+    rt.addCallback("q", cb)
+    rt.start()
+    h = rt.getInputHandler("S")
+    one = sa.Event(0, [None, None, None])
+    for e in evs:                      # one Event object and one data list, overwritten after every send
+        one.data[:] = e.data
+        one.timestamp = e.timestamp
+        h.send(one)
+    one.data[:] = ["ZZ", -1.0, -1]
+    for i in range(0, len(evs), 100):  # Event[] sends whose lists the caller clobbers right after
+        chunk = [sa.Event(e.timestamp + 10_000_000, list(e.data)) for e in evs[i:i + 100]]
+        h.send(chunk)
+        for c in chunk:
+            c.data[1] = -5.0
+    rt.shutdown()
+    shifted = [(t + 10_000_000, [(a + 10_000_000, d) for a, d in rows]) for t, rows in ref]
+    assert len(ref) > 50
+    assert cb.calls == ref + shifted
