@@ -1385,6 +1385,7 @@ static uint32_t sgd_max_key(const uint32_t* k, uint32_t n, bool skip_null) {
 
 int gen_push(GenEngine* e, const sg_batch* b, std::string& msg) {
     const GenProgram& G = e->host;
+    (void)hipGetLastError();   // (a stale error of an unrelated earlier call on this thread: rocPRIM reads it)
     if (b->stream >= (uint32_t)G.nstreams) { msg = "stream index out of range"; return SG_ERR_INVALID; }
     if (b->n_cols != (uint32_t)G.nattr[b->stream]) { msg = "column count does not match the stream"; return SG_ERR_INVALID; }
     if (b->n == 0) return SG_OK;

@@ -744,6 +744,9 @@ static void drain_one(sg_engine* e) {  // wait for the oldest in-flight batch
 
 int push(sg_engine* e, const sg_batch* b) {
     const Plan& pl = e->plan;
+    // rocPRIM reads the thread's last HIP error after its launches: an error some unrelated earlier call left
+    // on this thread (freeing another engine's buffers, say) must not fail this batch
+    (void)hipGetLastError();
     if (b->stream >= e->streams.size()) return fail(SG_ERR_INVALID, "stream index out of range");
     const auto& types = e->streams[b->stream].types;
     if (b->n_cols != types.size()) return fail(SG_ERR_INVALID, "column count does not match the stream");

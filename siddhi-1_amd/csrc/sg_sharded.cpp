@@ -166,12 +166,13 @@ struct ShardEngine {
                 for (void* x : st.cols) if (x) (void)hipFree(x);
                 for (void* x : st.nulls) if (x) (void)hipFree(x);
             }
-            for (void* x : {(void*)p.totals, (void*)p.err}) if (x) (void)hipFree(x);
+            if (p.totals) (void)hipFree(p.totals);   // (err lives in the same allocation)
             if (p.h_totals) (void)hipHostFree(p.h_totals);
             if (p.h_opos) (void)hipHostFree(p.h_opos);
             if (p.stream) (void)hipStreamDestroy(p.stream);
         }
         splits.clear();
+        (void)hipGetLastError();
     }
 
     // matches in host memory, in the single engine's order: `pend` collects them as the shards produce them
@@ -470,14 +471,18 @@ void push_device(ShardEngine* s, const sg_batch* b) {
                 q.next ^= 1u;
                 if (ps->armed) FAN_OK(hipStreamWaitEvent(q.stream, ps->done, 0));
                 FAN_OK(hipStreamWaitEvent(q.stream, split_done, 0));
-                FAN_OK(hipMemcpyPeerAsync(ps->ts, s->dev[r], st.ts + off[r], src, m * 8, q.stream));
-                FAN_OK(hipMemcpyPeerAsync(ps->key, s->dev[r], st.key + off[r], src, m * 4, q.stream));
+                const int dd = s->dev[r];
+                auto cp_part = [&](void* dst, const void* from, size_t bytes) {
+                    if (dd == src) FAN_OK(hipMemcpyAsync(dst, from, bytes, hipMemcpyDeviceToDevice, q.stream));
+                    else FAN_OK(hipMemcpyPeerAsync(dst, dd, from, src, bytes, q.stream));
+                };
+                cp_part(ps->ts, st.ts + off[r], m * 8);
+                cp_part(ps->key, st.key + off[r], m * 4);
                 for (uint32_t c2 = 0; c2 < nc; c2++) {
-                    FAN_OK(hipMemcpyPeerAsync(ps->cols[c2], s->dev[r], (const uint8_t*)st.cols[c2] + off[r] * cb[c2], src,
-                                              m * cb[c2], q.stream));
-                    if (nul[c2])
-                        FAN_OK(hipMemcpyPeerAsync(ps->nulls[c2], s->dev[r], st.nulls[c2] + off[r], src, m, q.stream));
+                    cp_part(ps->cols[c2], (const uint8_t*)st.cols[c2] + off[r] * cb[c2], m * cb[c2]);
+                    if (nul[c2]) cp_part(ps->nulls[c2], st.nulls[c2] + off[r], m);
                 }
+                (void)hipGetLastError();   // (a stale per-thread error would be picked up by the shard's launches)
                 // the split set may be reused once the copies ran
                 FAN_OK(hipEventRecord(st.done[r], q.stream));
                 st.armed[r] = 1;
