@@ -62,3 +62,25 @@ size_t sgd_group_scan_bytes(uint64_t max_entries);
 uint32_t sgd_group_tile_lds(uint64_t n, uint64_t K, uint32_t words);
 // queue the grouping of one batch on `stream` (W = payload words 1..4)
 hipError_t sgd_group_tiles(const GrpArgs& a, const PackSrc& src, int W, hipStream_t stream);
+
+// ---- the bucket split (grp_kernels.hip): after ONE radix pass on the key bits above SGD_BK_BITS, each bucket
+// of 2^SGD_BK_BITS keys is split by key in one workgroup (stable, LDS-staged output) and the per-key bounds are
+// written — replacing the radix sort's last pass and k_seg_bounds ----
+#define SGD_BK_BITS 10
+struct BucketArgs {
+    uint32_t n;           // events in the batch
+    uint32_t K;           // n_keys
+    uint32_t bits;        // key bits the radix pass sorted on (its end bit)
+    uint32_t nb;          // buckets: ceil(K / 2^SGD_BK_BITS)
+    uint32_t drop_null;   // SG_CFG_NULL_KEYS
+    uint32_t stage_bytes; // (set by sgd_bucket_split)
+    const uint32_t* skeys;// [n] keys as the radix pass left them
+    const void* tpay;     // [n] payload as the radix pass left it
+    void* pay;            // [n] key-sorted payload
+    uint32_t* blo;        // [nb + 1] first element of each bucket
+    uint32_t* seg_begin;  // [K]
+    uint32_t* seg_end;    // [K]
+    uint32_t* err;
+};
+// queue the bucket bounds + split of one batch on `stream` (W = payload words 1..4)
+hipError_t sgd_bucket_split(const BucketArgs& a, int W, hipStream_t stream);

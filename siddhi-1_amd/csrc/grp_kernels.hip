@@ -261,6 +261,145 @@ template <int W> hipError_t group_w(const GrpArgs& a, const PackSrc& src, hipStr
     return hipGetLastError();
 }
 
+// ---- the bucket split: the second half of the grouping after one radix pass on the high key bits --------
+// The radix pass (rocPRIM onesweep on bits [SGD_BK_BITS, bits)) leaves the batch stably grouped by bucket =
+// key >> SGD_BK_BITS (1024 keys).  One workgroup per bucket then splits it by key in three phases, with the
+// 16 waves each owning a contiguous eighth... sixteenth of the bucket (arrival order):
+//   count   each wave's events per key (LDS atomics: counts are order-free)
+//   scan    per key its range in the bucket (seg_begin / seg_end written here: no k_seg_bounds) and each
+//           wave's first position in it
+//   place   in passes over key windows whose output fits the LDS stage: every wave re-walks its events in
+//           order, ranks each of the window's events among its wave peers of the same key (ballots, a
+//           running offset per (wave, key): stable), stores it into the stage; the stage goes out as one
+//           contiguous, coalesced range.  A window too large for the stage (hot keys) is placed directly.
+#define BK_WAVES 16
+#define BK_STAGE_BYTES (88u * 1024u)   // beside 68 KB of counters and key starts (160 KB per CU)
+__global__ void __launch_bounds__(256) k_bucket_bounds(const uint32_t* __restrict__ skeys, uint32_t n, uint32_t bits,
+                                                       uint32_t nb, uint32_t K, uint32_t drop_null,
+                                                       uint32_t* __restrict__ blo, uint32_t* __restrict__ err) {
+    // blo[b] = first element of bucket b (b in [0, nb]); skeys sorted by (key & (2^bits - 1)) >> SGD_BK_BITS.
+    // Elements past the last bucket are dropped null keys or out-of-range ids (reported here: no split sees them)
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > n) return;
+    const uint32_t m = bits >= 32 ? 0xffffffffu : ((1u << bits) - 1u);
+    const uint32_t ki = i < n ? skeys[i] : 0u;
+    const uint32_t cur = i < n ? min((ki & m) >> SGD_BK_BITS, nb) : nb;
+    if (i < n && cur == nb && ki >= K && !(drop_null && ki == 0xffffffffu)) atomicOr(err, (uint32_t)SGD_ERR_KEY_RANGE);
+    const uint32_t prv = i > 0 ? min((skeys[i - 1] & m) >> SGD_BK_BITS, nb) : 0u;
+    if (i == 0) {
+        for (uint32_t b = 0; b <= cur; ++b) blo[b] = 0;
+    } else if (cur != prv) {
+        for (uint32_t b = prv + 1; b <= cur; ++b) blo[b] = i;
+    }
+    if (i == n && n > 0)
+        for (uint32_t b = cur + 1; b <= nb; ++b) blo[b] = n;  // (cur == nb here)
+}
+
+template <int W> __global__ void __launch_bounds__(BK_WAVES * 64) k_bucket_split(const BucketArgs a) {
+    __shared__ uint32_t cnt[BK_WAVES][1u << SGD_BK_BITS];  // counts, then each wave's running offset per key
+    __shared__ uint32_t wsum[BK_WAVES];
+    __shared__ uint32_t kstart[(1u << SGD_BK_BITS) + 1];
+    extern __shared__ uint32_t bk_stage[];
+    constexpr uint32_t KB = 1u << SGD_BK_BITS;
+    constexpr uint32_t SW = sizeof(Pay<W>) / 4;  // words per element
+    const uint32_t b = blockIdx.x;
+    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63, x = threadIdx.x;
+    const uint32_t lo = a.blo[b], hi = a.blo[b + 1];
+    const uint32_t n = hi - lo;
+    const uint32_t m = a.bits >= 32 ? 0xffffffffu : ((1u << a.bits) - 1u);
+    const uint32_t k0 = b * KB;  // first key of the bucket
+    for (uint32_t q = x; q < BK_WAVES * KB; q += BK_WAVES * 64) (&cnt[0][0])[q] = 0;
+    __syncthreads();
+    // wave w: events [lo + w*qn, lo + (w+1)*qn) of the bucket (qn a multiple of 64)
+    const uint32_t qn = ((n + BK_WAVES - 1) / BK_WAVES + 63u) & ~63u;
+    const uint32_t wlo = min(n, w * qn), whi = min(n, wlo + qn);
+    bool bad = false;
+    for (uint32_t j = wlo + lane; j < whi; j += 64) {
+        const uint32_t key = a.skeys[lo + j];
+        if (key < a.K && (key & m) >= k0 && (key & m) < k0 + KB) atomicAdd(&cnt[w][key - k0], 1u);
+        else if (!(a.drop_null && key == 0xffffffffu)) bad = true;
+    }
+    if (__ballot(bad) && lane == 0) atomicOr(a.err, (uint32_t)SGD_ERR_KEY_RANGE);
+    __syncthreads();
+    // scan: thread x = key k0 + x
+    uint32_t c[BK_WAVES], tot = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < BK_WAVES; ++q) { c[q] = cnt[q][x]; tot += c[q]; }
+    const uint32_t incl = wave_scan(tot, lane);
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    uint32_t run = incl - tot;
+    for (uint32_t q = 0; q < w; ++q) run += wsum[q];
+    kstart[x] = run;
+    if (x == KB - 1) kstart[KB] = run + tot;
+    if (k0 + x < a.K) {
+        a.seg_begin[k0 + x] = lo + run;
+        a.seg_end[k0 + x] = lo + run + tot;
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < BK_WAVES; ++q) { cnt[q][x] = run; run += c[q]; }
+    __syncthreads();
+    // place, window by window of keys
+    const uint32_t cap = a.stage_bytes / (SW * 4);   // elements the stage holds
+    const Pay<W>* in = (const Pay<W>*)a.tpay + lo;
+    uint32_t* out = (uint32_t*)((Pay<W>*)a.pay + lo);
+    for (uint32_t p0 = 0; p0 < KB;) {
+        // the window: as many keys from p0 as fit the stage (at least one); wave-uniform (LDS reads)
+        uint32_t p1 = p0 + 1;
+        for (uint32_t step = KB / 2; step >= 1; step >>= 1)
+            if (p1 + step <= KB && kstart[p1 + step] - kstart[p0] <= cap) p1 += step;
+        const uint32_t s0 = kstart[p0], s1 = kstart[p1];
+        const bool staged = s1 - s0 <= cap;
+        for (uint32_t j0 = wlo; j0 < whi; j0 += 64) {   // wave-uniform trips
+            const uint32_t j = j0 + lane;
+            const bool v = j < whi;
+            const uint32_t key = v ? a.skeys[lo + j] : 0xffffffffu;
+            const uint32_t sub = key - k0;
+            const bool sel = v && key < a.K && sub >= p0 && sub < p1;
+            const uint64_t act = __ballot(sel);
+            if (!act) continue;
+            const uint64_t mm = match_any<SGD_BK_BITS>(sub, act);
+            if (sel) {
+                const uint32_t before = lane_rank(mm);
+                const uint32_t base = cnt[w][sub];
+                if (before == 0) cnt[w][sub] = base + (uint32_t)__popcll(mm);
+                const uint32_t d = base + before;   // position in the bucket
+                const uint32_t* src = (const uint32_t*)(in + j);
+                uint32_t el[SW];
+#pragma unroll
+                for (uint32_t q = 0; q < SW; ++q) el[q] = src[q];
+                if (staged) {
+#pragma unroll
+                    for (uint32_t q = 0; q < SW; ++q) bk_stage[(d - s0) * SW + q] = el[q];
+                } else {
+#pragma unroll
+                    for (uint32_t q = 0; q < SW; ++q) out[(size_t)d * SW + q] = el[q];
+                }
+            }
+        }
+        __syncthreads();
+        if (staged) {   // the window's output range, coalesced
+            const uint32_t nw = (s1 - s0) * SW;
+            uint32_t* o = out + (size_t)s0 * SW;
+            for (uint32_t q = x; q < nw; q += BK_WAVES * 64) o[q] = bk_stage[q];
+            __syncthreads();
+        }
+        p0 = p1;
+    }
+}
+
+template <int W> hipError_t bucket_w(const BucketArgs& a, hipStream_t stream) {
+    static bool attrs = [] {
+        (void)hipFuncSetAttribute((const void*)k_bucket_split<W>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  BK_STAGE_BYTES);
+        (void)hipGetLastError();
+        return true;
+    }();
+    (void)attrs;
+    hipLaunchKernelGGL(k_bucket_split<W>, dim3(a.nb), dim3(BK_WAVES * 64), a.stage_bytes, stream, a);
+    return hipGetLastError();
+}
+
 }  // namespace
 
 size_t sgd_group_scan_bytes(uint64_t max_entries) {
@@ -294,5 +433,19 @@ hipError_t sgd_group_tiles(const GrpArgs& a, const PackSrc& src, int W, hipStrea
     case 2: return group_w<2>(a, src, stream);
     case 3: return group_w<3>(a, src, stream);
     default: return group_w<4>(a, src, stream);
+    }
+}
+
+hipError_t sgd_bucket_split(const BucketArgs& a0, int W, hipStream_t stream) {
+    BucketArgs a = a0;
+    a.stage_bytes = BK_STAGE_BYTES;
+    hipLaunchKernelGGL(k_bucket_bounds, dim3((a.n + 1 + 255) / 256), dim3(256), 0, stream, a.skeys, a.n, a.bits, a.nb,
+                       a.K, a.drop_null, a.blo, a.err);
+    if (hipError_t e = hipGetLastError()) return e;
+    switch (W) {
+    case 1: return bucket_w<1>(a, stream);
+    case 2: return bucket_w<2>(a, stream);
+    case 3: return bucket_w<3>(a, stream);
+    default: return bucket_w<4>(a, stream);
     }
 }

@@ -60,7 +60,9 @@ template <int W> struct PackFn {
     }
 };
 
-// the key-sorted payload grouping (sg_engine.hip): radix sort of the key ids carrying Pay<W> (W = 1..4)
-// gathered from the SoA columns by PackFn in the first pass; tmp == nullptr queries tmp_bytes
+// the key-sorted payload grouping (sg_engine.hip): radix sort of the key ids on bits [b0, bits) carrying Pay<W>
+// (W = 1..4) gathered from the SoA columns by PackFn in the first pass; tmp == nullptr queries tmp_bytes.
+// b0 = SGD_BK_BITS: one pass on the bucket bits only, the split inside each bucket is sgd_bucket_split's
 hipError_t sgd_sort_payload(int W, void* tmp, size_t& tmp_bytes, const uint32_t* keys, uint32_t* skeys,
-                            const PackSrc& src, void* out, uint32_t n, uint32_t bits, hipStream_t stream);
+                            const PackSrc& src, void* out, uint32_t n, uint32_t bits, hipStream_t stream,
+                            uint32_t b0 = 0);

@@ -127,28 +127,29 @@ using PayWideConfig = rocprim::radix_sort_config<
 
 template <int W>
 hipError_t sort_payload(void* tmp, size_t& tmp_bytes, const uint32_t* keys, uint32_t* skeys, const PackSrc& src,
-                        void* out, uint32_t n, uint32_t bits, hipStream_t stream) {
+                        void* out, uint32_t n, uint32_t b0, uint32_t bits, hipStream_t stream) {
     auto it = rocprim::make_transform_iterator(rocprim::counting_iterator<uint32_t>(0), PackFn<W>{src});
+    const uint32_t nbits = bits - b0;
     if constexpr (W == 1) {
-        if (bits > 16 && bits <= 20)
-            return rocprim::radix_sort_pairs<Pay16Config>(tmp, tmp_bytes, keys, skeys, it, (Pay<W>*)out, n, 0u, bits,
+        if ((nbits > 16 && nbits <= 20) || (b0 > 0 && nbits <= 10))
+            return rocprim::radix_sort_pairs<Pay16Config>(tmp, tmp_bytes, keys, skeys, it, (Pay<W>*)out, n, b0, bits,
                                                            stream);
     } else {
-        if (bits > 10 && bits <= 20)
-            return rocprim::radix_sort_pairs<PayWideConfig>(tmp, tmp_bytes, keys, skeys, it, (Pay<W>*)out, n, 0u, bits,
+        if (nbits <= 20 && (nbits > 10 || b0 > 0))
+            return rocprim::radix_sort_pairs<PayWideConfig>(tmp, tmp_bytes, keys, skeys, it, (Pay<W>*)out, n, b0, bits,
                                                              stream);
     }
-    return rocprim::radix_sort_pairs(tmp, tmp_bytes, keys, skeys, it, (Pay<W>*)out, n, 0u, bits, stream);
+    return rocprim::radix_sort_pairs(tmp, tmp_bytes, keys, skeys, it, (Pay<W>*)out, n, b0, bits, stream);
 }
 
 
 hipError_t sgd_sort_payload(int W, void* tmp, size_t& tmp_bytes, const uint32_t* keys, uint32_t* skeys,
-                          const PackSrc& src, void* out, uint32_t n, uint32_t bits, hipStream_t stream) {
+                          const PackSrc& src, void* out, uint32_t n, uint32_t bits, hipStream_t stream, uint32_t b0) {
     switch (W) {
-    case 1: return sort_payload<1>(tmp, tmp_bytes, keys, skeys, src, out, n, bits, stream);
-    case 2: return sort_payload<2>(tmp, tmp_bytes, keys, skeys, src, out, n, bits, stream);
-    case 3: return sort_payload<3>(tmp, tmp_bytes, keys, skeys, src, out, n, bits, stream);
-    default: return sort_payload<4>(tmp, tmp_bytes, keys, skeys, src, out, n, bits, stream);
+    case 1: return sort_payload<1>(tmp, tmp_bytes, keys, skeys, src, out, n, b0, bits, stream);
+    case 2: return sort_payload<2>(tmp, tmp_bytes, keys, skeys, src, out, n, b0, bits, stream);
+    case 3: return sort_payload<3>(tmp, tmp_bytes, keys, skeys, src, out, n, b0, bits, stream);
+    default: return sort_payload<4>(tmp, tmp_bytes, keys, skeys, src, out, n, b0, bits, stream);
     }
 }
 
@@ -222,6 +223,11 @@ struct sg_engine {
     void* g_tpay = nullptr;
     void* g_scan_tmp = nullptr;
     size_t g_scan_tmp_bytes = 0;
+    // bucket grouping (grp_kernels.hip sgd_bucket_split, the default when the keys take more than SGD_BK_BITS
+    // bits): one radix pass on the bucket bits into bk_tpay, then the per-bucket split; shared by the slots
+    bool bucket_grp = false;
+    void* bk_tpay = nullptr;
+    uint32_t* bk_blo = nullptr;
     uint32_t pay_words = 0;
     // per pushed batch, after its ordering: the {match count, error word} status block copied to pinned
     // host memory and an event, so a poll finds the completed batches without waiting for the others
@@ -576,10 +582,13 @@ void allocate(sg_engine* e) {
     for (int W = 1; W <= 4; ++W) {
         size_t tb = 0;
         PackSrc ps{};
-        for (uint32_t bits : {20u, 32u}) {
-            HIP_OK(sgd_sort_payload(W, nullptr, tb, e->slots[0].b_key, e->slots[0].skeys, ps, nullptr, (uint32_t)B, bits,
-                                  e->stream));
-            e->sort_tmp_bytes = std::max(e->sort_tmp_bytes, tb);
+        for (uint32_t bits : {20u, 32u, e->sort_bits}) {
+            for (uint32_t b0 : {0u, (uint32_t)SGD_BK_BITS}) {
+                if (b0 >= bits) continue;
+                HIP_OK(sgd_sort_payload(W, nullptr, tb, e->slots[0].b_key, e->slots[0].skeys, ps, nullptr, (uint32_t)B,
+                                        bits, e->stream, b0));
+                e->sort_tmp_bytes = std::max(e->sort_tmp_bytes, tb);
+            }
         }
     }
     e->sort_tmp = dalloc<uint8_t>(e->sort_tmp_bytes, o);
@@ -593,6 +602,14 @@ void allocate(sg_engine* e) {
         e->pay_words = maxw;
         for (auto& sl : e->slots)  // + one 16-B chunk: the LDS copy rounds up
             sl.pay = dalloc<uint32_t>((size_t)maxw * B + 4, o);
+        // the bucket grouping is opt-in (SG_BUCKET_GROUP=1): measured slower than the two-pass radix sort on C2
+        // (0.73 vs 0.51 ms, DESIGN §4: rocPRIM's one-pass iterator sort adds a copy of its odd pass, and the split
+        // of a 1024-key bucket cannot stage its 196 KB in LDS)
+        e->bucket_grp = e->plan.partitioned && e->sort_bits > SGD_BK_BITS && getenv("SG_BUCKET_GROUP");
+        if (e->bucket_grp) {
+            e->bk_tpay = dalloc<uint32_t>((size_t)maxw * B + 4, o);
+            e->bk_blo = dalloc<uint32_t>(((K + (1u << SGD_BK_BITS) - 1) >> SGD_BK_BITS) + 1, o);
+        }
         // the tile grouping is opt-in (SG_GROUP_TILES=1): measured slower than the radix sort on C2
         e->tile_grp = e->plan.partitioned && sgd_group_tiles_ok(K, B, 1) && getenv("SG_GROUP_TILES");
         if (e->tile_grp) {
@@ -901,6 +918,27 @@ int push(sg_engine* e, const sg_batch* b) {
                 ga.scan_tmp = e->g_scan_tmp;
                 ga.scan_tmp_bytes = e->g_scan_tmp_bytes;
                 HIP_OK(sgd_group_tiles(ga, ps, (int)wi, gs));
+                goto grouped;
+            }
+            if (e->bucket_grp) {
+                // one radix pass on the bucket bits, then each bucket of 2^SGD_BK_BITS keys split by key in LDS
+                // (stable), the per-key bounds written by the split
+                HIP_OK(sgd_sort_payload((int)wi, e->sort_tmp, tmp, keys, sl.skeys, ps, e->bk_tpay, n, e->sort_bits, gs,
+                                        SGD_BK_BITS));
+                BucketArgs ba{};
+                ba.n = n;
+                ba.K = e->K;
+                ba.bits = e->sort_bits;
+                ba.nb = (e->K + (1u << SGD_BK_BITS) - 1) >> SGD_BK_BITS;
+                ba.drop_null = e->null_keys ? 1u : 0u;
+                ba.skeys = sl.skeys;
+                ba.tpay = e->bk_tpay;
+                ba.pay = sl.pay;
+                ba.blo = e->bk_blo;
+                ba.seg_begin = sl.seg_begin;
+                ba.seg_end = sl.seg_end;
+                ba.err = e->err;
+                HIP_OK(sgd_bucket_split(ba, (int)wi, gs));
                 goto grouped;
             }
             HIP_OK(sgd_sort_payload((int)wi, e->sort_tmp, tmp, keys, sl.skeys, ps, sl.pay, n, e->sort_bits, gs));
@@ -1227,6 +1265,7 @@ int set_projection(sg_engine* e, const uint32_t* code, uint32_t words, const uin
             if (maxw > e->pay_words) {
                 e->pay_words = maxw;
                 for (auto& sl : e->slots) sl.pay = dalloc<uint32_t>((size_t)maxw * e->maxb + 4, e->owned);
+                if (e->bucket_grp) e->bk_tpay = dalloc<uint32_t>((size_t)maxw * e->maxb + 4, e->owned);
             }
         }
         const size_t K = e->K, C = e->cap, M = e->mcap;

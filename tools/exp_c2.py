@@ -20,7 +20,7 @@ import torch  # noqa: E402
 sa = importlib.import_module("siddhi-1_amd")
 synth = importlib.import_module("siddhi-1_amd.synth")
 B, K = 1 << 24, 1 << 20
-KNOBS = ("SG_JIT_EXTRA", "SGD_STAGE_CHUNKS", "SGD_REG_SLOTS")
+KNOBS = ("SG_JIT_EXTRA", "SGD_STAGE_CHUNKS", "SGD_REG_SLOTS", "SG_BUCKET_GROUP")
 
 
 def main():
