@@ -116,6 +116,7 @@ template <int NW, bool TM, bool FF = false> struct AbsKey {
             f1 = GF_STARTED;
             return true;     // (canon = false: the zeroed block is written whole)
         }
+        if (w0 & GEN_W0_DEEP) return false;   // (the lists are in the deep store: the wave-per-key kernels take it)
         canon = true;
         f0 = W(ks0 + KS_FLAGS);
         f1 = W(ks1 + KS_FLAGS);
@@ -759,7 +760,14 @@ template <int NW> __device__ void abs_timers(const GenArgs& a) {
             } else {
                 // the listener's collection of (due time, key) from the queue head (the A.10 check)
                 const uint32_t qh = L.W(L.ks1 + KS_QHEAD), ql = L.W(L.ks1 + KS_QLEN);
-                const int64_t h = ql ? L.R64(L.qword(qh < G.Q ? qh : 0u)) : 0;
+                int64_t h = 0;
+                if (ql && (L.W(0) & GEN_W0_DEEP) && a.deep) {   // (the queue in the deep store, normalised)
+                    const gu32* D = gp(a.deep) + (size_t)key * a.deepWords +
+                                    gen_deep_layout(G.L, G.Q, (uint32_t)NW).oQ;
+                    h = (int64_t)((uint64_t)D[0] | ((uint64_t)D[1] << 32));
+                } else if (ql) {
+                    h = L.R64(L.qword(qh < G.Q ? qh : 0u));
+                }
                 const bool due = ql != 0 && h <= a.now;
                 gp(a.t.dpair_key)[di] = due ? abs_ord64(h) : ~0ull;
                 gp(a.t.dpair_i)[di] = due ? li : GEN_PAIR_NONE;

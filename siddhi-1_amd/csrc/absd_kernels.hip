@@ -37,6 +37,10 @@
 #include "sg_engine.h"
 #include "reg_common.h"
 
+#ifndef ABSD_PROF
+#define ABSD_PROF 0
+#endif
+
 namespace {
 
 template <int NW> struct DEnt {
@@ -44,10 +48,77 @@ template <int NW> struct DEnt {
     uint64_t seq;
     uint32_t nb;
     uint32_t w[NW];
+    // (FF kernels) f1's operands read from the partial's e1, converted to the compare domain once, when the entry
+    // enters the LDS list (not per event and partial); kn bit i = operand i null
+    uint64_t k[2];
+    uint32_t kn;
 };
 
 // one key's absent-tail state, one wave (every member is wave-uniform except where noted)
-template <int NW> struct DeepKey {
+// A decoded compare (GenPre.ff) hoisted out of a scan: its fields as values, each operand's source (0 constant,
+// 1 the event, 2 the partial's e1, 3 null), word offset, width and null bit.  Built once per list scan and kept in
+// registers, so the scan's evaluations read no program word (every read of the constant program inside the scan
+// was a scalar load the wave waited on: a few thousand cycles per 64 partials)
+struct HoistF {
+    uint32_t op, dom;
+    uint32_t src[2], o[2], wide[2], a[2], from[2], cn[2];
+    uint64_t cb[2];
+};
+__device__ __forceinline__ HoistF hoist_f(const __attribute__((address_space(4))) GenProgram& G, int p, bool isF1,
+                                          int slot0, int slot1) {
+    const auto& P = G.pre[p];
+    HoistF f;
+    f.op = P.ff.op;
+    f.dom = P.ff.dom;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const uint32_t at = P.ff.attr[i] < GEN_MAXA ? P.ff.attr[i] : 0u;
+        const int32_t c = P.ff.chain[i];
+        const int sl = (int)P.ff.slot[i];
+        const int ty = G.attrType[0][at];
+        f.a[i] = at;
+        f.o[i] = G.absOff[at];
+        f.wide[i] = (ty == SG_T_LONG || ty == SG_T_DOUBLE) ? 1u : 0u;
+        f.from[i] = P.ff.from[i];
+        f.cb[i] = P.ff.cbits[i];
+        f.cn[i] = P.ff.cnull[i];
+        if (P.ff.isConst[i]) f.src[i] = 0u;
+        else if (c != 0 && c != -1) f.src[i] = 3u;
+        else if (isF1 ? sl == slot1 : sl == slot0) f.src[i] = 1u;
+        else if (isF1 && sl == slot0) f.src[i] = 2u;
+        else f.src[i] = 3u;
+    }
+    return f;
+}
+template <int NW>
+__device__ __forceinline__ bool hoisted_eval(const HoistF& f, const uint32_t (&ew)[NW], uint32_t enb,
+                                             const uint32_t (&xw)[NW], uint32_t xnb) {
+    GVal v[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        if (f.src[i] == 0u) {
+            v[i] = GVal{f.cb[i], f.cn[i] != 0u};   // (constants are already in the compare domain)
+        } else if (f.src[i] == 3u) {
+            v[i] = jo_cvt(GVal{0, true}, (int)f.from[i], (int)f.dom);
+        } else {
+            const bool e = f.src[i] == 1u;
+            uint32_t lo = 0, hi = 0;
+#pragma unroll
+            for (int q = 0; q < NW; ++q) {
+                const uint32_t w = e ? ew[q] : xw[q];
+                lo = (uint32_t)q == f.o[i] ? w : lo;
+                hi = (uint32_t)q == f.o[i] + 1u ? w : hi;
+            }
+            const uint64_t b = f.wide[i] ? ((uint64_t)lo | ((uint64_t)hi << 32)) : (uint64_t)lo;
+            v[i] = jo_cvt(GVal{b, (((e ? enb : xnb) >> f.a[i]) & 1u) != 0u}, (int)f.from[i], (int)f.dom);
+        }
+    }
+    return jo_compare((int)f.op, (int)f.dom, v[0], v[1]);
+}
+
+// FF: both filters are decoded compares (GenPre.ff): the kernel variant carries no interpreter (its registers and
+// scalar pressure made every evaluation of the kill scan a few thousand cycles of reloaded program words)
+template <int NW, bool FF = false> struct DeepKey {
     const cGenProgram& G;
     const GenArgs& A;
     gu32* S;
@@ -55,11 +126,18 @@ template <int NW> struct DeepKey {
     uint32_t ks0, ks1;
     int slot0, slot1;
     int lane;
-    // the lists in LDS: entries [0, n) in list order, [0, np) pending, [np, n) staged
+    // the lists in LDS: entries [0, n) in list order, [0, np) pending, [np, n) staged; the timer queue in LDS
+    // (a ring of Q entries from qh)
     int64_t* lts;
     uint64_t* lseq;
     uint32_t* lnb;
     uint32_t* lw;    // [NW][C]
+    uint64_t* lk;    // [2][C] (FF) f1's partial-side operands in the compare domain
+    uint32_t* lkn;   // [C]
+    int64_t* lq;     // [Q]
+    uint32_t Q;
+    gu32* D;         // this key's deep-store record (GEN_W0_DEEP), or nullptr (no deep store)
+    GenDeepLayout dl;
     uint32_t n, np;
     bool sbad;
     uint32_t seedPend, seedStg;
@@ -70,6 +148,22 @@ template <int NW> struct DeepKey {
     uint32_t err;
     unsigned long long scanned, created, matches;
     uint32_t rank;   // timer matches of this key's sweep so far
+    HoistF hf0, hf1;   // (FF) the filters, hoisted once per key
+#if ABSD_PROF
+    unsigned long long* pf = nullptr;   // (ABSD_PROF builds) the phase counters of absd_batch
+    uint64_t pt = 0;
+    __device__ __forceinline__ void stamp(int i) {
+        const uint64_t t_ = __builtin_amdgcn_s_memtime();
+        if (pf) pf[i] += t_ - pt;
+        pt = t_;
+    }
+#else
+    __device__ __forceinline__ void stamp(int) {}
+#endif
+    // the program's values the walk reads per event, copied once per key (each read of the constant program is a
+    // scalar load the wave waits on: per event they were ~70 loads of a few hundred cycles each)
+    int64_t within, waiting;
+    bool every;
 
     __device__ DeepKey(const GenArgs& a, uint8_t* smem, uint32_t key)
         : G(*(cGenProgram*)a.G), A(a), S(gp(a.state)), K(a.K), k(key), n(0), np(0), sbad(false), seedPend(0),
@@ -85,6 +179,27 @@ template <int NW> struct DeepKey {
         lseq = (uint64_t*)(smem + 8 * (size_t)C);
         lnb = (uint32_t*)(smem + 16 * (size_t)C);
         lw = (uint32_t*)(smem + 20 * (size_t)C);
+        const size_t kb = ((20 + 4 * (size_t)NW) * C + 7) & ~(size_t)7;
+        lk = (uint64_t*)(smem + kb);
+        lkn = (uint32_t*)(smem + kb + 16 * (size_t)C);
+        lq = (int64_t*)(smem + ((kb + 20 * (size_t)C + 7) & ~(size_t)7));
+        Q = G.Q;
+        dl = gen_deep_layout(G.L, G.Q, (uint32_t)NW);
+        D = a.deep ? gp(a.deep) + (size_t)key * a.deepWords : nullptr;
+        within = G.within;
+        waiting = G.pre[G.absP1].waiting;
+        every = G.absEvery != 0;
+        if constexpr (FF) {
+            hf0 = hoist_f(G, G.absP0, false, slot0, slot1);
+            hf1 = hoist_f(G, G.absP1, true, slot0, slot1);
+        }
+    }
+    __device__ __forceinline__ int64_t D64(uint32_t w_) const {
+        return (int64_t)((uint64_t)D[w_] | ((uint64_t)D[w_ + 1] << 32));
+    }
+    __device__ __forceinline__ void DW64(uint32_t w_, int64_t v) const {
+        D[w_] = (uint32_t)(uint64_t)v;
+        D[w_ + 1] = (uint32_t)((uint64_t)v >> 32);
     }
 
     __device__ __forceinline__ gu32& W(uint32_t w_) const { return S[gen_il(K, k, w_)]; }
@@ -104,6 +219,11 @@ template <int NW> struct DeepKey {
         e.nb = lnb[i];
 #pragma unroll
         for (int q = 0; q < NW; ++q) e.w[q] = lw[(size_t)q * C + i];
+        if constexpr (FF) {
+            e.k[0] = lk[i];
+            e.k[1] = lk[C + i];
+            e.kn = lkn[i];
+        }
     }
     __device__ __forceinline__ void put(uint32_t i, const DEnt<NW>& e) const {
         lts[i] = e.ts;
@@ -111,6 +231,49 @@ template <int NW> struct DeepKey {
         lnb[i] = e.nb;
 #pragma unroll
         for (int q = 0; q < NW; ++q) lw[(size_t)q * C + i] = e.w[q];
+        if constexpr (FF) {
+            lk[i] = e.k[0];
+            lk[C + i] = e.k[1];
+            lkn[i] = e.kn;
+        }
+    }
+    // (FF) f1's partial-side operands of entry x, converted to the compare domain
+    __device__ __forceinline__ void keys(const HoistF& h, DEnt<NW>& x) const {
+        x.kn = 0;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            x.k[i] = 0;
+            if (h.src[i] == 2u) {
+                uint32_t lo = 0, hi = 0;
+#pragma unroll
+                for (int q = 0; q < NW; ++q) {
+                    lo = (uint32_t)q == h.o[i] ? x.w[q] : lo;
+                    hi = (uint32_t)q == h.o[i] + 1u ? x.w[q] : hi;
+                }
+                const uint64_t b = h.wide[i] ? ((uint64_t)lo | ((uint64_t)hi << 32)) : (uint64_t)lo;
+                const GVal v = jo_cvt(GVal{b, ((x.nb >> h.a[i]) & 1u) != 0u}, (int)h.from[i], (int)h.dom);
+                x.k[i] = v.b;
+                x.kn |= (v.null ? 1u : 0u) << i;
+            }
+        }
+    }
+    // (FF) f1's operand i when it does not come from the partial (a constant, the event, null): once per event
+    __device__ __forceinline__ GVal evOperand(const HoistF& h, int i, const AbsEv<NW>& ev) const {
+        if (h.src[i] == 0u) return GVal{h.cb[i], h.cn[i] != 0u};
+        if (h.src[i] != 1u) return jo_cvt(GVal{0, true}, (int)h.from[i], (int)h.dom);
+        uint32_t lo = 0, hi = 0;
+#pragma unroll
+        for (int q = 0; q < NW; ++q) {
+            lo = (uint32_t)q == h.o[i] ? ev.w[q] : lo;
+            hi = (uint32_t)q == h.o[i] + 1u ? ev.w[q] : hi;
+        }
+        const uint64_t b = h.wide[i] ? ((uint64_t)lo | ((uint64_t)hi << 32)) : (uint64_t)lo;
+        return jo_cvt(GVal{b, ((ev.nb >> h.a[i]) & 1u) != 0u}, (int)h.from[i], (int)h.dom);
+    }
+    __device__ __forceinline__ bool killTest(const HoistF& h, const GVal& e0, const GVal& e1, const DEnt<NW>& x) const {
+        const GVal l = h.src[0] == 2u ? GVal{x.k[0], (x.kn & 1u) != 0u} : e0;
+        const GVal r = h.src[1] == 2u ? GVal{x.k[1], (x.kn & 2u) != 0u} : e1;
+        return jo_compare((int)h.op, (int)h.dom, l, r);
     }
 
     // ---- load: false = not this kernel's shape (the general kernels take the key)
@@ -141,49 +304,148 @@ template <int NW> struct DeepKey {
         const uint32_t ns = W(ks1 + KS_NLEN);
         if (np > G.L || ns > G.L || np + ns > C) return false;
         n = np + ns;
+        lst = R64(ks1 + KS_LST);
+        const uint32_t qh0 = W(ks1 + KS_QHEAD);
+        ql = W(ks1 + KS_QLEN);
+        if (qh0 >= Q || ql > Q) return false;
+        qh = 0;   // (the LDS ring starts normalised)
         bool ok = true, bad = false;
-        for (uint32_t c = 0; c < n; c += 64) {
-            const uint32_t i = c + (uint32_t)lane;
-            if (i < n) {
-                const uint32_t st = W(ks1 + KS_LISTS + (i < np ? i : G.L + i - np));
-                ok = ok && st < G.STCAP;
-                const uint32_t b = G.offST + (st < G.STCAP ? st : 0u) * G.stWords;
-                const uint32_t e = W(b + ST_SLOTS + (uint32_t)slot0);
-                ok = ok && W(b + ST_TYPE) == 0u && W(b + ST_RC) == 1u && e < G.SECAP &&
-                     W(b + ST_SLOTS + (uint32_t)slot1) == GEN_NIL;
-                const uint32_t eb = G.offSE + (e < G.SECAP ? e : 0u) * G.seWords;
-                const int64_t t = R64(b + ST_TS);
-                ok = ok && W(eb + SE_NEXT) == GEN_NIL && W(eb + SE_RC) == 1u && R64(eb + SE_TS) == t;
-                DEnt<NW> x;
-                x.ts = t;
-                x.seq = (uint64_t)R64(eb + SE_SEQ);
-                x.nb = W(eb + SE_NULL);
+        if (W(0) & GEN_W0_DEEP) {
+            // the record: contiguous per field, one coalesced access per 64 entries
+            if (!D) return false;
+            for (uint32_t c = 0; c < n; c += 64) {
+                const uint32_t i = c + (uint32_t)lane;
+                if (i < n) {
+                    DEnt<NW> x;
+                    x.ts = D64(dl.oTs + 2 * i);
+                    x.seq = (uint64_t)D64(dl.oSeq + 2 * i);
+                    x.nb = D[dl.oNb + i];
 #pragma unroll
-                for (int q = 0; q < NW; ++q) x.w[q] = W(eb + G.absWordAt[q]);
-                put(i, x);
+                    for (int q = 0; q < NW; ++q) x.w[q] = D[dl.oW + (uint32_t)q * G.L + i];
+                    put(i, x);
+                }
+            }
+            for (uint32_t c = 0; c < ql; c += 64) {
+                const uint32_t i = c + (uint32_t)lane;
+                if (i < ql) lq[i] = D64(dl.oQ + 2 * i);
+            }
+        } else {
+            for (uint32_t c = 0; c < n; c += 64) {
+                const uint32_t i = c + (uint32_t)lane;
+                if (i < n) {
+                    const uint32_t st = W(ks1 + KS_LISTS + (i < np ? i : G.L + i - np));
+                    ok = ok && st < G.STCAP;
+                    const uint32_t b = G.offST + (st < G.STCAP ? st : 0u) * G.stWords;
+                    const uint32_t e = W(b + ST_SLOTS + (uint32_t)slot0);
+                    ok = ok && W(b + ST_TYPE) == 0u && W(b + ST_RC) == 1u && e < G.SECAP &&
+                         W(b + ST_SLOTS + (uint32_t)slot1) == GEN_NIL;
+                    const uint32_t eb = G.offSE + (e < G.SECAP ? e : 0u) * G.seWords;
+                    const int64_t t = R64(b + ST_TS);
+                    ok = ok && W(eb + SE_NEXT) == GEN_NIL && W(eb + SE_RC) == 1u && R64(eb + SE_TS) == t;
+                    DEnt<NW> x;
+                    x.ts = t;
+                    x.seq = (uint64_t)R64(eb + SE_SEQ);
+                    x.nb = W(eb + SE_NULL);
+#pragma unroll
+                    for (int q = 0; q < NW; ++q) x.w[q] = W(eb + G.absWordAt[q]);
+                    put(i, x);
+                }
+            }
+            for (uint32_t c = 0; c < ql; c += 64) {
+                const uint32_t i = c + (uint32_t)lane;
+                if (i < ql) {
+                    uint32_t pos = qh0 + i;
+                    if (pos >= Q) pos -= Q;
+                    lq[i] = R64(qword(pos));
+                }
             }
         }
-        if (!wany(!ok)) {
+        if (wany(!ok)) return false;
+        __builtin_amdgcn_s_waitcnt(0);
+        __builtin_amdgcn_wave_barrier();
+        if constexpr (FF) {   // the entries' f1 keys (the lists come without them)
+            for (uint32_t c = 0; c < n; c += 64) {
+                const uint32_t i = c + (uint32_t)lane;
+                if (i < n) {
+                    DEnt<NW> x;
+                    get(i, x);
+                    keys(hf1, x);
+                    lk[i] = x.k[0];
+                    lk[C + i] = x.k[1];
+                    lkn[i] = x.kn;
+                }
+            }
             __builtin_amdgcn_s_waitcnt(0);
             __builtin_amdgcn_wave_barrier();
-            // staged partials out of ts order (promotion sorts them)
-            for (uint32_t c = np + 1; c < n; c += 64) {
-                const uint32_t i = c + (uint32_t)lane;
-                if (i < n && ts_before(lts[i], lts[i - 1])) bad = true;
-            }
-            sbad = wany(bad);
-        } else {
-            return false;
         }
-        lst = R64(ks1 + KS_LST);
-        qh = W(ks1 + KS_QHEAD);
-        ql = W(ks1 + KS_QLEN);
-        if (qh >= G.Q || ql > G.Q) return false;
+        // staged partials out of ts order (promotion sorts them)
+        for (uint32_t c = np + 1; c < n; c += 64) {
+            const uint32_t i = c + (uint32_t)lane;
+            if (i < n && ts_before(lts[i], lts[i - 1])) bad = true;
+        }
+        sbad = wany(bad);
         return true;
     }
 
-    // ---- store: the canonical layout (StateEvent 0 = the seed, 1 + j = partial j over StreamEvent j)
+    // the key's header words in the block (flags, the seed, list lengths, lastScheduledTime, queue length):
+    // lane 0; the queue is written normalised (head 0)
+    __device__ void store_header(uint32_t w0) const {
+        if (lane == 0) {
+            W(0) = w0;
+            W(ks0 + KS_FLAGS) = f0;
+            W(ks0 + KS_PLEN) = seedPend;
+            W(ks0 + KS_NLEN) = seedStg;
+            if (seedPend) W(ks0 + KS_LISTS) = 0u;
+            if (seedStg) W(ks0 + KS_LISTS + G.L) = 0u;
+            if (seedPend | seedStg) {
+                const uint32_t b = G.offST;
+                W64(b + ST_TS, seedPend ? seedPendTs : seedStgTs);
+                W(b + ST_TYPE) = 0u;
+                W(b + ST_RC) = 1u;
+                for (int s = 0; s < G.nslots; s++) W(b + ST_SLOTS + (uint32_t)s) = GEN_NIL;
+            }
+            W(ks1 + KS_FLAGS) = f1;
+            W64(ks1 + KS_LST, lst);
+            W(ks1 + KS_QHEAD) = 0u;
+            W(ks1 + KS_QLEN) = ql;
+            W(ks1 + KS_PLEN) = np;
+            W(ks1 + KS_NLEN) = n - np;
+        }
+    }
+
+    // ---- store into the deep-store record (GEN_W0_DEEP): the lists and the queue contiguous, the header in
+    // the block; falls back to the block's canonical layout without a deep store
     __device__ void store() const {
+        if (!D) {
+            store_general();
+            return;
+        }
+        for (uint32_t c = 0; c < n; c += 64) {
+            const uint32_t j = c + (uint32_t)lane;
+            if (j < n) {
+                DEnt<NW> x;
+                get(j, x);
+                DW64(dl.oTs + 2 * j, x.ts);
+                DW64(dl.oSeq + 2 * j, (int64_t)x.seq);
+                D[dl.oNb + j] = x.nb;
+#pragma unroll
+                for (int q = 0; q < NW; ++q) D[dl.oW + (uint32_t)q * G.L + j] = x.w[q];
+            }
+        }
+        for (uint32_t c = 0; c < ql; c += 64) {
+            const uint32_t i = c + (uint32_t)lane;
+            if (i < ql) {
+                uint32_t pos = qh + i;
+                if (pos >= Q) pos -= Q;
+                DW64(dl.oQ + 2 * i, lq[pos]);
+            }
+        }
+        store_header(1u | GEN_W0_DEEP);
+    }
+
+    // ---- store into the block, the canonical layout (StateEvent 0 = the seed, 1 + j = partial j over StreamEvent
+    // j; the queue normalised): what the general kernels and every host reader take
+    __device__ void store_general() const {
         for (uint32_t c = 0; c < n; c += 64) {
             const uint32_t j = c + (uint32_t)lane;
             if (j < n) {
@@ -221,52 +483,35 @@ template <int NW> struct DeepKey {
             if (n > 32 * x) m = (n >= 32 * (x + 1)) ? 0xffffffffu : ((1u << (n - 32 * x)) - 1u);
             W(G.offSEfree + x) = m;
         }
-        if (lane == 0) {
-            W(0) = 1u;
-            W(ks0 + KS_FLAGS) = f0;
-            W(ks0 + KS_PLEN) = seedPend;
-            W(ks0 + KS_NLEN) = seedStg;
-            if (seedPend) W(ks0 + KS_LISTS) = 0u;
-            if (seedStg) W(ks0 + KS_LISTS + G.L) = 0u;
-            if (seedPend | seedStg) {
-                const uint32_t b = G.offST;
-                W64(b + ST_TS, seedPend ? seedPendTs : seedStgTs);
-                W(b + ST_TYPE) = 0u;
-                W(b + ST_RC) = 1u;
-                for (int s = 0; s < G.nslots; s++) W(b + ST_SLOTS + (uint32_t)s) = GEN_NIL;
+        for (uint32_t c = 0; c < ql; c += 64) {
+            const uint32_t i = c + (uint32_t)lane;
+            if (i < ql) {
+                uint32_t pos = qh + i;
+                if (pos >= Q) pos -= Q;
+                W64(qword(i), lq[pos]);
             }
-            W(ks1 + KS_FLAGS) = f1;
-            W64(ks1 + KS_LST, lst);
-            W(ks1 + KS_QHEAD) = qh;
-            W(ks1 + KS_QLEN) = ql;
-            W(ks1 + KS_PLEN) = np;
-            W(ks1 + KS_NLEN) = n - np;
         }
+        store_header(1u);
     }
 
-    // a queue entry (other lanes of this wave may have written it in this walk: every store has completed
-    // (s_waitcnt) and the load goes to L2, bypassing the non-coherent vector L1)
-    __device__ __forceinline__ int64_t qread(uint32_t i) const {
-        __builtin_amdgcn_s_waitcnt(0);
-        const size_t a0 = gen_il(K, k, qword(i)), a1 = gen_il(K, k, qword(i) + 1);
-        const uint32_t lo = __hip_atomic_load((uint32_t*)&S[a0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t hi = __hip_atomic_load((uint32_t*)&S[a1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return (int64_t)((uint64_t)lo | ((uint64_t)hi << 32));
-    }
-    __device__ __forceinline__ int64_t deadline() const { return ql ? qread(qh) : GEN_NO_DEADLINE; }
+    // the timer queue in LDS (lanes append entries; a wave barrier before they are read)
+    __device__ __forceinline__ int64_t qread(uint32_t i) const { return lq[i]; }
+    __device__ __forceinline__ int64_t deadline() const { return ql ? lq[qh] : GEN_NO_DEADLINE; }
 
     // Scheduler.notifyAt under playback, `cnt` times at t (lanes [0, cnt) write one entry each)
     __device__ __forceinline__ void notifyAt(int64_t t, uint32_t cnt) {
-        if (ql + cnt > G.Q) { err |= GERR_CAP; return; }
+        if (ql + cnt > Q) { err |= GERR_CAP; return; }
         for (uint32_t c = 0; c < cnt; c += 64) {
             const uint32_t i = c + (uint32_t)lane;
             if (i < cnt) {
                 uint32_t pos = qh + ql + i;
-                while (pos >= G.Q) pos -= G.Q;
-                W64(qword(pos), t);
+                while (pos >= Q) pos -= Q;
+                lq[pos] = t;
             }
         }
         ql += cnt;
+        __builtin_amdgcn_s_waitcnt(0);
+        __builtin_amdgcn_wave_barrier();
     }
 
     // ---- values for the filters ----
@@ -289,7 +534,8 @@ template <int NW> struct DeepKey {
                                           if ((int)s == slot0 && (c == 0 || c == -1)) return attr(ev.w, ev.nb, a);
                                           return GVal{0, true};
                                       };
-        if (P.ff.on) return jo_fast(P.ff, var_);   // (gen_engine.h JoFast)
+        if constexpr (FF) return jo_fast(P.ff, var_);   // (gen_engine.h JoFast)
+        if (P.ff.on) return jo_fast(P.ff, var_);
         const GVal v = jo_eval<false>(G.code, P.fpc, P.flen, err, var_,
                                       [&](uint32_t s, int32_t c) -> bool { return !((int)s == slot0 && (c == 0 || c == -1)); });
         return !v.null && (v.b & 1);
@@ -303,7 +549,8 @@ template <int NW> struct DeepKey {
                                           if ((int)s == slot0) return attr(x.w, x.nb, a);
                                           return GVal{0, true};
                                       };
-        if (P.ff.on) return jo_fast(P.ff, var_);   // (gen_engine.h JoFast)
+        if constexpr (FF) return jo_fast(P.ff, var_);   // (gen_engine.h JoFast)
+        if (P.ff.on) return jo_fast(P.ff, var_);
         const GVal v = jo_eval<false>(G.code, P.fpc, P.flen, err, var_,
                                       [&](uint32_t s, int32_t c) -> bool {
                                           return !(((int)s == slot0 || (int)s == slot1) && (c == 0 || c == -1));
@@ -366,12 +613,12 @@ template <int NW> struct DeepKey {
 
     __device__ __forceinline__ bool expiredAt(int64_t ts, int64_t now) const {
         const int64_t d = ts - now;
-        return (d < 0 ? -d : d) > G.within;
+        return (d < 0 ? -d : d) > within;
     }
 
     // StreamPreStateProcessor.expireEvents on p1: the expired prefix of pending, any expired staged entry
     __device__ void expire(int64_t now) {
-        if (G.within == -1 || n == 0) return;
+        if (within == -1 || n == 0) return;
         // the first pending entry that survives ends the prefix
         uint32_t f = np;
         for (uint32_t c = 0; c < np; c += 64) {
@@ -393,35 +640,51 @@ template <int NW> struct DeepKey {
 
     // one event of this key (PatternMultiProcessStreamReceiver: stabilize, then p1, then p0)
     __device__ void event(const AbsEv<NW>& ev) {
+        stamp(1);
         expire(ev.ts);
         seedPend += seedStg;
         if (seedStg) seedPendTs = seedStgTs;
         seedStg = 0;
         promote();
+        stamp(2);
         // p1.processAndReturn: every pending partial whose f1 passes dies and reschedules (each kill sets
         // lastScheduledTime = ev.ts + T and notifies at it, AbsentStreamPostStateProcessor.java:36-56)
         scanned += np;
         uint32_t kills = 0;
+        const bool f1any = G.pre[G.absP1].flen != 0;
+        GVal e0{0, true}, e1{0, true};
+        if constexpr (FF) {
+            e0 = evOperand(hf1, 0, ev);
+            e1 = evOperand(hf1, 1, ev);
+        }
         for (uint32_t c = 0; c < np; c += 64) {
             const uint32_t i = c + (uint32_t)lane;
             bool kl = false;
             if (i < np) {
                 DEnt<NW> x;
                 get(i, x);
-                kl = evalF1(ev, x);
+                if constexpr (FF) kl = !f1any || killTest(hf1, e0, e1, x);
+                else kl = evalF1(ev, x);
             }
             kills += (uint32_t)__popcll(__ballot(kl));
         }
         if (kills) {
-            const int64_t t = ev.ts + G.pre[G.absP1].waiting;
+            const int64_t t = ev.ts + waiting;
             lst = t;
             notifyAt(t, kills);
-            compact([&](uint32_t i, const DEnt<NW>& x) { return !(i < np && evalF1(ev, x)); });
+            if constexpr (FF)
+                compact([&](uint32_t i, const DEnt<NW>& x) { return !(i < np && (!f1any || killTest(hf1, e0, e1, x))); });
+            else
+                compact([&](uint32_t i, const DEnt<NW>& x) { return !(i < np && evalF1(ev, x)); });
         }
+        stamp(3);
         // p0.processAndReturn over its seed
         if (seedPend) {
             scanned++;
-            if (evalF0(ev)) {
+            bool f0 = true;
+            if constexpr (FF) f0 = G.pre[G.absP0].flen == 0 || hoisted_eval<NW>(hf0, ev.w, ev.nb, ev.w, ev.nb);
+            else f0 = evalF0(ev);
+            if (f0) {
                 if (lane == 0) {
                     DEnt<NW> x;
                     x.ts = ev.ts;
@@ -429,22 +692,24 @@ template <int NW> struct DeepKey {
                     x.nb = ev.nb;
 #pragma unroll
                     for (int q = 0; q < NW; ++q) x.w[q] = ev.w[q];
+                    if constexpr (FF) keys(hf1, x);
                     put(n, x);
                 }
                 if (n > np && n > 0 && ts_before(ev.ts, lts[n - 1])) sbad = true;
                 __builtin_amdgcn_s_waitcnt(0);
                 __builtin_amdgcn_wave_barrier();
                 n++;
-                lst = ev.ts + G.pre[G.absP1].waiting;
+                lst = ev.ts + waiting;
                 notifyAt(lst, 1u);
                 seedPend = 0;
-                if (G.absEvery) {
+                if (every) {
                     seedStg = 1;
                     seedStgTs = ev.ts;
                     created++;
                 }
             }
         }
+        stamp(4);
     }
 
     // a timer match: a raw record of the general engine (trigger = timer, rank within this key's sweep)
@@ -472,12 +737,11 @@ template <int NW> struct DeepKey {
     // AbsentStreamPreStateProcessor.process for the TIMER event at currentTime = t (the clock is `now`)
     __device__ void timer(int64_t t, int64_t now) {
         promote();
-        const int64_t waiting = G.pre[G.absP1].waiting;
         scanned += np;
         auto due = [&](const DEnt<NW>& x) {
             return (x.ts == -1 && t >= lst) || (x.ts != -1 && t >= x.ts + waiting);
         };
-        auto gone = [&](const DEnt<NW>& x) { return G.within != -1 && expiredAt(x.ts, t); };
+        auto gone = [&](const DEnt<NW>& x) { return within != -1 && expiredAt(x.ts, t); };
         // the emitted partials in list order (sendEvent per partial: slot0 = e1, ts = currentTime)
         uint32_t emits = 0, drops = 0;
         for (uint32_t c = 0; c < np; c += 64) {
@@ -544,9 +808,15 @@ __device__ void absd_stats(const GenArgs& a, unsigned long long sc, unsigned lon
 }
 
 // ---- batch: one wave per handed-over key walks its events from where the register window stopped ----
-template <int NW> __device__ void absd_batch(const GenArgs& a) {
+// ABSD_PROF=1 (experiment builds): shader-clock cycles per phase (load, event fetch, expire + promote, kill scan,
+// seed, store) summed into GenOut.prof slots 0..5, events and loaded entries in 6, 7 (SG_GEN_PROF=1; printed when
+// the engine is destroyed)
+template <int NW, bool FF> __device__ void absd_batch(const GenArgs& a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const cGenProgram& G = *(cGenProgram*)a.G;
+#if ABSD_PROF
+    unsigned long long pf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
     unsigned long long sc = 0, cr = 0, ky = 0, fb = 0;
     uint32_t er = 0;
     const uint64_t nfb = *a.fb_n;
@@ -555,19 +825,54 @@ template <int NW> __device__ void absd_batch(const GenArgs& a) {
         const uint32_t key = __builtin_amdgcn_readfirstlane(gp(a.fb_list)[li]);
         const uint32_t b = __builtin_amdgcn_readfirstlane(gp(a.fb_start)[key]);
         const uint32_t e = __builtin_amdgcn_readfirstlane(gp(a.b.seg_end)[key]);
-        DeepKey<NW> L(a, smem, key);
+        DeepKey<NW, FF> L(a, smem, key);
+#if ABSD_PROF
+        L.pf = pf;
+        L.pt = __builtin_amdgcn_s_memtime();
+#endif
         if (!L.load()) {
             absd_handover(a, key, b);
             fb++;
             continue;
         }
+        L.stamp(0);
+#if ABSD_PROF
+        pf[6] += e - b;
+        pf[7] += L.n;
+#endif
         uint32_t i = b;
+        // the key's events, 64 at a time: lane j loads event i0 + j's payload words (one coalesced load per word),
+        // each event is then read out of the lanes (readlane) instead of a dependent global load per event
+        constexpr int MW = NW + 3;
+        uint32_t pw[MW];
+        const uint32_t st = a.b.payStride;
         for (; i < e; i++) {
             // at most one new partial and n + 1 queue entries per event: stop before an event that could overflow
             if (L.n + 1u > L.C || L.ql + L.n + 1u > G.Q) break;
             AbsEv<NW> ev;
             if (a.b.pay) {
-                abs_pay<NW>(a, i, tbase, ev);
+                const uint32_t j = (i - b) & 63u;
+                if (j == 0u) {
+                    const uint32_t my = i + (uint32_t)(threadIdx.x & 63);
+                    const gu32* pp = gp(a.b.pay) + (size_t)my * st;
+#pragma unroll
+                    for (int q = 0; q < MW; ++q) pw[q] = (my < e && (uint32_t)q < st) ? pp[q] : 0u;
+                }
+                uint32_t x[MW];
+#pragma unroll
+                for (int q = 0; q < MW; ++q) x[q] = (uint32_t)__builtin_amdgcn_readlane((int)pw[q], (int)j);
+                const uint32_t pos = x[0];
+#pragma unroll
+                for (int q = 0; q < NW; ++q) ev.w[q] = x[1 + q];
+                uint32_t toff = 0, nb = 0;
+#pragma unroll
+                for (int q = 1; q < MW; ++q) {
+                    if ((uint32_t)q == st - 1) toff = x[q];
+                    if (a.b.payNull && (uint32_t)q == st - 2) nb = x[q];
+                }
+                ev.nb = nb;
+                ev.ts = (int32_t)toff == SGD_TS_FAR ? gp(a.b.ts)[pos] : tbase + (int64_t)(int32_t)toff;
+                ev.seq = a.b.seq_base + pos;
             } else {
                 const uint32_t pos = a.b.sidx ? gp(a.b.sidx)[i] : i;
                 ev.ts = gp(a.b.ts)[pos];
@@ -576,23 +881,30 @@ template <int NW> __device__ void absd_batch(const GenArgs& a) {
             }
             L.event(ev);
         }
-        L.store();
-        if (i < e) {
+        L.stamp(1);
+        if (i < e) {   // the general kernels continue from event i: the block holds the key's lists again
+            L.store_general();
             absd_handover(a, key, i);
             fb++;
         } else {
+            L.store();
             if ((threadIdx.x & 63) == 0) gp(a.t.nd)[key] = L.deadline();
             ky++;
         }
+        L.stamp(5);
         sc += L.scanned;
         cr += L.created;
         er |= L.err;
     }
+#if ABSD_PROF
+    if ((threadIdx.x & 63) == 0 && a.o.prof)
+        for (int q = 0; q < 8; q++) atomicAdd(&a.o.prof[q], pf[q]);
+#endif
     absd_stats(a, sc, cr, 0ull, ky, er, fb);
 }
 
 // ---- timer sweep: one wave per handed-over due key ----
-template <int NW> __device__ void absd_timers(const GenArgs& a) {
+template <int NW, bool FF> __device__ void absd_timers(const GenArgs& a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const cGenProgram& G = *(cGenProgram*)a.G;
     unsigned long long sc = 0, cr = 0, ma = 0, fb = 0;
@@ -600,7 +912,7 @@ template <int NW> __device__ void absd_timers(const GenArgs& a) {
     const uint64_t nfb = *a.fb_n;
     for (uint64_t li = blockIdx.x; li < nfb; li += gridDim.x) {
         const uint32_t key = __builtin_amdgcn_readfirstlane(gp(a.fb_list)[li]);
-        DeepKey<NW> L(a, smem, key);
+        DeepKey<NW, FF> L(a, smem, key);
         if (!L.load()) {
             absd_handover(a, key, 0u);
             fb++;
@@ -627,15 +939,40 @@ template <int NW> __device__ void absd_timers(const GenArgs& a) {
     absd_stats(a, sc, cr, ma, 0ull, er, fb);
 }
 
+// ---- flush: every key whose lists live in the deep store written back to its block (the canonical layout), for
+// the readers of the blocks (snapshots, state documents, the fan-out's seq-map trim); a fixed grid of one-wave
+// work-groups strides over the keys ----
+template <int NW> __device__ void absd_flush(const GenArgs& a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint32_t er = 0;
+    for (uint32_t key = blockIdx.x; key < a.K; key += gridDim.x) {
+        const uint32_t w0 = __builtin_amdgcn_readfirstlane(gp(a.state)[gen_il(a.K, key, 0)]);
+        if (!(w0 & GEN_W0_DEEP)) continue;
+        DeepKey<NW> L(a, smem, key);
+        if (L.load()) L.store_general();
+        else er |= GERR_REF;   // (a deep record whose header does not validate: never written so)
+    }
+    if ((threadIdx.x & 63) == 0 && er) atomicOr(a.o.err, er);
+}
+
 }  // namespace
 
 // One kernel per captured-word count (NW), one wave per work-group, dynamic LDS = the key's lists.
 #define ABSD_KERNELS(NW)                                                                                            \
     extern "C" __global__ void __launch_bounds__(64) k_absd_batch_##NW(const GenArgs ap) {          \
-        absd_batch<NW>(ap);                                                                                        \
+        absd_batch<NW, false>(ap);                                                                                 \
     }                                                                                                               \
     extern "C" __global__ void __launch_bounds__(64) k_absd_timers_##NW(const GenArgs ap) {         \
-        absd_timers<NW>(ap);                                                                                       \
+        absd_timers<NW, false>(ap);                                                                                \
+    }                                                                                                               \
+    extern "C" __global__ void __launch_bounds__(64) k_absd_batchf_##NW(const GenArgs ap) {         \
+        absd_batch<NW, true>(ap);                                                                                  \
+    }                                                                                                               \
+    extern "C" __global__ void __launch_bounds__(64) k_absd_timersf_##NW(const GenArgs ap) {        \
+        absd_timers<NW, true>(ap);                                                                                 \
+    }                                                                                                               \
+    extern "C" __global__ void __launch_bounds__(64) k_absd_flush_##NW(const GenArgs ap) {          \
+        absd_flush<NW>(ap);                                                                                        \
     }
 ABSD_KERNELS(1)
 ABSD_KERNELS(2)

@@ -53,6 +53,26 @@ __host__ __device__ inline size_t gen_at(uint32_t K, uint32_t blockWords, uint32
 // (type, refcounts, slot links) of pool entries [0, bits 2..7) in place, so its stores skip them (cleared by
 // every other kernel that writes the block)
 #define GEN_W0_POOLC 2u
+// GEN_W0_DEEP: absd_kernels.hip keeps this key's absent-state lists and timer queue in its deep-store record
+// (GenArgs.deep, one contiguous SoA record per key: coalesced for the key's one wave); the block then holds
+// only the header words (flags, seed, list lengths, lastScheduledTime, queue length) and every component that
+// reads the lists from the block flushes the record back first (gen_host.hip gen_flush_deep)
+#define GEN_W0_DEEP 0x100u
+// a deep-store record in 32-bit words: ts[L] i64, seq[L] u64, null bits[L], attribute words[NW][L], queue[Q] i64
+struct GenDeepLayout {
+    uint32_t oTs, oSeq, oNb, oW, oQ, words;
+};
+__host__ __device__ inline GenDeepLayout gen_deep_layout(uint32_t L, uint32_t Q, uint32_t NW) {
+    GenDeepLayout d;
+    d.oTs = 0;
+    d.oSeq = 2 * L;
+    d.oNb = 4 * L;
+    d.oW = 5 * L;
+    d.oQ = (5 + NW) * L;
+    d.oQ += d.oQ & 1u;   // (8-B aligned: records start on even words)
+    d.words = d.oQ + 2 * Q;
+    return d;
+}
 #define ABS_R 8          // abs_kernels.hip: partials a key's register window holds
 #define ABS_MAXNW 8      // abs_kernels.hip: attribute words of an event it captures
 #define CNT_R 8          // cnt_kernels.hip: events a count chain in registers holds (the shape's max count)
@@ -265,6 +285,10 @@ struct GenArgs {
     uint32_t* fb2_list;
     unsigned long long* fb2_n;
     uint32_t* fb2_start;
+    // the deep store (GEN_W0_DEEP), deepWords words per key, or nullptr
+    uint32_t* deep;
+    uint32_t deepWords;
+    uint32_t pad3;
 };
 // GenArgs.mode
 #define GEN_M_KEYLIST 1u   // k_gen_batch: lane i walks key fb_list[i] from fb_start[key]

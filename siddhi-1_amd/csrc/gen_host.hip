@@ -41,7 +41,10 @@ static const AbsKernel kAbsBatchF[ABS_MAXNW + 1] = {nullptr, k_abs_batchf_1, k_a
                                                     k_abs_batchf_4, k_abs_batchf_5, k_abs_batchf_6, k_abs_batchf_7,
                                                     k_abs_batchf_8};
 #define ABSD_DECL(NW) extern "C" __global__ void k_absd_batch_##NW(const GenArgs ap); \
-                      extern "C" __global__ void k_absd_timers_##NW(const GenArgs ap);
+                      extern "C" __global__ void k_absd_timers_##NW(const GenArgs ap); \
+                      extern "C" __global__ void k_absd_batchf_##NW(const GenArgs ap); \
+                      extern "C" __global__ void k_absd_timersf_##NW(const GenArgs ap); \
+                      extern "C" __global__ void k_absd_flush_##NW(const GenArgs ap);
 ABSD_DECL(1) ABSD_DECL(2) ABSD_DECL(3) ABSD_DECL(4) ABSD_DECL(5) ABSD_DECL(6) ABSD_DECL(7) ABSD_DECL(8)
 static const AbsKernel kAbsdBatch[ABS_MAXNW + 1] = {nullptr, k_absd_batch_1, k_absd_batch_2, k_absd_batch_3,
                                                     k_absd_batch_4, k_absd_batch_5, k_absd_batch_6, k_absd_batch_7,
@@ -49,6 +52,15 @@ static const AbsKernel kAbsdBatch[ABS_MAXNW + 1] = {nullptr, k_absd_batch_1, k_a
 static const AbsKernel kAbsdTimers[ABS_MAXNW + 1] = {nullptr, k_absd_timers_1, k_absd_timers_2, k_absd_timers_3,
                                                      k_absd_timers_4, k_absd_timers_5, k_absd_timers_6, k_absd_timers_7,
                                                      k_absd_timers_8};
+static const AbsKernel kAbsdBatchF[ABS_MAXNW + 1] = {nullptr, k_absd_batchf_1, k_absd_batchf_2, k_absd_batchf_3,
+                                                     k_absd_batchf_4, k_absd_batchf_5, k_absd_batchf_6, k_absd_batchf_7,
+                                                     k_absd_batchf_8};
+static const AbsKernel kAbsdTimersF[ABS_MAXNW + 1] = {nullptr, k_absd_timersf_1, k_absd_timersf_2, k_absd_timersf_3,
+                                                      k_absd_timersf_4, k_absd_timersf_5, k_absd_timersf_6,
+                                                      k_absd_timersf_7, k_absd_timersf_8};
+static const AbsKernel kAbsdFlush[ABS_MAXNW + 1] = {nullptr, k_absd_flush_1, k_absd_flush_2, k_absd_flush_3,
+                                                    k_absd_flush_4, k_absd_flush_5, k_absd_flush_6, k_absd_flush_7,
+                                                    k_absd_flush_8};
 #define CNT_DECL(NW) extern "C" __global__ void k_cnt_batch_##NW(const GenArgs ap);
 CNT_DECL(1) CNT_DECL(2) CNT_DECL(3) CNT_DECL(4) CNT_DECL(5) CNT_DECL(6) CNT_DECL(7) CNT_DECL(8)
 static const AbsKernel kCntBatch[ABS_MAXNW + 1] = {nullptr, k_cnt_batch_1, k_cnt_batch_2, k_cnt_batch_3, k_cnt_batch_4,
@@ -774,8 +786,14 @@ __global__ void k_gen_live(const GenProgram* G, const uint32_t* S, uint32_t K, u
     if (k >= K) return;
     if (seg_begin && seg_begin[k] >= seg_end[k]) return;
     unsigned long long live = 0;
+    const bool deep = (S[gen_at(K, G->blockWords, G->offST, k, 0)] & GEN_W0_DEEP) != 0u;
     for (int p = 0; p < G->nprocs; p++) {
         const uint32_t ks = G->offKS + (uint32_t)p * G->ksWords;
+        if (deep && p == G->absP1) {   // (the lists are in the deep store: every entry holds its e1)
+            live += S[gen_at(K, G->blockWords, G->offST, k, ks + KS_PLEN)] +
+                    S[gen_at(K, G->blockWords, G->offST, k, ks + KS_NLEN)];
+            continue;
+        }
         for (int which = 0; which < 2; which++) {
             const uint32_t n = S[gen_at(K, G->blockWords, G->offST, k, ks + KS_PLEN + which)];
             for (uint32_t i = 0; i < n; i++) {
@@ -1045,6 +1063,8 @@ struct GenEngine {
     // keys the register-window kernels (abs_kernels.hip) hand to the general kernels
     uint32_t *fb_list = nullptr, *fb_start = nullptr;
     uint32_t *fb2_list = nullptr, *fb2_start = nullptr;  // the wave-per-key kernels' hand-over (absd_kernels.hip)
+    uint32_t* deep = nullptr;                             // their deep store (GEN_W0_DEEP): deepWords per key
+    uint32_t deepWords = 0;
     unsigned long long* fb2_n = nullptr;
     unsigned long long* fb_n = nullptr;
     uint32_t* pay = nullptr;   // the key-sorted payload of the register-window kernel (pack.h Pay<W>)
@@ -1134,6 +1154,8 @@ struct GenEngine {
         a.t = tm;
         a.now = now;
         a.now0 = now;
+        a.deep = deep;
+        a.deepWords = deepWords;
         return a;
     }
 };
@@ -1259,6 +1281,14 @@ GenEngine* gen_create(const uint32_t* ir, size_t nw, const sg_config& cfg, hipSt
                 e->fb2_list = e->dalloc<uint32_t>(K);
                 e->fb2_start = e->dalloc<uint32_t>(K);
                 e->fb2_n = e->dalloc<unsigned long long>(1);
+                // the deep store: one contiguous record per key (lists + timer queue), so a deep key's one wave
+                // reads and writes its state coalesced instead of one 4-B word per row of the interleaved block
+                // (SG_NO_DEEP: the block only); capped at 64 GB of the HBM
+                const GenDeepLayout dl = gen_deep_layout(G.L, G.Q, G.absNW);
+                if (!getenv("SG_NO_DEEP") && (uint64_t)dl.words * 4 * K <= (64ull << 30)) {
+                    e->deepWords = dl.words;
+                    e->deep = e->dalloc<uint32_t>((size_t)dl.words * K);
+                }
             }
             e->pay = e->dalloc<uint32_t>(B * 6);  // Pay<4>: 6 words
             e->wstats = e->dalloc<unsigned long long>((size_t)((K + 63) / 64) * GST_N);
@@ -1333,11 +1363,21 @@ static bool abs_on(const GenEngine* e) {
 // the wave-per-key kernels of absd_kernels.hip take the keys the register window hands over (their LDS slice:
 // one key's lists, partial_capacity entries of 20 + 4 NW bytes, within 64 KB); SG_NO_ABSD: A/B against the
 // general kernels (same results)
-static size_t absd_lds(const GenEngine* e) { return (size_t)e->host.L * (20u + 4u * e->host.absNW); }
+static size_t absd_lds(const GenEngine* e) {   // the key's lists (+ the f1 keys of the FF kernels), its timer queue
+    const size_t kb = ((size_t)e->host.L * (20u + 4u * e->host.absNW) + 7) & ~(size_t)7;
+    return ((kb + 20 * (size_t)e->host.L + 7) & ~(size_t)7) + 8 * (size_t)e->host.Q;
+}
 static bool absd_on(const GenEngine* e) { return e->fb2_list && absd_lds(e) <= 65536; }
 
 // the register-window kernel of cnt_kernels.hip runs this query (the shape, no device projection)
 static bool cnt_on(const GenEngine* e) { return e->host.cntOk && e->host.projN == 0 && e->fb_list; }
+
+// both filters of the absent-tail shape are decoded compares (GenPre.ff): the kernel variants without the interpreter
+static bool abs_ff(const GenEngine* e) {
+    const GenPre& f0 = e->host.pre[e->host.absP0];
+    const GenPre& f1 = e->host.pre[e->host.absP1];
+    return (f0.flen == 0 || f0.ff.on) && (f1.flen == 0 || f1.ff.on);
+}
 
 static void launch_gen(GenEngine* e, GenArgs a, int which) {
     const uint32_t blocks = (e->K + 63) / 64;
@@ -1350,16 +1390,17 @@ static void launch_gen(GenEngine* e, GenArgs a, int which) {
                            dim3(64), 0, e->stream, ap);
     else if (which == GEN_L_DEADLINES) hipLaunchKernelGGL(k_gen_deadlines, dim3(blocks), dim3(64), 0, e->stream, ap);
     else if (which == GEN_L_ABSD_BATCH || which == GEN_L_ABSD_TIMERS) {
-        // one wave per handed-over key (a fixed grid striding over the list, whose length is on the device)
-        hipLaunchKernelGGL(which == GEN_L_ABSD_BATCH ? kAbsdBatch[e->host.absNW] : kAbsdTimers[e->host.absNW],
-                           dim3(GEN_FB_BLOCKS), dim3(64), (unsigned)absd_lds(e), e->stream, ap);
+        // one wave per handed-over key (a fixed grid striding over the list, whose length is on the device); the
+        // variant without the interpreter when both filters are decoded compares
+        const bool ff = abs_ff(e);
+        const AbsKernel k = which == GEN_L_ABSD_BATCH ? (ff ? kAbsdBatchF : kAbsdBatch)[e->host.absNW]
+                                                       : (ff ? kAbsdTimersF : kAbsdTimers)[e->host.absNW];
+        hipLaunchKernelGGL(k, dim3(GEN_FB_BLOCKS), dim3(64), (unsigned)absd_lds(e), e->stream, ap);
     }
     else if (which == GEN_L_ABS_BATCH || which == GEN_L_ABS_TIMERS || which == GEN_L_CNT_BATCH) {
         // one lane per key / possible due slot (the due count is on the device); then the waves' counter rows
         // (the absent kernel's variant for decoded-compare filters when both of its filters are)
-        const GenPre& f0 = e->host.pre[e->host.absP0];
-        const GenPre& f1 = e->host.pre[e->host.absP1];
-        const bool ff = (f0.flen == 0 || f0.ff.on) && (f1.flen == 0 || f1.ff.on);
+        const bool ff = abs_ff(e);
         hipLaunchKernelGGL(which == GEN_L_ABS_BATCH   ? (ff ? kAbsBatchF[e->host.absNW] : kAbsBatch[e->host.absNW])
                            : which == GEN_L_CNT_BATCH ? kCntBatch[e->host.absNW]
                                                       : kAbsTimers[e->host.absNW],
@@ -1936,7 +1977,10 @@ void gen_stats(GenEngine* e, sg_stats* out) {
     out->partials_live = lv;
 }
 
+void gen_flush_deep(GenEngine* e);
+
 uint64_t gen_min_seq(GenEngine* e) {
+    gen_flush_deep(e);
     if (!e->minseq) e->minseq = e->dalloc<unsigned long long>(1);
     unsigned long long* m = e->minseq;
     unsigned long long h = ~0ull;
@@ -1959,8 +2003,8 @@ std::string gen_describe(const GenEngine* e) {
         push = (ff ? "k_abs_batchf_" : "k_abs_batch_") + nw + " (register window, lane per key)";
         adv = "k_abs_timers_" + nw + " (register window)";
         if (absd_on(e)) {
-            push += " + k_absd_batch_" + nw + " (deep keys, wave per key)";
-            adv += " + k_absd_timers_" + nw + " (deep keys)";
+            push += (ff ? " + k_absd_batchf_" : " + k_absd_batch_") + nw + " (deep keys, wave per key)";
+            adv += (ff ? " + k_absd_timersf_" : " + k_absd_timers_") + nw + " (deep keys)";
         }
         push += " + k_gen_batch (keys handed over)";
         adv += " + k_gen_timers (keys handed over)";
@@ -2012,9 +2056,21 @@ static bool gen_outputs_pending(GenEngine* e) {
     return n != 0;
 }
 
+// every key whose lists live in the deep store (GEN_W0_DEEP) written back to its block: before anything reads
+// the blocks' lists on the host or in a kernel that does not know the deep store
+void gen_flush_deep(GenEngine* e) {
+    if (!e->deep || !absd_on(e)) return;
+    GenArgs a = e->args();
+    const GenArgs& ap = a;
+    hipLaunchKernelGGL(kAbsdFlush[e->host.absNW], dim3(std::min<uint32_t>(e->K, 4096u)), dim3(64),
+                       (unsigned)absd_lds(e), e->stream, ap);
+    GH_OK(hipGetLastError());
+}
+
 int gen_snapshot(GenEngine* e, uint32_t* words, GenClock* clk, std::string& msg) {
     if (e->held) { msg = "release the polled matches before a snapshot"; return SG_ERR_STATE; }
     if (gen_outputs_pending(e)) { msg = "poll the emitted matches before a snapshot"; return SG_ERR_STATE; }
+    gen_flush_deep(e);
     GH_OK(hipMemcpyAsync(words, e->state, gen_state_words(e) * 4, hipMemcpyDeviceToHost, e->stream));
     GH_OK(hipStreamSynchronize(e->stream));
     clk->now = e->now;
