@@ -56,6 +56,24 @@ end;
 # this variant is the same shape with matches, benchmarked beside it
 C3_MIN1_QUERY = C3_QUERY.replace("<2:5>", "<1:5>")
 
+# BASELINE configs[2] names "logical and/or": the C3 shape with the logical AND (e2 and e3 both arrive, in
+# either order, before the sequence moves on; LogicalPreStateProcessor.java:43-202), on the general kernel
+C3_AND_QUERY = C3_MIN1_QUERY.replace(" or e3=", " and e3=")
+
+# a 3-state pattern (a chain past the two-state kernel's shape, StreamPreStateProcessor.java:364-403 per state),
+# on the general kernel
+P3_QUERY = """
+define stream StockStream (symbol string, price float, volume int);
+partition with (symbol of StockStream)
+begin
+  @info(name = 'query1')
+  from every e1=StockStream[price > 20] -> e2=StockStream[price > e1.price] -> e3=StockStream[price > e2.price]
+       within 10 sec
+  select e1.price as p1, e2.price as p2, e3.price as p3
+  insert into OutputStream;
+end;
+"""
+
 # BASELINE configs[3] (C4): absent state with a long within, playback clock (SURVEY §8d)
 C4_QUERY = """
 @app:playback

@@ -150,6 +150,30 @@ def test_c3_at_baseline_size(name):
     assert sg["events"] == 2 * B
 
 
+def _ordered_props(mg, seqs):
+    """every match: trigger seqs in order, the trigger and the first slot's e1 events of the match's key"""
+    if len(mg) == 0:
+        return
+    trig = mg.trigger_seq
+    assert np.all(np.diff(trig.astype(np.int64)) >= 0)
+    ev_t, ev_1 = _lookup(seqs, trig), _lookup(seqs, mg.slot_seq[:, 0, 0])
+    assert np.all(ev_t["key"] == mg.key) and np.all(ev_1["key"] == mg.key)
+    assert np.all(ev_1["price"] > 20)
+    assert np.all(mg.ts == ev_t["ts"])
+
+
+@pytest.mark.parametrize("name", ["C3_and", "P3"])
+def test_general_shapes_at_bench_size(name):
+    """the shapes that stay on the general kernel, benchmarked beside C3 (bench.py
+    other_configs C3_and, P3), at their bench size — 2^20 keys, 2^22-event batches — bit-exact with the oracle on
+    the keys k % 256 == 0"""
+    K, B = 1 << 20, 1 << 22
+    q = synth.C3_AND_QUERY if name == "C3_and" else synth.P3_QUERY
+    total, gpu, ora = _run(q, lambda b: synth.stock_ticks(b * B, B, K), K, B, 2, 32, 256, False, _ordered_props)
+    assert total > 10_000
+    assert gpu.stats()["events"] == 2 * B
+
+
 C4_CASES = {
     # (keys, burst, batch events, partial capacity, subset modulus)
     "C4": (1 << 20, 1, 1 << 22, 16, 256),

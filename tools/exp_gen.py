@@ -23,6 +23,8 @@ which = sys.argv[1:] or ["C3", "C3_min1", "C4", "C4_deep"]
 cfg = {
     "C3": (synth.C3_QUERY, lambda s: synth.stock_ticks(s * cb, cb, K), K, cb, 8, False),
     "C3_min1": (synth.C3_MIN1_QUERY, lambda s: synth.stock_ticks(s * cb, cb, K), K, cb, 8, False),
+    "C3_and": (synth.C3_AND_QUERY, lambda s: synth.stock_ticks(s * cb, cb, K), K, cb, 8, False),
+    "P3": (synth.P3_QUERY, lambda s: synth.stock_ticks(s * cb, cb, K), K, cb, 32, False),
     "C4": (synth.C4_QUERY, lambda s: synth.burst_ticks(s * cb, cb, K, 1), K, cb, 16, True),
     "C4_deep": (synth.C4_QUERY, lambda s: synth.burst_ticks(s * (cb // 16), cb // 16, K // 4, 16), K // 4, cb, 64,
                 True),

@@ -11,7 +11,7 @@ export SG_EXP_STEPS=${SG_EXP_STEPS:-3}
 OUT=${PMC_OUT:-gpurun_out/pmc_gen}
 RX='k_cnt_|k_abs|k_gen_batch|k_gen_timers'
 mkdir -p $OUT
-for cfg in ${PMC_CFGS:-C3 C3_min1 C4 C4_deep C4_deep_state}; do
+for cfg in ${PMC_CFGS:-C3 C3_min1 C3_and P3 C4 C4_deep C4_deep_state}; do
   timeout -s KILL 200 rocprofv3 --kernel-trace --stats -d $OUT/${cfg}_trace -o run --output-format csv \
       -- python3 tools/exp_gen.py $cfg > $OUT/${cfg}_trace.log 2>&1 || { echo "trace $cfg failed"; tail -5 $OUT/${cfg}_trace.log; exit 1; }
   echo "trace $cfg ok"

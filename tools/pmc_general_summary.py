@@ -18,7 +18,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SOURCES = ["abs_kernels.hip", "absd_kernels.hip", "cnt_kernels.hip", "gen_kernels.hip", "gen_host.hip",
            "reg_common.h", "gen_engine.h", "java_ops.h", "pack.h"]
 # the configs' pushed batch size (bench.py other_configs)
-EVENTS = {"C3": 1 << 22, "C3_min1": 1 << 22, "C4": 1 << 22, "C4_deep": 1 << 22, "C4_deep_state": 1 << 16}
+EVENTS = {"C3": 1 << 22, "C3_min1": 1 << 22, "C3_and": 1 << 22, "P3": 1 << 22, "C4": 1 << 22, "C4_deep": 1 << 22, "C4_deep_state": 1 << 16}
 BATCH_KERNELS = ("k_cnt_batch", "k_abs_batch", "k_gen_batch")
 
 
