@@ -139,6 +139,62 @@ def cpu_quota():
     return q
 
 
+def keep_heap():
+    """glibc: freed memory stays in the arenas (no trim), and blocks up to 32 MB come from the arenas instead of
+    one mmap each: the oracle's per-push temporaries then reuse pages instead of faulting fresh ones, and the
+    partition-parallel threads do not serialise on the process's memory-map lock (page faults, munmap)"""
+    try:
+        import ctypes
+        libc = ctypes.CDLL("libc.so.6")
+        libc.mallopt(-1, 1 << 30)          # M_TRIM_THRESHOLD
+        libc.mallopt(-2, 256 << 20)        # M_TOP_PAD
+        libc.mallopt(-3, 32 << 20)         # M_MMAP_THRESHOLD (glibc's maximum)
+    except (OSError, AttributeError):
+        pass
+
+
+def two_phase(T, pins, body):
+    """T persistent threads (thread r pinned to pins[r]) run body(r, 0) untimed, meet at a barrier, then run
+    body(r, 1) timed; returns (timed wall seconds, per-thread busy seconds).  The same thread runs both halves
+    of its shards: glibc gives each thread an arena of its own, and a thread started later can inherit another
+    thread's arena, so a fresh thread per half would free the first half's blocks into arenas other threads
+    allocate from (arena-lock contention, remote NUMA memory) -- the timed half would measure the allocator"""
+    import threading
+    busy, err = [0.0] * T, []
+    ready, go = threading.Barrier(T + 1), threading.Barrier(T + 1)
+
+    def work(r):
+        try:
+            if pins:
+                os.sched_setaffinity(0, {pins[r]})   # (the calling thread)
+            body(r, 0)
+        except BaseException as e:   # noqa: BLE001 (re-raised on the main thread)
+            err.append(e)
+        ready.wait()
+        go.wait()
+        if err:
+            return
+        try:
+            t = time.perf_counter()
+            body(r, 1)
+            busy[r] = time.perf_counter() - t
+        except BaseException as e:   # noqa: BLE001
+            err.append(e)
+
+    th = [threading.Thread(target=work, args=(r,)) for r in range(T)]
+    for x in th:
+        x.start()
+    ready.wait()
+    t0 = time.perf_counter()
+    go.wait()
+    for x in th:
+        x.join()
+    el = time.perf_counter() - t0
+    if err:
+        raise err[0]
+    return el, busy
+
+
 def cpu_baseline(sa, synth, n_keys, batch, seconds):
     """SURVEY §8(d) CPU legs, the CPU oracle (the C++ restatement of the reference engine; the reference
     JVM is not runnable here or on the box) on the host cores of the GPU box:
@@ -150,6 +206,7 @@ def cpu_baseline(sa, synth, n_keys, batch, seconds):
     Each leg is bounded to about `seconds` of CPU work."""
     import threading
     from oracle_backend import build_oracle
+    keep_heap()
     lib = build_oracle()
     app = sa.parse_app(synth.C2_QUERY)
     cq = sa.compile_query(app, app.queries[0], sa.StringDictionary())
@@ -228,29 +285,13 @@ def cpu_baseline(sa, synth, n_keys, batch, seconds):
     th0.start()
     th0.join()
     alone = alone[0]
-    busy = [0.0] * T
+    # thread r owns shards r, r + T, ... in both halves: an engine's memory is allocated and freed by one thread
+    def body(r, half):
+        for sh in range(r, S, T):
+            run_shard(engs[sh] if half else make(sh), shards[sh][half])
 
-    def phase(half):
-        # thread r owns shards r, r + T, ... in both halves: an engine's memory is allocated and freed by
-        # one thread (glibc's per-thread arenas; a free of another arena's block takes that arena's lock)
-        def work(r):
-            if pins:
-                os.sched_setaffinity(0, {pins[r]})   # (the calling thread)
-            t = time.perf_counter()
-            for sh in range(r, S, T):
-                run_shard(engs[sh] if half else make(sh), shards[sh][half])
-            busy[r] = time.perf_counter() - t
-
-        th = [threading.Thread(target=work, args=(r,)) for r in range(T)]
-        t0 = time.perf_counter()
-        for x in th:
-            x.start()
-        for x in th:
-            x.join()
-        return time.perf_counter() - t0
-
-    phase(0)
-    par = timed / phase(1)
+    el, busy = two_phase(T, pins, body)
+    par = timed / el
     for e in engs:
         e.close()
     # (iii) C1: unpartitioned, one key, R = 1 event per ms (10,000 events per 10 s window)
@@ -294,8 +335,8 @@ def cpu_general(sa, query, make_batch, n_keys, batch, warm, playback, seconds, l
       (ii) partition-parallel over the box's CPU share: keys sharded key % 4T, four oracle engines per pinned
            thread, each shard's events of the same batches (the same clock advances), the same untimed /
            timed split; an upper bound for any CPU engine."""
-    import threading
     from oracle_backend import build_oracle
+    keep_heap()
     lib = build_oracle()
     app = sa.parse_app(query)
     cq = sa.compile_query(app, app.queries[0], sa.StringDictionary())
@@ -364,7 +405,6 @@ def cpu_general(sa, query, make_batch, n_keys, batch, warm, playback, seconds, l
                                        (d["key"][idx] // np.uint32(S)).astype(np.uint32)))
     cache.clear()
     engs = [None] * S
-    busy_t = [0.0] * T
 
     def run(e, lst):
         last_adv = None
@@ -378,27 +418,15 @@ def cpu_general(sa, query, make_batch, n_keys, batch, warm, playback, seconds, l
                 e._sg_next += len(ts)
                 e.discard()
 
-    def phase(half):
-        def work(r):
-            if pins:
-                os.sched_setaffinity(0, {pins[r]})
-            t = time.perf_counter()
-            for sh in range(r, S, T):
-                if half == 0:
-                    engs[sh] = sa.NativeEngine(lib, "sgo_", cq.ir, n_keys=(n_keys + S - 1) // S)
-                    engs[sh]._sg_next = 0
-                run(engs[sh], parts[sh][half])
-            busy_t[r] = time.perf_counter() - t
-        th = [threading.Thread(target=work, args=(r,)) for r in range(T)]
-        t0 = time.perf_counter()
-        for x in th:
-            x.start()
-        for x in th:
-            x.join()
-        return time.perf_counter() - t0
+    def body(r, half):
+        for sh in range(r, S, T):
+            if half == 0:
+                engs[sh] = sa.NativeEngine(lib, "sgo_", cq.ir, n_keys=(n_keys + S - 1) // S)
+                engs[sh]._sg_next = 0
+            run(engs[sh], parts[sh][half])
 
-    phase(0)
-    par = n_timed / phase(1)
+    el, busy_t = two_phase(T, pins, body)
+    par = n_timed / el
     for e in engs:
         e.close()
     return {"value": single, "unit": "events/s", "cores": 1, "kind": "port",
