@@ -15,4 +15,3 @@ from .runtime import (Event, InputHandler, QueryCallback, ColumnarQueryCallback,
 from .compiler import compile_query, SiddhiAppCreationException  # noqa: F401
 from .siddhiql import parse_app, SiddhiParserException  # noqa: F401
 from .native import NativeEngine, EngineError, load_hip_library, load_library, jit_check, HIP_LIBRARY  # noqa: F401
-from .sharded import ShardedEngine  # noqa: F401

@@ -1,4 +1,4 @@
-"""Multi-device fan-out over N engines of any backend, in Python.
+"""Test model: the multi-device fan-out over N engines of any backend, in Python.
 
 The product's multi-device path is the C-ABI's own fan-out (sg_config.n_devices, csrc/sg_sharded.cpp: one
 sg_engine handle over one engine per device, what a JNI shim bound to siddhi_gpu.h gets; SiddhiManager(devices=..)
@@ -30,7 +30,11 @@ from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 
-from .native import SG_MEM_HOST, SG_NULL_SEQ, Matches, NativeEngine
+import importlib
+
+_native = importlib.import_module("siddhi-1_amd.native")
+SG_MEM_HOST, SG_NULL_SEQ, Matches, NativeEngine = (_native.SG_MEM_HOST, _native.SG_NULL_SEQ, _native.Matches,
+                                                   _native.NativeEngine)
 
 TIMER_SEQ = np.uint64(0xFFFFFFFFFFFFFFFF)
 BLANK_SEQ = np.uint64(0xFFFFFFFFFFFFFFFE)
@@ -205,7 +209,7 @@ class ShardedEngine:
 
     def state_export(self) -> bytes:
         """one state document over every shard (state_doc.py): keys and event seqs mapped to global ids"""
-        from . import state_doc as sd
+        sd = importlib.import_module("siddhi-1_amd.state_doc")
         docs = [sd.parse(b) for b in self._each(lambda r: self.shards[r].state_export())]
         out = sd.StateDoc(docs[0].n_procs, docs[0].n_slots, docs[0].desc, docs[0].now, docs[0].last_event_ts,
                           max(d.clock_flags for d in docs))
@@ -222,7 +226,7 @@ class ShardedEngine:
 
     def state_import(self, doc: bytes):
         """split a state document by owner shard; its events get fresh local seqs mapped to their global ones"""
-        from . import state_doc as sd
+        sd = importlib.import_module("siddhi-1_amd.state_doc")
         d = sd.parse(doc)
         parts = [sd.StateDoc(d.n_procs, d.n_slots, d.desc, d.now, d.last_event_ts, d.clock_flags) for _ in range(self.N)]
         for k in d.keys:

@@ -1,4 +1,4 @@
-"""ShardedEngine (siddhi-1_amd/sharded.py): one engine per device, keys sharded by key % N, matches merged
+"""ShardedEngine (tests/sharded_model.py, a Python model of csrc/sg_sharded.cpp): one engine per device, keys sharded by key % N, matches merged
 back into the single engine's order.  CPU: N oracle engines against one oracle engine on the same
 streams (two-state, count, SEQUENCE, absent with playback timers, purge, snapshot/restore), bit-exact;
 the same through the runtime API.  The device version is in test_gpu_sharded.py."""
@@ -9,6 +9,7 @@ import pytest
 
 from oracle_backend import build_oracle
 from test_purge import SHAPES as PSHAPES
+from sharded_model import ShardedEngine
 
 sa = importlib.import_module("siddhi-1_amd")
 synth = importlib.import_module("siddhi-1_amd.synth")
@@ -42,7 +43,7 @@ def run_property(shape, lib, prefix, devices, cabi=False):
         if cabi:
             return sa.NativeEngine(lib, prefix, cq.ir, n_keys=K, max_batch=1 << 14, partial_capacity=64,
                                    match_capacity=1 << 20, devices=devices)
-        return sa.ShardedEngine(lib, prefix, cq.ir, n_keys=K, devices=devices, max_batch=1 << 14,
+        return ShardedEngine(lib, prefix, cq.ir, n_keys=K, devices=devices, max_batch=1 << 14,
                                 partial_capacity=64, match_capacity=1 << 20)
     shd = mk_sharded()
     playback = "playback" in SHAPES[shape]
@@ -107,5 +108,5 @@ def test_sharded_runtime_api():
         return got
 
     single = run(lambda ir, nk: sa.NativeEngine(lib, "sgo_", ir, n_keys=nk, max_batch=64))
-    sharded = run(lambda ir, nk: sa.ShardedEngine(lib, "sgo_", ir, n_keys=nk, devices=(0, 0, 0, 0), max_batch=64))
+    sharded = run(lambda ir, nk: ShardedEngine(lib, "sgo_", ir, n_keys=nk, devices=(0, 0, 0, 0), max_batch=64))
     assert single == sharded and len(single) > 10

@@ -16,6 +16,7 @@ import pytest
 from oracle_backend import build_oracle
 from test_gpu_general import ABSENT, GENERAL, _burst_stream
 from test_gpu_parity import SHAPES
+from sharded_model import ShardedEngine
 
 sa = importlib.import_module("siddhi-1_amd")
 synth = importlib.import_module("siddhi-1_amd.synth")
@@ -257,7 +258,7 @@ def test_sharded_state_document_equals_single_engine(shape):
     cq = sa.compile_query(app, app.queries[0], sa.StringDictionary())
     lib = build_oracle()
     one = sa.NativeEngine(lib, "sgo_", cq.ir, n_keys=n_keys)
-    shd = sa.ShardedEngine(lib, "sgo_", cq.ir, n_keys=n_keys, devices=(0, 1, 2))
+    shd = ShardedEngine(lib, "sgo_", cq.ir, n_keys=n_keys, devices=(0, 1, 2))
     data = [(b * batch, synth.stock_ticks(b * batch, batch, n_keys, seed=30 + b, rate_per_ms=16)) for b in range(4)]
     for seq, d in data[:2]:
         for e in (one, shd):
@@ -266,7 +267,7 @@ def test_sharded_state_document_equals_single_engine(shape):
     d1, d3 = sd.parse(one.state_export()), sd.parse(shd.state_export())
     assert sd.logical(d1) == sd.logical(d3)
     # the single engine's document split across three fresh shards continues exactly
-    shd2 = sa.ShardedEngine(lib, "sgo_", cq.ir, n_keys=n_keys, devices=(0, 1, 2))
+    shd2 = ShardedEngine(lib, "sgo_", cq.ir, n_keys=n_keys, devices=(0, 1, 2))
     shd2.state_import(one.state_export())
     for seq, d in data[2:]:
         for e in (one, shd2):
