@@ -732,6 +732,125 @@ def api_columnar(sa, synth, n_keys, chunk, chunks, strings="object"):
                     "ColumnarQueryCallback, one send per chunk (host runtime + HIP engine), bounded sample"}
 
 
+def merge_leg(sa, lib, eng, step, first, steps, rank, world, dist, dev, B, torch, cap):
+    """N > 1 (north_star: "per-partition output is merged back in timestamp order on the host"): `steps` more
+    steps after the timed region, each rank's matches polled to host memory (pinned staging) and written to a
+    /dev/shm segment, then rank 0 merges the ranks' runs into timestamp order (sg_merge_ts: stable, equal
+    timestamps in rank order, parallel merge path over the host's CPU share).  Beside `value`, never as it.
+    Every fallible part reports into a flag all ranks reduce, so the ranks stay in step and a failure ends the
+    leg (recorded here) instead of hanging a collective."""
+    import ctypes as C
+    import numpy as np_
+    port = os.environ.get("MASTER_PORT", "0")
+    base = f"/dev/shm/sgmerge_{port}_"
+    mine = [base + f"{rank}_{x}" for x in ("hdr", "ts", "key")]
+    flag = torch.ones(1, dtype=torch.int32, device=dev)
+
+    def agree(ok):
+        flag.fill_(1 if ok else 0)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        return bool(flag.item())
+
+    err = None
+    try:
+        hdr = np_.memmap(mine[0], dtype=np_.int64, mode="w+", shape=(2,))
+        tsb = np_.memmap(mine[1], dtype=np_.int64, mode="w+", shape=(cap,))
+        keyb = np_.memmap(mine[2], dtype=np_.uint32, mode="w+", shape=(cap,))
+        ok = True
+    except Exception as e:   # noqa: BLE001 (reported in the line)
+        err, ok = repr(e), False
+    res = None
+    try:
+        if not agree(ok):
+            return {"error": err or "another rank could not create its segment"}
+        runs = None
+        if rank == 0:
+            try:
+                runs = [(np_.memmap(base + f"{r}_hdr", dtype=np_.int64, mode="r", shape=(2,)),
+                         np_.memmap(base + f"{r}_ts", dtype=np_.int64, mode="r", shape=(cap,)),
+                         np_.memmap(base + f"{r}_key", dtype=np_.uint32, mode="r", shape=(cap,))) for r in range(world)]
+                ok = True
+            except Exception as e:   # noqa: BLE001
+                err, ok = repr(e), False
+        if not agree(ok):
+            return {"error": err or "rank 0 could not map the segments"}
+        lib.sg_merge_ts.argtypes = [C.c_uint32, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64), C.c_uint32, C.c_void_p]
+        lib.sg_merge_ts.restype = C.c_int
+        threads = max(1, int(cpu_quota() or 1))
+        order = np_.empty(world * cap, dtype=np_.uint64) if rank == 0 else None
+        got = [0]
+
+        def sink():   # this rank's matches (a window that wraps the ring comes in two polls), global key ids
+            n = 0
+            while True:
+                m = eng.poll(copy=False)
+                k = len(m)
+                if k == 0:
+                    break
+                if n + k > cap:
+                    raise RuntimeError("merge segment full")
+                tsb[n:n + k] = m.ts
+                keyb[n:n + k] = m.key * np_.uint32(world) + np_.uint32(rank)
+                n += k
+            hdr[0] = n
+            got[0] += n
+
+        merged, merge_s = 0, 0.0
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for s in range(first, first + steps):
+            try:
+                step(s, sink)
+                ok = True
+            except Exception as e:   # noqa: BLE001
+                err, ok = repr(e), False
+            if not agree(ok):
+                break
+            if rank == 0:
+                try:
+                    tm = time.perf_counter()
+                    lens = [int(h[0]) for h, _, _ in runs]
+                    ptrs = (C.c_void_p * world)(*[t.ctypes.data if n else None for (_, t, _), n in zip(runs, lens)])
+                    ln = (C.c_uint64 * world)(*lens)
+                    rc = lib.sg_merge_ts(world, ptrs, ln, threads, order.ctypes.data)
+                    if rc != 0:
+                        raise RuntimeError(f"sg_merge_ts {rc}")
+                    merged += sum(lens)
+                    merge_s += time.perf_counter() - tm
+                    ok = True
+                except Exception as e:   # noqa: BLE001
+                    err, ok = repr(e), False
+            if not agree(ok):
+                break
+        else:
+            torch.cuda.synchronize()
+            dist.barrier()
+            el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+            dist.all_reduce(el, op=dist.ReduceOp.MAX)
+            el = float(el.item())
+            res = {"value": B * world * steps / el, "unit": "events/s", "steps": steps, "ms_per_step": el / steps * 1e3,
+                   "matches_per_step": merged / steps if rank == 0 else None,
+                   "merge_ms_per_step": merge_s / steps * 1e3 if rank == 0 else None,
+                   "merge_records_per_s": merged / merge_s if rank == 0 and merge_s > 0 else None,
+                   "merge_threads": threads,
+                   "what": "C5 steps with each rank's matches polled to host memory and merged by rank 0 into "
+                           "timestamp order (sg_merge_ts over /dev/shm segments; equal timestamps in rank order)"}
+        if res is None:
+            res = {"error": err or "a rank failed"}
+        return res
+    finally:
+        try:
+            dist.barrier()   # rank 0 has unmapped nothing yet: every rank removes its own segment after it
+        except Exception:    # noqa: BLE001
+            pass
+        for f in mine:
+            try:
+                os.remove(f)
+            except OSError:
+                pass
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -786,7 +905,9 @@ def main():
     # N > 1: one extra slice, so that every timed step also reshards the NEXT step's slice (below);
     # N = 1: ISO more steps after the timed region, run one at a time (the kernels alone on the GPU)
     ISO = 3
-    for s in range(total + (1 if world > 1 else ISO)):
+    # N > 1: MERGE more slices for the host timestamp-order merge leg after the timed region (merge_leg)
+    MERGE = 0 if os.environ.get("SG_BENCH_NO_MERGE") else 4
+    for s in range(total + (1 + MERGE if world > 1 else ISO)):
         base = s * world * B + rank * B
         # generated on the device, bit-identical to synth.stock_ticks (tests/test_synth.py)
         t = synth.stock_ticks_torch(torch, base, B, K * world, dev, rate_per_ms=2000 * world)
@@ -805,7 +926,7 @@ def main():
 
     nxt = [reshard_step(0) if world > 1 else None]
 
-    def step(s):
+    def step(s, sink=None):
         if world > 1:
             g = nxt[0]
             # the engine's stream waits for the exchange on the device (no host synchronisation)
@@ -826,7 +947,10 @@ def main():
             # waits for the step, so the exchange buffers the engine reads are never overwritten early
             nxt[0] = reshard_step(s + 1)
             del g
-            take_all(eng, False)
+            if sink is None:
+                take_all(eng, False)
+            else:
+                sink()
         else:
             # pipelined: the matches of the batches already complete; batch s's grouping runs while
             # batch s-1 advances (the engine's two streams), no host round trip between batches
@@ -865,6 +989,9 @@ def main():
             step(s)
             drain()
         iso = delta(sti0, eng.stats())
+    merge = None
+    if world > 1 and MERGE:
+        merge = merge_leg(sa, lib, eng, step, total, MERGE, rank, world, dist, dev, B, torch, 2 * maxb)
     if rs is not None:
         rs.check()   # a destination block overflow would have dropped events: the run is invalid
     events_all = B * args.steps * world
@@ -917,6 +1044,8 @@ def main():
         "work_per_step": {k: dst[k] / args.steps for k in ("matches", "partials_created", "partials_scanned",
                                                            "keys_touched", "live_at_batch_start")},
     }
+    if merge is not None:
+        out["merge_inclusive"] = merge
     if iso is not None:
         a_iso = iso["advance_ns"] / 1e9 / max(1, iso["advance_launches"])
         g_iso = algorithmic_bytes(iso) / max(1, iso["advance_launches"]) / a_iso / 1e9 if a_iso > 0 else 0.0

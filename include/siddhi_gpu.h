@@ -259,6 +259,14 @@ int sg_shard_pack_blocks(uint64_t n, const uint32_t* key, const int64_t* ts, con
 int sg_shard_unpack(uint64_t n, const uint32_t* rows, uint32_t n_cols, uint32_t* key, int64_t* ts,
                     uint32_t* const* cols_dev, void* stream);
 
+/* Host merge of per-shard match runs (north_star: per-partition output merged back in timestamp
+ * order on the host — the order MultiProcessStreamReceiver.java:119-121 hands StateEvents to the selector).
+ * Each run i (ts[i], len[i] entries, host memory) is one shard's matches in its own order, timestamps
+ * nondecreasing; out[total] receives the stable merge as (run << 48) | index: by timestamp, equal timestamps
+ * in run order, then in their run's order.  threads > 1: the output is cut into equal slices merged in
+ * parallel (merge path over the runs).  No device needed. */
+int sg_merge_ts(uint32_t n_runs, const int64_t* const* ts, const uint64_t* len, uint32_t threads, uint64_t* out);
+
 /* Partition-key dictionary (host ingest; no device needed).  Replaces the
  * String-keyed partition map of PartitionStreamReceiver.receive (partition/PartitionStreamReceiver.java:
  * 175-260), where ValuePartitionExecutor.execute (partition/executor/ValuePartitionExecutor.java:34-41)

@@ -81,12 +81,18 @@ template <int NW, bool TM, bool FF = false> struct AbsKey {
     uint32_t qb;
     uint32_t err;
     unsigned long long scanned, created, matches;
+    // the register-native record (GEN_W0_REG; nullptr: the block only).  In record mode the window is stored
+    // in list order (slot j at record entry j: slots [dmin, n) differ from the record) and the timer queue is
+    // linear (entries [qh, qh + ql) of its rows; stored from row 0)
+    gu32* R;
+    bool wasRec;
+    uint32_t dmin;
 
-    __device__ AbsKey(const GenProgram* g, uint32_t* state, uint32_t K_, uint32_t key)
+    __device__ AbsKey(const GenProgram* g, uint32_t* state, uint32_t K_, uint32_t key, uint32_t* rec = nullptr)
         : G(*(cGenProgram*)g), S(gp(state)), K(K_), k(key), n(0), np(0), used(0), dpool(0), canon(false),
           hw0(0), used0(0), seed0(false), seedTs0(0), sbad(false), seedPend(0), seedStg(0),
           seedPendTs(-1), seedStgTs(-1), f0(0), f1(0), lst(0), qh(0), ql(0), qhv(0), qb(0), err(0), scanned(0), created(0),
-          matches(0) {
+          matches(0), R(rec ? gp(rec) : nullptr), wasRec(false), dmin(0) {
         ks0 = G.offKS + (uint32_t)G.absP0 * G.ksWords;
         ks1 = G.offKS + (uint32_t)G.absP1 * G.ksWords;
         stream = G.slotStream[G.pre[G.absP0].stateId];
@@ -103,6 +109,93 @@ template <int NW, bool TM, bool FF = false> struct AbsKey {
         W(w_ + 1) = (uint32_t)((uint64_t)v >> 32);
     }
     __device__ __forceinline__ uint32_t qword(uint32_t i) const { return ks1 + KS_LISTS + 2 * G.L + 2 * i; }
+    // the record: header rows, window entry rows, the queue's 64-bit rows
+    __device__ __forceinline__ gu32& RW(uint32_t w_) const { return R[(size_t)w_ * K + k]; }
+    __device__ __forceinline__ uint32_t rev(uint32_t j, uint32_t f) const { return GEN_REC_EV + j * (5u + NW) + f; }
+    __device__ __forceinline__ __attribute__((address_space(1))) unsigned long long& Q64(uint32_t i) const {
+        return ((__attribute__((address_space(1))) unsigned long long*)(R + (size_t)gen_rec_q(NW) * K))[(size_t)i * K + k];
+    }
+    // queue entry at position p of the walk (record: linear rows; block: the ring)
+    __device__ __forceinline__ int64_t qget(uint32_t p) const {
+        if (R) return (int64_t)Q64(p);
+        return R64(qword(p >= G.Q ? p - G.Q : p));
+    }
+
+    // ---- the record (GEN_W0_REG): header row 0 = n | np << 4 | seedPend << 8 | seedStg << 9 | sbad << 10 |
+    // f0 << 16 | f1 << 24, rows 1-2 the seed's ts, 3-4 lastScheduledTime, 5 the queue length (head at row 0)
+    __device__ void loadRec() {
+        const uint32_t h = RW(0);
+        n = h & 15u;
+        np = (h >> 4) & 15u;
+        seedPend = (h >> 8) & 1u;
+        seedStg = (h >> 9) & 1u;
+        sbad = (h >> 10) & 1u;
+        f0 = (h >> 16) & 0xffu;
+        f1 = h >> 24;
+        seedPendTs = seedStgTs = (int64_t)((uint64_t)RW(1) | ((uint64_t)RW(2) << 32));
+        lst = (int64_t)((uint64_t)RW(3) | ((uint64_t)RW(4) << 32));
+        ql = RW(5);
+        qh = 0;
+#pragma unroll
+        for (int j = 0; j < ABS_R; ++j) {
+            // (every element loaded and assigned unconditionally — a slot past n reads the header row, a cache
+            // hit — because conditional assignments to the window's elements keep the key object in scratch)
+            const bool live = (uint32_t)j < n;
+            uint32_t x[5 + NW];
+#pragma unroll
+            for (int f = 0; f < 5 + NW; ++f) {
+                const uint32_t v = RW(live ? rev(j, (uint32_t)f) : 0u);
+                x[f] = live ? v : 0u;
+            }
+            seq[j] = (uint64_t)x[0] | ((uint64_t)x[1] << 32);
+            ts[j] = (int64_t)((uint64_t)x[2] | ((uint64_t)x[3] << 32));
+            nb[j] = x[4];
+#pragma unroll
+            for (int q = 0; q < NW; ++q) w[j][q] = x[5 + q];
+        }
+        wasRec = true;
+        dmin = n;
+    }
+    // the header, the window entries [dmin, n), the queue moved to row 0 when its head advanced
+    __device__ void storeRec() const {
+        if (!wasRec) W(0) = 1u | GEN_W0_REG;
+        const int64_t sts = seedPend ? seedPendTs : seedStgTs;
+        RW(0) = n | (np << 4) | (seedPend << 8) | (seedStg << 9) | (sbad ? 1024u : 0u) | (f0 << 16) | (f1 << 24);
+        RW(1) = (uint32_t)(uint64_t)sts;
+        RW(2) = (uint32_t)((uint64_t)sts >> 32);
+        RW(3) = (uint32_t)(uint64_t)lst;
+        RW(4) = (uint32_t)((uint64_t)lst >> 32);
+        RW(5) = ql;
+        for (uint32_t j = dmin; j < n; j++) {   // (slot j's registers picked by selects: no dynamic indexing)
+            uint32_t pn = 0, pw[NW];
+            int64_t t = 0;
+            uint64_t q = 0;
+#pragma unroll
+            for (int x = 0; x < NW; ++x) pw[x] = 0;
+#pragma unroll
+            for (int y = 0; y < ABS_R; ++y) {
+                if ((uint32_t)y == j) {
+                    t = ts[y]; q = seq[y]; pn = nb[y];
+#pragma unroll
+                    for (int x = 0; x < NW; ++x) pw[x] = w[y][x];
+                }
+            }
+            RW(rev(j, 0)) = (uint32_t)q;
+            RW(rev(j, 1)) = (uint32_t)(q >> 32);
+            RW(rev(j, 2)) = (uint32_t)(uint64_t)t;
+            RW(rev(j, 3)) = (uint32_t)((uint64_t)t >> 32);
+            RW(rev(j, 4)) = pn;
+#pragma unroll
+            for (int x = 0; x < NW; ++x) RW(rev(j, 5u + (uint32_t)x)) = pw[x];
+        }
+        if constexpr (TM) {   // (only a sweep pops)
+            if (qh)
+                for (uint32_t i = 0; i < ql; i++) Q64(i) = Q64(qh + i);
+        }
+    }
+    // the general layout from the registers (a hand-over to the general / wave-per-key kernels, a flush): the
+    // queue back into the block's ring from position 0, then every record (word 0 loses GEN_W0_REG)
+    __device__ __forceinline__ void store_general() const { store(true); }
 
     // ---- load: false = this key's lists are not of the shape the window holds (the general kernel takes it)
     __device__ __forceinline__ bool load() {
@@ -117,6 +210,12 @@ template <int NW, bool TM, bool FF = false> struct AbsKey {
             return true;     // (canon = false: the zeroed block is written whole)
         }
         if (w0 & GEN_W0_DEEP) return false;   // (the lists are in the deep store: the wave-per-key kernels take it)
+        if ((w0 & GEN_W0_REG) && R) {
+            loadRec();
+            if constexpr (TM) qfill();
+            else qhv = ql ? (int64_t)Q64(0) : 0;
+            return true;
+        }
         canon = true;
         f0 = W(ks0 + KS_FLAGS);
         f1 = W(ks1 + KS_FLAGS);
@@ -171,7 +270,7 @@ template <int NW, bool TM, bool FF = false> struct AbsKey {
         if (!ok) return false;
         // the partials' payload: the timer sweep of a key in this layout reads none of it (a timer tests
         // timestamps; an emitted partial's seq is read when it fires, and no record is rewritten)
-        if (!TM || !canon) {
+        if (!TM || !canon || R) {   // (record mode: the key's window is rewritten into the record)
 #pragma unroll
             for (int j = 0; j < ABS_R; ++j) {
                 if ((uint32_t)j < n) {
@@ -194,6 +293,7 @@ template <int NW, bool TM, bool FF = false> struct AbsKey {
                 }
             }
         }
+        if (R) canon = false;   // (record mode: no pool entries; a hand-over writes partial j at entry j)
         hw0 = (canon && (w0 & GEN_W0_POOLC)) ? (w0 >> 2) & 63u : 0u;
         used0 = used;
         if (!canon) {  // rewritten whole at the store, partial j at entry j
@@ -204,6 +304,13 @@ template <int NW, bool TM, bool FF = false> struct AbsKey {
         qh = W(ks1 + KS_QHEAD);
         ql = W(ks1 + KS_QLEN);
         if (qh >= G.Q || ql > G.Q) return false;
+        if (R) {   // record mode: the queue's entries from the ring to the record's rows [0, ql)
+            for (uint32_t i = 0; i < ql; i++) {
+                const uint32_t p = qh + i;
+                Q64(i) = (unsigned long long)R64(qword(p >= G.Q ? p - G.Q : p));
+            }
+            qh = 0;
+        }
         hdr(h0);
         if constexpr (TM) {
             qfill();
@@ -216,11 +323,7 @@ template <int NW, bool TM, bool FF = false> struct AbsKey {
     __device__ __forceinline__ void qfill() {
         qb = ql < (uint32_t)ABS_QP ? ql : (uint32_t)ABS_QP;
 #pragma unroll
-        for (int i = 0; i < ABS_QP; ++i) {
-            uint32_t pos = qh + (uint32_t)i;
-            pos = pos >= G.Q ? pos - G.Q : pos;
-            qbuf[i] = (uint32_t)i < qb ? R64(qword(pos)) : 0;
-        }
+        for (int i = 0; i < ABS_QP; ++i) qbuf[i] = (uint32_t)i < qb ? qget(qh + (uint32_t)i) : 0;
         qhv = qbuf[0];
     }
 
@@ -252,9 +355,17 @@ template <int NW, bool TM, bool FF = false> struct AbsKey {
 
     // ---- store: the header, the list words, the records of the partials this walk created (every record
     // when the key was loaded in another layout), the free bitmaps (word 0; all words then)
-    __device__ __forceinline__ void store() const {
-        if (!canon) {
-            store_all();
+    // (general: the general layout even in record mode — one call site of store_all, whose second inlined copy
+    // would keep the key object in scratch)
+    __device__ __forceinline__ void store(bool general = false) const {
+        if (R && !general) {
+            storeRec();
+            return;
+        }
+        if (R)   // the record's linear queue back into the block's ring from position 0
+            for (uint32_t i = 0; i < ql; i++) W64(qword(i), (int64_t)Q64(qh + i));
+        if (!canon || R) {
+            store_all(R ? 0u : qh);
             return;
         }
         uint32_t h[8];
@@ -351,7 +462,7 @@ template <int NW, bool TM, bool FF = false> struct AbsKey {
     }
     // a key loaded in another layout (or created here): every record, partial j at entry j (px[j] = j: the
     // window's entries were assigned in slot order), the constant words of the free entries, every bitmap word
-    __device__ __forceinline__ void store_all() const {
+    __device__ __forceinline__ void store_all(uint32_t qhead) const {
         W(0) = 1u | GEN_W0_POOLC | (n << 2);  // (entries [0, n) written below)
         W(ks0 + KS_FLAGS) = f0;
         W(ks0 + KS_PLEN) = seedPend;
@@ -367,7 +478,7 @@ template <int NW, bool TM, bool FF = false> struct AbsKey {
         }
         W(ks1 + KS_FLAGS) = f1;
         W64(ks1 + KS_LST, lst);
-        W(ks1 + KS_QHEAD) = qh;
+        W(ks1 + KS_QHEAD) = qhead;
         W(ks1 + KS_QLEN) = ql;
         W(ks1 + KS_PLEN) = np;
         W(ks1 + KS_NLEN) = n - np;
@@ -421,16 +532,16 @@ template <int NW, bool TM, bool FF = false> struct AbsKey {
 
     // Scheduler.notifyAt under playback (Scheduler.java:114-128): append to the key's queue
     __device__ __forceinline__ void notifyAt(int64_t t) {
-        if (ql >= G.Q) { err |= GERR_CAP; return; }
-        const uint32_t pos = (qh + ql) % G.Q;
-        W64(qword(pos), t);  // (TM: the buffer stays a prefix of the queue; a pop past it reloads)
+        if (ql >= G.Q || (R && qh + ql >= G.Q)) { err |= GERR_CAP; return; }
+        if (R) Q64(qh + ql) = (unsigned long long)t;   // (rows: a sweep pops before it appends, so qh + ql < Q)
+        else W64(qword((qh + ql) % G.Q), t);  // (TM: the buffer stays a prefix of the queue; a pop past it reloads)
         if (ql == 0) qhv = t;
         ql++;
     }
     __device__ __forceinline__ void qpop() {
         if constexpr (TM) {
             if (qb == 0) qfill();
-            qh = (qh + 1) % G.Q;
+            qh = R ? qh + 1 : (qh + 1) % G.Q;
             ql--;
 #pragma unroll
             for (int i = 0; i + 1 < ABS_QP; ++i) qbuf[i] = qbuf[i + 1];
@@ -438,9 +549,9 @@ template <int NW, bool TM, bool FF = false> struct AbsKey {
             if (qb == 0 && ql) qfill();
             if (ql) qhv = qbuf[0];
         } else {
-            qh = (qh + 1) % G.Q;
+            qh = R ? qh + 1 : (qh + 1) % G.Q;
             ql--;
-            if (ql) qhv = R64(qword(qh));
+            if (ql) qhv = qget(qh);
         }
     }
 
@@ -459,6 +570,8 @@ template <int NW, bool TM, bool FF = false> struct AbsKey {
         drop &= (n >= 32u ? 0xffffffffu : ((1u << n) - 1u));
         if (!drop) return;
         const uint32_t keep = ((n >= 32u ? 0xffffffffu : ((1u << n) - 1u))) & ~drop;
+        const uint32_t lo = (uint32_t)__ffs(drop) - 1u;   // the slots from the lowest dropped one move
+        dmin = lo < dmin ? lo : dmin;
         if (canon) {  // the dropped partials' pool entries are free again
 #pragma unroll
             for (int j = 0; j < ABS_R; ++j)
@@ -487,6 +600,7 @@ template <int NW, bool TM, bool FF = false> struct AbsKey {
     // updateState: the staged slots join the pending list, stable-sorted by ts (eventTimeComparator)
     __device__ __forceinline__ void promote() {
         if (n > np && sbad) {
+            dmin = np < dmin ? np : dmin;
 #pragma unroll
             for (int pass = 0; pass < ABS_R - 1; ++pass) {
 #pragma unroll
@@ -608,6 +722,7 @@ template <int NW, bool TM, bool FF = false> struct AbsKey {
                 // (staged; schedules e1.ts + T); `every`: p0.addEveryState (a new seed, staged, same ts)
                 const uint32_t t = n;
                 const uint32_t e = canon ? alloc() : t;   // (store_all writes partial j at entry j)
+                dmin = t < dmin ? t : dmin;
 #pragma unroll
                 for (int j = 0; j < ABS_R; ++j) {
                     if ((uint32_t)j == t) {
@@ -695,7 +810,7 @@ template <int NW, bool FF> __device__ void abs_batch(const GenArgs& a) {
         b = gp(a.b.seg_begin)[key];
         e = gp(a.b.seg_end)[key];
     }
-    AbsKey<NW, false, FF> L(a.G, a.state, a.K, key < a.K ? key : 0u);
+    AbsKey<NW, false, FF> L(a.G, a.state, a.K, key < a.K ? key : 0u, a.rec);
     bool walk = b < e;
     bool fb = false;
     uint32_t stop = b;
@@ -722,7 +837,7 @@ template <int NW, bool FF> __device__ void abs_batch(const GenArgs& a) {
             }
             L.event(ev);
         }
-        L.store();
+        L.store(i < e);   // (a hand-over: the general / wave-per-key kernels continue from the block)
         if (i < e) {
             fb = true;
             stop = i;
@@ -749,19 +864,23 @@ template <int NW> __device__ void abs_timers(const GenArgs& a) {
         const uint64_t di = base + threadIdx.x;
         const bool act = di < nd;
         const uint32_t key = act ? gp(a.t.due)[di] : 0u;
-        AbsKey<NW, true> L(a.G, a.state, a.K, key);
+        AbsKey<NW, true> L(a.G, a.state, a.K, key, a.rec);
         bool fb = false;
         if (act) {
-            if (!(L.W(0) & 1u)) {  // a key is created by its first event (not due)
+            const uint32_t w0 = L.W(0);
+            if (!(w0 & 1u)) {  // a key is created by its first event (not due)
                 gp(a.t.dpair_key)[di] = ~0ull;
                 gp(a.t.dpair_i)[di] = GEN_PAIR_NONE;
                 if (a.t.dpair_kid) gp(a.t.dpair_kid)[di] = GEN_PAIR_NONE;
                 gp(a.t.nd)[key] = GEN_NO_DEADLINE;
             } else {
                 // the listener's collection of (due time, key) from the queue head (the A.10 check)
-                const uint32_t qh = L.W(L.ks1 + KS_QHEAD), ql = L.W(L.ks1 + KS_QLEN);
+                const bool rec = (w0 & GEN_W0_REG) && L.R;
+                const uint32_t qh = rec ? 0u : L.W(L.ks1 + KS_QHEAD), ql = rec ? L.RW(5) : L.W(L.ks1 + KS_QLEN);
                 int64_t h = 0;
-                if (ql && (L.W(0) & GEN_W0_DEEP) && a.deep) {   // (the queue in the deep store, normalised)
+                if (ql && rec) {   // (the queue in the record, its head at row 0)
+                    h = (int64_t)L.Q64(0);
+                } else if (ql && (w0 & GEN_W0_DEEP) && a.deep) {   // (the queue in the deep store, normalised)
                     const gu32* D = gp(a.deep) + (size_t)key * a.deepWords +
                                     gen_deep_layout(G.L, G.Q, (uint32_t)NW).oQ;
                     h = (int64_t)((uint64_t)D[0] | ((uint64_t)D[1] << 32));
@@ -797,6 +916,16 @@ template <int NW> __device__ void abs_timers(const GenArgs& a) {
     abs_wave_stats(a, sc, cr, ma, 0ull, er, nfb);
 }
 
+// ---- the records written back to the blocks in the general layout (before a snapshot, ...) ----
+template <int NW> __device__ void abs_flush(const GenArgs& a) {
+    const uint32_t key = blockIdx.x * 64u + threadIdx.x;
+    if (key >= a.K || !a.rec) return;
+    AbsKey<NW, false> L(a.G, a.state, a.K, key, a.rec);
+    if (!(L.W(0) & GEN_W0_REG)) return;
+    L.load();
+    L.store_general();
+}
+
 }  // namespace
 
 // One kernel per captured-word count (NW = the stream's attributes as 32-bit words, long / double 2 each).
@@ -809,7 +938,8 @@ template <int NW> __device__ void abs_timers(const GenArgs& a) {
     }                                                                                                               \
     extern "C" __global__ void __launch_bounds__(64) k_abs_timers_##NW(const GenArgs ap) {          \
         abs_timers<NW>(ap);                                                                                        \
-    }
+    }                                                                                                               \
+    extern "C" __global__ void __launch_bounds__(64) k_abs_flush_##NW(const GenArgs ap) { abs_flush<NW>(ap); }
 ABS_KERNELS(1)
 ABS_KERNELS(2)
 ABS_KERNELS(3)

@@ -66,11 +66,15 @@ template <int NW> struct CntKey {
     unsigned long long resBase, resEnd;
     uint32_t resLeft;
     uint32_t trigRank;
+    // the register-native record (GEN_W0_REG; nullptr: the block only): chain events [dirty, n) differ from it
+    gu32* R;
+    uint32_t dirty;
+    bool wasRec;
 
     __device__ CntKey(const GenArgs& a, uint32_t key)
         : G(*(cGenProgram*)a.G), A(a), S(gp(a.state)), K(a.K), k(key), n(0), xts(-1), inP0p(false), inP0n(false),
           inL(false), seedN(false), f0(0), fA(0), fB(0), err(0), scanned(0), created(0), matches(0), resBase(0),
-          resEnd(0), resLeft(0), trigRank(0) {
+          resEnd(0), resLeft(0), trigRank(0), R(a.rec ? gp(a.rec) : nullptr), dirty(0), wasRec(false) {
         p0 = G.cntP0;
         pA = G.cntPA;
         pB = G.cntPB;
@@ -82,13 +86,6 @@ template <int NW> struct CntKey {
         ksB = G.offKS + (uint32_t)pB * G.ksWords;
         mn = G.pre[p0].minCount;
         mx = G.pre[p0].maxCount;
-    }
-    __device__ void retarget(uint32_t key) {
-        k = key;
-        n = 0;
-        xts = -1;
-        inP0p = inP0n = inL = seedN = false;
-        f0 = fA = fB = 0;
     }
 
     __device__ __forceinline__ gu32& W(uint32_t w_) const { return S[gen_il(K, k, w_)]; }
@@ -102,10 +99,70 @@ template <int NW> struct CntKey {
     __device__ __forceinline__ uint32_t stw(uint32_t se, uint32_t f) const { return G.offST + se * G.stWords + f; }
     __device__ __forceinline__ uint32_t sew(uint32_t e, uint32_t f) const { return G.offSE + e * G.seWords + f; }
 
+    // ---- the register-native record (GEN_W0_REG): header word = n | inP0p << 4 | inP0n << 5 | inL << 6 |
+    // seedN << 7 | f0 << 8 | fA << 16 | fB << 24, the partial's ts, then per chain event seq, ts, null bits, words
+    __device__ __forceinline__ gu32& RW(uint32_t w_) const { return R[(size_t)w_ * K + k]; }
+    __device__ __forceinline__ uint32_t rev(uint32_t j, uint32_t f) const { return GEN_REC_EV + j * (5u + NW) + f; }
+    __device__ void loadRec() {
+        const uint32_t h = RW(0);
+        xts = (int64_t)((uint64_t)RW(1) | ((uint64_t)RW(2) << 32));
+        n = h & 15u;
+        inP0p = (h >> 4) & 1u;
+        inP0n = (h >> 5) & 1u;
+        inL = (h >> 6) & 1u;
+        seedN = (h >> 7) & 1u;
+        f0 = (h >> 8) & 0xffu;
+        fA = (h >> 16) & 0xffu;
+        fB = h >> 24;
+#pragma unroll
+        for (int j = 0; j < CNT_R; ++j) {
+            ts[j] = 0;
+            seq[j] = 0;
+            nb[j] = 0;
+#pragma unroll
+            for (int q = 0; q < NW; ++q) w[j][q] = 0;
+            if ((uint32_t)j < n) {
+                seq[j] = (uint64_t)RW(rev(j, 0)) | ((uint64_t)RW(rev(j, 1)) << 32);
+                ts[j] = (int64_t)((uint64_t)RW(rev(j, 2)) | ((uint64_t)RW(rev(j, 3)) << 32));
+                nb[j] = RW(rev(j, 4));
+#pragma unroll
+                for (int q = 0; q < NW; ++q) w[j][q] = RW(rev(j, 5u + (uint32_t)q));
+            }
+        }
+        dirty = n;
+        wasRec = true;
+    }
+    // the header, the timestamp and the chain events appended since the load (a chain only grows at its end
+    // or restarts: the events below `dirty` are the record's already)
+    __device__ void storeRec() const {
+        if (!wasRec) W(0) = 1u | GEN_W0_REG;
+        RW(0) = n | (inP0p ? 16u : 0u) | (inP0n ? 32u : 0u) | (inL ? 64u : 0u) | (seedN ? 128u : 0u) | (f0 << 8) |
+                (fA << 16) | (fB << 24);
+        RW(1) = (uint32_t)(uint64_t)xts;
+        RW(2) = (uint32_t)((uint64_t)xts >> 32);
+#pragma unroll
+        for (int j = 0; j < CNT_R; ++j) {
+            if ((uint32_t)j >= dirty && (uint32_t)j < n) {
+                RW(rev(j, 0)) = (uint32_t)seq[j];
+                RW(rev(j, 1)) = (uint32_t)(seq[j] >> 32);
+                RW(rev(j, 2)) = (uint32_t)(uint64_t)ts[j];
+                RW(rev(j, 3)) = (uint32_t)((uint64_t)ts[j] >> 32);
+                RW(rev(j, 4)) = nb[j];
+#pragma unroll
+                for (int q = 0; q < NW; ++q) RW(rev(j, 5u + (uint32_t)q)) = w[j][q];
+            }
+        }
+    }
+
     // ---- load: false = the stored lists are not of this kernel's canonical shape (the general kernel
     // takes the key's run)
     __device__ bool load() {
-        if (!(W(0) & 1u)) {  // PartitionRuntimeImpl.initPartition: p0.init() stages one seed
+        const uint32_t w0 = W(0);
+        if (w0 & GEN_W0_REG) {
+            loadRec();
+            return true;
+        }
+        if (!(w0 & 1u)) {  // PartitionRuntimeImpl.initPartition: p0.init() stages one seed
             seedN = true;
             f0 = GF_INIT;
             return true;
@@ -398,6 +455,7 @@ template <int NW> struct CntKey {
             } else {
                 if (sP0) n = 0;  // X (if any) was the pair's alone and has left it: the seed starts a chain
                 if (n >= (uint32_t)CNT_R) { err |= GERR_CHAIN; return; }
+                dirty = n < dirty ? n : dirty;
 #pragma unroll
                 for (int j = 0; j < CNT_R; ++j) {
                     const bool here = (uint32_t)j == n;
@@ -463,7 +521,8 @@ template <int NW> __device__ void cnt_batch(const GenArgs& a) {
             }
             L.event(ev, pos);
         }
-        L.store();
+        if (L.R) L.storeRec();
+        else L.store();
         ky = 1;
     }
     // unused reserved raw slots are marked empty (k_gen_scatter skips them)
@@ -478,13 +537,24 @@ template <int NW> __device__ void cnt_batch(const GenArgs& a) {
     abs_wave_stats(a, L.scanned, L.created, L.matches, ky, L.err, fb ? 1ull : 0ull);
 }
 
+// ---- the records written back to the blocks in the canonical layout (before a snapshot, min-seq scan, ...) ----
+template <int NW> __device__ void cnt_flush(const GenArgs& a) {
+    const uint32_t key = blockIdx.x * 64u + threadIdx.x;
+    if (key >= a.K || !a.rec) return;
+    CntKey<NW> L(a, key);
+    if (!(L.W(0) & GEN_W0_REG)) return;
+    L.loadRec();
+    L.store();   // (word 0 = 1: the block is the key's state again)
+}
+
 }  // namespace
 
 // One kernel per captured-word count (NW = the stream's attributes as 32-bit words, long / double 2 each).
 #define CNT_KERNELS(NW)                                                                                             \
     extern "C" __global__ void __launch_bounds__(64) k_cnt_batch_##NW(const GenArgs ap) {           \
         cnt_batch<NW>(ap);                                                                                         \
-    }
+    }                                                                                                              \
+    extern "C" __global__ void __launch_bounds__(64) k_cnt_flush_##NW(const GenArgs ap) { cnt_flush<NW>(ap); }
 CNT_KERNELS(1)
 CNT_KERNELS(2)
 CNT_KERNELS(3)

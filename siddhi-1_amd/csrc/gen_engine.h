@@ -58,6 +58,14 @@ __host__ __device__ inline size_t gen_at(uint32_t K, uint32_t blockWords, uint32
 // only the header words (flags, seed, list lengths, lastScheduledTime, queue length) and every component that
 // reads the lists from the block flushes the record back first (gen_host.hip gen_flush_deep)
 #define GEN_W0_DEEP 0x100u
+// GEN_W0_REG: the register-window kernels (cnt_kernels.hip, abs_kernels.hip) keep this key's state in its
+// register-native record (GenArgs.rec, interleaved like the blocks: row w of key k at w * K + k; gen_rec_words
+// rows): a header (GEN_REC_EV rows: list lengths and memberships, flags, timestamps), the window's partials in
+// list order (GEN_REC_R entries of seq i64, ts i64, null bits, attribute words) and, for the absent shape, its
+// timer queue with the head at entry 0 (64-bit rows from gen_rec_q).  The block then holds only word 0; the
+// kernels write back only what changed, and every component that reads the lists from the block flushes the
+// records back first (gen_host.hip gen_flush_deep; k_gen_live / k_gen_min_seq read them in place)
+#define GEN_W0_REG 0x200u
 // a deep-store record in 32-bit words: ts[L] i64, seq[L] u64, null bits[L], attribute words[NW][L], queue[Q] i64
 struct GenDeepLayout {
     uint32_t oTs, oSeq, oNb, oW, oQ, words;
@@ -76,6 +84,15 @@ __host__ __device__ inline GenDeepLayout gen_deep_layout(uint32_t L, uint32_t Q,
 #define ABS_R 8          // abs_kernels.hip: partials a key's register window holds
 #define ABS_MAXNW 8      // abs_kernels.hip: attribute words of an event it captures
 #define CNT_R 8          // cnt_kernels.hip: events a count chain in registers holds (the shape's max count)
+#define GEN_REC_EV 8u     // a record's first partial row; each partial: seq lo, hi, ts lo, hi, null bits, NW words
+#define GEN_REC_R 8u      // partials a record holds (= ABS_R = CNT_R)
+static_assert(ABS_R == GEN_REC_R && CNT_R == GEN_REC_R, "the record holds the register windows");
+// the first row of the timer queue (even: its 64-bit rows are 8-B aligned), the rows of a record
+__host__ __device__ inline uint32_t gen_rec_q(uint32_t NW) {
+    const uint32_t r = GEN_REC_EV + GEN_REC_R * (5u + NW);
+    return r + (r & 1u);
+}
+__host__ __device__ inline uint32_t gen_rec_words(uint32_t NW, uint32_t Q) { return gen_rec_q(NW) + 2u * Q; }
 
 enum { GK_STREAM = 0, GK_COUNT = 1, GK_LOGICAL = 2 };
 
@@ -289,6 +306,8 @@ struct GenArgs {
     uint32_t* deep;
     uint32_t deepWords;
     uint32_t pad3;
+    // the register-native records (GEN_W0_REG), gen_rec_words rows, or nullptr
+    uint32_t* rec;
 };
 // GenArgs.mode
 #define GEN_M_KEYLIST 1u   // k_gen_batch: lane i walks key fb_list[i] from fb_start[key]

@@ -61,10 +61,17 @@ static const AbsKernel kAbsdTimersF[ABS_MAXNW + 1] = {nullptr, k_absd_timersf_1,
 static const AbsKernel kAbsdFlush[ABS_MAXNW + 1] = {nullptr, k_absd_flush_1, k_absd_flush_2, k_absd_flush_3,
                                                     k_absd_flush_4, k_absd_flush_5, k_absd_flush_6, k_absd_flush_7,
                                                     k_absd_flush_8};
-#define CNT_DECL(NW) extern "C" __global__ void k_cnt_batch_##NW(const GenArgs ap);
+#define CNT_DECL(NW) extern "C" __global__ void k_cnt_batch_##NW(const GenArgs ap); \
+    extern "C" __global__ void k_cnt_flush_##NW(const GenArgs ap);
 CNT_DECL(1) CNT_DECL(2) CNT_DECL(3) CNT_DECL(4) CNT_DECL(5) CNT_DECL(6) CNT_DECL(7) CNT_DECL(8)
 static const AbsKernel kCntBatch[ABS_MAXNW + 1] = {nullptr, k_cnt_batch_1, k_cnt_batch_2, k_cnt_batch_3, k_cnt_batch_4,
                                                    k_cnt_batch_5, k_cnt_batch_6, k_cnt_batch_7, k_cnt_batch_8};
+#define ABSF_DECL(NW) extern "C" __global__ void k_abs_flush_##NW(const GenArgs ap);
+ABSF_DECL(1) ABSF_DECL(2) ABSF_DECL(3) ABSF_DECL(4) ABSF_DECL(5) ABSF_DECL(6) ABSF_DECL(7) ABSF_DECL(8)
+static const AbsKernel kAbsFlush[ABS_MAXNW + 1] = {nullptr, k_abs_flush_1, k_abs_flush_2, k_abs_flush_3, k_abs_flush_4,
+                                                   k_abs_flush_5, k_abs_flush_6, k_abs_flush_7, k_abs_flush_8};
+static const AbsKernel kCntFlush[ABS_MAXNW + 1] = {nullptr, k_cnt_flush_1, k_cnt_flush_2, k_cnt_flush_3, k_cnt_flush_4,
+                                                   k_cnt_flush_5, k_cnt_flush_6, k_cnt_flush_7, k_cnt_flush_8};
 static const AbsKernel kAbsTimers[ABS_MAXNW + 1] = {nullptr, k_abs_timers_1, k_abs_timers_2, k_abs_timers_3,
                                                     k_abs_timers_4, k_abs_timers_5, k_abs_timers_6, k_abs_timers_7,
                                                     k_abs_timers_8};
@@ -781,12 +788,22 @@ __global__ void k_gen_iota(uint32_t* x, uint64_t n) {
 // live partial matches (StateEvents holding an event) in every list of every processor; with seg_begin /
 // seg_end, of the keys the batch touches only (sg_stats.live_at_batch_start, before the batch kernel)
 __global__ void k_gen_live(const GenProgram* G, const uint32_t* S, uint32_t K, unsigned long long* out,
-                           const uint32_t* seg_begin = nullptr, const uint32_t* seg_end = nullptr) {
+                           const uint32_t* rec, const uint32_t* seg_begin = nullptr, const uint32_t* seg_end = nullptr) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= K) return;
     if (seg_begin && seg_begin[k] >= seg_end[k]) return;
     unsigned long long live = 0;
-    const bool deep = (S[gen_at(K, G->blockWords, G->offST, k, 0)] & GEN_W0_DEEP) != 0u;
+    const uint32_t w0 = S[gen_at(K, G->blockWords, G->offST, k, 0)];
+    if ((w0 & GEN_W0_REG) && rec) {   // the state in its record (GEN_W0_REG)
+        const uint32_t h = rec[k];
+        if (G->cntOk)   // the count partial: one StateEvent in each list it is in
+            live = (h & 15u) ? ((h >> 4) & 1u) + ((h >> 5) & 1u) + 2u * ((h >> 6) & 1u) : 0u;
+        else            // the absent shape: each partial holds its e1 (the seed holds no event)
+            live = h & 15u;
+        if (live) atomicAdd(out, live);
+        return;
+    }
+    const bool deep = (w0 & GEN_W0_DEEP) != 0u;
     for (int p = 0; p < G->nprocs; p++) {
         const uint32_t ks = G->offKS + (uint32_t)p * G->ksWords;
         if (deep && p == G->absP1) {   // (the lists are in the deep store: every entry holds its e1)
@@ -811,10 +828,19 @@ __global__ void k_gen_live(const GenProgram* G, const uint32_t* S, uint32_t K, u
 
 // the smallest event seq any live partial still references: every StreamEvent a list's StateEvent reaches
 // (count chains followed), over every initialised key (the multi-device engine trims its seq maps below it)
-__global__ void k_gen_min_seq(const GenProgram* G, const uint32_t* S, uint32_t K, unsigned long long* out) {
+__global__ void k_gen_min_seq(const GenProgram* G, const uint32_t* S, uint32_t K, unsigned long long* out,
+                              const uint32_t* rec) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     unsigned long long m = ~0ull;
-    if (k < K && (S[gen_at(K, G->blockWords, G->offST, k, 0)] & 1u)) {
+    const uint32_t w0 = k < K ? S[gen_at(K, G->blockWords, G->offST, k, 0)] : 0u;
+    if ((w0 & GEN_W0_REG) && rec) {   // the state in its record (GEN_W0_REG): the events of its partials
+        const uint32_t n = rec[k] & 15u, ew = 5u + G->absNW;
+        for (uint32_t j = 0; j < n && j < GEN_REC_R; j++) {
+            const size_t o = (size_t)(GEN_REC_EV + j * ew) * K + k;
+            const unsigned long long q = (unsigned long long)rec[o] | ((unsigned long long)rec[o + K] << 32);
+            m = q < m ? q : m;
+        }
+    } else if (w0 & 1u) {
         auto W = [&](uint32_t w) { return S[gen_at(K, G->blockWords, G->offST, k, w)]; };
         for (int p = 0; p < G->nprocs; p++) {
             const uint32_t ks = G->offKS + (uint32_t)p * G->ksWords;
@@ -1065,6 +1091,7 @@ struct GenEngine {
     uint32_t *fb2_list = nullptr, *fb2_start = nullptr;  // the wave-per-key kernels' hand-over (absd_kernels.hip)
     uint32_t* deep = nullptr;                             // their deep store (GEN_W0_DEEP): deepWords per key
     uint32_t deepWords = 0;
+    uint32_t* rec = nullptr;   // the register-window kernels' records (GEN_W0_REG): gen_rec_words rows per key
     unsigned long long* fb2_n = nullptr;
     unsigned long long* fb_n = nullptr;
     uint32_t* pay = nullptr;   // the key-sorted payload of the register-window kernel (pack.h Pay<W>)
@@ -1156,6 +1183,7 @@ struct GenEngine {
         a.now0 = now;
         a.deep = deep;
         a.deepWords = deepWords;
+        a.rec = rec;
         return a;
     }
 };
@@ -1289,6 +1317,13 @@ GenEngine* gen_create(const uint32_t* ir, size_t nw, const sg_config& cfg, hipSt
                     e->deepWords = dl.words;
                     e->deep = e->dalloc<uint32_t>((size_t)dl.words * K);
                 }
+            }
+            const uint64_t rw = gen_rec_words(G.absNW, G.cntOk ? 0u : G.Q);
+            const bool regKernels = G.cntOk || (G.playback && G.partitioned && G.nStartup == 1 && e->keyorder);
+            if (regKernels && !getenv("SG_NO_REC") && rw * 4 * K <= (64ull << 30)) {
+                // the register-window kernels' records (GEN_W0_REG): a key's window coalesced across the wave's
+                // keys, written back only where it changed (SG_NO_REC: the blocks, rewritten per touch)
+                e->rec = e->dalloc<uint32_t>((size_t)rw * K);
             }
             e->pay = e->dalloc<uint32_t>(B * 6);  // Pay<4>: 6 words
             e->wstats = e->dalloc<unsigned long long>((size_t)((K + 63) / 64) * GST_N);
@@ -1543,7 +1578,7 @@ int gen_push(GenEngine* e, const sg_batch* b, std::string& msg) {
     a.o.seg_cap = e->rawCap / GEN_RAWSEG;
     if (e->timing)  // sg_stats.live_at_batch_start (outside the batch kernel's span)
         hipLaunchKernelGGL(k_gen_live, dim3((e->K + 255) / 256), dim3(256), 0, e->stream, e->dprog, e->state, e->K,
-                           e->stats + GST_LIVE0, e->seg_begin, e->seg_end);
+                           e->stats + GST_LIVE0, (const uint32_t*)e->rec, e->seg_begin, e->seg_end);
     if (abs_on(e)) {
         // the register-window kernel, then the general kernel over the keys it handed over; this shape
         // emits nothing on events (an absent state's processAndReturn returns nothing; its matches come
@@ -1955,7 +1990,8 @@ void gen_stats(GenEngine* e, sg_stats* out) {
     GH_OK(hipMemcpyAsync(s, e->stats, sizeof(s), hipMemcpyDeviceToHost, e->stream));
     unsigned long long* live = e->live;
     GH_OK(hipMemsetAsync(live, 0, 8, e->stream));
-    hipLaunchKernelGGL(k_gen_live, dim3((e->K + 255) / 256), dim3(256), 0, e->stream, e->dprog, e->state, e->K, live);
+    hipLaunchKernelGGL(k_gen_live, dim3((e->K + 255) / 256), dim3(256), 0, e->stream, e->dprog, e->state, e->K, live,
+                       (const uint32_t*)e->rec);
     unsigned long long lv = 0;
     GH_OK(hipMemcpyAsync(&lv, live, 8, hipMemcpyDeviceToHost, e->stream));
     GH_OK(hipStreamSynchronize(e->stream));
@@ -1977,15 +2013,16 @@ void gen_stats(GenEngine* e, sg_stats* out) {
     out->partials_live = lv;
 }
 
-void gen_flush_deep(GenEngine* e);
+void gen_flush_deep(GenEngine* e, bool rec = true);
 
 uint64_t gen_min_seq(GenEngine* e) {
-    gen_flush_deep(e);
+    gen_flush_deep(e, false);   // (k_gen_min_seq reads the records in place)
     if (!e->minseq) e->minseq = e->dalloc<unsigned long long>(1);
     unsigned long long* m = e->minseq;
     unsigned long long h = ~0ull;
     GH_OK(hipMemcpyAsync(m, &h, 8, hipMemcpyHostToDevice, e->stream));
-    hipLaunchKernelGGL(k_gen_min_seq, dim3((e->K + 255) / 256), dim3(256), 0, e->stream, e->dprog, e->state, e->K, m);
+    hipLaunchKernelGGL(k_gen_min_seq, dim3((e->K + 255) / 256), dim3(256), 0, e->stream, e->dprog, e->state, e->K, m,
+                       (const uint32_t*)e->rec);
     GH_OK(hipMemcpyAsync(&h, m, 8, hipMemcpyDeviceToHost, e->stream));
     GH_OK(hipStreamSynchronize(e->stream));
     return h;
@@ -2058,7 +2095,14 @@ static bool gen_outputs_pending(GenEngine* e) {
 
 // every key whose lists live in the deep store (GEN_W0_DEEP) written back to its block: before anything reads
 // the blocks' lists on the host or in a kernel that does not know the deep store
-void gen_flush_deep(GenEngine* e) {
+void gen_flush_deep(GenEngine* e, bool rec) {
+    if (e->rec && rec) {   // the register-window kernels' records
+        GenArgs a = e->args();
+        const GenArgs& ap = a;
+        hipLaunchKernelGGL(e->host.cntOk ? kCntFlush[e->host.absNW] : kAbsFlush[e->host.absNW], dim3((e->K + 63) / 64),
+                           dim3(64), 0, e->stream, ap);
+        GH_OK(hipGetLastError());
+    }
     if (!e->deep || !absd_on(e)) return;
     GenArgs a = e->args();
     const GenArgs& ap = a;

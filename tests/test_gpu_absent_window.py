@@ -48,14 +48,14 @@ SHAPES = {
 }
 
 
-def _engine(q, n_keys, batch, cap, general, monkeypatch):
+def _engine(q, n_keys, batch, cap, general, monkeypatch, env="SG_NO_ABS"):
     app = sa.parse_app(q)
     cq = sa.compile_query(app, app.queries[0], sa.StringDictionary())
     if general:
-        monkeypatch.setenv("SG_NO_ABS", "1")
+        monkeypatch.setenv(env, "1")
     e = sa.NativeEngine(sa.load_hip_library(), "sg_", cq.ir, n_keys=n_keys, max_batch=batch, partial_capacity=cap,
                         match_capacity=1 << 20)
-    monkeypatch.delenv("SG_NO_ABS", raising=False)
+    monkeypatch.delenv(env, raising=False)
     return cq, e
 
 
@@ -247,3 +247,36 @@ def test_absent_deep_state_across_pushes(monkeypatch):
     assert total > 0
     assert max(live0) >= 100, live0    # hundreds of live partials per touched key carried into a push
     assert gpu.stats()["partials_live"] == ora.stats()["partials_live"]
+
+
+@pytest.mark.parametrize("shape", ["c4", "short_for", "wide_types", "no_every"])
+def test_absent_records_vs_blocks_with_exports_between_pushes(shape, monkeypatch):
+    """the windows in their register-native records (GEN_W0_REG: partials in list order, the timer queue linear
+    from row 0; the default) against the kernels writing the blocks (SG_NO_REC=1) and the oracle, every counter:
+    a state export between pushes writes every record back to its block (the key continues from the block),
+    keys overflowing the window leave the record for the wave-per-key / general kernels and come back"""
+    q = SHAPES[shape]
+    n_keys = 64
+    d = _burst_stream(4000, n_keys, seed=17, max_burst=12)
+    n = len(d["ts"])
+    wide = "double" in q
+    _, rec = _engine(q, n_keys, 4096, 48, False, monkeypatch)
+    _, blk = _engine(q, n_keys, 4096, 48, True, monkeypatch, env="SG_NO_REC")
+    ora = _oracle(q, n_keys)
+    total = 0
+    for i, ch in enumerate(_chunks(n, 400)):
+        total += _drive([rec, blk, ora], d, [ch], wide=wide, start=int(d["ts"][0]) - 3 if i == 0 else None)
+        _stats_equal(rec, blk, ALL)
+        _stats_equal(rec, ora)
+        if i % 3 == 1:
+            assert sd.logical(sd.parse(rec.state_export()), seed_ts=True) == \
+                sd.logical(sd.parse(ora.state_export()), seed_ts=True)
+    for e in (rec, blk, ora):
+        e.advance_time(int(d["ts"][-1]) + 10_000)
+    ms = [e.poll() for e in (rec, blk, ora)]
+    _same(ms[0], ms[1])
+    _same(ms[0], ms[2])
+    assert total + len(ms[0]) > 0
+    assert rec.stats()["window_spills"] > 0 or shape != "c4"   # (bursts of 12 overflow the 8-slot window)
+    assert sd.logical(sd.parse(rec.state_export()), seed_ts=True) == sd.logical(sd.parse(ora.state_export()),
+                                                                                seed_ts=True)

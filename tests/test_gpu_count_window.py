@@ -58,13 +58,13 @@ def _compile(q):
     return sa.compile_query(app, app.queries[0], sa.StringDictionary())
 
 
-def _engine(q, n_keys, batch, general, monkeypatch, mcap=1 << 20):
+def _engine(q, n_keys, batch, general, monkeypatch, mcap=1 << 20, env="SG_NO_CNT"):
     cq = _compile(q)
     if general:
-        monkeypatch.setenv("SG_NO_CNT", "1")
+        monkeypatch.setenv(env, "1")
     e = sa.NativeEngine(sa.load_hip_library(), "sg_", cq.ir, n_keys=n_keys, max_batch=batch, partial_capacity=32,
                         match_capacity=mcap)
-    monkeypatch.delenv("SG_NO_CNT", raising=False)
+    monkeypatch.delenv(env, raising=False)
     return e
 
 
@@ -233,3 +233,29 @@ def test_count_window_handed_over_key_with_two_partials(monkeypatch):
     assert fast.stats()["window_spills"] > 0
     assert _drive([fast, ora2], d, cols, nul, rest[1:]) > 0
     _docs_equal(fast, ora2)
+
+
+@pytest.mark.parametrize("shape", ["c3_min1", "one_eight", "wide_types"])
+def test_count_records_vs_blocks_with_exports_between_pushes(shape, monkeypatch):
+    """the partials in their register-native records (GEN_W0_REG, the default) against the kernel writing the
+    canonical blocks after every run (SG_NO_REC=1) and against the oracle: a state export between pushes
+    writes every record back to its block (the key continues from the block, then from a fresh record), the
+    live-partial counter reads the records in place"""
+    q = SHAPES[shape]
+    n_keys = 64
+    d, cols, nul = _stream(8000, n_keys, seed=41, wide="double" in q)
+    rec = _engine(q, n_keys, 4096, False, monkeypatch)
+    blk = _engine(q, n_keys, 4096, True, monkeypatch, env="SG_NO_REC")
+    ora = _oracle(q, n_keys)
+    total = 0
+    for i, (lo, hi) in enumerate(_chunks(len(d["ts"]), 500)):
+        total += _drive([rec, blk, ora], d, cols, nul, [(lo, hi)])
+        if i % 3 == 2:
+            _docs_equal(rec, ora)
+        sr, sb, so = rec.stats(), blk.stats(), ora.stats()
+        for k in ALL:
+            assert sr[k] == sb[k], (k, sr[k], sb[k])
+        assert sr["partials_live"] == so["partials_live"]
+    assert total > 0
+    _docs_equal(rec, ora)
+    _docs_equal(blk, ora)

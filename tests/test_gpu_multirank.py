@@ -45,3 +45,25 @@ def test_two_rank_rehearsal_equals_single_engine(tmp_path):
     assert len(want) > 1000
     order = lambda a: a[np.lexsort((a[:, 1], a[:, 0]))]
     np.testing.assert_array_equal(order(got), order(want))
+
+
+def test_bench_two_rank_rehearsal_with_host_merge():
+    """bench.py's N > 1 path rehearsed on one GPU (two ranks on device 0, gloo exchange): the JSON line of
+    rank 0 carries the whole-job value and the host timestamp-order merge leg (sg_merge_ts over the ranks'
+    /dev/shm segments), and the segments are removed afterwards"""
+    import glob
+    import json
+    env = dict(os.environ, SG_BENCH_DEVICE="0", SG_BENCH_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", "29519", os.path.join(ROOT, "bench.py"), "--gpus", "2",
+           "--steps", "2", "--warmup", "1", "--keys", "4096", "--batch", str(1 << 16), "--no-cpu", "--no-extra"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["value"] > 0
+    mg = out["merge_inclusive"]
+    assert "error" not in mg, mg
+    assert mg["value"] > 0 and mg["matches_per_step"] > 0 and mg["merge_records_per_s"] > 0
+    assert not glob.glob("/dev/shm/sgmerge_29519_*")

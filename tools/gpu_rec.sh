@@ -9,7 +9,7 @@ export PYTHONUNBUFFERED=1
 TAG=${1:-r04c}
 echo "== tests $(date +%T)"
 timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_count_window.py \
-    tests/test_gpu_absent_window.py tests/test_gpu_sharded.py > gpurun_out/rec_tests_$TAG.log 2>&1 || { grep -E "PASS|FAIL|Error|error|assert" gpurun_out/rec_tests_$TAG.log | tail -40; exit 1; }
+    tests/test_gpu_absent_window.py tests/test_gpu_sharded.py tests/test_gpu_multirank.py > gpurun_out/rec_tests_$TAG.log 2>&1 || { grep -E "PASS|FAIL|Error|error|assert" gpurun_out/rec_tests_$TAG.log | tail -40; exit 1; }
 grep -cE "PASSED" gpurun_out/rec_tests_$TAG.log
 if [ -z "$QUICK" ]; then
 timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_general.py \
