@@ -828,7 +828,7 @@ template <int NW, bool FF> __device__ void abs_batch(const GenArgs& a) {
             if (L.n + 1u > L.cap_n() || L.ql + L.n + 1u > G.Q) break;
             AbsEv<NW> ev;
             if (a.b.pay) {
-                abs_pay<NW>(a, i, tbase, ev);
+                abs_pay<NW>(a, i, tbase, ev);   // (a prefetch of event i + 1 here puts the key object in scratch)
             } else {
                 const uint32_t pos = a.b.sidx ? gp(a.b.sidx)[i] : i;
                 ev.ts = gp(a.b.ts)[pos];

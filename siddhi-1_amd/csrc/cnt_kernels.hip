@@ -507,11 +507,13 @@ template <int NW> __device__ void cnt_batch(const GenArgs& a) {
     unsigned long long ky = 0;
     const int64_t tbase = a.b.pay ? gp(a.b.ts)[0] : 0;  // the payload's ts offsets are from the batch's first ts
     if (walk) {
+        PayAhead<NW> ahead;
+        ahead.first(a, b, e);
         for (uint32_t i = b; i < e; i++) {
             AbsEv<NW> ev;
             uint32_t pos;
             if (a.b.pay) {
-                abs_pay<NW>(a, i, tbase, ev);
+                ahead.next(a, i, e, tbase, ev);
                 pos = (uint32_t)(ev.seq - a.b.seq_base);
             } else {
                 pos = a.b.sidx ? gp(a.b.sidx)[i] : i;

@@ -1210,8 +1210,15 @@ __device__ void gen_wave_stats(const GenArgs& a, unsigned long long sc, unsigned
 // runs instead of the sum over j of the longest run (Poisson runs of a few events per key: one key per
 // lane leaves half of every wave's lane-steps idle).  A wave's 64 lanes still touch 64
 // consecutive keys of one row of the interleaved state at each j.
+// The kernels below read their GenArgs through the kernarg segment pointer instead of the by-value parameter:
+// the interpreter indexes its arrays (columns, null flags) at run time, and taking the parameter's address
+// made the compiler copy all ~600 B of it into scratch at kernel entry — 40 MB of writes per 1,024-wave
+// launch, even when every wave then left at once.
+__device__ __forceinline__ const GenArgs& gen_kernarg() {
+    return *(const GenArgs*)(const void*)__builtin_amdgcn_kernarg_segment_ptr();
+}
 extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GEN_WAVES, 8))) k_gen_batch(const GenArgs ap) {
-    const GenArgs& a = ap;
+    const GenArgs& a = gen_kernarg();
     // a hand-over launch (a fixed grid over a list whose length only the device knows) whose waves have no
     // key leave before the lane object exists: building it (it lives in scratch) wrote ~50 MB per empty launch
     if ((a.mode & GEN_M_KEYLIST) && (unsigned long long)blockIdx.x * 64u >= *a.fb_n) return;
@@ -1446,7 +1453,7 @@ extern "C" __global__ void __launch_bounds__(256) k_gen_collapse(const unsigned 
 #define GEN_TWAVES GEN_WAVES
 #endif
 extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GEN_TWAVES, 8))) k_gen_timers(const GenArgs ap) {
-    const GenArgs& a = ap;
+    const GenArgs& a = gen_kernarg();
 #if GENX_PROF
     const uint64_t t0_ = __builtin_amdgcn_s_memtime();
 #endif

@@ -95,13 +95,17 @@ template <int NW> __device__ void abs_gather(const GenArgs& a, const cGenProgram
 
 // event i of the key-sorted payload (pack.h Pay<W>): the batch position, the attribute words in attribute
 // order (= the window's word layout), the null bits when present, the timestamp offset from ts[0]
-template <int NW> __device__ __forceinline__ void abs_pay(const GenArgs& a, uint32_t i, int64_t tbase, AbsEv<NW>& ev) {
-    constexpr int MW = NW + 3;
+// (split in two so that a walk can load event i + 1's words while it processes event i)
+template <int NW> __device__ __forceinline__ void abs_pay_raw(const GenArgs& a, uint32_t i, uint32_t (&x)[NW + 3]) {
     const uint32_t st = a.b.payStride;
     const gu32* p = gp(a.b.pay) + (size_t)i * st;
-    uint32_t x[MW];
 #pragma unroll
-    for (int q = 0; q < MW; ++q) x[q] = (uint32_t)q < st ? p[q] : 0u;
+    for (int q = 0; q < NW + 3; ++q) x[q] = (uint32_t)q < st ? p[q] : 0u;
+}
+template <int NW> __device__ __forceinline__ void abs_pay_decode(const GenArgs& a, const uint32_t (&x)[NW + 3],
+                                                                 int64_t tbase, AbsEv<NW>& ev) {
+    constexpr int MW = NW + 3;
+    const uint32_t st = a.b.payStride;
     const uint32_t pos = x[0];
 #pragma unroll
     for (int q = 0; q < NW; ++q) ev.w[q] = x[1 + q];
@@ -115,5 +119,27 @@ template <int NW> __device__ __forceinline__ void abs_pay(const GenArgs& a, uint
     ev.ts = (int32_t)toff == SGD_TS_FAR ? gp(a.b.ts)[pos] : tbase + (int64_t)(int32_t)toff;
     ev.seq = a.b.seq_base + pos;
 }
+template <int NW> __device__ __forceinline__ void abs_pay(const GenArgs& a, uint32_t i, int64_t tbase, AbsEv<NW>& ev) {
+    uint32_t x[NW + 3];
+    abs_pay_raw<NW>(a, i, x);
+    abs_pay_decode<NW>(a, x, tbase, ev);
+}
+// the walk's payload words, one event ahead
+template <int NW> struct PayAhead {
+    uint32_t x[NW + 3];
+    __device__ __forceinline__ void first(const GenArgs& a, uint32_t b, uint32_t e) {
+#pragma unroll
+        for (int q = 0; q < NW + 3; ++q) x[q] = 0;
+        if (a.b.pay && b < e) abs_pay_raw<NW>(a, b, x);
+    }
+    // event i decoded, event i + 1's words requested
+    __device__ __forceinline__ void next(const GenArgs& a, uint32_t i, uint32_t e, int64_t tbase, AbsEv<NW>& ev) {
+        uint32_t c[NW + 3];
+#pragma unroll
+        for (int q = 0; q < NW + 3; ++q) c[q] = x[q];
+        if (i + 1 < e) abs_pay_raw<NW>(a, i + 1, x);
+        abs_pay_decode<NW>(a, c, tbase, ev);
+    }
+};
 
 }  // namespace
