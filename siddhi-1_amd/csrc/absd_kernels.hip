@@ -712,6 +712,201 @@ template <int NW, bool FF = false> struct DeepKey {
         stamp(4);
     }
 
+    // ---- m <= 64 consecutive events at once (lane j holds event j: `mine`).  Under the preconditions of
+    // chunkOk — the events' timestamps nondecreasing, the list sorted by ts and none of it later than the first
+    // event, room for every partial the chunk could create and every timer it could schedule — the per-event walk
+    // reduces to one decision per partial: it dies at the first later event that expires it (ts_j - ts > within:
+    // with sorted timestamps the expired entries are always a prefix, as expireEvents takes them) or whose f1
+    // passes (a kill), whichever comes first (expiry is tested before the kill scan of the same event).  So every
+    // partial, old or created in the chunk, is tested against the chunk's events lane-parallel, the survivors
+    // are compacted once, and each event's timer entries (its kills, then its new partial, all at ts_j + T) are
+    // written at once.  The start seed is a scalar chain over the events (f0 tested lane-parallel first).  The
+    // result — lists, seed, lastScheduledTime, queue, work counters — is the per-event walk's.
+    __device__ __forceinline__ int64_t rl64(int64_t x, uint32_t j) const {
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(uint64_t)x, (int)j);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)x >> 32), (int)j);
+        return (int64_t)(((uint64_t)hi << 32) | lo);
+    }
+    __device__ bool chunkOk(const AbsEv<NW>& mine, uint32_t m) const {
+        if (m < 2 || n + m > C || ql + n + 2u * m > Q) return false;
+        const bool act = (uint32_t)lane < m;
+        const int64_t t0 = rl64(mine.ts, 0);
+        const uint32_t pl = (uint32_t)(lane > 0 ? lane - 1 : 0);
+        const uint32_t plo = (uint32_t)__shfl((int)(uint32_t)(uint64_t)mine.ts, (int)pl, 64);
+        const uint32_t phi = (uint32_t)__shfl((int)(uint32_t)((uint64_t)mine.ts >> 32), (int)pl, 64);
+        const int64_t pts = (int64_t)(((uint64_t)phi << 32) | plo);
+        bool bad = act && (mine.ts == -1 || (lane > 0 && mine.ts < pts));
+        for (uint32_t c = 0; c < n; c += 64) {
+            const uint32_t i = c + (uint32_t)lane;
+            if (i < n) {
+                const int64_t t = lts[i];
+                bad = bad || t == -1 || t > t0 || (i + 1 < n && lts[i + 1] < t);
+            }
+        }
+        return !wany(bad);
+    }
+    // the first event (>= start) that expires / kills partial x: m when none
+    __device__ __forceinline__ void fate(const DEnt<NW>& x, uint32_t start, uint32_t m, const AbsEv<NW>& mine,
+                                         const GVal& me0, const GVal& me1, uint32_t& Kx, uint32_t& Ex) {
+        unsigned long long km = 0, em = 0;
+        const bool f1any = G.pre[G.absP1].flen != 0;
+        for (uint32_t j = 0; j < m; j++) {
+            const int64_t tj = rl64(mine.ts, j);
+            if (within != -1 && tj - x.ts > within) em |= 1ull << j;
+            bool kl;
+            if constexpr (FF) {
+                const GVal a0{(uint64_t)rl64((int64_t)me0.b, j), __builtin_amdgcn_readlane(me0.null ? 1 : 0, (int)j) != 0};
+                const GVal a1{(uint64_t)rl64((int64_t)me1.b, j), __builtin_amdgcn_readlane(me1.null ? 1 : 0, (int)j) != 0};
+                kl = !f1any || killTest(hf1, a0, a1, x);
+            } else {
+                AbsEv<NW> ev;
+                ev.ts = tj;
+                ev.seq = (uint64_t)rl64((int64_t)mine.seq, j);
+                ev.nb = (uint32_t)__builtin_amdgcn_readlane((int)mine.nb, (int)j);
+#pragma unroll
+                for (int q = 0; q < NW; ++q) ev.w[q] = (uint32_t)__builtin_amdgcn_readlane((int)mine.w[q], (int)j);
+                kl = evalF1(ev, x);
+            }
+            if (kl) km |= 1ull << j;
+        }
+        const unsigned long long keep = start >= 64u ? 0ull : ~((1ull << start) - 1ull);
+        km &= keep;
+        em &= keep;
+        Kx = km ? (uint32_t)(__ffsll((long long)km) - 1) : m;
+        Ex = em ? (uint32_t)(__ffsll((long long)em) - 1) : m;
+    }
+    __device__ void chunk(const AbsEv<NW>& mine, uint32_t m) {
+        const bool act = (uint32_t)lane < m;
+        // f0 on every event, then the seed in event order (updateState moves a staged seed to pending)
+        bool f0j = false;
+        if (act) {
+            if constexpr (FF) f0j = G.pre[G.absP0].flen == 0 || hoisted_eval<NW>(hf0, mine.w, mine.nb, mine.w, mine.nb);
+            else f0j = evalF0(mine);
+        }
+        const unsigned long long f0m = __ballot(f0j);
+        unsigned long long cm = 0;   // the events that create a partial
+        uint32_t sp = seedPend, ss = seedStg, seedScans = 0, made = 0;
+        int64_t spTs = seedPendTs, ssTs = seedStgTs;
+        for (uint32_t j = 0; j < m; j++) {
+            sp += ss;
+            if (ss) spTs = ssTs;
+            ss = 0;
+            if (sp) {
+                seedScans++;
+                if ((f0m >> j) & 1ull) {
+                    cm |= 1ull << j;
+                    sp = 0;
+                    if (every) {
+                        ss = 1;
+                        ssTs = rl64(mine.ts, j);
+                        made++;
+                    }
+                }
+            }
+        }
+        // f1's event-side operands, once per event (lane j)
+        GVal me0{0, true}, me1{0, true};
+        if constexpr (FF) {
+            if (act) {
+                me0 = evOperand(hf1, 0, mine);
+                me1 = evOperand(hf1, 1, mine);
+            }
+        }
+        unsigned long long scans = 0;
+        uint32_t kc = 0;   // lane j: the partials event j kills
+        auto count_kills = [&](uint32_t kat) {
+            for (uint32_t j = 0; j < m; j++) {
+                const uint32_t c = (uint32_t)__popcll(__ballot(kat == j));
+                if ((uint32_t)lane == j) kc += c;
+            }
+        };
+        const unsigned long long below = (1ull << lane) - 1ull;
+        // the list's partials (pending from event 0 on): fates, then compacted in place (a kept entry only moves
+        // down, below every entry not yet read)
+        uint32_t wpos = 0;
+        for (uint32_t c = 0; c < n; c += 64) {
+            const uint32_t i = c + (uint32_t)lane;
+            DEnt<NW> x{};
+            uint32_t Kx = m, Ex = m;
+            const bool valid = i < n;
+            if (valid) {
+                get(i, x);
+                fate(x, 0u, m, mine, me0, me1, Kx, Ex);
+            }
+            const bool dead = valid && (Ex < m || Kx < m);
+            const uint32_t kat = (valid && Kx < m && Kx < Ex) ? Kx : 64u;
+            if (valid) scans += (unsigned long long)min(min(Ex, Kx + 1u), m);
+            const bool keep = valid && !dead;
+            const unsigned long long km = __ballot(keep);
+            __builtin_amdgcn_s_waitcnt(0);
+            __builtin_amdgcn_wave_barrier();
+            if (keep) put(wpos + (uint32_t)__popcll(km & below), x);
+            wpos += (uint32_t)__popcll(km);
+            __builtin_amdgcn_s_waitcnt(0);
+            __builtin_amdgcn_wave_barrier();
+            if (__ballot(kat < 64u)) count_kills(kat);
+        }
+        // the chunk's new partials (lane j: created at event j, pending from event j + 1 on), appended in order
+        {
+            const bool valid = act && ((cm >> lane) & 1ull);
+            DEnt<NW> x{};
+            uint32_t Kx = m, Ex = m;
+            if (valid) {
+                x.ts = mine.ts;
+                x.seq = mine.seq;
+                x.nb = mine.nb;
+#pragma unroll
+                for (int q = 0; q < NW; ++q) x.w[q] = mine.w[q];
+                if constexpr (FF) keys(hf1, x);
+            }
+            if (__ballot(valid)) fate(x, (uint32_t)lane + 1u, m, mine, me0, me1, Kx, Ex);
+            const bool dead = valid && (Ex < m || Kx < m);
+            const uint32_t kat = (valid && Kx < m && Kx < Ex) ? Kx : 64u;
+            if (valid) {
+                const uint32_t last = min(min(Ex, Kx + 1u), m);
+                scans += last > (uint32_t)lane + 1u ? (unsigned long long)(last - (uint32_t)lane - 1u) : 0ull;
+            }
+            const bool keep = valid && !dead;
+            const unsigned long long km = __ballot(keep);
+            if (keep) put(wpos + (uint32_t)__popcll(km & below), x);
+            wpos += (uint32_t)__popcll(km);
+            __builtin_amdgcn_s_waitcnt(0);
+            __builtin_amdgcn_wave_barrier();
+            if (__ballot(kat < 64u)) count_kills(kat);
+        }
+        n = wpos;
+        np = n - (uint32_t)((cm >> (m - 1u)) & 1ull);   // (created at the last event: still staged)
+        sbad = false;
+        seedPend = sp;
+        seedStg = ss;
+        seedPendTs = spTs;
+        seedStgTs = ssTs;
+        // the timer queue: event j's kills, then its new partial, each at ts_j + T, in event order
+        const uint32_t cnt = act ? kc + (uint32_t)((cm >> lane) & 1ull) : 0u;
+        uint32_t off = cnt;
+        for (int d = 1; d < 64; d <<= 1) {   // inclusive prefix over the lanes
+            const uint32_t o = (uint32_t)__shfl_up((int)off, d, 64);
+            if (lane >= d) off += o;
+        }
+        const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)off, 63);
+        off -= cnt;
+        const int64_t t = mine.ts + waiting;
+        for (uint32_t x = 0; x < cnt; x++) {
+            uint32_t pos = qh + ql + off + x;
+            while (pos >= Q) pos -= Q;
+            lq[pos] = t;
+        }
+        ql += total;
+        const unsigned long long any = __ballot(cnt > 0u);
+        if (any) lst = rl64(t, (uint32_t)(63 - __builtin_clzll(any)));
+        __builtin_amdgcn_s_waitcnt(0);
+        __builtin_amdgcn_wave_barrier();
+        // work counters: each pending partial once per event's kill scan, the seed once per event it is pending
+        for (int d = 32; d > 0; d >>= 1) scans += __shfl_xor(scans, d, 64);
+        scanned += scans + seedScans;
+        created += made;
+    }
+
     // a timer match: a raw record of the general engine (trigger = timer, rank within this key's sweep)
     __device__ void project(uint64_t base, uint32_t r, uint64_t e1seq, int64_t t) {
         const unsigned long long slot = base + r;
@@ -821,6 +1016,7 @@ template <int NW, bool FF> __device__ void absd_batch(const GenArgs& a) {
     uint32_t er = 0;
     const uint64_t nfb = *a.fb_n;
     const int64_t tbase = a.b.pay ? gp(a.b.ts)[0] : 0;
+    const bool noChunk = (a.mode & GEN_M_NOCHUNK) != 0u;
     for (uint64_t li = blockIdx.x; li < nfb; li += gridDim.x) {
         const uint32_t key = __builtin_amdgcn_readfirstlane(gp(a.fb_list)[li]);
         const uint32_t b = __builtin_amdgcn_readfirstlane(gp(a.fb_start)[key]);
@@ -851,28 +1047,46 @@ template <int NW, bool FF> __device__ void absd_batch(const GenArgs& a) {
             if (L.n + 1u > L.C || L.ql + L.n + 1u > G.Q) break;
             AbsEv<NW> ev;
             if (a.b.pay) {
+                // payload words x of one event -> the event
+                auto decode = [&](const uint32_t (&x)[MW], AbsEv<NW>& o) {
+                    const uint32_t pos = x[0];
+#pragma unroll
+                    for (int q = 0; q < NW; ++q) o.w[q] = x[1 + q];
+                    uint32_t toff = 0, nb = 0;
+#pragma unroll
+                    for (int q = 1; q < MW; ++q) {
+                        if ((uint32_t)q == st - 1) toff = x[q];
+                        if (a.b.payNull && (uint32_t)q == st - 2) nb = x[q];
+                    }
+                    o.nb = nb;
+                    o.ts = (int32_t)toff == SGD_TS_FAR ? gp(a.b.ts)[pos] : tbase + (int64_t)(int32_t)toff;
+                    o.seq = a.b.seq_base + pos;
+                };
                 const uint32_t j = (i - b) & 63u;
                 if (j == 0u) {
                     const uint32_t my = i + (uint32_t)(threadIdx.x & 63);
                     const gu32* pp = gp(a.b.pay) + (size_t)my * st;
 #pragma unroll
                     for (int q = 0; q < MW; ++q) pw[q] = (my < e && (uint32_t)q < st) ? pp[q] : 0u;
+                    // the next (up to) 64 events at once when their order and the key's list allow it (chunk)
+                    const uint32_t m = e - i < 64u ? e - i : 64u;
+                    // (the decoded-compare variant only: the interpreter's evaluations per partial and event
+                    // put the interpreting kernel's key object in scratch)
+                    if (FF && !noChunk && m > 1u) {
+                        AbsEv<NW> mine{};
+                        if ((uint32_t)(threadIdx.x & 63) < m) decode(pw, mine);
+                        if (L.chunkOk(mine, m)) {
+                            L.chunk(mine, m);
+                            L.stamp(3);
+                            i += m - 1u;
+                            continue;
+                        }
+                    }
                 }
                 uint32_t x[MW];
 #pragma unroll
                 for (int q = 0; q < MW; ++q) x[q] = (uint32_t)__builtin_amdgcn_readlane((int)pw[q], (int)j);
-                const uint32_t pos = x[0];
-#pragma unroll
-                for (int q = 0; q < NW; ++q) ev.w[q] = x[1 + q];
-                uint32_t toff = 0, nb = 0;
-#pragma unroll
-                for (int q = 1; q < MW; ++q) {
-                    if ((uint32_t)q == st - 1) toff = x[q];
-                    if (a.b.payNull && (uint32_t)q == st - 2) nb = x[q];
-                }
-                ev.nb = nb;
-                ev.ts = (int32_t)toff == SGD_TS_FAR ? gp(a.b.ts)[pos] : tbase + (int64_t)(int32_t)toff;
-                ev.seq = a.b.seq_base + pos;
+                decode(x, ev);
             } else {
                 const uint32_t pos = a.b.sidx ? gp(a.b.sidx)[i] : i;
                 ev.ts = gp(a.b.ts)[pos];

@@ -1092,6 +1092,7 @@ struct GenEngine {
     uint32_t* deep = nullptr;                             // their deep store (GEN_W0_DEEP): deepWords per key
     uint32_t deepWords = 0;
     uint32_t* rec = nullptr;   // the register-window kernels' records (GEN_W0_REG): gen_rec_words rows per key
+    bool absd_nochunk = false; // SG_NO_ABSD_CHUNK: the wave-per-key batch walk event by event
     unsigned long long* fb2_n = nullptr;
     unsigned long long* fb_n = nullptr;
     uint32_t* pay = nullptr;   // the key-sorted payload of the register-window kernel (pack.h Pay<W>)
@@ -1305,6 +1306,7 @@ GenEngine* gen_create(const uint32_t* ir, size_t nw, const sg_config& cfg, hipSt
             e->fb_list = e->dalloc<uint32_t>(K);
             e->fb_start = e->dalloc<uint32_t>(K);
             e->fb_n = e->dalloc<unsigned long long>(1);
+            e->absd_nochunk = getenv("SG_NO_ABSD_CHUNK") != nullptr;
             if (G.absOk && !getenv("SG_NO_ABSD")) {
                 e->fb2_list = e->dalloc<uint32_t>(K);
                 e->fb2_start = e->dalloc<uint32_t>(K);
@@ -1591,7 +1593,10 @@ int gen_push(GenEngine* e, const sg_batch* b, std::string& msg) {
             a.fb2_list = e->fb2_list;
             a.fb2_n = e->fb2_n;
             a.fb2_start = e->fb2_start;
+            const uint32_t m0 = a.mode;
+            if (e->absd_nochunk) a.mode |= GEN_M_NOCHUNK;   // (SG_NO_ABSD_CHUNK: the per-event walk only)
             launch_gen(e, a, GEN_L_ABSD_BATCH);
+            a.mode = m0;
             a.fb_list = e->fb2_list;
             a.fb_n = e->fb2_n;
             a.fb_start = e->fb2_start;

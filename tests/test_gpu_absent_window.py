@@ -280,3 +280,60 @@ def test_absent_records_vs_blocks_with_exports_between_pushes(shape, monkeypatch
     assert rec.stats()["window_spills"] > 0 or shape != "c4"   # (bursts of 12 overflow the 8-slot window)
     assert sd.logical(sd.parse(rec.state_export()), seed_ts=True) == sd.logical(sd.parse(ora.state_export()),
                                                                                 seed_ts=True)
+
+
+@pytest.mark.parametrize("case", ["deep_c4", "deep_short_for", "deep_wide", "bursts_within"])
+def test_absent_deep_chunked_walk_equals_per_event(case, monkeypatch):
+    """the wave-per-key kernel's chunked walk (up to 64 events decided at once: each partial's expiry and kill
+    event found lane-parallel, one compaction, the timer entries written per event) against its per-event walk
+    (SG_NO_ABSD_CHUNK=1) and the oracle: matches, every work counter (partials scanned / created included), live
+    partials and the state documents, with expiry inside the chunks (short `within`) and chunks refused by the
+    preconditions (a list entry later than the chunk's first event, timers near the queue capacity)"""
+    n_keys, burst = 256, 16
+    if case == "deep_c4":
+        q = synth.C4_QUERY
+    elif case == "deep_short_for":
+        q = query(for_="40 milliseconds", within="within 90 milliseconds")
+    elif case == "deep_wide":
+        q = query(schema=WIDE, f1="price > e1.price + 0.5", for_="30 milliseconds", within="within 60 milliseconds")
+    else:
+        q = query(for_="3 milliseconds", within="within 7 milliseconds")
+    push = 1 << 13
+    ms_per_push = push // burst
+    wide = "double" in q
+    app = sa.parse_app(q)
+    cq = sa.compile_query(app, app.queries[0], sa.StringDictionary())
+    mk = lambda: sa.NativeEngine(sa.load_hip_library(), "sg_", cq.ir, n_keys=n_keys, max_batch=push,
+                                 partial_capacity=512, match_capacity=1 << 21, flags=sa.native.SG_CFG_TIMING)
+    chunked = mk()
+    monkeypatch.setenv("SG_NO_ABSD_CHUNK", "1")
+    serial = mk()
+    monkeypatch.delenv("SG_NO_ABSD_CHUNK", raising=False)
+    ora = sa.NativeEngine(build_oracle(), "sgo_", cq.ir, n_keys=n_keys)
+    total = 0
+    for p in range(8):
+        if case == "bursts_within":
+            d = _burst_stream(200, n_keys, seed=300 + p, max_burst=60)   # (<= push events)
+            d["ts"] = d["ts"] + p * 100_000
+        else:
+            d = synth.absent_deep_ticks(p * ms_per_push, ms_per_push, n_keys, burst)
+        for what in ("advance", "push"):
+            for e in (chunked, serial, ora):
+                if what == "advance":
+                    e.advance_time(int(d["ts"][-1]))
+                else:
+                    e.push(0, p * push, d["ts"], [c for c in _cols(d, wide)], None, d["key"])
+            ms = [e.poll() for e in (chunked, serial, ora)]
+            _same(ms[0], ms[1])
+            _same(ms[0], ms[2])
+            total += len(ms[0])
+        _stats_equal(chunked, serial, ALL)
+        _stats_equal(chunked, ora)
+    assert sd.logical(sd.parse(chunked.state_export()), seed_ts=True) == \
+        sd.logical(sd.parse(ora.state_export()), seed_ts=True)
+    for e in (chunked, serial, ora):   # every timer left fires
+        e.advance_time(int(d["ts"][-1]) + 120_000)
+    ms = [e.poll() for e in (chunked, serial, ora)]
+    _same(ms[0], ms[1])
+    _same(ms[0], ms[2])
+    assert total + len(ms[0]) > 0
