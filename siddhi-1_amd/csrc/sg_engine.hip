@@ -1479,8 +1479,32 @@ int sg_engine_create(const void* ir, size_t ir_len, const sg_config* cfg, sg_eng
         const char* pr = getenv("SG_STREAM_PRIO");
         int plo = 0, phi = 0;
         HIP_OK(hipDeviceGetStreamPriorityRange(&plo, &phi));
-        HIP_OK(hipStreamCreateWithPriority(&e->stream, hipStreamNonBlocking, (pr && pr[0] == 'm') ? phi : plo));
-        HIP_OK(hipStreamCreateWithPriority(&e->gstream, hipStreamNonBlocking, (pr && pr[0] == 'g') ? phi : plo));
+        // SG_CUMASK (experiments): "g:a/b" = the grouping stream on the CUs i with i % b < a, "m:a/b" = the main
+        // stream likewise, upper case ("G:a/b", "M:a/b") = the complement (i % b >= a); comma-separated, so that
+        // the two batches in flight can run on disjoint CU sets
+        const char* cm = getenv("SG_CUMASK");
+        auto masked = [&](char which, hipStream_t* st) -> bool {
+            if (!cm) return false;
+            for (const char* q = cm; *q; q++) {
+                if ((q[0] == which || q[0] == which - 32) && q[1] == ':') {
+                    const bool comp = q[0] == which - 32;
+                    unsigned a = 0, b = 1;
+                    if (sscanf(q + 2, "%u/%u", &a, &b) != 2 || b == 0) return false;
+                    int ncu = 0;
+                    HIP_OK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, cfg->device));
+                    std::vector<uint32_t> mk(((size_t)ncu + 31) / 32, 0u);
+                    for (int i = 0; i < ncu; i++)
+                        if (((unsigned)i % b < a) != comp) mk[(size_t)i / 32] |= 1u << (i % 32);
+                    HIP_OK(hipExtStreamCreateWithCUMask(st, (uint32_t)mk.size(), mk.data()));
+                    return true;
+                }
+            }
+            return false;
+        };
+        if (!masked('m', &e->stream))
+            HIP_OK(hipStreamCreateWithPriority(&e->stream, hipStreamNonBlocking, (pr && pr[0] == 'm') ? phi : plo));
+        if (!masked('g', &e->gstream))
+            HIP_OK(hipStreamCreateWithPriority(&e->gstream, hipStreamNonBlocking, (pr && pr[0] == 'g') ? phi : plo));
         HIP_OK(hipStreamCreateWithFlags(&e->pstream, hipStreamNonBlocking));
         e->async_host = (cfg->flags & SG_CFG_ASYNC_HOST) != 0;
         allocate(e);

@@ -20,7 +20,7 @@ import torch  # noqa: E402
 sa = importlib.import_module("siddhi-1_amd")
 synth = importlib.import_module("siddhi-1_amd.synth")
 B, K = 1 << 24, 1 << 20
-KNOBS = ("SG_JIT_EXTRA", "SGD_STAGE_CHUNKS", "SGD_REG_SLOTS", "SG_BUCKET_GROUP")
+KNOBS = ("SG_JIT_EXTRA", "SGD_STAGE_CHUNKS", "SGD_REG_SLOTS", "SG_BUCKET_GROUP", "SG_CUMASK", "SG_STREAM_PRIO")
 
 
 def main():
@@ -33,7 +33,8 @@ def main():
     cq = sa.compile_query(app, app.queries[0], sa.StringDictionary())
     dev = torch.device("cuda", 0)
     bat = []
-    for s in range(nb):
+    pb = int(os.environ.get("SG_EXP_PIPE", "6"))   # more batches, pushed pipelined after the serial ones
+    for s in range(nb + pb):
         d = synth.stock_ticks(s * B, B, K)
         bat.append({k: torch.from_numpy(v.view(np.int32) if v.dtype == np.uint32 else v).to(dev) for k, v in d.items()})
     torch.cuda.synchronize()
@@ -61,7 +62,30 @@ def main():
         eng.synchronize()
         st = eng.stats()
         n = nb - 1
-        print(json.dumps({"variant": name, "env": env,
+        # the pipelined step (bench.py's loop: ready polls, batch s+1's grouping beside batch s's advance)
+        import time
+        eng.synchronize()
+        t0 = time.perf_counter()
+        for s in range(nb, nb + pb):
+            t = bat[s]
+            eng.push(0, s * B, (B, t["ts"].data_ptr(), [t["symbol"].data_ptr(), t["price"].data_ptr(),
+                                                        t["volume"].data_ptr()], t["key"].data_ptr()),
+                     [0, 1, 2], mem=sa.native.SG_MEM_DEVICE)
+            while True:
+                m = eng.poll_device(ready=True)
+                n_m = int(m.n)
+                eng.release(m)
+                if n_m == 0:
+                    break
+        eng.synchronize()
+        while True:
+            m = eng.poll_device()
+            n_m = int(m.n)
+            eng.release(m)
+            if n_m == 0:
+                break
+        step_ms = (time.perf_counter() - t0) / max(1, pb) * 1e3
+        print(json.dumps({"variant": name, "env": env, "pipelined_step_ms": round(step_ms, 4),
                           "group_ms": round((st["group_ns"] - st0["group_ns"]) / 1e6 / n, 4),
                           "advance_ms": round((st["advance_ns"] - st0["advance_ns"]) / 1e6 / n, 4),
                           "order_ms": round((st["order_ns"] - st0["order_ns"]) / 1e6 / n, 4),
