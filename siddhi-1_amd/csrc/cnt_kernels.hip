@@ -377,7 +377,7 @@ template <int NW> struct CntKey {
         if (r >= resEnd) { err |= GERR_MATCHCAP; return; }
         gu32* rec = gp(A.o.raw) + r * A.o.recWords;
         rec[0] = pos;
-        rec[1] = trigRank++;
+        rec[1] = (trigRank++) | GEN_REC_PACKED;   // (the chains packed: the used words contiguous)
         rec[2] = (uint32_t)ev.seq;
         rec[3] = (uint32_t)(ev.seq >> 32);
         rec[4] = (uint32_t)(uint64_t)xts;
@@ -386,15 +386,16 @@ template <int NW> struct CntKey {
         gu32* lens = rec + 7;
         gu32* seqs = lens + G.nslots;
         for (int s = 0; s < G.nslots; s++) lens[s] = s == s0 ? n : (s == evSlot ? 1u : 0u);
+        // packed in slot order: e1's chain (slot s0), then the e2 / e3 event (its slot is s0 + 1 or s0 + 2)
 #pragma unroll
         for (int j = 0; j < CNT_R; ++j) {
             if ((uint32_t)j < n) {
-                seqs[2 * (s0 * G.MC + j)] = (uint32_t)seq[j];
-                seqs[2 * (s0 * G.MC + j) + 1] = (uint32_t)(seq[j] >> 32);
+                seqs[2 * j] = (uint32_t)seq[j];
+                seqs[2 * j + 1] = (uint32_t)(seq[j] >> 32);
             }
         }
-        seqs[2 * (evSlot * G.MC)] = (uint32_t)ev.seq;
-        seqs[2 * (evSlot * G.MC) + 1] = (uint32_t)(ev.seq >> 32);
+        seqs[2 * n] = (uint32_t)ev.seq;
+        seqs[2 * n + 1] = (uint32_t)(ev.seq >> 32);
         gp(A.o.t_cnt)[pos] += 1;
         if (A.mode & GEN_M_TFIRST) gp(A.o.t_first)[pos] = (uint32_t)r;
     }

@@ -312,6 +312,10 @@ struct GenArgs {
 // GenArgs.mode
 #define GEN_M_KEYLIST 1u   // k_gen_batch: lane i walks key fb_list[i] from fb_start[key]
 #define GEN_M_NOPAIRS 2u   // k_gen_timers over fb_list: the collapse pairs were recorded by k_abs_timers
+// a raw match record's word 1 (its rank within the trigger) with this bit: the slot chains are PACKED after the
+// chain lengths, slot by slot in slot order (slot s's entries at the sum of the lengths of the slots before
+// it), instead of at s * MC (cnt_kernels.hip: a match then writes its used words contiguously)
+#define GEN_REC_PACKED 0x80000000u
 #define GEN_M_NOCHUNK 8u   // k_absd_batch*: the per-event walk only (SG_NO_ABSD_CHUNK; A/B and parity tests)
 #define GEN_M_TFIRST 4u    // batch kernels: each trigger emits at most one match; record its raw slot in t_first
                            // (the ordering then gathers output-major, gen_host.hip k_gen_gather1)

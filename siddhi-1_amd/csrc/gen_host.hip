@@ -623,14 +623,17 @@ __device__ void write_out(const OutBufs& o, uint64_t d, const uint32_t* rec, boo
     o.key[d] = rec[6];
     const uint32_t* lens = rec + 7;
     const uint32_t* seqs = lens + o.nslots;
+    const bool packed = (rec[1] & GEN_REC_PACKED) != 0u;
+    uint32_t at = 0;   // (packed: the slot's first entry)
     for (uint32_t s = 0; s < o.nslots; s++) {
         const uint32_t n = lens[s];
         o.len[d * o.nslots + s] = n;
+        const uint32_t b = packed ? at : s * o.MC;
         for (uint32_t c = 0; c < o.MC; c++) {
-            const uint64_t q = c < n ? ((uint64_t)seqs[2 * (s * o.MC + c)] | ((uint64_t)seqs[2 * (s * o.MC + c) + 1] << 32))
-                                     : SG_NULL_SEQ;
+            const uint64_t q = c < n ? ((uint64_t)seqs[2 * (b + c)] | ((uint64_t)seqs[2 * (b + c) + 1] << 32)) : SG_NULL_SEQ;
             o.slot[(d * o.nslots + s) * o.MC + c] = q;
         }
+        at += n;
     }
     for (uint32_t i = 0; i < o.projN; i++) {  // the select list projected at emission (Lane::project)
         const uint32_t* pv = rec + o.projOff + 3 * i;
@@ -651,7 +654,7 @@ __global__ void k_gen_scatter(const uint32_t* raw, const unsigned long long* raw
         if (r - sg * seg_cap >= n) continue;
         const uint32_t* rec = raw + r * o.recWords;
         if (rec[0] >= 0xfffffffeu) continue;
-        write_out(o, *o.count + t_off[rec[0]] + rec[1], rec, false);
+        write_out(o, *o.count + t_off[rec[0]] + (rec[1] & ~GEN_REC_PACKED), rec, false);
     }
 }
 
@@ -706,7 +709,13 @@ __global__ void __launch_bounds__(256) k_gen_gather1(const uint32_t* __restrict_
         const uint32_t q = x / per, y = x % per, sl = y / mc, c = y % mc;
         const uint32_t* r = raw + (uint64_t)rb[w][q] * o.recWords;
         const uint32_t* seqs = r + 7 + ns;
-        o.slot[d0 * per + x] = c < r[7 + sl] ? ((uint64_t)seqs[2 * y] | ((uint64_t)seqs[2 * y + 1] << 32)) : SG_NULL_SEQ;
+        uint32_t b = sl * mc;
+        if (r[1] & GEN_REC_PACKED) {   // (packed chains: after the lengths of the slots before this one)
+            b = 0;
+            for (uint32_t s2 = 0; s2 < sl; s2++) b += r[7 + s2];
+        }
+        o.slot[d0 * per + x] = c < r[7 + sl] ? ((uint64_t)seqs[2 * (b + c)] | ((uint64_t)seqs[2 * (b + c) + 1] << 32))
+                                             : SG_NULL_SEQ;
     }
 }
 
