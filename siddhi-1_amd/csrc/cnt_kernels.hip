@@ -553,8 +553,15 @@ template <int NW> __device__ void cnt_flush(const GenArgs& a) {
 }  // namespace
 
 // One kernel per captured-word count (NW = the stream's attributes as 32-bit words, long / double 2 each).
+// The batch kernel's occupancy floor (waves per SIMD): 4 caps it at 128 VGPRs (150 uncapped: 3 waves), which spills
+// 96 B per lane but hides more of the walk's latency — measured C3 0.165 -> 0.146 ms, C3_min1 0.414 -> 0.386 ms per
+// 4.19M-event batch; 5 (96 VGPRs, 228 B spilled) is 2.7x slower (profiles/r04f/cnt_waves.log)
+#ifndef SG_CNT_WAVES
+#define SG_CNT_WAVES 4
+#endif
+#define CNT_OCC __attribute__((amdgpu_waves_per_eu(SG_CNT_WAVES, 8)))
 #define CNT_KERNELS(NW)                                                                                             \
-    extern "C" __global__ void __launch_bounds__(64) k_cnt_batch_##NW(const GenArgs ap) {           \
+    extern "C" __global__ void __launch_bounds__(64) CNT_OCC k_cnt_batch_##NW(const GenArgs ap) {   \
         cnt_batch<NW>(ap);                                                                                         \
     }                                                                                                              \
     extern "C" __global__ void __launch_bounds__(64) k_cnt_flush_##NW(const GenArgs ap) { cnt_flush<NW>(ap); }
