@@ -929,14 +929,21 @@ template <int NW> __device__ void abs_flush(const GenArgs& a) {
 }  // namespace
 
 // One kernel per captured-word count (NW = the stream's attributes as 32-bit words, long / double 2 each).
+// The batch and timer kernels' occupancy floor (waves per SIMD): 3 brings the timer sweep from 177 VGPRs (2 waves)
+// under 170 with no spill; measured per 4.19M-event batch C4 0.387 -> 0.366 ms, C4_deep 2.08 -> 1.99 ms of kernel
+// time (4: 128 VGPRs, 96-168 B spilled, C4 0.409 ms; profiles/r04f/abs_waves.log)
+#ifndef SG_ABS_WAVES
+#define SG_ABS_WAVES 3
+#endif
+#define ABS_OCC __attribute__((amdgpu_waves_per_eu(SG_ABS_WAVES, 8)))
 #define ABS_KERNELS(NW)                                                                                             \
-    extern "C" __global__ void __launch_bounds__(64) k_abs_batch_##NW(const GenArgs ap) {           \
+    extern "C" __global__ void __launch_bounds__(64) ABS_OCC k_abs_batch_##NW(const GenArgs ap) {   \
         abs_batch<NW, false>(ap);                                                                                  \
     }                                                                                                               \
-    extern "C" __global__ void __launch_bounds__(64) k_abs_batchf_##NW(const GenArgs ap) {          \
+    extern "C" __global__ void __launch_bounds__(64) ABS_OCC k_abs_batchf_##NW(const GenArgs ap) {  \
         abs_batch<NW, true>(ap);                                                                                   \
     }                                                                                                               \
-    extern "C" __global__ void __launch_bounds__(64) k_abs_timers_##NW(const GenArgs ap) {          \
+    extern "C" __global__ void __launch_bounds__(64) ABS_OCC k_abs_timers_##NW(const GenArgs ap) {  \
         abs_timers<NW>(ap);                                                                                        \
     }                                                                                                               \
     extern "C" __global__ void __launch_bounds__(64) k_abs_flush_##NW(const GenArgs ap) { abs_flush<NW>(ap); }
