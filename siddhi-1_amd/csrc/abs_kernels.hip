@@ -818,6 +818,7 @@ template <int NW, bool FF> __device__ void abs_batch(const GenArgs& a) {
         fb = true;
         walk = false;
     }
+
     unsigned long long ky = 0;
     const int64_t tbase = a.b.pay ? gp(a.b.ts)[0] : 0;  // the payload's ts offsets are from the batch's first ts
     if (walk) {
@@ -935,15 +936,15 @@ template <int NW> __device__ void abs_flush(const GenArgs& a) {
 #ifndef SG_ABS_WAVES
 #define SG_ABS_WAVES 3
 #endif
-#define ABS_OCC __attribute__((amdgpu_waves_per_eu(SG_ABS_WAVES, 8)))
+#define ABS_OCC(NW) __attribute__((amdgpu_waves_per_eu((NW) <= 3 ? SG_ABS_WAVES : 1, 8)))   // (wider events: no floor)
 #define ABS_KERNELS(NW)                                                                                             \
-    extern "C" __global__ void __launch_bounds__(64) ABS_OCC k_abs_batch_##NW(const GenArgs ap) {   \
+    extern "C" __global__ void __launch_bounds__(64) ABS_OCC(NW) k_abs_batch_##NW(const GenArgs ap) {   \
         abs_batch<NW, false>(ap);                                                                                  \
     }                                                                                                               \
-    extern "C" __global__ void __launch_bounds__(64) ABS_OCC k_abs_batchf_##NW(const GenArgs ap) {  \
+    extern "C" __global__ void __launch_bounds__(64) ABS_OCC(NW) k_abs_batchf_##NW(const GenArgs ap) {  \
         abs_batch<NW, true>(ap);                                                                                   \
     }                                                                                                               \
-    extern "C" __global__ void __launch_bounds__(64) ABS_OCC k_abs_timers_##NW(const GenArgs ap) {  \
+    extern "C" __global__ void __launch_bounds__(64) ABS_OCC(NW) k_abs_timers_##NW(const GenArgs ap) {  \
         abs_timers<NW>(ap);                                                                                        \
     }                                                                                                               \
     extern "C" __global__ void __launch_bounds__(64) k_abs_flush_##NW(const GenArgs ap) { abs_flush<NW>(ap); }

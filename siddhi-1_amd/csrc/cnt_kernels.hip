@@ -559,9 +559,9 @@ template <int NW> __device__ void cnt_flush(const GenArgs& a) {
 #ifndef SG_CNT_WAVES
 #define SG_CNT_WAVES 4
 #endif
-#define CNT_OCC __attribute__((amdgpu_waves_per_eu(SG_CNT_WAVES, 8)))
+#define CNT_OCC(NW) __attribute__((amdgpu_waves_per_eu((NW) <= 3 ? SG_CNT_WAVES : 1, 8)))   // (wider events: no floor)
 #define CNT_KERNELS(NW)                                                                                             \
-    extern "C" __global__ void __launch_bounds__(64) CNT_OCC k_cnt_batch_##NW(const GenArgs ap) {   \
+    extern "C" __global__ void __launch_bounds__(64) CNT_OCC(NW) k_cnt_batch_##NW(const GenArgs ap) {   \
         cnt_batch<NW>(ap);                                                                                         \
     }                                                                                                              \
     extern "C" __global__ void __launch_bounds__(64) k_cnt_flush_##NW(const GenArgs ap) { cnt_flush<NW>(ap); }
