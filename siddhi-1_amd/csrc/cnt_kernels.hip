@@ -62,9 +62,6 @@ template <int NW> struct CntKey {
     uint32_t f0, fA, fB;      // the processors' flag words
     uint32_t err;
     unsigned long long scanned, created, matches;
-    // this lane's reserved raw match slots (as the general kernel's Lane::project)
-    unsigned long long resBase, resEnd;
-    uint32_t resLeft;
     uint32_t trigRank;
     // the register-native record (GEN_W0_REG; nullptr: the block only): chain events [dirty, n) differ from it
     gu32* R;
@@ -73,8 +70,7 @@ template <int NW> struct CntKey {
 
     __device__ CntKey(const GenArgs& a, uint32_t key)
         : G(*(cGenProgram*)a.G), A(a), S(gp(a.state)), K(a.K), k(key), n(0), xts(-1), inP0p(false), inP0n(false),
-          inL(false), seedN(false), f0(0), fA(0), fB(0), err(0), scanned(0), created(0), matches(0), resBase(0),
-          resEnd(0), resLeft(0), trigRank(0), R(a.rec ? gp(a.rec) : nullptr), dirty(0), wasRec(false) {
+          inL(false), seedN(false), f0(0), fA(0), fB(0), err(0), scanned(0), created(0), matches(0), trigRank(0), R(a.rec ? gp(a.rec) : nullptr), dirty(0), wasRec(false) {
         p0 = G.cntP0;
         pA = G.cntPA;
         pB = G.cntPB;
@@ -365,14 +361,18 @@ template <int NW> struct CntKey {
 
     // ---- a match (QuerySelector input): X with e1's chain and the event in `evSlot` (Lane::project's record)
     __device__ void project(const AbsEv<NW>& ev, uint32_t pos, int evSlot) {
-        if (resLeft == 0) {
-            const uint32_t sg = blockIdx.x % A.o.nseg;
-            resBase = (unsigned long long)sg * A.o.seg_cap + atomicAdd(&A.o.raw_count[sg], (unsigned long long)GEN_RESCHUNK);
-            resEnd = (unsigned long long)(sg + 1) * A.o.seg_cap;
-            resLeft = GEN_RESCHUNK;
-        }
-        const unsigned long long r = resBase++;
-        resLeft--;
+        // one raw slot per match, reserved at once for the lanes of the wave that match here (one atomic per wave
+        // and call site; per-lane chunks left ~2.5 unused slots per matching key, each marked empty by a
+        // scattered store)
+        const unsigned long long act = __ballot(true);
+        const int leader = __ffsll((long long)act) - 1;
+        const uint32_t sg = blockIdx.x % A.o.nseg;
+        unsigned long long base = 0;
+        if ((int)(threadIdx.x & 63) == leader) base = atomicAdd(&A.o.raw_count[sg], (unsigned long long)__popcll(act));
+        base = __shfl(base, leader, 64);
+        const unsigned long long r = (unsigned long long)sg * A.o.seg_cap + base +
+                                     __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
+        const unsigned long long resEnd = (unsigned long long)(sg + 1) * A.o.seg_cap;
         matches++;
         if (r >= resEnd) { err |= GERR_MATCHCAP; return; }
         gu32* rec = gp(A.o.raw) + r * A.o.recWords;
@@ -527,14 +527,6 @@ template <int NW> __device__ void cnt_batch(const GenArgs& a) {
         if (L.R) L.storeRec();
         else L.store();
         ky = 1;
-    }
-    // unused reserved raw slots are marked empty (k_gen_scatter skips them)
-    for (uint32_t x = 0; x < L.resLeft; x++) {
-        const unsigned long long rr = L.resBase + x;
-        if (rr < L.resEnd) {
-            gp(a.o.raw)[rr * a.o.recWords] = 0xffffffffu;
-            gp(a.o.tk1)[rr] = 0xffffffffu;
-        }
     }
     abs_fallback(a, fb, key, b);
     abs_wave_stats(a, L.scanned, L.created, L.matches, ky, L.err, fb ? 1ull : 0ull);
