@@ -292,6 +292,10 @@ def cpu_baseline(sa, synth, n_keys, batch, seconds):
 
     el, busy = two_phase(T, pins, body)
     par = timed / el
+    # each thread's own rate on its shards (events / its busy time) against the one thread alone: the wall-clock
+    # value above is set by the slowest thread, and on a shared host one pinned core can be slowed by other work
+    ev_r = [sum(len(x[1]) for sh in range(r, S, T) for x in shards[sh][1]) for r in range(T)]
+    thr_vs_alone = [round(ev_r[r] / busy[r] / alone, 3) if busy[r] > 0 else None for r in range(T)]
     for e in engs:
         e.close()
     # (iii) C1: unpartitioned, one key, R = 1 event per ms (10,000 events per 10 s window)
@@ -315,6 +319,9 @@ def cpu_baseline(sa, synth, n_keys, batch, seconds):
                                    "one_thread_same_sample": alone,
                                    "pinned_cpus": pins,
                                    "per_thread_scaling": par / alone / T,
+                                   "per_thread_rate_vs_alone": thr_vs_alone,
+                                   "median_thread_vs_alone": sorted(x for x in thr_vs_alone if x is not None)[T // 2]
+                                   if any(x is not None for x in thr_vs_alone) else None,
                                    "vs_single_prefix": par / single / T,
                                    "thread_busy_s": [round(b, 3) for b in busy],
                                    "sample": f"first {total} events of the C2 stream, keys sharded key % {S} (4 shards "
