@@ -259,7 +259,7 @@ def cpu_baseline(sa, synth, n_keys, batch, seconds):
     # threads on SMT siblings share a core, and threads sharing an L3 thrash it (a shard's state is tens of
     # MB at 2^20 keys: one thread alone has the whole L3).  Every engine is created by the thread that runs
     # it, so its memory is first touched on that core's NUMA node.
-    pins = distinct_cores(T)
+    pins = [] if os.environ.get("SG_CPU_NOPIN") else distinct_cores(T)
     engs = [None] * S
 
     def make(sh):
