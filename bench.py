@@ -1075,7 +1075,7 @@ def main():
                         "semantics, DESIGN.md), 1,048,576 keys"),
             "C3_and": (synth.C3_AND_QUERY, lambda s: synth.stock_ticks(s * cb, cb, K), K, cb, 1, 8, False, 4,
                        "C3 with the logical AND: every e1=S[price>20]<1:5>, e2=S[price>e1[last].price] and "
-                       "e3=S[volume>1000] within 10 sec (SEQUENCE), 1,048,576 keys (general kernel)"),
+                       "e3=S[volume>1000] within 10 sec (SEQUENCE), 1,048,576 keys (register-window count kernel)"),
             "P3": (synth.P3_QUERY, lambda s: synth.stock_ticks(s * cb, cb, K), K, cb, 1, 32, False, 0,
                    "3-state pattern: every e1=S[price>20] -> e2=S[price>e1.price] -> e3=S[price>e2.price] within "
                    "10 sec, 1,048,576 keys (general kernel)"),

@@ -337,8 +337,9 @@ template <int NW> struct CntKey {
         const uint64_t b = (ty == SG_T_LONG || ty == SG_T_DOUBLE) ? ((uint64_t)lo | ((uint64_t)hi << 32)) : (uint64_t)lo;
         return GVal{b, ((nbits >> a) & 1u) != 0};
     }
-    // filter of processor p on X: slot s0 = the chain [0, len), slot `evSlot` = the event alone (or none)
-    __device__ bool evalOn(int p, uint32_t len, int evSlot, const AbsEv<NW>& ev) {
+    // filter of processor p on X: slot s0 = the chain [0, len), slots `evSlot` and `evSlot2` (the AND pair's
+    // partner slot, already filled by this event; -1: none) = the event alone
+    __device__ bool evalOn(int p, uint32_t len, int evSlot, const AbsEv<NW>& ev, int evSlot2 = -1) {
         const auto& P = G.pre[p];
         if (P.flen == 0) return true;
         auto var_ = [&](uint32_t s, uint32_t a, int32_t c) -> GVal {
@@ -346,21 +347,22 @@ template <int NW> struct CntKey {
                     const int i = chainIdx(c, len);
                     return i < 0 ? GVal{0, true} : chainAttr(i, a);
                 }
-                if ((int)s == evSlot && chainIdx(c, 1u) == 0) return word(ev.w, ev.nb, a);
+                if (((int)s == evSlot || (int)s == evSlot2) && chainIdx(c, 1u) == 0) return word(ev.w, ev.nb, a);
                 return GVal{0, true};
             };
         if (P.ff.on) return jo_fast(P.ff, var_);   // (gen_engine.h JoFast)
         const GVal v = jo_eval<false>(G.code, P.fpc, P.flen, err, var_,
                                       [&](uint32_t s, int32_t c) -> bool {
                 if ((int)s == s0) return chainIdx(c, len) < 0;
-                if ((int)s == evSlot) return chainIdx(c, 1u) != 0;
+                if ((int)s == evSlot || (int)s == evSlot2) return chainIdx(c, 1u) != 0;
                 return true;
             });
         return !v.null && (v.b & 1);
     }
 
-    // ---- a match (QuerySelector input): X with e1's chain and the event in `evSlot` (Lane::project's record)
-    __device__ void project(const AbsEv<NW>& ev, uint32_t pos, int evSlot) {
+    // ---- a match (QuerySelector input): X with e1's chain and the event in `evSlot` (and, for the AND pair, in
+    // `evSlot2` too) (Lane::project's record)
+    __device__ void project(const AbsEv<NW>& ev, uint32_t pos, int evSlot, int evSlot2 = -1) {
         // one raw slot per match, reserved at once for the lanes of the wave that match here (one atomic per wave
         // and call site; per-lane chunks left ~2.5 unused slots per matching key, each marked empty by a
         // scattered store)
@@ -385,8 +387,8 @@ template <int NW> struct CntKey {
         rec[6] = k;
         gu32* lens = rec + 7;
         gu32* seqs = lens + G.nslots;
-        for (int s = 0; s < G.nslots; s++) lens[s] = s == s0 ? n : (s == evSlot ? 1u : 0u);
-        // packed in slot order: e1's chain (slot s0), then the e2 / e3 event (its slot is s0 + 1 or s0 + 2)
+        for (int s = 0; s < G.nslots; s++) lens[s] = s == s0 ? n : ((s == evSlot || s == evSlot2) ? 1u : 0u);
+        // packed in slot order: e1's chain (slot s0), then the e2 / e3 event (its slots are s0 + 1 and s0 + 2)
 #pragma unroll
         for (int j = 0; j < CNT_R; ++j) {
             if ((uint32_t)j < n) {
@@ -396,6 +398,10 @@ template <int NW> struct CntKey {
         }
         seqs[2 * n] = (uint32_t)ev.seq;
         seqs[2 * n + 1] = (uint32_t)(ev.seq >> 32);
+        if (evSlot2 >= 0) {
+            seqs[2 * n + 2] = (uint32_t)ev.seq;
+            seqs[2 * n + 3] = (uint32_t)(ev.seq >> 32);
+        }
         gp(A.o.t_cnt)[pos] += 1;
         if (A.mode & GEN_M_TFIRST) gp(A.o.t_first)[pos] = (uint32_t)r;
     }
@@ -426,27 +432,32 @@ template <int NW> struct CntKey {
         seedN = false;
         inL = false;
         if (!xP0 && !xL) n = 0;  // a partial only p0's pending held dies at the reset
-        // pA, then pB: X in both pending lists (the partner's filled slot drops it from the second)
+        // pA, then pB: X in both pending lists.  OR (LogicalPreStateProcessor.java:143-180,
+        // LogicalPostStateProcessor.java:59-83): a pass of pA matches and fills e2, and the filled partner slot
+        // drops X from pB unseen; else pB's pass matches.  AND: pA's pass fills e2 and, without e3, only changes
+        // state (X leaves pA's pending, the slot kept); pB then tests X with e2 already this event and matches
+        // when both passed.  Either way X leaves both lists, and a filled slot makes the count state drop it
+        // below — so an AND match needs fA and fB on the same event.  (One call site per filter and one for the
+        // match: each inlined evaluation carries the interpreter, and more copies put the key object in scratch.)
         bool matched = false;
         if (xL) {
-            scanned++;
+            const bool both = G.cntAnd != 0;
+            scanned += 2;
             fA &= ~(uint32_t)GF_CHANGED;
-            if (evalOn(pA, n, sA, ev)) {
-                fA |= GF_CHANGED;
-                xts = ev.ts;
-                project(ev, pos, sA);
-                matched = true;
-            }
-            scanned++;
-            if (!matched) {
+            const bool a = evalOn(pA, n, sA, ev);
+            if (a) fA |= GF_CHANGED;
+            bool bp = false;
+            if (both || !a) {
                 fB &= ~(uint32_t)GF_CHANGED;
-                if (evalOn(pB, n, sB, ev)) {
-                    fB |= GF_CHANGED;
-                    xts = ev.ts;
-                    project(ev, pos, sB);
-                    matched = true;
-                }
+                bp = evalOn(pB, n, sB, ev, (both && a) ? sA : -1);
+                if (bp) fB |= GF_CHANGED;
             }
+            if (both ? (a && bp) : (a || bp)) {
+                xts = ev.ts;
+                const int lo = sA < sB ? sA : sB, hi = sA < sB ? sB : sA;
+                project(ev, pos, both ? lo : (a ? sA : sB), both ? hi : -1);
+            }
+            matched = a || bp;
         }
         // p0: X (its e2 / e3 slot filled: dropped; else the event joins the chain) or the seed
         if (xP0 || sP0) {

@@ -175,6 +175,7 @@ struct GenProgram {
     // them (the receiver's reverse order), cntWE: p0's withinEvery is p0 itself (an expired partial of p0's
     // lists is cloned into it, StreamPreStateProcessor.java:354-357); absNW / absOff give the word layout
     int32_t cntOk, cntP0, cntPA, cntPB, cntWE;
+    int32_t cntAnd, cntPad;   // the pair is a logical AND (`e2=S[fA] and e3=S[fB]`) instead of an OR
     uint32_t absWordAt[ABS_MAXNW];  // the StreamEvent record word (SE_ATTR + ...) of each captured word
 };
 

@@ -367,6 +367,7 @@ bool reg_layout(GenProgram& G) {
 // Anything else stays on the general kernels.
 void cnt_shape(GenProgram& G) {
     G.cntOk = 0;
+    G.cntAnd = 0;
     if (G.qtype != SG_Q_SEQUENCE || !G.partitioned || G.nstreams != 1 || G.nprocs != 3 || G.nslots != 3 ||
         G.nStartup != 0)
         return;
@@ -379,7 +380,8 @@ void cnt_shape(GenProgram& G) {
         P0.minCount > P0.maxCount || P0.countPost != p0)
         return;
     if (PA.kind != GK_LOGICAL || PB.kind != GK_LOGICAL || PA.absent || PB.absent || PA.isStart || PB.isStart ||
-        PA.logicalType != SG_L_OR || PB.logicalType != SG_L_OR || PA.partner != pB || PB.partner != pA)
+        PA.logicalType != PB.logicalType || (PA.logicalType != SG_L_OR && PA.logicalType != SG_L_AND) ||
+        PA.partner != pB || PB.partner != pA)
         return;
     if (Q0.nextStatePre != pA && Q0.nextStatePre != pB) return;
     if (Q0.nextEveryStatePre != p0 || Q0.callbackPre != GEN_NONE || Q0.hasNext) return;
@@ -403,6 +405,7 @@ void cnt_shape(GenProgram& G) {
     G.cntPA = pA;
     G.cntPB = pB;
     G.cntWE = P0.withinEvery == p0 ? 1 : 0;
+    G.cntAnd = PA.logicalType == SG_L_AND ? 1 : 0;
     G.cntOk = getenv("SG_NO_CNT") ? 0 : 1;  // (SG_NO_CNT: A/B timing against the general kernels; same results)
 }
 

@@ -57,7 +57,8 @@ end;
 C3_MIN1_QUERY = C3_QUERY.replace("<2:5>", "<1:5>")
 
 # BASELINE configs[2] names "logical and/or": the C3 shape with the logical AND (e2 and e3 both arrive, in
-# either order, before the sequence moves on; LogicalPreStateProcessor.java:43-202), on the general kernel
+# either order, before the sequence moves on; LogicalPreStateProcessor.java:43-202); under SEQUENCE semantics a
+# match needs both filters on one event (cnt_kernels.hip runs it)
 C3_AND_QUERY = C3_MIN1_QUERY.replace(" or e3=", " and e3=")
 
 # a 3-state pattern (a chain past the two-state kernel's shape, StreamPreStateProcessor.java:364-403 per state),

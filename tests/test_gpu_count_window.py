@@ -31,9 +31,9 @@ WIDE = "define stream S (symbol string, price double, volume long);\n"
 
 
 def query(cnt="<1:5>", fA="price>e1[last].price", fB="volume>1000", within="within 40 milliseconds",
-          schema=STOCK, f0="price>20"):
+          schema=STOCK, f0="price>20", op="or"):
     return (schema + "partition with (symbol of S) begin "
-            f"from every e1=S[{f0}]{cnt}, e2=S[{fA}] or e3=S[{fB}] {within} "
+            f"from every e1=S[{f0}]{cnt}, e2=S[{fA}] {op} e3=S[{fB}] {within} "
             "select e1[0].price as a insert into O; end;")
 
 
@@ -48,6 +48,12 @@ SHAPES = {
     "second_last": query(fA="price>e1[last-1].price", cnt="<1:6>"),
     "wide_types": query(schema=WIDE, fA="price > e1[last].price + 0.25", fB="volume > 1500"),
     "swapped": query(fA="volume>1500", fB="price<e1[last].price"),
+    # the logical AND pair (C3_and): a match needs both filters on one event (the compiler, as the reference's,
+    # does not let e3's filter read its partner e2)
+    "and_min1": query(op="and", fB="volume>700"),
+    "and_one_eight": query(op="and", cnt="<1:8>", f0="price>15", fB="volume>500"),
+    "and_first_entry": query(op="and", fA="price>e1[0].price", fB="volume>300"),
+    "and_wide": query(op="and", schema=WIDE, fA="price > e1[last].price + 0.25", fB="volume > 800"),
 }
 
 ALL = ("matches", "partials_created", "partials_scanned", "keys_touched", "partials_live")
