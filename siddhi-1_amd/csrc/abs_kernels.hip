@@ -948,6 +948,17 @@ template <int NW> __device__ void abs_flush(const GenArgs& a) {
         abs_timers<NW>(ap);                                                                                        \
     }                                                                                                               \
     extern "C" __global__ void __launch_bounds__(64) k_abs_flush_##NW(const GenArgs ap) { abs_flush<NW>(ap); }
+// (narrow events) the same batch / timer kernels at an occupancy floor of 4 (128 VGPRs, ~100 B spilled): the host
+// takes them when a launch has more waves than fit the chip at 3 per SIMD but not more than at 4 (C4_deep's
+// 262,144 keys: 4,096 waves run in one round instead of 1.33, gen_host.hip abs_occ4)
+#define ABS_KERNELS4(NW)                                                                                            \
+    extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8)))                    \
+    k_abs_batchf4_##NW(const GenArgs ap) { abs_batch<NW, true>(ap); }                                              \
+    extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8)))                    \
+    k_abs_timers4_##NW(const GenArgs ap) { abs_timers<NW>(ap); }
+ABS_KERNELS4(1)
+ABS_KERNELS4(2)
+ABS_KERNELS4(3)
 ABS_KERNELS(1)
 ABS_KERNELS(2)
 ABS_KERNELS(3)

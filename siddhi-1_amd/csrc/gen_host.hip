@@ -72,6 +72,11 @@ static const AbsKernel kAbsFlush[ABS_MAXNW + 1] = {nullptr, k_abs_flush_1, k_abs
                                                    k_abs_flush_5, k_abs_flush_6, k_abs_flush_7, k_abs_flush_8};
 static const AbsKernel kCntFlush[ABS_MAXNW + 1] = {nullptr, k_cnt_flush_1, k_cnt_flush_2, k_cnt_flush_3, k_cnt_flush_4,
                                                    k_cnt_flush_5, k_cnt_flush_6, k_cnt_flush_7, k_cnt_flush_8};
+#define ABS4_DECL(NW) extern "C" __global__ void k_abs_batchf4_##NW(const GenArgs ap); \
+    extern "C" __global__ void k_abs_timers4_##NW(const GenArgs ap);
+ABS4_DECL(1) ABS4_DECL(2) ABS4_DECL(3)
+static const AbsKernel kAbsBatchF4[4] = {nullptr, k_abs_batchf4_1, k_abs_batchf4_2, k_abs_batchf4_3};
+static const AbsKernel kAbsTimers4[4] = {nullptr, k_abs_timers4_1, k_abs_timers4_2, k_abs_timers4_3};
 static const AbsKernel kAbsTimers[ABS_MAXNW + 1] = {nullptr, k_abs_timers_1, k_abs_timers_2, k_abs_timers_3,
                                                     k_abs_timers_4, k_abs_timers_5, k_abs_timers_6, k_abs_timers_7,
                                                     k_abs_timers_8};
@@ -1105,6 +1110,8 @@ struct GenEngine {
     uint32_t deepWords = 0;
     uint32_t* rec = nullptr;   // the register-window kernels' records (GEN_W0_REG): gen_rec_words rows per key
     bool absd_nochunk = false; // SG_NO_ABSD_CHUNK: the wave-per-key batch walk event by event
+    bool abs_occ4 = true;      // the occupancy-4 absent kernels where they fit (SG_NO_ABS_OCC4: never)
+    uint32_t ncu = 256;        // compute units of the device
     unsigned long long* fb2_n = nullptr;
     unsigned long long* fb_n = nullptr;
     uint32_t* pay = nullptr;   // the key-sorted payload of the register-window kernel (pack.h Pay<W>)
@@ -1319,6 +1326,13 @@ GenEngine* gen_create(const uint32_t* ir, size_t nw, const sg_config& cfg, hipSt
             e->fb_start = e->dalloc<uint32_t>(K);
             e->fb_n = e->dalloc<unsigned long long>(1);
             e->absd_nochunk = getenv("SG_NO_ABSD_CHUNK") != nullptr;
+            e->abs_occ4 = getenv("SG_NO_ABS_OCC4") == nullptr;
+            {
+                int dev = 0, ncu = 0;
+                GH_OK(hipGetDevice(&dev));
+                GH_OK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+                if (ncu > 0) e->ncu = (uint32_t)ncu;
+            }
             if (G.absOk && !getenv("SG_NO_ABSD")) {
                 e->fb2_list = e->dalloc<uint32_t>(K);
                 e->fb2_start = e->dalloc<uint32_t>(K);
@@ -1448,11 +1462,14 @@ static void launch_gen(GenEngine* e, GenArgs a, int which) {
     }
     else if (which == GEN_L_ABS_BATCH || which == GEN_L_ABS_TIMERS || which == GEN_L_CNT_BATCH) {
         // one lane per key / possible due slot (the due count is on the device); then the waves' counter rows
-        // (the absent kernel's variant for decoded-compare filters when both of its filters are)
+        // (the absent kernel's variant for decoded-compare filters when both of its filters are; the occupancy-4
+        // build when the launch's waves fit the chip at 4 per SIMD but not at 3)
         const bool ff = abs_ff(e);
-        hipLaunchKernelGGL(which == GEN_L_ABS_BATCH   ? (ff ? kAbsBatchF[e->host.absNW] : kAbsBatch[e->host.absNW])
-                           : which == GEN_L_CNT_BATCH ? kCntBatch[e->host.absNW]
-                                                      : kAbsTimers[e->host.absNW],
+        const uint32_t NW = e->host.absNW;
+        const bool occ4 = e->abs_occ4 && NW <= 3 && blocks > 12u * e->ncu && blocks <= 16u * e->ncu;
+        hipLaunchKernelGGL(which == GEN_L_ABS_BATCH   ? (ff ? (occ4 ? kAbsBatchF4[NW] : kAbsBatchF[NW]) : kAbsBatch[NW])
+                           : which == GEN_L_CNT_BATCH ? kCntBatch[NW]
+                                                      : (occ4 ? kAbsTimers4[NW] : kAbsTimers[NW]),
                            dim3(blocks), dim3(64), 0, e->stream, ap);
         hipLaunchKernelGGL(k_gen_stats_reduce, dim3(GST_N, std::min<uint32_t>((blocks + 1023) / 1024, 16u)), dim3(256),
                            0, e->stream, e->wstats, blocks, e->stats);
@@ -2054,8 +2071,10 @@ std::string gen_describe(const GenEngine* e) {
         const GenPre& f0 = G.pre[G.absP0];
         const GenPre& f1 = G.pre[G.absP1];
         const bool ff = (f0.flen == 0 || f0.ff.on) && (f1.flen == 0 || f1.ff.on);
-        push = (ff ? "k_abs_batchf_" : "k_abs_batch_") + nw + " (register window, lane per key)";
-        adv = "k_abs_timers_" + nw + " (register window)";
+        const uint32_t blocks = (e->K + 63) / 64;
+        const bool occ4 = e->abs_occ4 && G.absNW <= 3 && blocks > 12u * e->ncu && blocks <= 16u * e->ncu;
+        push = (ff ? (occ4 ? "k_abs_batchf4_" : "k_abs_batchf_") : "k_abs_batch_") + nw + " (register window, lane per key)";
+        adv = (occ4 ? "k_abs_timers4_" : "k_abs_timers_") + nw + " (register window)";
         if (absd_on(e)) {
             push += (ff ? " + k_absd_batchf_" : " + k_absd_batch_") + nw + " (deep keys, wave per key)";
             adv += (ff ? " + k_absd_timersf_" : " + k_absd_timers_") + nw + " (deep keys)";
