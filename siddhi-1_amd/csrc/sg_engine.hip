@@ -113,17 +113,23 @@ size_t type_size(uint32_t t) {
 // passes over the data instead of three (rocPRIM's gfx950 default for this pair size is 8 bits);
 // 1024 x 16 items per block measured fastest for 2^24 events (tools/sweep/sort_sweep12.hip: 0.460 ms
 // against 0.538 at 1024 x 6 and 0.650 for the default configuration)
+// (MergeSortLimit 4096: rocPRIM's default sorts up to 1M items by block sort + merge passes instead — six merge
+// passes of ~31 us each for a 65,536-event push, against two onesweep passes)
 using Pay16Config = rocprim::radix_sort_config<
     rocprim::default_config, rocprim::default_config,
     rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 16>, rocprim::kernel_config<1024, 16>, 10,
-                                        rocprim::block_radix_rank_algorithm::match>>;
+                                        rocprim::block_radix_rank_algorithm::match>, 4096>;
 
 // wider payloads (16-24 B): rocPRIM's default onesweep for them takes 4-bit digits (5 passes over 2^20 keys);
 // 10-bit digits with 512 x 8 items per block keep the block's LDS within 160 KB and sort 20 key bits in 2
 using PayWideConfig = rocprim::radix_sort_config<
     rocprim::default_config, rocprim::default_config,
     rocprim::radix_sort_onesweep_config<rocprim::kernel_config<512, 8>, rocprim::kernel_config<512, 8>, 10,
-                                        rocprim::block_radix_rank_algorithm::match>>;
+                                        rocprim::block_radix_rank_algorithm::match>, 4096>;
+
+// every other sort: rocPRIM's own onesweep, but from 4096 items up (its default merge-sorts below 2^20)
+using OnesweepConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                                  rocprim::default_config, 4096>;
 
 template <int W>
 hipError_t sort_payload(void* tmp, size_t& tmp_bytes, const uint32_t* keys, uint32_t* skeys, const PackSrc& src,
@@ -139,7 +145,8 @@ hipError_t sort_payload(void* tmp, size_t& tmp_bytes, const uint32_t* keys, uint
             return rocprim::radix_sort_pairs<PayWideConfig>(tmp, tmp_bytes, keys, skeys, it, (Pay<W>*)out, n, b0, bits,
                                                              stream);
     }
-    return rocprim::radix_sort_pairs(tmp, tmp_bytes, keys, skeys, it, (Pay<W>*)out, n, b0, bits, stream);
+    return rocprim::radix_sort_pairs<OnesweepConfig>(tmp, tmp_bytes, keys, skeys, it, (Pay<W>*)out, n, b0, bits,
+                                                      stream);
 }
 
 
@@ -577,7 +584,7 @@ void allocate(sg_engine* e) {
         for (size_t i = 0; i < B; i++) h[i] = (uint32_t)i;
         HIP_OK(hipMemcpy(e->iota, h.data(), B * 4, hipMemcpyHostToDevice));
     }
-    HIP_OK(rocprim::radix_sort_pairs(nullptr, e->sort_tmp_bytes, e->slots[0].b_key, e->slots[0].skeys, e->iota,
+    HIP_OK(rocprim::radix_sort_pairs<OnesweepConfig>(nullptr, e->sort_tmp_bytes, e->slots[0].b_key, e->slots[0].skeys, e->iota,
                                      e->slots[0].sidx, (uint32_t)B, 0, 32, e->stream));
     for (int W = 1; W <= 4; ++W) {
         size_t tb = 0;
@@ -943,7 +950,7 @@ int push(sg_engine* e, const sg_batch* b) {
             }
             HIP_OK(sgd_sort_payload((int)wi, e->sort_tmp, tmp, keys, sl.skeys, ps, sl.pay, n, e->sort_bits, gs));
         } else {
-            HIP_OK(rocprim::radix_sort_pairs(e->sort_tmp, tmp, keys, sl.skeys, e->iota, sl.sidx, n, 0, e->sort_bits,
+            HIP_OK(rocprim::radix_sort_pairs<OnesweepConfig>(e->sort_tmp, tmp, keys, sl.skeys, e->iota, sl.sidx, n, 0, e->sort_bits,
                                              gs));
             pk.sidx = sl.sidx;
             launch(v.pack[role], pack_blocks, 256, &pk, gs);
