@@ -9,7 +9,6 @@
 #include <hip/hip_runtime.h>
 
 #include <rocprim/device/device_merge_sort.hpp>
-#include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
 
 #include <algorithm>
@@ -25,6 +24,7 @@
 #include "../../include/siddhi_gpu_ir.h"
 #include "gen_engine.h"
 #include "pack.h"
+#include "part.h"
 #include "gen_host.h"
 #include "pinned.h"
 #include "state_doc.h"
@@ -593,22 +593,6 @@ GenProgram* gen_build_program(const uint32_t* w, size_t nw, uint32_t partialCap)
     }
 }
 
-// ---------------------------------------------------------------------------------------------
-// device-side helpers of the engine
-// ---------------------------------------------------------------------------------------------
-__global__ void k_gen_bounds(const uint32_t* __restrict__ skeys, uint32_t n, uint32_t K, bool drop_null,
-                             uint32_t* seg_begin, uint32_t* seg_end, uint32_t* err) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t k = skeys[i];
-    if (k >= K) {  // SG_CFG_NULL_KEYS: SG_KEY_NULL events are dropped (null partition key)
-        if (!(drop_null && k == SG_KEY_NULL)) atomicOr(err, (uint32_t)GERR_KEY);
-        return;
-    }
-    if (i == 0 || skeys[i - 1] != k) seg_begin[k] = i;
-    if (i == n - 1 || skeys[i + 1] != k) seg_end[k] = i + 1;
-}
-
 struct OutBufs {
     uint64_t* trig;
     uint64_t* slot;
@@ -1040,10 +1024,6 @@ __global__ void k_timer_scatter(const uint32_t* raw, const unsigned long long* r
     write_out(o, *o.count + koff[rec[6]] + rec[1], rec, true);
 }
 
-// the due keys' sort: onesweep at every size (rocPRIM's default merge-sorts up to 2^20 items: ~20 passes)
-using KeySortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
-                                                 rocprim::default_config, 4096>;
-
 struct TimerLess {
     const uint32_t* k1;
     const int64_t* k2;
@@ -1078,9 +1058,8 @@ struct GenEngine {
     uint32_t* b_key = nullptr;
     std::vector<void*> b_cols;
     std::vector<uint8_t*> b_nulls;
-    uint32_t *skeys = nullptr, *sidx = nullptr, *iota = nullptr, *seg_begin = nullptr, *seg_end = nullptr;
-    void* sort_tmp = nullptr;
-    size_t sort_tmp_bytes = 0;
+    uint32_t *sidx = nullptr, *seg_begin = nullptr, *seg_end = nullptr;
+    PartScratch pscr{};      // the grouping's and the timer sorts' scratch (part.h)
     // matches
     uint32_t* raw = nullptr;
     unsigned long long* raw_count = nullptr;
@@ -1099,8 +1078,6 @@ struct GenEngine {
     uint64_t npairs_cap = 0;
     unsigned long long* pair_key_s = nullptr;
     uint32_t* pair_i_s = nullptr;
-    void* psort_tmp = nullptr;
-    size_t psort_tmp_bytes = 0;
     unsigned long long* live = nullptr;  // k_gen_live's sum (diagnostics)
     unsigned long long* minseq = nullptr;  // k_gen_min_seq's result
     // keys the register-window kernels (abs_kernels.hip) hand to the general kernels
@@ -1117,8 +1094,6 @@ struct GenEngine {
     uint32_t* pay = nullptr;   // the key-sorted payload of the register-window kernel (pack.h Pay<W>)
     unsigned long long* wstats = nullptr;  // its per-wave counter rows
     unsigned long long* tstage = nullptr;  // its staged timer matches
-    void* paysort_tmp = nullptr;
-    size_t paysort_tmp_bytes = 0;
     // timer matches ordered through the due keys (keyorder: partitioned, playback, one listener)
     bool keyorder = false;
     uint32_t *rel = nullptr, *srel = nullptr, *skid = nullptr, *kc = nullptr, *koff_s = nullptr, *koff = nullptr;
@@ -1128,8 +1103,6 @@ struct GenEngine {
     uint64_t htmask = 0;
     unsigned long long* ctr = nullptr;  // k_timer_prep's counters
     uint32_t* ht_ins = nullptr;         // [npairs_cap] the hash slot each due entry filled
-    void* ksort_tmp = nullptr;
-    size_t ksort_tmp_bytes = 0;
     void* kscan_tmp = nullptr;
     size_t kscan_tmp_bytes = 0;
     uint32_t* err = nullptr;
@@ -1242,15 +1215,9 @@ GenEngine* gen_create(const uint32_t* ir, size_t nw, const sg_config& cfg, hipSt
             e->b_cols.push_back(e->dalloc<uint64_t>(B));
             e->b_nulls.push_back(e->dalloc<uint8_t>(B));
         }
-        e->skeys = e->dalloc<uint32_t>(B);
         e->sidx = e->dalloc<uint32_t>(B);
-        e->iota = e->dalloc<uint32_t>(B);
-        hipLaunchKernelGGL(k_gen_iota, dim3((B + 255) / 256), dim3(256), 0, stream, e->iota, (uint64_t)B);
         e->seg_begin = e->dalloc<uint32_t>(K);
         e->seg_end = e->dalloc<uint32_t>(K);
-        GH_OK(rocprim::radix_sort_pairs(nullptr, e->sort_tmp_bytes, e->b_key, e->skeys, e->iota, e->sidx, (uint32_t)B,
-                                        0, 32, stream));
-        e->sort_tmp = e->dalloc<uint8_t>(e->sort_tmp_bytes);
         e->raw = e->dalloc<uint32_t>(e->rawCap * e->recWords);
         e->raw_count = e->dalloc<unsigned long long>(GEN_RAWSEG);
         e->t_cnt = e->dalloc<uint32_t>(B);
@@ -1284,9 +1251,6 @@ GenEngine* gen_create(const uint32_t* ir, size_t nw, const sg_config& cfg, hipSt
                 e->tm.dpair_i = e->dalloc<uint32_t>(e->npairs_cap);
                 e->pair_key_s = e->dalloc<unsigned long long>(e->npairs_cap);
                 e->pair_i_s = e->dalloc<uint32_t>(e->npairs_cap);
-                GH_OK(rocprim::radix_sort_pairs(nullptr, e->psort_tmp_bytes, e->tm.dpair_key, e->pair_key_s,
-                                                e->tm.dpair_i, e->pair_i_s, (size_t)e->npairs_cap, 0, 64, stream));
-                e->psort_tmp = e->dalloc<uint8_t>(e->psort_tmp_bytes);
                 if (G.nStartup == 1) {
                     e->keyorder = true;
                     e->tm.dpair_kid = e->dalloc<uint32_t>(K);
@@ -1307,13 +1271,6 @@ GenEngine* gen_create(const uint32_t* ir, size_t nw, const sg_config& cfg, hipSt
                     e->htmask = hs - 1;
                     e->ht_ins = e->dalloc<uint32_t>(std::max<uint64_t>(e->npairs_cap, 1));
                     GH_OK(hipMemsetAsync(e->ht, 0xff, hs * 8, stream));   // empty; kept empty by k_ht_clear
-                    size_t t1 = 0, t2 = 0;
-                    GH_OK(rocprim::radix_sort_pairs_desc<KeySortConfig>(nullptr, t1, e->rel, e->srel, e->kid_c, e->skid,
-                                                                        (size_t)K, 0, 32, stream));
-                    GH_OK(rocprim::radix_sort_pairs<KeySortConfig>(nullptr, t2, e->hkey_c, e->hkey_s, e->kid_c, e->skid,
-                                                                   (size_t)K, 0, 64, stream));
-                    e->ksort_tmp_bytes = std::max(t1, t2);
-                    e->ksort_tmp = e->dalloc<uint8_t>(e->ksort_tmp_bytes);
                     GH_OK(rocprim::exclusive_scan(nullptr, e->kscan_tmp_bytes, e->kc, e->koff_s, 0u, (size_t)K,
                                                   rocprim::plus<uint32_t>(), stream));
                     e->kscan_tmp = e->dalloc<uint8_t>(e->kscan_tmp_bytes);
@@ -1359,14 +1316,10 @@ GenEngine* gen_create(const uint32_t* ir, size_t nw, const sg_config& cfg, hipSt
                 e->tstage = e->dalloc<unsigned long long>((size_t)K * ABS_R * 2);
                 e->tm.tstage = e->tstage;
             }
-            PackSrc ps{};
-            for (int w = 1; w <= 4; w++)
-                for (uint32_t bq : {16u, 20u, 32u}) {  // (the configurations differ by key width)
-                    size_t tb = 0;
-                    GH_OK(sgd_sort_payload(w, nullptr, tb, e->b_key, e->skeys, ps, nullptr, (uint32_t)B, bq, stream));
-                    e->paysort_tmp_bytes = std::max(e->paysort_tmp_bytes, tb);
-                }
-            e->paysort_tmp = e->dalloc<uint8_t>(e->paysort_tmp_bytes);
+        }
+        {  // the grouping (B events) and the timer sorts (K keys, K x listeners due pairs)
+            const uint64_t sn = std::max<uint64_t>({(uint64_t)B, (uint64_t)K, e->npairs_cap, 1});
+            e->pscr = sgd_part_scratch(e->dalloc<uint8_t>(sgd_part_scratch_bytes(sn)), sn);
         }
         GH_OK(hipMemsetAsync(e->stats, 0, GST_N * 8, stream));
         e->err = e->dalloc<uint32_t>(1);
@@ -1548,8 +1501,6 @@ int gen_push(GenEngine* e, const sg_batch* b, std::string& msg) {
             }
         }
         hipEvent_t g0 = e->timing ? e->ev() : nullptr;
-        uint32_t bits = 1;  // SG_CFG_NULL_KEYS: one value more than the key range (SG_KEY_NULL sorts last)
-        while (bits < 32 && (1ull << bits) < (uint64_t)e->K + (e->null_keys ? 1u : 0u)) bits++;
         // the register-window kernel's grouping carries the events' words through the sort (gathered in
         // arrival order in the first pass, so each key's events end up contiguous, instead of a random
         // gather per event in the walk); other engines sort batch positions
@@ -1582,21 +1533,31 @@ int gen_push(GenEngine* e, const sg_batch* b, std::string& msg) {
             }
             ps.ts = a.b.ts;
         }
+        GroupArgs ga{};
+        ga.n = n;
+        ga.K = e->K;
+        ga.drop_null = e->null_keys ? 1u : 0u;
+        ga.keys = keys;
+        ga.seg_begin = e->seg_begin;
+        ga.seg_end = e->seg_end;
+        ga.err = e->err;
+        ga.s = e->pscr;
         if ((abs_on(e) || cnt_on(e)) && W >= 1 && W <= 4) {
-            size_t tmp = e->paysort_tmp_bytes;
-            GH_OK(sgd_sort_payload((int)W, e->paysort_tmp, tmp, keys, e->skeys, ps, e->pay, n, bits, e->stream));
+            ga.W = W;
+            ga.src = ps;
+            ga.out = e->pay;
+            GH_OK(sgd_group_sorted(ga, e->stream));
             a.b.pay = e->pay;
             a.b.payStride = W + 2;
             a.b.payNull = nul ? 1u : 0u;
             a.b.sidx = e->pay;  // (the general kernel over handed-over keys reads the positions from it)
             a.b.sidxStride = W + 2;
         } else {
-            size_t tmp = e->sort_tmp_bytes;
-            GH_OK(rocprim::radix_sort_pairs(e->sort_tmp, tmp, keys, e->skeys, e->iota, e->sidx, n, 0, bits, e->stream));
+            ga.W = 0;
+            ga.out = e->sidx;
+            GH_OK(sgd_group_sorted(ga, e->stream));
             a.b.sidx = e->sidx;
         }
-        hipLaunchKernelGGL(k_gen_bounds, dim3((n + 255) / 256), dim3(256), 0, e->stream, e->skeys, n, e->K,
-                           e->null_keys, e->seg_begin, e->seg_end, e->err);
         if (g0) e->spans.push_back({g0, e->ev(), 0});
     } else {
         GH_OK(hipMemcpyAsync(e->seg_end, &n, 4, hipMemcpyHostToDevice, e->stream));
@@ -1770,13 +1731,11 @@ int gen_advance(GenEngine* e, int64_t t, std::string& msg) {
             if (!kctr[1]) {
                 int bits = 1;
                 while (bits < 32 && (kctr[0] >> bits) != 0) bits++;
-                size_t tmp = e->ksort_tmp_bytes;
-                GH_OK(rocprim::radix_sort_pairs_desc<KeySortConfig>(e->ksort_tmp, tmp, e->rel, e->srel, e->kid_c, e->skid,
-                                                                    n, 0, bits, e->stream));
+                GH_OK(sgd_sort_pairs(e->rel, e->srel, e->kid_c, e->skid, (uint32_t)n, (uint32_t)bits, false, true, e->pscr,
+                                     e->stream));
             } else {
-                size_t tmp = e->ksort_tmp_bytes;
-                GH_OK(rocprim::radix_sort_pairs<KeySortConfig>(e->ksort_tmp, tmp, e->hkey_c, e->hkey_s, e->kid_c, e->skid,
-                                                               n, 0, 64, e->stream));
+                GH_OK(sgd_sort_pairs(e->hkey_c, e->hkey_s, e->kid_c, e->skid, (uint32_t)n, 64, true, false, e->pscr,
+                                     e->stream));
             }
             if (e->keep_heads) {  // (the sorted keys and their heads, for the multi-device merge)
                 std::vector<uint32_t> rel(n);
@@ -1813,9 +1772,8 @@ int gen_advance(GenEngine* e, int64_t t, std::string& msg) {
         // keys due at the same time only one (chosen by HashMap order) fires at this advance.  That
         // input has no defined result: detect it and fail instead of diverging silently.
         const size_t np = (size_t)(ndue * (uint64_t)G.nStartup);
-        size_t tmpb = e->psort_tmp_bytes;
-        GH_OK(rocprim::radix_sort_pairs(e->psort_tmp, tmpb, e->tm.dpair_key, e->pair_key_s, e->tm.dpair_i, e->pair_i_s,
-                                        np, 0, 64, e->stream));
+        GH_OK(sgd_sort_pairs(e->tm.dpair_key, e->pair_key_s, e->tm.dpair_i, e->pair_i_s, (uint32_t)np, 64, true, false,
+                             e->pscr, e->stream));
         hipLaunchKernelGGL(k_gen_collapse, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, e->stream, e->pair_key_s,
                            e->pair_i_s, (uint64_t)np, e->err);
         check = true;

@@ -464,6 +464,143 @@ __device__ __forceinline__ void glb_emit(const Slab& g, KeySt& s, const Ev& ev, 
     s.gnp = w1;
 }
 
+// ---- the fused grouping: a workgroup's tile split by key (part.h sgd_group_tiles_fused) ------------------------
+// The tile holds the events of the workgroup's SGD_BLOCK keys in arrival order, key & 255 in the position's top
+// byte.  Each wave takes a contiguous share of it, in rounds of 64, and ranks every event among its own earlier
+// events of the same key (wave ballots: "match any" over the 8 key bits, a u16 running count per (wave, key)
+// updated by the group's first lane: no atomics); lane x then turns the waves' counts of key x into the key's run
+// [kb, kb + kc) in the tile and each wave's place in it; the events move to their places (positions cleared of
+// the tag).  The result is what a key sort of the batch gives for these keys: the runs in key order, arrival
+// order within a run (PartitionStreamReceiver.java:175-260).
+__device__ __forceinline__ uint32_t lane_rank(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+__device__ __forceinline__ uint64_t match_key8(uint32_t v, uint64_t act) {
+    uint64_t m = act;
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+        const bool x = (v >> b) & 1u;
+        const uint64_t bb = __ballot(x);
+        m &= x ? bb : ~bb;
+    }
+    return m;
+}
+
+// lane = key: from the waves' counts cnt[w][lane], the key's run (kb, kc) and each wave's place (into cnt)
+template <class C>
+__device__ __forceinline__ void split_places(C* cnt, uint32_t& kb, uint32_t& kc) {
+    constexpr uint32_t NW = SGD_BLOCK / SGD_WAVE;
+    __shared__ uint32_t ws[NW];
+    const uint32_t tid = threadIdx.x, lane = tid & (SGD_WAVE - 1), w = tid / SGD_WAVE;
+    uint32_t cw[NW], t = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < NW; ++q) { cw[q] = cnt[q * SGD_BLOCK + tid]; t += cw[q]; }
+    const uint32_t incl = wave_incl_scan(t, (int)lane);
+    if (lane == SGD_WAVE - 1) ws[w] = incl;
+    __syncthreads();
+    uint32_t run = incl - t;
+    for (uint32_t q = 0; q < w; ++q) run += ws[q];
+    kb = run;
+    kc = t;
+#pragma unroll
+    for (uint32_t q = 0; q < NW; ++q) { cnt[q * SGD_BLOCK + tid] = (C)run; run += cw[q]; }
+    __syncthreads();
+}
+
+// the tile staged in LDS (`run`: element 0), nt <= SGD_SPLIT_CHUNKS(S) * SGD_BLOCK events: every element read into
+// registers before the places are known, written to its place after; cnt: NW * SGD_BLOCK u16 of LDS (after the
+// staging region: dynamic, so the launches without the split do not hold it)
+template <int S>
+__device__ __forceinline__ void tile_split_lds(uint32_t* run, uint32_t nt, uint16_t* cnt, uint32_t& kb, uint32_t& kc) {
+    constexpr uint32_t NW = SGD_BLOCK / SGD_WAVE;
+    constexpr uint32_t MC = SGD_SPLIT_CHUNKS(S);
+    const uint32_t tid = threadIdx.x, lane = tid & (SGD_WAVE - 1), w = tid / SGD_WAVE;
+    for (uint32_t x = tid; x < NW * SGD_BLOCK / 2; x += SGD_BLOCK) ((uint32_t*)cnt)[x] = 0u;
+    __syncthreads();
+    const uint32_t q = ((nt + NW - 1) / NW + SGD_WAVE - 1) & ~(uint32_t)(SGD_WAVE - 1);
+    const uint32_t lo = min(nt, w * q), hi = min(nt, lo + q);
+    uint16_t* mine = cnt + w * SGD_BLOCK;
+    uint32_t rk[MC];
+    uint32_t el[MC][S];
+#pragma unroll
+    for (uint32_t c = 0; c < MC; ++c) {
+        rk[c] = 0;
+        if (lo + c * SGD_WAVE < hi) {  // (wave-uniform)
+            const uint32_t j = lo + c * SGD_WAVE + lane;
+            const bool v = j < hi;
+            uint32_t kl = 0;
+            if (v) {
+#pragma unroll
+                for (int u = 0; u < S; ++u) el[c][u] = run[j * S + u];
+                kl = el[c][0] >> 24;
+            }
+            const uint64_t m = match_key8(kl, __ballot(v));
+            if (v) {
+                const uint32_t before = lane_rank(m);
+                const uint32_t base = mine[kl];
+                if (before == 0) mine[kl] = (uint16_t)(base + (uint32_t)__popcll(m));
+                rk[c] = kl | ((base + before) << 8) | 0x80000000u;
+            }
+        }
+    }
+    __syncthreads();
+    split_places(cnt, kb, kc);
+#pragma unroll
+    for (uint32_t c = 0; c < MC; ++c) {
+        if (rk[c] >> 31) {
+            const uint32_t d = mine[rk[c] & 255u] + ((rk[c] >> 8) & 0x7fffu);
+            el[c][0] &= 0xffffffu;
+#pragma unroll
+            for (int u = 0; u < S; ++u) run[d * S + u] = el[c][u];
+        }
+    }
+    __syncthreads();
+}
+
+// a tile too large for the LDS split: split from `src` (HBM) into `dst` (the key-sorted payload at the tile's
+// place), counted in one pass and placed in a second; cnt: NW * SGD_BLOCK words of LDS
+template <int S>
+__device__ __forceinline__ void tile_split_glb(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, uint32_t nt,
+                                               uint32_t* cnt, uint32_t& kb, uint32_t& kc) {
+    constexpr uint32_t NW = SGD_BLOCK / SGD_WAVE;
+    const uint32_t tid = threadIdx.x, lane = tid & (SGD_WAVE - 1), w = tid / SGD_WAVE;
+    for (uint32_t x = tid; x < NW * SGD_BLOCK; x += SGD_BLOCK) cnt[x] = 0u;
+    __syncthreads();
+    const uint32_t q = ((nt + NW - 1) / NW + SGD_WAVE - 1) & ~(uint32_t)(SGD_WAVE - 1);
+    const uint32_t lo = min(nt, w * q), hi = min(nt, lo + q);
+    uint32_t* mine = cnt + w * SGD_BLOCK;
+    for (uint32_t r0 = lo; r0 < hi; r0 += SGD_WAVE) {  // (wave-uniform trips)
+        const uint32_t j = r0 + lane;
+        const bool v = j < hi;
+        const uint32_t kl = v ? src[(size_t)j * S] >> 24 : 0u;
+        const uint64_t m = match_key8(kl, __ballot(v));
+        if (v && lane_rank(m) == 0) mine[kl] += (uint32_t)__popcll(m);
+    }
+    __syncthreads();
+    split_places(cnt, kb, kc);
+    for (uint32_t r0 = lo; r0 < hi; r0 += SGD_WAVE) {
+        const uint32_t j = r0 + lane;
+        const bool v = j < hi;
+        uint32_t el[S];
+        uint32_t kl = 0;
+        if (v) {
+#pragma unroll
+            for (int u = 0; u < S; ++u) el[u] = src[(size_t)j * S + u];
+            kl = el[0] >> 24;
+        }
+        const uint64_t m = match_key8(kl, __ballot(v));
+        if (v) {
+            const uint32_t before = lane_rank(m);
+            const uint32_t base = mine[kl];
+            if (before == 0) mine[kl] = base + (uint32_t)__popcll(m);
+            el[0] &= 0xffffffu;
+#pragma unroll
+            for (int u = 0; u < S; ++u) dst[(size_t)(base + before) * S + u] = el[u];
+        }
+    }
+    __syncthreads();
+}
+
 // ---- the kernel ---------------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t wave_min_u(uint32_t x) {
     for (int off = 32; off > 0; off >>= 1) x = min(x, (uint32_t)__shfl_xor((int)x, off, SGD_WAVE));
@@ -494,10 +631,13 @@ __device__ __forceinline__ void advance(const P2Params& p, const uint32_t gid) {
     const uint32_t K = p.n_keys;
     // round trip 1: the key's segment of the sorted batch and its header (independent loads)
     const uint32_t wave_id = gid / SGD_WAVE;
+    const bool fused = STG && p.tile_lo != nullptr;  // (uniform) the batch is grouped by tile, split here
     uint32_t b = 0, e = 0, h = 0, dfr = 0, rsm = SGD_NO_RESUME;
     if (k < K) {
-        b = p.seg_begin[k];
-        e = p.seg_end[k];
+        if (!fused) {
+            b = p.seg_begin[k];
+            e = p.seg_end[k];
+        }
         h = p.hdr[k];
     }
     // The staged pass stages the workgroup's runs whole (its keys are consecutive, so their runs are one
@@ -505,18 +645,58 @@ __device__ __forceinline__ void advance(const P2Params& p, const uint32_t gid) {
     // by run length was measured: 22% fewer VALU instructions, no faster — the workgroup's LDS is held
     // until its longest lane ends, so occupancy, not lane idling, bounds the walk.)
     uint32_t blo = 0, bhi = 0, rlo = 0;  // the workgroup's payload range; the wave's first event
+    bool fits = true;
+    bool tile_glb = false;  // fused: the tile was too large for LDS, split into the key-sorted payload in HBM
     if constexpr (STG) {
-        __shared__ uint32_t s_lo[NW], s_hi[NW];
-        const uint32_t nv = e - b;
-        rlo = uni(wave_min_u(nv > 0 ? b : 0xffffffffu));
-        const uint32_t hi = uni(wave_max_u(nv > 0 ? e : 0u));
-        if (lane == 0) { s_lo[wv] = rlo; s_hi[wv] = hi; }
-        __syncthreads();
-        blo = 0xffffffffu;
+        if (fused) {
+            // the workgroup's tile: staged in LDS and split by key there, or (too large: ~1 in 4096 at the C2
+            // density) split into the key-sorted payload in HBM by this workgroup and walked from there (L2)
+            blo = uni(p.tile_lo[blockIdx.x]);
+            bhi = uni(p.tile_lo[blockIdx.x + 1]);
+            const uint32_t nt = bhi - blo;
+            const uint64_t f_lo = (uint64_t)blo * SB / 16u, f_hi = ((uint64_t)bhi * SB + 15u) / 16u;
+            fits = nt <= SGD_SPLIT_CHUNKS(STRIDE) * SGD_BLOCK && f_hi - f_lo <= (uint64_t)p.stage_chunks * NW;
+            uint32_t kb = 0, kc = 0;
+            if (nt > 0 && fits) {
+                const uint32_t nch = (uint32_t)(f_hi - f_lo);
+                const sg_u32x4* src = (const sg_u32x4*)p.tpay + f_lo;
+                for (uint32_t c = wv * SGD_WAVE; c < nch; c += SGD_BLOCK)
+                    if (c + (uint32_t)lane < nch)
+                        __builtin_amdgcn_global_load_lds((sg_glb_ptr)(src + c + lane), (sg_lds_ptr)(sg_stage + c), 16, 0, 0);
+                __builtin_amdgcn_s_waitcnt(0);
+                __syncthreads();
+                uint32_t* tile = (uint32_t*)sg_stage + ((uint64_t)blo * SB - f_lo * 16u) / 4u;
+                tile_split_lds<STRIDE>(tile, nt, (uint16_t*)(sg_stage + (size_t)p.stage_chunks * NW), kb, kc);
+                if (p.write_sorted) {  // every key's run to the key-sorted payload (the aggregators read it)
+                    for (uint32_t x = threadIdx.x; x < nt * STRIDE; x += SGD_BLOCK)
+                        ((uint32_t*)p.payload)[(size_t)blo * STRIDE + x] = tile[x];
+                }
+            } else if (nt > 0) {
+                tile_split_glb<STRIDE>(p.tpay + (size_t)blo * STRIDE, (uint32_t*)p.payload + (size_t)blo * STRIDE, nt,
+                                       (uint32_t*)sg_stage, kb, kc);
+                tile_glb = true;
+                fits = true;
+            }
+            b = blo + kb;
+            e = b + kc;
+            if ((tile_glb || p.write_sorted) && k < K) {
+                p.seg_begin[k] = b;
+                p.seg_end[k] = e;
+            }
+            rlo = uni(wave_min_u(e > b ? b : 0xffffffffu));
+        } else {
+            __shared__ uint32_t s_lo[NW], s_hi[NW];
+            const uint32_t nv = e - b;
+            rlo = uni(wave_min_u(nv > 0 ? b : 0xffffffffu));
+            const uint32_t hi = uni(wave_max_u(nv > 0 ? e : 0u));
+            if (lane == 0) { s_lo[wv] = rlo; s_hi[wv] = hi; }
+            __syncthreads();
+            blo = 0xffffffffu;
 #pragma unroll
-        for (uint32_t w = 0; w < NW; ++w) { blo = min(blo, s_lo[w]); bhi = max(bhi, s_hi[w]); }
-        blo = uni(blo);
-        bhi = uni(bhi);
+            for (uint32_t w = 0; w < NW; ++w) { blo = min(blo, s_lo[w]); bhi = max(bhi, s_hi[w]); }
+            blo = uni(blo);
+            bhi = uni(bhi);
+        }
     }
     bool count_key = true;  // this pass owns the key's keys_touched / live_at_batch_start counts
     if constexpr (!STG) {
@@ -536,14 +716,33 @@ __device__ __forceinline__ void advance(const P2Params& p, const uint32_t gid) {
     const int nev = (int)(e - b);
     if (nev <= 0) h = 0;
     int iters = (int)uni((uint32_t)wave_max(nev));
+    // the HBM pass stages its wave's runs in LDS too when they fit (its keys are consecutive: one range of the
+    // key-sorted payload), so its walk waits on LDS, not on a dependent HBM load per event
+    bool from_lds = STG && !SGX_GLB_WALK && !tile_glb;
+    if constexpr (!STG) {
+        const uint32_t wl = uni(wave_min_u(nev > 0 ? b : 0xffffffffu));
+        const uint32_t wh = uni(wave_max_u(nev > 0 ? e : 0u));
+        if (wh > wl) {
+            const uint64_t h_lo = (uint64_t)wl * SB / 16u, h_hi = ((uint64_t)wh * SB + 15u) / 16u;
+            if (h_hi - h_lo <= (uint64_t)p.hbm_stage_chunks) {
+                blo = wl;
+                bhi = wh;
+                from_lds = true;
+                const uint32_t nch = (uint32_t)(h_hi - h_lo);
+                const sg_u32x4* src = (const sg_u32x4*)p.payload + h_lo;
+                for (uint32_t c = 0; c < nch; c += SGD_WAVE)
+                    if (c + (uint32_t)lane < nch)
+                        __builtin_amdgcn_global_load_lds((sg_glb_ptr)(src + c + lane), (sg_lds_ptr)(sg_stage + c), 16, 0, 0);
+            }
+        }
+    }
     // The workgroup's keys are consecutive, so their runs of the key-sorted payload form ONE
     // contiguous byte range: the waves copy it into LDS with 16-B global_load_lds (all copies in
     // flight at once, no VGPRs) and the lanes then walk their own runs out of LDS (a lane-private walk
     // through HBM touches every line ~8x, once per iteration, and thrashes L2).
     const uint64_t c_lo = (uint64_t)blo * SB / 16u, c_hi = ((uint64_t)bhi * SB + 15u) / 16u;
-    bool fits = true;
     if constexpr (STG) {
-        fits = SGX_GLB_WALK || bhi <= blo || c_hi - c_lo <= (uint64_t)p.stage_chunks * NW;
+        if (!fused) fits = SGX_GLB_WALK || bhi <= blo || c_hi - c_lo <= (uint64_t)p.stage_chunks * NW;
         // this wave's p.deferred entry: 1 = the HBM pass takes the whole workgroup (its range does not
         // fit); keys stopped early raise it to 2 after the walk (written after the barrier below)
         if (lane == 0) p.deferred[wave_id] = (!fits && bhi > blo) ? 1u : 0u;
@@ -633,7 +832,7 @@ __device__ __forceinline__ void advance(const P2Params& p, const uint32_t gid) {
                 next_l0 = p.raw_static + atomicAdd(p.raw_count, (unsigned long long)SGD_RAW_CHUNK);
         }
     }
-    if (!SGX_GLB_WALK && STG && fits && bhi > blo) {
+    if (!SGX_GLB_WALK && STG && !fused && fits && bhi > blo) {  // (fused: staged and split above)
         const uint32_t nch = (uint32_t)(c_hi - c_lo);
         const sg_u32x4* src = (const sg_u32x4*)p.payload + c_lo;
         for (uint32_t c = wv * SGD_WAVE; c < nch; c += SGD_BLOCK)
@@ -674,7 +873,7 @@ __device__ __forceinline__ void advance(const P2Params& p, const uint32_t gid) {
     }
 
     PayEl<STRIDE> cur, nxt;
-    if (run > 0) cur = (STG && !SGX_GLB_WALK) ? lds_pay<STRIDE>(lds_run, b - blo) : load_pay<STRIDE>(p.payload, b);
+    if (run > 0) cur = from_lds ? lds_pay<STRIDE>(lds_run, b - blo) : load_pay<STRIDE>(p.payload, b);
 
 #if SGX_PROF
     uint64_t prof_acc[5] = {0, 0, 0, 0, 0};
@@ -695,8 +894,8 @@ __device__ __forceinline__ void advance(const P2Params& p, const uint32_t gid) {
             }
         }
         if (it + 1 < run)  // next event in flight
-            nxt = (STG && !SGX_GLB_WALK) ? lds_pay<STRIDE>(lds_run, b - blo + (uint32_t)it + 1)
-                      : load_pay<STRIDE>(p.payload, b + (uint32_t)it + 1);
+            nxt = from_lds ? lds_pay<STRIDE>(lds_run, b - blo + (uint32_t)it + 1)
+                           : load_pay<STRIDE>(p.payload, b + (uint32_t)it + 1);
         Ev ev;
         int64_t ts = 0;
         uint32_t bi = 0;
@@ -796,8 +995,11 @@ __device__ __forceinline__ void advance(const P2Params& p, const uint32_t gid) {
             }
             if (c1) {
                 unsigned long long pos = chunk_base + incl - c1;
+                // the staged pass's single match without captures to carry: its e1 seq (a 32-bit offset from the
+                // batch's seq base) rides in the trigger's descriptor, so the ordering reads no raw slot for it
+                const bool inl = STG && SGX_BRANCHLESS && !SGQ_PROJ && c1 == 1u;
                 if (pos + c1 <= p.raw_capacity) {
-                    if (!SGX_NO_TDESC) p.t_desc[bi] = ((uint64_t)c1 << 32) | (uint64_t)(uint32_t)pos;  // count | first slot
+                    if (!SGX_NO_TDESC && !inl) p.t_desc[bi] = ((uint64_t)c1 << 32) | (uint64_t)(uint32_t)pos;  // count | first slot
                 } else {
                     atomicOr(p.err, (uint32_t)SGD_ERR_MATCH_CAP);
                 }
@@ -823,7 +1025,10 @@ __device__ __forceinline__ void advance(const P2Params& p, const uint32_t gid) {
                                 if (SGQ_CAPNULL) cn = here ? W.cn[j] : cn;
 #endif
                             }
-                            if (!SGX_NO_RAW && pos < p.raw_capacity) {
+                            if (inl) {
+                                if (!SGX_NO_TDESC && pos < p.raw_capacity)
+                                    p.t_desc[bi] = SGD_TD_INLINE | (1ull << 32) | (uint64_t)(uint32_t)(int32_t)sq;
+                            } else if (!SGX_NO_RAW && pos < p.raw_capacity) {
                                 p.raw_e1[pos] = sbase + (uint64_t)(int64_t)sq;
 #if SGQ_PROJ
 #pragma unroll
@@ -941,6 +1146,14 @@ __device__ __forceinline__ void advance(const P2Params& p, const uint32_t gid) {
         for (int i = 0; i < 5; ++i) p.prof[(size_t)wave_id * 8 + i] += prof_acc[i];
 #endif
     if (STG && rs != SGD_NO_RESUME) {  // the HBM pass resumes the key
+        if (fused && !tile_glb && !p.write_sorted) {  // (fused: its run was only in LDS)
+            for (int i = 0; i < nev; ++i)
+#pragma unroll
+                for (int u = 0; u < STRIDE; ++u)
+                    ((uint32_t*)p.payload)[(size_t)(b + (uint32_t)i) * STRIDE + u] = lds_run[(size_t)(b - blo + (uint32_t)i) * STRIDE + u];
+            p.seg_begin[k] = b;
+            p.seg_end[k] = e;
+        }
         p.resume[k] = rs;
         p.deferred[wave_id] = 2u;
     }

@@ -1,5 +1,5 @@
-// p2_kernels.hip — ahead-of-time gfx950 kernels around the NFA advance: per-key segment bounds of
-// the key-sorted batch, and the ordered scatter of the emitted matches.  The advance kernel itself is
+// p2_kernels.hip — ahead-of-time gfx950 kernels around the NFA advance: the ordered scatter of the emitted
+// matches, projection, aggregators, purge and the small helpers.  The advance kernel itself is
 // query-specialised and compiled at engine creation (p2_jit.hip, sg_jit.cpp).
 #include <hip/hip_runtime.h>
 
@@ -10,59 +10,6 @@
 #include "../../include/siddhi_gpu_ir.h"
 #include "java_ops.h"
 #include "sg_engine.h"
-
-// ------------------------------------------------------------------------------------------------
-// segment bounds of the key-sorted batch: seg_begin[k], seg_end[k]
-// ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ void seg_bound_one(uint32_t i, uint32_t k, uint32_t prev, uint32_t next, uint32_t n,
-                                              uint32_t n_keys, bool drop_null, uint32_t* __restrict__ seg_begin,
-                                              uint32_t* __restrict__ seg_end, uint32_t* __restrict__ err) {
-    if (k >= n_keys) {  // key id outside [0, n_keys): reject the batch loudly, never write out of bounds
-        // (SG_CFG_NULL_KEYS: an SG_KEY_NULL event is dropped, as the reference drops null-key events)
-        if (!(drop_null && k == 0xffffffffu)) atomicOr(err, (uint32_t)SGD_ERR_KEY_RANGE);
-        // such ids sort after every valid one: the first of them closes the bounds of the keys above
-        // the last valid run (no key keeps a stale segment of an earlier batch)
-        if (prev != k && (i == 0 || prev < n_keys))
-            for (uint32_t g = (i == 0) ? 0u : prev + 1; g < n_keys; ++g) seg_begin[g] = seg_end[g] = i;
-        return;
-    }
-    if (prev != k) {
-        seg_begin[k] = i;
-        // keys between the previous run and this one (or before the first run) have no events
-        for (uint32_t g = (i == 0) ? 0u : prev + 1; g < k && g < n_keys; ++g) seg_begin[g] = seg_end[g] = i;
-    }
-    if (next != k) {
-        seg_end[k] = i + 1;
-        if (i == n - 1)
-            for (uint32_t g = k + 1; g < n_keys; ++g) seg_begin[g] = seg_end[g] = n;
-    }
-}
-
-// four sorted keys per thread (one 16-B load + the neighbours on either side)
-__global__ void __launch_bounds__(256) k_seg_bounds(const uint32_t* __restrict__ skeys, uint32_t n,
-                                                    uint32_t n_keys, bool drop_null, uint32_t* __restrict__ seg_begin,
-                                                    uint32_t* __restrict__ seg_end, uint32_t* __restrict__ err) {
-    // every key gets its bounds written (keys without events get an empty [i, i) at the right spot),
-    // so no memset of the bound arrays is needed per batch
-    const uint32_t i0 = (blockIdx.x * blockDim.x + threadIdx.x) * 4u;
-    if (i0 >= n) return;
-    uint32_t k[6];  // k[0] = previous key, k[1..4] = this thread's keys, k[5] = next key
-    k[0] = (i0 == 0) ? 0xffffffffu : skeys[i0 - 1];
-    if (i0 + 4 <= n) {
-        const uint4 v = *reinterpret_cast<const uint4*>(skeys + i0);
-        k[1] = v.x; k[2] = v.y; k[3] = v.z; k[4] = v.w;
-    } else {
-        for (uint32_t q = 0; q < 4; ++q) k[q + 1] = (i0 + q < n) ? skeys[i0 + q] : 0u;
-    }
-    k[5] = (i0 + 4 < n) ? skeys[i0 + 4] : 0u;
-#pragma unroll
-    for (uint32_t q = 0; q < 4; ++q) {
-        const uint32_t i = i0 + q;
-        if (i >= n) break;
-        const uint32_t next = (i == n - 1) ? n_keys : k[q + 2];
-        seg_bound_one(i, k[q + 1], (i == 0) ? 0xffffffffu : k[q], next, n, n_keys, drop_null, seg_begin, seg_end, err);
-    }
-}
 
 // ------------------------------------------------------------------------------------------------
 // match ordering: batch event t's matches go to out_count + (exclusive prefix of the per-event counts
@@ -92,7 +39,7 @@ __global__ void __launch_bounds__(256) k_order_sums(const uint64_t* __restrict__
     uint32_t c = 0;
     for (uint32_t j = 0; j < SGD_ORDER_TILE / 256; ++j) {
         const uint32_t t = base + j * 256 + threadIdx.x;
-        if (t < n) c += (uint32_t)(t_desc[t] >> 32);
+        if (t < n) c += (uint32_t)(t_desc[t] >> 32) & 0x7fffffffu;
     }
     for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
     if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = c;
@@ -110,8 +57,8 @@ __global__ void __launch_bounds__(256) k_order_scatter(const ScatterParams s, ui
     __shared__ uint32_t wtot[ROWS][4];
     __shared__ uint32_t owner[WIN];          // window record -> tile-local trigger index
     __shared__ uint32_t loc[SGD_ORDER_TILE]; // tile-local trigger -> its first record (tile-local)
-    __shared__ uint16_t cnt[SGD_ORDER_TILE]; // tile-local trigger -> its record count (<= SGD_MAX_CAP)
-    __shared__ uint32_t fst[SGD_ORDER_TILE]; // tile-local trigger -> its first raw slot
+    __shared__ uint16_t cnt[SGD_ORDER_TILE]; // tile-local trigger -> its record count (<= SGD_MAX_CAP) | inline << 15
+    __shared__ uint32_t fst[SGD_ORDER_TILE]; // tile-local trigger -> its first raw slot (inline: e1 seq - seq_base)
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t base = blockIdx.x * SGD_ORDER_TILE;
     uint64_t d[ROWS];
@@ -123,7 +70,7 @@ __global__ void __launch_bounds__(256) k_order_scatter(const ScatterParams s, ui
     uint32_t incl[ROWS];
 #pragma unroll
     for (int j = 0; j < ROWS; ++j) {
-        incl[j] = ord_wave_incl_scan((uint32_t)(d[j] >> 32), lane);
+        incl[j] = ord_wave_incl_scan((uint32_t)(d[j] >> 32) & 0x7fffffffu, lane);
         if (lane == 63) wtot[j][wv] = incl[j];
     }
     __syncthreads();
@@ -137,10 +84,10 @@ __global__ void __launch_bounds__(256) k_order_scatter(const ScatterParams s, ui
             before += (w < wv) ? x : 0u;
             row += x;
         }
-        const uint32_t c = (uint32_t)(d[j] >> 32);
+        const uint32_t c = (uint32_t)(d[j] >> 32) & 0x7fffffffu;
         const uint32_t tl = j * 256 + threadIdx.x;
         loc[tl] = running + before + incl[j] - c;
-        cnt[tl] = (uint16_t)c;
+        cnt[tl] = (uint16_t)(c | ((d[j] & SGD_TD_INLINE) ? 0x8000u : 0u));
         if (s.out_first && base + tl < s.n) {  // aggregators: where each trigger's records start
             const uint64_t r = (*s.out_count + s.tile_off[blockIdx.x] + loc[tl]) % s.capacity;
             s.out_first[base + tl] = c ? (((uint64_t)c << 32) | r) : 0ull;
@@ -163,7 +110,7 @@ __global__ void __launch_bounds__(256) k_order_scatter(const ScatterParams s, ui
 #pragma unroll 1
         for (int j = 0; j < ROWS; ++j) {
             const uint32_t tl = j * 256 + threadIdx.x;
-            const uint32_t l0 = loc[tl], c = cnt[tl];
+            const uint32_t l0 = loc[tl], c = cnt[tl] & 0x7fffu;
             const uint32_t a = max(l0, w0), b = min(l0 + c, w1);
             for (uint32_t r = a; r < b; ++r) owner[r - w0] = tl;
         }
@@ -177,7 +124,9 @@ __global__ void __launch_bounds__(256) k_order_scatter(const ScatterParams s, ui
             if (o >= s.capacity) o -= s.capacity;
             s.o_trig[o] = trig;
             // {e1 seq, e2 seq} as one 16-B store
-            const uint64_t e1 = (SG_EXP(s.exp) & 1) ? 0ull : s.raw_e1[fst[tl] + (q - loc[tl])];
+            const uint64_t e1 = (SG_EXP(s.exp) & 1) ? 0ull
+                                : (cnt[tl] & 0x8000u) ? s.seq_base + (uint64_t)(int64_t)(int32_t)fst[tl]
+                                                      : s.raw_e1[fst[tl] + (q - loc[tl])];
             *reinterpret_cast<ulonglong2*>(s.o_slot + 2 * o) = make_ulonglong2(e1, trig);
             s.o_key[o] = s.key ? s.key[t] : 0u;
             s.o_ts[o] = s.ts[t];  // StreamPostStateProcessor.java:68: StateEvent ts = ts of the e2 event
@@ -395,14 +344,6 @@ __global__ void __launch_bounds__(256) k_min_seq(const uint32_t* __restrict__ hd
 // ------------------------------------------------------------------------------------------------
 // launch wrappers
 // ------------------------------------------------------------------------------------------------
-int sgd_launch_bounds(const uint32_t* skeys, uint32_t n, uint32_t n_keys, bool drop_null, uint32_t* seg_begin,
-                      uint32_t* seg_end, uint32_t* err, ihipStream_t* stream) {
-    if (n == 0) return 0;
-    hipLaunchKernelGGL(k_seg_bounds, dim3((n + 1023) / 1024), dim3(256), 0, stream, skeys, n, n_keys, drop_null,
-                       seg_begin, seg_end, err);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
 int sgd_launch_reset_keys(const uint32_t* keys, uint32_t n, uint32_t n_keys, uint32_t* hdr, uint32_t* err,
                           ihipStream_t* stream) {
     if (n == 0) return 0;

@@ -1,5 +1,5 @@
-// pack.h — the key-sorted payload element of the two-state engine and its gather from the SoA batch
-// columns (shared by the rocPRIM grouping in sg_engine.hip and the tile grouping in grp_kernels.hip)
+// pack.h — the key-sorted payload element of the engines and its gather from the SoA batch columns (the first
+// pass of the grouping, part_kernels.hip)
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -59,10 +59,3 @@ template <int W> struct PackFn {
         return o;
     }
 };
-
-// the key-sorted payload grouping (sg_engine.hip): radix sort of the key ids on bits [b0, bits) carrying Pay<W>
-// (W = 1..4) gathered from the SoA columns by PackFn in the first pass; tmp == nullptr queries tmp_bytes.
-// b0 = SGD_BK_BITS: one pass on the bucket bits only, the split inside each bucket is sgd_bucket_split's
-hipError_t sgd_sort_payload(int W, void* tmp, size_t& tmp_bytes, const uint32_t* keys, uint32_t* skeys,
-                            const PackSrc& src, void* out, uint32_t n, uint32_t bits, hipStream_t stream,
-                            uint32_t b0 = 0);

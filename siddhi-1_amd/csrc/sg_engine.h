@@ -33,7 +33,13 @@
 // advance kernel reads its full timestamp from the batch's ts column
 #define SGD_TS_FAR ((int32_t)0x80000000)
 #define SGD_TS_LIM (1ll << 30)
-#define SGD_RAW_CHUNK 256  // raw match slots a wave reserves at a time (the raw buffer has 2 chunks of slack per wave)
+#define SGD_RAW_CHUNK 256
+#define SGD_TD_INLINE (1ull << 63)  // t_desc: the trigger's one match carried inline (no raw slot)
+// the fused grouping's LDS split keeps up to this many 64-event rounds per wave in registers (p2_jit.hip
+// tile_split_lds): a tile of more than SGD_SPLIT_CHUNKS(stride) * SGD_BLOCK events goes to the HBM pass
+#define SGD_SPLIT_CHUNKS(stride) (80u / ((stride) + 1u))
+#define SGD_SPLIT_CNT_BYTES ((SGD_BLOCK / SGD_WAVE) * SGD_BLOCK * 2u)   // its per-(wave, key) u16 counters
+#define SGD_HBM_STAGE_BYTES 32768u  // the HBM pass: LDS staging of one wave's runs (dynamic LDS of its 1-wave groups)  // raw match slots a wave reserves at a time (the raw buffer has 2 chunks of slack per wave)
 
 // ---- filters ------------------------------------------------------------------------------------
 // A filter's IR bytecode (siddhi_gpu_ir.h) is lowered to DProg (variables resolved to event
@@ -87,8 +93,16 @@ struct P2Params {
     // key-sorted batch: element i = [batch position][filter column words..][null bits?][ts lo, hi]
     const uint32_t* payload;
     const int64_t* ts_col;             // the batch's timestamps in arrival order (ts_col[0]: the offsets' base)
-    const uint32_t* seg_begin;         // [n_keys]
-    const uint32_t* seg_end;           // [n_keys]
+    uint32_t* seg_begin;               // [n_keys] (fused grouping: written by the staged pass for the keys it
+    uint32_t* seg_end;                 //  leaves to the HBM pass, whose runs it writes to `payload`)
+    // fused grouping (part.h sgd_group_tiles_fused; null: `payload` is key-sorted with seg_begin / seg_end): the
+    // batch grouped by key tile (one tile = the SGD_BLOCK keys of one workgroup, arrival order within a tile,
+    // position bits 24..31 = key & 255) in `tpay`, tile t at [tile_lo[t], tile_lo[t + 1]); the staged pass splits
+    // its tile by key in LDS
+    const uint32_t* tile_lo;
+    const uint32_t* tpay;
+    uint32_t write_sorted;             // fused: also write every key's run to `payload` + seg bounds (aggregators)
+    uint32_t hbm_stage_chunks;         // the HBM pass's LDS staging per wave (16-B chunks; its dynamic LDS)
     // per-key state (SoA, partial j of key k at j * n_keys + k)
     uint32_t* hdr;
     int64_t* p_ts;
@@ -101,7 +115,8 @@ struct P2Params {
     uint64_t* raw_e1;
     unsigned long long* raw_count;
     uint64_t raw_capacity;
-    uint64_t* t_desc;                  // [max_batch] count << 32 | first raw slot; zero outside the
+    uint64_t* t_desc;                  // [max_batch] count << 32 | first raw slot, or (SGD_TD_INLINE) one match
+                                       // whose e1 seq - seq_base is the low word; zero outside the
                                        // advance -> scatter window
     unsigned long long* stats;         // [SGD_ST_N] cumulative (HBM pass adds here directly)
     unsigned long long* wstats;        // [n_keys / 64][SGD_ST_N] staged pass, this batch (k_stats_reduce)
@@ -134,8 +149,6 @@ struct PackParams {
 
 // ahead-of-time launch wrappers (p2_kernels.hip)
 struct ihipStream_t;
-int sgd_launch_bounds(const uint32_t* sorted_keys, uint32_t n, uint32_t n_keys, bool drop_null, uint32_t* seg_begin,
-                      uint32_t* seg_end, uint32_t* err, ihipStream_t* stream);
 // ordered output of one batch: o_*[(out_count + t_off[t] + r) % capacity] for the r-th match of batch event t
 struct ScatterParams {
     uint32_t n;

@@ -4,22 +4,18 @@
 // partition key resident in HBM (SoA slabs sized n_keys x partial_capacity), and per pushed
 // micro-batch runs:
 //   1. (host batches only) H2D copy of the SoA columns the filters read
-//   2. key grouping: stable LSD radix sort of (key id -> batch position) on ceil(log2 n_keys) bits
-//      (rocPRIM onesweep), then per-key segment bounds            — replaces the key-run grouping
-//      of PartitionStreamReceiver.receive(Event[]) (partition/PartitionStreamReceiver.java:175-260)
-//      and the per-key state lookup (util/snapshot/state/PartitionStateHolder.java:43-80)
-//   3. k_p2_advance: one lane per key advances that key's NFA over its events in arrival order
+//   2. key grouping (part_kernels.hip, hand-written): the batch stably partitioned by key tile (the 256 keys of
+//      one advance workgroup), the split by key happening inside the advance kernel's LDS staging (fused); or,
+//      for batches too dense per tile, LSD passes to a key-sorted payload + per-key segment bounds — replaces
+//      the key-run grouping of PartitionStreamReceiver.receive(Event[]) (partition/PartitionStreamReceiver.java:
+//      175-260) and the per-key state lookup (util/snapshot/state/PartitionStateHolder.java:43-80)
+//   3. k_adv_m: one lane per key advances that key's NFA over its events in arrival order
 //      (query/input/stream/state/StreamPreStateProcessor.java:308-403 and friends)
 // and on poll orders the accumulated matches by trigger seq (stable: per-key emission order kept).
 //
 // Query shapes outside the specialised two-state kernel (count, logical, SEQUENCE, absent states,
 // longer chains) run on the general device engine (gen_host.hip / gen_kernels.hip).
 #include <hip/hip_runtime.h>
-
-#include <rocprim/device/device_radix_sort.hpp>
-#include <rocprim/device/device_scan.hpp>
-#include <rocprim/iterator/counting_iterator.hpp>
-#include <rocprim/iterator/transform_iterator.hpp>
 
 #include <algorithm>
 #include <cmath>
@@ -34,8 +30,8 @@
 #include "../../include/siddhi_gpu_ir.h"
 #include "gen_engine.h"
 #include "gen_host.h"
-#include "grp.h"
 #include "pack.h"
+#include "part.h"
 #include "pinned.h"
 #include "sg_sharded.h"
 #include "state_doc.h"
@@ -109,58 +105,6 @@ size_t type_size(uint32_t t) {
 
 }  // namespace
 
-// 12-B payloads (one filter column): onesweep with 10-bit digits, so 2^11..2^20 keys sort in two
-// passes over the data instead of three (rocPRIM's gfx950 default for this pair size is 8 bits);
-// 1024 x 16 items per block measured fastest for 2^24 events (tools/sweep/sort_sweep12.hip: 0.460 ms
-// against 0.538 at 1024 x 6 and 0.650 for the default configuration)
-// (MergeSortLimit 4096: rocPRIM's default sorts up to 1M items by block sort + merge passes instead — six merge
-// passes of ~31 us each for a 65,536-event push, against two onesweep passes)
-using Pay16Config = rocprim::radix_sort_config<
-    rocprim::default_config, rocprim::default_config,
-    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 16>, rocprim::kernel_config<1024, 16>, 10,
-                                        rocprim::block_radix_rank_algorithm::match>, 4096>;
-
-// wider payloads (16-24 B): rocPRIM's default onesweep for them takes 4-bit digits (5 passes over 2^20 keys);
-// 10-bit digits with 512 x 8 items per block keep the block's LDS within 160 KB and sort 20 key bits in 2
-using PayWideConfig = rocprim::radix_sort_config<
-    rocprim::default_config, rocprim::default_config,
-    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<512, 8>, rocprim::kernel_config<512, 8>, 10,
-                                        rocprim::block_radix_rank_algorithm::match>, 4096>;
-
-// every other sort: rocPRIM's own onesweep, but from 4096 items up (its default merge-sorts below 2^20)
-using OnesweepConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
-                                                  rocprim::default_config, 4096>;
-
-template <int W>
-hipError_t sort_payload(void* tmp, size_t& tmp_bytes, const uint32_t* keys, uint32_t* skeys, const PackSrc& src,
-                        void* out, uint32_t n, uint32_t b0, uint32_t bits, hipStream_t stream) {
-    auto it = rocprim::make_transform_iterator(rocprim::counting_iterator<uint32_t>(0), PackFn<W>{src});
-    const uint32_t nbits = bits - b0;
-    if constexpr (W == 1) {
-        if ((nbits > 16 && nbits <= 20) || (b0 > 0 && nbits <= 10))
-            return rocprim::radix_sort_pairs<Pay16Config>(tmp, tmp_bytes, keys, skeys, it, (Pay<W>*)out, n, b0, bits,
-                                                           stream);
-    } else {
-        if (nbits <= 20 && (nbits > 10 || b0 > 0))
-            return rocprim::radix_sort_pairs<PayWideConfig>(tmp, tmp_bytes, keys, skeys, it, (Pay<W>*)out, n, b0, bits,
-                                                             stream);
-    }
-    return rocprim::radix_sort_pairs<OnesweepConfig>(tmp, tmp_bytes, keys, skeys, it, (Pay<W>*)out, n, b0, bits,
-                                                      stream);
-}
-
-
-hipError_t sgd_sort_payload(int W, void* tmp, size_t& tmp_bytes, const uint32_t* keys, uint32_t* skeys,
-                          const PackSrc& src, void* out, uint32_t n, uint32_t bits, hipStream_t stream, uint32_t b0) {
-    switch (W) {
-    case 1: return sort_payload<1>(tmp, tmp_bytes, keys, skeys, src, out, n, b0, bits, stream);
-    case 2: return sort_payload<2>(tmp, tmp_bytes, keys, skeys, src, out, n, b0, bits, stream);
-    case 3: return sort_payload<3>(tmp, tmp_bytes, keys, skeys, src, out, n, b0, bits, stream);
-    default: return sort_payload<4>(tmp, tmp_bytes, keys, skeys, src, out, n, b0, bits, stream);
-    }
-}
-
-
 struct sg_engine {
     ShardEngine* shard = nullptr;   // n_devices > 1: the multi-device fan-out (sg_sharded.cpp) behind this handle
     int device = 0;
@@ -172,7 +116,6 @@ struct sg_engine {
     std::vector<IRStream> streams;
     Plan plan;
     uint32_t K = 1, cap = 64, maxb = 0;
-    uint32_t sort_bits = 1;   // key bits the grouping sorts on (SG_CFG_NULL_KEYS: SG_KEY_NULL sorts last)
     bool null_keys = false;
     uint64_t mcap = 0;
     uint64_t raw_cap = 0;  // mcap + one reservation chunk of slack per advance-kernel wave
@@ -209,32 +152,21 @@ struct sg_engine {
         std::vector<uint8_t*> b_nulls;
         std::vector<void*> b_pcols;         // per projection column
         std::vector<uint8_t*> b_pnulls;
-        uint32_t* skeys = nullptr;
-        uint32_t* sidx = nullptr;
+        uint32_t* sidx = nullptr;           // wide payloads: batch positions in key order
         uint32_t* seg_begin = nullptr;
         uint32_t* seg_end = nullptr;
         void* pay = nullptr;                // key-sorted payload [max_batch] x pay_words
+        void* tpay = nullptr;               // fused grouping: the payload grouped by key tile [max_batch] x pay_words
+        uint32_t* tile_lo = nullptr;        // fused grouping: [n_tiles + 1]
         hipEvent_t grouped = nullptr, copied = nullptr, free_ev = nullptr;
         bool used = false;
     };
     Slot slots[2];
     uint64_t nbatch = 0;
-    uint32_t* iota = nullptr;
-    void* sort_tmp = nullptr;
-    size_t sort_tmp_bytes = 0;
-    // tile grouping (grp_kernels.hip; K <= 2^20, max_batch <= 2^24, payload <= 4 words): shared by the
-    // slots (both slots' groupings run on gstream, one after the other)
-    bool tile_grp = false;
-    uint32_t* g_mat = nullptr;
-    uint32_t* g_mscan = nullptr;
-    void* g_tpay = nullptr;
-    void* g_scan_tmp = nullptr;
-    size_t g_scan_tmp_bytes = 0;
-    // bucket grouping (grp_kernels.hip sgd_bucket_split, the default when the keys take more than SGD_BK_BITS
-    // bits): one radix pass on the bucket bits into bk_tpay, then the per-bucket split; shared by the slots
-    bool bucket_grp = false;
-    void* bk_tpay = nullptr;
-    uint32_t* bk_blo = nullptr;
+    // grouping scratch (part.h), shared by the slots: both slots' groupings run on gstream, one after the other
+    PartScratch pscr{};
+    bool fused_ok = false;        // the fused tile grouping is possible for this engine (K <= 2^20, max_batch <= 2^24)
+    bool fused_last = false;      // the last batch took it (sg_engine_describe)
     uint32_t pay_words = 0;
     // per pushed batch, after its ordering: the {match count, error word} status block copied to pinned
     // host memory and an event, so a poll finds the completed batches without waiting for the others
@@ -568,7 +500,6 @@ void allocate(sg_engine* e) {
             sl.b_cols.push_back(dalloc<uint64_t>(B, o));
             sl.b_nulls.push_back(dalloc<uint8_t>(B, o));
         }
-        sl.skeys = dalloc<uint32_t>(B, o);
         sl.sidx = dalloc<uint32_t>(B, o);
         sl.seg_begin = dalloc<uint32_t>(K, o);
         sl.seg_end = dalloc<uint32_t>(K, o);
@@ -578,27 +509,7 @@ void allocate(sg_engine* e) {
     }
     for (auto& x : e->done_ev) HIP_OK(hipEventCreateWithFlags(&x, hipEventDisableTiming));
     HIP_OK(hipHostMalloc((void**)&e->h_status, sizeof(unsigned long long) * 2 * sg_engine::RING, hipHostMallocDefault));
-    e->iota = dalloc<uint32_t>(B, o);
-    {
-        std::vector<uint32_t> h(B);
-        for (size_t i = 0; i < B; i++) h[i] = (uint32_t)i;
-        HIP_OK(hipMemcpy(e->iota, h.data(), B * 4, hipMemcpyHostToDevice));
-    }
-    HIP_OK(rocprim::radix_sort_pairs<OnesweepConfig>(nullptr, e->sort_tmp_bytes, e->slots[0].b_key, e->slots[0].skeys, e->iota,
-                                     e->slots[0].sidx, (uint32_t)B, 0, 32, e->stream));
-    for (int W = 1; W <= 4; ++W) {
-        size_t tb = 0;
-        PackSrc ps{};
-        for (uint32_t bits : {20u, 32u, e->sort_bits}) {
-            for (uint32_t b0 : {0u, (uint32_t)SGD_BK_BITS}) {
-                if (b0 >= bits) continue;
-                HIP_OK(sgd_sort_payload(W, nullptr, tb, e->slots[0].b_key, e->slots[0].skeys, ps, nullptr, (uint32_t)B,
-                                        bits, e->stream, b0));
-                e->sort_tmp_bytes = std::max(e->sort_tmp_bytes, tb);
-            }
-        }
-    }
-    e->sort_tmp = dalloc<uint8_t>(e->sort_tmp_bytes, o);
+    e->pscr = sgd_part_scratch(dalloc<uint8_t>(sgd_part_scratch_bytes(B), o), B);
     {
         uint32_t maxw = 1;  // payload words of the widest stream (+ null word)
         for (int s : {e->plan.s0, e->plan.s1}) {
@@ -607,26 +518,13 @@ void allocate(sg_engine* e) {
             maxw = std::max(maxw, sgj_stride(sgj_col_words(ty) + 1));
         }
         e->pay_words = maxw;
-        for (auto& sl : e->slots)  // + one 16-B chunk: the LDS copy rounds up
+        e->fused_ok = e->plan.partitioned && sgd_fused_ok(K, B, 1) && maxw <= 6 && !getenv("SG_NO_FUSED");
+        for (auto& sl : e->slots) {  // + one 16-B chunk: the LDS copy rounds up
             sl.pay = dalloc<uint32_t>((size_t)maxw * B + 4, o);
-        // the bucket grouping is opt-in (SG_BUCKET_GROUP=1): measured slower than the two-pass radix sort on C2
-        // (0.73 vs 0.51 ms, DESIGN §4: rocPRIM's one-pass iterator sort adds a copy of its odd pass, and the split
-        // of a 1024-key bucket cannot stage its 196 KB in LDS)
-        e->bucket_grp = e->plan.partitioned && e->sort_bits > SGD_BK_BITS && getenv("SG_BUCKET_GROUP");
-        if (e->bucket_grp) {
-            e->bk_tpay = dalloc<uint32_t>((size_t)maxw * B + 4, o);
-            e->bk_blo = dalloc<uint32_t>(((K + (1u << SGD_BK_BITS) - 1) >> SGD_BK_BITS) + 1, o);
-        }
-        // the tile grouping is opt-in (SG_GROUP_TILES=1): measured slower than the radix sort on C2
-        e->tile_grp = e->plan.partitioned && sgd_group_tiles_ok(K, B, 1) && getenv("SG_GROUP_TILES");
-        if (e->tile_grp) {
-            const uint64_t nt = (K + SGD_BLOCK - 1) / SGD_BLOCK, nb = (B + SGD_GRP_BLOCK_EVENTS - 1) / SGD_GRP_BLOCK_EVENTS;
-            e->g_mat = dalloc<uint32_t>(nt * nb + 1, o);
-            e->g_mscan = dalloc<uint32_t>(nt * nb + 1, o);
-            e->g_tpay = dalloc<uint32_t>((size_t)maxw * B + 4, o);
-            e->g_scan_tmp_bytes = sgd_group_scan_bytes(nt * nb + 1);
-            if (!e->g_scan_tmp_bytes) throw HipError("tile grouping: scan storage query failed");
-            e->g_scan_tmp = dalloc<uint8_t>(e->g_scan_tmp_bytes, o);
+            if (e->fused_ok) {
+                sl.tpay = dalloc<uint32_t>((size_t)maxw * B + 4, o);
+                sl.tile_lo = dalloc<uint32_t>((K + SGD_BLOCK - 1) / SGD_BLOCK + 1, o);
+            }
         }
     }
     // raw match slots per batch: waves reserve at most sum(live partials + events) up front, or
@@ -744,6 +642,27 @@ uint32_t stage_chunks_for(uint64_t n, uint64_t K, uint32_t stride_words) {
     const double chunks = std::ceil((std::ceil(want * stride_words * 4.0 / 16.0) + 1.0) / wpb);
     const double hi = std::floor((double)SGD_STAGE_MAX_BYTES / wpb / 16.0);
     return (uint32_t)std::max(64.0, std::min(chunks, hi));
+}
+
+// fused grouping: the LDS staging of a workgroup's tile (its events at this density plus 3.5 standard deviations
+// of a Poisson count, the few larger tiles split in HBM and walked by the HBM pass), sized so that three workgroups
+// share a CU at the C2 density (with the split's 2 KB of counters beside it); and whether the batch takes the fused
+// grouping at all (the split holds SGD_SPLIT_CHUNKS rounds of 64 events per wave in registers)
+static uint32_t stage_chunks_fused(uint64_t n, uint64_t K, uint32_t stride_words) {
+    const uint32_t wpb = SGD_BLOCK / SGD_WAVE;
+    const double mean = (double)n * SGD_BLOCK / (double)(K ? K : 1);
+    const double want = mean + 3.5 * std::sqrt(mean);
+    const double chunks = std::ceil((std::ceil(want * stride_words * 4.0 / 16.0) + 1.0) / wpb);
+    // three workgroups per CU: LDS is allocated in granules of 1,280 B on gfx950 (measured: a 54,064-B workgroup
+    // held two per CU, 53,360 B three), so a workgroup keeps within 42 granules = 53,760 B
+    const double three = std::floor((53760.0 - SGD_SPLIT_CNT_BYTES - 64.0) / wpb / 16.0);
+    const double hi = std::floor((double)(SGD_STAGE_MAX_BYTES - SGD_SPLIT_CNT_BYTES) / wpb / 16.0);
+    if (chunks <= three + 16.0) return (uint32_t)std::max(64.0, std::min(chunks, three));
+    return (uint32_t)std::max(64.0, std::min(chunks, hi));
+}
+static bool fused_density_ok(uint64_t n, uint64_t K, uint32_t stride_words) {
+    const double mean = (double)n * SGD_BLOCK / (double)(K ? K : 1);
+    return mean + 3.0 * std::sqrt(mean) <= (double)SGD_SPLIT_CHUNKS(stride_words) * SGD_BLOCK;
 }
 
 // largest key id of a host batch (branch-free, so it vectorises; range-checked after the H2D is queued);
@@ -879,11 +798,20 @@ int push(sg_engine* e, const sg_batch* b) {
     e->st.events += b->n;
     e->st.batches++;
     if (e->timing) { g0 = e->ev(); e->mark(g0, gs); }
+    bool fused = false;
     if (pl.partitioned) {
-        size_t tmp = e->sort_tmp_bytes;
+        GroupArgs ga{};
+        ga.n = n;
+        ga.K = e->K;
+        ga.drop_null = e->null_keys ? 1u : 0u;
+        ga.keys = keys;
+        ga.seg_begin = sl.seg_begin;
+        ga.seg_end = sl.seg_end;
+        ga.err = e->err;
+        ga.s = e->pscr;
         if (words <= 4) {
-            // sort the events WITH their payload (packed on the fly by the first radix pass): the
-            // advance kernel then reads one contiguous run per key
+            // the events WITH their payload (gathered from the SoA columns by the first pass): the advance kernel
+            // then reads one contiguous range per workgroup
             PackSrc ps{};
             ps.ts = ts;
             uint32_t wi = 0;
@@ -901,69 +829,32 @@ int push(sg_engine* e, const sg_batch* b) {
                 ps.kind[wi++] = 4;
             }
             if (wi == 0) ps.kind[wi++] = 5;
-            if (e->tile_grp && sgd_group_tiles_ok(e->K, n, wi)) {
-                // by key tile, then by key inside each tile in LDS (grp_kernels.hip): the same key-sorted
-                // payload and per-key bounds as the radix sort below
-                GrpArgs ga{};
-                ga.n = n;
-                ga.K = e->K;
-                ga.n_tiles = (e->K + SGD_BLOCK - 1) / SGD_BLOCK;
-                ga.nblk = (n + SGD_GRP_BLOCK_EVENTS - 1) / SGD_GRP_BLOCK_EVENTS;
-                ga.drop_null = e->null_keys ? 1u : 0u;
-                ga.tile_lds = sgd_group_tile_lds(n, e->K, wi);
-#ifdef SG_EXPERIMENTS
-                if (const char* x = getenv("SG_GRP_EXP")) ga.exp = (uint32_t)strtoul(x, nullptr, 0);
-#endif
-                ga.keys = keys;
-                ga.mat = e->g_mat;
-                ga.mscan = e->g_mscan;
-                ga.tpay = e->g_tpay;
-                ga.pay = sl.pay;
-                ga.seg_begin = sl.seg_begin;
-                ga.seg_end = sl.seg_end;
-                ga.err = e->err;
-                ga.scan_tmp = e->g_scan_tmp;
-                ga.scan_tmp_bytes = e->g_scan_tmp_bytes;
-                HIP_OK(sgd_group_tiles(ga, ps, (int)wi, gs));
-                goto grouped;
+            ga.W = wi;
+            ga.src = ps;
+            fused = e->fused_ok && sgd_fused_ok(e->K, n, wi) && fused_density_ok(n, e->K, stride);
+            if (fused) {
+                // grouped by key tile only; the split by key is the advance kernel's (tile_split_lds)
+                ga.out = sl.tpay;
+                HIP_OK(sgd_group_tiles_fused(ga, sl.tile_lo, gs));
+            } else {
+                ga.out = sl.pay;
+                HIP_OK(sgd_group_sorted(ga, gs));
             }
-            if (e->bucket_grp) {
-                // one radix pass on the bucket bits, then each bucket of 2^SGD_BK_BITS keys split by key in LDS
-                // (stable), the per-key bounds written by the split
-                HIP_OK(sgd_sort_payload((int)wi, e->sort_tmp, tmp, keys, sl.skeys, ps, e->bk_tpay, n, e->sort_bits, gs,
-                                        SGD_BK_BITS));
-                BucketArgs ba{};
-                ba.n = n;
-                ba.K = e->K;
-                ba.bits = e->sort_bits;
-                ba.nb = (e->K + (1u << SGD_BK_BITS) - 1) >> SGD_BK_BITS;
-                ba.drop_null = e->null_keys ? 1u : 0u;
-                ba.skeys = sl.skeys;
-                ba.tpay = e->bk_tpay;
-                ba.pay = sl.pay;
-                ba.blo = e->bk_blo;
-                ba.seg_begin = sl.seg_begin;
-                ba.seg_end = sl.seg_end;
-                ba.err = e->err;
-                HIP_OK(sgd_bucket_split(ba, (int)wi, gs));
-                goto grouped;
-            }
-            HIP_OK(sgd_sort_payload((int)wi, e->sort_tmp, tmp, keys, sl.skeys, ps, sl.pay, n, e->sort_bits, gs));
         } else {
-            HIP_OK(rocprim::radix_sort_pairs<OnesweepConfig>(e->sort_tmp, tmp, keys, sl.skeys, e->iota, sl.sidx, n, 0, e->sort_bits,
-                                             gs));
+            // wide payloads: batch positions in key order, then the payload packed from them
+            ga.W = 0;
+            ga.out = sl.sidx;
+            HIP_OK(sgd_group_sorted(ga, gs));
             pk.sidx = sl.sidx;
             launch(v.pack[role], pack_blocks, 256, &pk, gs);
         }
-        if (sgd_launch_bounds(sl.skeys, n, e->K, e->null_keys, sl.seg_begin, sl.seg_end, e->err, gs) != 0)
-            throw HipError("k_seg_bounds launch failed");
-    grouped:;
     } else {
         pk.sidx = nullptr;  // one key: arrival order
         launch(v.pack[role], pack_blocks, 256, &pk, gs);
         HIP_OK(hipMemsetD32Async((hipDeviceptr_t)sl.seg_begin, 0u, 1, gs));
         HIP_OK(hipMemsetD32Async((hipDeviceptr_t)sl.seg_end, (int)n, 1, gs));
     }
+    e->fused_last = fused;
     if (e->timing) { g1 = e->ev(); e->mark(g1, gs); e->spans.push_back({g0, g1, 0}); }
     HIP_OK(hipEventRecord(sl.grouped, gs));
     HIP_OK(hipStreamWaitEvent(e->stream, sl.grouped, 0));
@@ -975,6 +866,10 @@ int push(sg_engine* e, const sg_batch* b) {
     p.seq_base = b->seq_base;
     p.within = pl.within;
     p.payload = (const uint32_t*)sl.pay;
+    p.tile_lo = fused ? sl.tile_lo : nullptr;
+    p.tpay = (const uint32_t*)sl.tpay;
+    p.write_sorted = (fused && proj && e->n_agg) ? 1u : 0u;
+    p.hbm_stage_chunks = SGD_HBM_STAGE_BYTES / 16u;
     p.ts_col = ts;
     p.seg_begin = sl.seg_begin;
     p.seg_end = sl.seg_end;
@@ -1002,12 +897,16 @@ int push(sg_engine* e, const sg_batch* b) {
     hipEvent_t a0 = nullptr, a1 = nullptr;
     if (e->timing) { a0 = e->ev(); e->mark(a0); }
     {
-        p.stage_chunks = e->stage_override ? e->stage_override : stage_chunks_for(n, e->K, stride);
+        p.stage_chunks = e->stage_override ? std::max(64u, e->stage_override)
+                         : fused ? stage_chunks_fused(n, e->K, stride) : stage_chunks_for(n, e->K, stride);
         const uint32_t blocks = (e->K + SGD_BLOCK - 1) / SGD_BLOCK;
-        launch(v.adv[role], blocks, SGD_BLOCK, &p, e->stream, p.stage_chunks * 16u * (SGD_BLOCK / SGD_WAVE));
+        // (fused: the split's per-(wave, key) counters after the staging region)
+        launch(v.adv[role], blocks, SGD_BLOCK, &p, e->stream,
+               p.stage_chunks * 16u * (SGD_BLOCK / SGD_WAVE) + (fused ? SGD_SPLIT_CNT_BYTES : 0u));
         if (e->timing) { a1 = e->ev(); e->mark(a1); e->spans.push_back({a0, a1, 1}); a0 = e->ev(); e->mark(a0); }
         // one wave per work-group over the listed waves (a fixed grid: the list's length is on the device)
-        launch(v.adv_h[role], std::min<uint32_t>(blocks * (SGD_BLOCK / SGD_WAVE), e->hbm_grid), SGD_WAVE, &p, e->stream);
+        launch(v.adv_h[role], std::min<uint32_t>(blocks * (SGD_BLOCK / SGD_WAVE), e->hbm_grid), SGD_WAVE, &p, e->stream,
+               p.hbm_stage_chunks * 16u);
         if (e->timing) { a1 = e->ev(); e->mark(a1); e->spans.push_back({a0, a1, 3}); }
         if (sgd_launch_stats_reduce(e->wstats, blocks * (SGD_BLOCK / SGD_WAVE), e->stats, e->raw_count, e->dlist_n, e->stream) != 0)
             throw HipError("k_stats_reduce launch failed");
@@ -1271,8 +1170,11 @@ int set_projection(sg_engine* e, const uint32_t* code, uint32_t words, const uin
             }
             if (maxw > e->pay_words) {
                 e->pay_words = maxw;
-                for (auto& sl : e->slots) sl.pay = dalloc<uint32_t>((size_t)maxw * e->maxb + 4, e->owned);
-                if (e->bucket_grp) e->bk_tpay = dalloc<uint32_t>((size_t)maxw * e->maxb + 4, e->owned);
+                for (auto& sl : e->slots) {
+                    sl.pay = dalloc<uint32_t>((size_t)maxw * e->maxb + 4, e->owned);
+                    if (e->fused_ok) sl.tpay = dalloc<uint32_t>((size_t)maxw * e->maxb + 4, e->owned);
+                }
+                if (maxw > 6) e->fused_ok = false;
             }
         }
         const size_t K = e->K, C = e->cap, M = e->mcap;
@@ -1475,9 +1377,6 @@ int sg_engine_create(const void* ir, size_t ir_len, const sg_config* cfg, sg_eng
         e->jq = make_jit_query(e);
         (void)sgj_generate(e->jq, e->consts);  // validates the filters, fixes the constant table
         if (!e->plan.partitioned && e->K != 1) e->K = 1;
-        // the sort looks at the low sort_bits bits only: with SG_CFG_NULL_KEYS one more value than the
-        // key range, so that SG_KEY_NULL (all ones) sorts after every valid key
-        e->sort_bits = bits_for((uint64_t)e->K + (e->null_keys ? 1u : 0u));
         int ndev = 0;
         HIP_OK(hipGetDeviceCount(&ndev));
         if (cfg->device < 0 || cfg->device >= ndev) throw HipError("no such HIP device");
@@ -1726,9 +1625,12 @@ int sg_engine_describe(sg_engine* e, char* out, size_t out_len) {
     if (one->gen) {
         d = gen_describe(one->gen);
     } else {
-        d = std::string("push: ") + (one->tile_grp ? "k_grp_hist + k_grp_scatter + k_grp_tile" : "rocPRIM onesweep radix sort") +
-            " + k_seg_bounds (grouping, stream 2); k_adv_m (NFA advance, LDS-staged, lane per key) + k_adv_m_h "
-            "(NFA advance, HBM pass) + k_stats_reduce; k_order_sums + scan + k_order_scatter (ordering)";
+        d = std::string("push: ") +
+            (one->fused_last ? "k_part_hist + k_part_scan + k_part_scatter x2 + k_tile_bounds (grouping by key tile, stream 2); "
+                               "k_adv_m (key split in LDS + NFA advance, LDS-staged, lane per key)"
+                             : "k_part_hist + k_part_scan + k_part_scatter per 8-bit digit + k_part_bounds (grouping, stream 2); "
+                               "k_adv_m (NFA advance, LDS-staged, lane per key)") +
+            " + k_adv_m_h (NFA advance, HBM pass) + k_stats_reduce; k_order_sums + scan + k_order_scatter (ordering)";
         if (one->proj_n) d += " + k_project" + std::string(one->n_agg ? " + k_agg" : "");
     }
     if (e->shard) d = std::to_string(shd_count(e->shard)) + " shards, each " + d;

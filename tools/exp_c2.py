@@ -20,7 +20,7 @@ import torch  # noqa: E402
 sa = importlib.import_module("siddhi-1_amd")
 synth = importlib.import_module("siddhi-1_amd.synth")
 B, K = 1 << 24, 1 << 20
-KNOBS = ("SG_JIT_EXTRA", "SGD_STAGE_CHUNKS", "SGD_REG_SLOTS", "SG_BUCKET_GROUP", "SG_CUMASK", "SG_STREAM_PRIO")
+KNOBS = ("SG_JIT_EXTRA", "SGD_STAGE_CHUNKS", "SGD_REG_SLOTS", "SG_NO_FUSED", "SG_CUMASK", "SG_STREAM_PRIO")
 
 
 def main():
@@ -89,6 +89,7 @@ def main():
                           "group_ms": round((st["group_ns"] - st0["group_ns"]) / 1e6 / n, 4),
                           "advance_ms": round((st["advance_ns"] - st0["advance_ns"]) / 1e6 / n, 4),
                           "order_ms": round((st["order_ns"] - st0["order_ns"]) / 1e6 / n, 4),
+                          "hbm_pass_ms": round((st.get("advance_hbm_ns", 0) - st0.get("advance_hbm_ns", 0)) / 1e6 / n, 4),
                           "matches": (st["matches"] - st0["matches"]) / n,
                           "spills": (st["window_spills"] - st0["window_spills"]) / n}), flush=True)
         eng.close()
