@@ -204,3 +204,127 @@ def absent_deep_ticks(start_ms: int, n_ms: int, n_keys: int, burst: int, seed: i
     volume = (np.uint64(1) + h2 % np.uint64(2000)).astype(np.int32)
     ts = (np.int64(t0) + t.astype(np.int64)).astype(np.int64)
     return {"key": key, "ts": ts, "symbol": key.copy(), "price": price, "volume": volume}
+
+
+# ---- SURVEY §8(d) workload variants: Zipf s=1.1 keys ("reported separately") and the per-key random-walk price ----
+ZIPF_S = 1.1
+_ZIPF_CDF = {}
+_KEY_MIX = 0x9E3779B1  # odd: rank -> key id is a bijection of [0, 2^b) (hot keys spread over tiles and waves)
+
+
+def zipf_cdf(n_keys: int, s: float = ZIPF_S) -> np.ndarray:
+    """cumulative probabilities of Zipf ranks 1..n_keys (float64)"""
+    k = (n_keys, s)
+    if k not in _ZIPF_CDF:
+        w = 1.0 / np.power(np.arange(1, n_keys + 1, dtype=np.float64), s)
+        c = np.cumsum(w)
+        _ZIPF_CDF[k] = c / c[-1]
+    return _ZIPF_CDF[k]
+
+
+def _rank_to_key(rank, n_keys: int):
+    """rank r (0 = hottest) -> key id: (r * odd) mod n_keys for a power-of-two n_keys, else r"""
+    if n_keys & (n_keys - 1):
+        return rank
+    return (rank * _KEY_MIX) & (n_keys - 1)
+
+
+def zipf_ticks(start: int, n: int, n_keys: int, seed: int = SEED, rate_per_ms: int = 2000, t0: int = T0, s: float = ZIPF_S):
+    """stock_ticks with Zipf(s) partition keys: key = bijection(rank), rank ~ Zipf over n_keys ranks (the hottest key
+    ~12 % of the events at s = 1.1, 2^20 keys); the other fields as stock_ticks"""
+    d = stock_ticks(start, n, n_keys, seed, rate_per_ms, t0)
+    i = np.arange(start, start + n, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        base = np.uint64(seed) * np.uint64(0x100000001B3) if seed else np.uint64(0)
+        h = splitmix64(i * np.uint64(3) + base + np.uint64(0x7A))
+    u = (h >> np.uint64(11)).astype(np.float64) / float(1 << 53)
+    rank = np.minimum(np.searchsorted(zipf_cdf(n_keys, s), u, side="right"), n_keys - 1).astype(np.uint64)
+    key = _rank_to_key(rank, n_keys).astype(np.uint32)
+    d["key"] = key
+    d["symbol"] = key.copy()
+    return d
+
+
+def zipf_ticks_torch(torch, start: int, n: int, n_keys: int, device, seed: int = SEED, rate_per_ms: int = 2000,
+                     t0: int = T0, s: float = ZIPF_S):
+    """zipf_ticks on the device (bit-identical keys: the same splitmix draws and CDF table)"""
+    d = stock_ticks_torch(torch, start, n, n_keys, device, seed, rate_per_ms, t0)
+    i = torch.arange(start, start + n, dtype=torch.int64, device=device)
+    base = _i64((seed * 0x100000001B3) & ((1 << 64) - 1)) if seed else 0
+    h = splitmix64_torch(torch, i * 3 + base + 0x7A)
+    u = _srl(torch, h, 11).to(torch.float64) / float(1 << 53)
+    cdf = torch.from_numpy(zipf_cdf(n_keys, s)).to(device)
+    rank = torch.clamp(torch.searchsorted(cdf, u, right=True), max=n_keys - 1)
+    key = ((rank * _KEY_MIX) & (n_keys - 1)).to(torch.int32)
+    d["key"] = key
+    d["symbol"] = key.clone()
+    return d
+
+
+class RandomWalk:
+    """SURVEY §8(d) price model: per key p <- clamp(p + 0.25 N(0,1), 1, 100) rounded to f32 at each of the key's
+    events, initial U[10, 40] per key.  Stateful across batches (call step() on consecutive batches in order);
+    deterministic: the increments are Box-Muller normals of splitmix64 draws of the global event index.  Works on
+    numpy arrays or (with `torch`) on device tensors."""
+
+    def __init__(self, n_keys: int, seed: int = SEED, torch=None, device=None):
+        self.torch, self.device = torch, device
+        k = np.arange(n_keys, dtype=np.uint64)
+        with np.errstate(over="ignore"):
+            base = np.uint64(seed) * np.uint64(0x100000001B3) if seed else np.uint64(0)
+            h = splitmix64(k * np.uint64(5) + base + np.uint64(0x3F))
+        p = (10.0 + 30.0 * ((h >> np.uint64(40)).astype(np.float64) / float(1 << 24))).astype(np.float32)
+        self.seed = seed
+        self.p = torch.from_numpy(p).to(device) if torch is not None else p
+
+    def _inc(self, start: int, n: int):
+        i = np.arange(start, start + n, dtype=np.uint64)
+        with np.errstate(over="ignore"):
+            base = np.uint64(self.seed) * np.uint64(0x100000001B3) if self.seed else np.uint64(0)
+            h1 = splitmix64(i * np.uint64(3) + base + np.uint64(0x91))
+            h2 = splitmix64(i * np.uint64(3) + base + np.uint64(0x92))
+        u1 = ((h1 >> np.uint64(11)).astype(np.float64) + 1.0) / float(1 << 53)   # (0, 1]
+        u2 = (h2 >> np.uint64(11)).astype(np.float64) / float(1 << 53)
+        return 0.25 * np.sqrt(-2.0 * np.log(u1)) * np.cos(2.0 * np.pi * u2)
+
+    def step(self, key, start: int):
+        """the prices of events [start, start + n) whose keys are `key` (arrival order); advances the walk"""
+        t = self.torch
+        n = int(key.shape[0])
+        inc = self._inc(start, n)
+        if t is not None:
+            inc = t.from_numpy(inc).to(self.device)
+            k = key.to(t.int64)
+            order = t.argsort(k, stable=True)
+            ks = k[order]
+            first = t.ones(n, dtype=t.bool, device=self.device)
+            first[1:] = ks[1:] != ks[:-1]
+            pos = t.arange(n, device=self.device)
+            seg0 = t.cummax(t.where(first, pos, t.zeros_like(pos)), 0).values
+            rank = t.empty_like(pos)
+            rank[order] = pos - seg0
+            price = t.empty(n, dtype=t.float32, device=self.device)
+            for r in range(int(rank.max().item()) + 1 if n else 0):
+                idx = t.nonzero(rank == r).flatten()
+                kk = k[idx]
+                v = t.clamp(self.p[kk].to(t.float64) + inc[idx], 1.0, 100.0).to(t.float32)
+                self.p[kk] = v
+                price[idx] = v
+            return price
+        k = np.asarray(key).astype(np.int64)
+        order = np.argsort(k, kind="stable")
+        ks = k[order]
+        first = np.ones(n, dtype=bool)
+        first[1:] = ks[1:] != ks[:-1]
+        pos = np.arange(n)
+        seg0 = np.maximum.accumulate(np.where(first, pos, 0))
+        rank = np.empty(n, dtype=np.int64)
+        rank[order] = pos - seg0
+        price = np.empty(n, dtype=np.float32)
+        for r in range(int(rank.max()) + 1 if n else 0):
+            idx = np.nonzero(rank == r)[0]
+            kk = k[idx]
+            v = np.clip(self.p[kk].astype(np.float64) + inc[idx], 1.0, 100.0).astype(np.float32)
+            self.p[kk] = v
+            price[idx] = v
+        return price
