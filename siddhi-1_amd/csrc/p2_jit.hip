@@ -117,6 +117,12 @@ template <class A, class B> struct SgSel<false, A, B> { typedef B type; };
 #include "sgq_query.h"
 
 #define R SGQ_R
+// the hot-key pipeline (k_hot_*, end of file) exists for `every e1 -> e2` with both states on one stream
+#if SGQ_MULTI && SGQ_MODE == 1  // (SGD_P2_EVERY_FIRST: an enum, invisible to #if)
+#define SG_HOT 1
+#else
+#define SG_HOT 0
+#endif
 
 // ablation knobs for tools/exp_c2.py (JIT-time defines, experiment builds only); 0 in every shipped configuration
 #ifndef SGX_NO_RAW
@@ -702,9 +708,18 @@ __device__ __forceinline__ void advance(const P2Params& p, const uint32_t gid) {
     if constexpr (!STG) {
         dfr = uni(p.deferred[wave_id]);  // 1: the whole wave; 2: the keys with a resume point
         if (dfr == 0u) return;
-        if (dfr != 1u) {
+        if (k < K) rsm = p.resume[k];
+        if (rsm == SGD_HOT_DONE) {  // advanced by the hot-key pipeline
+            p.resume[k] = SGD_NO_RESUME;
             count_key = false;
-            if (k < K) rsm = p.resume[k];
+            e = b;
+        } else if (dfr == 1u) {
+            if (rsm == SGD_HOT_MARK) {  // a hot key the pipeline gave back (counted by the staged pass)
+                p.resume[k] = SGD_NO_RESUME;
+                count_key = false;
+            }
+        } else {
+            count_key = false;
             if (rsm != SGD_NO_RESUME) {
                 b += rsm;
                 p.resume[k] = SGD_NO_RESUME;
@@ -715,7 +730,18 @@ __device__ __forceinline__ void advance(const P2Params& p, const uint32_t gid) {
     }
     const int nev = (int)(e - b);
     if (nev <= 0) h = 0;
-    int iters = (int)uni((uint32_t)wave_max(nev));
+    // a hot key (SG_HOT): left to the hot-key pipeline (listed here), its lane walks nothing
+    bool hot = false;
+#if SG_HOT
+    if constexpr (STG) {
+        if (p.hot_min != 0u && k < K && (uint32_t)nev >= p.hot_min) {
+            const uint32_t slot = atomicAdd(p.hot_ctl, 1u);
+            hot = slot < p.hot_cap;
+            if (hot) p.hot_list[slot] = k;
+        }
+    }
+#endif
+    int iters = (int)uni((uint32_t)wave_max(hot ? 0 : nev));
     // the HBM pass stages its wave's runs in LDS too when they fit (its keys are consecutive: one range of the
     // key-sorted payload), so its walk waits on LDS, not on a dependent HBM load per event
     bool from_lds = STG && !SGX_GLB_WALK && !tile_glb;
@@ -760,8 +786,8 @@ __device__ __forceinline__ void advance(const P2Params& p, const uint32_t gid) {
     const Slab G{p.p_ts + k, p.p_seq + k, p.p_capw + k, p.p_capnull + k, K, (size_t)p.cap * K};
     bool hbm = n0 > (uint32_t)R;
     // events of the run this pass walks (the staged pass may stop a key early: resume point `rs`)
-    int run = nev;
-    uint32_t rs = SGD_NO_RESUME;
+    int run = hot ? 0 : nev;
+    uint32_t rs = (hot && fits) ? 0u : SGD_NO_RESUME;  // (a hot key resumes from 0 if the pipeline gives it back)
     if (STG && hbm && nev > 0) {  // more live partials than the window holds: all of it to the HBM pass
         rs = 0;
         run = 0;
@@ -845,10 +871,17 @@ __device__ __forceinline__ void advance(const P2Params& p, const uint32_t gid) {
         __builtin_amdgcn_s_waitcnt(0);
         __syncthreads();
     }
-    if (iters == 0) {  // no key of this wave has an event here (wave-uniform), or the HBM pass has it
+    // (a wave with hot keys in a staged workgroup goes on: their runs and resume points are written below)
+    if (iters == 0 && !(STG && fits && __ballot(hot) != 0ull)) {
+        // no key of this wave has an event here (wave-uniform), or the HBM pass has it; hot keys of a wave left
+        // to the HBM pass are counted here (the pipeline or, given back, the HBM pass advances them)
+        const unsigned long long hk = wave_sum(hot ? 1ull : 0ull), hl = wave_sum(hot ? (unsigned long long)n0 : 0ull);
+        if (STG && hot) p.resume[k] = SGD_HOT_MARK;
         if (STG && lane == 0) {
 #pragma unroll
             for (int i = 0; i < SGD_ST_N; ++i) p.wstats[(size_t)wave_id * SGD_ST_N + i] = 0;
+            p.wstats[(size_t)wave_id * SGD_ST_N + SGD_ST_KEYS] = hk;
+            p.wstats[(size_t)wave_id * SGD_ST_N + SGD_ST_LIVE0] = hl;
         }
         return;
     }
@@ -1145,12 +1178,19 @@ __device__ __forceinline__ void advance(const P2Params& p, const uint32_t gid) {
     if (lane == 0 && p.prof)  // one row per wave (no device-wide atomics), summed by the host
         for (int i = 0; i < 5; ++i) p.prof[(size_t)wave_id * 8 + i] += prof_acc[i];
 #endif
+    if (STG && fused && !tile_glb && !p.write_sorted) {
+        // fused: the runs of the keys the HBM pass resumes (or the hot-key pipeline takes) were only in LDS; the
+        // wave copies them to the key-sorted payload one key at a time, coalesced
+        for (uint64_t need = __ballot(rs != SGD_NO_RESUME); need; need &= need - 1ull) {
+            const int l = __builtin_ctzll(need);
+            const uint32_t lb = (uint32_t)__shfl((int)b, l, SGD_WAVE), ln = (uint32_t)__shfl(nev, l, SGD_WAVE);
+            uint32_t* dst = (uint32_t*)p.payload + (size_t)lb * STRIDE;
+            const uint32_t* src = lds_run + (size_t)(lb - blo) * STRIDE;
+            for (uint32_t x = (uint32_t)lane; x < ln * STRIDE; x += SGD_WAVE) dst[x] = src[x];
+        }
+    }
     if (STG && rs != SGD_NO_RESUME) {  // the HBM pass resumes the key
-        if (fused && !tile_glb && !p.write_sorted) {  // (fused: its run was only in LDS)
-            for (int i = 0; i < nev; ++i)
-#pragma unroll
-                for (int u = 0; u < STRIDE; ++u)
-                    ((uint32_t*)p.payload)[(size_t)(b + (uint32_t)i) * STRIDE + u] = lds_run[(size_t)(b - blo + (uint32_t)i) * STRIDE + u];
+        if (fused && !tile_glb && !p.write_sorted) {
             p.seg_begin[k] = b;
             p.seg_end[k] = e;
         }
@@ -1238,6 +1278,12 @@ __device__ __forceinline__ void pack(const PackParams& q) {
 // costs few work-groups
 template <bool S0, bool S1> __device__ __forceinline__ void hbm_pass(const P2Params& p) {
     const uint32_t n = __builtin_amdgcn_readfirstlane(*p.dlist_n);
+    if (p.hot_ctl && blockIdx.x == 0 && threadIdx.x == 0) {
+        // the batch's hot keys (after the pipeline): into the status block's spare word (the host turns the
+        // pipeline on while batches have them), and the list reset for the next batch
+        p.err[1] = p.hot_ctl[0];
+        p.hot_ctl[0] = 0u;
+    }
     for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
         const uint32_t w = __builtin_amdgcn_readfirstlane(p.dlist[i]);
         advance<S0, S1, false>(p, w * SGD_WAVE + threadIdx.x);
@@ -1255,3 +1301,526 @@ extern "C" __global__ void __launch_bounds__(SGD_WAVE) SGQ_OCC k_adv_s1_h(const 
 #endif
 extern "C" __global__ void __launch_bounds__(256) k_pack0(const PackParams q) { pack<SGQ_STRIDE0, 0>(q); }
 extern "C" __global__ void __launch_bounds__(256) k_pack1(const PackParams q) { pack<SGQ_STRIDE1, 1>(q); }
+
+// ---- hot keys -----------------------------------------------------------------------------------------------
+// `every e1=S[f0] -> e2=S[f1(e1, e2)] within T` on one stream.  A key with thousands of events in one batch (the
+// head of a Zipf key stream; the single key of an unpartitioned query) would serialise one lane of the staged walk.
+// Its run is advanced here instead, all partials at once.  When the run's timestamps are nondecreasing (and the
+// carried-in list is ts- and seq-ordered, with one start seed armed) the walk decomposes exactly:
+//   - every event e_j with f0 creates one partial (the start state's one seed fires and re-arms at each event:
+//     PatternMultiProcessStreamReceiver.java:31-40 with StreamPreStateProcessor.java:364-403), staged until the
+//     next event, whose stabilize promotes it (:308-323, identity order: its ts is the newest);
+//   - a pending partial dies at the first later event e_i that either expires it (|ts_j - ts_i| > T, tested at
+//     stabilize, before the state-1 scan: :118-129 / :325-361 — with ordered timestamps the expired partials
+//     are a prefix of the list, as the reference's prefix rule assumes) or satisfies f1(e_j, e_i) (a match,
+//     emitted by e_i; StreamPostStateProcessor.java:64-83);
+//   - the matches of one trigger are its matched partials in list order (creation order = seq order).
+// So a partial's fate is a first-hit search over the run, done in three rounds: a thread per partial over
+// SGD_HOT_L0 events, a wave per survivor over SGD_HOT_L1 more, then SGD_HOT_BLK-event blocks of the rest in
+// parallel (atomicMin of the hit).  The triggers' match counts, their raw slots, the slot fill and the in-trigger
+// seq order follow; the survivors (ordered) become the key's slab list.  A key whose run breaks the conditions
+// is left to the HBM pass (its resume word untouched), which walks it as before.
+#if SG_HOT
+#define SGD_HOT_L0 32u
+#define SGD_HOT_L1 512u
+#define SGD_HOT_BLK 4096u
+namespace {
+constexpr uint32_t HOT_NOTP = 0xfffffffeu;  // death word of a payload position whose event made no partial
+constexpr uint32_t HOT_LIVE = 0xffffffffu;  // no event of the run ends the partial (or not found yet)
+enum { HI_B = 0, HI_M, HI_EXOFF, HI_EVOFF, HI_N0, HI_BAD, HI_ALIVE, HI_KEY };
+enum { HC_N = 0, HC_EX, HC_EV, HC_N1, HC_N2, HC_MAXM };
+constexpr int HST = SGQ_STRIDE0;
+
+struct HotPart {
+    int64_t ts;
+    uint64_t seq;
+    uint32_t cw[SGQ_NCAPW > 0 ? SGQ_NCAPW : 1];
+    uint32_t cn;
+};
+
+// the last hot key h whose `field` offset is <= x (keys with nothing there share the next key's offset)
+__device__ __forceinline__ uint32_t hot_find(const uint32_t* info, uint32_t n, uint32_t x, int field) {
+    uint32_t lo = 0, hi = n;
+    while (hi - lo > 1u) {
+        const uint32_t mid = (lo + hi) / 2u;
+        if (info[mid * SGD_HOT_INFO + field] <= x) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+__device__ __forceinline__ int64_t hot_ts(const P2Params& p, const PayEl<HST>& x, int64_t obase) {
+    const int32_t toff = (int32_t)x.w[HST - 1];
+    return toff != SGD_TS_FAR ? obase + (int64_t)toff : p.ts_col[x.w[0]];
+}
+__device__ __forceinline__ HotPart hot_created(const P2Params& p, uint32_t pos, int64_t obase) {
+    const PayEl<HST> x = load_pay<HST>(p.payload, pos);
+    HotPart P;
+    P.ts = hot_ts(p, x, obase);
+    P.seq = p.seq_base + x.w[0];
+    P.cn = 0;
+#pragma unroll
+    for (int w = 0; w < (SGQ_NCAPW > 0 ? SGQ_NCAPW : 1); ++w) P.cw[w] = 0;
+    sgq_capture(sgq_ev0(x.w), P.cw, P.cn);
+    return P;
+}
+__device__ __forceinline__ Slab hot_slab(const P2Params& p, uint32_t k) {
+    return Slab{p.p_ts + k, p.p_seq + k, p.p_capw + k, p.p_capnull + k, p.n_keys, (size_t)p.cap * p.n_keys};
+}
+__device__ __forceinline__ HotPart hot_existing(const P2Params& p, uint32_t k, uint32_t j) {
+    const Slab G = hot_slab(p, k);
+    HotPart P;
+    P.ts = G.TS(j);
+    P.seq = G.SEQ(j);
+#pragma unroll
+    for (int w = 0; w < (SGQ_NCAPW > 0 ? SGQ_NCAPW : 1); ++w) P.cw[w] = w < SGQ_NCAPW ? G.CAP(w, j) : 0u;
+    P.cn = SGQ_CAPNULL ? G.NUL(j) : 0u;
+    return P;
+}
+// the partial in `slot`: created at payload position slot (run index slot - b), or carried in (index -1)
+__device__ __forceinline__ HotPart hot_part(const P2Params& p, uint32_t slot, const uint32_t* hi, int64_t obase,
+                                            int& start) {
+    if (slot < p.max_batch) {
+        start = (int)(slot - hi[HI_B]);
+        return hot_created(p, slot, obase);
+    }
+    start = -1;
+    return hot_existing(p, hi[HI_KEY], slot - p.max_batch - hi[HI_EXOFF]);
+}
+// event i of the run (payload position pos) ends partial P: 2i (expired) or 2i + 1 (matched); HOT_LIVE otherwise
+__device__ __forceinline__ uint32_t hot_test(const P2Params& p, const HotPart& P, uint32_t pos, uint32_t i,
+                                             int64_t obase) {
+    const PayEl<HST> x = load_pay<HST>(p.payload, pos);
+    if (SGQ_WITHIN && expired(P.ts, hot_ts(p, x, obase), p.within)) return i * 2u;
+    return sgq_f1(sgq_ev1(x.w), P.cw, P.cn, p) ? i * 2u + 1u : HOT_LIVE;
+}
+__device__ __forceinline__ void hot_wl_push(uint32_t* wl, uint32_t* cnt, bool push, uint32_t slot, uint32_t h,
+                                            uint32_t cur) {
+    const uint64_t bal = __ballot(push);
+    if (bal == 0ull) return;
+    uint32_t base = 0;
+    if ((threadIdx.x & (SGD_WAVE - 1)) == 0) base = atomicAdd(cnt, (uint32_t)__popcll(bal));
+    base = (uint32_t)__shfl((int)base, 0, SGD_WAVE);
+    if (push) {
+        const uint32_t q = base + lane_rank(bal);
+        wl[3u * q] = slot;
+        wl[3u * q + 1u] = h;
+        wl[3u * q + 2u] = cur;
+    }
+}
+__device__ __forceinline__ uint32_t hot_wl_cap(const P2Params& p) { return p.max_batch + p.hot_cap * p.cap; }
+}  // namespace
+
+// per hot key: its run, its state and the conditions; then the offsets of the carried-in partials and of the
+// runs in the flat index spaces of the kernels below (one workgroup)
+extern "C" __global__ void __launch_bounds__(1024) k_hot_prep(const P2Params p) {
+    uint32_t* ctl = p.hot_ctl;
+    const uint32_t n = min(ctl[HC_N], p.hot_cap);
+    const int64_t obase = p.ts_col[0];
+    const uint32_t K = p.n_keys;
+    for (uint32_t h = threadIdx.x; h < n; h += blockDim.x) {
+        const uint32_t k = p.hot_list[h];
+        uint32_t* hi = p.hot_info + (size_t)h * SGD_HOT_INFO;
+        const uint32_t b = p.seg_begin[k], m = p.seg_end[k] - b;
+        const uint32_t hd = p.hdr[k];
+        const uint32_t sp = SGD_H_SPEND(hd), ss = SGD_H_SSTG(hd) + (SGD_H_INIT(hd) ? 0u : 1u);
+        const uint32_t n0 = SGD_H_INIT(hd) ? SGD_H_NPEND(hd) + SGD_H_NSTG(hd) : 0u;
+        bool bad = sp + ss != 1u || n0 > p.cap || m == 0u;
+        if (!bad) {  // the carried-in list: ts and seq ordered, no ts -1, none newer than the run's first event
+            const int64_t t0 = hot_ts(p, load_pay<HST>(p.payload, b), obase);
+            bad = t0 == -1;
+            int64_t pt = 0;
+            uint64_t pq = 0;
+            for (uint32_t j = 0; j < n0 && !bad; ++j) {
+                const int64_t t = p.p_ts[(size_t)j * K + k];
+                const uint64_t q = p.p_seq[(size_t)j * K + k];
+                bad = t == -1 || t > t0 || (j > 0u && (t < pt || q <= pq));
+                pt = t;
+                pq = q;
+            }
+        }
+        hi[HI_B] = b;
+        hi[HI_M] = bad ? 0u : m;
+        hi[HI_N0] = bad ? 0u : n0;
+        hi[HI_BAD] = bad ? 1u : 0u;
+        hi[HI_ALIVE] = 0u;
+        hi[HI_KEY] = k;
+    }
+    __syncthreads();
+    // exclusive scans of (carried-in count, run length): each thread a contiguous span of keys
+    __shared__ uint32_t s_x[16], s_e[16], s_m[16];
+    const uint32_t lane = threadIdx.x & (SGD_WAVE - 1), w = threadIdx.x / SGD_WAVE;
+    const uint32_t per = (n + blockDim.x - 1u) / blockDim.x;
+    const uint32_t lo = min(n, threadIdx.x * per), hi_ = min(n, lo + per);
+    uint32_t sx = 0, se = 0, mm = 0;
+    for (uint32_t h = lo; h < hi_; ++h) {
+        sx += p.hot_info[(size_t)h * SGD_HOT_INFO + HI_N0];
+        const uint32_t m = p.hot_info[(size_t)h * SGD_HOT_INFO + HI_M];
+        se += m;
+        mm = max(mm, m);
+    }
+    const uint32_t ix = wave_incl_scan(sx, (int)lane), ie = wave_incl_scan(se, (int)lane);
+    mm = wave_max_u(mm);
+    if (lane == SGD_WAVE - 1) { s_x[w] = ix; s_e[w] = ie; s_m[w] = mm; }
+    __syncthreads();
+    uint32_t ox = ix - sx, oe = ie - se;
+    for (uint32_t u = 0; u < w; ++u) { ox += s_x[u]; oe += s_e[u]; }
+    for (uint32_t h = lo; h < hi_; ++h) {
+        uint32_t* hi = p.hot_info + (size_t)h * SGD_HOT_INFO;
+        hi[HI_EXOFF] = ox;
+        hi[HI_EVOFF] = oe;
+        ox += hi[HI_N0];
+        oe += hi[HI_M];
+    }
+    if (threadIdx.x == 0) {
+        uint32_t tx = 0, te = 0, tm = 0;
+        for (uint32_t u = 0; u < blockDim.x / SGD_WAVE; ++u) { tx += s_x[u]; te += s_e[u]; tm = max(tm, s_m[u]); }
+        ctl[HC_EX] = tx;
+        ctl[HC_EV] = te;
+        ctl[HC_N1] = 0u;
+        ctl[HC_N2] = 0u;
+        ctl[HC_MAXM] = tm;
+    }
+}
+
+// round 0, a thread per partial slot (carried-in partials, then every event of the runs): the event's checks
+// (timestamps nondecreasing, none -1), f0 (a partial or not) and the first SGD_HOT_L0 events after it
+extern "C" __global__ void __launch_bounds__(256) k_hot_r0(const P2Params p) {
+    const uint32_t* ctl = p.hot_ctl;
+    const uint32_t n = min(ctl[HC_N], p.hot_cap), nex = ctl[HC_EX], total = nex + ctl[HC_EV];
+    const int64_t obase = p.ts_col[0];
+    const uint32_t lane = threadIdx.x & (SGD_WAVE - 1);
+    for (uint32_t x0 = blockIdx.x * blockDim.x + (threadIdx.x & ~(SGD_WAVE - 1)); x0 < total;
+         x0 += gridDim.x * blockDim.x) {
+        const uint32_t x = x0 + lane;
+        bool unres = false;
+        uint32_t slot = 0, h = 0, cur = 0;
+        if (x < total) {
+            const bool ex = x < nex;
+            h = hot_find(p.hot_info, n, ex ? x : x - nex, ex ? HI_EXOFF : HI_EVOFF);
+            const uint32_t* hi = p.hot_info + (size_t)h * SGD_HOT_INFO;
+            const uint32_t b = hi[HI_B], m = hi[HI_M];
+            HotPart P;
+            int start = -1;
+            bool part = true;
+            if (ex) {
+                slot = p.max_batch + x;
+                P = hot_existing(p, hi[HI_KEY], x - hi[HI_EXOFF]);
+            } else {
+                const uint32_t i = x - nex - hi[HI_EVOFF], pos = b + i;
+                slot = pos;
+                start = (int)i;
+                const PayEl<HST> ev = load_pay<HST>(p.payload, pos);
+                const int64_t ts = hot_ts(p, ev, obase);
+                if (ts == -1 || (i > 0u && hot_ts(p, load_pay<HST>(p.payload, pos - 1u), obase) > ts))
+                    p.hot_info[(size_t)h * SGD_HOT_INFO + HI_BAD] = 1u;
+                p.hot_tcnt[pos] = 0u;
+                const SgEv0 e0 = sgq_ev0(ev.w);
+                part = sgq_f0(e0, p);
+                if (part) {
+                    P.ts = ts;
+                    P.seq = p.seq_base + ev.w[0];
+                    P.cn = 0;
+#pragma unroll
+                    for (int w = 0; w < (SGQ_NCAPW > 0 ? SGQ_NCAPW : 1); ++w) P.cw[w] = 0;
+                    sgq_capture(e0, P.cw, P.cn);
+                }
+            }
+            uint32_t d = HOT_NOTP;
+            if (part) {
+                d = HOT_LIVE;
+                const uint32_t i0 = (uint32_t)(start + 1), i1 = min(m, i0 + SGD_HOT_L0);
+                for (uint32_t i = i0; i < i1 && d == HOT_LIVE; ++i) d = hot_test(p, P, b + i, i, obase);
+                unres = d == HOT_LIVE && i1 < m;
+                cur = i1;
+            }
+            p.hot_death[slot] = d;
+        }
+        hot_wl_push(p.hot_wl, &p.hot_ctl[HC_N1], unres, slot, h, cur);
+    }
+}
+
+// round 1, a wave per partial round 0 left open: the next SGD_HOT_L1 events, 64 at a time
+extern "C" __global__ void __launch_bounds__(256) k_hot_r1(const P2Params p) {
+    const uint32_t n1 = p.hot_ctl[HC_N1];
+    const int64_t obase = p.ts_col[0];
+    const uint32_t lane = threadIdx.x & (SGD_WAVE - 1);
+    const uint32_t nw = gridDim.x * (blockDim.x / SGD_WAVE);
+    const uint32_t* wl = p.hot_wl;
+    for (uint32_t q = blockIdx.x * (blockDim.x / SGD_WAVE) + threadIdx.x / SGD_WAVE; q < n1; q += nw) {
+        const uint32_t slot = uni(wl[3u * q]), h = uni(wl[3u * q + 1u]), cur = uni(wl[3u * q + 2u]);
+        const uint32_t* hi = p.hot_info + (size_t)h * SGD_HOT_INFO;
+        const uint32_t b = uni(hi[HI_B]), m = uni(hi[HI_M]);
+        int start;
+        const HotPart P = hot_part(p, slot, hi, obase, start);
+        const uint32_t end = min(m, cur + SGD_HOT_L1);
+        uint32_t d = HOT_LIVE;
+        for (uint32_t i0 = cur; i0 < end; i0 += SGD_WAVE) {
+            const uint32_t i = i0 + lane;
+            const uint32_t c = i < end ? hot_test(p, P, b + i, i, obase) : HOT_LIVE;
+            const uint64_t hit = __ballot(c != HOT_LIVE);
+            if (hit) {
+                d = (uint32_t)__shfl((int)c, __builtin_ctzll(hit), SGD_WAVE);
+                break;
+            }
+        }
+        if (lane == 0) p.hot_death[slot] = d;
+        hot_wl_push(p.hot_wl + 3u * (size_t)hot_wl_cap(p), &p.hot_ctl[HC_N2], lane == 0 && d == HOT_LIVE && end < m,
+                    slot, h, end);
+    }
+}
+
+// round 2, a wave per (open partial, SGD_HOT_BLK-event block of the rest of its run), nearest blocks first; a
+// block behind a hit already found is skipped
+extern "C" __global__ void __launch_bounds__(256) k_hot_r2(const P2Params p) {
+    const uint32_t n2 = p.hot_ctl[HC_N2];
+    if (n2 == 0u) return;
+    const uint64_t total = (uint64_t)n2 * ((p.hot_ctl[HC_MAXM] + SGD_HOT_BLK - 1u) / SGD_HOT_BLK);
+    const int64_t obase = p.ts_col[0];
+    const uint32_t lane = threadIdx.x & (SGD_WAVE - 1);
+    const uint32_t nw = gridDim.x * (blockDim.x / SGD_WAVE);
+    const uint32_t* wl = p.hot_wl + 3u * (size_t)hot_wl_cap(p);
+    for (uint64_t t = blockIdx.x * (blockDim.x / SGD_WAVE) + threadIdx.x / SGD_WAVE; t < total; t += nw) {
+        const uint32_t q = (uint32_t)(t % n2), blk = (uint32_t)(t / n2);
+        const uint32_t slot = uni(wl[3u * q]), h = uni(wl[3u * q + 1u]), cur = uni(wl[3u * q + 2u]);
+        const uint32_t* hi = p.hot_info + (size_t)h * SGD_HOT_INFO;
+        const uint32_t b = uni(hi[HI_B]), m = uni(hi[HI_M]);
+        const uint64_t lo64 = (uint64_t)cur + (uint64_t)blk * SGD_HOT_BLK;
+        if (lo64 >= m) continue;
+        const uint32_t lo = (uint32_t)lo64, end = min(m, lo + SGD_HOT_BLK);
+        if (uni(__hip_atomic_load(&p.hot_death[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < 2u * lo) continue;
+        int start;
+        const HotPart P = hot_part(p, slot, hi, obase, start);
+        uint32_t d = HOT_LIVE;
+        for (uint32_t i0 = lo; i0 < end; i0 += SGD_WAVE) {
+            const uint32_t i = i0 + lane;
+            const uint32_t c = i < end ? hot_test(p, P, b + i, i, obase) : HOT_LIVE;
+            const uint64_t hit = __ballot(c != HOT_LIVE);
+            if (hit) {
+                d = (uint32_t)__shfl((int)c, __builtin_ctzll(hit), SGD_WAVE);
+                break;
+            }
+        }
+        if (lane == 0 && d != HOT_LIVE) atomicMin(&p.hot_death[slot], d);
+    }
+}
+
+// per partial slot: the counters (exact, as the walk counts them), the trigger's match count, the survivors
+extern "C" __global__ void __launch_bounds__(256) k_hot_emit(const P2Params p) {
+    const uint32_t* ctl = p.hot_ctl;
+    const uint32_t n = min(ctl[HC_N], p.hot_cap), nex = ctl[HC_EX], total = nex + ctl[HC_EV];
+    unsigned long long sc = 0, cr = 0, mt = 0;
+    for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < total; x += gridDim.x * blockDim.x) {
+        const bool ex = x < nex;
+        const uint32_t h = hot_find(p.hot_info, n, ex ? x : x - nex, ex ? HI_EXOFF : HI_EVOFF);
+        uint32_t* hi = p.hot_info + (size_t)h * SGD_HOT_INFO;
+        if (hi[HI_BAD]) continue;
+        const uint32_t b = hi[HI_B], m = hi[HI_M];
+        uint32_t slot;
+        int start;
+        if (ex) {
+            slot = p.max_batch + x;
+            start = -1;
+        } else {
+            slot = b + (x - nex - hi[HI_EVOFF]);
+            start = (int)(slot - b);
+            sc += 1;  // the start state's seed tests every event (one seed armed)
+        }
+        const uint32_t d = p.hot_death[slot];
+        if (d == HOT_NOTP) continue;
+        if (!ex) cr += 1;
+        if (d == HOT_LIVE) {  // scanned by every later event of the run; a survivor
+            sc += (unsigned long long)((int64_t)m - 1 - start);
+            const uint32_t a = atomicAdd(&hi[HI_ALIVE], 1u);
+            if (a < p.cap) p.hot_alive[(size_t)h * p.cap + a] = slot;
+        } else {  // scanned up to its end; the expiring event removes it before its scan
+            const uint32_t i = d >> 1;
+            sc += (unsigned long long)((int64_t)i - start - 1 + (int64_t)(d & 1u));
+            if (d & 1u) {
+                mt += 1;
+                atomicAdd(&p.hot_tcnt[b + i], 1u);
+            }
+        }
+    }
+    __shared__ unsigned long long s_r[3][4];
+    const uint32_t lane = threadIdx.x & (SGD_WAVE - 1), w = threadIdx.x / SGD_WAVE;
+    sc = wave_sum(sc);
+    cr = wave_sum(cr);
+    mt = wave_sum(mt);
+    if (lane == 0) { s_r[0][w] = sc; s_r[1][w] = cr; s_r[2][w] = mt; }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        unsigned long long v = 0;
+        for (uint32_t u = 0; u < blockDim.x / SGD_WAVE; ++u) v += s_r[threadIdx.x][u];
+        const int which = threadIdx.x == 0 ? SGD_ST_SCANNED : threadIdx.x == 1 ? SGD_ST_CREATED : SGD_ST_MATCHES;
+        if (v) atomicAdd(&p.stats[which], v);
+    }
+}
+
+// per run event: its matches' raw slots (one reservation per workgroup) and its trigger descriptor
+extern "C" __global__ void __launch_bounds__(256) k_hot_trig(const P2Params p) {
+    const uint32_t* ctl = p.hot_ctl;
+    const uint32_t n = min(ctl[HC_N], p.hot_cap), nev = ctl[HC_EV];
+    __shared__ uint32_t s_w[4];
+    __shared__ unsigned long long s_base;
+    const uint32_t lane = threadIdx.x & (SGD_WAVE - 1), w = threadIdx.x / SGD_WAVE;
+    for (uint32_t x0 = blockIdx.x * blockDim.x; x0 < nev; x0 += gridDim.x * blockDim.x) {
+        const uint32_t x = x0 + threadIdx.x;
+        uint32_t c = 0, pos = 0;
+        if (x < nev) {
+            const uint32_t h = hot_find(p.hot_info, n, x, HI_EVOFF);
+            const uint32_t* hi = p.hot_info + (size_t)h * SGD_HOT_INFO;
+            if (!hi[HI_BAD]) {
+                pos = hi[HI_B] + (x - hi[HI_EVOFF]);
+                c = p.hot_tcnt[pos];
+            }
+        }
+        const uint32_t incl = wave_incl_scan(c, (int)lane);
+        if (lane == SGD_WAVE - 1) s_w[w] = incl;
+        __syncthreads();
+        uint32_t off = incl - c, tot = 0;
+        for (uint32_t u = 0; u < blockDim.x / SGD_WAVE; ++u) {
+            if (u < w) off += s_w[u];
+            tot += s_w[u];
+        }
+        if (threadIdx.x == 0) s_base = tot ? atomicAdd(p.raw_count, (unsigned long long)tot) : 0ull;
+        __syncthreads();
+        if (c) {
+            const unsigned long long first = p.raw_static + s_base + off;
+            if (first + c <= p.raw_capacity)
+                p.t_desc[p.payload[(size_t)pos * HST]] = ((uint64_t)c << 32) | (uint64_t)(uint32_t)first;
+            else
+                atomicOr(p.err, (uint32_t)SGD_ERR_MATCH_CAP);
+            p.hot_tbase[pos] = (uint32_t)first;
+            p.hot_tcnt[pos] = 0u;  // (the fill's rank counter)
+        }
+        __syncthreads();
+    }
+}
+
+// per matched partial: its e1 seq (and captures) into a slot of its trigger's range
+extern "C" __global__ void __launch_bounds__(256) k_hot_place(const P2Params p) {
+    const uint32_t* ctl = p.hot_ctl;
+    const uint32_t n = min(ctl[HC_N], p.hot_cap), nex = ctl[HC_EX], total = nex + ctl[HC_EV];
+    const int64_t obase = p.ts_col[0];
+    for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < total; x += gridDim.x * blockDim.x) {
+        const bool ex = x < nex;
+        const uint32_t h = hot_find(p.hot_info, n, ex ? x : x - nex, ex ? HI_EXOFF : HI_EVOFF);
+        const uint32_t* hi = p.hot_info + (size_t)h * SGD_HOT_INFO;
+        if (hi[HI_BAD]) continue;
+        const uint32_t slot = ex ? p.max_batch + x : hi[HI_B] + (x - nex - hi[HI_EVOFF]);
+        const uint32_t d = p.hot_death[slot];
+        if (d == HOT_NOTP || d == HOT_LIVE || !(d & 1u)) continue;
+        const uint32_t tp = hi[HI_B] + (d >> 1);
+        const uint64_t dst = (uint64_t)p.hot_tbase[tp] + atomicAdd(&p.hot_tcnt[tp], 1u);
+        if (dst >= p.raw_capacity) continue;
+        int start;
+        const HotPart P = hot_part(p, slot, hi, obase, start);
+        p.raw_e1[dst] = P.seq;
+#if SGQ_PROJ
+#pragma unroll
+        for (int w = 0; w < SGQ_NCAPW; ++w) p.raw_capw[(size_t)w * p.raw_capacity + dst] = P.cw[w];
+        if (SGQ_CAPNULL) p.raw_capnull[dst] = P.cn;
+#endif
+    }
+}
+
+// per trigger with several matches: its range in list order (= e1 seq order; insertion sort, ranges are short)
+extern "C" __global__ void __launch_bounds__(256) k_hot_sort(const P2Params p) {
+    const uint32_t* ctl = p.hot_ctl;
+    const uint32_t n = min(ctl[HC_N], p.hot_cap), nev = ctl[HC_EV];
+    for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < nev; x += gridDim.x * blockDim.x) {
+        const uint32_t h = hot_find(p.hot_info, n, x, HI_EVOFF);
+        const uint32_t* hi = p.hot_info + (size_t)h * SGD_HOT_INFO;
+        if (hi[HI_BAD]) continue;
+        const uint32_t pos = hi[HI_B] + (x - hi[HI_EVOFF]);
+        const uint32_t c = p.hot_tcnt[pos];
+        if (c < 2u) continue;
+        const uint64_t f = p.hot_tbase[pos];
+        if (f + c > p.raw_capacity) continue;
+        for (uint32_t a = 1; a < c; ++a) {
+            const uint64_t v = p.raw_e1[f + a];
+#if SGQ_PROJ
+            uint32_t cw[SGQ_NCAPW > 0 ? SGQ_NCAPW : 1], cn = 0;
+#pragma unroll
+            for (int w = 0; w < SGQ_NCAPW; ++w) cw[w] = p.raw_capw[(size_t)w * p.raw_capacity + f + a];
+            if (SGQ_CAPNULL) cn = p.raw_capnull[f + a];
+#endif
+            uint32_t z = a;
+            while (z > 0u && p.raw_e1[f + z - 1u] > v) {
+                p.raw_e1[f + z] = p.raw_e1[f + z - 1u];
+#if SGQ_PROJ
+#pragma unroll
+                for (int w = 0; w < SGQ_NCAPW; ++w)
+                    p.raw_capw[(size_t)w * p.raw_capacity + f + z] = p.raw_capw[(size_t)w * p.raw_capacity + f + z - 1u];
+                if (SGQ_CAPNULL) p.raw_capnull[f + z] = p.raw_capnull[f + z - 1u];
+#endif
+                --z;
+            }
+            p.raw_e1[f + z] = v;
+#if SGQ_PROJ
+#pragma unroll
+            for (int w = 0; w < SGQ_NCAPW; ++w) p.raw_capw[(size_t)w * p.raw_capacity + f + z] = cw[w];
+            if (SGQ_CAPNULL) p.raw_capnull[f + z] = cn;
+#endif
+        }
+    }
+}
+
+// a workgroup per hot key: the survivors in list order to the key's slab, the header, and the resume word that
+// tells the HBM pass the key is done
+extern "C" __global__ void __launch_bounds__(256) k_hot_final(const P2Params p) {
+    const uint32_t n = min(p.hot_ctl[HC_N], p.hot_cap);
+    const int64_t obase = p.ts_col[0];
+    __shared__ uint32_t s_slot[SGD_MAX_CAP + 1], s_ord[SGD_MAX_CAP + 1], s_key[SGD_MAX_CAP + 1];
+    for (uint32_t h = blockIdx.x; h < n; h += gridDim.x) {
+        const uint32_t* hi = p.hot_info + (size_t)h * SGD_HOT_INFO;
+        if (hi[HI_BAD]) continue;  // (uniform) left to the HBM pass
+        const uint32_t k = hi[HI_KEY], b = hi[HI_B], m = hi[HI_M], na = hi[HI_ALIVE];
+        if (na > p.cap) {  // more partials than the slab holds
+            if (threadIdx.x == 0) {
+                atomicOr(p.err, (uint32_t)SGD_ERR_PARTIAL_CAP);
+                p.resume[k] = SGD_HOT_DONE;
+            }
+            continue;
+        }
+        for (uint32_t a = threadIdx.x; a < na; a += blockDim.x) {
+            const uint32_t s = p.hot_alive[(size_t)h * p.cap + a];
+            s_slot[a] = s;
+            s_key[a] = s >= p.max_batch ? s - p.max_batch - hi[HI_EXOFF] : p.cap + (s - b);  // list order
+        }
+        __syncthreads();
+        for (uint32_t a = threadIdx.x; a < na; a += blockDim.x) {
+            uint32_t r = 0;
+            const uint32_t ka = s_key[a];
+            for (uint32_t u = 0; u < na; ++u) r += s_key[u] < ka ? 1u : 0u;
+            s_ord[r] = s_slot[a];
+        }
+        __syncthreads();
+        // in place, 256 at a time: survivor o comes from list index >= o, so a chunk's writes land below every
+        // later chunk's reads
+        const Slab G = hot_slab(p, k);
+        for (uint32_t c0 = 0; c0 < na; c0 += blockDim.x) {
+            const uint32_t o = c0 + threadIdx.x;
+            HotPart P;
+            int start;
+            if (o < na) P = hot_part(p, s_ord[o], hi, obase, start);
+            __syncthreads();
+            if (o < na) {
+                G.TS(o) = P.ts;
+                G.SEQ(o) = P.seq;
+#pragma unroll
+                for (int w = 0; w < SGQ_NCAPW; ++w) G.CAP(w, o) = P.cw[w];
+                if (SGQ_CAPNULL) G.NUL(o) = P.cn;
+            }
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) {
+            // the last event's partial (if f0 held) is still staged, and the seed it used re-arms at the next event
+            const bool lastf0 = p.hot_death[b + m - 1u] != HOT_NOTP;
+            const uint32_t gns = lastf0 ? 1u : 0u;
+            p.hdr[k] = SGD_H_MAKE(na - gns, gns, lastf0 ? 0u : 1u, lastf0 ? 1u : 0u, 1u);
+            p.resume[k] = SGD_HOT_DONE;
+        }
+        __syncthreads();
+    }
+}
+#endif  // SG_HOT

@@ -33,13 +33,13 @@
 // advance kernel reads its full timestamp from the batch's ts column
 #define SGD_TS_FAR ((int32_t)0x80000000)
 #define SGD_TS_LIM (1ll << 30)
-#define SGD_RAW_CHUNK 256
+#define SGD_RAW_CHUNK 256  // raw match slots a wave reserves at a time (the raw buffer has 2 chunks of slack per wave)
 #define SGD_TD_INLINE (1ull << 63)  // t_desc: the trigger's one match carried inline (no raw slot)
 // the fused grouping's LDS split keeps up to this many 64-event rounds per wave in registers (p2_jit.hip
 // tile_split_lds): a tile of more than SGD_SPLIT_CHUNKS(stride) * SGD_BLOCK events goes to the HBM pass
 #define SGD_SPLIT_CHUNKS(stride) (80u / ((stride) + 1u))
 #define SGD_SPLIT_CNT_BYTES ((SGD_BLOCK / SGD_WAVE) * SGD_BLOCK * 2u)   // its per-(wave, key) u16 counters
-#define SGD_HBM_STAGE_BYTES 32768u  // the HBM pass: LDS staging of one wave's runs (dynamic LDS of its 1-wave groups)  // raw match slots a wave reserves at a time (the raw buffer has 2 chunks of slack per wave)
+#define SGD_HBM_STAGE_BYTES 32768u  // the HBM pass: LDS staging of one wave's runs (dynamic LDS of its 1-wave groups)
 
 // ---- filters ------------------------------------------------------------------------------------
 // A filter's IR bytecode (siddhi_gpu_ir.h) is lowered to DProg (variables resolved to event
@@ -77,6 +77,10 @@ enum {
     ((uint32_t)(np) | ((uint32_t)(ns) << 12) | ((uint32_t)(sp) << 24) | ((uint32_t)(ss) << 26) | ((uint32_t)(in) << 28))
 #define SGD_MAX_CAP 4095u
 #define SGD_NO_RESUME 0xffffffffu
+#define SGD_HOT_DONE 0xfffffffeu   // resume word: the hot-key pipeline advanced the key (the HBM pass skips it)
+#define SGD_HOT_MARK 0xfffffffdu   // resume word: a hot key of a wave the staged pass left whole (counted there)
+#define SGD_HOT_CTL 8
+#define SGD_HOT_INFO 8
 
 enum { SGD_ST_SCANNED = 0, SGD_ST_CREATED, SGD_ST_MATCHES, SGD_ST_KEYS, SGD_ST_LIVE0, SGD_ST_SPILLS, SGD_ST_N };
 
@@ -132,6 +136,21 @@ struct P2Params {
     uint32_t* raw_capw;                // SGQ_PROJ: [n_capw][raw_capacity] the matched partial's captures
     uint32_t* raw_capnull;             // SGQ_PROJ: [raw_capacity] their null bits
     uint32_t stage_chunks;             // LDS staging per wave, 16-B chunks (dynamic LDS = waves x this)
+    // hot keys (`every e1 -> e2` on one stream; p2_jit.hip k_hot_*): the staged pass leaves a key with at least
+    // hot_min events in the batch to the hot-key pipeline, which advances all of its partials at once (a
+    // partial's fate is the first later event that expires or matches it); 0 = off
+    uint32_t hot_min;
+    uint32_t hot_cap;                  // hot_list entries (further hot keys are walked by their lanes)
+    uint32_t max_batch;                // partial slots: [0, max_batch) created at that payload position, then the
+                                       // keys' partials carried in from the previous batch
+    uint32_t* hot_ctl;                 // [SGD_HOT_CTL] counters (hot_ctl[0]: hot keys listed; reset by the HBM pass)
+    uint32_t* hot_list;                // [hot_cap] keys
+    uint32_t* hot_info;                // [hot_cap][SGD_HOT_INFO] per hot key: run, offsets, checks, survivors
+    uint32_t* hot_death;               // [max_batch + hot_cap * cap] per partial slot: 2 * event + matched
+    uint32_t* hot_wl;                  // [2][max_batch + hot_cap * cap][3] unresolved partials (slot, key, cursor)
+    uint32_t* hot_tcnt;                // [max_batch] matches per trigger (by payload position)
+    uint32_t* hot_tbase;               // [max_batch] their first raw slot
+    uint32_t* hot_alive;               // [hot_cap][cap] surviving partial slots
     uint32_t pad;
     uint64_t cst[SGD_MAX_CONST];       // filter constants, already in their comparison domain
 };

@@ -135,6 +135,7 @@ struct sg_engine {
         hipFunction_t adv[2] = {nullptr, nullptr};   // [0]: multi / state-0 stream, [1]: state-1 stream
         hipFunction_t adv_h[2] = {nullptr, nullptr}; // the HBM pass over the waves the staged pass deferred
         hipFunction_t pack[2] = {nullptr, nullptr};
+        hipFunction_t hot[9] = {};                   // the hot-key pipeline (k_hot_prep .. k_hot_final)
     };
     JitQuery jq;
     std::vector<uint64_t> consts;
@@ -188,6 +189,15 @@ struct sg_engine {
     unsigned long long* prof = nullptr;  // SG_PROF: walk-phase clocks of the staged pass (experiments)
     size_t prof_rows = 0;
     uint32_t* resume = nullptr;    // per key: where the HBM pass resumes a key the staged pass stopped
+    // hot keys (`every e1 -> e2` on one stream, p2_jit.hip k_hot_*): the staged pass lists a key with >= hot_min
+    // events; the pipeline runs after it while recent batches had such keys (hot_on: their count comes back in
+    // the status block), otherwise the HBM pass walks them
+    bool hot_ok = false;
+    bool hot_on = true;
+    uint32_t hot_min = 0, hot_cap = 0;
+    uint32_t *hot_ctl = nullptr, *hot_list = nullptr, *hot_info = nullptr, *hot_death = nullptr, *hot_wl = nullptr;
+    uint32_t *hot_tcnt = nullptr, *hot_tbase = nullptr, *hot_alive = nullptr;
+    uint64_t hot_batches = 0;      // batches the pipeline ran on (sg_engine_describe)
     uint32_t hbm_grid = 2048;      // work-groups of the HBM pass (SG_HBM_GRID: experiments)
     uint32_t* dlist = nullptr;     // the waves the HBM pass takes, and their number
     uint32_t* dlist_n = nullptr;
@@ -552,6 +562,25 @@ void allocate(sg_engine* e) {
         e->prof_rows = nw;
     }
     HIP_OK(hipMemsetAsync(e->resume, 0xff, K * 4, e->stream));  // SGD_NO_RESUME
+    e->hot_ok = e->plan.s0 == e->plan.s1 && e->plan.mode == SGD_P2_EVERY_FIRST;
+    {
+        const char* x = getenv("SG_HOT_MIN");  // 0: off
+        e->hot_min = x ? (uint32_t)strtoul(x, nullptr, 0) : 256u;
+        if (e->hot_min == 0) e->hot_ok = false;
+    }
+    if (e->hot_ok) {
+        e->hot_cap = (uint32_t)std::min<size_t>({B / std::max(1u, e->hot_min) + 1, K, 65536, std::max<size_t>(1, (1u << 22) / C)});
+        const size_t slots = B + (size_t)e->hot_cap * C;
+        e->hot_ctl = dalloc<uint32_t>(SGD_HOT_CTL, o);
+        HIP_OK(hipMemsetAsync(e->hot_ctl, 0, SGD_HOT_CTL * 4, e->stream));
+        e->hot_list = dalloc<uint32_t>(e->hot_cap, o);
+        e->hot_info = dalloc<uint32_t>((size_t)e->hot_cap * SGD_HOT_INFO, o);
+        e->hot_death = dalloc<uint32_t>(slots, o);
+        e->hot_wl = dalloc<uint32_t>(2 * 3 * slots, o);
+        e->hot_tcnt = dalloc<uint32_t>(B, o);
+        e->hot_tbase = dalloc<uint32_t>(B, o);
+        e->hot_alive = dalloc<uint32_t>((size_t)e->hot_cap * C, o);
+    }
     e->tile_sum = dalloc<uint32_t>(B / SGD_ORDER_TILE + 1, o);
     e->tile_off = dalloc<uint32_t>(B / SGD_ORDER_TILE + 1, o);
     // the match count and the error word share 16 bytes, so poll reads both with one D2H copy
@@ -620,6 +649,11 @@ sg_engine::Variant& variant(sg_engine* e, bool evnull, bool capnull) {
         HIP_OK(hipModuleGetFunction(&r.adv_h[0], r.mod, "k_adv_s0_h"));
         HIP_OK(hipModuleGetFunction(&r.adv_h[1], r.mod, "k_adv_s1_h"));
     }
+    if (e->hot_ok) {
+        static const char* const names[9] = {"k_hot_prep", "k_hot_r0", "k_hot_r1", "k_hot_r2", "k_hot_emit",
+                                             "k_hot_trig", "k_hot_place", "k_hot_sort", "k_hot_final"};
+        for (int i = 0; i < 9; i++) HIP_OK(hipModuleGetFunction(&r.hot[i], r.mod, names[i]));
+    }
     HIP_OK(hipModuleGetFunction(&r.pack[0], r.mod, "k_pack0"));
     HIP_OK(hipModuleGetFunction(&r.pack[1], r.mod, "k_pack1"));
     return r;
@@ -682,6 +716,7 @@ static void drain_one(sg_engine* e) {  // wait for the oldest in-flight batch
     HIP_OK(hipEventSynchronize(e->done_ev[ri]));
     e->done_count = e->h_status[2 * ri];
     e->done_err |= (uint32_t)e->h_status[2 * ri + 1];
+    if (e->hot_ok) e->hot_on = (e->h_status[2 * ri + 1] >> 32) != 0;  // the batch's hot keys (p2_jit.hip hbm_pass)
     e->inflight.erase(e->inflight.begin());
 }
 
@@ -893,6 +928,21 @@ int push(sg_engine* e, const sg_batch* b) {
     p.err = e->err;
     p.raw_capw = e->raw_capw;
     p.raw_capnull = e->raw_capnull;
+    if (e->hot_ok) {
+        // a partitioned batch's keys hold n / K events on average: "hot" is far above that (and above hot_min)
+        p.hot_min = pl.partitioned ? std::max<uint32_t>(e->hot_min, (uint32_t)std::min<uint64_t>(8ull * n / e->K, 1u << 30))
+                                   : e->hot_min;
+        p.hot_cap = e->hot_cap;
+        p.max_batch = (uint32_t)e->maxb;
+        p.hot_ctl = e->hot_ctl;
+        p.hot_list = e->hot_list;
+        p.hot_info = e->hot_info;
+        p.hot_death = e->hot_death;
+        p.hot_wl = e->hot_wl;
+        p.hot_tcnt = e->hot_tcnt;
+        p.hot_tbase = e->hot_tbase;
+        p.hot_alive = e->hot_alive;
+    }
     for (size_t i = 0; i < e->consts.size(); i++) p.cst[i] = e->consts[i];
     hipEvent_t a0 = nullptr, a1 = nullptr;
     if (e->timing) { a0 = e->ev(); e->mark(a0); }
@@ -904,6 +954,11 @@ int push(sg_engine* e, const sg_batch* b) {
         launch(v.adv[role], blocks, SGD_BLOCK, &p, e->stream,
                p.stage_chunks * 16u * (SGD_BLOCK / SGD_WAVE) + (fused ? SGD_SPLIT_CNT_BYTES : 0u));
         if (e->timing) { a1 = e->ev(); e->mark(a1); e->spans.push_back({a0, a1, 1}); a0 = e->ev(); e->mark(a0); }
+        if (e->hot_ok && e->hot_on) {  // the hot keys the staged pass listed (fixed grids: the counts are on the device)
+            static const uint32_t grid[9] = {1, 1024, 512, 1024, 1024, 1024, 1024, 1024, 256};
+            for (int i = 0; i < 9; i++) launch(v.hot[i], grid[i], i == 0 ? 1024 : 256, &p, e->stream);
+            e->hot_batches++;
+        }
         // one wave per work-group over the listed waves (a fixed grid: the list's length is on the device)
         launch(v.adv_h[role], std::min<uint32_t>(blocks * (SGD_BLOCK / SGD_WAVE), e->hbm_grid), SGD_WAVE, &p, e->stream,
                p.hbm_stage_chunks * 16u);
@@ -1630,6 +1685,8 @@ int sg_engine_describe(sg_engine* e, char* out, size_t out_len) {
                                "k_adv_m (key split in LDS + NFA advance, LDS-staged, lane per key)"
                              : "k_part_hist + k_part_scan + k_part_scatter per 8-bit digit + k_part_bounds (grouping, stream 2); "
                                "k_adv_m (NFA advance, LDS-staged, lane per key)") +
+            (one->hot_batches ? " + k_hot_prep..k_hot_final (hot keys, partials in parallel, " +
+                                    std::to_string(one->hot_batches) + " batches)" : std::string()) +
             " + k_adv_m_h (NFA advance, HBM pass) + k_stats_reduce; k_order_sums + scan + k_order_scatter (ordering)";
         if (one->proj_n) d += " + k_project" + std::string(one->n_agg ? " + k_agg" : "");
     }

@@ -73,7 +73,7 @@ def main():
                           "order_ms": round((st["order_ns"] - st0["order_ns"]) / 1e6 / n, 4),
                           "matches": (st["matches"] - st0["matches"]) / n,
                           "spills": (st["window_spills"] - st0["window_spills"]) / n,
-                          "describe": eng.describe()[:60]}), flush=True)
+                          "hot_pipeline": "k_hot_prep" in eng.describe()}), flush=True)
         eng.close()
         del bat
         torch.cuda.empty_cache()
