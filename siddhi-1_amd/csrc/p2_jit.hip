@@ -662,6 +662,7 @@ __device__ __forceinline__ void advance(const P2Params& p, const uint32_t gid) {
             const uint32_t nt = bhi - blo;
             const uint64_t f_lo = (uint64_t)blo * SB / 16u, f_hi = ((uint64_t)bhi * SB + 15u) / 16u;
             fits = nt <= SGD_SPLIT_CHUNKS(STRIDE) * SGD_BLOCK && f_hi - f_lo <= (uint64_t)p.stage_chunks * NW;
+            if (nt > SGD_BIG_TILE && threadIdx.x == 0 && p.hot_ctl) atomicAdd(&p.hot_ctl[SGD_HOT_CTL_BIG], 1u);
             uint32_t kb = 0, kc = 0;
             if (nt > 0 && fits) {
                 const uint32_t nch = (uint32_t)(f_hi - f_lo);
@@ -769,6 +770,9 @@ __device__ __forceinline__ void advance(const P2Params& p, const uint32_t gid) {
     const uint64_t c_lo = (uint64_t)blo * SB / 16u, c_hi = ((uint64_t)bhi * SB + 15u) / 16u;
     if constexpr (STG) {
         if (!fused) fits = SGX_GLB_WALK || bhi <= blo || c_hi - c_lo <= (uint64_t)p.stage_chunks * NW;
+        // (a giant workgroup range: the host keeps the sorted grouping while batches have them)
+        if (!fused && bhi > blo && bhi - blo > SGD_BIG_TILE && threadIdx.x == 0 && p.hot_ctl)
+            atomicAdd(&p.hot_ctl[SGD_HOT_CTL_BIG], 1u);
         // this wave's p.deferred entry: 1 = the HBM pass takes the whole workgroup (its range does not
         // fit); keys stopped early raise it to 2 after the walk (written after the barrier below)
         if (lane == 0) p.deferred[wave_id] = (!fits && bhi > blo) ? 1u : 0u;
@@ -1279,10 +1283,11 @@ __device__ __forceinline__ void pack(const PackParams& q) {
 template <bool S0, bool S1> __device__ __forceinline__ void hbm_pass(const P2Params& p) {
     const uint32_t n = __builtin_amdgcn_readfirstlane(*p.dlist_n);
     if (p.hot_ctl && blockIdx.x == 0 && threadIdx.x == 0) {
-        // the batch's hot keys (after the pipeline): into the status block's spare word (the host turns the
-        // pipeline on while batches have them), and the list reset for the next batch
-        p.err[1] = p.hot_ctl[0];
+        // the batch's hot keys (after the pipeline) and giant workgroup ranges: into the status block's spare word
+        // (the host runs the pipeline / the sorted grouping while batches have them); reset for the next batch
+        p.err[1] = min(p.hot_ctl[0], 0xffffu) | (min(p.hot_ctl[SGD_HOT_CTL_BIG], 0xffffu) << 16);
         p.hot_ctl[0] = 0u;
+        p.hot_ctl[SGD_HOT_CTL_BIG] = 0u;
     }
     for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
         const uint32_t w = __builtin_amdgcn_readfirstlane(p.dlist[i]);
@@ -1315,20 +1320,22 @@ extern "C" __global__ void __launch_bounds__(256) k_pack1(const PackParams q) { 
 //     are a prefix of the list, as the reference's prefix rule assumes) or satisfies f1(e_j, e_i) (a match,
 //     emitted by e_i; StreamPostStateProcessor.java:64-83);
 //   - the matches of one trigger are its matched partials in list order (creation order = seq order).
-// So a partial's fate is a first-hit search over the run, done in three rounds: a thread per partial over
-// SGD_HOT_L0 events, a wave per survivor over SGD_HOT_L1 more, then SGD_HOT_BLK-event blocks of the rest in
-// parallel (atomicMin of the hit).  The triggers' match counts, their raw slots, the slot fill and the in-trigger
-// seq order follow; the survivors (ordered) become the key's slab list.  A key whose run breaks the conditions
-// is left to the HBM pass (its resume word untouched), which walks it as before.
+// So a partial's fate is a first-hit search over the run, done in rounds: a thread per partial over the
+// SGD_HOT_L0 events after it (staged in LDS), a wave per partial still open over SGD_HOT_L1 more, then blocks of
+// SGD_HOT_L1 events in parallel over spans 8x longer each round (atomicMin of the hit; the partials still open
+// are about inversely proportional to the distance scanned, so every round costs about the same).  The
+// triggers' match counts, their raw slots, the slot fill and the in-trigger seq order follow; the survivors
+// (ordered) become the key's slab list.  A key whose run breaks the conditions is left to the HBM pass (its
+// resume word untouched), which walks it as before.
 #if SG_HOT
-#define SGD_HOT_L0 32u
-#define SGD_HOT_L1 512u
-#define SGD_HOT_BLK 4096u
+#define SGD_HOT_C 256u     // round 0: events per workgroup
+#define SGD_HOT_L0 128u    // round 0: events each partial scans (staged in LDS after the workgroup's)
+#define SGD_HOT_L1 512u    // round 1: events each open partial scans; rounds >= 2: x8 per round
 namespace {
 constexpr uint32_t HOT_NOTP = 0xfffffffeu;  // death word of a payload position whose event made no partial
 constexpr uint32_t HOT_LIVE = 0xffffffffu;  // no event of the run ends the partial (or not found yet)
 enum { HI_B = 0, HI_M, HI_EXOFF, HI_EVOFF, HI_N0, HI_BAD, HI_ALIVE, HI_KEY };
-enum { HC_N = 0, HC_EX, HC_EV, HC_N1, HC_N2, HC_MAXM };
+enum { HC_N = 0, HC_EX, HC_EV, HC_L0, HC_L1, HC_MAXM, HC_BIG };
 constexpr int HST = SGQ_STRIDE0;
 
 struct HotPart {
@@ -1475,76 +1482,107 @@ extern "C" __global__ void __launch_bounds__(1024) k_hot_prep(const P2Params p) 
         for (uint32_t u = 0; u < blockDim.x / SGD_WAVE; ++u) { tx += s_x[u]; te += s_e[u]; tm = max(tm, s_m[u]); }
         ctl[HC_EX] = tx;
         ctl[HC_EV] = te;
-        ctl[HC_N1] = 0u;
-        ctl[HC_N2] = 0u;
+        ctl[HC_L0] = 0u;
+        ctl[HC_L1] = 0u;
         ctl[HC_MAXM] = tm;
     }
 }
 
-// round 0, a thread per partial slot (carried-in partials, then every event of the runs): the event's checks
-// (timestamps nondecreasing, none -1), f0 (a partial or not) and the first SGD_HOT_L0 events after it
-extern "C" __global__ void __launch_bounds__(256) k_hot_r0(const P2Params p) {
+// round 0.  The carried-in partials: a thread each over the first SGD_HOT_L0 events of the run (from HBM).  The
+// runs' events: a workgroup per SGD_HOT_C consecutive (flat) events, staged in LDS with the SGD_HOT_L0 events
+// after them; a thread per event checks it (timestamps nondecreasing, none -1), evaluates f0 (a partial or not)
+// and scans the staged events after it.  Every flat index's hot key goes to hot_fh for the kernels after.
+extern "C" __global__ void __launch_bounds__(SGD_HOT_C) k_hot_r0(const P2Params p) {
     const uint32_t* ctl = p.hot_ctl;
     const uint32_t n = min(ctl[HC_N], p.hot_cap), nex = ctl[HC_EX], total = nex + ctl[HC_EV];
     const int64_t obase = p.ts_col[0];
-    const uint32_t lane = threadIdx.x & (SGD_WAVE - 1);
-    for (uint32_t x0 = blockIdx.x * blockDim.x + (threadIdx.x & ~(SGD_WAVE - 1)); x0 < total;
-         x0 += gridDim.x * blockDim.x) {
+    const uint32_t lane = threadIdx.x & (SGD_WAVE - 1), tid = threadIdx.x;
+    for (uint32_t x0 = blockIdx.x * SGD_HOT_C + (tid & ~(SGD_WAVE - 1)); x0 < nex; x0 += gridDim.x * SGD_HOT_C) {
         const uint32_t x = x0 + lane;
         bool unres = false;
         uint32_t slot = 0, h = 0, cur = 0;
-        if (x < total) {
-            const bool ex = x < nex;
-            h = hot_find(p.hot_info, n, ex ? x : x - nex, ex ? HI_EXOFF : HI_EVOFF);
+        if (x < nex) {
+            h = hot_find(p.hot_info, n, x, HI_EXOFF);
+            p.hot_fh[x] = h;
             const uint32_t* hi = p.hot_info + (size_t)h * SGD_HOT_INFO;
             const uint32_t b = hi[HI_B], m = hi[HI_M];
-            HotPart P;
-            int start = -1;
-            bool part = true;
-            if (ex) {
-                slot = p.max_batch + x;
-                P = hot_existing(p, hi[HI_KEY], x - hi[HI_EXOFF]);
-            } else {
-                const uint32_t i = x - nex - hi[HI_EVOFF], pos = b + i;
-                slot = pos;
-                start = (int)i;
-                const PayEl<HST> ev = load_pay<HST>(p.payload, pos);
-                const int64_t ts = hot_ts(p, ev, obase);
-                if (ts == -1 || (i > 0u && hot_ts(p, load_pay<HST>(p.payload, pos - 1u), obase) > ts))
-                    p.hot_info[(size_t)h * SGD_HOT_INFO + HI_BAD] = 1u;
-                p.hot_tcnt[pos] = 0u;
-                const SgEv0 e0 = sgq_ev0(ev.w);
-                part = sgq_f0(e0, p);
-                if (part) {
-                    P.ts = ts;
-                    P.seq = p.seq_base + ev.w[0];
-                    P.cn = 0;
-#pragma unroll
-                    for (int w = 0; w < (SGQ_NCAPW > 0 ? SGQ_NCAPW : 1); ++w) P.cw[w] = 0;
-                    sgq_capture(e0, P.cw, P.cn);
-                }
-            }
-            uint32_t d = HOT_NOTP;
-            if (part) {
-                d = HOT_LIVE;
-                const uint32_t i0 = (uint32_t)(start + 1), i1 = min(m, i0 + SGD_HOT_L0);
-                for (uint32_t i = i0; i < i1 && d == HOT_LIVE; ++i) d = hot_test(p, P, b + i, i, obase);
-                unres = d == HOT_LIVE && i1 < m;
-                cur = i1;
-            }
+            slot = p.max_batch + x;
+            const HotPart P = hot_existing(p, hi[HI_KEY], x - hi[HI_EXOFF]);
+            uint32_t d = HOT_LIVE;
+            const uint32_t i1 = min(m, SGD_HOT_L0);
+            for (uint32_t i = 0; i < i1 && d == HOT_LIVE; ++i) d = hot_test(p, P, b + i, i, obase);
+            unres = d == HOT_LIVE && i1 < m;
+            cur = i1;
             p.hot_death[slot] = d;
         }
-        hot_wl_push(p.hot_wl, &p.hot_ctl[HC_N1], unres, slot, h, cur);
+        hot_wl_push(p.hot_wl + 3u * (size_t)hot_wl_cap(p), &p.hot_ctl[HC_L1], unres, slot, h, cur);
+    }
+    constexpr uint32_t ST = SGD_HOT_C + SGD_HOT_L0;
+    __shared__ uint32_t s_w[ST * HST];
+    __shared__ int64_t s_ts[ST];
+    for (uint32_t x0 = nex + blockIdx.x * SGD_HOT_C; x0 < total; x0 += gridDim.x * SGD_HOT_C) {
+        uint32_t h = 0, pos = 0, i = 0, m = 0;
+        for (uint32_t t = tid; t < ST; t += SGD_HOT_C) {
+            const uint32_t x = x0 + t;
+            if (x >= total) break;
+            const uint32_t hx = hot_find(p.hot_info, n, x - nex, HI_EVOFF);
+            const uint32_t* hi = p.hot_info + (size_t)hx * SGD_HOT_INFO;
+            const uint32_t ix = x - nex - hi[HI_EVOFF], px = hi[HI_B] + ix;
+            const PayEl<HST> ev = load_pay<HST>(p.payload, px);
+#pragma unroll
+            for (int u = 0; u < HST; ++u) s_w[t * HST + u] = ev.w[u];
+            s_ts[t] = hot_ts(p, ev, obase);
+            if (t < SGD_HOT_C) {
+                h = hx;
+                pos = px;
+                i = ix;
+                m = hi[HI_M];
+                p.hot_fh[x] = hx;
+            }
+        }
+        __syncthreads();
+        const uint32_t x = x0 + tid;
+        bool unres = false;
+        uint32_t cur = 0;
+        if (x < total) {
+            const int64_t ts = s_ts[tid];
+            const int64_t tp = i == 0u ? ts : tid > 0u ? s_ts[tid - 1] : hot_ts(p, load_pay<HST>(p.payload, pos - 1u), obase);
+            if (ts == -1 || tp > ts) p.hot_info[(size_t)h * SGD_HOT_INFO + HI_BAD] = 1u;
+            p.hot_tcnt[pos] = 0u;
+            const SgEv0 e0 = sgq_ev0(&s_w[tid * HST]);
+            uint32_t d = HOT_NOTP;
+            if (sgq_f0(e0, p)) {
+                HotPart P;
+                P.ts = ts;
+                P.cn = 0;
+#pragma unroll
+                for (int w = 0; w < (SGQ_NCAPW > 0 ? SGQ_NCAPW : 1); ++w) P.cw[w] = 0;
+                sgq_capture(e0, P.cw, P.cn);
+                d = HOT_LIVE;
+                const uint32_t nj = min(m - 1u - i, SGD_HOT_L0);
+                for (uint32_t j = 1; j <= nj && d == HOT_LIVE; ++j) {
+                    const uint32_t t = tid + j;
+                    if (SGQ_WITHIN && expired(P.ts, s_ts[t], p.within)) d = (i + j) * 2u;
+                    else if (sgq_f1(sgq_ev1(&s_w[t * HST]), P.cw, P.cn, p)) d = (i + j) * 2u + 1u;
+                }
+                unres = d == HOT_LIVE && i + 1u + nj < m;
+                cur = i + 1u + nj;
+            }
+            p.hot_death[pos] = d;
+        }
+        hot_wl_push(p.hot_wl + 3u * (size_t)hot_wl_cap(p), &p.hot_ctl[HC_L1], unres, pos, h, cur);
+        __syncthreads();
     }
 }
 
-// round 1, a wave per partial round 0 left open: the next SGD_HOT_L1 events, 64 at a time
+// round 1, a wave per partial round 0 left open: the next SGD_HOT_L1 events, 64 at a time; still open: to the
+// list of round 2
 extern "C" __global__ void __launch_bounds__(256) k_hot_r1(const P2Params p) {
-    const uint32_t n1 = p.hot_ctl[HC_N1];
+    const uint32_t n1 = p.hot_ctl[HC_L1];
     const int64_t obase = p.ts_col[0];
     const uint32_t lane = threadIdx.x & (SGD_WAVE - 1);
     const uint32_t nw = gridDim.x * (blockDim.x / SGD_WAVE);
-    const uint32_t* wl = p.hot_wl;
+    const uint32_t* wl = p.hot_wl + 3u * (size_t)hot_wl_cap(p);
     for (uint32_t q = blockIdx.x * (blockDim.x / SGD_WAVE) + threadIdx.x / SGD_WAVE; q < n1; q += nw) {
         const uint32_t slot = uni(wl[3u * q]), h = uni(wl[3u * q + 1u]), cur = uni(wl[3u * q + 2u]);
         const uint32_t* hi = p.hot_info + (size_t)h * SGD_HOT_INFO;
@@ -1563,29 +1601,34 @@ extern "C" __global__ void __launch_bounds__(256) k_hot_r1(const P2Params p) {
             }
         }
         if (lane == 0) p.hot_death[slot] = d;
-        hot_wl_push(p.hot_wl + 3u * (size_t)hot_wl_cap(p), &p.hot_ctl[HC_N2], lane == 0 && d == HOT_LIVE && end < m,
-                    slot, h, end);
+        hot_wl_push(p.hot_wl, &p.hot_ctl[HC_L0], lane == 0 && d == HOT_LIVE && end < m, slot, h, end);
     }
 }
 
-// round 2, a wave per (open partial, SGD_HOT_BLK-event block of the rest of its run), nearest blocks first; a
-// block behind a hit already found is skipped
-extern "C" __global__ void __launch_bounds__(256) k_hot_r2(const P2Params p) {
-    const uint32_t n2 = p.hot_ctl[HC_N2];
-    if (n2 == 0u) return;
-    const uint64_t total = (uint64_t)n2 * ((p.hot_ctl[HC_MAXM] + SGD_HOT_BLK - 1u) / SGD_HOT_BLK);
+// rounds 2, 3, ... (p.hot_round): the partials still open scan their next SGD_HOT_L1 << 3 (round - 1) events, a
+// wave per (partial, SGD_HOT_L1-event block), nearest blocks first, a block behind a hit already found skipped;
+// the hit is the least (atomicMin).  The round reads list (round & 1) and zeroes the other one, which
+// k_hot_rc fills with the partials still open after it.
+__device__ __forceinline__ uint32_t hot_span(uint32_t round) { return SGD_HOT_L1 << (3u * (round - 1u)); }
+extern "C" __global__ void __launch_bounds__(256) k_hot_rn(const P2Params p) {
+    const uint32_t in = p.hot_round & 1u;
+    const uint32_t nq = p.hot_ctl[HC_L0 + in];
+    if (blockIdx.x == 0 && threadIdx.x == 0) p.hot_ctl[HC_L0 + (in ^ 1u)] = 0u;
+    if (nq == 0u) return;
+    const uint32_t span = hot_span(p.hot_round), nblk = span / SGD_HOT_L1;
+    const uint64_t total = (uint64_t)nq * nblk;
     const int64_t obase = p.ts_col[0];
     const uint32_t lane = threadIdx.x & (SGD_WAVE - 1);
     const uint32_t nw = gridDim.x * (blockDim.x / SGD_WAVE);
-    const uint32_t* wl = p.hot_wl + 3u * (size_t)hot_wl_cap(p);
+    const uint32_t* wl = p.hot_wl + 3u * (size_t)hot_wl_cap(p) * in;
     for (uint64_t t = blockIdx.x * (blockDim.x / SGD_WAVE) + threadIdx.x / SGD_WAVE; t < total; t += nw) {
-        const uint32_t q = (uint32_t)(t % n2), blk = (uint32_t)(t / n2);
+        const uint32_t q = (uint32_t)(t % nq), blk = (uint32_t)(t / nq);
         const uint32_t slot = uni(wl[3u * q]), h = uni(wl[3u * q + 1u]), cur = uni(wl[3u * q + 2u]);
         const uint32_t* hi = p.hot_info + (size_t)h * SGD_HOT_INFO;
         const uint32_t b = uni(hi[HI_B]), m = uni(hi[HI_M]);
-        const uint64_t lo64 = (uint64_t)cur + (uint64_t)blk * SGD_HOT_BLK;
+        const uint64_t lo64 = (uint64_t)cur + (uint64_t)blk * SGD_HOT_L1;
         if (lo64 >= m) continue;
-        const uint32_t lo = (uint32_t)lo64, end = min(m, lo + SGD_HOT_BLK);
+        const uint32_t lo = (uint32_t)lo64, end = min(m, lo + SGD_HOT_L1);
         if (uni(__hip_atomic_load(&p.hot_death[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < 2u * lo) continue;
         int start;
         const HotPart P = hot_part(p, slot, hi, obase, start);
@@ -1602,15 +1645,35 @@ extern "C" __global__ void __launch_bounds__(256) k_hot_r2(const P2Params p) {
         if (lane == 0 && d != HOT_LIVE) atomicMin(&p.hot_death[slot], d);
     }
 }
+// after round p.hot_round: the partials it left open with events still ahead, to the next round's list
+extern "C" __global__ void __launch_bounds__(256) k_hot_rc(const P2Params p) {
+    const uint32_t in = p.hot_round & 1u;
+    const uint32_t nq = p.hot_ctl[HC_L0 + in];
+    const uint32_t span = hot_span(p.hot_round);
+    const uint32_t* wl = p.hot_wl + 3u * (size_t)hot_wl_cap(p) * in;
+    for (uint32_t x0 = blockIdx.x * blockDim.x + (threadIdx.x & ~(SGD_WAVE - 1)); x0 < nq; x0 += gridDim.x * blockDim.x) {
+        const uint32_t q = x0 + (threadIdx.x & (SGD_WAVE - 1));
+        bool open = false;
+        uint32_t slot = 0, h = 0, nxt = 0;
+        if (q < nq) {
+            slot = wl[3u * q];
+            h = wl[3u * q + 1u];
+            const uint64_t e64 = (uint64_t)wl[3u * q + 2u] + span;
+            open = p.hot_death[slot] == HOT_LIVE && e64 < p.hot_info[(size_t)h * SGD_HOT_INFO + HI_M];
+            nxt = (uint32_t)min(e64, (uint64_t)0xffffffffu);
+        }
+        hot_wl_push(p.hot_wl + 3u * (size_t)hot_wl_cap(p) * (in ^ 1u), &p.hot_ctl[HC_L0 + (in ^ 1u)], open, slot, h, nxt);
+    }
+}
 
 // per partial slot: the counters (exact, as the walk counts them), the trigger's match count, the survivors
 extern "C" __global__ void __launch_bounds__(256) k_hot_emit(const P2Params p) {
     const uint32_t* ctl = p.hot_ctl;
-    const uint32_t n = min(ctl[HC_N], p.hot_cap), nex = ctl[HC_EX], total = nex + ctl[HC_EV];
+    const uint32_t nex = ctl[HC_EX], total = nex + ctl[HC_EV];
     unsigned long long sc = 0, cr = 0, mt = 0;
     for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < total; x += gridDim.x * blockDim.x) {
         const bool ex = x < nex;
-        const uint32_t h = hot_find(p.hot_info, n, ex ? x : x - nex, ex ? HI_EXOFF : HI_EVOFF);
+        const uint32_t h = p.hot_fh[x];
         uint32_t* hi = p.hot_info + (size_t)h * SGD_HOT_INFO;
         if (hi[HI_BAD]) continue;
         const uint32_t b = hi[HI_B], m = hi[HI_M];
@@ -1658,7 +1721,7 @@ extern "C" __global__ void __launch_bounds__(256) k_hot_emit(const P2Params p) {
 // per run event: its matches' raw slots (one reservation per workgroup) and its trigger descriptor
 extern "C" __global__ void __launch_bounds__(256) k_hot_trig(const P2Params p) {
     const uint32_t* ctl = p.hot_ctl;
-    const uint32_t n = min(ctl[HC_N], p.hot_cap), nev = ctl[HC_EV];
+    const uint32_t nex = ctl[HC_EX], nev = ctl[HC_EV];
     __shared__ uint32_t s_w[4];
     __shared__ unsigned long long s_base;
     const uint32_t lane = threadIdx.x & (SGD_WAVE - 1), w = threadIdx.x / SGD_WAVE;
@@ -1666,7 +1729,7 @@ extern "C" __global__ void __launch_bounds__(256) k_hot_trig(const P2Params p) {
         const uint32_t x = x0 + threadIdx.x;
         uint32_t c = 0, pos = 0;
         if (x < nev) {
-            const uint32_t h = hot_find(p.hot_info, n, x, HI_EVOFF);
+            const uint32_t h = p.hot_fh[nex + x];
             const uint32_t* hi = p.hot_info + (size_t)h * SGD_HOT_INFO;
             if (!hi[HI_BAD]) {
                 pos = hi[HI_B] + (x - hi[HI_EVOFF]);
@@ -1699,11 +1762,11 @@ extern "C" __global__ void __launch_bounds__(256) k_hot_trig(const P2Params p) {
 // per matched partial: its e1 seq (and captures) into a slot of its trigger's range
 extern "C" __global__ void __launch_bounds__(256) k_hot_place(const P2Params p) {
     const uint32_t* ctl = p.hot_ctl;
-    const uint32_t n = min(ctl[HC_N], p.hot_cap), nex = ctl[HC_EX], total = nex + ctl[HC_EV];
+    const uint32_t nex = ctl[HC_EX], total = nex + ctl[HC_EV];
     const int64_t obase = p.ts_col[0];
     for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < total; x += gridDim.x * blockDim.x) {
         const bool ex = x < nex;
-        const uint32_t h = hot_find(p.hot_info, n, ex ? x : x - nex, ex ? HI_EXOFF : HI_EVOFF);
+        const uint32_t h = p.hot_fh[x];
         const uint32_t* hi = p.hot_info + (size_t)h * SGD_HOT_INFO;
         if (hi[HI_BAD]) continue;
         const uint32_t slot = ex ? p.max_batch + x : hi[HI_B] + (x - nex - hi[HI_EVOFF]);
@@ -1726,9 +1789,9 @@ extern "C" __global__ void __launch_bounds__(256) k_hot_place(const P2Params p) 
 // per trigger with several matches: its range in list order (= e1 seq order; insertion sort, ranges are short)
 extern "C" __global__ void __launch_bounds__(256) k_hot_sort(const P2Params p) {
     const uint32_t* ctl = p.hot_ctl;
-    const uint32_t n = min(ctl[HC_N], p.hot_cap), nev = ctl[HC_EV];
+    const uint32_t nex = ctl[HC_EX], nev = ctl[HC_EV];
     for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < nev; x += gridDim.x * blockDim.x) {
-        const uint32_t h = hot_find(p.hot_info, n, x, HI_EVOFF);
+        const uint32_t h = p.hot_fh[nex + x];
         const uint32_t* hi = p.hot_info + (size_t)h * SGD_HOT_INFO;
         if (hi[HI_BAD]) continue;
         const uint32_t pos = hi[HI_B] + (x - hi[HI_EVOFF]);

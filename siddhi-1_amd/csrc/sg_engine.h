@@ -80,6 +80,8 @@ enum {
 #define SGD_HOT_DONE 0xfffffffeu   // resume word: the hot-key pipeline advanced the key (the HBM pass skips it)
 #define SGD_HOT_MARK 0xfffffffdu   // resume word: a hot key of a wave the staged pass left whole (counted there)
 #define SGD_HOT_CTL 8
+#define SGD_HOT_CTL_BIG 6          // hot_ctl word: workgroups whose range exceeded SGD_BIG_TILE events
+#define SGD_BIG_TILE 65536u
 #define SGD_HOT_INFO 8
 
 enum { SGD_ST_SCANNED = 0, SGD_ST_CREATED, SGD_ST_MATCHES, SGD_ST_KEYS, SGD_ST_LIVE0, SGD_ST_SPILLS, SGD_ST_N };
@@ -151,7 +153,8 @@ struct P2Params {
     uint32_t* hot_tcnt;                // [max_batch] matches per trigger (by payload position)
     uint32_t* hot_tbase;               // [max_batch] their first raw slot
     uint32_t* hot_alive;               // [hot_cap][cap] surviving partial slots
-    uint32_t pad;
+    uint32_t* hot_fh;                  // [max_batch + hot_cap * cap] the hot key of each flat index (round 0)
+    uint32_t hot_round;                // the search round a k_hot_rn / k_hot_rc launch runs
     uint64_t cst[SGD_MAX_CONST];       // filter constants, already in their comparison domain
 };
 

@@ -135,7 +135,7 @@ struct sg_engine {
         hipFunction_t adv[2] = {nullptr, nullptr};   // [0]: multi / state-0 stream, [1]: state-1 stream
         hipFunction_t adv_h[2] = {nullptr, nullptr}; // the HBM pass over the waves the staged pass deferred
         hipFunction_t pack[2] = {nullptr, nullptr};
-        hipFunction_t hot[9] = {};                   // the hot-key pipeline (k_hot_prep .. k_hot_final)
+        hipFunction_t hot[10] = {};                  // the hot-key pipeline (k_hot_prep .. k_hot_final)
     };
     JitQuery jq;
     std::vector<uint64_t> consts;
@@ -194,9 +194,10 @@ struct sg_engine {
     // the status block), otherwise the HBM pass walks them
     bool hot_ok = false;
     bool hot_on = true;
+    bool skewed = false;           // recent batches had workgroup ranges > SGD_BIG_TILE events: sorted grouping
     uint32_t hot_min = 0, hot_cap = 0;
     uint32_t *hot_ctl = nullptr, *hot_list = nullptr, *hot_info = nullptr, *hot_death = nullptr, *hot_wl = nullptr;
-    uint32_t *hot_tcnt = nullptr, *hot_tbase = nullptr, *hot_alive = nullptr;
+    uint32_t *hot_tcnt = nullptr, *hot_tbase = nullptr, *hot_alive = nullptr, *hot_fh = nullptr;
     uint64_t hot_batches = 0;      // batches the pipeline ran on (sg_engine_describe)
     uint32_t hbm_grid = 2048;      // work-groups of the HBM pass (SG_HBM_GRID: experiments)
     uint32_t* dlist = nullptr;     // the waves the HBM pass takes, and their number
@@ -563,6 +564,8 @@ void allocate(sg_engine* e) {
     }
     HIP_OK(hipMemsetAsync(e->resume, 0xff, K * 4, e->stream));  // SGD_NO_RESUME
     e->hot_ok = e->plan.s0 == e->plan.s1 && e->plan.mode == SGD_P2_EVERY_FIRST;
+    e->hot_ctl = dalloc<uint32_t>(SGD_HOT_CTL, o);  // (every engine: the big-tile count lives here too)
+    HIP_OK(hipMemsetAsync(e->hot_ctl, 0, SGD_HOT_CTL * 4, e->stream));
     {
         const char* x = getenv("SG_HOT_MIN");  // 0: off
         e->hot_min = x ? (uint32_t)strtoul(x, nullptr, 0) : 256u;
@@ -571,8 +574,6 @@ void allocate(sg_engine* e) {
     if (e->hot_ok) {
         e->hot_cap = (uint32_t)std::min<size_t>({B / std::max(1u, e->hot_min) + 1, K, 65536, std::max<size_t>(1, (1u << 22) / C)});
         const size_t slots = B + (size_t)e->hot_cap * C;
-        e->hot_ctl = dalloc<uint32_t>(SGD_HOT_CTL, o);
-        HIP_OK(hipMemsetAsync(e->hot_ctl, 0, SGD_HOT_CTL * 4, e->stream));
         e->hot_list = dalloc<uint32_t>(e->hot_cap, o);
         e->hot_info = dalloc<uint32_t>((size_t)e->hot_cap * SGD_HOT_INFO, o);
         e->hot_death = dalloc<uint32_t>(slots, o);
@@ -580,6 +581,7 @@ void allocate(sg_engine* e) {
         e->hot_tcnt = dalloc<uint32_t>(B, o);
         e->hot_tbase = dalloc<uint32_t>(B, o);
         e->hot_alive = dalloc<uint32_t>((size_t)e->hot_cap * C, o);
+        e->hot_fh = dalloc<uint32_t>(slots, o);
     }
     e->tile_sum = dalloc<uint32_t>(B / SGD_ORDER_TILE + 1, o);
     e->tile_off = dalloc<uint32_t>(B / SGD_ORDER_TILE + 1, o);
@@ -650,9 +652,9 @@ sg_engine::Variant& variant(sg_engine* e, bool evnull, bool capnull) {
         HIP_OK(hipModuleGetFunction(&r.adv_h[1], r.mod, "k_adv_s1_h"));
     }
     if (e->hot_ok) {
-        static const char* const names[9] = {"k_hot_prep", "k_hot_r0", "k_hot_r1", "k_hot_r2", "k_hot_emit",
-                                             "k_hot_trig", "k_hot_place", "k_hot_sort", "k_hot_final"};
-        for (int i = 0; i < 9; i++) HIP_OK(hipModuleGetFunction(&r.hot[i], r.mod, names[i]));
+        static const char* const names[10] = {"k_hot_prep", "k_hot_r0",   "k_hot_r1",    "k_hot_rn",  "k_hot_rc",
+                                              "k_hot_emit", "k_hot_trig", "k_hot_place", "k_hot_sort", "k_hot_final"};
+        for (int i = 0; i < 10; i++) HIP_OK(hipModuleGetFunction(&r.hot[i], r.mod, names[i]));
     }
     HIP_OK(hipModuleGetFunction(&r.pack[0], r.mod, "k_pack0"));
     HIP_OK(hipModuleGetFunction(&r.pack[1], r.mod, "k_pack1"));
@@ -716,7 +718,12 @@ static void drain_one(sg_engine* e) {  // wait for the oldest in-flight batch
     HIP_OK(hipEventSynchronize(e->done_ev[ri]));
     e->done_count = e->h_status[2 * ri];
     e->done_err |= (uint32_t)e->h_status[2 * ri + 1];
-    if (e->hot_ok) e->hot_on = (e->h_status[2 * ri + 1] >> 32) != 0;  // the batch's hot keys (p2_jit.hip hbm_pass)
+    // the batch's hot keys and giant workgroup ranges (p2_jit.hip hbm_pass): the hot-key pipeline runs while
+    // batches have hot keys, the sorted grouping replaces the fused one while they have giant tiles (split by one
+    // workgroup each in the fused grouping)
+    const uint32_t w1 = (uint32_t)(e->h_status[2 * ri + 1] >> 32);
+    if (e->hot_ok) e->hot_on = (w1 & 0xffffu) != 0;
+    e->skewed = (w1 >> 16) != 0;
     e->inflight.erase(e->inflight.begin());
 }
 
@@ -866,7 +873,7 @@ int push(sg_engine* e, const sg_batch* b) {
             if (wi == 0) ps.kind[wi++] = 5;
             ga.W = wi;
             ga.src = ps;
-            fused = e->fused_ok && sgd_fused_ok(e->K, n, wi) && fused_density_ok(n, e->K, stride);
+            fused = e->fused_ok && !e->skewed && sgd_fused_ok(e->K, n, wi) && fused_density_ok(n, e->K, stride);
             if (fused) {
                 // grouped by key tile only; the split by key is the advance kernel's (tile_split_lds)
                 ga.out = sl.tpay;
@@ -928,13 +935,13 @@ int push(sg_engine* e, const sg_batch* b) {
     p.err = e->err;
     p.raw_capw = e->raw_capw;
     p.raw_capnull = e->raw_capnull;
+    p.hot_ctl = e->hot_ctl;
     if (e->hot_ok) {
         // a partitioned batch's keys hold n / K events on average: "hot" is far above that (and above hot_min)
         p.hot_min = pl.partitioned ? std::max<uint32_t>(e->hot_min, (uint32_t)std::min<uint64_t>(8ull * n / e->K, 1u << 30))
                                    : e->hot_min;
         p.hot_cap = e->hot_cap;
         p.max_batch = (uint32_t)e->maxb;
-        p.hot_ctl = e->hot_ctl;
         p.hot_list = e->hot_list;
         p.hot_info = e->hot_info;
         p.hot_death = e->hot_death;
@@ -942,6 +949,7 @@ int push(sg_engine* e, const sg_batch* b) {
         p.hot_tcnt = e->hot_tcnt;
         p.hot_tbase = e->hot_tbase;
         p.hot_alive = e->hot_alive;
+        p.hot_fh = e->hot_fh;
     }
     for (size_t i = 0; i < e->consts.size(); i++) p.cst[i] = e->consts[i];
     hipEvent_t a0 = nullptr, a1 = nullptr;
@@ -955,8 +963,19 @@ int push(sg_engine* e, const sg_batch* b) {
                p.stage_chunks * 16u * (SGD_BLOCK / SGD_WAVE) + (fused ? SGD_SPLIT_CNT_BYTES : 0u));
         if (e->timing) { a1 = e->ev(); e->mark(a1); e->spans.push_back({a0, a1, 1}); a0 = e->ev(); e->mark(a0); }
         if (e->hot_ok && e->hot_on) {  // the hot keys the staged pass listed (fixed grids: the counts are on the device)
-            static const uint32_t grid[9] = {1, 1024, 512, 1024, 1024, 1024, 1024, 1024, 256};
-            for (int i = 0; i < 9; i++) launch(v.hot[i], grid[i], i == 0 ? 1024 : 256, &p, e->stream);
+            launch(v.hot[0], 1, 1024, &p, e->stream);  // k_hot_prep
+            launch(v.hot[1], 2048, 256, &p, e->stream);  // k_hot_r0
+            launch(v.hot[2], 512, 256, &p, e->stream);  // k_hot_r1
+            // rounds 2.. until the spans scanned cover the longest possible run (round r: 512 << 3 (r - 1) events)
+            uint64_t covered = 128 + 512;
+            for (uint32_t r = 2; covered < e->maxb; r++) {
+                p.hot_round = r;
+                covered += 512ull << (3 * (r - 1));
+                launch(v.hot[3], 1024, 256, &p, e->stream);  // k_hot_rn
+                if (covered < e->maxb) launch(v.hot[4], 256, 256, &p, e->stream);  // k_hot_rc
+            }
+            for (int i = 5; i < 9; i++) launch(v.hot[i], 1024, 256, &p, e->stream);  // emit, trig, place, sort
+            launch(v.hot[9], 256, 256, &p, e->stream);  // k_hot_final
             e->hot_batches++;
         }
         // one wave per work-group over the listed waves (a fixed grid: the list's length is on the device)

@@ -201,3 +201,24 @@ def test_hot_keys_with_projection(monkeypatch):
     assert [(t, tuple(np.float32(x).view(np.uint32).item() if isinstance(x, np.float32) else x for x in r))
             for t, r in dev] == [(t, tuple(np.float32(x).view(np.uint32).item() if isinstance(x, np.float32) else x
                                            for x in r)) for t, r in host]
+
+
+def test_giant_tiles_switch_to_the_sorted_grouping(monkeypatch):
+    """a key with 70 % of 2^17-event batches: its tile (> SGD_BIG_TILE events) would be split by one workgroup in
+    the fused grouping; once a batch reports it, the engine groups the next batches with the sorted passes (the
+    hot key still to the pipeline), exact throughout"""
+    monkeypatch.setenv("SG_HOT_MIN", "256")
+    n_keys, n = 1 << 14, 1 << 17
+    cq, gpu, ora, lane = _pair(SHAPES["c2_every_within"], n_keys, n)
+    rng = np.random.default_rng(9)
+    batches = []
+    for b in range(5):
+        d = synth.stock_ticks(b * n, n, n_keys, seed=110 + b, rate_per_ms=64)
+        d["key"][rng.random(n) < 0.7] = 4321
+        d["symbol"] = d["key"].copy()
+        batches.append((b * n, d))
+    _run(gpu, ora, lane, batches)
+    desc = gpu.describe()
+    assert "per 8-bit digit" in desc and "k_hot_prep" in desc, desc
+    for e in (gpu, ora, lane):
+        e.close()
