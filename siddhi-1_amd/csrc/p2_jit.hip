@@ -608,6 +608,20 @@ __device__ __forceinline__ void tile_split_glb(const uint32_t* __restrict__ src,
 }
 
 // ---- the kernel ---------------------------------------------------------------------------------
+// a hot key (SG_HOT): at least p.hot_min events in the batch; listed for the hot-key pipeline (while its list has
+// room), its lane then walks nothing
+__device__ __forceinline__ bool list_hot(const P2Params& p, uint32_t k, uint32_t nev) {
+#if SG_HOT
+    if (p.hot_min != 0u && k < p.n_keys && nev >= p.hot_min) {
+        const uint32_t slot = atomicAdd(p.hot_ctl, 1u);
+        if (slot < p.hot_cap) {
+            p.hot_list[slot] = k;
+            return true;
+        }
+    }
+#endif
+    return false;
+}
 __device__ __forceinline__ uint32_t wave_min_u(uint32_t x) {
     for (int off = 32; off > 0; off >>= 1) x = min(x, (uint32_t)__shfl_xor((int)x, off, SGD_WAVE));
     return x;
@@ -651,6 +665,8 @@ __device__ __forceinline__ void advance(const P2Params& p, const uint32_t gid) {
     // by run length was measured: 22% fewer VALU instructions, no faster — the workgroup's LDS is held
     // until its longest lane ends, so occupancy, not lane idling, bounds the walk.)
     uint32_t blo = 0, bhi = 0, rlo = 0;  // the workgroup's payload range; the wave's first event
+    uint32_t gb = 0, ge = 0;              // the longest hot run inside it (not staged: the pipeline's)
+    bool hot = false;
     bool fits = true;
     bool tile_glb = false;  // fused: the tile was too large for LDS, split into the key-sorted payload in HBM
     if constexpr (STG) {
@@ -686,23 +702,37 @@ __device__ __forceinline__ void advance(const P2Params& p, const uint32_t gid) {
             }
             b = blo + kb;
             e = b + kc;
+            hot = list_hot(p, k, e - b);
             if ((tile_glb || p.write_sorted) && k < K) {
                 p.seg_begin[k] = b;
                 p.seg_end[k] = e;
             }
             rlo = uni(wave_min_u(e > b ? b : 0xffffffffu));
         } else {
-            __shared__ uint32_t s_lo[NW], s_hi[NW];
+            __shared__ uint32_t s_lo[NW], s_hi[NW], s_gl[NW], s_gb[NW];
             const uint32_t nv = e - b;
+            hot = list_hot(p, k, nv);
             rlo = uni(wave_min_u(nv > 0 ? b : 0xffffffffu));
             const uint32_t hi = uni(wave_max_u(nv > 0 ? e : 0u));
-            if (lane == 0) { s_lo[wv] = rlo; s_hi[wv] = hi; }
+            // the wave's longest hot run: left out of the LDS staging (the range of a workgroup holding a head key
+            // of a skewed stream then still fits)
+            const uint32_t gl = uni(wave_max_u(hot ? nv : 0u));
+            const uint64_t gm = __ballot(hot && nv == gl);
+            const uint32_t gw = gm ? (uint32_t)__shfl((int)b, __builtin_ctzll(gm), SGD_WAVE) : 0u;
+            if (lane == 0) { s_lo[wv] = rlo; s_hi[wv] = hi; s_gl[wv] = gl; s_gb[wv] = gw; }
             __syncthreads();
             blo = 0xffffffffu;
+            uint32_t glen = 0;
 #pragma unroll
-            for (uint32_t w = 0; w < NW; ++w) { blo = min(blo, s_lo[w]); bhi = max(bhi, s_hi[w]); }
+            for (uint32_t w = 0; w < NW; ++w) {
+                blo = min(blo, s_lo[w]);
+                bhi = max(bhi, s_hi[w]);
+                if (s_gl[w] > glen) { glen = s_gl[w]; gb = s_gb[w]; }
+            }
             blo = uni(blo);
             bhi = uni(bhi);
+            gb = uni(gb);
+            ge = gb + uni(glen);
         }
     }
     bool count_key = true;  // this pass owns the key's keys_touched / live_at_batch_start counts
@@ -731,17 +761,6 @@ __device__ __forceinline__ void advance(const P2Params& p, const uint32_t gid) {
     }
     const int nev = (int)(e - b);
     if (nev <= 0) h = 0;
-    // a hot key (SG_HOT): left to the hot-key pipeline (listed here), its lane walks nothing
-    bool hot = false;
-#if SG_HOT
-    if constexpr (STG) {
-        if (p.hot_min != 0u && k < K && (uint32_t)nev >= p.hot_min) {
-            const uint32_t slot = atomicAdd(p.hot_ctl, 1u);
-            hot = slot < p.hot_cap;
-            if (hot) p.hot_list[slot] = k;
-        }
-    }
-#endif
     int iters = (int)uni((uint32_t)wave_max(hot ? 0 : nev));
     // the HBM pass stages its wave's runs in LDS too when they fit (its keys are consecutive: one range of the
     // key-sorted payload), so its walk waits on LDS, not on a dependent HBM load per event
@@ -768,8 +787,11 @@ __device__ __forceinline__ void advance(const P2Params& p, const uint32_t gid) {
     // flight at once, no VGPRs) and the lanes then walk their own runs out of LDS (a lane-private walk
     // through HBM touches every line ~8x, once per iteration, and thrashes L2).
     const uint64_t c_lo = (uint64_t)blo * SB / 16u, c_hi = ((uint64_t)bhi * SB + 15u) / 16u;
+    // the gap: the 16-B chunks wholly inside the longest hot run [gb, ge) (the staging skips them)
+    const uint64_t c_g0 = ((uint64_t)gb * SB + 15u) / 16u, c_g1 = (uint64_t)ge * SB / 16u;
+    const uint32_t gap_ch = (ge > gb && c_g1 > c_g0) ? (uint32_t)(c_g1 - c_g0) : 0u;
     if constexpr (STG) {
-        if (!fused) fits = SGX_GLB_WALK || bhi <= blo || c_hi - c_lo <= (uint64_t)p.stage_chunks * NW;
+        if (!fused) fits = SGX_GLB_WALK || bhi <= blo || c_hi - c_lo - gap_ch <= (uint64_t)p.stage_chunks * NW;
         // (a giant workgroup range: the host keeps the sorted grouping while batches have them)
         if (!fused && bhi > blo && bhi - blo > SGD_BIG_TILE && threadIdx.x == 0 && p.hot_ctl)
             atomicAdd(&p.hot_ctl[SGD_HOT_CTL_BIG], 1u);
@@ -780,6 +802,7 @@ __device__ __forceinline__ void advance(const P2Params& p, const uint32_t gid) {
         if (!fits) iters = 0;
     }
     const uint32_t* lds_run = (const uint32_t*)sg_stage + ((uint64_t)blo * SB - c_lo * 16u) / 4u;  // element blo
+    const uint32_t* lrun = lds_run - ((gap_ch != 0u && b >= ge) ? gap_ch * 4u : 0u);  // (this lane's side of the gap)
 
     // round trip 2: the partials of the register window, the raw-slot reservation and the LDS copy,
     // all in flight together (nothing below reads a result before the barrier)
@@ -863,11 +886,15 @@ __device__ __forceinline__ void advance(const P2Params& p, const uint32_t gid) {
         }
     }
     if (!SGX_GLB_WALK && STG && !fused && fits && bhi > blo) {  // (fused: staged and split above)
-        const uint32_t nch = (uint32_t)(c_hi - c_lo);
+        const uint32_t nch = (uint32_t)(c_hi - c_lo) - gap_ch;
+        const uint32_t ga = gap_ch ? (uint32_t)(c_g0 - c_lo) : nch;  // chunks before the gap
         const sg_u32x4* src = (const sg_u32x4*)p.payload + c_lo;
-        for (uint32_t c = wv * SGD_WAVE; c < nch; c += SGD_BLOCK)
-            if (c + (uint32_t)lane < nch)
-                __builtin_amdgcn_global_load_lds((sg_glb_ptr)(src + c + lane), (sg_lds_ptr)(sg_stage + c), 16, 0, 0);
+        for (uint32_t c = wv * SGD_WAVE; c < nch; c += SGD_BLOCK) {
+            const uint32_t cc = c + (uint32_t)lane;
+            if (cc < nch)
+                __builtin_amdgcn_global_load_lds((sg_glb_ptr)(src + cc + (cc >= ga ? gap_ch : 0u)), (sg_lds_ptr)(sg_stage + c),
+                                                 16, 0, 0);
+        }
     }
     if constexpr (STG) {
         // every wave's LDS copies have landed (a wave reads runs other waves copied: each waits for its
@@ -910,7 +937,7 @@ __device__ __forceinline__ void advance(const P2Params& p, const uint32_t gid) {
     }
 
     PayEl<STRIDE> cur, nxt;
-    if (run > 0) cur = from_lds ? lds_pay<STRIDE>(lds_run, b - blo) : load_pay<STRIDE>(p.payload, b);
+    if (run > 0) cur = from_lds ? lds_pay<STRIDE>(lrun, b - blo) : load_pay<STRIDE>(p.payload, b);
 
 #if SGX_PROF
     uint64_t prof_acc[5] = {0, 0, 0, 0, 0};
@@ -931,7 +958,7 @@ __device__ __forceinline__ void advance(const P2Params& p, const uint32_t gid) {
             }
         }
         if (it + 1 < run)  // next event in flight
-            nxt = from_lds ? lds_pay<STRIDE>(lds_run, b - blo + (uint32_t)it + 1)
+            nxt = from_lds ? lds_pay<STRIDE>(lrun, b - blo + (uint32_t)it + 1)
                            : load_pay<STRIDE>(p.payload, b + (uint32_t)it + 1);
         Ev ev;
         int64_t ts = 0;
@@ -1520,12 +1547,18 @@ extern "C" __global__ void __launch_bounds__(SGD_HOT_C) k_hot_r0(const P2Params 
     constexpr uint32_t ST = SGD_HOT_C + SGD_HOT_L0;
     __shared__ uint32_t s_w[ST * HST];
     __shared__ int64_t s_ts[ST];
+    __shared__ uint32_t s_h0;
     for (uint32_t x0 = nex + blockIdx.x * SGD_HOT_C; x0 < total; x0 += gridDim.x * SGD_HOT_C) {
         uint32_t h = 0, pos = 0, i = 0, m = 0;
+        // the chunk's first key by binary search (one thread), each event's from there forward (hot runs are long:
+        // a chunk spans few keys)
+        if (tid == 0) s_h0 = hot_find(p.hot_info, n, x0 - nex, HI_EVOFF);
+        __syncthreads();
+        uint32_t hx = s_h0;
         for (uint32_t t = tid; t < ST; t += SGD_HOT_C) {
             const uint32_t x = x0 + t;
             if (x >= total) break;
-            const uint32_t hx = hot_find(p.hot_info, n, x - nex, HI_EVOFF);
+            while (hx + 1u < n && p.hot_info[(size_t)(hx + 1u) * SGD_HOT_INFO + HI_EVOFF] <= x - nex) ++hx;
             const uint32_t* hi = p.hot_info + (size_t)hx * SGD_HOT_INFO;
             const uint32_t ix = x - nex - hi[HI_EVOFF], px = hi[HI_B] + ix;
             const PayEl<HST> ev = load_pay<HST>(p.payload, px);
@@ -1538,6 +1571,7 @@ extern "C" __global__ void __launch_bounds__(SGD_HOT_C) k_hot_r0(const P2Params 
                 i = ix;
                 m = hi[HI_M];
                 p.hot_fh[x] = hx;
+                p.hot_fbi[x - nex] = ev.w[0];
             }
         }
         __syncthreads();
@@ -1548,7 +1582,7 @@ extern "C" __global__ void __launch_bounds__(SGD_HOT_C) k_hot_r0(const P2Params 
             const int64_t ts = s_ts[tid];
             const int64_t tp = i == 0u ? ts : tid > 0u ? s_ts[tid - 1] : hot_ts(p, load_pay<HST>(p.payload, pos - 1u), obase);
             if (ts == -1 || tp > ts) p.hot_info[(size_t)h * SGD_HOT_INFO + HI_BAD] = 1u;
-            p.hot_tcnt[pos] = 0u;
+            p.hot_tcnt[x - nex] = 0u;
             const SgEv0 e0 = sgq_ev0(&s_w[tid * HST]);
             uint32_t d = HOT_NOTP;
             if (sgq_f0(e0, p)) {
@@ -1699,7 +1733,7 @@ extern "C" __global__ void __launch_bounds__(256) k_hot_emit(const P2Params p) {
             sc += (unsigned long long)((int64_t)i - start - 1 + (int64_t)(d & 1u));
             if (d & 1u) {
                 mt += 1;
-                atomicAdd(&p.hot_tcnt[b + i], 1u);
+                atomicAdd(&p.hot_tcnt[hi[HI_EVOFF] + i], 1u);
             }
         }
     }
@@ -1720,22 +1754,13 @@ extern "C" __global__ void __launch_bounds__(256) k_hot_emit(const P2Params p) {
 
 // per run event: its matches' raw slots (one reservation per workgroup) and its trigger descriptor
 extern "C" __global__ void __launch_bounds__(256) k_hot_trig(const P2Params p) {
-    const uint32_t* ctl = p.hot_ctl;
-    const uint32_t nex = ctl[HC_EX], nev = ctl[HC_EV];
+    const uint32_t nev = p.hot_ctl[HC_EV];
     __shared__ uint32_t s_w[4];
     __shared__ unsigned long long s_base;
     const uint32_t lane = threadIdx.x & (SGD_WAVE - 1), w = threadIdx.x / SGD_WAVE;
     for (uint32_t x0 = blockIdx.x * blockDim.x; x0 < nev; x0 += gridDim.x * blockDim.x) {
         const uint32_t x = x0 + threadIdx.x;
-        uint32_t c = 0, pos = 0;
-        if (x < nev) {
-            const uint32_t h = p.hot_fh[nex + x];
-            const uint32_t* hi = p.hot_info + (size_t)h * SGD_HOT_INFO;
-            if (!hi[HI_BAD]) {
-                pos = hi[HI_B] + (x - hi[HI_EVOFF]);
-                c = p.hot_tcnt[pos];
-            }
-        }
+        const uint32_t c = x < nev ? p.hot_tcnt[x] : 0u;  // (0 for the events of keys given back)
         const uint32_t incl = wave_incl_scan(c, (int)lane);
         if (lane == SGD_WAVE - 1) s_w[w] = incl;
         __syncthreads();
@@ -1749,11 +1774,11 @@ extern "C" __global__ void __launch_bounds__(256) k_hot_trig(const P2Params p) {
         if (c) {
             const unsigned long long first = p.raw_static + s_base + off;
             if (first + c <= p.raw_capacity)
-                p.t_desc[p.payload[(size_t)pos * HST]] = ((uint64_t)c << 32) | (uint64_t)(uint32_t)first;
+                p.t_desc[p.hot_fbi[x]] = ((uint64_t)c << 32) | (uint64_t)(uint32_t)first;
             else
                 atomicOr(p.err, (uint32_t)SGD_ERR_MATCH_CAP);
-            p.hot_tbase[pos] = (uint32_t)first;
-            p.hot_tcnt[pos] = 0u;  // (the fill's rank counter)
+            p.hot_tbase[x] = (uint32_t)first;
+            p.hot_tcnt[x] = 0u;  // (the fill's rank counter)
         }
         __syncthreads();
     }
@@ -1772,7 +1797,7 @@ extern "C" __global__ void __launch_bounds__(256) k_hot_place(const P2Params p) 
         const uint32_t slot = ex ? p.max_batch + x : hi[HI_B] + (x - nex - hi[HI_EVOFF]);
         const uint32_t d = p.hot_death[slot];
         if (d == HOT_NOTP || d == HOT_LIVE || !(d & 1u)) continue;
-        const uint32_t tp = hi[HI_B] + (d >> 1);
+        const uint32_t tp = hi[HI_EVOFF] + (d >> 1);
         const uint64_t dst = (uint64_t)p.hot_tbase[tp] + atomicAdd(&p.hot_tcnt[tp], 1u);
         if (dst >= p.raw_capacity) continue;
         int start;
@@ -1788,16 +1813,11 @@ extern "C" __global__ void __launch_bounds__(256) k_hot_place(const P2Params p) 
 
 // per trigger with several matches: its range in list order (= e1 seq order; insertion sort, ranges are short)
 extern "C" __global__ void __launch_bounds__(256) k_hot_sort(const P2Params p) {
-    const uint32_t* ctl = p.hot_ctl;
-    const uint32_t nex = ctl[HC_EX], nev = ctl[HC_EV];
+    const uint32_t nev = p.hot_ctl[HC_EV];
     for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < nev; x += gridDim.x * blockDim.x) {
-        const uint32_t h = p.hot_fh[nex + x];
-        const uint32_t* hi = p.hot_info + (size_t)h * SGD_HOT_INFO;
-        if (hi[HI_BAD]) continue;
-        const uint32_t pos = hi[HI_B] + (x - hi[HI_EVOFF]);
-        const uint32_t c = p.hot_tcnt[pos];
+        const uint32_t c = p.hot_tcnt[x];
         if (c < 2u) continue;
-        const uint64_t f = p.hot_tbase[pos];
+        const uint64_t f = p.hot_tbase[x];
         if (f + c > p.raw_capacity) continue;
         for (uint32_t a = 1; a < c; ++a) {
             const uint64_t v = p.raw_e1[f + a];

@@ -150,8 +150,9 @@ struct P2Params {
     uint32_t* hot_info;                // [hot_cap][SGD_HOT_INFO] per hot key: run, offsets, checks, survivors
     uint32_t* hot_death;               // [max_batch + hot_cap * cap] per partial slot: 2 * event + matched
     uint32_t* hot_wl;                  // [2][max_batch + hot_cap * cap][3] unresolved partials (slot, key, cursor)
-    uint32_t* hot_tcnt;                // [max_batch] matches per trigger (by payload position)
+    uint32_t* hot_tcnt;                // [max_batch] matches per trigger (by flat event index)
     uint32_t* hot_tbase;               // [max_batch] their first raw slot
+    uint32_t* hot_fbi;                 // [max_batch] the batch position of each flat event
     uint32_t* hot_alive;               // [hot_cap][cap] surviving partial slots
     uint32_t* hot_fh;                  // [max_batch + hot_cap * cap] the hot key of each flat index (round 0)
     uint32_t hot_round;                // the search round a k_hot_rn / k_hot_rc launch runs

@@ -136,6 +136,7 @@ struct sg_engine {
         hipFunction_t adv_h[2] = {nullptr, nullptr}; // the HBM pass over the waves the staged pass deferred
         hipFunction_t pack[2] = {nullptr, nullptr};
         hipFunction_t hot[10] = {};                  // the hot-key pipeline (k_hot_prep .. k_hot_final)
+        uint32_t adv_static_lds = 0;                 // the staged pass's static LDS (beside its dynamic staging)
     };
     JitQuery jq;
     std::vector<uint64_t> consts;
@@ -197,7 +198,7 @@ struct sg_engine {
     bool skewed = false;           // recent batches had workgroup ranges > SGD_BIG_TILE events: sorted grouping
     uint32_t hot_min = 0, hot_cap = 0;
     uint32_t *hot_ctl = nullptr, *hot_list = nullptr, *hot_info = nullptr, *hot_death = nullptr, *hot_wl = nullptr;
-    uint32_t *hot_tcnt = nullptr, *hot_tbase = nullptr, *hot_alive = nullptr, *hot_fh = nullptr;
+    uint32_t *hot_tcnt = nullptr, *hot_tbase = nullptr, *hot_alive = nullptr, *hot_fh = nullptr, *hot_fbi = nullptr;
     uint64_t hot_batches = 0;      // batches the pipeline ran on (sg_engine_describe)
     uint32_t hbm_grid = 2048;      // work-groups of the HBM pass (SG_HBM_GRID: experiments)
     uint32_t* dlist = nullptr;     // the waves the HBM pass takes, and their number
@@ -582,6 +583,7 @@ void allocate(sg_engine* e) {
         e->hot_tbase = dalloc<uint32_t>(B, o);
         e->hot_alive = dalloc<uint32_t>((size_t)e->hot_cap * C, o);
         e->hot_fh = dalloc<uint32_t>(slots, o);
+        e->hot_fbi = dalloc<uint32_t>(B, o);
     }
     e->tile_sum = dalloc<uint32_t>(B / SGD_ORDER_TILE + 1, o);
     e->tile_off = dalloc<uint32_t>(B / SGD_ORDER_TILE + 1, o);
@@ -656,6 +658,11 @@ sg_engine::Variant& variant(sg_engine* e, bool evnull, bool capnull) {
                                               "k_hot_emit", "k_hot_trig", "k_hot_place", "k_hot_sort", "k_hot_final"};
         for (int i = 0; i < 10; i++) HIP_OK(hipModuleGetFunction(&r.hot[i], r.mod, names[i]));
     }
+    {
+        int sh = 0;
+        HIP_OK(hipFuncGetAttribute(&sh, HIP_FUNC_ATTRIBUTE_SHARED_SIZE_BYTES, r.adv[0]));
+        r.adv_static_lds = (uint32_t)sh;
+    }
     HIP_OK(hipModuleGetFunction(&r.pack[0], r.mod, "k_pack0"));
     HIP_OK(hipModuleGetFunction(&r.pack[1], r.mod, "k_pack1"));
     return r;
@@ -684,14 +691,14 @@ uint32_t stage_chunks_for(uint64_t n, uint64_t K, uint32_t stride_words) {
 // of a Poisson count, the few larger tiles split in HBM and walked by the HBM pass), sized so that three workgroups
 // share a CU at the C2 density (with the split's 2 KB of counters beside it); and whether the batch takes the fused
 // grouping at all (the split holds SGD_SPLIT_CHUNKS rounds of 64 events per wave in registers)
-static uint32_t stage_chunks_fused(uint64_t n, uint64_t K, uint32_t stride_words) {
+static uint32_t stage_chunks_fused(uint64_t n, uint64_t K, uint32_t stride_words, uint32_t static_lds) {
     const uint32_t wpb = SGD_BLOCK / SGD_WAVE;
     const double mean = (double)n * SGD_BLOCK / (double)(K ? K : 1);
     const double want = mean + 3.5 * std::sqrt(mean);
     const double chunks = std::ceil((std::ceil(want * stride_words * 4.0 / 16.0) + 1.0) / wpb);
     // three workgroups per CU: LDS is allocated in granules of 1,280 B on gfx950 (measured: a 54,064-B workgroup
     // held two per CU, 53,360 B three), so a workgroup keeps within 42 granules = 53,760 B
-    const double three = std::floor((53760.0 - SGD_SPLIT_CNT_BYTES - 64.0) / wpb / 16.0);
+    const double three = std::floor((53760.0 - SGD_SPLIT_CNT_BYTES - (double)static_lds) / wpb / 16.0);
     const double hi = std::floor((double)(SGD_STAGE_MAX_BYTES - SGD_SPLIT_CNT_BYTES) / wpb / 16.0);
     if (chunks <= three + 16.0) return (uint32_t)std::max(64.0, std::min(chunks, three));
     return (uint32_t)std::max(64.0, std::min(chunks, hi));
@@ -950,13 +957,14 @@ int push(sg_engine* e, const sg_batch* b) {
         p.hot_tbase = e->hot_tbase;
         p.hot_alive = e->hot_alive;
         p.hot_fh = e->hot_fh;
+        p.hot_fbi = e->hot_fbi;
     }
     for (size_t i = 0; i < e->consts.size(); i++) p.cst[i] = e->consts[i];
     hipEvent_t a0 = nullptr, a1 = nullptr;
     if (e->timing) { a0 = e->ev(); e->mark(a0); }
     {
         p.stage_chunks = e->stage_override ? std::max(64u, e->stage_override)
-                         : fused ? stage_chunks_fused(n, e->K, stride) : stage_chunks_for(n, e->K, stride);
+                         : fused ? stage_chunks_fused(n, e->K, stride, v.adv_static_lds) : stage_chunks_for(n, e->K, stride);
         const uint32_t blocks = (e->K + SGD_BLOCK - 1) / SGD_BLOCK;
         // (fused: the split's per-(wave, key) counters after the staging region)
         launch(v.adv[role], blocks, SGD_BLOCK, &p, e->stream,
