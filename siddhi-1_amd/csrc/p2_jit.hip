@@ -1358,13 +1358,18 @@ extern "C" __global__ void __launch_bounds__(256) k_pack1(const PackParams q) { 
 #define SGD_HOT_C 256u     // round 0: events per workgroup
 #define SGD_HOT_L0 128u    // round 0: events each partial scans (staged in LDS after the workgroup's)
 #define SGD_HOT_L1 512u    // round 1: events each open partial scans; rounds >= 2: x8 per round
+#define SGD_HOT_G 16u      // elements per thread of the list / reservation kernels (one atomic per 4096)
+#define SGD_HOT_FILL 4096u // k_hot_fill: run events per workgroup pass
 namespace {
-constexpr uint32_t HOT_NOTP = 0xfffffffeu;  // death word of a payload position whose event made no partial
+constexpr uint32_t HOT_NOTP = 0xfffffffeu;  // death word of a run event that made no partial
 constexpr uint32_t HOT_LIVE = 0xffffffffu;  // no event of the run ends the partial (or not found yet)
-enum { HI_B = 0, HI_M, HI_EXOFF, HI_EVOFF, HI_N0, HI_BAD, HI_ALIVE, HI_KEY };
-enum { HC_N = 0, HC_EX, HC_EV, HC_L0, HC_L1, HC_MAXM, HC_BIG };
+enum { HI_B = 0, HI_M, HI_EXOFF, HI_EVOFF, HI_N0, HI_BAD, HI_ALIVE, HI_KEY, HI_BLKOFF };
+enum { HC_N = 0, HC_EX, HC_EV, HC_L0, HC_L1, HC_MAXM, HC_BIG, HC_NBLK };
 constexpr int HST = SGQ_STRIDE0;
 
+// Flat index space of one batch's pipeline: [0, nex) the carried-in partials of the hot keys (key after key, list
+// order), then [nex, nex + nev) the events of their runs (key after key, run order).  Flat order within a key is
+// list order, so the survivors sorted by flat index are the key's new list.
 struct HotPart {
     int64_t ts;
     uint64_t seq;
@@ -1409,15 +1414,16 @@ __device__ __forceinline__ HotPart hot_existing(const P2Params& p, uint32_t k, u
     P.cn = SGQ_CAPNULL ? G.NUL(j) : 0u;
     return P;
 }
-// the partial in `slot`: created at payload position slot (run index slot - b), or carried in (index -1)
-__device__ __forceinline__ HotPart hot_part(const P2Params& p, uint32_t slot, const uint32_t* hi, int64_t obase,
-                                            int& start) {
-    if (slot < p.max_batch) {
-        start = (int)(slot - hi[HI_B]);
-        return hot_created(p, slot, obase);
+// the partial at flat index x (key info hi): carried in (run index -1) or created by run event x - nex - evoff
+__device__ __forceinline__ HotPart hot_part(const P2Params& p, uint32_t x, uint32_t nex, const uint32_t* hi,
+                                            int64_t obase, int& start) {
+    if (x < nex) {
+        start = -1;
+        return hot_existing(p, hi[HI_KEY], x - hi[HI_EXOFF]);
     }
-    start = -1;
-    return hot_existing(p, hi[HI_KEY], slot - p.max_batch - hi[HI_EXOFF]);
+    const uint32_t i = x - nex - hi[HI_EVOFF];
+    start = (int)i;
+    return hot_created(p, hi[HI_B] + i, obase);
 }
 // event i of the run (payload position pos) ends partial P: 2i (expired) or 2i + 1 (matched); HOT_LIVE otherwise
 __device__ __forceinline__ uint32_t hot_test(const P2Params& p, const HotPart& P, uint32_t pos, uint32_t i,
@@ -1426,30 +1432,44 @@ __device__ __forceinline__ uint32_t hot_test(const P2Params& p, const HotPart& P
     if (SGQ_WITHIN && expired(P.ts, hot_ts(p, x, obase), p.within)) return i * 2u;
     return sgq_f1(sgq_ev1(x.w), P.cw, P.cn, p) ? i * 2u + 1u : HOT_LIVE;
 }
-__device__ __forceinline__ void hot_wl_push(uint32_t* wl, uint32_t* cnt, bool push, uint32_t slot, uint32_t h,
-                                            uint32_t cur) {
-    const uint64_t bal = __ballot(push);
-    if (bal == 0ull) return;
-    uint32_t base = 0;
-    if ((threadIdx.x & (SGD_WAVE - 1)) == 0) base = atomicAdd(cnt, (uint32_t)__popcll(bal));
-    base = (uint32_t)__shfl((int)base, 0, SGD_WAVE);
-    if (push) {
-        const uint32_t q = base + lane_rank(bal);
-        wl[3u * q] = slot;
-        wl[3u * q + 1u] = h;
-        wl[3u * q + 2u] = cur;
+// a wave scans events [lo, end) of a run for partial P, 64 at a time: the first that ends it, or HOT_LIVE
+__device__ __forceinline__ uint32_t hot_wave_scan(const P2Params& p, const HotPart& P, uint32_t b, uint32_t lo,
+                                                  uint32_t end, int64_t obase) {
+    const uint32_t lane = threadIdx.x & (SGD_WAVE - 1);
+    for (uint32_t i0 = lo; i0 < end; i0 += SGD_WAVE) {
+        const uint32_t i = i0 + lane;
+        const uint32_t c = i < end ? hot_test(p, P, b + i, i, obase) : HOT_LIVE;
+        const uint64_t hit = __ballot(c != HOT_LIVE);
+        if (hit) return (uint32_t)__shfl((int)c, __builtin_ctzll(hit), SGD_WAVE);
     }
+    return HOT_LIVE;
 }
 __device__ __forceinline__ uint32_t hot_wl_cap(const P2Params& p) { return p.max_batch + p.hot_cap * p.cap; }
+__device__ __forceinline__ uint32_t* hot_list_buf(const P2Params& p, uint32_t which) {
+    return p.hot_wl + 3u * (size_t)hot_wl_cap(p) * which;
+}
+// workgroup-wide exclusive scan of one value per thread (blockDim.x = 256); *total = the sum
+__device__ __forceinline__ uint32_t hot_block_scan(uint32_t v, uint32_t* s_w, uint32_t& total) {
+    const uint32_t lane = threadIdx.x & (SGD_WAVE - 1), w = threadIdx.x / SGD_WAVE;
+    const uint32_t incl = wave_incl_scan(v, (int)lane);
+    if (lane == SGD_WAVE - 1) s_w[w] = incl;
+    __syncthreads();
+    uint32_t off = incl - v, tot = 0;
+    for (uint32_t u = 0; u < blockDim.x / SGD_WAVE; ++u) {
+        if (u < w) off += s_w[u];
+        tot += s_w[u];
+    }
+    __syncthreads();
+    total = tot;
+    return off;
+}
 }  // namespace
 
 // per hot key: its run, its state and the conditions; then the offsets of the carried-in partials and of the
-// runs in the flat index spaces of the kernels below (one workgroup)
+// runs in the flat index space (one workgroup)
 extern "C" __global__ void __launch_bounds__(1024) k_hot_prep(const P2Params p) {
     uint32_t* ctl = p.hot_ctl;
     const uint32_t n = min(ctl[HC_N], p.hot_cap);
-    const int64_t obase = p.ts_col[0];
-    const uint32_t K = p.n_keys;
     for (uint32_t h = threadIdx.x; h < n; h += blockDim.x) {
         const uint32_t k = p.hot_list[h];
         uint32_t* hi = p.hot_info + (size_t)h * SGD_HOT_INFO;
@@ -1457,20 +1477,8 @@ extern "C" __global__ void __launch_bounds__(1024) k_hot_prep(const P2Params p) 
         const uint32_t hd = p.hdr[k];
         const uint32_t sp = SGD_H_SPEND(hd), ss = SGD_H_SSTG(hd) + (SGD_H_INIT(hd) ? 0u : 1u);
         const uint32_t n0 = SGD_H_INIT(hd) ? SGD_H_NPEND(hd) + SGD_H_NSTG(hd) : 0u;
-        bool bad = sp + ss != 1u || n0 > p.cap || m == 0u;
-        if (!bad) {  // the carried-in list: ts and seq ordered, no ts -1, none newer than the run's first event
-            const int64_t t0 = hot_ts(p, load_pay<HST>(p.payload, b), obase);
-            bad = t0 == -1;
-            int64_t pt = 0;
-            uint64_t pq = 0;
-            for (uint32_t j = 0; j < n0 && !bad; ++j) {
-                const int64_t t = p.p_ts[(size_t)j * K + k];
-                const uint64_t q = p.p_seq[(size_t)j * K + k];
-                bad = t == -1 || t > t0 || (j > 0u && (t < pt || q <= pq));
-                pt = t;
-                pq = q;
-            }
-        }
+        // (the carried-in list's order is checked by round 0, a thread per partial)
+        const bool bad = sp + ss != 1u || n0 > p.cap || m == 0u;
         hi[HI_B] = b;
         hi[HI_M] = bad ? 0u : m;
         hi[HI_N0] = bad ? 0u : n0;
@@ -1479,86 +1487,99 @@ extern "C" __global__ void __launch_bounds__(1024) k_hot_prep(const P2Params p) 
         hi[HI_KEY] = k;
     }
     __syncthreads();
-    // exclusive scans of (carried-in count, run length): each thread a contiguous span of keys
-    __shared__ uint32_t s_x[16], s_e[16], s_m[16];
+    // exclusive scans of (carried-in count, run length, fill blocks): each thread a contiguous span of keys
+    __shared__ uint32_t s_x[16], s_e[16], s_m[16], s_b[16];
     const uint32_t lane = threadIdx.x & (SGD_WAVE - 1), w = threadIdx.x / SGD_WAVE;
     const uint32_t per = (n + blockDim.x - 1u) / blockDim.x;
     const uint32_t lo = min(n, threadIdx.x * per), hi_ = min(n, lo + per);
-    uint32_t sx = 0, se = 0, mm = 0;
+    uint32_t sx = 0, se = 0, mm = 0, sb = 0;
     for (uint32_t h = lo; h < hi_; ++h) {
         sx += p.hot_info[(size_t)h * SGD_HOT_INFO + HI_N0];
         const uint32_t m = p.hot_info[(size_t)h * SGD_HOT_INFO + HI_M];
         se += m;
+        sb += (m + SGD_HOT_FILL - 1u) / SGD_HOT_FILL;
         mm = max(mm, m);
     }
     const uint32_t ix = wave_incl_scan(sx, (int)lane), ie = wave_incl_scan(se, (int)lane);
+    const uint32_t ib = wave_incl_scan(sb, (int)lane);
     mm = wave_max_u(mm);
-    if (lane == SGD_WAVE - 1) { s_x[w] = ix; s_e[w] = ie; s_m[w] = mm; }
+    if (lane == SGD_WAVE - 1) { s_x[w] = ix; s_e[w] = ie; s_m[w] = mm; s_b[w] = ib; }
     __syncthreads();
-    uint32_t ox = ix - sx, oe = ie - se;
-    for (uint32_t u = 0; u < w; ++u) { ox += s_x[u]; oe += s_e[u]; }
+    uint32_t ox = ix - sx, oe = ie - se, ob = ib - sb;
+    for (uint32_t u = 0; u < w; ++u) { ox += s_x[u]; oe += s_e[u]; ob += s_b[u]; }
     for (uint32_t h = lo; h < hi_; ++h) {
         uint32_t* hi = p.hot_info + (size_t)h * SGD_HOT_INFO;
         hi[HI_EXOFF] = ox;
         hi[HI_EVOFF] = oe;
+        hi[HI_BLKOFF] = ob;
         ox += hi[HI_N0];
         oe += hi[HI_M];
+        ob += (hi[HI_M] + SGD_HOT_FILL - 1u) / SGD_HOT_FILL;
     }
     if (threadIdx.x == 0) {
-        uint32_t tx = 0, te = 0, tm = 0;
-        for (uint32_t u = 0; u < blockDim.x / SGD_WAVE; ++u) { tx += s_x[u]; te += s_e[u]; tm = max(tm, s_m[u]); }
+        uint32_t tx = 0, te = 0, tm = 0, tb = 0;
+        for (uint32_t u = 0; u < blockDim.x / SGD_WAVE; ++u) { tx += s_x[u]; te += s_e[u]; tm = max(tm, s_m[u]); tb += s_b[u]; }
         ctl[HC_EX] = tx;
         ctl[HC_EV] = te;
+        ctl[HC_NBLK] = tb;
         ctl[HC_L0] = 0u;
         ctl[HC_L1] = 0u;
         ctl[HC_MAXM] = tm;
     }
 }
 
+// the hot key of every run event (hot_fh): a workgroup per SGD_HOT_FILL events of one run (every thread finds
+// the run by the same binary search: broadcast loads, no barrier)
+extern "C" __global__ void __launch_bounds__(256) k_hot_fill(const P2Params p) {
+    const uint32_t* ctl = p.hot_ctl;
+    const uint32_t n = min(ctl[HC_N], p.hot_cap), nex = ctl[HC_EX], nblk = ctl[HC_NBLK];
+    for (uint32_t q = blockIdx.x; q < nblk; q += gridDim.x) {
+        const uint32_t h = hot_find(p.hot_info, n, q, HI_BLKOFF);
+        const uint32_t* hi = p.hot_info + (size_t)h * SGD_HOT_INFO;
+        const uint32_t j0 = (q - hi[HI_BLKOFF]) * SGD_HOT_FILL, j1 = min(hi[HI_M], j0 + SGD_HOT_FILL);
+        uint32_t* dst = p.hot_fh + nex + hi[HI_EVOFF];
+        for (uint32_t j = j0 + threadIdx.x; j < j1; j += blockDim.x) dst[j] = h;
+    }
+}
+
 // round 0.  The carried-in partials: a thread each over the first SGD_HOT_L0 events of the run (from HBM).  The
-// runs' events: a workgroup per SGD_HOT_C consecutive (flat) events, staged in LDS with the SGD_HOT_L0 events
-// after them; a thread per event checks it (timestamps nondecreasing, none -1), evaluates f0 (a partial or not)
-// and scans the staged events after it.  Every flat index's hot key goes to hot_fh for the kernels after.
+// runs' events: a workgroup per SGD_HOT_C consecutive flat events, staged in LDS with the SGD_HOT_L0 events after
+// them; a thread per event checks it (timestamps nondecreasing, none -1), evaluates f0 (a partial or not) and scans
+// the staged events after it.  Per flat index: its key (hot_fh), the partial's end so far (hot_death) and where the
+// scan goes on (hot_cur).  No list is built here: round 1 finds the open partials by their death word.
 extern "C" __global__ void __launch_bounds__(SGD_HOT_C) k_hot_r0(const P2Params p) {
     const uint32_t* ctl = p.hot_ctl;
     const uint32_t n = min(ctl[HC_N], p.hot_cap), nex = ctl[HC_EX], total = nex + ctl[HC_EV];
     const int64_t obase = p.ts_col[0];
-    const uint32_t lane = threadIdx.x & (SGD_WAVE - 1), tid = threadIdx.x;
-    for (uint32_t x0 = blockIdx.x * SGD_HOT_C + (tid & ~(SGD_WAVE - 1)); x0 < nex; x0 += gridDim.x * SGD_HOT_C) {
-        const uint32_t x = x0 + lane;
-        bool unres = false;
-        uint32_t slot = 0, h = 0, cur = 0;
-        if (x < nex) {
-            h = hot_find(p.hot_info, n, x, HI_EXOFF);
-            p.hot_fh[x] = h;
-            const uint32_t* hi = p.hot_info + (size_t)h * SGD_HOT_INFO;
-            const uint32_t b = hi[HI_B], m = hi[HI_M];
-            slot = p.max_batch + x;
-            const HotPart P = hot_existing(p, hi[HI_KEY], x - hi[HI_EXOFF]);
-            uint32_t d = HOT_LIVE;
-            const uint32_t i1 = min(m, SGD_HOT_L0);
-            for (uint32_t i = 0; i < i1 && d == HOT_LIVE; ++i) d = hot_test(p, P, b + i, i, obase);
-            unres = d == HOT_LIVE && i1 < m;
-            cur = i1;
-            p.hot_death[slot] = d;
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t x = blockIdx.x * SGD_HOT_C + tid; x < nex; x += gridDim.x * SGD_HOT_C) {
+        const uint32_t h = hot_find(p.hot_info, n, x, HI_EXOFF);
+        p.hot_fh[x] = h;
+        const uint32_t* hi = p.hot_info + (size_t)h * SGD_HOT_INFO;
+        const uint32_t b = hi[HI_B], m = hi[HI_M], j = x - hi[HI_EXOFF];
+        const HotPart P = hot_existing(p, hi[HI_KEY], j);
+        {  // the carried-in list: ts and seq ordered, no ts -1, none newer than the run's first event
+            const Slab G = hot_slab(p, hi[HI_KEY]);
+            const int64_t t0 = hot_ts(p, load_pay<HST>(p.payload, b), obase);
+            bool bad = P.ts == -1 || t0 == -1 || P.ts > t0;
+            if (j > 0u) bad |= P.ts < G.TS(j - 1u) || P.seq <= G.SEQ(j - 1u);
+            if (bad) p.hot_info[(size_t)h * SGD_HOT_INFO + HI_BAD] = 1u;
         }
-        hot_wl_push(p.hot_wl + 3u * (size_t)hot_wl_cap(p), &p.hot_ctl[HC_L1], unres, slot, h, cur);
+        uint32_t d = HOT_LIVE;
+        const uint32_t i1 = min(m, SGD_HOT_L0);
+        for (uint32_t i = 0; i < i1 && d == HOT_LIVE; ++i) d = hot_test(p, P, b + i, i, obase);
+        p.hot_death[x] = d;
+        p.hot_cur[x] = i1;
     }
     constexpr uint32_t ST = SGD_HOT_C + SGD_HOT_L0;
     __shared__ uint32_t s_w[ST * HST];
     __shared__ int64_t s_ts[ST];
-    __shared__ uint32_t s_h0;
     for (uint32_t x0 = nex + blockIdx.x * SGD_HOT_C; x0 < total; x0 += gridDim.x * SGD_HOT_C) {
         uint32_t h = 0, pos = 0, i = 0, m = 0;
-        // the chunk's first key by binary search (one thread), each event's from there forward (hot runs are long:
-        // a chunk spans few keys)
-        if (tid == 0) s_h0 = hot_find(p.hot_info, n, x0 - nex, HI_EVOFF);
-        __syncthreads();
-        uint32_t hx = s_h0;
         for (uint32_t t = tid; t < ST; t += SGD_HOT_C) {
             const uint32_t x = x0 + t;
             if (x >= total) break;
-            while (hx + 1u < n && p.hot_info[(size_t)(hx + 1u) * SGD_HOT_INFO + HI_EVOFF] <= x - nex) ++hx;
+            const uint32_t hx = p.hot_fh[x];
             const uint32_t* hi = p.hot_info + (size_t)hx * SGD_HOT_INFO;
             const uint32_t ix = x - nex - hi[HI_EVOFF], px = hi[HI_B] + ix;
             const PayEl<HST> ev = load_pay<HST>(p.payload, px);
@@ -1570,21 +1591,18 @@ extern "C" __global__ void __launch_bounds__(SGD_HOT_C) k_hot_r0(const P2Params 
                 pos = px;
                 i = ix;
                 m = hi[HI_M];
-                p.hot_fh[x] = hx;
                 p.hot_fbi[x - nex] = ev.w[0];
             }
         }
         __syncthreads();
         const uint32_t x = x0 + tid;
-        bool unres = false;
-        uint32_t cur = 0;
         if (x < total) {
             const int64_t ts = s_ts[tid];
             const int64_t tp = i == 0u ? ts : tid > 0u ? s_ts[tid - 1] : hot_ts(p, load_pay<HST>(p.payload, pos - 1u), obase);
             if (ts == -1 || tp > ts) p.hot_info[(size_t)h * SGD_HOT_INFO + HI_BAD] = 1u;
             p.hot_tcnt[x - nex] = 0u;
             const SgEv0 e0 = sgq_ev0(&s_w[tid * HST]);
-            uint32_t d = HOT_NOTP;
+            uint32_t d = HOT_NOTP, cur = 0;
             if (sgq_f0(e0, p)) {
                 HotPart P;
                 P.ts = ts;
@@ -1599,54 +1617,99 @@ extern "C" __global__ void __launch_bounds__(SGD_HOT_C) k_hot_r0(const P2Params 
                     if (SGQ_WITHIN && expired(P.ts, s_ts[t], p.within)) d = (i + j) * 2u;
                     else if (sgq_f1(sgq_ev1(&s_w[t * HST]), P.cw, P.cn, p)) d = (i + j) * 2u + 1u;
                 }
-                unres = d == HOT_LIVE && i + 1u + nj < m;
                 cur = i + 1u + nj;
             }
-            p.hot_death[pos] = d;
+            p.hot_death[x] = d;
+            p.hot_cur[x] = cur;
         }
-        hot_wl_push(p.hot_wl + 3u * (size_t)hot_wl_cap(p), &p.hot_ctl[HC_L1], unres, pos, h, cur);
         __syncthreads();
     }
 }
 
-// round 1, a wave per partial round 0 left open: the next SGD_HOT_L1 events, 64 at a time; still open: to the
-// list of round 2
+// round 1: a wave per 64 flat indices; each partial still open there scans its next SGD_HOT_L1 events (the wave
+// together, 64 at a time)
 extern "C" __global__ void __launch_bounds__(256) k_hot_r1(const P2Params p) {
-    const uint32_t n1 = p.hot_ctl[HC_L1];
+    const uint32_t* ctl = p.hot_ctl;
+    const uint32_t nex = ctl[HC_EX], total = nex + ctl[HC_EV];
     const int64_t obase = p.ts_col[0];
     const uint32_t lane = threadIdx.x & (SGD_WAVE - 1);
     const uint32_t nw = gridDim.x * (blockDim.x / SGD_WAVE);
-    const uint32_t* wl = p.hot_wl + 3u * (size_t)hot_wl_cap(p);
-    for (uint32_t q = blockIdx.x * (blockDim.x / SGD_WAVE) + threadIdx.x / SGD_WAVE; q < n1; q += nw) {
-        const uint32_t slot = uni(wl[3u * q]), h = uni(wl[3u * q + 1u]), cur = uni(wl[3u * q + 2u]);
-        const uint32_t* hi = p.hot_info + (size_t)h * SGD_HOT_INFO;
-        const uint32_t b = uni(hi[HI_B]), m = uni(hi[HI_M]);
-        int start;
-        const HotPart P = hot_part(p, slot, hi, obase, start);
-        const uint32_t end = min(m, cur + SGD_HOT_L1);
-        uint32_t d = HOT_LIVE;
-        for (uint32_t i0 = cur; i0 < end; i0 += SGD_WAVE) {
-            const uint32_t i = i0 + lane;
-            const uint32_t c = i < end ? hot_test(p, P, b + i, i, obase) : HOT_LIVE;
-            const uint64_t hit = __ballot(c != HOT_LIVE);
-            if (hit) {
-                d = (uint32_t)__shfl((int)c, __builtin_ctzll(hit), SGD_WAVE);
-                break;
+    for (uint32_t x0 = (blockIdx.x * (blockDim.x / SGD_WAVE) + threadIdx.x / SGD_WAVE) * SGD_WAVE; x0 < total;
+         x0 += nw * SGD_WAVE) {
+        const uint32_t x = x0 + lane;
+        uint32_t h = 0, cur = 0;
+        bool open = false;
+        if (x < total && p.hot_death[x] == HOT_LIVE) {
+            h = p.hot_fh[x];
+            cur = p.hot_cur[x];
+            open = cur < p.hot_info[(size_t)h * SGD_HOT_INFO + HI_M];
+        }
+        for (uint64_t bits = __ballot(open); bits; bits &= bits - 1ull) {
+            const int l = __builtin_ctzll(bits);
+            const uint32_t xl = (uint32_t)__shfl((int)x, l, SGD_WAVE), hl = (uint32_t)__shfl((int)h, l, SGD_WAVE);
+            const uint32_t cl = (uint32_t)__shfl((int)cur, l, SGD_WAVE);
+            const uint32_t* hi = p.hot_info + (size_t)hl * SGD_HOT_INFO;
+            const uint32_t b = uni(hi[HI_B]), m = uni(hi[HI_M]);
+            int start;
+            const HotPart P = hot_part(p, xl, nex, hi, obase, start);
+            const uint32_t end = min(m, cl + SGD_HOT_L1);
+            const uint32_t d = hot_wave_scan(p, P, b, cl, end, obase);
+            if (lane == 0) {
+                p.hot_death[xl] = d;
+                p.hot_cur[xl] = end;
             }
         }
-        if (lane == 0) p.hot_death[slot] = d;
-        hot_wl_push(p.hot_wl, &p.hot_ctl[HC_L0], lane == 0 && d == HOT_LIVE && end < m, slot, h, end);
+    }
+}
+
+// the partials still open after round 1, listed for round 2: SGD_HOT_G flat indices per thread, one atomic per
+// workgroup pass
+extern "C" __global__ void __launch_bounds__(256) k_hot_r1c(const P2Params p) {
+    const uint32_t* ctl = p.hot_ctl;
+    const uint32_t total = ctl[HC_EX] + ctl[HC_EV];
+    __shared__ uint32_t s_w[4];
+    __shared__ uint32_t s_base;
+    uint32_t* out = hot_list_buf(p, 0);
+    const uint32_t step = blockDim.x * SGD_HOT_G;
+    for (uint32_t x0 = blockIdx.x * step; x0 < total; x0 += gridDim.x * step) {
+        uint32_t mine = 0;
+        for (uint32_t g = 0; g < SGD_HOT_G; ++g) {
+            const uint32_t x = x0 + g * blockDim.x + threadIdx.x;
+            if (x < total && p.hot_death[x] == HOT_LIVE &&
+                p.hot_cur[x] < p.hot_info[(size_t)p.hot_fh[x] * SGD_HOT_INFO + HI_M])
+                mine++;
+        }
+        uint32_t tot;
+        uint32_t off = hot_block_scan(mine, s_w, tot);
+        if (tot == 0u) continue;
+        if (threadIdx.x == 0) s_base = atomicAdd(&p.hot_ctl[HC_L0], tot);
+        __syncthreads();
+        off += s_base;
+        for (uint32_t g = 0; g < SGD_HOT_G && mine; ++g) {
+            const uint32_t x = x0 + g * blockDim.x + threadIdx.x;
+            if (x < total && p.hot_death[x] == HOT_LIVE) {
+                const uint32_t h = p.hot_fh[x], c = p.hot_cur[x];
+                if (c < p.hot_info[(size_t)h * SGD_HOT_INFO + HI_M]) {
+                    out[3u * off] = x;
+                    out[3u * off + 1u] = h;
+                    out[3u * off + 2u] = c;
+                    off++;
+                    mine--;
+                }
+            }
+        }
+        __syncthreads();
     }
 }
 
 // rounds 2, 3, ... (p.hot_round): the partials still open scan their next SGD_HOT_L1 << 3 (round - 1) events, a
 // wave per (partial, SGD_HOT_L1-event block), nearest blocks first, a block behind a hit already found skipped;
-// the hit is the least (atomicMin).  The round reads list (round & 1) and zeroes the other one, which
-// k_hot_rc fills with the partials still open after it.
+// the hit is the least (atomicMin).  The round reads list (round & 1) and zeroes the other one, which k_hot_rc
+// fills with the partials still open after it.
 __device__ __forceinline__ uint32_t hot_span(uint32_t round) { return SGD_HOT_L1 << (3u * (round - 1u)); }
 extern "C" __global__ void __launch_bounds__(256) k_hot_rn(const P2Params p) {
     const uint32_t in = p.hot_round & 1u;
-    const uint32_t nq = p.hot_ctl[HC_L0 + in];
+    const uint32_t nq = p.hot_ctl[HC_L0 + in], nex = p.hot_ctl[HC_EX];
     if (blockIdx.x == 0 && threadIdx.x == 0) p.hot_ctl[HC_L0 + (in ^ 1u)] = 0u;
     if (nq == 0u) return;
     const uint32_t span = hot_span(p.hot_round), nblk = span / SGD_HOT_L1;
@@ -1654,29 +1717,20 @@ extern "C" __global__ void __launch_bounds__(256) k_hot_rn(const P2Params p) {
     const int64_t obase = p.ts_col[0];
     const uint32_t lane = threadIdx.x & (SGD_WAVE - 1);
     const uint32_t nw = gridDim.x * (blockDim.x / SGD_WAVE);
-    const uint32_t* wl = p.hot_wl + 3u * (size_t)hot_wl_cap(p) * in;
+    const uint32_t* wl = hot_list_buf(p, in);
     for (uint64_t t = blockIdx.x * (blockDim.x / SGD_WAVE) + threadIdx.x / SGD_WAVE; t < total; t += nw) {
         const uint32_t q = (uint32_t)(t % nq), blk = (uint32_t)(t / nq);
-        const uint32_t slot = uni(wl[3u * q]), h = uni(wl[3u * q + 1u]), cur = uni(wl[3u * q + 2u]);
+        const uint32_t x = uni(wl[3u * q]), h = uni(wl[3u * q + 1u]), cur = uni(wl[3u * q + 2u]);
         const uint32_t* hi = p.hot_info + (size_t)h * SGD_HOT_INFO;
         const uint32_t b = uni(hi[HI_B]), m = uni(hi[HI_M]);
         const uint64_t lo64 = (uint64_t)cur + (uint64_t)blk * SGD_HOT_L1;
         if (lo64 >= m) continue;
         const uint32_t lo = (uint32_t)lo64, end = min(m, lo + SGD_HOT_L1);
-        if (uni(__hip_atomic_load(&p.hot_death[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < 2u * lo) continue;
+        if (uni(__hip_atomic_load(&p.hot_death[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < 2u * lo) continue;
         int start;
-        const HotPart P = hot_part(p, slot, hi, obase, start);
-        uint32_t d = HOT_LIVE;
-        for (uint32_t i0 = lo; i0 < end; i0 += SGD_WAVE) {
-            const uint32_t i = i0 + lane;
-            const uint32_t c = i < end ? hot_test(p, P, b + i, i, obase) : HOT_LIVE;
-            const uint64_t hit = __ballot(c != HOT_LIVE);
-            if (hit) {
-                d = (uint32_t)__shfl((int)c, __builtin_ctzll(hit), SGD_WAVE);
-                break;
-            }
-        }
-        if (lane == 0 && d != HOT_LIVE) atomicMin(&p.hot_death[slot], d);
+        const HotPart P = hot_part(p, x, nex, hi, obase, start);
+        const uint32_t d = hot_wave_scan(p, P, b, lo, end, obase);
+        if (lane == 0 && d != HOT_LIVE) atomicMin(&p.hot_death[x], d);
     }
 }
 // after round p.hot_round: the partials it left open with events still ahead, to the next round's list
@@ -1684,50 +1738,54 @@ extern "C" __global__ void __launch_bounds__(256) k_hot_rc(const P2Params p) {
     const uint32_t in = p.hot_round & 1u;
     const uint32_t nq = p.hot_ctl[HC_L0 + in];
     const uint32_t span = hot_span(p.hot_round);
-    const uint32_t* wl = p.hot_wl + 3u * (size_t)hot_wl_cap(p) * in;
+    const uint32_t* wl = hot_list_buf(p, in);
+    uint32_t* out = hot_list_buf(p, in ^ 1u);
+    const uint32_t lane = threadIdx.x & (SGD_WAVE - 1);
     for (uint32_t x0 = blockIdx.x * blockDim.x + (threadIdx.x & ~(SGD_WAVE - 1)); x0 < nq; x0 += gridDim.x * blockDim.x) {
-        const uint32_t q = x0 + (threadIdx.x & (SGD_WAVE - 1));
+        const uint32_t q = x0 + lane;
         bool open = false;
-        uint32_t slot = 0, h = 0, nxt = 0;
+        uint32_t x = 0, h = 0, nxt = 0;
         if (q < nq) {
-            slot = wl[3u * q];
+            x = wl[3u * q];
             h = wl[3u * q + 1u];
             const uint64_t e64 = (uint64_t)wl[3u * q + 2u] + span;
-            open = p.hot_death[slot] == HOT_LIVE && e64 < p.hot_info[(size_t)h * SGD_HOT_INFO + HI_M];
+            open = p.hot_death[x] == HOT_LIVE && e64 < p.hot_info[(size_t)h * SGD_HOT_INFO + HI_M];
             nxt = (uint32_t)min(e64, (uint64_t)0xffffffffu);
         }
-        hot_wl_push(p.hot_wl + 3u * (size_t)hot_wl_cap(p) * (in ^ 1u), &p.hot_ctl[HC_L0 + (in ^ 1u)], open, slot, h, nxt);
+        const uint64_t bal = __ballot(open);  // (few: one atomic per wave that has any)
+        if (bal == 0ull) continue;
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(&p.hot_ctl[HC_L0 + (in ^ 1u)], (uint32_t)__popcll(bal));
+        base = (uint32_t)__shfl((int)base, 0, SGD_WAVE);
+        if (open) {
+            const uint32_t o = base + lane_rank(bal);
+            out[3u * o] = x;
+            out[3u * o + 1u] = h;
+            out[3u * o + 2u] = nxt;
+        }
     }
 }
 
-// per partial slot: the counters (exact, as the walk counts them), the trigger's match count, the survivors
+// per flat index: the counters (exact, as the walk counts them), the trigger's match count, the survivors
 extern "C" __global__ void __launch_bounds__(256) k_hot_emit(const P2Params p) {
     const uint32_t* ctl = p.hot_ctl;
     const uint32_t nex = ctl[HC_EX], total = nex + ctl[HC_EV];
     unsigned long long sc = 0, cr = 0, mt = 0;
     for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < total; x += gridDim.x * blockDim.x) {
-        const bool ex = x < nex;
         const uint32_t h = p.hot_fh[x];
         uint32_t* hi = p.hot_info + (size_t)h * SGD_HOT_INFO;
         if (hi[HI_BAD]) continue;
-        const uint32_t b = hi[HI_B], m = hi[HI_M];
-        uint32_t slot;
-        int start;
-        if (ex) {
-            slot = p.max_batch + x;
-            start = -1;
-        } else {
-            slot = b + (x - nex - hi[HI_EVOFF]);
-            start = (int)(slot - b);
-            sc += 1;  // the start state's seed tests every event (one seed armed)
-        }
-        const uint32_t d = p.hot_death[slot];
+        const uint32_t m = hi[HI_M];
+        const bool ex = x < nex;
+        const int start = ex ? -1 : (int)(x - nex - hi[HI_EVOFF]);
+        if (!ex) sc += 1;  // the start state's seed tests every event (one seed armed)
+        const uint32_t d = p.hot_death[x];
         if (d == HOT_NOTP) continue;
         if (!ex) cr += 1;
         if (d == HOT_LIVE) {  // scanned by every later event of the run; a survivor
             sc += (unsigned long long)((int64_t)m - 1 - start);
             const uint32_t a = atomicAdd(&hi[HI_ALIVE], 1u);
-            if (a < p.cap) p.hot_alive[(size_t)h * p.cap + a] = slot;
+            if (a < p.cap) p.hot_alive[(size_t)h * p.cap + a] = x;
         } else {  // scanned up to its end; the expiring event removes it before its scan
             const uint32_t i = d >> 1;
             sc += (unsigned long long)((int64_t)i - start - 1 + (int64_t)(d & 1u));
@@ -1752,33 +1810,39 @@ extern "C" __global__ void __launch_bounds__(256) k_hot_emit(const P2Params p) {
     }
 }
 
-// per run event: its matches' raw slots (one reservation per workgroup) and its trigger descriptor
+// per run event: its matches' raw slots (SGD_HOT_G events per thread, one reservation per workgroup pass) and its
+// trigger descriptor (the events of keys given back have no count)
 extern "C" __global__ void __launch_bounds__(256) k_hot_trig(const P2Params p) {
     const uint32_t nev = p.hot_ctl[HC_EV];
     __shared__ uint32_t s_w[4];
     __shared__ unsigned long long s_base;
-    const uint32_t lane = threadIdx.x & (SGD_WAVE - 1), w = threadIdx.x / SGD_WAVE;
-    for (uint32_t x0 = blockIdx.x * blockDim.x; x0 < nev; x0 += gridDim.x * blockDim.x) {
-        const uint32_t x = x0 + threadIdx.x;
-        const uint32_t c = x < nev ? p.hot_tcnt[x] : 0u;  // (0 for the events of keys given back)
-        const uint32_t incl = wave_incl_scan(c, (int)lane);
-        if (lane == SGD_WAVE - 1) s_w[w] = incl;
-        __syncthreads();
-        uint32_t off = incl - c, tot = 0;
-        for (uint32_t u = 0; u < blockDim.x / SGD_WAVE; ++u) {
-            if (u < w) off += s_w[u];
-            tot += s_w[u];
+    const uint32_t step = blockDim.x * SGD_HOT_G;
+    for (uint32_t x0 = blockIdx.x * step; x0 < nev; x0 += gridDim.x * step) {
+        uint32_t c[SGD_HOT_G], mine = 0;
+#pragma unroll
+        for (uint32_t g = 0; g < SGD_HOT_G; ++g) {
+            const uint32_t x = x0 + g * blockDim.x + threadIdx.x;
+            c[g] = x < nev ? p.hot_tcnt[x] : 0u;
+            mine += c[g];
         }
-        if (threadIdx.x == 0) s_base = tot ? atomicAdd(p.raw_count, (unsigned long long)tot) : 0ull;
+        uint32_t tot;
+        const uint32_t off = hot_block_scan(mine, s_w, tot);
+        if (tot == 0u) continue;
+        if (threadIdx.x == 0) s_base = atomicAdd(p.raw_count, (unsigned long long)tot);
         __syncthreads();
-        if (c) {
-            const unsigned long long first = p.raw_static + s_base + off;
-            if (first + c <= p.raw_capacity)
-                p.t_desc[p.hot_fbi[x]] = ((uint64_t)c << 32) | (uint64_t)(uint32_t)first;
-            else
-                atomicOr(p.err, (uint32_t)SGD_ERR_MATCH_CAP);
-            p.hot_tbase[x] = (uint32_t)first;
-            p.hot_tcnt[x] = 0u;  // (the fill's rank counter)
+        unsigned long long first = p.raw_static + s_base + off;
+#pragma unroll
+        for (uint32_t g = 0; g < SGD_HOT_G; ++g) {
+            if (c[g]) {
+                const uint32_t x = x0 + g * blockDim.x + threadIdx.x;
+                if (first + c[g] <= p.raw_capacity)
+                    p.t_desc[p.hot_fbi[x]] = ((uint64_t)c[g] << 32) | (uint64_t)(uint32_t)first;
+                else
+                    atomicOr(p.err, (uint32_t)SGD_ERR_MATCH_CAP);
+                p.hot_tbase[x] = (uint32_t)first;
+                p.hot_tcnt[x] = 0u;  // (the fill's rank counter)
+                first += c[g];
+            }
         }
         __syncthreads();
     }
@@ -1789,120 +1853,209 @@ extern "C" __global__ void __launch_bounds__(256) k_hot_place(const P2Params p) 
     const uint32_t* ctl = p.hot_ctl;
     const uint32_t nex = ctl[HC_EX], total = nex + ctl[HC_EV];
     const int64_t obase = p.ts_col[0];
+    (void)obase;
     for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < total; x += gridDim.x * blockDim.x) {
-        const bool ex = x < nex;
-        const uint32_t h = p.hot_fh[x];
-        const uint32_t* hi = p.hot_info + (size_t)h * SGD_HOT_INFO;
-        if (hi[HI_BAD]) continue;
-        const uint32_t slot = ex ? p.max_batch + x : hi[HI_B] + (x - nex - hi[HI_EVOFF]);
-        const uint32_t d = p.hot_death[slot];
+        const uint32_t d = p.hot_death[x];
         if (d == HOT_NOTP || d == HOT_LIVE || !(d & 1u)) continue;
+        const uint32_t* hi = p.hot_info + (size_t)p.hot_fh[x] * SGD_HOT_INFO;
+        if (hi[HI_BAD]) continue;
         const uint32_t tp = hi[HI_EVOFF] + (d >> 1);
         const uint64_t dst = (uint64_t)p.hot_tbase[tp] + atomicAdd(&p.hot_tcnt[tp], 1u);
         if (dst >= p.raw_capacity) continue;
-        int start;
-        const HotPart P = hot_part(p, slot, hi, obase, start);
-        p.raw_e1[dst] = P.seq;
 #if SGQ_PROJ
+        int start;
+        const HotPart P = hot_part(p, x, nex, hi, obase, start);
+        p.raw_e1[dst] = P.seq;
 #pragma unroll
         for (int w = 0; w < SGQ_NCAPW; ++w) p.raw_capw[(size_t)w * p.raw_capacity + dst] = P.cw[w];
         if (SGQ_CAPNULL) p.raw_capnull[dst] = P.cn;
+#else
+        p.raw_e1[dst] = x >= nex ? p.seq_base + p.hot_fbi[x - nex] : hot_slab(p, hi[HI_KEY]).SEQ(x - hi[HI_EXOFF]);
 #endif
     }
 }
 
-// per trigger with several matches: its range in list order (= e1 seq order; insertion sort, ranges are short)
+// per trigger with several matches: its range into list order (= e1 seq order).  A range of 2..8 by its thread
+// (values in registers, ranked by counting); longer ones by the wave of its 64 run events (one match per lane,
+// ranks by shuffles), beyond 64 by lane 0 (insertion sort)
 extern "C" __global__ void __launch_bounds__(256) k_hot_sort(const P2Params p) {
     const uint32_t nev = p.hot_ctl[HC_EV];
-    for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < nev; x += gridDim.x * blockDim.x) {
-        const uint32_t c = p.hot_tcnt[x];
-        if (c < 2u) continue;
-        const uint64_t f = p.hot_tbase[x];
-        if (f + c > p.raw_capacity) continue;
-        for (uint32_t a = 1; a < c; ++a) {
-            const uint64_t v = p.raw_e1[f + a];
+    const uint32_t lane = threadIdx.x & (SGD_WAVE - 1);
+    const uint32_t nw = gridDim.x * (blockDim.x / SGD_WAVE);
+    const uint64_t RC = p.raw_capacity;
+    for (uint32_t x0 = (blockIdx.x * (blockDim.x / SGD_WAVE) + threadIdx.x / SGD_WAVE) * SGD_WAVE; x0 < nev;
+         x0 += nw * SGD_WAVE) {
+        const uint32_t x = x0 + lane;
+        const uint32_t c = x < nev ? p.hot_tcnt[x] : 0u;
+        const uint32_t fb = c >= 2u ? p.hot_tbase[x] : 0u;
+        constexpr uint32_t SMALL = 8;
+        if (c >= 2u && c <= SMALL && (uint64_t)fb + c <= RC) {
+            uint64_t v[SMALL];
 #if SGQ_PROJ
-            uint32_t cw[SGQ_NCAPW > 0 ? SGQ_NCAPW : 1], cn = 0;
-#pragma unroll
-            for (int w = 0; w < SGQ_NCAPW; ++w) cw[w] = p.raw_capw[(size_t)w * p.raw_capacity + f + a];
-            if (SGQ_CAPNULL) cn = p.raw_capnull[f + a];
+            uint32_t cw[SMALL][SGQ_NCAPW > 0 ? SGQ_NCAPW : 1], cn[SMALL];
 #endif
-            uint32_t z = a;
-            while (z > 0u && p.raw_e1[f + z - 1u] > v) {
-                p.raw_e1[f + z] = p.raw_e1[f + z - 1u];
+#pragma unroll
+            for (uint32_t a = 0; a < SMALL; ++a) {
+                v[a] = a < c ? p.raw_e1[fb + a] : ~0ull;
 #if SGQ_PROJ
 #pragma unroll
-                for (int w = 0; w < SGQ_NCAPW; ++w)
-                    p.raw_capw[(size_t)w * p.raw_capacity + f + z] = p.raw_capw[(size_t)w * p.raw_capacity + f + z - 1u];
-                if (SGQ_CAPNULL) p.raw_capnull[f + z] = p.raw_capnull[f + z - 1u];
+                for (int w = 0; w < SGQ_NCAPW; ++w) cw[a][w] = a < c ? p.raw_capw[(size_t)w * RC + fb + a] : 0u;
+                cn[a] = (SGQ_CAPNULL && a < c) ? p.raw_capnull[fb + a] : 0u;
 #endif
-                --z;
             }
-            p.raw_e1[f + z] = v;
+#pragma unroll
+            for (uint32_t a = 0; a < SMALL; ++a) {
+                if (a < c) {
+                    uint32_t r = 0;
+#pragma unroll
+                    for (uint32_t u = 0; u < SMALL; ++u) r += v[u] < v[a] ? 1u : 0u;  // (distinct; ~0 pads rank last)
+                    p.raw_e1[fb + r] = v[a];
 #if SGQ_PROJ
 #pragma unroll
-            for (int w = 0; w < SGQ_NCAPW; ++w) p.raw_capw[(size_t)w * p.raw_capacity + f + z] = cw[w];
-            if (SGQ_CAPNULL) p.raw_capnull[f + z] = cn;
+                    for (int w = 0; w < SGQ_NCAPW; ++w) p.raw_capw[(size_t)w * RC + fb + r] = cw[a][w];
+                    if (SGQ_CAPNULL) p.raw_capnull[fb + r] = cn[a];
 #endif
+                }
+            }
+        }
+        for (uint64_t bits = __ballot(c > SMALL && (uint64_t)fb + c <= RC); bits; bits &= bits - 1ull) {
+            const int l = __builtin_ctzll(bits);
+            const uint32_t cl = uni((uint32_t)__shfl((int)c, l, SGD_WAVE));
+            const uint64_t f = uni((uint32_t)__shfl((int)fb, l, SGD_WAVE));
+            if (cl <= SGD_WAVE) {
+                const bool in = lane < cl;
+                const uint64_t v = in ? p.raw_e1[f + lane] : ~0ull;
+#if SGQ_PROJ
+                uint32_t cw[SGQ_NCAPW > 0 ? SGQ_NCAPW : 1], cn = 0;
+#pragma unroll
+                for (int w = 0; w < SGQ_NCAPW; ++w) cw[w] = in ? p.raw_capw[(size_t)w * RC + f + lane] : 0u;
+                if (SGQ_CAPNULL) cn = in ? p.raw_capnull[f + lane] : 0u;
+#endif
+                const uint32_t vlo = (uint32_t)v, vhi = (uint32_t)(v >> 32);
+                uint32_t r = 0;
+                for (uint32_t j = 0; j < cl; ++j) {  // (seqs are distinct)
+                    const uint64_t vj = (uint64_t)(uint32_t)__shfl((int)vlo, (int)j, SGD_WAVE) |
+                                        ((uint64_t)(uint32_t)__shfl((int)vhi, (int)j, SGD_WAVE) << 32);
+                    r += vj < v ? 1u : 0u;
+                }
+                if (in) {
+                    p.raw_e1[f + r] = v;
+#if SGQ_PROJ
+#pragma unroll
+                    for (int w = 0; w < SGQ_NCAPW; ++w) p.raw_capw[(size_t)w * RC + f + r] = cw[w];
+                    if (SGQ_CAPNULL) p.raw_capnull[f + r] = cn;
+#endif
+                }
+            } else if (lane == 0) {
+                for (uint32_t a = 1; a < cl; ++a) {
+                    const uint64_t v = p.raw_e1[f + a];
+#if SGQ_PROJ
+                    uint32_t cw[SGQ_NCAPW > 0 ? SGQ_NCAPW : 1], cn = 0;
+#pragma unroll
+                    for (int w = 0; w < SGQ_NCAPW; ++w) cw[w] = p.raw_capw[(size_t)w * RC + f + a];
+                    if (SGQ_CAPNULL) cn = p.raw_capnull[f + a];
+#endif
+                    uint32_t z = a;
+                    while (z > 0u && p.raw_e1[f + z - 1u] > v) {
+                        p.raw_e1[f + z] = p.raw_e1[f + z - 1u];
+#if SGQ_PROJ
+#pragma unroll
+                        for (int w = 0; w < SGQ_NCAPW; ++w) p.raw_capw[(size_t)w * RC + f + z] = p.raw_capw[(size_t)w * RC + f + z - 1u];
+                        if (SGQ_CAPNULL) p.raw_capnull[f + z] = p.raw_capnull[f + z - 1u];
+#endif
+                        --z;
+                    }
+                    p.raw_e1[f + z] = v;
+#if SGQ_PROJ
+#pragma unroll
+                    for (int w = 0; w < SGQ_NCAPW; ++w) p.raw_capw[(size_t)w * RC + f + z] = cw[w];
+                    if (SGQ_CAPNULL) p.raw_capnull[f + z] = cn;
+#endif
+                }
+            }
         }
     }
 }
 
-// a workgroup per hot key: the survivors in list order to the key's slab, the header, and the resume word that
-// tells the HBM pass the key is done
+// the key's header and the resume word that tells the HBM pass the key is done: the last event's partial (if f0
+// held) is still staged, and the seed it used re-arms at the next event
+__device__ __forceinline__ void hot_close(const P2Params& p, const uint32_t* hi, uint32_t nex, uint32_t na) {
+    const uint32_t k = hi[HI_KEY];
+    const bool lastf0 = p.hot_death[nex + hi[HI_EVOFF] + hi[HI_M] - 1u] != HOT_NOTP;
+    const uint32_t gns = lastf0 ? 1u : 0u;
+    p.hdr[k] = SGD_H_MAKE(na - gns, gns, lastf0 ? 0u : 1u, lastf0 ? 1u : 0u, 1u);
+    p.resume[k] = SGD_HOT_DONE;
+}
+__device__ __forceinline__ void hot_store(const P2Params& p, const Slab& G, uint32_t o, const HotPart& P) {
+    G.TS(o) = P.ts;
+    G.SEQ(o) = P.seq;
+#pragma unroll
+    for (int w = 0; w < SGQ_NCAPW; ++w) G.CAP(w, o) = P.cw[w];
+    if (SGQ_CAPNULL) G.NUL(o) = P.cn;
+}
+
+// a wave per hot key with at most 64 survivors: the survivors in list order (= flat order) to the key's slab (a
+// lane each: every lane reads its partial before any writes), the header, the resume word
 extern "C" __global__ void __launch_bounds__(256) k_hot_final(const P2Params p) {
-    const uint32_t n = min(p.hot_ctl[HC_N], p.hot_cap);
+    const uint32_t n = min(p.hot_ctl[HC_N], p.hot_cap), nex = p.hot_ctl[HC_EX];
     const int64_t obase = p.ts_col[0];
-    __shared__ uint32_t s_slot[SGD_MAX_CAP + 1], s_ord[SGD_MAX_CAP + 1], s_key[SGD_MAX_CAP + 1];
-    for (uint32_t h = blockIdx.x; h < n; h += gridDim.x) {
+    const uint32_t lane = threadIdx.x & (SGD_WAVE - 1);
+    const uint32_t nw = gridDim.x * (blockDim.x / SGD_WAVE);
+    for (uint32_t h = blockIdx.x * (blockDim.x / SGD_WAVE) + threadIdx.x / SGD_WAVE; h < n; h += nw) {
         const uint32_t* hi = p.hot_info + (size_t)h * SGD_HOT_INFO;
-        if (hi[HI_BAD]) continue;  // (uniform) left to the HBM pass
-        const uint32_t k = hi[HI_KEY], b = hi[HI_B], m = hi[HI_M], na = hi[HI_ALIVE];
+        if (uni(hi[HI_BAD])) continue;  // left to the HBM pass
+        const uint32_t na = uni(hi[HI_ALIVE]);
         if (na > p.cap) {  // more partials than the slab holds
-            if (threadIdx.x == 0) {
+            if (lane == 0) {
                 atomicOr(p.err, (uint32_t)SGD_ERR_PARTIAL_CAP);
-                p.resume[k] = SGD_HOT_DONE;
+                p.resume[hi[HI_KEY]] = SGD_HOT_DONE;
             }
             continue;
         }
-        for (uint32_t a = threadIdx.x; a < na; a += blockDim.x) {
-            const uint32_t s = p.hot_alive[(size_t)h * p.cap + a];
-            s_slot[a] = s;
-            s_key[a] = s >= p.max_batch ? s - p.max_batch - hi[HI_EXOFF] : p.cap + (s - b);  // list order
-        }
+        if (na > SGD_WAVE) continue;  // (k_hot_final_big)
+        const bool in = lane < na;
+        const uint32_t x = in ? p.hot_alive[(size_t)h * p.cap + lane] : 0xffffffffu;
+        uint32_t r = 0;
+        for (uint32_t u = 0; u < na; ++u) r += (uint32_t)__shfl((int)x, (int)u, SGD_WAVE) < x ? 1u : 0u;
+        HotPart P;
+        int start;
+        if (in) P = hot_part(p, x, nex, hi, obase, start);
+        if (in) hot_store(p, hot_slab(p, hi[HI_KEY]), r, P);
+        if (lane == 0) hot_close(p, hi, nex, na);
+    }
+}
+
+// a workgroup per hot key with more than 64 survivors (rare): ranked in LDS, moved 256 at a time in order
+extern "C" __global__ void __launch_bounds__(256) k_hot_final_big(const P2Params p) {
+    const uint32_t n = min(p.hot_ctl[HC_N], p.hot_cap), nex = p.hot_ctl[HC_EX];
+    const int64_t obase = p.ts_col[0];
+    __shared__ uint32_t s_x[SGD_MAX_CAP + 1], s_ord[SGD_MAX_CAP + 1];
+    for (uint32_t h = blockIdx.x; h < n; h += gridDim.x) {
+        const uint32_t* hi = p.hot_info + (size_t)h * SGD_HOT_INFO;
+        const uint32_t na = hi[HI_ALIVE];
+        if (hi[HI_BAD] || na <= SGD_WAVE || na > p.cap) continue;  // (uniform)
+        for (uint32_t a = threadIdx.x; a < na; a += blockDim.x) s_x[a] = p.hot_alive[(size_t)h * p.cap + a];
         __syncthreads();
-        for (uint32_t a = threadIdx.x; a < na; a += blockDim.x) {
+        for (uint32_t a = threadIdx.x; a < na; a += blockDim.x) {  // rank by flat index (distinct)
             uint32_t r = 0;
-            const uint32_t ka = s_key[a];
-            for (uint32_t u = 0; u < na; ++u) r += s_key[u] < ka ? 1u : 0u;
-            s_ord[r] = s_slot[a];
+            const uint32_t xa = s_x[a];
+            for (uint32_t u = 0; u < na; ++u) r += s_x[u] < xa ? 1u : 0u;
+            s_ord[r] = xa;
         }
         __syncthreads();
         // in place, 256 at a time: survivor o comes from list index >= o, so a chunk's writes land below every
         // later chunk's reads
-        const Slab G = hot_slab(p, k);
+        const Slab G = hot_slab(p, hi[HI_KEY]);
         for (uint32_t c0 = 0; c0 < na; c0 += blockDim.x) {
             const uint32_t o = c0 + threadIdx.x;
             HotPart P;
             int start;
-            if (o < na) P = hot_part(p, s_ord[o], hi, obase, start);
+            if (o < na) P = hot_part(p, s_ord[o], nex, hi, obase, start);
             __syncthreads();
-            if (o < na) {
-                G.TS(o) = P.ts;
-                G.SEQ(o) = P.seq;
-#pragma unroll
-                for (int w = 0; w < SGQ_NCAPW; ++w) G.CAP(w, o) = P.cw[w];
-                if (SGQ_CAPNULL) G.NUL(o) = P.cn;
-            }
+            if (o < na) hot_store(p, G, o, P);
             __syncthreads();
         }
-        if (threadIdx.x == 0) {
-            // the last event's partial (if f0 held) is still staged, and the seed it used re-arms at the next event
-            const bool lastf0 = p.hot_death[b + m - 1u] != HOT_NOTP;
-            const uint32_t gns = lastf0 ? 1u : 0u;
-            p.hdr[k] = SGD_H_MAKE(na - gns, gns, lastf0 ? 0u : 1u, lastf0 ? 1u : 0u, 1u);
-            p.resume[k] = SGD_HOT_DONE;
-        }
+        if (threadIdx.x == 0) hot_close(p, hi, nex, na);
         __syncthreads();
     }
 }

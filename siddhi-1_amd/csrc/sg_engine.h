@@ -82,7 +82,7 @@ enum {
 #define SGD_HOT_CTL 8
 #define SGD_HOT_CTL_BIG 6          // hot_ctl word: workgroups whose range exceeded SGD_BIG_TILE events
 #define SGD_BIG_TILE 65536u
-#define SGD_HOT_INFO 8
+#define SGD_HOT_INFO 16
 
 enum { SGD_ST_SCANNED = 0, SGD_ST_CREATED, SGD_ST_MATCHES, SGD_ST_KEYS, SGD_ST_LIVE0, SGD_ST_SPILLS, SGD_ST_N };
 
@@ -143,18 +143,18 @@ struct P2Params {
     // partial's fate is the first later event that expires or matches it); 0 = off
     uint32_t hot_min;
     uint32_t hot_cap;                  // hot_list entries (further hot keys are walked by their lanes)
-    uint32_t max_batch;                // partial slots: [0, max_batch) created at that payload position, then the
-                                       // keys' partials carried in from the previous batch
+    uint32_t max_batch;                // (sizes the flat index space: <= max_batch events + hot_cap * cap carried in)
     uint32_t* hot_ctl;                 // [SGD_HOT_CTL] counters (hot_ctl[0]: hot keys listed; reset by the HBM pass)
     uint32_t* hot_list;                // [hot_cap] keys
     uint32_t* hot_info;                // [hot_cap][SGD_HOT_INFO] per hot key: run, offsets, checks, survivors
-    uint32_t* hot_death;               // [max_batch + hot_cap * cap] per partial slot: 2 * event + matched
-    uint32_t* hot_wl;                  // [2][max_batch + hot_cap * cap][3] unresolved partials (slot, key, cursor)
+    uint32_t* hot_death;               // [flat] per partial: 2 * (ending event) + matched; or live / no partial
+    uint32_t* hot_cur;                 // [flat] the next event its search scans
+    uint32_t* hot_wl;                  // [2][flat][3] partials still open (flat index, key, cursor), by round
     uint32_t* hot_tcnt;                // [max_batch] matches per trigger (by flat event index)
     uint32_t* hot_tbase;               // [max_batch] their first raw slot
     uint32_t* hot_fbi;                 // [max_batch] the batch position of each flat event
-    uint32_t* hot_alive;               // [hot_cap][cap] surviving partial slots
-    uint32_t* hot_fh;                  // [max_batch + hot_cap * cap] the hot key of each flat index (round 0)
+    uint32_t* hot_alive;               // [hot_cap][cap] the survivors' flat indices
+    uint32_t* hot_fh;                  // [flat] the hot key of each flat index (round 0)
     uint32_t hot_round;                // the search round a k_hot_rn / k_hot_rc launch runs
     uint64_t cst[SGD_MAX_CONST];       // filter constants, already in their comparison domain
 };

@@ -135,7 +135,7 @@ struct sg_engine {
         hipFunction_t adv[2] = {nullptr, nullptr};   // [0]: multi / state-0 stream, [1]: state-1 stream
         hipFunction_t adv_h[2] = {nullptr, nullptr}; // the HBM pass over the waves the staged pass deferred
         hipFunction_t pack[2] = {nullptr, nullptr};
-        hipFunction_t hot[10] = {};                  // the hot-key pipeline (k_hot_prep .. k_hot_final)
+        hipFunction_t hot[13] = {};                  // the hot-key pipeline (k_hot_prep .. k_hot_final_big)
         uint32_t adv_static_lds = 0;                 // the staged pass's static LDS (beside its dynamic staging)
     };
     JitQuery jq;
@@ -197,8 +197,9 @@ struct sg_engine {
     bool hot_on = true;
     bool skewed = false;           // recent batches had workgroup ranges > SGD_BIG_TILE events: sorted grouping
     uint32_t hot_min = 0, hot_cap = 0;
+    uint64_t hot_factor = 4;       // "hot": also >= hot_factor x the batch's mean events per key (SG_HOT_FACTOR)
     uint32_t *hot_ctl = nullptr, *hot_list = nullptr, *hot_info = nullptr, *hot_death = nullptr, *hot_wl = nullptr;
-    uint32_t *hot_tcnt = nullptr, *hot_tbase = nullptr, *hot_alive = nullptr, *hot_fh = nullptr, *hot_fbi = nullptr;
+    uint32_t *hot_tcnt = nullptr, *hot_tbase = nullptr, *hot_alive = nullptr, *hot_fh = nullptr, *hot_fbi = nullptr, *hot_cur = nullptr;
     uint64_t hot_batches = 0;      // batches the pipeline ran on (sg_engine_describe)
     uint32_t hbm_grid = 2048;      // work-groups of the HBM pass (SG_HBM_GRID: experiments)
     uint32_t* dlist = nullptr;     // the waves the HBM pass takes, and their number
@@ -569,7 +570,8 @@ void allocate(sg_engine* e) {
     HIP_OK(hipMemsetAsync(e->hot_ctl, 0, SGD_HOT_CTL * 4, e->stream));
     {
         const char* x = getenv("SG_HOT_MIN");  // 0: off
-        e->hot_min = x ? (uint32_t)strtoul(x, nullptr, 0) : 256u;
+        e->hot_min = x ? (uint32_t)strtoul(x, nullptr, 0) : 64u;
+        if (const char* f = getenv("SG_HOT_FACTOR")) e->hot_factor = std::max(1ul, strtoul(f, nullptr, 0));
         if (e->hot_min == 0) e->hot_ok = false;
     }
     if (e->hot_ok) {
@@ -583,6 +585,7 @@ void allocate(sg_engine* e) {
         e->hot_tbase = dalloc<uint32_t>(B, o);
         e->hot_alive = dalloc<uint32_t>((size_t)e->hot_cap * C, o);
         e->hot_fh = dalloc<uint32_t>(slots, o);
+        e->hot_cur = dalloc<uint32_t>(slots, o);
         e->hot_fbi = dalloc<uint32_t>(B, o);
     }
     e->tile_sum = dalloc<uint32_t>(B / SGD_ORDER_TILE + 1, o);
@@ -654,9 +657,11 @@ sg_engine::Variant& variant(sg_engine* e, bool evnull, bool capnull) {
         HIP_OK(hipModuleGetFunction(&r.adv_h[1], r.mod, "k_adv_s1_h"));
     }
     if (e->hot_ok) {
-        static const char* const names[10] = {"k_hot_prep", "k_hot_r0",   "k_hot_r1",    "k_hot_rn",  "k_hot_rc",
-                                              "k_hot_emit", "k_hot_trig", "k_hot_place", "k_hot_sort", "k_hot_final"};
-        for (int i = 0; i < 10; i++) HIP_OK(hipModuleGetFunction(&r.hot[i], r.mod, names[i]));
+        static const char* const names[13] = {"k_hot_prep",  "k_hot_fill", "k_hot_r0",    "k_hot_r1",
+                                              "k_hot_r1c",   "k_hot_rn",   "k_hot_rc",    "k_hot_emit",
+                                              "k_hot_trig",  "k_hot_place", "k_hot_sort", "k_hot_final",
+                                              "k_hot_final_big"};
+        for (int i = 0; i < 13; i++) HIP_OK(hipModuleGetFunction(&r.hot[i], r.mod, names[i]));
     }
     {
         int sh = 0;
@@ -945,7 +950,7 @@ int push(sg_engine* e, const sg_batch* b) {
     p.hot_ctl = e->hot_ctl;
     if (e->hot_ok) {
         // a partitioned batch's keys hold n / K events on average: "hot" is far above that (and above hot_min)
-        p.hot_min = pl.partitioned ? std::max<uint32_t>(e->hot_min, (uint32_t)std::min<uint64_t>(8ull * n / e->K, 1u << 30))
+        p.hot_min = pl.partitioned ? std::max<uint32_t>(e->hot_min, (uint32_t)std::min<uint64_t>(e->hot_factor * n / e->K, 1u << 30))
                                    : e->hot_min;
         p.hot_cap = e->hot_cap;
         p.max_batch = (uint32_t)e->maxb;
@@ -957,6 +962,7 @@ int push(sg_engine* e, const sg_batch* b) {
         p.hot_tbase = e->hot_tbase;
         p.hot_alive = e->hot_alive;
         p.hot_fh = e->hot_fh;
+        p.hot_cur = e->hot_cur;
         p.hot_fbi = e->hot_fbi;
     }
     for (size_t i = 0; i < e->consts.size(); i++) p.cst[i] = e->consts[i];
@@ -971,19 +977,22 @@ int push(sg_engine* e, const sg_batch* b) {
                p.stage_chunks * 16u * (SGD_BLOCK / SGD_WAVE) + (fused ? SGD_SPLIT_CNT_BYTES : 0u));
         if (e->timing) { a1 = e->ev(); e->mark(a1); e->spans.push_back({a0, a1, 1}); a0 = e->ev(); e->mark(a0); }
         if (e->hot_ok && e->hot_on) {  // the hot keys the staged pass listed (fixed grids: the counts are on the device)
-            launch(v.hot[0], 1, 1024, &p, e->stream);  // k_hot_prep
-            launch(v.hot[1], 2048, 256, &p, e->stream);  // k_hot_r0
-            launch(v.hot[2], 512, 256, &p, e->stream);  // k_hot_r1
-            // rounds 2.. until the spans scanned cover the longest possible run (round r: 512 << 3 (r - 1) events)
+            launch(v.hot[0], 1, 1024, &p, e->stream);    // k_hot_prep
+            launch(v.hot[1], 1024, 256, &p, e->stream);  // k_hot_fill
+            launch(v.hot[2], 2048, 256, &p, e->stream);  // k_hot_r0
+            launch(v.hot[3], 1024, 256, &p, e->stream);  // k_hot_r1
             uint64_t covered = 128 + 512;
+            if (covered < e->maxb) launch(v.hot[4], 512, 256, &p, e->stream);  // k_hot_r1c
+            // rounds 2.. until the spans scanned cover the longest possible run (round r: 512 << 3 (r - 1) events)
             for (uint32_t r = 2; covered < e->maxb; r++) {
                 p.hot_round = r;
                 covered += 512ull << (3 * (r - 1));
-                launch(v.hot[3], 1024, 256, &p, e->stream);  // k_hot_rn
-                if (covered < e->maxb) launch(v.hot[4], 256, 256, &p, e->stream);  // k_hot_rc
+                launch(v.hot[5], 1024, 256, &p, e->stream);  // k_hot_rn
+                if (covered < e->maxb) launch(v.hot[6], 256, 256, &p, e->stream);  // k_hot_rc
             }
-            for (int i = 5; i < 9; i++) launch(v.hot[i], 1024, 256, &p, e->stream);  // emit, trig, place, sort
-            launch(v.hot[9], 256, 256, &p, e->stream);  // k_hot_final
+            for (int i = 7; i < 11; i++) launch(v.hot[i], 1024, 256, &p, e->stream);  // emit, trig, place, sort
+            launch(v.hot[11], 512, 256, &p, e->stream);  // k_hot_final
+            launch(v.hot[12], 64, 256, &p, e->stream);   // k_hot_final_big
             e->hot_batches++;
         }
         // one wave per work-group over the listed waves (a fixed grid: the list's length is on the device)

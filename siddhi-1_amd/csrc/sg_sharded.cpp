@@ -38,6 +38,7 @@
 
 #include <algorithm>
 #include <functional>
+#include <map>
 #include <future>
 #include <memory>
 #include <stdexcept>
@@ -73,7 +74,7 @@ const uint64_t kMagic = 0x3248534753ull;  // "SGSH2" (v2: seq maps with their ba
 struct SeqMap {
     uint64_t base = 0;
     std::vector<uint64_t> v;
-    uint64_t trim_at = 1u << 20;   // the size at which the next trim check runs (doubles with the live span)
+    uint64_t trim_at = 1u << 20;   // the size at which the next trim check runs (+ max(2^20, live span) after each)
     uint64_t end() const { return base + v.size(); }
     void trim(uint64_t keep_from) {
         if (keep_from <= base) return;
@@ -130,6 +131,7 @@ struct ShardEngine {
         uint32_t next = 0;
     };
     std::vector<DevSplit> splits;   // by source device ordinal (lazily)
+    std::map<void*, std::pair<int, hipEvent_t>> waits;   // sg_wait_stream: caller stream -> (device, event)
     std::vector<Peer> peers;        // per shard (lazily)
     bool force_peer = false;        // SG_FAN_PEER_COPY (tests): peer-copy every part, even on the source device
     uint64_t max_batch = 0;
@@ -137,6 +139,11 @@ struct ShardEngine {
 
     ~ShardEngine() { free_device_buffers(); }
     void free_device_buffers() {
+        for (auto& w : waits) {
+            (void)hipSetDevice(w.second.first);
+            (void)hipEventDestroy(w.second.second);
+        }
+        waits.clear();
         for (size_t r = 0; r < peers.size(); r++) {
             Peer& q = peers[r];
             if (!q.stream) continue;
@@ -417,6 +424,8 @@ void push_device(ShardEngine* s, const sg_batch* b) {
     FAN_OK(hipSetDevice(src));
     for (uint32_t r = 0; r < N; r++)   // this set's previous readers are done (on the device)
         if (st.armed[r]) FAN_OK(hipStreamWaitEvent(p.stream, st.done[r], 0));
+    for (auto& w : s->waits)           // the producers the caller named (sg_wait_stream)
+        FAN_OK(hipStreamWaitEvent(p.stream, w.second.second, 0));
     std::vector<const void*> cols(nc);
     std::vector<uint32_t> cb(nc);
     std::vector<const uint8_t*> nul(nc, nullptr);
@@ -554,6 +563,8 @@ int shd_push(ShardEngine* s, const sg_batch* b) {
             return SG_OK;
         }
         if (!b->key) throw ShardError(SG_ERR_INVALID, "partitioned query needs key ids");
+        // (host and device batches alike: the device split's buffers hold max_batch events)
+        if (n > s->max_batch) throw ShardError(SG_ERR_INVALID, "batch larger than max_batch");
         if (b->mem == SG_MEM_DEVICE) {
             push_device(s, b);
             return SG_OK;
@@ -863,7 +874,8 @@ void trim_maps(ShardEngine* s) {
         if (!due[r]) continue;
         SeqMap& m = s->gmap[r];
         m.trim(std::min(lo[r], m.end()));
-        m.trim_at = std::max<uint64_t>(1u << 20, 2 * m.v.size());
+        // the next check once as many entries again (at least 2^20) were appended: amortised over the pushes
+        m.trim_at = m.v.size() + std::max<uint64_t>(1u << 20, m.v.size());
         s->trims++;
     }
 }
@@ -975,6 +987,7 @@ int shd_reset_keys(ShardEngine* s, const uint32_t* keys, uint64_t n, uint32_t me
 // image: magic u64, N u32, pad u32 | per shard: u64 image bytes, u64 map base, u64 map entries, image, map (u64 each)
 int shd_snapshot(ShardEngine* s, void** buf, size_t* len) {
     try {
+        if (s->failed) throw ShardError(SG_ERR_STATE, "a previous call failed part-way: the shards are out of step");
         if (s->pend.n || s->held) throw ShardError(SG_ERR_STATE, "poll the matches first");
         std::vector<void*> img(s->N, nullptr);
         std::vector<size_t> il(s->N, 0);
@@ -1034,7 +1047,7 @@ int shd_restore(ShardEngine* s, const void* buf, size_t len) {
             maps[r].base = a[1];
             maps[r].v.resize(a[2]);
             memcpy(maps[r].v.data(), p + off, 8 * a[2]);
-            maps[r].trim_at = std::max<uint64_t>(1u << 20, 2 * a[2]);
+            maps[r].trim_at = a[2] + std::max<uint64_t>(1u << 20, a[2]);
             off += 8 * a[2];
         }
         s->each([&](uint32_t r) { return sg_restore(s->sh[r], img[r], il[r]); });
@@ -1050,6 +1063,7 @@ int shd_restore(ShardEngine* s, const void* buf, size_t len) {
 // one document over every shard: keys and event seqs mapped to global ids, keys in id order
 int shd_state_export(ShardEngine* s, void** buf, size_t* len) {
     try {
+        if (s->failed) throw ShardError(SG_ERR_STATE, "a previous call failed part-way: the shards are out of step");
         if (s->pend.n || s->held) throw ShardError(SG_ERR_STATE, "poll the matches first");
         std::vector<SdDoc> docs(s->N);
         s->each([&](uint32_t r) -> int {
@@ -1139,10 +1153,26 @@ int shd_state_import(ShardEngine* s, const void* buf, size_t len) {
     }
 }
 
+// the fan-out reads a device batch first on its source device's split stream: every later split waits for the
+// work queued on `stream` so far (one event per caller stream, recorded again by each call; no host wait)
 int shd_wait_stream(ShardEngine* s, void* stream) {
-    (void)s;
-    (void)stream;
-    return sg_set_error(SG_ERR_UNSUPPORTED, "sg_wait_stream: a multi-device engine stages device batches on the host");
+    try {
+        if (s->N == 1) return sg_wait_stream(s->sh[0], stream);   // (the one shard reads the caller's batch itself)
+        int dev = 0;
+        if (stream) FAN_OK(hipStreamGetDevice((hipStream_t)stream, &dev));
+        else FAN_OK(hipGetDevice(&dev));
+        FAN_OK(hipSetDevice(dev));
+        auto it = s->waits.find(stream);
+        if (it == s->waits.end()) {
+            hipEvent_t x = nullptr;
+            FAN_OK(hipEventCreateWithFlags(&x, hipEventDisableTiming));
+            it = s->waits.emplace(stream, std::make_pair(dev, x)).first;
+        }
+        FAN_OK(hipEventRecord(it->second.second, (hipStream_t)stream));
+        return SG_OK;
+    } catch (const std::exception& ex) {
+        return fail_from(ex);
+    }
 }
 
 sg_engine* shd_first(ShardEngine* s) { return s->sh[0]; }

@@ -453,6 +453,13 @@ class NativeEngine:
         if self._sync is not None:
             self._check(self._sync(self.h))
 
+    def wait_stream(self, stream_handle):
+        """sg_wait_stream: the engine's later work (a fan-out's later device splits) waits for what is queued on
+        the HIP stream `stream_handle` (an int handle, e.g. torch.cuda.Stream().cuda_stream; 0 = legacy default)"""
+        f = getattr(self.lib, self.p + "wait_stream")
+        f.argtypes = [C.c_void_p, C.c_void_p]
+        self._check(f(self.h, C.c_void_p(int(stream_handle) or None)))
+
     def reset_keys(self, keys):
         """Partition purge: the listed keys' NFA state back to never-seen (sg_reset_keys)."""
         f = getattr(self.lib, self.p + "reset_keys")

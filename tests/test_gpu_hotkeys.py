@@ -222,3 +222,25 @@ def test_giant_tiles_switch_to_the_sorted_grouping(monkeypatch):
     assert "per 8-bit digit" in desc and "k_hot_prep" in desc, desc
     for e in (gpu, ora, lane):
         e.close()
+
+
+def test_hot_many_survivors(monkeypatch):
+    """a hot key whose partials only expire (f1 never holds): ~160 live at every batch end, more than one wave of
+    survivors (k_hot_final_big orders them), carried across batches"""
+    monkeypatch.setenv("SG_HOT_MIN", "64")
+    q = ("define stream S (symbol string, price float, volume int);\n"
+         "partition with (symbol of S) begin from every e1=S[price>10] -> e2=S[price>e1.price + 100.0] "
+         "within 200 milliseconds select e1.price as a insert into O; end;")
+    n_keys, n = 4096, 1 << 16
+    cq, gpu, ora, lane = _pair(q, n_keys, n)
+    rng = np.random.default_rng(21)
+    batches = []
+    for b in range(3):
+        d = synth.stock_ticks(b * n, n, n_keys, seed=130 + b, rate_per_ms=16)
+        d["key"][rng.random(n) < 0.05] = 77
+        d["symbol"] = d["key"].copy()
+        batches.append((b * n, d))
+    sg = _run(gpu, ora, lane, batches)
+    assert sg["partials_live"] > 64
+    for e in (gpu, ora, lane):
+        e.close()

@@ -249,3 +249,43 @@ def test_cabi_fanout_seq_map_bounded(shape):
     assert st["host_staged_bytes"] == 0
     assert peak < 4 * B, peak            # bounded by the live span + the trim threshold, not by 100 * 2^20
     assert st["seq_map_entries"] < 4 * B
+
+
+def test_cabi_fanout_wait_stream_orders_the_split():
+    """a device batch written on a side stream (behind a long spin, no host synchronisation) and
+    handed over with sg_wait_stream is split only after the writes: the fan-out's matches equal one engine fed
+    the same batches after a full synchronisation"""
+    import numpy as np
+    from test_gpu_parity import _same
+    synth = importlib.import_module("siddhi-1_amd.synth")
+    app = sa.parse_app(SHAPES["two_state"])
+    cq = sa.compile_query(app, app.queries[0], sa.StringDictionary())
+    K, n = 301, 3000
+    lib = sa.load_hip_library()
+    mk = lambda devs=None: sa.NativeEngine(lib, "sg_", cq.ir, n_keys=K, max_batch=1 << 14, partial_capacity=64,
+                                           match_capacity=1 << 20, devices=devs)
+    one, fan = mk(), mk(_devices())
+    dev = torch.device("cuda", 0)
+    side = torch.cuda.Stream(device=dev)
+    keep = []
+    total = 0
+    for b in range(4):
+        d = synth.stock_ticks(b * n, n, K, seed=120 + b, rate_per_ms=4)
+        host = {k: torch.from_numpy(v.view("int32") if v.dtype.kind == "u" else v).pin_memory() for k, v in d.items()}
+        t = {k: torch.zeros_like(v, device=dev) for k, v in host.items()}
+        torch.cuda.synchronize()
+        with torch.cuda.stream(side):
+            torch.cuda._sleep(20_000_000)   # the writes land well after the push returns
+            for k in t:
+                t[k].copy_(host[k], non_blocking=True)
+        cols = (n, t["ts"].data_ptr(), [t["symbol"].data_ptr(), t["price"].data_ptr(), t["volume"].data_ptr()],
+                t["key"].data_ptr())
+        fan.wait_stream(side.cuda_stream)
+        fan.push(0, b * n, cols, [0, 1, 2], mem=sa.native.SG_MEM_DEVICE)
+        torch.cuda.synchronize()
+        one.push(0, b * n, cols, [0, 1, 2], mem=sa.native.SG_MEM_DEVICE)
+        keep.append((host, t))
+        mo, mf = one.poll(), fan.poll()
+        _same(mo, mf)
+        total += len(mo)
+    assert total > 0
