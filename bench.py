@@ -522,6 +522,98 @@ def _run_general(sa, cq, bats, lastts, n_keys, batch, steps, warmup, cap, playba
             "kernels": kernels}
 
 
+def variant_batches_np(synth, kind, K, B):
+    """numpy batches of a C2 workload variant for the CPU legs (bit-identical to the device generators): batch b of
+    the Zipf stream, or of the random-walk stream (the walk is stateful: stepped from batch 0 when b goes back)"""
+    st = {"walk": None, "next": 0}
+
+    def make(b):
+        if kind == "zipf":
+            return synth.zipf_ticks(b * B, B, K)
+        if st["walk"] is None or b < st["next"]:
+            st["walk"], st["next"] = synth.RandomWalk(K), 0
+        while True:
+            d = synth.stock_ticks(st["next"] * B, B, K)
+            d["price"] = st["walk"].step(d["key"], st["next"] * B)
+            st["next"] += 1
+            if st["next"] > b:
+                return d
+    return make
+
+
+def c2_variant(sa, synth, torch, dev, kind, K, B, steps, warmup, cpu_seconds, no_cpu):
+    """SURVEY §8(d) workload variants of C2 (same query, same engine, same pipelined loop as the headline):
+    `zipf` — partition keys Zipf(s=1.1) over the 2^20 keys (the hottest key ~12 % of every batch; keys far above the
+    batch's mean run go to the hot-key pipeline, which advances all their partials at once instead of one lane
+    walking them), `walk` — per-key random-walk prices (partials live longer, more of them per key: the register
+    window overflows into the HBM pass more often).  HBM-resident batches generated on the device; roofline of the
+    advance (staged pass + hot-key pipeline + HBM pass) over the §8d byte model; the CPU oracle on the same stream."""
+    app = sa.parse_app(synth.C2_QUERY)
+    cq = sa.compile_query(app, app.queries[0], sa.StringDictionary())
+    walk = synth.RandomWalk(K, torch=torch, device=dev) if kind == "walk" else None
+    bats = []
+    for s in range(warmup + steps):
+        if kind == "zipf":
+            d = synth.zipf_ticks_torch(torch, s * B, B, K, dev)
+        else:
+            d = synth.stock_ticks_torch(torch, s * B, B, K, dev)
+            d["price"] = walk.step(d["key"], s * B)
+        bats.append(d)
+    torch.cuda.synchronize()
+    eng = sa.NativeEngine(sa.load_hip_library(), "sg_", cq.ir, n_keys=K, max_batch=B, partial_capacity=256,
+                          match_capacity=2 * B, device=dev.index or 0, flags=sa.native.SG_CFG_TIMING)
+
+    def step(s):
+        t = bats[s]
+        eng.push(0, s * B, (B, t["ts"].data_ptr(), [t["symbol"].data_ptr(), t["price"].data_ptr(),
+                                                    t["volume"].data_ptr()], t["key"].data_ptr()),
+                 [0, 1, 2], mem=sa.native.SG_MEM_DEVICE)
+        take_all(eng, True)
+
+    for s in range(warmup):
+        step(s)
+    eng.synchronize()
+    take_all(eng, False)
+    st0 = eng.stats()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(warmup, warmup + steps):
+        step(s)
+    eng.synchronize()
+    take_all(eng, False)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    d = delta(st0, eng.stats())
+    kernels = eng.describe()
+    eng.close()
+    del bats
+    torch.cuda.empty_cache()
+    launches = max(1, d["advance_launches"])
+    adv_s = d["advance_ns"] / 1e9 / launches
+    alg = algorithmic_bytes(d) / launches
+    gbs = alg / adv_s / 1e9 if adv_s > 0 else 0.0
+    out = {"value": B * steps / el, "unit": "events/s", "ms_per_step": el / steps * 1e3, "keys": K,
+           "batch_events": B, "partial_capacity": 256, "engine": "two-state (C2)",
+           "workload": ("C2 with Zipf(s=1.1) partition keys over 1,048,576 keys (key = bijection of the Zipf rank; the "
+                        "hottest ~12 % of the events)") if kind == "zipf" else
+                       ("C2 with per-key random-walk prices: p <- clamp(p + 0.25 N(0,1), 1, 100) at each of the key's "
+                        "events, initial U[10, 40]"),
+           "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
+                        "traffic": None, "kernel": "k_adv_m + k_hot_* + k_adv_m_h (NFA advance)",
+                        "alg_bytes_per_launch": alg, "kernel_ms_per_launch": adv_s * 1e3,
+                        "hbm_pass_and_hot_ms_per_launch": d["advance_hbm_ns"] / 1e6 / launches},
+           "stages_ms_per_step": {"group": d["group_ns"] / 1e6 / steps, "advance": d["advance_ns"] / 1e6 / steps,
+                                  "order": d["order_ns"] / 1e6 / steps},
+           "work_per_step": {k: d[k] / steps for k in ("matches", "partials_created", "partials_scanned", "keys_touched",
+                                                       "live_at_batch_start", "window_spills", "hot_keys",
+                                                       "hot_events")},
+           "kernels": kernels}
+    if not no_cpu:
+        out["cpu_baseline"] = cpu_general(sa, synth.C2_QUERY, variant_batches_np(synth, kind, K, B), K, B, warmup,
+                                          False, cpu_seconds, "C2_" + kind)
+    return out
+
+
 def take_all(eng, ready):
     """poll + release device matches until none is left (a window that wraps the ring comes in two polls);
     ready=True takes only the batches already complete"""
@@ -1105,6 +1197,11 @@ def main():
         ds = out["other_configs"]["C4_deep_state"]["roofline"]["counters_per_step"]
         out["other_configs"]["C4_deep_state"]["live_per_touched_key_at_batch_start"] = \
             ds["live_at_batch_start"] / max(1.0, ds["keys_touched"])
+    if rank == 0 and world == 1 and not args.no_extra:
+        # SURVEY §8(d) workload variants of the headline config
+        for kind in ("zipf", "walk"):
+            out.setdefault("other_configs", {})["C2_" + kind] = c2_variant(
+                sa, synth, torch, dev, kind, K, B, max(4, args.steps // 8), 3, args.cpu_seconds / 3, args.no_cpu)
     if rank == 0 and world == 1 and not args.no_extra:
         out["pcie_inclusive"] = pcie_inclusive(sa, synth, torch, dev, cq, K, B, 4)
         out["output_inclusive"] = output_inclusive(sa, synth, torch, dev, K, B, 6)

@@ -78,7 +78,8 @@ typedef struct sg_config {
     uint32_t struct_size;      /* sizeof(sg_config) */
     int32_t device;            /* HIP device ordinal */
     uint32_t n_keys;           /* partition key ids are dense in [0, n_keys); 1 when unpartitioned */
-    uint32_t max_batch;        /* max events in one sg_push_batch */
+    uint32_t max_batch;        /* max events in one sg_push_batch (a multi-device engine: of the whole batch,
+                                  host or device, before its split) */
     uint32_t partial_capacity; /* max live partial matches per key */
     uint32_t flags;            /* SG_CFG_* */
     uint64_t match_capacity;   /* max matches held between two polls */
@@ -174,6 +175,10 @@ typedef struct sg_stats {
                                    batches are split on the device: 0) */
     uint64_t seq_map_entries;   /* multi-device engine: local -> global seq map entries it holds (trimmed
                                    below the oldest seq a live partial references after each poll) */
+    uint64_t hot_keys;          /* sum over batches of keys the hot-key pipeline advanced (far more events
+                                   than the batch's mean per key: all their partials at once, not one lane) */
+    uint64_t hot_events;        /* their events */
+    uint64_t seq_map_trims;     /* multi-device engine: seq map trims (each a min-seq scan of the due shards) */
 } sg_stats;
 
 /* ir/ir_len: an IR blob (siddhi_gpu_ir.h) of one query */
@@ -201,7 +206,9 @@ int sg_engine_describe(sg_engine* e, char* out, size_t out_len);
 int sg_synchronize(sg_engine* e);
 /* Device batches produced on another stream (a hipStream_t of the engine's device, NULL = the legacy
  * default stream): the engine's later work waits for everything queued on `stream` so far, without a
- * host synchronisation (the multi-GPU reshard hands its output over this way). */
+ * host synchronisation (the multi-GPU reshard hands its output over this way).  A multi-device engine
+ * (n_devices > 1): every later device-batch split waits for it (the stream may be on any of its devices;
+ * one event per stream, recorded again by each call). */
 int sg_wait_stream(sg_engine* e, void* stream);
 /* Partition purge (@purge(enable, interval, idle.period) on a partition; PartitionRuntimeImpl.java:368-401
  * removes idle keys and cleanGroupByStates() every state holder of the partition's queries, so the

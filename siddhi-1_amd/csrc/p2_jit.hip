@@ -608,20 +608,27 @@ __device__ __forceinline__ void tile_split_glb(const uint32_t* __restrict__ src,
 }
 
 // ---- the kernel ---------------------------------------------------------------------------------
-// a hot key (SG_HOT): at least p.hot_min events in the batch; listed for the hot-key pipeline (while its list has
-// room), its lane then walks nothing
-__device__ __forceinline__ bool list_hot(const P2Params& p, uint32_t k, uint32_t nev) {
+// a hot key (SG_HOT): at least p.hot_min events in the batch, or more live partials than the register window
+// holds (the staged pass would leave it to the HBM pass's slab walk); listed for the hot-key pipeline (while its
+// list has room), its lane then walks nothing
+__device__ __forceinline__ bool list_hot(const P2Params& p, uint32_t k, uint32_t nev, uint32_t h) {
 #if SG_HOT
-    if (p.hot_min != 0u && k < p.n_keys && nev >= p.hot_min) {
-        const uint32_t slot = atomicAdd(p.hot_ctl, 1u);
-        if (slot < p.hot_cap) {
-            p.hot_list[slot] = k;
-            return true;
-        }
+    const uint32_t n0 = SGD_H_INIT(h) ? SGD_H_NPEND(h) + SGD_H_NSTG(h) : 0u;
+    const bool want = p.hot_min != 0u && k < p.n_keys && nev > 0u && (nev >= p.hot_min || n0 >= p.hot_n0);
+    const uint64_t bal = __ballot(want);  // (one atomic per wave that has any)
+    if (bal == 0ull) return false;
+    uint32_t base = 0;
+    if ((threadIdx.x & (SGD_WAVE - 1)) == 0) base = atomicAdd(p.hot_ctl, (uint32_t)__popcll(bal));
+    base = (uint32_t)__shfl((int)base, 0, SGD_WAVE);
+    const uint32_t slot = base + lane_rank(bal);
+    if (want && slot < p.hot_cap) {
+        p.hot_list[slot] = k;
+        return true;
     }
 #endif
     return false;
 }
+
 __device__ __forceinline__ uint32_t wave_min_u(uint32_t x) {
     for (int off = 32; off > 0; off >>= 1) x = min(x, (uint32_t)__shfl_xor((int)x, off, SGD_WAVE));
     return x;
@@ -702,7 +709,7 @@ __device__ __forceinline__ void advance(const P2Params& p, const uint32_t gid) {
             }
             b = blo + kb;
             e = b + kc;
-            hot = list_hot(p, k, e - b);
+            hot = list_hot(p, k, e - b, h);
             if ((tile_glb || p.write_sorted) && k < K) {
                 p.seg_begin[k] = b;
                 p.seg_end[k] = e;
@@ -711,7 +718,7 @@ __device__ __forceinline__ void advance(const P2Params& p, const uint32_t gid) {
         } else {
             __shared__ uint32_t s_lo[NW], s_hi[NW], s_gl[NW], s_gb[NW];
             const uint32_t nv = e - b;
-            hot = list_hot(p, k, nv);
+            hot = list_hot(p, k, nv, h);
             rlo = uni(wave_min_u(nv > 0 ? b : 0xffffffffu));
             const uint32_t hi = uni(wave_max_u(nv > 0 ? e : 0u));
             // the wave's longest hot run: left out of the LDS staging (the range of a workgroup holding a head key
@@ -1269,6 +1276,8 @@ __device__ __forceinline__ void advance(const P2Params& p, const uint32_t gid) {
         w[SGD_ST_KEYS] = v3;
         w[SGD_ST_LIVE0] = v4;
         w[SGD_ST_SPILLS] = v5;
+        w[SGD_ST_HOTK] = 0;  // (the hot-key pipeline counts its keys into p.stats)
+        w[SGD_ST_HOTE] = 0;
     }
     if (!STG && lane == 0) {
         if (v0) atomicAdd(&p.stats[SGD_ST_SCANNED], v0);
@@ -1363,7 +1372,7 @@ extern "C" __global__ void __launch_bounds__(256) k_pack1(const PackParams q) { 
 namespace {
 constexpr uint32_t HOT_NOTP = 0xfffffffeu;  // death word of a run event that made no partial
 constexpr uint32_t HOT_LIVE = 0xffffffffu;  // no event of the run ends the partial (or not found yet)
-enum { HI_B = 0, HI_M, HI_EXOFF, HI_EVOFF, HI_N0, HI_BAD, HI_ALIVE, HI_KEY, HI_BLKOFF };
+enum { HI_B = 0, HI_M, HI_EXOFF, HI_EVOFF, HI_N0, HI_BAD, HI_ALIVE, HI_KEY, HI_BLKOFF, HI_ALOFF };
 enum { HC_N = 0, HC_EX, HC_EV, HC_L0, HC_L1, HC_MAXM, HC_BIG, HC_NBLK };
 constexpr int HST = SGQ_STRIDE0;
 
@@ -1444,7 +1453,7 @@ __device__ __forceinline__ uint32_t hot_wave_scan(const P2Params& p, const HotPa
     }
     return HOT_LIVE;
 }
-__device__ __forceinline__ uint32_t hot_wl_cap(const P2Params& p) { return p.max_batch + p.hot_cap * p.cap; }
+__device__ __forceinline__ uint32_t hot_wl_cap(const P2Params& p) { return p.max_batch + p.hot_exmax; }
 __device__ __forceinline__ uint32_t* hot_list_buf(const P2Params& p, uint32_t which) {
     return p.hot_wl + 3u * (size_t)hot_wl_cap(p) * which;
 }
@@ -1465,12 +1474,10 @@ __device__ __forceinline__ uint32_t hot_block_scan(uint32_t v, uint32_t* s_w, ui
 }
 }  // namespace
 
-// per hot key: its run, its state and the conditions; then the offsets of the carried-in partials and of the
-// runs in the flat index space (one workgroup)
-extern "C" __global__ void __launch_bounds__(1024) k_hot_prep(const P2Params p) {
-    uint32_t* ctl = p.hot_ctl;
-    const uint32_t n = min(ctl[HC_N], p.hot_cap);
-    for (uint32_t h = threadIdx.x; h < n; h += blockDim.x) {
+// per hot key (a thread each): its run, its state and the conditions
+extern "C" __global__ void __launch_bounds__(256) k_hot_prep(const P2Params p) {
+    const uint32_t n = min(p.hot_ctl[HC_N], p.hot_cap);
+    for (uint32_t h = blockIdx.x * blockDim.x + threadIdx.x; h < n; h += gridDim.x * blockDim.x) {
         const uint32_t k = p.hot_list[h];
         uint32_t* hi = p.hot_info + (size_t)h * SGD_HOT_INFO;
         const uint32_t b = p.seg_begin[k], m = p.seg_end[k] - b;
@@ -1486,46 +1493,68 @@ extern "C" __global__ void __launch_bounds__(1024) k_hot_prep(const P2Params p) 
         hi[HI_ALIVE] = 0u;
         hi[HI_KEY] = k;
     }
-    __syncthreads();
-    // exclusive scans of (carried-in count, run length, fill blocks): each thread a contiguous span of keys
-    __shared__ uint32_t s_x[16], s_e[16], s_m[16], s_b[16];
+}
+
+// the offsets of the hot keys' carried-in partials, run events, fill blocks and survivor regions in their index
+// spaces (exclusive scans, one workgroup: each thread a contiguous span of keys).  Keys whose carried-in partials
+// would pass the space's end (p.hot_exmax) are given back and the scans run again.
+__device__ __forceinline__ void hot_scan_pass(const P2Params& p, uint32_t n, bool last) {
+    __shared__ uint32_t s_x[16], s_e[16], s_m[16], s_b[16], s_a[16];
     const uint32_t lane = threadIdx.x & (SGD_WAVE - 1), w = threadIdx.x / SGD_WAVE;
     const uint32_t per = (n + blockDim.x - 1u) / blockDim.x;
     const uint32_t lo = min(n, threadIdx.x * per), hi_ = min(n, lo + per);
-    uint32_t sx = 0, se = 0, mm = 0, sb = 0;
+    uint32_t sx = 0, se = 0, mm = 0, sb = 0, sa = 0;
     for (uint32_t h = lo; h < hi_; ++h) {
-        sx += p.hot_info[(size_t)h * SGD_HOT_INFO + HI_N0];
-        const uint32_t m = p.hot_info[(size_t)h * SGD_HOT_INFO + HI_M];
+        const uint32_t* hi = p.hot_info + (size_t)h * SGD_HOT_INFO;
+        const uint32_t n0 = hi[HI_N0], m = hi[HI_M];
+        sx += n0;
         se += m;
         sb += (m + SGD_HOT_FILL - 1u) / SGD_HOT_FILL;
+        sa += min(p.cap, n0 + m);
         mm = max(mm, m);
     }
     const uint32_t ix = wave_incl_scan(sx, (int)lane), ie = wave_incl_scan(se, (int)lane);
-    const uint32_t ib = wave_incl_scan(sb, (int)lane);
+    const uint32_t ib = wave_incl_scan(sb, (int)lane), ia = wave_incl_scan(sa, (int)lane);
     mm = wave_max_u(mm);
-    if (lane == SGD_WAVE - 1) { s_x[w] = ix; s_e[w] = ie; s_m[w] = mm; s_b[w] = ib; }
+    if (lane == SGD_WAVE - 1) { s_x[w] = ix; s_e[w] = ie; s_m[w] = mm; s_b[w] = ib; s_a[w] = ia; }
     __syncthreads();
-    uint32_t ox = ix - sx, oe = ie - se, ob = ib - sb;
-    for (uint32_t u = 0; u < w; ++u) { ox += s_x[u]; oe += s_e[u]; ob += s_b[u]; }
+    uint32_t ox = ix - sx, oe = ie - se, ob = ib - sb, oa = ia - sa;
+    for (uint32_t u = 0; u < w; ++u) { ox += s_x[u]; oe += s_e[u]; ob += s_b[u]; oa += s_a[u]; }
     for (uint32_t h = lo; h < hi_; ++h) {
         uint32_t* hi = p.hot_info + (size_t)h * SGD_HOT_INFO;
+        const uint32_t n0 = hi[HI_N0], m = hi[HI_M];
+        if (!last && n0 && ox + n0 > p.hot_exmax) {  // (given back: the HBM pass walks it)
+            hi[HI_BAD] = 1u;
+            hi[HI_N0] = 0u;
+            hi[HI_M] = 0u;
+            continue;
+        }
         hi[HI_EXOFF] = ox;
         hi[HI_EVOFF] = oe;
         hi[HI_BLKOFF] = ob;
-        ox += hi[HI_N0];
-        oe += hi[HI_M];
-        ob += (hi[HI_M] + SGD_HOT_FILL - 1u) / SGD_HOT_FILL;
+        hi[HI_ALOFF] = oa;
+        ox += n0;
+        oe += m;
+        ob += (m + SGD_HOT_FILL - 1u) / SGD_HOT_FILL;
+        oa += min(p.cap, n0 + m);
     }
     if (threadIdx.x == 0) {
         uint32_t tx = 0, te = 0, tm = 0, tb = 0;
         for (uint32_t u = 0; u < blockDim.x / SGD_WAVE; ++u) { tx += s_x[u]; te += s_e[u]; tm = max(tm, s_m[u]); tb += s_b[u]; }
+        uint32_t* ctl = p.hot_ctl;
         ctl[HC_EX] = tx;
         ctl[HC_EV] = te;
         ctl[HC_NBLK] = tb;
+        ctl[HC_MAXM] = tm;
         ctl[HC_L0] = 0u;
         ctl[HC_L1] = 0u;
-        ctl[HC_MAXM] = tm;
     }
+    __syncthreads();
+}
+extern "C" __global__ void __launch_bounds__(1024) k_hot_scan(const P2Params p) {
+    const uint32_t n = min(p.hot_ctl[HC_N], p.hot_cap);
+    hot_scan_pass(p, n, false);
+    if (p.hot_ctl[HC_EX] > p.hot_exmax) hot_scan_pass(p, n, true);  // (uniform: after the pass's barrier)
 }
 
 // the hot key of every run event (hot_fh): a workgroup per SGD_HOT_FILL events of one run (every thread finds
@@ -1785,7 +1814,7 @@ extern "C" __global__ void __launch_bounds__(256) k_hot_emit(const P2Params p) {
         if (d == HOT_LIVE) {  // scanned by every later event of the run; a survivor
             sc += (unsigned long long)((int64_t)m - 1 - start);
             const uint32_t a = atomicAdd(&hi[HI_ALIVE], 1u);
-            if (a < p.cap) p.hot_alive[(size_t)h * p.cap + a] = x;
+            if (a < min(p.cap, hi[HI_N0] + m)) p.hot_alive[hi[HI_ALOFF] + a] = x;
         } else {  // scanned up to its end; the expiring event removes it before its scan
             const uint32_t i = d >> 1;
             sc += (unsigned long long)((int64_t)i - start - 1 + (int64_t)(d & 1u));
@@ -1985,6 +2014,8 @@ __device__ __forceinline__ void hot_close(const P2Params& p, const uint32_t* hi,
     const uint32_t gns = lastf0 ? 1u : 0u;
     p.hdr[k] = SGD_H_MAKE(na - gns, gns, lastf0 ? 0u : 1u, lastf0 ? 1u : 0u, 1u);
     p.resume[k] = SGD_HOT_DONE;
+    atomicAdd(&p.stats[SGD_ST_HOTK], 1ull);
+    atomicAdd(&p.stats[SGD_ST_HOTE], (unsigned long long)hi[HI_M]);
 }
 __device__ __forceinline__ void hot_store(const P2Params& p, const Slab& G, uint32_t o, const HotPart& P) {
     G.TS(o) = P.ts;
@@ -1994,14 +2025,17 @@ __device__ __forceinline__ void hot_store(const P2Params& p, const Slab& G, uint
     if (SGQ_CAPNULL) G.NUL(o) = P.cn;
 }
 
-// a wave per hot key with at most 64 survivors: the survivors in list order (= flat order) to the key's slab (a
-// lane each: every lane reads its partial before any writes), the header, the resume word
+// a wave per hot key with at most SGD_HOT_FW survivors: ranked by flat index (= list order) in the wave's LDS, then
+// moved to the key's slab 64 at a time in rank order (survivor o comes from list index >= o, so a round's writes
+// land below every later round's reads), the header, the resume word
+#define SGD_HOT_FW 256u
 extern "C" __global__ void __launch_bounds__(256) k_hot_final(const P2Params p) {
     const uint32_t n = min(p.hot_ctl[HC_N], p.hot_cap), nex = p.hot_ctl[HC_EX];
     const int64_t obase = p.ts_col[0];
-    const uint32_t lane = threadIdx.x & (SGD_WAVE - 1);
+    const uint32_t lane = threadIdx.x & (SGD_WAVE - 1), wv = threadIdx.x / SGD_WAVE;
     const uint32_t nw = gridDim.x * (blockDim.x / SGD_WAVE);
-    for (uint32_t h = blockIdx.x * (blockDim.x / SGD_WAVE) + threadIdx.x / SGD_WAVE; h < n; h += nw) {
+    __shared__ uint32_t s_in[4][SGD_HOT_FW], s_ord[4][SGD_HOT_FW];
+    for (uint32_t h = blockIdx.x * (blockDim.x / SGD_WAVE) + wv; h < n; h += nw) {
         const uint32_t* hi = p.hot_info + (size_t)h * SGD_HOT_INFO;
         if (uni(hi[HI_BAD])) continue;  // left to the HBM pass
         const uint32_t na = uni(hi[HI_ALIVE]);
@@ -2012,20 +2046,36 @@ extern "C" __global__ void __launch_bounds__(256) k_hot_final(const P2Params p) 
             }
             continue;
         }
-        if (na > SGD_WAVE) continue;  // (k_hot_final_big)
-        const bool in = lane < na;
-        const uint32_t x = in ? p.hot_alive[(size_t)h * p.cap + lane] : 0xffffffffu;
-        uint32_t r = 0;
-        for (uint32_t u = 0; u < na; ++u) r += (uint32_t)__shfl((int)x, (int)u, SGD_WAVE) < x ? 1u : 0u;
-        HotPart P;
-        int start;
-        if (in) P = hot_part(p, x, nex, hi, obase, start);
-        if (in) hot_store(p, hot_slab(p, hi[HI_KEY]), r, P);
+        if (na > SGD_HOT_FW) continue;  // (k_hot_final_big)
+        const uint32_t* pool = p.hot_alive + hi[HI_ALOFF];
+        for (uint32_t a = lane; a < na; a += SGD_WAVE) s_in[wv][a] = pool[a];
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t a = lane; a < na; a += SGD_WAVE) {
+            const uint32_t xa = s_in[wv][a];
+            uint32_t r = 0;
+            for (uint32_t u = 0; u < na; ++u) r += s_in[wv][u] < xa ? 1u : 0u;
+            s_ord[wv][r] = xa;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        const Slab G = hot_slab(p, hi[HI_KEY]);
+        for (uint32_t c0 = 0; c0 < na; c0 += SGD_WAVE) {
+            const uint32_t o = c0 + lane;
+            HotPart P;
+            int start;
+            if (o < na) P = hot_part(p, s_ord[wv][o], nex, hi, obase, start);
+            __builtin_amdgcn_s_waitcnt(0);  // (every lane's read of the round before any write)
+            __builtin_amdgcn_wave_barrier();
+            if (o < na) hot_store(p, G, o, P);
+        }
         if (lane == 0) hot_close(p, hi, nex, na);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
     }
 }
 
-// a workgroup per hot key with more than 64 survivors (rare): ranked in LDS, moved 256 at a time in order
+// a workgroup per hot key with more than SGD_HOT_FW survivors (rare): ranked in LDS, moved 256 at a time in order
 extern "C" __global__ void __launch_bounds__(256) k_hot_final_big(const P2Params p) {
     const uint32_t n = min(p.hot_ctl[HC_N], p.hot_cap), nex = p.hot_ctl[HC_EX];
     const int64_t obase = p.ts_col[0];
@@ -2033,8 +2083,8 @@ extern "C" __global__ void __launch_bounds__(256) k_hot_final_big(const P2Params
     for (uint32_t h = blockIdx.x; h < n; h += gridDim.x) {
         const uint32_t* hi = p.hot_info + (size_t)h * SGD_HOT_INFO;
         const uint32_t na = hi[HI_ALIVE];
-        if (hi[HI_BAD] || na <= SGD_WAVE || na > p.cap) continue;  // (uniform)
-        for (uint32_t a = threadIdx.x; a < na; a += blockDim.x) s_x[a] = p.hot_alive[(size_t)h * p.cap + a];
+        if (hi[HI_BAD] || na <= SGD_HOT_FW || na > p.cap) continue;  // (uniform)
+        for (uint32_t a = threadIdx.x; a < na; a += blockDim.x) s_x[a] = p.hot_alive[hi[HI_ALOFF] + a];
         __syncthreads();
         for (uint32_t a = threadIdx.x; a < na; a += blockDim.x) {  // rank by flat index (distinct)
             uint32_t r = 0;

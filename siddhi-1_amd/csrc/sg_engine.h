@@ -84,7 +84,8 @@ enum {
 #define SGD_BIG_TILE 65536u
 #define SGD_HOT_INFO 16
 
-enum { SGD_ST_SCANNED = 0, SGD_ST_CREATED, SGD_ST_MATCHES, SGD_ST_KEYS, SGD_ST_LIVE0, SGD_ST_SPILLS, SGD_ST_N };
+enum { SGD_ST_SCANNED = 0, SGD_ST_CREATED, SGD_ST_MATCHES, SGD_ST_KEYS, SGD_ST_LIVE0, SGD_ST_SPILLS, SGD_ST_HOTK,
+       SGD_ST_HOTE, SGD_ST_N };
 
 enum { SGD_ERR_PARTIAL_CAP = 1, SGD_ERR_MATCH_CAP = 2, SGD_ERR_KEY_RANGE = 4, SGD_ERR_PROJ = 8 };
 
@@ -139,8 +140,9 @@ struct P2Params {
     uint32_t* raw_capnull;             // SGQ_PROJ: [raw_capacity] their null bits
     uint32_t stage_chunks;             // LDS staging per wave, 16-B chunks (dynamic LDS = waves x this)
     // hot keys (`every e1 -> e2` on one stream; p2_jit.hip k_hot_*): the staged pass leaves a key with at least
-    // hot_min events in the batch to the hot-key pipeline, which advances all of its partials at once (a
-    // partial's fate is the first later event that expires or matches it); 0 = off
+    // hot_min events in the batch, or more live partials than its register window, to the hot-key pipeline,
+    // which advances all of its partials at once (a partial's fate is the first later event that expires or
+    // matches it); 0 = off
     uint32_t hot_min;
     uint32_t hot_cap;                  // hot_list entries (further hot keys are walked by their lanes)
     uint32_t max_batch;                // (sizes the flat index space: <= max_batch events + hot_cap * cap carried in)
@@ -153,9 +155,11 @@ struct P2Params {
     uint32_t* hot_tcnt;                // [max_batch] matches per trigger (by flat event index)
     uint32_t* hot_tbase;               // [max_batch] their first raw slot
     uint32_t* hot_fbi;                 // [max_batch] the batch position of each flat event
-    uint32_t* hot_alive;               // [hot_cap][cap] the survivors' flat indices
+    uint32_t* hot_alive;               // [flat] the survivors' flat indices, a region of min(cap, n0 + m) per key
     uint32_t* hot_fh;                  // [flat] the hot key of each flat index (round 0)
     uint32_t hot_round;                // the search round a k_hot_rn / k_hot_rc launch runs
+    uint32_t hot_exmax;                // flat indices for carried-in partials (keys past it are given back)
+    uint32_t hot_n0;                   // a key carrying in at least this many live partials is hot too
     uint64_t cst[SGD_MAX_CONST];       // filter constants, already in their comparison domain
 };
 

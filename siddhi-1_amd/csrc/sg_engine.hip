@@ -135,7 +135,7 @@ struct sg_engine {
         hipFunction_t adv[2] = {nullptr, nullptr};   // [0]: multi / state-0 stream, [1]: state-1 stream
         hipFunction_t adv_h[2] = {nullptr, nullptr}; // the HBM pass over the waves the staged pass deferred
         hipFunction_t pack[2] = {nullptr, nullptr};
-        hipFunction_t hot[13] = {};                  // the hot-key pipeline (k_hot_prep .. k_hot_final_big)
+        hipFunction_t hot[14] = {};                  // the hot-key pipeline (k_hot_prep .. k_hot_final_big)
         uint32_t adv_static_lds = 0;                 // the staged pass's static LDS (beside its dynamic staging)
     };
     JitQuery jq;
@@ -196,7 +196,8 @@ struct sg_engine {
     bool hot_ok = false;
     bool hot_on = true;
     bool skewed = false;           // recent batches had workgroup ranges > SGD_BIG_TILE events: sorted grouping
-    uint32_t hot_min = 0, hot_cap = 0;
+    uint32_t hot_min = 0, hot_cap = 0, hot_exmax = 0;
+    uint32_t hot_n0 = 0;           // carried-in live partials that make a key hot (0: the register window + 1)
     uint64_t hot_factor = 4;       // "hot": also >= hot_factor x the batch's mean events per key (SG_HOT_FACTOR)
     uint32_t *hot_ctl = nullptr, *hot_list = nullptr, *hot_info = nullptr, *hot_death = nullptr, *hot_wl = nullptr;
     uint32_t *hot_tcnt = nullptr, *hot_tbase = nullptr, *hot_alive = nullptr, *hot_fh = nullptr, *hot_fbi = nullptr, *hot_cur = nullptr;
@@ -572,18 +573,22 @@ void allocate(sg_engine* e) {
         const char* x = getenv("SG_HOT_MIN");  // 0: off
         e->hot_min = x ? (uint32_t)strtoul(x, nullptr, 0) : 64u;
         if (const char* f = getenv("SG_HOT_FACTOR")) e->hot_factor = std::max(1ul, strtoul(f, nullptr, 0));
+        if (const char* f = getenv("SG_HOT_N0")) e->hot_n0 = (uint32_t)strtoul(f, nullptr, 0);
         if (e->hot_min == 0) e->hot_ok = false;
     }
     if (e->hot_ok) {
-        e->hot_cap = (uint32_t)std::min<size_t>({B / std::max(1u, e->hot_min) + 1, K, 65536, std::max<size_t>(1, (1u << 22) / C)});
-        const size_t slots = B + (size_t)e->hot_cap * C;
+        // hot keys: up to every key (those with more live partials than the window are hot too); their carried-in
+        // partials get up to hot_exmax flat indices (further keys are given back to the HBM pass)
+        e->hot_cap = (uint32_t)std::min<size_t>(K, 1u << 20);
+        e->hot_exmax = (uint32_t)std::min<size_t>((size_t)K * C, std::max<size_t>(1u << 22, 2 * B));
+        const size_t slots = B + (size_t)e->hot_exmax;
         e->hot_list = dalloc<uint32_t>(e->hot_cap, o);
         e->hot_info = dalloc<uint32_t>((size_t)e->hot_cap * SGD_HOT_INFO, o);
         e->hot_death = dalloc<uint32_t>(slots, o);
         e->hot_wl = dalloc<uint32_t>(2 * 3 * slots, o);
         e->hot_tcnt = dalloc<uint32_t>(B, o);
         e->hot_tbase = dalloc<uint32_t>(B, o);
-        e->hot_alive = dalloc<uint32_t>((size_t)e->hot_cap * C, o);
+        e->hot_alive = dalloc<uint32_t>(slots, o);
         e->hot_fh = dalloc<uint32_t>(slots, o);
         e->hot_cur = dalloc<uint32_t>(slots, o);
         e->hot_fbi = dalloc<uint32_t>(B, o);
@@ -657,11 +662,11 @@ sg_engine::Variant& variant(sg_engine* e, bool evnull, bool capnull) {
         HIP_OK(hipModuleGetFunction(&r.adv_h[1], r.mod, "k_adv_s1_h"));
     }
     if (e->hot_ok) {
-        static const char* const names[13] = {"k_hot_prep",  "k_hot_fill", "k_hot_r0",    "k_hot_r1",
-                                              "k_hot_r1c",   "k_hot_rn",   "k_hot_rc",    "k_hot_emit",
-                                              "k_hot_trig",  "k_hot_place", "k_hot_sort", "k_hot_final",
-                                              "k_hot_final_big"};
-        for (int i = 0; i < 13; i++) HIP_OK(hipModuleGetFunction(&r.hot[i], r.mod, names[i]));
+        static const char* const names[14] = {"k_hot_prep",  "k_hot_scan",  "k_hot_fill", "k_hot_r0",
+                                              "k_hot_r1",    "k_hot_r1c",   "k_hot_rn",   "k_hot_rc",
+                                              "k_hot_emit",  "k_hot_trig",  "k_hot_place", "k_hot_sort",
+                                              "k_hot_final", "k_hot_final_big"};
+        for (int i = 0; i < 14; i++) HIP_OK(hipModuleGetFunction(&r.hot[i], r.mod, names[i]));
     }
     {
         int sh = 0;
@@ -953,6 +958,8 @@ int push(sg_engine* e, const sg_batch* b) {
         p.hot_min = pl.partitioned ? std::max<uint32_t>(e->hot_min, (uint32_t)std::min<uint64_t>(e->hot_factor * n / e->K, 1u << 30))
                                    : e->hot_min;
         p.hot_cap = e->hot_cap;
+        p.hot_exmax = e->hot_exmax;
+        p.hot_n0 = e->hot_n0 ? e->hot_n0 : e->reg_slots + 1;
         p.max_batch = (uint32_t)e->maxb;
         p.hot_list = e->hot_list;
         p.hot_info = e->hot_info;
@@ -977,22 +984,23 @@ int push(sg_engine* e, const sg_batch* b) {
                p.stage_chunks * 16u * (SGD_BLOCK / SGD_WAVE) + (fused ? SGD_SPLIT_CNT_BYTES : 0u));
         if (e->timing) { a1 = e->ev(); e->mark(a1); e->spans.push_back({a0, a1, 1}); a0 = e->ev(); e->mark(a0); }
         if (e->hot_ok && e->hot_on) {  // the hot keys the staged pass listed (fixed grids: the counts are on the device)
-            launch(v.hot[0], 1, 1024, &p, e->stream);    // k_hot_prep
-            launch(v.hot[1], 1024, 256, &p, e->stream);  // k_hot_fill
-            launch(v.hot[2], 2048, 256, &p, e->stream);  // k_hot_r0
-            launch(v.hot[3], 1024, 256, &p, e->stream);  // k_hot_r1
+            launch(v.hot[0], 512, 256, &p, e->stream);   // k_hot_prep
+            launch(v.hot[1], 1, 1024, &p, e->stream);    // k_hot_scan
+            launch(v.hot[2], 1024, 256, &p, e->stream);  // k_hot_fill
+            launch(v.hot[3], 2048, 256, &p, e->stream);  // k_hot_r0
+            launch(v.hot[4], 1024, 256, &p, e->stream);  // k_hot_r1
             uint64_t covered = 128 + 512;
-            if (covered < e->maxb) launch(v.hot[4], 512, 256, &p, e->stream);  // k_hot_r1c
+            if (covered < e->maxb) launch(v.hot[5], 512, 256, &p, e->stream);  // k_hot_r1c
             // rounds 2.. until the spans scanned cover the longest possible run (round r: 512 << 3 (r - 1) events)
             for (uint32_t r = 2; covered < e->maxb; r++) {
                 p.hot_round = r;
                 covered += 512ull << (3 * (r - 1));
-                launch(v.hot[5], 1024, 256, &p, e->stream);  // k_hot_rn
-                if (covered < e->maxb) launch(v.hot[6], 256, 256, &p, e->stream);  // k_hot_rc
+                launch(v.hot[6], 1024, 256, &p, e->stream);  // k_hot_rn
+                if (covered < e->maxb) launch(v.hot[7], 256, 256, &p, e->stream);  // k_hot_rc
             }
-            for (int i = 7; i < 11; i++) launch(v.hot[i], 1024, 256, &p, e->stream);  // emit, trig, place, sort
-            launch(v.hot[11], 512, 256, &p, e->stream);  // k_hot_final
-            launch(v.hot[12], 64, 256, &p, e->stream);   // k_hot_final_big
+            for (int i = 8; i < 12; i++) launch(v.hot[i], 1024, 256, &p, e->stream);  // emit, trig, place, sort
+            launch(v.hot[12], 1024, 256, &p, e->stream);  // k_hot_final
+            launch(v.hot[13], 64, 256, &p, e->stream);    // k_hot_final_big
             e->hot_batches++;
         }
         // one wave per work-group over the listed waves (a fixed grid: the list's length is on the device)
@@ -1697,6 +1705,8 @@ int sg_get_stats(sg_engine* e, sg_stats* out) {
         out->keys_touched = s[SGD_ST_KEYS];
         out->live_at_batch_start = s[SGD_ST_LIVE0];
         out->window_spills = s[SGD_ST_SPILLS];
+        out->hot_keys = s[SGD_ST_HOTK];
+        out->hot_events = s[SGD_ST_HOTE];
         // live partials now: sum of the headers' counts (host reduction; diagnostics only)
         std::vector<uint32_t> h(e->K);
         HIP_OK(hipMemcpy(h.data(), e->hdr, (size_t)e->K * 4, hipMemcpyDeviceToHost));

@@ -956,6 +956,7 @@ int shd_stats(ShardEngine* s, sg_stats* out) {
         out->host_staged_bytes = s->staged_bytes;
         out->seq_map_entries = 0;
         for (const SeqMap& m : s->gmap) out->seq_map_entries += m.v.size();
+        out->seq_map_trims = s->trims;
         return SG_OK;
     } catch (const std::exception& ex) {
         return fail_from(ex);
