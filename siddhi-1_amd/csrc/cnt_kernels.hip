@@ -501,6 +501,162 @@ template <int NW> struct CntKey {
     }
 };
 
+// ---- the fused grouping: a workgroup per 64-key tile splits it by key ----
+// (gen_host.hip groups the batch by tile = key >> 6 only, two 7-bit passes instead of three 8-bit ones; this kernel
+// then splits each tile by key into the key-sorted payload, one read and one write of the tile instead of a third
+// radix pass with its histogram and scan; PartitionStreamReceiver.java:175-260's per-key runs in arrival order are
+// what the split builds.  Splitting inside k_cnt_batch instead (the tile in LDS) was measured: the split's code in
+// the walk kernel costs it 1.1 KB of scratch per lane at its 128-VGPR cap, 10x slower.)
+__device__ __forceinline__ uint32_t cnt_rank(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+__device__ __forceinline__ uint64_t cnt_match6(uint32_t v, uint64_t act) {  // lanes holding the same 6-bit value
+    uint64_t m = act;
+#pragma unroll
+    for (int b = 0; b < 6; ++b) {
+        const bool x = (v >> b) & 1u;
+        const uint64_t bb = __ballot(x);
+        m &= x ? bb : ~bb;
+    }
+    return m;
+}
+__device__ __forceinline__ uint32_t cnt_excl_scan(uint32_t x) {
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t v = x;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t t = (uint32_t)__shfl_up((int)v, off, 64);
+        if (lane >= (uint32_t)off) v += t;
+    }
+    return v - x;
+}
+constexpr uint32_t CNT_MAXST = 6;  // payload words per element (W <= 4, + position and ts offset)
+
+// One wave per 64-key tile (tile = blockIdx.x, lane = key & 63): the tile's elements (arrival order, key & 255 tagged
+// in the position's top byte) counted per key, then placed into the key-sorted payload at the tile's range (arrival
+// order within a key, the tag cleared), with every key's [begin, end).
+// A tile of at most 64 * CNT_SPLIT_R events (the usual case) is loaded into registers at once, so the split waits for
+// memory once; larger tiles are read twice in 64-event rounds.
+constexpr uint32_t CNT_SPLIT_R = 8;
+#define CNT_WSYNC() do { __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront"); __builtin_amdgcn_wave_barrier(); } while (0)
+extern "C" __global__ void __launch_bounds__(256) k_cnt_split(const GenArgs a) {
+    // four tiles per workgroup, a wave each (waves sync among themselves only: LDS ops of one wave run in order)
+    __shared__ uint32_t s_cnt[4][64];
+    __shared__ uint32_t s_el[4][64 * CNT_SPLIT_R * 4];  // a small tile's elements, key-sorted (<= 4 words each)
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const uint32_t tile = blockIdx.x * 4u + w;
+    const uint32_t ntiles = (a.K + 63u) / 64u;
+    if (tile >= ntiles) return;
+    uint32_t* cnt = s_cnt[w];
+    const uint32_t key = tile * 64u + lane;
+    const uint32_t st = a.b.payStride;
+    const uint32_t lo = gp(a.b.tile_lo)[tile], nt = gp(a.b.tile_lo)[tile + 1] - lo;
+    const gu32* src = gp(a.b.tpay) + (size_t)lo * st;
+    gu32* dst = (gu32*)gp(a.b.pay) + (size_t)lo * st;
+    cnt[lane] = 0u;
+    // the host's skew check: only tiles past its threshold report (one device-wide counter hit by every workgroup
+    // serialises at the memory side: 16K atomics cost ~0.2 ms)
+    if (lane == 0 && nt > (1u << 14) && a.b.tileMax) atomicMax((uint32_t*)gp(a.b.tileMax), nt);
+    CNT_WSYNC();
+    uint32_t c = 0, kb = 0;
+    if (nt <= 64u * CNT_SPLIT_R) {
+        uint32_t el[CNT_SPLIT_R][CNT_MAXST];
+#pragma unroll
+        for (uint32_t r = 0; r < CNT_SPLIT_R; ++r) {
+            const uint32_t j = r * 64u + lane;
+#pragma unroll
+            for (uint32_t u = 0; u < CNT_MAXST; ++u) el[r][u] = (j < nt && u < st) ? src[(size_t)j * st + u] : 0u;
+        }
+        uint64_t mm[CNT_SPLIT_R];
+#pragma unroll
+        for (uint32_t r = 0; r < CNT_SPLIT_R; ++r) {  // (one wave: LDS ops in program order)
+            mm[r] = 0;
+            if (r * 64u < nt) {
+                const bool v = r * 64u + lane < nt;
+                const uint32_t kl = (el[r][0] >> 24) & 63u;
+                mm[r] = cnt_match6(kl, __ballot(v));
+                if (v && cnt_rank(mm[r]) == 0u) cnt[kl] += (uint32_t)__popcll(mm[r]);
+                CNT_WSYNC();
+            }
+        }
+        c = cnt[lane];
+        kb = cnt_excl_scan(c);
+        CNT_WSYNC();
+        cnt[lane] = kb;
+        CNT_WSYNC();
+#pragma unroll
+        for (uint32_t r = 0; r < CNT_SPLIT_R; ++r) {
+            if (r * 64u < nt) {
+                const bool v = r * 64u + lane < nt;
+                const uint32_t kl = (el[r][0] >> 24) & 63u;
+                uint32_t pos = 0;
+                if (v) {
+                    const uint32_t rk = cnt_rank(mm[r]), base = cnt[kl];
+                    pos = base + rk;
+                    if (rk == 0u) cnt[kl] = base + (uint32_t)__popcll(mm[r]);
+                }
+                CNT_WSYNC();
+                if (v) {
+                    el[r][0] &= 0xffffffu;
+                    if (st <= 4u) {  // placed in LDS, written out contiguously below
+#pragma unroll
+                        for (uint32_t u = 0; u < 4u; ++u)
+                            if (u < st) s_el[w][pos * st + u] = el[r][u];
+                    } else {
+#pragma unroll
+                        for (uint32_t u = 0; u < CNT_MAXST; ++u)
+                            if (u < st) dst[(size_t)pos * st + u] = el[r][u];
+                    }
+                }
+            }
+        }
+        if (st <= 4u) {  // the key-sorted tile, coalesced
+            CNT_WSYNC();
+            for (uint32_t x = lane; x < nt * st; x += 64u) dst[x] = s_el[w][x];
+        }
+    } else {
+        for (uint32_t r0 = 0; r0 < nt; r0 += 64u) {
+            const uint32_t j = r0 + lane;
+            const bool v = j < nt;
+            const uint32_t kl = v ? (src[(size_t)j * st] >> 24) & 63u : 0u;
+            const uint64_t m = cnt_match6(kl, __ballot(v));
+            if (v && cnt_rank(m) == 0u) cnt[kl] += (uint32_t)__popcll(m);
+            CNT_WSYNC();
+        }
+        c = cnt[lane];
+        kb = cnt_excl_scan(c);
+        CNT_WSYNC();
+        cnt[lane] = kb;
+        CNT_WSYNC();
+        for (uint32_t r0 = 0; r0 < nt; r0 += 64u) {
+            const uint32_t j = r0 + lane;
+            const bool v = j < nt;
+            uint32_t el[CNT_MAXST];
+#pragma unroll
+            for (uint32_t u = 0; u < CNT_MAXST; ++u) el[u] = (v && u < st) ? src[(size_t)j * st + u] : 0u;
+            const uint32_t kl = (el[0] >> 24) & 63u;
+            const uint64_t m = cnt_match6(kl, __ballot(v));
+            uint32_t pos = 0;
+            if (v) {
+                const uint32_t rk = cnt_rank(m), base = cnt[kl];
+                pos = base + rk;
+                if (rk == 0u) cnt[kl] = base + (uint32_t)__popcll(m);
+            }
+            CNT_WSYNC();
+            if (v) {
+                el[0] &= 0xffffffu;
+#pragma unroll
+                for (uint32_t u = 0; u < CNT_MAXST; ++u)
+                    if (u < st) dst[(size_t)pos * st + u] = el[u];
+            }
+        }
+    }
+    if (key < a.K) {
+        ((gu32*)gp(a.b.seg_begin))[key] = lo + kb;
+        ((gu32*)gp(a.b.seg_end))[key] = lo + kb + c;
+    }
+}
+
 // ---- batch: one lane per key walks its events of the key-sorted batch ----
 template <int NW> __device__ void cnt_batch(const GenArgs& a) {
     const uint32_t key = blockIdx.x * 64u + threadIdx.x;

@@ -225,7 +225,13 @@ struct GenBatch {
     uint32_t payStride;        // words per element (W + 2)
     uint32_t payNull;
     uint32_t sidxStride;       // 0 = 1
-    uint32_t pad;
+    // the fused grouping of the count kernel (gen_host.hip): the batch grouped by 64-key tile (Pay<W> elements, key &
+    // 255 in the position's bits 24..31), tile t at [tile_lo[t], tile_lo[t + 1]) of tpay; k_cnt_split splits each
+    // tile by key into `pay` and writes every key's bounds (its largest tile to tileMax)
+    uint32_t pad2;
+    const uint32_t* tile_lo;
+    const uint32_t* tpay;
+    uint32_t* tileMax;
 };
 
 struct GenOut {

@@ -81,6 +81,7 @@ static const AbsKernel kAbsTimers[ABS_MAXNW + 1] = {nullptr, k_abs_timers_1, k_a
                                                     k_abs_timers_4, k_abs_timers_5, k_abs_timers_6, k_abs_timers_7,
                                                     k_abs_timers_8};
 extern "C" __global__ void k_gen_timers(const GenArgs ap);
+extern "C" __global__ void k_cnt_split(const GenArgs a);
 extern "C" __global__ void k_gen_deadlines(const GenArgs ap);
 extern "C" __global__ void k_gen_due(const int64_t* nd, uint32_t K, int64_t now, uint32_t* due,
                                      unsigned long long* ndue);
@@ -1092,6 +1093,12 @@ struct GenEngine {
     unsigned long long* fb2_n = nullptr;
     unsigned long long* fb_n = nullptr;
     uint32_t* pay = nullptr;   // the key-sorted payload of the register-window kernel (pack.h Pay<W>)
+    bool cnt_fused = false;    // the count kernel's batches may take the fused tile grouping
+    bool cnt_fused_last = false;
+    bool cnt_skewed = false;   // a fused batch had a tile of more than 2^14 events: the sorted grouping from then on
+    uint32_t* tile_max = nullptr;
+    uint32_t* tpay = nullptr;  // fused: the batch grouped by 64-key tile (Pay<W>, key & 255 tagged), tile starts
+    uint32_t* tile_lo = nullptr;
     unsigned long long* wstats = nullptr;  // its per-wave counter rows
     unsigned long long* tstage = nullptr;  // its staged timer matches
     // timer matches ordered through the due keys (keyorder: partitioned, playback, one listener)
@@ -1311,6 +1318,14 @@ GenEngine* gen_create(const uint32_t* ir, size_t nw, const sg_config& cfg, hipSt
                 e->rec = e->dalloc<uint32_t>((size_t)rw * K);
             }
             e->pay = e->dalloc<uint32_t>(B * 6);  // Pay<4>: 6 words
+            // the count kernel's fused grouping (by 64-key tile; the kernel splits its tile by key in LDS)
+            e->cnt_fused = regKernels && G.partitioned && sgd_fused_ok(K, B, 1, 6) && !getenv("SG_NO_FUSED");
+            if (e->cnt_fused) {
+                e->tpay = e->dalloc<uint32_t>(B * 6);
+                e->tile_lo = e->dalloc<uint32_t>((K + 63) / 64 + 1);
+                e->tile_max = e->dalloc<uint32_t>(1);
+                GH_OK(hipMemsetAsync(e->tile_max, 0, 4, stream));
+            }
             e->wstats = e->dalloc<unsigned long long>((size_t)((K + 63) / 64) * GST_N);
             if (G.playback && G.partitioned && G.nStartup == 1) {
                 e->tstage = e->dalloc<unsigned long long>((size_t)K * ABS_R * 2);
@@ -1420,10 +1435,11 @@ static void launch_gen(GenEngine* e, GenArgs a, int which) {
         const bool ff = abs_ff(e);
         const uint32_t NW = e->host.absNW;
         const bool occ4 = e->abs_occ4 && NW <= 3 && blocks > 12u * e->ncu && blocks <= 16u * e->ncu;
+        const unsigned lds = 0;
         hipLaunchKernelGGL(which == GEN_L_ABS_BATCH   ? (ff ? (occ4 ? kAbsBatchF4[NW] : kAbsBatchF[NW]) : kAbsBatch[NW])
                            : which == GEN_L_CNT_BATCH ? kCntBatch[NW]
                                                       : (occ4 ? kAbsTimers4[NW] : kAbsTimers[NW]),
-                           dim3(blocks), dim3(64), 0, e->stream, ap);
+                           dim3(blocks), dim3(64), lds, e->stream, ap);
         hipLaunchKernelGGL(k_gen_stats_reduce, dim3(GST_N, std::min<uint32_t>((blocks + 1023) / 1024, 16u)), dim3(256),
                            0, e->stream, e->wstats, blocks, e->stats);
     }
@@ -1542,7 +1558,33 @@ int gen_push(GenEngine* e, const sg_batch* b, std::string& msg) {
         ga.seg_end = e->seg_end;
         ga.err = e->err;
         ga.s = e->pscr;
-        if ((abs_on(e) || cnt_on(e)) && W >= 1 && W <= 4) {
+        // the register-window kernels' batches (count, absent): grouped by 64-key tile (two 7-bit passes), then split by key per tile
+        // (k_cnt_split), instead of three 8-bit passes; while a batch has shown a tile of more than 2^14 events (one
+        // wave splits a tile), the sorted grouping
+        const bool fused = e->cnt_fused && !e->cnt_skewed && (cnt_on(e) || abs_on(e)) && W >= 1 && W <= 4;
+        e->cnt_fused_last = fused;
+        if (fused) {
+            ga.W = W;
+            ga.src = ps;
+            ga.out = e->tpay;
+            ga.tile_bits = 6;
+            GH_OK(sgd_group_tiles_fused(ga, e->tile_lo, e->stream));
+            a.b.pay = e->pay;
+            a.b.payStride = W + 2;
+            a.b.payNull = nul ? 1u : 0u;
+            a.b.sidx = e->pay;
+            a.b.sidxStride = W + 2;
+            a.b.tile_lo = e->tile_lo;
+            a.b.tpay = e->tpay;
+            a.b.tileMax = e->tile_max;
+            a.b.seg_begin = e->seg_begin;
+            a.b.seg_end = e->seg_end;
+            hipLaunchKernelGGL(k_cnt_split, dim3(((e->K + 63) / 64 + 3) / 4), dim3(256), 0, e->stream, a);
+            GH_OK(hipGetLastError());
+            a.b.tile_lo = nullptr;
+            a.b.tpay = nullptr;
+            a.b.tileMax = nullptr;
+        } else if ((abs_on(e) || cnt_on(e)) && W >= 1 && W <= 4) {
             ga.W = W;
             ga.src = ps;
             ga.out = e->pay;
@@ -1818,9 +1860,12 @@ int gen_poll(GenEngine* e, uint32_t mem, sg_match_batch* out, std::string& msg) 
     if (e->held) { msg = "previous matches not released"; return SG_ERR_STATE; }
     unsigned long long n = 0;
     uint32_t err = 0;
+    uint32_t tmax = 0;
     GH_OK(hipMemcpyAsync(&n, e->out.count, 8, hipMemcpyDeviceToHost, e->stream));
     GH_OK(hipMemcpyAsync(&err, e->err, 4, hipMemcpyDeviceToHost, e->stream));
+    if (e->tile_max) GH_OK(hipMemcpyAsync(&tmax, e->tile_max, 4, hipMemcpyDeviceToHost, e->stream));
     GH_OK(hipStreamSynchronize(e->stream));
+    if (tmax > (1u << 14)) e->cnt_skewed = true;  // (one wave splits a tile: skewed streams take the sorted grouping)
     if (err & GERR_KEY) {
         // reported once: the events with valid keys were processed, the others dropped
         const uint32_t rest = err & ~(uint32_t)GERR_KEY;
@@ -2045,6 +2090,9 @@ std::string gen_describe(const GenEngine* e) {
         push = "k_gen_batch (general interpreter, lane per key)";
         if (G.nStartup > 0) adv = "k_gen_timers (general interpreter)";
     }
+    if (e->cnt_fused_last)
+        push = "k_part_hist + k_part_scan + k_part_scatter x2 + k_tile_bounds (grouping by 64-key tile) + k_cnt_split "
+               "(key split per tile); " + push;
     return "push: " + push + (adv.empty() ? std::string() : "; advance: " + adv);
 }
 

@@ -63,6 +63,8 @@ struct GroupArgs {
     uint32_t* seg_end;       // [K]
     uint32_t* err;
     PartScratch s;
+    uint32_t tile_bits;      // sgd_group_tiles_fused: keys per tile = 2^tile_bits (0: SGD_PT_TILE_BITS)
+    uint32_t pad;
 };
 hipError_t sgd_group_sorted(const GroupArgs& a, hipStream_t stream);
 
@@ -70,8 +72,10 @@ hipError_t sgd_group_sorted(const GroupArgs& a, hipStream_t stream);
 // bits 24..31 = key & 255; tile_lo[t] = first element of tile t, tile_lo[n_tiles] = the valid count
 // (K <= 2^20, n <= 2^24)
 hipError_t sgd_group_tiles_fused(const GroupArgs& a, uint32_t* tile_lo, hipStream_t stream);
-inline bool sgd_fused_ok(uint64_t K, uint64_t max_batch, uint32_t W) {
-    return K >= 1 && K <= ((uint64_t)SGD_PT_MAX_TILES << SGD_PT_TILE_BITS) && max_batch <= SGD_PT_FUSED_MAX_BATCH &&
+inline bool sgd_fused_ok(uint64_t K, uint64_t max_batch, uint32_t W, uint32_t tile_bits = SGD_PT_TILE_BITS) {
+    // (tile codes travel as u16: at most 65,535 tiles; SGD_PT_MAX_TILES bounds the C2 advance grid)
+    const uint64_t max_tiles = tile_bits == SGD_PT_TILE_BITS ? SGD_PT_MAX_TILES : 65535u;
+    return K >= 1 && K <= (max_tiles << tile_bits) && max_batch <= SGD_PT_FUSED_MAX_BATCH &&
            W >= 1 && W <= 4;
 }
 

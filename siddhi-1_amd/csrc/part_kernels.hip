@@ -496,8 +496,9 @@ PartScratch sgd_part_scratch(void* base, uint64_t max_n) {
 }
 
 hipError_t sgd_group_tiles_fused(const GroupArgs& g, uint32_t* tile_lo, hipStream_t stream) {
-    if (!sgd_fused_ok(g.K, g.n, g.W) || g.n == 0) return hipErrorInvalidValue;
-    const uint32_t nt = (g.K + (1u << SGD_PT_TILE_BITS) - 1) >> SGD_PT_TILE_BITS;
+    const uint32_t tbits = g.tile_bits ? g.tile_bits : SGD_PT_TILE_BITS;
+    if (tbits > 8u || !sgd_fused_ok(g.K, g.n, g.W, tbits) || g.n == 0) return hipErrorInvalidValue;
+    const uint32_t nt = (g.K + (1u << tbits) - 1) >> tbits;
     const uint32_t tb = bits_for(nt);
     ElemArgs e{};
     e.ps = g.src;
@@ -508,7 +509,7 @@ hipError_t sgd_group_tiles_fused(const GroupArgs& g, uint32_t* tile_lo, hipStrea
     a.drop_null = g.drop_null;
     a.keys = g.keys;
     a.err = g.err;
-    a.shift = SGD_PT_TILE_BITS;
+    a.shift = tbits;
     if (tb <= SGD_PT_MAX_BITS) {  // one pass on the whole tile id: its digit starts are the tile starts
         a.dbits = tb;
         a.ndig = nt;
@@ -521,7 +522,7 @@ hipError_t sgd_group_tiles_fused(const GroupArgs& g, uint32_t* tile_lo, hipStrea
     const uint32_t b1 = tb / 2, b2 = tb - b1;
     a.dbits = b1;
     a.ndig = 1u << b1;
-    a.cshift = SGD_PT_TILE_BITS;
+    a.cshift = tbits;
     a.cmask = 0xffffu;
     a.side_out = g.s.keys[0];
     a.lo = g.s.lo[0];

@@ -265,3 +265,39 @@ def test_count_records_vs_blocks_with_exports_between_pushes(shape, monkeypatch)
     assert total > 0
     _docs_equal(rec, ora)
     _docs_equal(blk, ora)
+
+
+@pytest.mark.parametrize("skew", [False, True])
+@pytest.mark.parametrize("shape", ["c3_min1", "c3_as_written"])
+def test_count_fused_tile_grouping(shape, skew, monkeypatch):
+    """the count kernel's fused grouping (batches grouped by 64-key tile in two 7-bit passes, each tile split by key
+    by one wave of k_cnt_split; with one key holding 30 % of the batch, its tile thousands of events) == the sorted
+    grouping (SG_NO_FUSED) == the oracle"""
+    q = SHAPES[shape]
+    n_keys, n = 4096, 1 << 14   # (256 events per tile on average: the fused grouping's density)
+    fused = _engine(q, n_keys, n, False, monkeypatch)
+    srt = _engine(q, n_keys, n, True, monkeypatch, env="SG_NO_FUSED")
+    ora = _oracle(q, n_keys)
+    rng = np.random.default_rng(17)
+    total = 0
+    for b in range(3):
+        d = synth.stock_ticks(b * n, n, n_keys, seed=40 + b, rate_per_ms=8)
+        if skew:  # one key with 30 % of the batch: its tile is far over the LDS cap
+            d["key"][rng.random(n) < 0.3] = 1000
+            d["symbol"] = d["key"].copy()
+        for e in (fused, srt, ora):
+            e.push(0, b * n, d["ts"], [d["symbol"], d["price"], d["volume"]], None, d["key"])
+        ms = [e.poll() for e in (fused, srt, ora)]
+        _same(ms[0], ms[1])
+        _same(ms[0], ms[2])
+        total += len(ms[0])
+    sf, ss, so = fused.stats(), srt.stats(), ora.stats()
+    for k in ALL:
+        assert sf[k] == ss[k], (k, sf[k], ss[k])
+    for k in ("matches", "partials_live"):
+        assert sf[k] == so[k], (k, sf[k], so[k])
+    assert "k_cnt_split" in fused.describe(), fused.describe()
+    assert "k_cnt_split" not in srt.describe()
+    _docs_equal(fused, ora)
+    if shape == "c3_min1":
+        assert total > 0
