@@ -244,3 +244,51 @@ def test_hot_many_survivors(monkeypatch):
     assert sg["partials_live"] > 64
     for e in (gpu, ora, lane):
         e.close()
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("kind", ["zipf", "walk"])
+def test_c2_variants_at_bench_size_key_subset(kind):
+    """the bench's C2 variants at their size (2^20 keys, two 2^24-event batches): Zipf(s=1.1) keys — key 0 is the
+    hottest (~12 % of every batch, to the hot-key pipeline) and is in the subset — and per-key random-walk prices
+    (longer-lived partials, register-window spills).  Oracle on keys % 64 == 0 with the same arrival seqs, plus
+    size-independent properties of every match."""
+    from test_gpu_parity import _engines
+    n_keys, batch, mod = 1 << 20, 1 << 24, 64
+    cq, gpu, ora = _engines(synth.C2_QUERY, n_keys, batch, cap=256, mcap=1 << 24)
+    walk = synth.RandomWalk(n_keys) if kind == "walk" else None
+    seq, hot = 0, 0
+    for b in range(2):
+        if kind == "zipf":
+            d = synth.zipf_ticks(seq, batch, n_keys)
+        else:
+            d = synth.stock_ticks(seq, batch, n_keys)
+            d["price"] = walk.step(d["key"], seq)
+        gpu.push(0, seq, d["ts"], [d[c] for c in COLS], None, d["key"])
+        mg = gpu.poll()
+        idx = np.nonzero((d["key"] % mod) == 0)[0]
+        starts = np.concatenate([[0], np.nonzero(np.diff(idx) != 1)[0] + 1])
+        ends = np.concatenate([starts[1:], [len(idx)]])
+        for s, t in zip(starts, ends):
+            sl = idx[s:t]
+            ora.push(0, seq + int(sl[0]), d["ts"][sl], [d[c][sl] for c in COLS], None, d["key"][sl])
+        mo = ora.poll()
+        keep = (mg.key % mod) == 0
+        assert int(keep.sum()) == len(mo) and len(mo) > 0
+        assert np.array_equal(mg.trigger_seq[keep], mo.trigger_seq)
+        assert np.array_equal(mg.slot_seq[keep], mo.slot_seq)
+        hot += int((mg.key == 0).sum())
+        trig = mg.trigger_seq.astype(np.int64) - seq
+        e1 = mg.slot_seq[:, 0, 0].astype(np.int64)
+        assert np.all(np.diff(mg.trigger_seq.astype(np.int64)) >= 0)
+        assert np.all(e1 < mg.trigger_seq.astype(np.int64))
+        cur = e1 >= seq
+        p1, p2 = d["price"][e1[cur] - seq], d["price"][trig[cur]]
+        assert np.all(p1 > 20) and np.all(p2 > p1)
+        assert np.all(d["key"][trig] == mg.key)
+        seq += batch
+    st = gpu.stats()
+    if kind == "zipf":
+        assert hot > 1000 and st["hot_keys"] > 0 and "k_hot_prep" in gpu.describe()
+    gpu.close()
+    ora.close()
