@@ -638,8 +638,10 @@ __device__ void write_out(const OutBufs& o, uint64_t d, const uint32_t* rec, boo
 // batch matches: out_count + t_off[trigger] + rank (a grid-stride loop over the reserved raw slots); with
 // `only_if` (the GEN_M_TFIRST ordering's t_multi flag) the launch does nothing unless the flag is set
 __global__ void k_gen_scatter(const uint32_t* raw, const unsigned long long* raw_count, uint64_t seg_cap,
-                              uint32_t nseg, const uint32_t* t_off, OutBufs o, const uint32_t* only_if) {
+                              uint32_t nseg, const uint32_t* t_off, OutBufs o, const uint32_t* only_if,
+                              const unsigned long long* obase) {
     if (only_if && *only_if == 0u) return;
+    const unsigned long long base = *obase;
     for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < seg_cap * nseg;
          r += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t sg = r / seg_cap;  // reservation segment (GenOut)
@@ -647,31 +649,107 @@ __global__ void k_gen_scatter(const uint32_t* raw, const unsigned long long* raw
         if (r - sg * seg_cap >= n) continue;
         const uint32_t* rec = raw + r * o.recWords;
         if (rec[0] >= 0xfffffffeu) continue;
-        write_out(o, *o.count + t_off[rec[0]] + (rec[1] & ~GEN_REC_PACKED), rec, false);
+        write_out(o, base + t_off[rec[0]] + (rec[1] & ~GEN_REC_PACKED), rec, false);
     }
 }
 
-// batch matches when every trigger has at most one (GEN_M_TFIRST): output-major, one thread per trigger
-// event — the output writes of a wave are consecutive, the raw records are gathered
-// The matches of a wave's 64 triggers are consecutive output records (t_off is the scan of 0/1 counts), so
-// the slot chains ([n][n_slots][max_chain] u64: 192 B per match at C3_min1) and chain lengths are written by
-// the whole wave over its contiguous output range — lane j stores element j, j + 64, ... of the range,
-// reading the record word it needs (records found through an LDS table) — instead of one lane storing its
-// match's 192 B with 64 lanes' stores 192 B apart
-__global__ void __launch_bounds__(256) k_gen_gather1(const uint32_t* __restrict__ raw, const uint32_t* __restrict__ t_cnt,
-                                                     const uint32_t* __restrict__ t_off,
-                                                     const uint32_t* __restrict__ t_first, uint32_t n, OutBufs o,
-                                                     const uint32_t* __restrict__ t_multi) {
+// The batch ordering: output record of the r-th match of batch event t = the batch's base (the running count
+// before the batch) + the exclusive prefix of the per-event counts + r, i.e. ascending trigger seq, then emission
+// order (MultiProcessStreamReceiver.java:119-121).  Tiles of GEN_OT = 256 events: k_gen_tsum (tile totals),
+// k_gen_tscan (one workgroup: the tiles' offsets, the batch's base, the running count moved past the batch),
+// k_gen_order (a tile per workgroup: its events' offsets; the one-match-per-trigger gather; the counts reset for
+// the next batch — only the nonzero ones are written), k_gen_scatter for the records the gather does not take.
+#define GEN_OT 256u
+__global__ void __launch_bounds__(256) k_gen_tsum(const uint32_t* __restrict__ t_cnt, uint32_t n,
+                                                  uint32_t* __restrict__ tile_sum) {
+    // a wave per tile: 4 consecutive counts per lane
+    const uint32_t tile = blockIdx.x * 4u + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    const uint32_t i0 = tile * GEN_OT + lane * 4u;
+    uint32_t c = 0;
+    if (i0 + 3u < n) {
+        const uint4 v = *reinterpret_cast<const uint4*>(t_cnt + i0);
+        c = v.x + v.y + v.z + v.w;
+    } else {
+        for (uint32_t q = 0; q < 4u; ++q) c += i0 + q < n ? t_cnt[i0 + q] : 0u;
+    }
+    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
+    if (lane == 0 && tile * GEN_OT < n) tile_sum[tile] = c;
+}
+
+// one workgroup of 1024 threads: tile_off = exclusive scan of tile_sum; *obase = the running count; the count
+// moves past the batch (every later launch of this batch reads *obase, never the count)
+__global__ void __launch_bounds__(1024) k_gen_tscan(const uint32_t* __restrict__ tile_sum, uint32_t nt,
+                                                    uint32_t* __restrict__ tile_off, unsigned long long* count,
+                                                    unsigned long long* obase) {
+    __shared__ uint32_t ws[16];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+    const uint32_t per = (nt + 1023u) / 1024u, j0 = tid * per;
+    uint32_t s = 0;
+    for (uint32_t q = 0; q < per; ++q) s += j0 + q < nt ? tile_sum[j0 + q] : 0u;
+    uint32_t incl = s;
+    for (uint32_t off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += y;
+    }
+    if (lane == 63) ws[w] = incl;
+    __syncthreads();
+    uint32_t pre = 0, all = 0;
+    for (uint32_t q = 0; q < 16; ++q) {
+        pre += q < w ? ws[q] : 0u;
+        all += ws[q];
+    }
+    uint32_t x = pre + incl - s;
+    for (uint32_t q = 0; q < per; ++q) {
+        if (j0 + q < nt) {
+            tile_off[j0 + q] = x;
+            x += tile_sum[j0 + q];
+        }
+    }
+    if (tid == 0) {
+        const unsigned long long b = *count;
+        *obase = b;
+        *count = b + all;
+    }
+}
+
+// a tile of 256 events per workgroup.  GATHER (GEN_M_TFIRST, no trigger with several matches): each wave's matches
+// are consecutive output records (its counts are 0 / 1), so the slot chains ([n][n_slots][max_chain] u64: 192 B per
+// match at C3_min1) and chain lengths are written by the whole wave over its contiguous output range — lane j stores
+// element j, j + 64, ... of the range, reading the record word it needs (records found through an LDS table) —
+// instead of one lane storing its match's 192 B with 64 lanes' stores 192 B apart.  Otherwise each event's offset
+// goes to t_off for k_gen_scatter.
+template <bool GATHER>
+__global__ void __launch_bounds__(256) k_gen_order(const uint32_t* __restrict__ raw, uint32_t* __restrict__ t_cnt,
+                                                   uint32_t* __restrict__ t_off, const uint32_t* __restrict__ t_first,
+                                                   const uint32_t* __restrict__ tile_off, uint32_t n, OutBufs o,
+                                                   const uint32_t* __restrict__ t_multi,
+                                                   const unsigned long long* __restrict__ obase) {
     __shared__ uint32_t rb[4][64];   // per wave: the record index of its q-th match
-    if (*t_multi) return;            // (k_gen_scatter places the records)
+    __shared__ uint32_t wsum[4];
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const bool has = i < n && t_cnt[i] != 0u;
+    const uint32_t c = i < n ? t_cnt[i] : 0u;
+    uint32_t incl = c;
+    for (uint32_t off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += y;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    uint32_t pre = tile_off[blockIdx.x];
+    for (uint32_t q = 0; q < w; ++q) pre += wsum[q];
+    const uint32_t rel = pre + incl - c;   // this event's first record, relative to the batch's base
+    if (c) t_cnt[i] = 0u;                  // (the counts are zero again for the next batch)
+    if (!GATHER || *t_multi) {
+        if (c) t_off[i] = rel;
+        return;
+    }
+    const bool has = c != 0u;
     const uint64_t bm = __ballot(has);
     if (!bm) return;   // (wave-uniform)
     const uint32_t m = (uint32_t)__popcll(bm);
     const uint32_t first = (uint32_t)__ffsll((unsigned long long)bm) - 1u;
-    const uint64_t d0 = *o.count + __shfl(i < n ? t_off[i] : 0u, (int)first, 64);
+    const uint64_t d0 = *obase + __shfl(rel, (int)first, 64);
     if (d0 + m > o.cap) {   // (the capacity check of write_out, per wave)
         if (lane == 0) atomicOr(o.err, (uint32_t)GERR_MATCHCAP);
         return;
@@ -699,7 +777,7 @@ __global__ void __launch_bounds__(256) k_gen_gather1(const uint32_t* __restrict_
         o.len[d0 * ns + x] = r[7 + x % ns];
     }
     for (uint32_t x = lane; x < m * per; x += 64) {  // slot chains
-        const uint32_t q = x / per, y = x % per, sl = y / mc, c = y % mc;
+        const uint32_t q = x / per, y = x % per, sl = y / mc, cc = y % mc;
         const uint32_t* r = raw + (uint64_t)rb[w][q] * o.recWords;
         const uint32_t* seqs = r + 7 + ns;
         uint32_t b = sl * mc;
@@ -707,8 +785,8 @@ __global__ void __launch_bounds__(256) k_gen_gather1(const uint32_t* __restrict_
             b = 0;
             for (uint32_t s2 = 0; s2 < sl; s2++) b += r[7 + s2];
         }
-        o.slot[d0 * per + x] = c < r[7 + sl] ? ((uint64_t)seqs[2 * (b + c)] | ((uint64_t)seqs[2 * (b + c) + 1] << 32))
-                                             : SG_NULL_SEQ;
+        o.slot[d0 * per + x] = cc < r[7 + sl] ? ((uint64_t)seqs[2 * (b + cc)] | ((uint64_t)seqs[2 * (b + cc) + 1] << 32))
+                                              : SG_NULL_SEQ;
     }
 }
 
@@ -718,6 +796,19 @@ __global__ void k_gen_scatter_timers(const uint32_t* raw, const uint32_t* order,
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= *nvalid) return;
     write_out(o, *o.count + r, raw + (uint64_t)order[r] * o.recWords, true);
+}
+
+// a poll's status (gen_poll): count, error word, largest count-kernel tile -> pinned host memory; the count back to 0
+// when the poll will hand the window out (no error of `fail_mask`, within the capacity)
+__global__ void k_gen_status(unsigned long long* count, const uint32_t* err, const uint32_t* tile_max, uint64_t cap,
+                             uint32_t fail_mask, unsigned long long* st) {
+    if (threadIdx.x != 0) return;
+    const unsigned long long c = *count;
+    const uint32_t x = *err;
+    st[0] = c;
+    st[1] = x;
+    st[2] = tile_max ? *tile_max : 0u;
+    if ((x & fail_mask) == 0u && c <= cap) *count = 0ull;
 }
 
 __global__ void k_gen_bump(unsigned long long* count, const uint32_t* t_cnt, const uint32_t* t_off, uint32_t n,
@@ -1065,12 +1156,14 @@ struct GenEngine {
     uint32_t* raw = nullptr;
     unsigned long long* raw_count = nullptr;
     uint32_t *t_cnt = nullptr, *t_first = nullptr, *t_off = nullptr;
+    uint32_t *tile_sum = nullptr, *tile_off = nullptr;   // the batch ordering's per-tile totals / offsets (GEN_OT)
+    unsigned long long* obase = nullptr;                  // the running match count before the batch
+    unsigned long long* h_stat = nullptr;                 // gen_poll's status words (pinned, mapped)
+    unsigned long long* d_stat = nullptr;
     uint32_t* t_multi = nullptr;          // GenOut.t_multi
     int64_t* tk2 = nullptr;
     uint32_t *tk1 = nullptr, *tk3 = nullptr, *order_in = nullptr, *order_out = nullptr;
     unsigned long long* nvalid = nullptr;
-    void* scan_tmp = nullptr;
-    size_t scan_tmp_bytes = 0;
     void* msort_tmp = nullptr;
     size_t msort_tmp_bytes = 0;
     unsigned long long* stats = nullptr;
@@ -1154,6 +1247,7 @@ struct GenEngine {
         }
         for (auto& x : spans) { (void)hipEventDestroy(x.a); (void)hipEventDestroy(x.b); }
         for (void* p : owned) (void)hipFree(p);
+        if (h_stat) (void)hipHostFree(h_stat);
     }
 
     GenArgs args() const {
@@ -1239,9 +1333,9 @@ GenEngine* gen_create(const uint32_t* ir, size_t nw, const sg_config& cfg, hipSt
         e->order_in = e->dalloc<uint32_t>(e->rawCap);
         e->order_out = e->dalloc<uint32_t>(e->rawCap);
         e->nvalid = e->dalloc<unsigned long long>(1);
-        GH_OK(rocprim::exclusive_scan(nullptr, e->scan_tmp_bytes, e->t_cnt, e->t_off, 0u, (uint32_t)B,
-                                      rocprim::plus<uint32_t>(), stream));
-        e->scan_tmp = e->dalloc<uint8_t>(e->scan_tmp_bytes);
+        e->tile_sum = e->dalloc<uint32_t>(B / GEN_OT + 1);
+        e->tile_off = e->dalloc<uint32_t>(B / GEN_OT + 1);
+        e->obase = e->dalloc<unsigned long long>(1);
         TimerLess lt{e->tk1, e->tk2, e->tk3};
         GH_OK(rocprim::merge_sort(nullptr, e->msort_tmp_bytes, e->order_in, e->order_out, (size_t)e->rawCap, lt, stream));
         e->msort_tmp = e->dalloc<uint8_t>(e->msort_tmp_bytes);
@@ -1653,30 +1747,29 @@ int gen_push(GenEngine* e, const sg_batch* b, std::string& msg) {
         a.mode = GEN_M_KEYLIST | GEN_M_TFIRST;
     }
     launch_gen(e, a, GEN_L_BATCH);
-    // order: out_count + t_off[trigger] + rank
-    size_t tmp = e->scan_tmp_bytes;
-    GH_OK(rocprim::exclusive_scan(e->scan_tmp, tmp, e->t_cnt, e->t_off, 0u, n, rocprim::plus<uint32_t>(), e->stream));
+    // order: the batch's base + the exclusive prefix of the per-trigger counts + rank (k_gen_tsum / k_gen_tscan /
+    // k_gen_order; the counts are reset by k_gen_order)
+    const uint32_t nt = (n + GEN_OT - 1) / GEN_OT;
+    hipLaunchKernelGGL(k_gen_tsum, dim3((nt + 3) / 4), dim3(256), 0, e->stream, e->t_cnt, n, e->tile_sum);
+    hipLaunchKernelGGL(k_gen_tscan, dim3(1), dim3(1024), 0, e->stream, e->tile_sum, nt, e->tile_off, e->out.count, e->obase);
     const uint64_t maxRaw = e->rawCap;
+    const unsigned scat_grid = (unsigned)std::min<uint64_t>((maxRaw + 255) / 256, 1024);
     if (a.mode & GEN_M_TFIRST) {
         // output-major gather of the one match per trigger; a trigger of a handed-over key that emitted several
         // (t_multi, set on the device) turns it off and every record is placed by (t_off, rank) instead
-        hipLaunchKernelGGL(k_gen_gather1, dim3((n + 255) / 256), dim3(256), 0, e->stream, e->raw, e->t_cnt, e->t_off,
-                           e->t_first, n, e->out, (const uint32_t*)e->t_multi);
-        hipLaunchKernelGGL(k_gen_scatter, dim3((unsigned)std::min<uint64_t>((maxRaw + 255) / 256, 4096)), dim3(256), 0,
-                           e->stream, e->raw, e->raw_count, e->rawCap / GEN_RAWSEG, (uint32_t)GEN_RAWSEG, e->t_off, e->out,
-                           (const uint32_t*)e->t_multi);
+        hipLaunchKernelGGL(k_gen_order<true>, dim3(nt), dim3(256), 0, e->stream, e->raw, e->t_cnt, e->t_off, e->t_first,
+                           e->tile_off, n, e->out, (const uint32_t*)e->t_multi, (const unsigned long long*)e->obase);
+        hipLaunchKernelGGL(k_gen_scatter, dim3(scat_grid), dim3(256), 0, e->stream, e->raw, e->raw_count,
+                           e->rawCap / GEN_RAWSEG, (uint32_t)GEN_RAWSEG, e->t_off, e->out, (const uint32_t*)e->t_multi,
+                           (const unsigned long long*)e->obase);
     } else {
+        hipLaunchKernelGGL(k_gen_order<false>, dim3(nt), dim3(256), 0, e->stream, e->raw, e->t_cnt, e->t_off, e->t_first,
+                           e->tile_off, n, e->out, (const uint32_t*)e->t_multi, (const unsigned long long*)e->obase);
         hipLaunchKernelGGL(k_gen_scatter, dim3((unsigned)std::min<uint64_t>((maxRaw + 255) / 256, 4096)), dim3(256), 0,
                            e->stream, e->raw, e->raw_count, e->rawCap / GEN_RAWSEG, (uint32_t)GEN_RAWSEG, e->t_off, e->out,
-                           (const uint32_t*)nullptr);
+                           (const uint32_t*)nullptr, (const unsigned long long*)e->obase);
     }
-    hipLaunchKernelGGL(k_gen_bump, dim3(1), dim3(1), 0, e->stream, e->out.count, e->t_cnt, e->t_off, n,
-                       (const unsigned long long*)nullptr);
-    {
-        GenClearList cl;   // (the per-trigger counts back to zero for the next batch)
-        cl.add(e->t_cnt, (size_t)n * 4);
-        GH_OK(cl.launch(e->stream));
-    }
+    GH_OK(hipGetLastError());
     e->st.events += n;
     e->st.batches++;
     e->st.advance_launches++;
@@ -1858,13 +1951,20 @@ int gen_advance(GenEngine* e, int64_t t, std::string& msg) {
 
 int gen_poll(GenEngine* e, uint32_t mem, sg_match_batch* out, std::string& msg) {
     if (e->held) { msg = "previous matches not released"; return SG_ERR_STATE; }
-    unsigned long long n = 0;
-    uint32_t err = 0;
-    uint32_t tmax = 0;
-    GH_OK(hipMemcpyAsync(&n, e->out.count, 8, hipMemcpyDeviceToHost, e->stream));
-    GH_OK(hipMemcpyAsync(&err, e->err, 4, hipMemcpyDeviceToHost, e->stream));
-    if (e->tile_max) GH_OK(hipMemcpyAsync(&tmax, e->tile_max, 4, hipMemcpyDeviceToHost, e->stream));
+    // the count, the error word and the largest tile in one launch into pinned host memory (three copies were
+    // three blit launches); the count is reset there for the next window unless this poll fails
+    if (!e->h_stat) {
+        GH_OK(hipHostMalloc((void**)&e->h_stat, 4 * sizeof(unsigned long long), hipHostMallocMapped));
+        GH_OK(hipHostGetDevicePointer((void**)&e->d_stat, e->h_stat, 0));
+    }
+    hipLaunchKernelGGL(k_gen_status, dim3(1), dim3(64), 0, e->stream, e->out.count, (const uint32_t*)e->err,
+                       (const uint32_t*)e->tile_max, e->out.cap,
+                       (uint32_t)(GERR_KEY | GERR_CAP | GERR_MATCHCAP | GERR_CHAIN | GERR_REF), e->d_stat);
+    GH_OK(hipGetLastError());
     GH_OK(hipStreamSynchronize(e->stream));
+    const unsigned long long n = e->h_stat[0];
+    const uint32_t err = (uint32_t)e->h_stat[1];
+    const uint32_t tmax = (uint32_t)e->h_stat[2];
     if (tmax > (1u << 14)) e->cnt_skewed = true;  // (one wave splits a tile: skewed streams take the sorted grouping)
     if (err & GERR_KEY) {
         // reported once: the events with valid keys were processed, the others dropped
@@ -1911,8 +2011,7 @@ int gen_poll(GenEngine* e, uint32_t mem, sg_match_batch* out, std::string& msg) 
         out->chain_len = e->h_len.data();
         out->mem = SG_MEM_HOST;
     }
-    GH_OK(hipMemsetAsync(e->out.count, 0, 8, e->stream));
-    e->held = true;
+    e->held = true;   // (the count was reset by k_gen_status)
     e->polled = n;
     return SG_OK;
 }

@@ -47,6 +47,9 @@ __global__ void __launch_bounds__(256) k_order_sums(const uint64_t* __restrict__
     if (threadIdx.x == 0) tile_sum[blockIdx.x] = part[0] + part[1] + part[2] + part[3];
 }
 
+#ifndef SGD_ORDER_U
+#define SGD_ORDER_U 4
+#endif
 __global__ void __launch_bounds__(256) k_order_scatter(const ScatterParams s, uint32_t ntiles) {
     // Phase 1: all rows' descriptors are loaded up front, the 16 rows' wave scans combined through one
     // LDS round trip: every trigger of the tile gets its tile-local output offset.  Phase 2 is
@@ -116,25 +119,43 @@ __global__ void __launch_bounds__(256) k_order_scatter(const ScatterParams s, ui
         }
         __syncthreads();
         const uint64_t ring0 = out0 % s.capacity;
-        for (uint32_t q = w0 + threadIdx.x; q < w1; q += 256) {
-            const uint32_t tl = owner[q - w0];
-            const uint32_t t = base + tl;
-            const uint64_t trig = s.seq_base + t;
-            uint64_t o = ring0 + q;
-            if (o >= s.capacity) o -= s.capacity;
-            s.o_trig[o] = trig;
-            // {e1 seq, e2 seq} as one 16-B store
-            const uint64_t e1 = (SG_EXP(s.exp) & 1) ? 0ull
-                                : (cnt[tl] & 0x8000u) ? s.seq_base + (uint64_t)(int64_t)(int32_t)fst[tl]
-                                                      : s.raw_e1[fst[tl] + (q - loc[tl])];
-            *reinterpret_cast<ulonglong2*>(s.o_slot + 2 * o) = make_ulonglong2(e1, trig);
-            s.o_key[o] = s.key ? s.key[t] : 0u;
-            s.o_ts[o] = s.ts[t];  // StreamPostStateProcessor.java:68: StateEvent ts = ts of the e2 event
-            if (s.o_capw) {       // on-device projection: the partial's captures in output order
-                const uint64_t r = fst[tl] + (q - loc[tl]);
-                for (uint32_t w = 0; w < s.n_capw; ++w)
-                    s.o_capw[(size_t)w * s.capacity + o] = s.raw_capw[(size_t)w * s.raw_capacity + r];
-                s.o_capnull[o] = s.raw_capnull[r];
+        // SGD_ORDER_U records per thread per round: their owner lookups and their loads of the trigger's
+        // key / timestamp / e1 seq issued together before any store, so the loads' latencies overlap
+        for (uint32_t q0 = w0 + threadIdx.x; q0 < w1; q0 += 256 * SGD_ORDER_U) {
+            uint32_t tlu[SGD_ORDER_U], kyu[SGD_ORDER_U];
+            uint64_t e1u[SGD_ORDER_U], tsu[SGD_ORDER_U];
+#pragma unroll
+            for (int u = 0; u < SGD_ORDER_U; ++u) {
+                const uint32_t q = q0 + u * 256;
+                if (q < w1) {
+                    const uint32_t tl = owner[q - w0];
+                    const uint32_t t = base + tl;
+                    tlu[u] = tl;
+                    kyu[u] = s.key ? s.key[t] : 0u;
+                    tsu[u] = s.ts[t];
+                    e1u[u] = (SG_EXP(s.exp) & 1) ? 0ull
+                             : (cnt[tl] & 0x8000u) ? s.seq_base + (uint64_t)(int64_t)(int32_t)fst[tl]
+                                                   : s.raw_e1[fst[tl] + (q - loc[tl])];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < SGD_ORDER_U; ++u) {
+                const uint32_t q = q0 + u * 256;
+                if (q >= w1) break;
+                const uint32_t tl = tlu[u];
+                const uint64_t trig = s.seq_base + base + tl;
+                uint64_t o = ring0 + q;
+                if (o >= s.capacity) o -= s.capacity;
+                s.o_trig[o] = trig;
+                *reinterpret_cast<ulonglong2*>(s.o_slot + 2 * o) = make_ulonglong2(e1u[u], trig);  // {e1, e2} seqs
+                s.o_key[o] = kyu[u];
+                s.o_ts[o] = tsu[u];  // StreamPostStateProcessor.java:68: StateEvent ts = ts of the e2 event
+                if (s.o_capw) {      // on-device projection: the partial's captures in output order
+                    const uint64_t r = fst[tl] + (q - loc[tl]);
+                    for (uint32_t w = 0; w < s.n_capw; ++w)
+                        s.o_capw[(size_t)w * s.capacity + o] = s.raw_capw[(size_t)w * s.raw_capacity + r];
+                    s.o_capnull[o] = s.raw_capnull[r];
+                }
             }
         }
         __syncthreads();  // the owner map is rebuilt for the next window

@@ -235,6 +235,31 @@ __global__ void __launch_bounds__(SGD_PT_THREADS) k_part_scatter(const PassArgs 
         const uint64_t i = i0 + (uint64_t)j * 64u;
         k[j] = i < nv ? ((const T*)a.keys)[i] : (T)0;
     }
+    // the events' elements, loaded with the keys (their places are ranked below: the loads' latency overlaps
+    // the ranking instead of following it)
+    uint32_t el[EPT][S];
+#pragma unroll
+    for (uint32_t j = 0; j < EPT; ++j) {
+        const uint64_t i64 = i0 + (uint64_t)j * 64u;
+        const uint32_t i = (uint32_t)i64;
+        if (i64 < nv) {
+            if constexpr (SRC == PT_GATHER) {
+                const Pay<S - 2> p = PackFn<S - 2>{e.ps}(i);
+                el[j][0] = p.idx;
+#pragma unroll
+                for (int u = 0; u < S - 2; ++u) el[j][1 + u] = p.w[u];
+                el[j][S - 1] = (uint32_t)p.ts;
+            } else if constexpr (SRC == PT_IDX) {
+                el[j][0] = i;
+            } else {
+#pragma unroll
+                for (int u = 0; u < S; ++u) el[j][u] = ((const uint32_t*)e.in)[(size_t)i * S + u];
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < S; ++u) el[j][u] = 0u;
+        }
+    }
     // the chunk's global start in each digit's range: digit starts (tot scanned, wave 0) + the row scan
     if (w == 0) {
         const uint32_t q = (ND + 63u) / 64u;  // <= 4
@@ -312,24 +337,13 @@ __global__ void __launch_bounds__(SGD_PT_THREADS) k_part_scatter(const PassArgs 
     for (uint32_t j = 0; j < EPT; ++j) {
         const uint32_t x = pk[j];
         if (x >> 31) {
-            const uint32_t i = (uint32_t)(i0 + (uint64_t)j * 64u);
-            uint32_t el[S];
             if constexpr (SRC == PT_GATHER) {
-                const Pay<S - 2> p = PackFn<S - 2>{e.ps}(i);
-                el[0] = e.tag ? (p.idx | (((x >> 17) & 255u) << 24)) : p.idx;
-#pragma unroll
-                for (int u = 0; u < S - 2; ++u) el[1 + u] = p.w[u];
-                el[S - 1] = (uint32_t)p.ts;
-            } else if constexpr (SRC == PT_IDX) {
-                el[0] = i;
-            } else {
-#pragma unroll
-                for (int u = 0; u < S; ++u) el[u] = ((const uint32_t*)e.in)[(size_t)i * S + u];
+                if (e.tag) el[j][0] |= ((x >> 17) & 255u) << 24;
             }
             const uint32_t d = x & 255u;
             const uint32_t pos = mine[d] + ((x >> 8) & 511u);
 #pragma unroll
-            for (int u = 0; u < S; ++u) el_l[pos * S + u] = el[u];
+            for (int u = 0; u < S; ++u) el_l[pos * S + u] = el[j][u];
             dg[pos] = (uint8_t)d;
             if constexpr (SIDE == PS_KEY) side_l[pos] = k[j];
             if constexpr (SIDE == PS_CODE) side_l[pos] = (uint16_t)(((uint64_t)k[j] >> a.cshift) & a.cmask);
@@ -394,7 +408,10 @@ __global__ void __launch_bounds__(256) k_part_bounds(const uint32_t* __restrict_
 }
 
 // ---- host side ----------------------------------------------------------------------------------------
-constexpr uint32_t ept_of(uint32_t S) { return S <= 4 ? 4u : 2u; }
+#ifndef SGD_PT_EPT_NARROW
+#define SGD_PT_EPT_NARROW 4
+#endif
+constexpr uint32_t ept_of(uint32_t S) { return S <= 4 ? (uint32_t)SGD_PT_EPT_NARROW : 2u; }
 constexpr uint32_t PT_HC = 8;  // chunks per histogram block
 
 uint32_t nblk_of(uint64_t n, uint32_t S) {

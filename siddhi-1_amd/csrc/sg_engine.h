@@ -206,7 +206,9 @@ struct ScatterParams {
                                // record (0: no match); NULL otherwise
     uint32_t exp;              // ordering ablations (EXTRA=-DSG_EXPERIMENTS builds only: wrong results), 0 otherwise
 };
+#ifndef SGD_ORDER_TILE
 #define SGD_ORDER_TILE 4096  // triggers per workgroup of the ordering kernels (256 threads x 16 rows)
+#endif
 // On-device projection of the select list (sg_set_projection) for the two-state kernel: after the ordering
 // of a batch, item i of every match of the batch is evaluated (java_ops.h) over the match's e1 captures
 // (VAR b = 0, w1 = capture index) and its trigger event's batch columns (VAR b = 1, w1 = attribute).
