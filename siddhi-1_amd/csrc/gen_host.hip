@@ -660,10 +660,14 @@ __global__ void k_gen_scatter(const uint32_t* raw, const unsigned long long* raw
 // k_gen_order (a tile per workgroup: its events' offsets; the one-match-per-trigger gather; the counts reset for
 // the next batch — only the nonzero ones are written), k_gen_scatter for the records the gather does not take.
 #define GEN_OT 256u
-__global__ void __launch_bounds__(256) k_gen_tsum(const uint32_t* __restrict__ t_cnt, uint32_t n,
-                                                  uint32_t* __restrict__ tile_sum) {
-    // a wave per tile: 4 consecutive counts per lane
-    const uint32_t tile = blockIdx.x * 4u + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
+#define GEN_OST 16u   // tiles per super tile (one k_gen_tsum workgroup): k_gen_tscan scans the super tiles
+__global__ void __launch_bounds__(1024) k_gen_tsum(const uint32_t* __restrict__ t_cnt, uint32_t n,
+                                                   uint32_t* __restrict__ tile_pre, uint32_t* __restrict__ sup_sum) {
+    // a wave per tile (4 consecutive counts per lane), a workgroup per super tile: each tile's prefix inside its
+    // super tile, the super tile's total
+    __shared__ uint32_t ts[GEN_OST];
+    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const uint32_t tile = blockIdx.x * GEN_OST + w;
     const uint32_t i0 = tile * GEN_OT + lane * 4u;
     uint32_t c = 0;
     if (i0 + 3u < n) {
@@ -673,19 +677,34 @@ __global__ void __launch_bounds__(256) k_gen_tsum(const uint32_t* __restrict__ t
         for (uint32_t q = 0; q < 4u; ++q) c += i0 + q < n ? t_cnt[i0 + q] : 0u;
     }
     for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
-    if (lane == 0 && tile * GEN_OT < n) tile_sum[tile] = c;
+    if (lane == 0) ts[w] = c;
+    __syncthreads();
+    if (threadIdx.x < GEN_OST) {
+        uint32_t pre = 0, all = 0;
+        for (uint32_t q = 0; q < GEN_OST; ++q) {
+            pre += q < threadIdx.x ? ts[q] : 0u;
+            all += ts[q];
+        }
+        if ((blockIdx.x * GEN_OST + threadIdx.x) * GEN_OT < n) tile_pre[blockIdx.x * GEN_OST + threadIdx.x] = pre;
+        if (threadIdx.x == 0) sup_sum[blockIdx.x] = all;
+    }
 }
 
-// one workgroup of 1024 threads: tile_off = exclusive scan of tile_sum; *obase = the running count; the count
-// moves past the batch (every later launch of this batch reads *obase, never the count)
-__global__ void __launch_bounds__(1024) k_gen_tscan(const uint32_t* __restrict__ tile_sum, uint32_t nt,
-                                                    uint32_t* __restrict__ tile_off, unsigned long long* count,
+// one workgroup of 1024 threads: sup_off = exclusive scan of the super tiles' totals; *obase = the running count;
+// the count moves past the batch (every later launch of this batch reads *obase, never the count)
+__global__ void __launch_bounds__(1024) k_gen_tscan(const uint32_t* __restrict__ sup_sum, uint32_t ns,
+                                                    uint32_t* __restrict__ sup_off, unsigned long long* count,
                                                     unsigned long long* obase) {
     __shared__ uint32_t ws[16];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
-    const uint32_t per = (nt + 1023u) / 1024u, j0 = tid * per;
-    uint32_t s = 0;
-    for (uint32_t q = 0; q < per; ++q) s += j0 + q < nt ? tile_sum[j0 + q] : 0u;
+    constexpr uint32_t PER = 8;   // (<= 8192 super tiles: batches up to 2^25 events; checked on the host)
+    uint32_t v[PER], s = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < PER; ++q) {
+        const uint32_t j = tid * PER + q;
+        v[q] = j < ns ? sup_sum[j] : 0u;
+        s += v[q];
+    }
     uint32_t incl = s;
     for (uint32_t off = 1; off < 64; off <<= 1) {
         const uint32_t y = __shfl_up(incl, off, 64);
@@ -699,11 +718,11 @@ __global__ void __launch_bounds__(1024) k_gen_tscan(const uint32_t* __restrict__
         all += ws[q];
     }
     uint32_t x = pre + incl - s;
-    for (uint32_t q = 0; q < per; ++q) {
-        if (j0 + q < nt) {
-            tile_off[j0 + q] = x;
-            x += tile_sum[j0 + q];
-        }
+#pragma unroll
+    for (uint32_t q = 0; q < PER; ++q) {
+        const uint32_t j = tid * PER + q;
+        if (j < ns) sup_off[j] = x;
+        x += v[q];
     }
     if (tid == 0) {
         const unsigned long long b = *count;
@@ -721,7 +740,8 @@ __global__ void __launch_bounds__(1024) k_gen_tscan(const uint32_t* __restrict__
 template <bool GATHER>
 __global__ void __launch_bounds__(256) k_gen_order(const uint32_t* __restrict__ raw, uint32_t* __restrict__ t_cnt,
                                                    uint32_t* __restrict__ t_off, const uint32_t* __restrict__ t_first,
-                                                   const uint32_t* __restrict__ tile_off, uint32_t n, OutBufs o,
+                                                   const uint32_t* __restrict__ tile_pre,
+                                                   const uint32_t* __restrict__ sup_off, uint32_t n, OutBufs o,
                                                    const uint32_t* __restrict__ t_multi,
                                                    const unsigned long long* __restrict__ obase) {
     __shared__ uint32_t rb[4][64];   // per wave: the record index of its q-th match
@@ -736,7 +756,7 @@ __global__ void __launch_bounds__(256) k_gen_order(const uint32_t* __restrict__ 
     }
     if (lane == 63) wsum[w] = incl;
     __syncthreads();
-    uint32_t pre = tile_off[blockIdx.x];
+    uint32_t pre = sup_off[blockIdx.x / GEN_OST] + tile_pre[blockIdx.x];
     for (uint32_t q = 0; q < w; ++q) pre += wsum[q];
     const uint32_t rel = pre + incl - c;   // this event's first record, relative to the batch's base
     if (c) t_cnt[i] = 0u;                  // (the counts are zero again for the next batch)
@@ -798,7 +818,7 @@ __global__ void k_gen_scatter_timers(const uint32_t* raw, const uint32_t* order,
     write_out(o, *o.count + r, raw + (uint64_t)order[r] * o.recWords, true);
 }
 
-// a poll's status (gen_poll): count, error word, largest count-kernel tile -> pinned host memory; the count back to 0
+// a poll's status (gen_poll): count, error word, largest count-kernel tile -> st (copied to the host); the count back to 0
 // when the poll will hand the window out (no error of `fail_mask`, within the capacity)
 __global__ void k_gen_status(unsigned long long* count, const uint32_t* err, const uint32_t* tile_max, uint64_t cap,
                              uint32_t fail_mask, unsigned long long* st) {
@@ -1156,9 +1176,9 @@ struct GenEngine {
     uint32_t* raw = nullptr;
     unsigned long long* raw_count = nullptr;
     uint32_t *t_cnt = nullptr, *t_first = nullptr, *t_off = nullptr;
-    uint32_t *tile_sum = nullptr, *tile_off = nullptr;   // the batch ordering's per-tile totals / offsets (GEN_OT)
+    uint32_t *tile_pre = nullptr, *sup_sum = nullptr, *sup_off = nullptr;   // the batch ordering's tile prefixes
     unsigned long long* obase = nullptr;                  // the running match count before the batch
-    unsigned long long* h_stat = nullptr;                 // gen_poll's status words (pinned, mapped)
+    unsigned long long h_stat[4] = {0, 0, 0, 0};          // gen_poll's status words and their device copy
     unsigned long long* d_stat = nullptr;
     uint32_t* t_multi = nullptr;          // GenOut.t_multi
     int64_t* tk2 = nullptr;
@@ -1247,7 +1267,6 @@ struct GenEngine {
         }
         for (auto& x : spans) { (void)hipEventDestroy(x.a); (void)hipEventDestroy(x.b); }
         for (void* p : owned) (void)hipFree(p);
-        if (h_stat) (void)hipHostFree(h_stat);
     }
 
     GenArgs args() const {
@@ -1297,6 +1316,8 @@ GenEngine* gen_create(const uint32_t* ir, size_t nw, const sg_config& cfg, hipSt
             GH_OK(hipMemsetAsync(e->prof, 0, 64, stream));
         }
         e->maxb = cfg.max_batch ? cfg.max_batch : (1u << 20);
+        // (k_gen_tscan: one workgroup of 1024 threads x 8 super tiles of GEN_OT * GEN_OST events)
+        if (e->maxb > 8192ull * GEN_OT * GEN_OST) throw std::runtime_error("max_batch above 2^25 events");
         e->mcap = cfg.match_capacity ? cfg.match_capacity : (uint64_t)e->maxb * 4;
         const GenProgram& G = e->host;
         e->recWords = 7 + (uint32_t)G.nslots + 2 * (uint32_t)G.nslots * G.MC;
@@ -1333,8 +1354,9 @@ GenEngine* gen_create(const uint32_t* ir, size_t nw, const sg_config& cfg, hipSt
         e->order_in = e->dalloc<uint32_t>(e->rawCap);
         e->order_out = e->dalloc<uint32_t>(e->rawCap);
         e->nvalid = e->dalloc<unsigned long long>(1);
-        e->tile_sum = e->dalloc<uint32_t>(B / GEN_OT + 1);
-        e->tile_off = e->dalloc<uint32_t>(B / GEN_OT + 1);
+        e->tile_pre = e->dalloc<uint32_t>(B / GEN_OT + 1);
+        e->sup_sum = e->dalloc<uint32_t>(B / (GEN_OT * GEN_OST) + 1);
+        e->sup_off = e->dalloc<uint32_t>(B / (GEN_OT * GEN_OST) + 1);
         e->obase = e->dalloc<unsigned long long>(1);
         TimerLess lt{e->tk1, e->tk2, e->tk3};
         GH_OK(rocprim::merge_sort(nullptr, e->msort_tmp_bytes, e->order_in, e->order_out, (size_t)e->rawCap, lt, stream));
@@ -1749,22 +1771,24 @@ int gen_push(GenEngine* e, const sg_batch* b, std::string& msg) {
     launch_gen(e, a, GEN_L_BATCH);
     // order: the batch's base + the exclusive prefix of the per-trigger counts + rank (k_gen_tsum / k_gen_tscan /
     // k_gen_order; the counts are reset by k_gen_order)
-    const uint32_t nt = (n + GEN_OT - 1) / GEN_OT;
-    hipLaunchKernelGGL(k_gen_tsum, dim3((nt + 3) / 4), dim3(256), 0, e->stream, e->t_cnt, n, e->tile_sum);
-    hipLaunchKernelGGL(k_gen_tscan, dim3(1), dim3(1024), 0, e->stream, e->tile_sum, nt, e->tile_off, e->out.count, e->obase);
+    const uint32_t nt = (n + GEN_OT - 1) / GEN_OT, nsup = (nt + GEN_OST - 1) / GEN_OST;
+    hipLaunchKernelGGL(k_gen_tsum, dim3(nsup), dim3(1024), 0, e->stream, e->t_cnt, n, e->tile_pre, e->sup_sum);
+    hipLaunchKernelGGL(k_gen_tscan, dim3(1), dim3(1024), 0, e->stream, e->sup_sum, nsup, e->sup_off, e->out.count, e->obase);
     const uint64_t maxRaw = e->rawCap;
     const unsigned scat_grid = (unsigned)std::min<uint64_t>((maxRaw + 255) / 256, 1024);
     if (a.mode & GEN_M_TFIRST) {
         // output-major gather of the one match per trigger; a trigger of a handed-over key that emitted several
         // (t_multi, set on the device) turns it off and every record is placed by (t_off, rank) instead
         hipLaunchKernelGGL(k_gen_order<true>, dim3(nt), dim3(256), 0, e->stream, e->raw, e->t_cnt, e->t_off, e->t_first,
-                           e->tile_off, n, e->out, (const uint32_t*)e->t_multi, (const unsigned long long*)e->obase);
+                           e->tile_pre, e->sup_off, n, e->out, (const uint32_t*)e->t_multi,
+                           (const unsigned long long*)e->obase);
         hipLaunchKernelGGL(k_gen_scatter, dim3(scat_grid), dim3(256), 0, e->stream, e->raw, e->raw_count,
                            e->rawCap / GEN_RAWSEG, (uint32_t)GEN_RAWSEG, e->t_off, e->out, (const uint32_t*)e->t_multi,
                            (const unsigned long long*)e->obase);
     } else {
         hipLaunchKernelGGL(k_gen_order<false>, dim3(nt), dim3(256), 0, e->stream, e->raw, e->t_cnt, e->t_off, e->t_first,
-                           e->tile_off, n, e->out, (const uint32_t*)e->t_multi, (const unsigned long long*)e->obase);
+                           e->tile_pre, e->sup_off, n, e->out, (const uint32_t*)e->t_multi,
+                           (const unsigned long long*)e->obase);
         hipLaunchKernelGGL(k_gen_scatter, dim3((unsigned)std::min<uint64_t>((maxRaw + 255) / 256, 4096)), dim3(256), 0,
                            e->stream, e->raw, e->raw_count, e->rawCap / GEN_RAWSEG, (uint32_t)GEN_RAWSEG, e->t_off, e->out,
                            (const uint32_t*)nullptr, (const unsigned long long*)e->obase);
@@ -1951,16 +1975,14 @@ int gen_advance(GenEngine* e, int64_t t, std::string& msg) {
 
 int gen_poll(GenEngine* e, uint32_t mem, sg_match_batch* out, std::string& msg) {
     if (e->held) { msg = "previous matches not released"; return SG_ERR_STATE; }
-    // the count, the error word and the largest tile in one launch into pinned host memory (three copies were
-    // three blit launches); the count is reset there for the next window unless this poll fails
-    if (!e->h_stat) {
-        GH_OK(hipHostMalloc((void**)&e->h_stat, 4 * sizeof(unsigned long long), hipHostMallocMapped));
-        GH_OK(hipHostGetDevicePointer((void**)&e->d_stat, e->h_stat, 0));
-    }
+    // the count, the error word and the largest tile gathered by one launch and copied to the host at once (three
+    // copies were three blit launches); the count is reset there for the next window unless this poll fails
+    if (!e->d_stat) e->d_stat = e->dalloc<unsigned long long>(4);
     hipLaunchKernelGGL(k_gen_status, dim3(1), dim3(64), 0, e->stream, e->out.count, (const uint32_t*)e->err,
                        (const uint32_t*)e->tile_max, e->out.cap,
                        (uint32_t)(GERR_KEY | GERR_CAP | GERR_MATCHCAP | GERR_CHAIN | GERR_REF), e->d_stat);
     GH_OK(hipGetLastError());
+    GH_OK(hipMemcpyAsync(e->h_stat, e->d_stat, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, e->stream));
     GH_OK(hipStreamSynchronize(e->stream));
     const unsigned long long n = e->h_stat[0];
     const uint32_t err = (uint32_t)e->h_stat[1];
