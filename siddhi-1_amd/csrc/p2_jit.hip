@@ -117,6 +117,9 @@ template <class A, class B> struct SgSel<false, A, B> { typedef B type; };
 #include "sgq_query.h"
 
 #define R SGQ_R
+#ifndef SGQ_RH
+#define SGQ_RH SGQ_R  // the HBM pass's register window (keys the staged pass stopped: often more partials)
+#endif
 // the hot-key pipeline (k_hot_*, end of file) exists for `every e1 -> e2` with both states on one stream
 #if SGQ_MULTI && SGQ_MODE == 1  // (SGD_P2_EVERY_FIRST: an enum, invisible to #if)
 #define SG_HOT 1
@@ -296,14 +299,14 @@ struct Slab {
 // OFF (the staged pass): timestamps and seqs are held as 32-bit offsets from a per-launch base (half
 // the registers and VALU of 64-bit values); ts -1 (eventTimeComparator's "unset") never occurs there
 // (such keys stop and go to the HBM pass), so the ts order is a plain compare.
-template <bool OFF> struct Win {
+template <bool OFF, int RR> struct Win {
     typedef typename SgSel<OFF, int32_t, int64_t>::type TS;
     typedef typename SgSel<OFF, int32_t, uint64_t>::type SQ;
     __device__ __forceinline__ static bool lt(TS a, TS b) { return OFF ? a < b : ts_before((int64_t)a, (int64_t)b); }
-    TS ts[R];
-    SQ seq[R];
-    uint32_t cw[R][SGQ_NCAPW > 0 ? SGQ_NCAPW : 1];
-    uint32_t cn[R];
+    TS ts[RR];
+    SQ seq[RR];
+    uint32_t cw[RR][SGQ_NCAPW > 0 ? SGQ_NCAPW : 1];
+    uint32_t cn[RR];
     uint32_t live;  // slot holds a partial
     uint32_t stg;   // subset of live: staged (pre1's newAndEvery list), all above the pending slots
     uint32_t tail;  // appends go here (one past the highest live slot)
@@ -320,18 +323,18 @@ template <bool OFF> struct Win {
     __device__ __forceinline__ void fix_tail() { tail = live ? 32u - __clz(live) : 0u; }
 
     // close the holes, keeping slot order: every live slot moves down by the number of free
-    // slots below it, in log2(R) collision-free steps of 1, 2, 4, ... (static register indices)
+    // slots below it, in log2(RR) collision-free steps of 1, 2, 4, ... (static register indices)
     __device__ __forceinline__ void compact() {
         if ((live & (live + 1u)) == 0u) { tail = __popc(live); return; }  // already a prefix
-        uint32_t d[R];
+        uint32_t d[RR];
 #pragma unroll
-        for (int j = 0; j < R; ++j) d[j] = __popc(~live & ((1u << j) - 1u));
+        for (int j = 0; j < RR; ++j) d[j] = __popc(~live & ((1u << j) - 1u));
         uint32_t cur = live;
 #pragma unroll
-        for (int s = 0; (1 << s) < R; ++s) {
+        for (int s = 0; (1 << s) < RR; ++s) {
             const int sh = 1 << s;
 #pragma unroll
-            for (int j = sh; j < R; ++j) {
+            for (int j = sh; j < RR; ++j) {
                 const bool mv = ((cur >> j) & 1u) && ((d[j] >> s) & 1u);
                 if (mv) {
                     copy_slot(j - sh, j);
@@ -351,9 +354,9 @@ template <bool OFF> struct Win {
         compact();
         const uint32_t n = tail, lo = n - __popc(stg);
 #pragma unroll
-        for (int pass = 0; pass < R - 1; ++pass) {
+        for (int pass = 0; pass < RR - 1; ++pass) {
 #pragma unroll
-            for (int j = 0; j + 1 < R; ++j) {
+            for (int j = 0; j + 1 < RR; ++j) {
                 if ((uint32_t)j >= lo && (uint32_t)(j + 1) < n && lt(ts[j + 1], ts[j])) {
                     TS t = ts[j]; ts[j] = ts[j + 1]; ts[j + 1] = t;
                     SQ q = seq[j]; seq[j] = seq[j + 1]; seq[j + 1] = q;
@@ -646,7 +649,7 @@ __device__ __forceinline__ uint32_t wave_max_u(uint32_t x) {
 // kernels, so the staged walk carries no global load and no vmcnt wait behind the match stores.
 // gid: the lane's global index (key): blockIdx.x * SGD_BLOCK + threadIdx.x in the staged pass; the HBM pass
 // runs one wave per work-group over the list of deferred waves (gid = wave * 64 + lane)
-template <bool S0, bool S1, bool STG>
+template <bool S0, bool S1, bool STG, int RR, bool KL = false>
 __device__ __forceinline__ void advance(const P2Params& p, const uint32_t gid) {
     typedef typename SgSel<S0, SgEv0, SgEv1>::type Ev;
     constexpr int STRIDE = S0 ? SGQ_STRIDE0 : SGQ_STRIDE1;
@@ -654,7 +657,8 @@ __device__ __forceinline__ void advance(const P2Params& p, const uint32_t gid) {
     constexpr uint32_t NW = SGD_BLOCK / SGD_WAVE;
     const int lane = threadIdx.x & (SGD_WAVE - 1);
     const uint32_t wv = threadIdx.x / SGD_WAVE;
-    const uint32_t k = gid;
+    // KL (the HBM pass over the stopped keys): lane gid takes the gid-th listed key (none past the list's end)
+    const uint32_t k = KL ? (gid < p.dlist_n[1] ? p.klist[gid] : 0xffffffffu) : gid;
     const uint32_t K = p.n_keys;
     // round trip 1: the key's segment of the sorted batch and its header (independent loads)
     const uint32_t wave_id = gid / SGD_WAVE;
@@ -744,7 +748,7 @@ __device__ __forceinline__ void advance(const P2Params& p, const uint32_t gid) {
     }
     bool count_key = true;  // this pass owns the key's keys_touched / live_at_batch_start counts
     if constexpr (!STG) {
-        dfr = uni(p.deferred[wave_id]);  // 1: the whole wave; 2: the keys with a resume point
+        dfr = KL ? 2u : uni(p.deferred[wave_id]);  // 1: the whole wave; 2: the keys with a resume point
         if (dfr == 0u) return;
         if (k < K) rsm = p.resume[k];
         if (rsm == SGD_HOT_DONE) {  // advanced by the hot-key pipeline
@@ -818,7 +822,7 @@ __device__ __forceinline__ void advance(const P2Params& p, const uint32_t gid) {
     const uint32_t n0 = s.gnp + s.gns;
     const unsigned long long st_live0 = (nev > 0 && count_key) ? (unsigned long long)n0 : 0ull;
     const Slab G{p.p_ts + k, p.p_seq + k, p.p_capw + k, p.p_capnull + k, K, (size_t)p.cap * K};
-    bool hbm = n0 > (uint32_t)R;
+    bool hbm = n0 > (uint32_t)RR;
     // events of the run this pass walks (the staged pass may stop a key early: resume point `rs`)
     int run = hot ? 0 : nev;
     uint32_t rs = (hot && fits) ? 0u : SGD_NO_RESUME;  // (a hot key resumes from 0 if the pipeline gives it back)
@@ -838,13 +842,13 @@ __device__ __forceinline__ void advance(const P2Params& p, const uint32_t gid) {
     const int64_t obase = p.ts_col[0];
     const int64_t tbase = STG ? obase : 0;
     const uint64_t sbase = STG ? p.seq_base : 0;
-    Win<STG> W;
-    typedef typename Win<STG>::TS WTS;
-    typedef typename Win<STG>::SQ WSQ;
+    Win<STG, RR> W;
+    typedef typename Win<STG, RR>::TS WTS;
+    typedef typename Win<STG, RR>::SQ WSQ;
     bool far = false;
     W.live = 0; W.stg = 0; W.tail = 0;
 #pragma unroll
-    for (int j = 0; j < R; ++j) {
+    for (int j = 0; j < RR; ++j) {
         const bool ld = run > 0 && !hbm && (uint32_t)j < n0;
         const int64_t t = ld ? G.TS(j) : 0;
         const uint64_t q = ld ? G.SEQ(j) : 0;
@@ -880,7 +884,7 @@ __device__ __forceinline__ void advance(const P2Params& p, const uint32_t gid) {
         if constexpr (BOUNDED && STG) {
             // the wave's events + 64 R window partials bound its matches: [rlo + w*64R, ...) is disjoint
             // from every other wave's range
-            chunk_base = (unsigned long long)rlo + (unsigned long long)wave_id * (unsigned long long)(SGD_WAVE * R);
+            chunk_base = (unsigned long long)rlo + (unsigned long long)wave_id * (unsigned long long)(SGD_WAVE * RR);
         } else if constexpr (BOUNDED) {
             const uint32_t bound = nev > 0 ? n0 + (S0 ? (uint32_t)nev : 0u) : 0u;
             const uint32_t wb = (uint32_t)wave_sum((unsigned long long)bound);
@@ -956,7 +960,7 @@ __device__ __forceinline__ void advance(const P2Params& p, const uint32_t gid) {
             // the partials this event can add: every start seed fires at most once (+1: the
             // withinEvery re-arm of `every (e1 -> e2)`); stop here if the window could overflow, or
             // if the event's timestamp is outside the range of the band expiry test
-            if (act && (__popc(W.live) + s.spend + s.sstg + ((SGQ_MODE & SGD_P2_EVERY_BOTH) ? 1u : 0u) > (uint32_t)R ||
+            if (act && (__popc(W.live) + s.spend + s.sstg + ((SGQ_MODE & SGD_P2_EVERY_BOTH) ? 1u : 0u) > (uint32_t)RR ||
                         (int32_t)cur.w[STRIDE - 1] == SGD_TS_FAR || cur.w[0] > 0x7fffffffu)) {
                 rs = (uint32_t)it;
                 run = it;
@@ -984,10 +988,10 @@ __device__ __forceinline__ void advance(const P2Params& p, const uint32_t gid) {
                         const int32_t tn = toff, w32 = (int32_t)within;
                         const int32_t lo = tn - w32, hi = tn + w32;
 #pragma unroll
-                        for (int j = 0; j < R; ++j) X |= (((W.ts[j] < lo) | (W.ts[j] > hi)) ? 1u : 0u) << j;
+                        for (int j = 0; j < RR; ++j) X |= (((W.ts[j] < lo) | (W.ts[j] > hi)) ? 1u : 0u) << j;
                     } else {
 #pragma unroll
-                        for (int j = 0; j < R; ++j) X |= (expired((int64_t)W.ts[j], ts, within) ? 1u : 0u) << j;
+                        for (int j = 0; j < RR; ++j) X |= (expired((int64_t)W.ts[j], ts, within) ? 1u : 0u) << j;
                     }
                     X &= W.live;
                     if (X) {
@@ -1029,11 +1033,11 @@ __device__ __forceinline__ void advance(const P2Params& p, const uint32_t gid) {
                     const uint32_t P = W.live & ~W.stg;
                     if (SGX_BRANCHLESS) {
 #pragma unroll
-                        for (int j = 0; j < R; ++j) H |= (sgq_f1(ev, W.cw[j], W.cn[j], p) ? 1u : 0u) << j;
+                        for (int j = 0; j < RR; ++j) H |= (sgq_f1(ev, W.cw[j], W.cn[j], p) ? 1u : 0u) << j;
                         H &= P;
                     } else {
 #pragma unroll
-                        for (int j = 0; j < R; ++j) {
+                        for (int j = 0; j < RR; ++j) {
                             if (((P >> j) & 1u) && sgq_f1(ev, W.cw[j], W.cn[j], p)) H |= 1u << j;
                         }
                     }
@@ -1087,7 +1091,7 @@ __device__ __forceinline__ void advance(const P2Params& p, const uint32_t gid) {
                             for (int w = 0; w < SGQ_NCAPW; ++w) cw[w] = 0;
 #endif
 #pragma unroll
-                            for (int j = 0; j < R; ++j) {
+                            for (int j = 0; j < RR; ++j) {
                                 const bool here = j == jj;
                                 sq = here ? W.seq[j] : sq;
 #if SGQ_PROJ
@@ -1114,7 +1118,7 @@ __device__ __forceinline__ void advance(const P2Params& p, const uint32_t gid) {
                     W.fix_tail();
                 } else if (!GLB || !hbm) {
 #pragma unroll
-                    for (int j = 0; j < R; ++j) {
+                    for (int j = 0; j < RR; ++j) {
                         if ((H >> j) & 1u) {
                             if (!SGX_NO_RAW && pos < p.raw_capacity) {
                                 p.raw_e1[pos] = sbase + (uint64_t)(int64_t)W.seq[j];
@@ -1157,12 +1161,12 @@ __device__ __forceinline__ void advance(const P2Params& p, const uint32_t gid) {
                     sgq_capture(ev, cw, cn);
                     const uint64_t seq = p.seq_base + bi;
                     for (uint32_t q = 0; q < s.spend; ++q) {
-                        if ((!GLB || !hbm) && W.tail >= (uint32_t)R) W.compact();
-                        if (!GLB && W.tail >= (uint32_t)R) { overflow = true; break; }  // excluded by the stop rule
-                        if (GLB && !hbm && W.tail >= (uint32_t)R) {
+                        if ((!GLB || !hbm) && W.tail >= (uint32_t)RR) W.compact();
+                        if (!GLB && W.tail >= (uint32_t)RR) { overflow = true; break; }  // excluded by the stop rule
+                        if (GLB && !hbm && W.tail >= (uint32_t)RR) {
                             // the window is full of live partials: move the list to the HBM slab
 #pragma unroll
-                            for (int j = 0; j < R; ++j) {
+                            for (int j = 0; j < RR; ++j) {
                                 G.TS(j) = tbase + (int64_t)W.ts[j];
                                 G.SEQ(j) = sbase + (uint64_t)(int64_t)W.seq[j];
 #pragma unroll
@@ -1170,14 +1174,14 @@ __device__ __forceinline__ void advance(const P2Params& p, const uint32_t gid) {
                                 if (SGQ_CAPNULL) G.NUL(j) = W.cn[j];
                             }
                             s.gns = __popc(W.stg);
-                            s.gnp = R - s.gns;
+                            s.gnp = RR - s.gns;
                             hbm = true;
                             spills++;
                         }
                         if (!GLB || !hbm) {
                             const uint32_t t = W.tail;
 #pragma unroll
-                            for (int j = 0; j < R; ++j) {
+                            for (int j = 0; j < RR; ++j) {
                                 if ((uint32_t)j == t) {
                                     W.ts[j] = (WTS)(ts - tbase);
                                     W.seq[j] = (WSQ)(seq - sbase);
@@ -1187,7 +1191,7 @@ __device__ __forceinline__ void advance(const P2Params& p, const uint32_t gid) {
                                 }
                             }
                             const WTS to = (WTS)(ts - tbase);
-                            if (W.stg && Win<STG>::lt(to, W.slast)) W.sbad = true;
+                            if (W.stg && Win<STG, RR>::lt(to, W.slast)) W.sbad = true;
                             W.slast = to;
                             W.live |= 1u << t;
                             W.stg |= 1u << t;
@@ -1235,8 +1239,16 @@ __device__ __forceinline__ void advance(const P2Params& p, const uint32_t gid) {
         p.resume[k] = rs;
         p.deferred[wave_id] = 2u;
     }
-    if constexpr (STG) {  // a wave with resumed keys joins the HBM pass's list (once)
-        if (__ballot(rs != SGD_NO_RESUME) != 0ull && lane == 0) p.dlist[atomicAdd(p.dlist_n, 1u)] = wave_id;
+    if constexpr (STG) {  // the resumed keys join the HBM pass's key list (one reservation per wave)
+        const uint64_t rb = __ballot(rs != SGD_NO_RESUME);
+        if (rb && !p.klist) {
+            if (lane == 0) p.dlist[atomicAdd(p.dlist_n, 1u)] = wave_id;
+        } else if (rb) {
+            uint32_t base = 0;
+            if (lane == 0) base = atomicAdd(&p.dlist_n[1], (uint32_t)__popcll(rb));
+            base = (uint32_t)__shfl((int)base, 0, SGD_WAVE);
+            if (rs != SGD_NO_RESUME) p.klist[base + lane_rank(rb)] = k;
+        }
     }
     if (run > 0) {
         uint32_t np, ns;
@@ -1244,7 +1256,7 @@ __device__ __forceinline__ void advance(const P2Params& p, const uint32_t gid) {
             W.compact();
             const uint32_t n = W.tail;
 #pragma unroll
-            for (int j = 0; j < R; ++j) {
+            for (int j = 0; j < RR; ++j) {
                 if ((uint32_t)j < n) {
                     G.TS(j) = tbase + (int64_t)W.ts[j];
                     G.SEQ(j) = sbase + (uint64_t)(int64_t)W.seq[j];
@@ -1312,6 +1324,13 @@ __device__ __forceinline__ void pack(const PackParams& q) {
 #define SGQ_WAVES 2
 #endif
 #define SGQ_OCC __attribute__((amdgpu_waves_per_eu(SGQ_WAVES, 8)))
+// the HBM pass with a window wider than the staged pass's: one wave per SIMD may hold it all in registers (its few
+// waves walk the keys the staged pass stopped, where the slab walk's dependent HBM loads per partial were the cost)
+#if SGQ_RH > SGQ_R
+#define SGQ_OCC_H __attribute__((amdgpu_waves_per_eu(1, 8)))
+#else
+#define SGQ_OCC_H SGQ_OCC
+#endif
 // k_adv_*: the staged pass; k_adv_*_h: the HBM pass over the waves the staged pass deferred
 // the HBM pass: one wave per work-group, striding over the waves the staged pass listed (p.dlist: the
 // workgroups whose range did not fit LDS, the waves with resumed keys), so a batch with few of them
@@ -1327,18 +1346,22 @@ template <bool S0, bool S1> __device__ __forceinline__ void hbm_pass(const P2Par
     }
     for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
         const uint32_t w = __builtin_amdgcn_readfirstlane(p.dlist[i]);
-        advance<S0, S1, false>(p, w * SGD_WAVE + threadIdx.x);
+        advance<S0, S1, false, SGQ_RH>(p, w * SGD_WAVE + threadIdx.x);
     }
+    // the keys the staged pass stopped, 64 to a wave
+    const uint32_t nk = p.klist ? __builtin_amdgcn_readfirstlane(p.dlist_n[1]) : 0u;
+    for (uint32_t i = blockIdx.x; i * SGD_WAVE < nk; i += gridDim.x)
+        advance<S0, S1, false, SGQ_RH, true>(p, i * SGD_WAVE + threadIdx.x);
 }
 #define SG_GID (blockIdx.x * SGD_BLOCK + threadIdx.x)
 #if SGQ_MULTI
-extern "C" __global__ void __launch_bounds__(SGD_BLOCK) SGQ_OCC k_adv_m(const P2Params p) { advance<true, true, true>(p, SG_GID); }
-extern "C" __global__ void __launch_bounds__(SGD_WAVE) SGQ_OCC k_adv_m_h(const P2Params p) { hbm_pass<true, true>(p); }
+extern "C" __global__ void __launch_bounds__(SGD_BLOCK) SGQ_OCC k_adv_m(const P2Params p) { advance<true, true, true, SGQ_R>(p, SG_GID); }
+extern "C" __global__ void __launch_bounds__(SGD_WAVE) SGQ_OCC_H k_adv_m_h(const P2Params p) { hbm_pass<true, true>(p); }
 #else
-extern "C" __global__ void __launch_bounds__(SGD_BLOCK) SGQ_OCC k_adv_s0(const P2Params p) { advance<true, false, true>(p, SG_GID); }
-extern "C" __global__ void __launch_bounds__(SGD_BLOCK) SGQ_OCC k_adv_s1(const P2Params p) { advance<false, true, true>(p, SG_GID); }
-extern "C" __global__ void __launch_bounds__(SGD_WAVE) SGQ_OCC k_adv_s0_h(const P2Params p) { hbm_pass<true, false>(p); }
-extern "C" __global__ void __launch_bounds__(SGD_WAVE) SGQ_OCC k_adv_s1_h(const P2Params p) { hbm_pass<false, true>(p); }
+extern "C" __global__ void __launch_bounds__(SGD_BLOCK) SGQ_OCC k_adv_s0(const P2Params p) { advance<true, false, true, SGQ_R>(p, SG_GID); }
+extern "C" __global__ void __launch_bounds__(SGD_BLOCK) SGQ_OCC k_adv_s1(const P2Params p) { advance<false, true, true, SGQ_R>(p, SG_GID); }
+extern "C" __global__ void __launch_bounds__(SGD_WAVE) SGQ_OCC_H k_adv_s0_h(const P2Params p) { hbm_pass<true, false>(p); }
+extern "C" __global__ void __launch_bounds__(SGD_WAVE) SGQ_OCC_H k_adv_s1_h(const P2Params p) { hbm_pass<false, true>(p); }
 #endif
 extern "C" __global__ void __launch_bounds__(256) k_pack0(const PackParams q) { pack<SGQ_STRIDE0, 0>(q); }
 extern "C" __global__ void __launch_bounds__(256) k_pack1(const PackParams q) { pack<SGQ_STRIDE1, 1>(q); }
@@ -1366,6 +1389,7 @@ extern "C" __global__ void __launch_bounds__(256) k_pack1(const PackParams q) { 
 #if SG_HOT
 #define SGD_HOT_C 256u     // round 0: events per workgroup
 #define SGD_HOT_L0 128u    // round 0: events each partial scans (staged in LDS after the workgroup's)
+#define SGD_HOT_R0A 16u    // round 0: of them, the events a lane scans for its own partial (then a wave per partial)
 #define SGD_HOT_L1 512u    // round 1: events each open partial scans; rounds >= 2: x8 per round
 #define SGD_HOT_G 16u      // elements per thread of the list / reservation kernels (one atomic per 4096)
 #define SGD_HOT_FILL 4096u // k_hot_fill: run events per workgroup pass
@@ -1441,15 +1465,31 @@ __device__ __forceinline__ uint32_t hot_test(const P2Params& p, const HotPart& P
     if (SGQ_WITHIN && expired(P.ts, hot_ts(p, x, obase), p.within)) return i * 2u;
     return sgq_f1(sgq_ev1(x.w), P.cw, P.cn, p) ? i * 2u + 1u : HOT_LIVE;
 }
-// a wave scans events [lo, end) of a run for partial P, 64 at a time: the first that ends it, or HOT_LIVE
+// a wave scans events [lo, end) of a run for partial P, 64 at a time: the first that ends it, or HOT_LIVE.  The
+// payload of SGD_HOT_SB consecutive 64-event chunks is loaded at once (one round trip per 256 events instead of
+// one per 64: the partials scanned here are the long-lived ones)
+#define SGD_HOT_SB 4
 __device__ __forceinline__ uint32_t hot_wave_scan(const P2Params& p, const HotPart& P, uint32_t b, uint32_t lo,
                                                   uint32_t end, int64_t obase) {
     const uint32_t lane = threadIdx.x & (SGD_WAVE - 1);
-    for (uint32_t i0 = lo; i0 < end; i0 += SGD_WAVE) {
-        const uint32_t i = i0 + lane;
-        const uint32_t c = i < end ? hot_test(p, P, b + i, i, obase) : HOT_LIVE;
-        const uint64_t hit = __ballot(c != HOT_LIVE);
-        if (hit) return (uint32_t)__shfl((int)c, __builtin_ctzll(hit), SGD_WAVE);
+    for (uint32_t i0 = lo; i0 < end; i0 += SGD_WAVE * SGD_HOT_SB) {
+        PayEl<HST> x[SGD_HOT_SB];
+#pragma unroll
+        for (int u = 0; u < SGD_HOT_SB; ++u) {
+            const uint32_t i = i0 + (uint32_t)u * SGD_WAVE + lane;
+            if (i < end) x[u] = load_pay<HST>(p.payload, b + i);
+        }
+#pragma unroll
+        for (int u = 0; u < SGD_HOT_SB; ++u) {
+            const uint32_t i = i0 + (uint32_t)u * SGD_WAVE + lane;
+            uint32_t c = HOT_LIVE;
+            if (i < end) {
+                if (SGQ_WITHIN && expired(P.ts, hot_ts(p, x[u], obase), p.within)) c = i * 2u;
+                else if (sgq_f1(sgq_ev1(x[u].w), P.cw, P.cn, p)) c = i * 2u + 1u;
+            }
+            const uint64_t hit = __ballot(c != HOT_LIVE);
+            if (hit) return (uint32_t)__shfl((int)c, __builtin_ctzll(hit), SGD_WAVE);
+        }
     }
     return HOT_LIVE;
 }
@@ -1603,6 +1643,8 @@ extern "C" __global__ void __launch_bounds__(SGD_HOT_C) k_hot_r0(const P2Params 
     constexpr uint32_t ST = SGD_HOT_C + SGD_HOT_L0;
     __shared__ uint32_t s_w[ST * HST];
     __shared__ int64_t s_ts[ST];
+    __shared__ uint32_t s_open[SGD_HOT_C], s_oi[SGD_HOT_C], s_onj[SGD_HOT_C], s_nopen;
+    const uint32_t lane = tid & (SGD_WAVE - 1), wv = tid / SGD_WAVE;
     for (uint32_t x0 = nex + blockIdx.x * SGD_HOT_C; x0 < total; x0 += gridDim.x * SGD_HOT_C) {
         uint32_t h = 0, pos = 0, i = 0, m = 0;
         for (uint32_t t = tid; t < ST; t += SGD_HOT_C) {
@@ -1623,6 +1665,7 @@ extern "C" __global__ void __launch_bounds__(SGD_HOT_C) k_hot_r0(const P2Params 
                 p.hot_fbi[x - nex] = ev.w[0];
             }
         }
+        if (tid == 0) s_nopen = 0u;
         __syncthreads();
         const uint32_t x = x0 + tid;
         if (x < total) {
@@ -1641,15 +1684,52 @@ extern "C" __global__ void __launch_bounds__(SGD_HOT_C) k_hot_r0(const P2Params 
                 sgq_capture(e0, P.cw, P.cn);
                 d = HOT_LIVE;
                 const uint32_t nj = min(m - 1u - i, SGD_HOT_L0);
-                for (uint32_t j = 1; j <= nj && d == HOT_LIVE; ++j) {
+                // the first SGD_HOT_R0A events a lane each (most partials end there); the rest of the window below,
+                // a wave per partial still open (a lane-per-partial scan ran every wave to its longest scan)
+                const uint32_t na = min(nj, SGD_HOT_R0A);
+                for (uint32_t j = 1; j <= na && d == HOT_LIVE; ++j) {
                     const uint32_t t = tid + j;
                     if (SGQ_WITHIN && expired(P.ts, s_ts[t], p.within)) d = (i + j) * 2u;
                     else if (sgq_f1(sgq_ev1(&s_w[t * HST]), P.cw, P.cn, p)) d = (i + j) * 2u + 1u;
                 }
                 cur = i + 1u + nj;
+                if (d == HOT_LIVE && nj > na) {  // (its death word is written by the wave that finishes it)
+                    const uint32_t o = atomicAdd(&s_nopen, 1u);
+                    s_open[o] = tid;
+                    s_oi[o] = i;
+                    s_onj[o] = nj;
+                    d = HOT_NOTP - 1u;  // (marker: not written here)
+                }
             }
-            p.hot_death[x] = d;
+            if (d != HOT_NOTP - 1u) p.hot_death[x] = d;
             p.hot_cur[x] = cur;
+        }
+        __syncthreads();
+        const uint32_t no = s_nopen;
+        for (uint32_t q = wv; q < no; q += SGD_HOT_C / SGD_WAVE) {
+            const uint32_t tq = s_open[q], iq = s_oi[q], njq = s_onj[q];
+            HotPart P;
+            P.ts = s_ts[tq];
+            P.cn = 0;
+#pragma unroll
+            for (int w = 0; w < (SGQ_NCAPW > 0 ? SGQ_NCAPW : 1); ++w) P.cw[w] = 0;
+            sgq_capture(sgq_ev0(&s_w[tq * HST]), P.cw, P.cn);
+            uint32_t d = HOT_LIVE;
+            for (uint32_t j0 = SGD_HOT_R0A + 1u; j0 <= njq; j0 += SGD_WAVE) {
+                const uint32_t j = j0 + lane;
+                uint32_t c = HOT_LIVE;
+                if (j <= njq) {
+                    const uint32_t t = tq + j;
+                    if (SGQ_WITHIN && expired(P.ts, s_ts[t], p.within)) c = (iq + j) * 2u;
+                    else if (sgq_f1(sgq_ev1(&s_w[t * HST]), P.cw, P.cn, p)) c = (iq + j) * 2u + 1u;
+                }
+                const uint64_t hit = __ballot(c != HOT_LIVE);
+                if (hit) {
+                    d = (uint32_t)__shfl((int)c, __builtin_ctzll(hit), SGD_WAVE);
+                    break;
+                }
+            }
+            if (lane == 0) p.hot_death[x0 + tq] = d;
         }
         __syncthreads();
     }

@@ -322,7 +322,8 @@ __global__ void __launch_bounds__(256) k_stats_reduce(const unsigned long long* 
                                                       uint32_t* __restrict__ dlist_n) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {  // the next advance's atomic slot counter and HBM-pass list
         *raw_count = 0;
-        *dlist_n = 0;
+        dlist_n[0] = 0;
+        dlist_n[1] = 0;
     }
     __shared__ unsigned long long part[SGD_ST_N][4];
     unsigned long long acc[SGD_ST_N];

@@ -22,6 +22,7 @@
 #define SGD_MAX_CAPS 8     // slot-0 attributes captured into a partial match
 #define SGD_MAX_CONST 32   // filter constants (kernel arguments, so equal-shaped queries share code)
 #define SGD_MAX_REG 16     // register window (partials per lane) upper bound
+#define SGD_MAX_REG_HBM 31 // the HBM pass's register window upper bound (a 32-bit slot mask, shifts by n < 32)
 #define SGD_WAVE 64
 #ifndef SGD_BLOCK
 #define SGD_BLOCK 256      // lanes (= keys) per workgroup of the advance kernel
@@ -132,7 +133,9 @@ struct P2Params {
     uint32_t* deferred;                // [n_keys / 64] waves the staged pass left to the HBM pass:
                                        // 1 = the whole wave, 2 = the keys with a resume point
     uint32_t* dlist;                   // [n_keys / 64] the waves the HBM pass takes (appended by the staged pass)
-    uint32_t* dlist_n;                 // their number (reset after the batch by k_stats_reduce)
+    uint32_t* dlist_n;                 // [2] their number, then klist's (reset after the batch by k_stats_reduce)
+    uint32_t* klist;                   // [n_keys] the keys the staged pass stopped (the HBM pass resumes them, a
+                                       // lane each: a wave of them, not the waves they sit in)
     uint32_t* resume;                  // [n_keys] event index (in the key's run) where the HBM pass
                                        // resumes a key the staged pass stopped; SGD_NO_RESUME otherwise
     unsigned long long* prof;          // SGX_PROF experiments only (NULL otherwise)

@@ -205,6 +205,7 @@ struct sg_engine {
     uint32_t hbm_grid = 2048;      // work-groups of the HBM pass (SG_HBM_GRID: experiments)
     uint32_t* dlist = nullptr;     // the waves the HBM pass takes, and their number
     uint32_t* dlist_n = nullptr;
+    uint32_t* klist = nullptr;     // the keys the staged pass stopped (the HBM pass's lanes)
     uint32_t* tile_sum = nullptr;  // ordering: matches per tile of triggers, and its exclusive scan
     uint32_t* tile_off = nullptr;
     unsigned long long* out_count = nullptr;
@@ -258,6 +259,8 @@ struct sg_engine {
     PinnedVec<uint64_t> h_pval;
     PinnedVec<uint8_t> h_pnull;
     uint32_t reg_slots = 12;  // SGD_REG_SLOTS: partials per key held in registers by the advance kernel
+    uint32_t reg_slots_hbm = 16;  // SGD_REG_SLOTS_HBM: the HBM pass's window (the keys the staged pass stopped;
+                                  // 24 walks C2_walk 10 % faster but compiles 3.5x slower per query)
     uint32_t stage_override = 0;  // SGD_STAGE_CHUNKS: fixed LDS staging per wave (tests force the HBM path)
     uint64_t spills = 0;
 
@@ -557,9 +560,10 @@ void allocate(sg_engine* e) {
     e->deferred = dalloc<uint32_t>((K + SGD_BLOCK - 1) / SGD_BLOCK * (SGD_BLOCK / SGD_WAVE), o);
     e->resume = dalloc<uint32_t>(K, o);
     e->dlist = dalloc<uint32_t>((K + SGD_BLOCK - 1) / SGD_BLOCK * (SGD_BLOCK / SGD_WAVE), o);
-    e->dlist_n = dalloc<uint32_t>(1, o);  // zeroed here, then by k_stats_reduce after every advance
+    e->dlist_n = dalloc<uint32_t>(2, o);  // zeroed here, then by k_stats_reduce after every advance
+    e->klist = dalloc<uint32_t>(K, o);
     if (const char* x = getenv("SG_HBM_GRID")) e->hbm_grid = std::max(1u, (uint32_t)strtoul(x, nullptr, 0));
-    HIP_OK(hipMemsetAsync(e->dlist_n, 0, 4, e->stream));
+    HIP_OK(hipMemsetAsync(e->dlist_n, 0, 8, e->stream));
     if (getenv("SG_PROF")) {
         e->prof = dalloc<unsigned long long>(nw * 8, o);
         HIP_OK(hipMemsetAsync(e->prof, 0, nw * 64, e->stream));
@@ -622,6 +626,7 @@ JitQuery make_jit_query(sg_engine* e) {
     q.multi = pl.s0 == pl.s1;
     q.within = pl.within >= 0;
     q.reg_slots = e->reg_slots;
+    q.reg_slots_hbm = e->reg_slots_hbm;
     for (int r = 0; r < 2; r++) {
         const int s = r == 0 ? pl.s0 : pl.s1;
         for (uint32_t a : pl.evcols[s]) q.coltypes[r].push_back(e->streams[s].types[a]);
@@ -946,6 +951,7 @@ int push(sg_engine* e, const sg_batch* b) {
     p.resume = e->resume;
     p.dlist = e->dlist;
     p.dlist_n = e->dlist_n;
+    p.klist = getenv("SG_NO_KLIST") ? nullptr : e->klist;
     p.stats = e->stats;
     p.wstats = e->wstats;
     p.raw_static = e->raw_static;
@@ -1433,8 +1439,14 @@ int sg_engine_create(const void* ir, size_t ir_len, const sg_config* cfg, sg_eng
         e->cfg = *cfg;
         e->device = cfg->device;
         e->timing = (cfg->flags & SG_CFG_TIMING) != 0;
-        if (const char* d = getenv("SGD_REG_SLOTS")) e->reg_slots = (uint32_t)strtoul(d, nullptr, 0);
+        if (const char* d = getenv("SGD_REG_SLOTS")) {
+            e->reg_slots = (uint32_t)strtoul(d, nullptr, 0);
+            e->reg_slots_hbm = e->reg_slots;  // (a forced window: the HBM pass spills at the same size)
+        }
+        if (const char* d = getenv("SGD_REG_SLOTS_HBM")) e->reg_slots_hbm = (uint32_t)strtoul(d, nullptr, 0);
         if (e->reg_slots < 1 || e->reg_slots > SGD_MAX_REG) throw std::invalid_argument("SGD_REG_SLOTS out of [1, 16]");
+        if (e->reg_slots_hbm < 1 || e->reg_slots_hbm > SGD_MAX_REG_HBM)
+            throw std::invalid_argument("SGD_REG_SLOTS_HBM out of [1, 31]");
         if (const char* d = getenv("SGD_STAGE_CHUNKS")) e->stage_override = (uint32_t)strtoul(d, nullptr, 0);
         if (e->stage_override * 16ull * (SGD_BLOCK / SGD_WAVE) > SGD_STAGE_MAX_BYTES)
             throw std::invalid_argument("SGD_STAGE_CHUNKS above the LDS staging bound");
@@ -1446,6 +1458,7 @@ int sg_engine_create(const void* ir, size_t ir_len, const sg_config* cfg, sg_eng
         if (e->cap > SGD_MAX_CAP) throw std::invalid_argument("partial_capacity above 4095");
         // the register window never holds more partials than the key's slab can take when it spills
         if (e->reg_slots > e->cap) e->reg_slots = e->cap;
+        if (e->reg_slots_hbm > e->cap) e->reg_slots_hbm = e->cap;
         if (e->mcap >= (1ull << 31)) throw std::invalid_argument("match_capacity must be < 2^31");
         if (ir_len < SG_IR_HDR_WORDS * 4 || ir_len % 4) throw std::invalid_argument("IR too short");
         if (((const uint32_t*)ir)[0] != SG_IR_MAGIC || ((const uint32_t*)ir)[1] != SG_IR_VERSION)
@@ -2168,7 +2181,8 @@ int sg_jit_check(const void* ir, size_t ir_len, uint32_t variant_flags, char* ou
     try {
         e = new sg_engine();
         e->device = -1;
-        if (const char* d = getenv("SGD_REG_SLOTS")) e->reg_slots = (uint32_t)strtoul(d, nullptr, 0);
+        if (const char* d = getenv("SGD_REG_SLOTS")) e->reg_slots = e->reg_slots_hbm = (uint32_t)strtoul(d, nullptr, 0);
+        if (const char* d = getenv("SGD_REG_SLOTS_HBM")) e->reg_slots_hbm = (uint32_t)strtoul(d, nullptr, 0);
         build_plan(e, ir, ir_len);
         JitQuery q = make_jit_query(e);
         q.evnull = (variant_flags & 1u) != 0;

@@ -348,6 +348,9 @@ std::string sgj_generate(const JitQuery& q, std::vector<uint64_t>& consts) {
     }
 #endif
     o << "#define SGQ_R " << q.reg_slots << "\n";
+    const uint32_t rh = q.reg_slots_hbm ? q.reg_slots_hbm : q.reg_slots;
+    if (rh > SGD_MAX_REG_HBM) throw std::runtime_error("HBM-pass register window out of range");
+    o << "#define SGQ_RH " << rh << "\n";
     o << "#define SGQ_MODE " << q.mode << "\n";
     o << "#define SGQ_MULTI " << (q.multi ? 1 : 0) << "\n";
     o << "#define SGQ_WITHIN " << (q.within ? 1 : 0) << "\n";

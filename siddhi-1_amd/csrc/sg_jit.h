@@ -18,6 +18,7 @@ struct JitQuery {
     bool multi = false;                   // both states read the same stream
     bool within = false;
     uint32_t reg_slots = 12;              // SGQ_R
+    uint32_t reg_slots_hbm = 0;           // SGQ_RH (0: SGQ_R)
     std::vector<uint32_t> coltypes[2];    // types of the filter columns of stream s0 / s1
     const DProg* f0 = nullptr;
     const DProg* f1 = nullptr;
