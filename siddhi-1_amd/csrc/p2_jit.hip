@@ -1324,8 +1324,9 @@ __device__ __forceinline__ void pack(const PackParams& q) {
 #define SGQ_WAVES 2
 #endif
 #define SGQ_OCC __attribute__((amdgpu_waves_per_eu(SGQ_WAVES, 8)))
-// the HBM pass with a window wider than the staged pass's: one wave per SIMD may hold it all in registers (its few
-// waves walk the keys the staged pass stopped, where the slab walk's dependent HBM loads per partial were the cost)
+// the HBM pass over the stopped keys (k_adv_*_k), with a window wider than the staged pass's: one wave per SIMD may
+// hold it all in registers (its few waves walk the keys the staged pass stopped, where the slab walk's dependent HBM
+// loads per partial were the cost)
 #if SGQ_RH > SGQ_R
 #define SGQ_OCC_H __attribute__((amdgpu_waves_per_eu(1, 8)))
 #else
@@ -1346,9 +1347,11 @@ template <bool S0, bool S1> __device__ __forceinline__ void hbm_pass(const P2Par
     }
     for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
         const uint32_t w = __builtin_amdgcn_readfirstlane(p.dlist[i]);
-        advance<S0, S1, false, SGQ_RH>(p, w * SGD_WAVE + threadIdx.x);
+        advance<S0, S1, false, SGQ_R>(p, w * SGD_WAVE + threadIdx.x);
     }
-    // the keys the staged pass stopped, 64 to a wave
+}
+// the keys the staged pass stopped (p.klist), 64 to a wave, with the HBM pass's wider window
+template <bool S0, bool S1> __device__ __forceinline__ void hbm_keys(const P2Params& p) {
     const uint32_t nk = p.klist ? __builtin_amdgcn_readfirstlane(p.dlist_n[1]) : 0u;
     for (uint32_t i = blockIdx.x; i * SGD_WAVE < nk; i += gridDim.x)
         advance<S0, S1, false, SGQ_RH, true>(p, i * SGD_WAVE + threadIdx.x);
@@ -1356,12 +1359,15 @@ template <bool S0, bool S1> __device__ __forceinline__ void hbm_pass(const P2Par
 #define SG_GID (blockIdx.x * SGD_BLOCK + threadIdx.x)
 #if SGQ_MULTI
 extern "C" __global__ void __launch_bounds__(SGD_BLOCK) SGQ_OCC k_adv_m(const P2Params p) { advance<true, true, true, SGQ_R>(p, SG_GID); }
-extern "C" __global__ void __launch_bounds__(SGD_WAVE) SGQ_OCC_H k_adv_m_h(const P2Params p) { hbm_pass<true, true>(p); }
+extern "C" __global__ void __launch_bounds__(SGD_WAVE) SGQ_OCC k_adv_m_h(const P2Params p) { hbm_pass<true, true>(p); }
+extern "C" __global__ void __launch_bounds__(SGD_WAVE) SGQ_OCC_H k_adv_m_k(const P2Params p) { hbm_keys<true, true>(p); }
 #else
 extern "C" __global__ void __launch_bounds__(SGD_BLOCK) SGQ_OCC k_adv_s0(const P2Params p) { advance<true, false, true, SGQ_R>(p, SG_GID); }
 extern "C" __global__ void __launch_bounds__(SGD_BLOCK) SGQ_OCC k_adv_s1(const P2Params p) { advance<false, true, true, SGQ_R>(p, SG_GID); }
-extern "C" __global__ void __launch_bounds__(SGD_WAVE) SGQ_OCC_H k_adv_s0_h(const P2Params p) { hbm_pass<true, false>(p); }
-extern "C" __global__ void __launch_bounds__(SGD_WAVE) SGQ_OCC_H k_adv_s1_h(const P2Params p) { hbm_pass<false, true>(p); }
+extern "C" __global__ void __launch_bounds__(SGD_WAVE) SGQ_OCC k_adv_s0_h(const P2Params p) { hbm_pass<true, false>(p); }
+extern "C" __global__ void __launch_bounds__(SGD_WAVE) SGQ_OCC k_adv_s1_h(const P2Params p) { hbm_pass<false, true>(p); }
+extern "C" __global__ void __launch_bounds__(SGD_WAVE) SGQ_OCC_H k_adv_s0_k(const P2Params p) { hbm_keys<true, false>(p); }
+extern "C" __global__ void __launch_bounds__(SGD_WAVE) SGQ_OCC_H k_adv_s1_k(const P2Params p) { hbm_keys<false, true>(p); }
 #endif
 extern "C" __global__ void __launch_bounds__(256) k_pack0(const PackParams q) { pack<SGQ_STRIDE0, 0>(q); }
 extern "C" __global__ void __launch_bounds__(256) k_pack1(const PackParams q) { pack<SGQ_STRIDE1, 1>(q); }

@@ -134,6 +134,7 @@ struct sg_engine {
         hipModule_t mod = nullptr;
         hipFunction_t adv[2] = {nullptr, nullptr};   // [0]: multi / state-0 stream, [1]: state-1 stream
         hipFunction_t adv_h[2] = {nullptr, nullptr}; // the HBM pass over the waves the staged pass deferred
+        hipFunction_t adv_k[2] = {nullptr, nullptr}; // ... and over the keys it stopped (wider window)
         hipFunction_t pack[2] = {nullptr, nullptr};
         hipFunction_t hot[14] = {};                  // the hot-key pipeline (k_hot_prep .. k_hot_final_big)
         uint32_t adv_static_lds = 0;                 // the staged pass's static LDS (beside its dynamic staging)
@@ -658,6 +659,8 @@ sg_engine::Variant& variant(sg_engine* e, bool evnull, bool capnull) {
     if (q.multi) {
         HIP_OK(hipModuleGetFunction(&r.adv[0], r.mod, "k_adv_m"));
         HIP_OK(hipModuleGetFunction(&r.adv_h[0], r.mod, "k_adv_m_h"));
+        HIP_OK(hipModuleGetFunction(&r.adv_k[0], r.mod, "k_adv_m_k"));
+        r.adv_k[1] = r.adv_k[0];
         r.adv[1] = r.adv[0];
         r.adv_h[1] = r.adv_h[0];
     } else {
@@ -665,6 +668,8 @@ sg_engine::Variant& variant(sg_engine* e, bool evnull, bool capnull) {
         HIP_OK(hipModuleGetFunction(&r.adv[1], r.mod, "k_adv_s1"));
         HIP_OK(hipModuleGetFunction(&r.adv_h[0], r.mod, "k_adv_s0_h"));
         HIP_OK(hipModuleGetFunction(&r.adv_h[1], r.mod, "k_adv_s1_h"));
+        HIP_OK(hipModuleGetFunction(&r.adv_k[0], r.mod, "k_adv_s0_k"));
+        HIP_OK(hipModuleGetFunction(&r.adv_k[1], r.mod, "k_adv_s1_k"));
     }
     if (e->hot_ok) {
         static const char* const names[14] = {"k_hot_prep",  "k_hot_scan",  "k_hot_fill", "k_hot_r0",
@@ -1011,6 +1016,8 @@ int push(sg_engine* e, const sg_batch* b) {
         }
         // one wave per work-group over the listed waves (a fixed grid: the list's length is on the device)
         launch(v.adv_h[role], std::min<uint32_t>(blocks * (SGD_BLOCK / SGD_WAVE), e->hbm_grid), SGD_WAVE, &p, e->stream,
+               p.hbm_stage_chunks * 16u);
+        launch(v.adv_k[role], std::min<uint32_t>(blocks * (SGD_BLOCK / SGD_WAVE), e->hbm_grid), SGD_WAVE, &p, e->stream,
                p.hbm_stage_chunks * 16u);
         if (e->timing) { a1 = e->ev(); e->mark(a1); e->spans.push_back({a0, a1, 3}); }
         if (sgd_launch_stats_reduce(e->wstats, blocks * (SGD_BLOCK / SGD_WAVE), e->stats, e->raw_count, e->dlist_n, e->stream) != 0)
@@ -1746,7 +1753,7 @@ int sg_engine_describe(sg_engine* e, char* out, size_t out_len) {
                                "k_adv_m (NFA advance, LDS-staged, lane per key)") +
             (one->hot_batches ? " + k_hot_prep..k_hot_final (hot keys, partials in parallel, " +
                                     std::to_string(one->hot_batches) + " batches)" : std::string()) +
-            " + k_adv_m_h (NFA advance, HBM pass) + k_stats_reduce; k_order_sums + scan + k_order_scatter (ordering)";
+            " + k_adv_m_h / k_adv_m_k (NFA advance, HBM pass: the waves left whole / the keys stopped) + k_stats_reduce; k_order_sums + scan + k_order_scatter (ordering)";
         if (one->proj_n) d += " + k_project" + std::string(one->n_agg ? " + k_agg" : "");
     }
     if (e->shard) d = std::to_string(shd_count(e->shard)) + " shards, each " + d;
