@@ -2120,7 +2120,7 @@ extern "C" __global__ void __launch_bounds__(256) k_hot_final(const P2Params p) 
     const int64_t obase = p.ts_col[0];
     const uint32_t lane = threadIdx.x & (SGD_WAVE - 1), wv = threadIdx.x / SGD_WAVE;
     const uint32_t nw = gridDim.x * (blockDim.x / SGD_WAVE);
-    __shared__ uint32_t s_in[4][SGD_HOT_FW], s_ord[4][SGD_HOT_FW];
+    __shared__ uint32_t s_ord[4][SGD_HOT_FW];
     for (uint32_t h = blockIdx.x * (blockDim.x / SGD_WAVE) + wv; h < n; h += nw) {
         const uint32_t* hi = p.hot_info + (size_t)h * SGD_HOT_INFO;
         if (uni(hi[HI_BAD])) continue;  // left to the HBM pass
@@ -2134,17 +2134,31 @@ extern "C" __global__ void __launch_bounds__(256) k_hot_final(const P2Params p) 
         }
         if (na > SGD_HOT_FW) continue;  // (k_hot_final_big)
         const uint32_t* pool = p.hot_alive + hi[HI_ALOFF];
-        for (uint32_t a = lane; a < na; a += SGD_WAVE) s_in[wv][a] = pool[a];
+        // the survivors (listed in emit's atomic order) sorted by flat index — list order — with a bitonic network
+        // over the next power of two (padding sorts last): log^2 stages of 64-lane compare-exchanges instead of a
+        // rank count over all pairs
+        uint32_t np2 = 1;
+        while (np2 < na) np2 <<= 1;
+        uint32_t* so = s_ord[wv];
+        for (uint32_t a = lane; a < np2; a += SGD_WAVE) so[a] = a < na ? pool[a] : 0xffffffffu;
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
-        for (uint32_t a = lane; a < na; a += SGD_WAVE) {
-            const uint32_t xa = s_in[wv][a];
-            uint32_t r = 0;
-            for (uint32_t u = 0; u < na; ++u) r += s_in[wv][u] < xa ? 1u : 0u;
-            s_ord[wv][r] = xa;
+        for (uint32_t kk = 2; kk <= np2; kk <<= 1) {
+            for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
+                for (uint32_t i = lane; i < np2; i += SGD_WAVE) {
+                    const uint32_t ij = i ^ j;
+                    if (ij > i) {
+                        const uint32_t va = so[i], vb = so[ij];
+                        if ((va > vb) == ((i & kk) == 0u)) {
+                            so[i] = vb;
+                            so[ij] = va;
+                        }
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+            }
         }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
         const Slab G = hot_slab(p, hi[HI_KEY]);
         for (uint32_t c0 = 0; c0 < na; c0 += SGD_WAVE) {
             const uint32_t o = c0 + lane;
