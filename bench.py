@@ -713,6 +713,49 @@ def output_inclusive(sa, synth, torch, dev, n_keys, batch, steps):
                     "columns copied to host memory (sg_poll_matches + sg_get_projection to host)"}
 
 
+def fanout_one_gpu(sa, synth, torch, dev, cq, n_keys, batch, steps):
+    """The C-ABI's own multi-device fan-out (sg_config.n_devices, csrc/sg_sharded.cpp) rehearsed with two shards
+    on this one GPU, against the single engine on the same device batches with the same host polls (the fan-out
+    merges the shards' matches into host memory, so both legs poll to the host).  The shards share the GPU: the
+    ratio prices the fan-out's own work (the device split, the per-push host wait for the per-owner totals, the
+    host seq maps and merge), not a speed-up.  `host_syncs_per_push` = sg_stats.host_syncs / pushes."""
+    W = 2
+    bats = [synth.stock_ticks_torch(torch, s * batch, batch, n_keys, dev) for s in range(steps + W)]
+    torch.cuda.synchronize()
+    res = {}
+    for label, devs in (("single", None), ("fanout", [dev.index or 0] * 2)):
+        eng = sa.NativeEngine(sa.load_hip_library(), "sg_", cq.ir, n_keys=n_keys, max_batch=batch,
+                              partial_capacity=64, match_capacity=2 * batch, device=dev.index or 0, devices=devs)
+
+        def step(s):
+            t = bats[s]
+            eng.push(0, s * batch, (batch, t["ts"].data_ptr(), [t["symbol"].data_ptr(), t["price"].data_ptr(),
+                                                                t["volume"].data_ptr()], t["key"].data_ptr()),
+                     [0, 1, 2], mem=sa.native.SG_MEM_DEVICE)
+            return len(eng.poll(copy=False))
+
+        for s in range(W):
+            step(s)
+        eng.synchronize()
+        st0 = eng.stats()
+        t0 = time.perf_counter()
+        n = sum(step(s) for s in range(W, W + steps))
+        el = time.perf_counter() - t0
+        st = eng.stats()
+        eng.close()
+        res[label] = {"value": batch * steps / el, "ms_per_step": el / steps * 1e3, "matches_per_step": n / steps,
+                      "host_syncs_per_push": (st["host_syncs"] - st0["host_syncs"]) / steps,
+                      "host_staged_bytes": st["host_staged_bytes"]}
+    f, s1 = res["fanout"], res["single"]
+    return {"value": f["value"], "unit": "events/s", "ms_per_step": f["ms_per_step"], "n_shards": 2,
+            "single_engine_same_polls": s1["value"], "ratio_to_single": f["value"] / s1["value"],
+            "matches_per_step": f["matches_per_step"], "host_syncs_per_push": f["host_syncs_per_push"],
+            "host_staged_bytes": f["host_staged_bytes"], "keys": n_keys, "batch_events": batch,
+            "what": "C2 through sg_engine_create(n_devices = 2) with both shards on this GPU, device batches, "
+                    "blocking polls to host memory (the fan-out merges there); beside it the single engine with "
+                    "the same polls"}
+
+
 def api_inclusive(sa, synth, n_keys, chunk, chunks):
     """C2 through the product API end to end (SiddhiManager -> InputHandler.send(Event[]) -> the HIP engine
     -> QueryCallback.receive, one callback per trigger with the projected select list): the host side the
@@ -1205,6 +1248,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_extra:
         out["pcie_inclusive"] = pcie_inclusive(sa, synth, torch, dev, cq, K, B, 4)
         out["output_inclusive"] = output_inclusive(sa, synth, torch, dev, K, B, 6)
+        out["fanout_one_gpu"] = fanout_one_gpu(sa, synth, torch, dev, cq, K, 1 << 22, 6)
         out["api_inclusive"] = api_inclusive(sa, synth, 1 << 16, 1 << 16, 16)
         out["api_async"] = api_async(sa, synth, 1 << 16, 1 << 20)
         out["api_columnar"] = api_columnar(sa, synth, 1 << 20, 1 << 20, 8)

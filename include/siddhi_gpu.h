@@ -179,6 +179,8 @@ typedef struct sg_stats {
                                    than the batch's mean per key: all their partials at once, not one lane) */
     uint64_t hot_events;        /* their events */
     uint64_t seq_map_trims;     /* multi-device engine: seq map trims (each a min-seq scan of the due shards) */
+    uint64_t host_syncs;        /* multi-device engine: host waits its device-batch pushes made (the split's
+                                   per-owner totals and positions read back: one per push) */
 } sg_stats;
 
 /* ir/ir_len: an IR blob (siddhi_gpu_ir.h) of one query */

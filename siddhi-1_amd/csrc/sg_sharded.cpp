@@ -37,6 +37,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <functional>
 #include <map>
 #include <future>
@@ -94,6 +96,7 @@ struct ShardEngine {
     bool failed = false;                             // a call failed part-way (shards out of step)
     uint64_t staged_bytes = 0;                       // batch bytes copied to host memory (host splits of device batches: none)
     uint64_t trims = 0;
+    uint64_t host_syncs = 0;   // host waits of the device-batch pushes (sg_stats.host_syncs)
     // device batches: split on their own device (fan_split), two buffer sets used alternately; set j's events
     // done[r] (on shard r's device) are recorded behind what reads set j for shard r — the shard's push, or the
     // peer copy of its part — and the next split into set j waits for them on the device
@@ -447,6 +450,7 @@ void push_device(ShardEngine* s, const sg_batch* b) {
     FAN_OK(hipMemcpyAsync(p.h_totals, p.totals, (N + 1) * 4, hipMemcpyDeviceToHost, p.stream));
     FAN_OK(hipMemcpyAsync(p.h_opos, st.opos, n * 4, hipMemcpyDeviceToHost, p.stream));
     FAN_OK(hipStreamSynchronize(p.stream));
+    s->host_syncs++;
     if (p.h_totals[N]) throw ShardError(SG_ERR_INVALID, "key id outside [0, n_keys)");
     // validated: nothing has changed yet (a rejected batch leaves every shard as it was)
     std::vector<uint64_t> off(N + 1, 0);
@@ -697,8 +701,14 @@ namespace {
 // order of the keys' queue heads (each shard emitted its keys in that order; two shards' keys sharing a head is
 // the Scheduler collapse the single engine refuses), or by (fire time, key) for an engine that does
 // not order by heads
+static double fan_now() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+static const bool g_fan_prof = getenv("SG_FAN_PROF") != nullptr;   // (experiments: phase times to stderr)
+
 void collect(ShardEngine* s, bool timers) {
     const uint32_t N = s->N;
+    const double c0 = g_fan_prof ? fan_now() : 0.0;
     std::vector<ShardEngine::Out> parts(N);
     std::vector<std::vector<uint32_t>> hk(N);
     std::vector<std::vector<int64_t>> ht(N);
@@ -732,6 +742,7 @@ void collect(ShardEngine* s, bool timers) {
         if (timers && s->heads) sg_internal_heads(s->sh[r], hk[r], ht[r]);
         return sg_release_matches(s->sh[r], &m);
     });
+    const double c1 = g_fan_prof ? fan_now() : 0.0;
     struct Ref {
         uint32_t r;
         uint64_t i;
@@ -762,6 +773,26 @@ void collect(ShardEngine* s, bool timers) {
             for (uint64_t i = 0; i < p.n; i++) ord.push_back({r, i, 0});
         }
     }
+    // batch matches only (no timer match in any part): each shard's run is already in trigger order (its local
+    // seqs map to increasing global ones), and one trigger's matches all come from one shard, so the order is an
+    // N-way merge of the runs by trigger seq — O(n N) instead of a comparison sort of every match
+    bool merge = !timers;
+    for (uint32_t r = 0; r < N && merge; r++)
+        for (uint64_t i = 0; i < parts[r].n; i++)
+            if (parts[r].trig[i] == SG_TIMER_SEQ || (i > 0 && parts[r].trig[i] < parts[r].trig[i - 1])) {
+                merge = false;
+                break;
+            }
+    if (merge) {
+        ord.clear();
+        std::vector<uint64_t> at(N, 0);
+        for (uint64_t x = 0; x < total; x++) {
+            uint32_t best = N;
+            for (uint32_t r = 0; r < N; r++)
+                if (at[r] < parts[r].n && (best == N || parts[r].trig[at[r]] < parts[best].trig[at[best]])) best = r;
+            ord.push_back({best, at[best]++, 0});
+        }
+    } else
     std::stable_sort(ord.begin(), ord.end(), [&](const Ref& a, const Ref& b) {
         const ShardEngine::Out &A = parts[a.r], &B = parts[b.r];
         const bool ta = A.trig[a.i] == SG_TIMER_SEQ, tb = B.trig[b.i] == SG_TIMER_SEQ;
@@ -779,6 +810,7 @@ void collect(ShardEngine* s, bool timers) {
                 throw ShardError(SG_ERR_UNSUPPORTED,
                                  "two partition keys share a timer due time at one clock advance (reference Scheduler "
                                  "collapse quirk, SURVEY A.10): input not supported");
+    const double c2 = g_fan_prof ? fan_now() : 0.0;
     // append to pend (the chain dimension grows to the widest shard's)
     ShardEngine::Out& o = s->pend;
     uint32_t mc = std::max(o.n ? o.mc : 1u, 1u), ns = 0, ni = o.n ? o.ni : 0;
@@ -833,6 +865,9 @@ void collect(ShardEngine* s, bool timers) {
     o.pval.swap(pv);
     o.pnull.swap(pn);
     o.n = n1;
+    if (g_fan_prof)
+        fprintf(stderr, "fan collect: shard polls + seq mapping %.2f ms, order %.2f ms, append %.2f ms (%llu matches)\n",
+                (c1 - c0) * 1e3, (c2 - c1) * 1e3, (fan_now() - c2) * 1e3, (unsigned long long)total);
 }
 
 }  // namespace
@@ -894,7 +929,9 @@ int shd_poll(ShardEngine* s, uint32_t mem, sg_match_batch* out) {
             s->failed = true;   // shards that released their matches before another failed lost them
             throw;
         }
+        const double t0 = g_fan_prof ? fan_now() : 0.0;
         trim_maps(s);
+        if (g_fan_prof) fprintf(stderr, "fan trim %.2f ms\n", (fan_now() - t0) * 1e3);
         s->out = std::move(s->pend);
         s->pend = ShardEngine::Out();
         const ShardEngine::Out& o = s->out;
@@ -957,6 +994,7 @@ int shd_stats(ShardEngine* s, sg_stats* out) {
         out->seq_map_entries = 0;
         for (const SeqMap& m : s->gmap) out->seq_map_entries += m.v.size();
         out->seq_map_trims = s->trims;
+        out->host_syncs = s->host_syncs;
         return SG_OK;
     } catch (const std::exception& ex) {
         return fail_from(ex);

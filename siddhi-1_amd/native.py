@@ -66,7 +66,7 @@ class sg_stats(C.Structure):
                                           "live_at_batch_start", "group_ns", "advance_ns", "order_ns",
                                           "advance_launches", "window_spills", "advance_hbm_ns",
                                           "host_staged_bytes", "seq_map_entries", "hot_keys", "hot_events",
-                                          "seq_map_trims")]
+                                          "seq_map_trims", "host_syncs")]
 
 
 class sg_projection(C.Structure):

@@ -198,6 +198,8 @@ def test_cabi_fanout_device_batches_stay_on_device(shape, peer, monkeypatch):
     st = fan.stats()
     assert st["host_staged_bytes"] == 0
     assert st["events"] == one.stats()["events"]
+    # the split's per-owner totals still come back to the host: one host wait per device push, none on one engine
+    assert st["host_syncs"] == 8 and one.stats()["host_syncs"] == 0
     assert fan.describe().startswith("2 shards") or len(_devices()) > 2
 
 
