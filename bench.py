@@ -713,6 +713,11 @@ def output_inclusive(sa, synth, torch, dev, n_keys, batch, steps):
                     "columns copied to host memory (sg_poll_matches + sg_get_projection to host)"}
 
 
+def progress(msg):
+    """a progress line on stderr (the JSON line stays the only stdout output)"""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def fanout_one_gpu(sa, synth, torch, dev, cq, n_keys, batch, steps):
     """The C-ABI's own multi-device fan-out (sg_config.n_devices, csrc/sg_sharded.cpp) rehearsed with two shards
     on this one GPU, against the single engine on the same device batches with the same host polls (the fan-out
@@ -1196,6 +1201,8 @@ def main():
     eng.close()
     del batches
     torch.cuda.empty_cache()
+    if rank == 0:
+        progress(f"C2: {out['value']:.3e} events/s ({out['ms_per_step']:.3f} ms per step)")
     if rank == 0 and world == 1 and not args.no_extra:
         steps = max(3, args.steps // 4)
         cb = 1 << 22
@@ -1237,6 +1244,7 @@ def main():
             if not args.no_cpu:
                 r["cpu_baseline"] = cpu_general(sa, q, mk, keys, bsz, warm, pb, args.cpu_seconds / 3, name)
             out["other_configs"][name] = r
+            progress(f"{name}: {r['value']:.3e} events/s")
         ds = out["other_configs"]["C4_deep_state"]["roofline"]["counters_per_step"]
         out["other_configs"]["C4_deep_state"]["live_per_touched_key_at_batch_start"] = \
             ds["live_at_batch_start"] / max(1.0, ds["keys_touched"])
@@ -1245,14 +1253,18 @@ def main():
         for kind in ("zipf", "walk"):
             out.setdefault("other_configs", {})["C2_" + kind] = c2_variant(
                 sa, synth, torch, dev, kind, K, B, max(4, args.steps // 8), 3, args.cpu_seconds / 3, args.no_cpu)
+            progress(f"C2_{kind}: {out['other_configs']['C2_' + kind]['value']:.3e} events/s")
     if rank == 0 and world == 1 and not args.no_extra:
         out["pcie_inclusive"] = pcie_inclusive(sa, synth, torch, dev, cq, K, B, 4)
         out["output_inclusive"] = output_inclusive(sa, synth, torch, dev, K, B, 6)
+        progress("pcie / output legs done")
         out["fanout_one_gpu"] = fanout_one_gpu(sa, synth, torch, dev, cq, K, 1 << 22, 6)
+        progress("fan-out leg done")
         out["api_inclusive"] = api_inclusive(sa, synth, 1 << 16, 1 << 16, 16)
         out["api_async"] = api_async(sa, synth, 1 << 16, 1 << 20)
         out["api_columnar"] = api_columnar(sa, synth, 1 << 20, 1 << 20, 8)
         out["api_columnar_cat"] = api_columnar(sa, synth, 1 << 20, 1 << 20, 8, strings="categorical")
+        progress("API legs done")
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(sa, synth, K, B, args.cpu_seconds)
     if rank == 0:
