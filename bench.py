@@ -713,6 +713,84 @@ def output_inclusive(sa, synth, torch, dev, n_keys, batch, steps):
                     "columns copied to host memory (sg_poll_matches + sg_get_projection to host)"}
 
 
+LINE_MAX = 8192   # the driver recovers the JSON line from a bounded stdout tail (BENCH_r05: a 23.5 KB line was lost)
+
+
+def _r(x, n=4):
+    """a float rounded to n significant digits (None and non-floats unchanged)"""
+    if isinstance(x, float):
+        return float(f"{x:.{n}g}")
+    return x
+
+
+def compact_line(out, detail_path):
+    """The ONE stdout line: the contract's headline fields, the roofline of the advance kernel, the CPU baseline, and
+    every other leg summarised to {value, ms_per_step, frac, traffic_ratio}.  The full record (per-leg counters,
+    samples, kernel lists) goes to `detail_path`, which the line names.  Bounded by LINE_MAX."""
+    keep = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data")
+    line = {k: out[k] for k in keep}
+    c = out["config"]
+    line["config"] = {"workload": c["workload"], "keys_per_gpu": c["keys_per_gpu"],
+                      "batch_events_per_gpu": c["batch_events_per_gpu"], "parallelism": c["parallelism"]}
+    rf = out["roofline"]
+    line["roofline"] = {k: _r(rf.get(k), 6) for k in ("bound", "achieved", "peak", "unit", "frac", "traffic",
+                                                        "kernel", "alg_bytes_per_launch", "kernel_ms_per_launch")}
+    if rf.get("isolated"):
+        line["roofline"]["isolated"] = {k: _r(v) for k, v in rf["isolated"].items()}
+    line["stages_ms_per_step"] = {k: _r(v) for k, v in out["stages_ms_per_step"].items()}
+    if out.get("stages_ms_isolated"):
+        line["stages_ms_isolated"] = {k: _r(v) for k, v in out["stages_ms_isolated"].items()}
+    cb = out.get("cpu_baseline")
+    if cb:
+        line["cpu_baseline"] = {"value": _r(cb["value"]), "unit": cb["unit"], "cores": cb["cores"], "kind": cb["kind"],
+                                "sample": f"{cb['sample'].split(' (')[0]}, single-thread CPU oracle",
+                                "partition_parallel": {"value": _r(cb["partition_parallel"]["value"]),
+                                                       "threads": cb["partition_parallel"]["threads"]}}
+    extra = {}
+    for name, r in (out.get("other_configs") or {}).items():
+        x = r.get("roofline") or {}
+        per = x.get("alg_bytes_per_step") or x.get("alg_bytes_per_launch")
+        e = {"value": _r(r["value"]), "ms_per_step": _r(r["ms_per_step"]), "frac": _r(x.get("frac"))}
+        e["traffic_ratio"] = _r(x["traffic"] / per) if x.get("traffic") and per else None
+        if r.get("cpu_baseline"):
+            e["cpu"] = _r(r["cpu_baseline"]["value"])
+        extra[name] = e
+    for name in ("pcie_inclusive", "output_inclusive", "fanout_one_gpu", "api_inclusive", "api_async", "api_columnar",
+                 "api_columnar_cat", "merge_inclusive"):
+        r = out.get(name)
+        if r:
+            e = {"value": _r(r.get("value")), "ms_per_step": _r(r.get("ms_per_step"))}
+            if name == "fanout_one_gpu":
+                e["ratio_to_single"] = _r(r["ratio_to_single"])
+                e["host_syncs_per_push"] = r["host_syncs_per_push"]
+            if "error" in r:
+                e["error"] = str(r["error"])[:200]
+            extra[name] = e
+    if extra:
+        line["extra"] = extra
+    line["detail"] = detail_path
+    s = json.dumps(line, separators=(",", ":"))
+    if len(s) > LINE_MAX:   # never lose the headline: drop the summaries first
+        line.pop("extra", None)
+        s = json.dumps(line, separators=(",", ":"))
+    return s
+
+
+def write_detail(out, rank):
+    """the full record beside the line: SG_BENCH_DETAIL, else profiles/bench_detail_last.json; the path written
+    (or None when it cannot be written)"""
+    path = os.environ.get("SG_BENCH_DETAIL") or os.path.join("profiles", "bench_detail_last.json")
+    try:
+        full = path if os.path.isabs(path) else os.path.join(ROOT, path)
+        os.makedirs(os.path.dirname(full), exist_ok=True)
+        with open(full, "w") as f:
+            json.dump(out, f, indent=1)
+        return path
+    except OSError:
+        return None
+
+
 def progress(msg):
     """a progress line on stderr (the JSON line stays the only stdout output)"""
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
@@ -1268,7 +1346,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(sa, synth, K, B, args.cpu_seconds)
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        print(compact_line(out, write_detail(out, rank)), flush=True)
     if dist:
         dist.destroy_process_group()
 

@@ -584,20 +584,16 @@ void allocate(sg_engine* e) {
     }
     if (e->hot_ok) {
         // hot keys: up to every key (those with more live partials than the window are hot too); their carried-in
-        // partials get up to hot_exmax flat indices (further keys are given back to the HBM pass)
+        // partials get up to hot_exmax flat indices (further keys are given back to the HBM pass; SG_HOT_EXMAX bounds
+        // it, tests force the give-back that way).  Only the key list is allocated here: the pipeline's per-event and
+        // per-partial buffers (hot_buffers) come with the first batch that runs it, so an engine whose stream never
+        // has a hot key (uniform C2: ~2.3 GB at 2^24-event batches) never holds them.
         e->hot_cap = (uint32_t)std::min<size_t>(K, 1u << 20);
         e->hot_exmax = (uint32_t)std::min<size_t>((size_t)K * C, std::max<size_t>(1u << 22, 2 * B));
-        const size_t slots = B + (size_t)e->hot_exmax;
+        if (const char* x = getenv("SG_HOT_EXMAX")) e->hot_exmax = std::max(1u, (uint32_t)strtoul(x, nullptr, 0));
         e->hot_list = dalloc<uint32_t>(e->hot_cap, o);
         e->hot_info = dalloc<uint32_t>((size_t)e->hot_cap * SGD_HOT_INFO, o);
-        e->hot_death = dalloc<uint32_t>(slots, o);
-        e->hot_wl = dalloc<uint32_t>(2 * 3 * slots, o);
-        e->hot_tcnt = dalloc<uint32_t>(B, o);
-        e->hot_tbase = dalloc<uint32_t>(B, o);
-        e->hot_alive = dalloc<uint32_t>(slots, o);
-        e->hot_fh = dalloc<uint32_t>(slots, o);
-        e->hot_cur = dalloc<uint32_t>(slots, o);
-        e->hot_fbi = dalloc<uint32_t>(B, o);
+        e->hot_on = false;  // (set by the first batch that lists hot keys: drain_one)
     }
     e->tile_sum = dalloc<uint32_t>(B / SGD_ORDER_TILE + 1, o);
     e->tile_off = dalloc<uint32_t>(B / SGD_ORDER_TILE + 1, o);
@@ -738,6 +734,22 @@ static uint32_t sgd_max_key(const uint32_t* k, uint32_t n, bool skip_null) {
     else
         for (uint32_t i = 0; i < n; i++) m = k[i] > m ? k[i] : m;
     return m;
+}
+
+// the hot-key pipeline's buffers, allocated the first time a batch runs it (kept for the engine's life):
+// B + hot_exmax flat slots (events of the hot runs, then the carried-in partials) x 10 words, 3 x B words
+static void hot_buffers(sg_engine* e) {
+    if (e->hot_death) return;
+    auto& o = e->owned;
+    const size_t B = e->maxb, slots = B + (size_t)e->hot_exmax;
+    e->hot_death = dalloc<uint32_t>(slots, o);
+    e->hot_wl = dalloc<uint32_t>(2 * 3 * slots, o);
+    e->hot_tcnt = dalloc<uint32_t>(B, o);
+    e->hot_tbase = dalloc<uint32_t>(B, o);
+    e->hot_alive = dalloc<uint32_t>(slots, o);
+    e->hot_fh = dalloc<uint32_t>(slots, o);
+    e->hot_cur = dalloc<uint32_t>(slots, o);
+    e->hot_fbi = dalloc<uint32_t>(B, o);
 }
 
 // a batch is complete once its ordering ran: record its status block into the pinned ring
@@ -965,6 +977,7 @@ int push(sg_engine* e, const sg_batch* b) {
     p.raw_capw = e->raw_capw;
     p.raw_capnull = e->raw_capnull;
     p.hot_ctl = e->hot_ctl;
+    if (e->hot_ok && e->hot_on) hot_buffers(e);
     if (e->hot_ok) {
         // a partitioned batch's keys hold n / K events on average: "hot" is far above that (and above hot_min)
         p.hot_min = pl.partitioned ? std::max<uint32_t>(e->hot_min, (uint32_t)std::min<uint64_t>(e->hot_factor * n / e->K, 1u << 30))

@@ -19,7 +19,9 @@ def test_bench_emits_one_contract_line():
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1
+    assert len(lines[0]) <= 8192   # the driver parses the line from a bounded stdout tail
     d = json.loads(lines[0])
+    assert os.path.exists(os.path.join(ROOT, d["detail"]))
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
               "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
         assert k in d, k

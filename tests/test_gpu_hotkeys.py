@@ -292,3 +292,31 @@ def test_c2_variants_at_bench_size_key_subset(kind):
         assert hot > 1000 and st["hot_keys"] > 0 and "k_hot_prep" in gpu.describe()
     gpu.close()
     ora.close()
+
+
+@pytest.mark.parametrize("exmax", ["48", "400"])
+def test_hot_partials_given_back_above_exmax(exmax, monkeypatch):
+    """several hot keys carrying ~160 live partials each into every batch, with the pipeline's flat index space for
+    carried-in partials (hot_exmax, SG_HOT_EXMAX) smaller than their sum: k_hot_scan's second pass gives the keys
+    past the limit back to the HBM pass (p2_jit.hip hot_scan_pass), still exact against the oracle and the lane walk"""
+    monkeypatch.setenv("SG_HOT_MIN", "64")
+    monkeypatch.setenv("SG_HOT_EXMAX", exmax)
+    q = ("define stream S (symbol string, price float, volume int);\n"
+         "partition with (symbol of S) begin from every e1=S[price>10] -> e2=S[price>e1.price + 100.0] "
+         "within 200 milliseconds select e1.price as a insert into O; end;")
+    n_keys, n = 4096, 1 << 16
+    cq, gpu, ora, lane = _pair(q, n_keys, n)
+    rng = np.random.default_rng(31)
+    batches = []
+    for b in range(4):
+        d = synth.stock_ticks(b * n, n, n_keys, seed=150 + b, rate_per_ms=16)
+        u = rng.random(n)
+        for i, k in enumerate((77, 78, 79, 80, 81)):
+            d["key"][(u >= 0.04 * i) & (u < 0.04 * (i + 1))] = k
+        d["symbol"] = d["key"].copy()
+        batches.append((b * n, d))
+    sg = _run(gpu, ora, lane, batches)
+    assert sg["partials_live"] > 5 * 64
+    assert "k_hot_prep" in gpu.describe()
+    for e in (gpu, ora, lane):
+        e.close()
