@@ -734,8 +734,9 @@ def compact_line(out, detail_path):
     line["config"] = {"workload": c["workload"], "keys_per_gpu": c["keys_per_gpu"],
                       "batch_events_per_gpu": c["batch_events_per_gpu"], "parallelism": c["parallelism"]}
     rf = out["roofline"]
-    line["roofline"] = {k: _r(rf.get(k), 6) for k in ("bound", "achieved", "peak", "unit", "frac", "traffic",
-                                                        "kernel", "alg_bytes_per_launch", "kernel_ms_per_launch")}
+    line["roofline"] = {k: rf.get(k) if k in ("achieved", "peak", "frac") else _r(rf.get(k), 6)
+                        for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel", "alg_bytes_per_launch",
+                                  "kernel_ms_per_launch")}
     if rf.get("isolated"):
         line["roofline"]["isolated"] = {k: _r(v) for k, v in rf["isolated"].items()}
     line["stages_ms_per_step"] = {k: _r(v) for k, v in out["stages_ms_per_step"].items()}
@@ -1087,6 +1088,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the C3 / C4 lines")
+    ap.add_argument("--legs", default=None, help="comma-separated subset of the other legs to run (experiments)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -1316,23 +1318,29 @@ def main():
                               "hundreds of live partials per key at every push"),
         }
         out["other_configs"] = {}
+        legs = set(args.legs.split(",")) if args.legs else None
         for name, (q, mk, keys, bsz, warm, cap, pb, extra, wl) in gcfg.items():
+            if legs is not None and name not in legs:
+                continue
             r = dict(run_general(sa, synth, torch, dev, q, mk, keys, bsz, 16 if name == "C4_deep_state" else steps,
                                  warm, cap, playback=pb, extra_in=extra, label=name), workload=wl)
             if not args.no_cpu:
                 r["cpu_baseline"] = cpu_general(sa, q, mk, keys, bsz, warm, pb, args.cpu_seconds / 3, name)
             out["other_configs"][name] = r
             progress(f"{name}: {r['value']:.3e} events/s")
-        ds = out["other_configs"]["C4_deep_state"]["roofline"]["counters_per_step"]
-        out["other_configs"]["C4_deep_state"]["live_per_touched_key_at_batch_start"] = \
-            ds["live_at_batch_start"] / max(1.0, ds["keys_touched"])
+        if "C4_deep_state" in out["other_configs"]:
+            ds = out["other_configs"]["C4_deep_state"]["roofline"]["counters_per_step"]
+            out["other_configs"]["C4_deep_state"]["live_per_touched_key_at_batch_start"] = \
+                ds["live_at_batch_start"] / max(1.0, ds["keys_touched"])
     if rank == 0 and world == 1 and not args.no_extra:
         # SURVEY §8(d) workload variants of the headline config
         for kind in ("zipf", "walk"):
+            if args.legs and "C2_" + kind not in args.legs.split(","):
+                continue
             out.setdefault("other_configs", {})["C2_" + kind] = c2_variant(
                 sa, synth, torch, dev, kind, K, B, max(4, args.steps // 8), 3, args.cpu_seconds / 3, args.no_cpu)
             progress(f"C2_{kind}: {out['other_configs']['C2_' + kind]['value']:.3e} events/s")
-    if rank == 0 and world == 1 and not args.no_extra:
+    if rank == 0 and world == 1 and not args.no_extra and not args.legs:
         out["pcie_inclusive"] = pcie_inclusive(sa, synth, torch, dev, cq, K, B, 4)
         out["output_inclusive"] = output_inclusive(sa, synth, torch, dev, K, B, 6)
         progress("pcie / output legs done")

@@ -66,6 +66,10 @@ __host__ __device__ inline size_t gen_at(uint32_t K, uint32_t blockWords, uint32
 // kernels write back only what changed, and every component that reads the lists from the block flushes the
 // records back first (gen_host.hip gen_flush_deep; k_gen_live / k_gen_min_seq read them in place)
 #define GEN_W0_REG 0x200u
+// GEN_W0_CHN: chn_kernels.hip stored this key's lists (in the general layout: partial j = StateEvent j, the seed =
+// StateEvent CHN_R, events below min(64, SECAP)), so its next load skips the shape checks; the general kernel clears
+// the mark when it takes the key over
+#define GEN_W0_CHN 0x400u
 // a deep-store record in 32-bit words: ts[L] i64, seq[L] u64, null bits[L], attribute words[NW][L], queue[Q] i64
 struct GenDeepLayout {
     uint32_t oTs, oSeq, oNb, oW, oQ, words;
@@ -177,7 +181,21 @@ struct GenProgram {
     int32_t cntOk, cntP0, cntPA, cntPB, cntWE;
     int32_t cntAnd, cntPad;   // the pair is a logical AND (`e2=S[fA] and e3=S[fB]`) instead of an OR
     uint32_t absWordAt[ABS_MAXNW];  // the StreamEvent record word (SE_ATTR + ...) of each captured word
+    // the chained stream states `[every] e1=S[f0] -> e2=S[f1] -> ... -> en=S[f(n-1)] [within W]` (PATTERN,
+    // partitioned, one stream, 2 <= n <= CHN_MAXN), which run on the register-window kernel of chn_kernels.hip
+    // (gen_host.hip chn_shape): chnP[i] the processor of state i, chnEvery: `every` re-arms p0's seed; the attribute
+    // words later filters read of a captured event are kept in the window (chnKW of them: event word chnKeepW[c] of
+    // attribute chnKeepA[c]; chnAttrK[a] = the kept index of attribute a's first word, or -1) and chnSlotEv[s] is
+    // the event index (state) whose event slot s holds
+    int32_t chnOk, chnN, chnEvery, chnKW;
+    int32_t chnP[4];
+    uint32_t chnKeepW[2], chnKeepA[2];
+    int32_t chnAttrK[GEN_MAXA];
+    int32_t chnSlotEv[GEN_MAXSLOT];
 };
+#define CHN_MAXN 4       // chn_kernels.hip: states of a chain
+// chn_kernels.hip: partials a key's register window holds, for a chain of n states
+#define CHN_R(n) ((n) == 2 ? 24 : (n) == 3 ? 20 : 12)
 
 // KeyState field offsets inside a processor's record
 #define KS_FLAGS 0

@@ -66,6 +66,13 @@ static const AbsKernel kAbsdFlush[ABS_MAXNW + 1] = {nullptr, k_absd_flush_1, k_a
 CNT_DECL(1) CNT_DECL(2) CNT_DECL(3) CNT_DECL(4) CNT_DECL(5) CNT_DECL(6) CNT_DECL(7) CNT_DECL(8)
 static const AbsKernel kCntBatch[ABS_MAXNW + 1] = {nullptr, k_cnt_batch_1, k_cnt_batch_2, k_cnt_batch_3, k_cnt_batch_4,
                                                    k_cnt_batch_5, k_cnt_batch_6, k_cnt_batch_7, k_cnt_batch_8};
+#define CHN_DECL(NE) extern "C" __global__ void k_chn_batch_##NE##_0(const GenArgs ap); \
+    extern "C" __global__ void k_chn_batch_##NE##_1(const GenArgs ap); extern "C" __global__ void k_chn_batch_##NE##_2(const GenArgs ap);
+CHN_DECL(1) CHN_DECL(2) CHN_DECL(3)
+// [n - 2][kept words]: the chain kernels (chn_kernels.hip)
+static const AbsKernel kChnBatch[CHN_MAXN - 1][3] = {{k_chn_batch_1_0, k_chn_batch_1_1, k_chn_batch_1_2},
+                                                     {k_chn_batch_2_0, k_chn_batch_2_1, k_chn_batch_2_2},
+                                                     {k_chn_batch_3_0, k_chn_batch_3_1, k_chn_batch_3_2}};
 #define ABSF_DECL(NW) extern "C" __global__ void k_abs_flush_##NW(const GenArgs ap);
 ABSF_DECL(1) ABSF_DECL(2) ABSF_DECL(3) ABSF_DECL(4) ABSF_DECL(5) ABSF_DECL(6) ABSF_DECL(7) ABSF_DECL(8)
 static const AbsKernel kAbsFlush[ABS_MAXNW + 1] = {nullptr, k_abs_flush_1, k_abs_flush_2, k_abs_flush_3, k_abs_flush_4,
@@ -415,6 +422,85 @@ void cnt_shape(GenProgram& G) {
     G.cntOk = getenv("SG_NO_CNT") ? 0 : 1;  // (SG_NO_CNT: A/B timing against the general kernels; same results)
 }
 
+// the chained stream-state shape of chn_kernels.hip:
+//     [every] e1=S[f0] -> e2=S[f1] -> ... -> en=S[f(n-1)] [within W]      (PATTERN, partitioned, one stream, 2 <= n <= 4)
+// with the processors wired as StateInputStreamParser wires that query (each state's post processor feeding the next
+// state's addState, the last one's reaching the selector; `every` only around e1), no timers, single-event slots.
+// The attribute words the filters read of earlier events are kept in the kernel's window (at most two words).
+// Anything else stays on the general kernels.
+void chn_shape(GenProgram& G) {
+    G.chnOk = 0;
+    const int n = G.nprocs;
+    if (G.qtype != SG_Q_PATTERN || !G.partitioned || G.nstreams != 1 || n < 2 || n > CHN_MAXN || G.nslots != n ||
+        G.nStartup != 0 || G.MC != 1 || G.nAll != n)
+        return;
+    const GenRecv& R = G.recv[0];
+    if (R.n != n || R.nStateProcs != n || !R.multi) return;
+    for (int i = 0; i < n; i++) {
+        const int p = R.procs[i];
+        if (p < 0 || p >= n) return;
+        const GenPre& P = G.pre[p];
+        const GenPost& Q = G.post[p];
+        // (p0's withinEvery is p0 itself under `every ... within`: it clones an EXPIRED entry of p0's own lists, which
+        // hold only blank seeds, never expired — StreamPreStateProcessor.java:118-129 reads the start event)
+        if (P.kind != GK_STREAM || P.absent || P.isStart != (i == 0) ||
+            !(P.withinEvery == GEN_NONE || (i == 0 && P.withinEvery == p)))
+            return;
+        if (Q.callbackPre != GEN_NONE || P.thisPost != p) return;
+        if (i + 1 < n) {
+            if (Q.nextStatePre != R.procs[i + 1] || Q.hasNext) return;
+        } else if (Q.nextStatePre != GEN_NONE || !Q.hasNext) {
+            return;
+        }
+        if (Q.nextEveryStatePre != GEN_NONE && !(i == 0 && Q.nextEveryStatePre == p)) return;
+        if (P.stateId < 0 || P.stateId >= n || G.slotStream[P.stateId] != 0) return;
+        for (int j = 0; j < i; j++)
+            if (G.pre[R.procs[j]].stateId == P.stateId) return;
+        if (!shallow(G, P)) return;
+        G.chnP[i] = p;
+    }
+    if (G.within != -1 && (G.nStartIds != 1 || G.startIds[0] != G.pre[G.chnP[0]].stateId)) return;
+    if (!reg_layout(G)) return;
+    const int R_ = CHN_R(n);
+    // (the window's lists, StateEvents 0 .. R and its events below min(64, SECAP) fit the block; 16-bit pool entries)
+    if (G.L < (uint32_t)R_ || G.STCAP < (uint32_t)R_ + 1u || (uint32_t)(R_ * (n - 1)) > std::min<uint32_t>(64u, G.SECAP) ||
+        G.SECAP >= 0xffffu)
+        return;
+    for (int s = 0; s < GEN_MAXSLOT; s++) G.chnSlotEv[s] = -1;
+    for (int i = 0; i < n; i++) G.chnSlotEv[G.pre[G.chnP[i]].stateId] = i;
+    // the attributes the filters read of an earlier state's event
+    uint32_t want = 0;
+    for (int t = 0; t < n; t++) {
+        const GenPre& P = G.pre[G.chnP[t]];
+        for (uint32_t pc = P.fpc, end = P.fpc + P.flen; pc < end;) {
+            const uint32_t w = G.code[pc], op = w & 0xffu, b = (w >> 16) & 0xffu;
+            if (op == SG_OP_VAR && (int)b != P.stateId) {
+                const uint32_t a = G.code[pc + 1];
+                if (a >= (uint32_t)G.nattr[0]) return;
+                want |= 1u << a;
+            }
+            pc += (uint32_t)sg_op_len(op);
+        }
+    }
+    int kw = 0;
+    for (int a = 0; a < GEN_MAXA; a++) G.chnAttrK[a] = -1;
+    for (int a = 0; a < G.nattr[0]; a++) {
+        if (!((want >> a) & 1u)) continue;
+        const bool wide = G.attrType[0][a] == SG_T_LONG || G.attrType[0][a] == SG_T_DOUBLE;
+        if (kw + (wide ? 2 : 1) > 2) return;
+        G.chnAttrK[a] = kw;
+        for (int h = 0; h < (wide ? 2 : 1); h++) {
+            G.chnKeepW[kw] = G.absOff[a] + (uint32_t)h;
+            G.chnKeepA[kw] = (uint32_t)a;
+            kw++;
+        }
+    }
+    G.chnKW = kw;
+    G.chnN = n;
+    G.chnEvery = G.post[G.chnP[0]].nextEveryStatePre == G.chnP[0] ? 1 : 0;
+    G.chnOk = getenv("SG_NO_CHN") ? 0 : 1;  // (SG_NO_CHN: A/B timing against the general kernels; same results)
+}
+
 // the absent-tail shape of abs_kernels.hip: `[every] e1=S[f0] -> not S[f1] for T [within W]` with the
 // processors wired exactly as the kernels restate them (anything else stays on the general kernels)
 // A filter program `operand [CVT] operand [CVT] CMP` (include/siddhi_gpu_ir.h encodings) as a JoFast, each
@@ -587,6 +673,7 @@ GenProgram* gen_build_program(const uint32_t* w, size_t nw, uint32_t partialCap)
         for (int x = 0; x < G->nprocs; x++) G->pre[x].ff = jo_fast_decode(G->code, G->pre[x].fpc, G->pre[x].flen);
         abs_shape(*G);
         cnt_shape(*G);
+        chn_shape(*G);
         return G;
     } catch (...) {
         delete G;
@@ -1401,7 +1488,7 @@ GenEngine* gen_create(const uint32_t* ir, size_t nw, const sg_config& cfg, hipSt
             }
         }
         e->live = e->dalloc<unsigned long long>(1);
-        if (G.absOk || G.cntOk) {
+        if (G.absOk || G.cntOk || G.chnOk) {
             e->fb_list = e->dalloc<uint32_t>(K);
             e->fb_start = e->dalloc<uint32_t>(K);
             e->fb_n = e->dalloc<unsigned long long>(1);
@@ -1435,7 +1522,7 @@ GenEngine* gen_create(const uint32_t* ir, size_t nw, const sg_config& cfg, hipSt
             }
             e->pay = e->dalloc<uint32_t>(B * 6);  // Pay<4>: 6 words
             // the count kernel's fused grouping (by 64-key tile; the kernel splits its tile by key in LDS)
-            e->cnt_fused = regKernels && G.partitioned && sgd_fused_ok(K, B, 1, 6) && !getenv("SG_NO_FUSED");
+            e->cnt_fused = (regKernels || G.chnOk) && G.partitioned && sgd_fused_ok(K, B, 1, 6) && !getenv("SG_NO_FUSED");
             if (e->cnt_fused) {
                 e->tpay = e->dalloc<uint32_t>(B * 6);
                 e->tile_lo = e->dalloc<uint32_t>((K + 63) / 64 + 1);
@@ -1488,7 +1575,7 @@ static size_t type_size(int t) {
 
 // the kernels take GenArgs (608 B) by value in their kernel arguments
 enum { GEN_L_BATCH = 0, GEN_L_TIMERS = 1, GEN_L_DEADLINES = 2, GEN_L_ABS_BATCH = 3, GEN_L_ABS_TIMERS = 4, GEN_L_CNT_BATCH = 5,
-       GEN_L_ABSD_BATCH = 6, GEN_L_ABSD_TIMERS = 7 };
+       GEN_L_ABSD_BATCH = 6, GEN_L_ABSD_TIMERS = 7, GEN_L_CHN_BATCH = 8 };
 // the general kernels over the keys a register-window kernel handed over: a fixed grid striding the list
 #define GEN_FB_BLOCKS 1024u
 // timer sweeps: a fixed grid of one-wave blocks striding over the due keys (their number is on the device)
@@ -1518,6 +1605,10 @@ static bool absd_on(const GenEngine* e) { return e->fb2_list && absd_lds(e) <= 6
 
 // the register-window kernel of cnt_kernels.hip runs this query (the shape, no device projection)
 static bool cnt_on(const GenEngine* e) { return e->host.cntOk && e->host.projN == 0 && e->fb_list; }
+// the chain kernel of chn_kernels.hip runs this query (the shape, no device projection)
+static bool chn_on(const GenEngine* e) { return e->host.chnOk && e->host.projN == 0 && e->fb_list; }
+// the kernels that read the key-sorted payload with every attribute word of the event
+static bool pay_on(const GenEngine* e) { return abs_on(e) || cnt_on(e) || chn_on(e); }
 
 // both filters of the absent-tail shape are decoded compares (GenPre.ff): the kernel variants without the interpreter
 static bool abs_ff(const GenEngine* e) {
@@ -1543,6 +1634,11 @@ static void launch_gen(GenEngine* e, GenArgs a, int which) {
         const AbsKernel k = which == GEN_L_ABSD_BATCH ? (ff ? kAbsdBatchF : kAbsdBatch)[e->host.absNW]
                                                        : (ff ? kAbsdTimersF : kAbsdTimers)[e->host.absNW];
         hipLaunchKernelGGL(k, dim3(GEN_FB_BLOCKS), dim3(64), (unsigned)absd_lds(e), e->stream, ap);
+    }
+    else if (which == GEN_L_CHN_BATCH) {   // one lane per key, then the waves' counter rows
+        hipLaunchKernelGGL(kChnBatch[e->host.chnN - 2][e->host.chnKW], dim3(blocks), dim3(64), 0, e->stream, ap);
+        hipLaunchKernelGGL(k_gen_stats_reduce, dim3(GST_N, std::min<uint32_t>((blocks + 1023) / 1024, 16u)), dim3(256),
+                           0, e->stream, e->wstats, blocks, e->stats);
     }
     else if (which == GEN_L_ABS_BATCH || which == GEN_L_ABS_TIMERS || which == GEN_L_CNT_BATCH) {
         // one lane per key / possible due slot (the due count is on the device); then the waves' counter rows
@@ -1616,7 +1712,7 @@ int gen_push(GenEngine* e, const sg_batch* b, std::string& msg) {
         cl.add(e->seg_end, (size_t)e->K * 4);
         cl.add(e->raw_count, 8 * GEN_RAWSEG);
         cl.add(e->t_multi, 4);
-        if (abs_on(e) || cnt_on(e)) cl.add(e->fb_n, 8);
+        if (pay_on(e)) cl.add(e->fb_n, 8);
         if (abs_on(e) && absd_on(e)) cl.add(e->fb2_n, 8);
         GH_OK(cl.launch(e->stream));
     }
@@ -1639,7 +1735,7 @@ int gen_push(GenEngine* e, const sg_batch* b, std::string& msg) {
         PackSrc ps{};
         uint32_t W = 0;
         bool nul = false;
-        if (abs_on(e) || cnt_on(e)) {
+        if (pay_on(e)) {
             const int st = (int)b->stream;
             for (int c = 0; c < G.nattr[st] && W <= 4; c++) {
                 const int t = G.attrType[st][c];
@@ -1677,7 +1773,7 @@ int gen_push(GenEngine* e, const sg_batch* b, std::string& msg) {
         // the register-window kernels' batches (count, absent): grouped by 64-key tile (two 7-bit passes), then split by key per tile
         // (k_cnt_split), instead of three 8-bit passes; while a batch has shown a tile of more than 2^14 events (one
         // wave splits a tile), the sorted grouping
-        const bool fused = e->cnt_fused && !e->cnt_skewed && (cnt_on(e) || abs_on(e)) && W >= 1 && W <= 4;
+        const bool fused = e->cnt_fused && !e->cnt_skewed && pay_on(e) && W >= 1 && W <= 4;
         e->cnt_fused_last = fused;
         if (fused) {
             ga.W = W;
@@ -1700,7 +1796,7 @@ int gen_push(GenEngine* e, const sg_batch* b, std::string& msg) {
             a.b.tile_lo = nullptr;
             a.b.tpay = nullptr;
             a.b.tileMax = nullptr;
-        } else if ((abs_on(e) || cnt_on(e)) && W >= 1 && W <= 4) {
+        } else if (pay_on(e) && W >= 1 && W <= 4) {
             ga.W = W;
             ga.src = ps;
             ga.out = e->pay;
@@ -1767,6 +1863,13 @@ int gen_push(GenEngine* e, const sg_batch* b, std::string& msg) {
         a.mode = GEN_M_TFIRST;   // (this shape emits at most one match per event)
         launch_gen(e, a, GEN_L_CNT_BATCH);
         a.mode = GEN_M_KEYLIST | GEN_M_TFIRST;
+    } else if (chn_on(e)) {
+        // the chain kernel, then the general kernel over the keys it handed over (from the event where each stopped)
+        a.fb_list = e->fb_list;
+        a.fb_n = e->fb_n;
+        a.fb_start = e->fb_start;
+        launch_gen(e, a, GEN_L_CHN_BATCH);
+        a.mode = GEN_M_KEYLIST;
     }
     launch_gen(e, a, GEN_L_BATCH);
     // order: the batch's base + the exclusive prefix of the per-trigger counts + rank (k_gen_tsum / k_gen_tscan /
@@ -2207,6 +2310,9 @@ std::string gen_describe(const GenEngine* e) {
         adv += " + k_gen_timers (keys handed over)";
     } else if (cnt_on(e)) {
         push = "k_cnt_batch_" + nw + " (register window, lane per key) + k_gen_batch (keys handed over)";
+    } else if (chn_on(e)) {
+        push = "k_chn_batch_" + std::to_string(G.chnN - 1) + "_" + std::to_string(G.chnKW) +
+               " (chained states, register window, lane per key) + k_gen_batch (keys handed over)";
     } else {
         push = "k_gen_batch (general interpreter, lane per key)";
         if (G.nStartup > 0) adv = "k_gen_timers (general interpreter)";

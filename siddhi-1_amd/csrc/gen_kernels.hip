@@ -1110,7 +1110,8 @@ struct Lane {
     __device__ void initKey() __restrict__ {  // PartitionRuntimeImpl.initPartition -> StateStreamRuntime.initPartition
         const uint32_t w0 = W(0);
         if (w0 & 1u) {
-            if (w0 & GEN_W0_POOLC) W(0) = 1u;  // (this kernel's allocations do not keep abs_kernels' pool words)
+            // (this kernel's allocations do not keep abs_kernels' pool words, nor chn_kernels' layout)
+            if (w0 & (GEN_W0_POOLC | GEN_W0_CHN)) W(0) = 1u;
             return;
         }
         W(0) = 1u;

@@ -1074,7 +1074,7 @@ __device__ __forceinline__ void advance(const P2Params& p, const uint32_t gid) {
                 // batch's seq base) rides in the trigger's descriptor, so the ordering reads no raw slot for it
                 const bool inl = STG && SGX_BRANCHLESS && !SGQ_PROJ && c1 == 1u;
                 if (pos + c1 <= p.raw_capacity) {
-                    if (!SGX_NO_TDESC && !inl) p.t_desc[bi] = ((uint64_t)c1 << 32) | (uint64_t)(uint32_t)pos;  // count | first slot
+                    if (!SGX_NO_TDESC && !inl) p.t_desc[bi] = p.td_tag | ((uint64_t)c1 << 32) | (uint64_t)(uint32_t)pos;  // count | first slot
                 } else {
                     atomicOr(p.err, (uint32_t)SGD_ERR_MATCH_CAP);
                 }
@@ -1102,7 +1102,7 @@ __device__ __forceinline__ void advance(const P2Params& p, const uint32_t gid) {
                             }
                             if (inl) {
                                 if (!SGX_NO_TDESC && pos < p.raw_capacity)
-                                    p.t_desc[bi] = SGD_TD_INLINE | (1ull << 32) | (uint64_t)(uint32_t)(int32_t)sq;
+                                    p.t_desc[bi] = SGD_TD_INLINE | p.td_tag | (1ull << 32) | (uint64_t)(uint32_t)(int32_t)sq;
                             } else if (!SGX_NO_RAW && pos < p.raw_capacity) {
                                 p.raw_e1[pos] = sbase + (uint64_t)(int64_t)sq;
 #if SGQ_PROJ
@@ -1951,7 +1951,7 @@ extern "C" __global__ void __launch_bounds__(256) k_hot_trig(const P2Params p) {
             if (c[g]) {
                 const uint32_t x = x0 + g * blockDim.x + threadIdx.x;
                 if (first + c[g] <= p.raw_capacity)
-                    p.t_desc[p.hot_fbi[x]] = ((uint64_t)c[g] << 32) | (uint64_t)(uint32_t)first;
+                    p.t_desc[p.hot_fbi[x]] = p.td_tag | ((uint64_t)c[g] << 32) | (uint64_t)(uint32_t)first;
                 else
                     atomicOr(p.err, (uint32_t)SGD_ERR_MATCH_CAP);
                 p.hot_tbase[x] = (uint32_t)first;

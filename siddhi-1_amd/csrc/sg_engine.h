@@ -36,6 +36,12 @@
 #define SGD_TS_LIM (1ll << 30)
 #define SGD_RAW_CHUNK 256  // raw match slots a wave reserves at a time (the raw buffer has 2 chunks of slack per wave)
 #define SGD_TD_INLINE (1ull << 63)  // t_desc: the trigger's one match carried inline (no raw slot)
+// t_desc word: [0, 32) first raw slot (or the inline e1 seq offset), [32, 47) match count (<= SGD_MAX_CAP), [47, 63)
+// the batch's tag (an entry written under another batch's tag reads as "no match": the ordering never clears
+// t_desc), bit 63 inline
+#define SGD_TD_CNT(d) ((uint32_t)((d) >> 32) & 0x7fffu)
+#define SGD_TD_TAGOF(d) ((uint32_t)((d) >> 47) & 0xffffu)
+#define SGD_TD_TAG(epoch) ((uint64_t)(epoch) << 47)
 // the fused grouping's LDS split keeps up to this many 64-event rounds per wave in registers (p2_jit.hip
 // tile_split_lds): a tile of more than SGD_SPLIT_CHUNKS(stride) * SGD_BLOCK events goes to the HBM pass
 #define SGD_SPLIT_CHUNKS(stride) (80u / ((stride) + 1u))
@@ -163,6 +169,7 @@ struct P2Params {
     uint32_t hot_round;                // the search round a k_hot_rn / k_hot_rc launch runs
     uint32_t hot_exmax;                // flat indices for carried-in partials (keys past it are given back)
     uint32_t hot_n0;                   // a key carrying in at least this many live partials is hot too
+    uint64_t td_tag;                   // SGD_TD_TAG of this batch, or-ed into every t_desc entry written
     uint64_t cst[SGD_MAX_CONST];       // filter constants, already in their comparison domain
 };
 
@@ -185,9 +192,9 @@ struct ScatterParams {
     uint64_t seq_base;
     const uint32_t* key;       // batch key ids (NULL: unpartitioned -> key 0)
     const int64_t* ts;
-    uint64_t* t_desc;          // count << 32 | first raw slot per batch event (reset here)
+    const uint64_t* t_desc;    // per batch event: SGD_TD_CNT matches from the first raw slot (entries of this batch's tag)
+    uint32_t epoch;            // this batch's t_desc tag
     uint32_t* tile_sum;        // [ceil(n / SGD_ORDER_TILE)] matches per tile of triggers
-    uint32_t* tile_off;        // exclusive scan of tile_sum
     const uint64_t* raw_e1;
     unsigned long long* out_count;     // matches ordered so far (monotonic; record r at r % capacity)
     unsigned long long* batch_total;
@@ -271,10 +278,9 @@ int sgd_launch_agg(const AggParams& a, ihipStream_t* stream);
 int sgd_launch_reset_agg(const uint32_t* keys, uint32_t n, uint32_t K, uint32_t n_agg, int64_t* st_n, uint64_t* st_v,
                          uint8_t* st_has, ihipStream_t* stream);
 int sgd_launch_project(const ProjParams& p, ihipStream_t* stream);
-// ordering of one batch's matches: per-tile sums, their exclusive scan (scan_tmp: rocPRIM scratch of
-// scan_bytes), then the tile-local scan + scatter; also bumps out_count
-int sgd_launch_scatter(const ScatterParams& s, void* scan_tmp, size_t scan_bytes, ihipStream_t* stream);
-size_t sgd_scatter_scan_bytes(uint32_t max_n);
+// ordering of one batch's matches: per-tile totals, then per tile its prefix, the tile-local scan and the scatter;
+// also bumps out_count
+int sgd_launch_scatter(const ScatterParams& s, ihipStream_t* stream);
 // partition purge: hdr[keys[i]] = 0 (key range errors -> err)
 int sgd_launch_reset_keys(const uint32_t* keys, uint32_t n, uint32_t n_keys, uint32_t* hdr, uint32_t* err,
                           ihipStream_t* stream);

@@ -208,12 +208,10 @@ struct sg_engine {
     uint32_t* dlist = nullptr;     // the waves the HBM pass takes, and their number
     uint32_t* dlist_n = nullptr;
     uint32_t* klist = nullptr;     // the keys the staged pass stopped (the HBM pass's lanes)
-    uint32_t* tile_sum = nullptr;  // ordering: matches per tile of triggers, and its exclusive scan
-    uint32_t* tile_off = nullptr;
+    uint32_t* tile_sum = nullptr;  // ordering: matches per tile of triggers
+    uint32_t td_epoch = 0;         // the current batch's t_desc tag (1..0xffff; t_desc cleared at the wrap)
     unsigned long long* out_count = nullptr;
     unsigned long long* batch_total = nullptr;
-    void* scan_tmp = nullptr;
-    size_t scan_tmp_bytes = 0;
     unsigned long long* stats = nullptr;
     uint32_t* err = nullptr;
     // ordered output
@@ -596,7 +594,6 @@ void allocate(sg_engine* e) {
         e->hot_on = false;  // (set by the first batch that lists hot keys: drain_one)
     }
     e->tile_sum = dalloc<uint32_t>(B / SGD_ORDER_TILE + 1, o);
-    e->tile_off = dalloc<uint32_t>(B / SGD_ORDER_TILE + 1, o);
     // the match count and the error word share 16 bytes, so poll reads both with one D2H copy
     e->out_count = dalloc<unsigned long long>(2, o);
     e->err = (uint32_t*)(e->out_count + 1);
@@ -606,8 +603,6 @@ void allocate(sg_engine* e) {
     HIP_OK(hipMemsetAsync(e->out_count, 0, 16, e->stream));
     HIP_OK(hipMemsetAsync(e->stats, 0, SGD_ST_N * 8, e->stream));
     HIP_OK(hipMemsetAsync(e->err, 0, 4, e->stream));
-    e->scan_tmp_bytes = sgd_scatter_scan_bytes((uint32_t)B);
-    e->scan_tmp = dalloc<uint8_t>(e->scan_tmp_bytes, o);
     e->o_trig = dalloc<uint64_t>(M, o);
     e->o_slot = dalloc<uint64_t>(2 * M, o);
     e->o_key = dalloc<uint32_t>(M, o);
@@ -998,6 +993,13 @@ int push(sg_engine* e, const sg_batch* b) {
         p.hot_fbi = e->hot_fbi;
     }
     for (size_t i = 0; i < e->consts.size(); i++) p.cst[i] = e->consts[i];
+    // this batch's t_desc tag: entries of earlier batches read as empty, so the ordering clears nothing; at the
+    // tag's wrap t_desc is cleared once
+    if (++e->td_epoch > 0xffffu) {
+        HIP_OK(hipMemsetAsync(e->t_desc, 0, e->maxb * 8, e->stream));
+        e->td_epoch = 1;
+    }
+    p.td_tag = SGD_TD_TAG(e->td_epoch);
     hipEvent_t a0 = nullptr, a1 = nullptr;
     if (e->timing) { a0 = e->ev(); e->mark(a0); }
     {
@@ -1049,8 +1051,8 @@ int push(sg_engine* e, const sg_batch* b) {
         sp.key = pl.partitioned ? (dev ? b->key : sl.b_key) : nullptr;
         sp.ts = ts;
         sp.t_desc = e->t_desc;
+        sp.epoch = e->td_epoch;
         sp.tile_sum = e->tile_sum;
-        sp.tile_off = e->tile_off;
         sp.raw_e1 = e->raw_e1;
         sp.out_count = e->out_count;
         sp.batch_total = e->batch_total;
@@ -1071,7 +1073,7 @@ int push(sg_engine* e, const sg_batch* b) {
 #ifdef SG_EXPERIMENTS
         if (const char* x = getenv("SG_ORDER_EXP")) sp.exp = (uint32_t)strtoul(x, nullptr, 0);
 #endif
-        if (sgd_launch_scatter(sp, e->scan_tmp, e->scan_tmp_bytes, e->stream) != 0)
+        if (sgd_launch_scatter(sp, e->stream) != 0)
             throw HipError("ordering launch failed");
         if (proj) {
             if (e->n_agg) {  // aggregator arguments, then their per-key values in output order

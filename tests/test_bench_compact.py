@@ -44,7 +44,7 @@ def test_compact_line_fields_and_size():
         assert k in d, k
     assert d["value"] == 1.6e10 and d["detail"] == "profiles/d.json"
     rf = d["roofline"]
-    assert rf["traffic"] == 6.9e8 and abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-5
+    assert rf["traffic"] == 6.9e8 and abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-12
     assert d["cpu_baseline"]["cores"] == 1 and d["cpu_baseline"]["partition_parallel"]["threads"] == 16
     assert d["extra"]["L0"] == {"value": 1e10, "ms_per_step": 0.4, "frac": 0.1, "traffic_ratio": 3.0, "cpu": 1e6}
     assert d["extra"]["fanout_one_gpu"]["ratio_to_single"] == 0.6

@@ -63,7 +63,8 @@ def test_bench_two_rank_rehearsal_with_host_merge():
     assert len(lines) == 1, r.stdout[-2000:]
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["value"] > 0
-    mg = out["merge_inclusive"]
+    assert "error" not in out["extra"]["merge_inclusive"], out["extra"]
+    mg = json.load(open(os.path.join(ROOT, out["detail"])))["merge_inclusive"]   # (the full record beside the line)
     assert "error" not in mg, mg
     assert mg["value"] > 0 and mg["matches_per_step"] > 0 and mg["merge_records_per_s"] > 0
     assert not glob.glob("/dev/shm/sgmerge_29519_*")
