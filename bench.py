@@ -803,7 +803,7 @@ def fanout_one_gpu(sa, synth, torch, dev, cq, n_keys, batch, steps):
     merges the shards' matches into host memory, so both legs poll to the host).  The shards share the GPU: the
     ratio prices the fan-out's own work (the device split, the per-push host wait for the per-owner totals, the
     host seq maps and merge), not a speed-up.  `host_syncs_per_push` = sg_stats.host_syncs / pushes."""
-    W = 2
+    W = 4   # (the stream's live population and the fan-out's host staging reach their steady size over ~4 pushes)
     bats = [synth.stock_ticks_torch(torch, s * batch, batch, n_keys, dev) for s in range(steps + W)]
     torch.cuda.synchronize()
     res = {}

@@ -201,6 +201,9 @@ int sg_advance_time(sg_engine* e, int64_t now_ms);
 int sg_poll_matches(sg_engine* e, uint32_t mem, sg_match_batch* out);
 int sg_release_matches(sg_engine* e, sg_match_batch* m);
 int sg_get_stats(sg_engine* e, sg_stats* out);
+/* sg_stats only grows at its end, and sg_get_stats writes the whole struct of this header: a caller built against
+ * an older header passes its own sizeof(sg_stats) here and gets exactly that prefix (out_size 0: SG_ERR_INVALID). */
+int sg_get_stats_sized(sg_engine* e, sg_stats* out, size_t out_size);
 /* Diagnostics: the kernels this engine dispatches per push and per clock advance, in launch order, as a
  * NUL-terminated line of text truncated to out_len (no reference counterpart: the query plan a profiler's
  * kernel names map to, as EXPLAIN would print it). */
@@ -209,8 +212,8 @@ int sg_synchronize(sg_engine* e);
 /* Device batches produced on another stream (a hipStream_t of the engine's device, NULL = the legacy
  * default stream): the engine's later work waits for everything queued on `stream` so far, without a
  * host synchronisation (the multi-GPU reshard hands its output over this way).  A multi-device engine
- * (n_devices > 1): every later device-batch split waits for it (the stream may be on any of its devices;
- * one event per stream, recorded again by each call). */
+ * (n_devices > 1): the next device-batch split waits for it (the stream may be on any of its devices; each
+ * call records one event, waited on once by that split; the caller's current device is left unchanged). */
 int sg_wait_stream(sg_engine* e, void* stream);
 /* Partition purge (@purge(enable, interval, idle.period) on a partition; PartitionRuntimeImpl.java:368-401
  * removes idle keys and cleanGroupByStates() every state holder of the partition's queries, so the

@@ -1265,7 +1265,7 @@ struct GenEngine {
     uint32_t *t_cnt = nullptr, *t_first = nullptr, *t_off = nullptr;
     uint32_t *tile_pre = nullptr, *sup_sum = nullptr, *sup_off = nullptr;   // the batch ordering's tile prefixes
     unsigned long long* obase = nullptr;                  // the running match count before the batch
-    unsigned long long h_stat[4] = {0, 0, 0, 0};          // gen_poll's status words and their device copy
+    PinnedVec<unsigned long long> h_stat;                 // gen_poll's status words (pinned: one DMA copy) and their device copy
     unsigned long long* d_stat = nullptr;
     uint32_t* t_multi = nullptr;          // GenOut.t_multi
     int64_t* tk2 = nullptr;
@@ -2085,11 +2085,13 @@ int gen_poll(GenEngine* e, uint32_t mem, sg_match_batch* out, std::string& msg) 
                        (const uint32_t*)e->tile_max, e->out.cap,
                        (uint32_t)(GERR_KEY | GERR_CAP | GERR_MATCHCAP | GERR_CHAIN | GERR_REF), e->d_stat);
     GH_OK(hipGetLastError());
-    GH_OK(hipMemcpyAsync(e->h_stat, e->d_stat, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, e->stream));
+    e->h_stat.resize(4);
+    GH_OK(hipMemcpyAsync(e->h_stat.data(), e->d_stat, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                         e->stream));
     GH_OK(hipStreamSynchronize(e->stream));
-    const unsigned long long n = e->h_stat[0];
-    const uint32_t err = (uint32_t)e->h_stat[1];
-    const uint32_t tmax = (uint32_t)e->h_stat[2];
+    const unsigned long long n = e->h_stat.data()[0];
+    const uint32_t err = (uint32_t)e->h_stat.data()[1];
+    const uint32_t tmax = (uint32_t)e->h_stat.data()[2];
     if (tmax > (1u << 14)) e->cnt_skewed = true;  // (one wave splits a tile: skewed streams take the sorted grouping)
     if (err & GERR_KEY) {
         // reported once: the events with valid keys were processed, the others dropped

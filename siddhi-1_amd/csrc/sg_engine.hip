@@ -1721,6 +1721,14 @@ int sg_synchronize(sg_engine* e) {
     }
 }
 
+int sg_get_stats_sized(sg_engine* e, sg_stats* out, size_t out_size) {
+    if (!out || out_size == 0) return fail(SG_ERR_INVALID, "null stats or zero size");
+    sg_stats full{};
+    const int rc = sg_get_stats(e, &full);
+    if (rc == SG_OK) memcpy(out, &full, std::min(out_size, sizeof(sg_stats)));
+    return rc;
+}
+
 int sg_get_stats(sg_engine* e, sg_stats* out) {
     if (!e || !out) return fail(SG_ERR_INVALID, "null argument");
     if (e->shard) return shd_stats(e->shard, out);

@@ -35,16 +35,17 @@
 #include "sg_sharded.h"
 
 #include <string.h>
+#include <sys/mman.h>
 
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <functional>
-#include <map>
 #include <future>
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include <hip/hip_runtime.h>
@@ -53,6 +54,69 @@
 #include "state_doc.h"
 
 namespace {
+
+// host threads for the fan-out's per-element work (seq maps, merge, gather): SG_FAN_THREADS, else the hardware's
+// threads capped at 16 (the GPU boxes give a GPU's process 16 CPUs)
+uint32_t fan_threads() {
+    static const uint32_t t = [] {
+        if (const char* x = getenv("SG_FAN_THREADS")) return std::max(1u, (uint32_t)strtoul(x, nullptr, 0));
+        return std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    }();
+    return t;
+}
+// the allocator of the fan-out's host staging (seq maps, polled matches, merge codes: tens to hundreds of MB that
+// grow with the match rate): value-initialisation is a no-op, so a resize does not zero-fill what is about to be
+// overwritten, and blocks of 4 MB and more are mapped with transparent huge pages asked for, so first touching a
+// grown buffer costs one fault per 2 MB rather than per 4 KB
+template <class T> struct RawAlloc {
+    using value_type = T;
+    static constexpr size_t kBig = 4u << 20;
+    static constexpr int kPopulateWrite = 23;   // MADV_POPULATE_WRITE (Linux 5.14)
+    RawAlloc() = default;
+    template <class U> RawAlloc(const RawAlloc<U>&) {}
+    T* allocate(size_t n) {
+        const size_t b = n * sizeof(T);
+        if (b < kBig) return std::allocator<T>().allocate(n);
+        void* p = mmap(nullptr, b, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+        if (p == MAP_FAILED) throw std::bad_alloc();
+        (void)madvise(p, b, MADV_HUGEPAGE);
+        (void)madvise(p, b, kPopulateWrite);   // (faulted in by one call; kernels before 5.14 fault on first touch)
+        return (T*)p;
+    }
+    void deallocate(T* p, size_t n) {
+        const size_t b = n * sizeof(T);
+        if (b < kBig) std::allocator<T>().deallocate(p, n);
+        else munmap(p, b);
+    }
+    template <class U> void construct(U* p) { ::new ((void*)p) U; }
+    template <class U, class... A> void construct(U* p, A&&... a) { ::new ((void*)p) U(std::forward<A>(a)...); }
+    template <class U> bool operator==(const RawAlloc<U>&) const { return true; }
+    template <class U> bool operator!=(const RawAlloc<U>&) const { return false; }
+};
+template <class T> using RawVec = std::vector<T, RawAlloc<T>>;
+// a buffer sized to at least n elements: it only grows (by a quarter more than asked, so a slowly rising match
+// count does not regrow it every poll), so a reused buffer is neither re-initialised nor page-faulted again (the
+// element count that matters is kept beside it); keep = false: the old contents are not needed (not copied)
+template <class V> typename V::value_type* grow_to(V& v, size_t n, bool keep = true) {
+    if (v.size() >= n) return v.data();
+    const size_t c = n + n / 4;
+    if (!keep) V().swap(v);
+    v.reserve(c);
+    v.resize(c);
+    return v.data();
+}
+// fn(lo, hi) over [0, n) cut into up to T slices of at least 2^15 elements, run on T threads (the caller's included)
+template <class F> void par_for(uint64_t n, uint32_t T, const F& fn) {
+    T = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(T, n >> 15));
+    if (T <= 1) {
+        fn((uint64_t)0, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (uint32_t t = 1; t < T; t++) th.emplace_back([&, t] { fn(n * t / T, n * (t + 1) / T); });
+    fn((uint64_t)0, n / T);
+    for (auto& x : th) x.join();
+}
 
 struct ShardError : std::runtime_error {
     int code;
@@ -71,18 +135,80 @@ const uint64_t kMagic = 0x3248534753ull;  // "SGSH2" (v2: seq maps with their ba
 
 }  // namespace
 
-// a shard's local -> global seq map: local seq base + i maps to v[i]; entries below `base` were trimmed (no live
-// partial and no pending match references them)
+// a shard's local -> global seq map over the live local seqs [base, top): entries below `base` were trimmed (no live
+// partial and no pending match references them).  Stored in chunks of 2^20 entries (8 MB, huge pages, faulted in
+// when mapped) indexed by local seq >> 20: an append never moves what is there, a trim hands the chunks wholly
+// below `base` to a spare list the next appends take from — no copy and no fresh page once the map has reached its
+// peak (twice its live span: the trim check runs when it has doubled) (a contiguous vector regrew and re-faulted tens of MB, 10-30 ms, every few pushes)
+struct SeqChunkFree {
+    void operator()(uint64_t* p) const { munmap(p, 8ull << 20); }
+};
+using SeqChunk = std::unique_ptr<uint64_t[], SeqChunkFree>;
+
 struct SeqMap {
-    uint64_t base = 0;
-    std::vector<uint64_t> v;
-    uint64_t trim_at = 1u << 20;   // the size at which the next trim check runs (+ max(2^20, live span) after each)
-    uint64_t end() const { return base + v.size(); }
+    static constexpr uint32_t kShift = 20;
+    static constexpr uint64_t kMask = (1ull << kShift) - 1;
+    static constexpr size_t kSpare = 256;   // spare chunks kept (2 GB; in practice the map's peak less its live span)
+    uint64_t base = 0, top = 0;
+    uint64_t c0 = 0;                 // chunk number of chunks[0]
+    std::vector<SeqChunk> chunks, spare;
+    uint64_t trim_at = 1u << 20;     // the size at which the next trim check runs (+ max(2^20, live span) after each)
+    uint64_t size() const { return top - base; }
+    uint64_t end() const { return top; }
+    void reset(uint64_t b) {
+        chunks.clear();
+        base = top = b;
+        c0 = b >> kShift;
+    }
+    const uint64_t* ptr(uint64_t l) const { return chunks[(l >> kShift) - c0].get() + (l & kMask); }
+    uint64_t at(uint64_t l) const { return *ptr(l); }
+    static SeqChunk new_chunk() {
+        const size_t b = 8ull << 20;
+        void* p = mmap(nullptr, b, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+        if (p == MAP_FAILED) throw std::bad_alloc();
+        (void)madvise(p, b, MADV_HUGEPAGE);
+        (void)madvise(p, b, 23);   // MADV_POPULATE_WRITE (Linux 5.14; before it, faulted on first touch)
+        return SeqChunk((uint64_t*)p);
+    }
+    // n more entries at the end: fn(offset, dst, count) fills each contiguous piece of them
+    template <class F> void append_with(uint64_t n, const F& fn) {
+        if (chunks.empty()) c0 = top >> kShift;
+        for (uint64_t done = 0; done < n;) {
+            const uint64_t l = top + done, c = l >> kShift;
+            while (c - c0 >= chunks.size()) {
+                if (!spare.empty()) {
+                    chunks.push_back(std::move(spare.back()));
+                    spare.pop_back();
+                } else {
+                    chunks.push_back(new_chunk());
+                }
+            }
+            const uint64_t k = std::min<uint64_t>(n - done, ((c + 1) << kShift) - l);
+            fn(done, chunks[c - c0].get() + (l & kMask), k);
+            done += k;
+        }
+        top += n;
+    }
+    void append(const uint64_t* p, uint64_t n) {
+        append_with(n, [&](uint64_t o, uint64_t* d, uint64_t k) { memcpy(d, p + o, 8 * k); });
+    }
+    // fn(ptr, count) over the live entries in order
+    template <class F> void for_pieces(const F& fn) const {
+        for (uint64_t l = base; l < top;) {
+            const uint64_t k = std::min<uint64_t>(top - l, (((l >> kShift) + 1) << kShift) - l);
+            fn(ptr(l), k);
+            l += k;
+        }
+    }
     void trim(uint64_t keep_from) {
         if (keep_from <= base) return;
-        const uint64_t d = std::min<uint64_t>(keep_from - base, v.size());
-        v.erase(v.begin(), v.begin() + (ptrdiff_t)d);
-        base += d;
+        base = std::min(keep_from, top);
+        size_t d = 0;
+        while (d < chunks.size() && ((c0 + d + 1) << kShift) <= base) d++;
+        for (size_t i = 0; i < d; i++)
+            if (spare.size() < kSpare) spare.push_back(std::move(chunks[i]));
+        chunks.erase(chunks.begin(), chunks.begin() + (ptrdiff_t)d);
+        c0 += d;
     }
 };
 
@@ -134,7 +260,16 @@ struct ShardEngine {
         uint32_t next = 0;
     };
     std::vector<DevSplit> splits;   // by source device ordinal (lazily)
-    std::map<void*, std::pair<int, hipEvent_t>> waits;   // sg_wait_stream: caller stream -> (device, event)
+    // sg_wait_stream: one event per (caller stream, device), recorded by the call and waited on once by the next
+    // device split (then free for reuse by any stream of its device: the list is bounded by the streams named
+    // between two pushes, not by every stream ever named)
+    struct Wait {
+        void* stream;
+        int device;
+        hipEvent_t ev;
+        bool pending;
+    };
+    std::vector<Wait> waits;
     std::vector<Peer> peers;        // per shard (lazily)
     bool force_peer = false;        // SG_FAN_PEER_COPY (tests): peer-copy every part, even on the source device
     uint64_t max_batch = 0;
@@ -143,8 +278,8 @@ struct ShardEngine {
     ~ShardEngine() { free_device_buffers(); }
     void free_device_buffers() {
         for (auto& w : waits) {
-            (void)hipSetDevice(w.second.first);
-            (void)hipEventDestroy(w.second.second);
+            (void)hipSetDevice(w.device);
+            (void)hipEventDestroy(w.ev);
         }
         waits.clear();
         for (size_t r = 0; r < peers.size(); r++) {
@@ -190,12 +325,15 @@ struct ShardEngine {
     struct Out {
         uint64_t n = 0;
         uint32_t ns = 0, mc = 1, ni = 0;
-        std::vector<uint64_t> trig, slot, pval;
-        std::vector<uint32_t> key, len;
-        std::vector<int64_t> ts;
+        RawVec<uint64_t> trig, slot;
+        RawVec<uint32_t> key, len;
+        RawVec<int64_t> ts;
+        std::vector<uint64_t> pval;
         std::vector<uint8_t> pnull;
     };
     Out pend, out;
+    RawVec<uint64_t> codes;   // collect's output order
+    std::vector<Out> parts;   // collect's per-shard staging (kept: its buffers are reused, not page-faulted per poll)
     bool held = false;
     bool proj = false;
     bool heads = false;   // every shard orders its timer matches by the keys' queue heads (and reports them)
@@ -234,7 +372,7 @@ struct ShardEngine {
         if (local >= SG_BLANK_SEQ) return local;   // null / blank / timer markers pass through
         const SeqMap& m = gmap[r];
         if (local < m.base || local >= m.end()) throw ShardError(SG_ERR_DEVICE, "shard seq outside its map");
-        return m.v[local - m.base];
+        return m.at(local);
     }
 };
 
@@ -352,6 +490,11 @@ namespace {
         if (e_ != hipSuccess) throw ShardError(SG_ERR_DEVICE, std::string(#x) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
+static double fan_now() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+static const bool g_fan_prof = getenv("SG_FAN_PROF") != nullptr;   // (experiments: phase times to stderr)
+
 template <class T> T* fan_alloc(size_t n) {
     void* p = nullptr;
     FAN_OK(hipMalloc(&p, std::max<size_t>(n, 1) * sizeof(T)));
@@ -427,8 +570,11 @@ void push_device(ShardEngine* s, const sg_batch* b) {
     FAN_OK(hipSetDevice(src));
     for (uint32_t r = 0; r < N; r++)   // this set's previous readers are done (on the device)
         if (st.armed[r]) FAN_OK(hipStreamWaitEvent(p.stream, st.done[r], 0));
-    for (auto& w : s->waits)           // the producers the caller named (sg_wait_stream)
-        FAN_OK(hipStreamWaitEvent(p.stream, w.second.second, 0));
+    for (auto& w : s->waits)           // the producers the caller named since the last push (sg_wait_stream)
+        if (w.pending) {
+            FAN_OK(hipStreamWaitEvent(p.stream, w.ev, 0));
+            w.pending = false;
+        }
     std::vector<const void*> cols(nc);
     std::vector<uint32_t> cb(nc);
     std::vector<const uint8_t*> nul(nc, nullptr);
@@ -447,10 +593,12 @@ void push_device(ShardEngine* s, const sg_batch* b) {
                              ocols.data(), onul.data(), st.opos, st.key, p.totals, p.err, st.scratch, p.scratch_len,
                              p.stream);
     if (rc != SG_OK) throw ShardError(rc, "device split of the batch failed");
+    const double q0 = g_fan_prof ? fan_now() : 0.0;
     FAN_OK(hipMemcpyAsync(p.h_totals, p.totals, (N + 1) * 4, hipMemcpyDeviceToHost, p.stream));
     FAN_OK(hipMemcpyAsync(p.h_opos, st.opos, n * 4, hipMemcpyDeviceToHost, p.stream));
     FAN_OK(hipStreamSynchronize(p.stream));
     s->host_syncs++;
+    const double q1 = g_fan_prof ? fan_now() : 0.0;
     if (p.h_totals[N]) throw ShardError(SG_ERR_INVALID, "key id outside [0, n_keys)");
     // validated: nothing has changed yet (a rejected batch leaves every shard as it was)
     std::vector<uint64_t> off(N + 1, 0);
@@ -516,10 +664,12 @@ void push_device(ShardEngine* s, const sg_batch* b) {
             }
             c.cols = cp.data();
             c.nulls = anyNull ? np.data() : nullptr;
+            const double v0 = g_fan_prof ? fan_now() : 0.0;
             int rc2 = sg_wait_stream(s->sh[r], wait_on);
             if (rc2 != SG_OK) return rc2;
             rc2 = sg_push_batch(s->sh[r], &c);
             if (rc2 != SG_OK) return rc2;
+            const double v1 = g_fan_prof ? fan_now() : 0.0;
             pushed[r] = 1;
             // what reads the part is queued: the buffers it lives in are free once the shard's engine ran it
             if (copy) {
@@ -529,10 +679,16 @@ void push_device(ShardEngine* s, const sg_batch* b) {
                 sg_internal_record(s->sh[r], st.done[r]);
                 st.armed[r] = 1;
             }
-            SeqMap& g = s->gmap[r];
-            const size_t g0 = g.v.size();
-            g.v.resize(g0 + m);
-            for (uint64_t i = 0; i < m; i++) g.v[g0 + i] = b->seq_base + p.h_opos[off[r] + i];
+            const uint32_t* op = p.h_opos + off[r];
+            const uint64_t sb = b->seq_base;
+            s->gmap[r].append_with(m, [&](uint64_t o, uint64_t* gv, uint64_t k) {
+                par_for(k, std::max(1u, fan_threads() / N), [&](uint64_t lo, uint64_t hi) {
+                    for (uint64_t i = lo; i < hi; i++) gv[i] = sb + op[o + i];
+                });
+            });
+            if (g_fan_prof)
+                fprintf(stderr, "fan shard %u: push %.2f ms, seq map %.2f ms\n", r, (v1 - v0) * 1e3,
+                        (fan_now() - v1) * 1e3);
             return SG_OK;
         });
     } catch (...) {
@@ -542,6 +698,9 @@ void push_device(ShardEngine* s, const sg_batch* b) {
         throw;
     }
     (void)hipEventDestroy(split_done);
+    if (g_fan_prof)
+        fprintf(stderr, "fan push: split + wait %.2f ms, shard pushes + seq maps %.2f ms\n", (q1 - q0) * 1e3,
+                (fan_now() - q1) * 1e3);
 }
 
 }  // namespace
@@ -561,9 +720,10 @@ int shd_push(ShardEngine* s, const sg_batch* b) {
             c.seq_base = m.end();
             const int rc = sg_push_batch(s->sh[0], &c);
             if (rc != SG_OK) return rc;
-            const size_t m0 = m.v.size();
-            m.v.resize(m0 + n);
-            for (uint64_t i = 0; i < n; i++) m.v[m0 + i] = b->seq_base + i;
+            const uint64_t sb = b->seq_base;
+            m.append_with(n, [&](uint64_t o, uint64_t* mv, uint64_t k) {
+                for (uint64_t i = 0; i < k; i++) mv[i] = sb + o + i;
+            });
             return SG_OK;
         }
         if (!b->key) throw ShardError(SG_ERR_INVALID, "partitioned query needs key ids");
@@ -663,7 +823,7 @@ int shd_push(ShardEngine* s, const sg_batch* b) {
                 const int rc = sg_push_batch(s->sh[r], &c);
                 if (rc == SG_OK) {
                     pushed[r] = 1;
-                    m.v.insert(m.v.end(), u.glob.begin(), u.glob.end());
+                    m.append(u.glob.data(), u.glob.size());
                 }
                 return rc;
             });
@@ -701,36 +861,61 @@ namespace {
 // order of the keys' queue heads (each shard emitted its keys in that order; two shards' keys sharing a head is
 // the Scheduler collapse the single engine refuses), or by (fire time, key) for an engine that does
 // not order by heads
-static double fan_now() {
-    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
-}
-static const bool g_fan_prof = getenv("SG_FAN_PROF") != nullptr;   // (experiments: phase times to stderr)
 
 void collect(ShardEngine* s, bool timers) {
     const uint32_t N = s->N;
     const double c0 = g_fan_prof ? fan_now() : 0.0;
-    std::vector<ShardEngine::Out> parts(N);
+    std::vector<ShardEngine::Out>& parts = s->parts;
+    parts.resize(N);
     std::vector<std::vector<uint32_t>> hk(N);
     std::vector<std::vector<int64_t>> ht(N);
     s->each([&](uint32_t r) -> int {
         sg_match_batch m{};
+        const double w0 = g_fan_prof ? fan_now() : 0.0;
         int rc = sg_poll_matches(s->sh[r], SG_MEM_HOST, &m);
         if (rc != SG_OK) return rc;
+        const double w1 = g_fan_prof ? fan_now() : 0.0;
         ShardEngine::Out& p = parts[r];
         p.n = m.n;
         p.ns = m.n_slots;
         p.mc = m.max_chain ? m.max_chain : 1;
-        p.trig.resize(p.n);
-        p.key.resize(p.n);
-        p.ts.resize(p.n);
-        p.len.assign(m.chain_len, m.chain_len + p.n * p.ns);
-        p.slot.resize(p.n * p.ns * p.mc);
-        for (uint64_t i = 0; i < p.n; i++) {
-            p.trig[i] = m.trigger_seq[i] == SG_TIMER_SEQ ? SG_TIMER_SEQ : s->map_seq(r, m.trigger_seq[i]);
-            p.key[i] = N > 1 ? m.key[i] * N + r : m.key[i];
-            p.ts[i] = m.ts[i];
-        }
-        for (size_t j = 0; j < p.slot.size(); j++) p.slot[j] = s->map_seq(r, m.slot_seq[j]);
+        grow_to(p.trig, p.n, false);
+        grow_to(p.key, p.n, false);
+        grow_to(p.ts, p.n, false);
+        grow_to(p.len, p.n * p.ns, false);
+        grow_to(p.slot, p.n * p.ns * p.mc, false);
+        // local -> global seqs (the shard's map), global key ids: sliced over this shard's share of the host threads
+        const SeqMap& gm = s->gmap[r];
+        const uint64_t mb = gm.base, me = gm.end();
+        bool bad = false;
+        const uint64_t spm = (uint64_t)p.ns * p.mc;
+        par_for(p.n, std::max(1u, fan_threads() / N), [&](uint64_t lo, uint64_t hi) {
+            bool b = false;
+            auto map = [&](uint64_t l) -> uint64_t {
+                if (l >= SG_BLANK_SEQ) return l;   // null / blank / timer markers pass through
+                if (l < mb || l >= me) { b = true; return l; }
+                return gm.at(l);
+            };
+            const uint64_t PD = 24;   // (the slot seqs' map entries are scattered: fetched this many matches ahead)
+            for (uint64_t i = lo; i < hi; i++) {
+                if (i + PD < hi)
+                    for (uint64_t q = 0; q < spm; q++) {
+                        const uint64_t l = m.slot_seq[(i + PD) * spm + q];
+                        if (l >= mb && l < me) __builtin_prefetch(gm.ptr(l));
+                    }
+                const uint64_t tl = m.trigger_seq[i], tg = tl == SG_TIMER_SEQ ? SG_TIMER_SEQ : map(tl);
+                p.trig[i] = tg;
+                p.key[i] = N > 1 ? m.key[i] * N + r : m.key[i];
+                p.ts[i] = m.ts[i];
+                for (uint64_t q = 0; q < p.ns; q++) p.len[i * p.ns + q] = m.chain_len[i * p.ns + q];
+                for (uint64_t q = 0; q < spm; q++) {   // (the trigger's own slot is mapped already)
+                    const uint64_t l = m.slot_seq[i * spm + q];
+                    p.slot[i * spm + q] = l == tl ? tg : map(l);
+                }
+            }
+            if (b) bad = true;   // (a benign race: every writer stores true)
+        });
+        if (bad) throw ShardError(SG_ERR_DEVICE, "shard seq outside its map");
         if (s->proj) {
             sg_projection pr{};
             rc = sg_get_projection(s->sh[r], SG_MEM_HOST, &pr);
@@ -740,15 +925,14 @@ void collect(ShardEngine* s, bool timers) {
             p.pnull.assign(pr.null, pr.null + (size_t)pr.n_items * p.n);
         }
         if (timers && s->heads) sg_internal_heads(s->sh[r], hk[r], ht[r]);
-        return sg_release_matches(s->sh[r], &m);
+        const double w2 = g_fan_prof ? fan_now() : 0.0;
+        rc = sg_release_matches(s->sh[r], &m);
+        if (g_fan_prof)
+            fprintf(stderr, "fan shard %u: poll %.2f ms, map %.2f ms, release %.2f ms\n", r, (w1 - w0) * 1e3,
+                    (w2 - w1) * 1e3, (fan_now() - w2) * 1e3);
+        return rc;
     });
     const double c1 = g_fan_prof ? fan_now() : 0.0;
-    struct Ref {
-        uint32_t r;
-        uint64_t i;
-        int64_t head;
-    };
-    std::vector<Ref> ord;
     uint64_t total = 0;
     for (uint32_t r = 0; r < N; r++) {
         total += parts[r].n;
@@ -756,60 +940,71 @@ void collect(ShardEngine* s, bool timers) {
         s->mchain = std::max(s->mchain, parts[r].mc);
     }
     if (total == 0) return;
-    ord.reserve(total);
-    for (uint32_t r = 0; r < N; r++) {
-        const ShardEngine::Out& p = parts[r];
-        if (timers && s->heads) {
-            // the shard's output is its emitting keys' matches, key after key in head order (hk / ht)
-            size_t g = 0;
-            for (uint64_t i = 0; i < p.n; i++) {
-                const uint32_t lk = N > 1 ? p.key[i] / N : p.key[i];
-                if (i > 0 && p.key[i] != p.key[i - 1]) g++;
-                while (g < hk[r].size() && hk[r][g] != lk) g++;
-                if (g >= hk[r].size()) throw ShardError(SG_ERR_DEVICE, "timer match of a key without a recorded head");
-                ord.push_back({r, i, ht[r][g]});
-            }
-        } else {
-            for (uint64_t i = 0; i < p.n; i++) ord.push_back({r, i, 0});
-        }
-    }
+    // the output order as (shard << 48 | index) codes
+    RawVec<uint64_t>& code = s->codes;
+    grow_to(code, total, false);
     // batch matches only (no timer match in any part): each shard's run is already in trigger order (its local
     // seqs map to increasing global ones), and one trigger's matches all come from one shard, so the order is an
-    // N-way merge of the runs by trigger seq — O(n N) instead of a comparison sort of every match
+    // N-way merge of the runs by trigger seq: the parallel merge path of sg_merge_ts over the host threads
     bool merge = !timers;
     for (uint32_t r = 0; r < N && merge; r++)
         for (uint64_t i = 0; i < parts[r].n; i++)
-            if (parts[r].trig[i] == SG_TIMER_SEQ || (i > 0 && parts[r].trig[i] < parts[r].trig[i - 1])) {
-                merge = false;
+            if (parts[r].trig[i] >= (1ull << 63) || (i > 0 && parts[r].trig[i] < parts[r].trig[i - 1])) {
+                merge = false;   // (a timer match, or a run out of order)
                 break;
             }
     if (merge) {
-        ord.clear();
-        std::vector<uint64_t> at(N, 0);
-        for (uint64_t x = 0; x < total; x++) {
-            uint32_t best = N;
-            for (uint32_t r = 0; r < N; r++)
-                if (at[r] < parts[r].n && (best == N || parts[r].trig[at[r]] < parts[best].trig[at[best]])) best = r;
-            ord.push_back({best, at[best]++, 0});
+        std::vector<const int64_t*> runs(N);
+        std::vector<uint64_t> lens(N);
+        for (uint32_t r = 0; r < N; r++) {
+            runs[r] = (const int64_t*)parts[r].trig.data();
+            lens[r] = parts[r].n;
         }
-    } else
-    std::stable_sort(ord.begin(), ord.end(), [&](const Ref& a, const Ref& b) {
-        const ShardEngine::Out &A = parts[a.r], &B = parts[b.r];
-        const bool ta = A.trig[a.i] == SG_TIMER_SEQ, tb = B.trig[b.i] == SG_TIMER_SEQ;
-        if (ta != tb) return ta;
-        if (ta && s->heads) return a.head < b.head;
-        if (ta) {
-            if (A.ts[a.i] != B.ts[b.i]) return A.ts[a.i] < B.ts[b.i];
-            return A.key[a.i] < B.key[b.i];
+        if (sg_merge_ts(N, runs.data(), lens.data(), fan_threads(), code.data()) != SG_OK)
+            throw ShardError(SG_ERR_DEVICE, "merge of the shards' matches failed");
+    } else {
+        struct Ref {
+            uint32_t r;
+            uint64_t i;
+            int64_t head;
+        };
+        std::vector<Ref> ord;
+        ord.reserve(total);
+        for (uint32_t r = 0; r < N; r++) {
+            const ShardEngine::Out& p = parts[r];
+            if (timers && s->heads) {
+                // the shard's output is its emitting keys' matches, key after key in head order (hk / ht)
+                size_t g = 0;
+                for (uint64_t i = 0; i < p.n; i++) {
+                    const uint32_t lk = N > 1 ? p.key[i] / N : p.key[i];
+                    if (i > 0 && p.key[i] != p.key[i - 1]) g++;
+                    while (g < hk[r].size() && hk[r][g] != lk) g++;
+                    if (g >= hk[r].size()) throw ShardError(SG_ERR_DEVICE, "timer match of a key without a recorded head");
+                    ord.push_back({r, i, ht[r][g]});
+                }
+            } else {
+                for (uint64_t i = 0; i < p.n; i++) ord.push_back({r, i, 0});
+            }
         }
-        return A.trig[a.i] < B.trig[b.i];
-    });
-    if (timers && s->heads)
-        for (size_t x = 1; x < ord.size(); x++)
-            if (ord[x].r != ord[x - 1].r && ord[x].head == ord[x - 1].head)
-                throw ShardError(SG_ERR_UNSUPPORTED,
-                                 "two partition keys share a timer due time at one clock advance (reference Scheduler "
-                                 "collapse quirk, SURVEY A.10): input not supported");
+        std::stable_sort(ord.begin(), ord.end(), [&](const Ref& a, const Ref& b) {
+            const ShardEngine::Out &A = parts[a.r], &B = parts[b.r];
+            const bool ta = A.trig[a.i] == SG_TIMER_SEQ, tb = B.trig[b.i] == SG_TIMER_SEQ;
+            if (ta != tb) return ta;
+            if (ta && s->heads) return a.head < b.head;
+            if (ta) {
+                if (A.ts[a.i] != B.ts[b.i]) return A.ts[a.i] < B.ts[b.i];
+                return A.key[a.i] < B.key[b.i];
+            }
+            return A.trig[a.i] < B.trig[b.i];
+        });
+        if (timers && s->heads)
+            for (size_t x = 1; x < ord.size(); x++)
+                if (ord[x].r != ord[x - 1].r && ord[x].head == ord[x - 1].head)
+                    throw ShardError(SG_ERR_UNSUPPORTED,
+                                     "two partition keys share a timer due time at one clock advance (reference Scheduler "
+                                     "collapse quirk, SURVEY A.10): input not supported");
+        for (uint64_t x = 0; x < total; x++) code[x] = ((uint64_t)ord[x].r << 48) | ord[x].i;
+    }
     const double c2 = g_fan_prof ? fan_now() : 0.0;
     // append to pend (the chain dimension grows to the widest shard's)
     ShardEngine::Out& o = s->pend;
@@ -822,7 +1017,7 @@ void collect(ShardEngine* s, bool timers) {
         }
     if (o.n && o.ns != ns) throw ShardError(SG_ERR_DEVICE, "shards disagree on the slot count");
     if (o.n && mc != o.mc) {  // re-pad what is pending
-        std::vector<uint64_t> sl(o.n * ns * mc, SG_NULL_SEQ);
+        RawVec<uint64_t> sl(o.n * ns * mc, SG_NULL_SEQ);
         for (uint64_t q = 0; q < o.n * ns; q++)
             for (uint32_t c = 0; c < o.mc; c++) sl[q * mc + c] = o.slot[q * o.mc + c];
         o.slot.swap(sl);
@@ -834,11 +1029,11 @@ void collect(ShardEngine* s, bool timers) {
     o.ns = ns;
     o.mc = mc;
     o.ni = ni;
-    o.trig.resize(n1);
-    o.key.resize(n1);
-    o.ts.resize(n1);
-    o.len.resize(n1 * ns, 0);
-    o.slot.resize(n1 * ns * mc, SG_NULL_SEQ);
+    grow_to(o.trig, n1);
+    grow_to(o.key, n1);
+    grow_to(o.ts, n1);
+    grow_to(o.len, n1 * ns);
+    grow_to(o.slot, n1 * ns * mc);
     // projection: item-major over the pending rows -> rebuilt with the new row count
     std::vector<uint64_t> pv((size_t)ni * n1, 0);
     std::vector<uint8_t> pn((size_t)ni * n1, 0);
@@ -847,21 +1042,24 @@ void collect(ShardEngine* s, bool timers) {
             pv[(size_t)it * n1 + q] = o.pval[(size_t)it * n0 + q];
             pn[(size_t)it * n1 + q] = o.pnull[(size_t)it * n0 + q];
         }
-    for (uint64_t x = 0; x < total; x++) {
-        const ShardEngine::Out& p = parts[ord[x].r];
-        const uint64_t i = ord[x].i, d = n0 + x;
-        o.trig[d] = p.trig[i];
-        o.key[d] = p.key[i];
-        o.ts[d] = p.ts[i];
-        for (uint32_t sl = 0; sl < ns; sl++) {
-            o.len[d * ns + sl] = p.len[i * ns + sl];
-            for (uint32_t c = 0; c < p.mc; c++) o.slot[(d * ns + sl) * mc + c] = p.slot[(i * ns + sl) * p.mc + c];
+    par_for(total, fan_threads(), [&](uint64_t lo, uint64_t hi) {
+        for (uint64_t x = lo; x < hi; x++) {
+            const ShardEngine::Out& p = parts[code[x] >> 48];
+            const uint64_t i = code[x] & ((1ull << 48) - 1), d = n0 + x;
+            o.trig[d] = p.trig[i];
+            o.key[d] = p.key[i];
+            o.ts[d] = p.ts[i];
+            for (uint32_t sl = 0; sl < ns; sl++) {
+                o.len[d * ns + sl] = p.len[i * ns + sl];
+                for (uint32_t c = 0; c < mc; c++)
+                    o.slot[(d * ns + sl) * mc + c] = c < p.mc ? p.slot[(i * ns + sl) * p.mc + c] : SG_NULL_SEQ;
+            }
+            for (uint32_t it = 0; it < p.ni; it++) {
+                pv[(size_t)it * n1 + d] = p.pval[(size_t)it * p.n + i];
+                pn[(size_t)it * n1 + d] = p.pnull[(size_t)it * p.n + i];
+            }
         }
-        for (uint32_t it = 0; it < p.ni; it++) {
-            pv[(size_t)it * n1 + d] = p.pval[(size_t)it * p.n + i];
-            pn[(size_t)it * n1 + d] = p.pnull[(size_t)it * p.n + i];
-        }
-    }
+    });
     o.pval.swap(pv);
     o.pnull.swap(pn);
     o.n = n1;
@@ -898,7 +1096,7 @@ void trim_maps(ShardEngine* s) {
     std::vector<char> due(s->N, 0);
     bool any = false;
     for (uint32_t r = 0; r < s->N; r++)
-        if (s->gmap[r].v.size() >= s->gmap[r].trim_at) due[r] = any = 1;
+        if (s->gmap[r].size() >= s->gmap[r].trim_at) due[r] = any = 1;
     if (!any) return;
     std::vector<uint64_t> lo(s->N, 0);
     s->each([&](uint32_t r) -> int {
@@ -910,7 +1108,7 @@ void trim_maps(ShardEngine* s) {
         SeqMap& m = s->gmap[r];
         m.trim(std::min(lo[r], m.end()));
         // the next check once as many entries again (at least 2^20) were appended: amortised over the pushes
-        m.trim_at = m.v.size() + std::max<uint64_t>(1u << 20, m.v.size());
+        m.trim_at = m.size() + std::max<uint64_t>(1u << 20, m.size());
         s->trims++;
     }
 }
@@ -932,8 +1130,12 @@ int shd_poll(ShardEngine* s, uint32_t mem, sg_match_batch* out) {
         const double t0 = g_fan_prof ? fan_now() : 0.0;
         trim_maps(s);
         if (g_fan_prof) fprintf(stderr, "fan trim %.2f ms\n", (fan_now() - t0) * 1e3);
-        s->out = std::move(s->pend);
-        s->pend = ShardEngine::Out();
+        std::swap(s->out, s->pend);   // (pend keeps the old output's buffers, emptied: no fresh pages per poll)
+        ShardEngine::Out& e = s->pend;   // (its buffers keep their sizes: only n counts)
+        e.n = 0;
+        e.ns = 0;
+        e.mc = 1;
+        e.ni = 0;
         const ShardEngine::Out& o = s->out;
         out->n = o.n;
         out->n_slots = o.n ? o.ns : s->nslots;
@@ -966,7 +1168,7 @@ int shd_get_projection(ShardEngine* s, uint32_t mem, sg_projection* out) {
 
 int shd_release(ShardEngine* s, sg_match_batch* m) {
     s->held = false;
-    s->out = ShardEngine::Out();
+    s->out.n = 0;   // (its buffers are kept for the next poll's collect)
     if (m) memset(m, 0, sizeof(*m));
     return SG_OK;
 }
@@ -992,7 +1194,7 @@ int shd_stats(ShardEngine* s, sg_stats* out) {
         // each shard's sub-batches)
         out->host_staged_bytes = s->staged_bytes;
         out->seq_map_entries = 0;
-        for (const SeqMap& m : s->gmap) out->seq_map_entries += m.v.size();
+        for (const SeqMap& m : s->gmap) out->seq_map_entries += m.size();
         out->seq_map_trims = s->trims;
         out->host_syncs = s->host_syncs;
         return SG_OK;
@@ -1032,7 +1234,7 @@ int shd_snapshot(ShardEngine* s, void** buf, size_t* len) {
         std::vector<size_t> il(s->N, 0);
         s->each([&](uint32_t r) { return sg_snapshot(s->sh[r], &img[r], &il[r]); });
         size_t total = 16;
-        for (uint32_t r = 0; r < s->N; r++) total += 24 + il[r] + 8 * s->gmap[r].v.size();
+        for (uint32_t r = 0; r < s->N; r++) total += 24 + il[r] + 8 * s->gmap[r].size();
         uint8_t* o = (uint8_t*)malloc(total);
         if (!o) throw ShardError(SG_ERR_CAPACITY, "out of host memory");
         size_t off = 0;
@@ -1041,10 +1243,10 @@ int shd_snapshot(ShardEngine* s, void** buf, size_t* len) {
         put(&kMagic, 8);
         put(hdr, 8);
         for (uint32_t r = 0; r < s->N; r++) {
-            const uint64_t a[3] = {il[r], s->gmap[r].base, s->gmap[r].v.size()};
+            const uint64_t a[3] = {il[r], s->gmap[r].base, s->gmap[r].size()};
             put(a, 24);
             put(img[r], il[r]);
-            put(s->gmap[r].v.data(), 8 * s->gmap[r].v.size());
+            s->gmap[r].for_pieces([&](const uint64_t* q, uint64_t k) { put(q, 8 * k); });
             sg_free_buffer(img[r]);
         }
         *buf = o;
@@ -1083,9 +1285,8 @@ int shd_restore(ShardEngine* s, const void* buf, size_t len) {
             il[r] = a[0];
             off += a[0];
             if (a[2] > (len - off) / 8) throw ShardError(SG_ERR_INVALID, "sharded snapshot truncated");
-            maps[r].base = a[1];
-            maps[r].v.resize(a[2]);
-            memcpy(maps[r].v.data(), p + off, 8 * a[2]);
+            maps[r].reset(a[1]);
+            maps[r].append((const uint64_t*)(const void*)(p + off), a[2]);
             maps[r].trim_at = a[2] + std::max<uint64_t>(1u << 20, a[2]);
             off += 8 * a[2];
         }
@@ -1184,7 +1385,7 @@ int shd_state_import(ShardEngine* s, const void* buf, size_t len) {
             const std::vector<uint8_t> bytes = sd_write(parts[r]);
             return sg_state_import(s->sh[r], bytes.data(), bytes.size());
         });
-        for (uint32_t r = 0; r < s->N; r++) s->gmap[r].v.insert(s->gmap[r].v.end(), add[r].begin(), add[r].end());
+        for (uint32_t r = 0; r < s->N; r++) s->gmap[r].append(add[r].data(), add[r].size());
         s->failed = false;
         return SG_OK;
     } catch (const std::exception& ex) {
@@ -1192,22 +1393,38 @@ int shd_state_import(ShardEngine* s, const void* buf, size_t len) {
     }
 }
 
-// the fan-out reads a device batch first on its source device's split stream: every later split waits for the
-// work queued on `stream` so far (one event per caller stream, recorded again by each call; no host wait)
+// the fan-out reads a device batch first on its source device's split stream: the next split waits for the work
+// queued on `stream` so far (one event per call, taken once by that split; no host wait)
 int shd_wait_stream(ShardEngine* s, void* stream) {
     try {
         if (s->N == 1) return sg_wait_stream(s->sh[0], stream);   // (the one shard reads the caller's batch itself)
-        int dev = 0;
+        int prev = 0, dev = 0;
+        FAN_OK(hipGetDevice(&prev));
         if (stream) FAN_OK(hipStreamGetDevice((hipStream_t)stream, &dev));
-        else FAN_OK(hipGetDevice(&dev));
-        FAN_OK(hipSetDevice(dev));
-        auto it = s->waits.find(stream);
-        if (it == s->waits.end()) {
+        else dev = prev;
+        // this stream's entry, else a free one of its device (events belong to a device), else a new one
+        ShardEngine::Wait* w = nullptr;
+        for (auto& x : s->waits)
+            if (x.device == dev && x.stream == stream) w = &x;
+        for (size_t i = 0; i < s->waits.size() && !w; i++)
+            if (s->waits[i].device == dev && !s->waits[i].pending) w = &s->waits[i];
+        int rc = SG_OK;
+        if (hipSetDevice(dev) != hipSuccess) rc = SG_ERR_DEVICE;
+        if (rc == SG_OK && !w) {
             hipEvent_t x = nullptr;
-            FAN_OK(hipEventCreateWithFlags(&x, hipEventDisableTiming));
-            it = s->waits.emplace(stream, std::make_pair(dev, x)).first;
+            if (hipEventCreateWithFlags(&x, hipEventDisableTiming) != hipSuccess) rc = SG_ERR_DEVICE;
+            else {
+                s->waits.push_back({stream, dev, x, false});
+                w = &s->waits.back();
+            }
         }
-        FAN_OK(hipEventRecord(it->second.second, (hipStream_t)stream));
+        if (rc == SG_OK && hipEventRecord(w->ev, (hipStream_t)stream) != hipSuccess) rc = SG_ERR_DEVICE;
+        if (rc == SG_OK) {
+            w->stream = stream;
+            w->pending = true;
+        }
+        (void)hipSetDevice(prev);   // (the caller's current device is left as it was)
+        if (rc != SG_OK) throw ShardError(rc, "sg_wait_stream: event on the caller's stream failed");
         return SG_OK;
     } catch (const std::exception& ex) {
         return fail_from(ex);

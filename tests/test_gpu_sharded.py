@@ -291,3 +291,74 @@ def test_cabi_fanout_wait_stream_orders_the_split():
         _same(mo, mf)
         total += len(mo)
     assert total > 0
+
+
+def test_cabi_fanout_wait_stream_fresh_stream_per_batch():
+    """a caller that makes a new producer stream for every batch — each wait is taken once by the
+    next split (the events are reused, not one per stream ever named) and the caller's current device is left
+    as it was; the matches equal one engine fed after full synchronisations"""
+    from test_gpu_parity import _same
+    synth = importlib.import_module("siddhi-1_amd.synth")
+    app = sa.parse_app(SHAPES["two_state"])
+    cq = sa.compile_query(app, app.queries[0], sa.StringDictionary())
+    K, n = 257, 2000
+    lib = sa.load_hip_library()
+    mk = lambda devs=None: sa.NativeEngine(lib, "sg_", cq.ir, n_keys=K, max_batch=1 << 13, partial_capacity=64,
+                                           match_capacity=1 << 20, devices=devs)
+    one, fan = mk(), mk(_devices())
+    dev = torch.device("cuda", 0)
+    keep = []
+    total = 0
+    for b in range(6):
+        d = synth.stock_ticks(b * n, n, K, seed=300 + b, rate_per_ms=4)
+        host = {k: torch.from_numpy(v.view("int32") if v.dtype.kind == "u" else v).pin_memory() for k, v in d.items()}
+        t = {k: torch.zeros_like(v, device=dev) for k, v in host.items()}
+        torch.cuda.synchronize()
+        side = torch.cuda.Stream(device=dev)
+        with torch.cuda.stream(side):
+            torch.cuda._sleep(5_000_000)
+            for k in t:
+                t[k].copy_(host[k], non_blocking=True)
+        cols = (n, t["ts"].data_ptr(), [t["symbol"].data_ptr(), t["price"].data_ptr(), t["volume"].data_ptr()],
+                t["key"].data_ptr())
+        before = torch.cuda.current_device()
+        fan.wait_stream(side.cuda_stream)
+        assert torch.cuda.current_device() == before
+        fan.push(0, b * n, cols, [0, 1, 2], mem=sa.native.SG_MEM_DEVICE)
+        torch.cuda.synchronize()
+        one.push(0, b * n, cols, [0, 1, 2], mem=sa.native.SG_MEM_DEVICE)
+        keep.append((host, t, side))
+        mo, mf = one.poll(), fan.poll()
+        _same(mo, mf)
+        total += len(mo)
+    assert total > 0
+
+
+@pytest.mark.parametrize("multi", [False, True])
+def test_get_stats_sized_writes_only_the_callers_prefix(multi):
+    """sg_get_stats_sized copies min(out_size, sizeof(sg_stats)) — a caller built against an older,
+    shorter sg_stats gets its prefix and nothing past it"""
+    import ctypes as C
+    import numpy as np
+    synth = importlib.import_module("siddhi-1_amd.synth")
+    app = sa.parse_app(SHAPES["two_state"])
+    cq = sa.compile_query(app, app.queries[0], sa.StringDictionary())
+    lib = sa.load_hip_library()
+    e = sa.NativeEngine(lib, "sg_", cq.ir, n_keys=64, max_batch=4096, partial_capacity=32,
+                        devices=_devices() if multi else None)
+    d = synth.stock_ticks(0, 3000, 64, seed=9)
+    e.push(0, 0, d["ts"], [d["symbol"], d["price"], d["volume"]], None, d["key"])
+    e.poll()
+    full = e.stats()
+    nf = len(sa.native.sg_stats._fields_)
+    f = lib.sg_get_stats_sized
+    f.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
+    f.restype = C.c_int
+    for words in (1, 8, nf - 4, nf):
+        buf = np.full(nf + 4, 0xA5A5A5A5A5A5A5A5, dtype=np.uint64)
+        assert f(e.h, buf.ctypes.data, words * 8) == 0
+        for i, (name, _) in enumerate(sa.native.sg_stats._fields_[:words]):
+            if name not in ("group_ns", "advance_ns", "order_ns", "advance_hbm_ns"):
+                assert int(buf[i]) == full[name], name
+        assert (buf[words:] == np.uint64(0xA5A5A5A5A5A5A5A5)).all(), words
+    assert f(e.h, 0, 0) != 0
