@@ -47,13 +47,14 @@ def algorithmic_bytes(st):
             + 16 * st["partials_created"] + 24 * st["matches"])
 
 
-def pmc_traffic_general(cfg):
-    """NFA-kernel HBM bytes per pushed batch of a general-engine config from the committed PMC summary
+def pmc_traffic_general(cfg, summary="pmc_traffic_general.json"):
+    """NFA-kernel HBM bytes per pushed batch of a general-engine config (or, from pmc_traffic_variants.json, of a
+    C2 workload variant: every advance kernel of the push) from the committed PMC summary
     (tools/pmc_general_summary.py), only when it was measured on these exact kernel sources; (None, None)
     otherwise"""
     try:
         import hashlib
-        t = json.load(open(os.path.join(ROOT, "tools", "pmc_traffic_general.json")))
+        t = json.load(open(os.path.join(ROOT, "tools", summary)))
         h = hashlib.sha1()
         for f in t["sources"]:
             h.update(open(os.path.join(ROOT, "siddhi-1_amd", "csrc", f), "rb").read())
@@ -592,6 +593,7 @@ def c2_variant(sa, synth, torch, dev, kind, K, B, steps, warmup, cpu_seconds, no
     adv_s = d["advance_ns"] / 1e9 / launches
     alg = algorithmic_bytes(d) / launches
     gbs = alg / adv_s / 1e9 if adv_s > 0 else 0.0
+    traffic, traffic_src = pmc_traffic_general("C2_" + kind, "pmc_traffic_variants.json")
     out = {"value": B * steps / el, "unit": "events/s", "ms_per_step": el / steps * 1e3, "keys": K,
            "batch_events": B, "partial_capacity": 256, "engine": "two-state (C2)",
            "workload": ("C2 with Zipf(s=1.1) partition keys over 1,048,576 keys (key = bijection of the Zipf rank; the "
@@ -599,7 +601,8 @@ def c2_variant(sa, synth, torch, dev, kind, K, B, steps, warmup, cpu_seconds, no
                        ("C2 with per-key random-walk prices: p <- clamp(p + 0.25 N(0,1), 1, 100) at each of the key's "
                         "events, initial U[10, 40]"),
            "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
-                        "traffic": None, "kernel": "k_adv_m + k_hot_* + k_adv_m_h + k_adv_m_k (NFA advance)",
+                        "traffic": traffic, "traffic_source": traffic_src,
+                        "kernel": "k_adv_m + k_hot_* + k_adv_m_h + k_adv_m_k (NFA advance)",
                         "alg_bytes_per_launch": alg, "kernel_ms_per_launch": adv_s * 1e3,
                         "hbm_pass_and_hot_ms_per_launch": d["advance_hbm_ns"] / 1e6 / launches},
            "stages_ms_per_step": {"group": d["group_ns"] / 1e6 / steps, "advance": d["advance_ns"] / 1e6 / steps,

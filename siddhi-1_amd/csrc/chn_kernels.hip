@@ -57,11 +57,11 @@ namespace {
 #ifndef CHN_ABL
 #define CHN_ABL 0
 #endif
-constexpr int CHN_NW = 4;   // payload words of an event this kernel decodes (pack.h Pay<W>, W <= 4)
+constexpr int CHN_NW = CHN_MAXNW;   // attribute words of an event (pack.h Pay<W>, W <= 4; chn_shape checks absNW)
 constexpr uint32_t CHN_ORD_MASK = 0xffffffu;   // order stamp: low 24 bits of ord[]; the kept words' null bits above
 
-template <int NE, int KW> struct ChnKey {
-    static constexpr int R = CHN_R(NE + 1);
+template <int NE, int KW, int RR> struct ChnKey {
+    static constexpr int R = RR;
     static constexpr int XW = (NE + 1) / 2;   // 16-bit pool entries, two per word
     const cGenProgram& G;
     const GenArgs& A;
@@ -88,12 +88,15 @@ template <int NE, int KW> struct ChnKey {
                                     // only gets its new event's slot word and its timestamp
     bool stHigh, outside;           // loaded with a StateEvent past the first bitmap word / an event past CHN_PA: the store
                                     // rewrites those bitmap words too
+    bool canonOK;                   // the block was fresh or canonical: every dead slot's canonical entries are free, so
+                                    // a captured event is written to its entry (and its StateEvent updated) as it is
+                                    // captured, from the event's registers; else the store places and copies it
     uint32_t err;
     uint32_t scanned, created, matches;   // (this key's run: < 2^32)
 
     __device__ __forceinline__ ChnKey(const GenArgs& a, uint32_t key)
         : G(*(cGenProgram*)a.G), A(a), S(gp(a.state)), K(a.K), k(key), live(0), stg(0), pl0(0), pl1(0), stamp(0),
-          seedP(false), seedN(false), seedTs(-1), dirty(0), whole(0), stHigh(false), outside(false), err(0), scanned(0), created(0),
+          seedP(false), seedN(false), seedTs(-1), dirty(0), whole(0), stHigh(false), outside(false), canonOK(false), err(0), scanned(0), created(0),
           matches(0) {
         tbase = a.b.pay ? gp(a.b.ts)[0] : 0;
         sbase = a.b.seq_base;
@@ -122,6 +125,12 @@ template <int NE, int KW> struct ChnKey {
     }
     // new events take pool entries below PA (the window's R * NE events always fit there, chn_shape)
     __device__ __forceinline__ uint32_t poolArea() const { return G.SECAP < 64u ? G.SECAP : 64u; }
+    // the canonical pool entry of event i of the partial in slot j (a partial owns its events: `every` only on p0, so
+    // no clone shares them).  A block stored with every event at its canonical entry is marked GEN_W0_CHN and read
+    // back slot by slot: all lanes of the wave at slot j read the same words of their keys, adjacent in the
+    // key-interleaved block — coalesced, where a walk in list order reads a different entry per lane (one 64-B
+    // sector per 4-B word: ~4.6 KB per key per batch at P3)
+    static __device__ __forceinline__ uint32_t canon(int j, int i) { return (uint32_t)(j * NE + i); }
     __device__ __forceinline__ uint32_t& sqw(int j, int i) const { return cold[((uint32_t)i * R + (uint32_t)j) * 64u + lane]; }
     __device__ __forceinline__ uint32_t& ixw(int j, int h) const {
         return cold[((uint32_t)(NE + h) * R + (uint32_t)j) * 64u + lane];
@@ -137,6 +146,7 @@ template <int NE, int KW> struct ChnKey {
             seedN = true;
             seedTs = -1;
             fl[0] = GF_INIT;
+            canonOK = true;
             return true;     // (a fresh or purged key's block is zero)
         }
         const bool trusted = w0 == (1u | GEN_W0_CHN);
@@ -159,6 +169,7 @@ template <int NE, int KW> struct ChnKey {
                 seedN = nl != 0u;
             }
         }
+        if (trusted) return canonOK = loadCanonical();
         // every partial of every list, in list order (its order stamp), pending before newAndEvery
         const uint32_t PA = poolArea();
         for (int s = 1; s <= NE; ++s) {
@@ -250,6 +261,62 @@ template <int NE, int KW> struct ChnKey {
         }
         if (!trusted) dirty = whole = live;
         return true;
+    }
+
+    // a block this kernel stored in the canonical layout: the lists give each slot's state, staging and order stamp
+    // (list entry = StateEvent = slot; the list rows are read at the same position by every lane), then slot by slot
+    // the captured events at their canonical entries
+    __device__ __forceinline__ bool loadCanonical() {
+        for (int s = 1; s <= NE; ++s) {
+            for (uint32_t which = 0; which < 2u; ++which) {
+                const uint32_t n = W(ks(s) + KS_PLEN + which);
+                for (uint32_t e = 0; e < n; ++e) {
+                    const uint32_t j = W(ks(s) + KS_LISTS + which * G.L + e);
+                    if (stamp >= (uint32_t)R || j >= (uint32_t)R || ((live >> j) & 1u)) return false;
+#pragma unroll
+                    for (int jj = 0; jj < R; ++jj) ord[jj] = (uint32_t)jj == j ? stamp : ord[jj];
+                    live |= 1u << j;
+                    if (which) stg |= 1u << j;
+                    if ((uint32_t)(s - 1) & 1u) pl0 |= 1u << j;
+                    if ((uint32_t)(s - 1) & 2u) pl1 |= 1u << j;
+                    stamp++;
+                }
+            }
+        }
+        bool ok = true;
+#pragma unroll
+        for (int jj = 0; jj < R; ++jj) {
+            if (!((live >> jj) & 1u)) continue;
+            const int s = (int)(((pl0 >> jj) & 1u) | (((pl1 >> jj) & 1u) << 1)) + 1;
+            uint32_t nbits = 0;
+#pragma unroll
+            for (int i = 0; i < NE; ++i) {
+                if (i >= s) continue;
+                const uint32_t ev = canon(jj, i);
+                const int64_t d = R64(sew(ev, SE_SEQ)) - (int64_t)sbase;
+                ok &= d >= INT32_MIN && d <= INT32_MAX;
+                sqw(jj, i) = (uint32_t)(int32_t)d;
+                if (i == 0) {
+                    const int64_t t = R64(sew(ev, SE_TS));
+                    const int64_t o = t - tbase;
+                    ok &= t != -1 && o > -SGD_TS_LIM && o < SGD_TS_LIM;
+                    t1[jj] = (int32_t)o;
+                }
+                if (KW > 0) {
+                    const uint32_t nb = W(sew(ev, SE_NULL));
+#pragma unroll
+                    for (int c = 0; c < KW; ++c) {
+                        kw[jj][i][c] = W(sew(ev, G.absWordAt[G.chnKeepW[c]]));
+                        nbits |= ((nb >> G.chnKeepA[c]) & 1u) << (i * KW + c);
+                    }
+                }
+            }
+            ord[jj] |= nbits << 24;
+#pragma unroll
+            for (int h = 0; h < XW; ++h)
+                ixw(jj, h) = canon(jj, 2 * h) | ((2 * h + 1 < NE ? canon(jj, 2 * h + 1) : 0xffffu) << 16);
+        }
+        return ok;
     }
 
     // the kept words and their null bits of the partial in slot j (j at run time: selects over the static slots, so
@@ -421,6 +488,30 @@ template <int NE, int KW> struct ChnKey {
         gp(A.o.t_cnt)[pos] = c;
     }
 
+    // ---- a captured event written where it is captured (canonOK): its StreamEvent at the canonical entry from the
+    // event's registers (every attribute word is in ev.w: reg_layout), the StateEvent's slot word and timestamp
+    __device__ __forceinline__ void putEvent(uint32_t to, const AbsEv<CHN_NW>& ev) const {
+        W64(sew(to, SE_SEQ), (int64_t)ev.seq);
+        W64(sew(to, SE_TS), ev.ts);
+        W(sew(to, SE_NEXT)) = GEN_NIL;
+        W(sew(to, SE_RC)) = 1u;
+#pragma unroll
+        for (int q = 0; q < CHN_NW; ++q)
+            if ((uint32_t)q < G.absNW) W(sew(to, G.absWordAt[q])) = ev.w[q];
+        W(sew(to, SE_NULL)) = ev.nb;
+    }
+    __device__ __forceinline__ void captured(int j, int i, const AbsEv<CHN_NW>& ev, bool fresh) const {
+        const uint32_t e = canon(j, i), sb = G.offST + (uint32_t)j * G.stWords;
+        putEvent(e, ev);
+        if (fresh) {
+            for (int q = 0; q < G.nslots; q++) W(sb + ST_SLOTS + (uint32_t)q) = GEN_NIL;
+            W(sb + ST_TYPE) = 0u;
+            W(sb + ST_RC) = 1u;
+        }
+        W(sb + ST_SLOTS + sid(i)) = e;
+        W64(sb + ST_TS, ev.ts);
+    }
+
     // ---- one event of this key; false: stopped before it (the window could overflow, or the timestamp is
     // outside the 32-bit offsets), the general kernel continues from it
     __device__ __forceinline__ bool event(const AbsEv<CHN_NW>& ev, uint32_t pos) {
@@ -507,8 +598,14 @@ template <int NE, int KW> struct ChnKey {
                     ord[jj] = here ? (stamp | (((ord[jj] >> 24) | nbn) << 24)) : ord[jj];
                 }
                 stamp++;
-                sqw(j, s) = (uint32_t)qn;   // the event's seq, no pool entry yet (LDS)
-                ixw(j, s >> 1) |= 0xffffu << ((s & 1) * 16);
+                sqw(j, s) = (uint32_t)qn;   // the event's seq (LDS)
+                if (canonOK) {              // its pool entry, written now
+                    const uint32_t sh = (uint32_t)(s & 1) * 16u;
+                    ixw(j, s >> 1) = (ixw(j, s >> 1) & ~(0xffffu << sh)) | (canon(j, s) << sh);
+                    captured(j, s, ev, false);
+                } else {                    // no pool entry yet: the store places it
+                    ixw(j, s >> 1) |= 0xffffu << ((s & 1) * 16);
+                }
             }
             dirty |= H;
             const uint32_t ns = (uint32_t)s;   // new state s + 1: (s) in the planes
@@ -528,7 +625,7 @@ template <int NE, int KW> struct ChnKey {
             const bool hit = evalOn(0, none, ev);
             fl[0] = hit ? (fl[0] | GF_CHANGED) : (fl[0] & ~(uint32_t)GF_CHANGED);
             if (hit) {
-                const uint32_t fr = ~live & ((1u << R) - 1u);
+                const uint32_t fr = ~live & (R >= 32 ? 0xffffffffu : ((1u << (R & 31)) - 1u));
                 const int j = __ffs(fr) - 1;   // (the window had room: checked above)
                 uint32_t nb = 0;
                 uint32_t wk[KW > 0 ? KW : 1];
@@ -551,7 +648,8 @@ template <int NE, int KW> struct ChnKey {
                 }
                 sqw(j, 0) = (uint32_t)qn;
 #pragma unroll
-                for (int h = 0; h < XW; ++h) ixw(j, h) = 0xffffffffu;
+                for (int h = 0; h < XW; ++h) ixw(j, h) = (h == 0 && canonOK) ? (canon(j, 0) | 0xffff0000u) : 0xffffffffu;
+                if (canonOK) captured(j, 0, ev, true);
                 stamp++;
                 live |= 1u << j;
                 stg |= 1u << j;
@@ -592,9 +690,8 @@ template <int NE, int KW> struct ChnKey {
     }
 
     // ---- store: the lists (rewritten), partial j = StateEvent j (rewritten when dirty), the seed = StateEvent R; the
-    // events carried in stay where they are, the events captured in this batch take free pool entries below PA
+    // events carried in stay where they are, the events captured in this batch take their canonical pool entries
     __device__ __forceinline__ void store() {
-        W(0) = 1u | GEN_W0_CHN;
 #pragma unroll
         for (int i = 0; i <= NE; ++i) W(ks(i) + KS_FLAGS) = fl[i];
         W(ks(0) + KS_PLEN) = seedP ? 1u : 0u;
@@ -618,25 +715,28 @@ template <int NE, int KW> struct ChnKey {
                 if (e < PA) occ |= 1ull << e;
             }
         }
-        // the partials in stamp order: each one's list position is the count of its list so far
-        uint32_t plen[NE + 1], nlen[NE + 1];
+        // the lists, row by row: each list's members in stamp order (lanes at the same position write adjacent words)
 #pragma unroll
-        for (int q = 0; q <= NE; ++q) plen[q] = nlen[q] = 0;
-        for (uint32_t m = live; m;) {
-            const int j = firstOf(m);
-            m &= ~(1u << j);
-            const int s = (int)(((pl0 >> j) & 1u) | (((pl1 >> j) & 1u) << 1)) + 1;
-            const bool staged = (stg >> j) & 1u;
-            uint32_t r = 0;
+        for (int q = 1; q <= NE; ++q) {
+            const uint32_t M = smask(q);
 #pragma unroll
-            for (int q = 1; q <= NE; ++q) {
-                r = q == s ? (staged ? nlen[q] : plen[q]) : r;
-                nlen[q] += (q == s && staged) ? 1u : 0u;
-                plen[q] += (q == s && !staged) ? 1u : 0u;
+            for (uint32_t which = 0; which < 2u; ++which) {
+                uint32_t r = 0;
+                for (uint32_t m = M & (which ? stg : ~stg); m; r++) {
+                    const int j = firstOf(m);
+                    m &= ~(1u << j);
+                    W(ks(q) + KS_LISTS + which * G.L + r) = (uint32_t)j;
+                }
+                W(ks(q) + KS_PLEN + which) = r;
             }
-            W(ks(s) + KS_LISTS + (staged ? G.L : 0u) + r) = (uint32_t)j;
-            if (!((dirty >> j) & 1u)) continue;   // (its StateEvent and events are in place)
-            // its StateEvent: ts = its last event's (StreamPostStateProcessor.java:68)
+        }
+        // the rewritten partials, slot by slot: partial j = StateEvent j, its new events at their canonical entries
+        // (an entry an event carried in from a general layout holds: the lowest free one, and the block is stored
+        // unmarked, to be read back through the checked path)
+        bool canonical = true;
+        for (int j = 0; j < R && !canonOK; ++j) {   // (canonOK: written as they were captured)
+            if (!((dirty >> j) & 1u)) continue;
+            const int s = (int)(((pl0 >> j) & 1u) | (((pl1 >> j) & 1u) << 1)) + 1;
             const uint32_t sb = G.offST + (uint32_t)j * G.stWords;
             const bool all = (whole >> j) & 1u;
             if (all)
@@ -645,7 +745,8 @@ template <int NE, int KW> struct ChnKey {
                 uint32_t e = getIx(j, i);
                 const uint32_t pos = sqw(j, i);   // (captured in this batch: its batch position)
                 if (e == 0xffffu) {
-                    e = (uint32_t)(__ffsll((long long)~occ) - 1);   // (< PA: the window's events fit, chn_shape)
+                    e = canon(j, i);
+                    if ((occ >> e) & 1ull) e = (uint32_t)(__ffsll((long long)~occ) - 1);   // (< PA, chn_shape)
                     occ |= 1ull << e;
                     storeEvent(e, pos);
                     if (i == s - 1) W64(sb + ST_TS, gp(A.b.ts)[pos]);
@@ -654,21 +755,22 @@ template <int NE, int KW> struct ChnKey {
                     if (i == s - 1) W64(sb + ST_TS, R64(sew(e, SE_TS)));
                     W(sb + ST_SLOTS + sid(i)) = e;
                 }
+                canonical &= e == canon(j, i);
             }
             if (all) {
                 W(sb + ST_TYPE) = 0u;
                 W(sb + ST_RC) = 1u;
             }
         }
-#pragma unroll
-        for (int q = 1; q <= NE; ++q) {
-            W(ks(q) + KS_PLEN) = plen[q];
-            W(ks(q) + KS_NLEN) = nlen[q];
-        }
+        // (a partial not rewritten was loaded from a marked, canonical block: a block loaded through the checked path
+        // has every partial rewritten)
+        W(0) = canonical ? (1u | GEN_W0_CHN) : 1u;
         // free bitmaps: StateEvents = the live slots and the seed; StreamEvents = the entries referenced
-        W(G.offSTfree) = live | ((seedP || seedN) ? (1u << R) : 0u);
+        const uint32_t seedBit = (seedP || seedN) ? 1u : 0u;   // (the seed is StateEvent R: word R / 32)
+        W(G.offSTfree) = live | (R < 32 ? seedBit << (R & 31) : 0u);
+        if (R >= 32) W(G.offSTfree + 1) = seedBit;
         if (stHigh)
-            for (uint32_t q = 1; q < (G.STCAP + 31) / 32; q++) W(G.offSTfree + q) = 0u;
+            for (uint32_t q = R >= 32 ? 2u : 1u; q < (G.STCAP + 31) / 32; q++) W(G.offSTfree + q) = 0u;
         const uint32_t nw = (G.SECAP + 31) / 32;
         W(G.offSEfree) = (uint32_t)occ;
         if (nw > 1) W(G.offSEfree + 1) = (uint32_t)(occ >> 32);
@@ -719,62 +821,117 @@ __device__ __forceinline__ void chn_gather(const GenArgs& a, const cGenProgram& 
 }
 
 // ---- batch: one lane per key walks its events of the key-sorted batch ----
+// ---- one key's run [b, e) of the key-sorted batch by one lane: false = handed over at `stop` (the general kernel,
+// or the wide window, continues from the event where it stopped; stop = b: the block is not this kernel's)
+template <int NE, int KW, int RR> struct ChnRun {
+    unsigned long long scanned = 0, created = 0, matches = 0, keys = 0;
+    uint32_t err = 0;
+    bool fb = false;
+    uint32_t stop = 0;
+    __device__ __forceinline__ void run(const GenArgs& a, uint32_t key, uint32_t b, uint32_t e, uint32_t* cold) {
+        ChnKey<NE, KW, RR> L(a, key);
+        L.cold = cold;
+        bool walk = b < e;
+        fb = false;
+        stop = b;
+        if (walk && !(CHN_ABL == 3 ? (L.seedN = true, true) : L.load())) {  // not this kernel's state: handed over whole
+            fb = true;
+            walk = false;
+        }
+        if (walk) {
+            const cGenProgram& G = *(cGenProgram*)a.G;
+            PayAhead<CHN_NW> ahead;
+            ahead.first(a, b, e);
+            uint32_t i = b;
+            for (; i < e; i++) {
+                AbsEv<CHN_NW> ev;
+                uint32_t pos;
+                if (a.b.pay) {
+                    ahead.next(a, i, e, L.tbase, ev);
+                    pos = (uint32_t)(ev.seq - a.b.seq_base);
+                } else {
+                    pos = a.b.sidx ? gp(a.b.sidx)[i] : i;
+                    ev.ts = gp(a.b.ts)[pos];
+                    ev.seq = a.b.seq_base + pos;
+                    chn_gather(a, G, pos, ev);
+                }
+                if (CHN_ABL == 2) continue;
+                if (!L.event(ev, pos)) break;
+            }
+            if (CHN_ABL != 1) L.store();   // (a hand-over: the next kernel continues from the block)
+            if (i < e) {
+                fb = true;
+                stop = i;
+            } else {
+                keys++;
+            }
+        }
+        scanned += L.scanned;
+        created += L.created;
+        matches += L.matches;
+        err |= L.err;
+    }
+};
+
+// ---- batch: one lane per key walks its events of the key-sorted batch ----
 template <int NE, int KW> __device__ __forceinline__ void chn_batch(const GenArgs& a) {
+    constexpr int R = CHN_R(NE + 1);
     const uint32_t key = blockIdx.x * 64u + threadIdx.x;
     uint32_t b = 0, e = 0;
     if (key < a.K) {
         b = gp(a.b.seg_begin)[key];
         e = gp(a.b.seg_end)[key];
     }
-    __shared__ uint32_t cold[CHN_R(NE + 1) * (NE + (NE + 1) / 2) * 64];
-    ChnKey<NE, KW> L(a, key < a.K ? key : 0u);
-    L.cold = cold;
-    bool walk = b < e;
-    bool fb = false;
-    uint32_t stop = b;
-    if (walk && !(CHN_ABL == 3 ? (L.seedN = true, true) : L.load())) {  // not this kernel's state: the general kernel walks the whole run
-        fb = true;
-        walk = false;
-    }
-    unsigned long long ky = 0;
-    if (walk) {
-        const cGenProgram& G = *(cGenProgram*)a.G;
-        PayAhead<CHN_NW> ahead;
-        ahead.first(a, b, e);
-        uint32_t i = b;
-        for (; i < e; i++) {
-            AbsEv<CHN_NW> ev;
-            uint32_t pos;
-            if (a.b.pay) {
-                ahead.next(a, i, e, L.tbase, ev);
-                pos = (uint32_t)(ev.seq - a.b.seq_base);
-            } else {
-                pos = a.b.sidx ? gp(a.b.sidx)[i] : i;
-                ev.ts = gp(a.b.ts)[pos];
-                ev.seq = a.b.seq_base + pos;
-                chn_gather(a, G, pos, ev);
+    __shared__ uint32_t cold[R * (NE + (NE + 1) / 2) * 64];
+    ChnRun<NE, KW, R> r;
+    r.run(a, key < a.K ? key : 0u, b, e, cold);
+    abs_fallback(a, r.fb, key, r.stop);
+    abs_wave_stats(a, r.scanned, r.created, r.matches, r.keys, r.err, r.fb ? 1ull : 0ull);
+}
+
+// ---- the keys the chain kernel handed over (its window full, or a block it cannot take), in the wide window: a
+// fixed grid of waves striding the list (its length is on the device), each key from the event where it stopped;
+// what this window cannot hold goes on to the general kernel (fb2).  Its hand-overs are not counted again as
+// window spills.
+template <int NE, int KW> __device__ __forceinline__ void chn_wide(const GenArgs& a) {
+    constexpr int R = CHN_RW(NE + 1);
+    __shared__ uint32_t cold[R * (NE + (NE + 1) / 2) * 64];
+    ChnRun<NE, KW, R> r;
+    const unsigned long long n = *a.fb_n;
+    for (unsigned long long base = (unsigned long long)blockIdx.x * 64u; base < n;
+         base += (unsigned long long)gridDim.x * 64u) {   // (wave-uniform)
+        const unsigned long long li = base + threadIdx.x;
+        uint32_t key = 0, b = 0, e = 0;
+        if (li < n) {
+            key = gp(a.fb_list)[li];
+            b = gp(a.fb_start)[key];
+            e = gp(a.b.seg_end)[key];
+        }
+        r.run(a, key, b, e, cold);
+        // (wave-aggregated append to the general kernel's list)
+        const unsigned long long m = __ballot(r.fb);
+        if (m) {
+            const int lane = threadIdx.x & 63;
+            unsigned long long b0 = 0;
+            if (lane == __ffsll((long long)m) - 1) b0 = atomicAdd(a.fb2_n, (unsigned long long)__popcll(m));
+            b0 = __shfl(b0, __ffsll((long long)m) - 1, 64);
+            if (r.fb) {
+                gp(a.fb2_list)[b0 + __popcll(m & ((1ull << lane) - 1ull))] = key;
+                gp(a.fb2_start)[key] = r.stop;
             }
-            if (CHN_ABL == 2) continue;
-            if (!L.event(ev, pos)) break;
-        }
-        if (CHN_ABL != 1) L.store();   // (a hand-over: the general kernel continues from the block)
-        if (i < e) {
-            fb = true;
-            stop = i;
-        } else {
-            ky = 1;
         }
     }
-    abs_fallback(a, fb, key, stop);
-    abs_wave_stats(a, L.scanned, L.created, L.matches, ky, L.err, fb ? 1ull : 0ull);
+    abs_wave_stats(a, r.scanned, r.created, r.matches, r.keys, r.err, 0ull);
 }
 
 }  // namespace
 
-// One kernel per (events a partial can hold, attribute words kept per captured event).  Occupancy floor 3 waves per
-// SIMD (168 VGPRs): the window and the event in flight stay in registers.
+// One kernel per (events a partial can hold, attribute words kept per captured event).  Occupancy floor 2 waves per
+// SIMD (256 VGPRs): the window, the event in flight and the captured event's stores stay in registers — at 3 waves
+// (168 VGPRs) the 3-state kernel spilled ~240 B per lane inside the walk and ran P3 at 8.7e8 events/s, at 2 at
+// 1.09e9 (tools/exp_chain.py, one box, same build otherwise)
 #ifndef SG_CHN_WAVES
-#define SG_CHN_WAVES 3
+#define SG_CHN_WAVES 2
 #endif
 #define CHN_KERNEL(NE, KW)                                                                                          \
     extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SG_CHN_WAVES, 8)))          \
@@ -791,3 +948,19 @@ CHN_KERNEL(2, 2)
 CHN_KERNEL(3, 0)
 CHN_KERNEL(3, 1)
 CHN_KERNEL(3, 2)
+// the wide window: one wave per SIMD (up to 512 VGPRs)
+#define CHN_WIDE_KERNEL(NE, KW)                                                                                     \
+    extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 8)))                     \
+    k_chn_wide_##NE##_##KW(const GenArgs ap) {                                                                      \
+        (void)ap;                                                                                                   \
+        chn_wide<NE, KW>(*(const GenArgs*)(const void*)__builtin_amdgcn_kernarg_segment_ptr());                     \
+    }
+CHN_WIDE_KERNEL(1, 0)
+CHN_WIDE_KERNEL(1, 1)
+CHN_WIDE_KERNEL(1, 2)
+CHN_WIDE_KERNEL(2, 0)
+CHN_WIDE_KERNEL(2, 1)
+CHN_WIDE_KERNEL(2, 2)
+CHN_WIDE_KERNEL(3, 0)
+CHN_WIDE_KERNEL(3, 1)
+CHN_WIDE_KERNEL(3, 2)

@@ -188,14 +188,19 @@ struct GenProgram {
     // attribute chnKeepA[c]; chnAttrK[a] = the kept index of attribute a's first word, or -1) and chnSlotEv[s] is
     // the event index (state) whose event slot s holds
     int32_t chnOk, chnN, chnEvery, chnKW;
+    int32_t chnWide;   // the wide-window kernel takes the keys the chain kernel hands over (its window fits the block)
     int32_t chnP[4];
     uint32_t chnKeepW[2], chnKeepA[2];
     int32_t chnAttrK[GEN_MAXA];
     int32_t chnSlotEv[GEN_MAXSLOT];
 };
 #define CHN_MAXN 4       // chn_kernels.hip: states of a chain
-// chn_kernels.hip: partials a key's register window holds, for a chain of n states
+#define CHN_MAXNW 4      // chn_kernels.hip CHN_NW: attribute words of a chained-state stream's event
+// chn_kernels.hip: partials a key's register window holds, for a chain of n states (k_chn_batch, 2 waves per SIMD),
+// and the wide window of the kernel the keys that outgrow it go to (k_chn_wide, 1 wave per SIMD: up to 512 VGPRs;
+// its canonical pool entries, n - 1 per partial, stay below 64)
 #define CHN_R(n) ((n) == 2 ? 24 : (n) == 3 ? 20 : 12)
+#define CHN_RW(n) ((n) == 2 ? 32 : (n) == 3 ? 32 : 21)
 
 // KeyState field offsets inside a processor's record
 #define KS_FLAGS 0

@@ -69,10 +69,16 @@ static const AbsKernel kCntBatch[ABS_MAXNW + 1] = {nullptr, k_cnt_batch_1, k_cnt
 #define CHN_DECL(NE) extern "C" __global__ void k_chn_batch_##NE##_0(const GenArgs ap); \
     extern "C" __global__ void k_chn_batch_##NE##_1(const GenArgs ap); extern "C" __global__ void k_chn_batch_##NE##_2(const GenArgs ap);
 CHN_DECL(1) CHN_DECL(2) CHN_DECL(3)
-// [n - 2][kept words]: the chain kernels (chn_kernels.hip)
+#define CHNW_DECL(NE) extern "C" __global__ void k_chn_wide_##NE##_0(const GenArgs ap); \
+    extern "C" __global__ void k_chn_wide_##NE##_1(const GenArgs ap); extern "C" __global__ void k_chn_wide_##NE##_2(const GenArgs ap);
+CHNW_DECL(1) CHNW_DECL(2) CHNW_DECL(3)
+// [n - 2][kept words]: the chain kernels (chn_kernels.hip), and their wide-window kernels over the keys handed over
 static const AbsKernel kChnBatch[CHN_MAXN - 1][3] = {{k_chn_batch_1_0, k_chn_batch_1_1, k_chn_batch_1_2},
                                                      {k_chn_batch_2_0, k_chn_batch_2_1, k_chn_batch_2_2},
                                                      {k_chn_batch_3_0, k_chn_batch_3_1, k_chn_batch_3_2}};
+static const AbsKernel kChnWide[CHN_MAXN - 1][3] = {{k_chn_wide_1_0, k_chn_wide_1_1, k_chn_wide_1_2},
+                                                    {k_chn_wide_2_0, k_chn_wide_2_1, k_chn_wide_2_2},
+                                                    {k_chn_wide_3_0, k_chn_wide_3_1, k_chn_wide_3_2}};
 #define ABSF_DECL(NW) extern "C" __global__ void k_abs_flush_##NW(const GenArgs ap);
 ABSF_DECL(1) ABSF_DECL(2) ABSF_DECL(3) ABSF_DECL(4) ABSF_DECL(5) ABSF_DECL(6) ABSF_DECL(7) ABSF_DECL(8)
 static const AbsKernel kAbsFlush[ABS_MAXNW + 1] = {nullptr, k_abs_flush_1, k_abs_flush_2, k_abs_flush_3, k_abs_flush_4,
@@ -430,6 +436,7 @@ void cnt_shape(GenProgram& G) {
 // Anything else stays on the general kernels.
 void chn_shape(GenProgram& G) {
     G.chnOk = 0;
+    G.chnWide = 0;
     const int n = G.nprocs;
     if (G.qtype != SG_Q_PATTERN || !G.partitioned || G.nstreams != 1 || n < 2 || n > CHN_MAXN || G.nslots != n ||
         G.nStartup != 0 || G.MC != 1 || G.nAll != n)
@@ -460,7 +467,9 @@ void chn_shape(GenProgram& G) {
         G.chnP[i] = p;
     }
     if (G.within != -1 && (G.nStartIds != 1 || G.startIds[0] != G.pre[G.chnP[0]].stateId)) return;
-    if (!reg_layout(G)) return;
+    // (every attribute word of the event in the kernel's registers: its filters read them there, and a captured event
+    // is written to its pool entry from them)
+    if (!reg_layout(G) || G.absNW > CHN_MAXNW) return;
     const int R_ = CHN_R(n);
     // (the window's lists, StateEvents 0 .. R and its events below min(64, SECAP) fit the block; 16-bit pool entries)
     if (G.L < (uint32_t)R_ || G.STCAP < (uint32_t)R_ + 1u || (uint32_t)(R_ * (n - 1)) > std::min<uint32_t>(64u, G.SECAP) ||
@@ -497,6 +506,9 @@ void chn_shape(GenProgram& G) {
     }
     G.chnKW = kw;
     G.chnN = n;
+    const int RW = CHN_RW(n);
+    G.chnWide = !getenv("SG_NO_CHN_WIDE") && G.L >= (uint32_t)RW && G.STCAP >= (uint32_t)RW + 1u &&
+                (uint32_t)(RW * (n - 1)) <= std::min<uint32_t>(64u, G.SECAP);
     G.chnEvery = G.post[G.chnP[0]].nextEveryStatePre == G.chnP[0] ? 1 : 0;
     G.chnOk = getenv("SG_NO_CHN") ? 0 : 1;  // (SG_NO_CHN: A/B timing against the general kernels; same results)
 }
@@ -1500,6 +1512,11 @@ GenEngine* gen_create(const uint32_t* ir, size_t nw, const sg_config& cfg, hipSt
                 GH_OK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
                 if (ncu > 0) e->ncu = (uint32_t)ncu;
             }
+            if (G.chnOk && G.chnWide) {   // (the wide chain kernel's hand-over list)
+                e->fb2_list = e->dalloc<uint32_t>(K);
+                e->fb2_start = e->dalloc<uint32_t>(K);
+                e->fb2_n = e->dalloc<unsigned long long>(1);
+            }
             if (G.absOk && !getenv("SG_NO_ABSD")) {
                 e->fb2_list = e->dalloc<uint32_t>(K);
                 e->fb2_start = e->dalloc<uint32_t>(K);
@@ -1575,7 +1592,7 @@ static size_t type_size(int t) {
 
 // the kernels take GenArgs (608 B) by value in their kernel arguments
 enum { GEN_L_BATCH = 0, GEN_L_TIMERS = 1, GEN_L_DEADLINES = 2, GEN_L_ABS_BATCH = 3, GEN_L_ABS_TIMERS = 4, GEN_L_CNT_BATCH = 5,
-       GEN_L_ABSD_BATCH = 6, GEN_L_ABSD_TIMERS = 7, GEN_L_CHN_BATCH = 8 };
+       GEN_L_ABSD_BATCH = 6, GEN_L_ABSD_TIMERS = 7, GEN_L_CHN_BATCH = 8, GEN_L_CHN_WIDE = 9 };
 // the general kernels over the keys a register-window kernel handed over: a fixed grid striding the list
 #define GEN_FB_BLOCKS 1024u
 // timer sweeps: a fixed grid of one-wave blocks striding over the due keys (their number is on the device)
@@ -1607,6 +1624,7 @@ static bool absd_on(const GenEngine* e) { return e->fb2_list && absd_lds(e) <= 6
 static bool cnt_on(const GenEngine* e) { return e->host.cntOk && e->host.projN == 0 && e->fb_list; }
 // the chain kernel of chn_kernels.hip runs this query (the shape, no device projection)
 static bool chn_on(const GenEngine* e) { return e->host.chnOk && e->host.projN == 0 && e->fb_list; }
+static bool chn_wide_on(const GenEngine* e) { return chn_on(e) && e->host.chnWide && e->fb2_list; }
 // the kernels that read the key-sorted payload with every attribute word of the event
 static bool pay_on(const GenEngine* e) { return abs_on(e) || cnt_on(e) || chn_on(e); }
 
@@ -1639,6 +1657,11 @@ static void launch_gen(GenEngine* e, GenArgs a, int which) {
         hipLaunchKernelGGL(kChnBatch[e->host.chnN - 2][e->host.chnKW], dim3(blocks), dim3(64), 0, e->stream, ap);
         hipLaunchKernelGGL(k_gen_stats_reduce, dim3(GST_N, std::min<uint32_t>((blocks + 1023) / 1024, 16u)), dim3(256),
                            0, e->stream, e->wstats, blocks, e->stats);
+    }
+    else if (which == GEN_L_CHN_WIDE) {   // a fixed grid striding the hand-over list (its length is on the device)
+        const uint32_t wb = std::min<uint32_t>(GEN_FB_BLOCKS, blocks);
+        hipLaunchKernelGGL(kChnWide[e->host.chnN - 2][e->host.chnKW], dim3(wb), dim3(64), 0, e->stream, ap);
+        hipLaunchKernelGGL(k_gen_stats_reduce, dim3(GST_N, 1), dim3(256), 0, e->stream, e->wstats, wb, e->stats);
     }
     else if (which == GEN_L_ABS_BATCH || which == GEN_L_ABS_TIMERS || which == GEN_L_CNT_BATCH) {
         // one lane per key / possible due slot (the due count is on the device); then the waves' counter rows
@@ -1713,7 +1736,7 @@ int gen_push(GenEngine* e, const sg_batch* b, std::string& msg) {
         cl.add(e->raw_count, 8 * GEN_RAWSEG);
         cl.add(e->t_multi, 4);
         if (pay_on(e)) cl.add(e->fb_n, 8);
-        if (abs_on(e) && absd_on(e)) cl.add(e->fb2_n, 8);
+        if ((abs_on(e) && absd_on(e)) || chn_wide_on(e)) cl.add(e->fb2_n, 8);
         GH_OK(cl.launch(e->stream));
     }
     if (G.partitioned) {
@@ -1869,6 +1892,15 @@ int gen_push(GenEngine* e, const sg_batch* b, std::string& msg) {
         a.fb_n = e->fb_n;
         a.fb_start = e->fb_start;
         launch_gen(e, a, GEN_L_CHN_BATCH);
+        if (chn_wide_on(e)) {   // the keys it handed over, in the wide window; what that cannot hold goes on
+            a.fb2_list = e->fb2_list;
+            a.fb2_n = e->fb2_n;
+            a.fb2_start = e->fb2_start;
+            launch_gen(e, a, GEN_L_CHN_WIDE);
+            a.fb_list = e->fb2_list;
+            a.fb_n = e->fb2_n;
+            a.fb_start = e->fb2_start;
+        }
         a.mode = GEN_M_KEYLIST;
     }
     launch_gen(e, a, GEN_L_BATCH);
@@ -2314,7 +2346,11 @@ std::string gen_describe(const GenEngine* e) {
         push = "k_cnt_batch_" + nw + " (register window, lane per key) + k_gen_batch (keys handed over)";
     } else if (chn_on(e)) {
         push = "k_chn_batch_" + std::to_string(G.chnN - 1) + "_" + std::to_string(G.chnKW) +
-               " (chained states, register window, lane per key) + k_gen_batch (keys handed over)";
+               " (chained states, register window, lane per key) + " +
+               (chn_wide_on(e) ? "k_chn_wide_" + std::to_string(G.chnN - 1) + "_" + std::to_string(G.chnKW) +
+                                     " (the keys handed over, wide window) + "
+                               : std::string()) +
+               "k_gen_batch (keys handed over)";
     } else {
         push = "k_gen_batch (general interpreter, lane per key)";
         if (G.nStartup > 0) adv = "k_gen_timers (general interpreter)";

@@ -86,6 +86,7 @@ enum {
 #define SGD_NO_RESUME 0xffffffffu
 #define SGD_HOT_DONE 0xfffffffeu   // resume word: the hot-key pipeline advanced the key (the HBM pass skips it)
 #define SGD_HOT_MARK 0xfffffffdu   // resume word: a hot key of a wave the staged pass left whole (counted there)
+#define SGD_HOT_IDLE 8             // drained batches in a row without hot keys before the pipeline's buffers go back
 #define SGD_HOT_CTL 8
 #define SGD_HOT_CTL_BIG 6          // hot_ctl word: workgroups whose range exceeded SGD_BIG_TILE events
 #define SGD_BIG_TILE 65536u

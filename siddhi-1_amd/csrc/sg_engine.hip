@@ -196,6 +196,9 @@ struct sg_engine {
     // the status block), otherwise the HBM pass walks them
     bool hot_ok = false;
     bool hot_on = true;
+    uint32_t hot_idle = 0;         // drained batches in a row without hot keys (the pipeline's buffers are given
+                                   // back after SGD_HOT_IDLE of them)
+    std::vector<void*> hot_owned;  // the pipeline's per-event / per-partial buffers (hot_buffers)
     bool skewed = false;           // recent batches had workgroup ranges > SGD_BIG_TILE events: sorted grouping
     uint32_t hot_min = 0, hot_cap = 0, hot_exmax = 0;
     uint32_t hot_n0 = 0;           // carried-in live partials that make a key hot (0: the HBM pass's window + 1:
@@ -313,6 +316,7 @@ struct sg_engine {
         for (auto& sp : spans) { (void)hipEventDestroy(sp.a); (void)hipEventDestroy(sp.b); }
         for (auto x : free_events) (void)hipEventDestroy(x);
         for (void* p : owned) (void)hipFree(p);
+        for (void* p : hot_owned) (void)hipFree(p);
         for (auto& kv : variants)
             if (kv.second.mod) (void)hipModuleUnload(kv.second.mod);
         if (stream) (void)hipStreamDestroy(stream);
@@ -584,14 +588,16 @@ void allocate(sg_engine* e) {
         // hot keys: up to every key (those with more live partials than the window are hot too); their carried-in
         // partials get up to hot_exmax flat indices (further keys are given back to the HBM pass; SG_HOT_EXMAX bounds
         // it, tests force the give-back that way).  Only the key list is allocated here: the pipeline's per-event and
-        // per-partial buffers (hot_buffers) come with the first batch that runs it, so an engine whose stream never
-        // has a hot key (uniform C2: ~2.3 GB at 2^24-event batches) never holds them.
+        // per-partial buffers (hot_buffers, ~2.3 GB at 2^24-event batches) come with the first batch that runs it and
+        // are given back once SGD_HOT_IDLE batches in a row had no hot key: an engine whose stream has none (uniform
+        // C2) holds them only over its first batches.  The first batch runs the pipeline: the host cannot know in
+        // advance whether a device batch has hot keys, and a hot key left to the HBM pass is walked by one lane,
+        // quadratic in its run (a Zipf stream's first batch: 1.85 s).
         e->hot_cap = (uint32_t)std::min<size_t>(K, 1u << 20);
         e->hot_exmax = (uint32_t)std::min<size_t>((size_t)K * C, std::max<size_t>(1u << 22, 2 * B));
         if (const char* x = getenv("SG_HOT_EXMAX")) e->hot_exmax = std::max(1u, (uint32_t)strtoul(x, nullptr, 0));
         e->hot_list = dalloc<uint32_t>(e->hot_cap, o);
         e->hot_info = dalloc<uint32_t>((size_t)e->hot_cap * SGD_HOT_INFO, o);
-        e->hot_on = false;  // (set by the first batch that lists hot keys: drain_one)
     }
     e->tile_sum = dalloc<uint32_t>(B / SGD_ORDER_TILE + 1, o);
     // the match count and the error word share 16 bytes, so poll reads both with one D2H copy
@@ -735,7 +741,7 @@ static uint32_t sgd_max_key(const uint32_t* k, uint32_t n, bool skip_null) {
 // B + hot_exmax flat slots (events of the hot runs, then the carried-in partials) x 10 words, 3 x B words
 static void hot_buffers(sg_engine* e) {
     if (e->hot_death) return;
-    auto& o = e->owned;
+    auto& o = e->hot_owned;
     const size_t B = e->maxb, slots = B + (size_t)e->hot_exmax;
     e->hot_death = dalloc<uint32_t>(slots, o);
     e->hot_wl = dalloc<uint32_t>(2 * 3 * slots, o);
@@ -745,6 +751,16 @@ static void hot_buffers(sg_engine* e) {
     e->hot_fh = dalloc<uint32_t>(slots, o);
     e->hot_cur = dalloc<uint32_t>(slots, o);
     e->hot_fbi = dalloc<uint32_t>(B, o);
+}
+
+// ... and given back (no batch in flight runs the pipeline: it ran only while the batches drained before it had hot
+// keys, and the last SGD_HOT_IDLE drained ones had none; the stream is drained anyway, this happens once per idle run)
+static void hot_release(sg_engine* e) {
+    if (!e->hot_death) return;
+    HIP_OK(hipStreamSynchronize(e->stream));
+    for (void* p : e->hot_owned) (void)hipFree(p);
+    e->hot_owned.clear();
+    e->hot_death = e->hot_wl = e->hot_tcnt = e->hot_tbase = e->hot_alive = e->hot_fh = e->hot_cur = e->hot_fbi = nullptr;
 }
 
 // a batch is complete once its ordering ran: record its status block into the pinned ring
@@ -757,7 +773,10 @@ static void drain_one(sg_engine* e) {  // wait for the oldest in-flight batch
     // batches have hot keys, the sorted grouping replaces the fused one while they have giant tiles (split by one
     // workgroup each in the fused grouping)
     const uint32_t w1 = (uint32_t)(e->h_status[2 * ri + 1] >> 32);
-    if (e->hot_ok) e->hot_on = (w1 & 0xffffu) != 0;
+    if (e->hot_ok) {
+        e->hot_on = (w1 & 0xffffu) != 0;
+        e->hot_idle = e->hot_on ? 0 : e->hot_idle + 1;
+    }
     e->skewed = (w1 >> 16) != 0;
     e->inflight.erase(e->inflight.begin());
 }
@@ -973,6 +992,7 @@ int push(sg_engine* e, const sg_batch* b) {
     p.raw_capnull = e->raw_capnull;
     p.hot_ctl = e->hot_ctl;
     if (e->hot_ok && e->hot_on) hot_buffers(e);
+    else if (e->hot_ok && e->hot_idle >= SGD_HOT_IDLE) hot_release(e);
     if (e->hot_ok) {
         // a partitioned batch's keys hold n / K events on average: "hot" is far above that (and above hot_min)
         p.hot_min = pl.partitioned ? std::max<uint32_t>(e->hot_min, (uint32_t)std::min<uint64_t>(e->hot_factor * n / e->K, 1u << 30))

@@ -6,8 +6,8 @@ oracle and against the general kernel it shortcuts (SG_NO_CHN=1), bit-exact:
 * match records (trigger seq, key, ts, every slot's event), every work counter (scanned, created — the clones
   `every` stages —, keys touched, live partials) and the exported state documents (the kernel writes the general
   engine's blocks in a canonical layout: the document must not notice), over several pushes with state carried;
-* 3- and 4-state chains, with and without `every` and `within`, filters reading e1 and e2 (two kept words), long /
-  double attributes, nulls, random streams with several keys;
+* 3- and 4-state chains, with and without `every` and `within`, filters reading e1 and e2 (two kept words), double
+  attributes, nulls, random streams with several keys; a five-word event stays on the general kernel;
 * the hand-overs to the general kernel: more live partials than the window holds (from the event where the key
   stops), timestamps out of order, an imported oracle document (pool entries in the oracle's order), one-event
   pushes (the canonical layout after every event).
@@ -29,7 +29,8 @@ sd = importlib.import_module("siddhi-1_amd.state_doc")
 pytestmark = pytest.mark.gpu
 
 STOCK = "define stream S (symbol string, price float, volume int);\n"
-WIDE = "define stream S (symbol string, price double, volume long);\n"
+WIDE = "define stream S (symbol string, price double, volume int);\n"     # (4 attribute words: the kernel's limit)
+WIDER = "define stream S (symbol string, price double, volume long);\n"   # (5: the general kernel)
 
 
 def chain(filters, every=True, within="within 200 milliseconds", schema=STOCK):
@@ -76,7 +77,7 @@ def _oracle(q, n_keys):
 def _stream(n, n_keys, seed, nulls=False, wide=False, rate=3):
     d = synth.stock_ticks(0, n, n_keys, seed=seed, rate_per_ms=rate)
     price = d["price"].astype(np.float64) if wide else d["price"]
-    vol = d["volume"].astype(np.int64) if wide else d["volume"]
+    vol = d["volume"]
     nul = None
     if nulls:
         nul = [None, ((d["volume"] % 13) == 5).astype(np.uint8), ((d["volume"] % 11) == 3).astype(np.uint8)]
@@ -128,6 +129,20 @@ def test_chain_window_equals_oracle_and_general(shape, monkeypatch):
     _docs_equal(fast, gen)
 
 
+def test_five_attribute_words_stay_on_the_general_kernel(monkeypatch):
+    """an event of more attribute words than the chain kernel holds in registers (double + long: 5) is not this
+    kernel's shape: the general kernel runs it, equal to the oracle"""
+    q = chain(["price>20", "price>e1.price", "volume>e2.volume"], schema=WIDER)
+    n_keys = 32
+    d = synth.stock_ticks(0, 5000, n_keys, seed=13, rate_per_ms=3)
+    cols = [d["symbol"], d["price"].astype(np.float64), d["volume"].astype(np.int64)]
+    e = _engine(q, n_keys, 4096, False, monkeypatch)
+    assert "k_chn_batch" not in e.describe(), e.describe()
+    ora = _oracle(q, n_keys)
+    assert _drive([e, ora], d, cols, None, _chunks(len(d["ts"]), 800)) > 0
+    _docs_equal(e, ora)
+
+
 def test_chain_window_nulls(monkeypatch):
     q = SHAPES["p3_two_words"]
     n_keys = 40
@@ -142,13 +157,19 @@ def test_chain_window_nulls(monkeypatch):
     _docs_equal(fast, ora)
 
 
-def test_chain_window_overflow_hands_over(monkeypatch):
-    """a filter that rarely passes: state-1 partials pile up past the window (12 for three states), the key is stored and the
-    general kernel continues from the event where it stopped; later batches load it back"""
+@pytest.mark.parametrize("wide", [True, False])
+def test_chain_window_overflow_hands_over(wide, monkeypatch):
+    """a filter that rarely passes: state-1 partials pile up past the window (20 for three states), the key is stored
+    and the wide-window kernel (32) continues from the event where it stopped, then the general kernel from where
+    that one stopped (wide = False: the general kernel directly); later batches load it back"""
     q = chain(["price>10", "price>39.5", "price>e2.price"], within="within 300 milliseconds")
     n_keys = 16
     d, cols, nul = _stream(8000, n_keys, seed=19, rate=2)
+    if not wide:
+        monkeypatch.setenv("SG_NO_CHN_WIDE", "1")
     fast = _engine(q, n_keys, 4096, False, monkeypatch, cap=64)
+    monkeypatch.delenv("SG_NO_CHN_WIDE", raising=False)
+    assert ("k_chn_wide" in fast.describe()) == wide, fast.describe()
     gen = _engine(q, n_keys, 4096, True, monkeypatch, cap=64)
     ora = _oracle(q, n_keys)
     total = _drive([fast, gen, ora], d, cols, nul, _chunks(len(d["ts"]), 1000))
@@ -210,14 +231,16 @@ def test_chain_window_after_foreign_import_and_exports(shape, monkeypatch):
 
 
 def test_p3_at_bench_keys(monkeypatch):
-    """the bench's P3 leg at its size (2^20 keys, 2^22-event pushes): chain kernel == general kernel, every match
-    and counter, three pushes with state carried"""
+    """the bench's P3 leg at its size (2^20 keys, 2^22-event pushes, partial capacity 32): chain kernel == general
+    kernel, every match and counter, seven pushes with state carried — past the 10-second window's fill, where keys
+    outgrow the 20-slot window and go to the wide window (and beyond it to the general kernel)"""
     q = synth.P3_QUERY
     K, B = 1 << 20, 1 << 22
     fast = _engine(q, K, B, False, monkeypatch, mcap=B)
+    assert "k_chn_wide" in fast.describe(), fast.describe()
     gen = _engine(q, K, B, True, monkeypatch, mcap=B)
     total = 0
-    for s in range(3):
+    for s in range(7):
         d = synth.stock_ticks(s * B, B, K)
         for e in (fast, gen):
             e.push(0, s * B, d["ts"], [d["symbol"], d["price"], d["volume"]], None, d["key"])
@@ -226,5 +249,6 @@ def test_p3_at_bench_keys(monkeypatch):
         total += len(mf)
     assert total > 0
     sf, sg = fast.stats(), gen.stats()
+    assert sf["window_spills"] > 0
     for k in ALL:
         assert sf[k] == sg[k], (k, sf[k], sg[k])

@@ -320,3 +320,52 @@ def test_hot_partials_given_back_above_exmax(exmax, monkeypatch):
     assert "k_hot_prep" in gpu.describe()
     for e in (gpu, ora, lane):
         e.close()
+
+
+def test_hot_pipeline_from_the_first_batch_and_buffers_given_back(monkeypatch):
+    """the first batch an engine sees runs the hot-key pipeline (a Zipf head key left to one HBM-pass lane is
+    quadratic in its run), and after SGD_HOT_IDLE (8) batches in a row without a hot key the pipeline's buffers
+    are freed (device memory back to its level before they were allocated); a later hot batch allocates them again,
+    bit-exact with the oracle throughout"""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+
+    def free_bytes():
+        f, t = ctypes.c_size_t(), ctypes.c_size_t()
+        assert hip.hipMemGetInfo(ctypes.byref(f), ctypes.byref(t)) == 0
+        return f.value
+
+    monkeypatch.setenv("SG_HOT_MIN", "64")
+    n_keys, n = 1 << 14, 1 << 18
+    cq, gpu, ora, lane = _pair(SHAPES["c2_every_within"], n_keys, n)
+    seq = 0
+
+    def push(d):
+        nonlocal seq
+        for e in (gpu, ora, lane):
+            e.push(0, seq, d["ts"], [d[c] for c in COLS], None, d["key"])
+        mg = gpu.poll()
+        _same(mg, ora.poll())
+        _same(mg, lane.poll())
+        seq += len(d["ts"])
+
+    gpu.synchronize()
+    free0 = free_bytes()
+    push(_zipf(seq, n, n_keys, 70, 64))
+    assert gpu.stats()["hot_keys"] > 0, "the first batch did not run the pipeline"
+    free_hot = free_bytes()
+    assert free0 - free_hot > 20 << 20, (free0, free_hot)   # B + hot_exmax slots x 40 B + 3 x B words
+    for b in range(10):
+        push(synth.stock_ticks(seq, 1 << 14, n_keys, seed=80 + b, rate_per_ms=64))
+    gpu.synchronize()
+    free_idle = free_bytes()
+    assert free_idle - free_hot > 20 << 20, (free_hot, free_idle)
+    h0 = gpu.stats()["hot_keys"]
+    push(_zipf(seq, n, n_keys, 71, 64))
+    push(_zipf(seq, n, n_keys, 72, 64))
+    assert gpu.stats()["hot_keys"] > h0
+    sg, so = gpu.stats(), ora.stats()
+    for f in ("partials_live", "matches"):
+        assert sg[f] == so[f], (f, sg[f], so[f])
+    for e in (gpu, ora, lane):
+        e.close()

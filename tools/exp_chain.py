@@ -39,6 +39,11 @@ def main():
                             t["key"].data_ptr()), [0, 1, 2], mem=sa.native.SG_MEM_DEVICE)
         m = eng.poll_device()
         eng.release(m)
+        if os.environ.get("CHN_PER_STEP"):   # (per push: wall time and the counters, the engine synchronised)
+            eng.synchronize()
+            st = eng.stats()
+            print(f"step {s}: {time.perf_counter() - (t0 or time.perf_counter()):.4f} s, live {st['partials_live']}, "
+                  f"spills {st['window_spills']}, matches {st['matches']}", flush=True)
     eng.synchronize()
     el = time.perf_counter() - t0
     st = eng.stats()

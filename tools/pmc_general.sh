@@ -1,6 +1,6 @@
 #!/bin/bash
 # PMC counters + kernel traces of the NFA kernels the general-engine configs actually run (register-window
-# k_cnt_* / k_abs_* / k_absd_*, the interpreter k_gen_batch / k_gen_timers), one counter group per rocprofv3
+# k_cnt_* / k_abs_* / k_absd_* / k_chn_*, the interpreter k_gen_batch / k_gen_timers), one counter group per rocprofv3
 # pass (MI355X_MICROARCH.md: FETCH_SIZE and WRITE_SIZE in passes of their own, <= 8 SQ counters per pass).
 #   PMC_CFGS="C3 C3_min1 C4 C4_deep C4_deep_state" PMC_OUT=gpurun_out/pmc_gen tools/pmc_general.sh
 # Summary: python tools/pmc_general_summary.py gpurun_out/pmc_gen
@@ -9,7 +9,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 export SG_EXP_STEPS=${SG_EXP_STEPS:-3}
 OUT=${PMC_OUT:-gpurun_out/pmc_gen}
-RX='k_cnt_|k_abs|k_gen_batch|k_gen_timers'
+RX='k_cnt_|k_abs|k_chn_|k_gen_batch|k_gen_timers'
 mkdir -p $OUT
 for cfg in ${PMC_CFGS:-C3 C3_min1 C3_and P3 C4 C4_deep C4_deep_state}; do
   timeout -s KILL 200 rocprofv3 --kernel-trace --stats -d $OUT/${cfg}_trace -o run --output-format csv \

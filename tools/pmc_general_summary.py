@@ -15,16 +15,21 @@ from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # the sources the general configs' NFA kernels are built from (bench.py checks the same hash)
-SOURCES = ["abs_kernels.hip", "absd_kernels.hip", "cnt_kernels.hip", "gen_kernels.hip", "gen_host.hip",
-           "reg_common.h", "gen_engine.h", "java_ops.h", "pack.h"]
+SOURCES = ["abs_kernels.hip", "absd_kernels.hip", "cnt_kernels.hip", "chn_kernels.hip", "gen_kernels.hip",
+           "gen_host.hip", "reg_common.h", "gen_engine.h", "java_ops.h", "pack.h"]
 # the configs' pushed batch size (bench.py other_configs)
 EVENTS = {"C3": 1 << 22, "C3_min1": 1 << 22, "C3_and": 1 << 22, "P3": 1 << 22, "C4": 1 << 22, "C4_deep": 1 << 22, "C4_deep_state": 1 << 16}
-BATCH_KERNELS = ("k_cnt_batch", "k_abs_batch", "k_gen_batch")
+BATCH_KERNELS = ("k_cnt_batch", "k_abs_batch", "k_chn_batch", "k_gen_batch")
+# --variants: the C2 workload variants (tools/pmc_variants.sh): the two-state engine's advance kernels, all in the
+# query-specialised p2_jit.hip (staged pass, HBM passes, hot-key pipeline)
+VAR_SOURCES = ["p2_jit.hip"]
+VAR_EVENTS = {"C2_zipf": 1 << 24, "C2_walk": 1 << 24}
+VAR_BATCH_KERNELS = ("k_adv_m",)
 
 
-def sources_hash():
+def sources_hash(sources):
     h = hashlib.sha1()
-    for f in SOURCES:
+    for f in sources:
         h.update(open(os.path.join(ROOT, "siddhi-1_amd", "csrc", f), "rb").read())
     return h.hexdigest()
 
@@ -34,7 +39,12 @@ def main():
     ap.add_argument("dir")
     ap.add_argument("--json")
     ap.add_argument("--profiles", default=None)
+    ap.add_argument("--variants", action="store_true")
     args = ap.parse_args()
+    global EVENTS, BATCH_KERNELS
+    sources = SOURCES
+    if args.variants:
+        EVENTS, BATCH_KERNELS, sources = VAR_EVENTS, VAR_BATCH_KERNELS, VAR_SOURCES
     lines, out = [], {}
     for cfg in EVENTS:
         files = sorted(glob.glob(os.path.join(args.dir, f"{cfg}_g*", "run_counter_collection.csv")))
@@ -78,11 +88,12 @@ def main():
     print(text)
     open(os.path.join(args.dir, "summary.txt"), "w").write(text + "\n")
     if args.json:
-        json.dump({"configs": out, "kernel_src_sha1": sources_hash(), "sources": SOURCES,
+        json.dump({"configs": out, "kernel_src_sha1": sources_hash(sources), "sources": sources,
                    "profiles": args.profiles or args.dir,
-                   "method": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950) and WRITE_SIZE in separate passes over "
-                             "tools/exp_gen.py <cfg>, tools/pmc_general.sh; bytes of every NFA-kernel dispatch / "
-                             "pushed batches"}, open(args.json, "w"), indent=1)
+                   "method": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950) and WRITE_SIZE in separate passes over " +
+                             ("tools/exp_variants.py, tools/pmc_variants.sh" if args.variants else
+                              "tools/exp_gen.py <cfg>, tools/pmc_general.sh") + "; bytes of every NFA-kernel dispatch "
+                             "/ pushed batches"}, open(args.json, "w"), indent=1)
 
 
 if __name__ == "__main__":
