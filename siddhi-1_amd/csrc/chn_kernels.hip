@@ -53,7 +53,8 @@
 
 namespace {
 
-// CHN_ABL (experiment builds only, wrong results): 1 = no store, 2 = no event walked, 3 = every key loaded as fresh
+// CHN_ABL (experiment builds only, wrong results): 1 = no store, 2 = no event walked, 3 = every key loaded as fresh,
+// 4 = captured events' pool entries not written
 #ifndef CHN_ABL
 #define CHN_ABL 0
 #endif
@@ -502,7 +503,7 @@ template <int NE, int KW, int RR> struct ChnKey {
     }
     __device__ __forceinline__ void captured(int j, int i, const AbsEv<CHN_NW>& ev, bool fresh) const {
         const uint32_t e = canon(j, i), sb = G.offST + (uint32_t)j * G.stWords;
-        putEvent(e, ev);
+        if (CHN_ABL != 4) putEvent(e, ev);
         if (fresh) {
             for (int q = 0; q < G.nslots; q++) W(sb + ST_SLOTS + (uint32_t)q) = GEN_NIL;
             W(sb + ST_TYPE) = 0u;
