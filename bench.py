@@ -1303,7 +1303,7 @@ def main():
                        "e3=S[volume>1000] within 10 sec (SEQUENCE), 1,048,576 keys (register-window count kernel)"),
             "P3": (synth.P3_QUERY, lambda s: synth.stock_ticks(s * cb, cb, K), K, cb, 1, 32, False, 0,
                    "3-state pattern: every e1=S[price>20] -> e2=S[price>e1.price] -> e3=S[price>e2.price] within "
-                   "10 sec, 1,048,576 keys (general kernel)"),
+                   "10 sec, 1,048,576 keys (chain kernel: register window per key, the wide window for the keys that outgrow it)"),
             "C4": (synth.C4_QUERY, lambda s: synth.burst_ticks(s * cb, cb, K, 1), K, cb, 1, 16, True, 0,
                    "C4: every e1=S[price>20] -> not S[price>e1.price] for 30 sec within 60 sec, @app:playback, "
                    "1,048,576 keys, one event per ms (distinct timer due times), 4,194,304-event batches, the "
