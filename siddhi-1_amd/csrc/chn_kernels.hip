@@ -58,6 +58,9 @@ namespace {
 #ifndef CHN_ABL
 #define CHN_ABL 0
 #endif
+#ifndef CHN_DEFER
+#define CHN_DEFER 1   // captured events written at the store, slot by slot (0: as they are captured)
+#endif
 constexpr int CHN_NW = CHN_MAXNW;   // attribute words of an event (pack.h Pay<W>, W <= 4; chn_shape checks absNW)
 constexpr uint32_t CHN_ORD_MASK = 0xffffffu;   // order stamp: low 24 bits of ord[]; the kept words' null bits above
 
@@ -80,6 +83,7 @@ template <int NE, int KW, int RR> struct ChnKey {
     // captured in this batch)
     uint32_t* cold;
     uint32_t lane;
+    uint32_t runB, cur;             // the key's run start and the payload index of the event being walked
     uint32_t stamp;                 // the next order stamp
     bool seedP, seedN;              // p0's seed in pending / newAndEvery
     int64_t seedTs;
@@ -96,8 +100,9 @@ template <int NE, int KW, int RR> struct ChnKey {
     uint32_t scanned, created, matches;   // (this key's run: < 2^32)
 
     __device__ __forceinline__ ChnKey(const GenArgs& a, uint32_t key)
-        : G(*(cGenProgram*)a.G), A(a), S(gp(a.state)), K(a.K), k(key), live(0), stg(0), pl0(0), pl1(0), stamp(0),
-          seedP(false), seedN(false), seedTs(-1), dirty(0), whole(0), stHigh(false), outside(false), canonOK(false), err(0), scanned(0), created(0),
+        : G(*(cGenProgram*)a.G), A(a), S(gp(a.state)), K(a.K), k(key), live(0), stg(0), pl0(0), pl1(0), runB(0), cur(0), stamp(0),
+          seedP(false), seedN(false), seedTs(-1), dirty(0), whole(0), stHigh(false), outside(false),
+          canonOK(false), err(0), scanned(0), created(0),
           matches(0) {
         tbase = a.b.pay ? gp(a.b.ts)[0] : 0;
         sbase = a.b.seq_base;
@@ -501,6 +506,15 @@ template <int NE, int KW, int RR> struct ChnKey {
             if ((uint32_t)q < G.absNW) W(sew(to, G.absWordAt[q])) = ev.w[q];
         W(sew(to, SE_NULL)) = ev.nb;
     }
+    // canonOK: a captured event's 16-bit entry in the LDS column — deferred (0x8000 | its index in the key's run:
+    // written at the store, slot by slot, if its partial is still alive, from the key-sorted payload), or, without a
+    // payload or past 0x7fff events into the run, its canonical pool entry written now
+    __device__ __forceinline__ uint32_t capture(int j, int i, const AbsEv<CHN_NW>& ev, bool fresh) const {
+        const uint32_t d = cur - runB;
+        if (CHN_DEFER && A.b.pay && d < 0x7fffu) return 0x8000u | d;
+        captured(j, i, ev, fresh);
+        return canon(j, i);
+    }
     __device__ __forceinline__ void captured(int j, int i, const AbsEv<CHN_NW>& ev, bool fresh) const {
         const uint32_t e = canon(j, i), sb = G.offST + (uint32_t)j * G.stWords;
         if (CHN_ABL != 4) putEvent(e, ev);
@@ -600,10 +614,9 @@ template <int NE, int KW, int RR> struct ChnKey {
                 }
                 stamp++;
                 sqw(j, s) = (uint32_t)qn;   // the event's seq (LDS)
-                if (canonOK) {              // its pool entry, written now
+                if (canonOK) {              // its canonical pool entry, written now or at the store
                     const uint32_t sh = (uint32_t)(s & 1) * 16u;
-                    ixw(j, s >> 1) = (ixw(j, s >> 1) & ~(0xffffu << sh)) | (canon(j, s) << sh);
-                    captured(j, s, ev, false);
+                    ixw(j, s >> 1) = (ixw(j, s >> 1) & ~(0xffffu << sh)) | (capture(j, s, ev, false) << sh);
                 } else {                    // no pool entry yet: the store places it
                     ixw(j, s >> 1) |= 0xffffu << ((s & 1) * 16);
                 }
@@ -649,8 +662,8 @@ template <int NE, int KW, int RR> struct ChnKey {
                 }
                 sqw(j, 0) = (uint32_t)qn;
 #pragma unroll
-                for (int h = 0; h < XW; ++h) ixw(j, h) = (h == 0 && canonOK) ? (canon(j, 0) | 0xffff0000u) : 0xffffffffu;
-                if (canonOK) captured(j, 0, ev, true);
+                for (int h = 0; h < XW; ++h) ixw(j, h) = 0xffffffffu;
+                if (canonOK) ixw(j, 0) = capture(j, 0, ev, true) | 0xffff0000u;
                 stamp++;
                 live |= 1u << j;
                 stg |= 1u << j;
@@ -712,8 +725,34 @@ template <int NE, int KW, int RR> struct ChnKey {
             const int j = __ffs(m) - 1;
             const int s = (int)(((pl0 >> j) & 1u) | (((pl1 >> j) & 1u) << 1)) + 1;
             for (int i = 0; i < s; ++i) {
-                const uint32_t e = getIx(j, i);
+                const uint32_t e = canonOK ? canon(j, i) : getIx(j, i);
                 if (e < PA) occ |= 1ull << e;
+            }
+        }
+        if (canonOK) {   // the deferred events of the partials alive now, slot by slot (every lane at slot j writes
+                         // the same rows of its key: adjacent words), and their StateEvents
+            for (int j = 0; j < R; ++j) {
+                if (!((dirty >> j) & 1u) || !((live >> j) & 1u)) continue;
+                const int s = (int)(((pl0 >> j) & 1u) | (((pl1 >> j) & 1u) << 1)) + 1;
+                const uint32_t sb = G.offST + (uint32_t)j * G.stWords;
+                const bool all = (whole >> j) & 1u;
+                if (all) {
+                    for (int q = 0; q < G.nslots; q++) W(sb + ST_SLOTS + (uint32_t)q) = GEN_NIL;
+                    W(sb + ST_TYPE) = 0u;
+                    W(sb + ST_RC) = 1u;
+                }
+                for (int i = 0; i < s; ++i) {
+                    const uint32_t h = getIx(j, i);
+                    if (!(h & 0x8000u)) {   // (written when captured, or carried in)
+                        if (all) W(sb + ST_SLOTS + sid(i)) = canon(j, i);
+                        continue;
+                    }
+                    AbsEv<CHN_NW> ev;
+                    abs_pay<CHN_NW>(A, runB + (h & 0x7fffu), tbase, ev);
+                    putEvent(canon(j, i), ev);
+                    W(sb + ST_SLOTS + sid(i)) = canon(j, i);
+                    if (i == s - 1) W64(sb + ST_TS, ev.ts);
+                }
             }
         }
         // the lists, row by row: each list's members in stamp order (lanes at the same position write adjacent words)
@@ -832,6 +871,7 @@ template <int NE, int KW, int RR> struct ChnRun {
     __device__ __forceinline__ void run(const GenArgs& a, uint32_t key, uint32_t b, uint32_t e, uint32_t* cold) {
         ChnKey<NE, KW, RR> L(a, key);
         L.cold = cold;
+        L.runB = b;
         bool walk = b < e;
         fb = false;
         stop = b;
@@ -857,6 +897,7 @@ template <int NE, int KW, int RR> struct ChnRun {
                     chn_gather(a, G, pos, ev);
                 }
                 if (CHN_ABL == 2) continue;
+                L.cur = i;
                 if (!L.event(ev, pos)) break;
             }
             if (CHN_ABL != 1) L.store();   // (a hand-over: the next kernel continues from the block)
