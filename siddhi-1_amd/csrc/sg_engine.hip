@@ -316,7 +316,10 @@ struct sg_engine {
         for (auto& sp : spans) { (void)hipEventDestroy(sp.a); (void)hipEventDestroy(sp.b); }
         for (auto x : free_events) (void)hipEventDestroy(x);
         for (void* p : owned) (void)hipFree(p);
-        for (void* p : hot_owned) (void)hipFree(p);
+        if (!hot_owned.empty()) {   // (stream-ordered allocations: freed on the stream, then drained)
+            for (void* p : hot_owned) (void)hipFreeAsync(p, stream);
+            (void)hipStreamSynchronize(stream);
+        }
         for (auto& kv : variants)
             if (kv.second.mod) (void)hipModuleUnload(kv.second.mod);
         if (stream) (void)hipStreamDestroy(stream);
@@ -737,28 +740,34 @@ static uint32_t sgd_max_key(const uint32_t* k, uint32_t n, bool skip_null) {
     return m;
 }
 
-// the hot-key pipeline's buffers, allocated the first time a batch runs it (kept for the engine's life):
-// B + hot_exmax flat slots (events of the hot runs, then the carried-in partials) x 10 words, 3 x B words
+// the hot-key pipeline's buffers, allocated the first time a batch runs it: B + hot_exmax flat slots (events of the
+// hot runs, then the carried-in partials) x 10 words, 3 x B words.  Stream-ordered (hipMallocAsync on the engine's
+// main stream, the one every k_hot_* kernel runs on), so neither taking nor giving them back waits on the host: a
+// hipFree in the middle of a pipelined run drained both batches in flight (a one-time stall of a few ms)
+template <class T> static T* hot_alloc(sg_engine* e, size_t n) {
+    void* p = nullptr;
+    HIP_OK(hipMallocAsync(&p, n * sizeof(T), e->stream));
+    e->hot_owned.push_back(p);
+    return (T*)p;
+}
 static void hot_buffers(sg_engine* e) {
     if (e->hot_death) return;
-    auto& o = e->hot_owned;
     const size_t B = e->maxb, slots = B + (size_t)e->hot_exmax;
-    e->hot_death = dalloc<uint32_t>(slots, o);
-    e->hot_wl = dalloc<uint32_t>(2 * 3 * slots, o);
-    e->hot_tcnt = dalloc<uint32_t>(B, o);
-    e->hot_tbase = dalloc<uint32_t>(B, o);
-    e->hot_alive = dalloc<uint32_t>(slots, o);
-    e->hot_fh = dalloc<uint32_t>(slots, o);
-    e->hot_cur = dalloc<uint32_t>(slots, o);
-    e->hot_fbi = dalloc<uint32_t>(B, o);
+    e->hot_death = hot_alloc<uint32_t>(e, slots);
+    e->hot_wl = hot_alloc<uint32_t>(e, 2 * 3 * slots);
+    e->hot_tcnt = hot_alloc<uint32_t>(e, B);
+    e->hot_tbase = hot_alloc<uint32_t>(e, B);
+    e->hot_alive = hot_alloc<uint32_t>(e, slots);
+    e->hot_fh = hot_alloc<uint32_t>(e, slots);
+    e->hot_cur = hot_alloc<uint32_t>(e, slots);
+    e->hot_fbi = hot_alloc<uint32_t>(e, B);
 }
 
-// ... and given back (no batch in flight runs the pipeline: it ran only while the batches drained before it had hot
-// keys, and the last SGD_HOT_IDLE drained ones had none; the stream is drained anyway, this happens once per idle run)
+// ... and given back, on the same stream behind the last kernel that could read them (no batch in flight runs the
+// pipeline: it ran only while the batches drained before it had hot keys, and the last SGD_HOT_IDLE had none)
 static void hot_release(sg_engine* e) {
     if (!e->hot_death) return;
-    HIP_OK(hipStreamSynchronize(e->stream));
-    for (void* p : e->hot_owned) (void)hipFree(p);
+    for (void* p : e->hot_owned) HIP_OK(hipFreeAsync(p, e->stream));
     e->hot_owned.clear();
     e->hot_death = e->hot_wl = e->hot_tcnt = e->hot_tbase = e->hot_alive = e->hot_fh = e->hot_cur = e->hot_fbi = nullptr;
 }

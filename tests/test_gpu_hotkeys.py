@@ -325,15 +325,16 @@ def test_hot_partials_given_back_above_exmax(exmax, monkeypatch):
 def test_hot_pipeline_from_the_first_batch_and_buffers_given_back(monkeypatch):
     """the first batch an engine sees runs the hot-key pipeline (a Zipf head key left to one HBM-pass lane is
     quadratic in its run), and after SGD_HOT_IDLE (8) batches in a row without a hot key the pipeline's buffers
-    are freed (device memory back to its level before they were allocated); a later hot batch allocates them again,
+    are freed (stream-ordered: the device pool's used bytes fall back); a later hot batch allocates them again,
     bit-exact with the oracle throughout"""
     import ctypes
     hip = ctypes.CDLL("libamdhip64.so")
 
-    def free_bytes():
-        f, t = ctypes.c_size_t(), ctypes.c_size_t()
-        assert hip.hipMemGetInfo(ctypes.byref(f), ctypes.byref(t)) == 0
-        return f.value
+    def pool_used():   # the pipeline's buffers are stream-ordered allocations from the device's default pool
+        pool, v = ctypes.c_void_p(), ctypes.c_uint64()
+        assert hip.hipDeviceGetDefaultMemPool(ctypes.byref(pool), 0) == 0
+        assert hip.hipMemPoolGetAttribute(pool, 0x7, ctypes.byref(v)) == 0   # hipMemPoolAttrUsedMemCurrent
+        return v.value
 
     monkeypatch.setenv("SG_HOT_MIN", "64")
     n_keys, n = 1 << 14, 1 << 18
@@ -350,16 +351,16 @@ def test_hot_pipeline_from_the_first_batch_and_buffers_given_back(monkeypatch):
         seq += len(d["ts"])
 
     gpu.synchronize()
-    free0 = free_bytes()
+    used0 = pool_used()
     push(_zipf(seq, n, n_keys, 70, 64))
     assert gpu.stats()["hot_keys"] > 0, "the first batch did not run the pipeline"
-    free_hot = free_bytes()
-    assert free0 - free_hot > 20 << 20, (free0, free_hot)   # B + hot_exmax slots x 40 B + 3 x B words
+    used_hot = pool_used()
+    assert used_hot - used0 > 20 << 20, (used0, used_hot)   # B + hot_exmax slots x 40 B + 3 x B words
     for b in range(10):
         push(synth.stock_ticks(seq, 1 << 14, n_keys, seed=80 + b, rate_per_ms=64))
     gpu.synchronize()
-    free_idle = free_bytes()
-    assert free_idle - free_hot > 20 << 20, (free_hot, free_idle)
+    used_idle = pool_used()
+    assert used_hot - used_idle > 20 << 20, (used_hot, used_idle)
     h0 = gpu.stats()["hot_keys"]
     push(_zipf(seq, n, n_keys, 71, 64))
     push(_zipf(seq, n, n_keys, 72, 64))
