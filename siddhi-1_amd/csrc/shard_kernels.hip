@@ -14,12 +14,11 @@
 // Kernels (tiles of SH_TILE events, one workgroup each, SH_WAVES waves; wave w owns the contiguous
 // sub-range [w * SH_TILE / SH_WAVES, ...) of its tile, walked in rounds of 64 events):
 //   k_sh_count   per (destination, tile) counts, destination-major (so one exclusive scan gives every
-//                tile's first row per destination)
+//                tile's first row per destination: k_sh_scan, one workgroup — world x tiles counts, 8K for 8
+//                ranks at 4M events)
 //   k_sh_scatter stable rank per event by ballot per destination and round, rows written
 //   k_sh_unpack  rows -> SoA columns
 #include <hip/hip_runtime.h>
-
-#include <rocprim/device/device_scan.hpp>
 
 #include <cstdint>
 
@@ -245,6 +244,32 @@ __global__ void __launch_bounds__(256) k_fan_col(uint64_t n, const uint32_t* __r
     if (p != 0xffffffffu) out[p] = in[e];
 }
 
+// exclusive scan of the (destination, tile) counts by one workgroup: each thread sums a contiguous slice, the
+// slice sums are scanned across the block (wave DPP-free shuffles + one LDS round), then each thread writes its
+// slice's prefixes (the counts are world x tiles: thousands, a few reads per thread)
+__global__ void __launch_bounds__(1024) k_sh_scan(const uint32_t* __restrict__ in, uint32_t* __restrict__ out, uint64_t n) {
+    __shared__ uint32_t wsum[16];
+    const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const uint64_t per = (n + 1023) / 1024, a = (uint64_t)t * per, b = a + per < n ? a + per : n;
+    uint32_t s = 0;
+    for (uint64_t i = a; i < b; ++i) s += in[i];
+    uint32_t x = s;   // inclusive scan over the wave
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(x, off, 64);
+        if ((int)lane >= off) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    uint32_t before = 0;
+    for (uint32_t v = 0; v < w; ++v) before += wsum[v];
+    uint32_t run = before + x - s;   // exclusive prefix of this thread's slice
+    for (uint64_t i = a; i < b; ++i) {
+        const uint32_t c = in[i];
+        out[i] = run;
+        run += c;
+    }
+}
+
 // per-shard totals from the scanned offsets (shard-major): total[d] = off[d + 1][0] - off[d][0]
 __global__ void k_fan_totals(const uint32_t* off, uint32_t world, uint32_t ntiles, const uint32_t* last_cnt,
                              uint32_t* totals) {
@@ -276,15 +301,10 @@ static int shard_pack(uint64_t n, const uint32_t* key, const int64_t* ts, const 
     a.overflow = overflow;
     a.ntiles = (uint32_t)((n + SH_TILE - 1) / SH_TILE);
     const size_t ncnt = (size_t)world * a.ntiles;
-    size_t tmp = 0;
-    if (rocprim::exclusive_scan(nullptr, tmp, (uint32_t*)nullptr, (uint32_t*)nullptr, 0u, ncnt,
-                                rocprim::plus<uint32_t>(), s) != hipSuccess)
-        return SG_ERR_DEVICE;
-    const size_t need = 2 * ncnt * 4 + tmp + 256;
+    const size_t need = 2 * ncnt * 4 + 256;
     if (!scratch || scratch_len < need) return SG_ERR_CAPACITY;
     uint32_t* cnt = (uint32_t*)scratch;
     uint32_t* off = cnt + ncnt;
-    void* stmp = (void*)(((uintptr_t)(off + ncnt) + 255) & ~(uintptr_t)255);
     if (cap && hipMemsetAsync(overflow, 0, 4, s) != hipSuccess) return SG_ERR_DEVICE;
     if (n == 0) {
         if (hipMemsetAsync(dest_counts, 0, world * 8, s) != hipSuccess) return SG_ERR_DEVICE;
@@ -295,8 +315,7 @@ static int shard_pack(uint64_t n, const uint32_t* key, const int64_t* ts, const 
     }
     a.counts = cnt;
     hipLaunchKernelGGL(k_sh_count, dim3(a.ntiles), dim3(SH_WAVES * 64), 0, s, a);
-    if (rocprim::exclusive_scan(stmp, tmp, cnt, off, 0u, ncnt, rocprim::plus<uint32_t>(), s) != hipSuccess)
-        return SG_ERR_DEVICE;
+    hipLaunchKernelGGL(k_sh_scan, dim3(1), dim3(1024), 0, s, (const uint32_t*)cnt, off, (uint64_t)ncnt);
     a.counts = off;
     a.rows = rows;
     hipLaunchKernelGGL(k_sh_scatter, dim3(a.ntiles), dim3(SH_WAVES * 64), 0, s, a);
@@ -337,24 +356,18 @@ int fan_split(uint64_t n, const uint32_t* key, uint32_t K, uint32_t world, bool 
     a.null_keys = null_keys ? 1u : 0u;
     a.ntiles = (uint32_t)((n + SH_TILE - 1) / SH_TILE);
     const size_t ncnt = (size_t)world * a.ntiles;
-    size_t tmp = 0;
-    if (rocprim::exclusive_scan(nullptr, tmp, (uint32_t*)nullptr, (uint32_t*)nullptr, 0u, ncnt,
-                                rocprim::plus<uint32_t>(), s) != hipSuccess)
-        return SG_ERR_DEVICE;
-    const size_t need = 2 * ncnt * 4 + (size_t)n * 4 + tmp + 512;
+    const size_t need = 2 * ncnt * 4 + (size_t)n * 4 + 512;
     if (!scratch || scratch_len < need) return SG_ERR_CAPACITY;
     uint32_t* cnt = (uint32_t*)scratch;
     uint32_t* off = cnt + ncnt;
     a.pos = off + ncnt;
-    void* stmp = (void*)(((uintptr_t)(a.pos + n) + 255) & ~(uintptr_t)255);
     a.opos = opos;
     a.okey = okey;
     a.err = err;
     if (hipMemsetAsync(err, 0, 4, s) != hipSuccess) return SG_ERR_DEVICE;
     a.counts = cnt;
     hipLaunchKernelGGL(k_fan_count, dim3(a.ntiles), dim3(SH_WAVES * 64), 0, s, a);
-    if (rocprim::exclusive_scan(stmp, tmp, cnt, off, 0u, ncnt, rocprim::plus<uint32_t>(), s) != hipSuccess)
-        return SG_ERR_DEVICE;
+    hipLaunchKernelGGL(k_sh_scan, dim3(1), dim3(1024), 0, s, (const uint32_t*)cnt, off, (uint64_t)ncnt);
     a.counts = off;
     hipLaunchKernelGGL(k_fan_rank, dim3(a.ntiles), dim3(SH_WAVES * 64), 0, s, a);
     hipLaunchKernelGGL(k_fan_totals, dim3(1), dim3(64), 0, s, off, world, a.ntiles, cnt, totals);
@@ -376,10 +389,7 @@ int fan_split(uint64_t n, const uint32_t* key, uint32_t K, uint32_t world, bool 
 size_t fan_split_scratch_bytes(uint64_t n, uint32_t world) {
     const uint32_t ntiles = (uint32_t)((n + SH_TILE - 1) / SH_TILE);
     const size_t ncnt = (size_t)world * ntiles;
-    size_t tmp = 0;
-    (void)rocprim::exclusive_scan(nullptr, tmp, (uint32_t*)nullptr, (uint32_t*)nullptr, 0u, ncnt,
-                                  rocprim::plus<uint32_t>(), (hipStream_t)0);
-    return 2 * ncnt * 4 + (size_t)n * 4 + tmp + 512;
+    return 2 * ncnt * 4 + (size_t)n * 4 + 512;
 }
 
 extern "C" {
@@ -387,10 +397,7 @@ extern "C" {
 size_t sg_shard_scratch_bytes(uint64_t n, uint32_t world) {
     const uint32_t ntiles = (uint32_t)((n + SH_TILE - 1) / SH_TILE);
     const size_t ncnt = (size_t)world * ntiles;
-    size_t tmp = 0;
-    (void)rocprim::exclusive_scan(nullptr, tmp, (uint32_t*)nullptr, (uint32_t*)nullptr, 0u, ncnt,
-                                  rocprim::plus<uint32_t>(), (hipStream_t)0);
-    return 2 * ncnt * 4 + tmp + 256;
+    return 2 * ncnt * 4 + 256;
 }
 
 int sg_shard_unpack(uint64_t n, const uint32_t* rows, uint32_t n_cols, uint32_t* key, int64_t* ts,
