@@ -199,7 +199,11 @@ struct GenProgram {
 // chn_kernels.hip: partials a key's register window holds, for a chain of n states (k_chn_batch, 2 waves per SIMD),
 // and the wide window of the kernel the keys that outgrow it go to (k_chn_wide, 1 wave per SIMD: up to 512 VGPRs;
 // its canonical pool entries, n - 1 per partial, stay below 64)
-#define CHN_R(n) ((n) == 2 ? 24 : (n) == 3 ? 20 : 12)
+#ifndef CHN_R3
+#define CHN_R3 24        // (the 3-state window: P3 per push 16 slots 3.63 ms, 20: 3.68-3.72, 24: 3.46-3.59 — 247 VGPRs,
+                         // no spill at two waves per SIMD, 18 KB of LDS per wave; experiment builds override it)
+#endif
+#define CHN_R(n) ((n) == 2 ? 24 : (n) == 3 ? CHN_R3 : 12)
 #define CHN_RW(n) ((n) == 2 ? 32 : (n) == 3 ? 32 : 21)
 
 // KeyState field offsets inside a processor's record

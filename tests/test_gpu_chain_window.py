@@ -159,7 +159,7 @@ def test_chain_window_nulls(monkeypatch):
 
 @pytest.mark.parametrize("wide", [True, False])
 def test_chain_window_overflow_hands_over(wide, monkeypatch):
-    """a filter that rarely passes: state-1 partials pile up past the window (20 for three states), the key is stored
+    """a filter that rarely passes: state-1 partials pile up past the window (24 for three states), the key is stored
     and the wide-window kernel (32) continues from the event where it stopped, then the general kernel from where
     that one stopped (wide = False: the general kernel directly); later batches load it back"""
     q = chain(["price>10", "price>39.5", "price>e2.price"], within="within 300 milliseconds")
@@ -256,8 +256,8 @@ def test_chain_window_after_foreign_import_and_exports(shape, monkeypatch):
 
 def test_p3_at_bench_keys(monkeypatch):
     """the bench's P3 leg at its size (2^20 keys, 2^22-event pushes, partial capacity 32): chain kernel == general
-    kernel, every match and counter, seven pushes with state carried — past the 10-second window's fill, where keys
-    outgrow the 20-slot window and go to the wide window (and beyond it to the general kernel)"""
+    kernel, every match and counter, seven pushes with state carried — past the 10-second window's fill (with the
+    24-slot window no key outgrows it here; the overflow tests above take the hand-overs)"""
     q = synth.P3_QUERY
     K, B = 1 << 20, 1 << 22
     fast = _engine(q, K, B, False, monkeypatch, mcap=B)
@@ -273,6 +273,5 @@ def test_p3_at_bench_keys(monkeypatch):
         total += len(mf)
     assert total > 0
     sf, sg = fast.stats(), gen.stats()
-    assert sf["window_spills"] > 0
     for k in ALL:
         assert sf[k] == sg[k], (k, sf[k], sg[k])
